@@ -1,0 +1,170 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X state-transition hot path (BASELINE.json metric).
+
+Headline (``value``): batched BLAKE2b-512[:32] hashes/s over 1,048,576 synthetic 512-byte
+proto3 AttestationRecord encodings per GPU (BASELINE.json configs[1]), inputs resident in
+HBM, one ``pz_dev_blake2b512_fixed`` launch per step.  With ``--gpus N`` (torchrun, one
+process per GPU) each rank hashes its own batch (message batches shard with no collective:
+``scaling`` = "weak"), and ``value`` = all records hashed / max-over-ranks wall time.
+
+Also reported on the same line: ``roofline`` (the hash kernel's VALU roofline fraction,
+kernel time from HIP events on the launch stream) and ``cpu_baseline`` (the oracle's C
+restatement on this host's cores, rank 0 at N=1 only).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "validator-epoch updates/sec + hashes/sec (1/2/4/8 MI355X) vs Go CPU ref"
+
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters")
+N_CU = 256
+CLK_HZ = 2.4e9
+LANE_OPS_PER_CU_CLK = 128          # 4 SIMD-32 x 32 lanes (wave64 issues over 2 cycles)
+VALU_PEAK = N_CU * LANE_OPS_PER_CU_CLK * CLK_HZ   # 78.6e12 32-bit lane-ops/s
+HBM_PEAK = 8.0e12                  # B/s (spec)
+# ISA-minimal VALU lane-ops per BLAKE2b compression on gfx950:
+# per G: 6 x v_lshl_add_u64 + 8 x v_xor_b32 + 6 x v_alignbit_b32 = 20; 96 G per compression.
+OPS_PER_COMPRESSION = 96 * 20
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--records", type=int, default=1 << 20)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def load_pmc_traffic():
+    path = os.path.join(ROOT, "profiles", "hash_pmc_traffic.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return None
+
+
+def cpu_baseline(records_np):
+    """Time the oracle's C restatement (oracle/c) over the same records on 1 core."""
+    try:
+        from oracle import cport
+    except Exception as e:  # pragma: no cover - reported, not fatal
+        return {"value": None, "unit": "hashes/s", "cores": 0, "kind": "port",
+                "sample": "unavailable: %s" % e}
+    n = records_np.shape[0]
+    t0 = time.perf_counter()
+    cport.hash_fixed(records_np, 512, 32)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "hashes/s", "cores": 1, "kind": "port",
+            "sample": "%d x 512-B records (the full per-GPU batch), 1 thread, portable C BLAKE2b "
+                      "(oracle/c/blake2b_ref.c), %.2f s" % (n, dt)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from prysm_amd import _lib, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    _lib.lib.call("pz_init", local)
+
+    n = args.records
+    recs = synth.attestation_records_512(n, seed=2 + rank)
+    d_in = torch.from_numpy(recs.reshape(-1)).to(dev)
+    d_out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = ctypes.c_void_p(stream.cuda_stream)
+
+    def step():
+        _lib.lib.call("pz_dev_blake2b512_fixed", d_in.data_ptr(), 512, 512, n, d_out.data_ptr(), 32, sh)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        step()
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+
+    if rank == 0:
+        total = n * world * args.steps
+        value = total / wall
+        ops = n * 4 * OPS_PER_COMPRESSION
+        achieved = ops / (kern_ms * 1e-3)
+        pmc = load_pmc_traffic()
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "hashes/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic",
+            "config": {"workload": "batched BLAKE2b-512[:32] of 512-B proto3 AttestationRecord "
+                                   "encodings (BASELINE configs[1])",
+                       "records_per_gpu": n, "record_bytes": 512, "global_batch": n * world,
+                       "parallelism": "batch-shard x%d" % world},
+            "roofline": {
+                "bound": "valu",
+                "achieved": achieved / 1e12,
+                "peak": VALU_PEAK / 1e12,
+                "unit": "T lane-ops/s",
+                "frac": achieved / VALU_PEAK,
+                "traffic": pmc.get("bytes_per_launch") if pmc else None,
+                "kernel": "pz_b2b_fixed_kernel",
+                "kernel_ms": kern_ms,
+                "algorithmic_ops_per_launch": ops,
+                "hbm_view": {"bytes_per_launch": n * (512 + 32),
+                             "achieved_GBps": n * 544 / (kern_ms * 1e-3) / 1e9,
+                             "peak_GBps": HBM_PEAK / 1e9},
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(recs)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,116 @@
+/*
+ * prysm_hip.h — C ABI of the MI355X-native state-transition hot path.
+ *
+ * This is the drop-in boundary: the entry points a cgo shim inside the reference's Go
+ * packages would bind.  Every function is `extern "C"`, takes plain
+ * pointers and sizes, never retains a caller pointer after it returns, and is thread-safe
+ * (per-device mutex; one library-owned HIP stream per device for the host-pointer API).
+ *
+ * Two flavours:
+ *   pz_*      host pointers, synchronous (the Go-API drop-in; data is copied H2D/D2H);
+ *   pz_dev_*  device pointers, enqueued on the caller's hipStream_t (passed as void*),
+ *             asynchronous; used by the device-resident mirror and the benchmark.
+ *
+ * Paths below are relative to the reference tree (/root/reference).  All arithmetic is
+ * integer and bit-exact with the Go reference (uint64 wrap-around, MSB-first bitfields).
+ *
+ * The library fails loudly: if no gfx950 device is usable every compute entry point
+ * returns PZ_EDEVICE; there is no CPU fallback.
+ */
+#ifndef PRYSM_HIP_H
+#define PRYSM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------------------ */
+#define PZ_OK         0
+#define PZ_ENIL      -1  /* nil message: Go returns proto.ErrNil-wrapped error (types/*_test.go) */
+#define PZ_EINDEX    -2  /* Go index-out-of-range panic (CheckBit / committee / record index) */
+#define PZ_ETOOMANY  -3  /* > params.MaxValidators (utils/shuffle.go:15-17) */
+#define PZ_EDEVICE   -4  /* HIP failure or no usable gfx950 device */
+#define PZ_ENOTFOUND -5  /* committee lookup failed: Go error (blockchain/core.go:373) */
+#define PZ_EINVAL    -6  /* malformed arguments (null pointer with n > 0, bad sizes) */
+#define PZ_ERANGE    -7  /* slice bounds out of range (Go panic, blockchain/core.go:353) */
+
+/* params/config.go:4-26 */
+#define PZ_ATTESTER_REWARD      1ULL
+#define PZ_CYCLE_LENGTH         64
+#define PZ_SHARD_COUNT          1024
+#define PZ_DEFAULT_BALANCE      32ULL
+#define PZ_MAX_VALIDATORS       4194304ULL
+#define PZ_MIN_COMMITTEE_SIZE   128
+#define PZ_DEFAULT_END_DYNASTY  9999999999999999999ULL
+
+/* ---- runtime ------------------------------------------------------------------------ */
+int         pz_init(int device);          /* select/initialise a device for this thread */
+int         pz_device_count(int* count);
+const char* pz_last_error(void);          /* thread-local message for the last failure */
+int         pz_version(void);             /* ABI version: 1 */
+
+/* ---- H: BLAKE2b-512 of serialized messages ------------------------------------------
+ * Replaces `h := blake2b.Sum512(data); copy(hash[:], h[:32])` at
+ *   types/block.go:73-76          (*Block).Hash
+ *   types/attestation.go:55-58    (*Attestation).Hash
+ *   types/attestation.go:74-76    (*Attestation).Key
+ *   types/state.go:145-148        (*ActiveState).Hash
+ *   types/state.go:244-247        (*CrystallizedState).Hash
+ *   blockchain/core.go:290        processAttestation message hash (keeps all 64 bytes)
+ *   utils/shuffle.go:19           ShuffleIndices seed stream (keeps all 64 bytes)
+ * Messages are CSR: message i is msgs[offsets[i] .. offsets[i+1]); offsets has n+1 entries.
+ * out receives n * out_bytes bytes (out_bytes = 32: the hot path's truncated digest; 64: full).
+ */
+int pz_blake2b512_batch(const uint8_t* msgs, const uint64_t* offsets, uint64_t n,
+                        uint8_t* out, uint32_t out_bytes);
+
+/* Device-resident forms (device pointers; caller's stream).  The CSR form requires 4
+ * readable bytes past msgs[offsets[n]-1] (the library's own buffers are padded). */
+int pz_dev_blake2b512_batch(const uint8_t* d_msgs, const uint64_t* d_offsets, uint64_t n,
+                            uint8_t* d_out, uint32_t out_bytes, void* stream);
+/* Fixed-length records: message i is d_msgs[i*stride .. i*stride+len); stride % 16 == 0,
+ * d_msgs 16-byte aligned, stride >= len.  This is the batched-record fast path. */
+int pz_dev_blake2b512_fixed(const uint8_t* d_msgs, uint64_t stride, uint64_t len, uint64_t n,
+                            uint8_t* d_out, uint32_t out_bytes, void* stream);
+
+/* ---- T/R: validator-set filters (casper/validator.go) ------------------------------- */
+#define PZ_KIND_ACTIVE 0  /* start <= dyn < end        casper/validator.go:45-53 */
+#define PZ_KIND_EXITED 1  /* start <  dyn && end <= dyn casper/validator.go:57-65 */
+#define PZ_KIND_QUEUED 2  /* start >  dyn               casper/validator.go:69-77 */
+/* out (capacity n) receives the ascending indices; *count their number (0 == Go nil). */
+int pz_validator_indices(const uint64_t* start_dynasty, const uint64_t* end_dynasty, uint64_t n,
+                         uint64_t dynasty, int kind, uint32_t* out, uint64_t* count);
+
+/* casper/validator.go:93-102 GetAttestersTotalDeposit: popcount of every pending
+ * attestation's bitfield bytes (concatenated) x DefaultBalance. */
+int pz_attesters_total_deposit(const uint8_t* bits, uint64_t nbytes, uint64_t* out);
+
+/* casper/incentives.go:14-32 CalculateRewards, in place on balance[n].
+ * Pending attestations are CSR bitfields (bits, boffs[natt+1]); the reward bit for rank i
+ * is CheckBit(last bitfield, active[i]) and the target is balance[i] (rank, not index).
+ * Returns PZ_EINDEX (balances untouched) where Go would panic. *applied = 1 when the
+ * 2/3 threshold held. */
+int pz_calculate_rewards(uint64_t* balance, const uint64_t* start_dynasty,
+                         const uint64_t* end_dynasty, uint64_t n, uint64_t dynasty,
+                         uint64_t total_deposit, const uint8_t* bits, const uint64_t* boffs,
+                         uint64_t natt, int* applied);
+
+/* blockchain/core.go:515-545 processCrosslinks tallies: for attestation a with committee
+ * c = att_committee[a] (members committee[coffs[c] .. coffs[c+1])):
+ *   total[a] = sum balance[member], vote[a] = sum balance[member] * CheckBit(bits_a, pos). */
+int pz_crosslink_tally(const uint32_t* committee, const uint64_t* coffs, uint64_t ncomm,
+                       const uint32_t* att_committee, const uint8_t* bits, const uint64_t* boffs,
+                       uint64_t natt, const uint64_t* balance, uint64_t nval,
+                       uint64_t* vote_out, uint64_t* total_out);
+
+/* utils/shuffle.go:14-33 ShuffleIndices, in place.  Host-resident by design (a sequential
+ * swap chain); only the 64-byte seed stream blake2b.Sum512(seed) is computed on the GPU. */
+int pz_shuffle_indices(const uint8_t seed[32], uint32_t* list, uint64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PRYSM_HIP_H */

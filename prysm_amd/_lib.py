@@ -1,0 +1,119 @@
+"""ctypes binding of ``libprysm_hip.so`` (include/prysm_hip.h).
+
+Loading fails loudly: if the in-tree library is missing, importing a compute entry point
+raises ``PzError`` — there is no CPU fallback anywhere in ``prysm_amd``.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+library_path = os.path.join(HERE, "libprysm_hip.so")
+
+PZ_OK = 0
+PZ_ENIL = -1
+PZ_EINDEX = -2
+PZ_ETOOMANY = -3
+PZ_EDEVICE = -4
+PZ_ENOTFOUND = -5
+PZ_EINVAL = -6
+PZ_ERANGE = -7
+
+_NAMES = {PZ_ENIL: "ENIL", PZ_EINDEX: "EINDEX", PZ_ETOOMANY: "ETOOMANY", PZ_EDEVICE: "EDEVICE",
+          PZ_ENOTFOUND: "ENOTFOUND", PZ_EINVAL: "EINVAL", PZ_ERANGE: "ERANGE"}
+
+
+class PzError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (%d): %s" % (_NAMES.get(code, "?"), code, msg))
+        self.code = code
+
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_u64p = ctypes.POINTER(ctypes.c_uint64)
+c_intp = ctypes.POINTER(ctypes.c_int)
+u64 = ctypes.c_uint64
+u32 = ctypes.c_uint32
+vp = ctypes.c_void_p
+
+# name -> argtypes (all return int status unless listed in _RESTYPES)
+SIGNATURES = {
+    "pz_init": [ctypes.c_int],
+    "pz_device_count": [c_intp],
+    "pz_last_error": [],
+    "pz_version": [],
+    "pz_blake2b512_batch": [vp, vp, u64, vp, u32],
+    "pz_dev_blake2b512_batch": [vp, vp, u64, vp, u32, vp],
+    "pz_dev_blake2b512_fixed": [vp, u64, u64, u64, vp, u32, vp],
+}
+_RESTYPES = {"pz_last_error": ctypes.c_char_p}
+
+
+class _Lib:
+    def __init__(self):
+        self._dll = None
+
+    def _load(self):
+        if self._dll is None:
+            if not os.path.exists(library_path):
+                raise PzError(PZ_EDEVICE, "HIP library not built: %s (run __graft_entry__.build())"
+                              % library_path)
+            dll = ctypes.CDLL(library_path)
+            for name, args in SIGNATURES.items():
+                fn = getattr(dll, name)
+                fn.argtypes = args
+                fn.restype = _RESTYPES.get(name, ctypes.c_int)
+            self._dll = dll
+        return self._dll
+
+    @property
+    def dll(self):
+        return self._load()
+
+    def call(self, name, *args):
+        rc = getattr(self._load(), name)(*args)
+        if rc != PZ_OK:
+            raise PzError(rc, self._load().pz_last_error().decode())
+        return rc
+
+
+lib = _Lib()
+
+
+def ptr(a):
+    """Host pointer of a C-contiguous numpy array (None for empty)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data if a.size else None
+
+
+def as_u8(buf):
+    return np.frombuffer(bytes(buf), dtype=np.uint8) if not isinstance(buf, np.ndarray) else buf
+
+
+def blake2b512_batch(messages, out_bytes=32):
+    """Hash a list of byte strings on the GPU; returns a list of ``out_bytes``-byte digests."""
+    n = len(messages)
+    if n == 0:
+        return []
+    offsets = np.zeros(n + 1, dtype=np.uint64)
+    offsets[1:] = np.cumsum([len(m) for m in messages], dtype=np.uint64)
+    data = np.frombuffer(b"".join(bytes(m) for m in messages) + b"\0" * 16, dtype=np.uint8)
+    out = np.empty(n * out_bytes, dtype=np.uint8)
+    lib.call("pz_blake2b512_batch", ptr(data), ptr(offsets), n, ptr(out), out_bytes)
+    raw = out.tobytes()
+    return [raw[i * out_bytes:(i + 1) * out_bytes] for i in range(n)]
+
+
+def blake2b512_csr(data, offsets, out_bytes=32):
+    """Hash CSR messages (numpy uint8 data, uint64 offsets[n+1]); returns (n, out_bytes) uint8."""
+    n = len(offsets) - 1
+    out = np.empty((max(n, 0), out_bytes), dtype=np.uint8)
+    if n > 0:
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lib.call("pz_blake2b512_batch", ptr(data), ptr(offsets), n, ptr(out), out_bytes)
+    return out

@@ -1,0 +1,269 @@
+// BLAKE2b-512 batch kernels for gfx950 (CDNA4, wave64).
+//
+// Restates RFC 7693 (the algorithm of golang.org/x/crypto/blake2b @ a49355c, which the
+// reference calls at types/block.go:74, types/attestation.go:56,74, types/state.go:146,245,
+// blockchain/core.go:290 and utils/shuffle.go:19) as one-lane-per-message integer code:
+//   * the 16-word state v[] and the chaining value h[] live in VGPR pairs;
+//   * 64-bit adds lower to v_lshl_add_u64 (one VALU op on gfx950);
+//   * rotr 32 is a register-pair swap, rotr 24/16/63 are two v_alignbit_b32 each;
+//   * 12 rounds are fully unrolled so sigma[] indexes registers statically.
+// Fixed-length records are staged global->LDS with coalesced 16-byte loads (8 lanes cover
+// one 128-byte block) and read back one row per lane; variable-length (CSR) messages are
+// read per lane with dword loads + v_alignbit funnel shifts.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "blake2b_kernels.h"
+
+namespace pz {
+
+#define IV0 0x6a09e667f3bcc908ULL
+#define IV1 0xbb67ae8584caa73bULL
+#define IV2 0x3c6ef372fe94f82bULL
+#define IV3 0xa54ff53a5f1d36f1ULL
+#define IV4 0x510e527fade682d1ULL
+#define IV5 0x9b05688c2b3e6c1fULL
+#define IV6 0x1f83d9abfb41bd6bULL
+#define IV7 0x5be0cd19137e2179ULL
+
+__device__ __forceinline__ uint64_t pack(uint32_t lo, uint32_t hi) {
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t rotr32(uint64_t x) { return (x >> 32) | (x << 32); }
+__device__ __forceinline__ uint64_t rotr24(uint64_t x) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return pack(__builtin_amdgcn_alignbit(hi, lo, 24), __builtin_amdgcn_alignbit(lo, hi, 24));
+}
+__device__ __forceinline__ uint64_t rotr16(uint64_t x) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return pack(__builtin_amdgcn_alignbit(hi, lo, 16), __builtin_amdgcn_alignbit(lo, hi, 16));
+}
+__device__ __forceinline__ uint64_t rotr63(uint64_t x) {  // == rotl 1
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return pack(__builtin_amdgcn_alignbit(lo, hi, 31), __builtin_amdgcn_alignbit(hi, lo, 31));
+}
+
+#define G(a, b, c, d, x, y)        \
+  do {                             \
+    a = a + b + (x);               \
+    d = rotr32(d ^ a);             \
+    c = c + d;                     \
+    b = rotr24(b ^ c);             \
+    a = a + b + (y);               \
+    d = rotr16(d ^ a);             \
+    c = c + d;                     \
+    b = rotr63(b ^ c);             \
+  } while (0)
+
+// One round with the message permutation sigma[r] spelled out as literals (RFC 7693 §2.7).
+#define ROUND(s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15) \
+  do {                                                                             \
+    G(v0, v4, v8, v12, m[s0], m[s1]);                                              \
+    G(v1, v5, v9, v13, m[s2], m[s3]);                                              \
+    G(v2, v6, v10, v14, m[s4], m[s5]);                                             \
+    G(v3, v7, v11, v15, m[s6], m[s7]);                                             \
+    G(v0, v5, v10, v15, m[s8], m[s9]);                                             \
+    G(v1, v6, v11, v12, m[s10], m[s11]);                                           \
+    G(v2, v7, v8, v13, m[s12], m[s13]);                                            \
+    G(v3, v4, v9, v14, m[s14], m[s15]);                                            \
+  } while (0)
+
+// RFC 7693 compression function F(h, m, t, f); t < 2^64 here (messages < 16 EiB).
+__device__ __forceinline__ void compress(uint64_t h[8], const uint64_t m[16], uint64_t t,
+                                         bool last) {
+  uint64_t v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3];
+  uint64_t v4 = h[4], v5 = h[5], v6 = h[6], v7 = h[7];
+  uint64_t v8 = IV0, v9 = IV1, v10 = IV2, v11 = IV3;
+  uint64_t v12 = IV4 ^ t, v13 = IV5, v14 = last ? ~IV6 : IV6, v15 = IV7;
+  ROUND(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+  ROUND(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3);
+  ROUND(11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4);
+  ROUND(7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8);
+  ROUND(9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13);
+  ROUND(2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9);
+  ROUND(12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11);
+  ROUND(13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10);
+  ROUND(6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5);
+  ROUND(10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0);
+  ROUND(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+  ROUND(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3);
+  h[0] ^= v0 ^ v8;
+  h[1] ^= v1 ^ v9;
+  h[2] ^= v2 ^ v10;
+  h[3] ^= v3 ^ v11;
+  h[4] ^= v4 ^ v12;
+  h[5] ^= v5 ^ v13;
+  h[6] ^= v6 ^ v14;
+  h[7] ^= v7 ^ v15;
+}
+
+__device__ __forceinline__ void init_h(uint64_t h[8]) {
+  // parameter block: digest length 64, key length 0, fanout 1, depth 1
+  h[0] = IV0 ^ 0x01010040ULL;
+  h[1] = IV1; h[2] = IV2; h[3] = IV3; h[4] = IV4; h[5] = IV5; h[6] = IV6; h[7] = IV7;
+}
+
+__device__ __forceinline__ void store_digest(uint8_t* out, const uint64_t h[8], uint32_t out_bytes) {
+  // out is 32- or 64-byte aligned per message (out + i*out_bytes with a 16-B aligned base)
+  uint4* o = reinterpret_cast<uint4*>(out);
+  o[0] = make_uint4((uint32_t)h[0], (uint32_t)(h[0] >> 32), (uint32_t)h[1], (uint32_t)(h[1] >> 32));
+  o[1] = make_uint4((uint32_t)h[2], (uint32_t)(h[2] >> 32), (uint32_t)h[3], (uint32_t)(h[3] >> 32));
+  if (out_bytes == 64) {
+    o[2] = make_uint4((uint32_t)h[4], (uint32_t)(h[4] >> 32), (uint32_t)h[5], (uint32_t)(h[5] >> 32));
+    o[3] = make_uint4((uint32_t)h[6], (uint32_t)(h[6] >> 32), (uint32_t)h[7], (uint32_t)(h[7] >> 32));
+  }
+}
+
+// Zero bytes [keep, 16) of a 16-byte chunk (keep in 0..16).
+__device__ __forceinline__ uint4 mask_chunk(uint4 c, uint32_t keep) {
+  uint32_t w[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int lo = 4 * k;
+    uint32_t valid = keep <= (uint32_t)lo ? 0u : (keep >= (uint32_t)lo + 4 ? 4u : keep - lo);
+    uint32_t msk = valid >= 4 ? 0xffffffffu : ((1u << (8 * valid)) - 1u);
+    w[k] &= msk;
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// ------------------------------------------------------------------------------------------
+// Fixed-length records, LDS-staged.  One wave = 64 consecutive messages; each wave owns a
+// private LDS slab [64 rows][144 B] (128-B block + 16-B pad: conflict-free ds_read_b128).
+// ------------------------------------------------------------------------------------------
+constexpr int kWavesPerBlock = 4;
+constexpr int kRowBytes = 144;
+constexpr int kSlabBytes = 64 * kRowBytes;
+
+extern "C" __global__ void __launch_bounds__(256)
+pz_b2b_fixed_kernel(const uint8_t* __restrict__ msgs, uint64_t stride, uint64_t len, uint64_t n,
+                    uint8_t* __restrict__ out, uint32_t out_bytes) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerBlock * kSlabBytes];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  uint8_t* slab = lds + wave * kSlabBytes;
+  const uint64_t m0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * 64;
+  if (m0 >= n) return;  // whole wave idle (wave-uniform)
+  const uint64_t msg = m0 + lane;
+  const uint64_t nblocks = len == 0 ? 1 : (len + 127) / 128;
+
+  uint64_t h[8];
+  init_h(h);
+  for (uint64_t t = 0; t < nblocks; ++t) {
+    // ---- stage: 512 16-byte chunks (64 msgs x 8 parts), 8 per lane, coalesced per 8 lanes
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int c = it * 64 + lane;
+      const int cm = c >> 3, part = c & 7;
+      const uint64_t gm = m0 + cm;
+      const uint64_t boff = t * 128 + part * 16;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (gm < n && boff < len) {
+        v = *reinterpret_cast<const uint4*>(msgs + gm * stride + boff);
+        if (boff + 16 > len) v = mask_chunk(v, (uint32_t)(len - boff));
+      }
+      *reinterpret_cast<uint4*>(slab + cm * kRowBytes + part * 16) = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- read this lane's row
+    uint64_t m[16];
+    const uint4* row = reinterpret_cast<const uint4*>(slab + lane * kRowBytes);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      uint4 q = row[k];
+      m[2 * k] = pack(q.x, q.y);
+      m[2 * k + 1] = pack(q.z, q.w);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const bool last = (t + 1 == nblocks);
+    const uint64_t ctr = last ? len : (t + 1) * 128;
+    compress(h, m, ctr, last);
+  }
+  if (msg < n) store_digest(out + msg * out_bytes, h, out_bytes);
+}
+
+// ------------------------------------------------------------------------------------------
+// CSR (variable-length) messages: one lane per message, per-lane dword loads.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t load_dword_tail(const uint8_t* p, uint32_t nbytes) {
+  // nbytes in 1..3: byte loads so nothing past the message is touched
+  uint32_t w = p[0];
+  if (nbytes > 1) w |= (uint32_t)p[1] << 8;
+  if (nbytes > 2) w |= (uint32_t)p[2] << 16;
+  return w;
+}
+
+// Load the 128-byte block at p (rem bytes of the message remain from p; bytes >= rem are 0).
+// Requires the CSR contract: 4 readable bytes past the message end.
+__device__ __forceinline__ void load_block_csr(const uint8_t* p, uint64_t rem, uint64_t m[16]) {
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* base = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(addr & 3) * 8;
+  const uint32_t keep = rem >= 128 ? 128u : (uint32_t)rem;
+  // aligned dwords covering [p, p+keep): at most 33
+  uint32_t w[33];
+  const uint32_t ndw = (uint32_t)(((addr & 3) + keep + 3) >> 2);
+#pragma unroll
+  for (int k = 0; k < 33; ++k) w[k] = (uint32_t)k < ndw ? base[k] : 0u;
+  uint32_t d[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    uint32_t x = sh ? __builtin_amdgcn_alignbit(w[k + 1], w[k], sh) : w[k];
+    const uint32_t lo = 4u * k;
+    uint32_t valid = keep <= lo ? 0u : (keep >= lo + 4 ? 4u : keep - lo);
+    d[k] = x & (valid >= 4 ? 0xffffffffu : ((1u << (8 * valid)) - 1u));
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) m[k] = pack(d[2 * k], d[2 * k + 1]);
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+pz_b2b_csr_kernel(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ offsets,
+                  uint64_t n, uint8_t* __restrict__ out, uint32_t out_bytes) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t beg = offsets[i], end = offsets[i + 1];
+  const uint64_t len = end - beg;
+  const uint64_t nblocks = len == 0 ? 1 : (len + 127) / 128;
+  uint64_t h[8];
+  init_h(h);
+  for (uint64_t t = 0; t < nblocks; ++t) {
+    uint64_t m[16];
+    const uint64_t rem = len - t * 128;
+    if (len == 0) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) m[k] = 0;
+    } else {
+      load_block_csr(msgs + beg + t * 128, rem, m);
+    }
+    const bool last = (t + 1 == nblocks);
+    compress(h, m, last ? len : (t + 1) * 128, last);
+  }
+  store_digest(out + i * out_bytes, h, out_bytes);
+}
+
+// ---- host-side launchers (declared in blake2b_kernels.h) ---------------------------------
+hipError_t launch_b2b_fixed(const uint8_t* msgs, uint64_t stride, uint64_t len, uint64_t n,
+                            uint8_t* out, uint32_t out_bytes, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const uint64_t waves = (n + 63) / 64;
+  const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+  hipLaunchKernelGGL(pz_b2b_fixed_kernel, dim3((uint32_t)blocks), dim3(64 * kWavesPerBlock), 0,
+                     stream, msgs, stride, len, n, out, out_bytes);
+  return hipGetLastError();
+}
+
+hipError_t launch_b2b_csr(const uint8_t* msgs, const uint64_t* offsets, uint64_t n, uint8_t* out,
+                          uint32_t out_bytes, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const uint64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(pz_b2b_csr_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, msgs,
+                     offsets, n, out, out_bytes);
+  return hipGetLastError();
+}
+
+}  // namespace pz

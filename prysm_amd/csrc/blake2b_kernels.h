@@ -1,0 +1,11 @@
+// Launchers for the BLAKE2b batch kernels (blake2b.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pz {
+hipError_t launch_b2b_fixed(const uint8_t* msgs, uint64_t stride, uint64_t len, uint64_t n,
+                            uint8_t* out, uint32_t out_bytes, hipStream_t stream);
+hipError_t launch_b2b_csr(const uint8_t* msgs, const uint64_t* offsets, uint64_t n, uint8_t* out,
+                          uint32_t out_bytes, hipStream_t stream);
+}  // namespace pz

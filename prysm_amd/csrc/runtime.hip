@@ -1,0 +1,198 @@
+// C-ABI runtime: device contexts, staging buffers, error reporting and the host-pointer
+// (Go drop-in) entry points of include/prysm_hip.h.  Thread-safe: one mutex and one
+// library-owned stream per device; the host-pointer API never retains caller pointers.
+#include "runtime.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "blake2b_kernels.h"
+
+namespace pz {
+
+static thread_local std::string g_err;
+static thread_local int g_device = -1;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(PZ_EDEVICE, "%s: %s", what, hipGetErrorString(e));
+}
+
+static std::mutex g_ctx_mu;
+static std::vector<DeviceCtx*> g_ctx;
+
+DeviceCtx* DeviceCtx::get(int dev) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  if ((int)g_ctx.size() <= dev) g_ctx.resize(dev + 1, nullptr);
+  if (!g_ctx[dev]) {
+    DeviceCtx* c = new DeviceCtx();
+    c->device = dev;
+    g_ctx[dev] = c;
+  }
+  return g_ctx[dev];
+}
+
+int DeviceCtx::ensure_stream() {
+  if (stream) return PZ_OK;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+  return PZ_OK;
+}
+
+int DevBuf::reserve(size_t bytes) {
+  if (bytes <= cap) return PZ_OK;
+  if (ptr) (void)hipFree(ptr);
+  ptr = nullptr;
+  cap = 0;
+  size_t want = bytes + 256;  // padding: CSR readers may touch 4 bytes past the end
+  hipError_t e = hipMalloc(&ptr, want);
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc");
+  cap = bytes;
+  return PZ_OK;
+}
+
+// Resolve the calling thread's device and lock it.  Fails loudly when no device exists.
+int acquire(DeviceCtx** out) {
+  if (g_device < 0) {
+    int rc = pz_init(0);
+    if (rc != PZ_OK) return rc;
+  }
+  DeviceCtx* c = DeviceCtx::get(g_device);
+  hipError_t e = hipSetDevice(c->device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  *out = c;
+  return PZ_OK;
+}
+
+}  // namespace pz
+
+using namespace pz;
+
+extern "C" {
+
+int pz_version(void) { return 1; }
+
+const char* pz_last_error(void) { return g_err.c_str(); }
+
+int pz_device_count(int* count) {
+  if (!count) return fail(PZ_EINVAL, "count is null");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return hip_fail(e, "hipGetDeviceCount");
+  }
+  *count = n;
+  return PZ_OK;
+}
+
+int pz_init(int device) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0)
+    return fail(PZ_EDEVICE, "no HIP device available (%s)",
+                e != hipSuccess ? hipGetErrorString(e) : "0 devices");
+  if (device < 0 || device >= n) return fail(PZ_EINVAL, "device %d out of range [0,%d)", device, n);
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, device);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(PZ_EDEVICE, "device %d is %s; this library is built for gfx950 only", device,
+                prop.gcnArchName);
+  g_device = device;
+  DeviceCtx* c = DeviceCtx::get(device);
+  std::lock_guard<std::mutex> lk(c->mu);
+  return c->ensure_stream();
+}
+
+// ---- H -------------------------------------------------------------------------------------
+int pz_dev_blake2b512_fixed(const uint8_t* d_msgs, uint64_t stride, uint64_t len, uint64_t n,
+                            uint8_t* d_out, uint32_t out_bytes, void* stream) {
+  if (out_bytes != 32 && out_bytes != 64) return fail(PZ_EINVAL, "out_bytes must be 32 or 64");
+  if (n == 0) return PZ_OK;
+  if (!d_msgs || !d_out) return fail(PZ_EINVAL, "null pointer");
+  if (stride % 16 || stride < len || (reinterpret_cast<uintptr_t>(d_msgs) & 15) ||
+      (reinterpret_cast<uintptr_t>(d_out) & 15))
+    return fail(PZ_EINVAL, "fixed layout needs 16-B aligned buffers, stride %% 16 == 0, stride >= len");
+  hipError_t e = launch_b2b_fixed(d_msgs, stride, len, n, d_out, out_bytes, (hipStream_t)stream);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "pz_b2b_fixed_kernel");
+}
+
+int pz_dev_blake2b512_batch(const uint8_t* d_msgs, const uint64_t* d_offsets, uint64_t n,
+                            uint8_t* d_out, uint32_t out_bytes, void* stream) {
+  if (out_bytes != 32 && out_bytes != 64) return fail(PZ_EINVAL, "out_bytes must be 32 or 64");
+  if (n == 0) return PZ_OK;
+  if (!d_msgs || !d_offsets || !d_out) return fail(PZ_EINVAL, "null pointer");
+  if (reinterpret_cast<uintptr_t>(d_out) & 15) return fail(PZ_EINVAL, "d_out must be 16-B aligned");
+  hipError_t e = launch_b2b_csr(d_msgs, d_offsets, n, d_out, out_bytes, (hipStream_t)stream);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "pz_b2b_csr_kernel");
+}
+
+int pz_blake2b512_batch(const uint8_t* msgs, const uint64_t* offsets, uint64_t n, uint8_t* out,
+                        uint32_t out_bytes) {
+  if (out_bytes != 32 && out_bytes != 64) return fail(PZ_EINVAL, "out_bytes must be 32 or 64");
+  if (n == 0) return PZ_OK;
+  if (!offsets || !out) return fail(PZ_EINVAL, "null pointer");
+  const uint64_t base = offsets[0], total = offsets[n] - offsets[0];
+  if (total && !msgs) return fail(PZ_EINVAL, "null msgs");
+  for (uint64_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) return fail(PZ_EINVAL, "offsets not monotone at %llu", (unsigned long long)i);
+
+  DeviceCtx* c;
+  int rc = acquire(&c);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = c->ensure_stream())) return rc;
+  hipStream_t s = c->stream;
+
+  // Uniform records at a 16-B multiple stride use the LDS-staged fixed-length kernel.
+  const uint64_t len0 = offsets[1] - offsets[0];
+  bool uniform = (len0 % 16 == 0) && len0 > 0;
+  for (uint64_t i = 1; uniform && i < n; ++i) uniform = (offsets[i + 1] - offsets[i]) == len0;
+
+  if ((rc = c->in.reserve(total + 16))) return rc;
+  if ((rc = c->out.reserve(n * out_bytes))) return rc;
+  hipError_t e;
+  if (total) {
+    e = hipMemcpyAsync(c->in.ptr, msgs + base, total, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync H2D");
+  }
+  if (uniform) {
+    e = launch_b2b_fixed((const uint8_t*)c->in.ptr, len0, len0, n, (uint8_t*)c->out.ptr, out_bytes, s);
+  } else {
+    std::vector<uint64_t> rel(n + 1);
+    for (uint64_t i = 0; i <= n; ++i) rel[i] = offsets[i] - base;
+    if ((rc = c->aux.reserve((n + 1) * sizeof(uint64_t)))) return rc;
+    e = hipMemcpyAsync(c->aux.ptr, rel.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync H2D offsets");
+    // the pageable source must stay alive until the copy completes
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    e = launch_b2b_csr((const uint8_t*)c->in.ptr, (const uint64_t*)c->aux.ptr, n,
+                       (uint8_t*)c->out.ptr, out_bytes, s);
+  }
+  if (e != hipSuccess) return hip_fail(e, "blake2b launch");
+  e = hipMemcpyAsync(out, c->out.ptr, n * out_bytes, hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync D2H");
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  return PZ_OK;
+}
+
+}  // extern "C"

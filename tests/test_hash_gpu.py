@@ -1,0 +1,55 @@
+"""BLAKE2b-512 batch kernels vs the oracle (hashlib, RFC 7693).  Bit-exact."""
+import numpy as np
+import pytest
+
+from oracle import ref
+from prysm_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def test_rfc7693_abc_gpu():
+    d = _lib.blake2b512_batch([b"abc"], out_bytes=64)[0]
+    assert d == ref.sum512(b"abc")
+
+
+def test_lengths_0_to_600():
+    # every block boundary, empty message, partial dwords
+    msgs = [bytes((i * 7 + j) & 0xFF for j in range(i)) for i in range(0, 601)]
+    for ob in (32, 64):
+        got = _lib.blake2b512_batch(msgs, out_bytes=ob)
+        for m, g in zip(msgs, got):
+            assert g == ref.sum512(m)[:ob], len(m)
+
+
+def test_fixed_512_records_uniform_path():
+    rng = np.random.default_rng(2)
+    n = 5000  # not a multiple of 64 or 256: exercises the tail wave
+    data = rng.integers(0, 256, size=n * 512, dtype=np.uint8)
+    offs = np.arange(n + 1, dtype=np.uint64) * 512
+    got = _lib.blake2b512_csr(data, offs)
+    raw = data.tobytes()
+    for i in range(0, n, 37):
+        assert got[i].tobytes() == ref.hash32(raw[i * 512:(i + 1) * 512])
+    assert got[n - 1].tobytes() == ref.hash32(raw[(n - 1) * 512:])
+
+
+@pytest.mark.parametrize("rec", [16, 112, 128, 144, 256, 400])
+def test_fixed_other_lengths(rec):
+    rng = np.random.default_rng(rec)
+    n = 300
+    data = rng.integers(0, 256, size=n * rec, dtype=np.uint8)
+    offs = np.arange(n + 1, dtype=np.uint64) * rec
+    got = _lib.blake2b512_csr(data, offs, out_bytes=64)
+    raw = data.tobytes()
+    for i in range(n):
+        assert got[i].tobytes() == ref.sum512(raw[i * rec:(i + 1) * rec])
+
+
+def test_ragged_unaligned_csr():
+    rng = np.random.default_rng(7)
+    lens = rng.integers(0, 700, size=777)
+    msgs = [rng.integers(0, 256, size=int(l), dtype=np.uint8).tobytes() for l in lens]
+    got = _lib.blake2b512_batch(msgs)
+    for m, g in zip(msgs, got):
+        assert g == ref.hash32(m)
