@@ -43,7 +43,94 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--records", type=int, default=1 << 20)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-epoch", action="store_true")
+    p.add_argument("--no-hash", action="store_true")
+    p.add_argument("--epoch-validators", type=int, default=0,
+                   help="validators per epoch instance (default: 65,536 at N=1, 1,048,576 at N>1)")
+    p.add_argument("--epoch-instances", type=int, default=0,
+                   help="independent epoch instances per step (default: 16.7M validator-epochs/step)")
     return p.parse_args()
+
+
+# Algorithmic HBM bytes per validator-epoch: 16 B start/end
+# dynasty + 16 B balance read-modify-write + 1/8 B last-bitfield bit + 1/8 B committee bitfield
+# popcount + 12 B crosslink committee gather (u32 member + u64 balance).
+EPOCH_BYTES_PER_VALIDATOR = 44.25
+
+
+def epoch_leg(args, torch, dist, dev, rank, world):
+    """BASELINE configs[2] (N=1: 65,536 validators, B instances per step) / configs[3]
+    (N>1: 1,048,576 validators sharded over the ranks, RCCL all-reduce of the sums)."""
+    from prysm_amd import casper, synth
+    from prysm_amd.epoch import DeviceEpoch
+
+    nval = args.epoch_validators or (65536 if world == 1 else 1 << 20)
+    ninst = args.epoch_instances or max(1, (1 << 24) // nval)
+    seed_a = b"A" + bytes(31)  # common.Hash{'A'} (casper/sharding_test.go:57)
+    shuffled = casper.shuffle_indices(seed_a, np.arange(nval, dtype=np.uint32))
+    inst = synth.epoch_batch(nval, ninst, seed=3, shuffled=shuffled)
+    de = DeviceEpoch(inst, dev, rank=rank, world=world)
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(args.warmup):
+        de.step(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        de.step(stream)
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    step_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    units = nval * ninst * args.steps
+    local_units = (de.hi - de.lo) * ninst
+    achieved = local_units * EPOCH_BYTES_PER_VALIDATOR / (step_ms * 1e-3)
+    out = {
+        "metric": "validator-epoch updates/s",
+        "value": units / wall,
+        "unit": "validator-epochs/s",
+        "ms_per_step": wall / args.steps * 1e3,
+        "config": {"workload": "stateRecalc data-parallel part: crosslink tallies+winners, attester "
+                               "popcount, CalculateRewards, next-cycle balance (BASELINE configs[%d])"
+                               % (2 if world == 1 else 3),
+                   "validators": nval, "instances_per_step": ninst, "attestations_per_instance": inst["natt"],
+                   "parallelism": "validator-shard x%d + RCCL all-reduce" % world if world > 1 else "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK, "traffic": None,
+                     "kernel": "epoch step (count+winner+compact+reward, device time of the whole step)",
+                     "step_device_ms": step_ms,
+                     "algorithmic_bytes_per_launch": local_units * EPOCH_BYTES_PER_VALIDATOR},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = epoch_cpu_baseline(inst)
+    return out
+
+
+def epoch_cpu_baseline(inst):
+    """The oracle's C restatement of the same epoch (AoS, 1 thread), on one instance."""
+    try:
+        from oracle import cport
+        t0 = time.perf_counter()
+        reps = cport.epoch_instance_timed(inst, 0)
+        dt = time.perf_counter() - t0
+        return {"value": reps * inst["nval"] / dt, "unit": "validator-epochs/s", "cores": 1, "kind": "port",
+                "sample": "%d x one %d-validator epoch instance (AoS records, 1 thread, oracle/c/epoch_ref.c), "
+                          "%.2f s" % (reps, inst["nval"], dt)}
+    except Exception as e:  # pragma: no cover
+        return {"value": None, "unit": "validator-epochs/s", "cores": 0, "kind": "port",
+                "sample": "unavailable: %s" % e}
 
 
 def load_pmc_traffic():
@@ -120,6 +207,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
 
+    epoch = None if args.no_epoch else epoch_leg(args, torch, dist, dev, rank, world)
+
     if rank == 0:
         total = n * world * args.steps
         value = total / wall
@@ -160,6 +249,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(recs)
+        if epoch is not None:
+            line["epoch"] = epoch
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -29,7 +29,7 @@ extern "C" {
 
 /* ---- status codes ------------------------------------------------------------------ */
 #define PZ_OK         0
-#define PZ_ENIL      -1  /* nil message: Go returns proto.ErrNil-wrapped error (types/*_test.go) */
+#define PZ_ENIL      -1  /* nil message: Go returns a proto.ErrNil-wrapped error (types/block_test.go:37-43) */
 #define PZ_EINDEX    -2  /* Go index-out-of-range panic (CheckBit / committee / record index) */
 #define PZ_ETOOMANY  -3  /* > params.MaxValidators (utils/shuffle.go:15-17) */
 #define PZ_EDEVICE   -4  /* HIP failure or no usable gfx950 device */
@@ -106,9 +106,80 @@ int pz_crosslink_tally(const uint32_t* committee, const uint64_t* coffs, uint64_
                        uint64_t natt, const uint64_t* balance, uint64_t nval,
                        uint64_t* vote_out, uint64_t* total_out);
 
+/* blockchain/core.go:502-558 processCrosslinks, complete: tallies as above, then the in-order
+ * winner rule — for each shard the FIRST attestation with 3*vote >= 2*total (uint64 wrap)
+ * and dynasty > rec_dynasty[shard] wins.  winner[s] (capacity nrec) receives the winning
+ * attestation index or UINT32_MAX; the caller rewrites records[s] = {dynasty, that
+ * attestation's ShardBlockHash, slot}.  PZ_EINDEX where Go would panic. */
+int pz_process_crosslinks(const uint32_t* committee, const uint64_t* coffs, uint64_t ncomm,
+                          const uint32_t* att_committee, const uint32_t* att_shard,
+                          const uint8_t* bits, const uint64_t* boffs, uint64_t natt,
+                          const uint64_t* balance, uint64_t nval, const uint64_t* rec_dynasty,
+                          uint64_t nrec, uint64_t dynasty, uint32_t* winner,
+                          uint64_t* vote_out, uint64_t* total_out);
+
 /* utils/shuffle.go:14-33 ShuffleIndices, in place.  Host-resident by design (a sequential
  * swap chain); only the 64-byte seed stream blake2b.Sum512(seed) is computed on the GPU. */
 int pz_shuffle_indices(const uint8_t seed[32], uint32_t* list, uint64_t n);
+
+/* ---- device-resident batched epoch transition (throughput mode, multi-GPU shards) -----
+ * B independent instances of the data-parallel part of stateRecalc (blockchain/core.go:
+ * 433-464): crosslink tallies + winners, attester popcount, CalculateRewards and the
+ * next-cycle total balance.  All pointers are device pointers.  Validators are
+ * instance-major [B][nval]; this rank holds global indices [val_offset, val_offset+nval)
+ * of nval_global.  The caller zeroes `scal` and fills `winner` with 0xFF before step 1.
+ * Single GPU: pz_dev_epoch_count -> pz_dev_epoch_finish.  Multi-GPU: count ->
+ * all-reduce(sum) over the contiguous block {scal, vote, total} -> finish ->
+ * all-reduce(sum) of scal[.][PZ_SCAL_NEXT_BAL] (only the all-active rank path is
+ * supported across ranks; single-rank handles any active set). */
+#define PZ_SCAL_POP       0  /* attester bit count (deposit = 32 * this)               */
+#define PZ_SCAL_NACT      1  /* validators matching `kind` in range                     */
+#define PZ_SCAL_ERR_XL    2  /* != 0: processCrosslinks would panic                     */
+#define PZ_SCAL_ERR_RWD   3  /* != 0: CalculateRewards would panic (if threshold holds)  */
+#define PZ_SCAL_APPLIED   4  /* 1: threshold held, balances updated                     */
+#define PZ_SCAL_NEXT_BAL  5  /* sum of post-reward balances of active validators         */
+#define PZ_SCAL_MAXIDX1   6  /* 1 + max matching global index (0: none)                 */
+#define PZ_SCAL_COUNT     8
+#define PZ_XLERR_MEMBER   1ULL
+#define PZ_XLERR_BITFIELD 2ULL
+#define PZ_XLERR_SHARD    4ULL
+
+typedef struct pz_epoch_batch {
+  uint32_t ninst;                 /* B */
+  uint64_t nval;                  /* validators per instance on this rank */
+  uint64_t val_offset;            /* global index of local validator 0 */
+  uint64_t nval_global;           /* validators per instance over all ranks */
+  int kind;                       /* PZ_KIND_* (epoch transition: PZ_KIND_ACTIVE) */
+  uint64_t* balance;              /* [B][nval] in/out */
+  const uint64_t* start;          /* [B][nval] */
+  const uint64_t* end;            /* [B][nval] */
+  const uint64_t* dynasty;        /* [B] CurrentDynasty */
+  const uint64_t* total_deposit;  /* [B] TotalDeposits */
+  uint32_t natt;                  /* pending attestations per instance */
+  const uint8_t* bits;            /* CSR bitfield bytes over B*natt attestations */
+  const uint64_t* boffs;          /* [B*natt + 1] */
+  uint64_t max_inst_bytes;        /* max bitfield bytes of one instance */
+  uint32_t pop_rank, pop_world;   /* popcount chunks split over ranks (0, 1 single GPU) */
+  const uint32_t* committee;      /* committee members (global validator indices) */
+  const uint64_t* coffs;          /* [ncomm + 1] */
+  const uint32_t* att_comm;       /* [B*natt] committee id of each attestation */
+  const uint32_t* att_shard;      /* [B*natt] shard id of each attestation */
+  uint32_t nrec;                  /* crosslink records per instance */
+  const uint64_t* rec_dynasty;    /* [B][nrec] */
+  uint32_t* winner;               /* [B][nrec] out */
+  uint64_t* vote;                 /* [B*natt] out */
+  uint64_t* total;                /* [B*natt] out */
+  uint64_t* scal;                 /* [B][PZ_SCAL_COUNT] out */
+  uint64_t* act_mask;             /* [B][ceil(nval/64)] scratch (general rank path) */
+  uint32_t* blk_cnt;              /* [B][ceil(nval/2048)] scratch */
+  uint32_t* act_list;             /* [B][nval_global] scratch (general rank path) */
+} pz_epoch_batch;
+
+/* Pass 1 (pre-reward balances): classify/count, attester popcount, crosslink tallies. */
+int pz_dev_epoch_count(const pz_epoch_batch* b, void* stream);
+/* Pass 2 (after any cross-rank all-reduce): winners, active-list compaction when needed,
+ * rewards in place and the post-reward total. */
+int pz_dev_epoch_finish(const pz_epoch_batch* b, void* stream);
 
 #ifdef __cplusplus
 }

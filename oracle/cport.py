@@ -35,3 +35,70 @@ def hash_csr(data, offsets, out_bytes=32):
     dll().oracle_blake2b512_csr(data.ctypes.data if data.size else None, offsets.ctypes.data, n,
                                 out.ctypes.data, out_bytes)
     return out
+
+
+def _epoch_sig(d):
+    vp, u64, sz = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t
+    d.oracle_epoch_build.restype = vp
+    d.oracle_epoch_build.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, sz, vp, vp, vp, vp, sz, vp, sz, u64, u64]
+    d.oracle_epoch_run.argtypes = [vp, u64]
+    d.oracle_epoch_results.argtypes = [vp, vp, vp, vp, vp, vp]
+    d.oracle_epoch_free.argtypes = [vp]
+
+
+def _build_epoch(inst, b):
+    d = dll()
+    if not getattr(d, "_epoch_sig", False):
+        _epoch_sig(d)
+        d._epoch_sig = True
+    natt = inst["natt"]
+    ncomm = len(inst["coffs"]) - 1
+    keep = []
+
+    def P(a, dt):
+        a = np.ascontiguousarray(a, dtype=dt)
+        keep.append(a)
+        return a.ctypes.data
+
+    bo = inst["boffs"][b * natt:(b + 1) * natt + 1]
+    e = d.oracle_epoch_build(
+        P(inst["start"][b], np.uint64), P(inst["end"][b], np.uint64), P(inst["balance"][b], np.uint64),
+        inst["nval"], P(inst["bits"], np.uint8), P(bo, np.uint64),
+        P(inst["att_slot"][b * natt:(b + 1) * natt], np.uint64), P(inst["att_shard"][b * natt:(b + 1) * natt], np.uint32),
+        natt, P(inst["committee"], np.uint32), P(inst["coffs"], np.uint64),
+        P(inst["att_slot"][:ncomm].astype(np.uint32), np.uint32), P(inst["att_shard"][:ncomm], np.uint32), ncomm,
+        P(inst["rec_dynasty"][b], np.uint64), inst["rec_dynasty"].shape[1], int(inst["dynasty"][b]),
+        int(inst["total_deposit"][b]))
+    return d, e
+
+
+def epoch_instance(inst, b, slot=0):
+    """Run instance ``b`` once -> (balance, winner int64 (-1 none), applied, next_balance, panicked)."""
+    d, e = _build_epoch(inst, b)
+    try:
+        d.oracle_epoch_run(e, slot)
+        bal = np.empty(inst["nval"], dtype=np.uint64)
+        win = np.empty(inst["rec_dynasty"].shape[1], dtype=np.int64)
+        ap, pn = ctypes.c_int(0), ctypes.c_int(0)
+        nb = ctypes.c_uint64(0)
+        d.oracle_epoch_results(e, bal.ctypes.data, win.ctypes.data, ctypes.byref(ap), ctypes.byref(nb),
+                               ctypes.byref(pn))
+        return bal, win, bool(ap.value), nb.value, bool(pn.value)
+    finally:
+        d.oracle_epoch_free(e)
+
+
+def epoch_instance_timed(inst, b, min_seconds=3.0, max_reps=1000):
+    """Time repeated epoch transitions of instance ``b`` (AoS build not timed); returns the
+    number of repetitions done in the caller's timed region."""
+    import time
+    d, e = _build_epoch(inst, b)
+    try:
+        reps = 0
+        t0 = time.perf_counter()
+        while reps < max_reps and (reps == 0 or time.perf_counter() - t0 < min_seconds):
+            d.oracle_epoch_run(e, 0)
+            reps += 1
+        return reps
+    finally:
+        d.oracle_epoch_free(e)

@@ -47,7 +47,33 @@ SIGNATURES = {
     "pz_blake2b512_batch": [vp, vp, u64, vp, u32],
     "pz_dev_blake2b512_batch": [vp, vp, u64, vp, u32, vp],
     "pz_dev_blake2b512_fixed": [vp, u64, u64, u64, vp, u32, vp],
+    "pz_validator_indices": [vp, vp, u64, u64, ctypes.c_int, vp, c_u64p],
+    "pz_attesters_total_deposit": [vp, u64, c_u64p],
+    "pz_calculate_rewards": [vp, vp, vp, u64, u64, u64, vp, vp, u64, c_intp],
+    "pz_crosslink_tally": [vp, vp, u64, vp, vp, vp, u64, vp, u64, vp, vp],
+    "pz_process_crosslinks": [vp, vp, u64, vp, vp, vp, vp, u64, vp, u64, vp, u64, u64, vp, vp, vp],
+    "pz_shuffle_indices": [vp, vp, u64],
+    "pz_dev_epoch_count": [vp, vp],
+    "pz_dev_epoch_finish": [vp, vp],
 }
+
+
+class EpochBatch(ctypes.Structure):
+    """Mirror of ``pz_epoch_batch`` (include/prysm_hip.h)."""
+    _fields_ = [
+        ("ninst", ctypes.c_uint32), ("nval", u64), ("val_offset", u64), ("nval_global", u64),
+        ("kind", ctypes.c_int), ("balance", vp), ("start", vp), ("end", vp), ("dynasty", vp),
+        ("total_deposit", vp), ("natt", ctypes.c_uint32), ("bits", vp), ("boffs", vp),
+        ("max_inst_bytes", u64), ("pop_rank", ctypes.c_uint32), ("pop_world", ctypes.c_uint32),
+        ("committee", vp), ("coffs", vp), ("att_comm", vp), ("att_shard", vp),
+        ("nrec", ctypes.c_uint32), ("rec_dynasty", vp), ("winner", vp), ("vote", vp), ("total", vp),
+        ("scal", vp), ("act_mask", vp), ("blk_cnt", vp), ("act_list", vp),
+    ]
+
+
+SCAL_POP, SCAL_NACT, SCAL_ERR_XL, SCAL_ERR_RWD, SCAL_APPLIED, SCAL_NEXT_BAL, SCAL_MAXIDX1 = range(7)
+SCAL_COUNT = 8
+KIND_ACTIVE, KIND_EXITED, KIND_QUEUED = 0, 1, 2
 _RESTYPES = {"pz_last_error": ctypes.c_char_p}
 
 

@@ -1,0 +1,122 @@
+"""Host-side mirror of the reference's ``beacon-chain/casper`` package over the HIP C ABI.
+
+Validators are SoA numpy arrays (``start``, ``end``, ``balance``: uint64) — the packing a
+cgo shim does from ``[]*pb.ValidatorRecord``.  Pending attestations are CSR bitfields
+(``bits``: uint8 bytes, ``boffs``: uint64 offsets[natt+1]).  Errors mirror Go: a panic in
+the reference raises ``PzError`` with code ``PZ_EINDEX``.
+
+Functions that are sequential by nature (``ShuffleIndices``, committee splitting) run on the
+host by design (BASELINE.json north_star); everything data-parallel runs on the GPU.
+"""
+import ctypes
+
+import numpy as np
+
+from prysm_amd import _lib
+from prysm_amd._lib import KIND_ACTIVE, KIND_EXITED, KIND_QUEUED, lib, ptr
+from prysm_amd.params import CYCLE_LENGTH, MIN_COMMITTEE_SIZE, SHARD_COUNT
+
+_u64 = np.uint64
+
+
+def _arr(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+def _indices(start, end, dynasty, kind):
+    start, end = _arr(start, _u64), _arr(end, _u64)
+    n = start.shape[0]
+    out = np.empty(max(n, 1), dtype=np.uint32)
+    cnt = ctypes.c_uint64(0)
+    lib.call("pz_validator_indices", ptr(start), ptr(end), n, int(dynasty), kind, ptr(out), ctypes.byref(cnt))
+    return out[:cnt.value].copy()
+
+
+def active_validator_indices(start, end, dynasty):
+    """casper/validator.go:45-53 (empty array where Go returns nil)."""
+    return _indices(start, end, dynasty, KIND_ACTIVE)
+
+
+def exited_validator_indices(start, end, dynasty):
+    """casper/validator.go:57-65."""
+    return _indices(start, end, dynasty, KIND_EXITED)
+
+
+def queued_validator_indices(start, end, dynasty):
+    """casper/validator.go:69-77."""
+    return _indices(start, end, dynasty, KIND_QUEUED)
+
+
+def get_attesters_total_deposit(bits):
+    """casper/validator.go:93-102 over the concatenated bitfield bytes of all attestations."""
+    bits = _arr(bits, np.uint8)
+    out = ctypes.c_uint64(0)
+    lib.call("pz_attesters_total_deposit", ptr(bits), bits.size, ctypes.byref(out))
+    return out.value
+
+
+def calculate_rewards(balance, start, end, dynasty, total_deposit, bits, boffs):
+    """casper/incentives.go:14-32.  ``balance`` (uint64, C-contiguous) is updated in place,
+    like the reference mutating ``validators[i].Balance``.  Returns True when the 2/3
+    threshold held (rewards applied)."""
+    assert isinstance(balance, np.ndarray) and balance.dtype == _u64 and balance.flags["C_CONTIGUOUS"]
+    start, end = _arr(start, _u64), _arr(end, _u64)
+    bits, boffs = _arr(bits, np.uint8), _arr(boffs, _u64)
+    natt = max(boffs.shape[0] - 1, 0)
+    applied = ctypes.c_int(0)
+    lib.call("pz_calculate_rewards", ptr(balance), ptr(start), ptr(end), balance.shape[0], int(dynasty),
+             int(total_deposit), ptr(bits), ptr(boffs) if natt else None, natt, ctypes.byref(applied))
+    return bool(applied.value)
+
+
+def shuffle_indices(seed32, validator_list):
+    """utils/shuffle.go:14-33 (host swap chain; seed stream hashed on the GPU).  In place on a
+    uint32 array; returns it."""
+    lst = validator_list if isinstance(validator_list, np.ndarray) else np.array(validator_list, dtype=np.uint32)
+    assert lst.dtype == np.uint32 and lst.flags["C_CONTIGUOUS"]
+    seed = np.frombuffer(bytes(seed32).ljust(32, b"\0")[:32], dtype=np.uint8).copy()
+    lib.call("pz_shuffle_indices", ptr(seed), ptr(lst), lst.shape[0])
+    return lst
+
+
+def split_indices(l, n):
+    """utils/shuffle.go:36-44."""
+    return [l[len(l) * i // n: len(l) * (i + 1) // n] for i in range(n)]
+
+
+def get_committee_params(num_validators):
+    """casper/sharding.go:60-73."""
+    if num_validators >= CYCLE_LENGTH * MIN_COMMITTEE_SIZE:
+        return num_validators // (CYCLE_LENGTH * MIN_COMMITTEE_SIZE * 2) + 1, 1
+    spc = 1
+    while num_validators * spc < MIN_COMMITTEE_SIZE * CYCLE_LENGTH and spc < CYCLE_LENGTH:
+        spc *= 2
+    return 1, spc
+
+
+def split_by_slot_shard(shuffled, crosslink_start_shard):
+    """casper/sharding.go:27-53 -> [slot][(shard_id, committee uint32 array)]."""
+    cps, spc = get_committee_params(len(shuffled))
+    out = []
+    for i, vs in enumerate(split_indices(shuffled, CYCLE_LENGTH)):
+        shard_start = crosslink_start_shard + i * cps // spc
+        out.append([((shard_start + j) % SHARD_COUNT, np.asarray(c, dtype=np.uint32))
+                    for j, c in enumerate(split_indices(vs, cps))])
+    return out
+
+
+def shuffle_validators_to_committees(seed32, start, end, dynasty, crosslink_start_shard):
+    """casper/sharding.go:11-21."""
+    idx = active_validator_indices(start, end, dynasty)
+    return split_by_slot_shard(shuffle_indices(seed32, idx), crosslink_start_shard)
+
+
+def rotate_validator_set(balance, start, end, dynasty):
+    """casper/validator.go:17-41 over the GPU filters (in place on ``start``/``end``)."""
+    active = active_validator_indices(start, end, dynasty)
+    upper = len(active) // 30 + 1
+    low = active[balance[active] < 16]
+    end[low] = dynasty
+    queued = queued_validator_indices(start, end, dynasty)
+    start[queued[:min(upper, len(queued))]] = dynasty
+    return start, end

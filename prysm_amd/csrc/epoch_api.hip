@@ -1,0 +1,354 @@
+// C-ABI entry points for the T/R part of the hot path (include/prysm_hip.h): host-pointer
+// drop-ins for the casper / blockchain Go functions, the device-resident batched epoch API,
+// and the host-resident ShuffleIndices.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "epoch.h"
+#include "runtime.h"
+
+namespace pz {
+namespace {
+
+// Copies host arrays into the context's staging slots and tracks the stream.
+struct Stager {
+  DeviceCtx* c;
+  hipStream_t s;
+  int next = 0;
+  int rc = PZ_OK;
+
+  template <typename T>
+  T* up(const T* host, size_t count) {
+    if (rc) return nullptr;
+    DevBuf& b = c->slot[next++];
+    size_t bytes = count * sizeof(T);
+    if ((rc = b.reserve(bytes ? bytes : 16))) return nullptr;
+    if (bytes && host) {
+      hipError_t e = hipMemcpyAsync(b.ptr, host, bytes, hipMemcpyHostToDevice, s);
+      if (e != hipSuccess) { rc = hip_fail(e, "hipMemcpyAsync H2D"); return nullptr; }
+    }
+    return static_cast<T*>(b.ptr);
+  }
+  template <typename T>
+  T* zeros(size_t count, int byte = 0) {
+    if (rc) return nullptr;
+    DevBuf& b = c->slot[next++];
+    size_t bytes = count * sizeof(T);
+    if ((rc = b.reserve(bytes ? bytes : 16))) return nullptr;
+    if (bytes) {
+      hipError_t e = hipMemsetAsync(b.ptr, byte, bytes, s);
+      if (e != hipSuccess) { rc = hip_fail(e, "hipMemsetAsync"); return nullptr; }
+    }
+    return static_cast<T*>(b.ptr);
+  }
+  template <typename T>
+  int down(T* host, const T* dev, size_t count) {
+    if (rc || !count) return rc;
+    hipError_t e = hipMemcpyAsync(host, dev, count * sizeof(T), hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync D2H");
+    return rc;
+  }
+  int sync() {
+    if (rc) return rc;
+    hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+    return rc;
+  }
+  int check(hipError_t e, const char* what) {
+    if (!rc && e != hipSuccess) rc = hip_fail(e, what);
+    return rc;
+  }
+};
+
+// Host CSR offsets rebased to 0 (so device buffers hold only the referenced bytes).
+std::vector<uint64_t> rebase(const uint64_t* offs, uint64_t n) {
+  std::vector<uint64_t> r(n + 1);
+  for (uint64_t i = 0; i <= n; ++i) r[i] = offs[i] - offs[0];
+  return r;
+}
+
+int check_csr(const uint64_t* offs, uint64_t n, const char* what) {
+  if (!offs) return fail(PZ_EINVAL, "%s offsets are null", what);
+  for (uint64_t i = 0; i < n; ++i)
+    if (offs[i + 1] < offs[i]) return fail(PZ_EINVAL, "%s offsets not monotone at %llu", what, (unsigned long long)i);
+  return PZ_OK;
+}
+
+EpochArgs blank_args() {
+  EpochArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.ninst = 1;
+  a.pop_world = 1;
+  return a;
+}
+
+}  // namespace
+}  // namespace pz
+
+using namespace pz;
+
+extern "C" {
+
+int pz_validator_indices(const uint64_t* start, const uint64_t* end, uint64_t n, uint64_t dynasty,
+                         int kind, uint32_t* out, uint64_t* count) {
+  if (!count) return fail(PZ_EINVAL, "count is null");
+  if (kind < PZ_KIND_ACTIVE || kind > PZ_KIND_QUEUED) return fail(PZ_EINVAL, "bad kind %d", kind);
+  *count = 0;
+  if (n == 0) return PZ_OK;
+  if (!start || !end || !out) return fail(PZ_EINVAL, "null pointer");
+  DeviceCtx* c;
+  int rc = acquire(&c);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = c->ensure_stream())) return rc;
+  Stager st{c, c->stream};
+  EpochArgs a = blank_args();
+  a.nval = a.nval_global = n;
+  a.kind = kind;
+  a.start = st.up(start, n);
+  a.end = st.up(end, n);
+  a.dynasty = st.up(&dynasty, 1);
+  a.scal = st.zeros<uint64_t>(kScal);
+  a.act_mask = st.zeros<uint64_t>((n + 63) / 64);
+  a.blk_cnt = st.zeros<uint32_t>(vblocks_per_inst(n));
+  a.act_list = st.zeros<uint32_t>(n);
+  if (st.rc) return st.rc;
+  st.check(launch_epoch_count(a, true, false, false, st.s), "pz_epoch_count_kernel");
+  st.check(launch_epoch_compact(a, true, st.s), "pz_epoch_compact_kernel");
+  uint64_t scal[kScal];
+  st.down(scal, a.scal, kScal);
+  if (st.sync()) return st.rc;
+  *count = scal[kNact];
+  st.down(out, a.act_list, scal[kNact]);
+  return st.sync();
+}
+
+int pz_attesters_total_deposit(const uint8_t* bits, uint64_t nbytes, uint64_t* out) {
+  if (!out) return fail(PZ_EINVAL, "out is null");
+  *out = 0;
+  if (nbytes == 0) return PZ_OK;
+  if (!bits) return fail(PZ_EINVAL, "bits is null");
+  DeviceCtx* c;
+  int rc = acquire(&c);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = c->ensure_stream())) return rc;
+  Stager st{c, c->stream};
+  EpochArgs a = blank_args();
+  const uint64_t offs[2] = {0, nbytes};
+  a.natt = 1;
+  a.bits = st.up(bits, nbytes);
+  a.boffs = st.up(offs, 2);
+  a.max_inst_bytes = nbytes;
+  a.scal = st.zeros<uint64_t>(kScal);
+  if (st.rc) return st.rc;
+  st.check(launch_epoch_count(a, false, true, false, st.s), "pz_epoch_count_kernel");
+  uint64_t scal[kScal];
+  st.down(scal, a.scal, kScal);
+  if (st.sync()) return st.rc;
+  *out = scal[kPop] * PZ_DEFAULT_BALANCE;  // uint64 wrap, casper/validator.go:101
+  return PZ_OK;
+}
+
+int pz_calculate_rewards(uint64_t* balance, const uint64_t* start, const uint64_t* end, uint64_t n,
+                         uint64_t dynasty, uint64_t total_deposit, const uint8_t* bits,
+                         const uint64_t* boffs, uint64_t natt, int* applied) {
+  if (applied) *applied = 0;
+  if (n && (!balance || !start || !end)) return fail(PZ_EINVAL, "null validator arrays");
+  if (natt) {
+    int rc0 = check_csr(boffs, natt, "bitfield");
+    if (rc0) return rc0;
+  }
+  if (natt > 0xffffffffull) return fail(PZ_EINVAL, "too many attestations");
+  DeviceCtx* c;
+  int rc = acquire(&c);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = c->ensure_stream())) return rc;
+  Stager st{c, c->stream};
+  EpochArgs a = blank_args();
+  a.nval = a.nval_global = n;
+  a.kind = PZ_KIND_ACTIVE;
+  a.balance = st.up(balance, n);
+  a.start = st.up(start, n);
+  a.end = st.up(end, n);
+  a.dynasty = st.up(&dynasty, 1);
+  a.total_deposit = st.up(&total_deposit, 1);
+  a.natt = (uint32_t)natt;
+  std::vector<uint64_t> rb;
+  if (natt) {
+    rb = rebase(boffs, natt);
+    a.bits = st.up(bits ? bits + boffs[0] : bits, rb[natt]);
+    a.boffs = st.up(rb.data(), natt + 1);
+    a.max_inst_bytes = rb[natt];
+  }
+  a.scal = st.zeros<uint64_t>(kScal);
+  a.act_mask = st.zeros<uint64_t>((n + 63) / 64);
+  a.blk_cnt = st.zeros<uint32_t>(vblocks_per_inst(n));
+  a.act_list = st.zeros<uint32_t>(n ? n : 1);
+  if (st.rc) return st.rc;
+  if (natt && rb[natt] && !bits) return fail(PZ_EINVAL, "bits is null");
+  st.check(launch_epoch_count(a, true, true, false, st.s), "pz_epoch_count_kernel");
+  st.check(launch_epoch_compact(a, false, st.s), "pz_epoch_compact_kernel");
+  st.check(launch_epoch_reward(a, st.s), "pz_epoch_reward_kernel");
+  uint64_t scal[kScal];
+  st.down(scal, a.scal, kScal);
+  if (st.sync()) return st.rc;
+  const uint64_t dep = scal[kPop] * PZ_DEFAULT_BALANCE;
+  const bool thr = dep * 3ull >= total_deposit * 2ull;
+  if (thr && scal[kNact] > 0 && scal[kErrRwd])
+    return fail(PZ_EINDEX, natt ? "CheckBit index out of range (incentives.go:23)"
+                                : "index out of range [-1]: no attestations (incentives.go:23)");
+  if (applied) *applied = scal[kApplied] ? 1 : 0;
+  if (scal[kApplied]) {
+    st.down(balance, a.balance, n);
+    return st.sync();
+  }
+  return PZ_OK;
+}
+
+static int xl_common(const uint32_t* committee, const uint64_t* coffs, uint64_t ncomm,
+                     const uint32_t* att_committee, const uint32_t* att_shard, const uint8_t* bits,
+                     const uint64_t* boffs, uint64_t natt, const uint64_t* balance, uint64_t nval,
+                     const uint64_t* rec_dynasty, uint64_t nrec, uint64_t dynasty, uint32_t* winner,
+                     uint64_t* vote_out, uint64_t* total_out) {
+  if (natt == 0) {
+    for (uint64_t s = 0; winner && s < nrec; ++s) winner[s] = 0xffffffffu;
+    return PZ_OK;
+  }
+  if (!att_committee || !vote_out || !total_out) return fail(PZ_EINVAL, "null pointer");
+  if (natt > 0xffffffffull || nrec > 0xffffffffull) return fail(PZ_EINVAL, "sizes exceed 32 bits");
+  int rc;
+  if ((rc = check_csr(coffs, ncomm, "committee"))) return rc;
+  if ((rc = check_csr(boffs, natt, "bitfield"))) return rc;
+  for (uint64_t i = 0; i < natt; ++i)
+    if (att_committee[i] >= ncomm) return fail(PZ_EINVAL, "attestation %llu names committee %u of %llu",
+                                               (unsigned long long)i, att_committee[i], (unsigned long long)ncomm);
+  DeviceCtx* c;
+  if ((rc = acquire(&c))) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = c->ensure_stream())) return rc;
+  Stager st{c, c->stream};
+  EpochArgs a = blank_args();
+  a.nval = a.nval_global = nval;
+  a.balance = st.up(const_cast<uint64_t*>(balance), nval);
+  a.natt = (uint32_t)natt;
+  std::vector<uint64_t> rb = rebase(boffs, natt), rc_ = rebase(coffs, ncomm);
+  a.bits = st.up(bits ? bits + boffs[0] : bits, rb[natt]);
+  a.boffs = st.up(rb.data(), natt + 1);
+  a.max_inst_bytes = rb[natt];
+  a.committee = st.up(committee ? committee + coffs[0] : committee, rc_[ncomm]);
+  a.coffs = st.up(rc_.data(), ncomm + 1);
+  a.att_comm = st.up(att_committee, natt);
+  a.vote = st.zeros<uint64_t>(natt);
+  a.total = st.zeros<uint64_t>(natt);
+  a.scal = st.zeros<uint64_t>(kScal);
+  if (winner) {
+    a.att_shard = st.up(att_shard, natt);
+    a.nrec = (uint32_t)nrec;
+    a.rec_dynasty = st.up(rec_dynasty, nrec);
+    a.winner = st.zeros<uint32_t>(nrec, 0xff);
+    std::vector<uint64_t> dyn(1, dynasty);
+    a.dynasty = st.up(dyn.data(), 1);
+    if (st.rc) return st.rc;
+    if (!att_shard || (nrec && !rec_dynasty)) return fail(PZ_EINVAL, "null crosslink record arrays");
+  }
+  if (st.rc) return st.rc;
+  st.check(launch_epoch_count(a, false, false, true, st.s), "pz_epoch_count_kernel");
+  if (winner) st.check(launch_epoch_winners(a, st.s), "pz_epoch_winner_kernel");
+  uint64_t scal[kScal];
+  st.down(scal, a.scal, kScal);
+  st.down(vote_out, a.vote, natt);
+  st.down(total_out, a.total, natt);
+  if (winner) st.down(winner, a.winner, nrec);
+  if (st.sync()) return st.rc;
+  if (scal[kErrXl]) {
+    const uint64_t e = scal[kErrXl];
+    return fail(PZ_EINDEX, "processCrosslinks would panic:%s%s%s",
+                (e & kErrMember) ? " committee member >= len(validators)" : "",
+                (e & kErrBitfield) ? " bitfield shorter than committee (CheckBit)" : "",
+                (e & kErrShard) ? " shard id >= len(crosslinkRecords)" : "");
+  }
+  return PZ_OK;
+}
+
+int pz_crosslink_tally(const uint32_t* committee, const uint64_t* coffs, uint64_t ncomm,
+                       const uint32_t* att_committee, const uint8_t* bits, const uint64_t* boffs,
+                       uint64_t natt, const uint64_t* balance, uint64_t nval, uint64_t* vote_out,
+                       uint64_t* total_out) {
+  return xl_common(committee, coffs, ncomm, att_committee, nullptr, bits, boffs, natt, balance, nval,
+                   nullptr, 0, 0, nullptr, vote_out, total_out);
+}
+
+int pz_process_crosslinks(const uint32_t* committee, const uint64_t* coffs, uint64_t ncomm,
+                          const uint32_t* att_committee, const uint32_t* att_shard,
+                          const uint8_t* bits, const uint64_t* boffs, uint64_t natt,
+                          const uint64_t* balance, uint64_t nval, const uint64_t* rec_dynasty,
+                          uint64_t nrec, uint64_t dynasty, uint32_t* winner, uint64_t* vote_out,
+                          uint64_t* total_out) {
+  if (!winner) return fail(PZ_EINVAL, "winner is null");
+  return xl_common(committee, coffs, ncomm, att_committee, att_shard, bits, boffs, natt, balance, nval,
+                   rec_dynasty, nrec, dynasty, winner, vote_out, total_out);
+}
+
+// ---- device-resident batched epoch -------------------------------------------------------
+static int check_batch(const pz_epoch_batch* b) {
+  if (!b) return fail(PZ_EINVAL, "batch is null");
+  if (!b->ninst || !b->scal || !b->dynasty || !b->start || !b->end || !b->balance)
+    return fail(PZ_EINVAL, "batch: missing validator arrays / scal");
+  if (b->nval_global < b->val_offset + b->nval) return fail(PZ_EINVAL, "batch: shard exceeds nval_global");
+  if (b->natt && (!b->bits || !b->boffs)) return fail(PZ_EINVAL, "batch: missing bitfields");
+  if (b->committee && b->natt && (!b->coffs || !b->att_comm || !b->vote || !b->total))
+    return fail(PZ_EINVAL, "batch: missing committee arrays");
+  if (b->pop_world == 0 || b->pop_rank >= b->pop_world) return fail(PZ_EINVAL, "batch: bad pop split");
+  return PZ_OK;
+}
+
+int pz_dev_epoch_count(const pz_epoch_batch* b, void* stream) {
+  int rc = check_batch(b);
+  if (rc) return rc;
+  hipError_t e = launch_epoch_count(*b, true, true, b->committee != nullptr, (hipStream_t)stream);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "pz_epoch_count_kernel");
+}
+
+int pz_dev_epoch_finish(const pz_epoch_batch* b, void* stream) {
+  int rc = check_batch(b);
+  if (rc) return rc;
+  if (!b->total_deposit) return fail(PZ_EINVAL, "batch: total_deposit is null");
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipSuccess;
+  if (b->committee && b->natt && b->nrec && b->winner && b->att_shard && b->rec_dynasty)
+    e = launch_epoch_winners(*b, s);
+  if (e == hipSuccess && b->nval == b->nval_global && b->act_mask && b->blk_cnt && b->act_list)
+    e = launch_epoch_compact(*b, false, s);
+  if (e == hipSuccess) e = launch_epoch_reward(*b, s);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "epoch finish");
+}
+
+// ---- host-resident shuffle ---------------------------------------------------------------
+int pz_shuffle_indices(const uint8_t seed[32], uint32_t* list, uint64_t n) {
+  if (n > PZ_MAX_VALIDATORS) return fail(PZ_ETOOMANY, "Validator count has exceeded MaxValidator Count");
+  if (!seed) return fail(PZ_EINVAL, "seed is null");
+  if (n && !list) return fail(PZ_EINVAL, "list is null");
+  uint8_t hs[64];
+  const uint64_t offs[2] = {0, 32};
+  int rc = pz_blake2b512_batch(seed, offs, 1, hs, 64);  // utils/shuffle.go:19 (on the GPU)
+  if (rc) return rc;
+  uint32_t sw[21];  // utils/shuffle.go:25-26: byte-wrapped sum of 3 seed bytes, j = 0,3,..,60
+  for (int j = 0, k = 0; j + 3 < 64; j += 3, ++k) sw[k] = (uint8_t)(hs[j] + hs[j + 1] + hs[j + 2]);
+  for (uint64_t i = 0; i + 1 < n; ++i) {
+    const uint64_t rem = n - i;
+    for (int k = 0; k < 21; ++k) {
+      const uint64_t p = sw[k] % rem + i;
+      const uint32_t t = list[i];
+      list[i] = list[p];
+      list[p] = t;
+    }
+  }
+  return PZ_OK;
+}
+
+}  // extern "C"

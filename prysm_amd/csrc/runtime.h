@@ -22,7 +22,8 @@ struct DeviceCtx {
   int device = 0;
   std::mutex mu;
   hipStream_t stream = nullptr;
-  DevBuf in, out, aux, aux2, aux3, aux4, aux5, aux6;
+  DevBuf in, out, aux;
+  DevBuf slot[24];  // staging for the T/R host-pointer entry points
   static DeviceCtx* get(int dev);
   int ensure_stream();
 };

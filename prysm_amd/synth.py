@@ -28,6 +28,67 @@ def _varint_fixed(values, width):
     return out
 
 
+def committees_csr(shuffled, crosslink_start_shard=0):
+    """casper/sharding.go:27-53 on a shuffled index list -> (committee uint32, coffs uint64,
+    slot_of uint32, shard_of uint32) with committees ordered slot-major."""
+    from prysm_amd.casper import split_by_slot_shard
+    members, offs, slots, shards = [], [0], [], []
+    for s, arr in enumerate(split_by_slot_shard(list(shuffled), crosslink_start_shard)):
+        for shard, c in arr:
+            members.append(np.asarray(c, dtype=np.uint32))
+            offs.append(offs[-1] + len(c))
+            slots.append(s)
+            shards.append(shard)
+    return (np.concatenate(members) if members else np.zeros(0, np.uint32), np.array(offs, dtype=np.uint64),
+            np.array(slots, dtype=np.uint32), np.array(shards, dtype=np.uint32))
+
+
+def epoch_batch(nval, ninst, seed=3, shuffled=None, density=0.75, last_bits=None):
+    """Synthetic epoch instances shaped like BASELINE configs[2]/[3]:
+    all validators active (start 0, end DefaultEndDynasty), balances 32 +- jitter in
+    [16, 48], one attestation per committee (~75% (density 0.75) or ~50% bits set, trailing bits zero) plus a
+    final attestation whose bitfield has ``nval`` bits (the incentives_test.go:24-25 shape),
+    TotalDeposits = sum(balance), CurrentDynasty 1, crosslink records at dynasty 0.
+    ``shuffled`` is the shuffled active index list (ShuffleIndices(Hash{'A'}, 0..N-1)); the
+    committees are shared by all instances."""
+    from prysm_amd.params import DEFAULT_END_DYNASTY
+    rng = np.random.default_rng(seed)
+    if shuffled is None:
+        shuffled = np.arange(nval, dtype=np.uint32)
+    committee, coffs, c_slot, c_shard = committees_csr(shuffled)
+    ncomm = len(coffs) - 1
+    natt = ncomm + 1
+    sizes = np.diff(coffs).astype(np.int64)
+    start = np.zeros((ninst, nval), dtype=np.uint64)
+    end = np.full((ninst, nval), DEFAULT_END_DYNASTY, dtype=np.uint64)
+    balance = rng.integers(16, 49, size=(ninst, nval), dtype=np.uint64)
+    kfinal = last_bits if last_bits is not None else nval
+    blens = np.concatenate([(sizes + 7) // 8, [(kfinal + 7) // 8]])
+    per_inst = int(blens.sum())
+    boffs = np.zeros(ninst * natt + 1, dtype=np.uint64)
+    boffs[1:] = np.cumsum(np.tile(blens, ninst))
+    # ~75% of bits set (OR of two uniform bytes), then the trailing pad bits of every
+    # bitfield cleared (validateAttesterBitfields, core.go:384-392)
+    bits = rng.integers(0, 256, size=ninst * per_inst, dtype=np.uint8)
+    if density >= 0.75:
+        bits |= rng.integers(0, 256, size=ninst * per_inst, dtype=np.uint8)
+    kbits = np.concatenate([sizes, [kfinal]])
+    tail = (kbits % 8).astype(np.uint8)
+    last_byte = np.tile(np.cumsum(blens) - 1, ninst) + np.repeat(np.arange(ninst) * per_inst, natt)
+    keep = np.tile(np.where(tail == 0, 0xFF, (0xFF << (8 - tail)) & 0xFF).astype(np.uint8), ninst)
+    bits[last_byte] &= keep
+    att_comm = np.tile(np.concatenate([np.arange(ncomm), [ncomm - 1]]).astype(np.uint32), ninst)
+    att_shard = np.tile(np.concatenate([c_shard, [c_shard[-1]]]).astype(np.uint32), ninst)
+    att_slot = np.tile(np.concatenate([c_slot, [c_slot[-1]]]).astype(np.uint64), ninst)
+    with np.errstate(over="ignore"):
+        total = balance.sum(axis=1, dtype=np.uint64)
+    return dict(nval=nval, ninst=ninst, natt=natt, start=start, end=end, balance=balance,
+                dynasty=np.ones(ninst, dtype=np.uint64), total_deposit=total, bits=bits, boffs=boffs,
+                committee=committee, coffs=coffs, att_comm=att_comm, att_shard=att_shard,
+                att_slot=att_slot, rec_dynasty=np.zeros((ninst, 1024), dtype=np.uint64),
+                max_inst_bytes=per_inst)
+
+
 def attestation_records_512(n, seed=2):
     """(n, 512) uint8 array of canonical AttestationRecord encodings."""
     rng = np.random.default_rng(seed)

@@ -1,6 +1,6 @@
-// Microbenchmark: issue rate of the VALU instructions the BLAKE2b kernel is made of, on
-// every CU (gfx950).  Each lane runs 8 independent chains of one instruction in inline asm;
-// the rate is reported as lane-instructions per second and per CU-cycle at the measured clock.
+// Microbenchmark: issue rate of candidate VALU instructions for the BLAKE2b G function on
+// every CU (gfx950).  Each lane runs 8 independent register chains of one instruction form
+// in inline asm; rates are reported per CU-cycle at 2.4 GHz and relative to v_xor_b32.
 // Build: hipcc --offload-arch=gfx950 -O3 tools/valu_rates.hip -o build/valu_rates
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -8,67 +8,91 @@
 
 #define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
+#define X4(ins) ins "\n" ins "\n" ins "\n" ins
 template <int OP>
-__global__ void __launch_bounds__(256) k(uint32_t* out, int iters, uint64_t* clk) {
+__global__ void __launch_bounds__(256) k(uint32_t* out, int iters) {
   uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
   uint32_t b0 = a0 * 3, b1 = a1 * 3, b2 = a2 * 3, b3 = a3 * 3, b4 = a4 * 3, b5 = a5 * 3, b6 = a6 * 3, b7 = a7 * 3;
-  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+  const uint32_t sel = __builtin_amdgcn_readfirstlane(0x05040706u + (iters >> 30));
   for (int i = 0; i < iters; ++i) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      if (OP == 0) {  // v_xor_b32
-        asm volatile("v_xor_b32 %0, %0, %1\n v_xor_b32 %2, %2, %3\n v_xor_b32 %4, %4, %5\n v_xor_b32 %6, %6, %7" : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1), "+v"(a2), "+v"(b2), "+v"(a3), "+v"(b3));
-        asm volatile("v_xor_b32 %0, %0, %1\n v_xor_b32 %2, %2, %3\n v_xor_b32 %4, %4, %5\n v_xor_b32 %6, %6, %7" : "+v"(a4), "+v"(b4), "+v"(a5), "+v"(b5), "+v"(a6), "+v"(b6), "+v"(a7), "+v"(b7));
-      } else if (OP == 1) {  // v_alignbit_b32
-        asm volatile("v_alignbit_b32 %0, %0, %1, 24\n v_alignbit_b32 %2, %2, %3, 24\n v_alignbit_b32 %4, %4, %5, 24\n v_alignbit_b32 %6, %6, %7, 24" : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1), "+v"(a2), "+v"(b2), "+v"(a3), "+v"(b3));
-        asm volatile("v_alignbit_b32 %0, %0, %1, 24\n v_alignbit_b32 %2, %2, %3, 24\n v_alignbit_b32 %4, %4, %5, 24\n v_alignbit_b32 %6, %6, %7, 24" : "+v"(a4), "+v"(b4), "+v"(a5), "+v"(b5), "+v"(a6), "+v"(b6), "+v"(a7), "+v"(b7));
-      } else if (OP == 2) {  // v_lshl_add_u64 (64-bit add)
-        asm volatile("v_lshl_add_u64 %0, %0, 0, %1\n v_lshl_add_u64 %2, %2, 0, %3" : "+v"(*(uint64_t*)&a0), "+v"(*(uint64_t*)&b0), "+v"(*(uint64_t*)&a2), "+v"(*(uint64_t*)&b2));
-        asm volatile("v_lshl_add_u64 %0, %0, 0, %1\n v_lshl_add_u64 %2, %2, 0, %3" : "+v"(*(uint64_t*)&a4), "+v"(*(uint64_t*)&b4), "+v"(*(uint64_t*)&a6), "+v"(*(uint64_t*)&b6));
-      } else {  // v_add_co_u32 + v_addc_co_u32 pair (64-bit add the other way), counted as 2
-        asm volatile("v_add_co_u32 %0, vcc, %0, %1\n v_addc_co_u32 %2, vcc, %2, %3, vcc" : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1) :: "vcc");
-        asm volatile("v_add_co_u32 %0, vcc, %0, %1\n v_addc_co_u32 %2, vcc, %2, %3, vcc" : "+v"(a2), "+v"(b2), "+v"(a3), "+v"(b3) :: "vcc");
-        asm volatile("v_add_co_u32 %0, vcc, %0, %1\n v_addc_co_u32 %2, vcc, %2, %3, vcc" : "+v"(a4), "+v"(b4), "+v"(a5), "+v"(b5) :: "vcc");
-        asm volatile("v_add_co_u32 %0, vcc, %0, %1\n v_addc_co_u32 %2, vcc, %2, %3, vcc" : "+v"(a6), "+v"(b6), "+v"(a7), "+v"(b7) :: "vcc");
+#define EIGHT(fmt) \
+  asm volatile(fmt : "+v"(a0) : "v"(b0)); asm volatile(fmt : "+v"(a1) : "v"(b1)); \
+  asm volatile(fmt : "+v"(a2) : "v"(b2)); asm volatile(fmt : "+v"(a3) : "v"(b3)); \
+  asm volatile(fmt : "+v"(a4) : "v"(b4)); asm volatile(fmt : "+v"(a5) : "v"(b5)); \
+  asm volatile(fmt : "+v"(a6) : "v"(b6)); asm volatile(fmt : "+v"(a7) : "v"(b7));
+      if (OP == 0) { EIGHT("v_xor_b32 %0, %0, %1") }
+      else if (OP == 1) { EIGHT("v_alignbit_b32 %0, %0, %1, 24") }
+      else if (OP == 2) {  // selector from an SGPR (VOP3 takes no literal on gfx9)
+#define PERM(a, b) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "s"(sel));
+        PERM(a0, b0) PERM(a1, b1) PERM(a2, b2) PERM(a3, b3) PERM(a4, b4) PERM(a5, b5) PERM(a6, b6) PERM(a7, b7)
+      }
+      else if (OP == 3) { EIGHT("v_add_u32 %0, %0, %1") }
+      else if (OP == 4) { EIGHT("v_add3_u32 %0, %0, %1, %0") }
+      else if (OP == 5) { EIGHT("v_lshl_or_b32 %0, %0, 1, %1") }
+      else if (OP == 6) { EIGHT("v_bitop3_b32 %0, %0, %1, %0 bitop3:0x96") }
+      else if (OP == 7) {  // 64-bit add via v_lshl_add_u64, 4 independent pairs
+        asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(*(uint64_t*)&a0) : "v"(*(uint64_t*)&b0));
+        asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(*(uint64_t*)&a2) : "v"(*(uint64_t*)&b2));
+        asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(*(uint64_t*)&a4) : "v"(*(uint64_t*)&b4));
+        asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(*(uint64_t*)&a6) : "v"(*(uint64_t*)&b6));
+        asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(*(uint64_t*)&a0) : "v"(*(uint64_t*)&b0));
+        asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(*(uint64_t*)&a2) : "v"(*(uint64_t*)&b2));
+        asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(*(uint64_t*)&a4) : "v"(*(uint64_t*)&b4));
+        asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(*(uint64_t*)&a6) : "v"(*(uint64_t*)&b6));
+      } else if (OP == 8) {  // 64-bit add as v_add_co_u32 + v_addc_co_u32 with private SGPR carries
+#define ADDCO(lo, hi, blo, bhi, c) asm volatile("v_add_co_u32 %0, %2, %0, %3\n v_addc_co_u32 %1, %2, %1, %4, %2" : "+v"(lo), "+v"(hi), "=&s"(c) : "v"(blo), "v"(bhi));
+        ADDCO(a0, a1, b0, b1, c0) ADDCO(a2, a3, b2, b3, c1) ADDCO(a4, a5, b4, b5, c2) ADDCO(a6, a7, b6, b7, c3)
+      } else if (OP == 9) {  // 64-bit shift
+        asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(*(uint64_t*)&a0)); asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(*(uint64_t*)&a2));
+        asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(*(uint64_t*)&a4)); asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(*(uint64_t*)&a6));
+        asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(*(uint64_t*)&b0)); asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(*(uint64_t*)&b2));
+        asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(*(uint64_t*)&b4)); asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(*(uint64_t*)&b6));
+      } else if (OP == 10) {  // v_mad_u64_u32 (64-bit result)
+#define MAD(lo, hi, b, c) asm volatile("v_mad_u64_u32 %0, %1, %2, 1, %0" : "+v"(*(uint64_t*)&lo), "=&s"(c) : "v"(b));
+        MAD(a0, a1, b0, c0) MAD(a2, a3, b2, c1) MAD(a4, a5, b4, c2) MAD(a6, a7, b6, c3)
+        MAD(a0, a1, b1, c0) MAD(a2, a3, b3, c1) MAD(a4, a5, b5, c2) MAD(a6, a7, b7, c3)
+      } else if (OP == 11) {  // v_add_co_u32 alone (VOP3, private carries)
+#define CO(lo, b, c) asm volatile("v_add_co_u32 %0, %1, %0, %2" : "+v"(lo), "=&s"(c) : "v"(b));
+        CO(a0, b0, c0) CO(a1, b1, c1) CO(a2, b2, c2) CO(a3, b3, c3) CO(a4, b4, c0) CO(a5, b5, c1) CO(a6, b6, c2) CO(a7, b7, c3)
       }
     }
   }
-  uint64_t t1 = __builtin_amdgcn_s_memtime();
-  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
-  if (threadIdx.x == 0 && blockIdx.x == 0) *clk = t1 - t0;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7 ^ b0 ^ b2 ^ b4 ^ b6 ^ (uint32_t)(c0 ^ c1 ^ c2 ^ c3);
 }
 
+typedef void (*kfn)(uint32_t*, int);
 int main() {
-  int cus = 0;
   hipDeviceProp_t p;
   CHK(hipGetDeviceProperties(&p, 0));
-  cus = p.multiProcessorCount;
-  const int blocks = cus * 8, threads = 256, iters = 2000;
-  uint32_t* out; uint64_t* clk;
+  const int cus = p.multiProcessorCount;
+  const int blocks = cus * 8, threads = 256, iters = 1000;
+  uint32_t* out;
   CHK(hipMalloc(&out, (size_t)blocks * threads * 4));
-  CHK(hipMalloc(&clk, 8));
   hipEvent_t e0, e1;
   CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
-  const char* names[4] = {"v_xor_b32", "v_alignbit_b32", "v_lshl_add_u64", "v_add_co+v_addc_co"};
-  // instructions per lane per inner (r) iteration: 8, 8, 4, 8
-  const double per_r[4] = {8, 8, 4, 8};
-  for (int op = 0; op < 4; ++op) {
-    for (int rep = 0; rep < 2; ++rep) {
+  struct { const char* name; kfn f; double per_r; } ops[] = {
+      {"v_xor_b32", k<0>, 8}, {"v_alignbit_b32", k<1>, 8}, {"v_perm_b32", k<2>, 8},
+      {"v_add_u32", k<3>, 8}, {"v_add3_u32", k<4>, 8}, {"v_lshl_or_b32", k<5>, 8},
+      {"v_bitop3_b32", k<6>, 8}, {"v_lshl_add_u64", k<7>, 8}, {"v_add_co+v_addc_co (s carry)", k<8>, 8},
+      {"v_lshlrev_b64", k<9>, 8}, {"v_mad_u64_u32", k<10>, 8}, {"v_add_co_u32 (s carry)", k<11>, 8}};
+  double xor_rate = 0;
+  for (auto& o : ops) {
+    float best = 1e30f;
+    for (int rep = 0; rep < 3; ++rep) {
       CHK(hipEventRecord(e0));
-      if (op == 0) hipLaunchKernelGGL(k<0>, dim3(blocks), dim3(threads), 0, 0, out, iters, clk);
-      if (op == 1) hipLaunchKernelGGL(k<1>, dim3(blocks), dim3(threads), 0, 0, out, iters, clk);
-      if (op == 2) hipLaunchKernelGGL(k<2>, dim3(blocks), dim3(threads), 0, 0, out, iters, clk);
-      if (op == 3) hipLaunchKernelGGL(k<3>, dim3(blocks), dim3(threads), 0, 0, out, iters, clk);
+      hipLaunchKernelGGL(o.f, dim3(blocks), dim3(threads), 0, 0, out, iters);
       CHK(hipEventRecord(e1));
       CHK(hipEventSynchronize(e1));
       float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
-      uint64_t cyc; CHK(hipMemcpy(&cyc, clk, 8, hipMemcpyDeviceToHost));
-      double lane_ops = (double)blocks * threads * iters * 16 * per_r[op];
-      double rate = lane_ops / (ms * 1e-3);
-      if (rep == 1)
-        printf("%-20s %8.3f ms  %7.2f T lane-instr/s  (%.1f lane-instr per CU-cycle at 2.4 GHz)  block0 cycles %llu\n",
-               names[op], ms, rate / 1e12, rate / (cus * 2.4e9), (unsigned long long)cyc);
+      if (ms < best) best = ms;
     }
+    double rate = (double)blocks * threads * iters * 16 * o.per_r / (best * 1e-3);
+    if (xor_rate == 0) xor_rate = rate;
+    printf("%-30s %8.3f ms  %7.2f T lane-instr/s  %6.1f per CU-cycle@2.4GHz  rel. xor %.3f\n", o.name, best,
+           rate / 1e12, rate / (cus * 2.4e9), rate / xor_rate);
   }
   return 0;
 }
