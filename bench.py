@@ -147,14 +147,14 @@ def cpu_baseline(records_np):
         from oracle import cport
     except Exception as e:  # pragma: no cover - reported, not fatal
         return {"value": None, "unit": "hashes/s", "cores": 0, "kind": "port",
-                "sample": "unavailable: %s" % e}
+                "sample": "unavailable: %s" % e}, None
     n = records_np.shape[0]
     t0 = time.perf_counter()
-    cport.hash_fixed(records_np, 512, 32)
+    digests = cport.hash_fixed(records_np, 512, 32)
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "hashes/s", "cores": 1, "kind": "port",
             "sample": "%d x 512-B records (the full per-GPU batch), 1 thread, portable C BLAKE2b "
-                      "(oracle/c/blake2b_ref.c), %.2f s" % (n, dt)}
+                      "(oracle/c/blake2b_ref.c), %.2f s" % (n, dt)}, digests
 
 
 def main():
@@ -248,7 +248,12 @@ def main():
             },
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(recs)
+            cb, digests = cpu_baseline(recs)
+            line["cpu_baseline"] = cb
+            if digests is not None:  # the checker: GPU digests of the timed batch vs the C port
+                gpu = d_out.cpu().numpy().reshape(n, 32)
+                line["parity"] = "bit-exact vs cpu_baseline on all %d digests: %s" % (
+                    n, bool(np.array_equal(gpu, digests)))
         if epoch is not None:
             line["epoch"] = epoch
         print(json.dumps(line), flush=True)

@@ -8,6 +8,18 @@ import os
 
 import numpy as np
 
+# One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64 and loads it into the
+# global symbol scope at import; when torch is present we import it BEFORE loading our
+# library so that libprysm_hip.so binds to that same runtime (device pointers, streams and
+# events are then interchangeable with torch's).  Without torch (e.g. a cgo host) the
+# library binds to /opt/rocm's runtime.  Initialising two different HIP runtimes in one
+# process fails ("No HIP GPUs are available"), so this order is load-bearing.
+try:  # pragma: no cover - import side effect only
+    import torch  # noqa: F401
+    HAVE_TORCH = True
+except ImportError:  # pragma: no cover
+    HAVE_TORCH = False
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 library_path = os.path.join(HERE, "libprysm_hip.so")
 

@@ -10,3 +10,6 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP C-ABI)")
+
+# Load PyTorch (and its HIP runtime) before the product library: see prysm_amd/_lib.py.
+import torch  # noqa: E402,F401
