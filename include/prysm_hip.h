@@ -175,6 +175,39 @@ typedef struct pz_epoch_batch {
   uint32_t* act_list;             /* [B][nval_global] scratch (general rank path) */
 } pz_epoch_batch;
 
+/* ---- T: block vote-cache tally (blockchain/core.go:300-345 calculateBlockVoteCache) ----
+ * Each signed parent hash h has a dense slot id (host-assigned; the host keeps the 32-byte
+ * hash -> slot map exactly like the Go map key).  A work item (attestation a, slot s) adds
+ * every committee member of a whose bit is set and who is not yet in s's voter set:
+ * totals[s] += balance[v].  Slots own an nval-bit dedup bitmap (words_per_slot u32 words).
+ * Items of many blocks may share a launch as long as no balance changes between them
+ * (balances change only in stateRecalc).  *err != 0 where Go would panic. */
+typedef struct pz_vote_batch {
+  const uint32_t* committee;   /* committee members (validator indices) */
+  const uint64_t* coffs;       /* [ncomm + 1] */
+  const uint32_t* att_comm;    /* [natt] committee id of each attestation */
+  const uint8_t* bits;         /* CSR bitfields of the attestations */
+  const uint64_t* boffs;       /* [natt + 1] */
+  const uint32_t* item_att;    /* [nitems] */
+  const uint32_t* item_slot;   /* [nitems] */
+  uint64_t nitems;
+  const uint64_t* balance;     /* [nval] */
+  uint64_t nval;
+  uint32_t* bitmaps;           /* [nslots][words_per_slot] in/out */
+  uint64_t words_per_slot;     /* >= ceil(nval / 32) */
+  uint64_t* totals;            /* [nslots] in/out (VoteTotalDeposit) */
+  uint64_t* err;               /* [1] in/out */
+} pz_vote_batch;
+
+int pz_dev_vote_tally(const pz_vote_batch* b, void* stream);
+
+/* Host-pointer form: same inputs; bitmaps/totals are read and written back in place. */
+int pz_vote_tally(const uint32_t* committee, const uint64_t* coffs, uint64_t ncomm,
+                  const uint32_t* att_comm, const uint8_t* bits, const uint64_t* boffs,
+                  uint64_t natt, const uint32_t* item_att, const uint32_t* item_slot,
+                  uint64_t nitems, const uint64_t* balance, uint64_t nval, uint32_t* bitmaps,
+                  uint64_t nslots, uint64_t words_per_slot, uint64_t* totals);
+
 /* Pass 1 (pre-reward balances): classify/count, attester popcount, crosslink tallies. */
 int pz_dev_epoch_count(const pz_epoch_batch* b, void* stream);
 /* Pass 2 (after any cross-rank all-reduce): winners, active-list compaction when needed,

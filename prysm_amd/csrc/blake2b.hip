@@ -135,6 +135,7 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kRowBytes = 144;
 constexpr int kSlabBytes = 64 * kRowBytes;
 
+// Requires stride < 2^26 (64 messages x stride fit 32-bit offsets; the launcher checks).
 extern "C" __global__ void __launch_bounds__(256)
 pz_b2b_fixed_kernel(const uint8_t* __restrict__ msgs, uint64_t stride, uint64_t len, uint64_t n,
                     uint8_t* __restrict__ out, uint32_t out_bytes) {
@@ -146,24 +147,40 @@ pz_b2b_fixed_kernel(const uint8_t* __restrict__ msgs, uint64_t stride, uint64_t 
   if (m0 >= n) return;  // whole wave idle (wave-uniform)
   const uint64_t msg = m0 + lane;
   const uint64_t nblocks = len == 0 ? 1 : (len + 127) / 128;
+  // Chunk `it` of this lane: message row r = it*8 + lane/8, 16-byte part lane%8.  A wave
+  // instruction therefore reads 8 whole 128-B lines; offsets are 32-bit against the
+  // wave-uniform base (SGPR pair), so the address math stays out of the 64-bit VALU.
+  const uint8_t* wbase = msgs + m0 * stride;
+  const uint32_t lrow = (uint32_t)lane >> 3, lpart = (uint32_t)lane & 7;
+  const uint32_t s32 = (uint32_t)stride;
+  const bool full_wave = m0 + 64 <= n;
+  const uint32_t rows_left = full_wave ? 64u : (uint32_t)(n - m0);
 
   uint64_t h[8];
   init_h(h);
   for (uint64_t t = 0; t < nblocks; ++t) {
-    // ---- stage: 512 16-byte chunks (64 msgs x 8 parts), 8 per lane, coalesced per 8 lanes
+    // ---- stage: 512 16-byte chunks (64 msgs x 8 parts), 8 per lane, all loads in flight
+    const uint32_t boff = (uint32_t)t * 128u + lpart * 16u;
+    uint4 v[8];
+    if (full_wave && (t + 1 < nblocks || (len & 127) == 0)) {  // wave-uniform fast path
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int c = it * 64 + lane;
-      const int cm = c >> 3, part = c & 7;
-      const uint64_t gm = m0 + cm;
-      const uint64_t boff = t * 128 + part * 16;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (gm < n && boff < len) {
-        v = *reinterpret_cast<const uint4*>(msgs + gm * stride + boff);
-        if (boff + 16 > len) v = mask_chunk(v, (uint32_t)(len - boff));
+      for (int it = 0; it < 8; ++it)
+        v[it] = *reinterpret_cast<const uint4*>(wbase + ((it * 8u + lrow) * s32 + boff));
+    } else {  // tail wave / partial last block: clamp addresses, zero what lies outside
+      const uint32_t safe_off = boff < (uint32_t)len ? boff : 0u;
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const uint32_t r = it * 8u + lrow;
+        const bool ok = r < rows_left && boff < (uint32_t)len;
+        const uint32_t rr = r < rows_left ? r : 0u;
+        uint4 q = *reinterpret_cast<const uint4*>(wbase + (rr * s32 + safe_off));
+        if (boff + 16 > (uint32_t)len) q = mask_chunk(q, boff < (uint32_t)len ? (uint32_t)len - boff : 0u);
+        v[it] = ok ? q : make_uint4(0, 0, 0, 0);
       }
-      *reinterpret_cast<uint4*>(slab + cm * kRowBytes + part * 16) = v;
     }
+#pragma unroll
+    for (int it = 0; it < 8; ++it)
+      *reinterpret_cast<uint4*>(slab + (it * 8 + lrow) * kRowBytes + lpart * 16) = v[it];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

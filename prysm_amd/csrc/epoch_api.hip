@@ -9,6 +9,7 @@
 
 #include "epoch.h"
 #include "runtime.h"
+#include "votes.h"
 
 namespace pz {
 namespace {
@@ -326,6 +327,67 @@ int pz_dev_epoch_finish(const pz_epoch_batch* b, void* stream) {
     e = launch_epoch_compact(*b, false, s);
   if (e == hipSuccess) e = launch_epoch_reward(*b, s);
   return e == hipSuccess ? PZ_OK : hip_fail(e, "epoch finish");
+}
+
+// ---- vote-cache tally ----------------------------------------------------------------------
+int pz_dev_vote_tally(const pz_vote_batch* b, void* stream) {
+  if (!b) return fail(PZ_EINVAL, "batch is null");
+  if (!b->nitems) return PZ_OK;
+  if (!b->committee || !b->coffs || !b->att_comm || !b->bits || !b->boffs || !b->item_att || !b->item_slot ||
+      !b->balance || !b->bitmaps || !b->totals || !b->err)
+    return fail(PZ_EINVAL, "vote batch: null pointer");
+  if (b->words_per_slot * 32 < b->nval) return fail(PZ_EINVAL, "vote batch: words_per_slot too small");
+  hipError_t e = launch_vote_tally(*b, (hipStream_t)stream);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "pz_vote_tally_kernel");
+}
+
+int pz_vote_tally(const uint32_t* committee, const uint64_t* coffs, uint64_t ncomm, const uint32_t* att_comm,
+                  const uint8_t* bits, const uint64_t* boffs, uint64_t natt, const uint32_t* item_att,
+                  const uint32_t* item_slot, uint64_t nitems, const uint64_t* balance, uint64_t nval,
+                  uint32_t* bitmaps, uint64_t nslots, uint64_t words_per_slot, uint64_t* totals) {
+  if (!nitems) return PZ_OK;
+  int rc;
+  if ((rc = check_csr(coffs, ncomm, "committee"))) return rc;
+  if ((rc = check_csr(boffs, natt, "bitfield"))) return rc;
+  if (!item_att || !item_slot || !att_comm || !bitmaps || !totals) return fail(PZ_EINVAL, "null pointer");
+  if (words_per_slot * 32 < nval) return fail(PZ_EINVAL, "words_per_slot too small");
+  for (uint64_t i = 0; i < nitems; ++i) {
+    if (item_att[i] >= natt || item_slot[i] >= nslots)
+      return fail(PZ_EINVAL, "work item %llu out of range", (unsigned long long)i);
+  }
+  for (uint64_t a = 0; a < natt; ++a)
+    if (att_comm[a] >= ncomm) return fail(PZ_EINVAL, "attestation %llu names a missing committee", (unsigned long long)a);
+  DeviceCtx* c;
+  if ((rc = acquire(&c))) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = c->ensure_stream())) return rc;
+  Stager st{c, c->stream};
+  std::vector<uint64_t> rb = rebase(boffs, natt), rc_ = rebase(coffs, ncomm);
+  pz_vote_batch v;
+  std::memset(&v, 0, sizeof v);
+  v.committee = st.up(committee ? committee + coffs[0] : committee, rc_[ncomm]);
+  v.coffs = st.up(rc_.data(), ncomm + 1);
+  v.att_comm = st.up(att_comm, natt);
+  v.bits = st.up(bits ? bits + boffs[0] : bits, rb[natt]);
+  v.boffs = st.up(rb.data(), natt + 1);
+  v.item_att = st.up(item_att, nitems);
+  v.item_slot = st.up(item_slot, nitems);
+  v.nitems = nitems;
+  v.balance = st.up(balance, nval);
+  v.nval = nval;
+  v.bitmaps = st.up(bitmaps, nslots * words_per_slot);
+  v.words_per_slot = words_per_slot;
+  v.totals = st.up(totals, nslots);
+  v.err = st.zeros<uint64_t>(1);
+  if (st.rc) return st.rc;
+  st.check(launch_vote_tally(v, st.s), "pz_vote_tally_kernel");
+  uint64_t err = 0;
+  st.down(&err, v.err, 1);
+  st.down(bitmaps, v.bitmaps, nslots * words_per_slot);
+  st.down(totals, v.totals, nslots);
+  if (st.sync()) return st.rc;
+  if (err) return fail(PZ_EINDEX, "calculateBlockVoteCache would panic (short bitfield or voter >= len(validators))");
+  return PZ_OK;
 }
 
 // ---- host-resident shuffle ---------------------------------------------------------------

@@ -127,9 +127,9 @@ int pz_dev_blake2b512_fixed(const uint8_t* d_msgs, uint64_t stride, uint64_t len
   if (out_bytes != 32 && out_bytes != 64) return fail(PZ_EINVAL, "out_bytes must be 32 or 64");
   if (n == 0) return PZ_OK;
   if (!d_msgs || !d_out) return fail(PZ_EINVAL, "null pointer");
-  if (stride % 16 || stride < len || (reinterpret_cast<uintptr_t>(d_msgs) & 15) ||
+  if (stride % 16 || stride < len || stride >= (1ull << 26) || (reinterpret_cast<uintptr_t>(d_msgs) & 15) ||
       (reinterpret_cast<uintptr_t>(d_out) & 15))
-    return fail(PZ_EINVAL, "fixed layout needs 16-B aligned buffers, stride %% 16 == 0, stride >= len");
+    return fail(PZ_EINVAL, "fixed layout needs 16-B aligned buffers, stride %% 16 == 0, len <= stride < 64 MiB");
   hipError_t e = launch_b2b_fixed(d_msgs, stride, len, n, d_out, out_bytes, (hipStream_t)stream);
   return e == hipSuccess ? PZ_OK : hip_fail(e, "pz_b2b_fixed_kernel");
 }
@@ -163,7 +163,7 @@ int pz_blake2b512_batch(const uint8_t* msgs, const uint64_t* offsets, uint64_t n
 
   // Uniform records at a 16-B multiple stride use the LDS-staged fixed-length kernel.
   const uint64_t len0 = offsets[1] - offsets[0];
-  bool uniform = (len0 % 16 == 0) && len0 > 0;
+  bool uniform = (len0 % 16 == 0) && len0 > 0 && len0 < (1ull << 26);
   for (uint64_t i = 1; uniform && i < n; ++i) uniform = (offsets[i + 1] - offsets[i]) == len0;
 
   if ((rc = c->in.reserve(total + 16))) return rc;

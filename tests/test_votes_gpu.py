@@ -1,0 +1,64 @@
+"""calculateBlockVoteCache (core.go:300-345) on the GPU vs the scalar oracle, including
+dedup across attestations/blocks, skipped oblique hashes and accumulation over blocks."""
+import numpy as np
+import pytest
+
+from oracle import ref
+from oracle import schema as opb
+from prysm_amd.votes import VoteCache
+
+pytestmark = pytest.mark.gpu
+U64 = np.uint64
+
+
+def test_vote_cache_vs_oracle():
+    rng = np.random.default_rng(12)
+    nval = 3000
+    _, cs = ref.new_genesis_states(nval)
+    for v in cs.validators:
+        v.balance = int(rng.integers(1, 1000))
+    astate = opb.ActiveState()
+    hashes = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(128)]
+    astate.recent_block_hashes.extend(hashes)
+    # committees of the genesis shuffle, slot-major CSR
+    comms, coffs, key = [], [0], {}
+    for s in range(64):
+        for sc in cs.shard_and_committees_for_slots[s].array_shard_and_committee:
+            key[(s, sc.shard_id)] = len(comms)
+            comms.append(np.array(sc.committee, np.uint32))
+            coffs.append(coffs[-1] + len(sc.committee))
+    committee = np.concatenate(comms)
+    coffs = np.array(coffs, U64)
+    cache_o = {}
+    vc = VoteCache(nval)
+    balance = np.array([v.balance for v in cs.validators], U64)
+    for block_slot in (10, 11, 12):
+        atts = []
+        for _ in range(6):
+            s = int(rng.integers(block_slot - 3, block_slot + 1))
+            sc = cs.shard_and_committees_for_slots[s].array_shard_and_committee[0]
+            k = len(sc.committee)
+            bf = np.packbits((rng.random(k) < 0.6).astype(np.uint8)).tobytes()
+            obl = [hashes[int(rng.integers(0, 128))] for _ in range(int(rng.integers(0, 3)))]
+            if rng.random() < 0.5:
+                obl.append(b"\x07")  # short oblique: right-aligned by BytesToHash, never equal
+            atts.append(opb.AttestationRecord(slot=s, shard_id=sc.shard_id, attester_bitfield=bf,
+                                              oblique_parent_hashes=obl))
+        items, bits, boffs, att_comm = [], [], [0], []
+        for ai, a in enumerate(atts):
+            ref.calculate_block_vote_cache(cs, astate, cache_o, block_slot, a)
+            parents = ref.get_signed_parent_hashes(astate, block_slot, a)
+            obl = [bytes(o) for o in a.oblique_parent_hashes]
+            for h in parents:
+                if any(h == o for o in obl):
+                    continue
+                items.append((ai, vc.slot(h)))
+            bits.append(np.frombuffer(a.attester_bitfield, np.uint8))
+            boffs.append(boffs[-1] + len(a.attester_bitfield))
+            att_comm.append(key[(a.slot, a.shard_id)])
+        vc.tally(committee, coffs, np.array(att_comm, np.uint32), np.concatenate(bits), np.array(boffs, U64),
+                 items, balance)
+    assert set(vc.slot_of) == set(cache_o)
+    for h, (voters, total) in cache_o.items():
+        assert vc.total(h) == total
+        assert vc.voters(h).tolist() == sorted(voters)
