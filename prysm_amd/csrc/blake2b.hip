@@ -141,7 +141,7 @@ pz_b2b_fixed_kernel(const uint8_t* __restrict__ msgs, uint64_t stride, uint64_t 
                     uint8_t* __restrict__ out, uint32_t out_bytes) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerBlock * kSlabBytes];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform -> SGPR math
   uint8_t* slab = lds + wave * kSlabBytes;
   const uint64_t m0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * 64;
   if (m0 >= n) return;  // whole wave idle (wave-uniform)
@@ -201,6 +201,137 @@ pz_b2b_fixed_kernel(const uint8_t* __restrict__ msgs, uint64_t stride, uint64_t 
     compress(h, m, ctr, last);
   }
   if (msg < n) store_digest(out + msg * out_bytes, h, out_bytes);
+}
+
+// ------------------------------------------------------------------------------------------
+// Persistent variant: the grid is sized to the resident waves and every wave walks groups of
+// 64 messages g, g+W, g+2W, ...  As soon as a block's 16 message words are in registers the
+// wave's LDS slab is free, so the NEXT block (of this group, or the first block of the wave's
+// next group) is fetched into it by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no
+// ds_write) while the current block is compressed.  DMA writes each wave-instruction's 1 KiB
+// linearly, so rows are unpadded 128 B and the bank-conflict fix moves to the SOURCE: 16-B
+// chunk k of message row r is stored at position k ^ ((r >> 1) & 7), which makes every
+// ds_read_b128 lane group hit 16 distinct 16-B bank quads.
+// ------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+constexpr int kDmaSlabBytes = 64 * 128;  // 8 KiB per wave
+
+struct FixedGeom {
+  const uint8_t* msgs;
+  uint64_t stride, len, n, ngroups, nblocks;
+  uint32_t lrow, lpart, s32;
+};
+
+__device__ __forceinline__ uint32_t chunk_pos(uint32_t r, uint32_t k) { return k ^ ((r >> 1) & 7u); }
+
+__device__ __forceinline__ bool block_is_full(const FixedGeom& G, uint64_t g, uint64_t t) {
+  return g * 64 + 64 <= G.n && (t + 1 < G.nblocks || (G.len & 127) == 0);
+}
+
+// Full block: 8 DMA instructions.  Instruction `it`, lane L fills row r = it*8 + L/8 at
+// position p = L%8, i.e. global chunk k = p ^ ((r>>1)&7) (the swizzle is an involution).
+__device__ __forceinline__ void dma_block(uint8_t* slab, const FixedGeom& G, uint64_t g, uint64_t t) {
+  const uint8_t* wbase = G.msgs + g * 64 * G.stride;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const uint32_t r = it * 8u + G.lrow;
+    const uint32_t k = chunk_pos(r, G.lpart);
+    const uint8_t* src = wbase + (r * G.s32 + (uint32_t)t * 128u + k * 16u);
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(slab + it * 1024), 16, 0, 0);
+  }
+}
+
+// Tail wave / partial last block: register path with clamped addresses and zero masking,
+// written into the same swizzled layout.
+__device__ __forceinline__ void reg_block(uint8_t* slab, const FixedGeom& G, uint64_t g, uint64_t t) {
+  const uint64_t m0 = g * 64;
+  const uint8_t* wbase = G.msgs + m0 * G.stride;
+  const uint32_t rows_left = m0 + 64 <= G.n ? 64u : (uint32_t)(G.n - m0);
+  const uint32_t len = (uint32_t)G.len;
+  const uint32_t boff = (uint32_t)t * 128u + G.lpart * 16u;
+  const uint32_t safe_off = boff < len ? boff : 0u;
+  uint4 v[8];
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const uint32_t r = it * 8u + G.lrow;
+    const bool ok = r < rows_left && boff < len;
+    const uint32_t rr = r < rows_left ? r : 0u;
+    uint4 q = *reinterpret_cast<const uint4*>(wbase + (rr * G.s32 + safe_off));
+    if (boff + 16 > len) q = mask_chunk(q, boff < len ? len - boff : 0u);
+    v[it] = ok ? q : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const uint32_t r = it * 8u + G.lrow;
+    *reinterpret_cast<uint4*>(slab + r * 128u + chunk_pos(r, G.lpart) * 16u) = v[it];
+  }
+}
+
+__device__ __forceinline__ void read_block_words(const uint8_t* slab, int lane, uint64_t m[16]) {
+  const uint32_t r = (uint32_t)lane;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint4 q = *reinterpret_cast<const uint4*>(slab + r * 128u + chunk_pos(r, (uint32_t)k) * 16u);
+    m[2 * k] = pack(q.x, q.y);
+    m[2 * k + 1] = pack(q.z, q.w);
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+pz_b2b_fixed_persistent_kernel(const uint8_t* __restrict__ msgs, uint64_t stride, uint64_t len, uint64_t n,
+                               uint8_t* __restrict__ out, uint32_t out_bytes) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerBlock * kDmaSlabBytes];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform -> SGPR math
+  uint8_t* slab = lds + wave * kDmaSlabBytes;
+  FixedGeom G;
+  G.msgs = msgs; G.stride = stride; G.len = len; G.n = n;
+  G.ngroups = (n + 63) / 64;
+  G.nblocks = len == 0 ? 1 : (len + 127) / 128;
+  G.lrow = (uint32_t)lane >> 3; G.lpart = (uint32_t)lane & 7; G.s32 = (uint32_t)stride;
+  const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
+  uint64_t g = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (g >= G.ngroups) return;  // wave-uniform
+  // Host contract (launch_b2b_fixed): n % 64 == 0 and stride >= nblocks*128, so every DMA
+  // reads whole 128-B blocks inside the record's own stride slot; bytes past `len` in the
+  // last block are zeroed in registers.
+  const uint32_t tail = (uint32_t)(G.len - (G.nblocks - 1) * 128);  // 0..128 valid bytes of the last block
+  uint64_t t = 0;
+  uint64_t h[8];
+  dma_block(slab, G, g, 0);
+  while (true) {  // flattened walk over this wave's (group, block) pairs
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint64_t m[16];
+    read_block_words(slab, lane, m);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // words in VGPRs: the slab is free
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t nt = t + 1 < G.nblocks ? t + 1 : 0;
+    const uint64_t ng = t + 1 < G.nblocks ? g : g + W;
+    if (ng < G.ngroups) dma_block(slab, G, ng, nt);  // lands while this block is compressed
+    if (t == 0) init_h(h);
+    const bool last = (t + 1 == G.nblocks);
+    if (last && tail < 128) {  // wave-uniform: zero bytes >= len of a partial last block
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t lo = 8u * k;
+        const uint32_t valid = tail <= lo ? 0u : (tail >= lo + 8 ? 8u : tail - lo);
+        m[k] &= valid >= 8 ? ~0ull : ((1ull << (8 * valid)) - 1ull);
+      }
+    }
+    compress(h, m, last ? G.len : (t + 1) * 128, last);
+    if (last) {
+      const uint64_t msg = g * 64 + lane;
+      if (msg < n) store_digest(out + msg * out_bytes, h, out_bytes);
+    }
+    t = nt;
+    g = ng;
+    if (g >= G.ngroups) break;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -264,14 +395,53 @@ pz_b2b_csr_kernel(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__
 }
 
 // ---- host-side launchers (declared in blake2b_kernels.h) ---------------------------------
-hipError_t launch_b2b_fixed(const uint8_t* msgs, uint64_t stride, uint64_t len, uint64_t n,
-                            uint8_t* out, uint32_t out_bytes, hipStream_t stream) {
+static int g_fixed_variant = 1;  // 1: persistent LDS-DMA kernel (+ plain tail), 0: plain grid
+
+static int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    cached[dev] = cus;
+  }
+  return cached[dev];
+}
+
+static hipError_t launch_plain(const uint8_t* msgs, uint64_t stride, uint64_t len, uint64_t n, uint8_t* out,
+                               uint32_t out_bytes, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const uint64_t waves = (n + 63) / 64;
   const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
   hipLaunchKernelGGL(pz_b2b_fixed_kernel, dim3((uint32_t)blocks), dim3(64 * kWavesPerBlock), 0,
                      stream, msgs, stride, len, n, out, out_bytes);
   return hipGetLastError();
+}
+
+hipError_t launch_b2b_fixed(const uint8_t* msgs, uint64_t stride, uint64_t len, uint64_t n,
+                            uint8_t* out, uint32_t out_bytes, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const uint64_t nblocks = len == 0 ? 1 : (len + 127) / 128;
+  const uint64_t nfull = n & ~63ull;
+  if (g_fixed_variant != 1 || stride < nblocks * 128 || nfull == 0)
+    return launch_plain(msgs, stride, len, n, out, out_bytes, stream);
+  // persistent grid: 4 resident 256-thread workgroups per CU (122 VGPRs -> 4 waves/SIMD)
+  const uint64_t groups = nfull / 64;
+  uint64_t blocks = (uint64_t)cu_count() * 4;
+  const uint64_t need = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (blocks > need) blocks = need;
+  hipLaunchKernelGGL(pz_b2b_fixed_persistent_kernel, dim3((uint32_t)blocks), dim3(64 * kWavesPerBlock), 0,
+                     stream, msgs, stride, len, nfull, out, out_bytes);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || nfull == n) return e;
+  return launch_plain(msgs + nfull * stride, stride, len, n - nfull, out + nfull * out_bytes, out_bytes, stream);
+}
+
+int set_fixed_variant(int v) {
+  const int old = g_fixed_variant;
+  g_fixed_variant = v;
+  return old;
 }
 
 hipError_t launch_b2b_csr(const uint8_t* msgs, const uint64_t* offsets, uint64_t n, uint8_t* out,

@@ -9,3 +9,9 @@ hipError_t launch_b2b_fixed(const uint8_t* msgs, uint64_t stride, uint64_t len, 
 hipError_t launch_b2b_csr(const uint8_t* msgs, const uint64_t* offsets, uint64_t n, uint8_t* out,
                           uint32_t out_bytes, hipStream_t stream);
 }  // namespace pz
+
+namespace pz {
+// Kernel variant for the fixed-length path (1: persistent LDS-DMA, 0: plain grid); returns the
+// previous one.  Exposed for in-process A/B timing (pz_debug_set_hash_variant).
+int set_fixed_variant(int v);
+}  // namespace pz

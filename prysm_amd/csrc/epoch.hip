@@ -62,13 +62,91 @@ __device__ __forceinline__ uint64_t block_reduce(uint64_t v, uint64_t* sh) {
 // ------------------------------------------------------------------------------------------
 struct CountGrid {
   uint64_t vbpi, nvb, pbpi, npb, nxb;
+  uint64_t xl_j;      // crosslink blocks per instance (4 attestations per block)
+  int xl_affine;      // 1: crosslink blocks of instance i land on XCD i % 8 (>= 8 instances)
 };
+
+// Crosslink tally for one attestation, one wave (core.go:533-545).  Members are processed
+// 256 at a time with every committee load, then every balance gather, in flight together
+// (two dependent round trips per 256 members instead of two per 64).
+__device__ __forceinline__ void crosslink_wave(const EpochArgs& a, uint64_t ga, int lane) {
+  const uint64_t inst = ga / a.natt;
+  const uint32_t c = a.att_comm[ga];
+  const uint64_t cb = a.coffs[c], k = a.coffs[c + 1] - cb;
+  const uint64_t bb = a.boffs[ga], blen = a.boffs[ga + 1] - bb;
+  const uint8_t* bf = a.bits + bb;
+  const uint64_t* B = a.balance + inst * a.nval;
+  const uint32_t* C = a.committee + cb;
+  uint64_t tot = 0, vote = 0;
+  bool e_mem = false, e_bf = false;
+  for (uint64_t r0 = 0; r0 < k; r0 += 256) {
+    uint32_t mem[4];
+    uint32_t byte[4];
+    uint64_t bal[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t i = r0 + j * 64 + lane;
+      mem[j] = C[i < k ? i : 0];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t i = r0 + j * 64 + lane;
+      byte[j] = (i < k && i < 8 * blen) ? bf[i >> 3] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t i = r0 + j * 64 + lane;
+      const uint64_t local = (uint64_t)mem[j] - a.val_offset;  // wraps huge when mem < val_offset
+      const bool own = i < k && mem[j] < a.nval_global && local < a.nval;
+      bal[j] = own ? B[local] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t i = r0 + j * 64 + lane;
+      if (i < k) {
+        e_mem |= mem[j] >= a.nval_global;
+        e_bf |= i >= 8 * blen;
+        tot += bal[j];
+        vote += ((byte[j] >> (7 - (uint32_t)(i & 7))) & 1u) ? bal[j] : 0;
+      }
+    }
+  }
+  tot = wave_sum(tot);
+  vote = wave_sum(vote);
+  const uint64_t e1 = __ballot(e_mem), e2 = __ballot(e_bf);
+  if (lane == 0) {
+    a.vote[ga] = vote;
+    a.total[ga] = tot;
+    const uint64_t ebits = (e1 ? kErrMember : 0) | (e2 ? kErrBitfield : 0);
+    if (ebits) atomicAdd((unsigned long long*)&a.scal[inst * kScal + kErrXl], (unsigned long long)ebits);
+  }
+}
 
 extern "C" __global__ void __launch_bounds__(kThreads)
 pz_epoch_count_kernel(EpochArgs a, CountGrid g) {
   __shared__ uint64_t sh[kThreads / 64];
-  const uint64_t b = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // Grid order: [crosslink blocks | validator blocks | popcount blocks].  The latency-bound
+  // gathers start first and overlap the streaming blocks behind them.
+  if (blockIdx.x < g.nxb) {
+    const uint64_t x = blockIdx.x;
+    uint64_t inst, j;
+    if (g.xl_affine) {  // blocks x and x+8 share an XCD: keep one instance's balances in one L2
+      const uint64_t qj = x >> 3;
+      inst = (qj / g.xl_j) * 8 + (x & 7);
+      j = qj % g.xl_j;
+    } else {
+      inst = x / g.xl_j;
+      j = x % g.xl_j;
+    }
+    const uint64_t att = j * (kThreads / 64) + wave;
+    if (inst >= a.ninst || att >= a.natt) return;
+    crosslink_wave(a, inst * a.natt + att, lane);
+    return;
+  }
+  const uint64_t b = blockIdx.x - g.nxb;
 
   if (b < g.nvb) {  // ---- classify + count + active mask + max active index
     const uint64_t inst = b / g.vbpi, chunk = b % g.vbpi;
@@ -112,7 +190,7 @@ pz_epoch_count_kernel(EpochArgs a, CountGrid g) {
     return;
   }
 
-  if (b < g.nvb + g.npb) {  // ---- popcount of this instance's bitfield bytes
+  {  // ---- popcount of this instance's bitfield bytes
     const uint64_t pb = b - g.nvb;
     const uint64_t inst = pb / g.pbpi, chunk = pb % g.pbpi;
     if (chunk % a.pop_world != a.pop_rank) return;
@@ -132,38 +210,6 @@ pz_epoch_count_kernel(EpochArgs a, CountGrid g) {
     }
     uint64_t c = block_reduce<false>(cnt, sh);
     if (tid == 0 && c) atomicAdd((unsigned long long*)&a.scal[inst * kScal + kPop], (unsigned long long)c);
-    return;
-  }
-
-  // ---- crosslink tally: one wave per attestation (core.go:533-545)
-  const uint64_t ga = (b - g.nvb - g.npb) * (kThreads / 64) + wave;
-  if (ga >= (uint64_t)a.ninst * a.natt) return;
-  const uint64_t inst = ga / a.natt;
-  const uint32_t c = a.att_comm[ga];
-  const uint64_t cb = a.coffs[c], k = a.coffs[c + 1] - cb;
-  const uint64_t bb = a.boffs[ga], blen = a.boffs[ga + 1] - bb;
-  const uint8_t* bf = a.bits + bb;
-  const uint64_t* B = a.balance + inst * a.nval;
-  uint64_t tot = 0, vote = 0, err = 0;
-  for (uint64_t i = lane; i < k; i += 64) {
-    const uint64_t m = a.committee[cb + i];
-    if (m >= a.nval_global) { err |= kErrMember; continue; }
-    const uint64_t local = m - a.val_offset;  // wraps huge when m < val_offset
-    if (local < a.nval) {
-      const uint64_t bal = B[local];
-      tot += bal;
-      if (i < 8 * blen) vote += bit_at(bf, i) ? bal : 0;
-    }
-    if (i >= 8 * blen) err |= kErrBitfield;
-  }
-  tot = wave_sum(tot);
-  vote = wave_sum(vote);
-  const uint64_t e1 = __ballot((err & kErrMember) != 0), e2 = __ballot((err & kErrBitfield) != 0);
-  if (lane == 0) {
-    a.vote[ga] = vote;
-    a.total[ga] = tot;
-    const uint64_t ebits = (e1 ? kErrMember : 0) | (e2 ? kErrBitfield : 0);
-    if (ebits) atomicAdd((unsigned long long*)&a.scal[inst * kScal + kErrXl], (unsigned long long)ebits);
   }
 }
 
@@ -281,7 +327,10 @@ hipError_t launch_epoch_count(const EpochArgs& a, bool do_val, bool do_pop, bool
   g.nvb = do_val ? (uint64_t)a.ninst * g.vbpi : 0;
   g.pbpi = (a.max_inst_bytes + kPopBytesPerBlock - 1) / kPopBytesPerBlock;
   g.npb = (do_pop && a.natt) ? (uint64_t)a.ninst * g.pbpi : 0;
-  g.nxb = (do_xl && a.natt) ? ((uint64_t)a.ninst * a.natt + 3) / 4 : 0;
+  g.xl_j = ((uint64_t)a.natt + 3) / 4;
+  g.xl_affine = a.ninst >= 8 ? 1 : 0;
+  const uint64_t xl_inst = g.xl_affine ? ((uint64_t)a.ninst + 7) / 8 * 8 : a.ninst;
+  g.nxb = (do_xl && a.natt) ? xl_inst * g.xl_j : 0;
   const uint64_t blocks = g.nvb + g.npb + g.nxb;
   if (!blocks) return hipSuccess;
   hipLaunchKernelGGL(pz_epoch_count_kernel, dim3((uint32_t)blocks), dim3(kThreads), 0, s, a, g);

@@ -414,3 +414,13 @@ int pz_shuffle_indices(const uint8_t seed[32], uint32_t* list, uint64_t n) {
 }
 
 }  // extern "C"
+
+// Internal: launch pass 1 with a subset of its block ranges (per-part timing in tools/).
+extern "C" int pz_debug_epoch_count(const pz_epoch_batch* b, int do_val, int do_pop, int do_xl, void* stream) {
+  hipError_t e = pz::launch_epoch_count(*b, do_val != 0, do_pop != 0, do_xl != 0, (hipStream_t)stream);
+  return e == hipSuccess ? PZ_OK : pz::hip_fail(e, "pz_epoch_count_kernel");
+}
+extern "C" int pz_debug_epoch_reward(const pz_epoch_batch* b, void* stream) {
+  hipError_t e = pz::launch_epoch_reward(*b, (hipStream_t)stream);
+  return e == hipSuccess ? PZ_OK : pz::hip_fail(e, "pz_epoch_reward_kernel");
+}

@@ -196,3 +196,6 @@ int pz_blake2b512_batch(const uint8_t* msgs, const uint64_t* offsets, uint64_t n
 }
 
 }  // extern "C"
+
+// Internal: select the fixed-length hash kernel variant for in-process A/B benchmarking.
+extern "C" int pz_debug_set_hash_variant(int v) { return pz::set_fixed_variant(v); }

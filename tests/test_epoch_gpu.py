@@ -233,7 +233,8 @@ def _oracle_epoch(inst, b):
     return nb, applied, onp.active_balance_sum(nb, s, e, int(inst["dynasty"][b])), v, t, win
 
 
-@pytest.mark.parametrize("n,B,inactive", [(65536, 3, False), (5000, 2, True), (20000, 1, True)])
+@pytest.mark.parametrize("n,B,inactive", [(65536, 3, False), (5000, 2, True), (20000, 1, True), (4096, 9, False),
+                                          (3000, 17, True)])
 def test_device_epoch_vs_oracle(n, B, inactive):
     import torch
 

@@ -1,0 +1,54 @@
+"""Per-part device time of the epoch step (HIP events, one process, interleaved rounds)."""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from prysm_amd import _lib, casper, synth  # noqa: E402
+from prysm_amd.epoch import DeviceEpoch  # noqa: E402
+
+
+def main(nval=65536, ninst=256, rounds=5, reps=10):
+    dll = _lib.lib.dll
+    dev = torch.device("cuda", 0)
+    sh_ = casper.shuffle_indices(b"A" + bytes(31), np.arange(nval, dtype=np.uint32))
+    inst = synth.epoch_batch(nval, ninst, seed=3, shuffled=sh_)
+    de = DeviceEpoch(inst, dev)
+    s = torch.cuda.current_stream(dev)
+    sh = ctypes.c_void_p(s.cuda_stream)
+    bp = ctypes.byref(de.batch)
+    parts = {
+        "count_val": lambda: dll.pz_debug_epoch_count(bp, 1, 0, 0, sh),
+        "count_pop": lambda: dll.pz_debug_epoch_count(bp, 0, 1, 0, sh),
+        "count_xl": lambda: dll.pz_debug_epoch_count(bp, 0, 0, 1, sh),
+        "count_all": lambda: dll.pz_debug_epoch_count(bp, 1, 1, 1, sh),
+        "reward": lambda: dll.pz_debug_epoch_reward(bp, sh),
+        "step": lambda: de.step(s),
+    }
+    res = {k: [] for k in parts}
+    de.step(s)
+    for r in range(rounds):
+        for k, f in parts.items():
+            f()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(reps):
+                f()
+            e1.record(s)
+            torch.cuda.synchronize()
+            res[k].append(e0.elapsed_time(e1) / reps * 1e3)
+    med = {k: float(np.median(v)) for k, v in res.items()}
+    vb = nval * ninst
+    print(json.dumps({"nval": nval, "ninst": ninst, "median_us": med,
+                      "val_GBps": vb * 16 / (med["count_val"] * 1e-6) / 1e9,
+                      "reward_GBps": vb * 16 / (med["reward"] * 1e-6) / 1e9,
+                      "xl_GBps_algorithmic": vb * 12 / (med["count_xl"] * 1e-6) / 1e9}))
+
+
+if __name__ == "__main__":
+    main()
