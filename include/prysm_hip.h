@@ -127,7 +127,8 @@ int pz_shuffle_indices(const uint8_t seed[32], uint32_t* list, uint64_t n);
  * 433-464): crosslink tallies + winners, attester popcount, CalculateRewards and the
  * next-cycle total balance.  All pointers are device pointers.  Validators are
  * instance-major [B][nval]; this rank holds global indices [val_offset, val_offset+nval)
- * of nval_global.  The caller zeroes `scal` and fills `winner` with 0xFF before step 1.
+ * of nval_global.  `scal` must be zero before pass 1 (allocate it zeroed, then ping-pong
+ * with `scal_next`, which the finish pass zeroes); pass 1 initialises `winner` itself.
  * Single GPU: pz_dev_epoch_count -> pz_dev_epoch_finish.  Multi-GPU: count ->
  * all-reduce(sum) over the contiguous block {scal, vote, total} -> finish ->
  * all-reduce(sum) of scal[.][PZ_SCAL_NEXT_BAL] (only the all-active rank path is
@@ -173,6 +174,9 @@ typedef struct pz_epoch_batch {
   uint64_t* act_mask;             /* [B][ceil(nval/64)] scratch (general rank path) */
   uint32_t* blk_cnt;              /* [B][ceil(nval/2048)] scratch */
   uint32_t* act_list;             /* [B][nval_global] scratch (general rank path) */
+  uint64_t* scal_next;            /* optional [B][PZ_SCAL_COUNT]: zeroed by the finish pass so
+                                     the NEXT step can accumulate into it (ping-pong; saves a
+                                     memset launch per step) */
 } pz_epoch_batch;
 
 /* ---- T: block vote-cache tally (blockchain/core.go:300-345 calculateBlockVoteCache) ----

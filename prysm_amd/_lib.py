@@ -81,7 +81,7 @@ class EpochBatch(ctypes.Structure):
         ("max_inst_bytes", u64), ("pop_rank", ctypes.c_uint32), ("pop_world", ctypes.c_uint32),
         ("committee", vp), ("coffs", vp), ("att_comm", vp), ("att_shard", vp),
         ("nrec", ctypes.c_uint32), ("rec_dynasty", vp), ("winner", vp), ("vote", vp), ("total", vp),
-        ("scal", vp), ("act_mask", vp), ("blk_cnt", vp), ("act_list", vp),
+        ("scal", vp), ("act_mask", vp), ("blk_cnt", vp), ("act_list", vp), ("scal_next", vp),
     ]
 
 

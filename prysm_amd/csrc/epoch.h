@@ -37,6 +37,8 @@ hipError_t launch_epoch_winners(const EpochArgs& a, hipStream_t s);
 // General rank path: scan per-block counts and compact the active list (no-op per instance
 // when every validator is active).  Single-rank only (multi-rank gathers lists itself).
 hipError_t launch_epoch_compact(const EpochArgs& a, bool force, hipStream_t s);
+// Winners + compaction in one launch (the device-resident finish path).
+hipError_t launch_epoch_mid(const EpochArgs& a, bool winners, bool compact, hipStream_t s);
 // Pass 2: rewards (in place) + post-reward active balance sum.
 hipError_t launch_epoch_reward(const EpochArgs& a, hipStream_t s);
 

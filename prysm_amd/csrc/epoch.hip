@@ -60,8 +60,22 @@ __device__ __forceinline__ uint64_t block_reduce(uint64_t v, uint64_t* sh) {
 // ------------------------------------------------------------------------------------------
 // Pass 1: [validator blocks | popcount blocks | crosslink blocks (1 wave per attestation)]
 // ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+
+// Bit i of x -> bit 2i of the result (interleaves two 32-lane ballots into a 64-bit mask).
+__device__ __forceinline__ uint64_t spread32(uint32_t x) {
+  uint64_t v = x;
+  v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+  v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+  v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  v = (v | (v << 2)) & 0x3333333333333333ull;
+  v = (v | (v << 1)) & 0x5555555555555555ull;
+  return v;
+}
+
 struct CountGrid {
   uint64_t vbpi, nvb, pbpi, npb, nxb;
+  int vec;            // 1: validator arrays read 16 B per lane (nval even, 16-B aligned)
   uint64_t xl_j;      // crosslink blocks per instance (4 attestations per block)
   int xl_affine;      // 1: crosslink blocks of instance i land on XCD i % 8 (>= 8 instances)
 };
@@ -70,7 +84,7 @@ struct CountGrid {
 // 256 at a time with every committee load, then every balance gather, in flight together
 // (two dependent round trips per 256 members instead of two per 64).
 __device__ __forceinline__ void crosslink_wave(const EpochArgs& a, uint64_t ga, int lane) {
-  const uint64_t inst = ga / a.natt;
+  const uint64_t inst = (uint32_t)ga / (uint32_t)a.natt;  // 32-bit: B*natt < 2^32 (host-checked)
   const uint32_t c = a.att_comm[ga];
   const uint64_t cb = a.coffs[c], k = a.coffs[c + 1] - cb;
   const uint64_t bb = a.boffs[ga], blen = a.boffs[ga + 1] - bb;
@@ -128,18 +142,20 @@ pz_epoch_count_kernel(EpochArgs a, CountGrid g) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-  // Grid order: [crosslink blocks | validator blocks | popcount blocks].  The latency-bound
-  // gathers start first and overlap the streaming blocks behind them.
+  // Grid order: [crosslink blocks | validator blocks | popcount blocks]: the latency-bound
+  // gathers start first.  (An even interleave measured slower: its per-block 64-bit index
+  // division costs more than the overlap gains.)
   if (blockIdx.x < g.nxb) {
     const uint64_t x = blockIdx.x;
     uint64_t inst, j;
     if (g.xl_affine) {  // blocks x and x+8 share an XCD: keep one instance's balances in one L2
       const uint64_t qj = x >> 3;
-      inst = (qj / g.xl_j) * 8 + (x & 7);
-      j = qj % g.xl_j;
+      const uint32_t q32 = (uint32_t)qj / (uint32_t)g.xl_j;
+      inst = (uint64_t)q32 * 8 + (x & 7);
+      j = (uint32_t)qj - q32 * (uint32_t)g.xl_j;
     } else {
-      inst = x / g.xl_j;
-      j = x % g.xl_j;
+      inst = (uint32_t)x / (uint32_t)g.xl_j;
+      j = (uint32_t)x - (uint32_t)inst * (uint32_t)g.xl_j;
     }
     const uint64_t att = j * (kThreads / 64) + wave;
     if (inst >= a.ninst || att >= a.natt) return;
@@ -149,7 +165,7 @@ pz_epoch_count_kernel(EpochArgs a, CountGrid g) {
   const uint64_t b = blockIdx.x - g.nxb;
 
   if (b < g.nvb) {  // ---- classify + count + active mask + max active index
-    const uint64_t inst = b / g.vbpi, chunk = b % g.vbpi;
+    const uint64_t inst = (uint32_t)b / (uint32_t)g.vbpi, chunk = (uint32_t)b - (uint32_t)inst * (uint32_t)g.vbpi;
     const uint64_t base = chunk * kValPerBlock;
     const uint64_t d = a.dynasty[inst];
     const uint64_t* S = a.start + inst * a.nval;
@@ -157,17 +173,45 @@ pz_epoch_count_kernel(EpochArgs a, CountGrid g) {
     uint64_t* mask = a.act_mask ? a.act_mask + inst * ((a.nval + 63) / 64) : nullptr;
     uint32_t cnt = 0;
     uint64_t maxi1 = 0;
+    if (g.vec) {  // 16 B per lane: validators i0, i0+1 (nval even, arrays 16-B aligned)
 #pragma unroll
-    for (int j = 0; j < kValPerThread; ++j) {
-      const uint64_t i = base + (uint64_t)j * kThreads + tid;
-      bool act = false;
-      if (i < a.nval) act = kind_pred(a.kind, S[i], E[i], d);
-      const uint64_t bal = __ballot(act);
-      if (act) maxi1 = a.val_offset + i + 1;
-      if (lane == 0) {
-        cnt += (uint32_t)__popcll(bal);
-        const uint64_t w = (base + (uint64_t)j * kThreads + wave * 64) >> 6;
-        if (mask && (w << 6) < a.nval) mask[w] = bal;
+      for (int j = 0; j < kValPerThread / 2; ++j) {
+        const uint64_t wb = base + (uint64_t)j * (2 * kThreads) + wave * 128;
+        const uint64_t i0 = base + (uint64_t)j * (2 * kThreads) + 2 * tid;
+        bool a0 = false, a1 = false;
+        if (i0 < a.nval) {
+          const uint4 s = *reinterpret_cast<const uint4*>(S + i0);
+          const uint4 e = *reinterpret_cast<const uint4*>(E + i0);
+          a0 = kind_pred(a.kind, pack64(s.x, s.y), pack64(e.x, e.y), d);
+          a1 = kind_pred(a.kind, pack64(s.z, s.w), pack64(e.z, e.w), d);
+        }
+        const uint64_t b0 = __ballot(a0), b1 = __ballot(a1);
+        if (a1) maxi1 = a.val_offset + i0 + 2;
+        else if (a0) maxi1 = a.val_offset + i0 + 1;
+        if (lane == 0) {
+          cnt += (uint32_t)(__popcll(b0) + __popcll(b1));
+          if (mask) {  // lane L holds validators 2L, 2L+1: interleave the two ballots
+            const uint64_t w0 = wb >> 6;
+            const uint64_t m0 = spread32((uint32_t)b0) | (spread32((uint32_t)b1) << 1);
+            const uint64_t m1 = spread32((uint32_t)(b0 >> 32)) | (spread32((uint32_t)(b1 >> 32)) << 1);
+            if ((w0 << 6) < a.nval) mask[w0] = m0;
+            if (((w0 + 1) << 6) < a.nval) mask[w0 + 1] = m1;
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kValPerThread; ++j) {
+        const uint64_t i = base + (uint64_t)j * kThreads + tid;
+        bool act = false;
+        if (i < a.nval) act = kind_pred(a.kind, S[i], E[i], d);
+        const uint64_t bal = __ballot(act);
+        if (act) maxi1 = a.val_offset + i + 1;
+        if (lane == 0) {
+          cnt += (uint32_t)__popcll(bal);
+          const uint64_t w = (base + (uint64_t)j * kThreads + wave * 64) >> 6;
+          if (mask && (w << 6) < a.nval) mask[w] = bal;
+        }
       }
     }
     uint64_t c = block_reduce<false>(lane == 0 ? cnt : 0, sh);
@@ -192,7 +236,9 @@ pz_epoch_count_kernel(EpochArgs a, CountGrid g) {
 
   {  // ---- popcount of this instance's bitfield bytes
     const uint64_t pb = b - g.nvb;
-    const uint64_t inst = pb / g.pbpi, chunk = pb % g.pbpi;
+    const uint64_t inst = (uint32_t)pb / (uint32_t)g.pbpi, chunk = (uint32_t)pb - (uint32_t)inst * (uint32_t)g.pbpi;
+    if (chunk == 0 && a.winner)  // winners are reset here; the winner pass runs after this launch
+      for (uint32_t s = tid; s < a.nrec; s += kThreads) a.winner[inst * a.nrec + s] = 0xffffffffu;
     if (chunk % a.pop_world != a.pop_rank) return;
     const uint64_t beg = a.boffs[inst * a.natt], end = a.boffs[inst * a.natt + a.natt];
     const uint64_t cb = beg + chunk * kPopBytesPerBlock;
@@ -217,10 +263,8 @@ pz_epoch_count_kernel(EpochArgs a, CountGrid g) {
 // Crosslink winners (core.go:549-555): the first attestation, in order, whose 3*vote >=
 // 2*total and whose dynasty beats the shard's record wins that shard (atomicMin of index).
 // ------------------------------------------------------------------------------------------
-extern "C" __global__ void __launch_bounds__(kThreads) pz_epoch_winner_kernel(EpochArgs a) {
-  const uint64_t ga = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ga >= (uint64_t)a.ninst * a.natt) return;
-  const uint64_t inst = ga / a.natt;
+__device__ __forceinline__ void winner_one(const EpochArgs& a, uint64_t ga) {
+  const uint64_t inst = (uint32_t)ga / (uint32_t)a.natt;
   const uint64_t v = a.vote[ga], t = a.total[ga];
   if (3ull * v >= 2ull * t) {  // uint64 wrap, as in Go
     const uint32_t shard = a.att_shard[ga];
@@ -233,14 +277,19 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_epoch_winner_kernel(Ep
   }
 }
 
+extern "C" __global__ void __launch_bounds__(kThreads) pz_epoch_winner_kernel(EpochArgs a) {
+  const uint64_t ga = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ga >= (uint64_t)a.ninst * a.natt) return;
+  winner_one(a, ga);
+}
+
 // ------------------------------------------------------------------------------------------
 // General rank path: compacted active list act_list[inst][rank] = global index.
 // ------------------------------------------------------------------------------------------
-extern "C" __global__ void __launch_bounds__(kThreads)
-pz_epoch_compact_kernel(EpochArgs a, uint64_t vbpi, int force) {
+__device__ __forceinline__ void compact_block(const EpochArgs& a, uint64_t vbpi, int force, uint64_t blk) {
   __shared__ uint32_t wsum[kThreads / 64 * kValPerThread];
   __shared__ uint64_t base_off;
-  const uint64_t inst = blockIdx.x / vbpi, chunk = blockIdx.x % vbpi;
+  const uint64_t inst = (uint32_t)blk / (uint32_t)vbpi, chunk = (uint32_t)blk - (uint32_t)inst * (uint32_t)vbpi;
   const uint64_t nact = a.scal[inst * kScal + kNact];
   if (!force && nact == a.nval) return;  // rank == index: nothing to compact
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -273,13 +322,145 @@ pz_epoch_compact_kernel(EpochArgs a, uint64_t vbpi, int force) {
   }
 }
 
+extern "C" __global__ void __launch_bounds__(kThreads)
+pz_epoch_compact_kernel(EpochArgs a, uint64_t vbpi, int force) {
+  compact_block(a, vbpi, force, blockIdx.x);
+}
+
+// Finish pass 1 of 2 in one launch: [winner threads | compaction blocks].
+extern "C" __global__ void __launch_bounds__(kThreads)
+pz_epoch_mid_kernel(EpochArgs a, uint64_t vbpi, uint64_t nwb, int do_compact) {
+  if (blockIdx.x < nwb) {
+    const uint64_t ga = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ga < (uint64_t)a.ninst * a.natt) winner_one(a, ga);
+    return;
+  }
+  if (do_compact) compact_block(a, vbpi, 0, blockIdx.x - nwb);
+}
+
 // ------------------------------------------------------------------------------------------
 // Pass 2: CalculateRewards (incentives.go:14-32) fused with the next-cycle balance sum
 // (core.go:459-464).  Position p receives +-1 by CheckBit(last bitfield, active[p]).
 // ------------------------------------------------------------------------------------------
-extern "C" __global__ void __launch_bounds__(kThreads) pz_epoch_reward_kernel(EpochArgs a, uint64_t vbpi) {
+// One validator position: +-1 at rank p from bit active[p] of the last bitfield, and the
+// post-reward balance if p is active.
+__device__ __forceinline__ uint64_t reward_one(uint64_t bal, uint64_t gp, bool applied, uint64_t nact,
+                                               bool all_active, const uint32_t* list, const uint8_t* lastbf,
+                                               bool* changed) {
+  if (applied && gp < nact) {
+    const uint64_t idx = all_active ? gp : list[gp];
+    *changed = true;
+    return bit_at(lastbf, idx) ? bal + PZ_ATTESTER_REWARD : bal - PZ_ATTESTER_REWARD;
+  }
+  return bal;
+}
+
+// MODE is an ablation knob for tools/epoch_parts.py only (0 in the product): bit 1 skips the
+// last-bitfield loads, bit 2 skips the block reduction + atomic.  Results are wrong for MODE != 0.
+// scal_ro / boffs_ro / tdep_ro alias a.scal / a.boffs / a.total_deposit but are only read
+// (the slots written here, kApplied / kNextBal, are not the ones read), so they are
+// declared __restrict__ at the kernel boundary: the compiler then reads them with s_load
+// instead of vector loads that would queue behind, and reorder, the balance stream.
+template <int MODE>
+__device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
+                                            const uint64_t* __restrict__ scal_ro,
+                                            const uint64_t* __restrict__ boffs_ro,
+                                            const uint64_t* __restrict__ tdep_ro) {
   __shared__ uint64_t sh[kThreads / 64];
-  const uint64_t inst = blockIdx.x / vbpi, chunk = blockIdx.x % vbpi;
+  // 2-D grid: x = chunk within the instance, y = instance (no per-block division).  The next
+  // step's accumulators (scal_next) are zeroed at the END: a store ahead of the scalar reads
+  // would stop the compiler from using s_load for them.
+  if (vec) {  // 16 B per lane read-modify-write (nval even, arrays 16-B aligned)
+    const uint64_t inst = blockIdx.y, chunk = blockIdx.x;
+    const int tid = threadIdx.x;
+    uint64_t* B = a.balance + inst * a.nval;
+    const uint64_t base = chunk * kValPerBlock;
+    constexpr int kPairs = kValPerThread / 2;
+    // phase 1: every 16-B balance load in flight BEFORE the per-instance scalars are
+    // awaited (the scalar round trip would otherwise serialise in front of every block)
+    uint4 q[kPairs];
+#pragma unroll
+    for (int j = 0; j < kPairs; ++j) {
+      const uint64_t p = base + (uint64_t)j * (2 * kThreads) + 2 * tid;
+      q[j] = *reinterpret_cast<const uint4*>(B + (p < a.nval ? p : 0));
+    }
+    const uint64_t* sc = scal_ro + inst * kScal;
+    const uint64_t pop = sc[kPop], nact = sc[kNact];
+    const uint64_t dep = pop * PZ_DEFAULT_BALANCE;
+    const bool thr = (dep * 3ull) >= (tdep_ro[inst] * 2ull);  // uint64 wrap, incentives.go:18-20
+    // Go panics in processCrosslinks or CalculateRewards: leave balances untouched.  A
+    // predicate, not an early return, so the balance loads above cannot be sunk below it.
+    const bool skip = sc[kErrXl] != 0 || (thr && nact > 0 && sc[kErrRwd] != 0);
+    const bool applied = thr && !skip;
+    const bool all_active = (nact == a.nval_global);
+    const uint8_t* lastbf = a.natt ? a.bits + boffs_ro[inst * a.natt + a.natt - 1] : nullptr;
+    const uint64_t* mask = a.act_mask ? a.act_mask + inst * ((a.nval + 63) / 64) : nullptr;
+    const uint32_t* list = a.act_list ? a.act_list + inst * a.nval_global : nullptr;
+    uint64_t sum = 0;
+    // Fast bit path (all active, byte-aligned range): the wave needs 4 x 16 contiguous bytes
+    // of the last bitfield (positions base + j*512 + wave*128 + [0,128)); one byte load per
+    // lane fetches them and __shfl hands each lane its byte (one memory round trip instead
+    // of one per element).
+    const int lane = tid & 63, wave = tid >> 6;
+    const uint64_t gbase = a.val_offset + base;
+    const bool fastbits = (MODE & 1) == 0 && applied && all_active && lastbf && (gbase & 7) == 0;
+    uint32_t mybyte = 0;
+    if (fastbits) {
+      const uint64_t L = boffs_ro[inst * a.natt + a.natt] - boffs_ro[inst * a.natt + a.natt - 1];
+      const uint64_t bi = (gbase >> 3) + (uint64_t)(lane >> 4) * 64 + wave * 16 + (lane & 15);
+      mybyte = bi < L ? lastbf[bi] : 0u;
+    }
+    // phase 2: rewards + sums; phase 3: stores
+#pragma unroll
+    for (int j = 0; j < kPairs; ++j) {
+      const uint64_t p = base + (uint64_t)j * (2 * kThreads) + 2 * tid;
+      uint32_t byte_j = 0;
+      if (fastbits) byte_j = (uint32_t)__shfl((int)mybyte, j * 16 + (lane >> 2), 64);
+      if (p < a.nval) {
+        const uint64_t gp = a.val_offset + p;
+        bool changed = false;
+        uint64_t b0, b1;
+        if (MODE & 1) {
+          b0 = pack64(q[j].x, q[j].y) + 1;
+          b1 = pack64(q[j].z, q[j].w) - 1;
+          changed = applied;
+        } else if (fastbits) {  // gp < nact for every p < nval here (all active)
+          const uint32_t sh0 = 7u - (uint32_t)(gp & 7);
+          b0 = pack64(q[j].x, q[j].y);
+          b1 = pack64(q[j].z, q[j].w);
+          b0 = ((byte_j >> sh0) & 1u) ? b0 + PZ_ATTESTER_REWARD : b0 - PZ_ATTESTER_REWARD;
+          b1 = ((byte_j >> (sh0 - 1)) & 1u) ? b1 + PZ_ATTESTER_REWARD : b1 - PZ_ATTESTER_REWARD;
+          changed = true;
+        } else {
+          b0 = reward_one(pack64(q[j].x, q[j].y), gp, applied, nact, all_active, list, lastbf, &changed);
+          b1 = reward_one(pack64(q[j].z, q[j].w), gp + 1, applied, nact, all_active, list, lastbf, &changed);
+        }
+        if (changed) {
+          *reinterpret_cast<uint4*>(B + p) =
+              make_uint4((uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32));
+        }
+        if (all_active) {
+          sum += b0 + b1;
+        } else {
+          const uint64_t mw = mask[p >> 6];
+          sum += ((mw >> (p & 63)) & 1) ? b0 : 0;
+          sum += ((mw >> ((p + 1) & 63)) & 1) ? b1 : 0;
+        }
+      }
+    }
+    if (MODE & 2) {
+      asm volatile("" ::"v"(sum));
+      return;
+    }
+    uint64_t s = block_reduce<false>(sum, sh);
+    if (tid == 0) {
+      if (s && !skip) atomicAdd((unsigned long long*)&a.scal[inst * kScal + kNextBal], (unsigned long long)s);
+      if (chunk == 0) a.scal[inst * kScal + kApplied] = applied ? 1 : 0;
+    }
+    if (a.scal_next && chunk == 0 && tid < kScal) a.scal_next[inst * kScal + tid] = 0;
+    return;
+  }
+  const uint64_t inst = blockIdx.y, chunk = blockIdx.x;
   const int tid = threadIdx.x;
   const uint64_t* sc = a.scal + inst * kScal;
   const uint64_t pop = sc[kPop], nact = sc[kNact];
@@ -287,8 +468,9 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_epoch_reward_kernel(Ep
   const uint64_t dep = pop * PZ_DEFAULT_BALANCE;                 // GetAttestersTotalDeposit
   const bool applied = (dep * 3ull) >= (a.total_deposit[inst] * 2ull);  // uint64 wrap
   const bool rwd_err = applied && nact > 0 && sc[kErrRwd] != 0;
+  if (a.scal_next && chunk == 0 && tid < kScal) a.scal_next[inst * kScal + tid] = 0;
   if (xl_err || rwd_err) {  // Go panics before/while rewarding: leave balances untouched
-    if (blockIdx.x % vbpi == 0 && tid == 0) a.scal[inst * kScal + kApplied] = 0;
+    if (chunk == 0 && tid == 0) a.scal[inst * kScal + kApplied] = 0;
     return;
   }
   const bool all_active = (nact == a.nval_global);
@@ -320,13 +502,46 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_epoch_reward_kernel(Ep
   }
 }
 
+#define PZ_REWARD_KERNEL(NAME, MODE)                                                            \
+  extern "C" __global__ void __launch_bounds__(kThreads)                                         \
+  NAME(EpochArgs a, uint64_t vbpi, int vec, const uint64_t* __restrict__ scal_ro,                \
+       const uint64_t* __restrict__ boffs_ro, const uint64_t* __restrict__ tdep_ro) {            \
+    reward_body<MODE>(a, vbpi, vec, scal_ro, boffs_ro, tdep_ro);                                  \
+  }
+PZ_REWARD_KERNEL(pz_epoch_reward_kernel, 0)
+PZ_REWARD_KERNEL(pz_epoch_reward_dbg1_kernel, 1)
+PZ_REWARD_KERNEL(pz_epoch_reward_dbg2_kernel, 2)
+PZ_REWARD_KERNEL(pz_epoch_reward_dbg3_kernel, 3)
+#undef PZ_REWARD_KERNEL
+
+hipError_t launch_epoch_reward_mode(const EpochArgs& a, int mode, hipStream_t s) {
+  const uint64_t vbpi = vblocks_per_inst(a.nval);
+  if (!vbpi || !a.ninst) return hipSuccess;
+  const int vec = ((a.nval % 2 == 0) && !((reinterpret_cast<uintptr_t>(a.balance) |
+                                           reinterpret_cast<uintptr_t>(a.start) |
+                                           reinterpret_cast<uintptr_t>(a.end)) & 15)) ? 1 : 0;
+  const dim3 grid((uint32_t)vbpi, a.ninst);
+  if (mode == 1) hipLaunchKernelGGL(pz_epoch_reward_dbg1_kernel, grid, dim3(kThreads), 0, s, a, vbpi, vec, a.scal, a.boffs, a.total_deposit);
+  else if (mode == 2) hipLaunchKernelGGL(pz_epoch_reward_dbg2_kernel, grid, dim3(kThreads), 0, s, a, vbpi, vec, a.scal, a.boffs, a.total_deposit);
+  else if (mode == 3) hipLaunchKernelGGL(pz_epoch_reward_dbg3_kernel, grid, dim3(kThreads), 0, s, a, vbpi, vec, a.scal, a.boffs, a.total_deposit);
+  else hipLaunchKernelGGL(pz_epoch_reward_kernel, grid, dim3(kThreads), 0, s, a, vbpi, vec, a.scal, a.boffs,
+                          a.total_deposit);
+  return hipGetLastError();
+}
+
 // ---- launchers ---------------------------------------------------------------------------
+static bool vec_ok(const EpochArgs& a) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return (a.nval % 2 == 0) && al(a.start) && al(a.end) && al(a.balance);
+}
+
 hipError_t launch_epoch_count(const EpochArgs& a, bool do_val, bool do_pop, bool do_xl, hipStream_t s) {
   CountGrid g;
   g.vbpi = vblocks_per_inst(a.nval);
   g.nvb = do_val ? (uint64_t)a.ninst * g.vbpi : 0;
   g.pbpi = (a.max_inst_bytes + kPopBytesPerBlock - 1) / kPopBytesPerBlock;
   g.npb = (do_pop && a.natt) ? (uint64_t)a.ninst * g.pbpi : 0;
+  g.vec = vec_ok(a) ? 1 : 0;
   g.xl_j = ((uint64_t)a.natt + 3) / 4;
   g.xl_affine = a.ninst >= 8 ? 1 : 0;
   const uint64_t xl_inst = g.xl_affine ? ((uint64_t)a.ninst + 7) / 8 * 8 : a.ninst;
@@ -358,7 +573,19 @@ hipError_t launch_epoch_reward(const EpochArgs& a, hipStream_t s) {
   const uint64_t vbpi = vblocks_per_inst(a.nval);
   const uint64_t blocks = (uint64_t)a.ninst * vbpi;
   if (!blocks) return hipSuccess;
-  hipLaunchKernelGGL(pz_epoch_reward_kernel, dim3((uint32_t)blocks), dim3(kThreads), 0, s, a, vbpi);
+  hipLaunchKernelGGL(pz_epoch_reward_kernel, dim3((uint32_t)vbpi, a.ninst), dim3(kThreads), 0, s, a, vbpi,
+                     vec_ok(a) ? 1 : 0, a.scal, a.boffs, a.total_deposit);
+  return hipGetLastError();
+}
+
+hipError_t launch_epoch_mid(const EpochArgs& a, bool winners, bool compact, hipStream_t s) {
+  const uint64_t vbpi = vblocks_per_inst(a.nval);
+  const uint64_t n = winners ? (uint64_t)a.ninst * a.natt : 0;
+  const uint64_t nwb = (n + kThreads - 1) / kThreads;
+  const uint64_t ncb = compact ? (uint64_t)a.ninst * vbpi : 0;
+  if (!(nwb + ncb)) return hipSuccess;
+  hipLaunchKernelGGL(pz_epoch_mid_kernel, dim3((uint32_t)(nwb + ncb)), dim3(kThreads), 0, s, a, vbpi, nwb,
+                     compact ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -305,6 +305,8 @@ static int check_batch(const pz_epoch_batch* b) {
   if (b->committee && b->natt && (!b->coffs || !b->att_comm || !b->vote || !b->total))
     return fail(PZ_EINVAL, "batch: missing committee arrays");
   if (b->pop_world == 0 || b->pop_rank >= b->pop_world) return fail(PZ_EINVAL, "batch: bad pop split");
+  if (b->ninst > 65535 || (uint64_t)b->ninst * b->natt >= (1ull << 32) || b->nval >= (1ull << 32))
+    return fail(PZ_EINVAL, "batch: more than 65535 instances, 2^32 attestations or 2^32 validators");
   return PZ_OK;
 }
 
@@ -320,11 +322,9 @@ int pz_dev_epoch_finish(const pz_epoch_batch* b, void* stream) {
   if (rc) return rc;
   if (!b->total_deposit) return fail(PZ_EINVAL, "batch: total_deposit is null");
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipSuccess;
-  if (b->committee && b->natt && b->nrec && b->winner && b->att_shard && b->rec_dynasty)
-    e = launch_epoch_winners(*b, s);
-  if (e == hipSuccess && b->nval == b->nval_global && b->act_mask && b->blk_cnt && b->act_list)
-    e = launch_epoch_compact(*b, false, s);
+  const bool winners = b->committee && b->natt && b->nrec && b->winner && b->att_shard && b->rec_dynasty;
+  const bool compact = b->nval == b->nval_global && b->act_mask && b->blk_cnt && b->act_list;
+  hipError_t e = launch_epoch_mid(*b, winners, compact, s);  // one launch: winners + compaction
   if (e == hipSuccess) e = launch_epoch_reward(*b, s);
   return e == hipSuccess ? PZ_OK : hip_fail(e, "epoch finish");
 }
@@ -419,6 +419,13 @@ int pz_shuffle_indices(const uint8_t seed[32], uint32_t* list, uint64_t n) {
 extern "C" int pz_debug_epoch_count(const pz_epoch_batch* b, int do_val, int do_pop, int do_xl, void* stream) {
   hipError_t e = pz::launch_epoch_count(*b, do_val != 0, do_pop != 0, do_xl != 0, (hipStream_t)stream);
   return e == hipSuccess ? PZ_OK : pz::hip_fail(e, "pz_epoch_count_kernel");
+}
+namespace pz {
+hipError_t launch_epoch_reward_mode(const EpochArgs& a, int mode, hipStream_t s);
+}
+extern "C" int pz_debug_epoch_reward_mode(const pz_epoch_batch* b, int mode, void* stream) {
+  hipError_t e = pz::launch_epoch_reward_mode(*b, mode, (hipStream_t)stream);
+  return e == hipSuccess ? PZ_OK : pz::hip_fail(e, "pz_epoch_reward_kernel (mode)");
 }
 extern "C" int pz_debug_epoch_reward(const pz_epoch_batch* b, void* stream) {
   hipError_t e = pz::launch_epoch_reward(*b, (hipStream_t)stream);

@@ -49,11 +49,13 @@ class DeviceEpoch:
         self.rec_dynasty = T(inst["rec_dynasty"].view(np.int64))
         natt = inst["natt"]
         nrec = inst["rec_dynasty"].shape[1]
-        # {scal, vote, total} contiguous: one all-reduce combines every partial sum
-        self.red = torch.zeros(B * SCAL_COUNT + 2 * B * natt, dtype=torch.int64, device=device)
-        self.scal = self.red[:B * SCAL_COUNT]
-        self.vote = self.red[B * SCAL_COUNT:B * SCAL_COUNT + B * natt]
-        self.total = self.red[B * SCAL_COUNT + B * natt:]
+        # {scal, vote, total} contiguous: one all-reduce combines every partial sum.  Two such
+        # buffers ping-pong: the finish pass of step k zeroes the scal of step k+1, so no
+        # memset launch is needed per step.
+        self.reds = [torch.zeros(B * SCAL_COUNT + 2 * B * natt, dtype=torch.int64, device=device)
+                     for _ in range(2)]
+        self.cur = 0
+        self._bind_red(B, natt)
         self.winner = torch.full((B * nrec,), -1, dtype=torch.int32, device=device)
         self.act_mask = torch.zeros(B * ((n + 63) // 64), dtype=torch.int64, device=device)
         self.blk_cnt = torch.zeros(B * ((n + 2047) // 2048 + 1), dtype=torch.int32, device=device)
@@ -69,19 +71,29 @@ class DeviceEpoch:
         b.committee, b.coffs = self.committee.data_ptr(), self.coffs.data_ptr()
         b.att_comm, b.att_shard = self.att_comm.data_ptr(), self.att_shard.data_ptr()
         b.nrec, b.rec_dynasty, b.winner = nrec, self.rec_dynasty.data_ptr(), self.winner.data_ptr()
-        b.vote, b.total, b.scal = self.vote.data_ptr(), self.total.data_ptr(), self.scal.data_ptr()
         b.act_mask, b.blk_cnt, b.act_list = (self.act_mask.data_ptr(), self.blk_cnt.data_ptr(),
                                              self.act_list.data_ptr())
         self.batch = b
         self.B, self.N, self.natt, self.nrec = B, N, natt, nrec
+        self._point_batch()
+
+    def _bind_red(self, B, natt):
+        self.red = self.reds[self.cur]
+        self.scal = self.red[:B * SCAL_COUNT]
+        self.vote = self.red[B * SCAL_COUNT:B * SCAL_COUNT + B * natt]
+        self.total = self.red[B * SCAL_COUNT + B * natt:]
+
+    def _point_batch(self):
+        b = self.batch
+        b.vote, b.total, b.scal = self.vote.data_ptr(), self.total.data_ptr(), self.scal.data_ptr()
+        b.scal_next = self.reds[1 - self.cur].data_ptr()
 
     def step(self, stream=None):
-        """One epoch transition of all B instances (enqueued on ``stream``; no host sync)."""
+        """One epoch transition of all B instances (enqueued on ``stream``; no host sync).
+        Results (``results()``) are in the buffer this step used."""
         torch = self.torch
         s = stream if stream is not None else torch.cuda.current_stream(self.dev)
         sh = ctypes.c_void_p(s.cuda_stream)
-        self.red.zero_()
-        self.winner.fill_(-1)
         lib.call("pz_dev_epoch_count", ctypes.byref(self.batch), sh)
         if self.world > 1:
             import torch.distributed as dist
@@ -93,13 +105,19 @@ class DeviceEpoch:
             nb = col.contiguous()
             dist.all_reduce(nb, op=dist.ReduceOp.SUM, group=self.group)
             col.copy_(nb)
+        self.last = self.cur
+        self.cur = 1 - self.cur
+        self.results_red = self.red
+        self._bind_red(self.B, self.natt)
+        self._point_batch()
 
     def results(self):
         """Host copies: (balance [B][n] uint64, scal [B][8] uint64, vote, total, winner)."""
         cpu = lambda t: t.cpu().numpy()  # noqa: E731
-        B = self.B
+        B, natt = self.B, self.natt
+        red = cpu(self.results_red).view(np.uint64)
         return (cpu(self.balance).view(np.uint64).reshape(B, -1),
-                cpu(self.scal).view(np.uint64).reshape(B, SCAL_COUNT),
-                cpu(self.vote).view(np.uint64).reshape(B, -1),
-                cpu(self.total).view(np.uint64).reshape(B, -1),
+                red[:B * SCAL_COUNT].reshape(B, SCAL_COUNT),
+                red[B * SCAL_COUNT:B * SCAL_COUNT + B * natt].reshape(B, -1),
+                red[B * SCAL_COUNT + B * natt:].reshape(B, -1),
                 cpu(self.winner).view(np.uint32).reshape(B, -1))

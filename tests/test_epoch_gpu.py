@@ -259,3 +259,25 @@ def test_device_epoch_vs_oracle(n, B, inactive):
         np.testing.assert_array_equal(vote[b], v)
         np.testing.assert_array_equal(total[b], t)
         np.testing.assert_array_equal(win[b], w)
+
+
+def test_device_epoch_repeated_steps_ping_pong():
+    """Consecutive steps (ping-pong scal buffers, in-kernel winner reset) equal the oracle
+    applied step after step."""
+    import torch
+
+    from prysm_amd.epoch import DeviceEpoch
+    n, B = 8192, 8
+    shuffled = casper.shuffle_indices(ref.bytes_to_hash(b"A"), np.arange(n, dtype=np.uint32))
+    inst = synth.epoch_batch(n, B, seed=21, shuffled=shuffled)
+    de = DeviceEpoch(inst, torch.device("cuda", 0))
+    for step in range(3):
+        de.step()
+        torch.cuda.synchronize()
+        bal, scal, vote, total, win = de.results()
+        for b in range(B):
+            nb, applied, nxt, v, t, w = _oracle_epoch(inst, b)
+            np.testing.assert_array_equal(bal[b], nb)
+            assert int(scal[b, _lib.SCAL_NEXT_BAL]) == nxt and bool(scal[b, _lib.SCAL_APPLIED]) == applied
+            np.testing.assert_array_equal(win[b], w)
+            inst["balance"][b] = nb  # the oracle's next step starts from the new balances

@@ -28,8 +28,15 @@ def main(nval=65536, ninst=256, rounds=5, reps=10):
         "count_xl": lambda: dll.pz_debug_epoch_count(bp, 0, 0, 1, sh),
         "count_all": lambda: dll.pz_debug_epoch_count(bp, 1, 1, 1, sh),
         "reward": lambda: dll.pz_debug_epoch_reward(bp, sh),
+        "reward_nobits": lambda: dll.pz_debug_epoch_reward_mode(bp, 1, sh),
+        "reward_noreduce": lambda: dll.pz_debug_epoch_reward_mode(bp, 2, sh),
+        "reward_nobits_noreduce": lambda: dll.pz_debug_epoch_reward_mode(bp, 3, sh),
         "step": lambda: de.step(s),
+        # yardsticks on the same 16.7M x u64 balance array (same process, same device)
+        "torch_copy": lambda: yard.copy_(de.balance.view(-1)),
+        "torch_inplace_add": lambda: yard.add_(1),
     }
+    yard = torch.empty(de.balance.numel(), dtype=torch.int64, device=dev)
     res = {k: [] for k in parts}
     de.step(s)
     for r in range(rounds):

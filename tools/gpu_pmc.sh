@@ -1,0 +1,15 @@
+#!/bin/bash
+# rocprofv3 counter passes (one counter group per run, each under its own kill timeout).
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${1:-pmc}; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+run() {  # name, counters...
+  local name=$1; shift
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d $O/$name -o $name -- python3 $R/tools/pmc_workload.py > $O/$name.log 2>&1 || { echo "PASS $name FAILED"; tail -5 $O/$name.log; exit 20; }
+  echo "pass $name ok"
+}
+run fetch FETCH_SIZE
+run write WRITE_SIZE
+run sq SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT
+run grbm GRBM_GUI_ACTIVE GRBM_COUNT
+echo ALLDONE
