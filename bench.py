@@ -64,6 +64,8 @@ def parse():
 # dynasty + 16 B balance read-modify-write + 1/8 B last-bitfield bit + 1/8 B committee bitfield
 # popcount + 12 B crosslink committee gather (u32 member + u64 balance).
 EPOCH_BYTES_PER_VALIDATOR = 44.25
+EPOCH_KERNELS = ("pz_epoch_count_kernel", "pz_epoch_mid_kernel", "pz_epoch_reward_kernel")
+HASH_KERNEL = "pz_b2b_fixed_persistent_kernel"
 
 
 def epoch_leg(args, torch, dist, dev, rank, world):
@@ -116,7 +118,9 @@ def epoch_leg(args, torch, dist, dev, rank, world):
                    "validators": nval, "instances_per_step": ninst, "attestations_per_instance": inst["natt"],
                    "parallelism": "validator-shard x%d + RCCL all-reduce" % world if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK, "traffic": None,
+                     "frac": achieved / HBM_PEAK,
+                     "traffic": pmc_traffic(EPOCH_KERNELS) if (nval, ninst) == (65536, 256) else None,
+                     "traffic_source": PMC_SUMMARY + " (count+mid+reward, 65,536 x 256 workload)",
                      "kernel": "epoch step (count+winner+compact+reward, device time of the whole step)",
                      "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": local_units * EPOCH_BYTES_PER_VALIDATOR},
@@ -141,12 +145,23 @@ def epoch_cpu_baseline(inst):
                 "sample": "unavailable: %s" % e}
 
 
-def load_pmc_traffic():
-    path = os.path.join(ROOT, "profiles", "hash_pmc_traffic.json")
-    if os.path.exists(path):
-        with open(path) as f:
-            return json.load(f)
-    return None
+PMC_SUMMARY = os.path.join("profiles", "r01", "pmc_summary.json")
+
+
+def pmc_traffic(kernels):
+    """HBM bytes per launch of ``kernels`` (summed) from the committed rocprofv3 --pmc summary
+    (tools/gpu_pmc.sh + tools/pmc_summary.py: FETCH_SIZE doubled per the gfx950 correction,
+    WRITE_SIZE as is).  PMC counters cannot be read inside this process, so the figure comes
+    from a separate profiled run of the same workload; None if the summary is absent."""
+    path = os.path.join(ROOT, PMC_SUMMARY)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    try:
+        return float(sum(d[k]["hbm_bytes_per_launch"] for k in kernels))
+    except KeyError:
+        return None
 
 
 def cpu_baseline(records_np):
@@ -222,7 +237,6 @@ def main():
         value = total / wall
         ops = n * 4 * OPS_PER_COMPRESSION
         achieved = ops / (kern_ms * 1e-3)
-        pmc = load_pmc_traffic()
         line = {
             "metric": METRIC,
             "value": value,
@@ -249,8 +263,9 @@ def main():
                 "frac_of_measured_issue_rate": achieved / XOR_RATE_UNDER_LOAD,
                 "cost_model": "per compression 96 G x (6 add64 @1/0.304 + 8 xor + 6 alignbit @1/0.602) + 32 xor "
                               "= %.0f full-rate slots" % OPS_PER_COMPRESSION,
-                "traffic": pmc.get("bytes_per_launch") if pmc else None,
-                "kernel": "pz_b2b_fixed_kernel",
+                "traffic": pmc_traffic([HASH_KERNEL]) if n == 1 << 20 else None,
+                "traffic_source": PMC_SUMMARY,
+                "kernel": HASH_KERNEL,
                 "kernel_ms": kern_ms,
                 "algorithmic_ops_per_launch": ops,
                 "hbm_view": {"bytes_per_launch": n * (512 + 32),

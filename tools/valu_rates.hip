@@ -57,7 +57,19 @@ __global__ void __launch_bounds__(256) k(uint32_t* out, int iters) {
       } else if (OP == 11) {  // v_add_co_u32 alone (VOP3, private carries)
 #define CO(lo, b, c) asm volatile("v_add_co_u32 %0, %1, %0, %2" : "+v"(lo), "=&s"(c) : "v"(b));
         CO(a0, b0, c0) CO(a1, b1, c1) CO(a2, b2, c2) CO(a3, b3, c3) CO(a4, b4, c0) CO(a5, b5, c1) CO(a6, b6, c2) CO(a7, b7, c3)
-      }
+      } else if (OP == 12) {  // 64-bit add as VOP2 v_add_co_u32_e32 + v_addc_co_u32_e32 through VCC
+#define ADDVCC(lo, hi, blo, bhi) asm volatile("v_add_co_u32_e32 %0, vcc, %2, %0\n v_addc_co_u32_e32 %1, vcc, %3, %1, vcc" : "+v"(lo), "+v"(hi) : "v"(blo), "v"(bhi) : "vcc");
+        ADDVCC(a0, a1, b0, b1) ADDVCC(a2, a3, b2, b3) ADDVCC(a4, a5, b4, b5) ADDVCC(a6, a7, b6, b7)
+      } else if (OP == 13) { EIGHT("v_add_u32_e64 %0, %0, %1") }
+      else if (OP == 14) { EIGHT("v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1") }
+      else if (OP == 15) { EIGHT("v_lshlrev_b32_e32 %0, 1, %0") }
+      else if (OP == 16) { EIGHT("v_xor_b32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD") }
+      else if (OP == 17) { EIGHT("v_xor_b32_e64 %0, %0, %1") }
+      else if (OP == 18) {  // dependent chain: one 64-bit VCC add chain per lane-pair (latency)
+        ADDVCC(a0, a1, b0, b1) ADDVCC(a0, a1, b2, b3) ADDVCC(a0, a1, b4, b5) ADDVCC(a0, a1, b6, b7)
+      } else if (OP == 19) { EIGHT("v_alignbit_b32 %0, %0, %1, %1") }
+      else if (OP == 20) { EIGHT("v_mov_b32_sdwa %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0") }
+      else if (OP == 21) { EIGHT("v_lshl_add_u32 %0, %0, 1, %1") }
     }
   }
   out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7 ^ b0 ^ b2 ^ b4 ^ b6 ^ (uint32_t)(c0 ^ c1 ^ c2 ^ c3);
@@ -77,7 +89,11 @@ int main() {
       {"v_xor_b32", k<0>, 8}, {"v_alignbit_b32", k<1>, 8}, {"v_perm_b32", k<2>, 8},
       {"v_add_u32", k<3>, 8}, {"v_add3_u32", k<4>, 8}, {"v_lshl_or_b32", k<5>, 8},
       {"v_bitop3_b32", k<6>, 8}, {"v_lshl_add_u64", k<7>, 8}, {"v_add_co+v_addc_co (s carry)", k<8>, 8},
-      {"v_lshlrev_b64", k<9>, 8}, {"v_mad_u64_u32", k<10>, 8}, {"v_add_co_u32 (s carry)", k<11>, 8}};
+      {"v_lshlrev_b64", k<9>, 8}, {"v_mad_u64_u32", k<10>, 8}, {"v_add_co_u32 (s carry)", k<11>, 8},
+      {"v_add_co_e32+v_addc_co_e32 (vcc)", k<12>, 8}, {"v_add_u32_e64", k<13>, 8}, {"v_xor_b32_sdwa", k<14>, 8},
+      {"v_lshlrev_b32_e32", k<15>, 8}, {"v_xor_b32_sdwa dword", k<16>, 8}, {"v_xor_b32_e64", k<17>, 8},
+      {"vcc add64 dependent chain", k<18>, 8}, {"v_alignbit_b32 (vgpr shift)", k<19>, 8},
+      {"v_mov_b32_sdwa", k<20>, 8}, {"v_lshl_add_u32", k<21>, 8}};
   double xor_rate = 0;
   for (auto& o : ops) {
     float best = 1e30f;
