@@ -130,9 +130,10 @@ int pz_shuffle_indices(const uint8_t seed[32], uint32_t* list, uint64_t n);
  * of nval_global.  `scal` must be zero before pass 1 (allocate it zeroed, then ping-pong
  * with `scal_next`, which the finish pass zeroes); pass 1 initialises `winner` itself.
  * Single GPU: pz_dev_epoch_count -> pz_dev_epoch_finish.  Multi-GPU: count ->
- * all-reduce(sum) over the contiguous block {scal, vote, total} -> finish ->
- * all-reduce(sum) of scal[.][PZ_SCAL_NEXT_BAL] (only the all-active rank path is
- * supported across ranks; single-rank handles any active set). */
+ * all-reduce(sum) over the contiguous block {scal, vote, total} -> [when not every
+ * validator is active: all-gather act_mask -> pz_dev_epoch_gather_compact] -> finish ->
+ * all-reduce(sum) of scal[.][PZ_SCAL_NEXT_BAL].  After a multi-rank all-reduce,
+ * PZ_SCAL_MAXIDX1 holds the sum of the per-rank values (single rank: the value). */
 #define PZ_SCAL_POP       0  /* attester bit count (deposit = 32 * this)               */
 #define PZ_SCAL_NACT      1  /* validators matching `kind` in range                     */
 #define PZ_SCAL_ERR_XL    2  /* != 0: processCrosslinks would panic                     */
@@ -217,6 +218,15 @@ int pz_dev_epoch_count(const pz_epoch_batch* b, void* stream);
 /* Pass 2 (after any cross-rank all-reduce): winners, active-list compaction when needed,
  * rewards in place and the post-reward total. */
 int pz_dev_epoch_finish(const pz_epoch_batch* b, void* stream);
+
+/* Multi-rank general rank path (not every validator active): between count and finish,
+ * all-gather every rank's act_mask into gathered_mask[world][B][shard_words] (rank r owns the
+ * global validators [r*64*shard_words, (r+1)*64*shard_words)), then call this to rebuild the
+ * global compacted active list act_list[B][nval_global] on every rank; CalculateRewards
+ * (casper/incentives.go:22-28) reads it by global rank position.  gblk is scratch
+ * [B][ceil(nval_global/2048)] u32.  Instances with every validator active are skipped. */
+int pz_dev_epoch_gather_compact(const pz_epoch_batch* b, const uint64_t* gathered_mask, uint32_t world,
+                                uint64_t shard_words, uint32_t* gblk, void* stream);
 
 #ifdef __cplusplus
 }

@@ -67,6 +67,7 @@ SIGNATURES = {
     "pz_shuffle_indices": [vp, vp, u64],
     "pz_dev_epoch_count": [vp, vp],
     "pz_dev_epoch_finish": [vp, vp],
+    "pz_dev_epoch_gather_compact": [vp, vp, u32, u64, vp, vp],
     "pz_dev_vote_tally": [vp, vp],
     "pz_vote_tally": [vp, vp, u64, vp, vp, vp, u64, vp, vp, u64, vp, u64, vp, u64, u64, vp],
 }

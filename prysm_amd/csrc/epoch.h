@@ -37,6 +37,10 @@ hipError_t launch_epoch_winners(const EpochArgs& a, hipStream_t s);
 // General rank path: scan per-block counts and compact the active list (no-op per instance
 // when every validator is active).  Single-rank only (multi-rank gathers lists itself).
 hipError_t launch_epoch_compact(const EpochArgs& a, bool force, hipStream_t s);
+// Multi-rank general rank path: global active list from the all-gathered shard masks
+// gmask[world][B][sw] (gblk: scratch [B][vblocks_per_inst(nval_global)]).
+hipError_t launch_epoch_gather_compact(const EpochArgs& a, const uint64_t* gmask, uint64_t sw, uint32_t* gblk,
+                                       hipStream_t s);
 // Winners + compaction in one launch (the device-resident finish path).
 hipError_t launch_epoch_mid(const EpochArgs& a, bool winners, bool compact, hipStream_t s);
 // Pass 2: rewards (in place) + post-reward active balance sum.

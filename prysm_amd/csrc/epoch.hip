@@ -339,6 +339,73 @@ pz_epoch_mid_kernel(EpochArgs a, uint64_t vbpi, uint64_t nwb, int do_compact) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Multi-rank general rank path.  Each rank's count pass wrote the active bitmask of its own
+// shard; an all-gather hands every rank the rank-major stack gmask[world][B][shard_words]
+// (rank r owns global validators [r*64*shard_words, (r+1)*64*shard_words)).  From it every
+// rank rebuilds the same global compacted list act_list[B][nval_global], which the reward
+// pass reads by global rank position (incentives.go:22-23: validators[i] <- CheckBit(bf, a[i])).
+// Both kernels: grid (chunks of 2048 global validators, B), one wave per block; an instance
+// whose validators are all active (rank == index) is skipped.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t gmask_word(const uint64_t* gmask, uint32_t ninst, uint64_t sw, uint64_t inst,
+                                               uint64_t w) {
+  const uint64_t r = w / sw;
+  return gmask[(r * ninst + inst) * sw + (w - r * sw)];
+}
+
+constexpr int kWordsPerChunk = (int)(kValPerBlock / 64);  // 32
+
+extern "C" __global__ void __launch_bounds__(64)
+pz_epoch_gcount_kernel(EpochArgs a, const uint64_t* __restrict__ gmask, uint64_t sw, uint32_t* gblk) {
+  const uint64_t inst = blockIdx.y, chunk = blockIdx.x;
+  if (a.scal[inst * kScal + kNact] == a.nval_global) return;
+  const int lane = threadIdx.x;
+  const uint64_t nw = (a.nval_global + 63) / 64;
+  const uint64_t w = chunk * kWordsPerChunk + lane;
+  uint64_t c = (lane < kWordsPerChunk && w < nw) ? (uint64_t)__popcll(gmask_word(gmask, a.ninst, sw, inst, w)) : 0;
+  c = wave_sum(c);
+  if (lane == 0) gblk[inst * gridDim.x + chunk] = (uint32_t)c;
+}
+
+extern "C" __global__ void __launch_bounds__(64)
+pz_epoch_gcompact_kernel(EpochArgs a, const uint64_t* __restrict__ gmask, uint64_t sw, const uint32_t* gblk) {
+  const uint64_t inst = blockIdx.y, chunk = blockIdx.x;
+  if (a.scal[inst * kScal + kNact] == a.nval_global) return;
+  const int lane = threadIdx.x;
+  uint64_t base = 0;  // active validators in the chunks before this one
+  for (uint64_t c = lane; c < chunk; c += 64) base += gblk[inst * gridDim.x + c];
+  base = wave_sum(base);
+  const uint64_t nw = (a.nval_global + 63) / 64;
+  const uint64_t w = chunk * kWordsPerChunk + lane;
+  uint64_t bits = (lane < kWordsPerChunk && w < nw) ? gmask_word(gmask, a.ninst, sw, inst, w) : 0;
+  // exclusive prefix of the per-word counts across the wave (ascending word == ascending index)
+  const uint32_t cnt = (uint32_t)__popcll(bits);
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  uint64_t pos = base + incl - cnt;
+  uint32_t* out = a.act_list + inst * a.nval_global;
+  while (bits) {
+    const int b = __ffsll((unsigned long long)bits) - 1;
+    out[pos++] = (uint32_t)(w * 64 + b);
+    bits &= bits - 1;
+  }
+}
+
+hipError_t launch_epoch_gather_compact(const EpochArgs& a, const uint64_t* gmask, uint64_t sw, uint32_t* gblk,
+                                       hipStream_t s) {
+  const uint64_t chunks = vblocks_per_inst(a.nval_global);
+  if (!chunks || !a.ninst) return hipSuccess;
+  const dim3 grid((uint32_t)chunks, a.ninst);
+  hipLaunchKernelGGL(pz_epoch_gcount_kernel, grid, dim3(64), 0, s, a, gmask, sw, gblk);
+  hipLaunchKernelGGL(pz_epoch_gcompact_kernel, grid, dim3(64), 0, s, a, gmask, sw, gblk);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
 // Pass 2: CalculateRewards (incentives.go:14-32) fused with the next-cycle balance sum
 // (core.go:459-464).  Position p receives +-1 by CheckBit(last bitfield, active[p]).
 // ------------------------------------------------------------------------------------------

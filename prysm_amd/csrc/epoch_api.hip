@@ -329,6 +329,19 @@ int pz_dev_epoch_finish(const pz_epoch_batch* b, void* stream) {
   return e == hipSuccess ? PZ_OK : hip_fail(e, "epoch finish");
 }
 
+int pz_dev_epoch_gather_compact(const pz_epoch_batch* b, const uint64_t* gathered_mask, uint32_t world,
+                                uint64_t shard_words, uint32_t* gblk, void* stream) {
+  int rc = check_batch(b);
+  if (rc) return rc;
+  if (!gathered_mask || !gblk || !b->act_list) return fail(PZ_EINVAL, "gather_compact: null pointer");
+  if (!world || !shard_words || b->val_offset % (64 * shard_words) ||
+      (uint64_t)world * 64 * shard_words < b->nval_global || b->nval > 64 * shard_words)
+    return fail(PZ_EINVAL, "gather_compact: shards must be %llu-validator aligned ranges covering nval_global",
+                (unsigned long long)(64 * shard_words));
+  hipError_t e = launch_epoch_gather_compact(*b, gathered_mask, shard_words, gblk, (hipStream_t)stream);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "pz_epoch_gcompact_kernel");
+}
+
 // ---- vote-cache tally ----------------------------------------------------------------------
 int pz_dev_vote_tally(const pz_vote_batch* b, void* stream) {
   if (!b) return fail(PZ_EINVAL, "batch is null");

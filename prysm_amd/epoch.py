@@ -15,22 +15,48 @@ from prysm_amd import _lib
 from prysm_amd._lib import EpochBatch, SCAL_COUNT, lib
 
 
+def shard_words(nval_global, world):
+    """64-validator words per shard: every shard but the last holds exactly 64 * this many
+    validators, so the shards' active bitmasks concatenate (rank-major) into the global mask."""
+    return max(1, -(-nval_global // (64 * world)))
+
+
 def shard_range(nval_global, rank, world):
-    """Contiguous validator range [lo, hi) of ``rank`` (balanced to within one validator)."""
-    lo = nval_global * rank // world
-    hi = nval_global * (rank + 1) // world
-    return lo, hi
+    """Contiguous, 64-aligned validator range [lo, hi) of ``rank``."""
+    s = 64 * shard_words(nval_global, world)
+    return min(nval_global, rank * s), min(nval_global, (rank + 1) * s)
+
+
+class HipEpochKernels:
+    """The product kernels: the C-ABI entry points of libprysm_hip.so (include/prysm_hip.h)."""
+
+    def count(self, batch, stream):
+        lib.call("pz_dev_epoch_count", ctypes.byref(batch), stream)
+
+    def gather_compact(self, batch, gmask_ptr, world, sw, gblk_ptr, stream):
+        lib.call("pz_dev_epoch_gather_compact", ctypes.byref(batch), gmask_ptr, world, sw, gblk_ptr, stream)
+
+    def finish(self, batch, stream):
+        lib.call("pz_dev_epoch_finish", ctypes.byref(batch), stream)
 
 
 class DeviceEpoch:
     """B epoch instances resident on one GPU (one validator shard of each instance)."""
 
-    def __init__(self, inst, device, rank=0, world=1, group=None):
+    def __init__(self, inst, device, rank=0, world=1, group=None, kernels=None, general=None):
+        """``kernels``: the pass implementations (default: the HIP library).  ``general``:
+        run the multi-rank general rank path (all-gather of the active masks); by default
+        it is enabled when some validator of some instance is not active at its dynasty."""
         import torch
         self.torch = torch
-        self.dev = device
+        self.dev = torch.device(device)
+        self.kernels = kernels or HipEpochKernels()
         self.rank, self.world, self.group = rank, world, group
         B, N = inst["ninst"], inst["nval"]
+        if general is None:
+            d = inst["dynasty"][:, None]
+            general = not bool(np.all((inst["start"] <= d) & (d < inst["end"])))
+        self.general = bool(general) and world > 1
         lo, hi = shard_range(N, rank, world)
         self.lo, self.hi = lo, hi
         n = hi - lo
@@ -60,6 +86,13 @@ class DeviceEpoch:
         self.act_mask = torch.zeros(B * ((n + 63) // 64), dtype=torch.int64, device=device)
         self.blk_cnt = torch.zeros(B * ((n + 2047) // 2048 + 1), dtype=torch.int32, device=device)
         self.act_list = torch.zeros(max(B * N, 1), dtype=torch.int32, device=device)
+        self.sw = shard_words(N, world)
+        if self.general:
+            # this rank's mask padded to the common shard width, the gathered stack, and the
+            # per-chunk counts of the global compaction
+            self.mask_send = torch.zeros(B * self.sw, dtype=torch.int64, device=device)
+            self.gmask = torch.zeros(world * B * self.sw, dtype=torch.int64, device=device)
+            self.gblk = torch.zeros(B * ((N + 2047) // 2048), dtype=torch.int32, device=device)
         b = EpochBatch()
         b.ninst, b.nval, b.val_offset, b.nval_global = B, n, lo, N
         b.kind = _lib.KIND_ACTIVE
@@ -88,22 +121,63 @@ class DeviceEpoch:
         b.vote, b.total, b.scal = self.vote.data_ptr(), self.total.data_ptr(), self.scal.data_ptr()
         b.scal_next = self.reds[1 - self.cur].data_ptr()
 
-    def step(self, stream=None):
-        """One epoch transition of all B instances (enqueued on ``stream``; no host sync).
-        Results (``results()``) are in the buffer this step used."""
+    def _host_collectives(self):
+        import torch.distributed as dist
+        return self.dev.type == "cuda" and dist.get_backend(self.group) == "gloo"
+
+    def _all_reduce(self, t):
+        """Sum over ranks in place.  RCCL ("nccl") reduces device tensors over xGMI; the gloo
+        path (tests: several ranks sharing one GPU) reduces a host copy."""
+        import torch.distributed as dist
+        if self._host_collectives():
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+
+    def _all_gather_masks(self):
+        """act_mask [B][local words] of every rank -> gmask [world][B][sw] (rank-major)."""
+        import torch.distributed as dist
         torch = self.torch
-        s = stream if stream is not None else torch.cuda.current_stream(self.dev)
-        sh = ctypes.c_void_p(s.cuda_stream)
-        lib.call("pz_dev_epoch_count", ctypes.byref(self.batch), sh)
+        B, sw = self.B, self.sw
+        wl = self.act_mask.numel() // B
+        send = self.mask_send.view(B, sw)
+        send[:, :wl].copy_(self.act_mask.view(B, wl))
+        if self._host_collectives():  # small: B * nval_global / 8 bytes
+            parts = [torch.empty(B * sw, dtype=torch.int64) for _ in range(self.world)]
+            dist.all_gather(parts, self.mask_send.cpu(), group=self.group)
+            self.gmask.copy_(torch.cat(parts))
+        else:
+            dist.all_gather_into_tensor(self.gmask, self.mask_send, group=self.group)
+
+    def _stream_handle(self, stream):
+        if self.dev.type != "cuda":
+            return ctypes.c_void_p(0)
+        s = stream if stream is not None else self.torch.cuda.current_stream(self.dev)
+        return ctypes.c_void_p(s.cuda_stream)
+
+    def step(self, stream=None):
+        """One epoch transition of all B instances (enqueued on ``stream``; no host sync
+        on a single GPU).  Results (``results()``) are in the buffer this step used.
+
+        Multi-rank sequence: count (local partial sums) -> all-reduce {scal, vote, total}
+        -> [general path: all-gather active masks -> global compaction] -> finish (winners,
+        rewards on the local shard, partial next-cycle balance) -> all-reduce of that column.
+        Integer sums mod 2^64 commute, so the result is bit-exact for any reduction order."""
+        sh = self._stream_handle(stream)
+        self.kernels.count(self.batch, sh)
         if self.world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(self.red, op=dist.ReduceOp.SUM, group=self.group)
-        lib.call("pz_dev_epoch_finish", ctypes.byref(self.batch), sh)
+            self._all_reduce(self.red)
+            if self.general:
+                self._all_gather_masks()
+                self.kernels.gather_compact(self.batch, self.gmask.data_ptr(), self.world, self.sw,
+                                            self.gblk.data_ptr(), sh)
+        self.kernels.finish(self.batch, sh)
         if self.world > 1:
-            import torch.distributed as dist
             col = self.scal.view(self.B, SCAL_COUNT)[:, _lib.SCAL_NEXT_BAL]
             nb = col.contiguous()
-            dist.all_reduce(nb, op=dist.ReduceOp.SUM, group=self.group)
+            self._all_reduce(nb)
             col.copy_(nb)
         self.last = self.cur
         self.cur = 1 - self.cur

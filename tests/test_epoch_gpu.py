@@ -9,6 +9,8 @@ from oracle import schema as pb
 from prysm_amd import _lib, casper, synth
 from prysm_amd.params import DEFAULT_END_DYNASTY
 
+from epoch_ref_helpers import oracle_epoch
+
 pytestmark = pytest.mark.gpu
 U64 = np.uint64
 
@@ -219,18 +221,7 @@ def test_crosslink_short_bitfield_panics():
 
 
 # ---- device-resident batched epoch ---------------------------------------------------------
-def _oracle_epoch(inst, b):
-    bal = inst["balance"][b]
-    s, e = inst["start"][b], inst["end"][b]
-    natt = inst["natt"]
-    bo = inst["boffs"][b * natt:(b + 1) * natt + 1]
-    v, t = onp.crosslink_tallies(inst["committee"], inst["coffs"], inst["att_comm"][b * natt:(b + 1) * natt],
-                                 inst["bits"], bo, bal)
-    win = onp.crosslink_winners(v, t, inst["att_shard"][b * natt:(b + 1) * natt], inst["rec_dynasty"][b],
-                                int(inst["dynasty"][b]))
-    nb, applied = onp.calculate_rewards(bal, s, e, int(inst["dynasty"][b]), int(inst["total_deposit"][b]),
-                                        inst["bits"], bo)
-    return nb, applied, onp.active_balance_sum(nb, s, e, int(inst["dynasty"][b])), v, t, win
+_oracle_epoch = oracle_epoch
 
 
 @pytest.mark.parametrize("n,B,inactive", [(65536, 3, False), (5000, 2, True), (20000, 1, True), (4096, 9, False),
