@@ -341,7 +341,9 @@ def process_attestation(cstate, astate, block_slot, att):
 
 
 def calculate_block_vote_cache(cstate, astate, cache, block_slot, att):
-    """blockchain/core.go:300-345.  ``cache`` maps 32-byte hash -> [voter list, total]."""
+    """blockchain/core.go:300-345.  ``cache`` maps 32-byte hash -> [VoterIndices, total].
+    VoterIndices is an insertion-ordered dict (the Go slice's append order; the linear
+    membership scan of core.go:333-337 becomes a dict lookup, same answer)."""
     parents = get_signed_parent_hashes(astate, block_slot, att)
     committee = get_attester_indices(cstate, att)
     obliques = [bytes(o) for o in att.oblique_parent_hashes]
@@ -349,13 +351,13 @@ def calculate_block_vote_cache(cstate, astate, cache, block_slot, att):
         if any(h == o for o in obliques):
             continue
         if h not in cache:
-            cache[h] = [[], 0]
+            cache[h] = [{}, 0]
         entry = cache[h]
         for i, v in enumerate(committee):
             if not check_bit(att.attester_bitfield, i):
                 continue
             if v not in entry[0]:
-                entry[0].append(v)
+                entry[0][v] = None
                 entry[1] = (entry[1] + cstate.validators[v].balance) & M64
     return cache
 

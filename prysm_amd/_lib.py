@@ -86,6 +86,15 @@ class EpochBatch(ctypes.Structure):
     ]
 
 
+class VoteBatch(ctypes.Structure):
+    """Mirror of ``pz_vote_batch`` (include/prysm_hip.h)."""
+    _fields_ = [
+        ("committee", vp), ("coffs", vp), ("att_comm", vp), ("bits", vp), ("boffs", vp),
+        ("item_att", vp), ("item_slot", vp), ("nitems", u64), ("balance", vp), ("nval", u64),
+        ("bitmaps", vp), ("words_per_slot", u64), ("totals", vp), ("err", vp),
+    ]
+
+
 SCAL_POP, SCAL_NACT, SCAL_ERR_XL, SCAL_ERR_RWD, SCAL_APPLIED, SCAL_NEXT_BAL, SCAL_MAXIDX1 = range(7)
 SCAL_COUNT = 8
 KIND_ACTIVE, KIND_EXITED, KIND_QUEUED = 0, 1, 2

@@ -120,3 +120,65 @@ def attestation_records_512(n, seed=2):
     const(0x42, 20); put(_varint_fixed(sig[:, 0], 10)); put(_varint_fixed(sig[:, 1], 10))
     assert col == RECORD_BYTES, col
     return rec
+
+
+def genesis_committee_sizes(nval):
+    """Shard ids and member counts of the slot-0 committees of the genesis shuffle
+    (types/state.go:68-78 -> casper/sharding.go:27-53).  Sizes depend only on the validator
+    count, so no shuffle is needed to shape attestations for them."""
+    from prysm_amd.casper import split_by_slot_shard
+    slot0 = split_by_slot_shard(list(range(nval)), 0)[0]
+    return [(int(shard), int(len(c))) for shard, c in slot0]
+
+
+def chain_blocks(nval, nblocks, seed=1, participation=(1.0, 0.25), n_oblique=1, committees=None):
+    """A synthetic chain of ``nblocks`` blocks (slots 1..nblocks) that the reference's
+    ChainService.blockProcessing (blockchain/service.go:229-363) processes end to end.
+
+    Each block carries one AttestationRecord per slot-0 committee (``committees`` limits the
+    count).  Its slot is ``64 * (s // 64)`` for block slot ``s``: the only choice that never
+    makes the reference index ShardAndCommitteesForSlots with a wrapped-around
+    ``Slot - LastStateRecalc`` (core.go:367), neither in processAttestation nor in the
+    stateRecalc after next (pending attestations survive one recalc, core.go:445-450).
+    Bitfields have BitLength(k) bytes with clear trailing bits (core.go:377-394); committee
+    j of block s sets each bit with probability ``participation[(s + j) % len(participation)]``.
+    The default mix keeps the attester popcount under 2/3 of the deposits, so
+    CalculateRewards does not run into its CheckBit-by-global-index panic (SURVEY.md §0 fact
+    2); ``participation=(1.0,)`` reproduces that panic at the first cycle transition.
+
+    Timestamps are 8 s per slot (Timestamp{8*s, 0}); the parent of block 1 is the genesis
+    block.  Parent digests are computed here with hashlib (input generation only: the
+    replay under test recomputes every digest on the GPU and checks parents against them).
+    Returns the list of ``pb.BeaconBlock``."""
+    import hashlib
+
+    from prysm_amd import pb, wire
+    from prysm_amd.params import CYCLE_LENGTH
+
+    rng = np.random.default_rng(seed)
+    comms = genesis_committee_sizes(nval)
+    if committees is not None:
+        comms = comms[:committees]
+    parent = hashlib.blake2b(wire.beacon_block(pb.BeaconBlock(timestamp=pb.Timestamp())), digest_size=64).digest()[:32]
+    out = []
+    for s in range(1, nblocks + 1):
+        a_slot = CYCLE_LENGTH * (s // CYCLE_LENGTH)
+        atts = []
+        for j, (shard, k) in enumerate(comms):
+            p = participation[(s + j) % len(participation)]
+            nb = (k + 7) // 8
+            bits = (rng.random(8 * nb) < p)
+            bits[k:] = False
+            atts.append(pb.AttestationRecord(
+                slot=a_slot, shard_id=shard, justified_slot=0,
+                justified_block_hash=rng.bytes(32), shard_block_hash=rng.bytes(32),
+                attester_bitfield=np.packbits(bits).tobytes(),
+                oblique_parent_hashes=[rng.bytes(32) for _ in range(n_oblique)],
+                aggregate_sig=[int(x) for x in rng.integers(0, 1 << 63, size=2, dtype=np.uint64)]))
+        blk = pb.BeaconBlock(parent_hash=parent, slot_number=s, randao_reveal=rng.bytes(32),
+                             pow_chain_ref=rng.bytes(32), active_state_hash=rng.bytes(32),
+                             crystallized_state_hash=rng.bytes(32), timestamp=pb.Timestamp(8 * s, 0),
+                             attestations=atts)
+        out.append(blk)
+        parent = hashlib.blake2b(wire.beacon_block(blk), digest_size=64).digest()[:32]
+    return out

@@ -131,8 +131,33 @@ def reward_vectors():
     return cases
 
 
+def replay_vectors(nval=1024, nblocks=130, seed=1):
+    """oracle/replay.py over prysm_amd.synth.chain_blocks (input generation: numpy + hashlib)."""
+    import hashlib
+
+    from oracle import replay
+    from prysm_amd import synth
+    blocks = synth.chain_blocks(nval, nblocks, seed=seed)
+    pbs = [replay.to_pb_block(b) for b in blocks]
+    recs, roots = replay.replay(blocks, nval)
+    h = hashlib.sha256(b"".join(b.SerializeToString() for b in pbs)).hexdigest()
+    out = {"nval": nval, "nblocks": nblocks, "seed": seed, "blocks_sha256": h,
+           "records": [{"hash": r["hash"].hex(), "status": r["status"], "transition": r["transition"],
+                        "atts": [{k: (v.hex() if isinstance(v, bytes) else v) for k, v in a.items()} for a in r["atts"]]}
+                       for r in recs],
+           "roots": {k: v.hex() for k, v in roots.items() if isinstance(v, bytes)},
+           "vote_totals": {k.hex(): v for k, v in sorted(roots["vote_totals"].items())}}
+    try:  # the same generator with full participation: CalculateRewards panics (SURVEY.md §0 fact 2)
+        replay.replay(synth.chain_blocks(nval, 70, seed=seed, participation=(1.0,)), nval)
+        out["full_participation_panics_at"] = None
+    except ref.GoPanic as e:
+        out["full_participation_panics_at"] = str(e)
+    return out
+
+
 def main():
     fixtures = {
+        "replay_n1024.json": replay_vectors(),
         "blake2b.json": blake2b_vectors(),
         "attestations.json": attestation_vectors(),
         "blocks.json": block_vectors(),

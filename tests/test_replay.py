@@ -1,0 +1,198 @@
+"""Block pipeline parity (BASELINE configs[0] and the per-block work of configs[4]): the
+GPU-batched ``prysm_amd.blockchain.BeaconChain`` vs the oracle's restatement of
+``ChainService.blockProcessing`` (oracle/replay.py), bit-exact on every block digest,
+attestation Hash/Key, 64-byte message digest, vote-cache total and final state root.
+
+CPU: the oracle reproduces the committed fixture (tests/golden/replay_n1024.json, written by
+tests/golden/make_golden.py) and the generator still produces the same blocks.
+GPU: the product reproduces the fixture, a live oracle run at 65,536 validators (5
+committees per block, 64 signed parent hashes each), and the reference's panic.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from prysm_amd import synth
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def golden():
+    with open(os.path.join(HERE, "golden", "replay_n1024.json")) as f:
+        return json.load(f)
+
+
+def _hexrecs(recs):
+    return [{"hash": r["hash"].hex(), "status": r["status"], "transition": r["transition"],
+             "atts": [{k: (v.hex() if isinstance(v, bytes) else v) for k, v in a.items()} for a in r["atts"]]}
+            for r in recs]
+
+
+def _compare(recs, roots, g):
+    got = _hexrecs(recs)
+    assert len(got) == len(g["records"])
+    for i, (a, b) in enumerate(zip(got, g["records"])):
+        assert a == b, "block %d differs" % (i + 1)
+    for k, v in g["roots"].items():
+        assert roots[k].hex() == v, k
+    assert {k.hex(): v for k, v in roots["vote_totals"].items()} == g["vote_totals"]
+
+
+def test_generator_is_pinned():
+    from oracle import replay
+    g = golden()
+    blocks = synth.chain_blocks(g["nval"], g["nblocks"], seed=g["seed"])
+    h = hashlib.sha256(b"".join(replay.to_pb_block(b).SerializeToString() for b in blocks)).hexdigest()
+    assert h == g["blocks_sha256"]
+
+
+def test_oracle_replay_matches_golden():
+    from oracle import replay
+    g = golden()
+    recs, roots = replay.replay(synth.chain_blocks(g["nval"], g["nblocks"], seed=g["seed"]), g["nval"])
+    _compare(recs, roots, g)
+    assert sum(r["transition"] for r in recs) == 2 and all(r["status"] == "processed" for r in recs)
+
+
+def _product(nval, blocks):
+    from prysm_amd.blockchain import BeaconChain
+    ch = BeaconChain(nval)
+    recs = ch.process_blocks(blocks)
+    return recs, ch.roots()
+
+
+@pytest.mark.gpu
+def test_gpu_replay_matches_golden():
+    g = golden()
+    recs, roots = _product(g["nval"], synth.chain_blocks(g["nval"], g["nblocks"], seed=g["seed"]))
+    _compare(recs, roots, g)
+
+
+@pytest.mark.gpu
+def test_gpu_replay_in_two_batches_matches_golden():
+    """Blocks fed in two batches (deferred work flushed between calls) give the same result."""
+    from prysm_amd.blockchain import BeaconChain
+    g = golden()
+    blocks = synth.chain_blocks(g["nval"], g["nblocks"], seed=g["seed"])
+    ch = BeaconChain(g["nval"])
+    recs = ch.process_blocks(blocks[:70]) + ch.process_blocks(blocks[70:])
+    _compare(recs, ch.roots(), g)
+
+
+@pytest.mark.gpu
+def test_gpu_replay_vs_live_oracle_65536():
+    from oracle import replay
+    nval = 65536
+    blocks = synth.chain_blocks(nval, 70, seed=6)
+    o_recs, o_roots = replay.replay(blocks, nval)
+    recs, roots = _product(nval, blocks)
+    assert _hexrecs(recs) == _hexrecs(o_recs)
+    for k in ("chain_active", "chain_crystallized", "cand_active", "cand_crystallized"):
+        assert roots[k] == o_roots[k], k
+    assert roots["vote_totals"] == o_roots["vote_totals"]
+    assert sum(len(r["atts"]) for r in recs) == 70 * 5
+
+
+def _relink(blocks):
+    """Recompute parent digests after editing blocks (as the generator does)."""
+    from prysm_amd import pb, wire
+    parent = hashlib.blake2b(wire.beacon_block(pb.BeaconBlock(timestamp=pb.Timestamp())), digest_size=64).digest()[:32]
+    for b in blocks:
+        b.parent_hash = parent
+        parent = hashlib.blake2b(wire.beacon_block(b), digest_size=64).digest()[:32]
+    return blocks
+
+
+def edited_chain():
+    """1,000 validators (15- and 16-member committees, so trailing bitfield bits exist) with
+    invalid attestations mixed into valid blocks: canProcessAttestations follows the LAST
+    attestation (service.go:281-301), the vote cache still tallies every attestation of a
+    processed block (service.go:313-318), and a rejected block orphans its descendants."""
+    import dataclasses
+    blocks = synth.chain_blocks(1000, 24, seed=3)
+
+    def bad(k, **kw):
+        return dataclasses.replace(blocks[k].attestations[0], **kw)
+
+    v = blocks[2].attestations[0]
+    blocks[2].attestations = [bad(2, attester_bitfield=v.attester_bitfield + b"\x00"), v]
+    v = blocks[5].attestations[0]
+    blocks[5].attestations = [bad(5, attester_bitfield=v.attester_bitfield[:-1] + bytes([v.attester_bitfield[-1] | 1])), v]
+    v = blocks[8].attestations[0]
+    blocks[8].attestations = [v, bad(8, shard_id=999), v]
+    v = blocks[11].attestations[0]
+    blocks[11].attestations = [bad(11, justified_slot=7), v]
+    v = blocks[14].attestations[0]
+    blocks[14].attestations = [bad(14, oblique_parent_hashes=[b"\x05" * 5]), v]
+    v = blocks[19].attestations[0]
+    blocks[19].attestations = [v, bad(19, justified_slot=7)]
+    return _relink(blocks)
+
+
+def test_oracle_edited_chain_statuses():
+    from oracle import replay
+    recs, _ = replay.replay(edited_chain(), 1000)
+    st = [r["status"] for r in recs]
+    assert st[:19] == ["processed"] * 19 and st[19] == "attestations_rejected" and set(st[20:]) == {"no_parent"}
+    errs = [a["error"] for r in recs for a in r["atts"] if "error" in a]
+    assert len(errs) == 5
+
+
+def future_slot_chain():
+    """An attestation from a future slot is rejected by processAttestation, but the vote
+    cache loop still slices RecentBlockHashes with the wrapped start index: the reference
+    panics (core.go:353)."""
+    import dataclasses
+    blocks = synth.chain_blocks(1024, 8, seed=4)
+    v = blocks[5].attestations[0]
+    blocks[5].attestations = [dataclasses.replace(v, slot=100), v]
+    return _relink(blocks)
+
+
+def test_oracle_future_slot_panics():
+    from oracle import ref, replay
+    with pytest.raises(ref.GoPanic):
+        replay.replay(future_slot_chain(), 1024)
+
+
+@pytest.mark.gpu
+def test_gpu_future_slot_panics():
+    from prysm_amd.blockchain import BeaconChain, ChainPanic
+    with pytest.raises(ChainPanic):
+        BeaconChain(1024).process_blocks(future_slot_chain())
+
+
+@pytest.mark.gpu
+def test_gpu_replay_rejections_and_missing_parents():
+    from oracle import replay
+    blocks = edited_chain()
+    o_recs, o_roots = replay.replay(blocks, 1000)
+    recs, roots = _product(1000, blocks)
+    strip = lambda rs: [{**r, "atts": [a if "error" not in a else {"error": True} for a in r["atts"]]} for r in rs]  # noqa: E731
+    assert strip(_hexrecs(recs)) == strip(_hexrecs(o_recs))
+    for k in ("chain_active", "chain_crystallized", "cand_active", "cand_crystallized"):
+        assert roots[k] == o_roots[k], k
+    assert roots["vote_totals"] == o_roots["vote_totals"]
+
+
+@pytest.mark.gpu
+def test_gpu_replay_reproduces_reward_panic():
+    from prysm_amd.blockchain import BeaconChain, ChainPanic
+    g = golden()
+    assert g["full_participation_panics_at"]
+    ch = BeaconChain(g["nval"])
+    with pytest.raises(ChainPanic):
+        ch.process_blocks(synth.chain_blocks(g["nval"], 70, seed=g["seed"], participation=(1.0,)))
+
+
+def test_generator_shape():
+    blocks = synth.chain_blocks(65536, 3, seed=6)
+    assert [len(b.attestations) for b in blocks] == [5, 5, 5]
+    k = [len(a.attester_bitfield) for a in blocks[0].attestations]
+    assert k == [26, 26, 26, 26, 26]
+    assert all(len(a.oblique_parent_hashes) == 1 for a in blocks[0].attestations)
+    bf = np.frombuffer(blocks[0].attestations[0].attester_bitfield, np.uint8)
+    assert bf[-1] & 0x0F == 0  # 204 members: the last 4 bits are padding
