@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-epoch", action="store_true")
     p.add_argument("--no-hash", action="store_true")
+    p.add_argument("--no-replay", action="store_true")
+    p.add_argument("--replay-blocks", type=int, default=10000,
+                   help="blocks per sync replay (BASELINE configs[4]; 65,536 validators)")
     p.add_argument("--epoch-validators", type=int, default=0,
                    help="validators per epoch instance (default: 65,536 at N=1, 1,048,576 at N>1)")
     p.add_argument("--epoch-instances", type=int, default=0,
@@ -145,6 +148,72 @@ def epoch_cpu_baseline(inst):
                 "sample": "unavailable: %s" % e}
 
 
+def replay_leg(args, torch, dist, dev, rank, world):
+    """BASELINE configs[4]: sync replay of a synthetic 10,000-block chain through the block
+    pipeline (blockchain/service.go:229-363): per block the block digest, 5 attestations'
+    Hash / Key / 64-byte message digests, the vote-cache tally of 5 x 204-205 members x 63
+    signed parent hashes, and a stateRecalc every 64 blocks.  The control flow is sequential
+    (host walk); the hashing, tallies and epochs are batched on the GPU.  At N > 1 every rank
+    replays its own chain (seed + rank): block batches shard with no collective.  Also
+    BASELINE configs[0]: the 1,024-validator chain of tests/golden/replay_n1024.json, its
+    roots checked against the fixture."""
+    from prysm_amd import synth
+    from prysm_amd.blockchain import BeaconChain
+
+    nval, nb = 65536, args.replay_blocks
+    blocks = synth.chain_blocks(nval, nb, seed=6 + rank)
+    BeaconChain(nval, dev).process_blocks(blocks[:min(nb, 130)])  # warm-up
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ch = BeaconChain(nval, dev)
+    recs = ch.process_blocks(blocks)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    out = {"metric": "sync-replay blocks/s", "value": nb * world / wall, "unit": "blocks/s",
+           "ms_per_block": wall / nb * 1e3,
+           "config": {"workload": "sync replay: block + 5 x (attestation Hash, Key, message digest) + vote "
+                                  "tally per block, stateRecalc every 64 blocks (BASELINE configs[4])",
+                      "validators": nval, "blocks_per_gpu": nb, "attestations_per_block": 5,
+                      "parallelism": "independent chain per GPU x%d" % world},
+           "processed": sum(r["status"] == "processed" for r in recs),
+           "transitions": sum(r["transition"] for r in recs)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            from oracle import replay as oreplay
+            sample = blocks[:130]
+            t0 = time.perf_counter()
+            oreplay.replay(sample, nval)
+            dt = time.perf_counter() - t0
+            out["cpu_baseline"] = {"value": len(sample) / dt, "unit": "blocks/s", "cores": 1, "kind": "port",
+                                   "sample": "first %d blocks of the same chain through oracle/replay.py (scalar "
+                                             "restatement of blockProcessing, 1 thread), %.2f s" % (len(sample), dt)}
+        except Exception as e:  # pragma: no cover
+            out["cpu_baseline"] = {"value": None, "unit": "blocks/s", "cores": 0, "kind": "port",
+                                   "sample": "unavailable: %s" % e}
+    # configs[0]: the golden 1,024-validator chain (parity of the final roots on this box)
+    with open(os.path.join(ROOT, "tests", "golden", "replay_n1024.json")) as f:
+        g = json.load(f)
+    sim_blocks = synth.chain_blocks(g["nval"], g["nblocks"], seed=g["seed"])
+    t0 = time.perf_counter()
+    sc = BeaconChain(g["nval"], dev)
+    sc.process_blocks(sim_blocks)
+    roots = sc.roots()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    out["simulator"] = {"config": "BASELINE configs[0]: %d validators, %d blocks (2 cycle transitions)"
+                                  % (g["nval"], g["nblocks"]),
+                        "blocks_per_s": g["nblocks"] / dt,
+                        "roots_match_golden": all(roots[k].hex() == v for k, v in g["roots"].items()),
+                        "cand_crystallized_root": roots["cand_crystallized"].hex()}
+    return out
+
+
 PMC_SUMMARY = os.path.join("profiles", "r01", "pmc_summary.json")
 
 
@@ -231,6 +300,7 @@ def main():
         wall = float(t.item())
 
     epoch = None if args.no_epoch else epoch_leg(args, torch, dist, dev, rank, world)
+    replay = None if args.no_replay else replay_leg(args, torch, dist, dev, rank, world)
 
     if rank == 0:
         total = n * world * args.steps
@@ -282,6 +352,8 @@ def main():
                     n, bool(np.array_equal(gpu, digests)))
         if epoch is not None:
             line["epoch"] = epoch
+        if replay is not None:
+            line["replay"] = replay
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -226,7 +226,15 @@ class BeaconChain:
 
     # ---- core.go --------------------------------------------------------------------------
     def _recent(self, A):
-        return [bytes_to_hash(h) for h in A.data.recent_block_hashes]
+        """RecentBlockHashes() (types/state.go:189-195), memoised per ActiveState: only the
+        genesis list holds non-32-byte entries, and the list object is replaced (never
+        edited) whenever it changes."""
+        lst = A.data.recent_block_hashes
+        memo = getattr(A, "_recent_memo", None)
+        if memo is None or memo[0] is not lst:
+            memo = (lst, [h if len(h) == 32 else bytes_to_hash(h) for h in lst])
+            A._recent_memo = memo
+        return memo[1]
 
     def _signed_parents(self, A, block_slot, att):
         """core.go:348-360 (Go slices up to cap: beyond len panics)."""

@@ -49,7 +49,10 @@ def _msg(num, body):
 def _packed(num, values):
     if len(values) == 0:
         return b""
-    body = packed_varints(np.asarray(values, dtype=_U64))
+    if len(values) <= 64 and not isinstance(values, np.ndarray):  # short lists: scalar path
+        body = b"".join(varint(int(v)) for v in values)
+    else:
+        body = packed_varints(np.asarray(values, dtype=_U64))
     return _tag(num, 2) + varint(len(body)) + body
 
 

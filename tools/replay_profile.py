@@ -1,0 +1,45 @@
+"""Profile the GPU block pipeline on a synthetic chain (BASELINE configs[4] shape):
+python tools/replay_profile.py NVAL NBLOCKS [--cprofile]"""
+import cProfile
+import os
+import pstats
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402,F401
+
+from prysm_amd import synth  # noqa: E402
+from prysm_amd.blockchain import BeaconChain  # noqa: E402
+
+
+def main():
+    nval, nblocks = int(sys.argv[1]), int(sys.argv[2])
+    t = time.perf_counter()
+    blocks = synth.chain_blocks(nval, nblocks, seed=6)
+    print("generate %.3f s" % (time.perf_counter() - t), flush=True)
+    t = time.perf_counter()
+    ch = BeaconChain(nval)
+    torch.cuda.synchronize()
+    print("genesis %.3f s" % (time.perf_counter() - t), flush=True)
+    ch.process_blocks(blocks[:70])  # warm-up (kernels loaded)
+    ch = BeaconChain(nval)
+    prof = cProfile.Profile() if "--cprofile" in sys.argv else None
+    t = time.perf_counter()
+    if prof:
+        prof.enable()
+    recs = ch.process_blocks(blocks)
+    torch.cuda.synchronize()
+    if prof:
+        prof.disable()
+    dt = time.perf_counter() - t
+    print("process_blocks %.3f s -> %.1f blocks/s (%d processed)" % (dt, nblocks / dt, sum(r["status"] == "processed" for r in recs)), flush=True)
+    t = time.perf_counter()
+    ch.roots()
+    print("roots %.3f s" % (time.perf_counter() - t), flush=True)
+    if prof:
+        pstats.Stats(prof).sort_stats("cumulative").print_stats(25)
+
+
+if __name__ == "__main__":
+    main()
