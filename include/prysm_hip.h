@@ -228,6 +228,61 @@ int pz_dev_epoch_finish(const pz_epoch_batch* b, void* stream);
 int pz_dev_epoch_gather_compact(const pz_epoch_batch* b, const uint64_t* gathered_mask, uint32_t world,
                                 uint64_t shard_words, uint32_t* gblk, void* stream);
 
+/* ---- block pipeline: sync replay of serialized blocks ---------------------------------
+ * A chain object runs blocks through the reference's ChainService.blockProcessing
+ * (blockchain/service.go:229-363) and updateHead (:170-227) over BeaconChain (core.go),
+ * starting from the genesis states of `nval` validators (types/state.go:44-112).  Blocks are
+ * canonical proto3 BeaconBlock encodings (messages.proto:37-46), CSR (offsets[n+1]), as they
+ * arrive from the sync service (sync/service.go:147-164); a block that is not the canonical
+ * encoding of its own decoding is PZ_EINVAL (the reference hashes proto.Marshal of the decoded
+ * block).  Results per block and per attestation are what the reference stores or logs:
+ * block digest (Block.Hash), attestation Key/Hash (saveAttestation, Attestation.Hash) and the
+ * 64-byte processAttestation message digest (core.go:277-290).  Where the reference panics
+ * the call returns PZ_EINDEX and the chain is unusable afterwards.  Thread-safe per chain. */
+#define PZ_BLOCK_PROCESSED            0  /* became the candidate (and maybe a cycle transition) */
+#define PZ_BLOCK_NO_PARENT            1  /* parent never saved, slot > 1 (service.go:261-269)   */
+#define PZ_BLOCK_ATTS_REJECTED        2  /* last attestation failed / none (service.go:304-306)  */
+#define PZ_BLOCK_SAVED_NOT_CANDIDATE  3  /* saved, a candidate was already chosen (:331-333)     */
+#define PZ_ATT_PROCESSED              0
+#define PZ_ATT_NOT_PROCESSED          1  /* its block was dropped before processAttestation       */
+#define PZ_ATT_SLOT_HIGH              2  /* core.go:244-248 */
+#define PZ_ATT_SLOT_LOW               3  /* core.go:249-253 */
+#define PZ_ATT_JUSTIFIED              4  /* core.go:255-259 */
+#define PZ_ATT_NO_COMMITTEE           5  /* core.go:373     */
+#define PZ_ATT_BITFIELD_LEN           6  /* core.go:379-382 */
+#define PZ_ATT_TRAILING_BITS          7  /* core.go:385-392 */
+
+typedef struct pz_block_result {
+  uint8_t hash[32];      /* Block.Hash() */
+  int32_t status;        /* PZ_BLOCK_* */
+  int32_t transition;    /* 1: stateRecalc ran for this block */
+  uint32_t first_att;    /* index of its first attestation in att_out */
+  uint32_t natt;
+} pz_block_result;
+
+typedef struct pz_att_result {
+  int32_t status;        /* PZ_ATT_* */
+  uint32_t msg_len;      /* processAttestation message length */
+  uint8_t key[32];       /* Attestation.Key()  (types/attestation.go:61-77) */
+  uint8_t hash[32];      /* Attestation.Hash() (types/attestation.go:49-59) */
+  uint8_t msg_digest[64];/* blake2b.Sum512(msg) (core.go:290) */
+} pz_att_result;
+
+typedef struct pz_chain pz_chain;
+int  pz_chain_new(uint64_t nval, int device, pz_chain** out);
+void pz_chain_free(pz_chain* chain);
+/* Number of attestations in a batch of serialized blocks (host only; sizes att_out). */
+int  pz_count_attestations(const uint8_t* blocks, const uint64_t* offsets, uint64_t n, uint64_t* count);
+/* att_out: capacity att_cap >= the total number of attestations in the batch. */
+int  pz_chain_process_blocks(pz_chain* chain, const uint8_t* blocks, const uint64_t* offsets, uint64_t n,
+                             pz_block_result* block_out, pz_att_result* att_out, uint64_t att_cap);
+/* State roots (types/state.go:138-149, 237-248): out[0..31] chain ActiveState, [32..63] chain
+ * CrystallizedState, [64..127] the candidate's (zero when *has_candidate == 0). */
+int  pz_chain_roots(pz_chain* chain, uint8_t out[4 * 32], int* has_candidate);
+/* The block vote cache: *count entries (0 when the map is nil); fills hashes[32*i] and
+ * totals[i] (VoteTotalDeposit) when cap >= *count. */
+int  pz_chain_vote_totals(pz_chain* chain, uint8_t* hashes, uint64_t* totals, uint64_t cap, uint64_t* count);
+
 #ifdef __cplusplus
 }
 #endif

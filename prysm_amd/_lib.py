@@ -68,6 +68,12 @@ SIGNATURES = {
     "pz_dev_epoch_count": [vp, vp],
     "pz_dev_epoch_finish": [vp, vp],
     "pz_dev_epoch_gather_compact": [vp, vp, u32, u64, vp, vp],
+    "pz_chain_new": [u64, ctypes.c_int, vp],
+    "pz_chain_free": [vp],
+    "pz_count_attestations": [vp, vp, u64, c_u64p],
+    "pz_chain_process_blocks": [vp, vp, vp, u64, vp, vp, u64],
+    "pz_chain_roots": [vp, vp, c_intp],
+    "pz_chain_vote_totals": [vp, vp, vp, u64, c_u64p],
     "pz_dev_vote_tally": [vp, vp],
     "pz_vote_tally": [vp, vp, u64, vp, vp, vp, u64, vp, vp, u64, vp, u64, vp, u64, u64, vp],
 }
@@ -98,7 +104,7 @@ class VoteBatch(ctypes.Structure):
 SCAL_POP, SCAL_NACT, SCAL_ERR_XL, SCAL_ERR_RWD, SCAL_APPLIED, SCAL_NEXT_BAL, SCAL_MAXIDX1 = range(7)
 SCAL_COUNT = 8
 KIND_ACTIVE, KIND_EXITED, KIND_QUEUED = 0, 1, 2
-_RESTYPES = {"pz_last_error": ctypes.c_char_p}
+_RESTYPES = {"pz_last_error": ctypes.c_char_p, "pz_chain_free": None}
 
 
 class _Lib:

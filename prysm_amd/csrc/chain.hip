@@ -1,0 +1,1022 @@
+// Native block pipeline: the reference's ChainService.blockProcessing (beacon-chain/
+// blockchain/service.go:229-363) + updateHead (:170-227) over BeaconChain (core.go), fed with
+// serialized blocks, with every data-parallel step on the GPU.
+//
+// The walk over the blocks is sequential host code (scalar checks, hash-map lookups, small
+// copies); the device work is batched per call:
+//   * block / attestation Hash / attestation Key digests: one CSR BLAKE2b launch, before the
+//     walk (blocks are immutable inputs);
+//   * processAttestation message digests (core.go:277-290, 64 bytes): one launch, after it;
+//   * calculateBlockVoteCache (core.go:300-345): tally items queued during the walk, run by
+//     the vote kernel on the HBM-resident cache before every stateRecalc and at the end;
+//   * stateRecalc's processCrosslinks + CalculateRewards + next-cycle balance: one epoch
+//     instance (epoch.hip) on the HBM-resident validator arrays.
+// Reference semantics kept on purpose (each changes hashed bytes) are listed in DESIGN.md §7;
+// oracle/replay.py restates the same pipeline for the parity tests.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "blake2b_kernels.h"
+#include "epoch.h"
+#include "runtime.h"
+#include "votes.h"
+
+namespace pz {
+namespace chain {
+
+constexpr uint64_t kCycle = PZ_CYCLE_LENGTH;
+
+struct H32 {
+  uint8_t b[32];
+  bool operator==(const H32& o) const { return std::memcmp(b, o.b, 32) == 0; }
+};
+struct H32Hash {
+  size_t operator()(const H32& h) const {
+    uint64_t x;
+    std::memcpy(&x, h.b, 8);
+    return (size_t)(x ^ (x >> 29));
+  }
+};
+static const H32 kZero = {};
+
+// go-ethereum common.BytesToHash: last 32 bytes, right-aligned.
+static H32 bytes_to_hash(const uint8_t* p, size_t n) {
+  H32 h = kZero;
+  if (n > 32) {
+    p += n - 32;
+    n = 32;
+  }
+  if (n) std::memcpy(h.b + 32 - n, p, n);
+  return h;
+}
+// `var h [32]byte; copy(h[:], b)`: left-aligned, truncated.
+static H32 copy32(const uint8_t* p, size_t n) {
+  H32 h = kZero;
+  if (n) std::memcpy(h.b, p, n < 32 ? n : 32);
+  return h;
+}
+
+// ---- proto3 ---------------------------------------------------------------------------------
+static void put_varint(std::string& o, uint64_t x) {
+  while (x >= 0x80) {
+    o.push_back((char)((x & 0x7f) | 0x80));
+    x >>= 7;
+  }
+  o.push_back((char)x);
+}
+static void put_u(std::string& o, uint32_t f, uint64_t v) {
+  if (v) {
+    put_varint(o, (uint64_t)f << 3);
+    put_varint(o, v);
+  }
+}
+static void put_b(std::string& o, uint32_t f, const uint8_t* p, size_t n) {
+  if (n) {
+    put_varint(o, ((uint64_t)f << 3) | 2);
+    put_varint(o, n);
+    o.append((const char*)p, n);
+  }
+}
+static void put_msg(std::string& o, uint32_t f, const uint8_t* p, size_t n) {
+  put_varint(o, ((uint64_t)f << 3) | 2);
+  put_varint(o, n);
+  o.append((const char*)p, n);
+}
+
+struct Reader {
+  const uint8_t* p;
+  const uint8_t* e;
+  bool ok = true;
+  bool more() const { return ok && p < e; }
+  uint64_t varint() {
+    uint64_t x = 0;
+    for (int s = 0; s < 70; s += 7) {
+      if (p >= e) { ok = false; return 0; }
+      const uint8_t b = *p++;
+      x |= (uint64_t)(b & 0x7f) << s;
+      if (!(b & 0x80)) return x;
+    }
+    ok = false;
+    return 0;
+  }
+  bool span(const uint8_t** q, size_t* n) {
+    const uint64_t len = varint();
+    if (!ok || len > (uint64_t)(e - p)) { ok = false; return false; }
+    *q = p;
+    *n = (size_t)len;
+    p += len;
+    return true;
+  }
+  void skip(uint32_t wt) {
+    const uint8_t* q;
+    size_t n;
+    if (wt == 0) varint();
+    else if (wt == 2) span(&q, &n);
+    else if (wt == 1 && e - p >= 8) p += 8;
+    else if (wt == 5 && e - p >= 4) p += 4;
+    else ok = false;
+  }
+};
+
+// One AttestationRecord (messages.proto:110-119), owning its canonical encoding.
+struct Att {
+  std::string enc;
+  uint64_t slot = 0, shard = 0, jslot = 0;
+  uint32_t sbh_off = 0, sbh_len = 0, bf_off = 0, bf_len = 0;
+  std::vector<std::pair<uint32_t, uint32_t>> obl;  // (offset, length) into enc
+  const uint8_t* at(uint32_t off) const { return (const uint8_t*)enc.data() + off; }
+};
+using AttP = std::shared_ptr<const Att>;
+
+static bool parse_att(const uint8_t* p, size_t n, Att* a) {
+  a->enc.assign((const char*)p, n);
+  const uint8_t* base = (const uint8_t*)a->enc.data();
+  Reader r{base, base + n};
+  const uint8_t *jbh = nullptr, *q;
+  size_t jbh_len = 0, len;
+  std::vector<uint64_t> sig;
+  while (r.more()) {
+    const uint64_t key = r.varint();
+    const uint32_t f = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
+    if (f == 1 && wt == 0) a->slot = r.varint();
+    else if (f == 2 && wt == 0) a->shard = r.varint();
+    else if (f == 3 && wt == 0) a->jslot = r.varint();
+    else if (f == 4 && wt == 2) { r.span(&jbh, &jbh_len); }
+    else if (f == 5 && wt == 2) { if (r.span(&q, &len)) { a->sbh_off = (uint32_t)(q - base); a->sbh_len = (uint32_t)len; } }
+    else if (f == 6 && wt == 2) { if (r.span(&q, &len)) { a->bf_off = (uint32_t)(q - base); a->bf_len = (uint32_t)len; } }
+    else if (f == 7 && wt == 2) { if (r.span(&q, &len)) a->obl.push_back({(uint32_t)(q - base), (uint32_t)len}); }
+    else if (f == 8 && wt == 2) {
+      if (r.span(&q, &len)) {
+        Reader s{q, q + len};
+        while (s.more()) sig.push_back(s.varint());
+        r.ok = r.ok && s.ok;
+      }
+    } else return false;  // unknown / mistyped field: not a canonical encoding
+  }
+  if (!r.ok) return false;
+  // canonical check: the reference hashes proto.Marshal of the decoded message
+  std::string c;
+  put_u(c, 1, a->slot);
+  put_u(c, 2, a->shard);
+  put_u(c, 3, a->jslot);
+  put_b(c, 4, jbh, jbh_len);
+  put_b(c, 5, a->at(a->sbh_off), a->sbh_len);
+  put_b(c, 6, a->at(a->bf_off), a->bf_len);
+  for (auto& o : a->obl) put_msg(c, 7, a->at(o.first), o.second);
+  if (!sig.empty()) {
+    std::string body;
+    for (uint64_t v : sig) put_varint(body, v);
+    put_msg(c, 8, (const uint8_t*)body.data(), body.size());
+  }
+  return c == a->enc;
+}
+
+struct Block {
+  const uint8_t* data;
+  size_t len;
+  uint64_t slot = 0;
+  H32 parent = kZero;  // Block.ParentHash(): copy into [32]byte (types/block.go:80-84)
+  std::vector<AttP> atts;
+};
+
+static bool parse_block(const uint8_t* p, size_t n, Block* b) {
+  b->data = p;
+  b->len = n;
+  Reader r{p, p + n};
+  const uint8_t* fld[7] = {nullptr};
+  size_t flen[7] = {0};
+  bool has_ts = false;
+  uint64_t ts_s = 0, ts_n = 0;
+  const uint8_t* q;
+  size_t len;
+  while (r.more()) {
+    const uint64_t key = r.varint();
+    const uint32_t f = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
+    if (f == 2 && wt == 0) b->slot = r.varint();
+    else if ((f == 1 || (f >= 3 && f <= 6)) && wt == 2) r.span(&fld[f], &flen[f]);
+    else if (f == 7 && wt == 2) {
+      if (r.span(&q, &len)) {
+        has_ts = true;
+        Reader t{q, q + len};
+        while (t.more()) {
+          const uint64_t k2 = t.varint();
+          if (k2 == 0x08) ts_s = t.varint();
+          else if (k2 == 0x10) ts_n = t.varint();
+          else t.ok = false;
+        }
+        r.ok = r.ok && t.ok;
+      }
+    } else if (f == 8 && wt == 2) {
+      if (r.span(&q, &len)) {
+        auto a = std::make_shared<Att>();
+        if (!parse_att(q, len, a.get())) return false;
+        b->atts.push_back(a);
+      }
+    } else return false;
+  }
+  if (!r.ok) return false;
+  b->parent = copy32(fld[1], flen[1]);
+  std::string c;
+  put_b(c, 1, fld[1], flen[1]);
+  put_u(c, 2, b->slot);
+  for (int f = 3; f <= 6; ++f) put_b(c, f, fld[f], flen[f]);
+  if (has_ts) {
+    std::string t;
+    put_u(t, 1, ts_s);
+    put_u(t, 2, ts_n);
+    put_msg(c, 7, (const uint8_t*)t.data(), t.size());
+  }
+  for (auto& a : b->atts) put_msg(c, 8, (const uint8_t*)a->enc.data(), a->enc.size());
+  return c.size() == n && std::memcmp(c.data(), p, n) == 0;
+}
+
+// ---- chain state ----------------------------------------------------------------------------
+struct Crosslink {
+  uint64_t dynasty = 0, slot = 0;
+  std::string hash;
+};
+
+struct AState {               // types.ActiveState
+  std::vector<AttP> pending;  // PendingAttestations
+  std::vector<H32> recent;    // RecentBlockHashes, normalised
+  bool recent_raw_empty = false;  // genesis: every entry is a zero-length byte slice
+  bool cache_nil = false;     // the shared vote-cache map, or nil (SetBlockVoteCache(nil))
+};
+using AP = std::shared_ptr<AState>;
+
+struct CState {  // types.CrystallizedState (validators and committees live in the Engine)
+  uint64_t lsr = 0, streak = 0, jslot = 0, fslot = 0, dynasty = 0, start_shard = 0, tdep = 0, seed_reset = 0;
+  std::shared_ptr<std::vector<Crosslink>> xl;  // shared with the next state (mutated in place)
+};
+using CP = std::shared_ptr<CState>;
+
+template <typename T>
+struct DevArr {
+  T* p = nullptr;
+  size_t n = 0;
+  int alloc(size_t count) {
+    if (count <= n && p) return PZ_OK;
+    T* q = nullptr;
+    hipError_t e = hipMalloc((void**)&q, (count ? count : 1) * sizeof(T) + 256);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc");
+    if (p) (void)hipFree(p);
+    p = q;
+    n = count;
+    return PZ_OK;
+  }
+  ~DevArr() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+struct Engine {
+  uint64_t nval = 0;
+  int device = 0;
+  hipStream_t s = nullptr;
+  std::mutex mu;
+  bool poisoned = false;
+  // validators (shared by every CrystallizedState, like the Go pointer slice)
+  DevArr<uint64_t> balance, start, end;
+  std::vector<uint64_t> h_balance, h_start, h_end;
+  bool host_balance_valid = true;
+  // ShardAndCommitteesForSlots (immutable in this reference: stateRecalc copies it)
+  DevArr<uint32_t> committee;
+  DevArr<uint64_t> coffs;
+  std::vector<uint64_t> csize;
+  std::vector<std::vector<std::pair<uint64_t, uint32_t>>> lookup;  // [array] -> (shard, committee id)
+  std::string arrays_enc;  // field 12 of the CrystallizedState, every array
+  // block vote cache (one map shared by every ActiveState)
+  std::unordered_map<H32, uint32_t, H32Hash> slot_of;
+  std::vector<H32> slot_hash;
+  DevArr<uint32_t> bitmaps;
+  DevArr<uint64_t> totals;
+  uint64_t words = 0, cap = 0;
+  std::vector<uint8_t> q_bits;
+  std::vector<uint64_t> q_boffs{0};
+  std::vector<uint32_t> q_comm, q_item_att, q_item_slot;
+  DevArr<uint8_t> d_qbits;
+  DevArr<uint64_t> d_qboffs, d_err;
+  DevArr<uint32_t> d_qcomm, d_qia, d_qis;
+  // epoch scratch
+  DevArr<uint64_t> e_scal, e_mask, e_vote, e_total, e_rdyn, e_small, e_boffs;
+  DevArr<uint32_t> e_blk, e_list, e_win, e_comm, e_shard;
+  DevArr<uint8_t> e_bits;
+  // hashing scratch
+  DevArr<uint8_t> h_in, h_out;
+  DevArr<uint64_t> h_offs;
+  // chain
+  AP A;
+  CP C;
+  bool has_cand = false;
+  uint64_t cand_slot = 0;
+  AP cand_A;
+  CP cand_C;
+  std::unordered_set<H32, H32Hash> saved;
+};
+
+struct Panic {
+  std::string what;
+};
+struct Rejected {
+  int code;
+};
+
+static void check(int rc) {
+  if (rc) throw rc;
+}
+static void hchk(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw hip_fail(e, what);
+}
+
+template <typename T>
+static void upload(Engine& g, DevArr<T>& d, const T* h, size_t n) {
+  check(d.alloc(n));
+  if (n) hchk(hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, g.s), "H2D");
+}
+
+// Many messages -> 64-byte digests (one CSR launch).  Blocks until done.
+static void hash_many(Engine& g, const std::string& data, const std::vector<uint64_t>& offs, std::vector<uint8_t>& out) {
+  const size_t n = offs.size() - 1;
+  out.resize(n * 64);
+  if (!n) return;
+  check(g.h_in.alloc(data.size() + 16));
+  check(g.h_out.alloc(n * 64));
+  upload(g, g.h_offs, offs.data(), offs.size());
+  if (!data.empty()) hchk(hipMemcpyAsync(g.h_in.p, data.data(), data.size(), hipMemcpyHostToDevice, g.s), "H2D msgs");
+  hchk(launch_b2b_csr(g.h_in.p, g.h_offs.p, n, g.h_out.p, 64, g.s), "blake2b csr");
+  hchk(hipMemcpyAsync(out.data(), g.h_out.p, n * 64, hipMemcpyDeviceToHost, g.s), "D2H digests");
+  hchk(hipStreamSynchronize(g.s), "sync");
+}
+
+// ---- vote cache -------------------------------------------------------------------------------
+static uint32_t vote_slot(Engine& g, const H32& h) {
+  auto it = g.slot_of.find(h);
+  if (it != g.slot_of.end()) return it->second;
+  const uint32_t s = (uint32_t)g.slot_hash.size();
+  g.slot_of.emplace(h, s);
+  g.slot_hash.push_back(h);
+  if (s >= g.cap) {  // grow the device arrays, keeping their contents
+    const uint64_t nc = std::max<uint64_t>(64, 2 * g.cap);
+    DevArr<uint32_t> bm;
+    DevArr<uint64_t> tt;
+    check(bm.alloc(nc * g.words));
+    check(tt.alloc(nc));
+    hchk(hipMemsetAsync(bm.p, 0, nc * g.words * 4, g.s), "memset");
+    hchk(hipMemsetAsync(tt.p, 0, nc * 8, g.s), "memset");
+    if (g.cap) {
+      hchk(hipMemcpyAsync(bm.p, g.bitmaps.p, g.cap * g.words * 4, hipMemcpyDeviceToDevice, g.s), "D2D");
+      hchk(hipMemcpyAsync(tt.p, g.totals.p, g.cap * 8, hipMemcpyDeviceToDevice, g.s), "D2D");
+    }
+    hchk(hipStreamSynchronize(g.s), "sync");
+    std::swap(g.bitmaps.p, bm.p);
+    std::swap(g.bitmaps.n, bm.n);
+    std::swap(g.totals.p, tt.p);
+    std::swap(g.totals.n, tt.n);
+    g.cap = nc;
+  }
+  return s;
+}
+
+static void flush_votes(Engine& g) {
+  if (g.q_item_att.empty()) return;
+  upload(g, g.d_qbits, g.q_bits.data(), g.q_bits.size() + 0);
+  upload(g, g.d_qboffs, g.q_boffs.data(), g.q_boffs.size());
+  upload(g, g.d_qcomm, g.q_comm.data(), g.q_comm.size());
+  upload(g, g.d_qia, g.q_item_att.data(), g.q_item_att.size());
+  upload(g, g.d_qis, g.q_item_slot.data(), g.q_item_slot.size());
+  check(g.d_err.alloc(1));
+  hchk(hipMemsetAsync(g.d_err.p, 0, 8, g.s), "memset");
+  VoteArgs v;
+  std::memset(&v, 0, sizeof v);
+  v.committee = g.committee.p;
+  v.coffs = g.coffs.p;
+  v.att_comm = g.d_qcomm.p;
+  v.bits = g.d_qbits.p;
+  v.boffs = g.d_qboffs.p;
+  v.item_att = g.d_qia.p;
+  v.item_slot = g.d_qis.p;
+  v.nitems = g.q_item_att.size();
+  v.balance = g.balance.p;
+  v.nval = g.nval;
+  v.bitmaps = g.bitmaps.p;
+  v.words_per_slot = g.words;
+  v.totals = g.totals.p;
+  v.err = g.d_err.p;
+  hchk(launch_vote_tally(v, g.s), "vote tally");
+  uint64_t err = 0;
+  hchk(hipMemcpyAsync(&err, g.d_err.p, 8, hipMemcpyDeviceToHost, g.s), "D2H");
+  hchk(hipStreamSynchronize(g.s), "sync");  // also keeps the pageable sources alive
+  g.q_bits.clear();
+  g.q_boffs.assign(1, 0);
+  g.q_comm.clear();
+  g.q_item_att.clear();
+  g.q_item_slot.clear();
+  if (err) throw Panic{"calculateBlockVoteCache: CheckBit / validator index out of range"};
+}
+
+// ---- core.go ------------------------------------------------------------------------------------
+// getSignedParentHashes (core.go:348-360); Go slices up to cap, beyond len panics.
+static void signed_parents(const AState& A, uint64_t block_slot, const Att& a, std::vector<H32>& out) {
+  const uint64_t start = block_slot - a.slot;
+  const uint64_t end = block_slot - a.slot - (uint64_t)a.obl.size() + kCycle;
+  if (start > end || end > A.recent.size()) throw Panic{"slice bounds out of range (core.go:353)"};
+  out.assign(A.recent.begin() + (ptrdiff_t)start, A.recent.begin() + (ptrdiff_t)end);
+  for (auto& o : a.obl) out.push_back(bytes_to_hash(a.at(o.first), o.second));
+}
+
+// getAttesterIndices (core.go:363-374) -> committee id.
+static uint32_t attester_committee(const Engine& g, const CState& C, const Att& a) {
+  const uint64_t idx = a.slot - C.lsr;  // uint64 wrap, like Go
+  if (idx >= g.lookup.size()) throw Panic{"ShardAndCommitteesForSlots index out of range (core.go:367)"};
+  for (auto& sc : g.lookup[idx])
+    if (sc.first == a.shard) return sc.second;
+  throw Rejected{PZ_ATT_NO_COMMITTEE};
+}
+
+// processAttestation (core.go:240-297) -> builds the message whose digest the reference logs.
+static void process_attestation(Engine& g, uint64_t block_slot, const Att& a, std::vector<H32>& parents,
+                                std::string& msg) {
+  if ((int64_t)a.slot > (int64_t)block_slot) throw Rejected{PZ_ATT_SLOT_HIGH};
+  if ((int64_t)a.slot < (int64_t)block_slot - (int64_t)kCycle) throw Rejected{PZ_ATT_SLOT_LOW};
+  if (a.jslot != g.C->jslot) throw Rejected{PZ_ATT_JUSTIFIED};
+  signed_parents(*g.A, block_slot, a, parents);
+  const uint32_t c = attester_committee(g, *g.C, a);
+  const uint64_t k = g.csize[c];
+  if ((k + 7) / 8 != a.bf_len) throw Rejected{PZ_ATT_BITFIELD_LEN};  // core.go:379-382
+  if (k % 8 && (a.at(a.bf_off)[a.bf_len - 1] & (0xFFu >> (k % 8)))) throw Rejected{PZ_ATT_TRAILING_BITS};
+  msg.assign(10, '\0');
+  std::string v;
+  put_varint(v, a.slot % kCycle);
+  std::memcpy(&msg[0], v.data(), v.size());
+  for (auto& h : parents) {
+    msg.append((const char*)h.b, 32);
+    msg.push_back(' ');
+  }
+  v.clear();
+  put_varint(v, a.shard);
+  std::memcpy(&msg[0], v.data(), v.size());
+  msg.append((const char*)a.at(a.sbh_off), a.sbh_len);
+}
+
+// calculateBlockVoteCache (core.go:300-345): queue one tally item per signed parent hash.
+static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, std::vector<H32>& parents) {
+  signed_parents(*g.A, block_slot, a, parents);
+  const uint32_t c = attester_committee(g, *g.C, a);
+  const uint32_t ai = (uint32_t)g.q_comm.size();
+  g.q_comm.push_back(c);
+  g.q_bits.insert(g.q_bits.end(), a.at(a.bf_off), a.at(a.bf_off) + a.bf_len);
+  g.q_boffs.push_back(g.q_bits.size());
+  for (auto& h : parents) {
+    bool skip = false;
+    for (auto& o : a.obl)
+      if (o.second == 32 && std::memcmp(h.b, a.at(o.first), 32) == 0) skip = true;
+    if (skip) continue;
+    if (g.A->cache_nil) throw Panic{"assignment to entry in nil map (core.go:323)"};
+    g.q_item_att.push_back(ai);
+    g.q_item_slot.push_back(vote_slot(g, h));
+  }
+  if (g.q_item_att.size() > (1u << 22)) flush_votes(g);
+}
+
+// processCrosslinks + CalculateRewards + next-cycle balance on the device -> next balance.
+static uint64_t epoch_on_device(Engine& g, CState& C, const std::vector<AttP>& pending, uint64_t block_slot) {
+  const size_t na = pending.size();
+  std::vector<uint32_t> comm(na), shard(na);
+  std::vector<uint8_t> bits;
+  std::vector<uint64_t> boffs{0};
+  for (size_t i = 0; i < na; ++i) {
+    const Att& a = *pending[i];
+    try {
+      comm[i] = attester_committee(g, C, a);
+    } catch (Rejected&) {  // stateRecalc returns an error; the caller dereferences a nil state
+      throw Panic{"stateRecalc: committee lookup failed -> nil state dereference"};
+    }
+    if (a.shard > 0xffffffffull) throw Panic{"crosslink record index out of range"};
+    shard[i] = (uint32_t)a.shard;
+    bits.insert(bits.end(), a.at(a.bf_off), a.at(a.bf_off) + a.bf_len);
+    boffs.push_back(bits.size());
+  }
+  std::vector<Crosslink>& xl = *C.xl;
+  std::vector<uint64_t> rdyn(xl.size());
+  for (size_t s = 0; s < xl.size(); ++s) rdyn[s] = xl[s].dynasty;
+  const uint64_t small[2] = {C.dynasty, C.tdep};
+  upload(g, g.e_bits, bits.data(), bits.size());
+  upload(g, g.e_boffs, boffs.data(), boffs.size());
+  upload(g, g.e_comm, comm.data(), na);
+  upload(g, g.e_shard, shard.data(), na);
+  upload(g, g.e_rdyn, rdyn.data(), rdyn.size());
+  upload(g, g.e_small, small, 2);
+  check(g.e_scal.alloc(kScal));
+  check(g.e_vote.alloc(na + 1));
+  check(g.e_total.alloc(na + 1));
+  check(g.e_win.alloc(xl.size() + 1));
+  hchk(hipMemsetAsync(g.e_scal.p, 0, kScal * 8, g.s), "memset");
+  EpochArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.ninst = 1;
+  a.nval = a.nval_global = g.nval;
+  a.kind = PZ_KIND_ACTIVE;
+  a.balance = g.balance.p;
+  a.start = g.start.p;
+  a.end = g.end.p;
+  a.dynasty = g.e_small.p;
+  a.total_deposit = g.e_small.p + 1;
+  a.natt = (uint32_t)na;
+  a.bits = g.e_bits.p;
+  a.boffs = g.e_boffs.p;
+  a.max_inst_bytes = bits.size();
+  a.pop_rank = 0;
+  a.pop_world = 1;
+  a.committee = g.committee.p;
+  a.coffs = g.coffs.p;
+  a.att_comm = g.e_comm.p;
+  a.att_shard = g.e_shard.p;
+  a.nrec = (uint32_t)xl.size();
+  a.rec_dynasty = g.e_rdyn.p;
+  a.winner = g.e_win.p;
+  a.vote = g.e_vote.p;
+  a.total = g.e_total.p;
+  a.scal = g.e_scal.p;
+  a.act_mask = g.e_mask.p;
+  a.blk_cnt = g.e_blk.p;
+  a.act_list = g.e_list.p;
+  hchk(launch_epoch_count(a, true, true, true, g.s), "epoch count");
+  hchk(launch_epoch_mid(a, a.nrec > 0 && na > 0, true, g.s), "epoch mid");
+  hchk(launch_epoch_reward(a, g.s), "epoch reward");
+  uint64_t scal[kScal];
+  std::vector<uint32_t> win(xl.size());
+  hchk(hipMemcpyAsync(scal, g.e_scal.p, sizeof scal, hipMemcpyDeviceToHost, g.s), "D2H");
+  if (!win.empty()) hchk(hipMemcpyAsync(win.data(), g.e_win.p, win.size() * 4, hipMemcpyDeviceToHost, g.s), "D2H");
+  hchk(hipStreamSynchronize(g.s), "sync");
+  if (scal[kErrXl]) throw Panic{"processCrosslinks: index out of range (committee member, bitfield or shard)"};
+  const uint64_t dep = scal[kPop] * PZ_DEFAULT_BALANCE;
+  const bool thr = dep * 3ull >= C.tdep * 2ull;
+  if (thr && scal[kNact] > 0 && scal[kErrRwd]) throw Panic{"CalculateRewards: CheckBit index out of range (incentives.go:23)"};
+  if (na && !xl.empty()) {
+    for (size_t s = 0; s < xl.size(); ++s) {
+      if (win[s] == 0xffffffffu) continue;
+      const Att& w = *pending[win[s]];
+      xl[s].dynasty = C.dynasty;
+      xl[s].hash.assign((const char*)w.at(w.sbh_off), w.sbh_len);
+      xl[s].slot = block_slot;
+    }
+  }
+  if (scal[kApplied]) g.host_balance_valid = false;
+  return scal[kNextBal];
+}
+
+// stateRecalc (core.go:398-497) -> (new C, new A).
+static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slot, CP* nc_out, AP* na_out) {
+  flush_votes(g);
+  uint64_t streak = C->streak, justified = C->jslot, finalized = C->fslot;
+  const uint64_t lsr = C->lsr;
+  std::vector<uint64_t> tot(kCycle, 0);
+  if (!A->cache_nil) {
+    std::vector<uint64_t> all(g.slot_hash.size());
+    if (!all.empty()) {
+      hchk(hipMemcpyAsync(all.data(), g.totals.p, all.size() * 8, hipMemcpyDeviceToHost, g.s), "D2H");
+      hchk(hipStreamSynchronize(g.s), "sync");
+    }
+    for (uint64_t i = 0; i < kCycle && i < A->recent.size(); ++i) {
+      auto it = g.slot_of.find(A->recent[i]);
+      tot[i] = it == g.slot_of.end() ? 0 : all[it->second];
+    }
+  }
+  for (uint64_t i = 0; i < kCycle; ++i) {
+    const uint64_t slot = lsr - kCycle + i;
+    if (3ull * tot[i] >= 2ull * C->tdep) {
+      if (slot > justified) justified = slot;
+      ++streak;
+    } else {
+      streak = 0;
+    }
+    if (streak >= kCycle + 1 && slot - kCycle > finalized) finalized = slot - kCycle;
+  }
+  const uint64_t nxt = epoch_on_device(g, *C, A->pending, block_slot);
+  auto nc = std::make_shared<CState>();
+  nc->lsr = lsr + kCycle;
+  nc->jslot = justified;
+  nc->streak = streak;
+  nc->fslot = finalized;
+  nc->start_shard = 0;
+  nc->dynasty = 0;  // core.go:467-478 does not set CurrentDynasty
+  nc->seed_reset = C->seed_reset;
+  nc->tdep = nxt;
+  nc->xl = C->xl;
+  auto na = std::make_shared<AState>();
+  for (auto& p : A->pending)
+    if (p->slot > lsr) na->pending.push_back(p);
+  na->recent = A->recent;
+  if (na->recent.size() > 2 * kCycle) na->recent.erase(na->recent.begin(), na->recent.end() - 2 * kCycle);
+  na->cache_nil = A->cache_nil;
+  *nc_out = nc;
+  *na_out = na;
+}
+
+// ---- serialization of the states (state roots) --------------------------------------------
+static void sync_host_balance(Engine& g) {
+  if (g.host_balance_valid) return;
+  hchk(hipMemcpyAsync(g.h_balance.data(), g.balance.p, g.nval * 8, hipMemcpyDeviceToHost, g.s), "D2H");
+  hchk(hipStreamSynchronize(g.s), "sync");
+  g.host_balance_valid = true;
+}
+
+static std::string encode_active(const AState& A) {  // messages.proto:94-97
+  std::string o;
+  for (auto& p : A.pending) put_msg(o, 1, (const uint8_t*)p->enc.data(), p->enc.size());
+  for (auto& h : A.recent) put_msg(o, 2, h.b, A.recent_raw_empty ? 0 : 32);
+  return o;
+}
+
+static std::string encode_crystallized(Engine& g, const CState& C) {  // messages.proto:59-72
+  sync_host_balance(g);
+  std::string o;
+  o.reserve(g.nval * 18 + g.arrays_enc.size() + 16384);
+  put_u(o, 1, C.lsr);
+  put_u(o, 2, C.streak);
+  put_u(o, 3, C.jslot);
+  put_u(o, 4, C.fslot);
+  put_u(o, 5, C.dynasty);
+  put_u(o, 6, C.start_shard);
+  put_u(o, 7, C.tdep);
+  put_u(o, 9, C.seed_reset);
+  std::string r;
+  for (auto& x : *C.xl) {
+    r.clear();
+    put_u(r, 1, x.dynasty);
+    put_b(r, 2, (const uint8_t*)x.hash.data(), x.hash.size());
+    put_u(r, 3, x.slot);
+    put_msg(o, 10, (const uint8_t*)r.data(), r.size());
+  }
+  for (uint64_t i = 0; i < g.nval; ++i) {  // ValidatorRecord (public key / shard / bytes all zero)
+    r.clear();
+    put_u(r, 5, g.h_balance[i]);
+    put_u(r, 6, g.h_start[i]);
+    put_u(r, 7, g.h_end[i]);
+    put_msg(o, 11, (const uint8_t*)r.data(), r.size());
+  }
+  o += g.arrays_enc;
+  return o;
+}
+
+// ---- genesis (types/state.go:44-112) -------------------------------------------------------
+static int genesis(Engine& g) {
+  const uint64_t n = g.nval;
+  g.h_balance.assign(n, PZ_DEFAULT_BALANCE);
+  g.h_start.assign(n, 0);
+  g.h_end.assign(n, PZ_DEFAULT_END_DYNASTY);
+  // ShuffleValidatorsToCommittees(BytesToHash(empty seed), validators, 1, 0) (sharding.go:11-21)
+  std::vector<uint32_t> idx(n);
+  for (uint64_t i = 0; i < n; ++i) idx[i] = (uint32_t)i;
+  uint8_t seed[32] = {0};
+  int rc = pz_shuffle_indices(seed, idx.data(), n);
+  if (rc) return rc;
+  // getCommitteeParams (sharding.go:60-73)
+  uint64_t cps, spc = 1;
+  if (n >= kCycle * PZ_MIN_COMMITTEE_SIZE) {
+    cps = n / (kCycle * PZ_MIN_COMMITTEE_SIZE * 2) + 1;
+  } else {
+    cps = 1;
+    while (n * spc < PZ_MIN_COMMITTEE_SIZE * kCycle && spc < kCycle) spc *= 2;
+  }
+  // splitBySlotShard (sharding.go:27-53): 64 slot arrays; the genesis repeats them 4 times
+  std::vector<uint32_t> members;
+  std::vector<uint64_t> offs{0};
+  std::vector<std::vector<std::pair<uint64_t, uint32_t>>> base(kCycle);
+  std::string arr_enc[kCycle];
+  for (uint64_t i = 0; i < kCycle; ++i) {
+    const uint64_t s0 = n * i / kCycle, s1 = n * (i + 1) / kCycle, len = s1 - s0;
+    const uint64_t shard_start = i * cps / spc;
+    for (uint64_t j = 0; j < cps; ++j) {
+      const uint64_t c0 = s0 + len * j / cps, c1 = s0 + len * (j + 1) / cps;
+      const uint64_t shard = (shard_start + j) % PZ_SHARD_COUNT;
+      const uint32_t cid = (uint32_t)(offs.size() - 1);
+      members.insert(members.end(), idx.begin() + (ptrdiff_t)c0, idx.begin() + (ptrdiff_t)c1);
+      offs.push_back(members.size());
+      base[i].push_back({shard, cid});
+      std::string sc, packed;
+      put_u(sc, 1, shard);
+      for (uint64_t q = c0; q < c1; ++q) put_varint(packed, idx[q]);
+      if (!packed.empty()) put_msg(sc, 2, (const uint8_t*)packed.data(), packed.size());
+      put_msg(arr_enc[i], 1, (const uint8_t*)sc.data(), sc.size());
+    }
+  }
+  g.lookup.clear();
+  g.arrays_enc.clear();
+  for (int rep = 0; rep < 4; ++rep)
+    for (uint64_t i = 0; i < kCycle; ++i) {
+      g.lookup.push_back(base[i]);
+      put_msg(g.arrays_enc, 12, (const uint8_t*)arr_enc[i].data(), arr_enc[i].size());
+    }
+  g.csize.resize(offs.size() - 1);
+  for (size_t c = 0; c + 1 < offs.size(); ++c) g.csize[c] = offs[c + 1] - offs[c];
+  upload(g, g.committee, members.data(), members.size());
+  upload(g, g.coffs, offs.data(), offs.size());
+  upload(g, g.balance, g.h_balance.data(), n);
+  upload(g, g.start, g.h_start.data(), n);
+  upload(g, g.end, g.h_end.data(), n);
+  g.words = (n + 31) / 32;
+  check(g.e_mask.alloc((n + 63) / 64 + 1));
+  check(g.e_blk.alloc(vblocks_per_inst(n) + 1));
+  check(g.e_list.alloc(n + 1));
+  hchk(hipStreamSynchronize(g.s), "sync");
+  auto A = std::make_shared<AState>();
+  A->recent.assign(2 * kCycle, kZero);
+  A->recent_raw_empty = true;
+  auto C = std::make_shared<CState>();
+  C->dynasty = 1;
+  C->tdep = n * PZ_DEFAULT_BALANCE;
+  C->xl = std::make_shared<std::vector<Crosslink>>(PZ_SHARD_COUNT);
+  g.A = A;
+  g.C = C;
+  return PZ_OK;
+}
+
+// ---- blockProcessing (service.go:238-363) ---------------------------------------------------
+static int parse_all(const uint8_t* data, const uint64_t* offs, uint64_t n, std::vector<Block>& blocks) {
+  blocks.resize(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    if (offs[i + 1] < offs[i] || !parse_block(data + offs[i], offs[i + 1] - offs[i], &blocks[i]))
+      return fail(PZ_EINVAL, "block %llu is not a canonical BeaconBlock encoding", (unsigned long long)i);
+  }
+  return PZ_OK;
+}
+
+static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, pz_att_result* ar) {
+  const uint64_t n = blocks.size();
+  // device pass 1: block digests, attestation Hash and Key
+  std::string buf;
+  std::vector<uint64_t> ho{0};
+  uint64_t natt = 0;
+  for (auto& b : blocks) {
+    buf.append((const char*)b.data, b.len);
+    ho.push_back(buf.size());
+    natt += b.atts.size();
+  }
+  for (auto& b : blocks)
+    for (auto& a : b.atts) {
+      buf += a->enc;
+      ho.push_back(buf.size());
+    }
+  for (auto& b : blocks)
+    for (auto& a : b.atts) {  // Key() preimage (types/attestation.go:61-77)
+      std::string k(10, '\0'), v;
+      put_varint(v, a->slot);
+      std::memcpy(&k[0], v.data(), v.size());
+      v.clear();
+      put_varint(v, a->shard);
+      std::memcpy(&k[0], v.data(), v.size());
+      k.append((const char*)a->at(a->sbh_off), a->sbh_len);
+      for (auto& o : a->obl) {
+        const H32 h = copy32(a->at(o.first), o.second);
+        k.append((const char*)h.b, 32);
+      }
+      buf += k;
+      ho.push_back(buf.size());
+    }
+  std::vector<uint8_t> dg;
+  hash_many(g, buf, ho, dg);
+  // the walk
+  std::string msgs;
+  std::vector<uint64_t> mo{0};
+  std::vector<uint64_t> msg_att;
+  std::vector<H32> parents;
+  std::string msg;
+  uint64_t ai = 0;
+  for (uint64_t bi = 0; bi < n; ++bi) {
+    const Block& b = blocks[bi];
+    pz_block_result& r = br[bi];
+    std::memcpy(r.hash, &dg[bi * 64], 32);
+    r.status = PZ_BLOCK_PROCESSED;
+    r.transition = 0;
+    r.first_att = (uint32_t)ai;
+    r.natt = (uint32_t)b.atts.size();
+    const uint64_t a0 = ai;
+    ai += b.atts.size();
+    for (uint64_t j = 0; j < b.atts.size(); ++j) {
+      pz_att_result& x = ar[a0 + j];
+      std::memset(&x, 0, sizeof x);
+      x.status = PZ_ATT_NOT_PROCESSED;
+    }
+    H32 h;
+    std::memcpy(h.b, r.hash, 32);
+    if (b.slot > 1 && !g.saved.count(b.parent)) {
+      r.status = PZ_BLOCK_NO_PARENT;
+      continue;
+    }
+    std::vector<AttP> processed;
+    bool can_atts = false;
+    for (uint64_t j = 0; j < b.atts.size(); ++j) {
+      pz_att_result& x = ar[a0 + j];
+      try {
+        process_attestation(g, b.slot, *b.atts[j], parents, msg);
+      } catch (Rejected& e) {
+        can_atts = false;
+        x.status = e.code;
+        continue;
+      }
+      can_atts = true;
+      x.status = PZ_ATT_PROCESSED;
+      std::memcpy(x.hash, &dg[(n + a0 + j) * 64], 32);
+      std::memcpy(x.key, &dg[(n + natt + a0 + j) * 64], 32);
+      x.msg_len = (uint32_t)msg.size();
+      msgs += msg;
+      mo.push_back(msgs.size());
+      msg_att.push_back(a0 + j);
+      processed.push_back(b.atts[j]);
+    }
+    if (!can_atts) {
+      r.status = PZ_BLOCK_ATTS_REJECTED;
+      continue;
+    }
+    bool cache_nil = true;  // the map returned by the last calculateBlockVoteCache call
+    for (auto& a : b.atts) {
+      try {
+        queue_vote_cache(g, b.slot, *a, parents);
+        cache_nil = g.A->cache_nil;
+      } catch (Rejected&) {
+        cache_nil = true;
+      }
+    }
+    if (g.has_cand && b.slot > g.cand_slot && b.slot > 1) {  // updateHead (service.go:170-227)
+      g.A = g.cand_A;
+      g.C = g.cand_C;
+      g.has_cand = false;
+      g.cand_A.reset();
+      g.cand_C.reset();
+    }
+    g.saved.insert(h);
+    if (g.has_cand) {
+      r.status = PZ_BLOCK_SAVED_NOT_CANDIDATE;
+      continue;
+    }
+    AP A = g.A;
+    CP C = g.C;
+    if (b.slot >= C->lsr + kCycle) {  // IsCycleTransition (core.go:181-183)
+      r.transition = 1;
+      CP nc;
+      AP na;
+      state_recalc(g, C, A, b.slot, &nc, &na);
+      C = nc;
+      A = na;
+    }
+    // computeNewActiveState (core.go:223-237)
+    A->cache_nil = cache_nil;
+    A->pending.insert(A->pending.end(), processed.begin(), processed.end());
+    A->recent.push_back(h);
+    A->recent_raw_empty = false;
+    if (A->recent.size() > 2 * kCycle) A->recent.erase(A->recent.begin(), A->recent.end() - 2 * kCycle);
+    g.has_cand = true;
+    g.cand_slot = b.slot;
+    g.cand_A = A;
+    g.cand_C = C;
+  }
+  flush_votes(g);
+  std::vector<uint8_t> md;
+  hash_many(g, msgs, mo, md);
+  for (size_t i = 0; i < msg_att.size(); ++i) std::memcpy(ar[msg_att[i]].msg_digest, &md[i * 64], 64);
+}
+
+}  // namespace chain
+}  // namespace pz
+
+using namespace pz;
+using namespace pz::chain;
+
+struct pz_chain {
+  Engine g;
+};
+
+extern "C" {
+
+int pz_chain_new(uint64_t nval, int device, pz_chain** out) {
+  if (!out) return fail(PZ_EINVAL, "out is null");
+  *out = nullptr;
+  if (nval == 0 || nval > PZ_MAX_VALIDATORS) return fail(PZ_ETOOMANY, "validator count %llu out of range", (unsigned long long)nval);
+  int rc = pz_init(device);
+  if (rc) return rc;
+  auto* c = new pz_chain();
+  c->g.nval = nval;
+  c->g.device = device;
+  try {
+    hchk(hipStreamCreateWithFlags(&c->g.s, hipStreamNonBlocking), "hipStreamCreate");
+    check(genesis(c->g));
+  } catch (int e) {
+    if (c->g.s) (void)hipStreamDestroy(c->g.s);
+    delete c;
+    return e;
+  }
+  *out = c;
+  return PZ_OK;
+}
+
+void pz_chain_free(pz_chain* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->g.device);
+  if (c->g.s) (void)hipStreamSynchronize(c->g.s);
+  hipStream_t s = c->g.s;
+  delete c;
+  if (s) (void)hipStreamDestroy(s);
+}
+
+int pz_count_attestations(const uint8_t* blocks, const uint64_t* offsets, uint64_t n, uint64_t* count) {
+  if (!count) return fail(PZ_EINVAL, "count is null");
+  *count = 0;
+  if (n && (!blocks || !offsets)) return fail(PZ_EINVAL, "null pointer");
+  for (uint64_t i = 0; i < n; ++i) {
+    if (offsets[i + 1] < offsets[i]) return fail(PZ_EINVAL, "offsets not monotone");
+    Reader r{blocks + offsets[i], blocks + offsets[i + 1]};
+    while (r.more()) {
+      const uint64_t key = r.varint();
+      if ((key >> 3) == 8 && (key & 7) == 2) ++*count;
+      r.skip((uint32_t)(key & 7));
+    }
+  }
+  return PZ_OK;
+}
+
+int pz_chain_process_blocks(pz_chain* c, const uint8_t* blocks, const uint64_t* offsets, uint64_t n,
+                            pz_block_result* block_out, pz_att_result* att_out, uint64_t att_cap) {
+  if (!c) return fail(PZ_EINVAL, "chain is null");
+  if (n == 0) return PZ_OK;
+  if (!blocks || !offsets || !block_out) return fail(PZ_EINVAL, "null pointer");
+  std::lock_guard<std::mutex> lk(c->g.mu);
+  if (c->g.poisoned) return fail(PZ_EINDEX, "chain panicked earlier; create a new one");
+  hipError_t e = hipSetDevice(c->g.device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  // the output capacity is checked before any state changes
+  uint64_t natt = 0;
+  int rc0 = pz_count_attestations(blocks, offsets, n, &natt);
+  if (rc0) return rc0;
+  if (natt > att_cap || (natt && !att_out)) return fail(PZ_EINVAL, "att_out holds %llu results, need %llu",
+                                                        (unsigned long long)att_cap, (unsigned long long)natt);
+  std::vector<Block> parsed;
+  int rc = parse_all(blocks, offsets, n, parsed);  // before any state changes
+  if (rc) return rc;
+  try {
+    process(c->g, parsed, block_out, att_out);
+  } catch (Panic& p) {
+    c->g.poisoned = true;
+    return fail(PZ_EINDEX, "the reference panics here: %s", p.what.c_str());
+  } catch (int rc) {
+    c->g.poisoned = true;
+    return rc;
+  }
+  return PZ_OK;
+}
+
+int pz_chain_roots(pz_chain* c, uint8_t out[4 * 32], int* has_candidate) {
+  if (!c || !out) return fail(PZ_EINVAL, "null pointer");
+  std::lock_guard<std::mutex> lk(c->g.mu);
+  Engine& g = c->g;
+  try {
+    hchk(hipSetDevice(g.device), "hipSetDevice");
+    std::string buf;
+    std::vector<uint64_t> offs{0};
+    buf += encode_active(*g.A);
+    offs.push_back(buf.size());
+    buf += encode_crystallized(g, *g.C);
+    offs.push_back(buf.size());
+    if (g.has_cand) {
+      buf += encode_active(*g.cand_A);
+      offs.push_back(buf.size());
+      buf += encode_crystallized(g, *g.cand_C);
+      offs.push_back(buf.size());
+    }
+    std::vector<uint8_t> d;
+    hash_many(g, buf, offs, d);
+    std::memset(out, 0, 4 * 32);
+    for (size_t i = 0; i + 1 < offs.size(); ++i) std::memcpy(out + 32 * i, &d[64 * i], 32);
+    if (has_candidate) *has_candidate = g.has_cand ? 1 : 0;
+  } catch (int rc) {
+    return rc;
+  }
+  return PZ_OK;
+}
+
+int pz_chain_vote_totals(pz_chain* c, uint8_t* hashes, uint64_t* totals, uint64_t cap, uint64_t* count) {
+  if (!c || !count) return fail(PZ_EINVAL, "null pointer");
+  std::lock_guard<std::mutex> lk(c->g.mu);
+  Engine& g = c->g;
+  const AState& A = g.has_cand ? *g.cand_A : *g.A;
+  *count = A.cache_nil ? 0 : g.slot_hash.size();
+  if (*count > cap) return PZ_OK;  // caller retries with a larger buffer
+  if (!*count) return PZ_OK;
+  if (!hashes || !totals) return fail(PZ_EINVAL, "null pointer");
+  hipError_t e = hipSetDevice(g.device);
+  if (e == hipSuccess) e = hipMemcpyAsync(totals, g.totals.p, *count * 8, hipMemcpyDeviceToHost, g.s);
+  if (e == hipSuccess) e = hipStreamSynchronize(g.s);
+  if (e != hipSuccess) return hip_fail(e, "D2H vote totals");
+  for (uint64_t i = 0; i < *count; ++i) std::memcpy(hashes + 32 * i, g.slot_hash[i].b, 32);
+  return PZ_OK;
+}
+
+}  // extern "C"

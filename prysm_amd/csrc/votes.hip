@@ -41,6 +41,10 @@ pz_vote_tally_kernel(VoteArgs a) {
     const uint32_t v = a.committee[cb + i];
     if (v >= a.nval) { err |= PZ_XLERR_MEMBER; continue; }
     const uint32_t m = 1u << (v & 31);
+    // Voter bits only ever get set, so a plain read that already shows the bit is final;
+    // a stale 0 (another XCD's L2) just falls through to the atomic, which decides.  After
+    // the first attestation of a committee most voters are set: the atomics mostly vanish.
+    if (bm[v >> 5] & m) continue;
     const uint32_t old = atomicOr(&bm[v >> 5], m);
     if (!(old & m)) add += a.balance[v];
   }

@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402,F401
 
 from prysm_amd import synth  # noqa: E402
-from prysm_amd.blockchain import BeaconChain  # noqa: E402
+from prysm_amd.blockchain import BeaconChain, serialize_blocks  # noqa: E402
 
 
 def main():
@@ -26,14 +26,18 @@ def main():
     ch = BeaconChain(nval)
     prof = cProfile.Profile() if "--cprofile" in sys.argv else None
     t = time.perf_counter()
+    data, offs = serialize_blocks(blocks)
+    print("serialize %.3f s (%.1f MB)" % (time.perf_counter() - t, offs[-1] / 1e6), flush=True)
+    t = time.perf_counter()
     if prof:
         prof.enable()
-    recs = ch.process_blocks(blocks)
+    br, ar = ch.process_serialized(data, offs)
     torch.cuda.synchronize()
     if prof:
         prof.disable()
     dt = time.perf_counter() - t
-    print("process_blocks %.3f s -> %.1f blocks/s (%d processed)" % (dt, nblocks / dt, sum(r["status"] == "processed" for r in recs)), flush=True)
+    print("process_serialized %.3f s -> %.1f blocks/s (%d processed, %d attestations)"
+          % (dt, nblocks / dt, int((br["status"] == 0).sum()), len(ar)), flush=True)
     t = time.perf_counter()
     ch.roots()
     print("roots %.3f s" % (time.perf_counter() - t), flush=True)
