@@ -44,11 +44,27 @@ OPS_PER_COMPRESSION = 96 * SLOTS_PER_G + 32            # ~3652 full-rate slots
 XOR_RATE_UNDER_LOAD = 61.46e12                         # measured v_xor_b32 lane-ops/s (DVFS clock)
 
 
+def warm_clocks(step, torch, dev, ms):
+    """Run ``step`` back to back for ``ms`` milliseconds of wall time (untimed): from idle the
+    GPU clock ramps over ~100 ms of sustained load (first launches of the hash kernel take
+    0.40 ms, steady state 0.24 ms), so W short warmup steps alone would time the ramp."""
+    if ms <= 0:
+        return
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        for _ in range(8):
+            step()
+        torch.cuda.synchronize(dev)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--clock-warm-ms", type=float, default=400.0,
+                   help="untimed back-to-back launches before the warmup steps: MI355X clocks ramp "
+                        "from idle over ~100 launches of this kernel (tools/hash_steady.py)")
     p.add_argument("--records", type=int, default=1 << 20)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-epoch", action="store_true")
@@ -84,7 +100,9 @@ def epoch_leg(args, torch, dist, dev, rank, world):
     inst = synth.epoch_batch(nval, ninst, seed=3, shuffled=shuffled)
     de = DeviceEpoch(inst, dev, rank=rank, world=world)
     stream = torch.cuda.current_stream(dev)
-    for _ in range(args.warmup):
+    # a fixed count (not a time budget): at N > 1 every step holds collectives, so all ranks
+    # must run the same number of them
+    for _ in range(args.warmup + (30 if args.clock_warm_ms > 0 else 0)):
         de.step(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -283,6 +301,7 @@ def main():
     def step():
         _lib.lib.call("pz_dev_blake2b512_fixed", d_in.data_ptr(), 512, 512, n, d_out.data_ptr(), 32, sh)
 
+    warm_clocks(step, torch, dev, args.clock_warm_ms)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
