@@ -67,6 +67,8 @@ def parse():
                         "from idle over ~100 launches of this kernel (tools/hash_steady.py)")
     p.add_argument("--records", type=int, default=1 << 20)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-replay-blocks", type=int, default=520,
+                   help="blocks of the replay chain the CPU baseline (oracle/replay.py) processes (~8 s)")
     p.add_argument("--no-epoch", action="store_true")
     p.add_argument("--no-hash", action="store_true")
     p.add_argument("--no-replay", action="store_true")
@@ -85,6 +87,7 @@ def parse():
 EPOCH_BYTES_PER_VALIDATOR = 44.25
 EPOCH_KERNELS = ("pz_epoch_count_kernel", "pz_epoch_mid_kernel", "pz_epoch_reward_kernel")
 HASH_KERNEL = "pz_b2b_fixed_persistent_kernel"
+CPU_SAMPLE_S = 8.0  # seconds of CPU work per cpu_baseline leg (three legs: ~25 s in all)
 
 
 def epoch_leg(args, torch, dist, dev, rank, world):
@@ -155,9 +158,7 @@ def epoch_cpu_baseline(inst):
     """The oracle's C restatement of the same epoch (AoS, 1 thread), on one instance."""
     try:
         from oracle import cport
-        t0 = time.perf_counter()
-        reps = cport.epoch_instance_timed(inst, 0)
-        dt = time.perf_counter() - t0
+        reps, dt = cport.epoch_instance_timed(inst, 0, min_seconds=CPU_SAMPLE_S)
         return {"value": reps * inst["nval"] / dt, "unit": "validator-epochs/s", "cores": 1, "kind": "port",
                 "sample": "%d x one %d-validator epoch instance (AoS records, 1 thread, oracle/c/epoch_ref.c), "
                           "%.2f s" % (reps, inst["nval"], dt)}
@@ -198,6 +199,19 @@ def replay_leg(args, torch, dist, dev, rank, world):
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
+    # State roots (types/state.go:138-149, 237-248) of the replayed chain: the 1.7 MB
+    # CrystallizedState is one serial BLAKE2b chain of 13,416 compressions.  Timed on both
+    # routes: host threads (the default for messages >= 64 KiB) and a single GPU lane.
+    from prysm_amd import _lib
+    root_ms, root_vals = {}, {}
+    for label, thr in (("host_serial", _lib.serial_threshold_default()), ("gpu_lane", _lib.SERIAL_ON_GPU)):
+        with _lib.serial_threshold(thr):
+            t1 = time.perf_counter()
+            r = ch.roots()
+            root_ms[label] = (time.perf_counter() - t1) * 1e3
+            root_vals[label] = r
+    state_roots = {"ms_per_roots_call": root_ms, "routes_agree": root_vals["host_serial"] == root_vals["gpu_lane"],
+                   "what": "4 state roots (chain + candidate Active/Crystallized), serialization included"}
     recs = [{"status": "processed" if s == 0 else "other", "transition": bool(t)}
             for s, t in zip(br["status"], br["transition"])]
     out = {"metric": "sync-replay blocks/s", "value": nb * world / wall, "unit": "blocks/s",
@@ -208,11 +222,12 @@ def replay_leg(args, torch, dist, dev, rank, world):
                       "parallelism": "independent chain per GPU x%d" % world},
            "input": "serialized canonical BeaconBlock encodings, %.1f MB" % (int(offs[-1]) / 1e6),
            "processed": sum(r["status"] == "processed" for r in recs),
-           "transitions": sum(r["transition"] for r in recs)}
+           "transitions": sum(r["transition"] for r in recs),
+           "state_roots": state_roots}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             from oracle import replay as oreplay
-            sample = blocks[:130]
+            sample = blocks[:args.cpu_replay_blocks]
             t0 = time.perf_counter()
             oreplay.replay(sample, nval)
             dt = time.perf_counter() - t0
@@ -269,10 +284,14 @@ def cpu_baseline(records_np):
     n = records_np.shape[0]
     t0 = time.perf_counter()
     digests = cport.hash_fixed(records_np, 512, 32)
+    passes = 1
+    while time.perf_counter() - t0 < CPU_SAMPLE_S:
+        cport.hash_fixed(records_np, 512, 32)
+        passes += 1
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "hashes/s", "cores": 1, "kind": "port",
-            "sample": "%d x 512-B records (the full per-GPU batch), 1 thread, portable C BLAKE2b "
-                      "(oracle/c/blake2b_ref.c), %.2f s" % (n, dt)}, digests
+    return {"value": passes * n / dt, "unit": "hashes/s", "cores": 1, "kind": "port",
+            "sample": "%d pass(es) over the %d x 512-B records of the per-GPU batch, 1 thread, portable C "
+                      "BLAKE2b (oracle/c/blake2b_ref.c), %.2f s" % (passes, n, dt)}, digests
 
 
 def main():

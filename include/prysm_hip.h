@@ -67,6 +67,13 @@ int         pz_version(void);             /* ABI version: 1 */
 int pz_blake2b512_batch(const uint8_t* msgs, const uint64_t* offsets, uint64_t n,
                         uint8_t* out, uint32_t out_bytes);
 
+/* Long single messages (a state root is one serial chain of up to 221,844 compressions at
+ * 1M validators) cannot use more than one lane: the batch entry points above hash every
+ * message of at least `bytes` bytes on host threads (AVX2), concurrently with the GPU launch
+ * for the rest of the batch.  Default 65,536; UINT64_MAX keeps everything on
+ * the GPU.  Returns the previous value.  The pz_dev_* forms never leave the device. */
+uint64_t pz_set_serial_threshold(uint64_t bytes);
+
 /* Device-resident forms (device pointers; caller's stream).  The CSR form requires 4
  * readable bytes past msgs[offsets[n]-1] (the library's own buffers are padded). */
 int pz_dev_blake2b512_batch(const uint8_t* d_msgs, const uint64_t* d_offsets, uint64_t n,

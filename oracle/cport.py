@@ -88,9 +88,9 @@ def epoch_instance(inst, b, slot=0):
         d.oracle_epoch_free(e)
 
 
-def epoch_instance_timed(inst, b, min_seconds=3.0, max_reps=1000):
-    """Time repeated epoch transitions of instance ``b`` (AoS build not timed); returns the
-    number of repetitions done in the caller's timed region."""
+def epoch_instance_timed(inst, b, min_seconds=8.0, max_reps=100000):
+    """Time repeated epoch transitions of instance ``b``; returns (reps, seconds).  Only the
+    transitions are timed (building the AoS records is not)."""
     import time
     d, e = _build_epoch(inst, b)
     try:
@@ -99,6 +99,6 @@ def epoch_instance_timed(inst, b, min_seconds=3.0, max_reps=1000):
         while reps < max_reps and (reps == 0 or time.perf_counter() - t0 < min_seconds):
             d.oracle_epoch_run(e, 0)
             reps += 1
-        return reps
+        return reps, time.perf_counter() - t0
     finally:
         d.oracle_epoch_free(e)

@@ -57,6 +57,7 @@ SIGNATURES = {
     "pz_last_error": [],
     "pz_version": [],
     "pz_blake2b512_batch": [vp, vp, u64, vp, u32],
+    "pz_set_serial_threshold": [u64],
     "pz_dev_blake2b512_batch": [vp, vp, u64, vp, u32, vp],
     "pz_dev_blake2b512_fixed": [vp, u64, u64, u64, vp, u32, vp],
     "pz_validator_indices": [vp, vp, u64, u64, ctypes.c_int, vp, c_u64p],
@@ -104,7 +105,9 @@ class VoteBatch(ctypes.Structure):
 SCAL_POP, SCAL_NACT, SCAL_ERR_XL, SCAL_ERR_RWD, SCAL_APPLIED, SCAL_NEXT_BAL, SCAL_MAXIDX1 = range(7)
 SCAL_COUNT = 8
 KIND_ACTIVE, KIND_EXITED, KIND_QUEUED = 0, 1, 2
-_RESTYPES = {"pz_last_error": ctypes.c_char_p, "pz_chain_free": None}
+_RESTYPES = {"pz_last_error": ctypes.c_char_p, "pz_chain_free": None, "pz_set_serial_threshold": u64}
+SERIAL_DEFAULT = 65536        # the library's default serial threshold (bytes)
+SERIAL_ON_GPU = (1 << 64) - 1  # pz_set_serial_threshold value that keeps every message on the GPU
 
 
 class _Lib:
@@ -173,3 +176,28 @@ def blake2b512_csr(data, offsets, out_bytes=32):
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         lib.call("pz_blake2b512_batch", ptr(data), ptr(offsets), n, ptr(out), out_bytes)
     return out
+
+
+def set_serial_threshold(nbytes):
+    """Messages of at least ``nbytes`` bytes are hashed on host threads by the batch entry
+    points (serial chains); ``SERIAL_ON_GPU`` keeps all of them on the GPU.
+    Returns the previous threshold."""
+    return int(lib.dll.pz_set_serial_threshold(nbytes))
+
+
+def serial_threshold_default():
+    return SERIAL_DEFAULT
+
+
+class serial_threshold:
+    """Context manager form of :func:`set_serial_threshold`."""
+
+    def __init__(self, nbytes):
+        self.nbytes = nbytes
+
+    def __enter__(self):
+        self.old = set_serial_threshold(self.nbytes)
+        return self
+
+    def __exit__(self, *exc):
+        set_serial_threshold(self.old)

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "blake2b_kernels.h"
+#include "serial_hash.h"
 #include "epoch.h"
 #include "runtime.h"
 #include "votes.h"
@@ -347,13 +348,46 @@ static void hash_many(Engine& g, const std::string& data, const std::vector<uint
   const size_t n = offs.size() - 1;
   out.resize(n * 64);
   if (!n) return;
-  check(g.h_in.alloc(data.size() + 16));
-  check(g.h_out.alloc(n * 64));
-  upload(g, g.h_offs, offs.data(), offs.size());
-  if (!data.empty()) hchk(hipMemcpyAsync(g.h_in.p, data.data(), data.size(), hipMemcpyHostToDevice, g.s), "H2D msgs");
-  hchk(launch_b2b_csr(g.h_in.p, g.h_offs.p, n, g.h_out.p, 64, g.s), "blake2b csr");
-  hchk(hipMemcpyAsync(out.data(), g.h_out.p, n * 64, hipMemcpyDeviceToHost, g.s), "D2H digests");
+  // long messages (state roots: one serial chain each) on host threads, overlapping the GPU
+  std::vector<uint64_t> lng = long_messages(offs.data(), n);
+  SerialHashJob job;
+  job.start((const uint8_t*)data.data(), offs.data(), lng, out.data(), 64);
+  if (lng.size() == n) return;  // joined by the destructor
+  const std::string* src = &data;
+  const std::vector<uint64_t>* so = &offs;
+  std::string cat;
+  std::vector<uint64_t> co, idx;
+  if (!lng.empty()) {  // compact the batchable messages
+    co.push_back(0);
+    size_t k = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      if (k < lng.size() && lng[k] == i) {
+        ++k;
+        continue;
+      }
+      cat.append(data, offs[i], offs[i + 1] - offs[i]);
+      co.push_back(cat.size());
+      idx.push_back(i);
+    }
+    src = &cat;
+    so = &co;
+  }
+  const size_t m = so->size() - 1;
+  std::vector<uint8_t> part;
+  uint8_t* dst = out.data();
+  if (!lng.empty()) {
+    part.resize(m * 64);
+    dst = part.data();
+  }
+  check(g.h_in.alloc(src->size() + 16));
+  check(g.h_out.alloc(m * 64));
+  upload(g, g.h_offs, so->data(), so->size());
+  if (!src->empty()) hchk(hipMemcpyAsync(g.h_in.p, src->data(), src->size(), hipMemcpyHostToDevice, g.s), "H2D msgs");
+  hchk(launch_b2b_csr(g.h_in.p, g.h_offs.p, m, g.h_out.p, 64, g.s), "blake2b csr");
+  hchk(hipMemcpyAsync(dst, g.h_out.p, m * 64, hipMemcpyDeviceToHost, g.s), "D2H digests");
   hchk(hipStreamSynchronize(g.s), "sync");
+  job.join();
+  for (size_t j = 0; j < idx.size(); ++j) std::memcpy(&out[idx[j] * 64], &part[j * 64], 64);
 }
 
 // ---- vote cache -------------------------------------------------------------------------------

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "blake2b_kernels.h"
+#include "serial_hash.h"
 
 namespace pz {
 
@@ -157,6 +158,33 @@ int pz_blake2b512_batch(const uint8_t* msgs, const uint64_t* offsets, uint64_t n
   DeviceCtx* c;
   int rc = acquire(&c);
   if (rc) return rc;
+
+  // Long messages (serial chains) go to host threads while the GPU hashes the rest.
+  std::vector<uint64_t> lng = long_messages(offsets, n);
+  if (!lng.empty()) {
+    SerialHashJob job;
+    job.start(msgs, offsets, lng, out, out_bytes);
+    if (lng.size() == n) return PZ_OK;  // joined by the destructor
+    std::vector<uint8_t> cat;
+    std::vector<uint64_t> co{0}, idx;
+    size_t k = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      if (k < lng.size() && lng[k] == i) {
+        ++k;
+        continue;
+      }
+      cat.insert(cat.end(), msgs + offsets[i], msgs + offsets[i + 1]);
+      co.push_back(cat.size());
+      idx.push_back(i);
+    }
+    std::vector<uint8_t> part(idx.size() * out_bytes);
+    rc = pz_blake2b512_batch(cat.data(), co.data(), idx.size(), part.data(), out_bytes);
+    job.join();
+    if (rc) return rc;
+    for (size_t j = 0; j < idx.size(); ++j) std::memcpy(out + idx[j] * out_bytes, &part[j * out_bytes], out_bytes);
+    return PZ_OK;
+  }
+
   std::lock_guard<std::mutex> lk(c->mu);
   if ((rc = c->ensure_stream())) return rc;
   hipStream_t s = c->stream;
@@ -194,6 +222,8 @@ int pz_blake2b512_batch(const uint8_t* msgs, const uint64_t* offsets, uint64_t n
   if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
   return PZ_OK;
 }
+
+uint64_t pz_set_serial_threshold(uint64_t bytes) { return set_serial_threshold(bytes); }
 
 }  // extern "C"
 

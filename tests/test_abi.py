@@ -43,3 +43,23 @@ def test_epoch_batch_struct_layout():
             first, *rest = decl.split(",")
             fields += [first.split()[-1].lstrip("*")] + [r.strip().lstrip("*") for r in rest]
     assert fields == [f for f, _ in _lib.EpochBatch._fields_]
+
+
+def test_host_serial_hasher_matches_hashlib():
+    """The host BLAKE2b used for long serial messages (prysm_amd/csrc/serial_hash.cpp; no GPU
+    involved) against hashlib (RFC 7693) at every block boundary and a few long lengths."""
+    import hashlib
+
+    import numpy as np
+
+    fn = _lib.lib.dll.pz_debug_host_blake2b512
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+    fn.restype = None
+    rng = np.random.default_rng(1)
+    out = ctypes.create_string_buffer(64)
+    for n in list(range(0, 300)) + [1023, 1024, 1025, 65535, 65536, 200001]:
+        m = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        fn(m, n, out)
+        assert out.raw == hashlib.blake2b(m).digest(), n
+    assert _lib.lib.dll.pz_set_serial_threshold(12345) == 65536
+    assert _lib.lib.dll.pz_set_serial_threshold(65536) == 12345

@@ -74,3 +74,19 @@ def test_fixed_kernel_variants_agree_and_match_oracle():
         raw = data.tobytes()
         for i in list(range(0, n, 997)) + [n - 1]:
             assert outs[1][i].tobytes() == ref.hash32(raw[i * rec:(i + 1) * rec])
+
+
+@pytest.mark.parametrize("thr", [1000, _lib.SERIAL_ON_GPU])
+def test_long_messages_host_route_and_gpu_route_agree(thr):
+    """Messages at or above the serial threshold are hashed on host threads while the GPU
+    hashes the rest of the batch; both routes are bit-exact with hashlib, and
+    the digest order is kept when long and short messages interleave."""
+    rng = np.random.default_rng(5)
+    lens = [0, 999, 1000, 1001, 5, 70000, 128, 1000, 3, 131072, 0]
+    msgs = [rng.integers(0, 256, size=l, dtype=np.uint8).tobytes() for l in lens]
+    with _lib.serial_threshold(thr):
+        for ob in (32, 64):
+            got = _lib.blake2b512_batch(msgs, out_bytes=ob)
+            assert got == [ref.sum512(m)[:ob] for m in msgs]
+        only_long = [m for m in msgs if len(m) >= 1000]
+        assert _lib.blake2b512_batch(only_long, 64) == [ref.sum512(m) for m in only_long]

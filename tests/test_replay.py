@@ -72,6 +72,19 @@ def test_gpu_replay_matches_golden():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("serial", ["host", "gpu"])
+def test_gpu_replay_golden_roots_both_serial_routes(serial):
+    """State roots are single long messages: hashed on host threads at or above the serial
+    threshold, on one GPU lane below it.  Both routes reproduce the fixture's roots."""
+    from prysm_amd import _lib
+    g = golden()
+    thr = 1000 if serial == "host" else _lib.SERIAL_ON_GPU
+    with _lib.serial_threshold(thr):
+        recs, roots = _product(g["nval"], synth.chain_blocks(g["nval"], g["nblocks"], seed=g["seed"]))
+    _compare(recs, roots, g)
+
+
+@pytest.mark.gpu
 def test_gpu_replay_in_two_batches_matches_golden():
     """Blocks fed in two batches (deferred work flushed between calls) give the same result."""
     from prysm_amd.blockchain import BeaconChain
