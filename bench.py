@@ -97,7 +97,9 @@ def epoch_leg(args, torch, dist, dev, rank, world):
     from prysm_amd.epoch import DeviceEpoch
 
     nval = args.epoch_validators or (65536 if world == 1 else 1 << 20)
-    ninst = args.epoch_instances or max(1, (1 << 24) // nval)
+    # throughput mode: 16.7 M validator-epochs per GPU per step at every N (weak scaling; at
+    # N > 1 each rank holds 1/N of every 1M-validator instance and B grows with N)
+    ninst = args.epoch_instances or max(1, (1 << 24) * world // nval)
     seed_a = b"A" + bytes(31)  # common.Hash{'A'} (casper/sharding_test.go:57)
     shuffled = casper.shuffle_indices(seed_a, np.arange(nval, dtype=np.uint32))
     inst = synth.epoch_batch(nval, ninst, seed=3, shuffled=shuffled)
@@ -136,6 +138,7 @@ def epoch_leg(args, torch, dist, dev, rank, world):
         "value": units / wall,
         "unit": "validator-epochs/s",
         "ms_per_step": wall / args.steps * 1e3,
+        "scaling": "weak",
         "config": {"workload": "stateRecalc data-parallel part: crosslink tallies+winners, attester "
                                "popcount, CalculateRewards, next-cycle balance (BASELINE configs[%d])"
                                % (2 if world == 1 else 3),

@@ -8,6 +8,10 @@ hipError_t launch_b2b_fixed(const uint8_t* msgs, uint64_t stride, uint64_t len, 
                             uint8_t* out, uint32_t out_bytes, hipStream_t stream);
 hipError_t launch_b2b_csr(const uint8_t* msgs, const uint64_t* offsets, uint64_t n, uint8_t* out,
                           uint32_t out_bytes, hipStream_t stream);
+// processAttestation message digests (64 B each) from the engine's device hash log:
+// message i = hdr[16 i .. 16 i + 10) | 64 x (hlog[ids[64 i + r]] | ' ') | sbh[sbh_offs[i]..sbh_offs[i+1]).
+hipError_t launch_b2b_attmsg(const uint8_t* hlog, const uint32_t* ids, const uint8_t* hdr, const uint8_t* sbh,
+                            const uint64_t* sbh_offs, uint64_t n, uint8_t* out, hipStream_t stream);
 }  // namespace pz
 
 namespace pz {

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -248,6 +249,7 @@ struct Crosslink {
 struct AState {               // types.ActiveState
   std::vector<AttP> pending;  // PendingAttestations
   std::vector<H32> recent;    // RecentBlockHashes, normalised
+  std::vector<uint32_t> recent_ids;  // the same hashes as ids into Engine::hlog
   bool recent_raw_empty = false;  // genesis: every entry is a zero-length byte slice
   bool cache_nil = false;     // the shared vote-cache map, or nil (SetBlockVoteCache(nil))
 };
@@ -276,6 +278,11 @@ struct DevArr {
   ~DevArr() {
     if (p) (void)hipFree(p);
   }
+};
+
+enum ProfSlot {
+  kProfParse, kProfHash1, kProfCheck, kProfQueue, kProfFlush, kProfRecalc, kProfMsgHash, kProfWalk, kProfProcess,
+  kProfCount, kProfSlots
 };
 
 struct Engine {
@@ -321,6 +328,30 @@ struct Engine {
   AP cand_A;
   CP cand_C;
   std::unordered_set<H32, H32Hash> saved;
+  // append-only hash log: every block digest and oblique parent hash the walk meets gets an
+  // id; RecentBlockHashes carry ids too, so signed parent hashes are id ranges (no hashing of
+  // 32-byte keys per vote) and the processAttestation messages are assembled on the device
+  std::vector<H32> hlog;
+  std::vector<int32_t> hslot;  // vote-cache slot of each id (-1: not resolved yet)
+  DevArr<uint8_t> d_hlog;
+  uint64_t d_hlog_n = 0;
+  // processAttestation message batch (10-byte header, 64 parent ids, ShardBlockHash)
+  std::vector<uint8_t> m_hdr, m_sbh;
+  std::vector<uint32_t> m_ids;
+  std::vector<uint64_t> m_sboff{0};
+  DevArr<uint8_t> d_mhdr, d_msbh, d_mout;
+  DevArr<uint32_t> d_mids;
+  DevArr<uint64_t> d_msboff;
+  // wall-time accumulators (seconds) per phase, read by pz_debug_chain_profile
+  double prof[kProfSlots] = {};
+};
+
+// Accumulates the wall time of its scope into Engine::prof[slot].
+struct PhaseTimer {
+  double& acc;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  explicit PhaseTimer(double& a) : acc(a) {}
+  ~PhaseTimer() { acc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); }
 };
 
 struct Panic {
@@ -419,8 +450,21 @@ static uint32_t vote_slot(Engine& g, const H32& h) {
   return s;
 }
 
+static uint32_t log_hash(Engine& g, const H32& h) {
+  g.hlog.push_back(h);
+  g.hslot.push_back(-1);
+  return (uint32_t)(g.hlog.size() - 1);
+}
+
+static uint32_t slot_of_id(Engine& g, uint32_t id) {
+  int32_t& s = g.hslot[id];
+  if (s < 0) s = (int32_t)vote_slot(g, g.hlog[id]);
+  return (uint32_t)s;
+}
+
 static void flush_votes(Engine& g) {
   if (g.q_item_att.empty()) return;
+  PhaseTimer pt(g.prof[kProfFlush]);
   upload(g, g.d_qbits, g.q_bits.data(), g.q_bits.size() + 0);
   upload(g, g.d_qboffs, g.q_boffs.data(), g.q_boffs.size());
   upload(g, g.d_qcomm, g.q_comm.data(), g.q_comm.size());
@@ -458,12 +502,13 @@ static void flush_votes(Engine& g) {
 
 // ---- core.go ------------------------------------------------------------------------------------
 // getSignedParentHashes (core.go:348-360); Go slices up to cap, beyond len panics.
-static void signed_parents(const AState& A, uint64_t block_slot, const Att& a, std::vector<H32>& out) {
+// Returns ids into the hash log; always 64 of them (end - start + len(obliques)).
+static void signed_parents(Engine& g, const AState& A, uint64_t block_slot, const Att& a, std::vector<uint32_t>& out) {
   const uint64_t start = block_slot - a.slot;
   const uint64_t end = block_slot - a.slot - (uint64_t)a.obl.size() + kCycle;
-  if (start > end || end > A.recent.size()) throw Panic{"slice bounds out of range (core.go:353)"};
-  out.assign(A.recent.begin() + (ptrdiff_t)start, A.recent.begin() + (ptrdiff_t)end);
-  for (auto& o : a.obl) out.push_back(bytes_to_hash(a.at(o.first), o.second));
+  if (start > end || end > A.recent_ids.size()) throw Panic{"slice bounds out of range (core.go:353)"};
+  out.assign(A.recent_ids.begin() + (ptrdiff_t)start, A.recent_ids.begin() + (ptrdiff_t)end);
+  for (auto& o : a.obl) out.push_back(log_hash(g, bytes_to_hash(a.at(o.first), o.second)));
 }
 
 // getAttesterIndices (core.go:363-374) -> committee id.
@@ -476,46 +521,46 @@ static uint32_t attester_committee(const Engine& g, const CState& C, const Att& 
 }
 
 // processAttestation (core.go:240-297) -> builds the message whose digest the reference logs.
-static void process_attestation(Engine& g, uint64_t block_slot, const Att& a, std::vector<H32>& parents,
-                                std::string& msg) {
+static void process_attestation(Engine& g, uint64_t block_slot, const Att& a, std::vector<uint32_t>& parents) {
   if ((int64_t)a.slot > (int64_t)block_slot) throw Rejected{PZ_ATT_SLOT_HIGH};
   if ((int64_t)a.slot < (int64_t)block_slot - (int64_t)kCycle) throw Rejected{PZ_ATT_SLOT_LOW};
   if (a.jslot != g.C->jslot) throw Rejected{PZ_ATT_JUSTIFIED};
-  signed_parents(*g.A, block_slot, a, parents);
+  signed_parents(g, *g.A, block_slot, a, parents);
   const uint32_t c = attester_committee(g, *g.C, a);
   const uint64_t k = g.csize[c];
   if ((k + 7) / 8 != a.bf_len) throw Rejected{PZ_ATT_BITFIELD_LEN};  // core.go:379-382
   if (k % 8 && (a.at(a.bf_off)[a.bf_len - 1] & (0xFFu >> (k % 8)))) throw Rejected{PZ_ATT_TRAILING_BITS};
-  msg.assign(10, '\0');
+  // the message: a 10-byte buffer holding uvarint(slot % 64) overwritten by uvarint(shard)
+  // at offset 0, then "parent ' '" x 64, then ShardBlockHash; assembled on the device
+  uint8_t hdr[16] = {0};
   std::string v;
   put_varint(v, a.slot % kCycle);
-  std::memcpy(&msg[0], v.data(), v.size());
-  for (auto& h : parents) {
-    msg.append((const char*)h.b, 32);
-    msg.push_back(' ');
-  }
+  std::memcpy(hdr, v.data(), v.size());
   v.clear();
   put_varint(v, a.shard);
-  std::memcpy(&msg[0], v.data(), v.size());
-  msg.append((const char*)a.at(a.sbh_off), a.sbh_len);
+  std::memcpy(hdr, v.data(), v.size());
+  g.m_hdr.insert(g.m_hdr.end(), hdr, hdr + 16);
+  g.m_ids.insert(g.m_ids.end(), parents.begin(), parents.end());
+  g.m_sbh.insert(g.m_sbh.end(), a.at(a.sbh_off), a.at(a.sbh_off) + a.sbh_len);
+  g.m_sboff.push_back(g.m_sbh.size());
 }
 
 // calculateBlockVoteCache (core.go:300-345): queue one tally item per signed parent hash.
-static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, std::vector<H32>& parents) {
-  signed_parents(*g.A, block_slot, a, parents);
+static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, std::vector<uint32_t>& parents) {
+  signed_parents(g, *g.A, block_slot, a, parents);
   const uint32_t c = attester_committee(g, *g.C, a);
   const uint32_t ai = (uint32_t)g.q_comm.size();
   g.q_comm.push_back(c);
   g.q_bits.insert(g.q_bits.end(), a.at(a.bf_off), a.at(a.bf_off) + a.bf_len);
   g.q_boffs.push_back(g.q_bits.size());
-  for (auto& h : parents) {
+  for (uint32_t id : parents) {
     bool skip = false;
     for (auto& o : a.obl)
-      if (o.second == 32 && std::memcmp(h.b, a.at(o.first), 32) == 0) skip = true;
+      if (o.second == 32 && std::memcmp(g.hlog[id].b, a.at(o.first), 32) == 0) skip = true;
     if (skip) continue;
     if (g.A->cache_nil) throw Panic{"assignment to entry in nil map (core.go:323)"};
     g.q_item_att.push_back(ai);
-    g.q_item_slot.push_back(vote_slot(g, h));
+    g.q_item_slot.push_back(slot_of_id(g, id));
   }
   if (g.q_item_att.size() > (1u << 22)) flush_votes(g);
 }
@@ -610,6 +655,7 @@ static uint64_t epoch_on_device(Engine& g, CState& C, const std::vector<AttP>& p
 // stateRecalc (core.go:398-497) -> (new C, new A).
 static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slot, CP* nc_out, AP* na_out) {
   flush_votes(g);
+  PhaseTimer pt(g.prof[kProfRecalc]);
   uint64_t streak = C->streak, justified = C->jslot, finalized = C->fslot;
   const uint64_t lsr = C->lsr;
   std::vector<uint64_t> tot(kCycle, 0);
@@ -649,7 +695,11 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   for (auto& p : A->pending)
     if (p->slot > lsr) na->pending.push_back(p);
   na->recent = A->recent;
-  if (na->recent.size() > 2 * kCycle) na->recent.erase(na->recent.begin(), na->recent.end() - 2 * kCycle);
+  na->recent_ids = A->recent_ids;
+  if (na->recent.size() > 2 * kCycle) {
+    na->recent.erase(na->recent.begin(), na->recent.end() - 2 * kCycle);
+    na->recent_ids.erase(na->recent_ids.begin(), na->recent_ids.end() - 2 * kCycle);
+  }
   na->cache_nil = A->cache_nil;
   *nc_out = nc;
   *na_out = na;
@@ -763,7 +813,12 @@ static int genesis(Engine& g) {
   check(g.e_list.alloc(n + 1));
   hchk(hipStreamSynchronize(g.s), "sync");
   auto A = std::make_shared<AState>();
+  g.hlog.clear();
+  g.hslot.clear();
+  g.d_hlog_n = 0;
+  const uint32_t zero_id = log_hash(g, kZero);
   A->recent.assign(2 * kCycle, kZero);
+  A->recent_ids.assign(2 * kCycle, zero_id);
   A->recent_raw_empty = true;
   auto C = std::make_shared<CState>();
   C->dynasty = 1;
@@ -784,8 +839,27 @@ static int parse_all(const uint8_t* data, const uint64_t* offs, uint64_t n, std:
   return PZ_OK;
 }
 
+// Upload the hash-log entries appended since the last upload (the device copy grows,
+// keeping its contents).
+static void sync_hash_log(Engine& g) {
+  const uint64_t n = g.hlog.size();
+  if (n == g.d_hlog_n) return;
+  if (n * 32 > g.d_hlog.n) {
+    DevArr<uint8_t> nb;
+    check(nb.alloc(std::max<uint64_t>(n * 32, 2 * g.d_hlog.n)));
+    if (g.d_hlog_n) hchk(hipMemcpyAsync(nb.p, g.d_hlog.p, g.d_hlog_n * 32, hipMemcpyDeviceToDevice, g.s), "D2D");
+    hchk(hipStreamSynchronize(g.s), "sync");
+    std::swap(g.d_hlog.p, nb.p);
+    std::swap(g.d_hlog.n, nb.n);
+  }
+  hchk(hipMemcpyAsync(g.d_hlog.p + g.d_hlog_n * 32, g.hlog[g.d_hlog_n].b, (n - g.d_hlog_n) * 32,
+                      hipMemcpyHostToDevice, g.s), "H2D hash log");
+  g.d_hlog_n = n;
+}
+
 static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, pz_att_result* ar) {
   const uint64_t n = blocks.size();
+  const auto t_hash1 = std::chrono::steady_clock::now();
   // device pass 1: block digests, attestation Hash and Key
   std::string buf;
   std::vector<uint64_t> ho{0};
@@ -818,13 +892,25 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
     }
   std::vector<uint8_t> dg;
   hash_many(g, buf, ho, dg);
+  g.prof[kProfHash1] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_hash1).count();
   // the walk
-  std::string msgs;
-  std::vector<uint64_t> mo{0};
   std::vector<uint64_t> msg_att;
-  std::vector<H32> parents;
-  std::string msg;
+  std::vector<uint32_t> parents;
+  std::vector<uint32_t> block_id(n);
   uint64_t ai = 0;
+  g.m_hdr.clear();
+  g.m_ids.clear();
+  g.m_sbh.clear();
+  g.m_sboff.assign(1, 0);
+  g.m_hdr.reserve(16 * natt);
+  g.m_ids.reserve(kCycle * natt);
+  msg_att.reserve(natt);
+  for (uint64_t bi = 0; bi < n; ++bi) {
+    H32 h;
+    std::memcpy(h.b, &dg[bi * 64], 32);
+    block_id[bi] = log_hash(g, h);
+  }
+  auto t_walk = std::chrono::steady_clock::now();
   for (uint64_t bi = 0; bi < n; ++bi) {
     const Block& b = blocks[bi];
     pz_block_result& r = br[bi];
@@ -851,7 +937,8 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
     for (uint64_t j = 0; j < b.atts.size(); ++j) {
       pz_att_result& x = ar[a0 + j];
       try {
-        process_attestation(g, b.slot, *b.atts[j], parents, msg);
+        PhaseTimer pt(g.prof[kProfCheck]);
+        process_attestation(g, b.slot, *b.atts[j], parents);
       } catch (Rejected& e) {
         can_atts = false;
         x.status = e.code;
@@ -861,9 +948,7 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
       x.status = PZ_ATT_PROCESSED;
       std::memcpy(x.hash, &dg[(n + a0 + j) * 64], 32);
       std::memcpy(x.key, &dg[(n + natt + a0 + j) * 64], 32);
-      x.msg_len = (uint32_t)msg.size();
-      msgs += msg;
-      mo.push_back(msgs.size());
+      x.msg_len = (uint32_t)(10 + 33 * kCycle + b.atts[j]->sbh_len);
       msg_att.push_back(a0 + j);
       processed.push_back(b.atts[j]);
     }
@@ -874,6 +959,7 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
     bool cache_nil = true;  // the map returned by the last calculateBlockVoteCache call
     for (auto& a : b.atts) {
       try {
+        PhaseTimer pt(g.prof[kProfQueue]);
         queue_vote_cache(g, b.slot, *a, parents);
         cache_nil = g.A->cache_nil;
       } catch (Rejected&) {
@@ -906,17 +992,35 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
     A->cache_nil = cache_nil;
     A->pending.insert(A->pending.end(), processed.begin(), processed.end());
     A->recent.push_back(h);
+    A->recent_ids.push_back(block_id[bi]);
     A->recent_raw_empty = false;
-    if (A->recent.size() > 2 * kCycle) A->recent.erase(A->recent.begin(), A->recent.end() - 2 * kCycle);
+    if (A->recent.size() > 2 * kCycle) {
+      A->recent.erase(A->recent.begin(), A->recent.end() - 2 * kCycle);
+      A->recent_ids.erase(A->recent_ids.begin(), A->recent_ids.end() - 2 * kCycle);
+    }
     g.has_cand = true;
     g.cand_slot = b.slot;
     g.cand_A = A;
     g.cand_C = C;
   }
+  g.prof[kProfWalk] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_walk).count();
   flush_votes(g);
-  std::vector<uint8_t> md;
-  hash_many(g, msgs, mo, md);
-  for (size_t i = 0; i < msg_att.size(); ++i) std::memcpy(ar[msg_att[i]].msg_digest, &md[i * 64], 64);
+  PhaseTimer pt(g.prof[kProfMsgHash]);
+  const size_t nm = msg_att.size();
+  if (nm) {
+    sync_hash_log(g);
+    upload(g, g.d_mhdr, g.m_hdr.data(), g.m_hdr.size());
+    upload(g, g.d_mids, g.m_ids.data(), g.m_ids.size());
+    upload(g, g.d_msbh, g.m_sbh.data(), g.m_sbh.size() + 1);  // (+1: never an empty allocation)
+    upload(g, g.d_msboff, g.m_sboff.data(), g.m_sboff.size());
+    check(g.d_mout.alloc(nm * 64));
+    hchk(launch_b2b_attmsg(g.d_hlog.p, g.d_mids.p, g.d_mhdr.p, g.d_msbh.p, g.d_msboff.p, nm, g.d_mout.p, g.s),
+         "attestation message digests");
+    std::vector<uint8_t> md(nm * 64);
+    hchk(hipMemcpyAsync(md.data(), g.d_mout.p, nm * 64, hipMemcpyDeviceToHost, g.s), "D2H");
+    hchk(hipStreamSynchronize(g.s), "sync");  // also keeps the pageable sources alive
+    for (size_t i = 0; i < nm; ++i) std::memcpy(ar[msg_att[i]].msg_digest, &md[i * 64], 64);
+  }
 }
 
 }  // namespace chain
@@ -988,14 +1092,23 @@ int pz_chain_process_blocks(pz_chain* c, const uint8_t* blocks, const uint64_t* 
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   // the output capacity is checked before any state changes
   uint64_t natt = 0;
-  int rc0 = pz_count_attestations(blocks, offsets, n, &natt);
+  int rc0;
+  {
+    PhaseTimer pt(c->g.prof[kProfCount]);
+    rc0 = pz_count_attestations(blocks, offsets, n, &natt);
+  }
   if (rc0) return rc0;
   if (natt > att_cap || (natt && !att_out)) return fail(PZ_EINVAL, "att_out holds %llu results, need %llu",
                                                         (unsigned long long)att_cap, (unsigned long long)natt);
   std::vector<Block> parsed;
-  int rc = parse_all(blocks, offsets, n, parsed);  // before any state changes
+  int rc;
+  {
+    PhaseTimer pt(c->g.prof[kProfParse]);
+    rc = parse_all(blocks, offsets, n, parsed);  // before any state changes
+  }
   if (rc) return rc;
   try {
+    PhaseTimer pt(c->g.prof[kProfProcess]);
     process(c->g, parsed, block_out, att_out);
   } catch (Panic& p) {
     c->g.poisoned = true;
@@ -1054,3 +1167,12 @@ int pz_chain_vote_totals(pz_chain* c, uint8_t* hashes, uint64_t* totals, uint64_
 }
 
 }  // extern "C"
+
+// Internal (tools/replay_profile.py): cumulative wall seconds per phase of the block pipeline:
+// parse, digest batch 1 (blocks/Hash/Key), attestation checks + message assembly, vote-cache
+// queueing, vote tally flushes, stateRecalc (excluding its flush), message digests.
+extern "C" int pz_debug_chain_profile(pz_chain* c, double* out, int n) {
+  if (!c || !out) return PZ_EINVAL;
+  for (int i = 0; i < n && i < pz::chain::kProfSlots; ++i) out[i] = c->g.prof[i];
+  return pz::chain::kProfSlots;
+}

@@ -38,6 +38,15 @@ def main():
     dt = time.perf_counter() - t
     print("process_serialized %.3f s -> %.1f blocks/s (%d processed, %d attestations)"
           % (dt, nblocks / dt, int((br["status"] == 0).sum()), len(ar)), flush=True)
+    import ctypes
+    from prysm_amd import _lib
+    pv = (ctypes.c_double * 16)()
+    fn = _lib.lib.dll.pz_debug_chain_profile
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    k = fn(ch._h, pv, 16)
+    names = ["parse", "digests1", "att_checks+msg", "vote_queue", "vote_flush", "state_recalc", "msg_digests",
+             "walk(all)", "process(all)", "count_atts"]
+    print("phases (s): " + ", ".join("%s %.4f" % (names[i], pv[i]) for i in range(k)), flush=True)
     t = time.perf_counter()
     ch.roots()
     print("roots %.3f s" % (time.perf_counter() - t), flush=True)
