@@ -307,9 +307,15 @@ struct Engine {
   DevArr<uint32_t> bitmaps;
   DevArr<uint64_t> totals;
   uint64_t words = 0, cap = 0;
+  // pending tally work, grouped per (vote slot, committee): the union of the bitfields of
+  // every queued attestation of that committee signing that hash (dedup makes the union
+  // exact); one device work item per group
   std::vector<uint8_t> q_bits;
   std::vector<uint64_t> q_boffs{0};
   std::vector<uint32_t> q_comm, q_item_att, q_item_slot;
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> q_groups_of_slot;  // slot -> (committee, group)
+  std::vector<uint32_t> q_touched;                                            // slots with groups
+  uint64_t q_err = 0;                                                         // tally panic flag (D2H)
   DevArr<uint8_t> d_qbits;
   DevArr<uint64_t> d_qboffs, d_err;
   DevArr<uint32_t> d_qcomm, d_qia, d_qis;
@@ -462,8 +468,9 @@ static uint32_t slot_of_id(Engine& g, uint32_t id) {
   return (uint32_t)s;
 }
 
-static void flush_votes(Engine& g) {
-  if (g.q_item_att.empty()) return;
+// Enqueue the pending tally items (no sync); flush_votes_finish must follow a stream sync.
+static bool flush_votes_enqueue(Engine& g) {
+  if (g.q_item_att.empty()) return false;
   PhaseTimer pt(g.prof[kProfFlush]);
   upload(g, g.d_qbits, g.q_bits.data(), g.q_bits.size() + 0);
   upload(g, g.d_qboffs, g.q_boffs.data(), g.q_boffs.size());
@@ -489,15 +496,33 @@ static void flush_votes(Engine& g) {
   v.totals = g.totals.p;
   v.err = g.d_err.p;
   hchk(launch_vote_tally(v, g.s), "vote tally");
-  uint64_t err = 0;
-  hchk(hipMemcpyAsync(&err, g.d_err.p, 8, hipMemcpyDeviceToHost, g.s), "D2H");
-  hchk(hipStreamSynchronize(g.s), "sync");  // also keeps the pageable sources alive
+  g.q_err = 0;
+  hchk(hipMemcpyAsync(&g.q_err, g.d_err.p, 8, hipMemcpyDeviceToHost, g.s), "D2H");
+  return true;
+}
+
+// After the stream sync that completed flush_votes_enqueue's work (its pageable sources stay
+// alive until then): reset the queue and raise the panic the tally detected.
+static void flush_votes_finish(Engine& g) {
+  const uint64_t err = g.q_err;
+  g.q_err = 0;
   g.q_bits.clear();
   g.q_boffs.assign(1, 0);
   g.q_comm.clear();
   g.q_item_att.clear();
   g.q_item_slot.clear();
+  for (uint32_t sl : g.q_touched) g.q_groups_of_slot[sl].clear();
+  g.q_touched.clear();
   if (err) throw Panic{"calculateBlockVoteCache: CheckBit / validator index out of range"};
+}
+
+static void flush_votes(Engine& g) {
+  if (!flush_votes_enqueue(g)) return;
+  {
+    PhaseTimer pt(g.prof[kProfFlush]);
+    hchk(hipStreamSynchronize(g.s), "sync");
+  }
+  flush_votes_finish(g);
 }
 
 // ---- core.go ------------------------------------------------------------------------------------
@@ -549,28 +574,64 @@ static void process_attestation(Engine& g, uint64_t block_slot, const Att& a, st
 static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, std::vector<uint32_t>& parents) {
   signed_parents(g, *g.A, block_slot, a, parents);
   const uint32_t c = attester_committee(g, *g.C, a);
-  const uint32_t ai = (uint32_t)g.q_comm.size();
-  g.q_comm.push_back(c);
-  g.q_bits.insert(g.q_bits.end(), a.at(a.bf_off), a.at(a.bf_off) + a.bf_len);
-  g.q_boffs.push_back(g.q_bits.size());
+  const uint64_t k = g.csize[c], nb = (k + 7) / 8;
+  const uint8_t* bf = a.at(a.bf_off);
   for (uint32_t id : parents) {
     bool skip = false;
     for (auto& o : a.obl)
       if (o.second == 32 && std::memcmp(g.hlog[id].b, a.at(o.first), 32) == 0) skip = true;
     if (skip) continue;
     if (g.A->cache_nil) throw Panic{"assignment to entry in nil map (core.go:323)"};
-    g.q_item_att.push_back(ai);
-    g.q_item_slot.push_back(slot_of_id(g, id));
+    // the member loop reaches CheckBit(bitfield, 8 * len) when the committee is longer
+    if (k > 8ull * a.bf_len) throw Panic{"calculateBlockVoteCache: CheckBit index out of range (core.go:330)"};
+    const uint32_t sl = slot_of_id(g, id);
+    if (sl >= g.q_groups_of_slot.size()) g.q_groups_of_slot.resize(std::max<size_t>(sl + 1, 2 * g.q_groups_of_slot.size()));
+    auto& gs = g.q_groups_of_slot[sl];
+    uint32_t grp = UINT32_MAX;
+    for (auto& e : gs)
+      if (e.first == c) grp = e.second;
+    if (grp == UINT32_MAX) {  // new (slot, committee) group with an all-zero bitfield
+      if (gs.empty()) g.q_touched.push_back(sl);
+      grp = (uint32_t)g.q_comm.size();
+      gs.push_back({c, grp});
+      g.q_comm.push_back(c);
+      g.q_item_att.push_back(grp);
+      g.q_item_slot.push_back(sl);
+      g.q_bits.resize(g.q_bits.size() + nb, 0);
+      g.q_boffs.push_back(g.q_bits.size());
+    }
+    uint8_t* dst = g.q_bits.data() + g.q_boffs[grp];
+    uint64_t i = 0;  // union of the bitfields, 8 bytes at a time (positions >= k are never read)
+    for (; i + 8 <= nb; i += 8) {
+      uint64_t x, y;
+      std::memcpy(&x, dst + i, 8);
+      std::memcpy(&y, bf + i, 8);
+      x |= y;
+      std::memcpy(dst + i, &x, 8);
+    }
+    for (; i < nb; ++i) dst[i] |= bf[i];
   }
   if (g.q_item_att.size() > (1u << 22)) flush_votes(g);
 }
 
 // processCrosslinks + CalculateRewards + next-cycle balance on the device -> next balance.
-static uint64_t epoch_on_device(Engine& g, CState& C, const std::vector<AttP>& pending, uint64_t block_slot) {
-  const size_t na = pending.size();
-  std::vector<uint32_t> comm(na), shard(na);
+// Host staging of one device epoch; lives until the stream sync after epoch_enqueue.
+struct EpochJob {
+  std::vector<uint32_t> comm, shard, win;
   std::vector<uint8_t> bits;
-  std::vector<uint64_t> boffs{0};
+  std::vector<uint64_t> boffs{0}, rdyn;
+  uint64_t small[2] = {0, 0};
+  uint64_t scal[kScal] = {};
+};
+
+static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending, EpochJob& J) {
+  const size_t na = pending.size();
+  std::vector<uint32_t>& comm = J.comm;
+  std::vector<uint32_t>& shard = J.shard;
+  std::vector<uint8_t>& bits = J.bits;
+  std::vector<uint64_t>& boffs = J.boffs;
+  comm.resize(na);
+  shard.resize(na);
   for (size_t i = 0; i < na; ++i) {
     const Att& a = *pending[i];
     try {
@@ -584,9 +645,12 @@ static uint64_t epoch_on_device(Engine& g, CState& C, const std::vector<AttP>& p
     boffs.push_back(bits.size());
   }
   std::vector<Crosslink>& xl = *C.xl;
-  std::vector<uint64_t> rdyn(xl.size());
+  std::vector<uint64_t>& rdyn = J.rdyn;
+  rdyn.resize(xl.size());
   for (size_t s = 0; s < xl.size(); ++s) rdyn[s] = xl[s].dynasty;
-  const uint64_t small[2] = {C.dynasty, C.tdep};
+  uint64_t* small = J.small;
+  small[0] = C.dynasty;
+  small[1] = C.tdep;
   upload(g, g.e_bits, bits.data(), bits.size());
   upload(g, g.e_boffs, boffs.data(), boffs.size());
   upload(g, g.e_comm, comm.data(), na);
@@ -630,11 +694,18 @@ static uint64_t epoch_on_device(Engine& g, CState& C, const std::vector<AttP>& p
   hchk(launch_epoch_count(a, true, true, true, g.s), "epoch count");
   hchk(launch_epoch_mid(a, a.nrec > 0 && na > 0, true, g.s), "epoch mid");
   hchk(launch_epoch_reward(a, g.s), "epoch reward");
-  uint64_t scal[kScal];
-  std::vector<uint32_t> win(xl.size());
-  hchk(hipMemcpyAsync(scal, g.e_scal.p, sizeof scal, hipMemcpyDeviceToHost, g.s), "D2H");
-  if (!win.empty()) hchk(hipMemcpyAsync(win.data(), g.e_win.p, win.size() * 4, hipMemcpyDeviceToHost, g.s), "D2H");
-  hchk(hipStreamSynchronize(g.s), "sync");
+  J.win.resize(xl.size());
+  hchk(hipMemcpyAsync(J.scal, g.e_scal.p, sizeof J.scal, hipMemcpyDeviceToHost, g.s), "D2H");
+  if (!J.win.empty()) hchk(hipMemcpyAsync(J.win.data(), g.e_win.p, J.win.size() * 4, hipMemcpyDeviceToHost, g.s), "D2H");
+}
+
+// After the sync: the reference's panics, the crosslink winners, the next-cycle balance.
+static uint64_t epoch_finish(Engine& g, CState& C, const std::vector<AttP>& pending, uint64_t block_slot,
+                             const EpochJob& J) {
+  const size_t na = pending.size();
+  std::vector<Crosslink>& xl = *C.xl;
+  const uint64_t* scal = J.scal;
+  const std::vector<uint32_t>& win = J.win;
   if (scal[kErrXl]) throw Panic{"processCrosslinks: index out of range (committee member, bitfield or shard)"};
   const uint64_t dep = scal[kPop] * PZ_DEFAULT_BALANCE;
   const bool thr = dep * 3ull >= C.tdep * 2ull;
@@ -654,17 +725,24 @@ static uint64_t epoch_on_device(Engine& g, CState& C, const std::vector<AttP>& p
 
 // stateRecalc (core.go:398-497) -> (new C, new A).
 static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slot, CP* nc_out, AP* na_out) {
-  flush_votes(g);
+  // One stream sync for the whole transition: the pending vote tallies, the D2H of the
+  // totals the justification loop reads, and the device epoch (processCrosslinks,
+  // CalculateRewards, next balance; independent of the justification) are all enqueued first.
+  const bool flushed = flush_votes_enqueue(g);
   PhaseTimer pt(g.prof[kProfRecalc]);
   uint64_t streak = C->streak, justified = C->jslot, finalized = C->fslot;
   const uint64_t lsr = C->lsr;
   std::vector<uint64_t> tot(kCycle, 0);
+  std::vector<uint64_t> all;
   if (!A->cache_nil) {
-    std::vector<uint64_t> all(g.slot_hash.size());
-    if (!all.empty()) {
-      hchk(hipMemcpyAsync(all.data(), g.totals.p, all.size() * 8, hipMemcpyDeviceToHost, g.s), "D2H");
-      hchk(hipStreamSynchronize(g.s), "sync");
-    }
+    all.resize(g.slot_hash.size());
+    if (!all.empty()) hchk(hipMemcpyAsync(all.data(), g.totals.p, all.size() * 8, hipMemcpyDeviceToHost, g.s), "D2H");
+  }
+  EpochJob job;
+  epoch_enqueue(g, *C, A->pending, job);
+  hchk(hipStreamSynchronize(g.s), "sync");
+  if (flushed) flush_votes_finish(g);
+  if (!A->cache_nil) {
     for (uint64_t i = 0; i < kCycle && i < A->recent.size(); ++i) {
       auto it = g.slot_of.find(A->recent[i]);
       tot[i] = it == g.slot_of.end() ? 0 : all[it->second];
@@ -680,7 +758,7 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
     }
     if (streak >= kCycle + 1 && slot - kCycle > finalized) finalized = slot - kCycle;
   }
-  const uint64_t nxt = epoch_on_device(g, *C, A->pending, block_slot);
+  const uint64_t nxt = epoch_finish(g, *C, A->pending, block_slot, job);
   auto nc = std::make_shared<CState>();
   nc->lsr = lsr + kCycle;
   nc->jslot = justified;
