@@ -286,6 +286,12 @@ int  pz_chain_process_blocks(pz_chain* chain, const uint8_t* blocks, const uint6
 /* State roots (types/state.go:138-149, 237-248): out[0..31] chain ActiveState, [32..63] chain
  * CrystallizedState, [64..127] the candidate's (zero when *has_candidate == 0). */
 int  pz_chain_roots(pz_chain* chain, uint8_t out[4 * 32], int* has_candidate);
+/* Persistence format: the proto3 encoding the reference stores under activeStateLookupKey /
+ * crystallizedStateLookupKey (PersistActiveState / PersistCrystallizedState,
+ * blockchain/core.go:161-177, schema.go:17-27) — the bytes the state roots hash.
+ * which: 0 chain ActiveState, 1 chain CrystallizedState, 2 / 3 the candidate's (PZ_EINVAL
+ * when there is no candidate).  *len receives the size; bytes are written when cap >= *len. */
+int  pz_chain_state_bytes(pz_chain* chain, int which, uint8_t* out, uint64_t cap, uint64_t* len);
 /* The block vote cache: *count entries (0 when the map is nil); fills hashes[32*i] and
  * totals[i] (VoteTotalDeposit) when cap >= *count. */
 int  pz_chain_vote_totals(pz_chain* chain, uint8_t* hashes, uint64_t* totals, uint64_t cap, uint64_t* count);

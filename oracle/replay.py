@@ -137,9 +137,21 @@ class Chain:
         return out
 
 
-def replay(blocks, nval):
+    def state_bytes(self):
+        """The persisted encodings (blockchain/core.go:161-177) of the same four states."""
+        out = {"chain_active": ref.marshal(self.A.data), "chain_crystallized": ref.marshal(self.C)}
+        if self.candidate is not None:
+            _, A, C = self.candidate
+            out["cand_active"] = ref.marshal(A.data)
+            out["cand_crystallized"] = ref.marshal(C)
+        return out
+
+
+def replay(blocks, nval, with_state_bytes=False):
     """Run ``blocks`` (BeaconBlock-like objects, in order) through a fresh genesis chain of
-    ``nval`` validators -> (per-block records, roots dict)."""
+    ``nval`` validators -> (per-block records, roots dict[, state bytes dict])."""
     chain = Chain(nval)
     recs = [chain.process_block(to_pb_block(b)) for b in blocks]
+    if with_state_bytes:
+        return recs, chain.roots(), chain.state_bytes()
     return recs, chain.roots()

@@ -74,6 +74,7 @@ SIGNATURES = {
     "pz_count_attestations": [vp, vp, u64, c_u64p],
     "pz_chain_process_blocks": [vp, vp, vp, u64, vp, vp, u64],
     "pz_chain_roots": [vp, vp, c_intp],
+    "pz_chain_state_bytes": [vp, ctypes.c_int, vp, u64, c_u64p],
     "pz_chain_vote_totals": [vp, vp, vp, u64, c_u64p],
     "pz_dev_vote_tally": [vp, vp],
     "pz_vote_tally": [vp, vp, u64, vp, vp, vp, u64, vp, vp, u64, vp, u64, vp, u64, u64, vp],

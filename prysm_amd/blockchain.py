@@ -109,6 +109,23 @@ class BeaconChain:
             recs.append(rec)
         return recs
 
+    STATES = ("chain_active", "chain_crystallized", "cand_active", "cand_crystallized")
+
+    def state_bytes(self, which):
+        """The persisted proto3 encoding of a state (blockchain/core.go:161-177): ``which`` in
+        ``STATES``; None for a candidate state when there is no candidate."""
+        w = self.STATES.index(which)
+        n = ctypes.c_uint64(0)
+        try:
+            lib.call("pz_chain_state_bytes", self._h, w, None, 0, ctypes.byref(n))
+        except PzError as e:
+            if w >= 2 and e.code == _lib.PZ_EINVAL:
+                return None
+            raise
+        buf = np.zeros(max(n.value, 1), dtype=np.uint8)
+        lib.call("pz_chain_state_bytes", self._h, w, buf.ctypes.data, n.value, ctypes.byref(n))
+        return buf[:n.value].tobytes()
+
     def roots(self):
         """State roots (types/state.go:138-149, 237-248) of the chain's and the candidate's
         states, and the vote cache totals {hash: VoteTotalDeposit}."""

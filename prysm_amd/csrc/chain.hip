@@ -1227,6 +1227,24 @@ int pz_chain_roots(pz_chain* c, uint8_t out[4 * 32], int* has_candidate) {
   return PZ_OK;
 }
 
+int pz_chain_state_bytes(pz_chain* c, int which, uint8_t* out, uint64_t cap, uint64_t* len) {
+  if (!c || !len) return fail(PZ_EINVAL, "null pointer");
+  if (which < 0 || which > 3) return fail(PZ_EINVAL, "which must be 0..3");
+  std::lock_guard<std::mutex> lk(c->g.mu);
+  Engine& g = c->g;
+  if (which >= 2 && !g.has_cand) return fail(PZ_EINVAL, "no candidate state");
+  try {
+    hchk(hipSetDevice(g.device), "hipSetDevice");
+    const std::string b = (which & 1) ? encode_crystallized(g, which >= 2 ? *g.cand_C : *g.C)
+                                      : encode_active(which >= 2 ? *g.cand_A : *g.A);
+    *len = b.size();
+    if (out && cap >= b.size()) std::memcpy(out, b.data(), b.size());
+  } catch (int rc) {
+    return rc;
+  }
+  return PZ_OK;
+}
+
 int pz_chain_vote_totals(pz_chain* c, uint8_t* hashes, uint64_t* totals, uint64_t cap, uint64_t* count) {
   if (!c || !count) return fail(PZ_EINVAL, "null pointer");
   std::lock_guard<std::mutex> lk(c->g.mu);

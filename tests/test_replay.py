@@ -209,3 +209,28 @@ def test_generator_shape():
     assert all(len(a.oblique_parent_hashes) == 1 for a in blocks[0].attestations)
     bf = np.frombuffer(blocks[0].attestations[0].attester_bitfield, np.uint8)
     assert bf[-1] & 0x0F == 0  # 204 members: the last 4 bits are padding
+
+
+@pytest.mark.gpu
+def test_gpu_state_bytes_match_oracle_encoding():
+    """The persistence format (PersistActiveState / PersistCrystallizedState, core.go:161-177):
+    the engine's state encodings are byte-identical to the protobuf runtime's marshal of the
+    oracle's states, after genesis and after two cycle transitions, and they hash to the
+    roots."""
+    from oracle import ref
+    from oracle import replay as oreplay
+    from prysm_amd.blockchain import BeaconChain
+    nval = 1024
+    ch = BeaconChain(nval)
+    _, _, ob = oreplay.replay([], nval, with_state_bytes=True)
+    for k in ("chain_active", "chain_crystallized"):
+        assert ch.state_bytes(k) == ob[k], k
+    assert ch.state_bytes("cand_active") is None
+    blocks = synth.chain_blocks(nval, 130, seed=1)
+    ch.process_blocks(blocks)
+    _, oroots, ob = oreplay.replay(blocks, nval, with_state_bytes=True)
+    roots = ch.roots()
+    for k in BeaconChain.STATES:
+        b = ch.state_bytes(k)
+        assert b == ob[k], k
+        assert ref.hash32(b) == roots[k] == oroots[k], k
