@@ -57,6 +57,14 @@ def warm_clocks(step, torch, dev, ms):
         torch.cuda.synchronize(dev)
 
 
+def max_over_ranks(x, torch, dist, dev):
+    """MAX of a host float over the ranks (a device tensor for RCCL, a host one for gloo)."""
+    on_dev = dist.get_backend() == "nccl"
+    t = torch.tensor([x], dtype=torch.float64, device=dev if on_dev else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -67,6 +75,8 @@ def parse():
                         "from idle over ~100 launches of this kernel (tools/hash_steady.py)")
     p.add_argument("--records", type=int, default=1 << 20)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="collective backend at N > 1 (gloo: rehearsal with ranks sharing a GPU)")
     p.add_argument("--cpu-replay-blocks", type=int, default=520,
                    help="blocks of the replay chain the CPU baseline (oracle/replay.py) processes (~8 s)")
     p.add_argument("--no-epoch", action="store_true")
@@ -127,9 +137,7 @@ def epoch_leg(args, torch, dist, dev, rank, world):
     wall = time.perf_counter() - t0
     step_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+        wall = max_over_ranks(wall, torch, dist, dev)
     units = nval * ninst * args.steps
     local_units = (de.hi - de.lo) * ninst
     achieved = local_units * EPOCH_BYTES_PER_VALIDATOR / (step_ms * 1e-3)
@@ -199,9 +207,7 @@ def replay_leg(args, torch, dist, dev, rank, world):
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+        wall = max_over_ranks(wall, torch, dist, dev)
     # State roots (types/state.go:138-149, 237-248) of the replayed chain: the 1.7 MB
     # CrystallizedState is one serial BLAKE2b chain of 13,416 compressions.  Timed on both
     # routes: host threads (the default for messages >= 64 KiB) and a single GPU lane.
@@ -308,7 +314,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl")
+        # "nccl" is RCCL over xGMI; "gloo" only rehearses the N > 1 code path with several
+        # ranks sharing one GPU (collectives through host copies; not a measurement)
+        dist.init_process_group(args.backend)
+    if args.backend == "gloo":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     _lib.lib.call("pz_init", local)
@@ -344,9 +354,7 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+        wall = max_over_ranks(wall, torch, dist, dev)
 
     epoch = None if args.no_epoch else epoch_leg(args, torch, dist, dev, rank, world)
     replay = None if args.no_replay else replay_leg(args, torch, dist, dev, rank, world)
