@@ -185,6 +185,12 @@ typedef struct pz_epoch_batch {
   uint64_t* scal_next;            /* optional [B][PZ_SCAL_COUNT]: zeroed by the finish pass so
                                      the NEXT step can accumulate into it (ping-pong; saves a
                                      memset launch per step) */
+  const uint32_t* cpos;           /* optional, multi-rank: `committee`/`coffs` list only this
+                                     rank's members (global indices in [val_offset,
+                                     val_offset + nval), plus, on rank 0, any member >=
+                                     nval_global so that its panic is raised) and cpos[k] is
+                                     member k's position in its full committee (the bitfield
+                                     bit); NULL: full committees, position = index in the row */
 } pz_epoch_batch;
 
 /* ---- T: block vote-cache tally (blockchain/core.go:300-345 calculateBlockVoteCache) ----

@@ -91,6 +91,7 @@ class EpochBatch(ctypes.Structure):
         ("committee", vp), ("coffs", vp), ("att_comm", vp), ("att_shard", vp),
         ("nrec", ctypes.c_uint32), ("rec_dynasty", vp), ("winner", vp), ("vote", vp), ("total", vp),
         ("scal", vp), ("act_mask", vp), ("blk_cnt", vp), ("act_list", vp), ("scal_next", vp),
+        ("cpos", vp),
     ]
 
 

@@ -102,10 +102,16 @@ __device__ __forceinline__ void crosslink_wave(const EpochArgs& a, uint64_t ga, 
       const uint64_t i = r0 + j * 64 + lane;
       mem[j] = C[i < k ? i : 0];
     }
+    uint32_t pos[4];  // bitfield position of the member (its index in the full committee)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint64_t i = r0 + j * 64 + lane;
-      byte[j] = (i < k && i < 8 * blen) ? bf[i >> 3] : 0u;
+      pos[j] = a.cpos ? a.cpos[cb + (i < k ? i : 0)] : (uint32_t)i;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t i = r0 + j * 64 + lane;
+      byte[j] = (i < k && pos[j] < 8 * blen) ? bf[pos[j] >> 3] : 0u;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -119,9 +125,9 @@ __device__ __forceinline__ void crosslink_wave(const EpochArgs& a, uint64_t ga, 
       const uint64_t i = r0 + j * 64 + lane;
       if (i < k) {
         e_mem |= mem[j] >= a.nval_global;
-        e_bf |= i >= 8 * blen;
+        e_bf |= pos[j] >= 8 * blen;
         tot += bal[j];
-        vote += ((byte[j] >> (7 - (uint32_t)(i & 7))) & 1u) ? bal[j] : 0;
+        vote += ((byte[j] >> (7 - (pos[j] & 7))) & 1u) ? bal[j] : 0;
       }
     }
   }

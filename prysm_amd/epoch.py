@@ -27,6 +27,24 @@ def shard_range(nval_global, rank, world):
     return min(nval_global, rank * s), min(nval_global, (rank + 1) * s)
 
 
+def local_committees(committee, coffs, lo, hi, nval_global, keep_out_of_range):
+    """The committee CSR restricted to members in [lo, hi) (plus, when
+    ``keep_out_of_range``, members >= nval_global, whose panic that rank raises), with each
+    kept member's position in its full committee -> (committee, coffs, cpos)."""
+    committee = np.asarray(committee, dtype=np.uint32)
+    coffs = np.asarray(coffs, dtype=np.uint64)
+    rows = np.repeat(np.arange(len(coffs) - 1), np.diff(coffs).astype(np.int64))
+    pos = np.arange(committee.size, dtype=np.int64) - coffs[rows].astype(np.int64)
+    keep = (committee >= lo) & (committee < hi)
+    if keep_out_of_range:
+        keep |= committee >= nval_global
+    counts = np.bincount(rows[keep], minlength=len(coffs) - 1)
+    out_offs = np.zeros(len(coffs), dtype=np.uint64)
+    out_offs[1:] = np.cumsum(counts)
+    out = committee[keep]
+    return (out if out.size else np.zeros(1, np.uint32)), out_offs, pos[keep].astype(np.uint32)
+
+
 class HipEpochKernels:
     """The product kernels: the C-ABI entry points of libprysm_hip.so (include/prysm_hip.h)."""
 
@@ -68,8 +86,12 @@ class DeviceEpoch:
         self.total_deposit = T(inst["total_deposit"].view(np.int64))
         self.bits = T(np.concatenate([inst["bits"], np.zeros(16, np.uint8)]))
         self.boffs = T(inst["boffs"].view(np.int64))
-        self.committee = T(inst["committee"].view(np.int32))
-        self.coffs = T(inst["coffs"].view(np.int64))
+        committee, coffs, cpos = inst["committee"], inst["coffs"], None
+        if world > 1:  # this rank's members only (the crosslink gathers then shrink with N)
+            committee, coffs, cpos = local_committees(committee, coffs, lo, hi, N, rank == 0)
+        self.committee = T(committee.view(np.int32))
+        self.coffs = T(coffs.view(np.int64))
+        self.cpos = T(cpos.view(np.int32)) if cpos is not None else None
         self.att_comm = T(inst["att_comm"].view(np.int32))
         self.att_shard = T(inst["att_shard"].view(np.int32))
         self.rec_dynasty = T(inst["rec_dynasty"].view(np.int64))
@@ -102,6 +124,7 @@ class DeviceEpoch:
         b.max_inst_bytes = inst["max_inst_bytes"]
         b.pop_rank, b.pop_world = rank, world
         b.committee, b.coffs = self.committee.data_ptr(), self.coffs.data_ptr()
+        b.cpos = self.cpos.data_ptr() if self.cpos is not None else None
         b.att_comm, b.att_shard = self.att_comm.data_ptr(), self.att_shard.data_ptr()
         b.nrec, b.rec_dynasty, b.winner = nrec, self.rec_dynasty.data_ptr(), self.winner.data_ptr()
         b.act_mask, b.blk_cnt, b.act_list = (self.act_mask.data_ptr(), self.blk_cnt.data_ptr(),

@@ -53,6 +53,7 @@ class _View:
         self.winner = _arr(b.winner, np.uint32, B * self.nrec).reshape(B, self.nrec)
         self.coffs = _arr(b.coffs, U64, int(self._ncomm()) + 1)
         self.committee = _arr(b.committee, np.uint32, int(self.coffs[-1]) if self.coffs.size else 0)
+        self.cpos = _arr(b.cpos, np.uint32, self.committee.size) if b.cpos else None
 
     def _ncomm(self):
         if not self.natt:
@@ -106,15 +107,17 @@ class NumpyEpochKernels:
                     v.winner[i] = 0xFFFFFFFF
                 for a in range(v.natt if b.committee else 0):
                     c = int(v.att_comm[i, a])
-                    mem = v.committee[int(v.coffs[c]):int(v.coffs[c + 1])].astype(np.int64)
+                    lo_, hi_ = int(v.coffs[c]), int(v.coffs[c + 1])
+                    mem = v.committee[lo_:hi_].astype(np.int64)
+                    # bit position: index in the full committee (rank-local rows carry cpos)
+                    pos = v.cpos[lo_:hi_].astype(np.int64) if v.cpos is not None else np.arange(mem.size)
                     bf = v.bf(i, a)
                     err = 0
                     if mem.size and mem.max() >= v.N:
                         err |= 1
-                    if mem.size > 8 * bf.size:
+                    if pos.size and pos.max() >= 8 * bf.size:
                         err |= 2
                     own = (mem >= v.off) & (mem < v.off + v.n) & (mem < v.N)
-                    pos = np.arange(mem.size)
                     bal = np.zeros(mem.size, dtype=U64)
                     bal[own] = v.bal[i, mem[own] - v.off]
                     voted = np.zeros(mem.size, dtype=bool)
