@@ -90,3 +90,34 @@ def test_long_messages_host_route_and_gpu_route_agree(thr):
             assert got == [ref.sum512(m)[:ob] for m in msgs]
         only_long = [m for m in msgs if len(m) >= 1000]
         assert _lib.blake2b512_batch(only_long, 64) == [ref.sum512(m) for m in only_long]
+
+
+def test_batch_api_thread_safe():
+    """The host-pointer C ABI is thread-safe (per-device mutex, library stream): eight Python
+    threads (ctypes releases the GIL) hash different batches concurrently, mixing the GPU
+    route and the host serial route; every digest is still right."""
+    import threading
+
+    rng = np.random.default_rng(11)
+    batches = []
+    for t in range(8):
+        lens = rng.integers(0, 3000, size=200).tolist() + ([70000] if t % 2 else [])
+        batches.append([rng.integers(0, 256, size=l, dtype=np.uint8).tobytes() for l in lens])
+    out = [None] * len(batches)
+    errs = []
+
+    def work(i):
+        try:
+            for _ in range(3):
+                out[i] = _lib.blake2b512_batch(batches[i], out_bytes=64)
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(batches))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for msgs, got in zip(batches, out):
+        assert got == [ref.sum512(m) for m in msgs]
