@@ -80,7 +80,6 @@ def parse():
     p.add_argument("--cpu-replay-blocks", type=int, default=520,
                    help="blocks of the replay chain the CPU baseline (oracle/replay.py) processes (~8 s)")
     p.add_argument("--no-epoch", action="store_true")
-    p.add_argument("--no-hash", action="store_true")
     p.add_argument("--no-replay", action="store_true")
     p.add_argument("--replay-blocks", type=int, default=10000,
                    help="blocks per sync replay (BASELINE configs[4]; 65,536 validators)")
@@ -100,16 +99,16 @@ HASH_KERNEL = "pz_b2b_fixed_persistent_kernel"
 CPU_SAMPLE_S = 8.0  # seconds of CPU work per cpu_baseline leg (three legs: ~25 s in all)
 
 
-def epoch_leg(args, torch, dist, dev, rank, world):
+def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseline=True):
     """BASELINE configs[2] (N=1: 65,536 validators, B instances per step) / configs[3]
     (N>1: 1,048,576 validators sharded over the ranks, RCCL all-reduce of the sums)."""
     from prysm_amd import casper, synth
     from prysm_amd.epoch import DeviceEpoch
 
-    nval = args.epoch_validators or (65536 if world == 1 else 1 << 20)
+    nval = nval or args.epoch_validators or (65536 if world == 1 else 1 << 20)
     # throughput mode: 16.7 M validator-epochs per GPU per step at every N (weak scaling; at
     # N > 1 each rank holds 1/N of every 1M-validator instance and B grows with N)
-    ninst = args.epoch_instances or max(1, (1 << 24) * world // nval)
+    ninst = ninst or args.epoch_instances or max(1, (1 << 24) * world // nval)
     seed_a = b"A" + bytes(31)  # common.Hash{'A'} (casper/sharding_test.go:57)
     shuffled = casper.shuffle_indices(seed_a, np.arange(nval, dtype=np.uint32))
     inst = synth.epoch_batch(nval, ninst, seed=3, shuffled=shuffled)
@@ -149,7 +148,7 @@ def epoch_leg(args, torch, dist, dev, rank, world):
         "scaling": "weak",
         "config": {"workload": "stateRecalc data-parallel part: crosslink tallies+winners, attester "
                                "popcount, CalculateRewards, next-cycle balance (BASELINE configs[%d])"
-                               % (2 if world == 1 else 3),
+                               % (2 if (world == 1 and nval != 1 << 20) else 3),
                    "validators": nval, "instances_per_step": ninst, "attestations_per_instance": inst["natt"],
                    "parallelism": "validator-shard x%d + RCCL all-reduce" % world if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
@@ -160,7 +159,7 @@ def epoch_leg(args, torch, dist, dev, rank, world):
                      "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": local_units * EPOCH_BYTES_PER_VALIDATOR},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and baseline:
         out["cpu_baseline"] = epoch_cpu_baseline(inst)
     return out
 
@@ -357,6 +356,11 @@ def main():
         wall = max_over_ranks(wall, torch, dist, dev)
 
     epoch = None if args.no_epoch else epoch_leg(args, torch, dist, dev, rank, world)
+    # configs[3]'s instance size (1,048,576 validators) on this one GPU: the N = 1 point of
+    # the 1/2/4/8-GPU series that the N > 1 epoch leg runs (16 instances per GPU per step)
+    epoch_1m = None
+    if epoch is not None and world == 1 and not args.epoch_validators:
+        epoch_1m = epoch_leg(args, torch, dist, dev, rank, world, nval=1 << 20, ninst=16, baseline=False)
     replay = None if args.no_replay else replay_leg(args, torch, dist, dev, rank, world)
 
     if rank == 0:
@@ -409,6 +413,8 @@ def main():
                     n, bool(np.array_equal(gpu, digests)))
         if epoch is not None:
             line["epoch"] = epoch
+        if epoch_1m is not None:
+            line["epoch_1m_single_gpu"] = epoch_1m
         if replay is not None:
             line["replay"] = replay
         print(json.dumps(line), flush=True)
