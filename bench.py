@@ -81,6 +81,7 @@ def parse():
                    help="blocks of the replay chain the CPU baseline (oracle/replay.py) processes (~8 s)")
     p.add_argument("--no-epoch", action="store_true")
     p.add_argument("--no-replay", action="store_true")
+    p.add_argument("--no-wire", action="store_true")
     p.add_argument("--replay-blocks", type=int, default=10000,
                    help="blocks per sync replay (BASELINE configs[4]; 65,536 validators)")
     p.add_argument("--epoch-validators", type=int, default=0,
@@ -175,6 +176,89 @@ def epoch_cpu_baseline(inst):
     except Exception as e:  # pragma: no cover
         return {"value": None, "unit": "validator-epochs/s", "cores": 0, "kind": "port",
                 "sample": "unavailable: %s" % e}
+
+
+WIRE_KERNELS = ("pz_wire_val_size_kernel", "pz_wire_scan_kernel", "pz_wire_val_write_kernel")
+
+
+def wire_leg(args, torch, dist, dev, rank, world):
+    """the CrystallizedState's ValidatorRecords proto3-encoded on the
+    device from the resident SoA columns (pz_dev_wire_validators).  One step encodes 16
+    states of 1,048,576 validators (configs[3]'s size; the columns of the 16 states back to
+    back, which is the same bytes as 16 separate calls).  Algorithmic bytes per record: the
+    three u64 columns read once (24 B) + the encoded record written once."""
+    from prysm_amd import _lib, pb, wire
+
+    nval, nst = 1 << 20, 16
+    n = nval * nst
+    rng = np.random.default_rng(7 + rank)
+    bal = rng.integers(16, 49, size=n, dtype=np.uint64)
+    start = np.zeros(n, dtype=np.uint64)
+    end = np.full(n, 9999999999999999999, dtype=np.uint64)
+    cols_t = [torch.from_numpy(a.view(np.int64)).to(dev) for a in (bal, start, end)]
+    bound = int(_lib.lib.dll.pz_wire_validators_bound(n, 0))
+    d_out = torch.empty(bound, dtype=torch.uint8, device=dev)
+    d_scr = torch.empty(int(_lib.lib.dll.pz_wire_scratch_bytes(n)) // 8, dtype=torch.int64, device=dev)
+    d_tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    cols = _lib.ValidatorCols(None, None, None, None, None, None, *[t.data_ptr() for t in cols_t])
+    stream = torch.cuda.current_stream(dev)
+    sh = ctypes.c_void_p(stream.cuda_stream)
+
+    def step():
+        _lib.lib.call("pz_dev_wire_validators", ctypes.byref(cols), n, 11, d_out.data_ptr(), None,
+                      d_scr.data_ptr(), d_tot.data_ptr(), sh)
+
+    for _ in range(args.warmup + 20):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        step()
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    step_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    if world > 1:
+        wall = max_over_ranks(wall, torch, dist, dev)
+    total = int(d_tot.item())
+    alg = n * 24 + total
+    out = {
+        "metric": "ValidatorRecords proto3-encoded/s",
+        "value": n * world * args.steps / wall,
+        "unit": "records/s",
+        "ms_per_step": wall / args.steps * 1e3,
+        "scaling": "weak",
+        "config": {"workload": "CrystallizedState.validators (field 11) encoding of %d states x %d validators "
+                               "(configs[3] size) from device-resident balance/start/end columns" % (nst, nval),
+                   "records_per_gpu": n, "encoded_bytes_per_gpu": total,
+                   "parallelism": "independent states per rank" if world > 1 else "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": alg / (step_ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": alg / (step_ms * 1e-3) / HBM_PEAK, "traffic": None,
+                     "kernel": "pz_wire_val_kernel (device time of the step, tile-status memset included)", "step_device_ms": step_ms,
+                     "algorithmic_bytes_per_launch": alg},
+    }
+    if rank == 0 and world == 1:
+        # the checker: the first state's bytes against the C port, which is also the baseline
+        from oracle import cport
+        one = pb.Validators(nval, balance=bal[:nval], start_dynasty=start[:nval], end_dynasty=end[:nval])
+        want = cport.wire_validators(one)
+        got = d_out[:len(want)].cpu().numpy().tobytes()
+        out["parity"] = "byte-exact vs the C port on the first state's %d bytes: %s" % (len(want), got == want)
+        if not args.no_cpu_baseline:
+            reps, dt = cport.wire_validators_timed(one, min_seconds=CPU_SAMPLE_S / 2)
+            out["cpu_baseline"] = {"value": reps * nval / dt, "unit": "records/s", "cores": 1, "kind": "port",
+                                   "sample": "%d encodings of one %d-validator state (AoS records, size + marshal "
+                                             "pass, 1 thread, oracle/c/wire_ref.c), %.2f s" % (reps, nval, dt)}
+    return out
 
 
 def replay_leg(args, torch, dist, dev, rank, world):
@@ -362,6 +446,7 @@ def main():
     if epoch is not None and world == 1 and not args.epoch_validators:
         epoch_1m = epoch_leg(args, torch, dist, dev, rank, world, nval=1 << 20, ninst=16, baseline=False)
     replay = None if args.no_replay else replay_leg(args, torch, dist, dev, rank, world)
+    wire_out = None if args.no_wire else wire_leg(args, torch, dist, dev, rank, world)
 
     if rank == 0:
         total = n * world * args.steps
@@ -417,6 +502,8 @@ def main():
             line["epoch_1m_single_gpu"] = epoch_1m
         if replay is not None:
             line["replay"] = replay
+        if wire_out is not None:
+            line["wire"] = wire_out
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

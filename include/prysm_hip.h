@@ -83,6 +83,38 @@ int pz_dev_blake2b512_batch(const uint8_t* d_msgs, const uint64_t* d_offsets, ui
 int pz_dev_blake2b512_fixed(const uint8_t* d_msgs, uint64_t stride, uint64_t len, uint64_t n,
                             uint8_t* d_out, uint32_t out_bytes, void* stream);
 
+/* ---- a2 / §8f: proto3 encoding of ValidatorRecords on the device -------------------
+ * Replaces the validators span of gogo proto.Marshal(CrystallizedState) at
+ * types/state.go:141 (Marshal) and :240 (Hash); record layout messages.pb.go:803-809.
+ * Columns are SoA; a NULL scalar column means 0 in every record (omitted, as proto3 omits
+ * zero scalars); a bytes column is CSR (data + offsets[n+1]), NULL offsets = all empty.
+ * field_num > 0 frames every record as that length-delimited field (11 = the
+ * CrystallizedState's `validators`); 0 writes bare records (then offsets delimit them).
+ * offsets (optional, n+1) receive each record's start in out; offsets[n] = total length. */
+typedef struct pz_validator_cols {
+  const uint64_t* public_key;              /* field 1 */
+  const uint64_t* withdrawal_shard;        /* field 2 */
+  const uint8_t*  withdrawal_address;      /* field 3 (bytes) */
+  const uint64_t* withdrawal_address_offs;
+  const uint8_t*  randao_commitment;       /* field 4 (bytes) */
+  const uint64_t* randao_commitment_offs;
+  const uint64_t* balance;                 /* field 5 */
+  const uint64_t* start_dynasty;           /* field 6 */
+  const uint64_t* end_dynasty;             /* field 7 */
+} pz_validator_cols;
+/* Upper bound of the encoded length (bytes_total = both bytes columns' total length). */
+uint64_t pz_wire_validators_bound(uint64_t n, uint64_t bytes_total);
+/* Device scratch the pz_dev_ form needs for n records. */
+uint64_t pz_wire_scratch_bytes(uint64_t n);
+/* Host pointers, synchronous.  PZ_ERANGE (nothing written) when the encoding exceeds cap;
+ * *len always receives the encoded length. */
+int pz_wire_validators(const pz_validator_cols* v, uint64_t n, uint32_t field_num, uint8_t* out,
+                       uint64_t cap, uint64_t* offsets, uint64_t* len);
+/* Device pointers (columns included), caller's stream.  d_out must hold
+ * pz_wire_validators_bound(...) bytes; *d_total (device) receives the length. */
+int pz_dev_wire_validators(const pz_validator_cols* v, uint64_t n, uint32_t field_num, uint8_t* d_out,
+                           uint64_t* d_offsets, void* d_scratch, uint64_t* d_total, void* stream);
+
 /* ---- T/R: validator-set filters (casper/validator.go) ------------------------------- */
 #define PZ_KIND_ACTIVE 0  /* start <= dyn < end        casper/validator.go:45-53 */
 #define PZ_KIND_EXITED 1  /* start <  dyn && end <= dyn casper/validator.go:57-65 */

@@ -102,3 +102,67 @@ def epoch_instance_timed(inst, b, min_seconds=8.0, max_reps=100000):
         return reps, time.perf_counter() - t0
     finally:
         d.oracle_epoch_free(e)
+
+
+def _wire_build(v):
+    """pb.Validators -> AoS records behind a pointer array (oracle/c/wire_ref.c)."""
+    d = dll()
+    vp, u64, sz, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32
+    d.oracle_wire_build.restype = vp
+    d.oracle_wire_build.argtypes = [vp] * 9 + [sz]
+    d.oracle_wire_free.argtypes = [vp]
+    d.oracle_wire_validators.restype = u64
+    d.oracle_wire_validators.argtypes = [vp, u32, vp, u64]
+    n = len(v)
+    keep = []
+
+    def P(a, dt):
+        if a is None:
+            return None
+        a = np.ascontiguousarray(a, dtype=dt)
+        keep.append(a)
+        return a.ctypes.data if a.size else None
+
+    def csr(blobs):
+        if blobs is None:
+            return None, None
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum([len(b) for b in blobs], dtype=np.uint64)
+        return P(np.frombuffer(b"".join(blobs) + b"\0", dtype=np.uint8), np.uint8), P(offs, np.uint64)
+
+    wa, wao = csr(v.withdrawal_address)
+    rc, rco = csr(v.randao_commitment)
+    h = d.oracle_wire_build(P(v.public_key, np.uint64), P(v.withdrawal_shard, np.uint64), wa, wao, rc, rco,
+                            P(v.balance, np.uint64), P(v.start_dynasty, np.uint64), P(v.end_dynasty, np.uint64), n)
+    return d, h
+
+
+def wire_validators(v, field_num=11):
+    """The CrystallizedState.validators bytes of ``v`` (pb.Validators), field_num <= 15."""
+    d, h = _wire_build(v)
+    try:
+        total = d.oracle_wire_validators(h, field_num, None, 0)
+        out = np.empty(max(total, 1), dtype=np.uint8)
+        d.oracle_wire_validators(h, field_num, out.ctypes.data, total)
+        return out[:total].tobytes()
+    finally:
+        d.oracle_wire_free(h)
+
+
+def wire_validators_timed(v, min_seconds=8.0, max_reps=100000):
+    """Time repeated encodings of ``v`` (size pass + write pass, like proto.Marshal); returns
+    (reps, seconds).  Building the AoS records is not timed."""
+    import time
+    d, h = _wire_build(v)
+    try:
+        total = d.oracle_wire_validators(h, 11, None, 0)
+        out = np.empty(max(total, 1), dtype=np.uint8)
+        reps = 0
+        t0 = time.perf_counter()
+        while reps < max_reps and (reps == 0 or time.perf_counter() - t0 < min_seconds):
+            buf = np.empty(max(total, 1), dtype=np.uint8) if reps % 2 else out  # Marshal allocates
+            d.oracle_wire_validators(h, 11, buf.ctypes.data, total)
+            reps += 1
+        return reps, time.perf_counter() - t0
+    finally:
+        d.oracle_wire_free(h)

@@ -2,7 +2,7 @@
 
 Restates ``/root/reference/proto/beacon/p2p/v1/messages.proto:37-125`` as a
 FileDescriptorProto built field by field, so Google's protobuf runtime serves as an
-encoder that is independent of the product's own (``prysm_amd/csrc/host/wire.cpp``).
+encoder that is independent of the product's own (``prysm_amd/wire.py``, ``prysm_amd/csrc/wire.hip``).
 Field numbers, types and packing match the golang struct tags in
 ``messages.pb.go:224-232`` (BeaconBlock), ``:432-444`` (CrystallizedState), ``:559``
 (ShardAndCommitteeArray), ``:673-674`` (ShardAndCommittee, packed committee),

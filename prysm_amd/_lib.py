@@ -78,6 +78,10 @@ SIGNATURES = {
     "pz_chain_vote_totals": [vp, vp, vp, u64, c_u64p],
     "pz_dev_vote_tally": [vp, vp],
     "pz_vote_tally": [vp, vp, u64, vp, vp, vp, u64, vp, vp, u64, vp, u64, vp, u64, u64, vp],
+    "pz_wire_validators_bound": [u64, u64],
+    "pz_wire_scratch_bytes": [u64],
+    "pz_wire_validators": [vp, u64, u32, vp, u64, vp, c_u64p],
+    "pz_dev_wire_validators": [vp, u64, u32, vp, vp, vp, vp, vp],
 }
 
 
@@ -104,10 +108,20 @@ class VoteBatch(ctypes.Structure):
     ]
 
 
+class ValidatorCols(ctypes.Structure):
+    """Mirror of ``pz_validator_cols`` (include/prysm_hip.h)."""
+    _fields_ = [
+        ("public_key", vp), ("withdrawal_shard", vp), ("withdrawal_address", vp),
+        ("withdrawal_address_offs", vp), ("randao_commitment", vp), ("randao_commitment_offs", vp),
+        ("balance", vp), ("start_dynasty", vp), ("end_dynasty", vp),
+    ]
+
+
 SCAL_POP, SCAL_NACT, SCAL_ERR_XL, SCAL_ERR_RWD, SCAL_APPLIED, SCAL_NEXT_BAL, SCAL_MAXIDX1 = range(7)
 SCAL_COUNT = 8
 KIND_ACTIVE, KIND_EXITED, KIND_QUEUED = 0, 1, 2
-_RESTYPES = {"pz_last_error": ctypes.c_char_p, "pz_chain_free": None, "pz_set_serial_threshold": u64}
+_RESTYPES = {"pz_last_error": ctypes.c_char_p, "pz_chain_free": None, "pz_set_serial_threshold": u64,
+             "pz_wire_validators_bound": u64, "pz_wire_scratch_bytes": u64}
 SERIAL_DEFAULT = 65536        # the library's default serial threshold (bytes)
 SERIAL_ON_GPU = (1 << 64) - 1  # pz_set_serial_threshold value that keeps every message on the GPU
 

@@ -30,6 +30,7 @@
 #include "epoch.h"
 #include "runtime.h"
 #include "votes.h"
+#include "wire.h"
 
 namespace pz {
 namespace chain {
@@ -293,8 +294,13 @@ struct Engine {
   bool poisoned = false;
   // validators (shared by every CrystallizedState, like the Go pointer slice)
   DevArr<uint64_t> balance, start, end;
-  std::vector<uint64_t> h_balance, h_start, h_end;
-  bool host_balance_valid = true;
+  std::vector<uint64_t> h_balance, h_start, h_end;  // genesis values (uploaded once)
+  // field 11 of the CrystallizedState, encoded on the device from the resident validator
+  // arrays (wire.hip); re-encoded only after rewards changed a balance
+  std::string val_enc;
+  bool val_enc_valid = false;
+  DevArr<uint8_t> w_out;
+  DevArr<uint64_t> w_scratch, w_total;
   // ShardAndCommitteesForSlots (immutable in this reference: stateRecalc copies it)
   DevArr<uint32_t> committee;
   DevArr<uint64_t> coffs;
@@ -719,7 +725,7 @@ static uint64_t epoch_finish(Engine& g, CState& C, const std::vector<AttP>& pend
       xl[s].slot = block_slot;
     }
   }
-  if (scal[kApplied]) g.host_balance_valid = false;
+  if (scal[kApplied]) g.val_enc_valid = false;
   return scal[kNextBal];
 }
 
@@ -784,11 +790,29 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
 }
 
 // ---- serialization of the states (state roots) --------------------------------------------
-static void sync_host_balance(Engine& g) {
-  if (g.host_balance_valid) return;
-  hchk(hipMemcpyAsync(g.h_balance.data(), g.balance.p, g.nval * 8, hipMemcpyDeviceToHost, g.s), "D2H");
+static const std::string& validators_enc(Engine& g) {
+  if (g.val_enc_valid) return g.val_enc;
+  pz_validator_cols v{};
+  v.balance = g.balance.p;
+  v.start_dynasty = g.start.p;
+  v.end_dynasty = g.end.p;
+  WireValArgs a;
+  check(wire_val_args(&v, g.nval, 11, &a));
+  const uint64_t bound = pz_wire_validators_bound(g.nval, 0);
+  check(g.w_out.alloc(bound));
+  check(g.w_scratch.alloc(wire_tiles(g.nval) + 1));
+  check(g.w_total.alloc(1));
+  a.out = g.w_out.p;
+  a.total = g.w_total.p;
+  hchk(launch_wire_validators(a, g.w_scratch.p, g.s), "pz_wire_val_kernel");
+  uint64_t total = 0;
+  hchk(hipMemcpyAsync(&total, g.w_total.p, 8, hipMemcpyDeviceToHost, g.s), "D2H");
   hchk(hipStreamSynchronize(g.s), "sync");
-  g.host_balance_valid = true;
+  g.val_enc.resize(total);
+  hchk(hipMemcpyAsync(&g.val_enc[0], g.w_out.p, total, hipMemcpyDeviceToHost, g.s), "D2H");
+  hchk(hipStreamSynchronize(g.s), "sync");
+  g.val_enc_valid = true;
+  return g.val_enc;
 }
 
 static std::string encode_active(const AState& A) {  // messages.proto:94-97
@@ -799,9 +823,9 @@ static std::string encode_active(const AState& A) {  // messages.proto:94-97
 }
 
 static std::string encode_crystallized(Engine& g, const CState& C) {  // messages.proto:59-72
-  sync_host_balance(g);
+  const std::string& venc = validators_enc(g);
   std::string o;
-  o.reserve(g.nval * 18 + g.arrays_enc.size() + 16384);
+  o.reserve(venc.size() + g.arrays_enc.size() + 16384);
   put_u(o, 1, C.lsr);
   put_u(o, 2, C.streak);
   put_u(o, 3, C.jslot);
@@ -818,13 +842,7 @@ static std::string encode_crystallized(Engine& g, const CState& C) {  // message
     put_u(r, 3, x.slot);
     put_msg(o, 10, (const uint8_t*)r.data(), r.size());
   }
-  for (uint64_t i = 0; i < g.nval; ++i) {  // ValidatorRecord (public key / shard / bytes all zero)
-    r.clear();
-    put_u(r, 5, g.h_balance[i]);
-    put_u(r, 6, g.h_start[i]);
-    put_u(r, 7, g.h_end[i]);
-    put_msg(o, 11, (const uint8_t*)r.data(), r.size());
-  }
+  o += venc;  // ValidatorRecords (public key / shard / bytes all zero)
   o += g.arrays_enc;
   return o;
 }

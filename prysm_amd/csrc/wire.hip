@@ -1,0 +1,511 @@
+// proto3 encoding of ValidatorRecord columns on the device.
+//
+// Replaces the validators span of gogo `proto.Marshal(CrystallizedState)` at
+// types/state.go:141 (Marshal) and :240 (Hash); the record is messages.pb.go:803-809
+// (public_key 1, withdrawal_shard 2, withdrawal_address 3, randao_commitment 4, balance 5,
+// start_dynasty 6, end_dynasty 7).  proto3 rules: ascending field order, zero scalars and
+// empty bytes omitted, every record framed as a length-delimited repeated field.
+//
+// One launch (after a small memset of the tile-status words).  A workgroup takes a tile of
+// records, derives their encoded sizes, scans them, and learns the tile's output offset by a
+// decoupled look-back over its predecessors' published sizes.  Then it writes the tile's
+// bytes.  This is HBM-bound byte work, with no MFMA, and the columns are read once.
+//  * Scalar-only records (no bytes fields; the chain's CrystallizedState): 3,072 records per
+//    tile, streamed in sub-tiles of 1,024 with coalesced column loads.  The tile's encoding
+//    is built in a 64 KB LDS stage and stored with aligned dword stores.  A tile larger than the stage (records near the 61-byte maximum)
+//    writes lane by lane instead.
+//  * Records with bytes fields: 2,048 records per tile, sizes first, then (after the
+//    look-back) a second read of the records, written lane by lane straight to HBM.
+#include "wire.h"
+
+#include <hip/hip_runtime.h>
+
+
+#include "runtime.h"
+
+namespace pz {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kPer = 4, kSubRecs = kThreads * kPer;  // scalar kernel: sub-tiles of 1,024 records
+constexpr int kSub = 3, kTileRecs = kSub * kSubRecs;  // 3,072 records (one ticket) per tile
+constexpr int kStageBytes = 64 * 1024;                // the whole tile's encoding (21 B per record)
+constexpr int kBytesSub = 8, kBytesTileRecs = kBytesSub * kThreads;  // bytes-field kernel: 2,048
+
+__device__ __forceinline__ uint32_t vlen(uint64_t x) { return (uint32_t)((70 - __clzll(x | 1)) / 7); }
+
+__device__ __forceinline__ uint8_t* put_varint(uint8_t* p, uint64_t x) {
+  while (x >= 0x80) {
+    *p++ = (uint8_t)(x | 0x80);
+    x >>= 7;
+  }
+  *p++ = (uint8_t)x;
+  return p;
+}
+
+__device__ __forceinline__ uint32_t frame_size(const WireValArgs& a, uint64_t body) {
+  return (uint32_t)(a.field ? a.tag_len + vlen(body) + body : body);
+}
+
+__device__ __forceinline__ uint8_t* put_frame(const WireValArgs& a, uint8_t* p, uint64_t body) {
+  if (a.field) {
+    p = put_varint(p, ((uint64_t)a.field << 3) | 2);
+    p = put_varint(p, body);
+  }
+  return p;
+}
+
+// ---- scalar-only records -------------------------------------------------------------------
+struct SRec {
+  uint64_t v[5];  // fields 1, 2, 5, 6, 7
+};
+
+__device__ __forceinline__ uint32_t srec_body(const SRec& r) {
+  uint32_t body = 0;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) body += r.v[k] ? 1 + vlen(r.v[k]) : 0;
+  return body;
+}
+
+__device__ __forceinline__ uint8_t* put_srec(const WireValArgs& a, const SRec& r, uint32_t body, uint8_t* p) {
+  p = put_frame(a, p, body);
+  const uint8_t tags[5] = {1 << 3, 2 << 3, 5 << 3, 6 << 3, 7 << 3};
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    if (r.v[k]) {
+      *p++ = tags[k];
+      p = put_varint(p, r.v[k]);
+    }
+  return p;
+}
+
+// ---- records with bytes fields ---------------------------------------------------------------
+struct Rec {
+  uint64_t v[5];    // fields 1, 2, 5, 6, 7
+  uint64_t b0, b1;  // byte offsets of fields 3, 4
+  uint64_t l0, l1;  // their lengths
+  uint64_t body, size;
+};
+
+__device__ __forceinline__ void load_rec(const WireValArgs& a, uint64_t i, Rec& r) {
+  uint64_t body = 0;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    r.v[k] = a.col[k] ? a.col[k][i] : 0;
+    body += r.v[k] ? 1 + vlen(r.v[k]) : 0;
+  }
+  r.b0 = r.l0 = r.b1 = r.l1 = 0;
+  if (a.wa_offs) {
+    r.b0 = a.wa_offs[i];
+    r.l0 = a.wa_offs[i + 1] - r.b0;
+    body += r.l0 ? 1 + vlen(r.l0) + r.l0 : 0;
+  }
+  if (a.rc_offs) {
+    r.b1 = a.rc_offs[i];
+    r.l1 = a.rc_offs[i + 1] - r.b1;
+    body += r.l1 ? 1 + vlen(r.l1) + r.l1 : 0;
+  }
+  r.body = body;
+  r.size = a.field ? a.tag_len + vlen(body) + body : body;
+}
+
+__device__ __forceinline__ uint8_t* put_bytes(uint8_t* p, uint32_t tag, const uint8_t* src, uint64_t len) {
+  if (!len) return p;
+  *p++ = (uint8_t)tag;
+  p = put_varint(p, len);
+  for (uint64_t j = 0; j < len; ++j) p[j] = src[j];
+  return p + len;
+}
+
+__device__ __forceinline__ void put_rec(const WireValArgs& a, const Rec& r, uint8_t* p) {
+  p = put_frame(a, p, r.body);
+  if (r.v[0]) { *p++ = 1 << 3; p = put_varint(p, r.v[0]); }
+  if (r.v[1]) { *p++ = 2 << 3; p = put_varint(p, r.v[1]); }
+  p = put_bytes(p, (3 << 3) | 2, a.wa + r.b0, r.l0);
+  p = put_bytes(p, (4 << 3) | 2, a.rc + r.b1, r.l1);
+  if (r.v[2]) { *p++ = 5 << 3; p = put_varint(p, r.v[2]); }
+  if (r.v[3]) { *p++ = 6 << 3; p = put_varint(p, r.v[3]); }
+  if (r.v[4]) { *p++ = 7 << 3; p = put_varint(p, r.v[4]); }
+}
+
+// ---- tile offsets ----------------------------------------------------------------------------
+// Exclusive scan of one value per thread over the 256-thread block; returns the block total.
+__device__ __forceinline__ uint64_t block_scan(uint64_t x, uint64_t* excl, uint64_t* lds4) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint64_t inc = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += y;
+  }
+  if (lane == 63) lds4[wid] = inc;
+  __syncthreads();
+  uint64_t before = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; ++w) {
+    before += w < wid ? lds4[w] : 0;
+    total += lds4[w];
+  }
+  *excl = before + inc - x;
+  return total;
+}
+
+// Tile status words: flag in the top two bits, value below.  A tile publishes its aggregate
+// (A) as soon as it knows its size and its inclusive prefix (P) after the look-back.  Flag and
+// value travel in one 64-bit word, so relaxed agent-scope atomics suffice (no fence, which on
+// gfx950 would write back L2).
+constexpr uint64_t kFlagA = 1ull << 62, kFlagP = 2ull << 62, kVal = kFlagA - 1;
+
+__device__ __forceinline__ uint64_t ld_status(uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Decoupled look-back by the whole workgroup: 256 threads x 4 loads watch the 1,024 nearest
+// predecessors at once, so one round trip usually reaches a published inclusive prefix even
+// when every resident tile started together (a wave-wide window walked 64 tiles per round
+// trip, ~8 trips per dispatch round).  Returns the exclusive prefix of `tile` to every thread.
+constexpr int kLbPer = 4, kLbWin = kThreads * kLbPer;
+__device__ uint64_t lookback_block(uint64_t* status, uint64_t tile, uint64_t* lds, uint32_t* lds_first) {
+  uint64_t prefix = 0;
+  int64_t j = (int64_t)tile - 1;
+  while (true) {
+    uint64_t w[kLbPer];
+#pragma unroll
+    for (int q = 0; q < kLbPer; ++q) {
+      const int64_t idx = j - (threadIdx.x * kLbPer + q);
+      w[q] = idx >= 0 ? ld_status(status + idx) : kFlagP;  // before tile 0: prefix 0
+    }
+#pragma unroll
+    for (int q = 0; q < kLbPer; ++q) {
+      const int64_t idx = j - (threadIdx.x * kLbPer + q);
+      while (!(w[q] >> 62)) {
+        __builtin_amdgcn_s_sleep(1);
+        w[q] = ld_status(status + idx);
+      }
+    }
+    // nearest published inclusive prefix (distance d = threadIdx.x * kLbPer + q)
+    if (threadIdx.x == 0) *lds_first = kLbWin;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kLbPer; ++q)
+      if ((w[q] >> 62) == 2) {
+        atomicMin(lds_first, threadIdx.x * kLbPer + q);
+        break;
+      }
+    __syncthreads();
+    const uint32_t first = *lds_first;
+    uint64_t part = 0;
+#pragma unroll
+    for (int q = 0; q < kLbPer; ++q)
+      if (threadIdx.x * kLbPer + q <= first) part += w[q] & kVal;
+    uint64_t e;
+    prefix += block_scan(part, &e, lds);
+    __syncthreads();
+    if (first < (uint32_t)kLbWin) return prefix;
+    j -= kLbWin;
+  }
+}
+
+// Store stage[0..span) at out+base with dword stores: bytes up to the first 4-aligned
+// address, then dwords (each funnel-shifted out of two aligned LDS words), then the tail.
+__device__ __forceinline__ void store_stage(uint8_t* out, uint64_t base, const uint32_t* stage, uint32_t span) {
+  const uint8_t* st = reinterpret_cast<const uint8_t*>(stage);
+  const uint32_t lead = (uint32_t)((4 - (base & 3)) & 3);
+  const uint32_t head = lead < span ? lead : span;
+  if (threadIdx.x < head) out[base + threadIdx.x] = st[threadIdx.x];
+  const uint32_t nd = (span - head) >> 2;
+  uint32_t* dst = reinterpret_cast<uint32_t*>(out + base + head);
+  for (uint32_t j = threadIdx.x; j < nd; j += kThreads) {
+    const uint32_t w = head + 4 * j;  // byte position in the stage
+    dst[j] = head ? __builtin_amdgcn_alignbyte(stage[(w >> 2) + 1], stage[w >> 2], head) : stage[w >> 2];
+  }
+  const uint32_t t0 = head + 4 * nd;
+  if (t0 + threadIdx.x < span) out[base + t0 + threadIdx.x] = st[t0 + threadIdx.x];
+}
+
+// Record (j, p, t) of a tile = tile*kTileRecs + j*kSubRecs + p*kThreads + t: every column load
+// of a wave reads 512 contiguous bytes.
+__device__ __forceinline__ void load_sub(const WireValArgs& a, uint64_t first, SRec (&r)[kPer]) {
+#pragma unroll
+  for (int p = 0; p < kPer; ++p) {
+    const uint64_t i = first + p * kThreads + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) r[p].v[k] = (a.col[k] && i < a.n) ? a.col[k][i] : 0;
+  }
+}
+
+// Sizes of one sub-tile's records and their offsets inside the sub-tile (record order), from
+// ONE block scan: a record is at most 61 bytes and a sub-tile row p of 256 records at most
+// 15,616, so the four rows' sizes travel as four 16-bit lanes of one u64.
+__device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t first, const SRec (&r)[kPer],
+                                                uint32_t (&body)[kPer], uint32_t (&off)[kPer], uint64_t* lds) {
+  uint64_t packed = 0;
+#pragma unroll
+  for (int p = 0; p < kPer; ++p) {
+    body[p] = srec_body(r[p]);
+    const uint64_t i = first + p * kThreads + threadIdx.x;
+    packed |= (uint64_t)(i < a.n ? frame_size(a, body[p]) : 0) << (16 * p);
+  }
+  uint64_t e;
+  const uint64_t t = block_scan(packed, &e, lds);
+  __syncthreads();  // lds is reused by the next scan
+  uint32_t row = 0;
+#pragma unroll
+  for (int p = 0; p < kPer; ++p) {
+    off[p] = row + (uint32_t)((e >> (16 * p)) & 0xffff);
+    row += (uint32_t)((t >> (16 * p)) & 0xffff);
+  }
+  return row;
+}
+
+// One tile of kSub sub-tiles per workgroup, one ticket per tile.  Phase 1 streams the
+// columns (the next sub-tile's loads in flight during this one's scan) and builds the whole
+// tile's encoding in the LDS stage; the tile then publishes its size, looks back, and
+// stores the stage with aligned dword stores.  A tile whose encoding outgrows the stage
+// (records averaging over 21 bytes), or a call that wants record offsets, reads its
+// columns again after the look-back and writes lane by lane.  Tiles are large because a
+// single contended ticket counter serialises its atomics (~11 ns each).
+extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_val_kernel(WireValArgs a, uint32_t nt) {
+  __shared__ uint64_t lds[5];
+  __shared__ uint32_t s_tile, s_first;
+  __shared__ uint32_t stage[kStageBytes / 4 + 2];
+  if (threadIdx.x == 0) s_tile = atomicAdd(a.ticket, 1u);
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint64_t tfirst = (uint64_t)tile * kTileRecs;
+  uint8_t* st = reinterpret_cast<uint8_t*>(stage);
+  uint32_t agg = 0;
+  SRec cur[kPer], nxt[kPer];
+  load_sub(a, tfirst, cur);
+#pragma unroll
+  for (int j = 0; j < kSub; ++j) {
+    const uint64_t first = tfirst + (uint64_t)j * kSubRecs;
+    if (j + 1 < kSub) load_sub(a, first + kSubRecs, nxt);
+    uint32_t body[kPer], off[kPer];
+    const uint32_t span = sub_offsets(a, first, cur, body, off, lds);
+#pragma unroll
+    for (int p = 0; p < kPer; ++p) {
+      const uint32_t o = agg + off[p];
+      if (first + p * kThreads + threadIdx.x < a.n && o + frame_size(a, body[p]) <= kStageBytes)
+        put_srec(a, cur[p], body[p], st + o);
+    }
+    agg += span;
+#pragma unroll
+    for (int p = 0; p < kPer; ++p) cur[p] = nxt[p];
+  }
+  if (threadIdx.x == 0) st_status(a.status + tile, (tile == 0 ? kFlagP : kFlagA) | agg);
+  uint64_t base = 0;
+  if (tile > 0) {
+    base = lookback_block(a.status, tile, lds, &s_first);
+    if (threadIdx.x == 0) st_status(a.status + tile, kFlagP | (base + agg));
+  }
+  if (tile == nt - 1 && threadIdx.x == 0) {
+    *a.total = base + agg;
+    if (a.offs) a.offs[a.n] = base + agg;
+  }
+  if (agg <= kStageBytes && !a.offs) {
+    __syncthreads();
+    store_stage(a.out, base, stage, agg);
+    return;
+  }
+  uint64_t sbase = base;
+  for (int j = 0; j < kSub; ++j) {
+    const uint64_t first = tfirst + (uint64_t)j * kSubRecs;
+    load_sub(a, first, cur);
+    uint32_t body[kPer], off[kPer];
+    const uint32_t span = sub_offsets(a, first, cur, body, off, lds);
+#pragma unroll
+    for (int p = 0; p < kPer; ++p) {
+      const uint64_t i = first + p * kThreads + threadIdx.x;
+      if (i < a.n) {
+        if (a.offs) a.offs[i] = sbase + off[p];
+        put_srec(a, cur[p], body[p], a.out + sbase + off[p]);
+      }
+    }
+    sbase += span;
+  }
+}
+
+// Records with bytes fields: tiles of kBytesSub x 256 records, one per thread per sub-tile.
+// Phase 1 scans the sizes; after the look-back, phase 2 reads the records again and writes
+// each lane's record straight to HBM (a record has no size bound, so there is no stage).
+extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_val_bytes_kernel(WireValArgs a, uint32_t nt) {
+  __shared__ uint64_t lds[5];
+  __shared__ uint32_t s_tile, s_first;
+  if (threadIdx.x == 0) s_tile = atomicAdd(a.ticket, 1u);
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint64_t tfirst = (uint64_t)tile * kBytesTileRecs + threadIdx.x;
+  uint64_t excl[kBytesSub], sub_base[kBytesSub], agg = 0;
+#pragma unroll
+  for (int j = 0; j < kBytesSub; ++j) {
+    const uint64_t i = tfirst + (uint64_t)j * kThreads;
+    Rec r;
+    uint64_t mine = 0;
+    if (i < a.n) {
+      load_rec(a, i, r);
+      mine = r.size;
+    }
+    const uint64_t t = block_scan(mine, &excl[j], lds);
+    __syncthreads();
+    sub_base[j] = agg;
+    agg += t;
+  }
+  if (threadIdx.x == 0) st_status(a.status + tile, (tile == 0 ? kFlagP : kFlagA) | agg);
+  uint64_t base = 0;
+  if (tile > 0) {
+    base = lookback_block(a.status, tile, lds, &s_first);
+    if (threadIdx.x == 0) st_status(a.status + tile, kFlagP | (base + agg));
+  }
+  if (tile == nt - 1 && threadIdx.x == 0) {
+    *a.total = base + agg;
+    if (a.offs) a.offs[a.n] = base + agg;
+  }
+#pragma unroll
+  for (int j = 0; j < kBytesSub; ++j) {
+    const uint64_t i = tfirst + (uint64_t)j * kThreads;
+    if (i < a.n) {
+      Rec r;
+      load_rec(a, i, r);
+      const uint64_t o = base + sub_base[j] + excl[j];
+      if (a.offs) a.offs[i] = o;
+      put_rec(a, r, a.out + o);
+    }
+  }
+}
+
+}  // namespace
+
+static uint64_t tile_recs(bool bytes) { return bytes ? kBytesTileRecs : kTileRecs; }
+
+uint64_t wire_tiles(uint64_t n) {  // scratch bound: the smaller tile of the two kernels
+  constexpr uint64_t t = kBytesTileRecs < kTileRecs ? kBytesTileRecs : kTileRecs;
+  return (n + t - 1) / t;
+}
+
+// Scratch: status[nt] then the ticket; zeroed before every launch.
+hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t s) {
+  const bool bytes = a.wa_offs || a.rc_offs;
+  const uint64_t nt = (a.n + tile_recs(bytes) - 1) / tile_recs(bytes);
+  if (nt == 0) {
+    hipError_t e = hipMemsetAsync(a.total, 0, 8, s);
+    if (e == hipSuccess && a.offs) e = hipMemsetAsync(a.offs, 0, 8, s);
+    return e;
+  }
+  a.status = scratch;
+  a.ticket = reinterpret_cast<uint32_t*>(scratch + nt);
+  hipError_t e = hipMemsetAsync(scratch, 0, (nt + 1) * 8, s);
+  if (e != hipSuccess) return e;
+  if (bytes)
+    hipLaunchKernelGGL(pz_wire_val_bytes_kernel, dim3((uint32_t)nt), dim3(kThreads), 0, s, a, (uint32_t)nt);
+  else
+    hipLaunchKernelGGL(pz_wire_val_kernel, dim3((uint32_t)nt), dim3(kThreads), 0, s, a, (uint32_t)nt);
+  return hipGetLastError();
+}
+
+int wire_val_args(const pz_validator_cols* v, uint64_t n, uint32_t field_num, WireValArgs* a) {
+  if (!v) return fail(PZ_EINVAL, "columns are null");
+  if (field_num >= (1u << 29)) return fail(PZ_EINVAL, "field number %u out of range", field_num);
+  if ((v->withdrawal_address_offs && !v->withdrawal_address) ||
+      (v->randao_commitment_offs && !v->randao_commitment))
+    return fail(PZ_EINVAL, "bytes column without data");
+  *a = WireValArgs{};
+  a->col[0] = v->public_key;
+  a->col[1] = v->withdrawal_shard;
+  a->col[2] = v->balance;
+  a->col[3] = v->start_dynasty;
+  a->col[4] = v->end_dynasty;
+  a->wa = v->withdrawal_address;
+  a->wa_offs = v->withdrawal_address_offs;
+  a->rc = v->randao_commitment;
+  a->rc_offs = v->randao_commitment_offs;
+  a->n = n;
+  a->field = field_num;
+  uint64_t tag = ((uint64_t)field_num << 3) | 2;
+  a->tag_len = 1;
+  while (tag >= 0x80) {
+    tag >>= 7;
+    ++a->tag_len;
+  }
+  return PZ_OK;
+}
+
+}  // namespace pz
+
+using namespace pz;
+
+extern "C" {
+
+uint64_t pz_wire_validators_bound(uint64_t n, uint64_t bytes_total) { return n * 92 + bytes_total; }
+
+uint64_t pz_wire_scratch_bytes(uint64_t n) { return (wire_tiles(n) + 1) * 8; }
+
+int pz_dev_wire_validators(const pz_validator_cols* v, uint64_t n, uint32_t field_num, uint8_t* d_out,
+                           uint64_t* d_offsets, void* d_scratch, uint64_t* d_total, void* stream) {
+  WireValArgs a;
+  int rc = wire_val_args(v, n, field_num, &a);
+  if (rc) return rc;
+  if (!d_scratch || !d_total || (n && !d_out)) return fail(PZ_EINVAL, "null device pointer");
+  a.out = d_out;
+  a.offs = d_offsets;
+  a.total = d_total;
+  hipError_t e = launch_wire_validators(a, static_cast<uint64_t*>(d_scratch), static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "pz_wire_val_kernel");
+}
+
+int pz_wire_validators(const pz_validator_cols* v, uint64_t n, uint32_t field_num, uint8_t* out, uint64_t cap,
+                       uint64_t* offsets, uint64_t* len) {
+  if (!len) return fail(PZ_EINVAL, "len is null");
+  *len = 0;
+  WireValArgs a;
+  int rc = wire_val_args(v, n, field_num, &a);
+  if (rc) return rc;
+  if (n == 0) {
+    if (offsets) offsets[0] = 0;
+    return PZ_OK;
+  }
+  for (const uint64_t* o : {v->withdrawal_address_offs, v->randao_commitment_offs})
+    if (o && (rc = check_csr(o, n, "bytes column"))) return rc;
+  DeviceCtx* c;
+  if ((rc = acquire(&c))) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = c->ensure_stream())) return rc;
+  Stager st{c, c->stream};
+  for (int k = 0; k < 5; ++k)
+    if (a.col[k]) a.col[k] = st.up(a.col[k], n);
+  std::vector<uint64_t> wo, ro;
+  if (a.wa_offs) {
+    wo = rebase(a.wa_offs, n);
+    a.wa = st.up(v->withdrawal_address + v->withdrawal_address_offs[0], wo[n]);
+    a.wa_offs = st.up(wo.data(), n + 1);
+  }
+  if (a.rc_offs) {
+    ro = rebase(a.rc_offs, n);
+    a.rc = st.up(v->randao_commitment + v->randao_commitment_offs[0], ro[n]);
+    a.rc_offs = st.up(ro.data(), n + 1);
+  }
+  uint64_t nbytes = 0;
+  if (a.wa_offs) nbytes += wo[n];
+  if (a.rc_offs) nbytes += ro[n];
+  uint64_t* scratch = st.zeros<uint64_t>(wire_tiles(n) + 1);
+  a.total = st.zeros<uint64_t>(1);
+  a.offs = offsets ? st.zeros<uint64_t>(n + 1) : nullptr;
+  a.out = st.up<uint8_t>(nullptr, pz_wire_validators_bound(n, nbytes));
+  if (st.rc) return st.rc;
+  st.check(launch_wire_validators(a, scratch, st.s), "pz_wire_val_kernel");
+  uint64_t total = 0;
+  st.down(&total, a.total, 1);
+  if (st.sync()) return st.rc;
+  *len = total;
+  if (total > cap) return fail(PZ_ERANGE, "output needs %llu bytes, capacity %llu", (unsigned long long)total,
+                               (unsigned long long)cap);
+  if (!out) return fail(PZ_EINVAL, "out is null");
+  st.down(out, a.out, total);
+  if (offsets) st.down(offsets, a.offs, n + 1);
+  return st.sync();
+}
+
+}  // extern "C"

@@ -176,3 +176,37 @@ def crystallized_state(s):
     out.append(validators(s.validators))
     out += [_msg(12, shard_and_committee_array(a)) for a in s.shard_and_committees_for_slots]
     return b"".join(out)
+
+
+# ---- device encoder (prysm_amd/csrc/wire.hip) ------------------------------------------------
+def _csr(blobs, n):
+    if blobs is None:
+        return None, None
+    offs = np.zeros(n + 1, dtype=_U64)
+    offs[1:] = np.cumsum([len(b) for b in blobs], dtype=_U64)
+    data = np.frombuffer(b"".join(bytes(b) for b in blobs) + b"\0", dtype=np.uint8)
+    return data, offs
+
+
+def validators_device(v, field_num=11, with_offsets=False):
+    """The same bytes as :func:`validators`, encoded on the GPU by ``pz_wire_validators``
+    (size / scan / write kernels over the SoA columns).  ``field_num=0`` gives
+    bare records; ``with_offsets`` also returns each record's start (n+1 offsets)."""
+    from prysm_amd import _lib
+
+    n = len(v)
+    wa, wa_offs = _csr(v.withdrawal_address, n)
+    rc, rc_offs = _csr(v.randao_commitment, n)
+    cols = _lib.ValidatorCols(
+        _lib.ptr(v.public_key), _lib.ptr(v.withdrawal_shard), _lib.ptr(wa), _lib.ptr(wa_offs),
+        _lib.ptr(rc), _lib.ptr(rc_offs), _lib.ptr(v.balance), _lib.ptr(v.start_dynasty),
+        _lib.ptr(v.end_dynasty))
+    nbytes = (int(wa_offs[-1]) if wa_offs is not None else 0) + (int(rc_offs[-1]) if rc_offs is not None else 0)
+    cap = int(_lib.lib.dll.pz_wire_validators_bound(n, nbytes))
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    offs = np.empty(n + 1, dtype=_U64) if with_offsets else None
+    length = _lib.ctypes.c_uint64(0)
+    _lib.lib.call("pz_wire_validators", _lib.ctypes.byref(cols), n, field_num, _lib.ptr(out), cap,
+                  _lib.ptr(offs), _lib.ctypes.byref(length))
+    raw = out[:length.value].tobytes()
+    return (raw, offs) if with_offsets else raw

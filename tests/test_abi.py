@@ -4,6 +4,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 from prysm_amd import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -31,10 +33,11 @@ def test_version():
     assert _lib.lib.dll.pz_version() == 1
 
 
-def test_epoch_batch_struct_layout():
-    # pz_epoch_batch is passed by pointer from ctypes: field order/packing must match the header
+@pytest.mark.parametrize("name,cls", [("pz_epoch_batch", _lib.EpochBatch), ("pz_validator_cols", _lib.ValidatorCols)])
+def test_struct_layout(name, cls):
+    # the structs are passed by pointer from ctypes: field order/packing must match the header
     src = open(os.path.join(ROOT, "include", "prysm_hip.h")).read()
-    body = src[src.index("typedef struct pz_epoch_batch"):src.index("} pz_epoch_batch;")]
+    body = src[src.index("typedef struct %s" % name):src.index("} %s;" % name)]
     body = re.sub(r"/\*.*?\*/", "", body.split("{", 1)[1], flags=re.S)
     fields = []
     for decl in body.split(";"):
@@ -42,7 +45,7 @@ def test_epoch_batch_struct_layout():
         if decl:
             first, *rest = decl.split(",")
             fields += [first.split()[-1].lstrip("*")] + [r.strip().lstrip("*") for r in rest]
-    assert fields == [f for f, _ in _lib.EpochBatch._fields_]
+    assert fields == [f for f, _ in cls._fields_]
 
 
 def test_host_serial_hasher_matches_hashlib():

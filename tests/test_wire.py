@@ -124,3 +124,25 @@ def test_crystallized_state_bytes(n, with_bytes):
 def test_genesis_validator_record_13_bytes():
     v = pb.Validators(1, balance=[32], end_dynasty=[ref.DEFAULT_END_DYNASTY])
     assert wire.validators(v) == bytes.fromhex("5a0d282038ffff9fcfc8e0c8e38a01")
+
+
+def test_c_port_validators_match_protobuf_runtime():
+    """oracle/c/wire_ref.c (bench.py's wire cpu_baseline) against the runtime, bytes fields
+    included."""
+    from oracle import cport
+
+    rng = np.random.default_rng(21)
+    n = 500
+    v = pb.Validators(n, public_key=[rand_u64(rng) for _ in range(n)],
+                      withdrawal_shard=[rand_u64(rng) for _ in range(n)],
+                      withdrawal_address=[rand_bytes(rng, 0, 3) * 50 for _ in range(n)],
+                      randao_commitment=[rand_bytes(rng, 0, 40) for _ in range(n)],
+                      balance=[rand_u64(rng) for _ in range(n)], start_dynasty=[rand_u64(rng) for _ in range(n)],
+                      end_dynasty=[rand_u64(rng) for _ in range(n)])
+    o = opb.CrystallizedState()
+    for i in range(n):
+        o.validators.add(public_key=int(v.public_key[i]), withdrawal_shard=int(v.withdrawal_shard[i]),
+                         withdrawal_address=v.withdrawal_address[i], randao_commitment=v.randao_commitment[i],
+                         balance=int(v.balance[i]), start_dynasty=int(v.start_dynasty[i]),
+                         end_dynasty=int(v.end_dynasty[i]))
+    assert cport.wire_validators(v) == o.SerializeToString() == wire.validators(v)

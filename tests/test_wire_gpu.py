@@ -1,0 +1,141 @@
+"""Device proto3 encoder of ValidatorRecord columns (prysm_amd/csrc/wire.hip) against Google's
+protobuf runtime over the oracle schema (oracle/schema.py, pinned to messages.pb.go:803-809)
+and, at full size, against the host encoder (prysm_amd/wire.py, itself pinned to the runtime
+by tests/test_wire.py).  Byte-exact."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import schema as opb
+from prysm_amd import _lib, pb, wire
+
+pytestmark = pytest.mark.gpu
+
+
+def varint(x):
+    out = bytearray()
+    while x >= 0x80:
+        out.append((x & 0x7F) | 0x80)
+        x >>= 7
+    out.append(x)
+    return bytes(out)
+
+
+def rand_cols(rng, n, with_bytes):
+    mags = np.array([0, 1, 127, 128, 16383, 16384, (1 << 32) - 1, (1 << 63), (1 << 64) - 1], dtype=np.uint64)
+
+    def col():
+        pick = rng.integers(0, len(mags) + 1, size=n)
+        x = rng.integers(0, 1 << 62, size=n, dtype=np.uint64) * np.uint64(4) + np.uint64(3)
+        return np.where(pick < len(mags), mags[np.minimum(pick, len(mags) - 1)], x).astype(np.uint64)
+
+    def blobs():
+        if not with_bytes:
+            return None
+        lens = rng.choice([0, 0, 1, 20, 32, 127, 128, 300], size=n)
+        return [rng.integers(0, 256, size=int(k), dtype=np.uint8).tobytes() for k in lens]
+
+    return pb.Validators(n, public_key=col(), withdrawal_shard=col(), withdrawal_address=blobs(),
+                         randao_commitment=blobs(), balance=col(), start_dynasty=col(), end_dynasty=col())
+
+
+def oracle_record(v, i):
+    return opb.ValidatorRecord(
+        public_key=int(v.public_key[i]), withdrawal_shard=int(v.withdrawal_shard[i]),
+        withdrawal_address=v.withdrawal_address[i] if v.withdrawal_address is not None else b"",
+        randao_commitment=v.randao_commitment[i] if v.randao_commitment is not None else b"",
+        balance=int(v.balance[i]), start_dynasty=int(v.start_dynasty[i]),
+        end_dynasty=int(v.end_dynasty[i])).SerializeToString()
+
+
+def oracle_framed(v, field_num):
+    tag = varint((field_num << 3) | 2)
+    return b"".join(tag + varint(len(r)) + r for r in (oracle_record(v, i) for i in range(len(v))))
+
+
+@pytest.mark.parametrize("n", [1, 63, 255, 256, 257, 1000, 3000])
+@pytest.mark.parametrize("with_bytes", [False, True])
+def test_validators_match_protobuf_runtime(n, with_bytes):
+    v = rand_cols(np.random.default_rng(n * 2 + with_bytes), n, with_bytes)
+    got = wire.validators_device(v, 11)
+    assert got == oracle_framed(v, 11)
+    # the CrystallizedState framing is exactly the runtime's repeated field 11
+    o = opb.CrystallizedState()
+    for i in range(n):
+        o.validators.add().ParseFromString(oracle_record(v, i))
+    assert got == o.SerializeToString()
+
+
+@pytest.mark.parametrize("field_num", [1, 15, 16, 2047, 2048, (1 << 29) - 1])
+def test_framing_field_numbers(field_num):
+    v = rand_cols(np.random.default_rng(field_num % 1000), 600, False)
+    assert wire.validators_device(v, field_num) == oracle_framed(v, field_num)
+
+
+@pytest.mark.parametrize("with_bytes", [False, True])
+def test_bare_records_with_offsets(with_bytes):
+    n = 777
+    v = rand_cols(np.random.default_rng(5), n, with_bytes)
+    raw, offs = wire.validators_device(v, 0, with_offsets=True)
+    assert offs[0] == 0 and offs[-1] == len(raw)
+    for i in range(n):
+        assert raw[int(offs[i]):int(offs[i + 1])] == oracle_record(v, i), i
+
+
+def test_all_zero_records_and_empty():
+    v = pb.Validators(300)
+    assert wire.validators_device(v, 11) == b"\x5a\x00" * 300
+    raw, offs = wire.validators_device(v, 0, with_offsets=True)  # bare empty records: all offsets 0
+    assert raw == b"" and not offs.any()
+    assert wire.validators_device(pb.Validators(0), 11) == b""
+
+
+def test_genesis_validators_full_size():
+    """MaxValidators (4,194,304) genesis-style records vs the host encoder, plus 1M random."""
+    n = 1 << 22
+    v = pb.Validators(n, balance=np.full(n, 32, np.uint64),
+                      end_dynasty=np.full(n, 9999999999999999999, np.uint64))
+    got = wire.validators_device(v, 11)
+    assert got == wire.validators(v)
+    assert len(got) == n * 15
+    v = rand_cols(np.random.default_rng(9), 1 << 20, False)
+    assert wire.validators_device(v, 11) == wire.validators(v)
+
+
+def test_capacity_error():
+    v = rand_cols(np.random.default_rng(3), 100, False)
+    cols = _lib.ValidatorCols(None, None, None, None, None, None, _lib.ptr(v.balance), None, None)
+    out = np.empty(10, dtype=np.uint8)
+    length = ctypes.c_uint64(0)
+    with pytest.raises(_lib.PzError) as e:
+        _lib.lib.call("pz_wire_validators", ctypes.byref(cols), 100, 11, _lib.ptr(out), 10, None,
+                      ctypes.byref(length))
+    assert e.value.code == _lib.PZ_ERANGE
+    assert length.value == len(wire.validators(pb.Validators(100, balance=v.balance)))
+
+
+def test_device_entry_point_null_columns():
+    """pz_dev_wire_validators on device-resident columns (torch tensors, torch's stream), with
+    NULL columns for the fields that are zero, as the chain engine calls it."""
+    import torch
+
+    n = 100_003
+    rng = np.random.default_rng(11)
+    bal = rng.integers(16, 48, size=n, dtype=np.uint64)
+    end = np.full(n, 9999999999999999999, np.uint64)
+    d_bal = torch.from_numpy(bal.view(np.int64)).cuda()
+    d_end = torch.from_numpy(end.view(np.int64)).cuda()
+    bound = _lib.lib.dll.pz_wire_validators_bound(n, 0)
+    d_out = torch.zeros(bound, dtype=torch.uint8, device="cuda")
+    d_offs = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    d_scr = torch.zeros(_lib.lib.dll.pz_wire_scratch_bytes(n) // 8, dtype=torch.int64, device="cuda")
+    d_tot = torch.zeros(1, dtype=torch.int64, device="cuda")
+    cols = _lib.ValidatorCols(None, None, None, None, None, None, d_bal.data_ptr(), None, d_end.data_ptr())
+    _lib.lib.call("pz_dev_wire_validators", ctypes.byref(cols), n, 11, d_out.data_ptr(), d_offs.data_ptr(),
+                  d_scr.data_ptr(), d_tot.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    total = int(d_tot.item())
+    want = wire.validators(pb.Validators(n, balance=bal, end_dynasty=end))
+    assert total == len(want) == int(d_offs[-1].item())
+    assert d_out[:total].cpu().numpy().tobytes() == want

@@ -1,0 +1,48 @@
+"""Times pz_dev_wire_validators alone (16 states x 1,048,576 genesis-style validators, the
+bench's wire workload) with HIP events; small enough to run under rocprofv3 --pmc."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from prysm_amd import _lib  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+    n = 16 << 20
+    rng = np.random.default_rng(7)
+    cols_np = [rng.integers(16, 49, size=n, dtype=np.uint64), np.zeros(n, np.uint64),
+               np.full(n, 9999999999999999999, np.uint64)]
+    cols_t = [torch.from_numpy(a.view(np.int64)).cuda() for a in cols_np]
+    out = torch.empty(int(_lib.lib.dll.pz_wire_validators_bound(n, 0)), dtype=torch.uint8, device="cuda")
+    scr = torch.empty(int(_lib.lib.dll.pz_wire_scratch_bytes(n)) // 8, dtype=torch.int64, device="cuda")
+    tot = torch.zeros(1, dtype=torch.int64, device="cuda")
+    cols = _lib.ValidatorCols(None, None, None, None, None, None, *[t.data_ptr() for t in cols_t])
+    sh = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def run():
+        _lib.lib.call("pz_dev_wire_validators", ctypes.byref(cols), n, 11, out.data_ptr(), None, scr.data_ptr(),
+                      tot.data_ptr(), sh)
+
+    for _ in range(10):
+        run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    total = int(tot.item())
+    alg = n * 24 + total
+    print("wire: %d records, %d bytes, %.1f us/launch, %.0f GB/s algorithmic (%.1f%% of 8 TB/s)"
+          % (n, total, us, alg / us / 1e3, alg / us / 1e3 / 80))
+
+
+if __name__ == "__main__":
+    main()
