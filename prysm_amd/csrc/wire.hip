@@ -10,10 +10,10 @@
 // records, derives their encoded sizes, scans them, and learns the tile's output offset by a
 // decoupled look-back over its predecessors' published sizes.  Then it writes the tile's
 // bytes.  This is HBM-bound byte work, with no MFMA, and the columns are read once.
-//  * Scalar-only records (no bytes fields; the chain's CrystallizedState): 3,072 records per
-//    tile, streamed in sub-tiles of 1,024 with coalesced column loads.  The tile's encoding
-//    is built in a 64 KB LDS stage and stored with aligned dword stores.  A tile larger than the stage (records near the 61-byte maximum)
-//    writes lane by lane instead.
+//  * Scalar-only records (no bytes fields; the chain's CrystallizedState): 2,048 records per
+//    tile, loaded with coalesced column loads.  The tile's encoding is built in a 32 KB LDS
+//    stage and stored with aligned dword stores.  A tile larger than the stage (records
+//    averaging over 16 bytes) writes lane by lane instead.
 //  * Records with bytes fields: 2,048 records per tile, sizes first, then (after the
 //    look-back) a second read of the records, written lane by lane straight to HBM.
 #include "wire.h"
@@ -28,8 +28,8 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kPer = 4, kSubRecs = kThreads * kPer;  // scalar kernel: sub-tiles of 1,024 records
-constexpr int kSub = 3, kTileRecs = kSub * kSubRecs;  // 3,072 records (one ticket) per tile
-constexpr int kStageBytes = 64 * 1024;                // the whole tile's encoding (21 B per record)
+constexpr int kSub = 2, kTileRecs = kSub * kSubRecs;  // 2,048 records (one ticket) per tile
+constexpr int kStageBytes = 32 * 1024;                // the whole tile's encoding (16 B per record)
 constexpr int kBytesSub = 8, kBytesTileRecs = kBytesSub * kThreads;  // bytes-field kernel: 2,048
 
 __device__ __forceinline__ uint32_t vlen(uint64_t x) { return (uint32_t)((70 - __clzll(x | 1)) / 7); }
@@ -159,6 +159,13 @@ constexpr uint64_t kFlagA = 1ull << 62, kFlagP = 2ull << 62, kVal = kFlagA - 1;
 __device__ __forceinline__ uint64_t ld_status(uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// A coherent re-read for the spin: an `sc1` load is served by this XCD's L2, which can hold a
+// stale copy of another XCD's status line until it is evicted; an atomic is performed at the
+// coherence point.  (Stale reads are safe -- flags only move 0 -> A -> P and every published
+// value is final -- they only make the spin longer.)
+__device__ __forceinline__ uint64_t ld_status_fresh(uint64_t* p) {
+  return __hip_atomic_fetch_add(p, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -168,22 +175,27 @@ __device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
 // when every resident tile started together (a wave-wide window walked 64 tiles per round
 // trip, ~8 trips per dispatch round).  Returns the exclusive prefix of `tile` to every thread.
 constexpr int kLbPer = 4, kLbWin = kThreads * kLbPer;
-__device__ uint64_t lookback_block(uint64_t* status, uint64_t tile, uint64_t* lds, uint32_t* lds_first) {
+
+// First window's loads, issued early so their round trip overlaps other work.
+__device__ __forceinline__ void lookback_issue(uint64_t* status, uint64_t tile, uint64_t (&w)[kLbPer]) {
+#pragma unroll
+  for (int q = 0; q < kLbPer; ++q) {
+    const int64_t idx = (int64_t)tile - 1 - (threadIdx.x * kLbPer + q);
+    w[q] = idx >= 0 ? ld_status(status + idx) : kFlagP;  // before tile 0: prefix 0
+  }
+}
+
+__device__ uint64_t lookback_finish(uint64_t* status, uint64_t tile, uint64_t (&w)[kLbPer], uint64_t* lds,
+                                    uint32_t* lds_first) {
   uint64_t prefix = 0;
   int64_t j = (int64_t)tile - 1;
   while (true) {
-    uint64_t w[kLbPer];
-#pragma unroll
-    for (int q = 0; q < kLbPer; ++q) {
-      const int64_t idx = j - (threadIdx.x * kLbPer + q);
-      w[q] = idx >= 0 ? ld_status(status + idx) : kFlagP;  // before tile 0: prefix 0
-    }
 #pragma unroll
     for (int q = 0; q < kLbPer; ++q) {
       const int64_t idx = j - (threadIdx.x * kLbPer + q);
       while (!(w[q] >> 62)) {
         __builtin_amdgcn_s_sleep(1);
-        w[q] = ld_status(status + idx);
+        w[q] = ld_status_fresh(status + idx);
       }
     }
     // nearest published inclusive prefix (distance d = threadIdx.x * kLbPer + q)
@@ -206,7 +218,22 @@ __device__ uint64_t lookback_block(uint64_t* status, uint64_t tile, uint64_t* ld
     __syncthreads();
     if (first < (uint32_t)kLbWin) return prefix;
     j -= kLbWin;
+#pragma unroll
+    for (int q = 0; q < kLbPer; ++q) {
+      const int64_t idx = j - (threadIdx.x * kLbPer + q);
+      w[q] = idx >= 0 ? ld_status(status + idx) : kFlagP;
+    }
   }
+}
+
+// Decoupled look-back by the whole workgroup: 256 threads x 4 loads watch the 1,024 nearest
+// predecessors at once, so one round trip usually reaches a published inclusive prefix even
+// when every resident tile started together (a wave-wide window walked 64 tiles per round
+// trip, ~8 trips per dispatch round).  Returns the exclusive prefix of `tile` to every thread.
+__device__ uint64_t lookback_block(uint64_t* status, uint64_t tile, uint64_t* lds, uint32_t* lds_first) {
+  uint64_t w[kLbPer];
+  lookback_issue(status, tile, w);
+  return lookback_finish(status, tile, w, lds, lds_first);
 }
 
 // Store stage[0..span) at out+base with dword stores: bytes up to the first 4-aligned
@@ -261,12 +288,12 @@ __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t f
   return row;
 }
 
-// One tile of kSub sub-tiles per workgroup, one ticket per tile.  Phase 1 streams the
-// columns (the next sub-tile's loads in flight during this one's scan) and builds the whole
-// tile's encoding in the LDS stage; the tile then publishes its size, looks back, and
-// stores the stage with aligned dword stores.  A tile whose encoding outgrows the stage
-// (records averaging over 21 bytes), or a call that wants record offsets, reads its
-// columns again after the look-back and writes lane by lane.  Tiles are large because a
+// One tile of kSub sub-tiles per workgroup, one ticket per tile.  All of the tile's columns
+// are loaded at once; the sub-tiles' sizes are scanned and the tile publishes its size.
+// The look-back's first window is issued, the tile's encoding is built in the LDS stage
+// meanwhile, and after the look-back the stage is stored with aligned dword stores.  A tile
+// whose encoding outgrows the stage (records averaging over 16 bytes), or a call that wants
+// record offsets, writes lane by lane from registers instead.  Tiles are large because a
 // single contended ticket counter serialises its atomics (~11 ns each).
 extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_val_kernel(WireValArgs a, uint32_t nt) {
   __shared__ uint64_t lds[5];
@@ -277,29 +304,32 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_val_kernel(WireVa
   const uint32_t tile = s_tile;
   const uint64_t tfirst = (uint64_t)tile * kTileRecs;
   uint8_t* st = reinterpret_cast<uint8_t*>(stage);
+  // every sub-tile's columns in registers at once (kSub x kPer records per thread)
+  SRec r[kSub][kPer];
+#pragma unroll
+  for (int j = 0; j < kSub; ++j) load_sub(a, tfirst + (uint64_t)j * kSubRecs, r[j]);
+  uint32_t body[kSub][kPer], off[kSub][kPer], sub_base[kSub];
   uint32_t agg = 0;
-  SRec cur[kPer], nxt[kPer];
-  load_sub(a, tfirst, cur);
 #pragma unroll
   for (int j = 0; j < kSub; ++j) {
-    const uint64_t first = tfirst + (uint64_t)j * kSubRecs;
-    if (j + 1 < kSub) load_sub(a, first + kSubRecs, nxt);
-    uint32_t body[kPer], off[kPer];
-    const uint32_t span = sub_offsets(a, first, cur, body, off, lds);
-#pragma unroll
-    for (int p = 0; p < kPer; ++p) {
-      const uint32_t o = agg + off[p];
-      if (first + p * kThreads + threadIdx.x < a.n && o + frame_size(a, body[p]) <= kStageBytes)
-        put_srec(a, cur[p], body[p], st + o);
-    }
-    agg += span;
-#pragma unroll
-    for (int p = 0; p < kPer; ++p) cur[p] = nxt[p];
+    sub_base[j] = agg;
+    agg += sub_offsets(a, tfirst + (uint64_t)j * kSubRecs, r[j], body[j], off[j], lds);
   }
   if (threadIdx.x == 0) st_status(a.status + tile, (tile == 0 ? kFlagP : kFlagA) | agg);
+  // the look-back's first round trip overlaps the stage build
+  uint64_t w[kLbPer];
+  if (tile > 0) lookback_issue(a.status, tile, w);
+#pragma unroll
+  for (int j = 0; j < kSub; ++j)
+#pragma unroll
+    for (int p = 0; p < kPer; ++p) {
+      const uint32_t o = sub_base[j] + off[j][p];
+      if (tfirst + j * kSubRecs + p * kThreads + threadIdx.x < a.n && o + frame_size(a, body[j][p]) <= kStageBytes)
+        put_srec(a, r[j][p], body[j][p], st + o);
+    }
   uint64_t base = 0;
   if (tile > 0) {
-    base = lookback_block(a.status, tile, lds, &s_first);
+    base = lookback_finish(a.status, tile, w, lds, &s_first);
     if (threadIdx.x == 0) st_status(a.status + tile, kFlagP | (base + agg));
   }
   if (tile == nt - 1 && threadIdx.x == 0) {
@@ -311,22 +341,17 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_val_kernel(WireVa
     store_stage(a.out, base, stage, agg);
     return;
   }
-  uint64_t sbase = base;
-  for (int j = 0; j < kSub; ++j) {
-    const uint64_t first = tfirst + (uint64_t)j * kSubRecs;
-    load_sub(a, first, cur);
-    uint32_t body[kPer], off[kPer];
-    const uint32_t span = sub_offsets(a, first, cur, body, off, lds);
+#pragma unroll
+  for (int j = 0; j < kSub; ++j)
 #pragma unroll
     for (int p = 0; p < kPer; ++p) {
-      const uint64_t i = first + p * kThreads + threadIdx.x;
+      const uint64_t i = tfirst + j * kSubRecs + p * kThreads + threadIdx.x;
       if (i < a.n) {
-        if (a.offs) a.offs[i] = sbase + off[p];
-        put_srec(a, cur[p], body[p], a.out + sbase + off[p]);
+        const uint64_t o = base + sub_base[j] + off[j][p];
+        if (a.offs) a.offs[i] = o;
+        put_srec(a, r[j][p], body[j][p], a.out + o);
       }
     }
-    sbase += span;
-  }
 }
 
 // Records with bytes fields: tiles of kBytesSub x 256 records, one per thread per sub-tile.
