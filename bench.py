@@ -82,6 +82,7 @@ def parse():
     p.add_argument("--no-epoch", action="store_true")
     p.add_argument("--no-replay", action="store_true")
     p.add_argument("--no-wire", action="store_true")
+    p.add_argument("--no-attcheck", action="store_true")
     p.add_argument("--replay-blocks", type=int, default=10000,
                    help="blocks per sync replay (BASELINE configs[4]; 65,536 validators)")
     p.add_argument("--epoch-validators", type=int, default=0,
@@ -258,6 +259,125 @@ def wire_leg(args, torch, dist, dev, rank, world):
             out["cpu_baseline"] = {"value": reps * nval / dt, "unit": "records/s", "cores": 1, "kind": "port",
                                    "sample": "%d encodings of one %d-validator state (AoS records, size + marshal "
                                              "pass, 1 thread, oracle/c/wire_ref.c), %.2f s" % (reps, nval, dt)}
+    return out
+
+
+ATT_BYTES = 65  # per attestation: 5 u64 columns + its boffs entry + the bitfield's last byte + 16 B out
+
+
+def attcheck_columns(natt, seed):
+    """Synthetic processAttestation inputs at configs[2]'s committee shape (65,536 validators:
+    5 committees of 204-205 per slot, 256 ShardAndCommitteesForSlots arrays), blocks of slots
+    64-127 after a recalc at 0; 5 % of the attestations fail one of the checks."""
+    rng = np.random.default_rng(seed)
+    narr, per = 256, 5
+    arr_offs = np.arange(narr + 1, dtype=np.uint64) * per
+    arr_shard = ((np.arange(narr * per) // per % 64) * per + np.arange(narr * per) % per).astype(np.uint64) % 1024
+    arr_comm = ((np.arange(narr * per) // per % 64) * per + np.arange(narr * per) % per).astype(np.uint32)
+    sizes = np.full(64 * per, 204, dtype=np.uint64)
+    sizes[: 65536 - 204 * 64 * per] += 1
+    coffs = np.zeros(64 * per + 1, dtype=np.uint64)
+    coffs[1:] = np.cumsum(sizes)
+    bslot = rng.integers(64, 128, size=natt, dtype=np.uint64)
+    slot = bslot - rng.integers(0, 65, size=natt, dtype=np.uint64)
+    j = rng.integers(0, per, size=natt)
+    shard = arr_shard[slot.astype(np.int64) * per + j]
+    k = sizes[arr_comm[slot.astype(np.int64) * per + j]]
+    blen = (k + np.uint64(7)) // np.uint64(8)
+    bad = rng.random(natt) < 0.05
+    js = np.where(bad & (rng.random(natt) < 0.5), np.uint64(9), np.uint64(0)).astype(np.uint64)
+    blen = np.where(bad & (js == 0), blen + np.uint64(1), blen)
+    boffs = np.zeros(natt + 1, dtype=np.uint64)
+    boffs[1:] = np.cumsum(blen)
+    bits = rng.integers(0, 256, size=int(boffs[-1]) + 1, dtype=np.uint8)
+    last = (boffs[1:] - np.uint64(1)).astype(np.int64)
+    rem = (k % np.uint64(8)).astype(np.int64)
+    bits[last] &= np.where(rem > 0, (0xFF << (8 - rem)) & 0xFF, 0xFF).astype(np.uint8)
+    nob = np.zeros(natt, dtype=np.uint64)
+    cols = dict(slot=slot, justified_slot=js, shard_id=shard, n_oblique=nob, bits=bits, boffs=boffs, block_slot=bslot)
+    tab = dict(arr_offs=arr_offs, arr_shard=arr_shard, arr_comm=arr_comm, coffs=coffs)
+    return cols, tab
+
+
+def attcheck_leg(args, torch, dist, dev, rank, world):
+    """processAttestation's checks for a batch of 4M attestations on the
+    GPU (pz_dev_check_attestations, one lane each); attestations shard over the ranks."""
+    from prysm_amd import _lib
+
+    natt = 1 << 22
+    cols, tab = attcheck_columns(natt, seed=11 + rank)
+    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v.view(np.int32) if v.dtype == np.uint32
+                             else v).to(dev) for k, v in list(cols.items()) + list(tab.items())}
+    status = torch.empty(natt, dtype=torch.int32, device=dev)
+    comm = torch.empty(natt, dtype=torch.int32, device=dev)
+    pstart = torch.empty(natt, dtype=torch.int64, device=dev)
+    b = _lib.AttCheckBatch(natt, t["slot"].data_ptr(), t["justified_slot"].data_ptr(), t["shard_id"].data_ptr(),
+                           t["n_oblique"].data_ptr(), t["bits"].data_ptr(), t["boffs"].data_ptr(),
+                           t["block_slot"].data_ptr(), 0, 0, 128, 256, t["arr_offs"].data_ptr(),
+                           t["arr_shard"].data_ptr(), t["arr_comm"].data_ptr(), t["coffs"].data_ptr(),
+                           status.data_ptr(), comm.data_ptr(), pstart.data_ptr())
+    stream = torch.cuda.current_stream(dev)
+    sh = ctypes.c_void_p(stream.cuda_stream)
+
+    def step():
+        _lib.lib.call("pz_dev_check_attestations", ctypes.byref(b), sh)
+
+    for _ in range(args.warmup + 20):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        step()
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    step_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    if world > 1:
+        wall = max_over_ranks(wall, torch, dist, dev)
+    alg = natt * ATT_BYTES
+    out = {
+        "metric": "attestations checked/s (processAttestation, core.go:240-297)",
+        "value": natt * world * args.steps / wall,
+        "unit": "attestations/s",
+        "ms_per_step": wall / args.steps * 1e3,
+        "scaling": "weak",
+        "config": {"workload": "%d attestations per GPU at configs[2]'s committee shape (65,536 validators), "
+                               "5%% failing a check" % natt, "parallelism": "attestation-shard x%d" % world},
+        "roofline": {"bound": "hbm", "achieved": alg / (step_ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": alg / (step_ms * 1e-3) / HBM_PEAK, "traffic": None,
+                     "kernel": "pz_att_check_kernel", "step_device_ms": step_ms,
+                     "algorithmic_bytes_per_launch": alg},
+    }
+    if rank == 0 and world == 1:
+        from oracle import cport
+        ns = 1 << 20
+        sub = {k: (v[:ns + 1] if k == "boffs" else v[:ns]) for k, v in cols.items() if k != "bits"}
+        port = cport.AttCheck(sub["slot"], sub["justified_slot"], sub["shard_id"], sub["n_oblique"], cols["bits"],
+                              sub["boffs"], sub["block_slot"])
+        try:
+            want = port.run(0, 0, 128, tab["arr_offs"], tab["arr_shard"], tab["arr_comm"], tab["coffs"])
+            got = status[:ns].cpu().numpy()
+            out["parity"] = "status of the first %d attestations equal to the C port: %s" % (
+                ns, bool(np.array_equal(got, want)))
+            if not args.no_cpu_baseline:
+                reps, t1 = 0, time.perf_counter()
+                while reps == 0 or time.perf_counter() - t1 < CPU_SAMPLE_S / 4:
+                    port.run(0, 0, 128, tab["arr_offs"], tab["arr_shard"], tab["arr_comm"], tab["coffs"])
+                    reps += 1
+                dt = time.perf_counter() - t1
+                out["cpu_baseline"] = {"value": reps * ns / dt, "unit": "attestations/s", "cores": 1, "kind": "port",
+                                       "sample": "%d passes over %d attestations (AoS records, 1 thread, "
+                                                 "oracle/c/attcheck_ref.c), %.2f s" % (reps, ns, dt)}
+        finally:
+            port.close()
     return out
 
 
@@ -447,6 +567,7 @@ def main():
         epoch_1m = epoch_leg(args, torch, dist, dev, rank, world, nval=1 << 20, ninst=16, baseline=False)
     replay = None if args.no_replay else replay_leg(args, torch, dist, dev, rank, world)
     wire_out = None if args.no_wire else wire_leg(args, torch, dist, dev, rank, world)
+    att_out = None if args.no_attcheck else attcheck_leg(args, torch, dist, dev, rank, world)
 
     if rank == 0:
         total = n * world * args.steps
@@ -504,6 +625,8 @@ def main():
             line["replay"] = replay
         if wire_out is not None:
             line["wire"] = wire_out
+        if att_out is not None:
+            line["attcheck"] = att_out
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

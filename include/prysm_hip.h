@@ -297,6 +297,38 @@ int pz_dev_epoch_gather_compact(const pz_epoch_batch* b, const uint64_t* gathere
 #define PZ_ATT_BITFIELD_LEN           6  /* core.go:379-382 */
 #define PZ_ATT_TRAILING_BITS          7  /* core.go:385-392 */
 
+/* ---- §8f: processAttestation's checks for a batch, one GPU lane per attestation --------
+ * blockchain/core.go:240-297 with getSignedParentHashes (:348-360), getAttesterIndices
+ * (:363-374) and validateAttesterBitfields (:377-394), in Go's order.  Attestation i was
+ * carried by a block of slot block_slot[i]; the chain state is the one processAttestation
+ * reads (CrystallizedState.LastJustifiedSlot / LastStateRecalc / ShardAndCommitteesForSlots,
+ * len(ActiveState.RecentBlockHashes)).  status[i] receives PZ_ATT_PROCESSED or the first
+ * check that failed (PZ_ATT_*), or PZ_ERANGE / PZ_EINDEX where Go panics (the slice bounds
+ * of :353, the committee index of :367).  committee[i] (optional) receives the committee id
+ * (UINT32_MAX if not reached) and parents_start[i] (optional) the first RecentBlockHashes
+ * index the signed parent hashes start at. */
+typedef struct pz_att_check_batch {
+  uint64_t natt;
+  const uint64_t* slot;            /* AttestationRecord.Slot */
+  const uint64_t* justified_slot;  /* .JustifiedSlot */
+  const uint64_t* shard_id;        /* .ShardId */
+  const uint64_t* n_oblique;       /* len(.ObliqueParentHashes) */
+  const uint8_t*  bits;            /* .AttesterBitfield, CSR */
+  const uint64_t* boffs;           /* natt+1 */
+  const uint64_t* block_slot;      /* SlotNumber of the carrying block */
+  uint64_t last_justified_slot, last_state_recalc, n_recent;
+  uint64_t narr;                   /* len(ShardAndCommitteesForSlots) */
+  const uint64_t* arr_offs;        /* narr+1: array a = entries arr_offs[a] .. arr_offs[a+1] */
+  const uint64_t* arr_shard;       /* entry -> ShardId */
+  const uint32_t* arr_comm;        /* entry -> committee id */
+  const uint64_t* coffs;           /* committee c has coffs[c+1] - coffs[c] members */
+  int32_t*  status;
+  uint32_t* committee;
+  uint64_t* parents_start;
+} pz_att_check_batch;
+int pz_check_attestations(const pz_att_check_batch* b);                  /* host pointers */
+int pz_dev_check_attestations(const pz_att_check_batch* b, void* stream); /* device pointers */
+
 typedef struct pz_block_result {
   uint8_t hash[32];      /* Block.Hash() */
   int32_t status;        /* PZ_BLOCK_* */

@@ -166,3 +166,31 @@ def wire_validators_timed(v, min_seconds=8.0, max_reps=100000):
         return reps, time.perf_counter() - t0
     finally:
         d.oracle_wire_free(h)
+
+
+class AttCheck:
+    """oracle/c/attcheck_ref.c over numpy columns (the same layout pz_check_attestations takes)."""
+
+    def __init__(self, slot, js, shard, nob, bits, boffs, bslot):
+        d = dll()
+        vp, sz, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64
+        d.oracle_att_build.restype = vp
+        d.oracle_att_build.argtypes = [vp] * 7 + [sz]
+        d.oracle_att_free.argtypes = [vp]
+        d.oracle_att_check.argtypes = [vp, u64, u64, u64, u64, vp, vp, vp, vp, vp]
+        self.d, self.n = d, len(slot)
+        cols = [np.ascontiguousarray(x, dtype=np.uint64) for x in (slot, js, shard, nob)]
+        bits = np.ascontiguousarray(bits, dtype=np.uint8)
+        boffs = np.ascontiguousarray(boffs, dtype=np.uint64)
+        bslot = np.ascontiguousarray(bslot, dtype=np.uint64)
+        self.h = d.oracle_att_build(*[c.ctypes.data for c in cols], bits.ctypes.data, boffs.ctypes.data,
+                                    bslot.ctypes.data, self.n)
+
+    def run(self, ljs, lsr, n_recent, arr_offs, arr_shard, arr_comm, coffs):
+        status = np.empty(max(self.n, 1), dtype=np.int32)
+        self.d.oracle_att_check(self.h, ljs, lsr, n_recent, len(arr_offs) - 1, arr_offs.ctypes.data,
+                                arr_shard.ctypes.data, arr_comm.ctypes.data, coffs.ctypes.data, status.ctypes.data)
+        return status[:self.n]
+
+    def close(self):
+        self.d.oracle_att_free(self.h)

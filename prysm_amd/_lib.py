@@ -82,6 +82,8 @@ SIGNATURES = {
     "pz_wire_scratch_bytes": [u64],
     "pz_wire_validators": [vp, u64, u32, vp, u64, vp, c_u64p],
     "pz_dev_wire_validators": [vp, u64, u32, vp, vp, vp, vp, vp],
+    "pz_check_attestations": [vp],
+    "pz_dev_check_attestations": [vp, vp],
 }
 
 
@@ -114,6 +116,16 @@ class ValidatorCols(ctypes.Structure):
         ("public_key", vp), ("withdrawal_shard", vp), ("withdrawal_address", vp),
         ("withdrawal_address_offs", vp), ("randao_commitment", vp), ("randao_commitment_offs", vp),
         ("balance", vp), ("start_dynasty", vp), ("end_dynasty", vp),
+    ]
+
+
+class AttCheckBatch(ctypes.Structure):
+    """Mirror of ``pz_att_check_batch`` (include/prysm_hip.h)."""
+    _fields_ = [
+        ("natt", u64), ("slot", vp), ("justified_slot", vp), ("shard_id", vp), ("n_oblique", vp),
+        ("bits", vp), ("boffs", vp), ("block_slot", vp), ("last_justified_slot", u64),
+        ("last_state_recalc", u64), ("n_recent", u64), ("narr", u64), ("arr_offs", vp), ("arr_shard", vp),
+        ("arr_comm", vp), ("coffs", vp), ("status", vp), ("committee", vp), ("parents_start", vp),
     ]
 
 

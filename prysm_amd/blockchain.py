@@ -37,6 +37,49 @@ ATT_ERRORS = {2: "slot too high", 3: "slot too low", 4: "justified slot mismatch
               6: "bitfield length", 7: "non-zero trailing bits"}
 
 
+def check_attestations(atts, block_slots, last_justified_slot, last_state_recalc, n_recent,
+                       shard_and_committees):
+    """processAttestation's checks (blockchain/core.go:240-297, :348-394) for a batch of
+    attestations on the GPU (``pz_check_attestations``, one lane each).
+
+    ``atts``: AttestationRecord-like objects; ``block_slots[i]``: the slot of the block that
+    carries ``atts[i]``; the chain state: ``last_justified_slot``, ``last_state_recalc``,
+    ``n_recent`` = len(RecentBlockHashes) and ``shard_and_committees`` = ShardAndCommitteesForSlots
+    as a list (one per slot) of lists of ``(shard_id, committee)`` pairs.  Returns
+    ``(status, committee_index, parents_start)``: status PZ_ATT_PROCESSED, the first failed
+    check (PZ_ATT_*), or PZ_ERANGE / PZ_EINDEX where Go panics; committee_index counts the
+    table's (shard, committee) entries in order (-1 if not reached)."""
+    n = len(atts)
+    u64 = np.uint64
+    cols = {k: np.ascontiguousarray([getattr(a, k) for a in atts], dtype=u64)
+            for k in ("slot", "justified_slot", "shard_id")}
+    n_obl = np.ascontiguousarray([len(a.oblique_parent_hashes) for a in atts], dtype=u64)
+    bslot = np.ascontiguousarray(block_slots, dtype=u64)
+    bf = [bytes(a.attester_bitfield) for a in atts]
+    boffs = np.zeros(n + 1, dtype=u64)
+    boffs[1:] = np.cumsum([len(x) for x in bf], dtype=u64)
+    bits = np.frombuffer(b"".join(bf) + b"\0", dtype=np.uint8)
+    arr_offs = np.zeros(len(shard_and_committees) + 1, dtype=u64)
+    arr_offs[1:] = np.cumsum([len(arr) for arr in shard_and_committees], dtype=u64)
+    entries = [e for arr in shard_and_committees for e in arr]
+    arr_shard = np.ascontiguousarray([e[0] for e in entries] or [0], dtype=u64)
+    arr_comm = np.arange(max(len(entries), 1), dtype=np.uint32)
+    coffs = np.zeros(len(entries) + 1, dtype=u64)
+    coffs[1:] = np.cumsum([len(e[1]) for e in entries], dtype=u64)
+    status = np.zeros(max(n, 1), dtype=np.int32)
+    comm = np.zeros(max(n, 1), dtype=np.uint32)
+    pstart = np.zeros(max(n, 1), dtype=u64)
+    b = _lib.AttCheckBatch(
+        n, _lib.ptr(cols["slot"]), _lib.ptr(cols["justified_slot"]), _lib.ptr(cols["shard_id"]), _lib.ptr(n_obl),
+        _lib.ptr(bits), _lib.ptr(boffs), _lib.ptr(bslot), last_justified_slot, last_state_recalc, n_recent,
+        len(shard_and_committees), _lib.ptr(arr_offs), _lib.ptr(arr_shard), _lib.ptr(arr_comm), _lib.ptr(coffs),
+        _lib.ptr(status), _lib.ptr(comm), _lib.ptr(pstart))
+    lib.call("pz_check_attestations", ctypes.byref(b))
+    ci = comm[:n].astype(np.int64)
+    ci[comm[:n] == 0xFFFFFFFF] = -1
+    return status[:n], ci, pstart[:n]
+
+
 class ChainPanic(RuntimeError):
     """The reference would panic here (index out of range / nil map / nil state)."""
 

@@ -1,0 +1,146 @@
+// processAttestation's checks for a batch of attestations, one lane each.
+//
+// Restates, in Go's order, blockchain/core.go:240-297 processAttestation with its helpers
+// getSignedParentHashes (core.go:348-360: the RecentBlockHashes slice bounds),
+// getAttesterIndices (core.go:363-374: the committee of (Slot - LastStateRecalc, ShardId))
+// and validateAttesterBitfields (core.go:377-394: BitLength and zero trailing bits).  The
+// comparisons keep Go's types: the slot window compares int(slot) with int(block slot), the
+// slice bounds and the committee index are uint64 differences that wrap.
+//
+// Each attestation needs ~60 bytes of scalars and the last byte of its bitfield; the
+// committee table (ShardAndCommitteesForSlots: 256 arrays of a few (shard, committee)
+// pairs) is shared by all lanes and stays in L1/L2.  HBM-bound, no MFMA, no LDS.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "runtime.h"
+
+namespace pz {
+namespace {
+
+constexpr int kThreads = 256;
+
+extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_kernel(pz_att_check_batch b) {
+  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= b.natt) return;
+  // every per-attestation column is loaded up front (independent loads in flight together);
+  // only the committee table walk and the bitfield byte depend on them
+  const uint64_t s = b.slot[i], bs = b.block_slot[i], js = b.justified_slot[i], nob = b.n_oblique[i];
+  const uint64_t shard = b.shard_id[i], b0 = b.boffs[i], b1 = b.boffs[i + 1];
+  int32_t st = PZ_ATT_PROCESSED;
+  uint32_t comm = UINT32_MAX;
+  uint64_t pstart = 0;
+  if ((int64_t)s > (int64_t)bs) {
+    st = PZ_ATT_SLOT_HIGH;
+  } else if ((int64_t)s < (int64_t)bs - PZ_CYCLE_LENGTH) {
+    st = PZ_ATT_SLOT_LOW;
+  } else if (js != b.last_justified_slot) {
+    st = PZ_ATT_JUSTIFIED;
+  } else {
+    const uint64_t start = bs - s, end = bs - s - nob + PZ_CYCLE_LENGTH;
+    const uint64_t idx = s - b.last_state_recalc;
+    if (start > end || end > b.n_recent) {
+      st = PZ_ERANGE;  // Go panics: slice bounds out of range (core.go:353)
+    } else if (idx >= b.narr) {
+      st = PZ_EINDEX;  // Go panics: index out of range (core.go:367)
+    } else {
+      pstart = start;
+      for (uint64_t e = b.arr_offs[idx]; e < b.arr_offs[idx + 1]; ++e)
+        if (b.arr_shard[e] == shard) {
+          comm = b.arr_comm[e];
+          break;
+        }
+      if (comm == UINT32_MAX) {
+        st = PZ_ATT_NO_COMMITTEE;
+      } else {
+        const uint64_t k = b.coffs[comm + 1] - b.coffs[comm];
+        const uint64_t blen = b1 - b0;
+        if ((k + 7) / 8 != blen)
+          st = PZ_ATT_BITFIELD_LEN;
+        else if ((k & 7) && (b.bits[b0 + blen - 1] & (0xFFu >> (k & 7))))
+          st = PZ_ATT_TRAILING_BITS;
+      }
+    }
+  }
+  b.status[i] = st;
+  if (b.committee) b.committee[i] = comm;
+  if (b.parents_start) b.parents_start[i] = pstart;
+}
+
+int check_args(const pz_att_check_batch* b) {
+  if (!b) return fail(PZ_EINVAL, "batch is null");
+  if (b->natt && (!b->slot || !b->justified_slot || !b->shard_id || !b->n_oblique || !b->boffs || !b->block_slot ||
+                  !b->status))
+    return fail(PZ_EINVAL, "null attestation column");
+  if (b->narr && (!b->arr_offs || !b->arr_shard || !b->arr_comm || !b->coffs))
+    return fail(PZ_EINVAL, "null committee table");
+  return PZ_OK;
+}
+
+hipError_t launch_att_check(const pz_att_check_batch& b, hipStream_t s) {
+  if (!b.natt) return hipSuccess;
+  hipLaunchKernelGGL(pz_att_check_kernel, dim3((uint32_t)((b.natt + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                     s, b);
+  return hipGetLastError();
+}
+
+}  // namespace
+}  // namespace pz
+
+using namespace pz;
+
+extern "C" {
+
+int pz_dev_check_attestations(const pz_att_check_batch* b, void* stream) {
+  int rc = check_args(b);
+  if (rc) return rc;
+  hipError_t e = launch_att_check(*b, static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "pz_att_check_kernel");
+}
+
+int pz_check_attestations(const pz_att_check_batch* hb) {
+  int rc = check_args(hb);
+  if (rc) return rc;
+  const uint64_t n = hb->natt;
+  if (!n) return PZ_OK;
+  if ((rc = check_csr(hb->boffs, n, "bitfield"))) return rc;
+  if (hb->narr && (rc = check_csr(hb->arr_offs, hb->narr, "committee table"))) return rc;
+  uint64_t ncomm = 0;  // committee ids must index coffs
+  for (uint64_t e = 0; hb->narr && e < hb->arr_offs[hb->narr]; ++e)
+    ncomm = std::max<uint64_t>(ncomm, (uint64_t)hb->arr_comm[e] + 1);
+  DeviceCtx* c;
+  if ((rc = acquire(&c))) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = c->ensure_stream())) return rc;
+  Stager st{c, c->stream};
+  pz_att_check_batch d = *hb;
+  d.slot = st.up(hb->slot, n);
+  d.justified_slot = st.up(hb->justified_slot, n);
+  d.shard_id = st.up(hb->shard_id, n);
+  d.n_oblique = st.up(hb->n_oblique, n);
+  d.block_slot = st.up(hb->block_slot, n);
+  std::vector<uint64_t> bo = rebase(hb->boffs, n);
+  d.bits = st.up(hb->bits ? hb->bits + hb->boffs[0] : nullptr, bo[n]);
+  d.boffs = st.up(bo.data(), n + 1);
+  if (hb->narr) {
+    const uint64_t ne = hb->arr_offs[hb->narr];
+    d.arr_offs = st.up(hb->arr_offs, hb->narr + 1);
+    d.arr_shard = st.up(hb->arr_shard, ne);
+    d.arr_comm = st.up(hb->arr_comm, ne);
+    d.coffs = st.up(hb->coffs, ncomm + 1);
+  }
+  d.status = st.up<int32_t>(nullptr, n);
+  d.committee = hb->committee ? st.up<uint32_t>(nullptr, n) : nullptr;
+  d.parents_start = hb->parents_start ? st.up<uint64_t>(nullptr, n) : nullptr;
+  if (st.rc) return st.rc;
+  st.check(launch_att_check(d, st.s), "pz_att_check_kernel");
+  st.down(hb->status, d.status, n);
+  if (hb->committee) st.down(hb->committee, d.committee, n);
+  if (hb->parents_start) st.down(hb->parents_start, d.parents_start, n);
+  return st.sync();
+}
+
+}  // extern "C"
