@@ -243,7 +243,8 @@ def wire_leg(args, torch, dist, dev, rank, world):
                    "records_per_gpu": n, "encoded_bytes_per_gpu": total,
                    "parallelism": "independent states per rank" if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "achieved": alg / (step_ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9,
-                     "unit": "GB/s", "frac": alg / (step_ms * 1e-3) / HBM_PEAK, "traffic": None,
+                     "unit": "GB/s", "frac": alg / (step_ms * 1e-3) / HBM_PEAK,
+                     "traffic": pmc_traffic(["pz_wire_val_kernel"]), "traffic_source": PMC_SUMMARY,
                      "kernel": "pz_wire_val_kernel (device time of the step, tile-status memset included)", "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": alg},
     }
@@ -352,7 +353,8 @@ def attcheck_leg(args, torch, dist, dev, rank, world):
         "config": {"workload": "%d attestations per GPU at configs[2]'s committee shape (65,536 validators), "
                                "5%% failing a check" % natt, "parallelism": "attestation-shard x%d" % world},
         "roofline": {"bound": "hbm", "achieved": alg / (step_ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9,
-                     "unit": "GB/s", "frac": alg / (step_ms * 1e-3) / HBM_PEAK, "traffic": None,
+                     "unit": "GB/s", "frac": alg / (step_ms * 1e-3) / HBM_PEAK,
+                     "traffic": pmc_traffic(["pz_att_check_kernel"]), "traffic_source": PMC_SUMMARY,
                      "kernel": "pz_att_check_kernel", "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": alg},
     }

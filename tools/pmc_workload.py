@@ -1,5 +1,7 @@
-"""Small fixed workload for rocprofv3 --pmc passes: 3 hash launches (1M x 512 B) and 3
-epoch steps (65,536 validators x 256 instances), plus a torch copy as a bandwidth yardstick."""
+"""Small fixed workload for rocprofv3 --pmc passes: 3 hash launches (1M x 512 B), 3 epoch
+steps (65,536 validators x 256 instances), 3 validator-span encodings (16.7 M records) and 3
+attestation-check batches (4M), the bench's workloads, plus a torch copy as a bandwidth
+yardstick."""
 import ctypes
 import os
 import sys
@@ -31,6 +33,34 @@ def main():
     x = torch.empty(nval * B, dtype=torch.int64, device=dev)
     for _ in range(3):
         x.copy_(de.balance.view(-1))
+    # the bench's wire and attcheck legs, same inputs
+    import bench  # noqa: E402
+    nw = 16 << 20
+    rng = np.random.default_rng(7)
+    cols_t = [torch.from_numpy(a.view(np.int64)).to(dev) for a in (
+        rng.integers(16, 49, size=nw, dtype=np.uint64), np.zeros(nw, np.uint64),
+        np.full(nw, 9999999999999999999, np.uint64))]
+    w_out = torch.empty(int(_lib.lib.dll.pz_wire_validators_bound(nw, 0)), dtype=torch.uint8, device=dev)
+    w_scr = torch.empty(int(_lib.lib.dll.pz_wire_scratch_bytes(nw)) // 8, dtype=torch.int64, device=dev)
+    w_tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    vc = _lib.ValidatorCols(None, None, None, None, None, None, *[t.data_ptr() for t in cols_t])
+    for _ in range(3):
+        _lib.lib.call("pz_dev_wire_validators", ctypes.byref(vc), nw, 11, w_out.data_ptr(), None, w_scr.data_ptr(),
+                      w_tot.data_ptr(), sh)
+    cols, tab = bench.attcheck_columns(1 << 22, seed=11)
+    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v.view(np.int32) if v.dtype == np.uint32
+                             else v).to(dev) for k, v in list(cols.items()) + list(tab.items())}
+    na = 1 << 22
+    st = torch.empty(na, dtype=torch.int32, device=dev)
+    cm = torch.empty(na, dtype=torch.int32, device=dev)
+    ps = torch.empty(na, dtype=torch.int64, device=dev)
+    b = _lib.AttCheckBatch(na, t["slot"].data_ptr(), t["justified_slot"].data_ptr(), t["shard_id"].data_ptr(),
+                           t["n_oblique"].data_ptr(), t["bits"].data_ptr(), t["boffs"].data_ptr(),
+                           t["block_slot"].data_ptr(), 0, 0, 128, 256, t["arr_offs"].data_ptr(),
+                           t["arr_shard"].data_ptr(), t["arr_comm"].data_ptr(), t["coffs"].data_ptr(),
+                           st.data_ptr(), cm.data_ptr(), ps.data_ptr())
+    for _ in range(3):
+        _lib.lib.call("pz_dev_check_attestations", ctypes.byref(b), sh)
     torch.cuda.synchronize()
     print("pmc workload done")
 
