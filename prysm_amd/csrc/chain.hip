@@ -313,18 +313,23 @@ struct Engine {
   DevArr<uint32_t> bitmaps;
   DevArr<uint64_t> totals;
   uint64_t words = 0, cap = 0;
-  // pending tally work, grouped per (vote slot, committee): the union of the bitfields of
-  // every queued attestation of that committee signing that hash (dedup makes the union
-  // exact); one device work item per group
+  // pending tally work: per queued attestation its committee, bitfield, the hash-log ids of
+  // its 64 signed parent hashes and a mask of the ones equal to an oblique parent hash; the
+  // device expands them into (attestation, parent) items (pz_vote_ids_kernel)
   std::vector<uint8_t> q_bits;
   std::vector<uint64_t> q_boffs{0};
-  std::vector<uint32_t> q_comm, q_item_att, q_item_slot;
-  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> q_groups_of_slot;  // slot -> (committee, group)
-  std::vector<uint32_t> q_touched;                                            // slots with groups
-  uint64_t q_err = 0;                                                         // tally panic flag (D2H)
-  DevArr<uint8_t> d_qbits;
-  DevArr<uint64_t> d_qboffs, d_err;
-  DevArr<uint32_t> d_qcomm, d_qia, d_qis;
+  std::vector<uint32_t> q_comm, q_ids;
+  std::vector<uint64_t> q_skip;
+  uint64_t q_err = 0;  // tally panic flag (D2H)
+  DevArr<uint8_t> d_qbits, present;
+  DevArr<uint64_t> d_qboffs, d_qskip, d_err;
+  DevArr<uint32_t> d_qcomm, d_qids;
+  DevArr<uint32_t> d_id_slot;  // hash-log id -> vote-cache slot, uploaded up to d_id_slot_n
+  uint64_t d_id_slot_n = 0;
+  // per (slot, committee) union bitfields and touched flags of the tally's first pass
+  DevArr<uint32_t> ubits, uflag;
+  DevArr<uint32_t> d_leader;
+  uint64_t ncomm = 0, cwords = 1;
   // epoch scratch
   DevArr<uint64_t> e_scal, e_mask, e_vote, e_total, e_rdyn, e_small, e_boffs;
   DevArr<uint32_t> e_blk, e_list, e_win, e_comm, e_shard;
@@ -344,7 +349,7 @@ struct Engine {
   // id; RecentBlockHashes carry ids too, so signed parent hashes are id ranges (no hashing of
   // 32-byte keys per vote) and the processAttestation messages are assembled on the device
   std::vector<H32> hlog;
-  std::vector<int32_t> hslot;  // vote-cache slot of each id (-1: not resolved yet)
+  std::vector<uint32_t> id_slot;  // vote-cache slot of each id (resolved when it is logged)
   DevArr<uint8_t> d_hlog;
   uint64_t d_hlog_n = 0;
   // processAttestation message batch (10-byte header, 64 parent ids, ShardBlockHash)
@@ -444,64 +449,98 @@ static uint32_t vote_slot(Engine& g, const H32& h) {
     const uint64_t nc = std::max<uint64_t>(64, 2 * g.cap);
     DevArr<uint32_t> bm;
     DevArr<uint64_t> tt;
+    DevArr<uint8_t> pr;
     check(bm.alloc(nc * g.words));
     check(tt.alloc(nc));
+    check(pr.alloc(nc));
     hchk(hipMemsetAsync(bm.p, 0, nc * g.words * 4, g.s), "memset");
     hchk(hipMemsetAsync(tt.p, 0, nc * 8, g.s), "memset");
+    hchk(hipMemsetAsync(pr.p, 0, nc, g.s), "memset");
     if (g.cap) {
       hchk(hipMemcpyAsync(bm.p, g.bitmaps.p, g.cap * g.words * 4, hipMemcpyDeviceToDevice, g.s), "D2D");
       hchk(hipMemcpyAsync(tt.p, g.totals.p, g.cap * 8, hipMemcpyDeviceToDevice, g.s), "D2D");
+      hchk(hipMemcpyAsync(pr.p, g.present.p, g.cap, hipMemcpyDeviceToDevice, g.s), "D2D");
     }
     hchk(hipStreamSynchronize(g.s), "sync");
     std::swap(g.bitmaps.p, bm.p);
     std::swap(g.bitmaps.n, bm.n);
     std::swap(g.totals.p, tt.p);
     std::swap(g.totals.n, tt.n);
+    std::swap(g.present.p, pr.p);
+    std::swap(g.present.n, pr.n);
+    // the union buffers are all zero between flushes (and a slot is only created outside
+    // one): reallocate them zeroed
+    check(g.ubits.alloc(nc * g.ncomm * g.cwords));
+    check(g.uflag.alloc(nc * g.ncomm));
+    hchk(hipMemsetAsync(g.ubits.p, 0, nc * g.ncomm * g.cwords * 4, g.s), "memset");
+    hchk(hipMemsetAsync(g.uflag.p, 0, nc * g.ncomm * 4, g.s), "memset");
+    hchk(hipStreamSynchronize(g.s), "sync");
     g.cap = nc;
   }
   return s;
 }
 
-static uint32_t log_hash(Engine& g, const H32& h) {
+// Every logged hash gets its vote-cache slot at once (a slot is storage; whether the Go map
+// has an entry for the hash is the slot's `present` flag, set by the tally).  `votable` is
+// false for an id that can never be tallied: a 32-byte oblique parent hash is only ever a
+// parent of its own attestation, which skips it (core.go:313-320).
+static uint32_t log_hash(Engine& g, const H32& h, bool votable = true) {
   g.hlog.push_back(h);
-  g.hslot.push_back(-1);
+  g.id_slot.push_back(votable ? vote_slot(g, h) : UINT32_MAX);
   return (uint32_t)(g.hlog.size() - 1);
-}
-
-static uint32_t slot_of_id(Engine& g, uint32_t id) {
-  int32_t& s = g.hslot[id];
-  if (s < 0) s = (int32_t)vote_slot(g, g.hlog[id]);
-  return (uint32_t)s;
 }
 
 // Enqueue the pending tally items (no sync); flush_votes_finish must follow a stream sync.
 static bool flush_votes_enqueue(Engine& g) {
-  if (g.q_item_att.empty()) return false;
+  if (g.q_comm.empty()) return false;
   PhaseTimer pt(g.prof[kProfFlush]);
-  upload(g, g.d_qbits, g.q_bits.data(), g.q_bits.size() + 0);
+  // the id -> slot map grows append-only: upload the new tail (keeping the device contents)
+  const uint64_t nid = g.id_slot.size();
+  if (nid > g.d_id_slot.n) {
+    DevArr<uint32_t> grown;
+    check(grown.alloc(std::max<uint64_t>(nid, 2 * g.d_id_slot.n)));
+    if (g.d_id_slot_n)
+      hchk(hipMemcpyAsync(grown.p, g.d_id_slot.p, g.d_id_slot_n * 4, hipMemcpyDeviceToDevice, g.s), "D2D");
+    std::swap(g.d_id_slot.p, grown.p);
+    std::swap(g.d_id_slot.n, grown.n);
+  }
+  if (nid > g.d_id_slot_n)
+    hchk(hipMemcpyAsync(g.d_id_slot.p + g.d_id_slot_n, g.id_slot.data() + g.d_id_slot_n, (nid - g.d_id_slot_n) * 4,
+                        hipMemcpyHostToDevice, g.s), "H2D");
+  g.d_id_slot_n = nid;
+  upload(g, g.d_qbits, g.q_bits.data(), g.q_bits.size());
   upload(g, g.d_qboffs, g.q_boffs.data(), g.q_boffs.size());
   upload(g, g.d_qcomm, g.q_comm.data(), g.q_comm.size());
-  upload(g, g.d_qia, g.q_item_att.data(), g.q_item_att.size());
-  upload(g, g.d_qis, g.q_item_slot.data(), g.q_item_slot.size());
+  upload(g, g.d_qids, g.q_ids.data(), g.q_ids.size());
+  upload(g, g.d_qskip, g.q_skip.data(), g.q_skip.size());
   check(g.d_err.alloc(1));
   hchk(hipMemsetAsync(g.d_err.p, 0, 8, g.s), "memset");
-  VoteArgs v;
+  VoteIdArgs v;
   std::memset(&v, 0, sizeof v);
   v.committee = g.committee.p;
   v.coffs = g.coffs.p;
   v.att_comm = g.d_qcomm.p;
   v.bits = g.d_qbits.p;
   v.boffs = g.d_qboffs.p;
-  v.item_att = g.d_qia.p;
-  v.item_slot = g.d_qis.p;
-  v.nitems = g.q_item_att.size();
+  v.ids = g.d_qids.p;
+  v.skip = g.d_qskip.p;
+  v.id_slot = g.d_id_slot.p;
+  v.natt = g.q_comm.size();
   v.balance = g.balance.p;
   v.nval = g.nval;
   v.bitmaps = g.bitmaps.p;
   v.words_per_slot = g.words;
   v.totals = g.totals.p;
+  v.present = g.present.p;
   v.err = g.d_err.p;
-  hchk(launch_vote_tally(v, g.s), "vote tally");
+  check(g.d_leader.alloc(g.q_comm.size() * 64 + 1));
+  v.ubits = g.ubits.p;
+  v.uflag = g.uflag.p;
+  v.leader = g.d_leader.p + 1;
+  v.nlead = g.d_leader.p;
+  v.ncomm = g.ncomm;
+  v.cwords = g.cwords;
+  hchk(launch_vote_ids(v, g.s), "vote tally");
   g.q_err = 0;
   hchk(hipMemcpyAsync(&g.q_err, g.d_err.p, 8, hipMemcpyDeviceToHost, g.s), "D2H");
   return true;
@@ -515,10 +554,8 @@ static void flush_votes_finish(Engine& g) {
   g.q_bits.clear();
   g.q_boffs.assign(1, 0);
   g.q_comm.clear();
-  g.q_item_att.clear();
-  g.q_item_slot.clear();
-  for (uint32_t sl : g.q_touched) g.q_groups_of_slot[sl].clear();
-  g.q_touched.clear();
+  g.q_ids.clear();
+  g.q_skip.clear();
   if (err) throw Panic{"calculateBlockVoteCache: CheckBit / validator index out of range"};
 }
 
@@ -539,7 +576,7 @@ static void signed_parents(Engine& g, const AState& A, uint64_t block_slot, cons
   const uint64_t end = block_slot - a.slot - (uint64_t)a.obl.size() + kCycle;
   if (start > end || end > A.recent_ids.size()) throw Panic{"slice bounds out of range (core.go:353)"};
   out.assign(A.recent_ids.begin() + (ptrdiff_t)start, A.recent_ids.begin() + (ptrdiff_t)end);
-  for (auto& o : a.obl) out.push_back(log_hash(g, bytes_to_hash(a.at(o.first), o.second)));
+  for (auto& o : a.obl) out.push_back(log_hash(g, bytes_to_hash(a.at(o.first), o.second), o.second != 32));
 }
 
 // getAttesterIndices (core.go:363-374) -> committee id.
@@ -580,44 +617,23 @@ static void process_attestation(Engine& g, uint64_t block_slot, const Att& a, st
 static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, std::vector<uint32_t>& parents) {
   signed_parents(g, *g.A, block_slot, a, parents);
   const uint32_t c = attester_committee(g, *g.C, a);
-  const uint64_t k = g.csize[c], nb = (k + 7) / 8;
+  const uint64_t k = g.csize[c];
+  uint64_t skip = 0;  // parents equal to one of the raw oblique parent hashes (core.go:313-320)
+  for (auto& o : a.obl)
+    if (o.second == 32)
+      for (size_t j = 0; j < parents.size(); ++j)
+        if (std::memcmp(g.hlog[parents[j]].b, a.at(o.first), 32) == 0) skip |= 1ull << j;
+  if (skip == ~0ull) return;  // no map access at all
+  if (g.A->cache_nil) throw Panic{"assignment to entry in nil map (core.go:323)"};
+  // the member loop reaches CheckBit(bitfield, 8 * len) when the committee is longer
+  if (k > 8ull * a.bf_len) throw Panic{"calculateBlockVoteCache: CheckBit index out of range (core.go:330)"};
+  g.q_comm.push_back(c);
+  g.q_skip.push_back(skip);
+  g.q_ids.insert(g.q_ids.end(), parents.begin(), parents.end());
   const uint8_t* bf = a.at(a.bf_off);
-  for (uint32_t id : parents) {
-    bool skip = false;
-    for (auto& o : a.obl)
-      if (o.second == 32 && std::memcmp(g.hlog[id].b, a.at(o.first), 32) == 0) skip = true;
-    if (skip) continue;
-    if (g.A->cache_nil) throw Panic{"assignment to entry in nil map (core.go:323)"};
-    // the member loop reaches CheckBit(bitfield, 8 * len) when the committee is longer
-    if (k > 8ull * a.bf_len) throw Panic{"calculateBlockVoteCache: CheckBit index out of range (core.go:330)"};
-    const uint32_t sl = slot_of_id(g, id);
-    if (sl >= g.q_groups_of_slot.size()) g.q_groups_of_slot.resize(std::max<size_t>(sl + 1, 2 * g.q_groups_of_slot.size()));
-    auto& gs = g.q_groups_of_slot[sl];
-    uint32_t grp = UINT32_MAX;
-    for (auto& e : gs)
-      if (e.first == c) grp = e.second;
-    if (grp == UINT32_MAX) {  // new (slot, committee) group with an all-zero bitfield
-      if (gs.empty()) g.q_touched.push_back(sl);
-      grp = (uint32_t)g.q_comm.size();
-      gs.push_back({c, grp});
-      g.q_comm.push_back(c);
-      g.q_item_att.push_back(grp);
-      g.q_item_slot.push_back(sl);
-      g.q_bits.resize(g.q_bits.size() + nb, 0);
-      g.q_boffs.push_back(g.q_bits.size());
-    }
-    uint8_t* dst = g.q_bits.data() + g.q_boffs[grp];
-    uint64_t i = 0;  // union of the bitfields, 8 bytes at a time (positions >= k are never read)
-    for (; i + 8 <= nb; i += 8) {
-      uint64_t x, y;
-      std::memcpy(&x, dst + i, 8);
-      std::memcpy(&y, bf + i, 8);
-      x |= y;
-      std::memcpy(dst + i, &x, 8);
-    }
-    for (; i < nb; ++i) dst[i] |= bf[i];
-  }
-  if (g.q_item_att.size() > (1u << 22)) flush_votes(g);
+  g.q_bits.insert(g.q_bits.end(), bf, bf + (k + 7) / 8);
+  g.q_boffs.push_back(g.q_bits.size());
+  if (g.q_comm.size() > (1u << 16)) flush_votes(g);
 }
 
 // processCrosslinks + CalculateRewards + next-cycle balance on the device -> next balance.
@@ -898,6 +914,9 @@ static int genesis(Engine& g) {
     }
   g.csize.resize(offs.size() - 1);
   for (size_t c = 0; c + 1 < offs.size(); ++c) g.csize[c] = offs[c + 1] - offs[c];
+  g.ncomm = g.csize.size();
+  g.cwords = 1;
+  for (uint64_t k : g.csize) g.cwords = std::max<uint64_t>(g.cwords, (k + 31) / 32);
   upload(g, g.committee, members.data(), members.size());
   upload(g, g.coffs, offs.data(), offs.size());
   upload(g, g.balance, g.h_balance.data(), n);
@@ -910,7 +929,7 @@ static int genesis(Engine& g) {
   hchk(hipStreamSynchronize(g.s), "sync");
   auto A = std::make_shared<AState>();
   g.hlog.clear();
-  g.hslot.clear();
+  g.id_slot.clear();
   g.d_hlog_n = 0;
   const uint32_t zero_id = log_hash(g, kZero);
   A->recent.assign(2 * kCycle, kZero);
@@ -1268,15 +1287,28 @@ int pz_chain_vote_totals(pz_chain* c, uint8_t* hashes, uint64_t* totals, uint64_
   std::lock_guard<std::mutex> lk(c->g.mu);
   Engine& g = c->g;
   const AState& A = g.has_cand ? *g.cand_A : *g.A;
-  *count = A.cache_nil ? 0 : g.slot_hash.size();
-  if (*count > cap) return PZ_OK;  // caller retries with a larger buffer
-  if (!*count) return PZ_OK;
+  // the Go map holds the hashes some attestation signed (present), with their totals
+  std::vector<uint8_t> pres;
+  std::vector<uint64_t> tot;
+  if (!A.cache_nil && !g.slot_hash.empty()) {
+    pres.resize(g.slot_hash.size());
+    tot.resize(g.slot_hash.size());
+    hipError_t e = hipSetDevice(g.device);
+    if (e == hipSuccess) e = hipMemcpyAsync(pres.data(), g.present.p, pres.size(), hipMemcpyDeviceToHost, g.s);
+    if (e == hipSuccess) e = hipMemcpyAsync(tot.data(), g.totals.p, tot.size() * 8, hipMemcpyDeviceToHost, g.s);
+    if (e == hipSuccess) e = hipStreamSynchronize(g.s);
+    if (e != hipSuccess) return hip_fail(e, "D2H vote totals");
+  }
+  uint64_t n = 0;
+  for (uint8_t p : pres) n += p;
+  *count = n;
+  if (n > cap || !n) return PZ_OK;  // caller retries with a larger buffer
   if (!hashes || !totals) return fail(PZ_EINVAL, "null pointer");
-  hipError_t e = hipSetDevice(g.device);
-  if (e == hipSuccess) e = hipMemcpyAsync(totals, g.totals.p, *count * 8, hipMemcpyDeviceToHost, g.s);
-  if (e == hipSuccess) e = hipStreamSynchronize(g.s);
-  if (e != hipSuccess) return hip_fail(e, "D2H vote totals");
-  for (uint64_t i = 0; i < *count; ++i) std::memcpy(hashes + 32 * i, g.slot_hash[i].b, 32);
+  for (uint64_t i = 0, j = 0; i < pres.size(); ++i)
+    if (pres[i]) {
+      std::memcpy(hashes + 32 * j, g.slot_hash[i].b, 32);
+      totals[j++] = tot[i];
+    }
   return PZ_OK;
 }
 

@@ -8,4 +8,30 @@
 namespace pz {
 typedef pz_vote_batch VoteArgs;
 hipError_t launch_vote_tally(const VoteArgs& a, hipStream_t s);
+
+// The block engine's tally (chain.hip): natt attestations x their 64 signed parent hashes.
+struct VoteIdArgs {
+  const uint32_t* committee;
+  const uint64_t* coffs;
+  const uint32_t* att_comm;  // natt
+  const uint8_t* bits;       // CSR bitfields
+  const uint64_t* boffs;     // natt+1
+  const uint32_t* ids;       // natt x 64 hash-log ids of the signed parent hashes
+  const uint64_t* skip;      // natt: bit j set = parent j equals an oblique parent hash
+  const uint32_t* id_slot;   // hash-log id -> vote-cache slot
+  uint64_t natt;
+  const uint64_t* balance;
+  uint64_t nval;
+  uint32_t* bitmaps;
+  uint64_t words_per_slot;
+  uint64_t* totals;
+  uint8_t* present;  // per slot: the Go map has an entry
+  uint64_t* err;
+  uint32_t* ubits;   // per (slot, committee) group: union bitfield, cwords words (zero between flushes)
+  uint32_t* uflag;   // per group: touched in this flush (zero between flushes)
+  uint32_t* leader;  // the items that tally their group (compact list, *nlead entries)
+  uint32_t* nlead;
+  uint64_t ncomm, cwords;
+};
+hipError_t launch_vote_ids(const VoteIdArgs& a, hipStream_t s);
 }  // namespace pz
