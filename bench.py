@@ -263,6 +263,99 @@ def wire_leg(args, torch, dist, dev, rank, world):
     return out
 
 
+def wire_att_leg(args, torch, dist, dev, rank, world, d_digests):
+    """SURVEY.md §8f row 1 for attestations: the hash bench's 1M AttestationRecords (configs[1])
+    proto3-encoded on the device from their SoA columns (pz_dev_wire_attestations), then
+    hashed (pz_dev_blake2b512_batch, CSR).  The encode is timed alone and as encode + hash;
+    the digests are checked against the main leg's, whose records are the same bytes."""
+    from prysm_amd import _lib, synth, wire
+
+    n = args.records
+    cols = synth.attestation_columns_512(n, seed=2 + rank)
+    t = {k: torch.from_numpy(cols[k].view(np.int64) if cols[k].dtype == np.uint64 else cols[k]).to(dev)
+         for k in wire.ATT_COLS}
+    c = _lib.AttestationCols(*[t[k].data_ptr() for k in wire.ATT_COLS])
+    ne, ns = int(cols["oblique_first"][-1]), int(cols["aggregate_sig_first"][-1])
+    nbytes = sum(int(cols[k][-1]) for k in ("justified_block_hash_offs", "shard_block_hash_offs",
+                                            "attester_bitfield_offs", "oblique_offs"))
+    d_out = torch.empty(int(_lib.lib.dll.pz_wire_attestations_bound(n, nbytes, ne, ns)) + 16, dtype=torch.uint8,
+                        device=dev)
+    d_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    d_scr = torch.empty(int(_lib.lib.dll.pz_wire_attestations_scratch_bytes(n)), dtype=torch.uint8, device=dev)
+    d_dig = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = ctypes.c_void_p(stream.cuda_stream)
+
+    def encode():
+        _lib.lib.call("pz_dev_wire_attestations", ctypes.byref(c), n, 0, d_out.data_ptr(), d_offs.data_ptr(),
+                      d_scr.data_ptr(), sh)
+
+    def encode_hash():
+        encode()
+        _lib.lib.call("pz_dev_blake2b512_batch", d_out.data_ptr(), d_offs.data_ptr(), n, d_dig.data_ptr(), 32, sh)
+
+    def timed(fn):
+        for _ in range(args.warmup + 5):
+            fn()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(args.steps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+        if world > 1:
+            wall = max_over_ranks(wall, torch, dist, dev)
+        return wall, e0.elapsed_time(e1) / args.steps
+
+    wall_e, ms_e = timed(encode)
+    wall_eh, ms_eh = timed(encode_hash)
+    in_bytes = sum(int(cols[k].nbytes) for k in wire.ATT_COLS)
+    alg = in_bytes + n * 512 + (n + 1) * 8
+    out = {
+        "metric": "AttestationRecords proto3-encoded (+ hashed) /s from device columns",
+        "value": n * world * args.steps / wall_eh,
+        "unit": "records/s",
+        "ms_per_step": wall_eh / args.steps * 1e3,
+        "scaling": "weak",
+        "config": {"workload": "the %d x 512-B AttestationRecords of configs[1], encoded from SoA columns then "
+                               "BLAKE2b-512[:32] (CSR)" % n, "parallelism": "record-shard x%d" % world},
+        "encode_only": {"value": n * world * args.steps / wall_e, "ms_per_step": wall_e / args.steps * 1e3},
+        "roofline": {"bound": "hbm", "achieved": alg / (ms_e * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": alg / (ms_e * 1e-3) / HBM_PEAK,
+                     "traffic": pmc_traffic(["pz_wire_att_size_kernel", "pz_wire_att_write_kernel"]),
+                     "traffic_source": PMC_SUMMARY,
+                     "kernel": "pz_wire_att_size_kernel + scan + pz_wire_att_write_kernel (device time of the encode)",
+                     "step_device_ms": ms_e, "encode_hash_device_ms": ms_eh, "algorithmic_bytes_per_launch": alg},
+    }
+    if d_digests is not None:
+        out["parity"] = "digests of the encoded records equal the hash leg's on all %d records: %s" % (
+            n, bool(torch.equal(d_dig, d_digests)))
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import cport
+        port = cport.WireAtt(cols, n)
+        try:
+            reps, t1 = 0, time.perf_counter()
+            while reps == 0 or time.perf_counter() - t1 < CPU_SAMPLE_S / 4:
+                port.run()
+                reps += 1
+            dt = time.perf_counter() - t1
+        finally:
+            port.close()
+        out["cpu_baseline"] = {"value": reps * n / dt, "unit": "records/s (encode only)", "cores": 1, "kind": "port",
+                               "sample": "%d marshals of the %d records (AoS, Size + MarshalTo per record, 1 thread, "
+                                         "oracle/c/wire_ref.c), %.2f s" % (reps, n, dt)}
+    return out
+
+
 ATT_BYTES = 65  # per attestation: 5 u64 columns + its boffs entry + the bitfield's last byte + 16 B out
 
 
@@ -570,6 +663,7 @@ def main():
     replay = None if args.no_replay else replay_leg(args, torch, dist, dev, rank, world)
     wire_out = None if args.no_wire else wire_leg(args, torch, dist, dev, rank, world)
     att_out = None if args.no_attcheck else attcheck_leg(args, torch, dist, dev, rank, world)
+    watt_out = None if args.no_wire else wire_att_leg(args, torch, dist, dev, rank, world, d_out)
 
     if rank == 0:
         total = n * world * args.steps
@@ -629,6 +723,8 @@ def main():
             line["wire"] = wire_out
         if att_out is not None:
             line["attcheck"] = att_out
+        if watt_out is not None:
+            line["wire_att"] = watt_out
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -115,6 +115,43 @@ int pz_wire_validators(const pz_validator_cols* v, uint64_t n, uint32_t field_nu
 int pz_dev_wire_validators(const pz_validator_cols* v, uint64_t n, uint32_t field_num, uint8_t* d_out,
                            uint64_t* d_offsets, void* d_scratch, uint64_t* d_total, void* stream);
 
+/* ---- a2 / §8f: proto3 encoding of AttestationRecords on the device -------------------
+ * Replaces golang/protobuf proto.Marshal(AttestationRecord) at types/attestation.go:51,56
+ * (and the records inside BeaconBlock field 8, block.go:69, and ActiveState field 1,
+ * state.go:141); record layout messages.pb.go:889-896.  Scalars: NULL = 0 everywhere.
+ * Bytes fields: CSR (data + offsets[n+1]; NULL offsets = empty).  oblique_parent_hashes: an
+ * element CSR (data + oblique_offs[m+1]) and the element range of record i,
+ * oblique_first[i] .. oblique_first[i+1] (NULL = none).  aggregate_sig: values and the range
+ * of record i, aggregate_sig_first[i] .. [i+1] (NULL = none).  field_num frames each record
+ * (8: BeaconBlock.attestations, 1: ActiveState.pending_attestations; 0: bare records, the
+ * bytes Attestation.Hash() hashes).  offsets[i] = start of record i, offsets[n] = length. */
+typedef struct pz_attestation_cols {
+  const uint64_t* slot;                    /* field 1 */
+  const uint64_t* shard_id;                /* field 2 */
+  const uint64_t* justified_slot;          /* field 3 */
+  const uint8_t*  justified_block_hash;    /* field 4 */
+  const uint64_t* justified_block_hash_offs;
+  const uint8_t*  shard_block_hash;        /* field 5 */
+  const uint64_t* shard_block_hash_offs;
+  const uint8_t*  attester_bitfield;       /* field 6 */
+  const uint64_t* attester_bitfield_offs;
+  const uint8_t*  oblique_parent_hashes;   /* field 7 */
+  const uint64_t* oblique_offs;
+  const uint64_t* oblique_first;
+  const uint64_t* aggregate_sig;           /* field 8 */
+  const uint64_t* aggregate_sig_first;
+} pz_attestation_cols;
+uint64_t pz_wire_attestations_bound(uint64_t n, uint64_t bytes_total, uint64_t n_oblique, uint64_t n_sig);
+uint64_t pz_wire_attestations_scratch_bytes(uint64_t n);
+/* Host pointers, synchronous; ranges must start at 0.  PZ_ERANGE when the encoding exceeds
+ * cap (*len still receives its length). */
+int pz_wire_attestations(const pz_attestation_cols* a, uint64_t n, uint32_t field_num, uint8_t* out,
+                         uint64_t cap, uint64_t* offsets, uint64_t* len);
+/* Device pointers, caller's stream; d_out holds pz_wire_attestations_bound(...) bytes,
+ * d_offsets n+1 entries (required). */
+int pz_dev_wire_attestations(const pz_attestation_cols* a, uint64_t n, uint32_t field_num, uint8_t* d_out,
+                             uint64_t* d_offsets, void* d_scratch, void* stream);
+
 /* ---- T/R: validator-set filters (casper/validator.go) ------------------------------- */
 #define PZ_KIND_ACTIVE 0  /* start <= dyn < end        casper/validator.go:45-53 */
 #define PZ_KIND_EXITED 1  /* start <  dyn && end <= dyn casper/validator.go:57-65 */

@@ -194,3 +194,34 @@ class AttCheck:
 
     def close(self):
         self.d.oracle_att_free(self.h)
+
+
+class WireAtt:
+    """oracle/c/wire_ref.c's AttestationRecord marshaller over AoS records built from the
+    ``pz_attestation_cols`` columns (dict as made by prysm_amd.wire.attestation_columns)."""
+
+    KEYS = ("slot", "shard_id", "justified_slot", "justified_block_hash", "justified_block_hash_offs",
+            "shard_block_hash", "shard_block_hash_offs", "attester_bitfield", "attester_bitfield_offs",
+            "oblique_parent_hashes", "oblique_offs", "oblique_first", "aggregate_sig", "aggregate_sig_first")
+
+    def __init__(self, cols, n):
+        d = dll()
+        vp, u64, sz = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t
+        d.oracle_wire_att_build.restype = vp
+        d.oracle_wire_att_build.argtypes = [vp] * 14 + [sz]
+        d.oracle_wire_att_free.argtypes = [vp]
+        d.oracle_wire_attestations.restype = u64
+        d.oracle_wire_attestations.argtypes = [vp, vp, u64, vp]
+        self.keep = [np.ascontiguousarray(cols[k]) for k in self.KEYS]
+        self.d, self.n = d, n
+        self.h = d.oracle_wire_att_build(*[a.ctypes.data for a in self.keep], n)
+        self.total = d.oracle_wire_attestations(self.h, None, 0, None)
+        self.out = np.empty(max(self.total, 1), dtype=np.uint8)
+        self.offs = np.empty(n + 1, dtype=np.uint64)
+
+    def run(self):
+        self.d.oracle_wire_attestations(self.h, self.out.ctypes.data, self.total, self.offs.ctypes.data)
+        return self.out[:self.total].tobytes(), self.offs
+
+    def close(self):
+        self.d.oracle_wire_att_free(self.h)

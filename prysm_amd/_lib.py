@@ -83,6 +83,10 @@ SIGNATURES = {
     "pz_wire_validators": [vp, u64, u32, vp, u64, vp, c_u64p],
     "pz_dev_wire_validators": [vp, u64, u32, vp, vp, vp, vp, vp],
     "pz_check_attestations": [vp],
+    "pz_wire_attestations_bound": [u64, u64, u64, u64],
+    "pz_wire_attestations_scratch_bytes": [u64],
+    "pz_wire_attestations": [vp, u64, u32, vp, u64, vp, c_u64p],
+    "pz_dev_wire_attestations": [vp, u64, u32, vp, vp, vp, vp],
     "pz_dev_check_attestations": [vp, vp],
 }
 
@@ -119,6 +123,16 @@ class ValidatorCols(ctypes.Structure):
     ]
 
 
+class AttestationCols(ctypes.Structure):
+    """Mirror of ``pz_attestation_cols`` (include/prysm_hip.h)."""
+    _fields_ = [
+        ("slot", vp), ("shard_id", vp), ("justified_slot", vp), ("justified_block_hash", vp),
+        ("justified_block_hash_offs", vp), ("shard_block_hash", vp), ("shard_block_hash_offs", vp),
+        ("attester_bitfield", vp), ("attester_bitfield_offs", vp), ("oblique_parent_hashes", vp),
+        ("oblique_offs", vp), ("oblique_first", vp), ("aggregate_sig", vp), ("aggregate_sig_first", vp),
+    ]
+
+
 class AttCheckBatch(ctypes.Structure):
     """Mirror of ``pz_att_check_batch`` (include/prysm_hip.h)."""
     _fields_ = [
@@ -133,7 +147,8 @@ SCAL_POP, SCAL_NACT, SCAL_ERR_XL, SCAL_ERR_RWD, SCAL_APPLIED, SCAL_NEXT_BAL, SCA
 SCAL_COUNT = 8
 KIND_ACTIVE, KIND_EXITED, KIND_QUEUED = 0, 1, 2
 _RESTYPES = {"pz_last_error": ctypes.c_char_p, "pz_chain_free": None, "pz_set_serial_threshold": u64,
-             "pz_wire_validators_bound": u64, "pz_wire_scratch_bytes": u64}
+             "pz_wire_validators_bound": u64, "pz_wire_scratch_bytes": u64,
+             "pz_wire_attestations_bound": u64, "pz_wire_attestations_scratch_bytes": u64}
 SERIAL_DEFAULT = 65536        # the library's default serial threshold (bytes)
 SERIAL_ON_GPU = (1 << 64) - 1  # pz_set_serial_threshold value that keeps every message on the GPU
 

@@ -1,0 +1,390 @@
+// proto3 encoding of AttestationRecord columns on the device.
+//
+// Replaces golang/protobuf `proto.Marshal(AttestationRecord)` at types/attestation.go:51
+// (Marshal) and :56 (Hash), and the records inside BeaconBlock (field 8, block.go:69) and
+// ActiveState (field 1, state.go:141).  The record is messages.pb.go:889-896: slot 1,
+// shard_id 2, justified_slot 3 (varints, omitted when 0), justified_block_hash 4,
+// shard_block_hash 5, attester_bitfield 6 (bytes, omitted when empty), oblique_parent_hashes 7
+// (repeated bytes: every element emitted, an empty one as `3a 00`), aggregate_sig 8 (packed
+// varints, omitted when empty).
+//
+// Records are hundreds of bytes, so a wave owns a record.  Three launches:
+//   size   one lane per record
+//   scan   rocPRIM inclusive scan of the sizes into offsets[1..n]
+//   write  one wave per record: lane 0 writes the scalar headers, the lanes copy the bytes
+//          fields and oblique elements together and write one signature varint each, into
+//          the wave's 1 KB LDS stage, which then leaves in coalesced stores
+// The columns of a record are read twice (size, write); the output is written once.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+#include <rocprim/device/device_scan.hpp>
+#include <vector>
+
+#include "runtime.h"
+
+namespace pz {
+namespace {
+
+constexpr int kThreads = 256, kWaves = kThreads / 64;
+
+struct AttArgs {
+  const uint64_t* col[3];  // slot, shard_id, justified_slot
+  const uint8_t* bdat[3];  // justified_block_hash, shard_block_hash, attester_bitfield
+  const uint64_t* boff[3];
+  const uint8_t* odat;  // oblique parent hashes: element CSR
+  const uint64_t* ooff;
+  const uint64_t* ofirst;  // record i owns elements ofirst[i] .. ofirst[i+1]
+  const uint64_t* sig;
+  const uint64_t* sfirst;  // record i owns values sfirst[i] .. sfirst[i+1]
+  uint64_t n;
+  uint32_t field, tag_len;
+  uint64_t* sizes;
+  uint64_t* offs;  // n+1
+  uint8_t* out;
+};
+
+__device__ __forceinline__ uint32_t vlen(uint64_t x) { return (uint32_t)((70 - __clzll(x | 1)) / 7); }
+
+__device__ __forceinline__ uint8_t* put_varint(uint8_t* p, uint64_t x) {
+  while (x >= 0x80) {
+    *p++ = (uint8_t)(x | 0x80);
+    x >>= 7;
+  }
+  *p++ = (uint8_t)x;
+  return p;
+}
+
+__device__ __forceinline__ uint64_t wsum(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+
+// Inclusive scan over the wave.
+__device__ __forceinline__ uint64_t wscan(uint64_t x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+struct Head {  // the record's scalar part, the same on every lane
+  uint64_t v[3], bl[3], b0[3];
+  uint64_t o0, o1, s0, s1;
+};
+
+__device__ __forceinline__ void load_head(const AttArgs& a, uint64_t i, Head& h) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    h.v[k] = a.col[k] ? a.col[k][i] : 0;
+    h.b0[k] = a.boff[k] ? a.boff[k][i] : 0;
+    h.bl[k] = a.boff[k] ? a.boff[k][i + 1] - h.b0[k] : 0;
+  }
+  h.o0 = a.ofirst ? a.ofirst[i] : 0;
+  h.o1 = a.ofirst ? a.ofirst[i + 1] : 0;
+  h.s0 = a.sfirst ? a.sfirst[i] : 0;
+  h.s1 = a.sfirst ? a.sfirst[i + 1] : 0;
+}
+
+// Fields 1-6 (scalars and bytes), the oblique elements and the packed signature body.
+__device__ __forceinline__ void record_parts(const AttArgs& a, const Head& h, uint64_t* fixed, uint64_t* obl,
+                                             uint64_t* sigb) {
+  uint64_t f = 0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    f += h.v[k] ? 1 + vlen(h.v[k]) : 0;
+    f += h.bl[k] ? 1 + vlen(h.bl[k]) + h.bl[k] : 0;
+  }
+  const int lane = threadIdx.x & 63;
+  uint64_t o = 0, s = 0;
+  for (uint64_t e = h.o0 + lane; e < h.o1; e += 64) {
+    const uint64_t l = a.ooff[e + 1] - a.ooff[e];
+    o += 1 + vlen(l) + l;
+  }
+  for (uint64_t e = h.s0 + lane; e < h.s1; e += 64) s += vlen(a.sig[e]);
+  *fixed = f;
+  *obl = wsum(o);
+  *sigb = wsum(s);
+}
+
+__device__ __forceinline__ uint64_t body_size(uint64_t fixed, uint64_t obl, uint64_t sigb) {
+  return fixed + obl + (sigb ? 1 + vlen(sigb) + sigb : 0);
+}
+
+// One lane per record: the records' head loads are coalesced across lanes and a record's
+// element / value loads are independent of each other (a wave per record made each of 1M
+// waves wait through a chain of dependent loads: 0.53 ms for the config-2 batch).
+extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_size_kernel(AttArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= a.n) return;
+  Head h;
+  load_head(a, i, h);
+  uint64_t body = 0, sigb = 0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    body += h.v[k] ? 1 + vlen(h.v[k]) : 0;
+    body += h.bl[k] ? 1 + vlen(h.bl[k]) + h.bl[k] : 0;
+  }
+#pragma unroll 4
+  for (uint64_t e = h.o0; e < h.o1; ++e) {
+    const uint64_t l = a.ooff[e + 1] - a.ooff[e];
+    body += 1 + vlen(l) + l;
+  }
+#pragma unroll 4
+  for (uint64_t e = h.s0; e < h.s1; ++e) sigb += vlen(a.sig[e]);
+  body += sigb ? 1 + vlen(sigb) + sigb : 0;
+  a.sizes[i] = a.field ? a.tag_len + vlen(body) + body : body;
+}
+
+// Lane-parallel byte copy.
+__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t len) {
+  for (uint64_t j = threadIdx.x & 63; j < len; j += 64) dst[j] = src[j];
+}
+
+// Write record `h` at p (HBM or the wave's LDS stage).  Lane 0 writes the headers; the lanes
+// copy each bytes field / oblique element together and write one signature varint each.
+__device__ __forceinline__ void write_record(const AttArgs& a, const Head& h, uint64_t body, uint64_t sigb,
+                                             uint8_t* p) {
+  const int lane = threadIdx.x & 63;
+  if (a.field) {  // the frame, then fields in ascending order
+    if (lane == 0) {
+      uint8_t* q = put_varint(p, ((uint64_t)a.field << 3) | 2);
+      put_varint(q, body);
+    }
+    p += a.tag_len + vlen(body);
+  }
+  for (int k = 0; k < 3; ++k)  // fields 1-3
+    if (h.v[k]) {
+      if (lane == 0) {
+        p[0] = (uint8_t)((k + 1) << 3);
+        put_varint(p + 1, h.v[k]);
+      }
+      p += 1 + vlen(h.v[k]);
+    }
+  for (int k = 0; k < 3; ++k)  // fields 4-6
+    if (h.bl[k]) {
+      const uint32_t hl = 1 + vlen(h.bl[k]);
+      if (lane == 0) {
+        p[0] = (uint8_t)(((k + 4) << 3) | 2);
+        put_varint(p + 1, h.bl[k]);
+      }
+      copy_bytes(p + hl, a.bdat[k] + h.b0[k], h.bl[k]);
+      p += hl + h.bl[k];
+    }
+  for (uint64_t e = h.o0; e < h.o1; ++e) {  // field 7, element by element
+    const uint64_t b0 = a.ooff[e], l = a.ooff[e + 1] - b0;
+    const uint32_t hl = 1 + vlen(l);
+    if (lane == 0) {
+      p[0] = (7 << 3) | 2;
+      put_varint(p + 1, l);
+    }
+    copy_bytes(p + hl, a.odat + b0, l);
+    p += hl + l;
+  }
+  if (sigb) {  // field 8: packed varints, one value per lane
+    if (lane == 0) {
+      p[0] = (8 << 3) | 2;
+      put_varint(p + 1, sigb);
+    }
+    p += 1 + vlen(sigb);
+    for (uint64_t e0 = h.s0; e0 < h.s1; e0 += 64) {
+      const uint64_t e = e0 + lane;
+      const uint64_t x = e < h.s1 ? a.sig[e] : 0;
+      const uint64_t sz = e < h.s1 ? vlen(x) : 0;
+      const uint64_t inc = wscan(sz);
+      if (e < h.s1) put_varint(p + inc - sz, x);
+      p += __shfl(inc, 63, 64);
+    }
+  }
+}
+
+// A record that fits the wave's LDS stage is assembled there first: the source loads of all
+// its fields are then independent of the (LDS) stores, so they overlap instead of each field
+// waiting on the previous one's global store; the stage then leaves in coalesced stores.
+constexpr uint32_t kStage = 1024;
+
+extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_write_kernel(AttArgs a) {
+  __shared__ uint8_t stage[kWaves][kStage];
+  const uint64_t i = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (i >= a.n) return;
+  const int lane = threadIdx.x & 63;
+  Head h;
+  load_head(a, i, h);
+  uint64_t fixed, obl, sigb;
+  record_parts(a, h, &fixed, &obl, &sigb);
+  const uint64_t body = body_size(fixed, obl, sigb);
+  const uint64_t o = a.offs[i], size = a.offs[i + 1] - o;
+  if (size > kStage) {
+    write_record(a, h, body, sigb, a.out + o);
+    return;
+  }
+  uint8_t* st = stage[threadIdx.x >> 6];
+  write_record(a, h, body, sigb, st);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  for (uint64_t j = lane; j < size; j += 64) a.out[o + j] = st[j];
+}
+
+int att_args(const pz_attestation_cols* c, uint64_t n, uint32_t field_num, AttArgs* a) {
+  if (!c) return fail(PZ_EINVAL, "columns are null");
+  if (field_num >= (1u << 29)) return fail(PZ_EINVAL, "field number %u out of range", field_num);
+  *a = AttArgs{};
+  a->col[0] = c->slot;
+  a->col[1] = c->shard_id;
+  a->col[2] = c->justified_slot;
+  a->bdat[0] = c->justified_block_hash;
+  a->boff[0] = c->justified_block_hash_offs;
+  a->bdat[1] = c->shard_block_hash;
+  a->boff[1] = c->shard_block_hash_offs;
+  a->bdat[2] = c->attester_bitfield;
+  a->boff[2] = c->attester_bitfield_offs;
+  a->odat = c->oblique_parent_hashes;
+  a->ooff = c->oblique_offs;
+  a->ofirst = c->oblique_first;
+  a->sig = c->aggregate_sig;
+  a->sfirst = c->aggregate_sig_first;
+  for (int k = 0; k < 3; ++k)
+    if (a->boff[k] && !a->bdat[k]) return fail(PZ_EINVAL, "bytes column without data");
+  if (a->ofirst && (!a->ooff || !a->odat)) return fail(PZ_EINVAL, "oblique elements without data");
+  if (a->sfirst && !a->sig) return fail(PZ_EINVAL, "signature ranges without values");
+  a->n = n;
+  a->field = field_num;
+  uint64_t tag = ((uint64_t)field_num << 3) | 2;
+  a->tag_len = 1;
+  while (tag >= 0x80) {
+    tag >>= 7;
+    ++a->tag_len;
+  }
+  return PZ_OK;
+}
+
+size_t scan_bytes(uint64_t n) {
+  size_t bytes = 0;
+  (void)rocprim::inclusive_scan(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)n,
+                                rocprim::plus<uint64_t>(), (hipStream_t)0);
+  return (bytes + 255) & ~size_t(255);
+}
+
+// sizes -> offsets (offs[0] = 0, offs[n] = total); scratch: n sizes then the scan's storage.
+hipError_t launch_sizes_offsets(AttArgs a, void* scratch, hipStream_t s) {
+  a.sizes = static_cast<uint64_t*>(scratch);
+  hipError_t e = hipMemsetAsync(a.offs, 0, 8, s);
+  if (e != hipSuccess || !a.n) return e;
+  hipLaunchKernelGGL(pz_wire_att_size_kernel, dim3((uint32_t)((a.n + kThreads - 1) / kThreads)), dim3(kThreads), 0, s,
+                     a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  size_t bytes = scan_bytes(a.n);
+  return rocprim::inclusive_scan(static_cast<uint8_t*>(scratch) + ((a.n * 8 + 255) & ~uint64_t(255)), bytes, a.sizes,
+                                 a.offs + 1, (size_t)a.n, rocprim::plus<uint64_t>(), s);
+}
+
+hipError_t launch_write(const AttArgs& a, hipStream_t s) {
+  if (!a.n) return hipSuccess;
+  hipLaunchKernelGGL(pz_wire_att_write_kernel, dim3((uint32_t)((a.n + kWaves - 1) / kWaves)), dim3(kThreads), 0, s,
+                     a);
+  return hipGetLastError();
+}
+
+}  // namespace
+}  // namespace pz
+
+using namespace pz;
+
+extern "C" {
+
+uint64_t pz_wire_attestations_scratch_bytes(uint64_t n) { return ((n * 8 + 255) & ~uint64_t(255)) + scan_bytes(n); }
+
+uint64_t pz_wire_attestations_bound(uint64_t n, uint64_t bytes_total, uint64_t n_oblique, uint64_t n_sig) {
+  // frame 5+10, fields 1-3 3x11, fields 4-6 3x(1+10), field 8 header 11, per element 11, per value 10
+  return n * (15 + 33 + 33 + 11) + bytes_total + n_oblique * 11 + n_sig * 10;
+}
+
+int pz_dev_wire_attestations(const pz_attestation_cols* c, uint64_t n, uint32_t field_num, uint8_t* d_out,
+                             uint64_t* d_offsets, void* d_scratch, void* stream) {
+  AttArgs a;
+  int rc = att_args(c, n, field_num, &a);
+  if (rc) return rc;
+  if (!d_offsets || !d_scratch || (n && !d_out)) return fail(PZ_EINVAL, "null device pointer");
+  a.out = d_out;
+  a.offs = d_offsets;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e = launch_sizes_offsets(a, d_scratch, s);
+  if (e == hipSuccess) e = launch_write(a, s);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "pz_wire_att kernels");
+}
+
+int pz_wire_attestations(const pz_attestation_cols* c, uint64_t n, uint32_t field_num, uint8_t* out, uint64_t cap,
+                         uint64_t* offsets, uint64_t* len) {
+  if (!len) return fail(PZ_EINVAL, "len is null");
+  *len = 0;
+  AttArgs a;
+  int rc = att_args(c, n, field_num, &a);
+  if (rc) return rc;
+  if (n == 0) {
+    if (offsets) offsets[0] = 0;
+    return PZ_OK;
+  }
+  for (int k = 0; k < 3; ++k)
+    if (a.boff[k] && (rc = check_csr(a.boff[k], n, "bytes column"))) return rc;
+  if (a.ofirst && (rc = check_csr(a.ofirst, n, "oblique ranges"))) return rc;
+  if (a.sfirst && (rc = check_csr(a.sfirst, n, "signature ranges"))) return rc;
+  const uint64_t ne = a.ofirst ? c->oblique_first[n] : 0, ns = a.sfirst ? c->aggregate_sig_first[n] : 0;
+  if (a.ofirst && c->oblique_first[0] != 0) return fail(PZ_EINVAL, "oblique ranges must start at 0");
+  if (a.sfirst && c->aggregate_sig_first[0] != 0) return fail(PZ_EINVAL, "signature ranges must start at 0");
+  if (ne && (rc = check_csr(c->oblique_offs, ne, "oblique elements"))) return rc;
+  DeviceCtx* ctx;
+  if ((rc = acquire(&ctx))) return rc;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if ((rc = ctx->ensure_stream())) return rc;
+  Stager st{ctx, ctx->stream};
+  uint64_t bytes_total = 0;
+  std::vector<uint64_t> rb[3];
+  for (int k = 0; k < 3; ++k) {
+    if (a.col[k]) a.col[k] = st.up(a.col[k], n);
+    if (a.boff[k]) {
+      rb[k] = rebase(a.boff[k], n);
+      a.bdat[k] = st.up(a.bdat[k] + a.boff[k][0], rb[k][n]);
+      a.boff[k] = st.up(rb[k].data(), n + 1);
+      bytes_total += rb[k][n];
+    }
+  }
+  std::vector<uint64_t> oo;
+  if (a.ofirst) {
+    a.ofirst = st.up(a.ofirst, n + 1);
+    if (ne) {
+      oo = rebase(c->oblique_offs, ne);
+      a.odat = st.up(c->oblique_parent_hashes + c->oblique_offs[0], oo[ne]);
+      a.ooff = st.up(oo.data(), ne + 1);
+      bytes_total += oo[ne];
+    } else {
+      a.ooff = st.up(c->oblique_offs, 1);
+    }
+  }
+  if (a.sfirst) {
+    a.sfirst = st.up(a.sfirst, n + 1);
+    a.sig = st.up(c->aggregate_sig, std::max<uint64_t>(ns, 1));
+  }
+  void* scratch = st.up<uint8_t>(nullptr, pz_wire_attestations_scratch_bytes(n));
+  a.offs = st.zeros<uint64_t>(n + 1);
+  a.out = st.up<uint8_t>(nullptr, pz_wire_attestations_bound(n, bytes_total, ne, ns));
+  if (st.rc) return st.rc;
+  st.check(launch_sizes_offsets(a, scratch, st.s), "pz_wire_att_size_kernel");
+  uint64_t total = 0;
+  st.down(&total, a.offs + n, 1);
+  if (st.sync()) return st.rc;
+  *len = total;
+  if (total > cap) return fail(PZ_ERANGE, "output needs %llu bytes, capacity %llu", (unsigned long long)total,
+                               (unsigned long long)cap);
+  if (!out) return fail(PZ_EINVAL, "out is null");
+  st.check(launch_write(a, st.s), "pz_wire_att_write_kernel");
+  st.down(out, a.out, total);
+  if (offsets) st.down(offsets, a.offs, n + 1);
+  return st.sync();
+}
+
+}  // extern "C"

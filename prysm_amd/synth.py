@@ -122,6 +122,31 @@ def attestation_records_512(n, seed=2):
     return rec
 
 
+def attestation_columns_512(n, seed=2):
+    """The SoA columns of ``attestation_records_512(n, seed)`` (same random draws), in the CSR
+    layout of ``pz_attestation_cols``: encoding them gives exactly those 512-byte records."""
+    rng = np.random.default_rng(seed)
+    u64 = np.uint64
+    slot = rng.integers(1 << 14, 1 << 21, size=n, dtype=u64)
+    shard = rng.integers(128, 1024, size=n, dtype=u64)
+    jslot = rng.integers(1 << 14, 1 << 21, size=n, dtype=u64)
+    jbh = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    sbh = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    bf = rng.integers(0, 256, size=(n, BITFIELD_BYTES), dtype=np.uint8)
+    obl = np.stack([rng.integers(0, 256, size=(n, 32), dtype=np.uint8) for _ in range(N_OBLIQUE)], axis=1)
+    sig = rng.integers(1 << 63, (1 << 64) - 1, size=(n, 2), dtype=u64, endpoint=True)
+
+    def fixed(width, count):
+        return np.arange(count + 1, dtype=u64) * u64(width)
+
+    return dict(slot=slot, shard_id=shard, justified_slot=jslot,
+                justified_block_hash=jbh.reshape(-1), justified_block_hash_offs=fixed(32, n),
+                shard_block_hash=sbh.reshape(-1), shard_block_hash_offs=fixed(32, n),
+                attester_bitfield=bf.reshape(-1), attester_bitfield_offs=fixed(BITFIELD_BYTES, n),
+                oblique_parent_hashes=obl.reshape(-1), oblique_offs=fixed(32, n * N_OBLIQUE),
+                oblique_first=fixed(N_OBLIQUE, n), aggregate_sig=sig.reshape(-1), aggregate_sig_first=fixed(2, n))
+
+
 def genesis_committee_sizes(nval):
     """Shard ids and member counts of the slot-0 committees of the genesis shuffle
     (types/state.go:68-78 -> casper/sharding.go:27-53).  Sizes depend only on the validator

@@ -210,3 +210,46 @@ def validators_device(v, field_num=11, with_offsets=False):
                   _lib.ptr(offs), _lib.ctypes.byref(length))
     raw = out[:length.value].tobytes()
     return (raw, offs) if with_offsets else raw
+
+
+ATT_COLS = ("slot", "shard_id", "justified_slot", "justified_block_hash", "justified_block_hash_offs",
+            "shard_block_hash", "shard_block_hash_offs", "attester_bitfield", "attester_bitfield_offs",
+            "oblique_parent_hashes", "oblique_offs", "oblique_first", "aggregate_sig", "aggregate_sig_first")
+
+
+def attestation_columns(atts):
+    """pb.AttestationRecord list -> the SoA / CSR columns of ``pz_attestation_cols``."""
+    n = len(atts)
+    cols = {k: np.ascontiguousarray([getattr(a, k) for a in atts], dtype=_U64)
+            for k in ("slot", "shard_id", "justified_slot")}
+    for k in ("justified_block_hash", "shard_block_hash", "attester_bitfield"):
+        cols[k], cols[k + "_offs"] = _csr([bytes(getattr(a, k)) for a in atts], n)
+    elems = [bytes(h) for a in atts for h in a.oblique_parent_hashes]
+    cols["oblique_parent_hashes"], cols["oblique_offs"] = _csr(elems, len(elems))
+    cols["oblique_first"] = np.zeros(n + 1, dtype=_U64)
+    cols["oblique_first"][1:] = np.cumsum([len(a.oblique_parent_hashes) for a in atts])
+    cols["aggregate_sig"] = np.ascontiguousarray([v & M64 for a in atts for v in a.aggregate_sig] or [0], dtype=_U64)
+    cols["aggregate_sig_first"] = np.zeros(n + 1, dtype=_U64)
+    cols["aggregate_sig_first"][1:] = np.cumsum([len(a.aggregate_sig) for a in atts])
+    return cols
+
+
+def attestations_device(cols, n, field_num=0):
+    """AttestationRecords encoded on the GPU by ``pz_wire_attestations`` from columns (see
+    :func:`attestation_columns`).  Returns (bytes, offsets[n+1]); with ``field_num=0`` the
+    records are bare, as Attestation.Hash() hashes them."""
+    from prysm_amd import _lib
+
+    c = _lib.AttestationCols(*[_lib.ptr(np.ascontiguousarray(cols[k])) if cols.get(k) is not None else None
+                               for k in ATT_COLS])
+    nbytes = sum(int(cols[k][-1]) for k in ("justified_block_hash_offs", "shard_block_hash_offs",
+                                            "attester_bitfield_offs", "oblique_offs")) if n else 0
+    ne = int(cols["oblique_first"][-1]) if n else 0
+    ns = int(cols["aggregate_sig_first"][-1]) if n else 0
+    cap = int(_lib.lib.dll.pz_wire_attestations_bound(n, nbytes, ne, ns))
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    offs = np.empty(n + 1, dtype=_U64)
+    length = _lib.ctypes.c_uint64(0)
+    _lib.lib.call("pz_wire_attestations", _lib.ctypes.byref(c), n, field_num, _lib.ptr(out), cap, _lib.ptr(offs),
+                  _lib.ctypes.byref(length))
+    return out[:length.value].tobytes(), offs

@@ -146,3 +146,19 @@ def test_c_port_validators_match_protobuf_runtime():
                          balance=int(v.balance[i]), start_dynasty=int(v.start_dynasty[i]),
                          end_dynasty=int(v.end_dynasty[i]))
     assert cport.wire_validators(v) == o.SerializeToString() == wire.validators(v)
+
+
+def test_c_port_attestations_match_protobuf_runtime():
+    """oracle/c/wire_ref.c's AttestationRecord marshaller (bench.py's wire_att cpu_baseline)
+    against the runtime, on records that hit every field rule."""
+    from oracle import cport
+
+    rng = np.random.default_rng(33)
+    atts = [rand_att(rng) for _ in range(400)]
+    port = cport.WireAtt(wire.attestation_columns(atts), len(atts))
+    try:
+        raw, offs = port.run()
+    finally:
+        port.close()
+    for i, a in enumerate(atts):
+        assert raw[int(offs[i]):int(offs[i + 1])] == o_att(a).SerializeToString(), i

@@ -1,0 +1,89 @@
+"""Device proto3 encoder of AttestationRecord columns (prysm_amd/csrc/wire_att.hip) against
+Google's protobuf runtime over the oracle schema (oracle/schema.py, pinned to
+messages.pb.go:889-896) and the host encoder (prysm_amd/wire.py); and the config-2 records
+(synth.attestation_records_512) rebuilt from their columns.  Byte-exact."""
+import numpy as np
+import pytest
+
+from prysm_amd import _lib, pb, synth, wire
+from test_wire import o_att, rand_att, rand_bytes, rand_u64
+
+pytestmark = pytest.mark.gpu
+
+
+def varint(x):
+    out = bytearray()
+    while x >= 0x80:
+        out.append((x & 0x7F) | 0x80)
+        x >>= 7
+    out.append(x)
+    return bytes(out)
+
+
+@pytest.mark.parametrize("n,seed", [(1, 1), (7, 2), (300, 3), (2000, 4)])
+def test_bare_records_match_protobuf_runtime(n, seed):
+    rng = np.random.default_rng(seed)
+    atts = [rand_att(rng) for _ in range(n)]
+    raw, offs = wire.attestations_device(wire.attestation_columns(atts), n, 0)
+    assert offs[0] == 0 and offs[-1] == len(raw)
+    for i, a in enumerate(atts):
+        rec = raw[int(offs[i]):int(offs[i + 1])]
+        assert rec == o_att(a).SerializeToString() == wire.attestation_record(a), i
+
+
+@pytest.mark.parametrize("field_num", [8, 1, 16, (1 << 29) - 1])
+def test_framed_records(field_num):
+    rng = np.random.default_rng(field_num % 97)
+    atts = [rand_att(rng) for _ in range(500)]
+    raw, offs = wire.attestations_device(wire.attestation_columns(atts), len(atts), field_num)
+    tag = varint((field_num << 3) | 2)
+    want = b"".join(tag + varint(len(r)) + r for r in (wire.attestation_record(a) for a in atts))
+    assert raw == want
+
+
+def test_long_repeated_fields_and_empty_elements():
+    """More than 64 oblique hashes / signature values (several wave chunks), empty elements
+    (emitted as 3a 00), all-zero scalars, and records with nothing at all."""
+    rng = np.random.default_rng(9)
+    atts = [pb.AttestationRecord(slot=0, shard_id=0, justified_slot=0, justified_block_hash=b"", shard_block_hash=b"",
+                                 attester_bitfield=b"", oblique_parent_hashes=[], aggregate_sig=[])]
+    atts.append(pb.AttestationRecord(slot=5, shard_id=0, justified_slot=(1 << 64) - 1, justified_block_hash=b"x",
+                                     shard_block_hash=b"", attester_bitfield=rand_bytes(rng, 300, 301),
+                                     oblique_parent_hashes=[rand_bytes(rng, 0, 40) for _ in range(150)] + [b""],
+                                     aggregate_sig=[rand_u64(rng) for _ in range(200)]))
+    atts.append(pb.AttestationRecord(slot=1, shard_id=2, justified_slot=3, justified_block_hash=b"",
+                                     shard_block_hash=b"", attester_bitfield=b"", oblique_parent_hashes=[b""] * 65,
+                                     aggregate_sig=[0] * 70))
+    raw, offs = wire.attestations_device(wire.attestation_columns(atts), len(atts), 0)
+    for i, a in enumerate(atts):
+        assert raw[int(offs[i]):int(offs[i + 1])] == o_att(a).SerializeToString(), i
+    assert offs[1] == 0  # the empty record encodes to nothing
+
+
+def test_empty_batch():
+    raw, offs = wire.attestations_device(wire.attestation_columns([]), 0, 0)
+    assert raw == b"" and list(offs) == [0]
+
+
+def test_config2_records_rebuilt_from_columns():
+    """synth.attestation_columns_512 encodes to exactly the 512-byte records the hash bench
+    uses (BASELINE configs[1]), at 2^18 records."""
+    n = 1 << 18
+    cols = synth.attestation_columns_512(n, seed=2)
+    raw, offs = wire.attestations_device(cols, n, 0)
+    assert np.array_equal(offs, np.arange(n + 1, dtype=np.uint64) * 512)
+    assert raw == synth.attestation_records_512(n, seed=2).tobytes()
+
+
+def test_capacity_error():
+    rng = np.random.default_rng(5)
+    atts = [rand_att(rng) for _ in range(50)]
+    cols = wire.attestation_columns(atts)
+    c = _lib.AttestationCols(*[_lib.ptr(np.ascontiguousarray(cols[k])) for k in wire.ATT_COLS])
+    out = np.empty(8, dtype=np.uint8)
+    length = _lib.ctypes.c_uint64(0)
+    with pytest.raises(_lib.PzError) as e:
+        _lib.lib.call("pz_wire_attestations", _lib.ctypes.byref(c), 50, 0, _lib.ptr(out), 8, None,
+                      _lib.ctypes.byref(length))
+    assert e.value.code == _lib.PZ_ERANGE
+    assert length.value == sum(len(wire.attestation_record(a)) for a in atts)

@@ -1,6 +1,6 @@
 """Small fixed workload for rocprofv3 --pmc passes: 3 hash launches (1M x 512 B), 3 epoch
 steps (65,536 validators x 256 instances), 3 validator-span encodings (16.7 M records) and 3
-attestation-check batches (4M), the bench's workloads, plus a torch copy as a bandwidth
+attestation-check batches (4M) and 3 attestation encodings (1M), the bench's workloads, plus a torch copy as a bandwidth
 yardstick."""
 import ctypes
 import os
@@ -61,6 +61,18 @@ def main():
                            st.data_ptr(), cm.data_ptr(), ps.data_ptr())
     for _ in range(3):
         _lib.lib.call("pz_dev_check_attestations", ctypes.byref(b), sh)
+    # the bench's wire_att leg: the 1M config-2 records encoded from their columns
+    from prysm_amd import wire
+    cols = synth.attestation_columns_512(n, seed=2)
+    tc = {k: torch.from_numpy(cols[k].view(np.int64) if cols[k].dtype == np.uint64 else cols[k]).to(dev)
+          for k in wire.ATT_COLS}
+    ac = _lib.AttestationCols(*[tc[k].data_ptr() for k in wire.ATT_COLS])
+    a_out = torch.empty(n * 512 + 16, dtype=torch.uint8, device=dev)
+    a_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    a_scr = torch.empty(int(_lib.lib.dll.pz_wire_attestations_scratch_bytes(n)), dtype=torch.uint8, device=dev)
+    for _ in range(3):
+        _lib.lib.call("pz_dev_wire_attestations", ctypes.byref(ac), n, 0, a_out.data_ptr(), a_offs.data_ptr(),
+                      a_scr.data_ptr(), sh)
     torch.cuda.synchronize()
     print("pmc workload done")
 
