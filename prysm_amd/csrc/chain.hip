@@ -281,6 +281,25 @@ struct DevArr {
   }
 };
 
+// Grow-only pinned host buffer (hipHostMalloc), for asynchronous-capable H2D / D2H.
+struct PinBuf {
+  uint8_t* p = nullptr;
+  size_t n = 0;
+  int reserve(size_t bytes) {
+    if (bytes <= n && p) return PZ_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipHostMalloc((void**)&p, std::max<size_t>(bytes, 1), hipHostMallocDefault);
+    if (e != hipSuccess) return hip_fail(e, "hipHostMalloc");
+    n = bytes;
+    return PZ_OK;
+  }
+  ~PinBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
 enum ProfSlot {
   kProfParse, kProfHash1, kProfCheck, kProfQueue, kProfFlush, kProfRecalc, kProfMsgHash, kProfWalk, kProfProcess,
   kProfCount, kProfSlots
@@ -346,6 +365,7 @@ struct Engine {
   DevArr<uint32_t> e_blk, e_list, e_win, e_comm, e_shard;
   DevArr<uint8_t> e_bits;
   // hashing scratch
+  PinBuf pin_msgs, pin_offs, pin_dig;  // pinned staging of the digest batch
   DevArr<uint8_t> h_in, h_out;
   DevArr<uint64_t> h_offs;
   // chain
@@ -1023,38 +1043,108 @@ static void sync_hash_log(Engine& g) {
 static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, pz_att_result* ar) {
   const uint64_t n = blocks.size();
   const auto t_hash1 = std::chrono::steady_clock::now();
-  // device pass 1: block digests, attestation Hash and Key
-  std::string buf;
-  std::vector<uint64_t> ho{0};
-  uint64_t natt = 0;
+  // device pass 1: block digests, attestation Hash and Key, built straight into pinned
+  // memory (one H2D, one 32-byte-digest D2H); hash_many (64-byte digests, host threads for
+  // serial chains) only when a message reaches the serial threshold
+  uint64_t natt = 0, total = 0;
   for (auto& b : blocks) {
-    buf.append((const char*)b.data, b.len);
-    ho.push_back(buf.size());
     natt += b.atts.size();
+    total += b.len;
+    for (auto& a : b.atts) total += a->enc.size() + 10 + a->sbh_len + 32 * a->obl.size();
   }
+  const uint64_t nmsg = n + 2 * natt, thr = serial_threshold();
+  bool any_long = false;
+  for (auto& b : blocks) any_long |= b.len >= thr;
   for (auto& b : blocks)
-    for (auto& a : b.atts) {
-      buf += a->enc;
-      ho.push_back(buf.size());
+    for (auto& a : b.atts) any_long |= a->enc.size() >= thr || 10 + a->sbh_len + 32 * a->obl.size() >= thr;
+  std::vector<uint8_t> dg_slow;
+  const uint8_t* dg;
+  uint64_t dstride;
+  if (!any_long) {
+    check(g.pin_msgs.reserve(total + 16));
+    check(g.pin_offs.reserve((nmsg + 1) * 8));
+    check(g.pin_dig.reserve(nmsg * 32));
+    uint8_t* buf = g.pin_msgs.p;
+    uint64_t* ho = reinterpret_cast<uint64_t*>(g.pin_offs.p);
+    uint64_t pos = 0, k = 0;
+    ho[k++] = 0;
+    for (auto& b : blocks) {
+      std::memcpy(buf + pos, b.data, b.len);
+      ho[k++] = pos += b.len;
     }
-  for (auto& b : blocks)
-    for (auto& a : b.atts) {  // Key() preimage (types/attestation.go:61-77)
-      std::string k(10, '\0'), v;
-      put_varint(v, a->slot);
-      std::memcpy(&k[0], v.data(), v.size());
-      v.clear();
-      put_varint(v, a->shard);
-      std::memcpy(&k[0], v.data(), v.size());
-      k.append((const char*)a->at(a->sbh_off), a->sbh_len);
-      for (auto& o : a->obl) {
-        const H32 h = copy32(a->at(o.first), o.second);
-        k.append((const char*)h.b, 32);
+    for (auto& b : blocks)
+      for (auto& a : b.atts) {
+        std::memcpy(buf + pos, a->enc.data(), a->enc.size());
+        ho[k++] = pos += a->enc.size();
       }
-      buf += k;
+    for (auto& b : blocks)
+      for (auto& a : b.atts) {  // Key() preimage (types/attestation.go:61-77)
+        uint8_t* q = buf + pos;
+        std::memset(q, 0, 10);
+        uint8_t v[10];
+        size_t vl = 0;
+        for (uint64_t x = a->slot; ; x >>= 7) {
+          v[vl++] = (uint8_t)(x >= 0x80 ? (x & 0x7F) | 0x80 : x);
+          if (x < 0x80) break;
+        }
+        std::memcpy(q, v, vl);
+        vl = 0;
+        for (uint64_t x = a->shard; ; x >>= 7) {
+          v[vl++] = (uint8_t)(x >= 0x80 ? (x & 0x7F) | 0x80 : x);
+          if (x < 0x80) break;
+        }
+        std::memcpy(q, v, vl);
+        std::memcpy(q + 10, a->at(a->sbh_off), a->sbh_len);
+        uint64_t kl = 10 + a->sbh_len;
+        for (auto& o : a->obl) {
+          const H32 h = copy32(a->at(o.first), o.second);
+          std::memcpy(q + kl, h.b, 32);
+          kl += 32;
+        }
+        ho[k++] = pos += kl;
+      }
+    check(g.h_in.alloc(pos + 16));
+    check(g.h_out.alloc(nmsg * 32));
+    check(g.h_offs.alloc(nmsg + 1));
+    hchk(hipMemcpyAsync(g.h_offs.p, ho, (nmsg + 1) * 8, hipMemcpyHostToDevice, g.s), "H2D offsets");
+    if (pos) hchk(hipMemcpyAsync(g.h_in.p, buf, pos, hipMemcpyHostToDevice, g.s), "H2D msgs");
+    hchk(launch_b2b_csr(g.h_in.p, g.h_offs.p, nmsg, g.h_out.p, 32, g.s), "blake2b csr");
+    hchk(hipMemcpyAsync(g.pin_dig.p, g.h_out.p, nmsg * 32, hipMemcpyDeviceToHost, g.s), "D2H digests");
+    hchk(hipStreamSynchronize(g.s), "sync");
+    dg = g.pin_dig.p;
+    dstride = 32;
+  } else {
+    std::string buf;
+    std::vector<uint64_t> ho{0};
+    for (auto& b : blocks) {
+      buf.append((const char*)b.data, b.len);
       ho.push_back(buf.size());
     }
-  std::vector<uint8_t> dg;
-  hash_many(g, buf, ho, dg);
+    for (auto& b : blocks)
+      for (auto& a : b.atts) {
+        buf += a->enc;
+        ho.push_back(buf.size());
+      }
+    for (auto& b : blocks)
+      for (auto& a : b.atts) {  // Key() preimage (types/attestation.go:61-77)
+        std::string k(10, '\0'), v;
+        put_varint(v, a->slot);
+        std::memcpy(&k[0], v.data(), v.size());
+        v.clear();
+        put_varint(v, a->shard);
+        std::memcpy(&k[0], v.data(), v.size());
+        k.append((const char*)a->at(a->sbh_off), a->sbh_len);
+        for (auto& o : a->obl) {
+          const H32 h = copy32(a->at(o.first), o.second);
+          k.append((const char*)h.b, 32);
+        }
+        buf += k;
+        ho.push_back(buf.size());
+      }
+    hash_many(g, buf, ho, dg_slow);
+    dg = dg_slow.data();
+    dstride = 64;
+  }
   g.prof[kProfHash1] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_hash1).count();
   // the walk
   std::vector<uint64_t> msg_att;
@@ -1070,14 +1160,14 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
   msg_att.reserve(natt);
   for (uint64_t bi = 0; bi < n; ++bi) {
     H32 h;
-    std::memcpy(h.b, &dg[bi * 64], 32);
+    std::memcpy(h.b, dg + bi * dstride, 32);
     block_id[bi] = log_hash(g, h);
   }
   auto t_walk = std::chrono::steady_clock::now();
   for (uint64_t bi = 0; bi < n; ++bi) {
     const Block& b = blocks[bi];
     pz_block_result& r = br[bi];
-    std::memcpy(r.hash, &dg[bi * 64], 32);
+    std::memcpy(r.hash, dg + bi * dstride, 32);
     r.status = PZ_BLOCK_PROCESSED;
     r.transition = 0;
     r.first_att = (uint32_t)ai;
@@ -1109,8 +1199,8 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
       }
       can_atts = true;
       x.status = PZ_ATT_PROCESSED;
-      std::memcpy(x.hash, &dg[(n + a0 + j) * 64], 32);
-      std::memcpy(x.key, &dg[(n + natt + a0 + j) * 64], 32);
+      std::memcpy(x.hash, dg + (n + a0 + j) * dstride, 32);
+      std::memcpy(x.key, dg + (n + natt + a0 + j) * dstride, 32);
       x.msg_len = (uint32_t)(10 + 33 * kCycle + b.atts[j]->sbh_len);
       msg_att.push_back(a0 + j);
       processed.push_back(b.atts[j]);
