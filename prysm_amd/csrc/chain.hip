@@ -361,9 +361,11 @@ struct Engine {
   DevArr<uint32_t> d_leader;
   uint64_t ncomm = 0, cwords = 1;
   // epoch scratch
-  DevArr<uint64_t> e_scal, e_mask, e_vote, e_total, e_rdyn, e_small, e_boffs;
-  DevArr<uint32_t> e_blk, e_list, e_win, e_comm, e_shard;
-  DevArr<uint8_t> e_bits;
+  DevArr<uint64_t> e_scal, e_mask, e_vote, e_total;
+  DevArr<uint32_t> e_blk, e_list, e_win;
+  DevArr<uint8_t> e_pack;    // one H2D per transition: bitfields, offsets, committees, ...
+  PinBuf e_pin, e_pin_out;   // its pinned staging; the results' pinned landing (scal, winners)
+  PinBuf tot_pin;            // the vote totals the justification loop reads
   // hashing scratch
   PinBuf pin_msgs, pin_offs, pin_dig;  // pinned staging of the digest batch
   DevArr<uint8_t> h_in, h_out;
@@ -706,21 +708,28 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, std::
 // processCrosslinks + CalculateRewards + next-cycle balance on the device -> next balance.
 // Host staging of one device epoch; lives until the stream sync after epoch_enqueue.
 struct EpochJob {
-  std::vector<uint32_t> comm, shard, win;
-  std::vector<uint8_t> bits;
-  std::vector<uint64_t> boffs{0}, rdyn;
-  uint64_t small[2] = {0, 0};
+  std::vector<uint32_t> win;
+  size_t nrec = 0;
   uint64_t scal[kScal] = {};
 };
 
 static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending, EpochJob& J) {
   const size_t na = pending.size();
-  std::vector<uint32_t>& comm = J.comm;
-  std::vector<uint32_t>& shard = J.shard;
-  std::vector<uint8_t>& bits = J.bits;
-  std::vector<uint64_t>& boffs = J.boffs;
-  comm.resize(na);
-  shard.resize(na);
+  std::vector<Crosslink>& xl = *C.xl;
+  const size_t nrec = xl.size();
+  uint64_t nbits = 0;
+  for (auto& p : pending) nbits += p->bf_len;
+  // packed layout (16-byte aligned parts): boffs | rdyn | small | comm | shard | bits
+  auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
+  const size_t o_boffs = 0, o_rdyn = al((na + 1) * 8), o_small = o_rdyn + al(nrec * 8), o_comm = o_small + 16,
+               o_shard = o_comm + al(na * 4), o_bits = o_shard + al(na * 4), total = o_bits + al(nbits) + 16;
+  check(g.e_pin.reserve(total));
+  uint8_t* h = g.e_pin.p;
+  uint64_t* boffs = reinterpret_cast<uint64_t*>(h + o_boffs);
+  uint32_t* comm = reinterpret_cast<uint32_t*>(h + o_comm);
+  uint32_t* shard = reinterpret_cast<uint32_t*>(h + o_shard);
+  uint8_t* bits = h + o_bits;
+  boffs[0] = 0;
   for (size_t i = 0; i < na; ++i) {
     const Att& a = *pending[i];
     try {
@@ -730,27 +739,23 @@ static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending
     }
     if (a.shard > 0xffffffffull) throw Panic{"crosslink record index out of range"};
     shard[i] = (uint32_t)a.shard;
-    bits.insert(bits.end(), a.at(a.bf_off), a.at(a.bf_off) + a.bf_len);
-    boffs.push_back(bits.size());
+    std::memcpy(bits + boffs[i], a.at(a.bf_off), a.bf_len);
+    boffs[i + 1] = boffs[i] + a.bf_len;
   }
-  std::vector<Crosslink>& xl = *C.xl;
-  std::vector<uint64_t>& rdyn = J.rdyn;
-  rdyn.resize(xl.size());
-  for (size_t s = 0; s < xl.size(); ++s) rdyn[s] = xl[s].dynasty;
-  uint64_t* small = J.small;
+  uint64_t* rdyn = reinterpret_cast<uint64_t*>(h + o_rdyn);
+  for (size_t s = 0; s < nrec; ++s) rdyn[s] = xl[s].dynasty;
+  uint64_t* small = reinterpret_cast<uint64_t*>(h + o_small);
   small[0] = C.dynasty;
   small[1] = C.tdep;
-  upload(g, g.e_bits, bits.data(), bits.size());
-  upload(g, g.e_boffs, boffs.data(), boffs.size());
-  upload(g, g.e_comm, comm.data(), na);
-  upload(g, g.e_shard, shard.data(), na);
-  upload(g, g.e_rdyn, rdyn.data(), rdyn.size());
-  upload(g, g.e_small, small, 2);
+  // the previous transition's copies finished at its sync, so the staging is free
+  check(g.e_pack.alloc(total));
+  hchk(hipMemcpyAsync(g.e_pack.p, h, total, hipMemcpyHostToDevice, g.s), "H2D epoch");
   check(g.e_scal.alloc(kScal));
   check(g.e_vote.alloc(na + 1));
   check(g.e_total.alloc(na + 1));
-  check(g.e_win.alloc(xl.size() + 1));
+  check(g.e_win.alloc(nrec + 1));
   hchk(hipMemsetAsync(g.e_scal.p, 0, kScal * 8, g.s), "memset");
+  uint8_t* d = g.e_pack.p;
   EpochArgs a;
   std::memset(&a, 0, sizeof a);
   a.ninst = 1;
@@ -759,20 +764,20 @@ static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending
   a.balance = g.balance.p;
   a.start = g.start.p;
   a.end = g.end.p;
-  a.dynasty = g.e_small.p;
-  a.total_deposit = g.e_small.p + 1;
+  a.dynasty = reinterpret_cast<const uint64_t*>(d + o_small);
+  a.total_deposit = reinterpret_cast<const uint64_t*>(d + o_small) + 1;
   a.natt = (uint32_t)na;
-  a.bits = g.e_bits.p;
-  a.boffs = g.e_boffs.p;
-  a.max_inst_bytes = bits.size();
+  a.bits = d + o_bits;
+  a.boffs = reinterpret_cast<const uint64_t*>(d + o_boffs);
+  a.max_inst_bytes = nbits;
   a.pop_rank = 0;
   a.pop_world = 1;
   a.committee = g.committee.p;
   a.coffs = g.coffs.p;
-  a.att_comm = g.e_comm.p;
-  a.att_shard = g.e_shard.p;
-  a.nrec = (uint32_t)xl.size();
-  a.rec_dynasty = g.e_rdyn.p;
+  a.att_comm = reinterpret_cast<const uint32_t*>(d + o_comm);
+  a.att_shard = reinterpret_cast<const uint32_t*>(d + o_shard);
+  a.nrec = (uint32_t)nrec;
+  a.rec_dynasty = reinterpret_cast<const uint64_t*>(d + o_rdyn);
   a.winner = g.e_win.p;
   a.vote = g.e_vote.p;
   a.total = g.e_total.p;
@@ -783,9 +788,18 @@ static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending
   hchk(launch_epoch_count(a, true, true, true, g.s), "epoch count");
   hchk(launch_epoch_mid(a, a.nrec > 0 && na > 0, true, g.s), "epoch mid");
   hchk(launch_epoch_reward(a, g.s), "epoch reward");
-  J.win.resize(xl.size());
-  hchk(hipMemcpyAsync(J.scal, g.e_scal.p, sizeof J.scal, hipMemcpyDeviceToHost, g.s), "D2H");
-  if (!J.win.empty()) hchk(hipMemcpyAsync(J.win.data(), g.e_win.p, J.win.size() * 4, hipMemcpyDeviceToHost, g.s), "D2H");
+  check(g.e_pin_out.reserve(sizeof J.scal + nrec * 4 + 16));
+  hchk(hipMemcpyAsync(g.e_pin_out.p, g.e_scal.p, sizeof J.scal, hipMemcpyDeviceToHost, g.s), "D2H");
+  if (nrec)
+    hchk(hipMemcpyAsync(g.e_pin_out.p + sizeof J.scal, g.e_win.p, nrec * 4, hipMemcpyDeviceToHost, g.s), "D2H");
+  J.nrec = nrec;
+}
+
+// After the stream sync: the epoch results out of their pinned landing.
+static void epoch_collect(Engine& g, EpochJob& J) {
+  std::memcpy(J.scal, g.e_pin_out.p, sizeof J.scal);
+  J.win.resize(J.nrec);
+  if (J.nrec) std::memcpy(J.win.data(), g.e_pin_out.p + sizeof J.scal, J.nrec * 4);
 }
 
 // After the sync: the reference's panics, the crosslink winners, the next-cycle balance.
@@ -823,16 +837,18 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   uint64_t streak = C->streak, justified = C->jslot, finalized = C->fslot;
   const uint64_t lsr = C->lsr;
   std::vector<uint64_t> tot(kCycle, 0);
-  std::vector<uint64_t> all;
-  if (!A->cache_nil) {
-    all.resize(g.slot_hash.size());
-    if (!all.empty()) hchk(hipMemcpyAsync(all.data(), g.totals.p, all.size() * 8, hipMemcpyDeviceToHost, g.s), "D2H");
+  const uint64_t nslots = A->cache_nil ? 0 : g.slot_hash.size();
+  if (nslots) {
+    check(g.tot_pin.reserve(nslots * 8));
+    hchk(hipMemcpyAsync(g.tot_pin.p, g.totals.p, nslots * 8, hipMemcpyDeviceToHost, g.s), "D2H");
   }
   EpochJob job;
   epoch_enqueue(g, *C, A->pending, job);
   hchk(hipStreamSynchronize(g.s), "sync");
   flush_votes_finish(g);
-  if (!A->cache_nil) {
+  epoch_collect(g, job);
+  if (nslots) {
+    const uint64_t* all = reinterpret_cast<const uint64_t*>(g.tot_pin.p);
     for (uint64_t i = 0; i < kCycle && i < A->recent.size(); ++i) {
       auto it = g.slot_of.find(A->recent[i]);
       tot[i] = it == g.slot_of.end() ? 0 : all[it->second];
