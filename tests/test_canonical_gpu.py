@@ -1,0 +1,94 @@
+"""The block engine accepts exactly the canonical proto3 encodings: the
+reference hashes proto.Marshal of the DECODED block (types/block.go:69), so an input that is
+not the canonical encoding of its own decoding would hash differently from its bytes; the
+engine rejects it with PZ_EINVAL instead of guessing.  Each case below is a decodable
+BeaconBlock whose re-encoding differs from its bytes (or, for the accepted cases, does not),
+decided here independently by Google's protobuf runtime over the oracle schema."""
+import numpy as np
+import pytest
+
+from oracle import schema as opb
+from prysm_amd import _lib, pb, wire
+from prysm_amd.blockchain import BeaconChain
+
+pytestmark = pytest.mark.gpu
+
+ATT = pb.AttestationRecord(slot=0, shard_id=3, justified_slot=0, shard_block_hash=b"\x11" * 32,
+                           attester_bitfield=b"\xff\x00", oblique_parent_hashes=[b"\x22" * 32], aggregate_sig=[5, 7])
+
+
+def block(atts=(ATT,), ts=pb.Timestamp(8, 0)):
+    return pb.BeaconBlock(parent_hash=b"\x01" * 32, slot_number=1, timestamp=ts, attestations=list(atts))
+
+
+def frame(num, body):
+    return wire._msg(num, body)
+
+
+def canonical_by_runtime(raw):
+    m = opb.BeaconBlock()
+    m.ParseFromString(raw)
+    return m.SerializeToString() == raw
+
+
+def run(raw):
+    data = np.frombuffer(raw + bytes(16), dtype=np.uint8)
+    offs = np.array([0, len(raw)], dtype=np.uint64)
+    BeaconChain(1024).process_serialized(data, offs)
+
+
+def att_bytes(**over):
+    a = pb.AttestationRecord(**{**ATT.__dict__, **over})
+    return wire.attestation_record(a)
+
+
+E = wire.beacon_block(block())
+HEAD = E[:E.index(b"\x42")]  # everything before the attestation field
+A = wire.attestation_record(ATT)
+
+NONCANONICAL = {
+    "slot field repeated at the end": E + b"\x10\x01",
+    "non-minimal varint (slot)": E.replace(b"\x10\x01", b"\x10\x81\x00", 1),
+    "fields out of order": E.replace(b"\x10\x01", b"", 1) + b"\x10\x01",
+    "explicit empty bytes (randao_reveal)": E.replace(b"\x10\x01", b"\x10\x01\x1a\x00", 1),
+    "explicit zero scalar in the timestamp": E.replace(b"\x3a\x02\x08\x08", b"\x3a\x04\x08\x08\x10\x00", 1),
+    "attestation: explicit zero slot": HEAD + frame(8, b"\x08\x00" + A),
+    "attestation: empty packed signature": HEAD + frame(8, A + b"\x42\x00"),
+    "attestation: non-minimal length prefix": HEAD + b"\x42" + bytes([0x80 | len(A), 0x00]) + A
+    if len(A) < 128 else None,
+}
+CANONICAL = {
+    "as encoded": E,
+    "empty oblique element (every element is emitted)": wire.beacon_block(block(
+        [pb.AttestationRecord(**{**ATT.__dict__, "oblique_parent_hashes": [b""]})])),
+    "empty timestamp message (a set message is emitted)": wire.beacon_block(block(ts=pb.Timestamp(0, 0))),
+    "no attestations": wire.beacon_block(block(atts=())),
+}
+
+
+@pytest.mark.parametrize("name", [k for k, v in NONCANONICAL.items() if v is not None])
+def test_noncanonical_rejected(name):
+    raw = NONCANONICAL[name]
+    assert not canonical_by_runtime(raw), name  # the case really is non-canonical
+    with pytest.raises(_lib.PzError) as e:
+        run(raw)
+    assert e.value.code == _lib.PZ_EINVAL
+
+
+@pytest.mark.parametrize("name", list(CANONICAL))
+def test_canonical_accepted(name):
+    raw = CANONICAL[name]
+    assert canonical_by_runtime(raw), name
+    run(raw)
+
+
+def test_unknown_fields_rejected():
+    """Deliberately stricter than the reference: golang/protobuf keeps an unknown field in
+    XXX_unrecognized and re-emits it at the end, so Marshal(decode(x)) == x there; the engine
+    does not model unrecognized fields and rejects the block (PZ_EINVAL) rather than hash
+    bytes it does not understand."""
+    raw = E + b"\x48\x01"
+    assert canonical_by_runtime(raw)
+    with pytest.raises(_lib.PzError) as e:
+        run(raw)
+    assert e.value.code == _lib.PZ_EINVAL
