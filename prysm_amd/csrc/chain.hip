@@ -94,18 +94,28 @@ static void put_msg(std::string& o, uint32_t f, const uint8_t* p, size_t n) {
   o.append((const char*)p, n);
 }
 
+// Streaming proto3 reader that also checks canonical form: the reference hashes
+// proto.Marshal of the DECODED message, so the engine accepts exactly the inputs that equal
+// the re-encoding of their own decoding.  Instead of re-encoding, every rule Marshal applies
+// is checked while reading: minimal varints (keys, values, lengths), ascending field numbers
+// (a repeated field only repeats in a run), zero scalars and empty singular bytes omitted,
+// a packed repeated field never empty, and no unknown fields.
 struct Reader {
   const uint8_t* p;
   const uint8_t* e;
   bool ok = true;
   bool more() const { return ok && p < e; }
+  // a minimal varint (a 10-byte one must end in 0x01: only bit 63 left)
   uint64_t varint() {
     uint64_t x = 0;
-    for (int s = 0; s < 70; s += 7) {
+    for (int i = 0, s = 0; i < 10; ++i, s += 7) {
       if (p >= e) { ok = false; return 0; }
       const uint8_t b = *p++;
       x |= (uint64_t)(b & 0x7f) << s;
-      if (!(b & 0x80)) return x;
+      if (!(b & 0x80)) {
+        if ((i > 0 && b == 0) || (i == 9 && b != 1)) ok = false;
+        return x;
+      }
     }
     ok = false;
     return 0;
@@ -118,7 +128,7 @@ struct Reader {
     p += len;
     return true;
   }
-  void skip(uint32_t wt) {
+  void skip(uint32_t wt) {  // (only for counting; canonical form is checked by the parsers)
     const uint8_t* q;
     size_t n;
     if (wt == 0) varint();
@@ -126,6 +136,15 @@ struct Reader {
     else if (wt == 1 && e - p >= 8) p += 8;
     else if (wt == 5 && e - p >= 4) p += 4;
     else ok = false;
+  }
+  // the next key: field f with wire type wt, after field `prev`; `rep` = f may repeat
+  bool key(uint32_t prev, uint32_t* f, uint32_t* wt, uint32_t nfields, const uint32_t* types, uint32_t rep_mask) {
+    const uint64_t k = varint();
+    *f = (uint32_t)(k >> 3);
+    *wt = (uint32_t)(k & 7);
+    if (!ok || *f == 0 || *f > nfields || types[*f] != *wt) return ok = false;
+    if (*f < prev || (*f == prev && !((rep_mask >> *f) & 1))) return ok = false;
+    return true;
   }
 };
 
@@ -139,47 +158,38 @@ struct Att {
 };
 using AttP = std::shared_ptr<const Att>;
 
+// messages.pb.go:889-896: 1-3 varint, 4-6 bytes, 7 repeated bytes, 8 packed varints
 static bool parse_att(const uint8_t* p, size_t n, Att* a) {
+  static const uint32_t kTypes[9] = {9, 0, 0, 0, 2, 2, 2, 2, 2};
   a->enc.assign((const char*)p, n);
   const uint8_t* base = (const uint8_t*)a->enc.data();
   Reader r{base, base + n};
-  const uint8_t *jbh = nullptr, *q;
-  size_t jbh_len = 0, len;
-  std::vector<uint64_t> sig;
+  uint32_t prev = 0, f, wt;
+  const uint8_t* q;
+  size_t len;
   while (r.more()) {
-    const uint64_t key = r.varint();
-    const uint32_t f = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
-    if (f == 1 && wt == 0) a->slot = r.varint();
-    else if (f == 2 && wt == 0) a->shard = r.varint();
-    else if (f == 3 && wt == 0) a->jslot = r.varint();
-    else if (f == 4 && wt == 2) { r.span(&jbh, &jbh_len); }
-    else if (f == 5 && wt == 2) { if (r.span(&q, &len)) { a->sbh_off = (uint32_t)(q - base); a->sbh_len = (uint32_t)len; } }
-    else if (f == 6 && wt == 2) { if (r.span(&q, &len)) { a->bf_off = (uint32_t)(q - base); a->bf_len = (uint32_t)len; } }
-    else if (f == 7 && wt == 2) { if (r.span(&q, &len)) a->obl.push_back({(uint32_t)(q - base), (uint32_t)len}); }
-    else if (f == 8 && wt == 2) {
-      if (r.span(&q, &len)) {
-        Reader s{q, q + len};
-        while (s.more()) sig.push_back(s.varint());
-        r.ok = r.ok && s.ok;
-      }
-    } else return false;  // unknown / mistyped field: not a canonical encoding
+    if (!r.key(prev, &f, &wt, 8, kTypes, 1u << 7)) return false;
+    prev = f;
+    if (f <= 3) {
+      const uint64_t v = r.varint();
+      if (!v) return false;  // a zero scalar is omitted by Marshal
+      (f == 1 ? a->slot : f == 2 ? a->shard : a->jslot) = v;
+    } else if (!r.span(&q, &len)) {
+      return false;
+    } else if (f <= 6) {
+      if (!len) return false;  // an empty singular bytes field is omitted
+      if (f == 5) { a->sbh_off = (uint32_t)(q - base); a->sbh_len = (uint32_t)len; }
+      if (f == 6) { a->bf_off = (uint32_t)(q - base); a->bf_len = (uint32_t)len; }
+    } else if (f == 7) {
+      a->obl.push_back({(uint32_t)(q - base), (uint32_t)len});
+    } else {  // f == 8: packed, never empty
+      if (!len) return false;
+      Reader s{q, q + len};
+      while (s.more()) s.varint();
+      if (!s.ok) return false;
+    }
   }
-  if (!r.ok) return false;
-  // canonical check: the reference hashes proto.Marshal of the decoded message
-  std::string c;
-  put_u(c, 1, a->slot);
-  put_u(c, 2, a->shard);
-  put_u(c, 3, a->jslot);
-  put_b(c, 4, jbh, jbh_len);
-  put_b(c, 5, a->at(a->sbh_off), a->sbh_len);
-  put_b(c, 6, a->at(a->bf_off), a->bf_len);
-  for (auto& o : a->obl) put_msg(c, 7, a->at(o.first), o.second);
-  if (!sig.empty()) {
-    std::string body;
-    for (uint64_t v : sig) put_varint(body, v);
-    put_msg(c, 8, (const uint8_t*)body.data(), body.size());
-  }
-  return c == a->enc;
+  return r.ok;
 }
 
 struct Block {
@@ -190,55 +200,45 @@ struct Block {
   std::vector<AttP> atts;
 };
 
+// messages.pb.go:224-232: 1 bytes, 2 varint, 3-6 bytes, 7 Timestamp, 8 repeated records
 static bool parse_block(const uint8_t* p, size_t n, Block* b) {
+  static const uint32_t kTypes[9] = {9, 2, 0, 2, 2, 2, 2, 2, 2};
+  static const uint32_t kTsTypes[3] = {9, 0, 0};
   b->data = p;
   b->len = n;
   Reader r{p, p + n};
-  const uint8_t* fld[7] = {nullptr};
-  size_t flen[7] = {0};
-  bool has_ts = false;
-  uint64_t ts_s = 0, ts_n = 0;
+  uint32_t prev = 0, f, wt;
   const uint8_t* q;
   size_t len;
   while (r.more()) {
-    const uint64_t key = r.varint();
-    const uint32_t f = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
-    if (f == 2 && wt == 0) b->slot = r.varint();
-    else if ((f == 1 || (f >= 3 && f <= 6)) && wt == 2) r.span(&fld[f], &flen[f]);
-    else if (f == 7 && wt == 2) {
-      if (r.span(&q, &len)) {
-        has_ts = true;
-        Reader t{q, q + len};
-        while (t.more()) {
-          const uint64_t k2 = t.varint();
-          if (k2 == 0x08) ts_s = t.varint();
-          else if (k2 == 0x10) ts_n = t.varint();
-          else t.ok = false;
-        }
-        r.ok = r.ok && t.ok;
+    if (!r.key(prev, &f, &wt, 8, kTypes, 1u << 8)) return false;
+    prev = f;
+    if (f == 2) {
+      if (!(b->slot = r.varint())) return false;
+    } else if (!r.span(&q, &len)) {
+      return false;
+    } else if (f == 1 || f <= 6) {
+      if (!len) return false;
+      if (f == 1) b->parent = copy32(q, len);
+    } else if (f == 7) {  // Timestamp {int64 seconds = 1; int32 nanos = 2}; may be empty
+      Reader t{q, q + len};
+      uint32_t tp = 0, tf, twt;
+      while (t.more()) {
+        if (!t.key(tp, &tf, &twt, 2, kTsTypes, 0)) return false;
+        tp = tf;
+        const uint64_t v = t.varint();
+        if (!v) return false;
+        // int32: Marshal sign-extends the decoded 32-bit value
+        if (tf == 2 && v != (uint64_t)(int64_t)(int32_t)(uint32_t)v) return false;
       }
-    } else if (f == 8 && wt == 2) {
-      if (r.span(&q, &len)) {
-        auto a = std::make_shared<Att>();
-        if (!parse_att(q, len, a.get())) return false;
-        b->atts.push_back(a);
-      }
-    } else return false;
+      if (!t.ok) return false;
+    } else {  // f == 8
+      auto a = std::make_shared<Att>();
+      if (!parse_att(q, len, a.get())) return false;
+      b->atts.push_back(a);
+    }
   }
-  if (!r.ok) return false;
-  b->parent = copy32(fld[1], flen[1]);
-  std::string c;
-  put_b(c, 1, fld[1], flen[1]);
-  put_u(c, 2, b->slot);
-  for (int f = 3; f <= 6; ++f) put_b(c, f, fld[f], flen[f]);
-  if (has_ts) {
-    std::string t;
-    put_u(t, 1, ts_s);
-    put_u(t, 2, ts_n);
-    put_msg(c, 7, (const uint8_t*)t.data(), t.size());
-  }
-  for (auto& a : b->atts) put_msg(c, 8, (const uint8_t*)a->enc.data(), a->enc.size());
-  return c.size() == n && std::memcmp(c.data(), p, n) == 0;
+  return r.ok;
 }
 
 // ---- chain state ----------------------------------------------------------------------------

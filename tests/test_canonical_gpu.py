@@ -52,7 +52,10 @@ NONCANONICAL = {
     "fields out of order": E.replace(b"\x10\x01", b"", 1) + b"\x10\x01",
     "explicit empty bytes (randao_reveal)": E.replace(b"\x10\x01", b"\x10\x01\x1a\x00", 1),
     "explicit zero scalar in the timestamp": E.replace(b"\x3a\x02\x08\x08", b"\x3a\x04\x08\x08\x10\x00", 1),
+    "timestamp nanos beyond int32 (Marshal re-encodes the truncated int32)":
+        E.replace(b"\x3a\x02\x08\x08", b"\x3a\x08\x08\x08\x10" + wire.varint((1 << 32) + 5), 1),
     "attestation: explicit zero slot": HEAD + frame(8, b"\x08\x00" + A),
+    "attestation: field 7 run broken by field 8 then 7 again": HEAD + frame(8, A + wire._msg(7, b"\x33" * 32)),
     "attestation: empty packed signature": HEAD + frame(8, A + b"\x42\x00"),
     "attestation: non-minimal length prefix": HEAD + b"\x42" + bytes([0x80 | len(A), 0x00]) + A
     if len(A) < 128 else None,
@@ -63,6 +66,8 @@ CANONICAL = {
         [pb.AttestationRecord(**{**ATT.__dict__, "oblique_parent_hashes": [b""]})])),
     "empty timestamp message (a set message is emitted)": wire.beacon_block(block(ts=pb.Timestamp(0, 0))),
     "no attestations": wire.beacon_block(block(atts=())),
+    "negative timestamp seconds (10-byte varint)": wire.beacon_block(block(ts=pb.Timestamp(-5, 0))),
+    "negative nanos (sign-extended 10-byte varint)": wire.beacon_block(block(ts=pb.Timestamp(1, -3))),
 }
 
 
