@@ -69,33 +69,33 @@ pz_vote_tally_kernel(VoteArgs a) {
 // exact -- and elects the group's first item as its leader; pass 2 lets each leader tally the
 // union once and clear it.  (Tallying every item directly made up to 64 waves race on the
 // same voter words with atomics: 100 us per cycle instead of ~25.)
+// kUnionLanes lanes per item (a committee bitfield is at most a few words): 8 items a wave.
+constexpr uint32_t kUnionLanes = 8;
 extern "C" __global__ void __launch_bounds__(256)
 pz_vote_union_kernel(VoteIdArgs a) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t item = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t item = t / kUnionLanes;
+  const uint32_t sub = (uint32_t)(t % kUnionLanes);
   const uint64_t att = item >> 6;
   if (att >= a.natt) return;
-  bool lead = false;
-  if (!((a.skip[att] >> (item & 63)) & 1)) {  // an oblique parent hash (core.go:313-320) is skipped
-    const uint32_t slot = a.id_slot[a.ids[item]];
-    const uint32_t c = a.att_comm[att];
-    const uint64_t grp = (uint64_t)slot * a.ncomm + c;
-    const uint64_t k = a.coffs[c + 1] - a.coffs[c];
-    const uint64_t bb = a.boffs[att], blen = a.boffs[att + 1] - bb;
-    const uint64_t nbytes = min(blen, (k + 7) / 8);  // bits at positions >= k are never read
-    uint32_t* u = a.ubits + grp * a.cwords;
-    for (uint64_t w = lane; 4 * w < nbytes; w += 64) {
-      uint32_t x = 0;
+  if ((a.skip[att] >> (item & 63)) & 1) return;  // an oblique parent hash (core.go:313-320) is skipped
+  const uint32_t slot = a.id_slot[a.ids[item]];
+  const uint32_t c = a.att_comm[att];
+  const uint64_t grp = (uint64_t)slot * a.ncomm + c;
+  const uint64_t k = a.coffs[c + 1] - a.coffs[c];
+  const uint64_t bb = a.boffs[att], blen = a.boffs[att + 1] - bb;
+  const uint64_t nbytes = min(blen, (k + 7) / 8);  // bits at positions >= k are never read
+  uint32_t* u = a.ubits + grp * a.cwords;
+  for (uint64_t w = sub; 4 * w < nbytes; w += kUnionLanes) {
+    uint32_t x = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (4 * w + q < nbytes) x |= (uint32_t)a.bits[bb + 4 * w + q] << (8 * q);
-      if (x) atomicOr(&u[w], x);
-    }
-    if (lane == 0) {
-      a.present[slot] = 1;  // the map entry exists (core.go:322-326)
-      lead = atomicOr(&a.uflag[grp], 1u) == 0;
-      if (lead) a.leader[atomicAdd(a.nlead, 1u)] = (uint32_t)item;
-    }
+    for (int q = 0; q < 4; ++q)
+      if (4 * w + q < nbytes) x |= (uint32_t)a.bits[bb + 4 * w + q] << (8 * q);
+    if (x) atomicOr(&u[w], x);
+  }
+  if (sub == 0) {
+    a.present[slot] = 1;  // the map entry exists (core.go:322-326)
+    if (atomicOr(&a.uflag[grp], 1u) == 0) a.leader[atomicAdd(a.nlead, 1u)] = (uint32_t)item;
   }
 }
 
@@ -122,10 +122,10 @@ pz_vote_leader_kernel(VoteIdArgs a) {
 
 hipError_t launch_vote_ids(const VoteIdArgs& a, hipStream_t s) {
   if (!a.natt) return hipSuccess;
-  const uint64_t threads = a.natt * 64 * 64;
   hipError_t e = hipMemsetAsync(a.nlead, 0, 4, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(pz_vote_union_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, a);
+  const uint64_t uthreads = a.natt * 64 * kUnionLanes;
+  hipLaunchKernelGGL(pz_vote_union_kernel, dim3((uint32_t)((uthreads + 255) / 256)), dim3(256), 0, s, a);
   hipLaunchKernelGGL(pz_vote_leader_kernel, dim3(kLeaderWaves / 4), dim3(256), 0, s, a);
   return hipGetLastError();
 }
