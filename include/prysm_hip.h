@@ -198,6 +198,24 @@ int pz_process_crosslinks(const uint32_t* committee, const uint64_t* coffs, uint
  * swap chain); only the 64-byte seed stream blake2b.Sum512(seed) is computed on the GPU. */
 int pz_shuffle_indices(const uint8_t seed[32], uint32_t* list, uint64_t n);
 
+/* casper/validator.go:17-41 RotateValidatorSet, in place on start/end: active validators
+ * below DefaultBalance/2 exit (end = dynasty); then the first min(len(active)/30 + 1,
+ * len(queued)) queued validators, by ascending index, start (start = dynasty).  The active
+ * count, the exits and the queued list run on the device filter kernels. */
+int pz_rotate_validator_set(const uint64_t* balance, uint64_t* start, uint64_t* end, uint64_t n,
+                            uint64_t dynasty);
+
+/* casper/sharding.go:11-53 ShuffleValidatorsToCommittees: active indices (device filter),
+ * ShuffleIndices (host swap chain), then splitBySlotShard into CSR: slot s (0..63) holds
+ * committees slot_offs[s] .. slot_offs[s+1]; committee c has shard shard_id[c] and members
+ * members[coffs[c] .. coffs[c+1]].  members needs room for n, coffs for cap_comm+1 and shard_id
+ * for cap_comm entries, slot_offs for 65; PZ_ERANGE (with *ncomm = the count needed) when
+ * cap_comm is short, PZ_ETOOMANY above MaxValidators (utils/shuffle.go:15-17). */
+int pz_shuffle_validators_to_committees(const uint8_t seed[32], const uint64_t* start, const uint64_t* end,
+                                        uint64_t n, uint64_t dynasty, uint64_t crosslink_start_shard,
+                                        uint32_t* members, uint64_t* coffs, uint64_t* shard_id,
+                                        uint64_t* slot_offs, uint64_t cap_comm, uint64_t* ncomm);
+
 /* ---- device-resident batched epoch transition (throughput mode, multi-GPU shards) -----
  * B independent instances of the data-parallel part of stateRecalc (blockchain/core.go:
  * 433-464): crosslink tallies + winners, attester popcount, CalculateRewards and the

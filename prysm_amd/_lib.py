@@ -83,6 +83,8 @@ SIGNATURES = {
     "pz_wire_validators": [vp, u64, u32, vp, u64, vp, c_u64p],
     "pz_dev_wire_validators": [vp, u64, u32, vp, vp, vp, vp, vp],
     "pz_check_attestations": [vp],
+    "pz_rotate_validator_set": [vp, vp, vp, u64, u64],
+    "pz_shuffle_validators_to_committees": [vp, vp, vp, u64, u64, u64, vp, vp, vp, vp, u64, c_u64p],
     "pz_wire_attestations_bound": [u64, u64, u64, u64],
     "pz_wire_attestations_scratch_bytes": [u64],
     "pz_wire_attestations": [vp, u64, u32, vp, u64, vp, c_u64p],

@@ -106,17 +106,29 @@ def split_by_slot_shard(shuffled, crosslink_start_shard):
 
 
 def shuffle_validators_to_committees(seed32, start, end, dynasty, crosslink_start_shard):
-    """casper/sharding.go:11-21."""
-    idx = active_validator_indices(start, end, dynasty)
-    return split_by_slot_shard(shuffle_indices(seed32, idx), crosslink_start_shard)
+    """casper/sharding.go:11-21 through pz_shuffle_validators_to_committees (device filter,
+    host swap chain and split) -> [slot][(shard_id, committee uint32 array)]."""
+    start, end = _arr(start, _u64), _arr(end, _u64)
+    n = start.shape[0]
+    seed = np.frombuffer(bytes(seed32).ljust(32, b"\0")[:32], dtype=np.uint8).copy()
+    cap = CYCLE_LENGTH * (n // (CYCLE_LENGTH * MIN_COMMITTEE_SIZE * 2) + 1)
+    members = np.empty(max(n, 1), dtype=np.uint32)
+    coffs = np.empty(cap + 1, dtype=_u64)
+    shard = np.empty(cap, dtype=_u64)
+    slot_offs = np.empty(CYCLE_LENGTH + 1, dtype=_u64)
+    ncomm = ctypes.c_uint64(0)
+    lib.call("pz_shuffle_validators_to_committees", ptr(seed), ptr(start), ptr(end), n, int(dynasty),
+             int(crosslink_start_shard), ptr(members), ptr(coffs), ptr(shard), ptr(slot_offs), cap,
+             ctypes.byref(ncomm))
+    return [[(int(shard[c]), members[int(coffs[c]):int(coffs[c + 1])].copy())
+             for c in range(int(slot_offs[s]), int(slot_offs[s + 1]))] for s in range(CYCLE_LENGTH)]
 
 
 def rotate_validator_set(balance, start, end, dynasty):
-    """casper/validator.go:17-41 over the GPU filters (in place on ``start``/``end``)."""
-    active = active_validator_indices(start, end, dynasty)
-    upper = len(active) // 30 + 1
-    low = active[balance[active] < 16]
-    end[low] = dynasty
-    queued = queued_validator_indices(start, end, dynasty)
-    start[queued[:min(upper, len(queued))]] = dynasty
+    """casper/validator.go:17-41 through pz_rotate_validator_set (device filters), in place on
+    ``start`` / ``end`` (uint64 arrays); returns them."""
+    balance = _arr(balance, _u64)
+    for a in (start, end):
+        assert isinstance(a, np.ndarray) and a.dtype == _u64 and a.flags["C_CONTIGUOUS"]
+    lib.call("pz_rotate_validator_set", ptr(balance), ptr(start), ptr(end), start.shape[0], int(dynasty))
     return start, end

@@ -3,6 +3,7 @@
 // and the host-resident ShuffleIndices.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -20,6 +21,22 @@ EpochArgs blank_args() {
   a.ninst = 1;
   a.pop_world = 1;
   return a;
+}
+
+// casper/validator.go:21-26: every active validator below DefaultBalance/2 exits.
+extern "C" __global__ void __launch_bounds__(256)
+pz_rotate_exit_kernel(const uint64_t* __restrict__ balance, const uint64_t* __restrict__ start, uint64_t* end,
+                      uint64_t n, uint64_t dynasty) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  if (start[i] <= dynasty && dynasty < end[i] && balance[i] < PZ_DEFAULT_BALANCE / 2) end[i] = dynasty;
+}
+
+// casper/validator.go:33-39: the first k queued validators (ascending index) start now.
+extern "C" __global__ void __launch_bounds__(256)
+pz_rotate_induct_kernel(const uint32_t* __restrict__ queued, uint64_t k, uint64_t* start, uint64_t dynasty) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < k) start[queued[j]] = dynasty;
 }
 
 }  // namespace
@@ -359,6 +376,99 @@ int pz_shuffle_indices(const uint8_t seed[32], uint32_t* list, uint64_t n) {
       list[p] = t;
     }
   }
+  return PZ_OK;
+}
+
+int pz_rotate_validator_set(const uint64_t* balance, uint64_t* start, uint64_t* end, uint64_t n, uint64_t dynasty) {
+  if (n == 0) return PZ_OK;
+  if (!balance || !start || !end) return fail(PZ_EINVAL, "null pointer");
+  DeviceCtx* c;
+  int rc = acquire(&c);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = c->ensure_stream())) return rc;
+  Stager st{c, c->stream};
+  uint64_t* d_start = st.up(start, n);
+  uint64_t* d_end = st.up(end, n);
+  const uint64_t* d_bal = st.up(balance, n);
+  const uint64_t* d_dyn = st.up(&dynasty, 1);
+  // upperbound = len(ActiveValidatorIndices)/30 + 1, counted before the exits (validator.go:18)
+  EpochArgs a = blank_args();
+  a.nval = a.nval_global = n;
+  a.kind = PZ_KIND_ACTIVE;
+  a.start = d_start;
+  a.end = d_end;
+  a.dynasty = d_dyn;
+  a.scal = st.zeros<uint64_t>(kScal);
+  a.act_mask = st.zeros<uint64_t>((n + 63) / 64);
+  a.blk_cnt = st.zeros<uint32_t>(vblocks_per_inst(n));
+  a.act_list = st.zeros<uint32_t>(n);
+  EpochArgs q = a;  // QueuedValidatorIndices after the exits (their start is untouched)
+  q.kind = PZ_KIND_QUEUED;
+  q.scal = st.zeros<uint64_t>(kScal);
+  if (st.rc) return st.rc;
+  st.check(launch_epoch_count(a, true, false, false, st.s), "pz_epoch_count_kernel");
+  const dim3 grid((uint32_t)((n + 255) / 256));
+  hipLaunchKernelGGL(pz_rotate_exit_kernel, grid, dim3(256), 0, st.s, d_bal, d_start, d_end, n, dynasty);
+  st.check(hipGetLastError(), "pz_rotate_exit_kernel");
+  st.check(launch_epoch_count(q, true, false, false, st.s), "pz_epoch_count_kernel");
+  st.check(launch_epoch_compact(q, true, st.s), "pz_epoch_compact_kernel");
+  uint64_t sa[kScal], sq[kScal];
+  st.down(sa, a.scal, kScal);
+  st.down(sq, q.scal, kScal);
+  if (st.sync()) return st.rc;
+  const uint64_t k = std::min<uint64_t>(sa[kNact] / 30 + 1, sq[kNact]);
+  if (k) {
+    hipLaunchKernelGGL(pz_rotate_induct_kernel, dim3((uint32_t)((k + 255) / 256)), dim3(256), 0, st.s, q.act_list, k,
+                       d_start, dynasty);
+    st.check(hipGetLastError(), "pz_rotate_induct_kernel");
+  }
+  st.down(start, d_start, n);
+  st.down(end, d_end, n);
+  return st.sync();
+}
+
+int pz_shuffle_validators_to_committees(const uint8_t seed[32], const uint64_t* start, const uint64_t* end,
+                                        uint64_t n, uint64_t dynasty, uint64_t crosslink_start_shard,
+                                        uint32_t* members, uint64_t* coffs, uint64_t* shard_id, uint64_t* slot_offs,
+                                        uint64_t cap_comm, uint64_t* ncomm) {
+  if (!ncomm || !slot_offs) return fail(PZ_EINVAL, "null pointer");
+  *ncomm = 0;
+  // ActiveValidatorIndices on the device, then the host swap chain (sharding.go:12-16)
+  std::vector<uint32_t> idx(n ? n : 1);
+  uint64_t na = 0;
+  int rc = pz_validator_indices(start, end, n, dynasty, PZ_KIND_ACTIVE, idx.data(), &na);
+  if (rc) return rc;
+  if ((rc = pz_shuffle_indices(seed, idx.data(), na))) return rc;
+  // getCommitteeParams (sharding.go:60-73)
+  const uint64_t cyc = PZ_CYCLE_LENGTH;
+  uint64_t cps = 1, spc = 1;
+  if (na >= cyc * PZ_MIN_COMMITTEE_SIZE) {
+    cps = na / (cyc * PZ_MIN_COMMITTEE_SIZE * 2) + 1;
+  } else {
+    while (na * spc < PZ_MIN_COMMITTEE_SIZE * cyc && spc < cyc) spc *= 2;
+  }
+  if (cap_comm < cyc * cps) {
+    *ncomm = cyc * cps;
+    return fail(PZ_ERANGE, "need room for %llu committees", (unsigned long long)(cyc * cps));
+  }
+  if (!coffs || !shard_id || (na && !members)) return fail(PZ_EINVAL, "null pointer");
+  // splitBySlotShard (sharding.go:27-53): SplitIndices into 64 slots, each into cps committees
+  uint64_t c = 0;
+  coffs[0] = 0;
+  for (uint64_t i = 0; i < cyc; ++i) {
+    slot_offs[i] = c;
+    const uint64_t s0 = na * i / cyc, s1 = na * (i + 1) / cyc, len = s1 - s0;
+    const uint64_t shard_start = crosslink_start_shard + i * cps / spc;
+    for (uint64_t j = 0; j < cps; ++j, ++c) {
+      const uint64_t c0 = s0 + len * j / cps, c1 = s0 + len * (j + 1) / cps;
+      shard_id[c] = (shard_start + j) % PZ_SHARD_COUNT;
+      std::memcpy(members + coffs[c], idx.data() + c0, (c1 - c0) * 4);
+      coffs[c + 1] = coffs[c] + (c1 - c0);
+    }
+  }
+  slot_offs[cyc] = c;
+  *ncomm = c;
   return PZ_OK;
 }
 

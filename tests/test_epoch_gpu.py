@@ -272,3 +272,36 @@ def test_device_epoch_repeated_steps_ping_pong():
             assert int(scal[b, _lib.SCAL_NEXT_BAL]) == nxt and bool(scal[b, _lib.SCAL_APPLIED]) == applied
             np.testing.assert_array_equal(win[b], w)
             inst["balance"][b] = nb  # the oracle's next step starts from the new balances
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,seed", [(1, 1), (100, 2), (5000, 3), (70000, 4)])
+def test_rotate_validator_set_vs_oracle(n, seed):
+    """pz_rotate_validator_set against the oracle on mixed sets: active / queued / exited,
+    balances around the 16 cut, and more queued validators than len(active)/30 + 1."""
+    rng = np.random.default_rng(seed)
+    dyn = 50
+    start = rng.choice([0, 10, 49, 50, 51, 80], size=n).astype(U64)
+    end = rng.choice([20, 50, 51, 200, DEFAULT_END_DYNASTY], size=n).astype(U64)
+    bal = rng.integers(10, 40, size=n).astype(U64)
+    vals = [pb.ValidatorRecord(balance=int(b), start_dynasty=int(s), end_dynasty=int(e))
+            for b, s, e in zip(bal, start, end)]
+    ref.rotate_validator_set(vals, dyn)
+    s2, e2 = start.copy(), end.copy()
+    casper.rotate_validator_set(bal, s2, e2, dyn)
+    assert s2.tolist() == [v.start_dynasty for v in vals]
+    assert e2.tolist() == [v.end_dynasty for v in vals]
+
+
+@pytest.mark.gpu
+def test_committees_partial_active_and_start_shard():
+    n = 20000
+    rng = np.random.default_rng(8)
+    s = rng.choice([0, 0, 0, 7], size=n).astype(U64)
+    e = rng.choice([DEFAULT_END_DYNASTY, DEFAULT_END_DYNASTY, 2], size=n).astype(U64)
+    got = casper.shuffle_validators_to_committees(ref.bytes_to_hash(b"B"), s, e, 3, 1000)
+    vals = [pb.ValidatorRecord(start_dynasty=int(a), end_dynasty=int(b)) for a, b in zip(s, e)]
+    want = ref.shuffle_validators_to_committees(ref.bytes_to_hash(b"B"), vals, 3, 1000)
+    for g, w in zip(got, want):
+        assert [(sh, c.tolist()) for sh, c in g] == [(sc.shard_id, list(sc.committee))
+                                                     for sc in w.array_shard_and_committee]
