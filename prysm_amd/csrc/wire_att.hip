@@ -203,123 +203,244 @@ __device__ __forceinline__ void write_record(const AttArgs& a, const Head& h, ui
   }
 }
 
-// Gather by output position.  A record that fits the wave's 1 KB stage, with at most 64
-// oblique elements and 64 signature values, is written in two steps:
-//  1. layout: the literal bytes (tags, lengths, varints) go into the LDS stage, and a byte
-//     map marks which data segment (bytes field or oblique element) covers each output byte;
-//  2. gather: lane l produces output bytes l, l+64, ... -- a literal from the stage or a byte
-//     of its segment's source -- with every source load of the record issued before the
-//     first store, then stores them coalesced.
-// (Copying segment by segment made each copy's store wait for its load: ~14 dependent round
-// trips per record, 2.5 ms per 1M config-2 records.)  Other records take write_record.
-constexpr uint32_t kStage = 1024, kSegs = 3 + 64, kLiteral = 255;
+// Each half-wave (32 lanes) owns a record.  A record of at most kStage bytes whose
+// segments (bytes fields 4-6 and oblique elements, at most 29 elements) are each at most
+// kSegMax bytes, with at most 32 signature values, is assembled in the half's LDS stage and
+// stored from there:
+//  1. layout: sub-lane 0 writes the literal bytes (tags, lengths, scalar varints), sub-lane e
+//     an element's header and sub-lane v a signature varint;
+//  2. segments: sub-lane s copies segment s (s < 3: bytes field s, else element s - 3) with
+//     dword loads aligned on its source, realigned in registers and written into the stage
+//     byte by byte -- every lane's loads are in flight together;
+//  3. store: the stage holds record byte j at sh + j with sh = o mod 16, so its 16-byte
+//     blocks are the output's: whole blocks go out as dwordx4 stores, the two partial edge
+//     blocks (shared with the neighbouring records) byte by byte.
+// Other records are written by the whole wave, segment by segment (write_record).
+//
+// A record takes three dependent memory round trips (head -> element offsets -> segment
+// bytes), so the kernel is latency-bound; what raises throughput is records in flight and
+// few instructions per record:
+//  - two records per wave (rocprofv3: 57% of a wave's cycles were memory waits with one);
+//  - the record's head spread over the sub-lanes (one load instruction, read with readlane);
+//  - element / signature sizes scanned with DPP adds, not LDS permutes;
+//  - loads in the global address space: generic (flat) loads share lgkmcnt with the LDS
+//    reads, and a byte gather through a per-byte segment map made each load wait for two
+//    dependent LDS reads -- the earlier kernel fetched a record's bytes almost one round
+//    trip at a time.
+// (A persistent, software-pipelined variant that prefetched the next record's head needed
+// 130+ VGPRs -- 3 waves per SIMD -- and was slower.)
+constexpr uint32_t kStage = 768, kStageAlloc = kStage + 32, kSegMax = 64, kSegWords = kSegMax / 4 + 1;
+
+// Sub-lane k of the half loads head word k:
+//   0-2   slot, shard_id, justified_slot
+//   3-8   bytes fields 4-6: start, end (boff[k][i], boff[k][i+1])
+//   9-10  oblique element range     11-12  signature value range     13-14  offs[i], offs[i+1]
+constexpr int kHeadWords = 15;
+
+__device__ __forceinline__ uint64_t head_word(const AttArgs& a, int k, uint64_t i) {
+  const uint64_t* p = nullptr;
+  uint32_t d = 0;
+  if (k < 3) {
+    p = a.col[k];
+  } else if (k < 9) {
+    p = a.boff[(k - 3) >> 1];
+    d = (k - 3) & 1;
+  } else if (k < kHeadWords) {
+    p = k < 11 ? a.ofirst : k < 13 ? a.sfirst : a.offs;
+    d = (k - 9) & 1;
+  }
+  return p ? p[i + d] : 0;
+}
+
+__device__ __forceinline__ uint64_t rl64(uint64_t x, int k) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, k), hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), k);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Word k of this half's head.
+__device__ __forceinline__ uint64_t hw(uint64_t hv, int k, bool upper) {
+  const uint64_t lo = rl64(hv, k), hi = rl64(hv, 32 + k);
+  return upper ? hi : lo;
+}
+
+// Inclusive scan over each half-wave with DPP: rows of 16 by shifts of 1, 2, 4, 8, then
+// row 1's total into row 1 and row 3's... (row_bcast:15 adds row r-1's last lane to rows 1, 3).
+__device__ __forceinline__ uint32_t hscan32(uint32_t x) {
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);
+  return x;
+}
+
+__device__ __forceinline__ uint32_t half_total(uint32_t x, bool upper) {
+  const uint32_t lo = __builtin_amdgcn_readlane(x, 31), hi = __builtin_amdgcn_readlane(x, 63);
+  return upper ? hi : lo;
+}
 
 extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_write_kernel(AttArgs a) {
-  __shared__ uint8_t stage[kWaves][kStage];
-  __shared__ uint8_t segmap[kWaves][kStage];
-  __shared__ const uint8_t* seg_src[kWaves][kSegs];
-  __shared__ uint32_t seg_dst[kWaves][kSegs];
-  const uint64_t i = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-  if (i >= a.n) return;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kWaves][2][kStageAlloc];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int sl = lane & 31;
+  const bool upper = lane >= 32;
+  const uint64_t i0 = ((uint64_t)blockIdx.x * kWaves + w) * 2;  // the wave's records: i0, i0 + 1
+  if (i0 >= a.n) return;
+  const uint64_t i = i0 + upper;
+  const bool valid = i < a.n;
+  const uint64_t hv = valid && sl < kHeadWords ? head_word(a, sl, i) : 0;
   Head h;
-  load_head(a, i, h);
-  const uint64_t o = a.offs[i], size = a.offs[i + 1] - o;
-  const uint64_t nob = h.o1 - h.o0, nsig = h.s1 - h.s0;
-  if (size > kStage || nob > 64 || nsig > 64) {
-    uint64_t fixed, obl, sigb;
-    record_parts(a, h, &fixed, &obl, &sigb);
-    write_record(a, h, body_size(fixed, obl, sigb), sigb, a.out + o);
-    return;
-  }
-  // one lane per oblique element / signature value
-  uint64_t eb0 = 0, el = 0, sv = 0;
-  if ((uint64_t)lane < nob) {
-    eb0 = a.ooff[h.o0 + lane];
-    el = a.ooff[h.o0 + lane + 1] - eb0;
-  }
-  if ((uint64_t)lane < nsig) sv = a.sig[h.s0 + lane];
-  const uint64_t esz = (uint64_t)lane < nob ? 1 + vlen(el) + el : 0;
-  const uint64_t ssz = (uint64_t)lane < nsig ? vlen(sv) : 0;
-  const uint64_t einc = wscan(esz), sinc = wscan(ssz);
-  const uint64_t obl = __shfl(einc, 63, 64), sigb = __shfl(sinc, 63, 64);
-  uint64_t fixed = 0;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    fixed += h.v[k] ? 1 + vlen(h.v[k]) : 0;
-    fixed += h.bl[k] ? 1 + vlen(h.bl[k]) + h.bl[k] : 0;
+    h.v[k] = hw(hv, k, upper);
+    h.b0[k] = hw(hv, 3 + 2 * k, upper);
+    h.bl[k] = hw(hv, 4 + 2 * k, upper) - h.b0[k];
   }
-  const uint64_t body = body_size(fixed, obl, sigb);
-  uint8_t* st = stage[w];
-  uint8_t* map = segmap[w];
-  for (uint32_t j = lane; j < size; j += 64) map[j] = kLiteral;
-  __builtin_amdgcn_wave_barrier();
-  // 1. layout: lane 0 writes the frame and fields 1-6's headers; segments 0-2 are fields 4-6
-  uint32_t pos = 0;
-  if (a.field) {
-    if (lane == 0) {
-      uint8_t* q = put_varint(st, ((uint64_t)a.field << 3) | 2);
-      put_varint(q, body);
-    }
-    pos += a.tag_len + vlen(body);
+  h.o0 = hw(hv, 9, upper);
+  h.o1 = hw(hv, 10, upper);
+  h.s0 = hw(hv, 11, upper);
+  h.s1 = hw(hv, 12, upper);
+  const uint64_t o = hw(hv, 13, upper), size = hw(hv, 14, upper) - o;
+  const uint64_t nob = h.o1 - h.o0, nsig = h.s1 - h.s0;
+  bool fast = valid && size <= kStage && nob <= 29 && nsig <= 32;
+  // one sub-lane per element / signature value; segment s = sub-lane s
+  uint64_t eb0 = 0, sv = 0;
+  uint32_t el = 0;
+  if (fast && (uint64_t)sl < nob) {
+    eb0 = a.ooff[h.o0 + sl];
+    el = (uint32_t)(a.ooff[h.o0 + sl + 1] - eb0);
   }
+  if (fast && (uint64_t)sl < nsig) sv = a.sig[h.s0 + sl];
+  // this sub-lane's segment: source and length (element sl - 3 arrives from sub-lane sl - 3)
+  const uint32_t el_seg = (uint32_t)__shfl((int)el, lane - 3, 64);
+  const uint64_t eb_seg = ((uint64_t)(uint32_t)__shfl((int)(eb0 >> 32), lane - 3, 64) << 32) |
+                          (uint32_t)__shfl((int)(uint32_t)eb0, lane - 3, 64);
+  uint64_t seg_len = 0;
+  const uint8_t* seg_src = nullptr;
+#pragma unroll
   for (int k = 0; k < 3; ++k)
-    if (h.v[k]) {
-      if (lane == 0) {
-        st[pos] = (uint8_t)((k + 1) << 3);
-        put_varint(st + pos + 1, h.v[k]);
-      }
-      pos += 1 + vlen(h.v[k]);
+    if (sl == k) {
+      seg_len = h.bl[k];
+      seg_src = a.bdat[k] + h.b0[k];
     }
-  for (int k = 0; k < 3; ++k)
-    if (h.bl[k]) {
-      const uint32_t hl = 1 + vlen(h.bl[k]);
-      if (lane == 0) {
-        st[pos] = (uint8_t)(((k + 4) << 3) | 2);
-        put_varint(st + pos + 1, h.bl[k]);
-        seg_src[w][k] = a.bdat[k] + h.b0[k];
-        seg_dst[w][k] = pos + hl;
-      }
-      for (uint32_t j = lane; j < h.bl[k]; j += 64) map[pos + hl + j] = (uint8_t)k;
-      pos += hl + (uint32_t)h.bl[k];
-    }
-  // field 7: lane e lays out element e (segment 3 + e)
-  if ((uint64_t)lane < nob) {
-    const uint32_t ep = pos + (uint32_t)(einc - esz), hl = 1 + vlen(el);
-    st[ep] = (7 << 3) | 2;
-    put_varint(st + ep + 1, el);
-    seg_src[w][3 + lane] = a.odat + eb0;
-    seg_dst[w][3 + lane] = ep + hl;
-    for (uint32_t j = 0; j < el; ++j) map[ep + hl + j] = (uint8_t)(3 + lane);
+  if (sl >= 3 && (uint64_t)(sl - 3) < nob) {
+    seg_len = el_seg;
+    seg_src = a.odat + eb_seg;
   }
-  pos += (uint32_t)obl;
-  // field 8: the header by lane 0, one varint per lane
-  if (sigb) {
-    const uint32_t hl = 1 + vlen(sigb);
-    if (lane == 0) {
-      st[pos] = (8 << 3) | 2;
-      put_varint(st + pos + 1, sigb);
+  // a segment over kSegMax sends its record to the whole-wave path
+  const uint64_t long_seg = __ballot(fast && seg_len > kSegMax);
+  if ((long_seg >> (upper ? 32 : 0)) & 0xffffffffull) fast = false;
+  const uint32_t esz = fast && (uint64_t)sl < nob ? 1 + vlen(el) + el : 0;
+  const uint32_t ssz = fast && (uint64_t)sl < nsig ? vlen(sv) : 0;
+  const uint32_t einc = hscan32(esz), sinc = hscan32(ssz);
+  const uint32_t obl = half_total(einc, upper), sigb = half_total(sinc, upper);
+  // 2a. the segment loads go out first: dwords aligned on the source covering its bytes
+  typedef const __attribute__((address_space(1))) uint32_t gword;
+  const uint32_t len = fast ? (uint32_t)seg_len : 0;
+  const uint32_t r = (uint32_t)(uintptr_t)seg_src & 3;
+  gword* ws = reinterpret_cast<gword*>((uintptr_t)seg_src & ~(uintptr_t)3);
+  const uint32_t nw = len ? (r + len + 3) / 4 : 0;
+  uint32_t wv[kSegWords + 1];
+#pragma unroll
+  for (int k = 0; k <= (int)kSegWords; ++k) wv[k] = (uint32_t)k < nw ? ws[k] : 0;
+  // 1. layout
+  const uint32_t sh = (uint32_t)o & 15;
+  uint8_t* st = stage[w][upper] + sh;
+  uint32_t pos = 0, seg_dst = 0;
+  if (fast) {
+    uint64_t fixed = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      fixed += h.v[k] ? 1 + vlen(h.v[k]) : 0;
+      fixed += h.bl[k] ? 1 + vlen(h.bl[k]) + h.bl[k] : 0;
     }
-    if ((uint64_t)lane < nsig) put_varint(st + pos + hl + (uint32_t)(sinc - ssz), sv);
+    const uint64_t body = body_size(fixed, obl, sigb);
+    if (a.field) {
+      if (sl == 0) {
+        uint8_t* q = put_varint(st, ((uint64_t)a.field << 3) | 2);
+        put_varint(q, body);
+      }
+      pos += a.tag_len + vlen(body);
+    }
+    for (int k = 0; k < 3; ++k)
+      if (h.v[k]) {
+        if (sl == 0) {
+          st[pos] = (uint8_t)((k + 1) << 3);
+          put_varint(st + pos + 1, h.v[k]);
+        }
+        pos += 1 + vlen(h.v[k]);
+      }
+    for (int k = 0; k < 3; ++k)
+      if (h.bl[k]) {
+        const uint32_t hl = 1 + vlen(h.bl[k]);
+        if (sl == 0) {
+          st[pos] = (uint8_t)(((k + 4) << 3) | 2);
+          put_varint(st + pos + 1, h.bl[k]);
+        }
+        if (sl == k) seg_dst = pos + hl;
+        pos += hl + (uint32_t)h.bl[k];
+      }
+    // field 7: sub-lane e writes element e's header; its bytes are segment 3 + e
+    const uint32_t ep = pos + einc - esz;
+    if ((uint64_t)sl < nob) {
+      st[ep] = (7 << 3) | 2;
+      put_varint(st + ep + 1, el);
+    }
+    const uint32_t ed = (uint32_t)__shfl((int)(ep + 1 + vlen(el)), lane - 3, 64);
+    if (sl >= 3 && (uint64_t)(sl - 3) < nob) seg_dst = ed;
+    pos += obl;
+    // field 8: the header by sub-lane 0, one varint per sub-lane
+    if (sigb) {
+      const uint32_t hl = 1 + vlen(sigb);
+      if (sl == 0) {
+        st[pos] = (8 << 3) | 2;
+        put_varint(st + pos + 1, sigb);
+      }
+      if ((uint64_t)sl < nsig) put_varint(st + pos + hl + sinc - ssz, sv);
+    }
+  }
+  // 2b. realign the segment's words on its first byte and write them into the stage
+#pragma unroll
+  for (int k = 0; k < (int)kSegWords; ++k) {
+    const uint32_t d = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], r);
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if ((uint32_t)(4 * k + b) < len) st[seg_dst + 4 * k + b] = (uint8_t)(d >> (8 * b));
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  // 2. gather: every source load of the record before the first store
-  constexpr int kPerLane = kStage / 64;
-  uint8_t byte[kPerLane];
-#pragma unroll
-  for (int t = 0; t < kPerLane; ++t) {
-    const uint32_t j = lane + 64 * t;
-    byte[t] = 0;
-    if (j < size) {
-      const uint8_t sg = map[j];
-      byte[t] = sg == kLiteral ? st[j] : seg_src[w][sg][j - seg_dst[w][sg]];
+  // 3. store: stage block q <-> output block (o >> 4) + q
+  const uint32_t sz = fast ? (uint32_t)size : 0;
+  const uint32_t nblk = (sh + sz + 15) / 16;
+  const uint8_t* sb = stage[w][upper];
+  uint8_t* ob = a.out + (o - sh);
+  for (uint32_t q = sl; q < nblk; q += 32) {
+    const uint32_t lo = 16 * q, hi = lo + 16;
+    if (lo >= sh && hi <= sh + sz) {
+      *reinterpret_cast<uint4*>(ob + lo) = *reinterpret_cast<const uint4*>(sb + lo);
+    } else {
+      for (uint32_t x = max(lo, sh); x < min(hi, sh + sz); ++x) ob[x] = sb[x];
     }
   }
+  // records the half-wave layout does not take: the whole wave, segment by segment
+  for (int u = 0; u < 2; ++u) {
+    const uint64_t iu = i0 + u;
+    if (iu >= a.n) break;
+    if (__builtin_amdgcn_readlane((uint32_t)fast, 32 * u)) continue;
+    Head g;
 #pragma unroll
-  for (int t = 0; t < kPerLane; ++t) {
-    const uint32_t j = lane + 64 * t;
-    if (j < size) a.out[o + j] = byte[t];
+    for (int k = 0; k < 3; ++k) {
+      g.v[k] = rl64(hv, 32 * u + k);
+      g.b0[k] = rl64(hv, 32 * u + 3 + 2 * k);
+      g.bl[k] = rl64(hv, 32 * u + 4 + 2 * k) - g.b0[k];
+    }
+    g.o0 = rl64(hv, 32 * u + 9);
+    g.o1 = rl64(hv, 32 * u + 10);
+    g.s0 = rl64(hv, 32 * u + 11);
+    g.s1 = rl64(hv, 32 * u + 12);
+    uint64_t fixed, obl8, sigb8;
+    record_parts(a, g, &fixed, &obl8, &sigb8);
+    write_record(a, g, body_size(fixed, obl8, sigb8), sigb8, a.out + rl64(hv, 32 * u + 13));
   }
 }
 
@@ -378,8 +499,8 @@ hipError_t launch_sizes_offsets(AttArgs a, void* scratch, hipStream_t s) {
 
 hipError_t launch_write(const AttArgs& a, hipStream_t s) {
   if (!a.n) return hipSuccess;
-  hipLaunchKernelGGL(pz_wire_att_write_kernel, dim3((uint32_t)((a.n + kWaves - 1) / kWaves)), dim3(kThreads), 0, s,
-                     a);
+  hipLaunchKernelGGL(pz_wire_att_write_kernel, dim3((uint32_t)((a.n + 2 * kWaves - 1) / (2 * kWaves))), dim3(kThreads),
+                     0, s, a);
   return hipGetLastError();
 }
 
