@@ -8,12 +8,12 @@
 // (repeated bytes: every element emitted, an empty one as `3a 00`), aggregate_sig 8 (packed
 // varints, omitted when empty).
 //
-// Records are hundreds of bytes, so a wave owns a record.  Three launches:
+// Three launches:
 //   size   one lane per record
 //   scan   rocPRIM inclusive scan of the sizes into offsets[1..n]
-//   write  one wave per record: the record's literal bytes and a map of its data segments are
-//          laid out in LDS, then each lane gathers its output bytes (all source loads in
-//          flight at once) and stores them coalesced
+//   write  one 16-lane DPP row per record: the record is assembled in an LDS stage (literals
+//          by the row's lanes, data segments copied with aligned dword loads) and stored in
+//          16-byte blocks
 // The columns of a record are read twice (size, write); the output is written once.
 #include <hip/hip_runtime.h>
 
@@ -203,10 +203,10 @@ __device__ __forceinline__ void write_record(const AttArgs& a, const Head& h, ui
   }
 }
 
-// Each half-wave (32 lanes) owns a record.  A record of at most kStage bytes whose
-// segments (bytes fields 4-6 and oblique elements, at most 29 elements) are each at most
-// kSegMax bytes, with at most 32 signature values, is assembled in the half's LDS stage and
-// stored from there:
+// Each DPP row (16 lanes) owns a record, four per wave.  A record of at most kStage bytes
+// whose segments (bytes fields 4-6 and oblique elements, at most 13 elements) are each at
+// most kSegMax bytes, with at most 16 signature values, is assembled in the row's LDS stage
+// and stored from there:
 //  1. layout: sub-lane 0 writes the literal bytes (tags, lengths, scalar varints), sub-lane e
 //     an element's header and sub-lane v a signature varint;
 //  2. segments: sub-lane s copies segment s (s < 3: bytes field s, else element s - 3) with
@@ -219,10 +219,11 @@ __device__ __forceinline__ void write_record(const AttArgs& a, const Head& h, ui
 //
 // A record takes three dependent memory round trips (head -> element offsets -> segment
 // bytes), so the kernel is latency-bound; what raises throughput is records in flight and
-// few instructions per record:
-//  - two records per wave (rocprofv3: 57% of a wave's cycles were memory waits with one);
-//  - the record's head spread over the sub-lanes (one load instruction, read with readlane);
-//  - element / signature sizes scanned with DPP adds, not LDS permutes;
+// few instructions per record (1M config-2 records: 1.66 ms with a wave per record and a
+// per-byte gather, 0.82 ms with a record per half-wave, 0.45 ms with one per row):
+//  - four records per wave (rocprofv3: 57% of a wave's cycles were memory waits with one);
+//  - the record's head spread over the row (one load instruction, DPP row_newbcast reads);
+//  - element / signature sizes scanned with DPP row shifts, not LDS permutes;
 //  - loads in the global address space: generic (flat) loads share lgkmcnt with the LDS
 //    reads, and a byte gather through a per-byte segment map made each load wait for two
 //    dependent LDS reads -- the earlier kernel fetched a record's bytes almost one round
@@ -231,7 +232,10 @@ __device__ __forceinline__ void write_record(const AttArgs& a, const Head& h, ui
 // 130+ VGPRs -- 3 waves per SIMD -- and was slower.)
 constexpr uint32_t kStage = 768, kStageAlloc = kStage + 32, kSegMax = 64, kSegWords = kSegMax / 4 + 1;
 
-// Sub-lane k of the half loads head word k:
+// A record per DPP row: 16 lanes, four records per wave.
+constexpr int kRow = 16, kRecs = 64 / kRow, kMaxOblique = kRow - 3;
+
+// Sub-lane k of the row loads head word k:
 //   0-2   slot, shard_id, justified_slot
 //   3-8   bytes fields 4-6: start, end (boff[k][i], boff[k][i+1])
 //   9-10  oblique element range     11-12  signature value range     13-14  offs[i], offs[i+1]
@@ -257,52 +261,56 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, int k) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// Word k of this half's head.
-__device__ __forceinline__ uint64_t hw(uint64_t hv, int k, bool upper) {
-  const uint64_t lo = rl64(hv, k), hi = rl64(hv, 32 + k);
-  return upper ? hi : lo;
+// Lane K of this lane's row (DPP row_newbcast).
+template <int K>
+__device__ __forceinline__ uint32_t bc32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x150 + K, 0xf, 0xf, false);
+}
+template <int K>
+__device__ __forceinline__ uint64_t bc64(uint64_t x) {
+  return ((uint64_t)bc32<K>((uint32_t)(x >> 32)) << 32) | bc32<K>((uint32_t)x);
 }
 
-// Inclusive scan over each half-wave with DPP: rows of 16 by shifts of 1, 2, 4, 8, then
-// row 1's total into row 1 and row 3's... (row_bcast:15 adds row r-1's last lane to rows 1, 3).
-__device__ __forceinline__ uint32_t hscan32(uint32_t x) {
+// Lane l - 3 of the row (0 for l < 3; DPP row_shr:3).
+__device__ __forceinline__ uint32_t shr3(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x113, 0xf, 0xf, false);
+}
+
+// Inclusive scan over each row with DPP shifts of 1, 2, 4, 8.
+__device__ __forceinline__ uint32_t rscan32(uint32_t x) {
   x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);
   x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);
   x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);
   x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);
   return x;
 }
 
-__device__ __forceinline__ uint32_t half_total(uint32_t x, bool upper) {
-  const uint32_t lo = __builtin_amdgcn_readlane(x, 31), hi = __builtin_amdgcn_readlane(x, 63);
-  return upper ? hi : lo;
-}
-
 extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_write_kernel(AttArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kWaves][2][kStageAlloc];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kWaves][kRecs][kStageAlloc];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int sl = lane & 31;
-  const bool upper = lane >= 32;
-  const uint64_t i0 = ((uint64_t)blockIdx.x * kWaves + w) * 2;  // the wave's records: i0, i0 + 1
+  const int sl = lane & (kRow - 1), ri = lane / kRow;
+  const uint64_t i0 = ((uint64_t)blockIdx.x * kWaves + w) * kRecs;  // the wave's records: i0 .. i0 + 3
   if (i0 >= a.n) return;
-  const uint64_t i = i0 + upper;
+  const uint64_t i = i0 + ri;
   const bool valid = i < a.n;
   const uint64_t hv = valid && sl < kHeadWords ? head_word(a, sl, i) : 0;
   Head h;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    h.v[k] = hw(hv, k, upper);
-    h.b0[k] = hw(hv, 3 + 2 * k, upper);
-    h.bl[k] = hw(hv, 4 + 2 * k, upper) - h.b0[k];
-  }
-  h.o0 = hw(hv, 9, upper);
-  h.o1 = hw(hv, 10, upper);
-  h.s0 = hw(hv, 11, upper);
-  h.s1 = hw(hv, 12, upper);
-  const uint64_t o = hw(hv, 13, upper), size = hw(hv, 14, upper) - o;
+  h.v[0] = bc64<0>(hv);
+  h.v[1] = bc64<1>(hv);
+  h.v[2] = bc64<2>(hv);
+  h.b0[0] = bc64<3>(hv);
+  h.bl[0] = bc64<4>(hv) - h.b0[0];
+  h.b0[1] = bc64<5>(hv);
+  h.bl[1] = bc64<6>(hv) - h.b0[1];
+  h.b0[2] = bc64<7>(hv);
+  h.bl[2] = bc64<8>(hv) - h.b0[2];
+  h.o0 = bc64<9>(hv);
+  h.o1 = bc64<10>(hv);
+  h.s0 = bc64<11>(hv);
+  h.s1 = bc64<12>(hv);
+  const uint64_t o = bc64<13>(hv), size = bc64<14>(hv) - o;
   const uint64_t nob = h.o1 - h.o0, nsig = h.s1 - h.s0;
-  bool fast = valid && size <= kStage && nob <= 29 && nsig <= 32;
+  bool fast = valid && size <= kStage && nob <= kMaxOblique && nsig <= kRow;
   // one sub-lane per element / signature value; segment s = sub-lane s
   uint64_t eb0 = 0, sv = 0;
   uint32_t el = 0;
@@ -312,9 +320,8 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_write_kernel(
   }
   if (fast && (uint64_t)sl < nsig) sv = a.sig[h.s0 + sl];
   // this sub-lane's segment: source and length (element sl - 3 arrives from sub-lane sl - 3)
-  const uint32_t el_seg = (uint32_t)__shfl((int)el, lane - 3, 64);
-  const uint64_t eb_seg = ((uint64_t)(uint32_t)__shfl((int)(eb0 >> 32), lane - 3, 64) << 32) |
-                          (uint32_t)__shfl((int)(uint32_t)eb0, lane - 3, 64);
+  const uint32_t el_seg = shr3(el);
+  const uint64_t eb_seg = ((uint64_t)shr3((uint32_t)(eb0 >> 32)) << 32) | shr3((uint32_t)eb0);
   uint64_t seg_len = 0;
   const uint8_t* seg_src = nullptr;
 #pragma unroll
@@ -329,11 +336,11 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_write_kernel(
   }
   // a segment over kSegMax sends its record to the whole-wave path
   const uint64_t long_seg = __ballot(fast && seg_len > kSegMax);
-  if ((long_seg >> (upper ? 32 : 0)) & 0xffffffffull) fast = false;
+  if ((long_seg >> (kRow * ri)) & 0xffffull) fast = false;
   const uint32_t esz = fast && (uint64_t)sl < nob ? 1 + vlen(el) + el : 0;
   const uint32_t ssz = fast && (uint64_t)sl < nsig ? vlen(sv) : 0;
-  const uint32_t einc = hscan32(esz), sinc = hscan32(ssz);
-  const uint32_t obl = half_total(einc, upper), sigb = half_total(sinc, upper);
+  const uint32_t einc = rscan32(esz), sinc = rscan32(ssz);
+  const uint32_t obl = bc32<15>(einc), sigb = bc32<15>(sinc);
   // 2a. the segment loads go out first: dwords aligned on the source covering its bytes
   typedef const __attribute__((address_space(1))) uint32_t gword;
   const uint32_t len = fast ? (uint32_t)seg_len : 0;
@@ -345,7 +352,7 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_write_kernel(
   for (int k = 0; k <= (int)kSegWords; ++k) wv[k] = (uint32_t)k < nw ? ws[k] : 0;
   // 1. layout
   const uint32_t sh = (uint32_t)o & 15;
-  uint8_t* st = stage[w][upper] + sh;
+  uint8_t* st = stage[w][ri] + sh;
   uint32_t pos = 0, seg_dst = 0;
   if (fast) {
     uint64_t fixed = 0;
@@ -386,7 +393,7 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_write_kernel(
       st[ep] = (7 << 3) | 2;
       put_varint(st + ep + 1, el);
     }
-    const uint32_t ed = (uint32_t)__shfl((int)(ep + 1 + vlen(el)), lane - 3, 64);
+    const uint32_t ed = shr3(ep + 1 + vlen(el));
     if (sl >= 3 && (uint64_t)(sl - 3) < nob) seg_dst = ed;
     pos += obl;
     // field 8: the header by sub-lane 0, one varint per sub-lane
@@ -412,9 +419,9 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_write_kernel(
   // 3. store: stage block q <-> output block (o >> 4) + q
   const uint32_t sz = fast ? (uint32_t)size : 0;
   const uint32_t nblk = (sh + sz + 15) / 16;
-  const uint8_t* sb = stage[w][upper];
+  const uint8_t* sb = stage[w][ri];
   uint8_t* ob = a.out + (o - sh);
-  for (uint32_t q = sl; q < nblk; q += 32) {
+  for (uint32_t q = sl; q < nblk; q += kRow) {
     const uint32_t lo = 16 * q, hi = lo + 16;
     if (lo >= sh && hi <= sh + sz) {
       *reinterpret_cast<uint4*>(ob + lo) = *reinterpret_cast<const uint4*>(sb + lo);
@@ -423,24 +430,24 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_write_kernel(
     }
   }
   // records the half-wave layout does not take: the whole wave, segment by segment
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < kRecs; ++u) {
     const uint64_t iu = i0 + u;
     if (iu >= a.n) break;
-    if (__builtin_amdgcn_readlane((uint32_t)fast, 32 * u)) continue;
+    if (__builtin_amdgcn_readlane((uint32_t)fast, kRow * u)) continue;
     Head g;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      g.v[k] = rl64(hv, 32 * u + k);
-      g.b0[k] = rl64(hv, 32 * u + 3 + 2 * k);
-      g.bl[k] = rl64(hv, 32 * u + 4 + 2 * k) - g.b0[k];
+      g.v[k] = rl64(hv, kRow * u + k);
+      g.b0[k] = rl64(hv, kRow * u + 3 + 2 * k);
+      g.bl[k] = rl64(hv, kRow * u + 4 + 2 * k) - g.b0[k];
     }
-    g.o0 = rl64(hv, 32 * u + 9);
-    g.o1 = rl64(hv, 32 * u + 10);
-    g.s0 = rl64(hv, 32 * u + 11);
-    g.s1 = rl64(hv, 32 * u + 12);
+    g.o0 = rl64(hv, kRow * u + 9);
+    g.o1 = rl64(hv, kRow * u + 10);
+    g.s0 = rl64(hv, kRow * u + 11);
+    g.s1 = rl64(hv, kRow * u + 12);
     uint64_t fixed, obl8, sigb8;
     record_parts(a, g, &fixed, &obl8, &sigb8);
-    write_record(a, g, body_size(fixed, obl8, sigb8), sigb8, a.out + rl64(hv, 32 * u + 13));
+    write_record(a, g, body_size(fixed, obl8, sigb8), sigb8, a.out + rl64(hv, kRow * u + 13));
   }
 }
 
@@ -499,8 +506,8 @@ hipError_t launch_sizes_offsets(AttArgs a, void* scratch, hipStream_t s) {
 
 hipError_t launch_write(const AttArgs& a, hipStream_t s) {
   if (!a.n) return hipSuccess;
-  hipLaunchKernelGGL(pz_wire_att_write_kernel, dim3((uint32_t)((a.n + 2 * kWaves - 1) / (2 * kWaves))), dim3(kThreads),
-                     0, s, a);
+  hipLaunchKernelGGL(pz_wire_att_write_kernel, dim3((uint32_t)((a.n + kRecs * kWaves - 1) / (kRecs * kWaves))),
+                     dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 

@@ -62,20 +62,25 @@ def test_long_repeated_fields_and_empty_elements():
 
 @pytest.mark.parametrize("field_num", [0, 1])
 def test_half_wave_path_limits(field_num):
-    """Records at and just past the half-wave path's limits (wire_att.hip: 29 oblique
-    elements, 32 signature values, 64-byte segments, 768-byte records) next to each other, so
-    both paths share waves, with segment sources at every alignment."""
+    """Records at and just past the row path's limits (wire_att.hip: 13 oblique elements,
+    16 signature values, 64-byte segments, 768-byte records) next to each other, so both
+    paths share waves, with segment sources at every alignment."""
     rng = np.random.default_rng(11 + field_num)
     atts = []
-    for nob in (0, 1, 28, 29, 30, 32, 33):
+    for nob in (0, 1, 12, 13, 14, 33):
         for seg in (0, 1, 31, 32, 33, 63, 64, 65):
-            for nsig in (0, 31, 32, 33):
+            for nsig in (0, 15, 16, 17):
                 atts.append(pb.AttestationRecord(
                     slot=rand_u64(rng), shard_id=int(rng.integers(0, 3)), justified_slot=rand_u64(rng),
                     justified_block_hash=rand_bytes(rng, seg, seg + 1), shard_block_hash=rand_bytes(rng, 0, 66),
                     attester_bitfield=rand_bytes(rng, max(seg - 1, 0), seg + 2),
                     oblique_parent_hashes=[rand_bytes(rng, 0, min(seg, 24) + 1) for _ in range(nob)],
                     aggregate_sig=[rand_u64(rng) for _ in range(nsig)]))
+    for extra in (0, 13, 14, 22):  # 13 elements of 55 bytes: records of 753, 768, 769 and 777 bytes
+        atts.append(pb.AttestationRecord(slot=1, shard_id=1, justified_slot=1, justified_block_hash=b"",
+                                         shard_block_hash=rand_bytes(rng, extra, extra + 1), attester_bitfield=b"x",
+                                         oblique_parent_hashes=[rand_bytes(rng, 55, 56) for _ in range(13)],
+                                         aggregate_sig=[7]))
     rng.shuffle(atts)
     raw, offs = wire.attestations_device(wire.attestation_columns(atts), len(atts), field_num)
     tag = varint((field_num << 3) | 2) if field_num else b""
