@@ -3,7 +3,7 @@
 # build/ab/libprysm_hip_old.so for a same-box A/B.
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R; O=gpurun_out/${1:-watt}; mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_wire_att_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest.txt 2>&1 || { echo PYTEST_FAIL; tail -40 $O/pytest.txt; exit 12; }
+timeout -k 10 300 python -u -m pytest tests/test_wire_att_gpu.py tests/test_hash_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest.txt 2>&1 || { echo PYTEST_FAIL; tail -40 $O/pytest.txt; exit 12; }
 tail -2 $O/pytest.txt
 timeout -k 10 200 python -u tools/wire_att_probe.py 50 > $O/probe_new.txt 2>&1 || { echo PROBE_FAIL; tail -20 $O/probe_new.txt; exit 13; }
 cat $O/probe_new.txt

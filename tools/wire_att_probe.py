@@ -45,6 +45,21 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
+    # the CSR hash kernel over the encoded records (the encode + hash leg's second launch)
+    dig = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+
+    def run_hash():
+        _lib.lib.call("pz_dev_blake2b512_batch", out.data_ptr(), offs.data_ptr(), n, dig.data_ptr(), 32, sh)
+
+    for _ in range(20):
+        run_hash()
+    e0.record()
+    for _ in range(reps):
+        run_hash()
+    e1.record()
+    torch.cuda.synchronize()
+    hms = e0.elapsed_time(e1) / reps
+    print("csr hash: %.3f ms  %.2f G records/s" % (hms, n / hms / 1e6), flush=True)
     want = synth.attestation_records_512(n, seed=2).reshape(-1)
     ok = bool(np.array_equal(out[:want.size].cpu().numpy(), want))
     print("wire_att encode: %d records  %.3f ms  %.1f M records/s  parity=%s" % (n, ms, n / ms / 1e3, ok), flush=True)
