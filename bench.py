@@ -155,8 +155,11 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                    "parallelism": "validator-shard x%d + RCCL all-reduce" % world if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
-                     "traffic": pmc_traffic(EPOCH_KERNELS) if (nval, ninst) == (65536, 256) else None,
-                     "traffic_source": PMC_SUMMARY + " (count+mid+reward, 65,536 x 256 workload)",
+                     "traffic": (pmc_traffic(EPOCH_KERNELS) if (nval, ninst) == (65536, 256) else
+                                 pmc_traffic(EPOCH_KERNELS, PMC_SUMMARY_EPOCH_1M) if (nval, ninst) == (1 << 20, 16)
+                                 else None),
+                     "traffic_source": ("%s (count+mid+reward, %d x %d workload)"
+                                        % (PMC_SUMMARY if nval == 65536 else PMC_SUMMARY_EPOCH_1M, nval, ninst)),
                      "kernel": "epoch step (count+winner+compact+reward, device time of the whole step)",
                      "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": local_units * EPOCH_BYTES_PER_VALIDATOR},
@@ -563,14 +566,15 @@ def replay_leg(args, torch, dist, dev, rank, world):
 
 
 PMC_SUMMARY = os.path.join("profiles", "r01", "pmc_summary.json")
+PMC_SUMMARY_EPOCH_1M = os.path.join("profiles", "r01", "pmc_summary_epoch1m.json")
 
 
-def pmc_traffic(kernels):
+def pmc_traffic(kernels, summary=PMC_SUMMARY):
     """HBM bytes per launch of ``kernels`` (summed) from the committed rocprofv3 --pmc summary
     (tools/gpu_pmc.sh + tools/pmc_summary.py: FETCH_SIZE doubled per the gfx950 correction,
     WRITE_SIZE as is).  PMC counters cannot be read inside this process, so the figure comes
     from a separate profiled run of the same workload; None if the summary is absent."""
-    path = os.path.join(ROOT, PMC_SUMMARY)
+    path = os.path.join(ROOT, summary)
     if not os.path.exists(path):
         return None
     with open(path) as f:

@@ -6,4 +6,4 @@ R=$GRAFT_REPO_ROOT
 cd $R
 bash tools/gpu_session.sh $TAG || exit $?
 bash tools/gpu_pmc.sh ${TAG}_pmc || exit $?
-cd $R && python3 tools/pmc_summary.py gpurun_out/${TAG}_pmc > gpurun_out/${TAG}_pmc_summary.json && echo PMC_SUMMARY_OK
+cd $R && python3 tools/pmc_summary.py gpurun_out/${TAG}_pmc > gpurun_out/${TAG}_pmc_summary.json && python3 tools/pmc_summary.py gpurun_out/${TAG}_pmc_epoch1m > gpurun_out/${TAG}_pmc_summary_epoch1m.json && echo PMC_SUMMARY_OK

@@ -15,7 +15,24 @@ from prysm_amd import _lib, casper, synth  # noqa: E402
 from prysm_amd.epoch import DeviceEpoch  # noqa: E402
 
 
+def epoch_1m():
+    """Only the bench's configs[3]-sized epoch on one GPU (1,048,576 validators x 16
+    instances), 3 steps: its own counter passes, since the summary averages per kernel name."""
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream(dev)
+    nval, B = 1 << 20, 16
+    inst = synth.epoch_batch(nval, B, seed=3,
+                             shuffled=casper.shuffle_indices(b"A" + bytes(31), np.arange(nval, dtype=np.uint32)))
+    de = DeviceEpoch(inst, dev)
+    for _ in range(3):
+        de.step(s)
+    torch.cuda.synchronize()
+    print("pmc epoch_1m workload done")
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "epoch_1m":
+        return epoch_1m()
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream(dev)
     sh = ctypes.c_void_p(s.cuda_stream)
