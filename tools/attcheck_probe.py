@@ -1,0 +1,50 @@
+"""Times pz_dev_check_attestations alone on the bench's attcheck workload (4M attestations at
+configs[2]'s committee shape) with HIP events.  PZ_PROBE_LIB selects another build of the
+library for a same-box A/B."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from prysm_amd import _lib  # noqa: E402
+
+if os.environ.get("PZ_PROBE_LIB"):
+    _lib.library_path = os.environ["PZ_PROBE_LIB"]
+import bench  # noqa: E402
+
+
+def main():
+    natt = 1 << 22
+    cols, tab = bench.attcheck_columns(natt, seed=11)
+    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v.view(np.int32) if v.dtype == np.uint32
+                             else v).cuda() for k, v in list(cols.items()) + list(tab.items())}
+    st = torch.empty(natt, dtype=torch.int32, device="cuda")
+    cm = torch.empty(natt, dtype=torch.int32, device="cuda")
+    ps = torch.empty(natt, dtype=torch.int64, device="cuda")
+    b = _lib.AttCheckBatch(natt, t["slot"].data_ptr(), t["justified_slot"].data_ptr(), t["shard_id"].data_ptr(),
+                           t["n_oblique"].data_ptr(), t["bits"].data_ptr(), t["boffs"].data_ptr(),
+                           t["block_slot"].data_ptr(), 0, 0, 128, 256, t["arr_offs"].data_ptr(),
+                           t["arr_shard"].data_ptr(), t["arr_comm"].data_ptr(), t["coffs"].data_ptr(),
+                           st.data_ptr(), cm.data_ptr(), ps.data_ptr())
+    sh = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for _ in range(200):
+        _lib.lib.call("pz_dev_check_attestations", ctypes.byref(b), sh)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 100
+    e0.record()
+    for _ in range(reps):
+        _lib.lib.call("pz_dev_check_attestations", ctypes.byref(b), sh)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    digest = int(st.sum().item()) * 31 + int(cm.sum().item()) * 7 + int(ps.sum().item())
+    print("attcheck: %d attestations  %.4f ms  %.1f G/s  result digest %d" % (natt, ms, natt / ms / 1e6, digest),
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()
