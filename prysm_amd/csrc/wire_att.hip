@@ -353,58 +353,53 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_write_kernel(
   // 1. layout
   const uint32_t sh = (uint32_t)o & 15;
   uint8_t* st = stage[w][ri] + sh;
-  uint32_t pos = 0, seg_dst = 0;
-  if (fast) {
-    uint64_t fixed = 0;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      fixed += h.v[k] ? 1 + vlen(h.v[k]) : 0;
-      fixed += h.bl[k] ? 1 + vlen(h.bl[k]) + h.bl[k] : 0;
+  uint32_t seg_dst = 0;
+  if (fast) {  // row-uniform, so the row's DPP reads below see only active lanes
+    // Lane-parallel: sub-lane k (1-8) owns item k of the record -- fields 1-3 (tag +
+    // varint), the headers and bytes of fields 4-6, the elements of field 7, the header and
+    // values of field 8 -- and sub-lane 0 the frame.  One row scan of the items' spans
+    // places them all.
+    uint64_t val = 0;
+    uint32_t span = 0;
+    if (sl >= 1 && sl <= 3) {
+      val = sl == 1 ? h.v[0] : sl == 2 ? h.v[1] : h.v[2];
+      span = val ? 1 + vlen(val) : 0;
+    } else if (sl >= 4 && sl <= 6) {
+      val = sl == 4 ? h.bl[0] : sl == 5 ? h.bl[1] : h.bl[2];
+      span = val ? 1 + vlen(val) + (uint32_t)val : 0;
+    } else if (sl == 7) {
+      span = obl;
+    } else if (sl == 8) {
+      val = sigb;
+      span = sigb ? 1 + vlen(sigb) + sigb : 0;
     }
-    const uint64_t body = body_size(fixed, obl, sigb);
-    if (a.field) {
-      if (sl == 0) {
-        uint8_t* q = put_varint(st, ((uint64_t)a.field << 3) | 2);
-        put_varint(q, body);
-      }
-      pos += a.tag_len + vlen(body);
+    const uint32_t inc = rscan32(span);
+    const uint32_t body = bc32<8>(inc);
+    const uint32_t frame = a.field ? a.tag_len + vlen(body) : 0;
+    const uint32_t pos = frame + inc - span;
+    if (sl == 0 && a.field) {
+      uint8_t* q = put_varint(st, ((uint64_t)a.field << 3) | 2);
+      put_varint(q, body);
     }
-    for (int k = 0; k < 3; ++k)
-      if (h.v[k]) {
-        if (sl == 0) {
-          st[pos] = (uint8_t)((k + 1) << 3);
-          put_varint(st + pos + 1, h.v[k]);
-        }
-        pos += 1 + vlen(h.v[k]);
-      }
-    for (int k = 0; k < 3; ++k)
-      if (h.bl[k]) {
-        const uint32_t hl = 1 + vlen(h.bl[k]);
-        if (sl == 0) {
-          st[pos] = (uint8_t)(((k + 4) << 3) | 2);
-          put_varint(st + pos + 1, h.bl[k]);
-        }
-        if (sl == k) seg_dst = pos + hl;
-        pos += hl + (uint32_t)h.bl[k];
-      }
+    if (sl >= 1 && sl <= 8 && sl != 7 && val) {
+      st[pos] = (uint8_t)((sl << 3) | (sl >= 4 ? 2 : 0));
+      put_varint(st + pos + 1, val);
+    }
+    // bytes field f's data follows item 4 + f's header: sub-lane f (segment f) learns where
+    const uint32_t fd = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(pos + 1 + vlen(val)), 0x104, 0xf, 0xf, false);
+    if (sl < 3) seg_dst = fd;
     // field 7: sub-lane e writes element e's header; its bytes are segment 3 + e
-    const uint32_t ep = pos + einc - esz;
+    const uint32_t ep = bc32<7>(pos) + einc - esz;
     if ((uint64_t)sl < nob) {
       st[ep] = (7 << 3) | 2;
       put_varint(st + ep + 1, el);
     }
     const uint32_t ed = shr3(ep + 1 + vlen(el));
     if (sl >= 3 && (uint64_t)(sl - 3) < nob) seg_dst = ed;
-    pos += obl;
-    // field 8: the header by sub-lane 0, one varint per sub-lane
-    if (sigb) {
-      const uint32_t hl = 1 + vlen(sigb);
-      if (sl == 0) {
-        st[pos] = (8 << 3) | 2;
-        put_varint(st + pos + 1, sigb);
-      }
-      if ((uint64_t)sl < nsig) put_varint(st + pos + hl + sinc - ssz, sv);
-    }
+    // field 8: one varint per sub-lane after item 8's header.  (A DPP read of a lane that is
+    // inactive returns 0, so every row_newbcast runs outside the per-lane branches.)
+    const uint32_t sp = bc32<8>(pos) + 1 + vlen(sigb);
+    if ((uint64_t)sl < nsig) put_varint(st + sp + sinc - ssz, sv);
   }
   // 2b. realign the segment's words on its first byte and write them into the stage
 #pragma unroll
