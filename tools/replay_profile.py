@@ -9,7 +9,10 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402,F401
 
-from prysm_amd import synth  # noqa: E402
+from prysm_amd import _lib, synth  # noqa: E402
+
+if os.environ.get("PZ_PROBE_LIB"):  # A/B against another build of the library
+    _lib.library_path = os.environ["PZ_PROBE_LIB"]
 from prysm_amd.blockchain import BeaconChain, serialize_blocks  # noqa: E402
 
 
