@@ -164,9 +164,35 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                      "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": local_units * EPOCH_BYTES_PER_VALIDATOR},
     }
+    if world == 1 and baseline:
+        out["single_instance"] = epoch_single_instance(args, torch, dev, nval, shuffled)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and baseline:
         out["cpu_baseline"] = epoch_cpu_baseline(inst)
     return out
+
+
+def epoch_single_instance(args, torch, dev, nval, shuffled):
+    """the latency of ONE epoch instance (B = 1) at configs[2]'s size,
+    launch-bound at this size (2.9 MB of algorithmic traffic); device time by HIP events."""
+    from prysm_amd import synth
+    from prysm_amd.epoch import DeviceEpoch
+
+    de = DeviceEpoch(synth.epoch_batch(nval, 1, seed=3, shuffled=shuffled), dev)
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(args.warmup + 20):
+        de.step(stream)
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        de.step(stream)
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in evs]))
+    return {"validators": nval, "instances_per_step": 1, "device_ms_median": ms,
+            "wall_ms_per_step": wall / args.steps * 1e3, "validator_epochs_per_s": nval / (ms * 1e-3)}
 
 
 def epoch_cpu_baseline(inst):
