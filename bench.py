@@ -611,6 +611,28 @@ def pmc_traffic(kernels, summary=PMC_SUMMARY):
         return None
 
 
+def host_api_rate(records_np, reps=3):
+    """The PCIe-inclusive rate (never `value`): the host-pointer C-ABI a cgo caller would use,
+    pz_blake2b512_batch, over the same records from host memory (H2D of the batch, kernel,
+    D2H of the digests), wall clock, median of `reps` calls."""
+    from prysm_amd import _lib
+
+    n = records_np.shape[0]
+    flat = np.ascontiguousarray(records_np).reshape(-1)
+    offs = np.arange(n + 1, dtype=np.uint64) * records_np.shape[1]
+    out = np.empty(n * 32, dtype=np.uint8)
+    ts = []
+    for _ in range(reps + 1):
+        t0 = time.perf_counter()
+        _lib.lib.call("pz_blake2b512_batch", _lib.ptr(flat), _lib.ptr(offs), n, _lib.ptr(out), 32)
+        ts.append(time.perf_counter() - t0)
+    dt = float(np.median(ts[1:]))
+    return {"value": n / dt, "unit": "hashes/s", "ms_per_call": dt * 1e3,
+            "input_GBps": flat.nbytes / dt / 1e9,
+            "what": "pz_blake2b512_batch (host pointers): H2D of the %d x %d-B batch + kernel + D2H, "
+                    "median of %d calls" % (n, records_np.shape[1], reps)}
+
+
 def cpu_baseline(records_np):
     """Time the oracle's C restatement (oracle/c) over the same records on 1 core."""
     try:
@@ -736,6 +758,8 @@ def main():
                              "peak_GBps": HBM_PEAK / 1e9},
             },
         }
+        if world == 1:
+            line["host_api"] = host_api_rate(recs)
         if world == 1 and not args.no_cpu_baseline:
             cb, digests = cpu_baseline(recs)
             line["cpu_baseline"] = cb
