@@ -89,7 +89,9 @@ static void process_crosslinks(epoch_ctx* e, uint64_t slot) {
       if (check_bit(a->attester_bitfield, a->bitfield_len, (long)i, &e->panicked))
         vote += e->validators[sc->committee[i]]->balance;
     if (e->panicked) return;
-    if (3 * vote >= 2 * total && e->dynasty > e->records[a->shard_id].dynasty) {
+    if (3 * vote < 2 * total) continue;  /* Go's && short-circuits before the record index */
+    if (a->shard_id >= e->nrec) { e->panicked = 1; return; }
+    if (e->dynasty > e->records[a->shard_id].dynasty) {
       e->records[a->shard_id].dynasty = e->dynasty;
       e->records[a->shard_id].slot = slot;
       e->records[a->shard_id].blockhash_from = (int64_t)k;

@@ -374,9 +374,13 @@ def process_crosslinks(cstate, records, validators, pending, dynasty, slot):
         for i, a in enumerate(indices):
             if check_bit(att.attester_bitfield, i):
                 vote = (vote + validators[a].balance) & M64
+        # Go's && short-circuits: crosslinkRecords[ShardId] is indexed (and panics when out of
+        # range) only once the 2/3 test holds (core.go:549)
+        if (3 * vote) & M64 < (2 * total) & M64:
+            continue
         if att.shard_id >= len(records):
             raise GoPanic("crosslink record index out of range")
-        if (3 * vote) & M64 >= (2 * total) & M64 and dynasty > records[att.shard_id].dynasty:
+        if dynasty > records[att.shard_id].dynasty:
             rec = pb.CrosslinkRecord(dynasty=dynasty, blockhash=bytes(att.shard_block_hash), slot=slot)
             records[att.shard_id].CopyFrom(rec)
     return records

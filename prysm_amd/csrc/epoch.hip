@@ -78,6 +78,8 @@ struct CountGrid {
   int vec;            // 1: validator arrays read 16 B per lane (nval even, 16-B aligned)
   uint64_t xl_j;      // crosslink blocks per instance (4 attestations per block)
   int xl_affine;      // 1: crosslink blocks of instance i land on XCD i % 8 (>= 8 instances)
+  int do_pop;         // 0: the popcount blocks only reset the winners (no bitfield bytes, or
+                      //    a crosslink-only launch)
 };
 
 // Crosslink tally for one attestation, one wave (core.go:533-545).  Members are processed
@@ -245,7 +247,7 @@ pz_epoch_count_kernel(EpochArgs a, CountGrid g) {
     const uint64_t inst = (uint32_t)pb / (uint32_t)g.pbpi, chunk = (uint32_t)pb - (uint32_t)inst * (uint32_t)g.pbpi;
     if (chunk == 0 && a.winner)  // winners are reset here; the winner pass runs after this launch
       for (uint32_t s = tid; s < a.nrec; s += kThreads) a.winner[inst * a.nrec + s] = 0xffffffffu;
-    if (chunk % a.pop_world != a.pop_rank) return;
+    if (!g.do_pop || chunk % a.pop_world != a.pop_rank) return;
     const uint64_t beg = a.boffs[inst * a.natt], end = a.boffs[inst * a.natt + a.natt];
     const uint64_t cb = beg + chunk * kPopBytesPerBlock;
     if (cb >= end) return;
@@ -613,7 +615,14 @@ hipError_t launch_epoch_count(const EpochArgs& a, bool do_val, bool do_pop, bool
   g.vbpi = vblocks_per_inst(a.nval);
   g.nvb = do_val ? (uint64_t)a.ninst * g.vbpi : 0;
   g.pbpi = (a.max_inst_bytes + kPopBytesPerBlock - 1) / kPopBytesPerBlock;
-  g.npb = (do_pop && a.natt) ? (uint64_t)a.ninst * g.pbpi : 0;
+  // The popcount range also resets the crosslink winners (chunk 0 of each instance), so it
+  // keeps one block per instance whenever winners will be computed -- even when no bitfield
+  // has a byte (every pending attestation names an empty committee, nval < 64) or when this
+  // launch counts nothing but crosslinks.
+  const bool reset = do_xl && a.winner && a.natt;
+  if (reset && g.pbpi == 0) g.pbpi = 1;
+  g.do_pop = do_pop ? 1 : 0;
+  g.npb = ((do_pop || reset) && a.natt) ? (uint64_t)a.ninst * g.pbpi : 0;
   g.vec = vec_ok(a) ? 1 : 0;
   g.xl_j = ((uint64_t)a.natt + 3) / 4;
   g.xl_affine = a.ninst >= 8 ? 1 : 0;

@@ -76,6 +76,28 @@ def test_process_crosslinks_kat_gpu():
     assert win[0] == 0  # record 0 -> {Dynasty 5, Blockhash 'a', Slot 50}
 
 
+@pytest.mark.parametrize("bitfield,panics", [(b"\x00\x00", False), (b"zz", True)])
+def test_process_crosslinks_shard_out_of_range_gpu(bitfield, panics):
+    # blockchain/core.go:549: crosslinkRecords[ShardId] is indexed only when the 2/3 test holds,
+    # so a shard beyond the records panics (PZ_EINDEX) only for a qualifying attestation
+    _, cs = ref.new_genesis_states()
+    comm = list(cs.shard_and_committees_for_slots[0].array_shard_and_committee[0].committee)
+    committee = np.array(comm, dtype=np.uint32)
+    coffs = np.array([0, len(comm)], dtype=U64)
+    bits = np.frombuffer(bitfield, dtype=np.uint8).copy()
+    boffs = np.array([0, len(bitfield)], dtype=U64)
+    bal = np.full(1000, 10000, dtype=U64)
+    args = (committee, coffs, np.zeros(1, np.uint32), np.full(1, 1024, np.uint32), bits, boffs, bal,
+            np.ones(1024, dtype=U64), 5)
+    if panics:
+        with pytest.raises(_lib.PzError) as ei:
+            _lib_process_crosslinks(*args)
+        assert ei.value.code == _lib.PZ_EINDEX
+    else:
+        win, vote, total = _lib_process_crosslinks(*args)
+        assert (win == 0xFFFFFFFF).all() and vote[0] == 0 and total[0] == 10000 * len(comm)
+
+
 def _lib_process_crosslinks(committee, coffs, att_comm, att_shard, bits, boffs, bal, rec_dyn, dynasty):
     import ctypes
     natt = len(att_comm)
@@ -250,6 +272,39 @@ def test_device_epoch_vs_oracle(n, B, inactive):
         np.testing.assert_array_equal(vote[b], v)
         np.testing.assert_array_equal(total[b], t)
         np.testing.assert_array_equal(win[b], w)
+
+
+def test_device_epoch_configs3_size_vs_oracle():
+    """BASELINE configs[3]'s instance size on one GPU: 1,048,576 validators, the real 1M shuffle
+    (Hash{'A'}), 65 committees per slot (4,160 of 252-253 members) + the final N-bit
+    attestation.  Instance 0 is all active (rank == index, the bench's fast path); instance 1
+    has queued and exited validators (rank != index: the compaction path).  Bit-exact against
+    the numpy oracle on every balance, tally, winner and the next-cycle total."""
+    import torch
+
+    from prysm_amd.epoch import DeviceEpoch
+    n, B = 1 << 20, 2
+    shuffled = casper.shuffle_indices(ref.bytes_to_hash(b"A"), np.arange(n, dtype=np.uint32))
+    inst = synth.epoch_batch(n, B, seed=5, shuffled=shuffled)
+    sizes = np.diff(inst["coffs"]).astype(np.int64)
+    assert inst["natt"] == 4161 and sizes.size == 64 * 65 and set(sizes.tolist()) == {252, 253}
+    rng = np.random.default_rng(2)
+    inst["start"][1, rng.random(n) < 0.1] = 7   # queued at dynasty 1
+    inst["end"][1, rng.random(n) < 0.05] = 1    # exited at dynasty 1
+    de = DeviceEpoch(inst, torch.device("cuda", 0))
+    de.step()
+    torch.cuda.synchronize()
+    bal, scal, vote, total, win = de.results()
+    for b in range(B):
+        nb, applied, nxt, v, t, w = _oracle_epoch(inst, b)
+        assert applied and bool(scal[b, _lib.SCAL_APPLIED])
+        assert int(scal[b, _lib.SCAL_NACT]) == int(onp.indices(inst["start"][b], inst["end"][b], 1, 0).size)
+        np.testing.assert_array_equal(bal[b], nb)
+        assert int(scal[b, _lib.SCAL_NEXT_BAL]) == nxt
+        np.testing.assert_array_equal(vote[b], v)
+        np.testing.assert_array_equal(total[b], t)
+        np.testing.assert_array_equal(win[b], w)
+    assert int(scal[1, _lib.SCAL_NACT]) < n
 
 
 def test_device_epoch_repeated_steps_ping_pong():

@@ -79,7 +79,8 @@ def _spawn(world, n, B, inactive, use_gpu, steps=2):
     mp.spawn(_worker, args=(world, _free_port(), n, B, inactive, use_gpu, steps), nprocs=world, join=True)
 
 
-@pytest.mark.parametrize("world,n,B,inactive", [(2, 4096, 2, False), (2, 4096, 2, True), (3, 5000, 2, True)])
+@pytest.mark.parametrize("world,n,B,inactive", [(2, 4096, 2, False), (2, 4096, 2, True), (3, 5000, 2, True),
+                                                (8, 20000, 1, True)])
 def test_multirank_epoch_cpu_gloo(world, n, B, inactive):
     _spawn(world, n, B, inactive, use_gpu=False)
 
@@ -88,3 +89,12 @@ def test_multirank_epoch_cpu_gloo(world, n, B, inactive):
 @pytest.mark.parametrize("n,B,inactive", [(65536, 3, False), (20000, 2, True)])
 def test_multirank_epoch_gpu_gloo(n, B, inactive):
     _spawn(2, n, B, inactive, use_gpu=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inactive", [False, True])
+def test_multirank_epoch_gpu_gloo_configs3(inactive):
+    """BASELINE configs[3] exactly: 1,048,576 validators sharded over 8 ranks (131,072 each),
+    the real 1M shuffle (65 committees per slot), every rank's HIP kernels on cuda:0 and the
+    sums combined over gloo; bit-exact against the oracle on every rank's balance slice."""
+    _spawn(8, 1 << 20, 1, inactive, use_gpu=True, steps=1)

@@ -2,6 +2,8 @@
 hot path.  CPU only."""
 import hashlib
 
+import numpy as np
+
 import pytest
 
 from oracle import ref
@@ -220,3 +222,26 @@ def test_genesis_encodings():
     assert ref.marshal(v) == bytes.fromhex("282038ffff9fcfc8e0c8e38a01")
     active, _ = ref.new_genesis_states()
     assert ref.marshal(active) == bytes([0x12, 0x00]) * 128
+
+
+@pytest.mark.parametrize("bitfield,panics", [(b"\x00\x00", False), (b"zz", True)])
+def test_process_crosslinks_shard_index_short_circuit(bitfield, panics):
+    # blockchain/core.go:549: `3*vote >= 2*total && dynasty > crosslinkRecords[ShardId].Dynasty`
+    # indexes the records only when the 2/3 test holds, so an out-of-range shard panics only then
+    _, cs = ref.new_genesis_states()
+    vals = _validators([dict(balance=10000, start_dynasty=0, end_dynasty=ref.DEFAULT_END_DYNASTY)] * 1000)
+    att = pb.AttestationRecord(slot=0, shard_id=0, shard_block_hash=b"a", attester_bitfield=bitfield)
+    if panics:
+        with pytest.raises(ref.GoPanic):
+            ref.process_crosslinks(cs, [], vals, [att], 5, 50)
+    else:
+        assert ref.process_crosslinks(cs, [], vals, [att], 5, 50) == []
+    # the numpy twin agrees
+    from oracle import epoch_np as onp
+    vote = np.array([0 if not panics else 1], dtype=np.uint64)
+    total = np.array([1], dtype=np.uint64)
+    if panics:
+        with pytest.raises(ref.GoPanic):
+            onp.crosslink_winners(vote, total, np.array([0], np.uint32), np.zeros(0, np.uint64), 5)
+    else:
+        assert onp.crosslink_winners(vote, total, np.array([0], np.uint32), np.zeros(0, np.uint64), 5).size == 0

@@ -234,3 +234,22 @@ def test_gpu_state_bytes_match_oracle_encoding():
         b = ch.state_bytes(k)
         assert b == ob[k], k
         assert ref.hash32(b) == roots[k] == oroots[k], k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nval", [32, 40])
+def test_gpu_replay_empty_committees_vs_oracle(nval):
+    """Fewer than 64 validators: splitBySlotShard leaves the slot-0 committee empty, so every
+    pending attestation carries a zero-length bitfield (BitLength(0), core.go:377-394) and
+    names an empty committee, whose 3*0 >= 2*0 qualifies it for the crosslink (core.go:549).
+    No bitfield has a byte at the transitions, so the winner reset must not depend on the
+    popcount pass finding any."""
+    from oracle import replay
+    blocks = synth.chain_blocks(nval, 130, seed=5)
+    assert all(len(a.attester_bitfield) == 0 for b in blocks for a in b.attestations)
+    o_recs, o_roots = replay.replay(blocks, nval)
+    recs, roots = _product(nval, blocks)
+    assert _hexrecs(recs) == _hexrecs(o_recs)
+    assert sum(r["transition"] for r in recs) == 2
+    for k in ("chain_active", "chain_crystallized", "cand_active", "cand_crystallized"):
+        assert roots[k] == o_roots[k], k
