@@ -164,11 +164,35 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                      "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": local_units * EPOCH_BYTES_PER_VALIDATOR},
     }
+    if rank == 0 and world == 1:
+        out["parity"] = epoch_parity(inst, dev, torch)
     if world == 1 and baseline:
         out["single_instance"] = epoch_single_instance(args, torch, dev, nval, shuffled)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and baseline:
         out["cpu_baseline"] = epoch_cpu_baseline(inst)
     return out
+
+
+def epoch_parity(inst, dev, torch):
+    """The checker for the timed workload: one fresh step of the same B instances (the timed
+    loop has already stepped the balances many times), instance 0 compared bit-exactly with
+    the numpy oracle (oracle/epoch_np.py): balances, tallies, winners, next-cycle total."""
+    from prysm_amd import _lib
+    from prysm_amd.epoch import DeviceEpoch
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from epoch_ref_helpers import oracle_epoch
+
+    de = DeviceEpoch(inst, dev)
+    de.step()
+    torch.cuda.synchronize(dev)
+    bal, scal, vote, total, win = de.results()
+    nb, applied, nxt, v, t, w = oracle_epoch(inst, 0)
+    ok = (np.array_equal(bal[0], nb) and bool(scal[0, _lib.SCAL_APPLIED]) == applied
+          and int(scal[0, _lib.SCAL_NEXT_BAL]) == nxt and np.array_equal(vote[0], v)
+          and np.array_equal(total[0], t) and np.array_equal(win[0], w))
+    del de
+    return "instance 0 of the timed %d x %d workload, one step, bit-exact vs oracle/epoch_np: %s" % (
+        inst["ninst"], inst["nval"], ok)
 
 
 def epoch_single_instance(args, torch, dev, nval, shuffled):

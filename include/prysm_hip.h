@@ -51,6 +51,11 @@ int         pz_init(int device);          /* select/initialise a device for this
 int         pz_device_count(int* count);
 const char* pz_last_error(void);          /* thread-local message for the last failure */
 int         pz_version(void);             /* ABI version: 1 */
+/* Releases every device context the library created (streams, staging buffers).  Call it
+ * last, from one thread, after every pz_chain / pz_epoch_state / pz_comm has been freed;
+ * afterwards any entry point re-initialises lazily.  (The reference has no teardown: the Go
+ * process exits; a long-lived cgo host calls this on node shutdown, node/node.go:124-132.) */
+void        pz_shutdown(void);
 
 /* ---- H: BLAKE2b-512 of serialized messages ------------------------------------------
  * Replaces `h := blake2b.Sum512(data); copy(hash[:], h[:32])` at
@@ -327,6 +332,81 @@ int pz_dev_epoch_finish(const pz_epoch_batch* b, void* stream);
  * [B][ceil(nval_global/2048)] u32.  Instances with every validator active are skipped. */
 int pz_dev_epoch_gather_compact(const pz_epoch_batch* b, const uint64_t* gathered_mask, uint32_t world,
                                 uint64_t shard_words, uint32_t* gblk, void* stream);
+
+/* ---- multi-GPU: communicators (RCCL over xGMI) ------------------------------------------
+ * The reference is one Go process (ChainService.blockProcessing is one goroutine,
+ * blockchain/service.go:229); nothing in it is distributed.  North_star shards the epoch by
+ * validator range over the GPUs of one node and combines the participation and total-balance
+ * sums with RCCL all-reduce.  A pz_comm names the ranks of that partition:
+ *   pz_init_devices       one process drives ndev GPUs (ncclCommInitAll): the Go node's shape;
+ *   pz_comm_init_rank     one process per GPU (ncclCommInitRank), the id from rank 0's
+ *                         pz_comm_unique_id passed to every rank by the launcher;
+ *   pz_comm_init_loopback `world` ranks in this process on ONE device, collectives by device
+ *                         copies and a sum kernel (no RCCL): the sharded code path on a
+ *                         one-GPU machine (tests).
+ * librccl is resolved at run time (the copy already mapped into the process, else /opt/rocm's). */
+#define PZ_COMM_ID_BYTES 128
+typedef struct pz_comm pz_comm;
+int  pz_comm_unique_id(uint8_t id[PZ_COMM_ID_BYTES]);
+int  pz_comm_init_rank(const uint8_t id[PZ_COMM_ID_BYTES], int world, int rank, int device, pz_comm** out);
+int  pz_init_devices(int ndev, const int* devices /* NULL: 0..ndev-1 */, pz_comm** out);
+int  pz_comm_init_loopback(int world, int device, pz_comm** out);
+/* world = ranks in the partition, nlocal = ranks this process drives (global ranks
+ * first_rank .. first_rank+nlocal-1). */
+int  pz_comm_size(const pz_comm* comm, int* world, int* nlocal, int* first_rank);
+int  pz_comm_device(const pz_comm* comm, int local, int* device);
+void pz_comm_free(pz_comm* comm);
+
+/* H over the communicator: message batches shard with no collective.  Local rank i hashes
+ * messages [n*r/world, n*(r+1)/world) of the batch (r = first_rank + i), on its own device,
+ * all local ranks concurrently; out receives those digests (out_bytes each, at the message's
+ * index).  A single-process communicator (pz_init_devices) covers the whole batch, which is
+ * the multi-GPU form of pz_blake2b512_batch. */
+int pz_comm_blake2b512_batch(const pz_comm* comm, const uint8_t* msgs, const uint64_t* offsets, uint64_t n,
+                             uint8_t* out, uint32_t out_bytes);
+
+/* ---- multi-GPU: the device-resident, validator-range-sharded epoch ----------------------
+ * B independent epoch instances (the data-parallel part of stateRecalc, blockchain/core.go:
+ * 433-464), described by host arrays over ALL validators; each local rank of `comm` uploads
+ * its 64-aligned validator range [lo, hi) of every instance into its GPU's HBM (SoA,
+ * instance-major) and the committee members inside it.  comm == NULL: one device, world 1.
+ * A step enqueues (no host sync):
+ *   count -> RCCL all-reduce {scal, vote, total} -> [some validator inactive: all-gather of
+ *   the active masks -> global compaction] -> finish -> all-reduce of the next-cycle totals,
+ * the instances split in two parts so one part's collectives overlap the other's kernels.
+ * Results are those of pz_dev_epoch_count/finish (bit-exact with the reference; panics
+ * reported in scal[PZ_SCAL_ERR_*] with the balances untouched). */
+typedef struct pz_epoch_host {
+  uint32_t ninst;                  /* B */
+  uint64_t nval;                   /* N validators per instance */
+  const uint64_t* balance;         /* [B][N] */
+  const uint64_t* start;           /* [B][N] */
+  const uint64_t* end;             /* [B][N] */
+  const uint64_t* dynasty;         /* [B] */
+  const uint64_t* total_deposit;   /* [B] */
+  uint32_t natt;                   /* pending attestations per instance */
+  const uint8_t* bits;             /* CSR bitfields over B*natt attestations */
+  const uint64_t* boffs;           /* [B*natt + 1], boffs[0] == 0 */
+  const uint32_t* committee;       /* committee members (global validator indices) */
+  const uint64_t* coffs;           /* [ncomm + 1], coffs[0] == 0 */
+  uint64_t ncomm;
+  const uint32_t* att_comm;        /* [B*natt] */
+  const uint32_t* att_shard;       /* [B*natt] */
+  uint32_t nrec;                   /* crosslink records per instance */
+  const uint64_t* rec_dynasty;     /* [B][nrec] */
+} pz_epoch_host;
+typedef struct pz_epoch_state pz_epoch_state;
+int  pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epoch_state** out);
+int  pz_epoch_state_step(pz_epoch_state* st);
+int  pz_epoch_state_sync(pz_epoch_state* st);
+/* Local rank `local`'s validator range, device and compute stream (for event timing). */
+int  pz_epoch_state_shard(const pz_epoch_state* st, int local, uint64_t* lo, uint64_t* hi, int* device,
+                          void** stream);
+/* After a step (synchronises): local rank `local`'s balances [B][hi-lo], and the reduced
+ * scal [B][PZ_SCAL_COUNT], vote / total [B][natt] and winners [B][nrec] (any may be NULL). */
+int  pz_epoch_state_results(pz_epoch_state* st, int local, uint64_t* balance, uint64_t* scal, uint64_t* vote,
+                            uint64_t* total, uint32_t* winner);
+void pz_epoch_state_free(pz_epoch_state* st);
 
 /* ---- block pipeline: sync replay of serialized blocks ---------------------------------
  * A chain object runs blocks through the reference's ChainService.blockProcessing

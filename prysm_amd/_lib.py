@@ -90,6 +90,21 @@ SIGNATURES = {
     "pz_wire_attestations": [vp, u64, u32, vp, u64, vp, c_u64p],
     "pz_dev_wire_attestations": [vp, u64, u32, vp, vp, vp, vp],
     "pz_dev_check_attestations": [vp, vp],
+    "pz_shutdown": [],
+    "pz_comm_unique_id": [vp],
+    "pz_comm_init_rank": [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp],
+    "pz_init_devices": [ctypes.c_int, vp, vp],
+    "pz_comm_init_loopback": [ctypes.c_int, ctypes.c_int, vp],
+    "pz_comm_size": [vp, c_intp, c_intp, c_intp],
+    "pz_comm_device": [vp, ctypes.c_int, c_intp],
+    "pz_comm_free": [vp],
+    "pz_comm_blake2b512_batch": [vp, vp, vp, u64, vp, u32],
+    "pz_epoch_state_new": [vp, ctypes.c_int, vp, vp],
+    "pz_epoch_state_step": [vp],
+    "pz_epoch_state_sync": [vp],
+    "pz_epoch_state_shard": [vp, ctypes.c_int, c_u64p, c_u64p, c_intp, vp],
+    "pz_epoch_state_results": [vp, ctypes.c_int, vp, vp, vp, vp, vp],
+    "pz_epoch_state_free": [vp],
 }
 
 
@@ -104,6 +119,16 @@ class EpochBatch(ctypes.Structure):
         ("nrec", ctypes.c_uint32), ("rec_dynasty", vp), ("winner", vp), ("vote", vp), ("total", vp),
         ("scal", vp), ("act_mask", vp), ("blk_cnt", vp), ("act_list", vp), ("scal_next", vp),
         ("cpos", vp),
+    ]
+
+
+class EpochHost(ctypes.Structure):
+    """Mirror of ``pz_epoch_host`` (include/prysm_hip.h)."""
+    _fields_ = [
+        ("ninst", ctypes.c_uint32), ("nval", u64), ("balance", vp), ("start", vp), ("end", vp),
+        ("dynasty", vp), ("total_deposit", vp), ("natt", ctypes.c_uint32), ("bits", vp), ("boffs", vp),
+        ("committee", vp), ("coffs", vp), ("ncomm", u64), ("att_comm", vp), ("att_shard", vp),
+        ("nrec", ctypes.c_uint32), ("rec_dynasty", vp),
     ]
 
 
@@ -149,6 +174,7 @@ SCAL_POP, SCAL_NACT, SCAL_ERR_XL, SCAL_ERR_RWD, SCAL_APPLIED, SCAL_NEXT_BAL, SCA
 SCAL_COUNT = 8
 KIND_ACTIVE, KIND_EXITED, KIND_QUEUED = 0, 1, 2
 _RESTYPES = {"pz_last_error": ctypes.c_char_p, "pz_chain_free": None, "pz_set_serial_threshold": u64,
+             "pz_shutdown": None, "pz_comm_free": None, "pz_epoch_state_free": None,
              "pz_wire_validators_bound": u64, "pz_wire_scratch_bytes": u64,
              "pz_wire_attestations_bound": u64, "pz_wire_attestations_scratch_bytes": u64}
 SERIAL_DEFAULT = 65536        # the library's default serial threshold (bytes)

@@ -1,0 +1,304 @@
+// pz_comm: RCCL (over xGMI) and loopback communicators, and their C-ABI entry points
+// (include/prysm_hip.h, "multi-GPU").  See comm.h for the design.
+#include "comm.h"
+
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+
+#include "runtime.h"
+
+namespace pz {
+
+namespace {
+
+std::once_flag g_rccl_once;
+RcclApi g_rccl;
+int g_rccl_rc = PZ_OK;
+char g_rccl_err[256] = "";
+
+template <typename F>
+bool bind(void* h, const char* name, F* fn) {
+  *fn = reinterpret_cast<F>(dlsym(h, name));
+  return *fn != nullptr;
+}
+
+void load_rccl() {
+  // The copy already in the process first: under PyTorch-ROCm that is torch's librccl, built
+  // against the same HIP runtime this library binds to (see prysm_amd/_lib.py); otherwise
+  // /opt/rocm's.
+  const char* names[] = {"librccl.so", "librccl.so.1"};
+  void* h = nullptr;
+  for (const char* n : names)
+    if ((h = dlopen(n, RTLD_NOW | RTLD_NOLOAD))) { g_rccl.origin = "already loaded"; break; }
+  if (!h && (h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL))) g_rccl.origin = "librccl.so.1";
+  if (!h && (h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL))) g_rccl.origin = "/opt/rocm/lib/librccl.so.1";
+  if (!h) {
+    snprintf(g_rccl_err, sizeof g_rccl_err, "librccl not found: %s", dlerror());
+    g_rccl_rc = PZ_EDEVICE;
+    return;
+  }
+  bool ok = bind(h, "ncclGetUniqueId", &g_rccl.GetUniqueId) && bind(h, "ncclCommInitRank", &g_rccl.CommInitRank) &&
+            bind(h, "ncclCommInitAll", &g_rccl.CommInitAll) && bind(h, "ncclCommDestroy", &g_rccl.CommDestroy) &&
+            bind(h, "ncclAllReduce", &g_rccl.AllReduce) && bind(h, "ncclAllGather", &g_rccl.AllGather) &&
+            bind(h, "ncclGroupStart", &g_rccl.GroupStart) && bind(h, "ncclGroupEnd", &g_rccl.GroupEnd) &&
+            bind(h, "ncclGetErrorString", &g_rccl.GetErrorString);
+  if (!ok) {
+    snprintf(g_rccl_err, sizeof g_rccl_err, "librccl lacks an entry point: %s", dlerror());
+    g_rccl_rc = PZ_EDEVICE;
+  }
+}
+
+int nccl_fail(const RcclApi* api, ncclResult_t r, const char* what) {
+  return fail(PZ_EDEVICE, "%s: %s", what, api && api->GetErrorString ? api->GetErrorString(r) : "RCCL error");
+}
+
+// Sum of the loopback ranks' buffers, written back to every one of them.
+constexpr int kMaxLoopback = 64;
+struct LoopPtrs {
+  uint64_t* p[kMaxLoopback];
+};
+
+extern "C" __global__ void __launch_bounds__(256)
+pz_loopback_sum_kernel(LoopPtrs ptrs, int world, uint64_t count) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= count) return;
+  uint64_t s = 0;
+  for (int r = 0; r < world; ++r) s += ptrs.p[r][i];
+  for (int r = 0; r < world; ++r) ptrs.p[r][i] = s;
+}
+
+}  // namespace
+
+int rccl_api(const RcclApi** out) {
+  std::call_once(g_rccl_once, load_rccl);
+  if (g_rccl_rc) return fail(g_rccl_rc, "%s", g_rccl_err);
+  *out = &g_rccl;
+  return PZ_OK;
+}
+
+}  // namespace pz
+
+using namespace pz;
+
+// Orders the collective stream of every local rank after its compute stream.
+static int order_after(pz_comm* c, const hipStream_t* compute) {
+  for (int i = 0; i < c->nlocal; ++i) {
+    hipError_t e = hipSetDevice(c->dev[i]);
+    if (e == hipSuccess) e = hipEventRecord(c->ev_in[i], compute[i]);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->cstream[c->kind == pz_comm::LOOPBACK ? 0 : i], c->ev_in[i], 0);
+    if (e != hipSuccess) return hip_fail(e, "collective ordering");
+  }
+  return PZ_OK;
+}
+
+static int mark_done(pz_comm* c, hipEvent_t* done) {
+  for (int i = 0; i < c->nlocal; ++i) {
+    hipError_t e = hipSetDevice(c->dev[i]);
+    if (e == hipSuccess) e = hipEventRecord(done[i], c->cstream[c->kind == pz_comm::LOOPBACK ? 0 : i]);
+    if (e != hipSuccess) return hip_fail(e, "collective completion event");
+  }
+  return PZ_OK;
+}
+
+int pz_comm::allreduce_u64(uint64_t* const* bufs, size_t count, const hipStream_t* compute, hipEvent_t* done) {
+  int rc = order_after(this, compute);
+  if (rc) return rc;
+  if (count && world > 1) {
+    if (kind == LOOPBACK) {
+      LoopPtrs p;
+      for (int r = 0; r < world; ++r) p.p[r] = bufs[r];
+      (void)hipSetDevice(dev[0]);
+      hipLaunchKernelGGL(pz_loopback_sum_kernel, dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, cstream[0], p,
+                         world, (uint64_t)count);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return hip_fail(e, "pz_loopback_sum_kernel");
+    } else {
+      if (nlocal > 1) api->GroupStart();
+      ncclResult_t r = ncclSuccess;
+      for (int i = 0; i < nlocal && r == ncclSuccess; ++i) {
+        (void)hipSetDevice(dev[i]);
+        r = api->AllReduce(bufs[i], bufs[i], count, ncclUint64, ncclSum, nccl[i], cstream[i]);
+      }
+      ncclResult_t g = nlocal > 1 ? api->GroupEnd() : ncclSuccess;
+      if (r != ncclSuccess) return nccl_fail(api, r, "ncclAllReduce");
+      if (g != ncclSuccess) return nccl_fail(api, g, "ncclGroupEnd");
+    }
+  }
+  return mark_done(this, done);
+}
+
+int pz_comm::allgather(const void* const* send, void* const* recv, size_t bytes, const hipStream_t* compute,
+                       hipEvent_t* done) {
+  int rc = order_after(this, compute);
+  if (rc) return rc;
+  if (bytes) {
+    if (kind == LOOPBACK || world == 1) {
+      for (int i = 0; i < nlocal; ++i) {
+        (void)hipSetDevice(dev[i]);
+        for (int r = 0; r < world; ++r) {
+          hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(recv[i]) + (size_t)r * bytes, send[r], bytes,
+                                        hipMemcpyDeviceToDevice, cstream[kind == LOOPBACK ? 0 : i]);
+          if (e != hipSuccess) return hip_fail(e, "loopback all-gather copy");
+        }
+      }
+    } else {
+      if (nlocal > 1) api->GroupStart();
+      ncclResult_t r = ncclSuccess;
+      for (int i = 0; i < nlocal && r == ncclSuccess; ++i) {
+        (void)hipSetDevice(dev[i]);
+        r = api->AllGather(send[i], recv[i], bytes, ncclUint8, nccl[i], cstream[i]);
+      }
+      ncclResult_t g = nlocal > 1 ? api->GroupEnd() : ncclSuccess;
+      if (r != ncclSuccess) return nccl_fail(api, r, "ncclAllGather");
+      if (g != ncclSuccess) return nccl_fail(api, g, "ncclGroupEnd");
+    }
+  }
+  return mark_done(this, done);
+}
+
+pz_comm::~pz_comm() {
+  for (size_t i = 0; i < cstream.size(); ++i) {
+    (void)hipSetDevice(dev[i]);
+    if (cstream[i]) {
+      (void)hipStreamSynchronize(cstream[i]);
+      (void)hipStreamDestroy(cstream[i]);
+    }
+    if (i < ev_in.size() && ev_in[i]) (void)hipEventDestroy(ev_in[i]);
+  }
+  if (api)
+    for (ncclComm_t n : nccl)
+      if (n) api->CommDestroy(n);
+}
+
+// Creates the per-local-rank streams/events after dev[] is set.
+static int comm_setup(pz_comm* c) {
+  c->cstream.assign(c->nlocal, nullptr);
+  c->ev_in.assign(c->nlocal, nullptr);
+  for (int i = 0; i < c->nlocal; ++i) {
+    DeviceCtx* dc;
+    int rc = device_ctx(c->dev[i], &dc);  // gfx950 check + the device's library context
+    if (rc) return rc;
+    hipError_t e = hipSetDevice(c->dev[i]);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cstream[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_in[i], hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(e, "communicator stream/event");
+  }
+  return PZ_OK;
+}
+
+extern "C" {
+
+int pz_comm_unique_id(uint8_t id[PZ_COMM_ID_BYTES]) {
+  if (!id) return fail(PZ_EINVAL, "id is null");
+  const RcclApi* api;
+  int rc = rccl_api(&api);
+  if (rc) return rc;
+  ncclUniqueId u;
+  ncclResult_t r = api->GetUniqueId(&u);
+  if (r != ncclSuccess) return nccl_fail(api, r, "ncclGetUniqueId");
+  static_assert(sizeof(u.internal) == PZ_COMM_ID_BYTES, "unique id size");
+  std::memcpy(id, u.internal, PZ_COMM_ID_BYTES);
+  return PZ_OK;
+}
+
+int pz_comm_init_rank(const uint8_t id[PZ_COMM_ID_BYTES], int world, int rank, int device, pz_comm** out) {
+  if (!id || !out) return fail(PZ_EINVAL, "null pointer");
+  *out = nullptr;
+  if (world < 1 || rank < 0 || rank >= world) return fail(PZ_EINVAL, "rank %d of world %d", rank, world);
+  const RcclApi* api;
+  int rc = rccl_api(&api);
+  if (rc) return rc;
+  pz_comm* c = new pz_comm();
+  c->kind = pz_comm::RCCL;
+  c->api = api;
+  c->world = world;
+  c->nlocal = 1;
+  c->rank0 = rank;
+  c->dev = {device};
+  if ((rc = comm_setup(c))) {
+    delete c;
+    return rc;
+  }
+  ncclUniqueId u;
+  std::memcpy(u.internal, id, PZ_COMM_ID_BYTES);
+  c->nccl.assign(1, nullptr);
+  (void)hipSetDevice(device);
+  ncclResult_t r = api->CommInitRank(&c->nccl[0], world, u, rank);
+  if (r != ncclSuccess) {
+    c->nccl.clear();
+    delete c;
+    return nccl_fail(api, r, "ncclCommInitRank");
+  }
+  *out = c;
+  return PZ_OK;
+}
+
+int pz_init_devices(int ndev, const int* devices, pz_comm** out) {
+  if (!out) return fail(PZ_EINVAL, "out is null");
+  *out = nullptr;
+  int n = 0;
+  if (pz_device_count(&n)) return PZ_EDEVICE;
+  if (ndev < 1 || ndev > n) return fail(PZ_EINVAL, "ndev %d of %d devices", ndev, n);
+  const RcclApi* api;
+  int rc = rccl_api(&api);
+  if (rc) return rc;
+  pz_comm* c = new pz_comm();
+  c->kind = pz_comm::RCCL;
+  c->api = api;
+  c->world = c->nlocal = ndev;
+  c->rank0 = 0;
+  for (int i = 0; i < ndev; ++i) c->dev.push_back(devices ? devices[i] : i);
+  if ((rc = comm_setup(c))) {
+    delete c;
+    return rc;
+  }
+  c->nccl.assign(ndev, nullptr);
+  ncclResult_t r = api->CommInitAll(c->nccl.data(), ndev, c->dev.data());
+  if (r != ncclSuccess) {
+    c->nccl.clear();
+    delete c;
+    return nccl_fail(api, r, "ncclCommInitAll");
+  }
+  *out = c;
+  return PZ_OK;
+}
+
+int pz_comm_init_loopback(int world, int device, pz_comm** out) {
+  if (!out) return fail(PZ_EINVAL, "out is null");
+  *out = nullptr;
+  if (world < 1 || world > kMaxLoopback) return fail(PZ_EINVAL, "loopback world %d not in [1, %d]", world, kMaxLoopback);
+  pz_comm* c = new pz_comm();
+  c->kind = pz_comm::LOOPBACK;
+  c->world = c->nlocal = world;
+  c->rank0 = 0;
+  c->dev.assign(world, device);
+  int rc = comm_setup(c);
+  if (rc) {
+    delete c;
+    return rc;
+  }
+  *out = c;
+  return PZ_OK;
+}
+
+int pz_comm_size(const pz_comm* c, int* world, int* nlocal, int* first_rank) {
+  if (!c) return fail(PZ_EINVAL, "comm is null");
+  if (world) *world = c->world;
+  if (nlocal) *nlocal = c->nlocal;
+  if (first_rank) *first_rank = c->rank0;
+  return PZ_OK;
+}
+
+int pz_comm_device(const pz_comm* c, int local, int* device) {
+  if (!c || !device) return fail(PZ_EINVAL, "null pointer");
+  if (local < 0 || local >= c->nlocal) return fail(PZ_EINVAL, "local rank %d of %d", local, c->nlocal);
+  *device = c->dev[local];
+  return PZ_OK;
+}
+
+void pz_comm_free(pz_comm* c) { delete c; }
+
+}  // extern "C"

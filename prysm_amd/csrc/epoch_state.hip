@@ -1,0 +1,483 @@
+// pz_epoch_state: the device-resident, validator-range-sharded epoch transition behind the
+// C ABI (include/prysm_hip.h, "multi-GPU").  B independent instances of the data-parallel
+// part of stateRecalc (blockchain/core.go:433-464): processCrosslinks tallies + winners
+// (:502-558), GetAttestersTotalDeposit (casper/validator.go:93-102), CalculateRewards
+// (casper/incentives.go:14-32) and the next-cycle total (core.go:459-464).
+//
+// Each rank of the communicator owns the 64-aligned validator range [lo, hi) of every
+// instance (SoA, instance-major, in its GPU's HBM) and the committee members that fall in it,
+// each with its position in the full committee (its bitfield bit).  A step is
+//
+//   count (local partial sums)  -> all-reduce {scal, vote, total}            (RCCL, u64 sum)
+//   [some validator inactive: all-gather the active masks -> global compacted list]
+//   finish (winners, rewards on the local range, partial next-cycle total)
+//                               -> all-reduce of the next-cycle totals
+//
+// and the B instances are split in two parts so that one part's collectives run on the
+// collective stream while the other part's kernels run on the compute stream.  Integer sums
+// mod 2^64 commute, so every result is bit-exact for any reduction order.  The same code runs
+// every world size; at world 1 the collectives are skipped.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "comm.h"
+#include "epoch.h"
+#include "runtime.h"
+
+using namespace pz;
+
+namespace {
+
+struct Part {
+  uint32_t i0 = 0, B = 0;
+  uint64_t* red[2] = {nullptr, nullptr};  // ping-pong {scal[B][8], vote[B*natt], total[B*natt]}
+  int cur = 0;
+  uint64_t* results = nullptr;            // the red buffer of the last completed step
+  uint64_t* mask_send = nullptr;          // [B][sw]
+  uint64_t* gmask = nullptr;              // [world][B][sw]
+  uint32_t* gblk = nullptr;               // [B][vblocks(N)]
+  uint64_t* nb = nullptr;                 // [B] next-cycle totals, contiguous for the all-reduce
+  hipEvent_t ev_red = nullptr, ev_gather = nullptr, ev_nb = nullptr;
+  EpochArgs a;
+};
+
+struct Shard {
+  int dev = 0, grank = 0;
+  hipStream_t s = nullptr;
+  uint64_t lo = 0, hi = 0, n = 0, wl = 0;
+  std::vector<void*> allocs;
+  Part part[2];
+};
+
+}  // namespace
+
+struct pz_epoch_state {
+  pz_comm* comm = nullptr;  // null: one device, world 1
+  int world = 1;
+  uint32_t B = 0, natt = 0, nrec = 0, nparts = 1;
+  uint64_t N = 0, sw = 0, ncomm = 0;
+  bool general = false, all_active = true;
+  uint64_t steps = 0;
+  std::vector<Shard> sh;
+  ~pz_epoch_state();
+};
+
+namespace {
+
+template <typename T>
+int dalloc(Shard& s, T** p, size_t count, bool zero = true) {
+  const size_t bytes = (count ? count : 1) * sizeof(T) + 16;
+  hipError_t e = hipMalloc((void**)p, bytes);
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc (epoch state)");
+  s.allocs.push_back(*p);
+  if (zero && (e = hipMemset(*p, 0, bytes)) != hipSuccess) return hip_fail(e, "hipMemset (epoch state)");
+  return PZ_OK;
+}
+
+template <typename T>
+int upload(Shard& s, T** p, const T* host, size_t count) {
+  int rc = dalloc(s, p, count, false);
+  if (rc || !count) return rc;
+  hipError_t e = hipMemcpy(*p, host, count * sizeof(T), hipMemcpyHostToDevice);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "hipMemcpy H2D (epoch state)");
+}
+
+int upload_into(uint8_t* d, const uint8_t* host, size_t bytes) {
+  if (!bytes) return PZ_OK;
+  hipError_t e = hipMemcpy(d, host, bytes, hipMemcpyHostToDevice);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "hipMemcpy H2D (epoch state)");
+}
+
+// Rows [0, B) x columns [lo, hi) of a host [B][N] u64 array -> device [B][hi-lo].
+int upload_range(Shard& s, uint64_t** p, const uint64_t* host, uint32_t B, uint64_t N) {
+  int rc = dalloc(s, p, (size_t)B * s.n, false);
+  if (rc || !s.n) return rc;
+  hipError_t e = hipMemcpy2D(*p, s.n * 8, host + s.lo, N * 8, s.n * 8, B, hipMemcpyHostToDevice);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "hipMemcpy2D H2D (epoch state)");
+}
+
+uint64_t shard_words(uint64_t N, int world) { return std::max<uint64_t>(1, (N + 64ull * world - 1) / (64ull * world)); }
+
+int step_world1(pz_epoch_state* st) {
+  for (Shard& s : st->sh) {
+    (void)hipSetDevice(s.dev);
+    for (uint32_t p = 0; p < st->nparts; ++p) {
+      EpochArgs& a = s.part[p].a;
+      hipError_t e = launch_epoch_count(a, true, true, a.natt != 0, s.s);
+      if (e == hipSuccess) e = launch_epoch_mid(a, a.natt && st->nrec, true, s.s);
+      if (e == hipSuccess) e = launch_epoch_reward(a, s.s);
+      if (e != hipSuccess) return hip_fail(e, "epoch step");
+    }
+  }
+  return PZ_OK;
+}
+
+void flip(pz_epoch_state* st) {
+  for (Shard& s : st->sh)
+    for (uint32_t p = 0; p < st->nparts; ++p) {
+      Part& q = s.part[p];
+      q.results = q.red[q.cur];
+      q.cur ^= 1;
+      const uint64_t Bp = q.B, natt = st->natt;
+      q.a.scal = q.red[q.cur];
+      q.a.vote = q.red[q.cur] + Bp * kScal;
+      q.a.total = q.red[q.cur] + Bp * kScal + Bp * natt;
+      q.a.scal_next = q.red[q.cur ^ 1];
+    }
+}
+
+int wait(Shard& s, hipEvent_t ev) {
+  (void)hipSetDevice(s.dev);
+  hipError_t e = hipStreamWaitEvent(s.s, ev, 0);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "hipStreamWaitEvent");
+}
+
+int step_sharded(pz_epoch_state* st) {
+  pz_comm* c = st->comm;
+  const int L = (int)st->sh.size();
+  std::vector<hipStream_t> streams(L);
+  std::vector<uint64_t*> bufs(L);
+  std::vector<const void*> sends(L);
+  std::vector<void*> recvs(L);
+  std::vector<hipEvent_t> evs(L);
+  for (int i = 0; i < L; ++i) streams[i] = st->sh[i].s;
+  int rc;
+  // pass 1 of every part, each followed by the all-reduce of its partial sums
+  for (uint32_t p = 0; p < st->nparts; ++p) {
+    for (int i = 0; i < L; ++i) {
+      Shard& s = st->sh[i];
+      (void)hipSetDevice(s.dev);
+      hipError_t e = launch_epoch_count(s.part[p].a, true, true, s.part[p].a.natt != 0, s.s);
+      if (e != hipSuccess) return hip_fail(e, "pz_epoch_count_kernel");
+      bufs[i] = s.part[p].red[s.part[p].cur];
+      evs[i] = s.part[p].ev_red;
+    }
+    const uint64_t Bp = st->sh[0].part[p].B;
+    if ((rc = c->allreduce_u64(bufs.data(), Bp * kScal + 2 * Bp * st->natt, streams.data(), evs.data()))) return rc;
+  }
+  // pass 2 of every part (part 0's finish overlaps part 1's all-reduce)
+  for (uint32_t p = 0; p < st->nparts; ++p) {
+    for (int i = 0; i < L; ++i)
+      if ((rc = wait(st->sh[i], st->sh[i].part[p].ev_red))) return rc;
+    if (st->general) {  // rank != index: every rank rebuilds the global compacted active list
+      for (int i = 0; i < L; ++i) {
+        Shard& s = st->sh[i];
+        Part& q = s.part[p];
+        (void)hipSetDevice(s.dev);
+        if (s.wl) {
+          hipError_t e = hipMemcpy2DAsync(q.mask_send, st->sw * 8, q.a.act_mask, s.wl * 8, s.wl * 8, q.B,
+                                          hipMemcpyDeviceToDevice, s.s);
+          if (e != hipSuccess) return hip_fail(e, "active-mask pack");
+        }
+        sends[i] = q.mask_send;
+        recvs[i] = q.gmask;
+        evs[i] = q.ev_gather;
+      }
+      if ((rc = c->allgather(sends.data(), recvs.data(), (size_t)st->sh[0].part[p].B * st->sw * 8, streams.data(),
+                             evs.data())))
+        return rc;
+      for (int i = 0; i < L; ++i) {
+        Shard& s = st->sh[i];
+        Part& q = s.part[p];
+        if ((rc = wait(s, q.ev_gather))) return rc;
+        hipError_t e = launch_epoch_gather_compact(q.a, q.gmask, st->sw, q.gblk, s.s);
+        if (e != hipSuccess) return hip_fail(e, "pz_epoch_gcompact_kernel");
+      }
+    }
+    for (int i = 0; i < L; ++i) {
+      Shard& s = st->sh[i];
+      Part& q = s.part[p];
+      (void)hipSetDevice(s.dev);
+      hipError_t e = launch_epoch_mid(q.a, q.a.natt && st->nrec, false, s.s);
+      if (e == hipSuccess) e = launch_epoch_reward(q.a, s.s);
+      // the next-cycle totals (column kNextBal of scal) made contiguous for the all-reduce
+      if (e == hipSuccess)
+        e = hipMemcpy2DAsync(q.nb, 8, q.a.scal + kNextBal, kScal * 8, 8, q.B, hipMemcpyDeviceToDevice, s.s);
+      if (e != hipSuccess) return hip_fail(e, "epoch finish");
+      bufs[i] = q.nb;
+      evs[i] = q.ev_nb;
+    }
+    if ((rc = c->allreduce_u64(bufs.data(), st->sh[0].part[p].B, streams.data(), evs.data()))) return rc;
+  }
+  for (uint32_t p = 0; p < st->nparts; ++p)
+    for (int i = 0; i < L; ++i) {
+      Shard& s = st->sh[i];
+      Part& q = s.part[p];
+      if ((rc = wait(s, q.ev_nb))) return rc;
+      hipError_t e = hipMemcpy2DAsync(q.a.scal + kNextBal, kScal * 8, q.nb, 8, 8, q.B, hipMemcpyDeviceToDevice, s.s);
+      if (e != hipSuccess) return hip_fail(e, "next-cycle total unpack");
+    }
+  return PZ_OK;
+}
+
+int check_host(const pz_epoch_host* h) {
+  if (!h) return fail(PZ_EINVAL, "host description is null");
+  if (!h->ninst || !h->nval) return fail(PZ_EINVAL, "empty epoch (ninst %u, nval %llu)", h->ninst,
+                                          (unsigned long long)h->nval);
+  if (!h->balance || !h->start || !h->end || !h->dynasty || !h->total_deposit)
+    return fail(PZ_EINVAL, "missing validator arrays");
+  if (h->ninst > 65535 || (uint64_t)h->ninst * h->natt >= (1ull << 32) || h->nval >= (1ull << 32))
+    return fail(PZ_EINVAL, "more than 65535 instances, 2^32 attestations or 2^32 validators");
+  if (h->natt) {
+    if (!h->bits || !h->boffs || !h->att_comm || !h->att_shard || !h->committee || !h->coffs)
+      return fail(PZ_EINVAL, "missing attestation / committee arrays");
+    if (h->boffs[0] != 0) return fail(PZ_EINVAL, "boffs[0] must be 0");
+    int rc = check_csr(h->boffs, (uint64_t)h->ninst * h->natt, "bitfield");
+    if (rc || (rc = check_csr(h->coffs, h->ncomm, "committee"))) return rc;
+    if (h->coffs[0] != 0) return fail(PZ_EINVAL, "coffs[0] must be 0");
+    for (uint64_t i = 0; i < (uint64_t)h->ninst * h->natt; ++i)
+      if (h->att_comm[i] >= h->ncomm) return fail(PZ_EINVAL, "attestation %llu names committee %u of %llu",
+                                                  (unsigned long long)i, h->att_comm[i], (unsigned long long)h->ncomm);
+  }
+  if (h->nrec && !h->rec_dynasty) return fail(PZ_EINVAL, "missing crosslink record dynasties");
+  return PZ_OK;
+}
+
+// The committee CSR restricted to members in [lo, hi) (plus, on global rank 0, members >=
+// N, whose processCrosslinks panic that rank raises), each with its position in its full
+// committee.
+void local_committees(const pz_epoch_host* h, uint64_t lo, uint64_t hi, bool keep_oob, std::vector<uint32_t>& mem,
+                      std::vector<uint64_t>& offs, std::vector<uint32_t>& pos) {
+  offs.assign(h->ncomm + 1, 0);
+  for (uint64_t c = 0; c < h->ncomm; ++c) {
+    for (uint64_t k = h->coffs[c]; k < h->coffs[c + 1]; ++k) {
+      const uint32_t v = h->committee[k];
+      if ((v >= lo && v < hi) || (keep_oob && v >= h->nval)) {
+        mem.push_back(v);
+        pos.push_back((uint32_t)(k - h->coffs[c]));
+      }
+    }
+    offs[c + 1] = mem.size();
+  }
+}
+
+}  // namespace
+
+pz_epoch_state::~pz_epoch_state() {
+  for (Shard& s : sh) {
+    (void)hipSetDevice(s.dev);
+    if (s.s) (void)hipStreamSynchronize(s.s);
+    for (void* p : s.allocs) (void)hipFree(p);
+    for (Part& q : s.part) {
+      if (q.ev_red) (void)hipEventDestroy(q.ev_red);
+      if (q.ev_gather) (void)hipEventDestroy(q.ev_gather);
+      if (q.ev_nb) (void)hipEventDestroy(q.ev_nb);
+    }
+    if (s.s) (void)hipStreamDestroy(s.s);
+  }
+}
+
+extern "C" {
+
+int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epoch_state** out) {
+  if (!out) return fail(PZ_EINVAL, "out is null");
+  *out = nullptr;
+  int rc = check_host(h);
+  if (rc) return rc;
+  pz_epoch_state* st = new pz_epoch_state();
+  st->comm = comm;
+  st->world = comm ? comm->world : 1;
+  st->B = h->ninst;
+  st->N = h->nval;
+  st->natt = h->natt;
+  st->nrec = h->nrec;
+  st->ncomm = h->ncomm;
+  st->sw = shard_words(st->N, st->world);
+  for (uint64_t b = 0; b < st->B && st->all_active; ++b) {
+    const uint64_t d = h->dynasty[b];
+    for (uint64_t v = 0; v < st->N; ++v) {
+      const uint64_t k = b * st->N + v;
+      if (!(h->start[k] <= d && d < h->end[k])) {
+        st->all_active = false;
+        break;
+      }
+    }
+  }
+  st->general = !st->all_active && st->world > 1;
+  st->nparts = (st->world > 1 && st->B >= 2) ? 2 : 1;
+  const int nlocal = comm ? comm->nlocal : 1;
+  st->sh.resize(nlocal);
+  const uint64_t nb_total = h->natt ? h->boffs[(uint64_t)st->B * st->natt] : 0;
+  uint64_t max_inst_bytes = 0;
+  for (uint64_t b = 0; b < st->B && h->natt; ++b)
+    max_inst_bytes = std::max(max_inst_bytes, h->boffs[(b + 1) * st->natt] - h->boffs[b * st->natt]);
+  for (int i = 0; i < nlocal && !rc; ++i) {
+    Shard& s = st->sh[i];
+    s.dev = comm ? comm->dev[i] : device;
+    s.grank = comm ? comm->rank0 + i : 0;
+    const uint64_t span = 64 * st->sw;
+    s.lo = std::min<uint64_t>(st->N, (uint64_t)s.grank * span);
+    s.hi = std::min<uint64_t>(st->N, (uint64_t)(s.grank + 1) * span);
+    s.n = s.hi - s.lo;
+    s.wl = (s.n + 63) / 64;
+    DeviceCtx* dc;
+    if ((rc = device_ctx(s.dev, &dc))) break;
+    (void)hipSetDevice(s.dev);
+    hipError_t e = hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      rc = hip_fail(e, "hipStreamCreate");
+      break;
+    }
+    uint64_t *bal, *start, *end, *dyn, *tdep, *boffs = nullptr, *coffs = nullptr, *recd = nullptr;
+    uint8_t* bits = nullptr;
+    uint32_t *committee = nullptr, *cpos = nullptr, *att_comm = nullptr, *att_shard = nullptr;
+    uint32_t *winner, *blk_cnt, *act_list;
+    uint64_t* act_mask;
+    const uint64_t vbpi = vblocks_per_inst(s.n);
+    if ((rc = upload_range(s, &bal, h->balance, st->B, st->N)) || (rc = upload_range(s, &start, h->start, st->B, st->N)) ||
+        (rc = upload_range(s, &end, h->end, st->B, st->N)) || (rc = upload(s, &dyn, h->dynasty, st->B)) ||
+        (rc = upload(s, &tdep, h->total_deposit, st->B)))
+      break;
+    if (st->natt) {
+      std::vector<uint32_t> mem, pos;
+      std::vector<uint64_t> offs;
+      if (st->world > 1) {
+        local_committees(h, s.lo, s.hi, s.grank == 0, mem, offs, pos);
+      } else {
+        mem.assign(h->committee, h->committee + h->coffs[h->ncomm]);
+        offs.assign(h->coffs, h->coffs + h->ncomm + 1);
+      }
+      const uint64_t na = (uint64_t)st->B * st->natt;
+      if ((rc = dalloc(s, &bits, nb_total + 16)) || (rc = upload_into(bits, h->bits, nb_total)) ||
+          (rc = upload(s, &boffs, h->boffs, na + 1)) || (rc = upload(s, &committee, mem.data(), mem.size())) ||
+          (rc = upload(s, &coffs, offs.data(), offs.size())) || (rc = upload(s, &att_comm, h->att_comm, na)) ||
+          (rc = upload(s, &att_shard, h->att_shard, na)))
+        break;
+      if (st->world > 1 && (rc = upload(s, &cpos, pos.data(), pos.size()))) break;
+    }
+    if (st->nrec && (rc = upload(s, &recd, h->rec_dynasty, (size_t)st->B * st->nrec))) break;
+    if ((rc = dalloc(s, &winner, (size_t)st->B * std::max<uint32_t>(st->nrec, 1))) ||
+        (rc = dalloc(s, &act_mask, (size_t)st->B * std::max<uint64_t>(s.wl, 1))) ||
+        (rc = dalloc(s, &blk_cnt, (size_t)st->B * (vbpi + 1))) ||
+        (rc = dalloc(s, &act_list, st->all_active ? 1 : (size_t)st->B * st->N)))
+      break;
+    for (uint32_t p = 0; p < st->nparts && !rc; ++p) {
+      Part& q = s.part[p];
+      q.i0 = st->B * p / st->nparts;
+      q.B = st->B * (p + 1) / st->nparts - q.i0;
+      const uint64_t Bp = q.B, i0 = q.i0;
+      for (int k = 0; k < 2 && !rc; ++k) rc = dalloc(s, &q.red[k], Bp * kScal + 2 * Bp * st->natt);
+      if (rc) break;
+      if (st->general && ((rc = dalloc(s, &q.mask_send, Bp * st->sw)) ||
+                          (rc = dalloc(s, &q.gmask, (size_t)st->world * Bp * st->sw)) ||
+                          (rc = dalloc(s, &q.gblk, Bp * vblocks_per_inst(st->N)))))
+        break;
+      if ((rc = dalloc(s, &q.nb, Bp))) break;
+      e = hipEventCreateWithFlags(&q.ev_red, hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&q.ev_gather, hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&q.ev_nb, hipEventDisableTiming);
+      if (e != hipSuccess) {
+        rc = hip_fail(e, "hipEventCreate");
+        break;
+      }
+      EpochArgs& a = q.a;
+      std::memset(&a, 0, sizeof a);
+      a.ninst = q.B;
+      a.nval = s.n;
+      a.val_offset = s.lo;
+      a.nval_global = st->N;
+      a.kind = PZ_KIND_ACTIVE;
+      a.balance = bal + i0 * s.n;
+      a.start = start + i0 * s.n;
+      a.end = end + i0 * s.n;
+      a.dynasty = dyn + i0;
+      a.total_deposit = tdep + i0;
+      a.natt = st->natt;
+      if (st->natt) {
+        a.bits = bits;
+        a.boffs = boffs + i0 * st->natt;
+        a.max_inst_bytes = max_inst_bytes;
+        a.committee = committee;
+        a.coffs = coffs;
+        a.cpos = cpos;
+        a.att_comm = att_comm + i0 * st->natt;
+        a.att_shard = att_shard + i0 * st->natt;
+      }
+      a.pop_rank = (uint32_t)s.grank;
+      a.pop_world = (uint32_t)st->world;
+      a.nrec = st->nrec;
+      a.rec_dynasty = recd ? recd + i0 * st->nrec : nullptr;
+      a.winner = winner + i0 * std::max<uint32_t>(st->nrec, 1);
+      a.act_mask = act_mask + i0 * std::max<uint64_t>(s.wl, 1);
+      a.blk_cnt = blk_cnt + i0 * (vbpi + 1);
+      a.act_list = st->all_active ? act_list : act_list + i0 * st->N;
+      q.cur = 1;  // flip() below binds red[0] as the first step's buffer
+    }
+  }
+  if (rc) {
+    delete st;
+    return rc;
+  }
+  for (Shard& s : st->sh) {
+    (void)hipSetDevice(s.dev);
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+      delete st;
+      return hip_fail(e, "epoch state upload");
+    }
+  }
+  flip(st);
+  *out = st;
+  return PZ_OK;
+}
+
+int pz_epoch_state_step(pz_epoch_state* st) {
+  if (!st) return fail(PZ_EINVAL, "state is null");
+  int rc = st->world > 1 ? step_sharded(st) : step_world1(st);
+  if (rc) return rc;
+  flip(st);
+  ++st->steps;
+  return PZ_OK;
+}
+
+int pz_epoch_state_sync(pz_epoch_state* st) {
+  if (!st) return fail(PZ_EINVAL, "state is null");
+  for (Shard& s : st->sh) {
+    (void)hipSetDevice(s.dev);
+    hipError_t e = hipStreamSynchronize(s.s);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize (epoch state)");
+  }
+  return PZ_OK;
+}
+
+int pz_epoch_state_shard(const pz_epoch_state* st, int local, uint64_t* lo, uint64_t* hi, int* device,
+                         void** stream) {
+  if (!st) return fail(PZ_EINVAL, "state is null");
+  if (local < 0 || local >= (int)st->sh.size()) return fail(PZ_EINVAL, "local rank %d of %zu", local, st->sh.size());
+  const Shard& s = st->sh[local];
+  if (lo) *lo = s.lo;
+  if (hi) *hi = s.hi;
+  if (device) *device = s.dev;
+  if (stream) *stream = s.s;
+  return PZ_OK;
+}
+
+int pz_epoch_state_results(pz_epoch_state* st, int local, uint64_t* balance, uint64_t* scal, uint64_t* vote,
+                           uint64_t* total, uint32_t* winner) {
+  int rc = pz_epoch_state_shard(st, local, nullptr, nullptr, nullptr, nullptr);
+  if (rc || (rc = pz_epoch_state_sync(st))) return rc;
+  if (!st->steps) return fail(PZ_EINVAL, "no step has run");
+  Shard& s = st->sh[local];
+  (void)hipSetDevice(s.dev);
+  hipError_t e = hipSuccess;
+  for (uint32_t p = 0; p < st->nparts && e == hipSuccess; ++p) {
+    const Part& q = s.part[p];
+    const uint64_t Bp = q.B, i0 = q.i0, na = st->natt;
+    if (balance && s.n) e = hipMemcpy(balance + i0 * s.n, q.a.balance, Bp * s.n * 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && scal) e = hipMemcpy(scal + i0 * kScal, q.results, Bp * kScal * 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && vote && na)
+      e = hipMemcpy(vote + i0 * na, q.results + Bp * kScal, Bp * na * 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && total && na)
+      e = hipMemcpy(total + i0 * na, q.results + Bp * kScal + Bp * na, Bp * na * 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && winner && st->nrec)
+      e = hipMemcpy(winner + i0 * st->nrec, q.a.winner, Bp * st->nrec * 4, hipMemcpyDeviceToHost);
+  }
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "epoch state results D2H");
+}
+
+void pz_epoch_state_free(pz_epoch_state* st) { delete st; }
+
+}  // extern "C"

@@ -17,10 +17,12 @@ struct DevBuf {
   void* ptr = nullptr;
   size_t cap = 0;
   int reserve(size_t bytes);
+  void release();
 };
 
 struct DeviceCtx {
   int device = 0;
+  bool checked = false;  // gfx950 verified
   std::mutex mu;
   hipStream_t stream = nullptr;
   DevBuf in, out, aux;
@@ -32,6 +34,7 @@ struct DeviceCtx {
 int fail(int code, const char* fmt, ...);
 int hip_fail(hipError_t e, const char* what);
 int acquire(DeviceCtx** out);
+int device_ctx(int device, DeviceCtx** out);
 
 // Copies host arrays into the context's staging slots and tracks the stream.
 struct Stager {

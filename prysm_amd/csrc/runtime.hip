@@ -9,6 +9,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "blake2b_kernels.h"
@@ -68,6 +69,36 @@ int DevBuf::reserve(size_t bytes) {
   return PZ_OK;
 }
 
+void DevBuf::release() {
+  if (ptr) (void)hipFree(ptr);
+  ptr = nullptr;
+  cap = 0;
+}
+
+// A device's library context, after checking that it is a gfx950 (no fallback to anything
+// else); does not change the calling thread's default device.
+int device_ctx(int device, DeviceCtx** out) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0)
+    return fail(PZ_EDEVICE, "no HIP device available (%s)", e != hipSuccess ? hipGetErrorString(e) : "0 devices");
+  if (device < 0 || device >= n) return fail(PZ_EINVAL, "device %d out of range [0,%d)", device, n);
+  DeviceCtx* c = DeviceCtx::get(device);
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->checked) {
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+      return fail(PZ_EDEVICE, "device %d is %s; this library is built for gfx950 only", device, prop.gcnArchName);
+    c->checked = true;
+  }
+  int rc = c->ensure_stream();
+  if (rc) return rc;
+  *out = c;
+  return PZ_OK;
+}
+
 // Resolve the calling thread's device and lock it.  Fails loudly when no device exists.
 int acquire(DeviceCtx** out) {
   if (g_device < 0) {
@@ -104,22 +135,34 @@ int pz_device_count(int* count) {
 }
 
 int pz_init(int device) {
-  int n = 0;
-  hipError_t e = hipGetDeviceCount(&n);
-  if (e != hipSuccess || n == 0)
-    return fail(PZ_EDEVICE, "no HIP device available (%s)",
-                e != hipSuccess ? hipGetErrorString(e) : "0 devices");
-  if (device < 0 || device >= n) return fail(PZ_EINVAL, "device %d out of range [0,%d)", device, n);
-  hipDeviceProp_t prop;
-  e = hipGetDeviceProperties(&prop, device);
-  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
-  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-    return fail(PZ_EDEVICE, "device %d is %s; this library is built for gfx950 only", device,
-                prop.gcnArchName);
+  DeviceCtx* c;
+  int rc = device_ctx(device, &c);
+  if (rc) return rc;
   g_device = device;
-  DeviceCtx* c = DeviceCtx::get(device);
-  std::lock_guard<std::mutex> lk(c->mu);
-  return c->ensure_stream();
+  return PZ_OK;
+}
+
+void pz_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  for (DeviceCtx*& c : g_ctx) {
+    if (!c) continue;
+    {
+      std::lock_guard<std::mutex> l2(c->mu);
+      (void)hipSetDevice(c->device);
+      if (c->stream) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamDestroy(c->stream);
+      }
+      c->in.release();
+      c->out.release();
+      c->aux.release();
+      for (DevBuf& b : c->slot) b.release();
+    }
+    delete c;
+    c = nullptr;
+  }
+  g_ctx.clear();
+  g_device = -1;
 }
 
 // ---- H -------------------------------------------------------------------------------------
@@ -145,19 +188,17 @@ int pz_dev_blake2b512_batch(const uint8_t* d_msgs, const uint64_t* d_offsets, ui
   return e == hipSuccess ? PZ_OK : hip_fail(e, "pz_b2b_csr_kernel");
 }
 
-int pz_blake2b512_batch(const uint8_t* msgs, const uint64_t* offsets, uint64_t n, uint8_t* out,
-                        uint32_t out_bytes) {
-  if (out_bytes != 32 && out_bytes != 64) return fail(PZ_EINVAL, "out_bytes must be 32 or 64");
-  if (n == 0) return PZ_OK;
-  if (!offsets || !out) return fail(PZ_EINVAL, "null pointer");
-  const uint64_t base = offsets[0], total = offsets[n] - offsets[0];
-  if (total && !msgs) return fail(PZ_EINVAL, "null msgs");
-  for (uint64_t i = 0; i < n; ++i)
-    if (offsets[i + 1] < offsets[i]) return fail(PZ_EINVAL, "offsets not monotone at %llu", (unsigned long long)i);
+}  // extern "C"
 
-  DeviceCtx* c;
-  int rc = acquire(&c);
-  if (rc) return rc;
+namespace pz {
+// The batch hash on one device's context (arguments already validated).
+int hash_batch_on(DeviceCtx* c, const uint8_t* msgs, const uint64_t* offsets, uint64_t n, uint8_t* out,
+                  uint32_t out_bytes) {
+  if (n == 0) return PZ_OK;
+  hipError_t e0 = hipSetDevice(c->device);
+  if (e0 != hipSuccess) return hip_fail(e0, "hipSetDevice");
+  const uint64_t base = offsets[0], total = offsets[n] - offsets[0];
+  int rc;
 
   // Long messages (serial chains) go to host threads while the GPU hashes the rest.
   std::vector<uint64_t> lng = long_messages(offsets, n);
@@ -178,7 +219,7 @@ int pz_blake2b512_batch(const uint8_t* msgs, const uint64_t* offsets, uint64_t n
       idx.push_back(i);
     }
     std::vector<uint8_t> part(idx.size() * out_bytes);
-    rc = pz_blake2b512_batch(cat.data(), co.data(), idx.size(), part.data(), out_bytes);
+    rc = hash_batch_on(c, cat.data(), co.data(), idx.size(), part.data(), out_bytes);
     job.join();
     if (rc) return rc;
     for (size_t j = 0; j < idx.size(); ++j) std::memcpy(out + idx[j] * out_bytes, &part[j * out_bytes], out_bytes);
@@ -220,6 +261,61 @@ int pz_blake2b512_batch(const uint8_t* msgs, const uint64_t* offsets, uint64_t n
   if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync D2H");
   e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  return PZ_OK;
+}
+
+static int check_batch_args(const uint8_t* msgs, const uint64_t* offsets, uint64_t n, uint8_t* out,
+                            uint32_t out_bytes) {
+  if (out_bytes != 32 && out_bytes != 64) return fail(PZ_EINVAL, "out_bytes must be 32 or 64");
+  if (n == 0) return PZ_OK;
+  if (!offsets || !out) return fail(PZ_EINVAL, "null pointer");
+  if (offsets[n] != offsets[0] && !msgs) return fail(PZ_EINVAL, "null msgs");
+  for (uint64_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) return fail(PZ_EINVAL, "offsets not monotone at %llu", (unsigned long long)i);
+  return PZ_OK;
+}
+}  // namespace pz
+
+extern "C" {
+
+int pz_blake2b512_batch(const uint8_t* msgs, const uint64_t* offsets, uint64_t n, uint8_t* out,
+                        uint32_t out_bytes) {
+  int rc = check_batch_args(msgs, offsets, n, out, out_bytes);
+  if (rc || n == 0) return rc;
+  DeviceCtx* c;
+  if ((rc = acquire(&c))) return rc;
+  return hash_batch_on(c, msgs, offsets, n, out, out_bytes);
+}
+
+int pz_comm_blake2b512_batch(const pz_comm* comm, const uint8_t* msgs, const uint64_t* offsets, uint64_t n,
+                             uint8_t* out, uint32_t out_bytes) {
+  if (!comm) return fail(PZ_EINVAL, "comm is null");
+  int rc = check_batch_args(msgs, offsets, n, out, out_bytes);
+  if (rc || n == 0) return rc;
+  int world = 1, nlocal = 1, first = 0;
+  pz_comm_size(comm, &world, &nlocal, &first);
+  std::vector<int> rcs(nlocal, PZ_OK);
+  std::vector<std::string> errs(nlocal);
+  auto work = [&](int i) {
+    const uint64_t r = (uint64_t)(first + i);
+    const uint64_t a = n * r / world, b = n * (r + 1) / world;
+    int dev = 0;
+    DeviceCtx* c;
+    int k = pz_comm_device(comm, i, &dev);
+    if (!k) k = device_ctx(dev, &c);
+    if (!k && b > a) k = hash_batch_on(c, msgs, offsets + a, b - a, out + a * out_bytes, out_bytes);
+    rcs[i] = k;
+    if (k) errs[i] = g_err;
+  };
+  if (nlocal == 1) {
+    work(0);
+  } else {  // one host thread per local rank: the devices hash concurrently
+    std::vector<std::thread> th;
+    for (int i = 0; i < nlocal; ++i) th.emplace_back(work, i);
+    for (std::thread& t : th) t.join();
+  }
+  for (int i = 0; i < nlocal; ++i)
+    if (rcs[i]) return fail(rcs[i], "local rank %d: %s", i, errs[i].c_str());
   return PZ_OK;
 }
 

@@ -1,0 +1,147 @@
+"""Python face of the library's own multi-GPU layer (include/prysm_hip.h, "multi-GPU").
+
+``Comm`` wraps a ``pz_comm`` (RCCL over xGMI, or the in-process loopback used to run the
+sharded path on one GPU); ``NativeEpoch`` wraps a ``pz_epoch_state``: B epoch instances
+resident in HBM, sharded by validator range over the communicator's ranks, stepped entirely
+inside the C ABI (kernels and RCCL collectives on the library's streams).  This is the path a
+cgo caller links; ``prysm_amd.epoch.DeviceEpoch`` (torch.distributed collectives) is kept as
+the test double of the same orchestration.
+"""
+import ctypes
+
+import numpy as np
+
+from prysm_amd import _lib
+from prysm_amd._lib import EpochHost, SCAL_COUNT, lib, ptr
+
+COMM_ID_BYTES = 128
+
+
+class Comm:
+    """A ``pz_comm``.  Use the constructors below; ``free()`` (or garbage collection) releases it."""
+
+    def __init__(self, handle):
+        self.h = handle
+        w, nl, r0 = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        lib.call("pz_comm_size", self.h, ctypes.byref(w), ctypes.byref(nl), ctypes.byref(r0))
+        self.world, self.nlocal, self.first_rank = w.value, nl.value, r0.value
+
+    @staticmethod
+    def unique_id():
+        buf = (ctypes.c_uint8 * COMM_ID_BYTES)()
+        lib.call("pz_comm_unique_id", buf)
+        return bytes(buf)
+
+    @classmethod
+    def rank(cls, uid, world, rank, device):
+        """One process per GPU: RCCL rank ``rank`` of ``world`` (``uid`` from rank 0's
+        ``unique_id()``)."""
+        h = ctypes.c_void_p()
+        lib.call("pz_comm_init_rank", (ctypes.c_uint8 * COMM_ID_BYTES)(*uid), world, rank, device, ctypes.byref(h))
+        return cls(h)
+
+    @classmethod
+    def devices(cls, ndev, devices=None):
+        """One process driving ``ndev`` GPUs (ncclCommInitAll)."""
+        h = ctypes.c_void_p()
+        arr = (ctypes.c_int * ndev)(*devices) if devices is not None else None
+        lib.call("pz_init_devices", ndev, arr, ctypes.byref(h))
+        return cls(h)
+
+    @classmethod
+    def loopback(cls, world, device=0):
+        """``world`` ranks in this process on one device (collectives without RCCL)."""
+        h = ctypes.c_void_p()
+        lib.call("pz_comm_init_loopback", world, device, ctypes.byref(h))
+        return cls(h)
+
+    def hash_batch(self, data, offsets, out_bytes=32):
+        """pz_comm_blake2b512_batch: this process's ranks' slices of the CSR batch; rows of
+        other processes' slices are left zero."""
+        n = len(offsets) - 1
+        out = np.zeros((max(n, 0), out_bytes), dtype=np.uint8)
+        if n > 0:
+            data = np.ascontiguousarray(data, dtype=np.uint8)
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+            lib.call("pz_comm_blake2b512_batch", self.h, ptr(data), ptr(offsets), n, ptr(out), out_bytes)
+        return out
+
+    def free(self):
+        if self.h:
+            lib.dll.pz_comm_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # pragma: no cover - interpreter teardown
+            pass
+
+
+class NativeEpoch:
+    """``pz_epoch_state``: the same inputs as ``prysm_amd.epoch.DeviceEpoch`` (a
+    ``synth.epoch_batch``-shaped dict over all validators)."""
+
+    def __init__(self, inst, device=0, comm=None):
+        u64 = lambda a: np.ascontiguousarray(a, dtype=np.uint64)  # noqa: E731
+        u32 = lambda a: np.ascontiguousarray(a, dtype=np.uint32)  # noqa: E731
+        self._keep = k = dict(balance=u64(inst["balance"]), start=u64(inst["start"]), end=u64(inst["end"]),
+                              dynasty=u64(inst["dynasty"]), total_deposit=u64(inst["total_deposit"]),
+                              bits=np.ascontiguousarray(inst["bits"], dtype=np.uint8), boffs=u64(inst["boffs"]),
+                              committee=u32(inst["committee"]), coffs=u64(inst["coffs"]),
+                              att_comm=u32(inst["att_comm"]), att_shard=u32(inst["att_shard"]),
+                              rec_dynasty=u64(inst["rec_dynasty"]))
+        self.B, self.N, self.natt = int(inst["ninst"]), int(inst["nval"]), int(inst["natt"])
+        self.nrec = int(k["rec_dynasty"].shape[1]) if k["rec_dynasty"].ndim == 2 else int(k["rec_dynasty"].size)
+        h = EpochHost()
+        h.ninst, h.nval = self.B, self.N
+        h.balance, h.start, h.end = ptr(k["balance"]), ptr(k["start"]), ptr(k["end"])
+        h.dynasty, h.total_deposit = ptr(k["dynasty"]), ptr(k["total_deposit"])
+        h.natt, h.bits, h.boffs = self.natt, ptr(k["bits"]), ptr(k["boffs"])
+        h.committee, h.coffs, h.ncomm = ptr(k["committee"]), ptr(k["coffs"]), len(k["coffs"]) - 1
+        h.att_comm, h.att_shard = ptr(k["att_comm"]), ptr(k["att_shard"])
+        h.nrec, h.rec_dynasty = self.nrec, ptr(k["rec_dynasty"])
+        self.comm = comm
+        self.st = ctypes.c_void_p()
+        lib.call("pz_epoch_state_new", comm.h if comm is not None else None, device, ctypes.byref(h),
+                 ctypes.byref(self.st))
+        self._keep = None  # the library copied everything it needs
+        self.nlocal = comm.nlocal if comm is not None else 1
+
+    def step(self):
+        lib.call("pz_epoch_state_step", self.st)
+
+    def sync(self):
+        lib.call("pz_epoch_state_sync", self.st)
+
+    def shard(self, local=0):
+        """(lo, hi, device, stream handle) of local rank ``local``."""
+        lo, hi, dev, s = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int(), ctypes.c_void_p()
+        lib.call("pz_epoch_state_shard", self.st, local, ctypes.byref(lo), ctypes.byref(hi), ctypes.byref(dev),
+                 ctypes.byref(s))
+        return lo.value, hi.value, dev.value, s.value
+
+    def results(self, local=0):
+        """Host copies after the last step: (balance [B][hi-lo], scal [B][8], vote, total, winner)."""
+        lo, hi, _, _ = self.shard(local)
+        bal = np.empty((self.B, hi - lo), dtype=np.uint64)
+        scal = np.empty((self.B, SCAL_COUNT), dtype=np.uint64)
+        vote = np.empty((self.B, self.natt), dtype=np.uint64)
+        total = np.empty((self.B, self.natt), dtype=np.uint64)
+        win = np.empty((self.B, self.nrec), dtype=np.uint32)
+        lib.call("pz_epoch_state_results", self.st, local, ptr(bal), ptr(scal), ptr(vote), ptr(total), ptr(win))
+        return bal, scal, vote, total, win
+
+    def free(self):
+        if self.st:
+            lib.dll.pz_epoch_state_free(self.st)
+            self.st = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # pragma: no cover - interpreter teardown
+            pass
+
+
+__all__ = ["Comm", "NativeEpoch", "_lib"]

@@ -35,7 +35,8 @@ def test_version():
 
 @pytest.mark.parametrize("name,cls", [("pz_epoch_batch", _lib.EpochBatch), ("pz_validator_cols", _lib.ValidatorCols),
                                        ("pz_att_check_batch", _lib.AttCheckBatch),
-                                       ("pz_attestation_cols", _lib.AttestationCols)])
+                                       ("pz_attestation_cols", _lib.AttestationCols),
+                                       ("pz_epoch_host", _lib.EpochHost)])
 def test_struct_layout(name, cls):
     # the structs are passed by pointer from ctypes: field order/packing must match the header
     src = open(os.path.join(ROOT, "include", "prysm_hip.h")).read()

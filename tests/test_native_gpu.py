@@ -1,0 +1,141 @@
+"""The library's own multi-GPU layer (include/prysm_hip.h "multi-GPU"): pz_epoch_state stepped
+inside the C ABI, sharded by validator range over a pz_comm, bit-exact against the oracle.
+
+On a one-GPU box the sharded path runs over the loopback communicator (every rank on cuda:0,
+collectives by device copies + a sum kernel): the shard ranges, local committees with their
+bitfield positions, the two-part pipeline, the active-mask all-gather and the next-cycle
+all-reduce are the same code RCCL drives.  RCCL itself is exercised at world 1
+(pz_init_devices(1)); the multi-process RCCL form is what bench.py --gpus N runs."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import ref
+from prysm_amd import _lib, casper, synth
+from prysm_amd.native import Comm, NativeEpoch
+
+from epoch_ref_helpers import oracle_epoch
+
+pytestmark = pytest.mark.gpu
+
+
+def _inst(n, B, inactive, seed=5):
+    shuffled = casper.shuffle_indices(ref.bytes_to_hash(b"A"), np.arange(n, dtype=np.uint32))
+    inst = synth.epoch_batch(n, B, seed=seed, shuffled=shuffled)
+    if inactive:  # rank != index: the compaction / gathered-mask path
+        rng = np.random.default_rng(1)
+        inst["start"][:, rng.random(n) < 0.1] = 7
+        inst["end"][:, rng.random(n) < 0.1] = 1
+    return inst
+
+
+def _check(ne, inst, steps=1):
+    for _ in range(steps):
+        ne.step()
+        ne.sync()
+        want = [oracle_epoch(inst, b) for b in range(inst["ninst"])]
+        for local in range(ne.nlocal):
+            lo, hi, _, _ = ne.shard(local)
+            bal, scal, vote, total, win = ne.results(local)
+            for b, (nb, applied, nxt, v, t, w) in enumerate(want):
+                assert bool(scal[b, _lib.SCAL_APPLIED]) == applied, (local, b)
+                np.testing.assert_array_equal(bal[b], nb[lo:hi])
+                assert int(scal[b, _lib.SCAL_NEXT_BAL]) == nxt, (local, b)
+                np.testing.assert_array_equal(vote[b], v)
+                np.testing.assert_array_equal(total[b], t)
+                np.testing.assert_array_equal(win[b], w)
+        for b, (nb, *_rest) in enumerate(want):
+            inst["balance"][b] = nb
+
+
+@pytest.mark.parametrize("n,B,inactive", [(65536, 3, False), (5000, 2, True), (4096, 9, False), (3000, 5, True)])
+def test_native_epoch_single_device(n, B, inactive):
+    inst = _inst(n, B, inactive)
+    _check(NativeEpoch(inst, device=0), inst, steps=2)
+
+
+def test_native_epoch_rccl_world1():
+    comm = Comm.devices(1)
+    assert (comm.world, comm.nlocal) == (1, 1)
+    inst = _inst(8192, 4, True)
+    _check(NativeEpoch(inst, comm=comm), inst, steps=2)
+
+
+@pytest.mark.parametrize("world,n,B,inactive", [(2, 65536, 3, False), (2, 20000, 2, True), (3, 5000, 4, True),
+                                                (8, 20000, 1, True), (5, 3000, 7, False)])
+def test_native_epoch_sharded_loopback(world, n, B, inactive):
+    comm = Comm.loopback(world)
+    inst = _inst(n, B, inactive)
+    _check(NativeEpoch(inst, comm=comm), inst, steps=2)
+
+
+@pytest.mark.parametrize("inactive", [False, True])
+def test_native_epoch_configs3_world8_loopback(inactive):
+    """BASELINE configs[3]: 1,048,576 validators over 8 ranks (131,072 each), 65 committees per
+    slot, through the library's sharded step."""
+    inst = _inst(1 << 20, 2, inactive)
+    _check(NativeEpoch(inst, comm=Comm.loopback(8)), inst)
+
+
+def test_native_epoch_panic_flags_sharded():
+    """A committee member beyond the validator set: Go panics in processCrosslinks
+    (core.go:535); rank 0 keeps the out-of-range member, the flag survives the all-reduce and
+    no balance changes on any rank."""
+    inst = _inst(4096, 2, False)
+    inst["committee"] = inst["committee"].copy()
+    inst["committee"][5] = 4096 + 17
+    ne = NativeEpoch(inst, comm=Comm.loopback(3))
+    ne.step()
+    for local in range(3):
+        lo, hi, _, _ = ne.shard(local)
+        bal, scal, *_ = ne.results(local)
+        assert ((scal[:, _lib.SCAL_ERR_XL] & 1) == 1).all()  # PZ_XLERR_MEMBER
+        assert scal[:, _lib.SCAL_APPLIED].sum() == 0
+        np.testing.assert_array_equal(bal, inst["balance"][:, lo:hi])
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_comm_hash_batch_loopback(world):
+    rng = np.random.default_rng(world)
+    lens = rng.integers(0, 700, size=1001)
+    msgs = [rng.bytes(int(k)) for k in lens]
+    offs = np.zeros(len(msgs) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    data = np.frombuffer(b"".join(msgs) + bytes(16), dtype=np.uint8)
+    got = Comm.loopback(world).hash_batch(data, offs, 32)
+    for i, m in enumerate(msgs):
+        assert got[i].tobytes() == hashlib.blake2b(m).digest()[:32], i
+
+
+def test_comm_hash_batch_rccl_world1():
+    msgs = [bytes([i & 255]) * (i * 7) for i in range(300)]
+    offs = np.zeros(len(msgs) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(m) for m in msgs])
+    data = np.frombuffer(b"".join(msgs) + bytes(16), dtype=np.uint8)
+    got = Comm.devices(1).hash_batch(data, offs, 64)
+    assert [g.tobytes() for g in got] == [hashlib.blake2b(m).digest() for m in msgs]
+
+
+def test_unique_id_and_shutdown():
+    """ncclCommInitRank through the C ABI, then pz_shutdown (in a child process: it frees the
+    library's device contexts, which other tests' live objects may still hold)."""
+    import subprocess
+    import sys
+    code = r"""
+import hashlib, sys
+sys.path.insert(0, %r)
+from prysm_amd import _lib
+from prysm_amd.native import Comm
+uid = Comm.unique_id()
+assert len(uid) == 128
+c = Comm.rank(uid, 1, 0, 0)
+assert (c.world, c.nlocal, c.first_rank) == (1, 1, 0)
+c.free()
+assert _lib.blake2b512_batch([b"abc"], 64)[0] == hashlib.blake2b(b"abc").digest()
+_lib.lib.dll.pz_shutdown()
+assert _lib.blake2b512_batch([b"abcd"], 64)[0] == hashlib.blake2b(b"abcd").digest()
+print("ok")
+""" % (_lib.HERE.rsplit("/", 1)[0],)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stderr[-2000:]
