@@ -80,6 +80,9 @@ def parse():
     p.add_argument("--cpu-replay-blocks", type=int, default=520,
                    help="blocks of the replay chain the CPU baseline (oracle/replay.py) processes (~8 s)")
     p.add_argument("--no-epoch", action="store_true")
+    p.add_argument("--epoch-path", default="native", choices=["native", "torch"],
+                   help="native: pz_epoch_state (C ABI, the library's RCCL communicator); torch: DeviceEpoch "
+                        "over torch.distributed (the test double of the same orchestration)")
     p.add_argument("--no-replay", action="store_true")
     p.add_argument("--no-wire", action="store_true")
     p.add_argument("--no-attcheck", action="store_true")
@@ -101,11 +104,27 @@ HASH_KERNEL = "pz_b2b_fixed_persistent_kernel"
 CPU_SAMPLE_S = 8.0  # seconds of CPU work per cpu_baseline leg (three legs: ~25 s in all)
 
 
-def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseline=True):
+def native_comm(dist, rank, world, local):
+    """The library's own RCCL communicator over the torchrun ranks: rank 0's ncclUniqueId
+    (pz_comm_unique_id) reaches the others through the launcher's TCP store."""
+    from prysm_amd.native import Comm
+    store = dist.distributed_c10d._get_default_store()
+    if rank == 0:
+        store.set("pz_comm_uid", Comm.unique_id())
+    uid = store.get("pz_comm_uid")
+    return Comm.rank(uid, world, rank, local)
+
+
+def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseline=True, comm=None):
     """BASELINE configs[2] (N=1: 65,536 validators, B instances per step) / configs[3]
-    (N>1: 1,048,576 validators sharded over the ranks, RCCL all-reduce of the sums)."""
+    (N>1: 1,048,576 validators sharded over the ranks, RCCL all-reduce of the sums).
+
+    The step is pz_epoch_state_step: kernels and RCCL collectives enqueued by the C ABI on
+    the library's streams (the path a cgo caller links).  ``--epoch-path torch`` runs the
+    same orchestration through torch.distributed instead (prysm_amd.epoch.DeviceEpoch)."""
     from prysm_amd import casper, synth
     from prysm_amd.epoch import DeviceEpoch
+    from prysm_amd.native import NativeEpoch
 
     nval = nval or args.epoch_validators or (65536 if world == 1 else 1 << 20)
     # throughput mode: 16.7 M validator-epochs per GPU per step at every N (weak scaling; at
@@ -114,13 +133,23 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
     seed_a = b"A" + bytes(31)  # common.Hash{'A'} (casper/sharding_test.go:57)
     shuffled = casper.shuffle_indices(seed_a, np.arange(nval, dtype=np.uint32))
     inst = synth.epoch_batch(nval, ninst, seed=3, shuffled=shuffled)
-    de = DeviceEpoch(inst, dev, rank=rank, world=world)
-    stream = torch.cuda.current_stream(dev)
+    native = args.epoch_path == "native"
+    if native:
+        de = NativeEpoch(inst, device=dev.index, comm=comm if world > 1 else None)
+        lo, hi, _, sp = de.shard(0)
+        stream = torch.cuda.ExternalStream(sp, device=dev)
+        step = de.step
+    else:
+        de = DeviceEpoch(inst, dev, rank=rank, world=world)
+        lo, hi = de.lo, de.hi
+        stream = torch.cuda.current_stream(dev)
+        step = lambda: de.step(stream)  # noqa: E731
     # a fixed count (not a time budget): at N > 1 every step holds collectives, so all ranks
     # must run the same number of them
     for _ in range(args.warmup + (30 if args.clock_warm_ms > 0 else 0)):
-        de.step(stream)
+        step()
     torch.cuda.synchronize(dev)
+    stream.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -129,8 +158,9 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
     t0 = time.perf_counter()
     for e0, e1 in evs:
         e0.record(stream)
-        de.step(stream)
+        step()
         e1.record(stream)
+    stream.synchronize()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -140,7 +170,7 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
     if world > 1:
         wall = max_over_ranks(wall, torch, dist, dev)
     units = nval * ninst * args.steps
-    local_units = (de.hi - de.lo) * ninst
+    local_units = (hi - lo) * ninst
     achieved = local_units * EPOCH_BYTES_PER_VALIDATOR / (step_ms * 1e-3)
     out = {
         "metric": "validator-epoch updates/s",
@@ -152,7 +182,9 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                                "popcount, CalculateRewards, next-cycle balance (BASELINE configs[%d])"
                                % (2 if (world == 1 and nval != 1 << 20) else 3),
                    "validators": nval, "instances_per_step": ninst, "attestations_per_instance": inst["natt"],
-                   "parallelism": "validator-shard x%d + RCCL all-reduce" % world if world > 1 else "single GPU"},
+                   "parallelism": "validator-shard x%d + RCCL all-reduce" % world if world > 1 else "single GPU",
+                   "path": ("pz_epoch_state_step (C ABI: HIP kernels + the library's RCCL communicator)"
+                            if native else "DeviceEpoch (pz_dev_epoch_* + torch.distributed collectives)")},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
                      "traffic": (pmc_traffic(EPOCH_KERNELS) if (nval, ninst) == (65536, 256) else
@@ -164,8 +196,9 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                      "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": local_units * EPOCH_BYTES_PER_VALIDATOR},
     }
+    del de
     if rank == 0 and world == 1:
-        out["parity"] = epoch_parity(inst, dev, torch)
+        out["parity"] = epoch_parity(inst, dev)
     if world == 1 and baseline:
         out["single_instance"] = epoch_single_instance(args, torch, dev, nval, shuffled)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and baseline:
@@ -173,24 +206,24 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
     return out
 
 
-def epoch_parity(inst, dev, torch):
-    """The checker for the timed workload: one fresh step of the same B instances (the timed
-    loop has already stepped the balances many times), instance 0 compared bit-exactly with
-    the numpy oracle (oracle/epoch_np.py): balances, tallies, winners, next-cycle total."""
+def epoch_parity(inst, dev):
+    """The checker for the timed workload: one fresh step of the same B instances through
+    pz_epoch_state (the timed loop has already stepped the balances many times), instance 0
+    compared bit-exactly with the numpy oracle (oracle/epoch_np.py): balances, tallies,
+    winners, next-cycle total."""
     from prysm_amd import _lib
-    from prysm_amd.epoch import DeviceEpoch
+    from prysm_amd.native import NativeEpoch
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from epoch_ref_helpers import oracle_epoch
 
-    de = DeviceEpoch(inst, dev)
+    de = NativeEpoch(inst, device=dev.index)
     de.step()
-    torch.cuda.synchronize(dev)
     bal, scal, vote, total, win = de.results()
+    de.free()
     nb, applied, nxt, v, t, w = oracle_epoch(inst, 0)
     ok = (np.array_equal(bal[0], nb) and bool(scal[0, _lib.SCAL_APPLIED]) == applied
           and int(scal[0, _lib.SCAL_NEXT_BAL]) == nxt and np.array_equal(vote[0], v)
           and np.array_equal(total[0], t) and np.array_equal(win[0], w))
-    del de
     return "instance 0 of the timed %d x %d workload, one step, bit-exact vs oracle/epoch_np: %s" % (
         inst["ninst"], inst["nval"], ok)
 
@@ -199,20 +232,20 @@ def epoch_single_instance(args, torch, dev, nval, shuffled):
     """the latency of ONE epoch instance (B = 1) at configs[2]'s size,
     launch-bound at this size (2.9 MB of algorithmic traffic); device time by HIP events."""
     from prysm_amd import synth
-    from prysm_amd.epoch import DeviceEpoch
+    from prysm_amd.native import NativeEpoch
 
-    de = DeviceEpoch(synth.epoch_batch(nval, 1, seed=3, shuffled=shuffled), dev)
-    stream = torch.cuda.current_stream(dev)
+    de = NativeEpoch(synth.epoch_batch(nval, 1, seed=3, shuffled=shuffled), device=dev.index)
+    stream = torch.cuda.ExternalStream(de.shard(0)[3], device=dev)
     for _ in range(args.warmup + 20):
-        de.step(stream)
-    torch.cuda.synchronize(dev)
+        de.step()
+    stream.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for e0, e1 in evs:
         e0.record(stream)
-        de.step(stream)
+        de.step()
         e1.record(stream)
-    torch.cuda.synchronize(dev)
+    stream.synchronize()
     wall = time.perf_counter() - t0
     ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in evs]))
     return {"validators": nval, "instances_per_step": 1, "device_ms_median": ms,
@@ -730,7 +763,21 @@ def main():
     if world > 1:
         wall = max_over_ranks(wall, torch, dist, dev)
 
-    epoch = None if args.no_epoch else epoch_leg(args, torch, dist, dev, rank, world)
+    comm = None
+    if world > 1 and not args.no_epoch and args.epoch_path == "native":
+        # every rank must take the same path: agree on whether the communicator came up
+        err = None
+        try:
+            comm = native_comm(dist, rank, world, local)
+        except Exception as e:  # reported in the JSON line, never silent
+            err = "%s: %s" % (type(e).__name__, e)
+        ok = torch.tensor([0.0 if err else 1.0], device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if ok.item() < 1.0:
+            comm = None
+            args.epoch_path = "torch"
+            args.native_comm_error = err or "another rank failed to create its communicator"
+    epoch = None if args.no_epoch else epoch_leg(args, torch, dist, dev, rank, world, comm=comm)
     # configs[3]'s instance size (1,048,576 validators) on this one GPU: the N = 1 point of
     # the 1/2/4/8-GPU series that the N > 1 epoch leg runs (16 instances per GPU per step)
     epoch_1m = None
@@ -792,6 +839,8 @@ def main():
                 line["parity"] = "bit-exact vs cpu_baseline on all %d digests: %s" % (
                     n, bool(np.array_equal(gpu, digests)))
         if epoch is not None:
+            if getattr(args, "native_comm_error", None):
+                epoch["native_comm_error"] = args.native_comm_error
             line["epoch"] = epoch
         if epoch_1m is not None:
             line["epoch_1m_single_gpu"] = epoch_1m
