@@ -234,12 +234,14 @@ int pz_shuffle_validators_to_committees(const uint8_t seed[32], const uint64_t* 
  * all-reduce(sum) of scal[.][PZ_SCAL_NEXT_BAL].  After a multi-rank all-reduce,
  * PZ_SCAL_MAXIDX1 holds the sum of the per-rank values (single rank: the value). */
 #define PZ_SCAL_POP       0  /* attester bit count (deposit = 32 * this)               */
-#define PZ_SCAL_NACT      1  /* validators matching `kind` in range                     */
+#define PZ_SCAL_NACT      1  /* validators matching `kind` (written by the finish pass)  */
 #define PZ_SCAL_ERR_XL    2  /* != 0: processCrosslinks would panic                     */
 #define PZ_SCAL_ERR_RWD   3  /* != 0: CalculateRewards would panic (if threshold holds)  */
 #define PZ_SCAL_APPLIED   4  /* 1: threshold held, balances updated                     */
 #define PZ_SCAL_NEXT_BAL  5  /* sum of post-reward balances of active validators         */
 #define PZ_SCAL_MAXIDX1   6  /* 1 + max matching global index (0: none)                 */
+#define PZ_SCAL_NOMATCH   7  /* pass 1: validators in range NOT matching `kind` (all-reduced
+                                with the rest); pass 2 sets PZ_SCAL_NACT = nval_global - this */
 #define PZ_SCAL_COUNT     8
 #define PZ_XLERR_MEMBER   1ULL
 #define PZ_XLERR_BITFIELD 2ULL

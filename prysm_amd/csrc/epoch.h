@@ -16,7 +16,7 @@ namespace pz {
 enum : int {
   kPop = PZ_SCAL_POP, kNact = PZ_SCAL_NACT, kErrXl = PZ_SCAL_ERR_XL, kErrRwd = PZ_SCAL_ERR_RWD,
   kApplied = PZ_SCAL_APPLIED, kNextBal = PZ_SCAL_NEXT_BAL, kMaxIdx1 = PZ_SCAL_MAXIDX1,
-  kScal = PZ_SCAL_COUNT
+  kNoMatch = PZ_SCAL_NOMATCH, kScal = PZ_SCAL_COUNT
 };
 enum : uint64_t { kErrMember = PZ_XLERR_MEMBER, kErrBitfield = PZ_XLERR_BITFIELD, kErrShard = PZ_XLERR_SHARD };
 

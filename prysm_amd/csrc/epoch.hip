@@ -73,6 +73,8 @@ __device__ __forceinline__ uint64_t spread32(uint32_t x) {
   return v;
 }
 
+constexpr uint32_t kGroup = 32;  // chunks of one instance per round (validator / reward blocks)
+
 struct CountGrid {
   uint64_t vbpi, nvb, pbpi, npb, nxb;
   int vec;            // 1: validator arrays read 16 B per lane (nval even, 16-B aligned)
@@ -144,8 +146,11 @@ __device__ __forceinline__ void crosslink_wave(const EpochArgs& a, uint64_t ga, 
   }
 }
 
-extern "C" __global__ void __launch_bounds__(kThreads)
-pz_epoch_count_kernel(EpochArgs a, CountGrid g) {
+// V is an A/B knob for tools/ (0 in the product): bit 0 = validator blocks in rounds of
+// kGroup chunks per instance; bit 1 = a max-index atomic from every block; bit 2 = no
+// non-matching-count atomic (timing probe only: its results are wrong).
+template <int V>
+__device__ __forceinline__ void count_body(const EpochArgs& a, const CountGrid& g) {
   __shared__ uint64_t sh[kThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -173,7 +178,24 @@ pz_epoch_count_kernel(EpochArgs a, CountGrid g) {
   const uint64_t b = blockIdx.x - g.nxb;
 
   if (b < g.nvb) {  // ---- classify + count + active mask + max active index
-    const uint64_t inst = (uint32_t)b / (uint32_t)g.vbpi, chunk = (uint32_t)b - (uint32_t)inst * (uint32_t)g.vbpi;
+    // Instance-major order, one chunk of 2,048 validators per block (DRAM locality).  The
+    // epilogue's per-instance atomics are device-scope, performed at the memory side at ~12 ns
+    // each on one address, so they serialise when the blocks of one instance finish together
+    // (512 blocks per 1M-validator instance: 57.6 us for the pass against 47.5 without them).
+    // Blocks therefore count the validators that do NOT match `kind` (slot kNoMatch, an atomic
+    // only from a block that has some) and the finish pass turns that into kNact; with every
+    // validator active the pass issues one atomic per instance (the max index).
+    uint64_t chunk, inst;
+    if (V & 1) {  // r02 probe: rounds of kGroup chunks per instance
+      const uint32_t per_round = kGroup * a.ninst;
+      const uint32_t r = (uint32_t)b / per_round, rem = (uint32_t)b - r * per_round;
+      inst = rem / kGroup;
+      chunk = (uint64_t)r * kGroup + (rem % kGroup);
+      if (chunk >= g.vbpi) return;  // the last round's tail
+    } else {
+      inst = (uint32_t)b / (uint32_t)g.vbpi;
+      chunk = (uint32_t)b - (uint32_t)inst * (uint32_t)g.vbpi;
+    }
     const uint64_t base = chunk * kValPerBlock;
     const uint64_t d = a.dynasty[inst];
     const uint64_t* S = a.start + inst * a.nval;
@@ -181,6 +203,11 @@ pz_epoch_count_kernel(EpochArgs a, CountGrid g) {
     uint64_t* mask = a.act_mask ? a.act_mask + inst * ((a.nval + 63) / 64) : nullptr;
     uint32_t cnt = 0;
     uint64_t maxi1 = 0;
+    // the validator just past this block, loaded up front (it decides whether this block's
+    // max-index atomic is needed; see the epilogue)
+    const uint64_t bend = base + kValPerBlock < a.nval ? base + kValPerBlock : a.nval;
+    bool next_act = false;
+    if (!(V & 2) && tid == 0 && bend < a.nval) next_act = kind_pred(a.kind, S[bend], E[bend], d);
     if (g.vec) {  // 16 B per lane: validators i0, i0+1 (nval even, arrays 16-B aligned)
 #pragma unroll
       for (int j = 0; j < kValPerThread / 2; ++j) {
@@ -222,12 +249,17 @@ pz_epoch_count_kernel(EpochArgs a, CountGrid g) {
         }
       }
     }
-    uint64_t c = block_reduce<false>(lane == 0 ? cnt : 0, sh);
-    uint64_t m = block_reduce<true>(maxi1, sh);
+    const uint64_t c = block_reduce<false>(lane == 0 ? cnt : 0, sh);
+    const uint64_t m = block_reduce<true>(maxi1, sh);
     if (tid == 0) {
       if (a.blk_cnt) a.blk_cnt[inst * g.vbpi + chunk] = (uint32_t)c;
-      if (c) atomicAdd((unsigned long long*)&a.scal[inst * kScal + kNact], (unsigned long long)c);
-      if (m) atomicMax((unsigned long long*)&a.scal[inst * kScal + kMaxIdx1], (unsigned long long)m);
+      const uint64_t nomatch = (bend - base) - c;
+      if (nomatch && !(V & 4)) atomicAdd((unsigned long long*)&a.scal[inst * kScal + kNoMatch], (unsigned long long)nomatch);
+      // The max active index needs an atomic only from a block that can hold it: the last
+      // chunk, a block whose last validator is inactive, or one followed by an inactive
+      // validator.  With every validator active only the last chunk adds one.
+      const bool need = (V & 2) ? m != 0 : m && (bend == a.nval || m != a.val_offset + bend || !next_act);
+      if (need) atomicMax((unsigned long long*)&a.scal[inst * kScal + kMaxIdx1], (unsigned long long)m);
       // CalculateRewards would panic on CheckBit(last bitfield, m-1) (incentives.go:23)
       if (m && a.kind == PZ_KIND_ACTIVE) {
         uint64_t L = 0;
@@ -267,6 +299,23 @@ pz_epoch_count_kernel(EpochArgs a, CountGrid g) {
   }
 }
 
+#define PZ_COUNT_KERNEL(NAME, V) \
+  extern "C" __global__ void __launch_bounds__(kThreads) NAME(EpochArgs a, CountGrid g) { count_body<V>(a, g); }
+PZ_COUNT_KERNEL(pz_epoch_count_kernel, 0)
+PZ_COUNT_KERNEL(pz_epoch_count_v1_kernel, 1)
+PZ_COUNT_KERNEL(pz_epoch_count_v2_kernel, 2)
+PZ_COUNT_KERNEL(pz_epoch_count_v3_kernel, 3)
+PZ_COUNT_KERNEL(pz_epoch_count_v4_kernel, 4)
+PZ_COUNT_KERNEL(pz_epoch_count_v5_kernel, 5)
+#undef PZ_COUNT_KERNEL
+
+static int g_count_variant = 0;  // tools/ A/B only
+int set_count_variant(int v) {
+  const int old = g_count_variant;
+  g_count_variant = v & 7;
+  return old;
+}
+
 // ------------------------------------------------------------------------------------------
 // Crosslink winners (core.go:549-555): the first attestation, in order, whose 3*vote >=
 // 2*total and whose dynasty beats the shard's record wins that shard (atomicMin of index).
@@ -298,8 +347,7 @@ __device__ __forceinline__ void compact_block(const EpochArgs& a, uint64_t vbpi,
   __shared__ uint32_t wsum[kThreads / 64 * kValPerThread];
   __shared__ uint64_t base_off;
   const uint64_t inst = (uint32_t)blk / (uint32_t)vbpi, chunk = (uint32_t)blk - (uint32_t)inst * (uint32_t)vbpi;
-  const uint64_t nact = a.scal[inst * kScal + kNact];
-  if (!force && nact == a.nval) return;  // rank == index: nothing to compact
+  if (!force && a.scal[inst * kScal + kNoMatch] == 0) return;  // rank == index: nothing to compact
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) {
     uint64_t s = 0;
@@ -366,7 +414,7 @@ constexpr int kWordsPerChunk = (int)(kValPerBlock / 64);  // 32
 extern "C" __global__ void __launch_bounds__(64)
 pz_epoch_gcount_kernel(EpochArgs a, const uint64_t* __restrict__ gmask, uint64_t sw, uint32_t* gblk) {
   const uint64_t inst = blockIdx.y, chunk = blockIdx.x;
-  if (a.scal[inst * kScal + kNact] == a.nval_global) return;
+  if (a.scal[inst * kScal + kNoMatch] == 0) return;
   const int lane = threadIdx.x;
   const uint64_t nw = (a.nval_global + 63) / 64;
   const uint64_t w = chunk * kWordsPerChunk + lane;
@@ -378,7 +426,7 @@ pz_epoch_gcount_kernel(EpochArgs a, const uint64_t* __restrict__ gmask, uint64_t
 extern "C" __global__ void __launch_bounds__(64)
 pz_epoch_gcompact_kernel(EpochArgs a, const uint64_t* __restrict__ gmask, uint64_t sw, const uint32_t* gblk) {
   const uint64_t inst = blockIdx.y, chunk = blockIdx.x;
-  if (a.scal[inst * kScal + kNact] == a.nval_global) return;
+  if (a.scal[inst * kScal + kNoMatch] == 0) return;
   const int lane = threadIdx.x;
   uint64_t base = 0;  // active validators in the chunks before this one
   for (uint64_t c = lane; c < chunk; c += 64) base += gblk[inst * gridDim.x + c];
@@ -442,11 +490,14 @@ __device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
                                             const uint64_t* __restrict__ boffs_ro,
                                             const uint64_t* __restrict__ tdep_ro) {
   __shared__ uint64_t sh[kThreads / 64];
-  // 2-D grid: x = chunk within the instance, y = instance (no per-block division).  The next
+  // 2-D grid: x = instance, y = chunk (no per-block division).  The next
   // step's accumulators (scal_next) are zeroed at the END: a store ahead of the scalar reads
   // would stop the compiler from using s_load for them.
   if (vec) {  // 16 B per lane read-modify-write (nval even, arrays 16-B aligned)
-    const uint64_t inst = blockIdx.y, chunk = blockIdx.x;
+    // instance-minor order (x = instance, y = chunk): the next-cycle-total atomics of one
+    // instance never arrive in a burst (measured at 1M x 16: 39 us for the pass against 45 in
+    // rounds of kGroup chunks and 45 instance-major; at 65,536 x 256 all three ~39-40 us)
+    const uint64_t inst = blockIdx.x, chunk = blockIdx.y;
     const int tid = threadIdx.x;
     uint64_t* B = a.balance + inst * a.nval;
     const uint64_t base = chunk * kValPerBlock;
@@ -460,7 +511,7 @@ __device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
       q[j] = *reinterpret_cast<const uint4*>(B + (p < a.nval ? p : 0));
     }
     const uint64_t* sc = scal_ro + inst * kScal;
-    const uint64_t pop = sc[kPop], nact = sc[kNact];
+    const uint64_t pop = sc[kPop], nact = a.nval_global - sc[kNoMatch];
     const uint64_t dep = pop * PZ_DEFAULT_BALANCE;
     const bool thr = (dep * 3ull) >= (tdep_ro[inst] * 2ull);  // uint64 wrap, incentives.go:18-20
     // Go panics in processCrosslinks or CalculateRewards: leave balances untouched.  A
@@ -530,16 +581,20 @@ __device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
     uint64_t s = block_reduce<false>(sum, sh);
     if (tid == 0) {
       if (s && !skip) atomicAdd((unsigned long long*)&a.scal[inst * kScal + kNextBal], (unsigned long long)s);
-      if (chunk == 0) a.scal[inst * kScal + kApplied] = applied ? 1 : 0;
+      if (chunk == 0) {
+        a.scal[inst * kScal + kApplied] = applied ? 1 : 0;
+        a.scal[inst * kScal + kNact] = nact;
+      }
     }
     if (a.scal_next && chunk == 0 && tid < kScal) a.scal_next[inst * kScal + tid] = 0;
     return;
   }
-  const uint64_t inst = blockIdx.y, chunk = blockIdx.x;
+  const uint64_t inst = blockIdx.x, chunk = blockIdx.y;
   const int tid = threadIdx.x;
   const uint64_t* sc = a.scal + inst * kScal;
-  const uint64_t pop = sc[kPop], nact = sc[kNact];
+  const uint64_t pop = sc[kPop], nact = a.nval_global - sc[kNoMatch];
   const bool xl_err = sc[kErrXl] != 0;
+  if (chunk == 0 && tid == 0) a.scal[inst * kScal + kNact] = nact;
   const uint64_t dep = pop * PZ_DEFAULT_BALANCE;                 // GetAttestersTotalDeposit
   const bool applied = (dep * 3ull) >= (a.total_deposit[inst] * 2ull);  // uint64 wrap
   const bool rwd_err = applied && nact > 0 && sc[kErrRwd] != 0;
@@ -595,7 +650,7 @@ hipError_t launch_epoch_reward_mode(const EpochArgs& a, int mode, hipStream_t s)
   const int vec = ((a.nval % 2 == 0) && !((reinterpret_cast<uintptr_t>(a.balance) |
                                            reinterpret_cast<uintptr_t>(a.start) |
                                            reinterpret_cast<uintptr_t>(a.end)) & 15)) ? 1 : 0;
-  const dim3 grid((uint32_t)vbpi, a.ninst);
+  const dim3 grid(a.ninst, (uint32_t)vbpi);
   if (mode == 1) hipLaunchKernelGGL(pz_epoch_reward_dbg1_kernel, grid, dim3(kThreads), 0, s, a, vbpi, vec, a.scal, a.boffs, a.total_deposit);
   else if (mode == 2) hipLaunchKernelGGL(pz_epoch_reward_dbg2_kernel, grid, dim3(kThreads), 0, s, a, vbpi, vec, a.scal, a.boffs, a.total_deposit);
   else if (mode == 3) hipLaunchKernelGGL(pz_epoch_reward_dbg3_kernel, grid, dim3(kThreads), 0, s, a, vbpi, vec, a.scal, a.boffs, a.total_deposit);
@@ -613,7 +668,8 @@ static bool vec_ok(const EpochArgs& a) {
 hipError_t launch_epoch_count(const EpochArgs& a, bool do_val, bool do_pop, bool do_xl, hipStream_t s) {
   CountGrid g;
   g.vbpi = vblocks_per_inst(a.nval);
-  g.nvb = do_val ? (uint64_t)a.ninst * g.vbpi : 0;
+  g.nvb = do_val ? (g_count_variant & 1 ? (g.vbpi + kGroup - 1) / kGroup * kGroup * a.ninst
+                                        : (uint64_t)a.ninst * g.vbpi) : 0;
   g.pbpi = (a.max_inst_bytes + kPopBytesPerBlock - 1) / kPopBytesPerBlock;
   // The popcount range also resets the crosslink winners (chunk 0 of each instance), so it
   // keeps one block per instance whenever winners will be computed -- even when no bitfield
@@ -630,7 +686,15 @@ hipError_t launch_epoch_count(const EpochArgs& a, bool do_val, bool do_pop, bool
   g.nxb = (do_xl && a.natt) ? xl_inst * g.xl_j : 0;
   const uint64_t blocks = g.nvb + g.npb + g.nxb;
   if (!blocks) return hipSuccess;
-  hipLaunchKernelGGL(pz_epoch_count_kernel, dim3((uint32_t)blocks), dim3(kThreads), 0, s, a, g);
+  const dim3 grid((uint32_t)blocks);
+  switch (g_count_variant) {
+    case 1: hipLaunchKernelGGL(pz_epoch_count_v1_kernel, grid, dim3(kThreads), 0, s, a, g); break;
+    case 2: hipLaunchKernelGGL(pz_epoch_count_v2_kernel, grid, dim3(kThreads), 0, s, a, g); break;
+    case 3: hipLaunchKernelGGL(pz_epoch_count_v3_kernel, grid, dim3(kThreads), 0, s, a, g); break;
+    case 4: hipLaunchKernelGGL(pz_epoch_count_v4_kernel, grid, dim3(kThreads), 0, s, a, g); break;
+    case 5: hipLaunchKernelGGL(pz_epoch_count_v5_kernel, grid, dim3(kThreads), 0, s, a, g); break;
+    default: hipLaunchKernelGGL(pz_epoch_count_kernel, grid, dim3(kThreads), 0, s, a, g);
+  }
   return hipGetLastError();
 }
 
@@ -655,7 +719,7 @@ hipError_t launch_epoch_reward(const EpochArgs& a, hipStream_t s) {
   const uint64_t vbpi = vblocks_per_inst(a.nval);
   const uint64_t blocks = (uint64_t)a.ninst * vbpi;
   if (!blocks) return hipSuccess;
-  hipLaunchKernelGGL(pz_epoch_reward_kernel, dim3((uint32_t)vbpi, a.ninst), dim3(kThreads), 0, s, a, vbpi,
+  hipLaunchKernelGGL(pz_epoch_reward_kernel, dim3(a.ninst, (uint32_t)vbpi), dim3(kThreads), 0, s, a, vbpi,
                      vec_ok(a) ? 1 : 0, a.scal, a.boffs, a.total_deposit);
   return hipGetLastError();
 }

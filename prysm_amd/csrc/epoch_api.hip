@@ -75,8 +75,8 @@ int pz_validator_indices(const uint64_t* start, const uint64_t* end, uint64_t n,
   uint64_t scal[kScal];
   st.down(scal, a.scal, kScal);
   if (st.sync()) return st.rc;
-  *count = scal[kNact];
-  st.down(out, a.act_list, scal[kNact]);
+  *count = n - scal[kNoMatch];  // pass 1 counts the validators that do not match
+  st.down(out, a.act_list, *count);
   return st.sync();
 }
 
@@ -417,7 +417,7 @@ int pz_rotate_validator_set(const uint64_t* balance, uint64_t* start, uint64_t* 
   st.down(sa, a.scal, kScal);
   st.down(sq, q.scal, kScal);
   if (st.sync()) return st.rc;
-  const uint64_t k = std::min<uint64_t>(sa[kNact] / 30 + 1, sq[kNact]);
+  const uint64_t k = std::min<uint64_t>((n - sa[kNoMatch]) / 30 + 1, n - sq[kNoMatch]);
   if (k) {
     hipLaunchKernelGGL(pz_rotate_induct_kernel, dim3((uint32_t)((k + 255) / 256)), dim3(256), 0, st.s, q.act_list, k,
                        d_start, dynasty);
@@ -481,7 +481,10 @@ extern "C" int pz_debug_epoch_count(const pz_epoch_batch* b, int do_val, int do_
 }
 namespace pz {
 hipError_t launch_epoch_reward_mode(const EpochArgs& a, int mode, hipStream_t s);
+int set_count_variant(int v);
 }
+// Internal: select the count-pass variant for in-process A/B timing (tools/epoch_parts.py).
+extern "C" int pz_debug_set_count_variant(int v) { return pz::set_count_variant(v); }
 extern "C" int pz_debug_epoch_reward_mode(const pz_epoch_batch* b, int mode, void* stream) {
   hipError_t e = pz::launch_epoch_reward_mode(*b, mode, (hipStream_t)stream);
   return e == hipSuccess ? PZ_OK : pz::hip_fail(e, "pz_epoch_reward_kernel (mode)");

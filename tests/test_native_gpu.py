@@ -139,3 +139,23 @@ print("ok")
 """ % (_lib.HERE.rsplit("/", 1)[0],)
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
     assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stderr[-2000:]
+
+
+def test_max_active_index_scalar():
+    """PZ_SCAL_MAXIDX1 (1 + the largest active index) with the maximum at a block edge, in
+    the last block, inside a block, and with no active validator."""
+    n = 10000
+    inst = _inst(n, 4, False)
+    d = 1
+    inst["start"][1, 2048:] = 7          # last active = 2047, the last validator of block 0
+    rng = np.random.default_rng(3)
+    inst["end"][2, rng.random(n) < 0.3] = 1
+    inst["end"][2, 9000:] = 1            # last active inside block 4
+    inst["start"][3, :] = 9              # nothing active
+    ne = NativeEpoch(inst, device=0)
+    ne.step()
+    _, scal, *_ = ne.results()
+    for b in range(4):
+        act = np.nonzero((inst["start"][b] <= d) & (d < inst["end"][b]))[0]
+        assert int(scal[b, _lib.SCAL_MAXIDX1]) == (int(act[-1]) + 1 if act.size else 0), b
+        assert int(scal[b, _lib.SCAL_NACT]) == act.size

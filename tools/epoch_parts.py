@@ -28,6 +28,10 @@ def main(nval=65536, ninst=256, rounds=5, reps=10):
         "count_pop": lambda: dll.pz_debug_epoch_count(bp, 0, 1, 0, sh),
         "count_xl": lambda: dll.pz_debug_epoch_count(bp, 0, 0, 1, sh),
         "count_all": lambda: dll.pz_debug_epoch_count(bp, 1, 1, 1, sh),
+        # same-process A/B of the count-pass variants (pz_debug_set_count_variant)
+        **{"count_val_v%d" % v: (lambda v=v: (dll.pz_debug_set_count_variant(v),
+                                              dll.pz_debug_epoch_count(bp, 1, 0, 0, sh),
+                                              dll.pz_debug_set_count_variant(0))) for v in range(6)},
         "reward": lambda: dll.pz_debug_epoch_reward(bp, sh),
         "reward_nobits": lambda: dll.pz_debug_epoch_reward_mode(bp, 1, sh),
         "reward_noreduce": lambda: dll.pz_debug_epoch_reward_mode(bp, 2, sh),
@@ -37,6 +41,23 @@ def main(nval=65536, ninst=256, rounds=5, reps=10):
         "torch_inplace_add": lambda: yard.add_(1),
     }
     yard = torch.empty(de.balance.numel(), dtype=torch.int64, device=dev)
+    # overlap probes: the crosslink gathers on a second stream beside the validator stream
+    s2 = torch.cuda.Stream(dev)
+    sh2 = ctypes.c_void_p(s2.cuda_stream)
+    ev_a, ev_b = torch.cuda.Event(), torch.cuda.Event()
+
+    def two_streams(fa, fb):
+        ev_a.record(s)
+        s2.wait_event(ev_a)
+        fa()
+        fb()
+        ev_b.record(s2)
+        s.wait_event(ev_b)
+
+    parts["xl_beside_val"] = lambda: two_streams(lambda: dll.pz_debug_epoch_count(bp, 1, 0, 0, sh),
+                                                 lambda: dll.pz_debug_epoch_count(bp, 0, 0, 1, sh2))
+    parts["xl_then_val_1stream"] = lambda: (dll.pz_debug_epoch_count(bp, 0, 0, 1, sh),
+                                            dll.pz_debug_epoch_count(bp, 1, 0, 0, sh))
     # The parts run on the batch's CURRENT buffers: after a step those are the next step's
     # (zeroed) scal, so pass 2 would see pop = nact = 0 (threshold not met, general path).
     # Every pass-2 timing therefore restores a snapshot of a real pass-1 result first; the
@@ -84,4 +105,5 @@ def main(nval=65536, ninst=256, rounds=5, reps=10):
 
 
 if __name__ == "__main__":
-    main()
+    a = [int(x) for x in sys.argv[1:]]
+    main(*a)
