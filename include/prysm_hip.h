@@ -79,6 +79,13 @@ int pz_blake2b512_batch(const uint8_t* msgs, const uint64_t* offsets, uint64_t n
  * the GPU.  Returns the previous value.  The pz_dev_* forms never leave the device. */
 uint64_t pz_set_serial_threshold(uint64_t bytes);
 
+/* A batch of at most `compressions` BLAKE2b compressions in all (a drop-in Hash() call: one
+ * 100-600 B message is 1-5) is hashed on the calling thread: the GPU route's launch, PCIe
+ * copies and stream sync cost tens of microseconds against ~1 us of host work (DESIGN.md §3,
+ * the measured crossover).  0 sends every batch to the GPU.  Returns the previous value.
+ * The library still refuses to run without a gfx950 device. */
+uint64_t pz_set_small_batch_threshold(uint64_t compressions);
+
 /* Device-resident forms (device pointers; caller's stream).  The CSR form requires 4
  * readable bytes past msgs[offsets[n]-1] (the library's own buffers are padded). */
 int pz_dev_blake2b512_batch(const uint8_t* d_msgs, const uint64_t* d_offsets, uint64_t n,

@@ -58,6 +58,7 @@ SIGNATURES = {
     "pz_version": [],
     "pz_blake2b512_batch": [vp, vp, u64, vp, u32],
     "pz_set_serial_threshold": [u64],
+    "pz_set_small_batch_threshold": [u64],
     "pz_dev_blake2b512_batch": [vp, vp, u64, vp, u32, vp],
     "pz_dev_blake2b512_fixed": [vp, u64, u64, u64, vp, u32, vp],
     "pz_validator_indices": [vp, vp, u64, u64, ctypes.c_int, vp, c_u64p],
@@ -174,7 +175,7 @@ SCAL_POP, SCAL_NACT, SCAL_ERR_XL, SCAL_ERR_RWD, SCAL_APPLIED, SCAL_NEXT_BAL, SCA
 SCAL_COUNT = 8
 KIND_ACTIVE, KIND_EXITED, KIND_QUEUED = 0, 1, 2
 _RESTYPES = {"pz_last_error": ctypes.c_char_p, "pz_chain_free": None, "pz_set_serial_threshold": u64,
-             "pz_shutdown": None, "pz_comm_free": None, "pz_epoch_state_free": None,
+             "pz_shutdown": None, "pz_set_small_batch_threshold": u64, "pz_comm_free": None, "pz_epoch_state_free": None,
              "pz_wire_validators_bound": u64, "pz_wire_scratch_bytes": u64,
              "pz_wire_attestations_bound": u64, "pz_wire_attestations_scratch_bytes": u64}
 SERIAL_DEFAULT = 65536        # the library's default serial threshold (bytes)
@@ -258,6 +259,24 @@ def set_serial_threshold(nbytes):
 
 def serial_threshold_default():
     return SERIAL_DEFAULT
+
+
+SMALL_BATCH_DEFAULT = 256  # compressions (serial_hash.h PZ_SMALL_BATCH_DEFAULT)
+
+
+class small_batch_threshold:
+    """Context manager: batches of at most ``compressions`` compressions are hashed on the
+    calling thread (0: every batch on the GPU)."""
+
+    def __init__(self, compressions):
+        self.c = compressions
+
+    def __enter__(self):
+        self.old = int(lib.dll.pz_set_small_batch_threshold(self.c))
+        return self
+
+    def __exit__(self, *exc):
+        lib.dll.pz_set_small_batch_threshold(self.old)
 
 
 class serial_threshold:

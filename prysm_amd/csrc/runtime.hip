@@ -200,6 +200,22 @@ int hash_batch_on(DeviceCtx* c, const uint8_t* msgs, const uint64_t* offsets, ui
   const uint64_t base = offsets[0], total = offsets[n] - offsets[0];
   int rc;
 
+  // A small batch (a drop-in Hash() call hashes ONE 100-600 B message, types/block.go:67-77)
+  // costs a few compressions, ~1 us on one host core, against tens of microseconds of launch,
+  // PCIe copies and stream sync on the GPU route: below the measured crossover it is hashed
+  // on the calling thread (profiles/r02/hash_latency*.json).
+  if (n <= small_batch_threshold()) {
+    uint64_t comps = 0;
+    for (uint64_t i = 0; i < n && comps <= small_batch_threshold(); ++i)
+      comps += (offsets[i + 1] - offsets[i] + 127) / 128 + (offsets[i + 1] == offsets[i]);
+    if (comps <= small_batch_threshold()) {
+      std::vector<uint64_t> all(n);
+      for (uint64_t i = 0; i < n; ++i) all[i] = i;
+      host_blake2b512_many(msgs, offsets, all, out, out_bytes, 1);
+      return PZ_OK;
+    }
+  }
+
   // Long messages (serial chains) go to host threads while the GPU hashes the rest.
   std::vector<uint64_t> lng = long_messages(offsets, n);
   if (!lng.empty()) {
@@ -320,6 +336,7 @@ int pz_comm_blake2b512_batch(const pz_comm* comm, const uint8_t* msgs, const uin
 }
 
 uint64_t pz_set_serial_threshold(uint64_t bytes) { return set_serial_threshold(bytes); }
+uint64_t pz_set_small_batch_threshold(uint64_t compressions) { return set_small_batch_threshold(compressions); }
 
 }  // extern "C"
 

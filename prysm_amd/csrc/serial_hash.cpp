@@ -129,6 +129,7 @@ using CompressFn = void (*)(uint64_t*, const uint64_t*, uint64_t, bool);
 CompressFn pick() { return __builtin_cpu_supports("avx2") ? compress_avx2 : compress_scalar; }
 
 std::atomic<uint64_t> g_threshold{64 * 1024};
+std::atomic<uint64_t> g_small{PZ_SMALL_BATCH_DEFAULT};
 
 }  // namespace
 
@@ -171,6 +172,8 @@ void host_blake2b512_many(const uint8_t* data, const uint64_t* offsets, const st
 }
 
 uint64_t serial_threshold() { return g_threshold.load(); }
+uint64_t small_batch_threshold() { return g_small.load(); }
+uint64_t set_small_batch_threshold(uint64_t c) { return g_small.exchange(c); }
 uint64_t set_serial_threshold(uint64_t bytes) { return g_threshold.exchange(bytes); }
 
 }  // namespace pz

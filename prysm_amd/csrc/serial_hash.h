@@ -13,6 +13,9 @@
 #include <cstdint>
 #include <vector>
 
+// Default small-batch threshold in compressions (measured crossover).
+#define PZ_SMALL_BATCH_DEFAULT 256
+
 namespace pz {
 
 // Full BLAKE2b-512 (RFC 7693, unkeyed, 64-byte digest) of msg[0..len).
@@ -27,6 +30,11 @@ void host_blake2b512_many(const uint8_t* data, const uint64_t* offsets, const st
 // UINT64_MAX keeps every message on the GPU.
 uint64_t serial_threshold();
 uint64_t set_serial_threshold(uint64_t bytes);
+
+// Batches of at most this many compressions in all are hashed on the calling thread (the
+// drop-in Hash() latency path); 0 sends every batch to the GPU.
+uint64_t small_batch_threshold();
+uint64_t set_small_batch_threshold(uint64_t compressions);
 
 // Indices of the messages of a CSR batch that go to the host (length >= threshold).
 std::vector<uint64_t> long_messages(const uint64_t* offsets, uint64_t n);

@@ -8,6 +8,25 @@ from prysm_amd import _lib
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _gpu_route():
+    """These tests pin the GPU kernels: every batch, however small, goes to the device."""
+    with _lib.small_batch_threshold(0):
+        yield
+
+
+def test_small_batch_host_route_matches_oracle():
+    """Drop-in Hash() calls (one message, types/block.go:67-77) below the small-batch
+    threshold are hashed on the calling thread; same digests as the oracle, at every block
+    boundary, and a batch just above the threshold takes the GPU route with the same result."""
+    with _lib.small_batch_threshold(_lib.SMALL_BATCH_DEFAULT):
+        for n in list(range(0, 600)) + [8191, 8192]:
+            m = bytes((i * 31 + n) & 0xFF for i in range(n))
+            assert _lib.blake2b512_batch([m], 64)[0] == ref.sum512(m), n
+        msgs = [bytes([k]) * 512 for k in range(65)]  # 65 x 4 compressions > 256: the GPU route
+        assert _lib.blake2b512_batch(msgs, 32) == [ref.sum512(m)[:32] for m in msgs]
+
+
 def test_rfc7693_abc_gpu():
     d = _lib.blake2b512_batch([b"abc"], out_bytes=64)[0]
     assert d == ref.sum512(b"abc")
