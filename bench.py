@@ -648,6 +648,58 @@ def replay_leg(args, torch, dist, dev, rank, world):
     return out
 
 
+def shuffle_leg(args):
+    """utils.ShuffleIndices at configs[3]'s 1,048,576 validators
+    (host by design: a sequential swap chain, shuffle.go:14-33), and the whole
+    ShuffleValidatorsToCommittees (sharding.go:11-53: the device active filter, the swap chain,
+    splitBySlotShard into the committee CSR), which updateHead runs on every head
+    (blockchain/service.go:185-190).  Parity: the permutation against the C restatement."""
+    from oracle import cport
+    from prysm_amd import casper
+
+    n = 1 << 20
+    seed = b"A" + bytes(31)
+    base = np.arange(n, dtype=np.uint32)
+    ts = []
+    for _ in range(max(3, min(args.steps, 20))):
+        lst = base.copy()
+        t0 = time.perf_counter()
+        got = casper.shuffle_indices(seed, lst)  # in place, like the Go function
+        ts.append(time.perf_counter() - t0)
+    ms = float(np.median(ts)) * 1e3
+    start = np.zeros(n, dtype=np.uint64)
+    end = np.full(n, 9999999999999999999, dtype=np.uint64)
+    comm = casper.shuffle_validators_to_committees(seed, start, end, 1, 0)
+    # the C-ABI call alone, into preallocated CSR buffers
+    from prysm_amd import _lib
+    cap = 64 * (n // (64 * 128 * 2) + 1)
+    seed_a = np.frombuffer(seed, dtype=np.uint8).copy()
+    members, coffs = np.empty(n, np.uint32), np.empty(cap + 1, np.uint64)
+    shard, slot_offs, nc = np.empty(cap, np.uint64), np.empty(65, np.uint64), ctypes.c_uint64(0)
+    tc = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        _lib.lib.call("pz_shuffle_validators_to_committees", _lib.ptr(seed_a), _lib.ptr(start), _lib.ptr(end), n,
+                      1, 0, _lib.ptr(members), _lib.ptr(coffs), _lib.ptr(shard), _lib.ptr(slot_offs), cap,
+                      ctypes.byref(nc))
+        tc.append(time.perf_counter() - t0)
+    out = {"metric": "ShuffleIndices on 1,048,576 validators", "ms_per_call": ms,
+           "value": n / (ms * 1e-3), "unit": "validators/s",
+           "committees_ms_per_call": float(np.median(tc)) * 1e3,
+           "committees": "%d slots x %d committees" % (len(comm), len(comm[0])),
+           "path": "host swap chain without division (sw < 256 <= n - i: the swap targets are the fixed "
+                   "offsets i + sw[k]); seed stream BLAKE2b on the calling thread (small batch)",
+           "parity": "permutation equal to the C restatement (oracle/c/shuffle_ref.c): %s"
+                     % bool(np.array_equal(got, cport.shuffle_indices(seed, base)))}
+    if not args.no_cpu_baseline:
+        reps, dt = cport.shuffle_timed(seed, n, min_seconds=CPU_SAMPLE_S / 4)
+        out["cpu_baseline"] = {"value": reps * n / dt, "unit": "validators/s", "cores": 1, "kind": "port",
+                               "ms_per_call": dt / reps * 1e3,
+                               "sample": "%d ShuffleIndices calls on 1,048,576 indices (shuffle.go's modulo per swap, "
+                                         "1 thread, oracle/c/shuffle_ref.c), %.2f s" % (reps, dt)}
+    return out
+
+
 PMC_SUMMARY = os.path.join("profiles", "r01", "pmc_summary.json")
 PMC_SUMMARY_EPOCH_1M = os.path.join("profiles", "r01", "pmc_summary_epoch1m.json")
 
@@ -787,6 +839,7 @@ def main():
     wire_out = None if args.no_wire else wire_leg(args, torch, dist, dev, rank, world)
     att_out = None if args.no_attcheck else attcheck_leg(args, torch, dist, dev, rank, world)
     watt_out = None if args.no_wire else wire_att_leg(args, torch, dist, dev, rank, world, d_out)
+    shuf = shuffle_leg(args) if (rank == 0 and not args.no_epoch) else None
 
     if rank == 0:
         total = n * world * args.steps
@@ -852,6 +905,8 @@ def main():
             line["attcheck"] = att_out
         if watt_out is not None:
             line["wire_att"] = watt_out
+        if shuf is not None:
+            line["shuffle"] = shuf
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -207,7 +207,9 @@ int pz_process_crosslinks(const uint32_t* committee, const uint64_t* coffs, uint
                           uint64_t* vote_out, uint64_t* total_out);
 
 /* utils/shuffle.go:14-33 ShuffleIndices, in place.  Host-resident by design (a sequential
- * swap chain); only the 64-byte seed stream blake2b.Sum512(seed) is computed on the GPU. */
+ * swap chain, north_star); the 64-byte seed stream blake2b.Sum512(seed) goes through the batch
+ * hash API (one compression: the small-batch route).  While n - i > 255 every swap target is
+ * i + a fixed byte offset, so the chain runs division-free in a 256-entry window. */
 int pz_shuffle_indices(const uint8_t seed[32], uint32_t* list, uint64_t n);
 
 /* casper/validator.go:17-41 RotateValidatorSet, in place on start/end: active validators

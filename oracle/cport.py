@@ -225,3 +225,26 @@ class WireAtt:
 
     def close(self):
         self.d.oracle_wire_att_free(self.h)
+
+
+def shuffle_indices(seed32, values):
+    """utils.ShuffleIndices (shuffle.go:14-33) through the C restatement; returns a new uint32
+    array (the Go function shuffles in place and returns the slice)."""
+    d = dll()
+    d.oracle_shuffle_indices.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint64]
+    out = np.ascontiguousarray(values, dtype=np.uint32).copy()
+    rc = d.oracle_shuffle_indices(bytes(seed32), out.ctypes.data if out.size else None, out.size)
+    if rc:
+        raise ValueError("Validator count has exceeded MaxValidator Count")
+    return out
+
+
+def shuffle_timed(seed32, n, min_seconds=2.0):
+    """(reps, seconds) of the C restatement over 0..n-1 (the cpu_baseline of the shuffle leg)."""
+    import time
+    base = np.arange(n, dtype=np.uint32)
+    reps, t0 = 0, time.perf_counter()
+    while reps == 0 or time.perf_counter() - t0 < min_seconds:
+        shuffle_indices(seed32, base)
+        reps += 1
+    return reps, time.perf_counter() - t0

@@ -70,8 +70,9 @@ def calculate_rewards(balance, start, end, dynasty, total_deposit, bits, boffs):
 
 
 def shuffle_indices(seed32, validator_list):
-    """utils/shuffle.go:14-33 (host swap chain; seed stream hashed on the GPU).  In place on a
-    uint32 array; returns it."""
+    """utils/shuffle.go:14-33 through pz_shuffle_indices (host swap chain; the 32-byte seed's
+    BLAKE2b is a small batch, hashed on the calling thread).  In place on a uint32 array;
+    returns it."""
     lst = validator_list if isinstance(validator_list, np.ndarray) else np.array(validator_list, dtype=np.uint32)
     assert lst.dtype == np.uint32 and lst.flags["C_CONTIGUOUS"]
     seed = np.frombuffer(bytes(seed32).ljust(32, b"\0")[:32], dtype=np.uint8).copy()

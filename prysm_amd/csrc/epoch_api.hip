@@ -367,7 +367,28 @@ int pz_shuffle_indices(const uint8_t seed[32], uint32_t* list, uint64_t n) {
   if (rc) return rc;
   uint32_t sw[21];  // utils/shuffle.go:25-26: byte-wrapped sum of 3 seed bytes, j = 0,3,..,60
   for (int j = 0, k = 0; j + 3 < 64; j += 3, ++k) sw[k] = (uint8_t)(hs[j] + hs[j + 1] + hs[j + 2]);
-  for (uint64_t i = 0; i + 1 < n; ++i) {
+  // utils/shuffle.go:28-31: swap(i, sw[k] % (n - i) + i) for k = 0..20, i = 0..n-2.  Every
+  // sw[k] is a byte, so while n - i > 255 the modulo is the identity and the targets are the
+  // fixed offsets i + sw[k]: the 21 swaps of step i touch only the 256-entry window at i (L1
+  // resident, no division).  Only the last 255 steps need the modulo.
+  // (An offset of 0 swaps list[i] with itself: a no-op, dropped from the list.)
+  uint32_t off[21];
+  int noff = 0;
+  for (int k = 0; k < 21; ++k)
+    if (sw[k]) off[noff++] = sw[k];
+  const uint64_t fast = n > 256 ? n - 256 : 0;
+  uint32_t* L = list;
+  for (uint64_t i = 0; i < fast; ++i) {
+    uint32_t vi = L[i];  // list[i] stays in a register across its swaps
+    for (int k = 0; k < noff; ++k) {
+      uint32_t* q = L + i + off[k];
+      const uint32_t t = *q;
+      *q = vi;
+      vi = t;
+    }
+    L[i] = vi;
+  }
+  for (uint64_t i = fast; i + 1 < n; ++i) {
     const uint64_t rem = n - i;
     for (int k = 0; k < 21; ++k) {
       const uint64_t p = sw[k] % rem + i;

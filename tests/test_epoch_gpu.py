@@ -187,14 +187,17 @@ def test_calculate_rewards_panics_map_to_eindex():
 
 
 # ---- shuffle ------------------------------------------------------------------------------
-@pytest.mark.parametrize("n", [0, 1, 2, 20, 100, 1000, 1024, 65536])
+@pytest.mark.parametrize("n", [0, 1, 2, 20, 100, 256, 257, 258, 1000, 1024, 20000, 65536, 1 << 20])
 def test_shuffle_bit_exact(n):
+    """utils/shuffle.go:14-33 at every size up to configs[3]'s 1,048,576: the scalar oracle
+    (n <= 1024) and the C restatement (any n).  Hash{} (the genesis seed) has a zero swap
+    number (a self-swap), which the division-free window path must skip."""
+    from oracle import cport
     for seed in (ref.bytes_to_hash(b"A"), ref.bytes_to_hash(b""), bytes(range(32))):
         got = casper.shuffle_indices(seed, np.arange(n, dtype=np.uint32))
-        want = ref.shuffle_indices(seed, list(range(n))) if n <= 1024 else None
-        if want is not None:
-            assert got.tolist() == want
-        assert sorted(got.tolist()) == list(range(n))
+        if n <= 1024:
+            assert got.tolist() == ref.shuffle_indices(seed, list(range(n)))
+        np.testing.assert_array_equal(got, cport.shuffle_indices(seed, np.arange(n, dtype=np.uint32)))
 
 
 def test_shuffle_max_validators():

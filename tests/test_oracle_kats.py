@@ -245,3 +245,12 @@ def test_process_crosslinks_shard_index_short_circuit(bitfield, panics):
             onp.crosslink_winners(vote, total, np.array([0], np.uint32), np.zeros(0, np.uint64), 5)
     else:
         assert onp.crosslink_winners(vote, total, np.array([0], np.uint32), np.zeros(0, np.uint64), 5).size == 0
+
+
+def test_c_shuffle_restatement_matches_scalar_oracle():
+    # utils/shuffle.go:14-33: the C restatement (the large-n checker and CPU baseline) against
+    # the scalar oracle, including the genesis seed Hash{} whose swap numbers contain a 0
+    from oracle import cport
+    for n in (0, 1, 2, 20, 255, 256, 257, 1000):
+        for seed in (ref.bytes_to_hash(b"A"), ref.bytes_to_hash(b""), bytes(range(32))):
+            assert cport.shuffle_indices(seed, np.arange(n)).tolist() == ref.shuffle_indices(seed, list(range(n)))
