@@ -57,6 +57,20 @@ def warm_clocks(step, torch, dev, ms):
         torch.cuda.synchronize(dev)
 
 
+def host_info():
+    """The host the CPU baselines ran on (print nproc and the CPU model)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), model)
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return {"nproc": os.cpu_count(), "affinity": aff, "model": model,
+            "threads_all_cores": max(1, min(16, aff)),
+            "note": "all-cores lines use min(16, affinity) threads: the CPU share of one GPU on the bench boxes"}
+
+
 def max_over_ranks(x, torch, dist, dev):
     """MAX of a host float over the ranks (a device tensor for RCCL, a host one for gloo)."""
     on_dev = dist.get_backend() == "nccl"
@@ -77,8 +91,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="collective backend at N > 1 (gloo: rehearsal with ranks sharing a GPU)")
-    p.add_argument("--cpu-replay-blocks", type=int, default=520,
-                   help="blocks of the replay chain the CPU baseline (oracle/replay.py) processes (~8 s)")
+    p.add_argument("--cpu-replay-blocks", type=int, default=1040,
+                   help="blocks of the replay chain the CPU baseline (oracle/c/replay_ref.c) processes (~6 s)")
     p.add_argument("--no-epoch", action="store_true")
     p.add_argument("--epoch-path", default="native", choices=["native", "torch"],
                    help="native: pz_epoch_state (C ABI, the library's RCCL communicator); torch: DeviceEpoch "
@@ -257,9 +271,15 @@ def epoch_cpu_baseline(inst):
     try:
         from oracle import cport
         reps, dt = cport.epoch_instance_timed(inst, 0, min_seconds=CPU_SAMPLE_S)
+        host = cport.host_info()
+        T = host["threads_all_cores"]
+        ra, da = cport.epoch_all_cores_timed(inst, T, CPU_SAMPLE_S / 2)
         return {"value": reps * inst["nval"] / dt, "unit": "validator-epochs/s", "cores": 1, "kind": "port",
                 "sample": "%d x one %d-validator epoch instance (AoS records, 1 thread, oracle/c/epoch_ref.c), "
-                          "%.2f s" % (reps, inst["nval"], dt)}
+                          "%.2f s" % (reps, inst["nval"], dt),
+                "all_cores": {"value": ra * inst["nval"] / da, "cores": T,
+                              "sample": "%d transitions of %d independent %d-validator instances, one per thread, "
+                                        "%.2f s" % (ra, T, inst["nval"], da)}}
     except Exception as e:  # pragma: no cover
         return {"value": None, "unit": "validator-epochs/s", "cores": 0, "kind": "port",
                 "sample": "unavailable: %s" % e}
@@ -612,24 +632,39 @@ def replay_leg(args, torch, dist, dev, rank, world):
            "config": {"workload": "sync replay: block + 5 x (attestation Hash, Key, message digest) + vote "
                                   "tally per block, stateRecalc every 64 blocks (BASELINE configs[4])",
                       "validators": nval, "blocks_per_gpu": nb, "attestations_per_block": 5,
-                      "parallelism": "independent chain per GPU x%d" % world},
+                      "parallelism": "%d independent chain(s), one per GPU (replicas; not one batch-sharded "
+                                     "chain: DESIGN.md §6)" % world},
            "input": "serialized canonical BeaconBlock encodings, %.1f MB" % (int(offs[-1]) / 1e6),
            "processed": sum(r["status"] == "processed" for r in recs),
            "transitions": sum(r["transition"] for r in recs),
            "state_roots": state_roots}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        try:
-            from oracle import replay as oreplay
-            sample = blocks[:args.cpu_replay_blocks]
+    if rank == 0 and world == 1:
+        # the checker: the whole timed chain through the C restatement of the block pipeline
+        # (checker mode), compared with the GPU engine's records and roots
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from replay_port_helpers import mismatches, port_replay
+        t1 = time.perf_counter()
+        p_out, p_roots = port_replay(data, offs, nval, len(ar))
+        bad = mismatches(br, ar, root_vals["host_serial"], p_out, p_roots)
+        out["parity"] = ("all %d blocks and %d attestations (digests, statuses, transitions), the 4 state roots and "
+                         "%d vote-cache totals vs the C restatement of blockProcessing (oracle/c/replay_ref.c), "
+                         "%.1f s: %s" % (nb, len(ar), len(p_roots["vote_totals"]), time.perf_counter() - t1,
+                                         "bit-exact" if not bad else "MISMATCH " + ", ".join(bad)))
+        if not args.no_cpu_baseline:
+            from oracle import cport
+            sd, so = serialize_blocks(blocks[:args.cpu_replay_blocks])
+            nsa = sum(len(b.attestations) for b in blocks[:args.cpu_replay_blocks])
+            r = cport.Replay(nval)  # Go's algorithms: linear scan of VoterIndices (core.go:333-337)
             t0 = time.perf_counter()
-            oreplay.replay(sample, nval)
+            r.process(sd, so, nsa)
             dt = time.perf_counter() - t0
-            out["cpu_baseline"] = {"value": len(sample) / dt, "unit": "blocks/s", "cores": 1, "kind": "port",
-                                   "sample": "first %d blocks of the same chain through oracle/replay.py (scalar "
-                                             "restatement of blockProcessing, 1 thread), %.2f s" % (len(sample), dt)}
-        except Exception as e:  # pragma: no cover
-            out["cpu_baseline"] = {"value": None, "unit": "blocks/s", "cores": 0, "kind": "port",
-                                   "sample": "unavailable: %s" % e}
+            r.close()
+            out["cpu_baseline"] = {"value": (len(so) - 1) / dt, "unit": "blocks/s", "cores": 1,
+                                   "kind": "port",
+                                   "sample": "first %d blocks of the same serialized chain through the C restatement of "
+                                             "blockProcessing (oracle/c/replay_ref.c: decode, Marshal + BLAKE2b, "
+                                             "processAttestation, the vote cache with Go's O(k^2) voter scan, "
+                                             "stateRecalc over heap records), 1 thread, %.2f s" % (len(so) - 1, dt)}
     # configs[0]: the golden 1,024-validator chain (parity of the final roots on this box)
     with open(os.path.join(ROOT, "tests", "golden", "replay_n1024.json")) as f:
         g = json.load(f)
@@ -757,9 +792,13 @@ def cpu_baseline(records_np):
         cport.hash_fixed(records_np, 512, 32)
         passes += 1
     dt = time.perf_counter() - t0
+    T = cport.host_info()["threads_all_cores"]
+    na, da = cport.hash_all_cores_timed(records_np, 512, T, CPU_SAMPLE_S / 2)
     return {"value": passes * n / dt, "unit": "hashes/s", "cores": 1, "kind": "port",
             "sample": "%d pass(es) over the %d x 512-B records of the per-GPU batch, 1 thread, portable C "
-                      "BLAKE2b (oracle/c/blake2b_ref.c), %.2f s" % (passes, n, dt)}, digests
+                      "BLAKE2b (oracle/c/blake2b_ref.c), %.2f s" % (passes, n, dt),
+            "all_cores": {"value": na / da, "cores": T,
+                          "sample": "the same records split over %d threads, %.2f s" % (T, da)}}, digests
 
 
 def main():
@@ -884,6 +923,7 @@ def main():
         }
         if world == 1:
             line["host_api"] = host_api_rate(recs)
+        line["host"] = host_info()
         if world == 1 and not args.no_cpu_baseline:
             cb, digests = cpu_baseline(recs)
             line["cpu_baseline"] = cb

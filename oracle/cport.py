@@ -248,3 +248,145 @@ def shuffle_timed(seed32, n, min_seconds=2.0):
         shuffle_indices(seed32, base)
         reps += 1
     return reps, time.perf_counter() - t0
+
+
+def host_info():
+    """The host the CPU baselines ran on: its logical CPUs, this process's affinity, the model,
+    and the threads the all-cores lines use (capped at 16, the CPU share of one GPU on the
+    benchmark boxes)."""
+    import platform
+    model = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return {"nproc": os.cpu_count(), "affinity": aff, "model": model, "threads_all_cores": max(1, min(16, aff))}
+
+
+def parallel_timed(workers, min_seconds):
+    """Run every zero-argument callable of ``workers`` in its own thread (each one a C call
+    that releases the GIL), repeatedly, for ``min_seconds`` -> (total calls, seconds)."""
+    import threading
+    import time
+    counts = [0] * len(workers)
+    stop = threading.Event()
+
+    def loop(i):
+        while not stop.is_set() or counts[i] == 0:
+            workers[i]()
+            counts[i] += 1
+
+    ts = [threading.Thread(target=loop, args=(i,)) for i in range(len(workers))]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    time.sleep(min_seconds)
+    stop.set()
+    for t in ts:
+        t.join()
+    return sum(counts), time.perf_counter() - t0
+
+
+def epoch_all_cores_timed(inst, threads, min_seconds):
+    """One AoS epoch instance per thread (instances 0..threads-1), transitions timed
+    together -> (transitions, seconds)."""
+    built = [_build_epoch(inst, b % inst["ninst"]) for b in range(threads)]
+    try:
+        return parallel_timed([lambda d=d, e=e: d.oracle_epoch_run(e, 0) for d, e in built], min_seconds)
+    finally:
+        for d, e in built:
+            d.oracle_epoch_free(e)
+
+
+def hash_all_cores_timed(records, length, threads, min_seconds):
+    """The records split into ``threads`` slices, one hashing thread each -> (records hashed,
+    seconds)."""
+    records = np.ascontiguousarray(records, dtype=np.uint8)
+    n, stride = records.shape
+    cuts = [n * k // threads for k in range(threads + 1)]
+    outs = [np.empty((cuts[k + 1] - cuts[k], 32), dtype=np.uint8) for k in range(threads)]
+    d = dll()
+
+    def work(k):
+        m = cuts[k + 1] - cuts[k]
+        d.oracle_blake2b512_fixed(records[cuts[k]:].ctypes.data, stride, length, m, outs[k].ctypes.data, 32)
+
+    calls, dt = parallel_timed([lambda k=k: work(k) for k in range(threads)], min_seconds)
+    return calls * n // threads, dt
+
+
+class Replay:
+    """oracle/c/replay_ref.c: the C restatement of blockProcessing over a genesis chain."""
+
+    def __init__(self, nval, bitmap_dedup=False):
+        """``bitmap_dedup``: the checker mode (a voter bitmap per hash instead of Go's linear
+        scan of VoterIndices; the same sets, so the same results, in linear time)."""
+        d = dll()
+        if not getattr(d, "_replay_sig", False):
+            vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+            d.oracle_replay_new.restype = vp
+            d.oracle_replay_new.argtypes = [u64, ctypes.c_int]
+            d.oracle_replay_blocks.argtypes = [vp, vp, vp, u64, vp, vp, vp, vp, vp, vp, vp, vp, u64, vp]
+            d.oracle_replay_roots.argtypes = [vp, vp, vp]
+            d.oracle_replay_vote_totals.restype = u64
+            d.oracle_replay_vote_totals.argtypes = [vp, vp, vp, u64]
+            d.oracle_replay_free.argtypes = [vp]
+            d._replay_sig = True
+        self.d = d
+        self.h = d.oracle_replay_new(nval, 1 if bitmap_dedup else 0)
+
+    def process(self, data, offs, natt_total):
+        """Serialized blocks (CSR) -> dict of numpy arrays (block hash/status/transition, per
+        attestation status/key/hash/msg/msg_len).  Raises ``OraclePanic`` where Go panics."""
+        n = len(offs) - 1
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        r = dict(hash=np.zeros((n, 32), np.uint8), status=np.zeros(n, np.int32), transition=np.zeros(n, np.int32),
+                 att_status=np.zeros(natt_total, np.int32), key=np.zeros((natt_total, 32), np.uint8),
+                 att_hash=np.zeros((natt_total, 32), np.uint8), msg=np.zeros((natt_total, 64), np.uint8),
+                 msg_len=np.zeros(natt_total, np.uint32))
+        at = ctypes.c_uint64(0)
+        rc = self.d.oracle_replay_blocks(self.h, data.ctypes.data, offs.ctypes.data, n, r["hash"].ctypes.data,
+                                         r["status"].ctypes.data, r["transition"].ctypes.data,
+                                         r["att_status"].ctypes.data, r["key"].ctypes.data, r["att_hash"].ctypes.data,
+                                         r["msg"].ctypes.data, r["msg_len"].ctypes.data, natt_total, ctypes.byref(at))
+        if rc == -2:
+            raise OraclePanic("Go panic at block %d" % at.value)
+        if rc:
+            raise ValueError("undecodable block batch (rc %d)" % rc)
+        return r
+
+    def roots(self):
+        out = np.zeros(128, np.uint8)
+        hc = ctypes.c_int(0)
+        self.d.oracle_replay_roots(self.h, out.ctypes.data, ctypes.byref(hc))
+        b = out.tobytes()
+        r = {"chain_active": b[:32], "chain_crystallized": b[32:64]}
+        if hc.value:
+            r["cand_active"], r["cand_crystallized"] = b[64:96], b[96:128]
+        n = self.d.oracle_replay_vote_totals(self.h, None, None, 0)
+        hs = np.zeros((max(n, 1), 32), np.uint8)
+        ts = np.zeros(max(n, 1), np.uint64)
+        self.d.oracle_replay_vote_totals(self.h, hs.ctypes.data, ts.ctypes.data, n)
+        r["vote_totals"] = {hs[i].tobytes(): int(ts[i]) for i in range(n)}
+        return r
+
+    def close(self):
+        if self.h:
+            self.d.oracle_replay_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover
+            pass
+
+
+class OraclePanic(RuntimeError):
+    pass

@@ -253,3 +253,22 @@ def test_gpu_replay_empty_committees_vs_oracle(nval):
     assert sum(r["transition"] for r in recs) == 2
     for k in ("chain_active", "chain_crystallized", "cand_active", "cand_crystallized"):
         assert roots[k] == o_roots[k], k
+
+
+@pytest.mark.gpu
+def test_gpu_replay_configs4_full_chain_vs_c_port():
+    """BASELINE configs[4] at full size: the 10,000-block, 156-transition chain of the bench
+    (65,536 validators, seed 6) through the GPU engine and through the C restatement of the
+    block pipeline (oracle/c/replay_ref.c, checker mode): every block digest, status and
+    transition, every attestation status class, Key, Hash and message digest, the four state
+    roots and every vote-cache total."""
+    from prysm_amd.blockchain import BeaconChain, serialize_blocks
+    from replay_port_helpers import mismatches, port_replay
+    nval = 65536
+    blocks = synth.chain_blocks(nval, 10000, seed=6)
+    data, offs = serialize_blocks(blocks)
+    ch = BeaconChain(nval)
+    br, ar = ch.process_serialized(data, offs)
+    assert int(br["transition"].sum()) == 156
+    out, port_roots = port_replay(data, offs, nval, len(ar))
+    assert mismatches(br, ar, ch.roots(), out, port_roots) == []
