@@ -493,6 +493,14 @@ typedef struct pz_att_result {
 
 typedef struct pz_chain pz_chain;
 int  pz_chain_new(uint64_t nval, int device, pz_chain** out);
+/* NewBeaconChain over a database that holds a CrystallizedState (blockchain/core.go:86-95):
+ * the chain resumes from the stored encoding `cstate` (the bytes pz_chain_state_bytes returns
+ * for the chain's CrystallizedState, which updateHead persists, core.go:170-177) with the
+ * genesis ActiveState, exactly as the reference reloads; `saved_hashes` (32 bytes each) are
+ * the block hashes the database holds (hasBlock, core.go:591-601), so their children are
+ * processed.  PZ_EINVAL when the bytes do not decode (proto.Unmarshal's error). */
+int  pz_chain_new_from_state(const uint8_t* cstate, uint64_t len, const uint8_t* saved_hashes, uint64_t nsaved,
+                             int device, pz_chain** out);
 void pz_chain_free(pz_chain* chain);
 /* Number of attestations in a batch of serialized blocks (host only; sizes att_out). */
 int  pz_count_attestations(const uint8_t* blocks, const uint64_t* offsets, uint64_t n, uint64_t* count);

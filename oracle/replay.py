@@ -68,6 +68,23 @@ class Chain:
         self.candidate = None                   # (block, ActiveState, CrystallizedState)
         self.genesis = ref.new_genesis_block()
 
+    @classmethod
+    def reload(cls, crystallized_bytes, saved):
+        """NewBeaconChain with a stored CrystallizedState (blockchain/core.go:59-64,86-95): the
+        state is proto.Unmarshal'ed from the database, the ActiveState is the genesis one
+        (types/state.go:46-57, an empty vote-cache map), and hasBlock answers from the
+        database's saved blocks."""
+        self = cls.__new__(cls)
+        active, _ = ref.new_genesis_states(1)
+        cs = pb.CrystallizedState()
+        cs.ParseFromString(bytes(crystallized_bytes))
+        self.A = _Active(active, {})
+        self.C = cs
+        self.saved = set(bytes(h) for h in saved)
+        self.candidate = None
+        self.genesis = ref.new_genesis_block()
+        return self
+
     def update_head(self):
         """service.go:170-227: the candidate's states become the chain's states."""
         _, self.A, self.C = self.candidate
@@ -145,6 +162,14 @@ class Chain:
             out["cand_active"] = ref.marshal(A.data)
             out["cand_crystallized"] = ref.marshal(C)
         return out
+
+
+def replay_from(chain, blocks, with_state_bytes=False):
+    """Run ``blocks`` through an existing ``Chain`` (e.g. ``Chain.reload``)."""
+    recs = [chain.process_block(to_pb_block(b)) for b in blocks]
+    if with_state_bytes:
+        return recs, chain.roots(), chain.state_bytes()
+    return recs, chain.roots()
 
 
 def replay(blocks, nval, with_state_bytes=False):

@@ -71,6 +71,7 @@ SIGNATURES = {
     "pz_dev_epoch_finish": [vp, vp],
     "pz_dev_epoch_gather_compact": [vp, vp, u32, u64, vp, vp],
     "pz_chain_new": [u64, ctypes.c_int, vp],
+    "pz_chain_new_from_state": [vp, u64, vp, u64, ctypes.c_int, vp],
     "pz_chain_free": [vp],
     "pz_count_attestations": [vp, vp, u64, c_u64p],
     "pz_chain_process_blocks": [vp, vp, vp, u64, vp, vp, u64],

@@ -105,6 +105,24 @@ class BeaconChain:
         lib.call("pz_chain_new", nval, idx, ctypes.byref(self._h))
         self.nval = nval
 
+    @classmethod
+    def from_state(cls, crystallized_bytes, saved_hashes=(), device=None):
+        """NewBeaconChain with a stored CrystallizedState (blockchain/core.go:86-95): resume
+        from its encoding with the genesis ActiveState; ``saved_hashes`` are the block hashes
+        the database holds (hasBlock)."""
+        idx = 0
+        if device is not None:
+            import torch
+            idx = torch.device(device).index or 0
+        self = cls.__new__(cls)
+        self._h = ctypes.c_void_p()
+        cs = np.frombuffer(bytes(crystallized_bytes), dtype=np.uint8)
+        hs = np.frombuffer(b"".join(bytes(h) for h in saved_hashes), dtype=np.uint8)
+        lib.call("pz_chain_new_from_state", _lib.ptr(cs), cs.size, _lib.ptr(hs), len(saved_hashes), idx,
+                 ctypes.byref(self._h))
+        self.nval = None
+        return self
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:

@@ -19,6 +19,7 @@
 #include <chrono>
 #include <cstring>
 #include <memory>
+#include <map>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -258,6 +259,7 @@ using AP = std::shared_ptr<AState>;
 
 struct CState {  // types.CrystallizedState (validators and committees live in the Engine)
   uint64_t lsr = 0, streak = 0, jslot = 0, fslot = 0, dynasty = 0, start_shard = 0, tdep = 0, seed_reset = 0;
+  std::string seed;  // DynastySeed (empty at genesis; stateRecalc does not carry it)
   std::shared_ptr<std::vector<Crosslink>> xl;  // shared with the next state (mutated in place)
 };
 using CP = std::shared_ptr<CState>;
@@ -319,7 +321,12 @@ struct Engine {
   bool poisoned = false;
   // validators (shared by every CrystallizedState, like the Go pointer slice)
   DevArr<uint64_t> balance, start, end;
-  std::vector<uint64_t> h_balance, h_start, h_end;  // genesis values (uploaded once)
+  std::vector<uint64_t> h_balance, h_start, h_end;  // genesis / reloaded values (uploaded once)
+  // the other ValidatorRecord fields, resident only when a reloaded state has them non-zero
+  DevArr<uint64_t> pubkey, wshard, wa_offs, rc_offs;
+  DevArr<uint8_t> wa, rc;
+  bool has_pk = false, has_ws = false, has_wa = false, has_rc = false;
+  uint64_t val_bytes = 0;  // total withdrawal_address + randao_commitment bytes
   // field 11 of the CrystallizedState, encoded on the device from the resident validator
   // arrays (wire.hip); re-encoded only after rewards changed a balance
   std::string val_enc;
@@ -896,9 +903,13 @@ static const std::string& validators_enc(Engine& g) {
   v.balance = g.balance.p;
   v.start_dynasty = g.start.p;
   v.end_dynasty = g.end.p;
+  if (g.has_pk) v.public_key = g.pubkey.p;
+  if (g.has_ws) v.withdrawal_shard = g.wshard.p;
+  if (g.has_wa) { v.withdrawal_address = g.wa.p; v.withdrawal_address_offs = g.wa_offs.p; }
+  if (g.has_rc) { v.randao_commitment = g.rc.p; v.randao_commitment_offs = g.rc_offs.p; }
   WireValArgs a;
   check(wire_val_args(&v, g.nval, 11, &a));
-  const uint64_t bound = pz_wire_validators_bound(g.nval, 0);
+  const uint64_t bound = pz_wire_validators_bound(g.nval, g.val_bytes);
   check(g.w_out.alloc(bound));
   check(g.w_scratch.alloc(wire_tiles(g.nval) + 1));
   check(g.w_total.alloc(1));
@@ -933,6 +944,7 @@ static std::string encode_crystallized(Engine& g, const CState& C) {  // message
   put_u(o, 5, C.dynasty);
   put_u(o, 6, C.start_shard);
   put_u(o, 7, C.tdep);
+  put_b(o, 8, (const uint8_t*)C.seed.data(), C.seed.size());
   put_u(o, 9, C.seed_reset);
   std::string r;
   for (auto& x : *C.xl) {
@@ -942,9 +954,41 @@ static std::string encode_crystallized(Engine& g, const CState& C) {  // message
     put_u(r, 3, x.slot);
     put_msg(o, 10, (const uint8_t*)r.data(), r.size());
   }
-  o += venc;  // ValidatorRecords (public key / shard / bytes all zero)
+  o += venc;  // ValidatorRecords
   o += g.arrays_enc;
   return o;
+}
+
+// Uploads the validators and committees and installs the chain's states: C, and the genesis
+// ActiveState (types/state.go:46-57), which is also what NewBeaconChain keeps when it reloads
+// a stored CrystallizedState (blockchain/core.go:59-64).
+static void init_tail(Engine& g, const std::vector<uint32_t>& members, const std::vector<uint64_t>& offs, const CP& C) {
+  const uint64_t n = g.nval;
+  g.csize.resize(offs.size() - 1);
+  for (size_t c = 0; c + 1 < offs.size(); ++c) g.csize[c] = offs[c + 1] - offs[c];
+  g.ncomm = g.csize.size();
+  g.cwords = 1;
+  for (uint64_t k : g.csize) g.cwords = std::max<uint64_t>(g.cwords, (k + 31) / 32);
+  upload(g, g.committee, members.data(), members.size());
+  upload(g, g.coffs, offs.data(), offs.size());
+  upload(g, g.balance, g.h_balance.data(), n);
+  upload(g, g.start, g.h_start.data(), n);
+  upload(g, g.end, g.h_end.data(), n);
+  g.words = (n + 31) / 32;
+  check(g.e_mask.alloc((n + 63) / 64 + 1));
+  check(g.e_blk.alloc(vblocks_per_inst(n) + 1));
+  check(g.e_list.alloc(n + 1));
+  hchk(hipStreamSynchronize(g.s), "sync");
+  auto A = std::make_shared<AState>();
+  g.hlog.clear();
+  g.id_slot.clear();
+  g.d_hlog_n = 0;
+  const uint32_t zero_id = log_hash(g, kZero);
+  A->recent.assign(2 * kCycle, kZero);
+  A->recent_ids.assign(2 * kCycle, zero_id);
+  A->recent_raw_empty = true;
+  g.A = A;
+  g.C = C;
 }
 
 // ---- genesis (types/state.go:44-112) -------------------------------------------------------
@@ -996,35 +1040,170 @@ static int genesis(Engine& g) {
       g.lookup.push_back(base[i]);
       put_msg(g.arrays_enc, 12, (const uint8_t*)arr_enc[i].data(), arr_enc[i].size());
     }
-  g.csize.resize(offs.size() - 1);
-  for (size_t c = 0; c + 1 < offs.size(); ++c) g.csize[c] = offs[c + 1] - offs[c];
-  g.ncomm = g.csize.size();
-  g.cwords = 1;
-  for (uint64_t k : g.csize) g.cwords = std::max<uint64_t>(g.cwords, (k + 31) / 32);
-  upload(g, g.committee, members.data(), members.size());
-  upload(g, g.coffs, offs.data(), offs.size());
-  upload(g, g.balance, g.h_balance.data(), n);
-  upload(g, g.start, g.h_start.data(), n);
-  upload(g, g.end, g.h_end.data(), n);
-  g.words = (n + 31) / 32;
-  check(g.e_mask.alloc((n + 63) / 64 + 1));
-  check(g.e_blk.alloc(vblocks_per_inst(n) + 1));
-  check(g.e_list.alloc(n + 1));
-  hchk(hipStreamSynchronize(g.s), "sync");
-  auto A = std::make_shared<AState>();
-  g.hlog.clear();
-  g.id_slot.clear();
-  g.d_hlog_n = 0;
-  const uint32_t zero_id = log_hash(g, kZero);
-  A->recent.assign(2 * kCycle, kZero);
-  A->recent_ids.assign(2 * kCycle, zero_id);
-  A->recent_raw_empty = true;
   auto C = std::make_shared<CState>();
   C->dynasty = 1;
   C->tdep = n * PZ_DEFAULT_BALANCE;
   C->xl = std::make_shared<std::vector<Crosslink>>(PZ_SHARD_COUNT);
-  g.A = A;
-  g.C = C;
+  init_tail(g, members, offs, C);
+  return PZ_OK;
+}
+
+// ---- reload: NewBeaconChain with a stored CrystallizedState (blockchain/core.go:86-95) -------
+// proto.Unmarshal accepts any valid encoding (field order, unpacked repeated scalars, unknown
+// fields), so this reader is lenient, unlike the canonical-only block Reader.
+struct LRd {
+  const uint8_t* p;
+  const uint8_t* e;
+  bool bad = false;
+  uint64_t var() {
+    uint64_t x = 0;
+    for (int s = 0; s < 64 && p < e; s += 7) {
+      const uint8_t c = *p++;
+      x |= (uint64_t)(c & 0x7F) << s;
+      if (!(c & 0x80)) return x;
+    }
+    bad = true;
+    return 0;
+  }
+  LRd sub() {
+    const uint64_t n = var();
+    if (bad || (uint64_t)(e - p) < n) { bad = true; return LRd{p, p}; }
+    LRd r{p, p + n};
+    p += n;
+    return r;
+  }
+  void skip(uint32_t wt) {
+    if (wt == 0) var();
+    else if (wt == 2) sub();
+    else if (wt == 1 && e - p >= 8) p += 8;
+    else if (wt == 5 && e - p >= 4) p += 4;
+    else bad = true;
+  }
+};
+
+static int reload(Engine& g, const uint8_t* data, uint64_t len) {
+  auto C = std::make_shared<CState>();
+  C->xl = std::make_shared<std::vector<Crosslink>>();
+  std::vector<uint64_t> pk, ws;
+  std::string wa_bytes, rc_bytes;
+  std::vector<uint64_t> wa_offs{0}, rc_offs{0};
+  // ShardAndCommitteesForSlots: arrays of (shard, members); identical committees share an id
+  std::map<std::vector<uint32_t>, uint32_t> comm_id;
+  std::vector<uint32_t> members;
+  std::vector<uint64_t> offs{0};
+  g.lookup.clear();
+  g.arrays_enc.clear();
+  LRd r{data, data + len};
+  while (r.p < r.e && !r.bad) {
+    const uint64_t key = r.var();
+    const uint32_t f = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
+    if (wt == 0 && f >= 1 && f <= 9 && f != 8) {
+      const uint64_t v = r.var();
+      switch (f) {
+        case 1: C->lsr = v; break;
+        case 2: C->streak = v; break;
+        case 3: C->jslot = v; break;
+        case 4: C->fslot = v; break;
+        case 5: C->dynasty = v; break;
+        case 6: C->start_shard = v; break;
+        case 7: C->tdep = v; break;
+        default: C->seed_reset = v;
+      }
+    } else if (wt == 2 && f == 8) {
+      LRd b = r.sub();
+      C->seed.assign((const char*)b.p, b.e - b.p);
+    } else if (wt == 2 && f == 10) {  // CrosslinkRecord (messages.pb.go:983-985)
+      LRd m = r.sub();
+      Crosslink x;
+      while (m.p < m.e && !m.bad) {
+        const uint64_t k = m.var();
+        if (k == (1 << 3)) x.dynasty = m.var();
+        else if (k == ((2 << 3) | 2)) { LRd b = m.sub(); x.hash.assign((const char*)b.p, b.e - b.p); }
+        else if (k == (3 << 3)) x.slot = m.var();
+        else m.skip((uint32_t)(k & 7));
+      }
+      r.bad |= m.bad;
+      C->xl->push_back(std::move(x));
+    } else if (wt == 2 && f == 11) {  // ValidatorRecord (messages.pb.go:803-809)
+      LRd m = r.sub();
+      uint64_t col[8] = {};
+      std::string wab, rcb;
+      while (m.p < m.e && !m.bad) {
+        const uint64_t k = m.var();
+        const uint32_t ff = (uint32_t)(k >> 3), ww = (uint32_t)(k & 7);
+        if (ww == 0 && (ff == 1 || ff == 2 || (ff >= 5 && ff <= 7))) col[ff] = m.var();
+        else if (ww == 2 && ff == 3) { LRd b = m.sub(); wab.assign((const char*)b.p, b.e - b.p); }
+        else if (ww == 2 && ff == 4) { LRd b = m.sub(); rcb.assign((const char*)b.p, b.e - b.p); }
+        else m.skip(ww);
+      }
+      r.bad |= m.bad;
+      pk.push_back(col[1]);
+      ws.push_back(col[2]);
+      g.h_balance.push_back(col[5]);
+      g.h_start.push_back(col[6]);
+      g.h_end.push_back(col[7]);
+      wa_bytes += wab;
+      wa_offs.push_back(wa_bytes.size());
+      rc_bytes += rcb;
+      rc_offs.push_back(rc_bytes.size());
+    } else if (wt == 2 && f == 12) {  // ShardAndCommitteeArray (messages.pb.go:559, 673-674)
+      LRd m = r.sub();
+      std::vector<std::pair<uint64_t, uint32_t>> arr;
+      std::string arr_enc;
+      while (m.p < m.e && !m.bad) {
+        const uint64_t k = m.var();
+        if (k != ((1 << 3) | 2)) { m.skip((uint32_t)(k & 7)); continue; }
+        LRd q = m.sub();
+        uint64_t shard = 0;
+        std::vector<uint32_t> mem;
+        while (q.p < q.e && !q.bad) {
+          const uint64_t kk = q.var();
+          if (kk == (1 << 3)) shard = q.var();
+          else if (kk == ((2 << 3) | 2)) { LRd pk2 = q.sub(); while (pk2.p < pk2.e && !pk2.bad) mem.push_back((uint32_t)pk2.var()); q.bad |= pk2.bad; }
+          else if (kk == (2 << 3)) mem.push_back((uint32_t)q.var());
+          else q.skip((uint32_t)(kk & 7));
+        }
+        m.bad |= q.bad;
+        auto it = comm_id.find(mem);
+        uint32_t cid;
+        if (it == comm_id.end()) {
+          cid = (uint32_t)(offs.size() - 1);
+          comm_id.emplace(mem, cid);
+          members.insert(members.end(), mem.begin(), mem.end());
+          offs.push_back(members.size());
+        } else {
+          cid = it->second;
+        }
+        arr.push_back({shard, cid});
+        std::string sc, packed;
+        put_u(sc, 1, shard);
+        for (uint32_t v : mem) put_varint(packed, v);
+        if (!packed.empty()) put_msg(sc, 2, (const uint8_t*)packed.data(), packed.size());
+        put_msg(arr_enc, 1, (const uint8_t*)sc.data(), sc.size());
+      }
+      r.bad |= m.bad;
+      g.lookup.push_back(std::move(arr));
+      put_msg(g.arrays_enc, 12, (const uint8_t*)arr_enc.data(), arr_enc.size());
+    } else {
+      r.skip(wt);
+    }
+  }
+  if (r.bad) return fail(PZ_EINVAL, "stored CrystallizedState does not decode (proto.Unmarshal error)");
+  g.nval = g.h_balance.size();
+  if (g.nval == 0 || g.nval > PZ_MAX_VALIDATORS)
+    return fail(PZ_EINVAL, "stored state holds %llu validators", (unsigned long long)g.nval);
+  // (a committee member >= len(validators) panics where Go indexes it, not here)
+  auto any = [](const std::vector<uint64_t>& c) { for (uint64_t x : c) if (x) return true; return false; };
+  g.has_pk = any(pk);
+  g.has_ws = any(ws);
+  g.has_wa = !wa_bytes.empty();
+  g.has_rc = !rc_bytes.empty();
+  g.val_bytes = wa_bytes.size() + rc_bytes.size();
+  if (g.has_pk) upload(g, g.pubkey, pk.data(), pk.size());
+  if (g.has_ws) upload(g, g.wshard, ws.data(), ws.size());
+  if (g.has_wa) { upload(g, g.wa, (const uint8_t*)wa_bytes.data(), wa_bytes.size()); upload(g, g.wa_offs, wa_offs.data(), wa_offs.size()); }
+  if (g.has_rc) { upload(g, g.rc, (const uint8_t*)rc_bytes.data(), rc_bytes.size()); upload(g, g.rc_offs, rc_offs.data(), rc_offs.size()); }
+  init_tail(g, members, offs, C);
   return PZ_OK;
 }
 
@@ -1316,6 +1495,33 @@ int pz_chain_new(uint64_t nval, int device, pz_chain** out) {
   try {
     hchk(hipStreamCreateWithFlags(&c->g.s, hipStreamNonBlocking), "hipStreamCreate");
     check(genesis(c->g));
+  } catch (int e) {
+    if (c->g.s) (void)hipStreamDestroy(c->g.s);
+    delete c;
+    return e;
+  }
+  *out = c;
+  return PZ_OK;
+}
+
+int pz_chain_new_from_state(const uint8_t* cstate, uint64_t len, const uint8_t* saved_hashes, uint64_t nsaved,
+                            int device, pz_chain** out) {
+  if (!out) return fail(PZ_EINVAL, "out is null");
+  *out = nullptr;
+  if (!cstate || !len) return fail(PZ_EINVAL, "empty stored state");
+  if (nsaved && !saved_hashes) return fail(PZ_EINVAL, "saved_hashes is null");
+  int rc = pz_init(device);
+  if (rc) return rc;
+  auto* c = new pz_chain();
+  c->g.device = device;
+  try {
+    hchk(hipStreamCreateWithFlags(&c->g.s, hipStreamNonBlocking), "hipStreamCreate");
+    check(reload(c->g, cstate, len));
+    for (uint64_t i = 0; i < nsaved; ++i) {
+      H32 h;
+      std::memcpy(h.b, saved_hashes + 32 * i, 32);
+      c->g.saved.insert(h);
+    }
   } catch (int e) {
     if (c->g.s) (void)hipStreamDestroy(c->g.s);
     delete c;

@@ -254,3 +254,20 @@ def test_c_shuffle_restatement_matches_scalar_oracle():
     for n in (0, 1, 2, 20, 255, 256, 257, 1000):
         for seed in (ref.bytes_to_hash(b"A"), ref.bytes_to_hash(b""), bytes(range(32))):
             assert cport.shuffle_indices(seed, np.arange(n)).tolist() == ref.shuffle_indices(seed, list(range(n)))
+
+
+def test_oracle_reload_semantics():
+    # blockchain/core.go:59-64,86-95: a reloaded chain has the stored CrystallizedState and the
+    # genesis ActiveState; hasBlock answers from the saved blocks, so the next block extends it
+    from oracle import replay
+    from prysm_amd import synth
+    blocks = synth.chain_blocks(1024, 140, seed=2)
+    ch = replay.Chain(1024)
+    for b in blocks[:70]:
+        ch.process_block(replay.to_pb_block(b))
+    c2 = replay.Chain.reload(ref.marshal(ch.C), ch.saved)
+    assert ref.marshal(c2.C) == ref.marshal(ch.C)
+    active, _ = ref.new_genesis_states(1)
+    assert ref.marshal(c2.A.data) == ref.marshal(active) and c2.A.cache == {}
+    recs, _ = replay.replay_from(c2, blocks[70:])
+    assert recs[0]["status"] == "processed"

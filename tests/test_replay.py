@@ -272,3 +272,78 @@ def test_gpu_replay_configs4_full_chain_vs_c_port():
     assert int(br["transition"].sum()) == 156
     out, port_roots = port_replay(data, offs, nval, len(ar))
     assert mismatches(br, ar, ch.roots(), out, port_roots) == []
+
+
+def _saved_from(recs):
+    return [r["hash"] for r in recs if r["status"] in ("processed", "saved_not_candidate")]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nval,k,total", [(1024, 129, 200), (1000, 70, 140), (65536, 65, 140)])
+def test_gpu_resume_from_persisted_state_vs_oracle(nval, k, total):
+    """f3 read side: NewBeaconChain over a database holding a CrystallizedState
+    (blockchain/core.go:86-95).  The GPU chain runs k blocks; the persisted encoding of its
+    CrystallizedState (what updateHead stores, core.go:170-177) and the saved block hashes
+    seed a reloaded chain (genesis ActiveState, as the reference reloads), which runs the
+    remaining blocks.  The oracle does the same from the same bytes; every record and root
+    must agree."""
+    from oracle import replay
+    from prysm_amd.blockchain import BeaconChain
+    blocks = synth.chain_blocks(nval, total, seed=11)
+    ch = BeaconChain(nval)
+    recs = ch.process_blocks(blocks[:k])
+    cs_bytes = ch.state_bytes("chain_crystallized")
+    saved = _saved_from(recs)
+    o_chain = replay.Chain(nval)
+    o_recs = [o_chain.process_block(replay.to_pb_block(b)) for b in blocks[:k]]
+    assert _hexrecs(recs) == _hexrecs(o_recs) and set(saved) == o_chain.saved
+    from oracle import ref
+    assert cs_bytes == ref.marshal(o_chain.C)
+    ch2 = BeaconChain.from_state(cs_bytes, saved)
+    assert ch2.state_bytes("chain_crystallized") == cs_bytes
+    recs2 = ch2.process_blocks(blocks[k:])
+    o2 = replay.Chain.reload(cs_bytes, saved)
+    o_recs2, o_roots2 = replay.replay_from(o2, blocks[k:])
+    assert _hexrecs(recs2) == _hexrecs(o_recs2)
+    assert sum(r["transition"] for r in recs2) >= 1
+    roots2 = ch2.roots()
+    for key in ("chain_active", "chain_crystallized", "cand_active", "cand_crystallized"):
+        assert roots2[key] == o_roots2[key], key
+    assert roots2["vote_totals"] == o_roots2["vote_totals"]
+
+
+@pytest.mark.gpu
+def test_gpu_reload_general_state_encoding():
+    """A stored state with every ValidatorRecord field set (public key, withdrawal shard and
+    address, RANDAO commitment), a dynasty seed, non-genesis crosslinks and committees: the
+    reloaded chain re-encodes exactly the canonical bytes and hashes them like the oracle."""
+    from oracle import ref
+    from oracle import schema as pb
+    _, cs = ref.new_genesis_states(1000)
+    for i, v in enumerate(cs.validators):
+        v.public_key = (i * 7919) % 1000 + 1
+        v.withdrawal_shard = i % 3
+        v.withdrawal_address = bytes([i & 0xFF]) * (i % 21)
+        v.randao_commitment = bytes([(i * 3) & 0xFF]) * (i % 33)
+        v.balance = 30 + i % 5
+    cs.dynasty_seed = b"\x07" * 32
+    cs.dynasty_seed_last_reset = 5
+    cs.crosslink_records[3].CopyFrom(pb.CrosslinkRecord(dynasty=2, blockhash=b"\x09" * 32, slot=64))
+    cs.last_state_recalc = 64
+    cs.current_dynasty = 3
+    b = ref.marshal(cs)
+    from prysm_amd.blockchain import BeaconChain
+    ch = BeaconChain.from_state(b, [])
+    assert ch.state_bytes("chain_crystallized") == b
+    assert ch.roots()["chain_crystallized"] == ref.crystallized_state_hash(cs)
+    active, _ = ref.new_genesis_states(1)
+    assert ch.roots()["chain_active"] == ref.active_state_hash(active)
+
+
+@pytest.mark.gpu
+def test_gpu_reload_rejects_undecodable_state():
+    from prysm_amd import _lib
+    from prysm_amd.blockchain import BeaconChain
+    with pytest.raises(_lib.PzError) as ei:
+        BeaconChain.from_state(b"\x0a\xff", [])
+    assert ei.value.code == _lib.PZ_EINVAL
