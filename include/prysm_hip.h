@@ -230,6 +230,27 @@ int pz_shuffle_validators_to_committees(const uint8_t seed[32], const uint64_t* 
                                         uint32_t* members, uint64_t* coffs, uint64_t* shard_id,
                                         uint64_t* slot_offs, uint64_t cap_comm, uint64_t* ncomm);
 
+/* ---- a device-resident mirror of the validator set (SURVEY.md §8b "Ownership") ----------
+ * The Go APIs take []*pb.ValidatorRecord, so every host-pointer casper call above re-packs and
+ * re-copies the whole set.  A pz_state keeps one CrystallizedState's validators (SoA balance /
+ * start / end) in HBM, owned by the library; the shim syncs it explicitly (upload after the
+ * set changes, download when Go needs the balances) and the casper drop-ins run on it:
+ * only the attestation bitfields cross PCIe per call.  NULL columns in upload / download are
+ * skipped.  Same results and error codes as the host-pointer forms. */
+typedef struct pz_state pz_state;
+int  pz_state_new(uint64_t n, int device, pz_state** out);
+int  pz_state_upload(pz_state* st, const uint64_t* balance, const uint64_t* start_dynasty,
+                     const uint64_t* end_dynasty);
+int  pz_state_download(pz_state* st, uint64_t* balance, uint64_t* start_dynasty, uint64_t* end_dynasty);
+/* casper/validator.go:45-77 (pz_validator_indices on the mirror) */
+int  pz_state_validator_indices(pz_state* st, uint64_t dynasty, int kind, uint32_t* out, uint64_t* count);
+/* casper/incentives.go:14-32 (pz_calculate_rewards on the mirror's balances, in place) */
+int  pz_state_calculate_rewards(pz_state* st, uint64_t dynasty, uint64_t total_deposit, const uint8_t* bits,
+                                const uint64_t* boffs, uint64_t natt, int* applied);
+/* blockchain/core.go:459-464: sum of the active validators' balances (TotalDeposits) */
+int  pz_state_active_balance(pz_state* st, uint64_t dynasty, uint64_t* total);
+void pz_state_free(pz_state* st);
+
 /* ---- device-resident batched epoch transition (throughput mode, multi-GPU shards) -----
  * B independent instances of the data-parallel part of stateRecalc (blockchain/core.go:
  * 433-464): crosslink tallies + winners, attester popcount, CalculateRewards and the

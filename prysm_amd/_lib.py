@@ -93,6 +93,13 @@ SIGNATURES = {
     "pz_dev_wire_attestations": [vp, u64, u32, vp, vp, vp, vp],
     "pz_dev_check_attestations": [vp, vp],
     "pz_shutdown": [],
+    "pz_state_new": [u64, ctypes.c_int, vp],
+    "pz_state_upload": [vp, vp, vp, vp],
+    "pz_state_download": [vp, vp, vp, vp],
+    "pz_state_validator_indices": [vp, u64, ctypes.c_int, vp, c_u64p],
+    "pz_state_calculate_rewards": [vp, u64, u64, vp, vp, u64, c_intp],
+    "pz_state_active_balance": [vp, u64, c_u64p],
+    "pz_state_free": [vp],
     "pz_comm_unique_id": [vp],
     "pz_comm_init_rank": [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp],
     "pz_init_devices": [ctypes.c_int, vp, vp],
@@ -176,7 +183,7 @@ SCAL_POP, SCAL_NACT, SCAL_ERR_XL, SCAL_ERR_RWD, SCAL_APPLIED, SCAL_NEXT_BAL, SCA
 SCAL_COUNT = 8
 KIND_ACTIVE, KIND_EXITED, KIND_QUEUED = 0, 1, 2
 _RESTYPES = {"pz_last_error": ctypes.c_char_p, "pz_chain_free": None, "pz_set_serial_threshold": u64,
-             "pz_shutdown": None, "pz_set_small_batch_threshold": u64, "pz_comm_free": None, "pz_epoch_state_free": None,
+             "pz_shutdown": None, "pz_state_free": None, "pz_set_small_batch_threshold": u64, "pz_comm_free": None, "pz_epoch_state_free": None,
              "pz_wire_validators_bound": u64, "pz_wire_scratch_bytes": u64,
              "pz_wire_attestations_bound": u64, "pz_wire_attestations_scratch_bytes": u64}
 SERIAL_DEFAULT = 65536        # the library's default serial threshold (bytes)

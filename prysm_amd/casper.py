@@ -133,3 +133,57 @@ def rotate_validator_set(balance, start, end, dynasty):
         assert isinstance(a, np.ndarray) and a.dtype == _u64 and a.flags["C_CONTIGUOUS"]
     lib.call("pz_rotate_validator_set", ptr(balance), ptr(start), ptr(end), start.shape[0], int(dynasty))
     return start, end
+
+
+class ValidatorMirror:
+    """pz_state: one CrystallizedState's validator set resident in HBM (SURVEY.md §8b
+    "Ownership"); the casper functions on it copy only the attestation bitfields per call.
+    ``upload`` / ``download`` are the explicit sync points with the host records."""
+
+    def __init__(self, n, device=0):
+        self.n = int(n)
+        self.h = ctypes.c_void_p()
+        lib.call("pz_state_new", self.n, device, ctypes.byref(self.h))
+
+    def upload(self, balance=None, start=None, end=None):
+        cols = [None if c is None else _arr(c, _u64) for c in (balance, start, end)]
+        for c in cols:
+            assert c is None or c.shape == (self.n,)
+        lib.call("pz_state_upload", self.h, *[ptr(c) if c is not None else None for c in cols])
+
+    def download(self):
+        """-> (balance, start, end) uint64 arrays."""
+        out = [np.empty(self.n, dtype=_u64) for _ in range(3)]
+        lib.call("pz_state_download", self.h, *[ptr(c) for c in out])
+        return tuple(out)
+
+    def indices(self, dynasty, kind=_lib.KIND_ACTIVE):
+        out = np.empty(max(self.n, 1), dtype=np.uint32)
+        cnt = ctypes.c_uint64(0)
+        lib.call("pz_state_validator_indices", self.h, int(dynasty), kind, ptr(out), ctypes.byref(cnt))
+        return out[:cnt.value].copy()
+
+    def calculate_rewards(self, dynasty, total_deposit, bits, boffs):
+        """casper/incentives.go:14-32 on the resident balances -> applied."""
+        bits = _arr(bits, np.uint8)
+        boffs = _arr(boffs, _u64)
+        applied = ctypes.c_int(0)
+        lib.call("pz_state_calculate_rewards", self.h, int(dynasty), int(total_deposit), ptr(bits), ptr(boffs),
+                 max(len(boffs) - 1, 0), ctypes.byref(applied))
+        return bool(applied.value)
+
+    def active_balance(self, dynasty):
+        tot = ctypes.c_uint64(0)
+        lib.call("pz_state_active_balance", self.h, int(dynasty), ctypes.byref(tot))
+        return tot.value
+
+    def free(self):
+        if self.h:
+            lib.dll.pz_state_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # pragma: no cover
+            pass
