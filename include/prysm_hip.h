@@ -91,7 +91,11 @@ uint64_t pz_set_small_batch_threshold(uint64_t compressions);
 int pz_dev_blake2b512_batch(const uint8_t* d_msgs, const uint64_t* d_offsets, uint64_t n,
                             uint8_t* d_out, uint32_t out_bytes, void* stream);
 /* Fixed-length records: message i is d_msgs[i*stride .. i*stride+len); stride % 16 == 0,
- * d_msgs 16-byte aligned, stride >= len.  This is the batched-record fast path. */
+ * d_msgs 16-byte aligned, stride >= len.  This is the batched-record fast path.  The kernels
+ * load whole aligned chunks, so the buffer must be readable up to the end of the last
+ * record's chunk: (n-1)*stride + 128*ceil(len/128) bytes when stride >= 128*ceil(len/128)
+ * (the LDS-staged path), (n-1)*stride + 16*ceil(len/16) otherwise; a buffer of n*stride
+ * bytes with stride a multiple of 128 always suffices.  Bytes past len never affect a digest. */
 int pz_dev_blake2b512_fixed(const uint8_t* d_msgs, uint64_t stride, uint64_t len, uint64_t n,
                             uint8_t* d_out, uint32_t out_bytes, void* stream);
 
