@@ -87,6 +87,7 @@ struct CountGrid {
 // Crosslink tally for one attestation, one wave (core.go:533-545).  Members are processed
 // 256 at a time with every committee load, then every balance gather, in flight together
 // (two dependent round trips per 256 members instead of two per 64).
+template <int V>
 __device__ __forceinline__ void crosslink_wave(const EpochArgs& a, uint64_t ga, int lane) {
   const uint64_t inst = (uint32_t)ga / (uint32_t)a.natt;  // 32-bit: B*natt < 2^32 (host-checked)
   const uint32_t c = a.att_comm[ga];
@@ -122,7 +123,12 @@ __device__ __forceinline__ void crosslink_wave(const EpochArgs& a, uint64_t ga, 
       const uint64_t i = r0 + j * 64 + lane;
       const uint64_t local = (uint64_t)mem[j] - a.val_offset;  // wraps huge when mem < val_offset
       const bool own = i < k && mem[j] < a.nval_global && local < a.nval;
-      bal[j] = own ? B[local] : 0;
+      if (V & 8)  // probe: nontemporal gather
+        bal[j] = own ? __builtin_nontemporal_load(B + local) : 0;
+      else if (V & 16)  // probe: sc1 (L1-bypassing) gather
+        bal[j] = own ? __hip_atomic_load(B + local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+      else
+        bal[j] = own ? B[local] : 0;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -148,7 +154,8 @@ __device__ __forceinline__ void crosslink_wave(const EpochArgs& a, uint64_t ga, 
 
 // V is an A/B knob for tools/ (0 in the product): bit 0 = validator blocks in rounds of
 // kGroup chunks per instance; bit 1 = a max-index atomic from every block; bit 2 = no
-// non-matching-count atomic (timing probe only: its results are wrong).
+// non-matching-count atomic (timing probe only: its results are wrong); 8 / 16 = the crosslink
+// balance gathers as nontemporal / sc1 loads.
 template <int V>
 __device__ __forceinline__ void count_body(const EpochArgs& a, const CountGrid& g) {
   __shared__ uint64_t sh[kThreads / 64];
@@ -172,7 +179,7 @@ __device__ __forceinline__ void count_body(const EpochArgs& a, const CountGrid& 
     }
     const uint64_t att = j * (kThreads / 64) + wave;
     if (inst >= a.ninst || att >= a.natt) return;
-    crosslink_wave(a, inst * a.natt + att, lane);
+    crosslink_wave<V>(a, inst * a.natt + att, lane);
     return;
   }
   const uint64_t b = blockIdx.x - g.nxb;
@@ -307,12 +314,14 @@ PZ_COUNT_KERNEL(pz_epoch_count_v2_kernel, 2)
 PZ_COUNT_KERNEL(pz_epoch_count_v3_kernel, 3)
 PZ_COUNT_KERNEL(pz_epoch_count_v4_kernel, 4)
 PZ_COUNT_KERNEL(pz_epoch_count_v5_kernel, 5)
+PZ_COUNT_KERNEL(pz_epoch_count_v8_kernel, 8)
+PZ_COUNT_KERNEL(pz_epoch_count_v16_kernel, 16)
 #undef PZ_COUNT_KERNEL
 
 static int g_count_variant = 0;  // tools/ A/B only
 int set_count_variant(int v) {
   const int old = g_count_variant;
-  g_count_variant = v & 7;
+  g_count_variant = v;
   return old;
 }
 
@@ -693,6 +702,8 @@ hipError_t launch_epoch_count(const EpochArgs& a, bool do_val, bool do_pop, bool
     case 3: hipLaunchKernelGGL(pz_epoch_count_v3_kernel, grid, dim3(kThreads), 0, s, a, g); break;
     case 4: hipLaunchKernelGGL(pz_epoch_count_v4_kernel, grid, dim3(kThreads), 0, s, a, g); break;
     case 5: hipLaunchKernelGGL(pz_epoch_count_v5_kernel, grid, dim3(kThreads), 0, s, a, g); break;
+    case 8: hipLaunchKernelGGL(pz_epoch_count_v8_kernel, grid, dim3(kThreads), 0, s, a, g); break;
+    case 16: hipLaunchKernelGGL(pz_epoch_count_v16_kernel, grid, dim3(kThreads), 0, s, a, g); break;
     default: hipLaunchKernelGGL(pz_epoch_count_kernel, grid, dim3(kThreads), 0, s, a, g);
   }
   return hipGetLastError();

@@ -164,3 +164,41 @@ def new_genesis_states(num_validators=BOOTSTRAPPED_VALIDATORS_COUNT):
         crosslink_records=[pb.CrosslinkRecord() for _ in range(SHARD_COUNT)],
         validators=vals, shard_and_committees_for_slots=arrs + arrs)
     return active, CrystallizedState(cs)
+
+
+def message_shard(n, rank, world):
+    """The contiguous slice ``[lo, hi)`` of an n-message batch that ``rank`` of ``world``
+    hashes: the same split as pz_comm_blake2b512_batch (message batches shard with no
+    collective)."""
+    return n * rank // world, n * (rank + 1) // world
+
+
+def hash_batch_sharded(data, offsets, rank, world, group=None, out_bytes=32, hasher=None):
+    """H over one process per GPU: rank ``rank`` hashes its slice of the CSR batch on its GPU
+    (``hasher``: the C-ABI batch hash by default; tests substitute a CPU double), and the
+    digests are all-gathered over ``torch.distributed`` so every rank returns all n of them
+    (n x out_bytes uint8).  The gather is the caller's choice of output placement, not part of
+    the hash: a node that consumes its own slice skips it (``group=False``)."""
+    import torch
+    import torch.distributed as dist
+
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(offsets) - 1
+    lo, hi = message_shard(n, rank, world)
+    local_offs = offsets[lo:hi + 1] - offsets[lo]
+    local_data = np.ascontiguousarray(data[int(offsets[lo]):int(offsets[hi])], dtype=np.uint8)
+    local_data = np.concatenate([local_data, np.zeros(16, np.uint8)])
+    hasher = hasher or (lambda d, o: _lib.blake2b512_csr(d, o, out_bytes))
+    mine = hasher(local_data, local_offs) if hi > lo else np.zeros((0, out_bytes), np.uint8)
+    if group is False or world == 1:
+        return mine
+    per = -(-n // world)  # all-gather needs equal sizes: pad every slice to ceil(n / world)
+    send = torch.zeros(per * out_bytes, dtype=torch.uint8)
+    send[:mine.size] = torch.from_numpy(mine.reshape(-1).copy())
+    bufs = [torch.zeros_like(send) for _ in range(world)]
+    dist.all_gather(bufs, send, group=group)
+    out = np.zeros((n, out_bytes), np.uint8)
+    for r in range(world):
+        a, b = message_shard(n, r, world)
+        out[a:b] = bufs[r].numpy()[:(b - a) * out_bytes].reshape(b - a, out_bytes)
+    return out

@@ -32,6 +32,9 @@ def main(nval=65536, ninst=256, rounds=5, reps=10):
         **{"count_val_v%d" % v: (lambda v=v: (dll.pz_debug_set_count_variant(v),
                                               dll.pz_debug_epoch_count(bp, 1, 0, 0, sh),
                                               dll.pz_debug_set_count_variant(0))) for v in range(6)},
+        **{"count_xl_v%d" % v: (lambda v=v: (dll.pz_debug_set_count_variant(v),
+                                             dll.pz_debug_epoch_count(bp, 0, 0, 1, sh),
+                                             dll.pz_debug_set_count_variant(0))) for v in (0, 8, 16)},
         "reward": lambda: dll.pz_debug_epoch_reward(bp, sh),
         "reward_nobits": lambda: dll.pz_debug_epoch_reward_mode(bp, 1, sh),
         "reward_noreduce": lambda: dll.pz_debug_epoch_reward_mode(bp, 2, sh),
