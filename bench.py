@@ -734,8 +734,8 @@ def shuffle_leg(args):
     return out
 
 
-PMC_SUMMARY = os.path.join("profiles", "r01", "pmc_summary.json")
-PMC_SUMMARY_EPOCH_1M = os.path.join("profiles", "r01", "pmc_summary_epoch1m.json")
+PMC_SUMMARY = os.path.join("profiles", "r02", "pmc_summary.json")
+PMC_SUMMARY_EPOCH_1M = os.path.join("profiles", "r02", "pmc_summary_epoch1m.json")
 
 
 def pmc_traffic(kernels, summary=PMC_SUMMARY):
