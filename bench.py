@@ -96,6 +96,9 @@ def parse():
     p.add_argument("--epoch-path", default="native", choices=["native", "torch"],
                    help="native: pz_epoch_state (C ABI, the library's RCCL communicator); torch: DeviceEpoch "
                         "over torch.distributed (the test double of the same orchestration)")
+    p.add_argument("--epoch-layout", default="auto", choices=["auto", "index"],
+                   help="auto: committee order when every validator is active and the committees partition "
+                        "the set (pz_epoch_host.layout); index: validator-index order")
     p.add_argument("--no-replay", action="store_true")
     p.add_argument("--no-wire", action="store_true")
     p.add_argument("--no-attcheck", action="store_true")
@@ -148,7 +151,7 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
     inst = synth.epoch_batch(nval, ninst, seed=3, shuffled=shuffled)
     native = args.epoch_path == "native"
     if native:
-        de = NativeEpoch(inst, device=dev.index, comm=comm if world > 1 else None)
+        de = NativeEpoch(inst, device=dev.index, comm=comm if world > 1 else None, layout=args.epoch_layout)
         lo, hi, _, sp = de.shard(0)
         stream = torch.cuda.ExternalStream(sp, device=dev)
         step = de.step
@@ -196,6 +199,8 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                                % (2 if (world == 1 and nval != 1 << 20) else 3),
                    "validators": nval, "instances_per_step": ninst, "attestations_per_instance": inst["natt"],
                    "parallelism": "validator-shard x%d + RCCL all-reduce" % world if world > 1 else "single GPU",
+                   "layout": (("committee order" if de.committee_order else "index order") if native
+                              else "index order"),
                    "path": ("pz_epoch_state_step (C ABI: HIP kernels + the library's RCCL communicator)"
                             if native else "DeviceEpoch (pz_dev_epoch_* + torch.distributed collectives)")},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
@@ -232,9 +237,10 @@ def epoch_parity(inst, dev):
     de = NativeEpoch(inst, device=dev.index)
     de.step()
     bal, scal, vote, total, win = de.results()
+    idx = de.validators()  # the validator index of each balance column (committee order)
     de.free()
     nb, applied, nxt, v, t, w = oracle_epoch(inst, 0)
-    ok = (np.array_equal(bal[0], nb) and bool(scal[0, _lib.SCAL_APPLIED]) == applied
+    ok = (np.array_equal(bal[0], nb[idx]) and bool(scal[0, _lib.SCAL_APPLIED]) == applied
           and int(scal[0, _lib.SCAL_NEXT_BAL]) == nxt and np.array_equal(vote[0], v)
           and np.array_equal(total[0], t) and np.array_equal(win[0], w))
     return "instance 0 of the timed %d x %d workload, one step, bit-exact vs oracle/epoch_np: %s" % (

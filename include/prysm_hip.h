@@ -277,9 +277,12 @@ void pz_state_free(pz_state* st);
 #define PZ_SCAL_NOMATCH   7  /* pass 1: validators in range NOT matching `kind` (all-reduced
                                 with the rest); pass 2 sets PZ_SCAL_NACT = nval_global - this */
 #define PZ_SCAL_COUNT     8
+/* PZ_SCAL_ERR_XL is the sum, over every (attestation, rank) that found one, of the
+ * PZ_XLERR_* values below: != 0 is the panic; the bits name the cause when one raiser did. */
 #define PZ_XLERR_MEMBER   1ULL
 #define PZ_XLERR_BITFIELD 2ULL
 #define PZ_XLERR_SHARD    4ULL
+#define PZ_XLERR_LAYOUT   8ULL  /* committee-order layout used with a non-matching validator */
 
 typedef struct pz_epoch_batch {
   uint32_t ninst;                 /* B */
@@ -319,6 +322,16 @@ typedef struct pz_epoch_batch {
                                      nval_global so that its panic is raised) and cpos[k] is
                                      member k's position in its full committee (the bitfield
                                      bit); NULL: full committees, position = index in the row */
+  const uint32_t* co_index;       /* optional "committee order": the validator arrays of every
+                                     instance are stored in committee order -- committee c
+                                     occupies storage positions [coffs[c], coffs[c+1]) of
+                                     [0, nval_global), which the committees partition -- and
+                                     co_index[p - val_offset] is the validator index stored at
+                                     position p.  The crosslink tallies then stream contiguous
+                                     balances (no member gathers; `committee`/`cpos` unused) and
+                                     CalculateRewards reads bit co_index[p] of the last bitfield.
+                                     Requires every validator to match `kind` (else
+                                     PZ_XLERR_LAYOUT in scal[PZ_SCAL_ERR_XL]). */
 } pz_epoch_batch;
 
 /* ---- T: block vote-cache tally (blockchain/core.go:300-345 calculateBlockVoteCache) ----
@@ -406,7 +419,9 @@ int pz_comm_blake2b512_batch(const pz_comm* comm, const uint8_t* msgs, const uin
  * 433-464), described by host arrays over ALL validators; each local rank of `comm` uploads
  * its 64-aligned validator range [lo, hi) of every instance into its GPU's HBM (SoA,
  * instance-major) and the committee members inside it.  comm == NULL: one device, world 1.
- * A step enqueues (no host sync):
+ * When every validator is active and the committees partition the set, the validators are
+ * stored in committee order (pz_epoch_batch.co_index): the crosslink tallies stream contiguous
+ * balances and each rank holds a range of committee positions.  A step enqueues (no host sync):
  *   count -> RCCL all-reduce {scal, vote, total} -> [some validator inactive: all-gather of
  *   the active masks -> global compaction] -> finish -> all-reduce of the next-cycle totals,
  * the instances split in two parts so one part's collectives overlap the other's kernels.
@@ -430,7 +445,12 @@ typedef struct pz_epoch_host {
   const uint32_t* att_shard;       /* [B*natt] */
   uint32_t nrec;                   /* crosslink records per instance */
   const uint64_t* rec_dynasty;     /* [B][nrec] */
+  uint32_t layout;                 /* PZ_LAYOUT_AUTO: committee order when every validator is
+                                      active and the committees partition the set, else index
+                                      order; PZ_LAYOUT_INDEX: always index order */
 } pz_epoch_host;
+#define PZ_LAYOUT_AUTO  0
+#define PZ_LAYOUT_INDEX 1
 typedef struct pz_epoch_state pz_epoch_state;
 int  pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epoch_state** out);
 int  pz_epoch_state_step(pz_epoch_state* st);
@@ -438,10 +458,16 @@ int  pz_epoch_state_sync(pz_epoch_state* st);
 /* Local rank `local`'s validator range, device and compute stream (for event timing). */
 int  pz_epoch_state_shard(const pz_epoch_state* st, int local, uint64_t* lo, uint64_t* hi, int* device,
                           void** stream);
-/* After a step (synchronises): local rank `local`'s balances [B][hi-lo], and the reduced
+/* After a step (synchronises): the balances of the hi-lo validators local rank `local` holds
+ * ([B][hi-lo], in its storage order: pz_epoch_state_validators names them), and the reduced
  * scal [B][PZ_SCAL_COUNT], vote / total [B][natt] and winners [B][nrec] (any may be NULL). */
 int  pz_epoch_state_results(pz_epoch_state* st, int local, uint64_t* balance, uint64_t* scal, uint64_t* vote,
                             uint64_t* total, uint32_t* winner);
+/* The validator index held at each of local rank `local`'s hi-lo storage positions: lo.. in
+ * index order; the members of the committees, in committee order, in the committee-order
+ * layout (pz_epoch_batch.co_index), which *committee_order reports. */
+int  pz_epoch_state_validators(const pz_epoch_state* st, int local, uint32_t* index);
+int  pz_epoch_state_layout(const pz_epoch_state* st, int* committee_order);
 void pz_epoch_state_free(pz_epoch_state* st);
 
 /* ---- block pipeline: sync replay of serialized blocks ---------------------------------

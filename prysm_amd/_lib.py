@@ -114,6 +114,8 @@ SIGNATURES = {
     "pz_epoch_state_shard": [vp, ctypes.c_int, c_u64p, c_u64p, c_intp, vp],
     "pz_epoch_state_results": [vp, ctypes.c_int, vp, vp, vp, vp, vp],
     "pz_epoch_state_free": [vp],
+    "pz_epoch_state_validators": [vp, ctypes.c_int, vp],
+    "pz_epoch_state_layout": [vp, c_intp],
 }
 
 
@@ -127,7 +129,7 @@ class EpochBatch(ctypes.Structure):
         ("committee", vp), ("coffs", vp), ("att_comm", vp), ("att_shard", vp),
         ("nrec", ctypes.c_uint32), ("rec_dynasty", vp), ("winner", vp), ("vote", vp), ("total", vp),
         ("scal", vp), ("act_mask", vp), ("blk_cnt", vp), ("act_list", vp), ("scal_next", vp),
-        ("cpos", vp),
+        ("cpos", vp), ("co_index", vp),
     ]
 
 
@@ -137,7 +139,7 @@ class EpochHost(ctypes.Structure):
         ("ninst", ctypes.c_uint32), ("nval", u64), ("balance", vp), ("start", vp), ("end", vp),
         ("dynasty", vp), ("total_deposit", vp), ("natt", ctypes.c_uint32), ("bits", vp), ("boffs", vp),
         ("committee", vp), ("coffs", vp), ("ncomm", u64), ("att_comm", vp), ("att_shard", vp),
-        ("nrec", ctypes.c_uint32), ("rec_dynasty", vp),
+        ("nrec", ctypes.c_uint32), ("rec_dynasty", vp), ("layout", ctypes.c_uint32),
     ]
 
 

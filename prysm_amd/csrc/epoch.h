@@ -18,7 +18,10 @@ enum : int {
   kApplied = PZ_SCAL_APPLIED, kNextBal = PZ_SCAL_NEXT_BAL, kMaxIdx1 = PZ_SCAL_MAXIDX1,
   kNoMatch = PZ_SCAL_NOMATCH, kScal = PZ_SCAL_COUNT
 };
-enum : uint64_t { kErrMember = PZ_XLERR_MEMBER, kErrBitfield = PZ_XLERR_BITFIELD, kErrShard = PZ_XLERR_SHARD };
+enum : uint64_t {
+  kErrMember = PZ_XLERR_MEMBER, kErrBitfield = PZ_XLERR_BITFIELD, kErrShard = PZ_XLERR_SHARD,
+  kErrLayout = PZ_XLERR_LAYOUT
+};
 
 typedef pz_epoch_batch EpochArgs;
 

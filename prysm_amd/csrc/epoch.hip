@@ -87,8 +87,58 @@ struct CountGrid {
 // Crosslink tally for one attestation, one wave (core.go:533-545).  Members are processed
 // 256 at a time with every committee load, then every balance gather, in flight together
 // (two dependent round trips per 256 members instead of two per 64).
+// Committee-order layout (a.co_index): committee c is the contiguous storage range
+// [coffs[c], coffs[c+1]), so its balances stream coalesced and the bitfield bit of a member is
+// its offset in the range -- no member-index loads, no random balance gathers.  A rank adds
+// the part of the range it holds.
+__device__ __forceinline__ void crosslink_wave_co(const EpochArgs& a, uint64_t ga, int lane) {
+  const uint64_t inst = (uint32_t)ga / (uint32_t)a.natt;
+  const uint32_t c = a.att_comm[ga];
+  const uint64_t cb = a.coffs[c], ce = a.coffs[c + 1];
+  const uint64_t lo = cb > a.val_offset ? cb : a.val_offset;
+  const uint64_t hi = ce < a.val_offset + a.nval ? ce : a.val_offset + a.nval;
+  const uint64_t bb = a.boffs[ga], blen = a.boffs[ga + 1] - bb;
+  const uint8_t* bf = a.bits + bb;
+  const uint64_t* B = a.balance + inst * a.nval - a.val_offset;  // indexed by storage position
+  uint64_t tot = 0, vote = 0;
+  bool e_bf = false;
+  for (uint64_t p0 = lo; p0 < hi; p0 += 256) {
+    uint64_t bal[4];
+    uint32_t byte[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t p = p0 + j * 64 + lane;
+      const uint64_t pos = p - cb;
+      bal[j] = p < hi ? B[p] : 0;
+      byte[j] = (p < hi && pos < 8 * blen) ? bf[pos >> 3] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t p = p0 + j * 64 + lane;
+      if (p < hi) {
+        const uint64_t pos = p - cb;
+        e_bf |= pos >= 8 * blen;
+        tot += bal[j];
+        vote += ((byte[j] >> (7 - (uint32_t)(pos & 7))) & 1u) ? bal[j] : 0;
+      }
+    }
+  }
+  tot = wave_sum(tot);
+  vote = wave_sum(vote);
+  const uint64_t e2 = __ballot(e_bf);
+  if (lane == 0) {
+    a.vote[ga] = vote;
+    a.total[ga] = tot;
+    if (e2) atomicAdd((unsigned long long*)&a.scal[inst * kScal + kErrXl], (unsigned long long)kErrBitfield);
+  }
+}
+
 template <int V>
 __device__ __forceinline__ void crosslink_wave(const EpochArgs& a, uint64_t ga, int lane) {
+  if (a.co_index) {
+    crosslink_wave_co(a, ga, lane);
+    return;
+  }
   const uint64_t inst = (uint32_t)ga / (uint32_t)a.natt;  // 32-bit: B*natt < 2^32 (host-checked)
   const uint32_t c = a.att_comm[ga];
   const uint64_t cb = a.coffs[c], k = a.coffs[c + 1] - cb;
@@ -262,6 +312,9 @@ __device__ __forceinline__ void count_body(const EpochArgs& a, const CountGrid& 
       if (a.blk_cnt) a.blk_cnt[inst * g.vbpi + chunk] = (uint32_t)c;
       const uint64_t nomatch = (bend - base) - c;
       if (nomatch && !(V & 4)) atomicAdd((unsigned long long*)&a.scal[inst * kScal + kNoMatch], (unsigned long long)nomatch);
+      // the committee-order layout maps rank to index only when every validator matches
+      if (nomatch && a.co_index)
+        atomicOr((unsigned long long*)&a.scal[inst * kScal + kErrXl], (unsigned long long)kErrLayout);
       // The max active index needs an atomic only from a block that can hold it: the last
       // chunk, a block whose last validator is inactive, or one followed by an inactive
       // validator.  With every validator active only the last chunk adds one.
@@ -538,7 +591,18 @@ __device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
     // of one per element).
     const int lane = tid & 63, wave = tid >> 6;
     const uint64_t gbase = a.val_offset + base;
-    const bool fastbits = (MODE & 1) == 0 && applied && all_active && lastbf && (gbase & 7) == 0;
+    const bool fastbits = (MODE & 1) == 0 && applied && all_active && lastbf && (gbase & 7) == 0 && !a.co_index;
+    // committee order: position p holds validator co_index[p]; with every validator active its
+    // rank is its index, so its reward bit is bit co_index[p] of the last bitfield (incentives.go:
+    // 22-27); the index pair of each lane is loaded with the balances
+    uint2 cix[kPairs];
+    if (a.co_index && applied) {
+#pragma unroll
+      for (int j = 0; j < kPairs; ++j) {
+        const uint64_t p = base + (uint64_t)j * (2 * kThreads) + 2 * tid;
+        cix[j] = *reinterpret_cast<const uint2*>(a.co_index + (p < a.nval ? p : 0));
+      }
+    }
     uint32_t mybyte = 0;
     if (fastbits) {
       const uint64_t L = boffs_ro[inst * a.natt + a.natt] - boffs_ro[inst * a.natt + a.natt - 1];
@@ -559,6 +623,14 @@ __device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
           b0 = pack64(q[j].x, q[j].y) + 1;
           b1 = pack64(q[j].z, q[j].w) - 1;
           changed = applied;
+        } else if (a.co_index) {  // every validator active (the count pass checks): rank == index
+          b0 = pack64(q[j].x, q[j].y);
+          b1 = pack64(q[j].z, q[j].w);
+          if (applied) {
+            b0 = bit_at(lastbf, cix[j].x) ? b0 + PZ_ATTESTER_REWARD : b0 - PZ_ATTESTER_REWARD;
+            b1 = bit_at(lastbf, cix[j].y) ? b1 + PZ_ATTESTER_REWARD : b1 - PZ_ATTESTER_REWARD;
+            changed = true;
+          }
         } else if (fastbits) {  // gp < nact for every p < nval here (all active)
           const uint32_t sh0 = 7u - (uint32_t)(gp & 7);
           b0 = pack64(q[j].x, q[j].y);
@@ -627,7 +699,8 @@ __device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
     const uint64_t gp = a.val_offset + p;
     uint64_t bal = B[p];
     if (applied && gp < nact) {
-      const uint64_t idx = all_active ? gp : list[gp];
+      // committee order: the validator at p is co_index[p], rank == index (all active)
+      const uint64_t idx = a.co_index ? a.co_index[p] : all_active ? gp : list[gp];
       bal = bit_at(lastbf, idx) ? bal + PZ_ATTESTER_REWARD : bal - PZ_ATTESTER_REWARD;
       B[p] = bal;
     }

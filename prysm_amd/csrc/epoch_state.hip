@@ -60,6 +60,8 @@ struct pz_epoch_state {
   uint32_t B = 0, natt = 0, nrec = 0, nparts = 1;
   uint64_t N = 0, sw = 0, ncomm = 0;
   bool general = false, all_active = true;
+  bool co = false;                 // committee-order layout (see pz_epoch_batch.co_index)
+  std::vector<uint32_t> co_inv;    // storage position -> validator index (committee order)
   uint64_t steps = 0;
   std::vector<Shard> sh;
   ~pz_epoch_state();
@@ -97,6 +99,18 @@ int upload_range(Shard& s, uint64_t** p, const uint64_t* host, uint32_t B, uint6
   if (rc || !s.n) return rc;
   hipError_t e = hipMemcpy2D(*p, s.n * 8, host + s.lo, N * 8, s.n * 8, B, hipMemcpyHostToDevice);
   return e == hipSuccess ? PZ_OK : hip_fail(e, "hipMemcpy2D H2D (epoch state)");
+}
+
+// Committee order: rows [0, B) of a host [B][N] array, the validators stored at positions
+// [lo, hi) (inv[p] = the validator at position p) -> device [B][hi-lo].
+int upload_perm(Shard& s, uint64_t** p, const uint64_t* host, uint32_t B, uint64_t N, const uint32_t* inv) {
+  int rc = dalloc(s, p, (size_t)B * s.n, false);
+  if (rc || !s.n) return rc;
+  std::vector<uint64_t> tmp((size_t)B * s.n);
+  for (uint64_t b = 0; b < B; ++b)
+    for (uint64_t q = 0; q < s.n; ++q) tmp[b * s.n + q] = host[b * N + inv[s.lo + q]];
+  hipError_t e = hipMemcpy(*p, tmp.data(), tmp.size() * 8, hipMemcpyHostToDevice);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "hipMemcpy H2D (epoch state)");
 }
 
 uint64_t shard_words(uint64_t N, int world) { return std::max<uint64_t>(1, (N + 64ull * world - 1) / (64ull * world)); }
@@ -297,6 +311,21 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
     }
   }
   st->general = !st->all_active && st->world > 1;
+  // Committee order when every validator is active and the committees partition [0, N):
+  // the crosslink tallies then stream contiguous balances instead of gathering them.
+  if (st->all_active && h->natt && h->layout == PZ_LAYOUT_AUTO && h->coffs[h->ncomm] == st->N) {
+    std::vector<uint8_t> seen(st->N, 0);
+    bool part = true;
+    for (uint64_t k = 0; k < st->N && part; ++k) {
+      const uint32_t v = h->committee[k];
+      part = v < st->N && !seen[v];
+      if (part) seen[v] = 1;
+    }
+    if (part) {
+      st->co = true;
+      st->co_inv.assign(h->committee, h->committee + st->N);
+    }
+  }
   st->nparts = (st->world > 1 && st->B >= 2) ? 2 : 1;
   const int nlocal = comm ? comm->nlocal : 1;
   st->sh.resize(nlocal);
@@ -327,14 +356,28 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
     uint32_t *winner, *blk_cnt, *act_list;
     uint64_t* act_mask;
     const uint64_t vbpi = vblocks_per_inst(s.n);
-    if ((rc = upload_range(s, &bal, h->balance, st->B, st->N)) || (rc = upload_range(s, &start, h->start, st->B, st->N)) ||
-        (rc = upload_range(s, &end, h->end, st->B, st->N)) || (rc = upload(s, &dyn, h->dynasty, st->B)) ||
+    uint32_t* co_index = nullptr;
+    if (st->co) {
+      const uint32_t* inv = st->co_inv.data();
+      if ((rc = upload_perm(s, &bal, h->balance, st->B, st->N, inv)) ||
+          (rc = upload_perm(s, &start, h->start, st->B, st->N, inv)) ||
+          (rc = upload_perm(s, &end, h->end, st->B, st->N, inv)) || (rc = upload(s, &co_index, inv + s.lo, s.n)))
+        break;
+    } else if ((rc = upload_range(s, &bal, h->balance, st->B, st->N)) ||
+               (rc = upload_range(s, &start, h->start, st->B, st->N)) ||
+               (rc = upload_range(s, &end, h->end, st->B, st->N))) {
+      break;
+    }
+    if ((rc = upload(s, &dyn, h->dynasty, st->B)) ||
         (rc = upload(s, &tdep, h->total_deposit, st->B)))
       break;
     if (st->natt) {
       std::vector<uint32_t> mem, pos;
       std::vector<uint64_t> offs;
-      if (st->world > 1) {
+      if (st->co) {  // committee c = storage positions [coffs[c], coffs[c+1]); no member list
+        mem.assign(1, 0);
+        offs.assign(h->coffs, h->coffs + h->ncomm + 1);
+      } else if (st->world > 1) {
         local_committees(h, s.lo, s.hi, s.grank == 0, mem, offs, pos);
       } else {
         mem.assign(h->committee, h->committee + h->coffs[h->ncomm]);
@@ -346,7 +389,7 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
           (rc = upload(s, &coffs, offs.data(), offs.size())) || (rc = upload(s, &att_comm, h->att_comm, na)) ||
           (rc = upload(s, &att_shard, h->att_shard, na)))
         break;
-      if (st->world > 1 && (rc = upload(s, &cpos, pos.data(), pos.size()))) break;
+      if (st->world > 1 && !st->co && (rc = upload(s, &cpos, pos.data(), pos.size()))) break;
     }
     if (st->nrec && (rc = upload(s, &recd, h->rec_dynasty, (size_t)st->B * st->nrec))) break;
     if ((rc = dalloc(s, &winner, (size_t)st->B * std::max<uint32_t>(st->nrec, 1))) ||
@@ -393,6 +436,7 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
         a.committee = committee;
         a.coffs = coffs;
         a.cpos = cpos;
+        a.co_index = co_index;
         a.att_comm = att_comm + i0 * st->natt;
         a.att_shard = att_shard + i0 * st->natt;
       }
@@ -476,6 +520,20 @@ int pz_epoch_state_results(pz_epoch_state* st, int local, uint64_t* balance, uin
       e = hipMemcpy(winner + i0 * st->nrec, q.a.winner, Bp * st->nrec * 4, hipMemcpyDeviceToHost);
   }
   return e == hipSuccess ? PZ_OK : hip_fail(e, "epoch state results D2H");
+}
+
+int pz_epoch_state_validators(const pz_epoch_state* st, int local, uint32_t* index) {
+  if (!st || !index) return fail(PZ_EINVAL, "null pointer");
+  if (local < 0 || local >= (int)st->sh.size()) return fail(PZ_EINVAL, "local rank %d of %zu", local, st->sh.size());
+  const Shard& s = st->sh[local];
+  for (uint64_t q = 0; q < s.n; ++q) index[q] = st->co ? st->co_inv[s.lo + q] : (uint32_t)(s.lo + q);
+  return PZ_OK;
+}
+
+int pz_epoch_state_layout(const pz_epoch_state* st, int* committee_order) {
+  if (!st || !committee_order) return fail(PZ_EINVAL, "null pointer");
+  *committee_order = st->co ? 1 : 0;
+  return PZ_OK;
 }
 
 void pz_epoch_state_free(pz_epoch_state* st) { delete st; }

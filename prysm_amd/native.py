@@ -82,7 +82,9 @@ class NativeEpoch:
     """``pz_epoch_state``: the same inputs as ``prysm_amd.epoch.DeviceEpoch`` (a
     ``synth.epoch_batch``-shaped dict over all validators)."""
 
-    def __init__(self, inst, device=0, comm=None):
+    def __init__(self, inst, device=0, comm=None, layout="auto"):
+        """``layout``: "auto" (committee order when every validator is active and the
+        committees partition the set) or "index"."""
         u64 = lambda a: np.ascontiguousarray(a, dtype=np.uint64)  # noqa: E731
         u32 = lambda a: np.ascontiguousarray(a, dtype=np.uint32)  # noqa: E731
         self._keep = k = dict(balance=u64(inst["balance"]), start=u64(inst["start"]), end=u64(inst["end"]),
@@ -101,12 +103,16 @@ class NativeEpoch:
         h.committee, h.coffs, h.ncomm = ptr(k["committee"]), ptr(k["coffs"]), len(k["coffs"]) - 1
         h.att_comm, h.att_shard = ptr(k["att_comm"]), ptr(k["att_shard"])
         h.nrec, h.rec_dynasty = self.nrec, ptr(k["rec_dynasty"])
+        h.layout = {"auto": 0, "index": 1}[layout]
         self.comm = comm
         self.st = ctypes.c_void_p()
         lib.call("pz_epoch_state_new", comm.h if comm is not None else None, device, ctypes.byref(h),
                  ctypes.byref(self.st))
         self._keep = None  # the library copied everything it needs
         self.nlocal = comm.nlocal if comm is not None else 1
+        co = ctypes.c_int(0)
+        lib.call("pz_epoch_state_layout", self.st, ctypes.byref(co))
+        self.committee_order = bool(co.value)
 
     def step(self):
         lib.call("pz_epoch_state_step", self.st)
@@ -121,8 +127,16 @@ class NativeEpoch:
                  ctypes.byref(s))
         return lo.value, hi.value, dev.value, s.value
 
+    def validators(self, local=0):
+        """The validator index of each balance column ``results(local)`` returns."""
+        lo, hi, _, _ = self.shard(local)
+        idx = np.empty(hi - lo, dtype=np.uint32)
+        lib.call("pz_epoch_state_validators", self.st, local, ptr(idx))
+        return idx
+
     def results(self, local=0):
-        """Host copies after the last step: (balance [B][hi-lo], scal [B][8], vote, total, winner)."""
+        """Host copies after the last step: (balance [B][hi-lo] of the validators
+        ``validators(local)`` names, scal [B][8], vote, total, winner)."""
         lo, hi, _, _ = self.shard(local)
         bal = np.empty((self.B, hi - lo), dtype=np.uint64)
         scal = np.empty((self.B, SCAL_COUNT), dtype=np.uint64)

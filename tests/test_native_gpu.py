@@ -35,24 +35,63 @@ def _check(ne, inst, steps=1):
         ne.step()
         ne.sync()
         want = [oracle_epoch(inst, b) for b in range(inst["ninst"])]
+        held = []
         for local in range(ne.nlocal):
-            lo, hi, _, _ = ne.shard(local)
+            idx = ne.validators(local)
+            held.append(idx)
             bal, scal, vote, total, win = ne.results(local)
             for b, (nb, applied, nxt, v, t, w) in enumerate(want):
                 assert bool(scal[b, _lib.SCAL_APPLIED]) == applied, (local, b)
-                np.testing.assert_array_equal(bal[b], nb[lo:hi])
+                np.testing.assert_array_equal(bal[b], nb[idx])
                 assert int(scal[b, _lib.SCAL_NEXT_BAL]) == nxt, (local, b)
                 np.testing.assert_array_equal(vote[b], v)
                 np.testing.assert_array_equal(total[b], t)
                 np.testing.assert_array_equal(win[b], w)
+        if ne.comm is None or ne.nlocal == ne.comm.world:  # every validator held exactly once
+            np.testing.assert_array_equal(np.sort(np.concatenate(held)), np.arange(inst["nval"]))
         for b, (nb, *_rest) in enumerate(want):
             inst["balance"][b] = nb
 
 
+@pytest.mark.parametrize("layout", ["auto", "index"])
 @pytest.mark.parametrize("n,B,inactive", [(65536, 3, False), (5000, 2, True), (4096, 9, False), (3000, 5, True)])
-def test_native_epoch_single_device(n, B, inactive):
+def test_native_epoch_single_device(n, B, inactive, layout):
     inst = _inst(n, B, inactive)
-    _check(NativeEpoch(inst, device=0), inst, steps=2)
+    ne = NativeEpoch(inst, device=0, layout=layout)
+    # committee order whenever every validator is active (the synthetic committees partition)
+    assert ne.committee_order == (layout == "auto" and not inactive)
+    _check(ne, inst, steps=2)
+
+
+def test_native_epoch_committee_order_fallback():
+    """A validator in two committees (the committees no longer partition the set): index order,
+    still bit-exact."""
+    inst = _inst(4096, 2, False)
+    inst["committee"] = inst["committee"].copy()
+    inst["committee"][7] = inst["committee"][8]
+    ne = NativeEpoch(inst, device=0)
+    assert not ne.committee_order
+    _check(ne, inst)
+
+
+def test_native_epoch_committee_order_short_bitfield():
+    """Committee order with a bitfield one byte short of its committee: the bitfield panic
+    (core.go:538, PZ_XLERR_BITFIELD) is raised and no balance changes, as in index order."""
+    inst = _inst(4096, 2, False)
+    for layout in ("auto", "index"):
+        k = {key: (v.copy() if isinstance(v, np.ndarray) else v) for key, v in inst.items()}
+        bo = k["boffs"].astype(np.int64)
+        cut = int(bo[3]) - 1  # drop the last byte of attestation 2 of instance 0
+        k["bits"] = np.delete(k["bits"], cut)
+        bo[3:] -= 1
+        k["boffs"] = bo.astype(np.uint64)
+        ne = NativeEpoch(k, device=0, layout=layout)
+        assert ne.committee_order == (layout == "auto")
+        ne.step()
+        bal, scal, *_ = ne.results()
+        assert scal[0, _lib.SCAL_ERR_XL] & 2, layout  # PZ_XLERR_BITFIELD
+        assert scal[0, _lib.SCAL_APPLIED] == 0
+        np.testing.assert_array_equal(bal[0], k["balance"][0][ne.validators()])
 
 
 def test_native_epoch_rccl_world1():
@@ -64,18 +103,19 @@ def test_native_epoch_rccl_world1():
 
 @pytest.mark.parametrize("world,n,B,inactive", [(2, 65536, 3, False), (2, 20000, 2, True), (3, 5000, 4, True),
                                                 (8, 20000, 1, True), (5, 3000, 7, False)])
-def test_native_epoch_sharded_loopback(world, n, B, inactive):
+@pytest.mark.parametrize("layout", ["auto", "index"])
+def test_native_epoch_sharded_loopback(world, n, B, inactive, layout):
     comm = Comm.loopback(world)
     inst = _inst(n, B, inactive)
-    _check(NativeEpoch(inst, comm=comm), inst, steps=2)
+    _check(NativeEpoch(inst, comm=comm, layout=layout), inst, steps=2)
 
 
-@pytest.mark.parametrize("inactive", [False, True])
-def test_native_epoch_configs3_world8_loopback(inactive):
+@pytest.mark.parametrize("inactive,layout", [(False, "auto"), (False, "index"), (True, "auto")])
+def test_native_epoch_configs3_world8_loopback(inactive, layout):
     """BASELINE configs[3]: 1,048,576 validators over 8 ranks (131,072 each), 65 committees per
     slot, through the library's sharded step."""
     inst = _inst(1 << 20, 2, inactive)
-    _check(NativeEpoch(inst, comm=Comm.loopback(8)), inst)
+    _check(NativeEpoch(inst, comm=Comm.loopback(8), layout=layout), inst)
 
 
 def test_native_epoch_panic_flags_sharded():
