@@ -96,9 +96,10 @@ def parse():
     p.add_argument("--epoch-path", default="native", choices=["native", "torch"],
                    help="native: pz_epoch_state (C ABI, the library's RCCL communicator); torch: DeviceEpoch "
                         "over torch.distributed (the test double of the same orchestration)")
-    p.add_argument("--epoch-layout", default="auto", choices=["auto", "index"],
+    p.add_argument("--epoch-layout", default="auto", choices=["auto", "twopass", "index"],
                    help="auto: committee order when every validator is active and the committees partition "
-                        "the set (pz_epoch_host.layout); index: validator-index order")
+                        "the set, one-pass step (pz_epoch_host.layout); twopass: that layout, two-pass step; "
+                        "index: validator-index order")
     p.add_argument("--no-replay", action="store_true")
     p.add_argument("--no-wire", action="store_true")
     p.add_argument("--no-attcheck", action="store_true")
@@ -115,7 +116,8 @@ def parse():
 # dynasty + 16 B balance read-modify-write + 1/8 B last-bitfield bit + 1/8 B committee bitfield
 # popcount + 12 B crosslink committee gather (u32 member + u64 balance).
 EPOCH_BYTES_PER_VALIDATOR = 44.25
-EPOCH_KERNELS = ("pz_epoch_count_kernel", "pz_epoch_mid_kernel", "pz_epoch_reward_kernel")
+EPOCH_KERNELS = ("pz_epoch_pre_kernel", "pz_epoch_fused_kernel", "pz_epoch_mid_kernel")  # one-pass step
+EPOCH_KERNELS_TWOPASS = ("pz_epoch_count_kernel", "pz_epoch_mid_kernel", "pz_epoch_reward_kernel")
 HASH_KERNEL = "pz_b2b_fixed_persistent_kernel"
 CPU_SAMPLE_S = 8.0  # seconds of CPU work per cpu_baseline leg (three legs: ~25 s in all)
 
@@ -188,6 +190,8 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
     units = nval * ninst * args.steps
     local_units = (hi - lo) * ninst
     achieved = local_units * EPOCH_BYTES_PER_VALIDATOR / (step_ms * 1e-3)
+    one_pass = native and de.one_pass
+    kern = EPOCH_KERNELS if one_pass else EPOCH_KERNELS_TWOPASS
     out = {
         "metric": "validator-epoch updates/s",
         "value": units / wall,
@@ -199,18 +203,23 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                                % (2 if (world == 1 and nval != 1 << 20) else 3),
                    "validators": nval, "instances_per_step": ninst, "attestations_per_instance": inst["natt"],
                    "parallelism": "validator-shard x%d + RCCL all-reduce" % world if world > 1 else "single GPU",
-                   "layout": (("committee order" if de.committee_order else "index order") if native
-                              else "index order"),
+                   "layout": (("committee order, one-pass step" if de.one_pass else
+                               "committee order, two-pass step" if de.committee_order else "index order")
+                              if native else "index order"),
                    "path": ("pz_epoch_state_step (C ABI: HIP kernels + the library's RCCL communicator)"
                             if native else "DeviceEpoch (pz_dev_epoch_* + torch.distributed collectives)")},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
-                     "traffic": (pmc_traffic(EPOCH_KERNELS) if (nval, ninst) == (65536, 256) else
-                                 pmc_traffic(EPOCH_KERNELS, PMC_SUMMARY_EPOCH_1M) if (nval, ninst) == (1 << 20, 16)
+                     "traffic": (pmc_traffic(kern) if (nval, ninst) == (65536, 256) else
+                                 pmc_traffic(kern, PMC_SUMMARY_EPOCH_1M) if (nval, ninst) == (1 << 20, 16)
                                  else None),
-                     "traffic_source": ("%s (count+mid+reward, %d x %d workload)"
-                                        % (PMC_SUMMARY if nval == 65536 else PMC_SUMMARY_EPOCH_1M, nval, ninst)),
-                     "kernel": "epoch step (count+winner+compact+reward, device time of the whole step)",
+                     "traffic_source": ("%s (%s, %d x %d workload)"
+                                        % (PMC_SUMMARY if nval == 65536 else PMC_SUMMARY_EPOCH_1M, "+".join(kern),
+                                           nval, ninst)),
+                     "kernel": ("epoch step: pz_epoch_pre (bit count) + pz_epoch_fused (one pass: classify, "
+                                "crosslink tallies, rewards, next-cycle sum) + pz_epoch_mid (winners); device "
+                                "time of the whole step" if one_pass else
+                                "epoch step (count+winner+compact+reward, device time of the whole step)"),
                      "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": local_units * EPOCH_BYTES_PER_VALIDATOR},
     }

@@ -425,6 +425,11 @@ int pz_comm_blake2b512_batch(const pz_comm* comm, const uint8_t* msgs, const uin
  *   count -> RCCL all-reduce {scal, vote, total} -> [some validator inactive: all-gather of
  *   the active masks -> global compaction] -> finish -> all-reduce of the next-cycle totals,
  * the instances split in two parts so one part's collectives overlap the other's kernels.
+ * In committee order, unless some attestation names a shard >= nrec (that panic depends on
+ * the tallies), the step is one pass over the validators instead:
+ *   bit count -> one stream (classify, crosslink tallies on the pre-reward balances, reward,
+ *   next-cycle sum) -> RCCL all-reduce {scal, vote, total} -> winners
+ * (32 B per validator-epoch instead of 40; one collective per part).
  * Results are those of pz_dev_epoch_count/finish (bit-exact with the reference; panics
  * reported in scal[PZ_SCAL_ERR_*] with the balances untouched). */
 typedef struct pz_epoch_host {
@@ -447,10 +452,12 @@ typedef struct pz_epoch_host {
   const uint64_t* rec_dynasty;     /* [B][nrec] */
   uint32_t layout;                 /* PZ_LAYOUT_AUTO: committee order when every validator is
                                       active and the committees partition the set, else index
-                                      order; PZ_LAYOUT_INDEX: always index order */
+                                      order; PZ_LAYOUT_INDEX: always index order;
+                                      PZ_LAYOUT_TWOPASS: AUTO's layout, two-pass step */
 } pz_epoch_host;
-#define PZ_LAYOUT_AUTO  0
-#define PZ_LAYOUT_INDEX 1
+#define PZ_LAYOUT_AUTO    0
+#define PZ_LAYOUT_INDEX   1
+#define PZ_LAYOUT_TWOPASS 2  /* committee order as AUTO, but the two-pass step (A/B, tests) */
 typedef struct pz_epoch_state pz_epoch_state;
 int  pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epoch_state** out);
 int  pz_epoch_state_step(pz_epoch_state* st);
@@ -467,6 +474,8 @@ int  pz_epoch_state_results(pz_epoch_state* st, int local, uint64_t* balance, ui
  * index order; the members of the committees, in committee order, in the committee-order
  * layout (pz_epoch_batch.co_index), which *committee_order reports. */
 int  pz_epoch_state_validators(const pz_epoch_state* st, int local, uint32_t* index);
+/* *committee_order: 0 index order, 1 committee order (two-pass step), 2 committee order with
+ * the one-pass step. */
 int  pz_epoch_state_layout(const pz_epoch_state* st, int* committee_order);
 void pz_epoch_state_free(pz_epoch_state* st);
 

@@ -49,4 +49,42 @@ hipError_t launch_epoch_mid(const EpochArgs& a, bool winners, bool compact, hipS
 // Pass 2: rewards (in place) + post-reward active balance sum.
 hipError_t launch_epoch_reward(const EpochArgs& a, hipStream_t s);
 
+// ---- one-pass epoch (committee-order layout, every validator active) ----------------------
+// GetAttestersTotalDeposit depends on the bitfields only and CalculateRewards' reward bit of
+// the validator at rank i == index i (every validator active) is bit co_index[p] of the last
+// bitfield, so once the bit count is known one stream over the validators classifies them,
+// adds their PRE-reward balances into the crosslink tallies of their committee, applies the
+// reward and sums the post-reward balances: 32 B per validator-epoch instead of 40.
+//   pre   : bitfield popcount -> pre[inst].pop, zero vote/total, bitfield-length panics
+//   fused : the stream above (partial sums at N > 1: all-reduce {scal, vote, total} after)
+//   mid   : winners on the (reduced) tallies
+// The host enables it only when no attestation names a shard >= nrec (that panic depends on
+// the tallies, i.e. on balances the fused pass has already rewarded).
+constexpr int kPre = 2;  // pre[inst]: {bit count, PZ_XLERR_BITFIELD if a bitfield is short}
+struct FusedCommittee {        // per (instance, committee)
+  uint64_t boff;              // bits offset of its single attestation's bitfield
+  uint32_t nbits;             // 8 * that bitfield's length
+  uint32_t ga;                // that attestation's index in the instance; 0xFFFFFFFE: no
+                              // attestation; 0xFFFFFFFF: several (catt / catt_offs list them)
+};
+struct FusedArgs {
+  const uint4* items;         // [nitems] committee pieces of this rank: {first global position,
+                              // count <= 256, committee, committee's first position}; a piece
+                              // lies in [a + 256k, a + 256(k+1)) with a = the committee's first
+                              // position & ~1, so its 16-B pairs span <= 256 positions
+  uint64_t nitems;
+  const FusedCommittee* cinfo;  // [B][ncomm]
+  const uint32_t* catt_offs;  // [B][ncomm + 1] attestations of committee c: catt[catt_offs[c] ..)
+  const uint32_t* catt;       // [B][natt] attestation index within its instance, by committee
+  uint64_t ncomm;
+  uint64_t* pre;              // [B][kPre], zero before `pre`
+  uint64_t* pre_next;         // [B][kPre] zeroed by `fused` for the next step (ping-pong)
+  int rank0;                  // 1: this rank writes the per-instance scalars (bit count, flags,
+                              //    applied, nact, max index) that the all-reduce must not multiply
+};
+hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
+hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
+bool fused_ok(const EpochArgs& a);
+int set_fused_variant(int v);  // tools/ A/B only (pz_debug_set_fused_variant)  // 16-B vector path available (nval even, 16-B aligned arrays)
+
 }  // namespace pz

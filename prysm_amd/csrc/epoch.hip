@@ -741,6 +741,288 @@ hipError_t launch_epoch_reward_mode(const EpochArgs& a, int mode, hipStream_t s)
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------
+// One-pass epoch (committee order, every validator active; epoch.h "one-pass epoch").
+// ------------------------------------------------------------------------------------------
+// Pre: [popcount blocks (B x pbpi) | one thread per attestation].  Every rank counts every
+// bitfield byte (2 MB per 16.7 M validator-epochs) so that its fused pass knows the
+// threshold without a collective; rank 0 alone reports the count in scal.
+extern "C" __global__ void __launch_bounds__(kThreads)
+pz_epoch_pre_kernel(EpochArgs a, FusedArgs f, uint64_t pbpi, uint64_t npb) {
+  __shared__ uint64_t sh[kThreads / 64];
+  const int tid = threadIdx.x;
+  if (blockIdx.x < npb) {
+    const uint64_t pb = blockIdx.x;
+    const uint64_t inst = (uint32_t)pb / (uint32_t)pbpi, chunk = (uint32_t)pb - (uint32_t)inst * (uint32_t)pbpi;
+    if (chunk == 0 && a.winner)  // the winner pass runs after the fused pass
+      for (uint32_t s = tid; s < a.nrec; s += kThreads) a.winner[inst * a.nrec + s] = 0xffffffffu;
+    const uint64_t beg = a.boffs[inst * a.natt], end = a.boffs[inst * a.natt + a.natt];
+    const uint64_t cb = beg + chunk * kPopBytesPerBlock;
+    uint64_t cnt = 0;
+    if (cb < end) {
+      const uint64_t ce = end < cb + kPopBytesPerBlock ? end : cb + kPopBytesPerBlock;
+      for (uint64_t u = (cb & ~15ull) + 16ull * tid; u < ce; u += 16ull * kThreads) {
+        if (u >= cb && u + 16 <= ce) {
+          const uint4 q = *reinterpret_cast<const uint4*>(a.bits + u);
+          cnt += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
+        } else {
+          for (uint64_t k = u < cb ? cb : u; k < u + 16 && k < ce; ++k) cnt += __popc((uint32_t)a.bits[k]);
+        }
+      }
+    }
+    const uint64_t c = block_reduce<false>(cnt, sh);
+    if (tid == 0 && c) atomicAdd((unsigned long long*)&f.pre[inst * kPre], (unsigned long long)c);
+    return;
+  }
+  // one attestation: zero its tallies (the fused pass accumulates them) and raise the
+  // processCrosslinks panic of a bitfield shorter than its committee (CheckBit at a member
+  // position >= 8*len, core.go:538-541)
+  const uint64_t ga = (uint64_t)(blockIdx.x - npb) * kThreads + tid;
+  if (ga >= (uint64_t)a.ninst * a.natt) return;
+  a.vote[ga] = 0;
+  a.total[ga] = 0;
+  const uint32_t c = a.att_comm[ga];
+  const uint64_t k = a.coffs[c + 1] - a.coffs[c];
+  if (k > 8 * (a.boffs[ga + 1] - a.boffs[ga])) {
+    const uint64_t inst = (uint32_t)ga / (uint32_t)a.natt;
+    atomicOr((unsigned long long*)&f.pre[inst * kPre + 1], (unsigned long long)kErrBitfield);
+  }
+}
+
+// Fused: one wave per committee piece (FusedArgs.items: <= 256 positions of one committee,
+// pairs 16-B aligned), kFusedWaves pieces of one instance per block; grid (B, piece groups).
+// A wave streams start, end, balance and co_index of its piece (16 B per lane per pair, every
+// load issued before anything waits), adds the pre-reward balances into its committee's
+// tallies (two wave sums, two atomics per attestation of the committee), then classifies,
+// rewards, stores and sums; the block adds its next-cycle sum with one atomic.
+constexpr int kFusedWaves = 8;
+constexpr uint32_t kNoAtt = 0xFFFFFFFEu, kManyAtt = 0xFFFFFFFFu;
+
+// MODE: an ablation knob for tools/ (0 in the product; results are wrong otherwise): bit 0 no
+// crosslink tallies, bit 1 reward bit from the balance instead of the last bitfield, bit 2 no
+// balance store, bit 3 no start/end loads (every validator taken as active), bit 4 start/end
+// loads with the default cache policy, bit 5 instance-minor grid.
+//
+// Measured choices (tools/fused_parts.py, 65,536 x 256 / 1M x 16 step, us): start/end loads
+// nontemporal (read once per step: leaving the 256 MiB Infinity Cache to the balances, which
+// are read and written) 142 -> 128 / 132 -> 122; instance-major grid (DRAM locality) -> 126 / 119.
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld16_nt(const uint64_t* p) {
+  const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+
+template <int MODE>
+__device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro,
+                                           const uint64_t* __restrict__ boffs_ro, const uint64_t* __restrict__ tdep_ro,
+                                           const uint4* __restrict__ items_ro,
+                                           const FusedCommittee* __restrict__ cinfo_ro,
+                                           const uint32_t* __restrict__ catt_offs_ro,
+                                           const uint32_t* __restrict__ catt_ro) {
+  // per wave: {attestation of its committee (single-attestation committees), total, vote, next sum, nomatch}
+  __shared__ uint64_t xt[kFusedWaves], xv[kFusedWaves], xs[kFusedWaves], xn[kFusedWaves];
+  __shared__ uint32_t xg[kFusedWaves];
+  const uint64_t inst = (MODE & 32) ? blockIdx.x : blockIdx.y;
+  const uint64_t grp = (MODE & 32) ? blockIdx.y : blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t item = grp * kFusedWaves + wave;
+  const uint64_t pop = pre_ro[inst * kPre], ferr = pre_ro[inst * kPre + 1];
+  const uint64_t lb = boffs_ro[inst * a.natt + a.natt - 1];
+  const uint64_t L = boffs_ro[inst * a.natt + a.natt] - lb;
+  const bool thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (tdep_ro[inst] * 2ull);  // incentives.go:18-20
+  const bool rwd_err = (a.nval_global - 1) >= 8 * L;  // CheckBit(last, N-1) panics (incentives.go:23)
+  const bool skip = ferr != 0 || (thr && rwd_err);     // Go panics: balances stay untouched
+  const bool applied = thr && !skip;
+  uint64_t sum = 0, nm = 0, ts = 0, vs = 0;
+  uint32_t g1 = kNoAtt;  // the wave's single attestation, combined across the block below
+  if (item < f.nitems) {
+    const uint4 it = items_ro[item];  // {first position, count, committee, committee start}
+    const uint64_t ws = it.x, we = (uint64_t)it.x + it.y, cb = it.w;
+    const uint64_t p0 = (ws & ~1ull) - a.val_offset;  // local, even (val_offset is 64-aligned)
+    uint64_t* Bal = a.balance + inst * a.nval;
+    const uint64_t* S = a.start + inst * a.nval;
+    const uint64_t* E = a.end + inst * a.nval;
+    const FusedCommittee ci = cinfo_ro[inst * f.ncomm + it.z];
+    uint4 qb[2], qs[2], qe[2];
+    uint2 cix[2];
+    uint32_t by0[2], by1[2];  // the committee bitfield bytes holding each element's bit
+    bool v0[2], v1[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint64_t p = p0 + (uint64_t)j * 128 + 2 * lane, g = a.val_offset + p;
+      v0[j] = g >= ws && g < we;
+      v1[j] = g + 1 >= ws && g + 1 < we;
+      const uint64_t pp = (v0[j] || v1[j]) ? p : p0;
+      qb[j] = *reinterpret_cast<const uint4*>(Bal + pp);
+      if (MODE & 8) {
+        qs[j] = make_uint4(0, 0, 0, 0);
+        qe[j] = make_uint4(~0u, ~0u, ~0u, ~0u);
+      } else if (MODE & 16) {
+        qs[j] = *reinterpret_cast<const uint4*>(S + pp);
+        qe[j] = *reinterpret_cast<const uint4*>(E + pp);
+      } else {
+        qs[j] = ld16_nt(S + pp);
+        qe[j] = ld16_nt(E + pp);
+      }
+      cix[j] = (MODE & 2) ? make_uint2(0, 0) : *reinterpret_cast<const uint2*>(a.co_index + pp);
+      // branch-free, clamped: issued with the stream loads (bits past the bitfield are masked
+      // below; the pre pass has raised that panic)
+      by0[j] = by1[j] = 0;
+      if (!(MODE & 1) && ci.ga < kNoAtt && ci.nbits) {
+        const uint64_t q = g - cb, last = ci.nbits - 1;
+        by0[j] = a.bits[ci.boff + ((q < last ? q : last) >> 3)];
+        by1[j] = a.bits[ci.boff + ((q + 1 < last ? q + 1 : last) >> 3)];
+      }
+    }
+    // crosslink tallies on the pre-reward balances (core.go:533-545): position g of the
+    // committee is bit g - cb of each of its attestations' bitfields
+    if (!(MODE & 1) && ci.ga != kNoAtt) {
+      uint64_t t = 0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        t += (v0[j] ? pack64(qb[j].x, qb[j].y) : 0) + (v1[j] ? pack64(qb[j].z, qb[j].w) : 0);
+      ts = wave_sum(t);
+      if (ci.ga != kManyAtt) {
+        uint64_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const uint64_t q = a.val_offset + p0 + (uint64_t)j * 128 + 2 * lane - cb;
+          if (v0[j] && q < ci.nbits && ((by0[j] >> (7 - (uint32_t)(q & 7))) & 1)) v += pack64(qb[j].x, qb[j].y);
+          if (v1[j] && q + 1 < ci.nbits && ((by1[j] >> (7 - (uint32_t)((q + 1) & 7))) & 1))
+            v += pack64(qb[j].z, qb[j].w);
+        }
+        vs = wave_sum(v);
+        g1 = ci.ga;
+      } else {  // several attestations of this committee: direct atomics per attestation
+        const uint32_t* co = catt_offs_ro + inst * (f.ncomm + 1);
+        for (uint32_t k = co[it.z]; k < co[it.z + 1]; ++k) {
+          const uint64_t ga = catt_ro[inst * a.natt + k];
+          const uint64_t boff = boffs_ro[inst * a.natt + ga];
+          const uint64_t nbits = 8 * (boffs_ro[inst * a.natt + ga + 1] - boff);
+          const uint8_t* bf = a.bits + boff;
+          uint64_t v = 0;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const uint64_t q = a.val_offset + p0 + (uint64_t)j * 128 + 2 * lane - cb;
+            if (v0[j] && q < nbits && bit_at(bf, q)) v += pack64(qb[j].x, qb[j].y);
+            if (v1[j] && q + 1 < nbits && bit_at(bf, q + 1)) v += pack64(qb[j].z, qb[j].w);
+          }
+          v = wave_sum(v);
+          if (lane < 2) {  // one instruction: lane 0 the total, lane 1 the vote
+            uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + ga;
+            const uint64_t x = lane ? v : ts;
+            if (x) atomicAdd((unsigned long long*)dst, (unsigned long long)x);
+          }
+        }
+      }
+    }
+    // classify (validator.go:45-53), reward (incentives.go:22-27), store, sum (core.go:459-464)
+    const uint64_t d = a.dynasty[inst];
+    const uint8_t* lastbf = a.bits + lb;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint64_t p = p0 + (uint64_t)j * 128 + 2 * lane;
+      uint64_t b0 = pack64(qb[j].x, qb[j].y), b1 = pack64(qb[j].z, qb[j].w);
+      const bool a0 = pack64(qs[j].x, qs[j].y) <= d && d < pack64(qe[j].x, qe[j].y);
+      const bool a1 = pack64(qs[j].z, qs[j].w) <= d && d < pack64(qe[j].z, qe[j].w);
+      nm += (v0[j] && !a0 ? 1 : 0) + (v1[j] && !a1 ? 1 : 0);
+      if (applied) {  // every validator active: rank == index, the validator at p is co_index[p]
+        const bool r0 = (MODE & 2) ? (b0 & 1) : bit_at(lastbf, cix[j].x);
+        const bool r1 = (MODE & 2) ? (b1 & 1) : bit_at(lastbf, cix[j].y);
+        b0 = r0 ? b0 + PZ_ATTESTER_REWARD : b0 - PZ_ATTESTER_REWARD;
+        b1 = r1 ? b1 + PZ_ATTESTER_REWARD : b1 - PZ_ATTESTER_REWARD;
+        if (MODE & 4)
+          ;
+        else if (v0[j] && v1[j])
+          *reinterpret_cast<uint4*>(Bal + p) =
+              make_uint4((uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32));
+        else if (v0[j])
+          Bal[p] = b0;
+        else if (v1[j])
+          Bal[p + 1] = b1;
+      }
+      sum += (v0[j] && a0 ? b0 : 0) + (v1[j] && a1 ? b1 : 0);
+    }
+  }
+  sum = wave_sum(sum);
+  nm = wave_sum(nm);
+  if (lane == 0) {
+    xg[wave] = g1;
+    xt[wave] = ts;
+    xv[wave] = vs;
+    xs[wave] = sum;
+    xn[wave] = nm;
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  // Wave 0 adds the block's tallies: consecutive pieces of one committee are merged, and one
+  // atomic instruction carries every total (lanes 0-7) and vote (lanes 8-15).
+  if (lane < 2 * kFusedWaves) {
+    const int e = lane & (kFusedWaves - 1);
+    const uint32_t g = xg[e];
+    if (g < kNoAtt && (e == 0 || xg[e - 1] != g)) {  // head of a run of equal attestations
+      uint64_t x = 0;
+      for (int k = e; k < kFusedWaves && xg[k] == g; ++k) x += lane < kFusedWaves ? xt[k] : xv[k];
+      uint64_t* dst = (lane < kFusedWaves ? a.total : a.vote) + inst * a.natt + g;
+      if (x) atomicAdd((unsigned long long*)dst, (unsigned long long)x);
+    }
+  }
+  uint64_t* sc = a.scal + inst * kScal;
+  if (lane == 0) {
+    uint64_t s = 0, nmt = 0;
+    for (int w = 0; w < kFusedWaves; ++w) {
+      s += xs[w];
+      nmt += xn[w];
+    }
+    if (s && !skip) atomicAdd((unsigned long long*)&sc[kNextBal], (unsigned long long)s);
+    if (nmt) {  // the layout's rank == index premise is broken (the state never allows it)
+      atomicAdd((unsigned long long*)&sc[kNoMatch], (unsigned long long)nmt);
+      atomicOr((unsigned long long*)&sc[kErrXl], (unsigned long long)kErrLayout);
+    }
+    if (grp == 0 && f.rank0) {
+      sc[kPop] = pop;
+      sc[kApplied] = applied ? 1 : 0;
+      sc[kNact] = a.nval_global;
+      sc[kMaxIdx1] = a.nval_global;
+      sc[kErrRwd] = rwd_err ? 1 : 0;
+      if (ferr) atomicAdd((unsigned long long*)&sc[kErrXl], (unsigned long long)ferr);
+    }
+  }
+  if (grp == 0) {
+    if (a.scal_next && lane < kScal) a.scal_next[inst * kScal + lane] = 0;
+    if (lane < kPre) f.pre_next[inst * kPre + lane] = 0;
+  }
+}
+
+#define PZ_FUSED_KERNEL(NAME, MODE)                                                                       \
+  extern "C" __global__ void __launch_bounds__(64 * kFusedWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) \
+  NAME(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro, const uint64_t* __restrict__ boffs_ro, \
+       const uint64_t* __restrict__ tdep_ro, const uint4* __restrict__ items_ro,                             \
+       const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,              \
+       const uint32_t* __restrict__ catt_ro) {                                                             \
+    fused_body<MODE>(a, f, pre_ro, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);          \
+  }
+PZ_FUSED_KERNEL(pz_epoch_fused_kernel, 0)
+PZ_FUSED_KERNEL(pz_epoch_fused_dbg1_kernel, 1)
+PZ_FUSED_KERNEL(pz_epoch_fused_dbg2_kernel, 2)
+PZ_FUSED_KERNEL(pz_epoch_fused_dbg3_kernel, 3)
+PZ_FUSED_KERNEL(pz_epoch_fused_dbg4_kernel, 4)
+PZ_FUSED_KERNEL(pz_epoch_fused_dbg7_kernel, 7)
+PZ_FUSED_KERNEL(pz_epoch_fused_dbg8_kernel, 8)
+PZ_FUSED_KERNEL(pz_epoch_fused_dbg15_kernel, 15)
+PZ_FUSED_KERNEL(pz_epoch_fused_dbg16_kernel, 16)
+PZ_FUSED_KERNEL(pz_epoch_fused_dbg32_kernel, 32)
+PZ_FUSED_KERNEL(pz_epoch_fused_dbg48_kernel, 48)
+#undef PZ_FUSED_KERNEL
+
+static int g_fused_variant = 0;  // tools/ A/B only
+int set_fused_variant(int v) {
+  const int old = g_fused_variant;
+  g_fused_variant = v;
+  return old;
+}
+
 // ---- launchers ---------------------------------------------------------------------------
 static bool vec_ok(const EpochArgs& a) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
@@ -805,6 +1087,46 @@ hipError_t launch_epoch_reward(const EpochArgs& a, hipStream_t s) {
   if (!blocks) return hipSuccess;
   hipLaunchKernelGGL(pz_epoch_reward_kernel, dim3(a.ninst, (uint32_t)vbpi), dim3(kThreads), 0, s, a, vbpi,
                      vec_ok(a) ? 1 : 0, a.scal, a.boffs, a.total_deposit);
+  return hipGetLastError();
+}
+
+bool fused_ok(const EpochArgs& a) {
+  return vec_ok(a) && a.co_index && a.natt && (reinterpret_cast<uintptr_t>(a.co_index) & 7) == 0;
+}
+
+hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
+  uint64_t pbpi = (a.max_inst_bytes + kPopBytesPerBlock - 1) / kPopBytesPerBlock;
+  if (pbpi == 0) pbpi = 1;  // chunk 0 of each instance also resets the winners
+  const uint64_t npb = (uint64_t)a.ninst * pbpi;
+  const uint64_t nab = ((uint64_t)a.ninst * a.natt + kThreads - 1) / kThreads;
+  if (!a.ninst || !a.natt) return hipSuccess;
+  hipLaunchKernelGGL(pz_epoch_pre_kernel, dim3((uint32_t)(npb + nab)), dim3(kThreads), 0, s, a, f, pbpi, npb);
+  return hipGetLastError();
+}
+
+hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
+  if (!a.ninst) return hipSuccess;
+  const uint64_t groups = (f.nitems + kFusedWaves - 1) / kFusedWaves;
+  if (!groups) return hipSuccess;
+  // instance-major: x = piece group, y = instance (ablation 32: instance-minor)
+  const dim3 grid = (g_fused_variant & 32) ? dim3(a.ninst, (uint32_t)groups) : dim3((uint32_t)groups, a.ninst);
+  const dim3 block(64 * kFusedWaves);
+#define PZ_LAUNCH_FUSED(K) \
+  hipLaunchKernelGGL(K, grid, block, 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt)
+  switch (g_fused_variant) {
+    case 1: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg1_kernel); break;
+    case 2: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg2_kernel); break;
+    case 3: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg3_kernel); break;
+    case 4: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg4_kernel); break;
+    case 7: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg7_kernel); break;
+    case 8: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg8_kernel); break;
+    case 15: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg15_kernel); break;
+    case 16: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg16_kernel); break;
+    case 32: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg32_kernel); break;
+    case 48: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg48_kernel); break;
+    default: PZ_LAUNCH_FUSED(pz_epoch_fused_kernel);
+  }
+#undef PZ_LAUNCH_FUSED
   return hipGetLastError();
 }
 

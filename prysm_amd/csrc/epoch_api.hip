@@ -506,6 +506,7 @@ int set_count_variant(int v);
 }
 // Internal: select the count-pass variant for in-process A/B timing (tools/epoch_parts.py).
 extern "C" int pz_debug_set_count_variant(int v) { return pz::set_count_variant(v); }
+extern "C" int pz_debug_set_fused_variant(int v) { return pz::set_fused_variant(v); }
 extern "C" int pz_debug_epoch_reward_mode(const pz_epoch_batch* b, int mode, void* stream) {
   hipError_t e = pz::launch_epoch_reward_mode(*b, mode, (hipStream_t)stream);
   return e == hipSuccess ? PZ_OK : pz::hip_fail(e, "pz_epoch_reward_kernel (mode)");

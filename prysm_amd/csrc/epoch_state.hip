@@ -42,6 +42,7 @@ struct Part {
   uint64_t* nb = nullptr;                 // [B] next-cycle totals, contiguous for the all-reduce
   hipEvent_t ev_red = nullptr, ev_gather = nullptr, ev_nb = nullptr;
   EpochArgs a;
+  FusedArgs f;                            // one-pass step (pz_epoch_state::fused)
 };
 
 struct Shard {
@@ -61,6 +62,7 @@ struct pz_epoch_state {
   uint64_t N = 0, sw = 0, ncomm = 0;
   bool general = false, all_active = true;
   bool co = false;                 // committee-order layout (see pz_epoch_batch.co_index)
+  bool fused = false;              // one-pass step (epoch.h "one-pass epoch") on that layout
   std::vector<uint32_t> co_inv;    // storage position -> validator index (committee order)
   uint64_t steps = 0;
   std::vector<Shard> sh;
@@ -120,6 +122,13 @@ int step_world1(pz_epoch_state* st) {
     (void)hipSetDevice(s.dev);
     for (uint32_t p = 0; p < st->nparts; ++p) {
       EpochArgs& a = s.part[p].a;
+      if (st->fused) {
+        hipError_t e = launch_epoch_pre(a, s.part[p].f, s.s);
+        if (e == hipSuccess) e = launch_epoch_fused(a, s.part[p].f, s.s);
+        if (e == hipSuccess) e = launch_epoch_mid(a, st->nrec != 0, false, s.s);
+        if (e != hipSuccess) return hip_fail(e, "epoch step (one pass)");
+        continue;
+      }
       hipError_t e = launch_epoch_count(a, true, true, a.natt != 0, s.s);
       if (e == hipSuccess) e = launch_epoch_mid(a, a.natt && st->nrec, true, s.s);
       if (e == hipSuccess) e = launch_epoch_reward(a, s.s);
@@ -140,6 +149,9 @@ void flip(pz_epoch_state* st) {
       q.a.vote = q.red[q.cur] + Bp * kScal;
       q.a.total = q.red[q.cur] + Bp * kScal + Bp * natt;
       q.a.scal_next = q.red[q.cur ^ 1];
+      const uint64_t pre = Bp * kScal + 2 * Bp * natt;  // after {scal, vote, total}: not all-reduced
+      q.f.pre = q.red[q.cur] + pre;
+      q.f.pre_next = q.red[q.cur ^ 1] + pre;
     }
 }
 
@@ -149,7 +161,41 @@ int wait(Shard& s, hipEvent_t ev) {
   return e == hipSuccess ? PZ_OK : hip_fail(e, "hipStreamWaitEvent");
 }
 
+// One-pass step at N > 1: every part's pre + fused pass, each followed by the all-reduce of
+// its partial sums (the next-cycle totals are among them), then the winners.
+int step_sharded_fused(pz_epoch_state* st) {
+  pz_comm* c = st->comm;
+  const int L = (int)st->sh.size();
+  std::vector<hipStream_t> streams(L);
+  std::vector<uint64_t*> bufs(L);
+  std::vector<hipEvent_t> evs(L);
+  for (int i = 0; i < L; ++i) streams[i] = st->sh[i].s;
+  int rc;
+  for (uint32_t p = 0; p < st->nparts; ++p) {
+    for (int i = 0; i < L; ++i) {
+      Shard& s = st->sh[i];
+      (void)hipSetDevice(s.dev);
+      hipError_t e = launch_epoch_pre(s.part[p].a, s.part[p].f, s.s);
+      if (e == hipSuccess) e = launch_epoch_fused(s.part[p].a, s.part[p].f, s.s);
+      if (e != hipSuccess) return hip_fail(e, "epoch one-pass");
+      bufs[i] = s.part[p].red[s.part[p].cur];
+      evs[i] = s.part[p].ev_red;
+    }
+    const uint64_t Bp = st->sh[0].part[p].B;
+    if ((rc = c->allreduce_u64(bufs.data(), Bp * kScal + 2 * Bp * st->natt, streams.data(), evs.data()))) return rc;
+  }
+  for (uint32_t p = 0; p < st->nparts; ++p)
+    for (int i = 0; i < L; ++i) {
+      Shard& s = st->sh[i];
+      if ((rc = wait(s, s.part[p].ev_red))) return rc;
+      hipError_t e = launch_epoch_mid(s.part[p].a, st->nrec != 0, false, s.s);
+      if (e != hipSuccess) return hip_fail(e, "epoch winners");
+    }
+  return PZ_OK;
+}
+
 int step_sharded(pz_epoch_state* st) {
+  if (st->fused) return step_sharded_fused(st);
   pz_comm* c = st->comm;
   const int L = (int)st->sh.size();
   std::vector<hipStream_t> streams(L);
@@ -313,7 +359,7 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
   st->general = !st->all_active && st->world > 1;
   // Committee order when every validator is active and the committees partition [0, N):
   // the crosslink tallies then stream contiguous balances instead of gathering them.
-  if (st->all_active && h->natt && h->layout == PZ_LAYOUT_AUTO && h->coffs[h->ncomm] == st->N) {
+  if (st->all_active && h->natt && h->layout != PZ_LAYOUT_INDEX && h->coffs[h->ncomm] == st->N) {
     std::vector<uint8_t> seen(st->N, 0);
     bool part = true;
     for (uint64_t k = 0; k < st->N && part; ++k) {
@@ -325,6 +371,43 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
       st->co = true;
       st->co_inv.assign(h->committee, h->committee + st->N);
     }
+  }
+  // One pass needs every shard on the 16-B path (N even) and no shard panic (it depends on the
+  // tallies, which the one pass forms while it rewards).
+  if (st->co && h->layout == PZ_LAYOUT_AUTO && st->N % 2 == 0) {
+    st->fused = true;
+    for (uint64_t i = 0; i < (uint64_t)st->B * st->natt && st->fused; ++i) st->fused = h->att_shard[i] < st->nrec;
+  }
+  // attestations by committee, per instance (the one pass adds a committee's slice into each)
+  std::vector<uint32_t> catt_offs, catt;
+  std::vector<FusedCommittee> cinfo;
+  if (st->fused) {
+    const uint64_t nc1 = st->ncomm + 1;
+    catt_offs.assign((size_t)st->B * nc1, 0);
+    catt.resize((size_t)st->B * st->natt);
+    for (uint64_t b = 0; b < st->B; ++b) {
+      uint32_t* o = catt_offs.data() + b * nc1;
+      const uint32_t* ac = h->att_comm + b * st->natt;
+      for (uint64_t g = 0; g < st->natt; ++g) ++o[ac[g] + 1];
+      for (uint64_t k = 0; k < st->ncomm; ++k) o[k + 1] += o[k];
+      std::vector<uint32_t> fill(o, o + st->ncomm);
+      for (uint64_t g = 0; g < st->natt; ++g) catt[b * st->natt + fill[ac[g]]++] = (uint32_t)g;
+    }
+    cinfo.resize((size_t)st->B * st->ncomm);
+    for (uint64_t b = 0; b < st->B; ++b)
+      for (uint64_t c = 0; c < st->ncomm; ++c) {
+        const uint32_t* o = catt_offs.data() + b * nc1;
+        FusedCommittee& ci = cinfo[b * st->ncomm + c];
+        ci.boff = 0;
+        ci.nbits = 0;
+        ci.ga = o[c + 1] - o[c] == 0 ? 0xFFFFFFFEu : 0xFFFFFFFFu;
+        if (o[c + 1] - o[c] == 1) {
+          const uint64_t g = catt[b * st->natt + o[c]], ga = b * st->natt + g;
+          ci.ga = (uint32_t)g;
+          ci.boff = h->boffs[ga];
+          ci.nbits = (uint32_t)(8 * (h->boffs[ga + 1] - h->boffs[ga]));
+        }
+      }
   }
   st->nparts = (st->world > 1 && st->B >= 2) ? 2 : 1;
   const int nlocal = comm ? comm->nlocal : 1;
@@ -392,6 +475,28 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
       if (st->world > 1 && !st->co && (rc = upload(s, &cpos, pos.data(), pos.size()))) break;
     }
     if (st->nrec && (rc = upload(s, &recd, h->rec_dynasty, (size_t)st->B * st->nrec))) break;
+    uint32_t *d_catt_offs = nullptr, *d_catt = nullptr;
+    uint4* d_items = nullptr;
+    FusedCommittee* d_cinfo = nullptr;
+    uint64_t nitems = 0;
+    if (st->fused) {
+      // committee pieces inside [lo, hi): <= 256 positions, aligned to the committee's even base
+      std::vector<uint4> items;
+      for (uint64_t c = 0; c < st->ncomm; ++c) {
+        const uint64_t cb = h->coffs[c], ce = h->coffs[c + 1];
+        const uint64_t r0 = std::max(cb, s.lo), r1 = std::min(ce, s.hi), base = cb & ~1ull;
+        for (uint64_t x = r0; x < r1;) {
+          const uint64_t y = std::min(r1, base + ((x - base) / 256 + 1) * 256);
+          items.push_back(make_uint4((uint32_t)x, (uint32_t)(y - x), (uint32_t)c, (uint32_t)cb));
+          x = y;
+        }
+      }
+      nitems = items.size();
+      if ((rc = upload(s, &d_items, items.data(), items.size())) || (rc = upload(s, &d_cinfo, cinfo.data(), cinfo.size())) ||
+          (rc = upload(s, &d_catt_offs, catt_offs.data(), catt_offs.size())) ||
+          (rc = upload(s, &d_catt, catt.data(), catt.size())))
+        break;
+    }
     if ((rc = dalloc(s, &winner, (size_t)st->B * std::max<uint32_t>(st->nrec, 1))) ||
         (rc = dalloc(s, &act_mask, (size_t)st->B * std::max<uint64_t>(s.wl, 1))) ||
         (rc = dalloc(s, &blk_cnt, (size_t)st->B * (vbpi + 1))) ||
@@ -402,7 +507,7 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
       q.i0 = st->B * p / st->nparts;
       q.B = st->B * (p + 1) / st->nparts - q.i0;
       const uint64_t Bp = q.B, i0 = q.i0;
-      for (int k = 0; k < 2 && !rc; ++k) rc = dalloc(s, &q.red[k], Bp * kScal + 2 * Bp * st->natt);
+      for (int k = 0; k < 2 && !rc; ++k) rc = dalloc(s, &q.red[k], Bp * kScal + 2 * Bp * st->natt + Bp * kPre);
       if (rc) break;
       if (st->general && ((rc = dalloc(s, &q.mask_send, Bp * st->sw)) ||
                           (rc = dalloc(s, &q.gmask, (size_t)st->world * Bp * st->sw)) ||
@@ -448,6 +553,17 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
       a.act_mask = act_mask + i0 * std::max<uint64_t>(s.wl, 1);
       a.blk_cnt = blk_cnt + i0 * (vbpi + 1);
       a.act_list = st->all_active ? act_list : act_list + i0 * st->N;
+      std::memset(&q.f, 0, sizeof q.f);
+      if (st->fused) {
+        q.f.items = d_items;
+        q.f.nitems = nitems;
+        q.f.cinfo = d_cinfo + i0 * st->ncomm;
+        q.f.catt_offs = d_catt_offs + i0 * (st->ncomm + 1);
+        q.f.catt = d_catt + i0 * st->natt;
+        q.f.ncomm = st->ncomm;
+        q.f.rank0 = s.grank == 0 ? 1 : 0;
+        if (!fused_ok(a)) rc = fail(PZ_EINVAL, "one-pass epoch: validator arrays not on the 16-B path");
+      }
       q.cur = 1;  // flip() below binds red[0] as the first step's buffer
     }
   }
@@ -532,7 +648,7 @@ int pz_epoch_state_validators(const pz_epoch_state* st, int local, uint32_t* ind
 
 int pz_epoch_state_layout(const pz_epoch_state* st, int* committee_order) {
   if (!st || !committee_order) return fail(PZ_EINVAL, "null pointer");
-  *committee_order = st->co ? 1 : 0;
+  *committee_order = st->fused ? 2 : st->co ? 1 : 0;
   return PZ_OK;
 }
 

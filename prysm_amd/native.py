@@ -84,7 +84,8 @@ class NativeEpoch:
 
     def __init__(self, inst, device=0, comm=None, layout="auto"):
         """``layout``: "auto" (committee order when every validator is active and the
-        committees partition the set) or "index"."""
+        committees partition the set, with the one-pass step when no attestation names a
+        shard >= nrec), "twopass" (the same layout, two-pass step) or "index"."""
         u64 = lambda a: np.ascontiguousarray(a, dtype=np.uint64)  # noqa: E731
         u32 = lambda a: np.ascontiguousarray(a, dtype=np.uint32)  # noqa: E731
         self._keep = k = dict(balance=u64(inst["balance"]), start=u64(inst["start"]), end=u64(inst["end"]),
@@ -103,7 +104,7 @@ class NativeEpoch:
         h.committee, h.coffs, h.ncomm = ptr(k["committee"]), ptr(k["coffs"]), len(k["coffs"]) - 1
         h.att_comm, h.att_shard = ptr(k["att_comm"]), ptr(k["att_shard"])
         h.nrec, h.rec_dynasty = self.nrec, ptr(k["rec_dynasty"])
-        h.layout = {"auto": 0, "index": 1}[layout]
+        h.layout = {"auto": 0, "index": 1, "twopass": 2}[layout]
         self.comm = comm
         self.st = ctypes.c_void_p()
         lib.call("pz_epoch_state_new", comm.h if comm is not None else None, device, ctypes.byref(h),
@@ -113,6 +114,7 @@ class NativeEpoch:
         co = ctypes.c_int(0)
         lib.call("pz_epoch_state_layout", self.st, ctypes.byref(co))
         self.committee_order = bool(co.value)
+        self.one_pass = co.value == 2
 
     def step(self):
         lib.call("pz_epoch_state_step", self.st)

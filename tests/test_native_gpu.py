@@ -11,6 +11,7 @@ import hashlib
 import numpy as np
 import pytest
 
+from oracle import epoch_np as onp
 from oracle import ref
 from prysm_amd import _lib, casper, synth
 from prysm_amd.native import Comm, NativeEpoch
@@ -20,9 +21,9 @@ from epoch_ref_helpers import oracle_epoch
 pytestmark = pytest.mark.gpu
 
 
-def _inst(n, B, inactive, seed=5):
+def _inst(n, B, inactive, seed=5, **kw):
     shuffled = casper.shuffle_indices(ref.bytes_to_hash(b"A"), np.arange(n, dtype=np.uint32))
-    inst = synth.epoch_batch(n, B, seed=seed, shuffled=shuffled)
+    inst = synth.epoch_batch(n, B, seed=seed, shuffled=shuffled, **kw)
     if inactive:  # rank != index: the compaction / gathered-mask path
         rng = np.random.default_rng(1)
         inst["start"][:, rng.random(n) < 0.1] = 7
@@ -53,14 +54,70 @@ def _check(ne, inst, steps=1):
             inst["balance"][b] = nb
 
 
-@pytest.mark.parametrize("layout", ["auto", "index"])
-@pytest.mark.parametrize("n,B,inactive", [(65536, 3, False), (5000, 2, True), (4096, 9, False), (3000, 5, True)])
+LAYOUTS = ["auto", "twopass", "index"]
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+@pytest.mark.parametrize("n,B,inactive", [(65536, 3, False), (5000, 2, True), (4096, 9, False), (3000, 5, True),
+                                          (4097, 2, False), (1000, 3, False), (130, 2, False)])
 def test_native_epoch_single_device(n, B, inactive, layout):
     inst = _inst(n, B, inactive)
     ne = NativeEpoch(inst, device=0, layout=layout)
-    # committee order whenever every validator is active (the synthetic committees partition)
-    assert ne.committee_order == (layout == "auto" and not inactive)
+    # committee order whenever every validator is active (the synthetic committees partition);
+    # the one-pass step on it when N is even (16-B lanes) and every shard id is in range
+    assert ne.committee_order == (layout != "index" and not inactive)
+    assert ne.one_pass == (layout == "auto" and not inactive and n % 2 == 0)
     _check(ne, inst, steps=2)
+
+
+@pytest.mark.parametrize("density", [0.5, 0.75])
+def test_native_epoch_one_pass_threshold(density):
+    """Half the bits set: GetAttestersTotalDeposit stays under 2/3 of TotalDeposits, so no
+    reward is applied (incentives.go:18-20) while the tallies and winners still form."""
+    inst = _inst(8192, 4, False, density=density)
+    ne = NativeEpoch(inst, device=0)
+    assert ne.one_pass
+    _check(ne, inst, steps=2)
+
+
+def test_native_epoch_one_pass_reward_panic():
+    """The last bitfield shorter than the validator set with the threshold met: CheckBit(last,
+    N-1) panics in CalculateRewards (incentives.go:23): PZ_SCAL_ERR_RWD, balances untouched, in
+    every layout."""
+    n = 4096
+    inst = _inst(n, 3, False, last_bits=n - 8)
+    for layout in LAYOUTS:
+        k = {key: (v.copy() if isinstance(v, np.ndarray) else v) for key, v in inst.items()}
+        ne = NativeEpoch(k, device=0, layout=layout)
+        assert ne.one_pass == (layout == "auto")
+        ne.step()
+        bal, scal, vote, total, _ = ne.results()
+        for b in range(3):
+            assert scal[b, _lib.SCAL_ERR_RWD] != 0, (layout, b)
+            assert scal[b, _lib.SCAL_APPLIED] == 0, (layout, b)
+            np.testing.assert_array_equal(bal[b], k["balance"][b][ne.validators()])
+            natt = k["natt"]  # the tallies are formed before the panic
+            v, t = onp.crosslink_tallies(k["committee"], k["coffs"], k["att_comm"][b * natt:(b + 1) * natt],
+                                         k["bits"], k["boffs"][b * natt:(b + 1) * natt + 1], k["balance"][b])
+            np.testing.assert_array_equal(vote[b], v)
+            np.testing.assert_array_equal(total[b], t)
+
+
+def test_native_epoch_shard_out_of_range_two_pass():
+    """An attestation naming a shard >= nrec: that processCrosslinks panic depends on the
+    tallies (core.go:549), so the state keeps the two-pass step; with the vote under 2/3 there
+    is no panic and the step is bit-exact."""
+    inst = _inst(4096, 2, False)
+    inst["att_shard"] = inst["att_shard"].copy()
+    inst["att_shard"][0] = 5000  # > nrec (1024); its committee's vote must fail the threshold
+    natt = inst["natt"]
+    bo = inst["boffs"]
+    inst["bits"] = inst["bits"].copy()
+    inst["bits"][int(bo[0]):int(bo[1])] = 0
+    ne = NativeEpoch(inst, device=0)
+    assert ne.committee_order and not ne.one_pass
+    _check(ne, inst)
+    assert natt > 1
 
 
 def test_native_epoch_committee_order_fallback():
@@ -78,7 +135,7 @@ def test_native_epoch_committee_order_short_bitfield():
     """Committee order with a bitfield one byte short of its committee: the bitfield panic
     (core.go:538, PZ_XLERR_BITFIELD) is raised and no balance changes, as in index order."""
     inst = _inst(4096, 2, False)
-    for layout in ("auto", "index"):
+    for layout in LAYOUTS:
         k = {key: (v.copy() if isinstance(v, np.ndarray) else v) for key, v in inst.items()}
         bo = k["boffs"].astype(np.int64)
         cut = int(bo[3]) - 1  # drop the last byte of attestation 2 of instance 0
@@ -86,7 +143,8 @@ def test_native_epoch_committee_order_short_bitfield():
         bo[3:] -= 1
         k["boffs"] = bo.astype(np.uint64)
         ne = NativeEpoch(k, device=0, layout=layout)
-        assert ne.committee_order == (layout == "auto")
+        assert ne.committee_order == (layout != "index")
+        assert ne.one_pass == (layout == "auto")
         ne.step()
         bal, scal, *_ = ne.results()
         assert scal[0, _lib.SCAL_ERR_XL] & 2, layout  # PZ_XLERR_BITFIELD
@@ -103,19 +161,44 @@ def test_native_epoch_rccl_world1():
 
 @pytest.mark.parametrize("world,n,B,inactive", [(2, 65536, 3, False), (2, 20000, 2, True), (3, 5000, 4, True),
                                                 (8, 20000, 1, True), (5, 3000, 7, False)])
-@pytest.mark.parametrize("layout", ["auto", "index"])
+@pytest.mark.parametrize("layout", LAYOUTS)
 def test_native_epoch_sharded_loopback(world, n, B, inactive, layout):
     comm = Comm.loopback(world)
     inst = _inst(n, B, inactive)
     _check(NativeEpoch(inst, comm=comm, layout=layout), inst, steps=2)
 
 
-@pytest.mark.parametrize("inactive,layout", [(False, "auto"), (False, "index"), (True, "auto")])
+@pytest.mark.parametrize("inactive,layout", [(False, "auto"), (False, "twopass"), (False, "index"), (True, "auto")])
 def test_native_epoch_configs3_world8_loopback(inactive, layout):
     """BASELINE configs[3]: 1,048,576 validators over 8 ranks (131,072 each), 65 committees per
     slot, through the library's sharded step."""
     inst = _inst(1 << 20, 2, inactive)
     _check(NativeEpoch(inst, comm=Comm.loopback(8), layout=layout), inst)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_native_epoch_one_pass_bitfield_panic_sharded(world):
+    """A short bitfield under the sharded one-pass step: the flag (raised once, by rank 0's
+    pre pass) survives the all-reduce and no rank changes a balance."""
+    inst = _inst(4096, 3, False)
+    bo = inst["boffs"].astype(np.int64)
+    natt = inst["natt"]
+    cut = int(bo[natt + 4]) - 1  # instance 1, attestation 3
+    inst["bits"] = np.delete(inst["bits"], cut)
+    bo[natt + 4:] -= 1
+    inst["boffs"] = bo.astype(np.uint64)
+    ne = NativeEpoch(inst, comm=Comm.loopback(world))
+    assert ne.one_pass
+    ne.step()
+    for local in range(world):
+        bal, scal, *_ = ne.results(local)
+        assert int(scal[1, _lib.SCAL_ERR_XL]) == 2  # PZ_XLERR_BITFIELD, once
+        assert scal[1, _lib.SCAL_APPLIED] == 0
+        np.testing.assert_array_equal(bal[1], inst["balance"][1][ne.validators(local)])
+        for b in (0, 2):
+            nb, applied, nxt, *_ = oracle_epoch(inst, b)
+            assert bool(scal[b, _lib.SCAL_APPLIED]) == applied and int(scal[b, _lib.SCAL_NEXT_BAL]) == nxt
+            np.testing.assert_array_equal(bal[b], nb[ne.validators(local)])
 
 
 def test_native_epoch_panic_flags_sharded():

@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from prysm_amd import _lib, casper, synth  # noqa: E402
-from prysm_amd.epoch import DeviceEpoch  # noqa: E402
+from prysm_amd.native import NativeEpoch  # noqa: E402
 
 
 def epoch_1m():
@@ -23,9 +23,10 @@ def epoch_1m():
     nval, B = 1 << 20, 16
     inst = synth.epoch_batch(nval, B, seed=3,
                              shuffled=casper.shuffle_indices(b"A" + bytes(31), np.arange(nval, dtype=np.uint32)))
-    de = DeviceEpoch(inst, dev)
+    de = NativeEpoch(inst, device=0)  # the bench's path (pz_epoch_state, one-pass step)
     for _ in range(3):
-        de.step(s)
+        de.step()
+    de.sync()
     torch.cuda.synchronize()
     print("pmc epoch_1m workload done")
 
@@ -44,12 +45,14 @@ def main():
     nval, B = 65536, 256
     inst = synth.epoch_batch(nval, B, seed=3,
                              shuffled=casper.shuffle_indices(b"A" + bytes(31), np.arange(nval, dtype=np.uint32)))
-    de = DeviceEpoch(inst, dev)
+    de = NativeEpoch(inst, device=0)  # the bench's path (pz_epoch_state, one-pass step)
     for _ in range(3):
-        de.step(s)
+        de.step()
+    de.sync()
     x = torch.empty(nval * B, dtype=torch.int64, device=dev)
+    y = torch.empty_like(x)
     for _ in range(3):
-        x.copy_(de.balance.view(-1))
+        x.copy_(y)
     # the bench's wire and attcheck legs, same inputs
     import bench  # noqa: E402
     nw = 16 << 20
