@@ -361,6 +361,8 @@ struct Engine {
   DevArr<uint8_t> d_qpack, present;
   DevArr<uint64_t> d_err;    // sticky tally panic flag
   uint64_t* h_err = nullptr;  // its pinned host copy, read after a sync
+  DevArr<uint32_t> d_id_slot;  // hash-log id -> vote-cache slot, uploaded up to d_id_slot_n
+  uint64_t d_id_slot_n = 0;
   // per (slot, committee) union bitfields and touched flags of the tally's first pass
   DevArr<uint32_t> ubits, uflag;
   DevArr<uint32_t> d_leader;
@@ -387,7 +389,7 @@ struct Engine {
   // id; RecentBlockHashes carry ids too, so signed parent hashes are id ranges (no hashing of
   // 32-byte keys per vote) and the processAttestation messages are assembled on the device
   std::vector<H32> hlog;
-  std::vector<uint32_t> id_slot;  // vote-cache slot of each id (kSlotLazy until first tallied)
+  std::vector<uint32_t> id_slot;  // vote-cache slot of each id (resolved when it is logged)
   DevArr<uint8_t> d_hlog;
   uint64_t d_hlog_n = 0;
   // processAttestation message batch (10-byte header, 64 parent ids, ShardBlockHash)
@@ -518,16 +520,19 @@ static uint32_t vote_slot(Engine& g, const H32& h) {
   return s;
 }
 
-// A logged hash gets its vote-cache slot (an nval-bit voter bitmap and a total in HBM) only
-// when a flush first tallies a vote for it, like the Go map, which holds an entry only for a
-// hash some attestation signed (core.go:322-326): block digests nobody votes for cost no
-// bitmap (512 KiB per block at 4M validators when every digest had one).  `votable`
-// is false for an id that can never be tallied: a 32-byte oblique parent hash is only ever a
+// Every logged hash gets its vote-cache slot at once (a slot is storage; whether the Go map
+// has an entry for the hash is the slot's `present` flag, set by the tally).  A slot costs
+// nval/8 bytes of voter bitmap + 9 bytes in HBM: 8 KiB per block at 65,536 validators (80 MB
+// for configs[4]'s 10,000 blocks), 512 KiB at 4M; Go's VoteCache keeps a []uint32 of up to
+// nval voter indices per signed hash (core.go:322-340), 32x the bitmap when fully voted, and
+// in a live chain every block hash is signed.  Creating slots on a hash's first tally instead
+// (measured in round 2) put a resolve loop over every queued (attestation, parent) item in the
+// flush and cost 40 ms per 10,000 blocks (153 -> 88 k blocks/s, tools/gpu_replay_ab.sh).  `votable` is
+// false for an id that can never be tallied: a 32-byte oblique parent hash is only ever a
 // parent of its own attestation, which skips it (core.go:313-320).
-constexpr uint32_t kSlotLazy = UINT32_MAX - 1, kSlotNever = UINT32_MAX;
 static uint32_t log_hash(Engine& g, const H32& h, bool votable = true) {
   g.hlog.push_back(h);
-  g.id_slot.push_back(votable ? kSlotLazy : kSlotNever);
+  g.id_slot.push_back(votable ? vote_slot(g, h) : UINT32_MAX);
   return (uint32_t)(g.hlog.size() - 1);
 }
 
@@ -538,24 +543,13 @@ static uint32_t log_hash(Engine& g, const H32& h, bool votable = true) {
 static bool flush_votes_enqueue(Engine& g) {
   if (g.q_comm.empty()) return false;
   PhaseTimer pt(g.prof[kProfFlush]);
+  const uint64_t nid = g.id_slot.size(), new_ids = nid - g.d_id_slot_n;
   const uint64_t natt = g.q_comm.size();
-  // each queued (attestation, parent) item -> its vote-cache slot, created on first use (may
-  // grow the device arrays, which drains the stream: before any of this flush's copies)
-  for (size_t k = 0; k < g.q_ids.size(); ++k) {
-    if ((g.q_skip[k >> 6] >> (k & 63)) & 1) {
-      g.q_ids[k] = 0;  // skipped by the kernels
-      continue;
-    }
-    uint32_t& sl = g.id_slot[g.q_ids[k]];
-    if (sl == kSlotNever) throw Panic{"internal: a skipped-only parent hash reached the tally"};
-    if (sl == kSlotLazy) sl = vote_slot(g, g.hlog[g.q_ids[k]]);
-    g.q_ids[k] = sl;
-  }
   auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
-  // packed layout: boffs | skip | comm | slots | bits
+  // packed layout: boffs | skip | comm | ids | new id slots | bits
   const size_t o_boffs = 0, o_skip = o_boffs + al(g.q_boffs.size() * 8), o_comm = o_skip + al(natt * 8),
-               o_ids = o_comm + al(natt * 4), o_bits = o_ids + al(g.q_ids.size() * 4),
-               total = o_bits + al(g.q_bits.size());
+               o_ids = o_comm + al(natt * 4), o_slots = o_ids + al(g.q_ids.size() * 4),
+               o_bits = o_slots + al(new_ids * 4), total = o_bits + al(g.q_bits.size());
   if (g.q_arena_busy) {
     hchk(hipEventSynchronize(g.q_arena_ev), "event sync");
     g.q_arena_busy = false;
@@ -572,17 +566,31 @@ static bool flush_votes_enqueue(Engine& g) {
   std::memcpy(g.q_arena + o_skip, g.q_skip.data(), natt * 8);
   std::memcpy(g.q_arena + o_comm, g.q_comm.data(), natt * 4);
   std::memcpy(g.q_arena + o_ids, g.q_ids.data(), g.q_ids.size() * 4);
+  std::memcpy(g.q_arena + o_slots, g.id_slot.data() + g.d_id_slot_n, new_ids * 4);
   std::memcpy(g.q_arena + o_bits, g.q_bits.data(), g.q_bits.size());
   // Growing a device buffer frees the old one, which in-flight flushes may still read:
   // drain the stream first (rare: the buffers double).
-  if (total > g.d_qpack.n || natt * 64 + 1 > g.d_leader.n) {
+  if (total > g.d_qpack.n || nid > g.d_id_slot.n || natt * 64 + 1 > g.d_leader.n) {
     hchk(hipStreamSynchronize(g.s), "sync");
     check(g.d_qpack.alloc(std::max<uint64_t>(total, 2 * g.d_qpack.n)));
     check(g.d_leader.alloc(std::max<uint64_t>(natt * 64 + 1, 2 * g.d_leader.n)));
+    if (nid > g.d_id_slot.n) {  // the id -> slot map keeps its device contents
+      DevArr<uint32_t> grown;
+      check(grown.alloc(std::max<uint64_t>(nid, 2 * g.d_id_slot.n)));
+      if (g.d_id_slot_n)
+        hchk(hipMemcpyAsync(grown.p, g.d_id_slot.p, g.d_id_slot_n * 4, hipMemcpyDeviceToDevice, g.s), "D2D");
+      hchk(hipStreamSynchronize(g.s), "sync");
+      std::swap(g.d_id_slot.p, grown.p);
+      std::swap(g.d_id_slot.n, grown.n);
+    }
   }
   hchk(hipMemcpyAsync(g.d_qpack.p, g.q_arena, total, hipMemcpyHostToDevice, g.s), "H2D");
+  if (new_ids)
+    hchk(hipMemcpyAsync(g.d_id_slot.p + g.d_id_slot_n, g.d_qpack.p + o_slots, new_ids * 4, hipMemcpyDeviceToDevice,
+                        g.s), "D2D");
   hchk(hipEventRecord(g.q_arena_ev, g.s), "event");
   g.q_arena_busy = true;
+  g.d_id_slot_n = nid;
   if (!g.d_err.p) {
     check(g.d_err.alloc(1));
     hchk(hipMemsetAsync(g.d_err.p, 0, 8, g.s), "memset");
@@ -596,7 +604,7 @@ static bool flush_votes_enqueue(Engine& g) {
   v.boffs = reinterpret_cast<const uint64_t*>(g.d_qpack.p + o_boffs);
   v.ids = reinterpret_cast<const uint32_t*>(g.d_qpack.p + o_ids);
   v.skip = reinterpret_cast<const uint64_t*>(g.d_qpack.p + o_skip);
-  v.id_slot = nullptr;  // v.ids are vote-cache slots
+  v.id_slot = g.d_id_slot.p;
   v.natt = natt;
   v.balance = g.balance.p;
   v.nval = g.nval;

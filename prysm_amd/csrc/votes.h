@@ -18,7 +18,7 @@ struct VoteIdArgs {
   const uint64_t* boffs;     // natt+1
   const uint32_t* ids;       // natt x 64 hash-log ids of the signed parent hashes
   const uint64_t* skip;      // natt: bit j set = parent j equals an oblique parent hash
-  const uint32_t* id_slot;   // hash-log id -> vote-cache slot (nullptr: ids are slots)
+  const uint32_t* id_slot;   // hash-log id -> vote-cache slot
   uint64_t natt;
   const uint64_t* balance;
   uint64_t nval;

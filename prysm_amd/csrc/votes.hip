@@ -63,8 +63,8 @@ pz_vote_tally_kernel(VoteArgs a) {
 }
 
 // The block engine's form: work item (attestation, j) for each of its 64 signed parent
-// hashes, read from the hash log ids the walk recorded; the host resolves each to its vote-cache
-// slot at the flush (id_slot == nullptr: `ids` already are slots).  No host-side grouping: pass 1 ORs each item's
+// hashes, read from the hash log ids the walk recorded; the vote-cache slot of every id is
+// resolved by the host when the id is logged.  No host-side grouping: pass 1 ORs each item's
 // bitfield into the union bitfield of its (slot, committee) group -- dedup makes the union
 // exact -- and elects the group's first item as its leader; pass 2 lets each leader tally the
 // union once and clear it.  (Tallying every item directly made up to 64 waves race on the
@@ -79,7 +79,7 @@ pz_vote_union_kernel(VoteIdArgs a) {
   const uint64_t att = item >> 6;
   if (att >= a.natt) return;
   if ((a.skip[att] >> (item & 63)) & 1) return;  // an oblique parent hash (core.go:313-320) is skipped
-  const uint32_t slot = a.id_slot ? a.id_slot[a.ids[item]] : a.ids[item];
+  const uint32_t slot = a.id_slot[a.ids[item]];
   const uint32_t c = a.att_comm[att];
   const uint64_t grp = (uint64_t)slot * a.ncomm + c;
   const uint64_t k = a.coffs[c + 1] - a.coffs[c];
@@ -107,7 +107,7 @@ pz_vote_leader_kernel(VoteIdArgs a) {
   for (uint32_t li = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; li < n; li += kLeaderWaves) {
     const uint64_t item = a.leader[li];
     const uint64_t att = item >> 6;
-    const uint32_t slot = a.id_slot ? a.id_slot[a.ids[item]] : a.ids[item];
+    const uint32_t slot = a.id_slot[a.ids[item]];
     const uint32_t c = a.att_comm[att];
     const uint64_t grp = (uint64_t)slot * a.ncomm + c;
     uint32_t* u = a.ubits + grp * a.cwords;

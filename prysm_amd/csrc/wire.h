@@ -28,5 +28,6 @@ uint64_t wire_tiles(uint64_t n);
 int wire_val_args(const pz_validator_cols* v, uint64_t n, uint32_t field_num, WireValArgs* a);
 // scratch: (wire_tiles(n) + 1) u64, zeroed by the launcher
 hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t s);
+int set_wire_variant(int v);  // tools/ A/B only (pz_debug_set_wire_variant)
 
 }  // namespace pz

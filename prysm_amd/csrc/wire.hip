@@ -26,11 +26,11 @@
 namespace pz {
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kPer = 4, kSubRecs = kThreads * kPer;  // scalar kernel: sub-tiles of 1,024 records
-constexpr int kSub = 2, kTileRecs = kSub * kSubRecs;  // 2,048 records (one ticket) per tile
-constexpr int kStageBytes = 32 * 1024;                // the whole tile's encoding (16 B per record)
-constexpr int kBytesSub = 8, kBytesTileRecs = kBytesSub * kThreads;  // bytes-field kernel: 2,048
+constexpr int kThreads = 512;
+constexpr int kPer = 4, kSubRecs = kThreads * kPer;  // scalar kernel: sub-tiles of 2,048 records
+constexpr int kSub = 2, kTileRecs = kSub * kSubRecs;  // 4,096 records (one ticket) per tile
+constexpr int kStageBytes = 64 * 1024;                // the whole tile's encoding (16 B per record)
+constexpr int kBytesSub = 8, kBytesTileRecs = kBytesSub * kThreads;  // bytes-field kernel: 4,096
 
 __device__ __forceinline__ uint32_t vlen(uint64_t x) { return (uint32_t)((70 - __clzll(x | 1)) / 7); }
 
@@ -193,9 +193,14 @@ __device__ uint64_t lookback_finish(uint64_t* status, uint64_t tile, uint64_t (&
 #pragma unroll
     for (int q = 0; q < kLbPer; ++q) {
       const int64_t idx = j - (threadIdx.x * kLbPer + q);
-      while (!(w[q] >> 62)) {
+      // Poll with relaxed agent-scope (sc1) loads -- the R2 granule form of the HIP guide's
+      // Guideline 16: every status word is written by an agent-scope atomic store -- and fall
+      // back to the atomic re-read after 256 polls.  Polling by atomics alone made every
+      // spinning tile queue at the memory-side atomic unit of the same few status lines
+      // (~12 ns each): 295 us per 16.7 M records against 178 without the look-back.
+      for (uint32_t spins = 0; !(w[q] >> 62); ++spins) {
         __builtin_amdgcn_s_sleep(1);
-        w[q] = ld_status_fresh(status + idx);
+        w[q] = spins < 256 ? ld_status(status + idx) : ld_status_fresh(status + idx);
       }
     }
     // nearest published inclusive prefix (distance d = threadIdx.x * kLbPer + q)
@@ -236,20 +241,25 @@ __device__ uint64_t lookback_block(uint64_t* status, uint64_t tile, uint64_t* ld
   return lookback_finish(status, tile, w, lds, lds_first);
 }
 
-// Store stage[0..span) at out+base with dword stores: bytes up to the first 4-aligned
-// address, then dwords (each funnel-shifted out of two aligned LDS words), then the tail.
+// Store stage[0..span) at out+base with 16-B stores: bytes up to the first 16-aligned
+// address, then 16-B chunks (each funnel-shifted out of five LDS words), then the tail.
 __device__ __forceinline__ void store_stage(uint8_t* out, uint64_t base, const uint32_t* stage, uint32_t span) {
   const uint8_t* st = reinterpret_cast<const uint8_t*>(stage);
-  const uint32_t lead = (uint32_t)((4 - (base & 3)) & 3);
+  const uint32_t lead = (uint32_t)((16 - (base & 15)) & 15);
   const uint32_t head = lead < span ? lead : span;
   if (threadIdx.x < head) out[base + threadIdx.x] = st[threadIdx.x];
-  const uint32_t nd = (span - head) >> 2;
-  uint32_t* dst = reinterpret_cast<uint32_t*>(out + base + head);
-  for (uint32_t j = threadIdx.x; j < nd; j += kThreads) {
-    const uint32_t w = head + 4 * j;  // byte position in the stage
-    dst[j] = head ? __builtin_amdgcn_alignbyte(stage[(w >> 2) + 1], stage[w >> 2], head) : stage[w >> 2];
+  const uint32_t nq = (span - head) >> 4, sh = head & 3;
+  uint4* dst = reinterpret_cast<uint4*>(out + base + head);
+  for (uint32_t j = threadIdx.x; j < nq; j += kThreads) {
+    const uint32_t w0 = (head + 16 * j) >> 2;  // first LDS word of the chunk
+    uint32_t x[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) x[k] = stage[w0 + k];
+    dst[j] = sh ? make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], sh), __builtin_amdgcn_alignbyte(x[2], x[1], sh),
+                             __builtin_amdgcn_alignbyte(x[3], x[2], sh), __builtin_amdgcn_alignbyte(x[4], x[3], sh))
+                : make_uint4(x[0], x[1], x[2], x[3]);
   }
-  const uint32_t t0 = head + 4 * nd;
+  const uint32_t t0 = head + 16 * nq;
   if (t0 + threadIdx.x < span) out[base + t0 + threadIdx.x] = st[t0 + threadIdx.x];
 }
 
@@ -265,8 +275,8 @@ __device__ __forceinline__ void load_sub(const WireValArgs& a, uint64_t first, S
 }
 
 // Sizes of one sub-tile's records and their offsets inside the sub-tile (record order), from
-// ONE block scan: a record is at most 61 bytes and a sub-tile row p of 256 records at most
-// 15,616, so the four rows' sizes travel as four 16-bit lanes of one u64.
+// ONE block scan: a record is at most 61 bytes and a sub-tile row p of 512 records at most
+// 31,232, so the four rows' sizes travel as four 16-bit lanes of one u64.
 __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t first, const SRec (&r)[kPer],
                                                 uint32_t (&body)[kPer], uint32_t (&off)[kPer], uint64_t* lds) {
   uint64_t packed = 0;
@@ -288,47 +298,68 @@ __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t f
   return row;
 }
 
-// One tile of kSub sub-tiles per workgroup, one ticket per tile.  All of the tile's columns
-// are loaded at once; the sub-tiles' sizes are scanned and the tile publishes its size.
-// The look-back's first window is issued, the tile's encoding is built in the LDS stage
-// meanwhile, and after the look-back the stage is stored with aligned dword stores.  A tile
-// whose encoding outgrows the stage (records averaging over 16 bytes), or a call that wants
-// record offsets, writes lane by lane from registers instead.  Tiles are large because a
-// single contended ticket counter serialises its atomics (~11 ns each).
-extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_val_kernel(WireValArgs a, uint32_t nt) {
-  __shared__ uint64_t lds[5];
+// One tile of kSub sub-tiles (4,096 records) per 512-thread workgroup, one ticket per tile.
+// Phase 1 loads each sub-tile's columns, keeps only the records' offsets inside the tile (one
+// block scan per sub-tile) and drops the values; the tile publishes its size and issues the
+// look-back's first window.  Phase 2 loads the columns again -- the tile's 96 KiB were just
+// read, so these come from L2 -- and builds the encoding in the 64 KiB LDS stage while the
+// look-back is in flight; after it the stage is stored with 16-B stores.  A tile whose
+// encoding outgrows the stage (records averaging over 16 bytes), or a call that wants record
+// offsets, writes lane by lane from registers instead.  Tiles are large because a single
+// contended ticket counter serialises its atomics (~11 ns each).
+// Measured (tools/wire_probe.py, 16.7 M records, us): r2b's 256-thread tiles of 2,048 with
+// every value held in registers through the scan (152 VGPRs) 255; reloading from L2 at 256
+// threads 296 (phase 1 got faster, the look-back's share grew); these 512-thread tiles 241.
+// Dropped: building the stage by dword ORs from a register accumulator instead of byte
+// writes 305 (the 64-bit shifts cost more VALU than the LDS byte writes); persistent
+// workgroups pipelining the next tile's phase 1 under the look-back 278 (128 VGPRs + spills).
+// V: an ablation knob for tools/wire_probe.py (0 in the product; output wrong otherwise):
+// bit 0 tile = blockIdx (no ticket), bit 1 no stage build, bit 2 no look-back, bit 3 no store.
+template <int V>
+__device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
+  __shared__ uint64_t lds[kThreads / 64 + 1];
   __shared__ uint32_t s_tile, s_first;
-  __shared__ uint32_t stage[kStageBytes / 4 + 2];
-  if (threadIdx.x == 0) s_tile = atomicAdd(a.ticket, 1u);
+  __shared__ __attribute__((aligned(16))) uint32_t stage[kStageBytes / 4 + 8];
+  if (V & 1) {
+    if (threadIdx.x == 0) s_tile = blockIdx.x;
+  } else if (threadIdx.x == 0) {
+    s_tile = atomicAdd(a.ticket, 1u);
+  }
   __syncthreads();
   const uint32_t tile = s_tile;
   const uint64_t tfirst = (uint64_t)tile * kTileRecs;
-  uint8_t* st = reinterpret_cast<uint8_t*>(stage);
-  // every sub-tile's columns in registers at once (kSub x kPer records per thread)
-  SRec r[kSub][kPer];
-#pragma unroll
-  for (int j = 0; j < kSub; ++j) load_sub(a, tfirst + (uint64_t)j * kSubRecs, r[j]);
-  uint32_t body[kSub][kPer], off[kSub][kPer], sub_base[kSub];
-  uint32_t agg = 0;
+  // phase 1: sizes -> offsets inside the tile
+  uint32_t off[kSub][kPer], agg = 0;
 #pragma unroll
   for (int j = 0; j < kSub; ++j) {
-    sub_base[j] = agg;
-    agg += sub_offsets(a, tfirst + (uint64_t)j * kSubRecs, r[j], body[j], off[j], lds);
+    SRec r[kPer];
+    uint32_t body[kPer];
+    load_sub(a, tfirst + (uint64_t)j * kSubRecs, r);
+    const uint32_t sub = sub_offsets(a, tfirst + (uint64_t)j * kSubRecs, r, body, off[j], lds);
+#pragma unroll
+    for (int p = 0; p < kPer; ++p) off[j][p] += agg;
+    agg += sub;
   }
   if (threadIdx.x == 0) st_status(a.status + tile, (tile == 0 ? kFlagP : kFlagA) | agg);
-  // the look-back's first round trip overlaps the stage build
+  // the look-back's first round trip overlaps phase 2
   uint64_t w[kLbPer];
-  if (tile > 0) lookback_issue(a.status, tile, w);
+  if (!(V & 4) && tile > 0) lookback_issue(a.status, tile, w);
+  const bool staged = agg <= kStageBytes && !a.offs;
+  if (staged && !(V & 2)) {
+    uint8_t* st = reinterpret_cast<uint8_t*>(stage);
 #pragma unroll
-  for (int j = 0; j < kSub; ++j)
+    for (int j = 0; j < kSub; ++j) {
+      SRec r[kPer];
+      load_sub(a, tfirst + (uint64_t)j * kSubRecs, r);
 #pragma unroll
-    for (int p = 0; p < kPer; ++p) {
-      const uint32_t o = sub_base[j] + off[j][p];
-      if (tfirst + j * kSubRecs + p * kThreads + threadIdx.x < a.n && o + frame_size(a, body[j][p]) <= kStageBytes)
-        put_srec(a, r[j][p], body[j][p], st + o);
+      for (int p = 0; p < kPer; ++p)
+        if (tfirst + j * kSubRecs + p * kThreads + threadIdx.x < a.n) put_srec(a, r[p], srec_body(r[p]), st + off[j][p]);
     }
+  }
   uint64_t base = 0;
-  if (tile > 0) {
+  if (V & 4) {
+    base = (uint64_t)tile * 15 * kTileRecs;
+  } else if (tile > 0) {
     base = lookback_finish(a.status, tile, w, lds, &s_first);
     if (threadIdx.x == 0) st_status(a.status + tile, kFlagP | (base + agg));
   }
@@ -336,29 +367,43 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_val_kernel(WireVa
     *a.total = base + agg;
     if (a.offs) a.offs[a.n] = base + agg;
   }
-  if (agg <= kStageBytes && !a.offs) {
+  if (staged) {
     __syncthreads();
-    store_stage(a.out, base, stage, agg);
+    if (!(V & 8)) store_stage(a.out, base, stage, agg);
     return;
   }
 #pragma unroll
-  for (int j = 0; j < kSub; ++j)
+  for (int j = 0; j < kSub; ++j) {
+    SRec r[kPer];
+    load_sub(a, tfirst + (uint64_t)j * kSubRecs, r);
 #pragma unroll
     for (int p = 0; p < kPer; ++p) {
       const uint64_t i = tfirst + j * kSubRecs + p * kThreads + threadIdx.x;
       if (i < a.n) {
-        const uint64_t o = base + sub_base[j] + off[j][p];
+        const uint64_t o = base + off[j][p];
         if (a.offs) a.offs[i] = o;
-        put_srec(a, r[j][p], body[j][p], a.out + o);
+        put_srec(a, r[p], srec_body(r[p]), a.out + o);
       }
     }
+  }
 }
+
+#define PZ_WIRE_VAL_KERNEL(NAME, V) \
+  extern "C" __global__ void __launch_bounds__(kThreads) NAME(WireValArgs a, uint32_t nt) { wire_val_body<V>(a, nt); }
+PZ_WIRE_VAL_KERNEL(pz_wire_val_kernel, 0)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v1_kernel, 1)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v2_kernel, 2)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v4_kernel, 4)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v8_kernel, 8)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v7_kernel, 7)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v15_kernel, 15)
+#undef PZ_WIRE_VAL_KERNEL
 
 // Records with bytes fields: tiles of kBytesSub x 256 records, one per thread per sub-tile.
 // Phase 1 scans the sizes; after the look-back, phase 2 reads the records again and writes
 // each lane's record straight to HBM (a record has no size bound, so there is no stage).
 extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_val_bytes_kernel(WireValArgs a, uint32_t nt) {
-  __shared__ uint64_t lds[5];
+  __shared__ uint64_t lds[kThreads / 64 + 1];
   __shared__ uint32_t s_tile, s_first;
   if (threadIdx.x == 0) s_tile = atomicAdd(a.ticket, 1u);
   __syncthreads();
@@ -411,6 +456,8 @@ uint64_t wire_tiles(uint64_t n) {  // scratch bound: the smaller tile of the two
   return (n + t - 1) / t;
 }
 
+static int g_wire_variant = 0;  // tools/ A/B only
+
 // Scratch: status[nt] then the ticket; zeroed before every launch.
 hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t s) {
   const bool bytes = a.wa_offs || a.rc_offs;
@@ -427,8 +474,20 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
   if (bytes)
     hipLaunchKernelGGL(pz_wire_val_bytes_kernel, dim3((uint32_t)nt), dim3(kThreads), 0, s, a, (uint32_t)nt);
   else
-    hipLaunchKernelGGL(pz_wire_val_kernel, dim3((uint32_t)nt), dim3(kThreads), 0, s, a, (uint32_t)nt);
+    switch (g_wire_variant) {
+#define PZ_CASE(V) \
+  case V: hipLaunchKernelGGL(pz_wire_val_v##V##_kernel, dim3((uint32_t)nt), dim3(kThreads), 0, s, a, (uint32_t)nt); break;
+      PZ_CASE(1) PZ_CASE(2) PZ_CASE(4) PZ_CASE(8) PZ_CASE(7) PZ_CASE(15)
+#undef PZ_CASE
+      default: hipLaunchKernelGGL(pz_wire_val_kernel, dim3((uint32_t)nt), dim3(kThreads), 0, s, a, (uint32_t)nt);
+    }
   return hipGetLastError();
+}
+
+int set_wire_variant(int v) {
+  const int old = g_wire_variant;
+  g_wire_variant = v;
+  return old;
 }
 
 int wire_val_args(const pz_validator_cols* v, uint64_t n, uint32_t field_num, WireValArgs* a) {
@@ -467,6 +526,8 @@ extern "C" {
 uint64_t pz_wire_validators_bound(uint64_t n, uint64_t bytes_total) { return n * 92 + bytes_total; }
 
 uint64_t pz_wire_scratch_bytes(uint64_t n) { return (wire_tiles(n) + 1) * 8; }
+
+int pz_debug_set_wire_variant(int v) { return set_wire_variant(v); }
 
 int pz_dev_wire_validators(const pz_validator_cols* v, uint64_t n, uint32_t field_num, uint8_t* d_out,
                            uint64_t* d_offsets, void* d_scratch, uint64_t* d_total, void* stream) {

@@ -28,20 +28,30 @@ def main():
         _lib.lib.call("pz_dev_wire_validators", ctypes.byref(cols), n, 11, out.data_ptr(), None, scr.data_ptr(),
                       tot.data_ptr(), sh)
 
-    for _ in range(10):
-        run()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        run()
-    e1.record()
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / reps
+    def timed():
+        for _ in range(10):
+            run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / reps
+
+    us = timed()
     total = int(tot.item())
     alg = n * 24 + total
     print("wire: %d records, %d bytes, %.1f us/launch, %.0f GB/s algorithmic (%.1f%% of 8 TB/s)"
           % (n, total, us, alg / us / 1e3, alg / us / 1e3 / 80))
+    if len(sys.argv) > 2:  # ablation (wire.hip wire_val_body V, one tile per workgroup): results wrong for V != 0
+        names = {1: "tile = blockIdx (no ticket)", 2: "no stage build", 4: "no look-back", 8: "no store",
+                 7: "1+2+4", 15: "1+2+4+8"}
+        for v in (0, 1, 2, 4, 8, 7, 15, 0):
+            _lib.lib.dll.pz_debug_set_wire_variant(v)
+            print("  variant %2d %-28s %.1f us" % (v, names.get(v, "product"), timed()))
+        _lib.lib.dll.pz_debug_set_wire_variant(0)
 
 
 if __name__ == "__main__":
