@@ -567,8 +567,8 @@ def attcheck_leg(args, torch, dist, dev, rank, world):
                                "5%% failing a check" % natt, "parallelism": "attestation-shard x%d" % world},
         "roofline": {"bound": "hbm", "achieved": alg / (step_ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": alg / (step_ms * 1e-3) / HBM_PEAK,
-                     "traffic": pmc_traffic(["pz_att_check_kernel"]), "traffic_source": PMC_SUMMARY,
-                     "kernel": "pz_att_check_kernel", "step_device_ms": step_ms,
+                     "traffic": pmc_traffic(["pz_att_check_x2_kernel"]), "traffic_source": PMC_SUMMARY,
+                     "kernel": "pz_att_check_x2_kernel", "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": alg},
     }
     if rank == 0 and world == 1:

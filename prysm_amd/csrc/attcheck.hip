@@ -23,13 +23,10 @@ namespace {
 
 constexpr int kThreads = 256;
 
-extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_kernel(pz_att_check_batch b) {
-  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= b.natt) return;
-  // every per-attestation column is loaded up front (independent loads in flight together);
-  // only the committee table walk and the bitfield byte depend on them
-  const uint64_t s = b.slot[i], bs = b.block_slot[i], js = b.justified_slot[i], nob = b.n_oblique[i];
-  const uint64_t shard = b.shard_id[i], b0 = b.boffs[i], b1 = b.boffs[i + 1];
+// One attestation's checks from its loaded scalars (Go's order; see the file comment).
+__device__ __forceinline__ void check_one(const pz_att_check_batch& b, uint64_t s, uint64_t bs, uint64_t js,
+                                          uint64_t nob, uint64_t shard, uint64_t b0, uint64_t b1, int32_t* st_out,
+                                          uint32_t* comm_out, uint64_t* pstart_out) {
   int32_t st = PZ_ATT_PROCESSED;
   uint32_t comm = UINT32_MAX;
   uint64_t pstart = 0;
@@ -60,14 +57,61 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_kernel(pz_at
         const uint64_t blen = b1 - b0;
         if ((k + 7) / 8 != blen)
           st = PZ_ATT_BITFIELD_LEN;
-        else if ((k & 7) && (b.bits[b0 + blen - 1] & (0xFFu >> (k & 7))))
+        else if ((k & 7) && (b.bits[b0 + blen - 1] & (0xFFu >> (k & 7))))  // only when bits pad the byte
           st = PZ_ATT_TRAILING_BITS;
       }
     }
   }
+  *st_out = st;
+  *comm_out = comm;
+  *pstart_out = pstart;
+}
+
+// One lane per attestation, 8-B column loads (any alignment).
+extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_kernel(pz_att_check_batch b) {
+  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= b.natt) return;
+  // every per-attestation column is loaded up front (independent loads in flight together);
+  // only the committee table walk and the bitfield byte depend on them
+  int32_t st;
+  uint32_t comm;
+  uint64_t pstart;
+  check_one(b, b.slot[i], b.block_slot[i], b.justified_slot[i], b.n_oblique[i], b.shard_id[i], b.boffs[i],
+            b.boffs[i + 1], &st, &comm, &pstart);
   b.status[i] = st;
   if (b.committee) b.committee[i] = comm;
   if (b.parents_start) b.parents_start[i] = pstart;
+}
+
+// Two attestations per lane with 16-B column loads and 8/16-B stores (every column and output
+// 16-B aligned): half the memory instructions of the one-per-lane form and full-width
+// streaming requests.
+extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_x2_kernel(pz_att_check_batch b) {
+  const uint64_t i = 2 * ((uint64_t)blockIdx.x * kThreads + threadIdx.x);
+  if (i >= b.natt) return;
+  if (i + 1 >= b.natt) {  // odd tail
+    int32_t st;
+    uint32_t comm;
+    uint64_t pstart;
+    check_one(b, b.slot[i], b.block_slot[i], b.justified_slot[i], b.n_oblique[i], b.shard_id[i], b.boffs[i],
+              b.boffs[i + 1], &st, &comm, &pstart);
+    b.status[i] = st;
+    if (b.committee) b.committee[i] = comm;
+    if (b.parents_start) b.parents_start[i] = pstart;
+    return;
+  }
+  auto ld2 = [](const uint64_t* p) { return *reinterpret_cast<const ulonglong2*>(p); };
+  const ulonglong2 s = ld2(b.slot + i), bs = ld2(b.block_slot + i), js = ld2(b.justified_slot + i);
+  const ulonglong2 nob = ld2(b.n_oblique + i), sh = ld2(b.shard_id + i), bo = ld2(b.boffs + i);
+  const uint64_t bo2 = b.boffs[i + 2];
+  int32_t st0, st1;
+  uint32_t c0, c1;
+  uint64_t p0, p1;
+  check_one(b, s.x, bs.x, js.x, nob.x, sh.x, bo.x, bo.y, &st0, &c0, &p0);
+  check_one(b, s.y, bs.y, js.y, nob.y, sh.y, bo.y, bo2, &st1, &c1, &p1);
+  *reinterpret_cast<int2*>(b.status + i) = make_int2(st0, st1);
+  if (b.committee) *reinterpret_cast<uint2*>(b.committee + i) = make_uint2(c0, c1);
+  if (b.parents_start) *reinterpret_cast<ulonglong2*>(b.parents_start + i) = make_ulonglong2(p0, p1);
 }
 
 int check_args(const pz_att_check_batch* b) {
@@ -82,8 +126,19 @@ int check_args(const pz_att_check_batch* b) {
 
 hipError_t launch_att_check(const pz_att_check_batch& b, hipStream_t s) {
   if (!b.natt) return hipSuccess;
-  hipLaunchKernelGGL(pz_att_check_kernel, dim3((uint32_t)((b.natt + kThreads - 1) / kThreads)), dim3(kThreads), 0,
-                     s, b);
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const bool x2 = al(b.slot) && al(b.block_slot) && al(b.justified_slot) && al(b.n_oblique) && al(b.shard_id) &&
+                  al(b.boffs) && (reinterpret_cast<uintptr_t>(b.status) & 7) == 0 &&
+                  (!b.committee || (reinterpret_cast<uintptr_t>(b.committee) & 7) == 0) &&
+                  (!b.parents_start || al(b.parents_start));
+  if (x2) {
+    const uint64_t lanes = (b.natt + 1) / 2;
+    hipLaunchKernelGGL(pz_att_check_x2_kernel, dim3((uint32_t)((lanes + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                       s, b);
+  } else {
+    hipLaunchKernelGGL(pz_att_check_kernel, dim3((uint32_t)((b.natt + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                       s, b);
+  }
   return hipGetLastError();
 }
 

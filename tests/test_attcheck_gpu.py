@@ -93,3 +93,50 @@ def test_go_int_conversion_of_huge_slots():
 def test_empty_batch():
     status, comm, pstart = check_attestations([], [], 0, 0, 128, [])
     assert len(status) == 0
+
+
+@pytest.mark.parametrize("natt,shift", [(4097, 0), (4096, 1), (1, 0)])
+def test_device_forms_match_c_port(natt, shift):
+    """pz_dev_check_attestations on bench.attcheck_columns' inputs: 16-B-aligned columns take
+    the two-per-lane kernel (odd tail included), columns shifted by one element the one-per-lane
+    kernel; both equal the C port (oracle/c/attcheck_ref.c)."""
+    import ctypes
+
+    import torch
+
+    import bench
+    from oracle import cport
+
+    cols, tab = bench.attcheck_columns(natt, seed=5)
+    dev = torch.device("cuda", 0)
+
+    def put(v):
+        a = v.view(np.int64) if v.dtype == np.uint64 else v.view(np.int32) if v.dtype == np.uint32 else v
+        buf = torch.zeros(a.size + shift + 2, dtype=torch.from_numpy(a[:1]).dtype, device=dev)
+        buf[shift:shift + a.size] = torch.from_numpy(a).to(dev)
+        return buf, buf[shift:]
+
+    keep, t = [], {}
+    for k, v in list(cols.items()) + list(tab.items()):
+        buf, view = put(v)
+        keep.append(buf)
+        t[k] = view
+    status = torch.empty(natt + 1, dtype=torch.int32, device=dev)[shift:]
+    comm = torch.empty(natt + 1, dtype=torch.int32, device=dev)[shift:]
+    pstart = torch.empty(natt + 2, dtype=torch.int64, device=dev)[shift:]
+    b = _lib.AttCheckBatch(natt, t["slot"].data_ptr(), t["justified_slot"].data_ptr(), t["shard_id"].data_ptr(),
+                           t["n_oblique"].data_ptr(), t["bits"].data_ptr(), t["boffs"].data_ptr(),
+                           t["block_slot"].data_ptr(), 0, 0, 128, 256, t["arr_offs"].data_ptr(),
+                           t["arr_shard"].data_ptr(), t["arr_comm"].data_ptr(), t["coffs"].data_ptr(),
+                           status.data_ptr(), comm.data_ptr(), pstart.data_ptr())
+    _lib.lib.call("pz_dev_check_attestations", ctypes.byref(b), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    port = cport.AttCheck(cols["slot"], cols["justified_slot"], cols["shard_id"], cols["n_oblique"], cols["bits"],
+                          cols["boffs"], cols["block_slot"])
+    try:
+        want = port.run(0, 0, 128, tab["arr_offs"], tab["arr_shard"], tab["arr_comm"], tab["coffs"])
+    finally:
+        port.close()
+    np.testing.assert_array_equal(status[:natt].cpu().numpy(), want)
+    ok = want == PROCESSED
+    np.testing.assert_array_equal(pstart[:natt].cpu().numpy()[ok], (cols["block_slot"] - cols["slot"])[ok].view(np.int64))
