@@ -10,6 +10,9 @@ namespace pz {
 
 struct WireValArgs {
   const uint64_t* col[5];  // public_key, withdrawal_shard, balance, start_dynasty, end_dynasty
+  const uint64_t* ccol[5];  // the non-NULL columns of col, in field order (scalar-only kernel)
+  uint32_t ctag[5];         // their proto3 tags
+  uint32_t nc;              // how many
   const uint8_t* wa;       // withdrawal_address bytes (CSR wa_offs, n+1; NULL offs = all empty)
   const uint64_t* wa_offs;
   const uint8_t* rc;       // randao_commitment bytes

@@ -56,24 +56,28 @@ __device__ __forceinline__ uint8_t* put_frame(const WireValArgs& a, uint8_t* p, 
 }
 
 // ---- scalar-only records -------------------------------------------------------------------
+// NC = the number of non-NULL columns (WireValArgs.ccol/ctag, in field order): a record holds
+// only those, so a tile's values fit in registers (3 columns for the chain's states).
+template <int NC>
 struct SRec {
-  uint64_t v[5];  // fields 1, 2, 5, 6, 7
+  uint64_t v[NC > 0 ? NC : 1];
 };
 
-__device__ __forceinline__ uint32_t srec_body(const SRec& r) {
+template <int NC>
+__device__ __forceinline__ uint32_t srec_body(const SRec<NC>& r) {
   uint32_t body = 0;
 #pragma unroll
-  for (int k = 0; k < 5; ++k) body += r.v[k] ? 1 + vlen(r.v[k]) : 0;
+  for (int k = 0; k < NC; ++k) body += r.v[k] ? 1 + vlen(r.v[k]) : 0;
   return body;
 }
 
-__device__ __forceinline__ uint8_t* put_srec(const WireValArgs& a, const SRec& r, uint32_t body, uint8_t* p) {
+template <int NC>
+__device__ __forceinline__ uint8_t* put_srec(const WireValArgs& a, const SRec<NC>& r, uint32_t body, uint8_t* p) {
   p = put_frame(a, p, body);
-  const uint8_t tags[5] = {1 << 3, 2 << 3, 5 << 3, 6 << 3, 7 << 3};
 #pragma unroll
-  for (int k = 0; k < 5; ++k)
+  for (int k = 0; k < NC; ++k)
     if (r.v[k]) {
-      *p++ = tags[k];
+      *p++ = (uint8_t)a.ctag[k];
       p = put_varint(p, r.v[k]);
     }
   return p;
@@ -265,19 +269,21 @@ __device__ __forceinline__ void store_stage(uint8_t* out, uint64_t base, const u
 
 // Record (j, p, t) of a tile = tile*kTileRecs + j*kSubRecs + p*kThreads + t: every column load
 // of a wave reads 512 contiguous bytes.
-__device__ __forceinline__ void load_sub(const WireValArgs& a, uint64_t first, SRec (&r)[kPer]) {
+template <int NC>
+__device__ __forceinline__ void load_sub(const WireValArgs& a, uint64_t first, SRec<NC> (&r)[kPer]) {
 #pragma unroll
   for (int p = 0; p < kPer; ++p) {
     const uint64_t i = first + p * kThreads + threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) r[p].v[k] = (a.col[k] && i < a.n) ? a.col[k][i] : 0;
+    for (int k = 0; k < NC; ++k) r[p].v[k] = i < a.n ? a.ccol[k][i] : 0;
   }
 }
 
 // Sizes of one sub-tile's records and their offsets inside the sub-tile (record order), from
 // ONE block scan: a record is at most 61 bytes and a sub-tile row p of 512 records at most
 // 31,232, so the four rows' sizes travel as four 16-bit lanes of one u64.
-__device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t first, const SRec (&r)[kPer],
+template <int NC>
+__device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t first, const SRec<NC> (&r)[kPer],
                                                 uint32_t (&body)[kPer], uint32_t (&off)[kPer], uint64_t* lds) {
   uint64_t packed = 0;
 #pragma unroll
@@ -299,23 +305,24 @@ __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t f
 }
 
 // One tile of kSub sub-tiles (4,096 records) per 512-thread workgroup, one ticket per tile.
-// Phase 1 loads each sub-tile's columns, keeps only the records' offsets inside the tile (one
-// block scan per sub-tile) and drops the values; the tile publishes its size and issues the
-// look-back's first window.  Phase 2 loads the columns again -- the tile's 96 KiB were just
-// read, so these come from L2 -- and builds the encoding in the 64 KiB LDS stage while the
-// look-back is in flight; after it the stage is stored with 16-B stores.  A tile whose
-// encoding outgrows the stage (records averaging over 16 bytes), or a call that wants record
-// offsets, writes lane by lane from registers instead.  Tiles are large because a single
-// contended ticket counter serialises its atomics (~11 ns each).
-// Measured (tools/wire_probe.py, 16.7 M records, us): r2b's 256-thread tiles of 2,048 with
-// every value held in registers through the scan (152 VGPRs) 255; reloading from L2 at 256
-// threads 296 (phase 1 got faster, the look-back's share grew); these 512-thread tiles 241.
+// Phase 1 loads every column of the tile into registers at once (NC per record: only the
+// non-NULL columns), sizes the records and scans each sub-tile (one block scan each); the tile
+// publishes its size and issues the look-back's first window, builds its encoding in the
+// 64 KiB LDS stage while that round trip is in flight, and after the look-back stores the
+// stage with 16-B stores.  A tile whose encoding outgrows the stage (records averaging over
+// 16 bytes), or a call that wants record offsets, writes lane by lane from registers instead.
+// Tiles are large because a single contended ticket counter serialises its atomics (~11 ns).
+// Measured (tools/wire_probe.py, 16.7 M records, us): r2b's 256-thread tiles of 2,048 with all
+// five column slots in registers (152 VGPRs) 255; dropping the values after phase 1 and
+// reloading them for the build (512-thread tiles) 241, but the reloads miss L2 (96 KiB per
+// tile x 64 tiles per XCD > 4 MiB): 1,025 MB of traffic per launch against 654 algorithmic.
 // Dropped: building the stage by dword ORs from a register accumulator instead of byte
 // writes 305 (the 64-bit shifts cost more VALU than the LDS byte writes); persistent
 // workgroups pipelining the next tile's phase 1 under the look-back 278 (128 VGPRs + spills).
 // V: an ablation knob for tools/wire_probe.py (0 in the product; output wrong otherwise):
-// bit 0 tile = blockIdx (no ticket), bit 1 no stage build, bit 2 no look-back, bit 3 no store.
-template <int V>
+// bit 0 tile = blockIdx (no ticket), bit 1 no stage build, bit 2 no look-back, bit 3 no store,
+// bit 4 reload the values for the build instead of holding them.
+template <int V, int NC>
 __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   __shared__ uint64_t lds[kThreads / 64 + 1];
   __shared__ uint32_t s_tile, s_first;
@@ -328,20 +335,20 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   __syncthreads();
   const uint32_t tile = s_tile;
   const uint64_t tfirst = (uint64_t)tile * kTileRecs;
+  constexpr bool kHold = !(V & 16) && NC <= 3;  // 4-5 columns held would spill: reload them
   // phase 1: sizes -> offsets inside the tile
-  uint32_t off[kSub][kPer], agg = 0;
+  SRec<NC> r[kSub][kPer];
+  uint32_t off[kSub][kPer], body[kSub][kPer], agg = 0;
 #pragma unroll
   for (int j = 0; j < kSub; ++j) {
-    SRec r[kPer];
-    uint32_t body[kPer];
-    load_sub(a, tfirst + (uint64_t)j * kSubRecs, r);
-    const uint32_t sub = sub_offsets(a, tfirst + (uint64_t)j * kSubRecs, r, body, off[j], lds);
+    load_sub(a, tfirst + (uint64_t)j * kSubRecs, r[kHold ? j : 0]);
+    const uint32_t sub = sub_offsets(a, tfirst + (uint64_t)j * kSubRecs, r[kHold ? j : 0], body[j], off[j], lds);
 #pragma unroll
     for (int p = 0; p < kPer; ++p) off[j][p] += agg;
     agg += sub;
   }
   if (threadIdx.x == 0) st_status(a.status + tile, (tile == 0 ? kFlagP : kFlagA) | agg);
-  // the look-back's first round trip overlaps phase 2
+  // the look-back's first round trip overlaps the stage build
   uint64_t w[kLbPer];
   if (!(V & 4) && tile > 0) lookback_issue(a.status, tile, w);
   const bool staged = agg <= kStageBytes && !a.offs;
@@ -349,11 +356,11 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
     uint8_t* st = reinterpret_cast<uint8_t*>(stage);
 #pragma unroll
     for (int j = 0; j < kSub; ++j) {
-      SRec r[kPer];
-      load_sub(a, tfirst + (uint64_t)j * kSubRecs, r);
+      if (!kHold) load_sub(a, tfirst + (uint64_t)j * kSubRecs, r[0]);
 #pragma unroll
       for (int p = 0; p < kPer; ++p)
-        if (tfirst + j * kSubRecs + p * kThreads + threadIdx.x < a.n) put_srec(a, r[p], srec_body(r[p]), st + off[j][p]);
+        if (tfirst + j * kSubRecs + p * kThreads + threadIdx.x < a.n)
+          put_srec(a, r[kHold ? j : 0][p], body[j][p], st + off[j][p]);
     }
   }
   uint64_t base = 0;
@@ -374,29 +381,38 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   }
 #pragma unroll
   for (int j = 0; j < kSub; ++j) {
-    SRec r[kPer];
-    load_sub(a, tfirst + (uint64_t)j * kSubRecs, r);
+    if (!kHold) load_sub(a, tfirst + (uint64_t)j * kSubRecs, r[0]);
 #pragma unroll
     for (int p = 0; p < kPer; ++p) {
       const uint64_t i = tfirst + j * kSubRecs + p * kThreads + threadIdx.x;
       if (i < a.n) {
         const uint64_t o = base + off[j][p];
         if (a.offs) a.offs[i] = o;
-        put_srec(a, r[p], srec_body(r[p]), a.out + o);
+        put_srec(a, r[kHold ? j : 0][p], body[j][p], a.out + o);
       }
     }
   }
 }
 
-#define PZ_WIRE_VAL_KERNEL(NAME, V) \
-  extern "C" __global__ void __launch_bounds__(kThreads) NAME(WireValArgs a, uint32_t nt) { wire_val_body<V>(a, nt); }
-PZ_WIRE_VAL_KERNEL(pz_wire_val_kernel, 0)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v1_kernel, 1)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v2_kernel, 2)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v4_kernel, 4)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v8_kernel, 8)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v7_kernel, 7)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v15_kernel, 15)
+#define PZ_WIRE_VAL_KERNEL(NAME, V, NC)                                        \
+  extern "C" __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) \
+  NAME(WireValArgs a, uint32_t nt) {                                             \
+    wire_val_body<V, NC>(a, nt);                                                 \
+  }
+PZ_WIRE_VAL_KERNEL(pz_wire_val_c0_kernel, 0, 0)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_c1_kernel, 0, 1)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_c2_kernel, 0, 2)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_kernel, 0, 3)  // the chain's states: balance, start, end
+PZ_WIRE_VAL_KERNEL(pz_wire_val_c4_kernel, 0, 4)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_c5_kernel, 0, 5)
+// ablation variants (3 columns)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v1_kernel, 1, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v2_kernel, 2, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v4_kernel, 4, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v8_kernel, 8, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v7_kernel, 7, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v15_kernel, 15, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v16_kernel, 16, 3)
 #undef PZ_WIRE_VAL_KERNEL
 
 // Records with bytes fields: tiles of kBytesSub x 256 records, one per thread per sub-tile.
@@ -469,18 +485,40 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
   }
   a.status = scratch;
   a.ticket = reinterpret_cast<uint32_t*>(scratch + nt);
+  a.nc = 0;  // the non-NULL columns, in field order (the scalar-only kernel holds only these)
+  const uint32_t tags[5] = {1 << 3, 2 << 3, 5 << 3, 6 << 3, 7 << 3};
+  for (int k = 0; k < 5; ++k)
+    if (a.col[k]) {
+      a.ccol[a.nc] = a.col[k];
+      a.ctag[a.nc++] = tags[k];
+    }
   hipError_t e = hipMemsetAsync(scratch, 0, (nt + 1) * 8, s);
   if (e != hipSuccess) return e;
   if (bytes)
     hipLaunchKernelGGL(pz_wire_val_bytes_kernel, dim3((uint32_t)nt), dim3(kThreads), 0, s, a, (uint32_t)nt);
   else
-    switch (g_wire_variant) {
+  {
+    const dim3 g((uint32_t)nt), b(kThreads);
+    const uint32_t n32 = (uint32_t)nt;
+    if (g_wire_variant && a.nc == 3) {
+      switch (g_wire_variant) {
 #define PZ_CASE(V) \
-  case V: hipLaunchKernelGGL(pz_wire_val_v##V##_kernel, dim3((uint32_t)nt), dim3(kThreads), 0, s, a, (uint32_t)nt); break;
-      PZ_CASE(1) PZ_CASE(2) PZ_CASE(4) PZ_CASE(8) PZ_CASE(7) PZ_CASE(15)
+  case V: hipLaunchKernelGGL(pz_wire_val_v##V##_kernel, g, b, 0, s, a, n32); break;
+        PZ_CASE(1) PZ_CASE(2) PZ_CASE(4) PZ_CASE(8) PZ_CASE(7) PZ_CASE(15) PZ_CASE(16)
 #undef PZ_CASE
-      default: hipLaunchKernelGGL(pz_wire_val_kernel, dim3((uint32_t)nt), dim3(kThreads), 0, s, a, (uint32_t)nt);
+        default: hipLaunchKernelGGL(pz_wire_val_kernel, g, b, 0, s, a, n32);
+      }
+    } else {
+      switch (a.nc) {
+        case 0: hipLaunchKernelGGL(pz_wire_val_c0_kernel, g, b, 0, s, a, n32); break;
+        case 1: hipLaunchKernelGGL(pz_wire_val_c1_kernel, g, b, 0, s, a, n32); break;
+        case 2: hipLaunchKernelGGL(pz_wire_val_c2_kernel, g, b, 0, s, a, n32); break;
+        case 3: hipLaunchKernelGGL(pz_wire_val_kernel, g, b, 0, s, a, n32); break;
+        case 4: hipLaunchKernelGGL(pz_wire_val_c4_kernel, g, b, 0, s, a, n32); break;
+        default: hipLaunchKernelGGL(pz_wire_val_c5_kernel, g, b, 0, s, a, n32);
+      }
     }
+  }
   return hipGetLastError();
 }
 
