@@ -356,6 +356,11 @@ typedef struct pz_vote_batch {
   uint64_t words_per_slot;     /* >= ceil(nval / 32) */
   uint64_t* totals;            /* [nslots] in/out (VoteTotalDeposit) */
   uint64_t* err;               /* [1] in/out */
+  uint64_t val_offset;         /* validator-range shard: this rank holds
+                                  validators [val_offset, val_offset + nval) of nval_global;
+                                  balance and the bitmaps index v - val_offset and the members
+                                  outside the range are skipped (another rank adds them) */
+  uint64_t nval_global;        /* 0: no shard (nval_global = nval, val_offset = 0) */
 } pz_vote_batch;
 
 int pz_dev_vote_tally(const pz_vote_batch* b, void* stream);
@@ -366,6 +371,21 @@ int pz_vote_tally(const uint32_t* committee, const uint64_t* coffs, uint64_t nco
                   uint64_t natt, const uint32_t* item_att, const uint32_t* item_slot,
                   uint64_t nitems, const uint64_t* balance, uint64_t nval, uint32_t* bitmaps,
                   uint64_t nslots, uint64_t words_per_slot, uint64_t* totals);
+
+typedef struct pz_comm pz_comm;  /* the ranks of a multi-GPU partition ("multi-GPU" below) */
+/* The same tally sharded by validator range over the ranks of `comm`:
+ * every local rank tallies the items' committee members in its 64-aligned validator range
+ * [lo, hi) into its slice of the bitmaps (words [lo/32, hi/32) of every slot), and one RCCL
+ * all-reduce (u64 sum) of the per-slot partial totals gives every rank the totals
+ * (stateRecalc reads them, core.go:413-418).  Dedup stays exact: a voter's bit lives on the
+ * one rank that owns it.  Host arrays as in pz_vote_tally; `totals` receives the global
+ * totals; only the bitmap words of this process's local ranks are written back (one process
+ * per GPU: each process holds its own slice). */
+int pz_comm_vote_tally(const pz_comm* comm, const uint32_t* committee, const uint64_t* coffs, uint64_t ncomm,
+                       const uint32_t* att_comm, const uint8_t* bits, const uint64_t* boffs, uint64_t natt,
+                       const uint32_t* item_att, const uint32_t* item_slot, uint64_t nitems,
+                       const uint64_t* balance, uint64_t nval, uint32_t* bitmaps, uint64_t nslots,
+                       uint64_t words_per_slot, uint64_t* totals);
 
 /* Pass 1 (pre-reward balances): classify/count, attester popcount, crosslink tallies. */
 int pz_dev_epoch_count(const pz_epoch_batch* b, void* stream);

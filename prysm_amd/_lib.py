@@ -80,6 +80,7 @@ SIGNATURES = {
     "pz_chain_vote_totals": [vp, vp, vp, u64, c_u64p],
     "pz_dev_vote_tally": [vp, vp],
     "pz_vote_tally": [vp, vp, u64, vp, vp, vp, u64, vp, vp, u64, vp, u64, vp, u64, u64, vp],
+    "pz_comm_vote_tally": [vp, vp, vp, u64, vp, vp, vp, u64, vp, vp, u64, vp, u64, vp, u64, u64, vp],
     "pz_wire_validators_bound": [u64, u64],
     "pz_wire_scratch_bytes": [u64],
     "pz_wire_validators": [vp, u64, u32, vp, u64, vp, c_u64p],
@@ -149,6 +150,7 @@ class VoteBatch(ctypes.Structure):
         ("committee", vp), ("coffs", vp), ("att_comm", vp), ("bits", vp), ("boffs", vp),
         ("item_att", vp), ("item_slot", vp), ("nitems", u64), ("balance", vp), ("nval", u64),
         ("bitmaps", vp), ("words_per_slot", u64), ("totals", vp), ("err", vp),
+        ("val_offset", u64), ("nval_global", u64),
     ]
 
 

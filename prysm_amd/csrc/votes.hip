@@ -23,10 +23,14 @@ __device__ __forceinline__ uint64_t wsum64(uint64_t v) {
 }
 
 // One wave: attestation `att` (committee c, bitfield) adds its new voters to `slot`.
+// A validator-range shard (lo, nval of nval_global) adds only its own members: balance and
+// bm are indexed by v - lo.
 __device__ __forceinline__ void tally_item(const uint32_t* __restrict__ committee, const uint64_t* __restrict__ coffs,
                                            uint32_t c, const uint8_t* bf, uint64_t blen,
                                            const uint64_t* __restrict__ balance, uint64_t nval, uint32_t* bm,
-                                           uint64_t* total, uint64_t* errp) {
+                                           uint64_t* total, uint64_t* errp, uint64_t lo = 0,
+                                           uint64_t nval_global = 0) {
+  if (!nval_global) nval_global = nval;
   const int lane = threadIdx.x & 63;
   const uint64_t cb = coffs[c], k = coffs[c + 1] - cb;
   uint64_t add = 0, err = 0;
@@ -34,14 +38,16 @@ __device__ __forceinline__ void tally_item(const uint32_t* __restrict__ committe
     if (i >= 8 * blen) { err |= PZ_XLERR_BITFIELD; continue; }  // CheckBit would panic
     if (!((bf[i >> 3] >> (7 - (uint32_t)(i & 7))) & 1u)) continue;
     const uint32_t v = committee[cb + i];
-    if (v >= nval) { err |= PZ_XLERR_MEMBER; continue; }
-    const uint32_t m = 1u << (v & 31);
+    if (v >= nval_global) { err |= PZ_XLERR_MEMBER; continue; }
+    const uint64_t lv = (uint64_t)v - lo;  // wraps huge below the range
+    if (lv >= nval) continue;              // another rank's validator
+    const uint32_t m = 1u << (lv & 31);
     // Voter bits only ever get set, so a plain read that already shows the bit is final;
     // a stale 0 (another XCD's L2) just falls through to the atomic, which decides.  After
     // the first attestation of a committee most voters are set: the atomics mostly vanish.
-    if (bm[v >> 5] & m) continue;
-    const uint32_t old = atomicOr(&bm[v >> 5], m);
-    if (!(old & m)) add += balance[v];
+    if (bm[lv >> 5] & m) continue;
+    const uint32_t old = atomicOr(&bm[lv >> 5], m);
+    if (!(old & m)) add += balance[lv];
   }
   add = wsum64(add);
   const uint64_t e1 = __ballot(err != 0);
@@ -59,7 +65,7 @@ pz_vote_tally_kernel(VoteArgs a) {
   const uint32_t slot = a.item_slot[item];
   const uint64_t bb = a.boffs[att];
   tally_item(a.committee, a.coffs, a.att_comm[att], a.bits + bb, a.boffs[att + 1] - bb, a.balance, a.nval,
-             a.bitmaps + (uint64_t)slot * a.words_per_slot, a.totals + slot, a.err);
+             a.bitmaps + (uint64_t)slot * a.words_per_slot, a.totals + slot, a.err, a.val_offset, a.nval_global);
 }
 
 // The block engine's form: work item (attestation, j) for each of its 64 signed parent

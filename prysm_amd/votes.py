@@ -47,17 +47,23 @@ class VoteCache:
         bits = np.unpackbits(self.bitmaps[s].view(np.uint8), bitorder="little")[:self.nval]
         return np.nonzero(bits)[0].astype(np.uint32)
 
-    def tally(self, committee, coffs, att_comm, bits, boffs, items, balance):
-        """Apply work items [(attestation index, slot)] in one GPU launch."""
+    def tally(self, committee, coffs, att_comm, bits, boffs, items, balance, comm=None):
+        """Apply work items [(attestation index, slot)] in one GPU launch; with ``comm`` (a
+        ``prysm_amd.native.Comm``) sharded by validator range over its ranks, the per-slot
+        totals combined by one all-reduce (pz_comm_vote_tally)."""
         if not items:
             return
         ia = np.ascontiguousarray([a for a, _ in items], dtype=np.uint32)
         isl = np.ascontiguousarray([s for _, s in items], dtype=np.uint32)
         bm = np.ascontiguousarray(self.bitmaps)
         tt = np.ascontiguousarray(self.totals)
-        lib.call("pz_vote_tally", ptr(committee), ptr(coffs), len(coffs) - 1, ptr(att_comm), ptr(bits), ptr(boffs),
-                 len(att_comm), ptr(ia), ptr(isl), len(items), ptr(np.ascontiguousarray(balance, dtype=np.uint64)),
-                 self.nval, ptr(bm), bm.shape[0], self.words, ptr(tt))
+        args = (ptr(committee), ptr(coffs), len(coffs) - 1, ptr(att_comm), ptr(bits), ptr(boffs),
+                len(att_comm), ptr(ia), ptr(isl), len(items), ptr(np.ascontiguousarray(balance, dtype=np.uint64)),
+                self.nval, ptr(bm), bm.shape[0], self.words, ptr(tt))
+        if comm is None:
+            lib.call("pz_vote_tally", *args)
+        else:
+            lib.call("pz_comm_vote_tally", comm.h, *args)
         self.bitmaps, self.totals = bm, tt
 
 

@@ -11,7 +11,12 @@ pytestmark = pytest.mark.gpu
 U64 = np.uint64
 
 
-def test_vote_cache_vs_oracle():
+@pytest.mark.parametrize("world", [0, 1, 2, 3, 8])
+def test_vote_cache_vs_oracle(world):
+    """world 0: the one-GPU tally; world >= 1: pz_comm_vote_tally sharded by validator range
+    over a loopback communicator, the per-slot totals all-reduced."""
+    from prysm_amd.native import Comm
+    comm = Comm.loopback(world) if world else None
     rng = np.random.default_rng(12)
     nval = 3000
     _, cs = ref.new_genesis_states(nval)
@@ -57,8 +62,34 @@ def test_vote_cache_vs_oracle():
             boffs.append(boffs[-1] + len(a.attester_bitfield))
             att_comm.append(key[(a.slot, a.shard_id)])
         vc.tally(committee, coffs, np.array(att_comm, np.uint32), np.concatenate(bits), np.array(boffs, U64),
-                 items, balance)
+                 items, balance, comm=comm)
     assert set(vc.slot_of) == set(cache_o)
     for h, (voters, total) in cache_o.items():
         assert vc.total(h) == total
         assert vc.voters(h).tolist() == sorted(voters)
+
+
+def test_sharded_vote_tally_panics():
+    """A committee member >= len(validators) (core.go:329 indexes Validators[v]) and a short
+    bitfield (CheckBit, core.go:328): the sharded tally raises PZ_EINDEX like the one-GPU form."""
+    from prysm_amd import _lib
+    from prysm_amd.native import Comm
+    nval = 1000
+    committee = np.arange(200, dtype=np.uint32)
+    coffs = np.array([0, 100, 200], U64)
+    balance = np.full(nval, 5, U64)
+    for bad in ("member", "bitfield"):
+        c = committee.copy()
+        bits = np.full(26, 0xFF, np.uint8)
+        boffs = np.array([0, 13, 26], U64)
+        if bad == "member":
+            c[150] = nval + 3
+        else:
+            bits, boffs = bits[:25], np.array([0, 13, 25], U64)
+        for world in (0, 3):
+            vc = VoteCache(nval)
+            items = [(0, vc.slot(b"a" * 32)), (1, vc.slot(b"b" * 32))]
+            with pytest.raises(_lib.PzError) as e:
+                vc.tally(c, coffs, np.array([0, 1], np.uint32), bits, boffs, items, balance,
+                         comm=Comm.loopback(world) if world else None)
+            assert e.value.code == _lib.PZ_EINDEX, (bad, world)
