@@ -801,11 +801,15 @@ constexpr uint32_t kNoAtt = 0xFFFFFFFEu, kManyAtt = 0xFFFFFFFFu;
 // MODE: an ablation knob for tools/ (0 in the product; results are wrong otherwise): bit 0 no
 // crosslink tallies, bit 1 reward bit from the balance instead of the last bitfield, bit 2 no
 // balance store, bit 3 no start/end loads (every validator taken as active), bit 4 start/end
-// loads with the default cache policy, bit 5 instance-minor grid.
+// loads with the default cache policy, bit 5 instance-major grid.
 //
 // Measured choices (tools/fused_parts.py, 65,536 x 256 / 1M x 16 step, us): start/end loads
 // nontemporal (read once per step: leaving the 256 MiB Infinity Cache to the balances, which
-// are read and written) 142 -> 128 / 132 -> 122; instance-major grid (DRAM locality) -> 126 / 119.
+// are read and written) 142 -> 128 / 132 -> 122.  Grid order: instance-major won before the
+// block-merged tally atomics (126 / 119 against 128 / 122); with them instance-minor is
+// 2-5 us faster on every box measured since (107 / 100 against 110 / 103).  Staging the last
+// bitfield in LDS (65,536 validators: 8 KiB per instance) measured 112 against 110: the block
+// barrier costs more than the random L2 lookups it removes.
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld16_nt(const uint64_t* p) {
   const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
@@ -822,8 +826,8 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
   // per wave: {attestation of its committee (single-attestation committees), total, vote, next sum, nomatch}
   __shared__ uint64_t xt[kFusedWaves], xv[kFusedWaves], xs[kFusedWaves], xn[kFusedWaves];
   __shared__ uint32_t xg[kFusedWaves];
-  const uint64_t inst = (MODE & 32) ? blockIdx.x : blockIdx.y;
-  const uint64_t grp = (MODE & 32) ? blockIdx.y : blockIdx.x;
+  const uint64_t inst = (MODE & 32) ? blockIdx.y : blockIdx.x;
+  const uint64_t grp = (MODE & 32) ? blockIdx.x : blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint64_t item = grp * kFusedWaves + wave;
@@ -836,8 +840,11 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
   const bool applied = thr && !skip;
   uint64_t sum = 0, nm = 0, ts = 0, vs = 0;
   uint32_t g1 = kNoAtt;  // the wave's single attestation, combined across the block below
-  if (item < f.nitems) {
-    const uint4 it = items_ro[item];  // {first position, count, committee, committee start}
+  // every wave runs the body (a wave without a piece has no element in range)
+  const bool have = item < f.nitems;
+  {
+    // {first position, count, committee, committee start}
+    const uint4 it = have ? items_ro[item] : make_uint4((uint32_t)a.val_offset, 0, 0, (uint32_t)a.val_offset);
     const uint64_t ws = it.x, we = (uint64_t)it.x + it.y, cb = it.w;
     const uint64_t p0 = (ws & ~1ull) - a.val_offset;  // local, even (val_offset is 64-aligned)
     uint64_t* Bal = a.balance + inst * a.nval;
@@ -1108,12 +1115,13 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f, hipStream_
   if (!a.ninst) return hipSuccess;
   const uint64_t groups = (f.nitems + kFusedWaves - 1) / kFusedWaves;
   if (!groups) return hipSuccess;
-  // instance-major: x = piece group, y = instance (ablation 32: instance-minor)
-  const dim3 grid = (g_fused_variant & 32) ? dim3(a.ninst, (uint32_t)groups) : dim3((uint32_t)groups, a.ninst);
+  const int variant = g_fused_variant;
+  // instance-minor: x = instance, y = piece group (ablation 32: instance-major)
+  const dim3 grid = (variant & 32) ? dim3((uint32_t)groups, a.ninst) : dim3(a.ninst, (uint32_t)groups);
   const dim3 block(64 * kFusedWaves);
 #define PZ_LAUNCH_FUSED(K) \
   hipLaunchKernelGGL(K, grid, block, 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt)
-  switch (g_fused_variant) {
+  switch (variant) {
     case 1: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg1_kernel); break;
     case 2: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg2_kernel); break;
     case 3: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg3_kernel); break;
