@@ -171,20 +171,21 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    # one event pair around the K back-to-back steps: the average launch duration without
+    # per-step event packets between the launches (what rocprofv3's kernel trace averages)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for e0, e1 in evs:
-        e0.record(stream)
+    ev0.record(stream)
+    for _ in range(args.steps):
         step()
-        e1.record(stream)
+    ev1.record(stream)
     stream.synchronize()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    step_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    step_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
         wall = max_over_ranks(wall, torch, dist, dev)
     units = nval * ninst * args.steps
@@ -335,19 +336,20 @@ def wire_leg(args, torch, dist, dev, rank, world):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    # one event pair around the K back-to-back steps: the average launch duration without
+    # per-step event packets between the launches (what rocprofv3's kernel trace averages)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for e0, e1 in evs:
-        e0.record(stream)
+    ev0.record(stream)
+    for _ in range(args.steps):
         step()
-        e1.record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    step_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    step_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
         wall = max_over_ranks(wall, torch, dist, dev)
     total = int(d_tot.item())
@@ -542,18 +544,20 @@ def attcheck_leg(args, torch, dist, dev, rank, world):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # one event pair around the K back-to-back steps: the average launch duration without
+    # per-step event packets between the launches (what rocprofv3's kernel trace averages)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for e0, e1 in evs:
-        e0.record(stream)
+    ev0.record(stream)
+    for _ in range(args.steps):
         step()
-        e1.record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    step_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    step_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
         wall = max_over_ranks(wall, torch, dist, dev)
     alg = natt * ATT_BYTES
@@ -852,19 +856,20 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    # one event pair around the K back-to-back steps: the average launch duration without
+    # per-step event packets between the launches (what rocprofv3's kernel trace averages)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for e0, e1 in evs:
-        e0.record(stream)
+    ev0.record(stream)
+    for _ in range(args.steps):
         step()
-        e1.record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
         wall = max_over_ranks(wall, torch, dist, dev)
 
