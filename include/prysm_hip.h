@@ -448,8 +448,11 @@ int pz_comm_blake2b512_batch(const pz_comm* comm, const uint8_t* msgs, const uin
  * In committee order, unless some attestation names a shard >= nrec (that panic depends on
  * the tallies), the step is one pass over the validators instead:
  *   bit count -> one stream (classify, crosslink tallies on the pre-reward balances, reward,
- *   next-cycle sum) -> RCCL all-reduce {scal, vote, total} -> winners
- * (32 B per validator-epoch instead of 40; one collective per part).
+ *   next-cycle sum) -> winners -> one grouped RCCL collective (u64 sum of scal, u32 minimum
+ *   of the winners)
+ * (32 B per validator-epoch instead of 40).  Its ranks hold committee-aligned ranges, so the
+ * vote/total of an attestation are complete on the rank holding its committee;
+ * pz_epoch_state_tallies completes them everywhere.
  * Results are those of pz_dev_epoch_count/finish (bit-exact with the reference; panics
  * reported in scal[PZ_SCAL_ERR_*] with the balances untouched). */
 typedef struct pz_epoch_host {
@@ -494,6 +497,11 @@ int  pz_epoch_state_results(pz_epoch_state* st, int local, uint64_t* balance, ui
  * index order; the members of the committees, in committee order, in the committee-order
  * layout (pz_epoch_batch.co_index), which *committee_order reports. */
 int  pz_epoch_state_validators(const pz_epoch_state* st, int local, uint32_t* index);
+/* The sharded one-pass step leaves each attestation's vote/total complete only on the rank
+ * holding its committee (its winners are exact everywhere: proposed by that rank, combined by
+ * a minimum all-reduce); this collective (every rank calls it) completes them on every rank
+ * for pz_epoch_state_results.  A no-op for the other steps. */
+int  pz_epoch_state_tallies(pz_epoch_state* st);
 /* *committee_order: 0 index order, 1 committee order (two-pass step), 2 committee order with
  * the one-pass step. */
 int  pz_epoch_state_layout(const pz_epoch_state* st, int* committee_order);

@@ -117,6 +117,7 @@ SIGNATURES = {
     "pz_epoch_state_free": [vp],
     "pz_epoch_state_validators": [vp, ctypes.c_int, vp],
     "pz_epoch_state_layout": [vp, c_intp],
+    "pz_epoch_state_tallies": [vp],
 }
 
 

@@ -60,6 +60,10 @@ struct pz_comm {
   // starts after everything enqueued so far on compute[i]; done[i] is recorded when local
   // rank i's result is ready.
   int allreduce_u64(uint64_t* const* bufs, size_t count, const hipStream_t* compute, hipEvent_t* done);
+  // One group of two all-reduces in place: a u64 sum over sbufs (scount) and a u32 minimum
+  // over mbufs (mcount) -- one collective launch on RCCL.
+  int allreduce_sum_min(uint64_t* const* sbufs, size_t scount, uint32_t* const* mbufs, size_t mcount,
+                        const hipStream_t* compute, hipEvent_t* done);
   // All-gather: local rank i contributes `bytes` from send[i]; recv[i] receives all ranks'
   // contributions, rank-major (world * bytes).
   int allgather(const void* const* send, void* const* recv, size_t bytes, const hipStream_t* compute,

@@ -70,6 +70,19 @@ pz_loopback_sum_kernel(LoopPtrs ptrs, int world, uint64_t count) {
   for (int r = 0; r < world; ++r) ptrs.p[r][i] = s;
 }
 
+struct LoopPtrs32 {
+  uint32_t* p[kMaxLoopback];
+};
+
+extern "C" __global__ void __launch_bounds__(256)
+pz_loopback_min_kernel(LoopPtrs32 ptrs, int world, uint64_t count) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= count) return;
+  uint32_t m = 0xFFFFFFFFu;
+  for (int r = 0; r < world; ++r) m = min(m, ptrs.p[r][i]);
+  for (int r = 0; r < world; ++r) ptrs.p[r][i] = m;
+}
+
 }  // namespace
 
 int rccl_api(const RcclApi** out) {
@@ -124,6 +137,44 @@ int pz_comm::allreduce_u64(uint64_t* const* bufs, size_t count, const hipStream_
       }
       ncclResult_t g = nlocal > 1 ? api->GroupEnd() : ncclSuccess;
       if (r != ncclSuccess) return nccl_fail(api, r, "ncclAllReduce");
+      if (g != ncclSuccess) return nccl_fail(api, g, "ncclGroupEnd");
+    }
+  }
+  return mark_done(this, done);
+}
+
+int pz_comm::allreduce_sum_min(uint64_t* const* sbufs, size_t scount, uint32_t* const* mbufs, size_t mcount,
+                               const hipStream_t* compute, hipEvent_t* done) {
+  int rc = order_after(this, compute);
+  if (rc) return rc;
+  if (world > 1 && (scount || mcount)) {
+    if (kind == LOOPBACK) {
+      (void)hipSetDevice(dev[0]);
+      if (scount) {
+        LoopPtrs p;
+        for (int r = 0; r < world; ++r) p.p[r] = sbufs[r];
+        hipLaunchKernelGGL(pz_loopback_sum_kernel, dim3((uint32_t)((scount + 255) / 256)), dim3(256), 0, cstream[0],
+                           p, world, (uint64_t)scount);
+      }
+      if (mcount) {
+        LoopPtrs32 p;
+        for (int r = 0; r < world; ++r) p.p[r] = mbufs[r];
+        hipLaunchKernelGGL(pz_loopback_min_kernel, dim3((uint32_t)((mcount + 255) / 256)), dim3(256), 0, cstream[0],
+                           p, world, (uint64_t)mcount);
+      }
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return hip_fail(e, "loopback sum/min");
+    } else {
+      api->GroupStart();
+      ncclResult_t r = ncclSuccess;
+      for (int i = 0; i < nlocal && r == ncclSuccess; ++i) {
+        (void)hipSetDevice(dev[i]);
+        if (scount) r = api->AllReduce(sbufs[i], sbufs[i], scount, ncclUint64, ncclSum, nccl[i], cstream[i]);
+        if (r == ncclSuccess && mcount)
+          r = api->AllReduce(mbufs[i], mbufs[i], mcount, ncclUint32, ncclMin, nccl[i], cstream[i]);
+      }
+      ncclResult_t g = api->GroupEnd();
+      if (r != ncclSuccess) return nccl_fail(api, r, "ncclAllReduce (sum/min)");
       if (g != ncclSuccess) return nccl_fail(api, g, "ncclGroupEnd");
     }
   }

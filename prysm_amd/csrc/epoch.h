@@ -81,9 +81,13 @@ struct FusedArgs {
   uint64_t* pre_next;         // [B][kPre] zeroed by `fused` for the next step (ping-pong)
   int rank0;                  // 1: this rank writes the per-instance scalars (bit count, flags,
                               //    applied, nact, max index) that the all-reduce must not multiply
+  uint64_t vstride;           // row stride of balance/start/end (>= nval, even)
+  int own_only;               // sharded: winners proposed only for the attestations whose
+                              //    committee this rank holds (pz_epoch_fwin_kernel)
 };
 hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
+hipError_t launch_epoch_fwin(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
 bool fused_ok(const EpochArgs& a);
 int set_fused_variant(int v);  // tools/ A/B only (pz_debug_set_fused_variant)  // 16-B vector path available (nval even, 16-B aligned arrays)
 

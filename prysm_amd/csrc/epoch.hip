@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/prysm_hip.h"
 #include "epoch.h"
 
@@ -846,10 +848,10 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     // {first position, count, committee, committee start}
     const uint4 it = have ? items_ro[item] : make_uint4((uint32_t)a.val_offset, 0, 0, (uint32_t)a.val_offset);
     const uint64_t ws = it.x, we = (uint64_t)it.x + it.y, cb = it.w;
-    const uint64_t p0 = (ws & ~1ull) - a.val_offset;  // local, even (val_offset is 64-aligned)
-    uint64_t* Bal = a.balance + inst * a.nval;
-    const uint64_t* S = a.start + inst * a.nval;
-    const uint64_t* E = a.end + inst * a.nval;
+    const uint64_t p0 = (ws - a.val_offset) & ~1ull;  // local and even: the 16-B pair of ws
+    uint64_t* Bal = a.balance + inst * f.vstride;
+    const uint64_t* S = a.start + inst * f.vstride;
+    const uint64_t* E = a.end + inst * f.vstride;
     const FusedCommittee ci = cinfo_ro[inst * f.ncomm + it.z];
     uint4 qb[2], qs[2], qe[2];
     uint2 cix[2];
@@ -1089,7 +1091,9 @@ hipError_t launch_epoch_compact(const EpochArgs& a, bool force, hipStream_t s) {
 }
 
 hipError_t launch_epoch_reward(const EpochArgs& a, hipStream_t s) {
-  const uint64_t vbpi = vblocks_per_inst(a.nval);
+  // at least one chunk per instance: chunk 0 also writes the per-instance scalars (applied,
+  // active count) and zeroes the next step's, even for a rank whose range is empty
+  const uint64_t vbpi = std::max<uint64_t>(1, vblocks_per_inst(a.nval));
   const uint64_t blocks = (uint64_t)a.ninst * vbpi;
   if (!blocks) return hipSuccess;
   hipLaunchKernelGGL(pz_epoch_reward_kernel, dim3(a.ninst, (uint32_t)vbpi), dim3(kThreads), 0, s, a, vbpi,
@@ -1097,8 +1101,34 @@ hipError_t launch_epoch_reward(const EpochArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// The one-pass stream loads 16-B pairs at even local indices: the arrays must be 16-B aligned
+// (an odd range's last pair reads the allocation's padding, and stores only its own element).
 bool fused_ok(const EpochArgs& a) {
-  return vec_ok(a) && a.co_index && a.natt && (reinterpret_cast<uintptr_t>(a.co_index) & 7) == 0;
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return al(a.start) && al(a.end) && al(a.balance) && a.co_index && a.natt &&
+         (reinterpret_cast<uintptr_t>(a.co_index) & 7) == 0;
+}
+
+// Winners of the one-pass step.  Sharded (f.own_only), committees never straddle ranks, so an
+// attestation's tallies are complete on the rank holding its committee's first position (the
+// last rank for an empty committee at the end) and zero elsewhere: each rank proposes the
+// winners among the attestations it owns and a u32 minimum all-reduce picks the first.
+extern "C" __global__ void __launch_bounds__(kThreads) pz_epoch_fwin_kernel(EpochArgs a, FusedArgs f) {
+  const uint64_t ga = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ga >= (uint64_t)a.ninst * a.natt) return;
+  if (f.own_only) {
+    const uint64_t cb = a.coffs[a.att_comm[ga]], lo = a.val_offset, hi = lo + a.nval;
+    if (!((cb >= lo && cb < hi) || (cb == a.nval_global && hi == a.nval_global))) return;
+  }
+  winner_one(a, ga);
+}
+
+hipError_t launch_epoch_fwin(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
+  const uint64_t n = (uint64_t)a.ninst * a.natt;
+  if (!n || !a.nrec) return hipSuccess;
+  hipLaunchKernelGGL(pz_epoch_fwin_kernel, dim3((uint32_t)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, a,
+                     f);
+  return hipGetLastError();
 }
 
 hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
@@ -1113,8 +1143,9 @@ hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f, hipStream_t 
 
 hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
   if (!a.ninst) return hipSuccess;
-  const uint64_t groups = (f.nitems + kFusedWaves - 1) / kFusedWaves;
-  if (!groups) return hipSuccess;
+  // at least one group: group 0 writes the per-instance scalars and zeroes the next step's
+  // accumulators, also on a rank whose range holds no piece
+  const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
   const int variant = g_fused_variant;
   // instance-minor: x = instance, y = piece group (ablation 32: instance-major)
   const dim3 grid = (variant & 32) ? dim3((uint32_t)groups, a.ninst) : dim3(a.ninst, (uint32_t)groups);

@@ -49,6 +49,8 @@ struct Shard {
   int dev = 0, grank = 0;
   hipStream_t s = nullptr;
   uint64_t lo = 0, hi = 0, n = 0, wl = 0;
+  uint64_t np = 0;  // row stride of the validator arrays: n, or n rounded up to even for the
+                    // one-pass step (its 16-B pairs start at even local indices of every row)
   std::vector<void*> allocs;
   Part part[2];
 };
@@ -106,11 +108,11 @@ int upload_range(Shard& s, uint64_t** p, const uint64_t* host, uint32_t B, uint6
 // Committee order: rows [0, B) of a host [B][N] array, the validators stored at positions
 // [lo, hi) (inv[p] = the validator at position p) -> device [B][hi-lo].
 int upload_perm(Shard& s, uint64_t** p, const uint64_t* host, uint32_t B, uint64_t N, const uint32_t* inv) {
-  int rc = dalloc(s, p, (size_t)B * s.n, false);
+  int rc = dalloc(s, p, (size_t)B * s.np, false);
   if (rc || !s.n) return rc;
-  std::vector<uint64_t> tmp((size_t)B * s.n);
+  std::vector<uint64_t> tmp((size_t)B * s.np, 0);  // rows of np (the pad element stays 0)
   for (uint64_t b = 0; b < B; ++b)
-    for (uint64_t q = 0; q < s.n; ++q) tmp[b * s.n + q] = host[b * N + inv[s.lo + q]];
+    for (uint64_t q = 0; q < s.n; ++q) tmp[b * s.np + q] = host[b * N + inv[s.lo + q]];
   hipError_t e = hipMemcpy(*p, tmp.data(), tmp.size() * 8, hipMemcpyHostToDevice);
   return e == hipSuccess ? PZ_OK : hip_fail(e, "hipMemcpy H2D (epoch state)");
 }
@@ -161,36 +163,42 @@ int wait(Shard& s, hipEvent_t ev) {
   return e == hipSuccess ? PZ_OK : hip_fail(e, "hipStreamWaitEvent");
 }
 
-// One-pass step at N > 1: every part's pre + fused pass, each followed by the all-reduce of
-// its partial sums (the next-cycle totals are among them), then the winners.
+// One-pass step at N > 1.  The ranks' ranges are committee-aligned, so every committee's
+// tallies are complete on one rank: per part, pre + fused + the winners each rank owns, then
+// ONE grouped collective -- a u64 sum of the per-instance scalars (partial next-cycle totals,
+// flags) and a u32 minimum of the proposed winners -- while the next part computes.  The
+// per-attestation vote/total stay on their owner ranks (pz_epoch_state_tallies completes
+// them on demand): 8 B x (8 + nrec/2) per instance cross xGMI instead of 16 B per attestation.
 int step_sharded_fused(pz_epoch_state* st) {
   pz_comm* c = st->comm;
   const int L = (int)st->sh.size();
   std::vector<hipStream_t> streams(L);
-  std::vector<uint64_t*> bufs(L);
+  std::vector<uint64_t*> sbufs(L);
+  std::vector<uint32_t*> mbufs(L);
   std::vector<hipEvent_t> evs(L);
   for (int i = 0; i < L; ++i) streams[i] = st->sh[i].s;
   int rc;
   for (uint32_t p = 0; p < st->nparts; ++p) {
     for (int i = 0; i < L; ++i) {
       Shard& s = st->sh[i];
+      Part& q = s.part[p];
       (void)hipSetDevice(s.dev);
-      hipError_t e = launch_epoch_pre(s.part[p].a, s.part[p].f, s.s);
-      if (e == hipSuccess) e = launch_epoch_fused(s.part[p].a, s.part[p].f, s.s);
+      hipError_t e = launch_epoch_pre(q.a, q.f, s.s);
+      if (e == hipSuccess) e = launch_epoch_fused(q.a, q.f, s.s);
+      if (e == hipSuccess) e = launch_epoch_fwin(q.a, q.f, s.s);
       if (e != hipSuccess) return hip_fail(e, "epoch one-pass");
-      bufs[i] = s.part[p].red[s.part[p].cur];
-      evs[i] = s.part[p].ev_red;
+      sbufs[i] = q.red[q.cur];
+      mbufs[i] = q.a.winner;
+      evs[i] = q.ev_red;
     }
     const uint64_t Bp = st->sh[0].part[p].B;
-    if ((rc = c->allreduce_u64(bufs.data(), Bp * kScal + 2 * Bp * st->natt, streams.data(), evs.data()))) return rc;
+    if ((rc = c->allreduce_sum_min(sbufs.data(), Bp * kScal, mbufs.data(), st->nrec ? Bp * st->nrec : 0,
+                                   streams.data(), evs.data())))
+      return rc;
   }
   for (uint32_t p = 0; p < st->nparts; ++p)
-    for (int i = 0; i < L; ++i) {
-      Shard& s = st->sh[i];
-      if ((rc = wait(s, s.part[p].ev_red))) return rc;
-      hipError_t e = launch_epoch_mid(s.part[p].a, st->nrec != 0, false, s.s);
-      if (e != hipSuccess) return hip_fail(e, "epoch winners");
-    }
+    for (int i = 0; i < L; ++i)
+      if ((rc = wait(st->sh[i], st->sh[i].part[p].ev_red))) return rc;
   return PZ_OK;
 }
 
@@ -296,6 +304,20 @@ int check_host(const pz_epoch_host* h) {
   return PZ_OK;
 }
 
+// Rank r's first storage position in the committee-order one-pass step: the committee start
+// nearest to r*N/world (so every committee, and its tallies, lives on one rank).
+uint64_t committee_boundary(const pz_epoch_host* h, uint64_t r, int world, uint64_t N) {
+  if (r == 0) return 0;
+  if (r >= (uint64_t)world) return N;
+  const uint64_t t = N * r / (uint64_t)world;
+  const uint64_t* e = h->coffs + h->ncomm + 1;
+  const uint64_t* it = std::lower_bound(h->coffs, e, t);
+  uint64_t b = it == e ? N : *it;
+  if (it != h->coffs && t - *(it - 1) < b - t) b = *(it - 1);
+  // monotone in r: never before the previous rank's boundary
+  return std::max<uint64_t>(b, r > 1 ? committee_boundary(h, r - 1, world, N) : 0);
+}
+
 // The committee CSR restricted to members in [lo, hi) (plus, on global rank 0, members >=
 // N, whose processCrosslinks panic that rank raises), each with its position in its full
 // committee.
@@ -372,9 +394,9 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
       st->co_inv.assign(h->committee, h->committee + st->N);
     }
   }
-  // One pass needs every shard on the 16-B path (N even) and no shard panic (it depends on the
-  // tallies, which the one pass forms while it rewards).
-  if (st->co && h->layout == PZ_LAYOUT_AUTO && st->N % 2 == 0) {
+  // One pass needs no shard panic (it depends on the tallies, which the one pass forms while
+  // it rewards).
+  if (st->co && h->layout == PZ_LAYOUT_AUTO) {
     st->fused = true;
     for (uint64_t i = 0; i < (uint64_t)st->B * st->natt && st->fused; ++i) st->fused = h->att_shard[i] < st->nrec;
   }
@@ -423,7 +445,12 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
     const uint64_t span = 64 * st->sw;
     s.lo = std::min<uint64_t>(st->N, (uint64_t)s.grank * span);
     s.hi = std::min<uint64_t>(st->N, (uint64_t)(s.grank + 1) * span);
+    if (st->fused && st->world > 1) {  // committee-aligned ranges: no committee straddles two ranks
+      s.lo = committee_boundary(h, (uint64_t)s.grank, st->world, st->N);
+      s.hi = committee_boundary(h, (uint64_t)s.grank + 1, st->world, st->N);
+    }
     s.n = s.hi - s.lo;
+    s.np = st->fused ? (s.n + 1) & ~1ull : s.n;
     s.wl = (s.n + 63) / 64;
     DeviceCtx* dc;
     if ((rc = device_ctx(s.dev, &dc))) break;
@@ -480,11 +507,12 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
     FusedCommittee* d_cinfo = nullptr;
     uint64_t nitems = 0;
     if (st->fused) {
-      // committee pieces inside [lo, hi): <= 256 positions, aligned to the committee's even base
+      // committee pieces inside [lo, hi): <= 256 positions from the committee's first even
+      // local position (local index = position - lo; the kernel pairs even local indices)
       std::vector<uint4> items;
       for (uint64_t c = 0; c < st->ncomm; ++c) {
         const uint64_t cb = h->coffs[c], ce = h->coffs[c + 1];
-        const uint64_t r0 = std::max(cb, s.lo), r1 = std::min(ce, s.hi), base = cb & ~1ull;
+        const uint64_t r0 = std::max(cb, s.lo), r1 = std::min(ce, s.hi), base = s.lo + ((r0 - s.lo) & ~1ull);
         for (uint64_t x = r0; x < r1;) {
           const uint64_t y = std::min(r1, base + ((x - base) / 256 + 1) * 256);
           items.push_back(make_uint4((uint32_t)x, (uint32_t)(y - x), (uint32_t)c, (uint32_t)cb));
@@ -528,9 +556,9 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
       a.val_offset = s.lo;
       a.nval_global = st->N;
       a.kind = PZ_KIND_ACTIVE;
-      a.balance = bal + i0 * s.n;
-      a.start = start + i0 * s.n;
-      a.end = end + i0 * s.n;
+      a.balance = bal + i0 * s.np;
+      a.start = start + i0 * s.np;
+      a.end = end + i0 * s.np;
       a.dynasty = dyn + i0;
       a.total_deposit = tdep + i0;
       a.natt = st->natt;
@@ -562,6 +590,8 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
         q.f.catt = d_catt + i0 * st->natt;
         q.f.ncomm = st->ncomm;
         q.f.rank0 = s.grank == 0 ? 1 : 0;
+        q.f.own_only = st->world > 1 ? 1 : 0;
+        q.f.vstride = s.np;
         if (!fused_ok(a)) rc = fail(PZ_EINVAL, "one-pass epoch: validator arrays not on the 16-B path");
       }
       q.cur = 1;  // flip() below binds red[0] as the first step's buffer
@@ -626,7 +656,8 @@ int pz_epoch_state_results(pz_epoch_state* st, int local, uint64_t* balance, uin
   for (uint32_t p = 0; p < st->nparts && e == hipSuccess; ++p) {
     const Part& q = s.part[p];
     const uint64_t Bp = q.B, i0 = q.i0, na = st->natt;
-    if (balance && s.n) e = hipMemcpy(balance + i0 * s.n, q.a.balance, Bp * s.n * 8, hipMemcpyDeviceToHost);
+    if (balance && s.n)
+      e = hipMemcpy2D(balance + i0 * s.n, s.n * 8, q.a.balance, s.np * 8, s.n * 8, Bp, hipMemcpyDeviceToHost);
     if (e == hipSuccess && scal) e = hipMemcpy(scal + i0 * kScal, q.results, Bp * kScal * 8, hipMemcpyDeviceToHost);
     if (e == hipSuccess && vote && na)
       e = hipMemcpy(vote + i0 * na, q.results + Bp * kScal, Bp * na * 8, hipMemcpyDeviceToHost);
@@ -639,11 +670,36 @@ int pz_epoch_state_results(pz_epoch_state* st, int local, uint64_t* balance, uin
 }
 
 int pz_epoch_state_validators(const pz_epoch_state* st, int local, uint32_t* index) {
-  if (!st || !index) return fail(PZ_EINVAL, "null pointer");
+  if (!st) return fail(PZ_EINVAL, "null pointer");
   if (local < 0 || local >= (int)st->sh.size()) return fail(PZ_EINVAL, "local rank %d of %zu", local, st->sh.size());
   const Shard& s = st->sh[local];
+  if (!index && s.n) return fail(PZ_EINVAL, "null pointer");  // an empty range may pass NULL
   for (uint64_t q = 0; q < s.n; ++q) index[q] = st->co ? st->co_inv[s.lo + q] : (uint32_t)(s.lo + q);
   return PZ_OK;
+}
+
+int pz_epoch_state_tallies(pz_epoch_state* st) {
+  if (!st) return fail(PZ_EINVAL, "state is null");
+  if (!st->steps) return fail(PZ_EINVAL, "no step has run");
+  if (!(st->fused && st->world > 1) || !st->natt) return PZ_OK;  // already complete on every rank
+  const int L = (int)st->sh.size();
+  std::vector<hipStream_t> streams(L);
+  std::vector<uint64_t*> bufs(L);
+  std::vector<hipEvent_t> evs(L);
+  int rc;
+  for (uint32_t p = 0; p < st->nparts; ++p) {
+    for (int i = 0; i < L; ++i) {
+      Part& q = st->sh[i].part[p];
+      streams[i] = st->sh[i].s;
+      bufs[i] = q.results + (uint64_t)q.B * kScal;  // {vote, total} of the last step
+      evs[i] = q.ev_nb;
+    }
+    if ((rc = st->comm->allreduce_u64(bufs.data(), 2ull * st->sh[0].part[p].B * st->natt, streams.data(), evs.data())))
+      return rc;
+    for (int i = 0; i < L; ++i)
+      if ((rc = wait(st->sh[i], st->sh[i].part[p].ev_nb))) return rc;
+  }
+  return pz_epoch_state_sync(st);
 }
 
 int pz_epoch_state_layout(const pz_epoch_state* st, int* committee_order) {

@@ -129,6 +129,11 @@ class NativeEpoch:
                  ctypes.byref(s))
         return lo.value, hi.value, dev.value, s.value
 
+    def tallies(self):
+        """Complete every attestation's vote/total on every rank after a sharded one-pass
+        step (a collective; a no-op otherwise)."""
+        lib.call("pz_epoch_state_tallies", self.st)
+
     def validators(self, local=0):
         """The validator index of each balance column ``results(local)`` returns."""
         lo, hi, _, _ = self.shard(local)

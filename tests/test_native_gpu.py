@@ -35,6 +35,7 @@ def _check(ne, inst, steps=1):
     for _ in range(steps):
         ne.step()
         ne.sync()
+        ne.tallies()  # sharded one-pass: vote/total complete on every rank (no-op otherwise)
         want = [oracle_epoch(inst, b) for b in range(inst["ninst"])]
         held = []
         for local in range(ne.nlocal):
@@ -64,9 +65,9 @@ def test_native_epoch_single_device(n, B, inactive, layout):
     inst = _inst(n, B, inactive)
     ne = NativeEpoch(inst, device=0, layout=layout)
     # committee order whenever every validator is active (the synthetic committees partition);
-    # the one-pass step on it when N is even (16-B lanes) and every shard id is in range
+    # the one-pass step on it when every shard id is in range
     assert ne.committee_order == (layout != "index" and not inactive)
-    assert ne.one_pass == (layout == "auto" and not inactive and n % 2 == 0)
+    assert ne.one_pass == (layout == "auto" and not inactive)
     _check(ne, inst, steps=2)
 
 
@@ -160,7 +161,8 @@ def test_native_epoch_rccl_world1():
 
 
 @pytest.mark.parametrize("world,n,B,inactive", [(2, 65536, 3, False), (2, 20000, 2, True), (3, 5000, 4, True),
-                                                (8, 20000, 1, True), (5, 3000, 7, False)])
+                                                (8, 20000, 1, True), (5, 3000, 7, False), (3, 4099, 4, False),
+                                                (7, 1001, 3, False)])
 @pytest.mark.parametrize("layout", LAYOUTS)
 def test_native_epoch_sharded_loopback(world, n, B, inactive, layout):
     comm = Comm.loopback(world)
@@ -282,3 +284,33 @@ def test_max_active_index_scalar():
         act = np.nonzero((inst["start"][b] <= d) & (d < inst["end"][b]))[0]
         assert int(scal[b, _lib.SCAL_MAXIDX1]) == (int(act[-1]) + 1 if act.size else 0), b
         assert int(scal[b, _lib.SCAL_NACT]) == act.size
+
+
+def test_native_epoch_sharded_ranges_are_committee_aligned():
+    """The sharded one-pass step splits the committee-order positions at committee starts: no
+    committee straddles two ranks, and without pz_epoch_state_tallies a rank's vote/total are
+    complete exactly for the attestations whose committee it holds (zero elsewhere)."""
+    inst = _inst(20000, 2, False)
+    world = 3
+    ne = NativeEpoch(inst, comm=Comm.loopback(world))
+    assert ne.one_pass
+    coffs = inst["coffs"].astype(np.int64)
+    starts = []
+    for local in range(world):
+        lo, hi, _, _ = ne.shard(local)
+        starts.append(lo)
+        assert lo in set(coffs.tolist()) and hi in set(coffs.tolist())
+    ne.step()
+    ne.sync()
+    natt = inst["natt"]
+    for local in range(world):
+        lo, hi, _, _ = ne.shard(local)
+        _, _, vote, total, win = ne.results(local)
+        for b in range(2):
+            _, _, _, v, t, w = oracle_epoch(inst, b)
+            cb = coffs[inst["att_comm"][b * natt:(b + 1) * natt]]
+            own = (cb >= lo) & ((cb < hi) | ((cb == 20000) & (hi == 20000)))
+            np.testing.assert_array_equal(vote[b][own], v[own])
+            np.testing.assert_array_equal(total[b][own], t[own])
+            np.testing.assert_array_equal(np.where(own, 0, vote[b]), 0)
+            np.testing.assert_array_equal(win[b], w)  # winners exact on every rank
