@@ -13,7 +13,7 @@ def main(path):
             print("%-20s %.4g %s ms/step %.4f frac %.3f device_ms %.4f" % (
                 k, v["value"], v["unit"], v["ms_per_step"], r["frac"], r["step_device_ms"]))
     if "replay" in d:
-        print("replay %.0f blocks/s parity: %s" % (d["replay"]["value"], d["replay"]["parity"][-12:]))
+        print("replay %.0f blocks/s parity: %s" % (d["replay"]["value"], str(d["replay"].get("parity"))[-12:]))
 
 
 if __name__ == "__main__":
