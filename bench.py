@@ -203,7 +203,11 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                                "popcount, CalculateRewards, next-cycle balance (BASELINE configs[%d])"
                                % (2 if (world == 1 and nval != 1 << 20) else 3),
                    "validators": nval, "instances_per_step": ninst, "attestations_per_instance": inst["natt"],
-                   "parallelism": "validator-shard x%d + RCCL all-reduce" % world if world > 1 else "single GPU",
+                   "parallelism": (("committee-aligned validator shard x%d + one grouped RCCL collective per "
+                                    "part (sum of scalars, min of winners)" % world) if (world > 1 and native and
+                                                                                       de.one_pass)
+                                   else ("validator-shard x%d + RCCL all-reduce" % world) if world > 1
+                                   else "single GPU"),
                    "layout": (("committee order, one-pass step" if de.one_pass else
                                "committee order, two-pass step" if de.committee_order else "index order")
                               if native else "index order"),
