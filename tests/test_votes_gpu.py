@@ -11,12 +11,13 @@ pytestmark = pytest.mark.gpu
 U64 = np.uint64
 
 
-@pytest.mark.parametrize("world", [0, 1, 2, 3, 8])
+@pytest.mark.parametrize("world", [0, 1, 2, 3, 8, "rccl1"])
 def test_vote_cache_vs_oracle(world):
     """world 0: the one-GPU tally; world >= 1: pz_comm_vote_tally sharded by validator range
-    over a loopback communicator, the per-slot totals all-reduced."""
+    over a loopback communicator (SURVEY §8e row 3), the per-slot totals all-reduced;
+    "rccl1": the same entry over an RCCL communicator of one GPU."""
     from prysm_amd.native import Comm
-    comm = Comm.loopback(world) if world else None
+    comm = Comm.devices(1) if world == "rccl1" else Comm.loopback(world) if world else None
     rng = np.random.default_rng(12)
     nval = 3000
     _, cs = ref.new_genesis_states(nval)
