@@ -506,6 +506,10 @@ int  pz_epoch_state_tallies(pz_epoch_state* st);
  * the one-pass step. */
 int  pz_epoch_state_layout(const pz_epoch_state* st, int* committee_order);
 void pz_epoch_state_free(pz_epoch_state* st);
+/* Host only (no device call): the layout a pz_epoch_state would choose for h (as
+ * pz_epoch_state_layout) and global rank `rank`'s storage positions [lo, hi) in a world of
+ * `world` ranks.  Lets a launcher size each rank's memory before any device is opened. */
+int  pz_epoch_plan(const pz_epoch_host* h, int world, int rank, uint64_t* lo, uint64_t* hi, int* committee_order);
 
 /* ---- block pipeline: sync replay of serialized blocks ---------------------------------
  * A chain object runs blocks through the reference's ChainService.blockProcessing

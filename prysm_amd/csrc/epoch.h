@@ -88,7 +88,7 @@ struct FusedArgs {
 hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_epoch_fwin(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
-bool fused_ok(const EpochArgs& a);
-int set_fused_variant(int v);  // tools/ A/B only (pz_debug_set_fused_variant)  // 16-B vector path available (nval even, 16-B aligned arrays)
+bool fused_ok(const EpochArgs& a);  // 16-B vector path available (16-B aligned validator rows)
+int set_fused_variant(int v);       // tools/ A/B only (pz_debug_set_fused_variant)
 
 }  // namespace pz

@@ -318,6 +318,58 @@ uint64_t committee_boundary(const pz_epoch_host* h, uint64_t r, int world, uint6
   return std::max<uint64_t>(b, r > 1 ? committee_boundary(h, r - 1, world, N) : 0);
 }
 
+// The step a pz_epoch_state takes for h (host only; pz_epoch_plan exports it).
+struct Plan {
+  bool all_active = true;  // every validator active in every instance
+  bool co = false;         // committee-order layout (see pz_epoch_batch.co_index)
+  bool fused = false;      // one-pass step on that layout
+};
+Plan plan_layout(const pz_epoch_host* h) {
+  Plan p;
+  const uint64_t N = h->nval;
+  for (uint64_t b = 0; b < h->ninst && p.all_active; ++b) {
+    const uint64_t d = h->dynasty[b];
+    for (uint64_t v = 0; v < N; ++v) {
+      const uint64_t k = b * N + v;
+      if (!(h->start[k] <= d && d < h->end[k])) {
+        p.all_active = false;
+        break;
+      }
+    }
+  }
+  // Committee order when every validator is active and the committees partition [0, N):
+  // the crosslink tallies then stream contiguous balances instead of gathering them.
+  if (p.all_active && h->natt && h->layout != PZ_LAYOUT_INDEX && h->coffs[h->ncomm] == N) {
+    std::vector<uint8_t> seen(N, 0);
+    bool part = true;
+    for (uint64_t k = 0; k < N && part; ++k) {
+      const uint32_t v = h->committee[k];
+      part = v < N && !seen[v];
+      if (part) seen[v] = 1;
+    }
+    p.co = part;
+  }
+  // One pass needs no shard panic (it depends on the tallies, which the one pass forms while
+  // it rewards).
+  if (p.co && h->layout == PZ_LAYOUT_AUTO) {
+    p.fused = true;
+    for (uint64_t i = 0; i < (uint64_t)h->ninst * h->natt && p.fused; ++i) p.fused = h->att_shard[i] < h->nrec;
+  }
+  return p;
+}
+
+// Global rank r's storage positions [lo, hi): 64-aligned validator ranges, or committee-
+// aligned ones for the sharded one-pass step (no committee straddles two ranks).
+void shard_range(const pz_epoch_host* h, const Plan& p, int r, int world, uint64_t* lo, uint64_t* hi) {
+  const uint64_t N = h->nval, span = 64 * shard_words(N, world);
+  *lo = std::min<uint64_t>(N, (uint64_t)r * span);
+  *hi = std::min<uint64_t>(N, (uint64_t)(r + 1) * span);
+  if (p.fused && world > 1) {
+    *lo = committee_boundary(h, (uint64_t)r, world, N);
+    *hi = committee_boundary(h, (uint64_t)r + 1, world, N);
+  }
+}
+
 // The committee CSR restricted to members in [lo, hi) (plus, on global rank 0, members >=
 // N, whose processCrosslinks panic that rank raises), each with its position in its full
 // committee.
@@ -368,38 +420,12 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
   st->nrec = h->nrec;
   st->ncomm = h->ncomm;
   st->sw = shard_words(st->N, st->world);
-  for (uint64_t b = 0; b < st->B && st->all_active; ++b) {
-    const uint64_t d = h->dynasty[b];
-    for (uint64_t v = 0; v < st->N; ++v) {
-      const uint64_t k = b * st->N + v;
-      if (!(h->start[k] <= d && d < h->end[k])) {
-        st->all_active = false;
-        break;
-      }
-    }
-  }
+  const Plan pl = plan_layout(h);
+  st->all_active = pl.all_active;
   st->general = !st->all_active && st->world > 1;
-  // Committee order when every validator is active and the committees partition [0, N):
-  // the crosslink tallies then stream contiguous balances instead of gathering them.
-  if (st->all_active && h->natt && h->layout != PZ_LAYOUT_INDEX && h->coffs[h->ncomm] == st->N) {
-    std::vector<uint8_t> seen(st->N, 0);
-    bool part = true;
-    for (uint64_t k = 0; k < st->N && part; ++k) {
-      const uint32_t v = h->committee[k];
-      part = v < st->N && !seen[v];
-      if (part) seen[v] = 1;
-    }
-    if (part) {
-      st->co = true;
-      st->co_inv.assign(h->committee, h->committee + st->N);
-    }
-  }
-  // One pass needs no shard panic (it depends on the tallies, which the one pass forms while
-  // it rewards).
-  if (st->co && h->layout == PZ_LAYOUT_AUTO) {
-    st->fused = true;
-    for (uint64_t i = 0; i < (uint64_t)st->B * st->natt && st->fused; ++i) st->fused = h->att_shard[i] < st->nrec;
-  }
+  st->co = pl.co;
+  st->fused = pl.fused;
+  if (st->co) st->co_inv.assign(h->committee, h->committee + st->N);
   // attestations by committee, per instance (the one pass adds a committee's slice into each)
   std::vector<uint32_t> catt_offs, catt;
   std::vector<FusedCommittee> cinfo;
@@ -442,13 +468,7 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
     Shard& s = st->sh[i];
     s.dev = comm ? comm->dev[i] : device;
     s.grank = comm ? comm->rank0 + i : 0;
-    const uint64_t span = 64 * st->sw;
-    s.lo = std::min<uint64_t>(st->N, (uint64_t)s.grank * span);
-    s.hi = std::min<uint64_t>(st->N, (uint64_t)(s.grank + 1) * span);
-    if (st->fused && st->world > 1) {  // committee-aligned ranges: no committee straddles two ranks
-      s.lo = committee_boundary(h, (uint64_t)s.grank, st->world, st->N);
-      s.hi = committee_boundary(h, (uint64_t)s.grank + 1, st->world, st->N);
-    }
+    shard_range(h, pl, s.grank, st->world, &s.lo, &s.hi);
     s.n = s.hi - s.lo;
     s.np = st->fused ? (s.n + 1) & ~1ull : s.n;
     s.wl = (s.n + 63) / 64;
@@ -709,5 +729,16 @@ int pz_epoch_state_layout(const pz_epoch_state* st, int* committee_order) {
 }
 
 void pz_epoch_state_free(pz_epoch_state* st) { delete st; }
+
+int pz_epoch_plan(const pz_epoch_host* h, int world, int rank, uint64_t* lo, uint64_t* hi, int* committee_order) {
+  if (!lo || !hi || !committee_order) return fail(PZ_EINVAL, "null pointer");
+  if (world < 1 || rank < 0 || rank >= world) return fail(PZ_EINVAL, "rank %d outside world %d", rank, world);
+  int rc = check_host(h);
+  if (rc) return rc;
+  const Plan p = plan_layout(h);
+  shard_range(h, p, rank, world, lo, hi);
+  *committee_order = p.fused ? 2 : p.co ? 1 : 0;
+  return PZ_OK;
+}
 
 }  // extern "C"

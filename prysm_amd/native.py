@@ -78,6 +78,40 @@ class Comm:
             pass
 
 
+def _epoch_host(inst, layout="auto"):
+    """(``pz_epoch_host`` over a ``synth.epoch_batch``-shaped dict, the arrays it points into)."""
+    u64 = lambda a: np.ascontiguousarray(a, dtype=np.uint64)  # noqa: E731
+    u32 = lambda a: np.ascontiguousarray(a, dtype=np.uint32)  # noqa: E731
+    k = dict(balance=u64(inst["balance"]), start=u64(inst["start"]), end=u64(inst["end"]),
+             dynasty=u64(inst["dynasty"]), total_deposit=u64(inst["total_deposit"]),
+             bits=np.ascontiguousarray(inst["bits"], dtype=np.uint8), boffs=u64(inst["boffs"]),
+             committee=u32(inst["committee"]), coffs=u64(inst["coffs"]),
+             att_comm=u32(inst["att_comm"]), att_shard=u32(inst["att_shard"]),
+             rec_dynasty=u64(inst["rec_dynasty"]))
+    h = EpochHost()
+    h.ninst, h.nval, h.natt = int(inst["ninst"]), int(inst["nval"]), int(inst["natt"])
+    h.balance, h.start, h.end = ptr(k["balance"]), ptr(k["start"]), ptr(k["end"])
+    h.dynasty, h.total_deposit = ptr(k["dynasty"]), ptr(k["total_deposit"])
+    h.bits, h.boffs = ptr(k["bits"]), ptr(k["boffs"])
+    h.committee, h.coffs, h.ncomm = ptr(k["committee"]), ptr(k["coffs"]), len(k["coffs"]) - 1
+    h.att_comm, h.att_shard = ptr(k["att_comm"]), ptr(k["att_shard"])
+    h.nrec = int(k["rec_dynasty"].shape[1]) if k["rec_dynasty"].ndim == 2 else int(k["rec_dynasty"].size)
+    h.rec_dynasty = ptr(k["rec_dynasty"])
+    h.layout = {"auto": 0, "index": 1, "twopass": 2}[layout]
+    return h, k
+
+
+def epoch_plan(inst, world, rank, layout="auto"):
+    """``pz_epoch_plan`` (host only, no device): (lo, hi, layout code) of global rank ``rank``
+    -- the storage positions a ``NativeEpoch`` rank of that world would hold and whether its
+    step is index order (0), committee order (1) or the one-pass step (2)."""
+    h, keep = _epoch_host(inst, layout)
+    lo, hi, co = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+    lib.call("pz_epoch_plan", ctypes.byref(h), world, rank, ctypes.byref(lo), ctypes.byref(hi), ctypes.byref(co))
+    del keep
+    return lo.value, hi.value, co.value
+
+
 class NativeEpoch:
     """``pz_epoch_state``: the same inputs as ``prysm_amd.epoch.DeviceEpoch`` (a
     ``synth.epoch_batch``-shaped dict over all validators)."""
@@ -86,25 +120,8 @@ class NativeEpoch:
         """``layout``: "auto" (committee order when every validator is active and the
         committees partition the set, with the one-pass step when no attestation names a
         shard >= nrec), "twopass" (the same layout, two-pass step) or "index"."""
-        u64 = lambda a: np.ascontiguousarray(a, dtype=np.uint64)  # noqa: E731
-        u32 = lambda a: np.ascontiguousarray(a, dtype=np.uint32)  # noqa: E731
-        self._keep = k = dict(balance=u64(inst["balance"]), start=u64(inst["start"]), end=u64(inst["end"]),
-                              dynasty=u64(inst["dynasty"]), total_deposit=u64(inst["total_deposit"]),
-                              bits=np.ascontiguousarray(inst["bits"], dtype=np.uint8), boffs=u64(inst["boffs"]),
-                              committee=u32(inst["committee"]), coffs=u64(inst["coffs"]),
-                              att_comm=u32(inst["att_comm"]), att_shard=u32(inst["att_shard"]),
-                              rec_dynasty=u64(inst["rec_dynasty"]))
-        self.B, self.N, self.natt = int(inst["ninst"]), int(inst["nval"]), int(inst["natt"])
-        self.nrec = int(k["rec_dynasty"].shape[1]) if k["rec_dynasty"].ndim == 2 else int(k["rec_dynasty"].size)
-        h = EpochHost()
-        h.ninst, h.nval = self.B, self.N
-        h.balance, h.start, h.end = ptr(k["balance"]), ptr(k["start"]), ptr(k["end"])
-        h.dynasty, h.total_deposit = ptr(k["dynasty"]), ptr(k["total_deposit"])
-        h.natt, h.bits, h.boffs = self.natt, ptr(k["bits"]), ptr(k["boffs"])
-        h.committee, h.coffs, h.ncomm = ptr(k["committee"]), ptr(k["coffs"]), len(k["coffs"]) - 1
-        h.att_comm, h.att_shard = ptr(k["att_comm"]), ptr(k["att_shard"])
-        h.nrec, h.rec_dynasty = self.nrec, ptr(k["rec_dynasty"])
-        h.layout = {"auto": 0, "index": 1, "twopass": 2}[layout]
+        h, self._keep = _epoch_host(inst, layout)
+        self.B, self.N, self.natt, self.nrec = int(h.ninst), int(h.nval), int(h.natt), int(h.nrec)
         self.comm = comm
         self.st = ctypes.c_void_p()
         lib.call("pz_epoch_state_new", comm.h if comm is not None else None, device, ctypes.byref(h),
