@@ -937,8 +937,9 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
       const bool a1 = pack64(qs[j].z, qs[j].w) <= d && d < pack64(qe[j].z, qe[j].w);
       nm += (v0[j] && !a0 ? 1 : 0) + (v1[j] && !a1 ? 1 : 0);
       if (applied) {  // every validator active: rank == index, the validator at p is co_index[p]
-        const bool r0 = (MODE & 2) ? (b0 & 1) : bit_at(lastbf, cix[j].x);
-        const bool r1 = (MODE & 2) ? (b1 & 1) : bit_at(lastbf, cix[j].y);
+        // an element outside the piece looks up bit 0 (its co_index may be a row's pad)
+        const bool r0 = (MODE & 2) ? (b0 & 1) : bit_at(lastbf, v0[j] ? cix[j].x : 0u);
+        const bool r1 = (MODE & 2) ? (b1 & 1) : bit_at(lastbf, v1[j] ? cix[j].y : 0u);
         b0 = r0 ? b0 + PZ_ATTESTER_REWARD : b0 - PZ_ATTESTER_REWARD;
         b1 = r1 ? b1 + PZ_ATTESTER_REWARD : b1 - PZ_ATTESTER_REWARD;
         if (MODE & 4)

@@ -491,8 +491,13 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
       const uint32_t* inv = st->co_inv.data();
       if ((rc = upload_perm(s, &bal, h->balance, st->B, st->N, inv)) ||
           (rc = upload_perm(s, &start, h->start, st->B, st->N, inv)) ||
-          (rc = upload_perm(s, &end, h->end, st->B, st->N, inv)) || (rc = upload(s, &co_index, inv + s.lo, s.n)))
+          (rc = upload_perm(s, &end, h->end, st->B, st->N, inv)))
         break;
+      // np entries: the pad position of an odd range holds a valid index too (the one-pass
+      // kernel reads co_index by 16-B pairs and looks every element's bit up unconditionally)
+      std::vector<uint32_t> ci(inv + s.lo, inv + s.hi);
+      ci.resize(std::max<uint64_t>(s.np, s.n), s.n ? inv[s.lo] : 0);
+      if ((rc = upload(s, &co_index, ci.data(), ci.size()))) break;
     } else if ((rc = upload_range(s, &bal, h->balance, st->B, st->N)) ||
                (rc = upload_range(s, &start, h->start, st->B, st->N)) ||
                (rc = upload_range(s, &end, h->end, st->B, st->N))) {

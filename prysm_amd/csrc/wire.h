@@ -25,6 +25,7 @@ struct WireValArgs {
   uint64_t* total;  // device u64
   uint64_t* status;  // per-tile look-back words (set by the launcher from the scratch)
   uint32_t* ticket;
+  uint64_t* trace;   // tools/ only: per-tile phase timestamps (variant 32), else NULL
 };
 
 uint64_t wire_tiles(uint64_t n);
@@ -32,5 +33,6 @@ int wire_val_args(const pz_validator_cols* v, uint64_t n, uint32_t field_num, Wi
 // scratch: (wire_tiles(n) + 1) u64, zeroed by the launcher
 hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t s);
 int set_wire_variant(int v);  // tools/ A/B only (pz_debug_set_wire_variant)
+void set_wire_trace(uint64_t* dev);  // tools/ only: variant 32's timestamp buffer [tiles][8]
 
 }  // namespace pz

@@ -20,6 +20,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 
 #include "runtime.h"
 
@@ -174,75 +176,80 @@ __device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Decoupled look-back by the whole workgroup: 256 threads x 4 loads watch the 1,024 nearest
+// Decoupled look-back by the whole workgroup: 512 threads x LB loads watch the 512*LB nearest
 // predecessors at once, so one round trip usually reaches a published inclusive prefix even
-// when every resident tile started together (a wave-wide window walked 64 tiles per round
-// trip, ~8 trips per dispatch round).  Returns the exclusive prefix of `tile` to every thread.
-constexpr int kLbPer = 4, kLbWin = kThreads * kLbPer;
+// when every resident tile started together.  Entry q*512 + t of a window (distance from the
+// tile) is thread t's q-th: each load instruction reads 64 consecutive status words (4 lines).
+// Returns the exclusive prefix of `tile` to every thread.
+constexpr int kLbPer = 4;
 
 // First window's loads, issued early so their round trip overlaps other work.
-__device__ __forceinline__ void lookback_issue(uint64_t* status, uint64_t tile, uint64_t (&w)[kLbPer]) {
+template <int LB>
+__device__ __forceinline__ void lookback_issue(uint64_t* status, uint64_t tile, uint64_t (&w)[LB]) {
 #pragma unroll
-  for (int q = 0; q < kLbPer; ++q) {
-    const int64_t idx = (int64_t)tile - 1 - (threadIdx.x * kLbPer + q);
+  for (int q = 0; q < LB; ++q) {
+    const int64_t idx = (int64_t)tile - 1 - (q * kThreads + threadIdx.x);
     w[q] = idx >= 0 ? ld_status(status + idx) : kFlagP;  // before tile 0: prefix 0
   }
 }
 
-__device__ uint64_t lookback_finish(uint64_t* status, uint64_t tile, uint64_t (&w)[kLbPer], uint64_t* lds,
+template <int LB>
+__device__ uint64_t lookback_finish(uint64_t* status, uint64_t tile, uint64_t (&w)[LB], uint64_t* lds,
                                     uint32_t* lds_first) {
+  constexpr uint32_t kWin = kThreads * LB;
   uint64_t prefix = 0;
   int64_t j = (int64_t)tile - 1;
   while (true) {
+    // Poll with relaxed agent-scope (sc1) loads -- the R2 granule form of the HIP guide's
+    // Guideline 16: every status word is written by an agent-scope atomic store -- and fall
+    // back to the atomic re-read after 256 polls.  Polling by atomics alone made every
+    // spinning tile queue at the memory-side atomic unit of the same few status lines
+    // (~12 ns each): 295 us per 16.7 M records against 178 without the look-back.  A lane's
+    // unpublished entries are re-read together: one round trip per poll, not one per entry.
+    for (uint32_t spins = 0;; ++spins) {
+      bool wait = false;
 #pragma unroll
-    for (int q = 0; q < kLbPer; ++q) {
-      const int64_t idx = j - (threadIdx.x * kLbPer + q);
-      // Poll with relaxed agent-scope (sc1) loads -- the R2 granule form of the HIP guide's
-      // Guideline 16: every status word is written by an agent-scope atomic store -- and fall
-      // back to the atomic re-read after 256 polls.  Polling by atomics alone made every
-      // spinning tile queue at the memory-side atomic unit of the same few status lines
-      // (~12 ns each): 295 us per 16.7 M records against 178 without the look-back.
-      for (uint32_t spins = 0; !(w[q] >> 62); ++spins) {
-        __builtin_amdgcn_s_sleep(1);
-        w[q] = spins < 256 ? ld_status(status + idx) : ld_status_fresh(status + idx);
+      for (int q = 0; q < LB; ++q) wait |= !(w[q] >> 62);
+      if (!wait) break;
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int q = 0; q < LB; ++q) {
+        const int64_t idx = j - (q * kThreads + threadIdx.x);
+        if (!(w[q] >> 62)) w[q] = spins < 256 ? ld_status(status + idx) : ld_status_fresh(status + idx);
       }
     }
-    // nearest published inclusive prefix (distance d = threadIdx.x * kLbPer + q)
-    if (threadIdx.x == 0) *lds_first = kLbWin;
+    // nearest published inclusive prefix (distance d = q * kThreads + threadIdx.x)
+    if (threadIdx.x == 0) *lds_first = kWin;
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < kLbPer; ++q)
+    for (int q = 0; q < LB; ++q)
       if ((w[q] >> 62) == 2) {
-        atomicMin(lds_first, threadIdx.x * kLbPer + q);
+        atomicMin(lds_first, q * kThreads + threadIdx.x);
         break;
       }
     __syncthreads();
     const uint32_t first = *lds_first;
     uint64_t part = 0;
 #pragma unroll
-    for (int q = 0; q < kLbPer; ++q)
-      if (threadIdx.x * kLbPer + q <= first) part += w[q] & kVal;
+    for (int q = 0; q < LB; ++q)
+      if (q * kThreads + threadIdx.x <= first) part += w[q] & kVal;
     uint64_t e;
     prefix += block_scan(part, &e, lds);
     __syncthreads();
-    if (first < (uint32_t)kLbWin) return prefix;
-    j -= kLbWin;
+    if (first < kWin) return prefix;
+    j -= kWin;
 #pragma unroll
-    for (int q = 0; q < kLbPer; ++q) {
-      const int64_t idx = j - (threadIdx.x * kLbPer + q);
+    for (int q = 0; q < LB; ++q) {
+      const int64_t idx = j - (q * kThreads + threadIdx.x);
       w[q] = idx >= 0 ? ld_status(status + idx) : kFlagP;
     }
   }
 }
 
-// Decoupled look-back by the whole workgroup: 256 threads x 4 loads watch the 1,024 nearest
-// predecessors at once, so one round trip usually reaches a published inclusive prefix even
-// when every resident tile started together (a wave-wide window walked 64 tiles per round
-// trip, ~8 trips per dispatch round).  Returns the exclusive prefix of `tile` to every thread.
 __device__ uint64_t lookback_block(uint64_t* status, uint64_t tile, uint64_t* lds, uint32_t* lds_first) {
   uint64_t w[kLbPer];
-  lookback_issue(status, tile, w);
-  return lookback_finish(status, tile, w, lds, lds_first);
+  lookback_issue<kLbPer>(status, tile, w);
+  return lookback_finish<kLbPer>(status, tile, w, lds, lds_first);
 }
 
 // Store stage[0..span) at out+base with 16-B stores: bytes up to the first 16-aligned
@@ -284,13 +291,12 @@ __device__ __forceinline__ void load_sub(const WireValArgs& a, uint64_t first, S
 // 31,232, so the four rows' sizes travel as four 16-bit lanes of one u64.
 template <int NC>
 __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t first, const SRec<NC> (&r)[kPer],
-                                                uint32_t (&body)[kPer], uint32_t (&off)[kPer], uint64_t* lds) {
+                                                uint32_t (&off)[kPer], uint64_t* lds) {
   uint64_t packed = 0;
 #pragma unroll
   for (int p = 0; p < kPer; ++p) {
-    body[p] = srec_body(r[p]);
     const uint64_t i = first + p * kThreads + threadIdx.x;
-    packed |= (uint64_t)(i < a.n ? frame_size(a, body[p]) : 0) << (16 * p);
+    packed |= (uint64_t)(i < a.n ? frame_size(a, srec_body(r[p])) : 0) << (16 * p);
   }
   uint64_t e;
   const uint64_t t = block_scan(packed, &e, lds);
@@ -321,12 +327,16 @@ __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t f
 // workgroups pipelining the next tile's phase 1 under the look-back 278 (128 VGPRs + spills).
 // V: an ablation knob for tools/wire_probe.py (0 in the product; output wrong otherwise):
 // bit 0 tile = blockIdx (no ticket), bit 1 no stage build, bit 2 no look-back, bit 3 no store,
-// bit 4 reload the values for the build instead of holding them.
+// bit 4 reload the values for the build instead of holding them, bit 5 (the product plus)
+// per-tile phase timestamps into a.trace (tools/wire_trace.py); bits 6/7 a look-back window of
+// 1,024 / 512 predecessors instead of 2,048.
 template <int V, int NC>
 __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   __shared__ uint64_t lds[kThreads / 64 + 1];
   __shared__ uint32_t s_tile, s_first;
   __shared__ __attribute__((aligned(16))) uint32_t stage[kStageBytes / 4 + 8];
+  uint64_t ts[6];
+  if (V & 32) ts[0] = wall_clock64();
   if (V & 1) {
     if (threadIdx.x == 0) s_tile = blockIdx.x;
   } else if (threadIdx.x == 0) {
@@ -334,23 +344,37 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   }
   __syncthreads();
   const uint32_t tile = s_tile;
+  if (V & 32) ts[1] = wall_clock64();
   const uint64_t tfirst = (uint64_t)tile * kTileRecs;
   constexpr bool kHold = !(V & 16) && NC <= 3;  // 4-5 columns held would spill: reload them
   // phase 1: sizes -> offsets inside the tile
   SRec<NC> r[kSub][kPer];
-  uint32_t off[kSub][kPer], body[kSub][kPer], agg = 0;
+  // A record's body size is recomputed for its build rather than held: 8 more live VGPRs
+  // spilled, and a spill reload's vmcnt(0) waited for the look-back loads in flight.
+  uint32_t off[kSub][kPer], agg = 0;
+  if (kHold) {  // every sub-tile's loads in flight at once: one round trip, not kSub
+#pragma unroll
+    for (int j = 0; j < kSub; ++j) load_sub(a, tfirst + (uint64_t)j * kSubRecs, r[j]);
+  }
 #pragma unroll
   for (int j = 0; j < kSub; ++j) {
-    load_sub(a, tfirst + (uint64_t)j * kSubRecs, r[kHold ? j : 0]);
-    const uint32_t sub = sub_offsets(a, tfirst + (uint64_t)j * kSubRecs, r[kHold ? j : 0], body[j], off[j], lds);
+    if (!kHold) load_sub(a, tfirst + (uint64_t)j * kSubRecs, r[0]);
+    const uint32_t sub = sub_offsets(a, tfirst + (uint64_t)j * kSubRecs, r[kHold ? j : 0], off[j], lds);
 #pragma unroll
     for (int p = 0; p < kPer; ++p) off[j][p] += agg;
     agg += sub;
   }
+  // Every column load has landed (the scans used them).  Say so to the compiler's wait-count
+  // pass: the loads sit under divergent branches, and without this it re-waits for them in
+  // the stage build, where a vmcnt wait also drains the look-back loads issued below
+  // (tools/wire_trace.py: the build took 6.8 us with them in flight, 4.7 without).
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0), expcnt/lgkmcnt untouched
   if (threadIdx.x == 0) st_status(a.status + tile, (tile == 0 ? kFlagP : kFlagA) | agg);
+  if (V & 32) ts[2] = wall_clock64();
   // the look-back's first round trip overlaps the stage build
-  uint64_t w[kLbPer];
-  if (!(V & 4) && tile > 0) lookback_issue(a.status, tile, w);
+  constexpr int LB = (V & 128) ? 1 : (V & 64) ? 2 : kLbPer;  // window ablation (tools/)
+  uint64_t w[LB];
+  if (!(V & 4) && tile > 0) lookback_issue<LB>(a.status, tile, w);
   const bool staged = agg <= kStageBytes && !a.offs;
   if (staged && !(V & 2)) {
     uint8_t* st = reinterpret_cast<uint8_t*>(stage);
@@ -360,14 +384,15 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
 #pragma unroll
       for (int p = 0; p < kPer; ++p)
         if (tfirst + j * kSubRecs + p * kThreads + threadIdx.x < a.n)
-          put_srec(a, r[kHold ? j : 0][p], body[j][p], st + off[j][p]);
+          put_srec(a, r[kHold ? j : 0][p], srec_body(r[kHold ? j : 0][p]), st + off[j][p]);
     }
   }
+  if (V & 32) ts[3] = wall_clock64();
   uint64_t base = 0;
   if (V & 4) {
     base = (uint64_t)tile * 15 * kTileRecs;
   } else if (tile > 0) {
-    base = lookback_finish(a.status, tile, w, lds, &s_first);
+    base = lookback_finish<LB>(a.status, tile, w, lds, &s_first);
     if (threadIdx.x == 0) st_status(a.status + tile, kFlagP | (base + agg));
   }
   if (tile == nt - 1 && threadIdx.x == 0) {
@@ -376,7 +401,18 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   }
   if (staged) {
     __syncthreads();
+    if (V & 32) ts[4] = wall_clock64();
     if (!(V & 8)) store_stage(a.out, base, stage, agg);
+    if (V & 32) {
+      __syncthreads();
+      ts[5] = wall_clock64();
+      if (threadIdx.x == 0) {
+        uint64_t* t = a.trace + 8 * (uint64_t)tile;
+        for (int k = 0; k < 6; ++k) t[k] = ts[k];
+        t[6] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID
+        t[7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
+      }
+    }
     return;
   }
 #pragma unroll
@@ -388,7 +424,7 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
       if (i < a.n) {
         const uint64_t o = base + off[j][p];
         if (a.offs) a.offs[i] = o;
-        put_srec(a, r[kHold ? j : 0][p], body[j][p], a.out + o);
+        put_srec(a, r[kHold ? j : 0][p], srec_body(r[kHold ? j : 0][p]), a.out + o);
       }
     }
   }
@@ -413,6 +449,11 @@ PZ_WIRE_VAL_KERNEL(pz_wire_val_v8_kernel, 8, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v7_kernel, 7, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v15_kernel, 15, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v16_kernel, 16, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v32_kernel, 32, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v34_kernel, 34, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v36_kernel, 36, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v96_kernel, 96, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v160_kernel, 160, 3)
 #undef PZ_WIRE_VAL_KERNEL
 
 // Records with bytes fields: tiles of kBytesSub x 256 records, one per thread per sub-tile.
@@ -463,6 +504,12 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_val_bytes_kernel(
   }
 }
 
+// Zeroes the look-back scratch: one dispatch (hipMemsetAsync of an odd number of 8-B words
+// issued two ROCclr fill kernels, ~10 us per call).
+extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_zero_kernel(uint64_t* p, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kThreads) p[i] = 0;
+}
+
 }  // namespace
 
 static uint64_t tile_recs(bool bytes) { return bytes ? kBytesTileRecs : kTileRecs; }
@@ -472,7 +519,8 @@ uint64_t wire_tiles(uint64_t n) {  // scratch bound: the smaller tile of the two
   return (n + t - 1) / t;
 }
 
-static int g_wire_variant = 0;  // tools/ A/B only
+static int g_wire_variant = 0;       // tools/ A/B only
+static uint64_t* g_wire_trace = nullptr;  // tools/ only
 
 // Scratch: status[nt] then the ticket; zeroed before every launch.
 hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t s) {
@@ -492,8 +540,11 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
       a.ccol[a.nc] = a.col[k];
       a.ctag[a.nc++] = tags[k];
     }
-  hipError_t e = hipMemsetAsync(scratch, 0, (nt + 1) * 8, s);
-  if (e != hipSuccess) return e;
+  {
+    const uint64_t words = nt + 1;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(64, (words + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(pz_wire_zero_kernel, dim3(blocks), dim3(kThreads), 0, s, scratch, words);
+  }
   if (bytes)
     hipLaunchKernelGGL(pz_wire_val_bytes_kernel, dim3((uint32_t)nt), dim3(kThreads), 0, s, a, (uint32_t)nt);
   else
@@ -506,6 +557,14 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
   case V: hipLaunchKernelGGL(pz_wire_val_v##V##_kernel, g, b, 0, s, a, n32); break;
         PZ_CASE(1) PZ_CASE(2) PZ_CASE(4) PZ_CASE(8) PZ_CASE(7) PZ_CASE(15) PZ_CASE(16)
 #undef PZ_CASE
+#define PZ_TRACE(V)                                                     \
+  case V:                                                               \
+    if (!g_wire_trace) return hipErrorInvalidValue;                     \
+    a.trace = g_wire_trace;                                             \
+    hipLaunchKernelGGL(pz_wire_val_v##V##_kernel, g, b, 0, s, a, n32);  \
+    break;
+        PZ_TRACE(32) PZ_TRACE(34) PZ_TRACE(36) PZ_TRACE(96) PZ_TRACE(160)
+#undef PZ_TRACE
         default: hipLaunchKernelGGL(pz_wire_val_kernel, g, b, 0, s, a, n32);
       }
     } else {
@@ -527,6 +586,8 @@ int set_wire_variant(int v) {
   g_wire_variant = v;
   return old;
 }
+
+void set_wire_trace(uint64_t* dev) { g_wire_trace = dev; }
 
 int wire_val_args(const pz_validator_cols* v, uint64_t n, uint32_t field_num, WireValArgs* a) {
   if (!v) return fail(PZ_EINVAL, "columns are null");
@@ -566,6 +627,8 @@ uint64_t pz_wire_validators_bound(uint64_t n, uint64_t bytes_total) { return n *
 uint64_t pz_wire_scratch_bytes(uint64_t n) { return (wire_tiles(n) + 1) * 8; }
 
 int pz_debug_set_wire_variant(int v) { return set_wire_variant(v); }
+
+void pz_debug_set_wire_trace(void* dev) { set_wire_trace(static_cast<uint64_t*>(dev)); }
 
 int pz_dev_wire_validators(const pz_validator_cols* v, uint64_t n, uint32_t field_num, uint8_t* d_out,
                            uint64_t* d_offsets, void* d_scratch, uint64_t* d_total, void* stream) {
