@@ -195,7 +195,7 @@ __device__ __forceinline__ void lookback_issue(uint64_t* status, uint64_t tile, 
 
 template <int LB>
 __device__ uint64_t lookback_finish(uint64_t* status, uint64_t tile, uint64_t (&w)[LB], uint64_t* lds,
-                                    uint32_t* lds_first) {
+                                    uint32_t* lds_first, uint32_t* polls = nullptr) {
   constexpr uint32_t kWin = kThreads * LB;
   uint64_t prefix = 0;
   int64_t j = (int64_t)tile - 1;
@@ -211,6 +211,7 @@ __device__ uint64_t lookback_finish(uint64_t* status, uint64_t tile, uint64_t (&
 #pragma unroll
       for (int q = 0; q < LB; ++q) wait |= !(w[q] >> 62);
       if (!wait) break;
+      if (polls) ++*polls;  // tools/ trace only
       __builtin_amdgcn_s_sleep(1);
 #pragma unroll
       for (int q = 0; q < LB; ++q) {
@@ -329,7 +330,8 @@ __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t f
 // bit 0 tile = blockIdx (no ticket), bit 1 no stage build, bit 2 no look-back, bit 3 no store,
 // bit 4 reload the values for the build instead of holding them, bit 5 (the product plus)
 // per-tile phase timestamps into a.trace (tools/wire_trace.py); bits 6/7 a look-back window of
-// 1,024 / 512 predecessors instead of 2,048.
+// 1,024 / 512 predecessors instead of 2,048, bit 8 (trace) wait for the look-back's first
+// window right after issuing it, to time its round trip.
 template <int V, int NC>
 __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   __shared__ uint64_t lds[kThreads / 64 + 1];
@@ -375,6 +377,12 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   constexpr int LB = (V & 128) ? 1 : (V & 64) ? 2 : kLbPer;  // window ablation (tools/)
   uint64_t w[LB];
   if (!(V & 4) && tile > 0) lookback_issue<LB>(a.status, tile, w);
+  uint64_t ts_arrive = 0;
+  uint32_t polls = 0;
+  if (V & 256) {  // trace: the first window's round trip alone (no overlap with the build)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    ts_arrive = wall_clock64();
+  }
   const bool staged = agg <= kStageBytes && !a.offs;
   if (staged && !(V & 2)) {
     uint8_t* st = reinterpret_cast<uint8_t*>(stage);
@@ -392,7 +400,7 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   if (V & 4) {
     base = (uint64_t)tile * 15 * kTileRecs;
   } else if (tile > 0) {
-    base = lookback_finish<LB>(a.status, tile, w, lds, &s_first);
+    base = lookback_finish<LB>(a.status, tile, w, lds, &s_first, (V & 32) ? &polls : nullptr);
     if (threadIdx.x == 0) st_status(a.status + tile, kFlagP | (base + agg));
   }
   if (tile == nt - 1 && threadIdx.x == 0) {
@@ -407,10 +415,13 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
       __syncthreads();
       ts[5] = wall_clock64();
       if (threadIdx.x == 0) {
-        uint64_t* t = a.trace + 8 * (uint64_t)tile;
+        uint64_t* t = a.trace + 16 * (uint64_t)tile;
         for (int k = 0; k < 6; ++k) t[k] = ts[k];
         t[6] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID
         t[7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
+        t[8] = ts_arrive;
+        t[9] = polls;                        // re-polls by thread 0 (the nearest entries)
+        t[10] = tile > 0 ? s_first : 0;      // distance of the nearest published prefix (last window)
       }
     }
     return;
@@ -454,6 +465,7 @@ PZ_WIRE_VAL_KERNEL(pz_wire_val_v34_kernel, 34, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v36_kernel, 36, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v96_kernel, 96, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v160_kernel, 160, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v288_kernel, 288, 3)
 #undef PZ_WIRE_VAL_KERNEL
 
 // Records with bytes fields: tiles of kBytesSub x 256 records, one per thread per sub-tile.
@@ -563,7 +575,7 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
     a.trace = g_wire_trace;                                             \
     hipLaunchKernelGGL(pz_wire_val_v##V##_kernel, g, b, 0, s, a, n32);  \
     break;
-        PZ_TRACE(32) PZ_TRACE(34) PZ_TRACE(36) PZ_TRACE(96) PZ_TRACE(160)
+        PZ_TRACE(32) PZ_TRACE(34) PZ_TRACE(36) PZ_TRACE(96) PZ_TRACE(160) PZ_TRACE(288)
 #undef PZ_TRACE
         default: hipLaunchKernelGGL(pz_wire_val_kernel, g, b, 0, s, a, n32);
       }

@@ -27,7 +27,7 @@ def main():
     scr = torch.empty(int(dll.pz_wire_scratch_bytes(n)) // 8, dtype=torch.int64, device="cuda")
     tot = torch.zeros(1, dtype=torch.int64, device="cuda")
     nt = (n + 4095) // 4096
-    trace = torch.zeros(nt * 8, dtype=torch.int64, device="cuda")
+    trace = torch.zeros(nt * 16, dtype=torch.int64, device="cuda")
     cols = _lib.ValidatorCols(None, None, None, None, None, None, *[t.data_ptr() for t in cols_t])
     sh = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
@@ -39,13 +39,13 @@ def main():
         run()
     ref = out[:int(tot.item())].clone()
     dll.pz_debug_set_wire_trace(ctypes.c_void_p(trace.data_ptr()))
-    variant = int(sys.argv[1]) if len(sys.argv) > 1 else 32  # 34: no stage build, 36: no look-back
+    variant = int(sys.argv[1]) if len(sys.argv) > 1 else 32  # 34: no stage build, 36: no look-back, 288: time the first poll
     dll.pz_debug_set_wire_variant(variant)
     res = []
     for rep in range(5):
         run()
         torch.cuda.synchronize()
-        t = trace.cpu().numpy().reshape(nt, 8)
+        t = trace.cpu().numpy().reshape(nt, 16)
         ts = t[:, :6].astype(np.int64)
         same = bool(torch.equal(out[:ref.numel()], ref)) if variant == 32 else None
         t0 = ts[:, 0].min()
@@ -68,6 +68,12 @@ def main():
             "tiles_per_xcc": np.bincount(xcc, minlength=8).tolist(),
             "first_wave_lookback_us": round(float(np.median(d[np.argsort(ts[:, 0])[:512], 3])), 2),
             "late_wave_lookback_us": round(float(np.median(d[np.argsort(ts[:, 0])[-1024:], 3])), 2),
+            "thread0_repolls": {"median": float(np.median(t[1:, 9])), "p90": float(np.percentile(t[1:, 9], 90)),
+                                "max": int(t[1:, 9].max())},
+            "nearest_prefix_distance": {"median": float(np.median(t[1:, 10])),
+                                        "p90": float(np.percentile(t[1:, 10], 90))},
+            "first_window_round_trip_us": (round(float(np.median((t[1:, 8] - ts[1:, 2]) * 10 / 1e3)), 2)
+                                           if variant & 256 else None),
         })
     dll.pz_debug_set_wire_variant(0)
     dll.pz_debug_set_wire_trace(None)
