@@ -139,3 +139,31 @@ def test_device_entry_point_null_columns():
     want = wire.validators(pb.Validators(n, balance=bal, end_dynasty=end))
     assert total == len(want) == int(d_offs[-1].item())
     assert d_out[:total].cpu().numpy().tobytes() == want
+
+
+def _scalar_cols(rng, n, which):
+    """Random scalar columns for the fields in `which`, the rest NULL; magnitudes mixed so
+    varints take 1-10 bytes and some 4,096-record tiles outgrow the 64 KiB LDS stage."""
+    out = {}
+    for k in which:
+        mags = rng.integers(0, 64, size=n)
+        out[k] = (rng.integers(0, 1 << 63, size=n, dtype=np.uint64) >> mags.astype(np.uint64)).astype(np.uint64)
+        out[k][rng.random(n) < 0.1] = 0
+    return pb.Validators(n, **out)
+
+
+@pytest.mark.parametrize("which", [("balance",), ("balance", "end_dynasty"), ("balance", "start_dynasty", "end_dynasty"),
+                                   ("public_key", "balance", "end_dynasty")])
+@pytest.mark.parametrize("offsets", [False, True])
+def test_scalar_columns_many_tiles(which, offsets):
+    """The scalar-only kernel with 1-3 non-NULL columns over 12 tiles of 4,096 records (the
+    look-back across tiles, a ragged last tile), framed against the host encoder and bare with
+    record offsets against the protobuf runtime record by record."""
+    n = 4096 * 11 + 1234
+    v = _scalar_cols(np.random.default_rng(len(which) * 10 + offsets), n, which)
+    if offsets:
+        raw, offs = wire.validators_device(v, 0, with_offsets=True)
+        assert offs[0] == 0 and offs[-1] == len(raw)
+        assert raw == b"".join(oracle_record(v, i) for i in range(n))
+    else:
+        assert wire.validators_device(v, 11) == wire.validators(v)
