@@ -34,7 +34,9 @@ constexpr int kSub = 2, kTileRecs = kSub * kSubRecs;  // 4,096 records (one tick
 constexpr int kStageBytes = 64 * 1024;                // the whole tile's encoding (16 B per record)
 constexpr int kBytesSub = 8, kBytesTileRecs = kBytesSub * kThreads;  // bytes-field kernel: 4,096
 
-__device__ __forceinline__ uint32_t vlen(uint64_t x) { return (uint32_t)((70 - __clzll(x | 1)) / 7); }
+// varint length: (70 - clz) / 7 for 70 - clz in [6, 70] as a multiply by 37 and a shift (a
+// 24-bit multiply instead of the quarter-rate high multiply of a division by 7)
+__device__ __forceinline__ uint32_t vlen(uint64_t x) { return ((uint32_t)(70 - __clzll(x | 1)) * 37u) >> 8; }
 
 __device__ __forceinline__ uint8_t* put_varint(uint8_t* p, uint64_t x) {
   while (x >= 0x80) {
@@ -156,6 +158,36 @@ __device__ __forceinline__ uint64_t block_scan(uint64_t x, uint64_t* excl, uint6
   return total;
 }
 
+// Inclusive scan of a u32 over the wave by DPP: row shifts 1, 2, 4, 8 (Hillis-Steele inside
+// each 16-lane row; bound_ctrl feeds 0 where a shift leaves the row), then row broadcasts 15
+// and 31 carry the row totals.  No LDS traffic (a __shfl_up is a ds_bpermute round trip).
+__device__ __forceinline__ uint32_t wave_iscan_u32(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast31
+  return x;
+}
+
+// block_scan for values made of independent 16-bit lanes whose block sums stay below 2^16 (the
+// scalar kernel's packed sub-tile sizes): each 32-bit half scans on its own, carry-free.
+__device__ __forceinline__ uint64_t block_scan_packed(uint64_t x, uint64_t* excl, uint64_t* lds4) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t inc = ((uint64_t)wave_iscan_u32((uint32_t)(x >> 32)) << 32) | wave_iscan_u32((uint32_t)x);
+  if (lane == 63) lds4[wid] = inc;
+  __syncthreads();
+  uint64_t before = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; ++w) {
+    before += w < wid ? lds4[w] : 0;
+    total += lds4[w];
+  }
+  *excl = before + inc - x;
+  return total;
+}
+
 // Tile status words: flag in the top two bits, value below.  A tile publishes its aggregate
 // (A) as soon as it knows its size and its inclusive prefix (P) after the look-back.  Flag and
 // value travel in one 64-bit word, so relaxed agent-scope atomics suffice (no fence, which on
@@ -193,13 +225,88 @@ __device__ __forceinline__ void lookback_issue(uint64_t* status, uint64_t tile, 
   }
 }
 
+// Sum of a u32 over the wave by DPP (no LDS traffic), returned to every lane: quad swaps,
+// half-row and row mirrors, then the row broadcasts 15 and 31 into lane 63.
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, false);   // quad_perm 1,0,3,2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, false);   // quad_perm 2,3,0,1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xf, 0xf, false);  // row_half_mirror
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xf, 0xf, false);  // row_mirror
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast31
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// One look-back window reduced with ONE workgroup barrier (the scalar-only kernel).  Entry
+// (q, thread t) sits at distance q*512 + t.  Every wave finds, by ballot, its nearest published
+// prefix P and sums its entries per level by DPP; lane 0 publishes [nearest distance | sum of
+// its entries before that P], the per-level sums and the P value.  After the barrier every
+// thread combines the 8 waves' records: all entries nearer than the block's nearest P are
+// aggregates, whose sums fit 32 bits (a scalar-only tile encodes to at most 4,096 x 61 B and
+// a window holds at most 2,048 entries), plus the P itself.  `slots` is 8 waves x 4 u64.
+// Returns the window's contribution; *found says whether it held a P.
 template <int LB>
+__device__ __forceinline__ uint64_t lookback_window_waves(const uint64_t (&w)[LB], uint64_t* slots, bool* found) {
+  static_assert(LB <= 4, "per-level sums are packed two per slot");
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t dw = 0xffffffffu, pa = 0, T[4] = {0, 0, 0, 0};
+  uint64_t pval = 0;
+#pragma unroll
+  for (int q = 0; q < LB; ++q) {
+    const uint32_t v = (uint32_t)(w[q] & kVal);  // meaningful for aggregates only
+    T[q] = wave_sum_u32(v);
+    const uint64_t m = __ballot((w[q] >> 62) == 2);
+    if (dw == 0xffffffffu && m) {  // wave-uniform
+      const uint32_t lf = (uint32_t)__builtin_ctzll(m);
+      dw = (uint32_t)q * kThreads + 64 * wv + lf;
+      pa = wave_sum_u32(lane < lf ? v : 0);
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w[q], (int)lf);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(w[q] >> 32), (int)lf);
+      pval = (((uint64_t)hi << 32) | lo) & kVal;
+    }
+  }
+  if (lane == 0) {
+    slots[4 * wv + 0] = ((uint64_t)pa << 32) | dw;
+    slots[4 * wv + 1] = ((uint64_t)T[1] << 32) | T[0];
+    slots[4 * wv + 2] = ((uint64_t)T[3] << 32) | T[2];
+    slots[4 * wv + 3] = pval;
+  }
+  __syncthreads();
+  // Lane x < 8 of every wave reads wave x's record; the nearest P by 8 readlanes (scalar).
+  constexpr int kW = kThreads / 64;
+  static_assert(kW <= 64, "one lane per wave record");
+  const uint32_t x = lane < kW ? lane : 0;
+  const uint64_t s0 = slots[4 * x], s1 = slots[4 * x + 1], s2 = slots[4 * x + 2], s3 = slots[4 * x + 3];
+  uint32_t first = 0xffffffffu, wf = 0;
+#pragma unroll
+  for (int y = 0; y < kW; ++y) {
+    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)s0, y);
+    if (d < first) first = d, wf = (uint32_t)y;
+  }
+  *found = first != 0xffffffffu;
+  const uint32_t qf = *found ? first / kThreads : LB;
+  const uint32_t tq[4] = {(uint32_t)s1, (uint32_t)(s1 >> 32), (uint32_t)s2, (uint32_t)(s2 >> 32)};
+  uint32_t c = 0;
+#pragma unroll
+  for (int q = 0; q < LB; ++q)
+    if ((uint32_t)q < qf || ((uint32_t)q == qf && x < wf)) c += tq[q];
+  if (lane == wf) c += (uint32_t)(s0 >> 32);  // the nearest P's wave: its aggregates before the P
+  uint64_t sum = wave_sum_u32(lane < kW ? c : 0);
+  if (*found) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)s3, (int)wf);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(s3 >> 32), (int)wf);
+    sum += ((uint64_t)hi << 32) | lo;
+  }
+  return sum;
+}
+
+template <int LB, bool kWaves = false>
 __device__ uint64_t lookback_finish(uint64_t* status, uint64_t tile, uint64_t (&w)[LB], uint64_t* lds,
-                                    uint32_t* lds_first, uint32_t* polls = nullptr) {
+                                    uint32_t* lds_first, uint32_t* polls = nullptr, uint64_t* slots = nullptr) {
   constexpr uint32_t kWin = kThreads * LB;
   uint64_t prefix = 0;
   int64_t j = (int64_t)tile - 1;
-  while (true) {
+  for (uint32_t win = 0;; ++win) {
     // Poll with relaxed agent-scope (sc1) loads -- the R2 granule form of the HIP guide's
     // Guideline 16: every status word is written by an agent-scope atomic store -- and fall
     // back to the atomic re-read after 256 polls.  Polling by atomics alone made every
@@ -218,6 +325,18 @@ __device__ uint64_t lookback_finish(uint64_t* status, uint64_t tile, uint64_t (&
         const int64_t idx = j - (q * kThreads + threadIdx.x);
         if (!(w[q] >> 62)) w[q] = spins < 256 ? ld_status(status + idx) : ld_status_fresh(status + idx);
       }
+    }
+    if (kWaves) {  // slots alternate by window: a wave is at most one barrier ahead
+      bool found;
+      prefix += lookback_window_waves<LB>(w, slots + (win & 1) * 4 * (kThreads / 64), &found);
+      if (found) return prefix;
+      j -= kWin;
+#pragma unroll
+      for (int q = 0; q < LB; ++q) {
+        const int64_t idx = j - (q * kThreads + threadIdx.x);
+        w[q] = idx >= 0 ? ld_status(status + idx) : kFlagP;
+      }
+      continue;
     }
     // nearest published inclusive prefix (distance d = q * kThreads + threadIdx.x)
     if (threadIdx.x == 0) *lds_first = kWin;
@@ -290,7 +409,7 @@ __device__ __forceinline__ void load_sub(const WireValArgs& a, uint64_t first, S
 // Sizes of one sub-tile's records and their offsets inside the sub-tile (record order), from
 // ONE block scan: a record is at most 61 bytes and a sub-tile row p of 512 records at most
 // 31,232, so the four rows' sizes travel as four 16-bit lanes of one u64.
-template <int NC>
+template <int NC, bool kShflScan = false>
 __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t first, const SRec<NC> (&r)[kPer],
                                                 uint32_t (&off)[kPer], uint64_t* lds) {
   uint64_t packed = 0;
@@ -300,7 +419,7 @@ __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t f
     packed |= (uint64_t)(i < a.n ? frame_size(a, srec_body(r[p])) : 0) << (16 * p);
   }
   uint64_t e;
-  const uint64_t t = block_scan(packed, &e, lds);
+  const uint64_t t = kShflScan ? block_scan(packed, &e, lds) : block_scan_packed(packed, &e, lds);
   __syncthreads();  // lds is reused by the next scan
   uint32_t row = 0;
 #pragma unroll
@@ -331,14 +450,21 @@ __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t f
 // bit 4 reload the values for the build instead of holding them, bit 5 (the product plus)
 // per-tile phase timestamps into a.trace (tools/wire_trace.py); bits 6/7 a look-back window of
 // 1,024 / 512 predecessors instead of 2,048, bit 8 (trace) wait for the look-back's first
-// window right after issuing it, to time its round trip.
+// window right after issuing it, to time its round trip, bit 9 no mid-build re-read of the
+// window's unpublished entries, bit 10 the look-back window reduced by an LDS atomic and a
+// block scan (four barriers) instead of by waves (one), bit 11 the sub-tile sizes scanned by
+// __shfl_up (ds_bpermute) instead of DPP.
 template <int V, int NC>
 __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   __shared__ uint64_t lds[kThreads / 64 + 1];
-  __shared__ uint32_t s_tile, s_first;
+  __shared__ uint32_t s_tile, s_first, s_polls;
+  __shared__ uint64_t s_build_end, s_lbslots[2 * 4 * (kThreads / 64)];
   __shared__ __attribute__((aligned(16))) uint32_t stage[kStageBytes / 4 + 8];
   uint64_t ts[6];
-  if (V & 32) ts[0] = wall_clock64();
+  if (V & 32) {
+    ts[0] = wall_clock64();
+    if (threadIdx.x == 0) s_build_end = 0, s_polls = 0;
+  }
   if (V & 1) {
     if (threadIdx.x == 0) s_tile = blockIdx.x;
   } else if (threadIdx.x == 0) {
@@ -361,7 +487,8 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
 #pragma unroll
   for (int j = 0; j < kSub; ++j) {
     if (!kHold) load_sub(a, tfirst + (uint64_t)j * kSubRecs, r[0]);
-    const uint32_t sub = sub_offsets(a, tfirst + (uint64_t)j * kSubRecs, r[kHold ? j : 0], off[j], lds);
+    const uint32_t sub =
+        sub_offsets<NC, (V & 2048) != 0>(a, tfirst + (uint64_t)j * kSubRecs, r[kHold ? j : 0], off[j], lds);
 #pragma unroll
     for (int p = 0; p < kPer; ++p) off[j][p] += agg;
     agg += sub;
@@ -391,24 +518,42 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
       if (!kHold) load_sub(a, tfirst + (uint64_t)j * kSubRecs, r[0]);
 #pragma unroll
       for (int p = 0; p < kPer; ++p)
-        if (tfirst + j * kSubRecs + p * kThreads + threadIdx.x < a.n)
-          put_srec(a, r[kHold ? j : 0][p], srec_body(r[kHold ? j : 0][p]), st + off[j][p]);
+        if (tfirst + j * kSubRecs + p * kThreads + threadIdx.x < a.n) {
+          const SRec<NC>& rec = r[kHold ? j : 0][p];
+          put_srec(a, rec, srec_body(rec), st + off[j][p]);
+        }
+      // Halfway through the build, re-read the window entries that were not yet published:
+      // a predecessor that started just before this tile usually publishes while the first
+      // window is in flight, and the re-read's round trip now overlaps the second half of the
+      // build instead of following it (tools/wire_trace.py: one re-poll per tile, ~1.2 us).
+      if (j == kSub / 2 - 1 && !(V & (512 | 4)) && tile > 0) {
+#pragma unroll
+        for (int q = 0; q < LB; ++q) {
+          const int64_t idx = (int64_t)tile - 1 - (q * kThreads + threadIdx.x);
+          if (!(w[q] >> 62)) w[q] = ld_status(a.status + idx);
+        }
+      }
     }
   }
-  if (V & 32) ts[3] = wall_clock64();
+  if (V & 32) {
+    ts[3] = wall_clock64();
+    if ((threadIdx.x & 63) == 0) atomicMax(&s_build_end, ts[3]);
+  }
   uint64_t base = 0;
   if (V & 4) {
     base = (uint64_t)tile * 15 * kTileRecs;
   } else if (tile > 0) {
-    base = lookback_finish<LB>(a.status, tile, w, lds, &s_first, (V & 32) ? &polls : nullptr);
+    base = lookback_finish<LB, !(V & 1024)>(a.status, tile, w, lds, &s_first, (V & 32) ? &polls : nullptr, s_lbslots);
     if (threadIdx.x == 0) st_status(a.status + tile, kFlagP | (base + agg));
+    if (V & 32) atomicMax(&s_polls, polls);
   }
   if (tile == nt - 1 && threadIdx.x == 0) {
     *a.total = base + agg;
     if (a.offs) a.offs[a.n] = base + agg;
   }
   if (staged) {
-    __syncthreads();
+    // the stage is complete: the wave-reduced look-back's barrier follows every wave's build
+    if ((V & (4 | 1024)) || tile == 0) __syncthreads();
     if (V & 32) ts[4] = wall_clock64();
     if (!(V & 8)) store_stage(a.out, base, stage, agg);
     if (V & 32) {
@@ -422,6 +567,8 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
         t[8] = ts_arrive;
         t[9] = polls;                        // re-polls by thread 0 (the nearest entries)
         t[10] = tile > 0 ? s_first : 0;      // distance of the nearest published prefix (last window)
+        t[11] = s_build_end;                 // the last wave's end of the stage build
+        t[12] = s_polls;                     // re-polls, most of any thread
       }
     }
     return;
@@ -466,6 +613,11 @@ PZ_WIRE_VAL_KERNEL(pz_wire_val_v36_kernel, 36, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v96_kernel, 96, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v160_kernel, 160, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v288_kernel, 288, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v512_kernel, 512, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v544_kernel, 544, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v1024_kernel, 1024, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v1056_kernel, 1056, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v2048_kernel, 2048, 3)
 #undef PZ_WIRE_VAL_KERNEL
 
 // Records with bytes fields: tiles of kBytesSub x 256 records, one per thread per sub-tile.
@@ -567,7 +719,7 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
       switch (g_wire_variant) {
 #define PZ_CASE(V) \
   case V: hipLaunchKernelGGL(pz_wire_val_v##V##_kernel, g, b, 0, s, a, n32); break;
-        PZ_CASE(1) PZ_CASE(2) PZ_CASE(4) PZ_CASE(8) PZ_CASE(7) PZ_CASE(15) PZ_CASE(16)
+        PZ_CASE(1) PZ_CASE(2) PZ_CASE(4) PZ_CASE(8) PZ_CASE(7) PZ_CASE(15) PZ_CASE(16) PZ_CASE(512) PZ_CASE(1024) PZ_CASE(2048)
 #undef PZ_CASE
 #define PZ_TRACE(V)                                                     \
   case V:                                                               \
@@ -575,7 +727,7 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
     a.trace = g_wire_trace;                                             \
     hipLaunchKernelGGL(pz_wire_val_v##V##_kernel, g, b, 0, s, a, n32);  \
     break;
-        PZ_TRACE(32) PZ_TRACE(34) PZ_TRACE(36) PZ_TRACE(96) PZ_TRACE(160) PZ_TRACE(288)
+        PZ_TRACE(32) PZ_TRACE(34) PZ_TRACE(36) PZ_TRACE(96) PZ_TRACE(160) PZ_TRACE(288) PZ_TRACE(544) PZ_TRACE(1056)
 #undef PZ_TRACE
         default: hipLaunchKernelGGL(pz_wire_val_kernel, g, b, 0, s, a, n32);
       }

@@ -47,8 +47,11 @@ def main():
           % (n, total, us, alg / us / 1e3, alg / us / 1e3 / 80))
     if len(sys.argv) > 2:  # ablation (wire.hip wire_val_body V, one tile per workgroup): results wrong for V != 0
         names = {1: "tile = blockIdx (no ticket)", 2: "no stage build", 4: "no look-back", 8: "no store",
-                 7: "1+2+4", 15: "1+2+4+8", 16: "reload values for the build"}
-        for v in (0, 16, 1, 2, 4, 8, 7, 15, 0):
+                 7: "1+2+4", 15: "1+2+4+8", 16: "reload values for the build",
+                 512: "no mid-build re-read of the window",
+                 1024: "look-back reduced by LDS atomic + block scan",
+                 2048: "sub-tile scans by shfl_up"}
+        for v in (0, 2048, 0, 2048, 1024, 1, 2, 4, 8, 0):
             _lib.lib.dll.pz_debug_set_wire_variant(v)
             print("  variant %2d %-28s %.1f us" % (v, names.get(v, "product"), timed()))
         _lib.lib.dll.pz_debug_set_wire_variant(0)

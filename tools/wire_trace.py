@@ -47,7 +47,7 @@ def main():
         torch.cuda.synchronize()
         t = trace.cpu().numpy().reshape(nt, 16)
         ts = t[:, :6].astype(np.int64)
-        same = bool(torch.equal(out[:ref.numel()], ref)) if variant == 32 else None
+        same = bool(torch.equal(out[:ref.numel()], ref)) if variant in (32, 544) else None
         t0 = ts[:, 0].min()
         d = np.diff(ts, axis=1) * 10 / 1e3  # us (100 MHz)
         life = (ts[:, 5] - ts[:, 0]) * 10 / 1e3
@@ -72,6 +72,8 @@ def main():
                                 "max": int(t[1:, 9].max())},
             "nearest_prefix_distance": {"median": float(np.median(t[1:, 10])),
                                         "p90": float(np.percentile(t[1:, 10], 90))},
+            "build_end_last_wave_after_thread0_us": round(float(np.median((t[:, 11] - ts[:, 3]) * 10 / 1e3)), 2),
+            "repolls_most_of_any_thread": {"median": float(np.median(t[1:, 12])), "p90": float(np.percentile(t[1:, 12], 90))},
             "first_window_round_trip_us": (round(float(np.median((t[1:, 8] - ts[1:, 2]) * 10 / 1e3)), 2)
                                            if variant & 256 else None),
         })
