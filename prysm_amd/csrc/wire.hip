@@ -6,15 +6,16 @@
 // start_dynasty 6, end_dynasty 7).  proto3 rules: ascending field order, zero scalars and
 // empty bytes omitted, every record framed as a length-delimited repeated field.
 //
-// One launch (after a small memset of the tile-status words).  A workgroup takes a tile of
-// records, derives their encoded sizes, scans them, and learns the tile's output offset by a
-// decoupled look-back over its predecessors' published sizes.  Then it writes the tile's
+// One launch (after a one-dispatch reset of the tile-status words).  A workgroup takes a tile
+// of records, derives their encoded sizes, scans them, and learns the tile's output offset by
+// a decoupled look-back over its predecessors' published sizes.  Then it writes the tile's
 // bytes.  This is HBM-bound byte work, with no MFMA, and the columns are read once.
-//  * Scalar-only records (no bytes fields; the chain's CrystallizedState): 2,048 records per
-//    tile, loaded with coalesced column loads.  The tile's encoding is built in a 32 KB LDS
-//    stage and stored with aligned dword stores.  A tile larger than the stage (records
-//    averaging over 16 bytes) writes lane by lane instead.
-//  * Records with bytes fields: 2,048 records per tile, sizes first, then (after the
+//  * Scalar-only records (no bytes fields; the chain's CrystallizedState): 4,096 records per
+//    512-thread tile, loaded with coalesced column loads and held in registers.  The tile's
+//    encoding is built in a 64 KiB LDS stage while the look-back is in flight and stored with
+//    16-B stores.  A tile larger than the stage (records averaging over 16 bytes) writes lane
+//    by lane instead.
+//  * Records with bytes fields: 4,096 records per tile, sizes first, then (after the
 //    look-back) a second read of the records, written lane by lane straight to HBM.
 #include "wire.h"
 
