@@ -375,6 +375,7 @@ __device__ uint64_t lookback_block(uint64_t* status, uint64_t tile, uint64_t* ld
 
 // Store stage[0..span) at out+base with 16-B stores: bytes up to the first 16-aligned
 // address, then 16-B chunks (each funnel-shifted out of five LDS words), then the tail.
+template <bool kNt = false>
 __device__ __forceinline__ void store_stage(uint8_t* out, uint64_t base, const uint32_t* stage, uint32_t span) {
   const uint8_t* st = reinterpret_cast<const uint8_t*>(stage);
   const uint32_t lead = (uint32_t)((16 - (base & 15)) & 15);
@@ -387,23 +388,32 @@ __device__ __forceinline__ void store_stage(uint8_t* out, uint64_t base, const u
     uint32_t x[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) x[k] = stage[w0 + k];
-    dst[j] = sh ? make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], sh), __builtin_amdgcn_alignbyte(x[2], x[1], sh),
-                             __builtin_amdgcn_alignbyte(x[3], x[2], sh), __builtin_amdgcn_alignbyte(x[4], x[3], sh))
-                : make_uint4(x[0], x[1], x[2], x[3]);
+    const uint4 v = sh ? make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], sh), __builtin_amdgcn_alignbyte(x[2], x[1], sh),
+                                    __builtin_amdgcn_alignbyte(x[3], x[2], sh), __builtin_amdgcn_alignbyte(x[4], x[3], sh))
+                       : make_uint4(x[0], x[1], x[2], x[3]);
+    if (kNt) {
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      v4u t;
+      t.x = v.x, t.y = v.y, t.z = v.z, t.w = v.w;
+      __builtin_nontemporal_store(t, reinterpret_cast<v4u*>(dst + j));
+    } else {
+      dst[j] = v;
+    }
   }
   const uint32_t t0 = head + 16 * nq;
   if (t0 + threadIdx.x < span) out[base + t0 + threadIdx.x] = st[t0 + threadIdx.x];
 }
 
 // Record (j, p, t) of a tile = tile*kTileRecs + j*kSubRecs + p*kThreads + t: every column load
-// of a wave reads 512 contiguous bytes.
-template <int NC>
+// of a wave reads 512 contiguous bytes.  kNt: nontemporal loads (the columns are read once;
+// tools/wire_probe.py r2m: 164 -> 154 us per 16.7 M records).
+template <int NC, bool kNt = false>
 __device__ __forceinline__ void load_sub(const WireValArgs& a, uint64_t first, SRec<NC> (&r)[kPer]) {
 #pragma unroll
   for (int p = 0; p < kPer; ++p) {
     const uint64_t i = first + p * kThreads + threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < NC; ++k) r[p].v[k] = i < a.n ? a.ccol[k][i] : 0;
+    for (int k = 0; k < NC; ++k) r[p].v[k] = i < a.n ? (kNt ? __builtin_nontemporal_load(a.ccol[k] + i) : a.ccol[k][i]) : 0;
   }
 }
 
@@ -454,7 +464,8 @@ __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t f
 // window right after issuing it, to time its round trip, bit 9 no mid-build re-read of the
 // window's unpublished entries, bit 10 the look-back window reduced by an LDS atomic and a
 // block scan (four barriers) instead of by waves (one), bit 11 the sub-tile sizes scanned by
-// __shfl_up (ds_bpermute) instead of DPP.
+// __shfl_up (ds_bpermute) instead of DPP, bit 12 column loads with the default cache policy
+// instead of nontemporal, bit 13 nontemporal output stores.
 template <int V, int NC>
 __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   __shared__ uint64_t lds[kThreads / 64 + 1];
@@ -483,7 +494,7 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   uint32_t off[kSub][kPer], agg = 0;
   if (kHold) {  // every sub-tile's loads in flight at once: one round trip, not kSub
 #pragma unroll
-    for (int j = 0; j < kSub; ++j) load_sub(a, tfirst + (uint64_t)j * kSubRecs, r[j]);
+    for (int j = 0; j < kSub; ++j) load_sub<NC, !(V & 4096)>(a, tfirst + (uint64_t)j * kSubRecs, r[j]);
   }
 #pragma unroll
   for (int j = 0; j < kSub; ++j) {
@@ -556,7 +567,7 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
     // the stage is complete: the wave-reduced look-back's barrier follows every wave's build
     if ((V & (4 | 1024)) || tile == 0) __syncthreads();
     if (V & 32) ts[4] = wall_clock64();
-    if (!(V & 8)) store_stage(a.out, base, stage, agg);
+    if (!(V & 8)) store_stage<(V & 8192) != 0>(a.out, base, stage, agg);
     if (V & 32) {
       __syncthreads();
       ts[5] = wall_clock64();
@@ -619,6 +630,9 @@ PZ_WIRE_VAL_KERNEL(pz_wire_val_v544_kernel, 544, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v1024_kernel, 1024, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v1056_kernel, 1056, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v2048_kernel, 2048, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v4096_kernel, 4096, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v8192_kernel, 8192, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v12288_kernel, 12288, 3)
 #undef PZ_WIRE_VAL_KERNEL
 
 // Records with bytes fields: tiles of kBytesSub x 256 records, one per thread per sub-tile.
@@ -720,7 +734,7 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
       switch (g_wire_variant) {
 #define PZ_CASE(V) \
   case V: hipLaunchKernelGGL(pz_wire_val_v##V##_kernel, g, b, 0, s, a, n32); break;
-        PZ_CASE(1) PZ_CASE(2) PZ_CASE(4) PZ_CASE(8) PZ_CASE(7) PZ_CASE(15) PZ_CASE(16) PZ_CASE(512) PZ_CASE(1024) PZ_CASE(2048)
+        PZ_CASE(1) PZ_CASE(2) PZ_CASE(4) PZ_CASE(8) PZ_CASE(7) PZ_CASE(15) PZ_CASE(16) PZ_CASE(512) PZ_CASE(1024) PZ_CASE(2048) PZ_CASE(4096) PZ_CASE(8192) PZ_CASE(12288)
 #undef PZ_CASE
 #define PZ_TRACE(V)                                                     \
   case V:                                                               \

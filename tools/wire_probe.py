@@ -50,8 +50,9 @@ def main():
                  7: "1+2+4", 15: "1+2+4+8", 16: "reload values for the build",
                  512: "no mid-build re-read of the window",
                  1024: "look-back reduced by LDS atomic + block scan",
-                 2048: "sub-tile scans by shfl_up"}
-        for v in (0, 2048, 0, 2048, 1024, 1, 2, 4, 8, 0):
+                 2048: "sub-tile scans by shfl_up", 4096: "default-policy column loads",
+                 8192: "nontemporal output stores", 12288: "default-policy loads, nontemporal stores"}
+        for v in (0, 4096, 8192, 12288, 0, 4096, 8192, 12288, 1, 2, 4, 8, 0):
             _lib.lib.dll.pz_debug_set_wire_variant(v)
             print("  variant %2d %-28s %.1f us" % (v, names.get(v, "product"), timed()))
         _lib.lib.dll.pz_debug_set_wire_variant(0)
