@@ -86,7 +86,12 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_kernel(pz_at
 // Two attestations per lane with 16-B column loads and 8/16-B stores (every column and output
 // 16-B aligned): half the memory instructions of the one-per-lane form and full-width
 // streaming requests.
-extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_x2_kernel(pz_att_check_batch b) {
+// NT: nontemporal column loads (every column is read once): 80 -> 67 us per 4 M attestations
+// (tools/attcheck_probe.py, profiles/r02/attcheck_probe_r2o.txt).
+// (The bitfield byte stays a cached load: a 64-B line holds ~2.5 bitfields, so a nontemporal
+// byte load re-fetches it: 87 us against 67, profiles/r02/attcheck_probe_ntb_r2o.txt.)
+template <bool NT>
+__device__ __forceinline__ void att_check_x2_body(const pz_att_check_batch& b) {
   const uint64_t i = 2 * ((uint64_t)blockIdx.x * kThreads + threadIdx.x);
   if (i >= b.natt) return;
   if (i + 1 >= b.natt) {  // odd tail
@@ -100,7 +105,14 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_x2_kernel(pz
     if (b.parents_start) b.parents_start[i] = pstart;
     return;
   }
-  auto ld2 = [](const uint64_t* p) { return *reinterpret_cast<const ulonglong2*>(p); };
+  auto ld2 = [](const uint64_t* p) {
+    if (NT) {
+      typedef unsigned long long v2u __attribute__((ext_vector_type(2)));
+      const v2u x = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
+      return make_ulonglong2(x.x, x.y);
+    }
+    return *reinterpret_cast<const ulonglong2*>(p);
+  };
   const ulonglong2 s = ld2(b.slot + i), bs = ld2(b.block_slot + i), js = ld2(b.justified_slot + i);
   const ulonglong2 nob = ld2(b.n_oblique + i), sh = ld2(b.shard_id + i), bo = ld2(b.boffs + i);
   const uint64_t bo2 = b.boffs[i + 2];
@@ -113,6 +125,15 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_x2_kernel(pz
   if (b.committee) *reinterpret_cast<uint2*>(b.committee + i) = make_uint2(c0, c1);
   if (b.parents_start) *reinterpret_cast<ulonglong2*>(b.parents_start + i) = make_ulonglong2(p0, p1);
 }
+
+extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_x2_kernel(pz_att_check_batch b) {
+  att_check_x2_body<true>(b);
+}
+extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_x2_cached_kernel(pz_att_check_batch b) {
+  att_check_x2_body<false>(b);  // A/B: default-policy column loads
+}
+
+static int g_attcheck_variant = 0;  // tools/ A/B only: 1 default-policy column loads
 
 int check_args(const pz_att_check_batch* b) {
   if (!b) return fail(PZ_EINVAL, "batch is null");
@@ -133,8 +154,12 @@ hipError_t launch_att_check(const pz_att_check_batch& b, hipStream_t s) {
                   (!b.parents_start || al(b.parents_start));
   if (x2) {
     const uint64_t lanes = (b.natt + 1) / 2;
-    hipLaunchKernelGGL(pz_att_check_x2_kernel, dim3((uint32_t)((lanes + kThreads - 1) / kThreads)), dim3(kThreads), 0,
-                       s, b);
+    if (g_attcheck_variant & 1)
+      hipLaunchKernelGGL(pz_att_check_x2_cached_kernel, dim3((uint32_t)((lanes + kThreads - 1) / kThreads)),
+                         dim3(kThreads), 0, s, b);
+    else
+      hipLaunchKernelGGL(pz_att_check_x2_kernel, dim3((uint32_t)((lanes + kThreads - 1) / kThreads)), dim3(kThreads),
+                         0, s, b);
   } else {
     hipLaunchKernelGGL(pz_att_check_kernel, dim3((uint32_t)((b.natt + kThreads - 1) / kThreads)), dim3(kThreads), 0,
                        s, b);
@@ -199,3 +224,9 @@ int pz_check_attestations(const pz_att_check_batch* hb) {
 }
 
 }  // extern "C"
+
+extern "C" int pz_debug_set_attcheck_variant(int v) {
+  const int old = pz::g_attcheck_variant;
+  pz::g_attcheck_variant = v;
+  return old;
+}

@@ -33,17 +33,27 @@ def main():
     for _ in range(200):
         _lib.lib.call("pz_dev_check_attestations", ctypes.byref(b), sh)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 100
-    e0.record()
-    for _ in range(reps):
-        _lib.lib.call("pz_dev_check_attestations", ctypes.byref(b), sh)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+    def timed(reps=100):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            _lib.lib.call("pz_dev_check_attestations", ctypes.byref(b), sh)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    ms = timed()
     digest = int(st.sum().item()) * 31 + int(cm.sum().item()) * 7 + int(ps.sum().item())
     print("attcheck: %d attestations  %.4f ms  %.1f G/s  result digest %d" % (natt, ms, natt / ms / 1e6, digest),
           flush=True)
+    dll = _lib.lib.dll
+    if hasattr(dll, "pz_debug_set_attcheck_variant"):  # same-process A/B (1: default-policy column loads)
+        for v in (0, 1, 0, 1, 0):
+            dll.pz_debug_set_attcheck_variant(v)
+            ms = timed()
+            d = int(st.sum().item()) * 31 + int(cm.sum().item()) * 7 + int(ps.sum().item())
+            print("  variant %d  %.4f ms  same digest %s" % (v, ms, d == digest), flush=True)
+        dll.pz_debug_set_attcheck_variant(0)
 
 
 if __name__ == "__main__":
