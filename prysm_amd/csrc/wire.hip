@@ -247,7 +247,8 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
 // a window holds at most 2,048 entries), plus the P itself.  `slots` is 8 waves x 4 u64.
 // Returns the window's contribution; *found says whether it held a P.
 template <int LB>
-__device__ __forceinline__ uint64_t lookback_window_waves(const uint64_t (&w)[LB], uint64_t* slots, bool* found) {
+__device__ __forceinline__ uint64_t lookback_window_waves(const uint64_t (&w)[LB], uint64_t* slots, bool* found,
+                                                          uint32_t* trace_first) {
   static_assert(LB <= 4, "per-level sums are packed two per slot");
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t dw = 0xffffffffu, pa = 0, T[4] = {0, 0, 0, 0};
@@ -285,6 +286,7 @@ __device__ __forceinline__ uint64_t lookback_window_waves(const uint64_t (&w)[LB
     if (d < first) first = d, wf = (uint32_t)y;
   }
   *found = first != 0xffffffffu;
+  if (threadIdx.x == 0) *trace_first = first;  // tools/wire_trace.py: the nearest prefix's distance
   const uint32_t qf = *found ? first / kThreads : LB;
   const uint32_t tq[4] = {(uint32_t)s1, (uint32_t)(s1 >> 32), (uint32_t)s2, (uint32_t)(s2 >> 32)};
   uint32_t c = 0;
@@ -329,7 +331,7 @@ __device__ uint64_t lookback_finish(uint64_t* status, uint64_t tile, uint64_t (&
     }
     if (kWaves) {  // slots alternate by window: a wave is at most one barrier ahead
       bool found;
-      prefix += lookback_window_waves<LB>(w, slots + (win & 1) * 4 * (kThreads / 64), &found);
+      prefix += lookback_window_waves<LB>(w, slots + (win & 1) * 4 * (kThreads / 64), &found, lds_first);
       if (found) return prefix;
       j -= kWin;
 #pragma unroll
