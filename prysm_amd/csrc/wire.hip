@@ -467,7 +467,8 @@ __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t f
 // window's unpublished entries, bit 10 the look-back window reduced by an LDS atomic and a
 // block scan (four barriers) instead of by waves (one), bit 11 the sub-tile sizes scanned by
 // __shfl_up (ds_bpermute) instead of DPP, bit 12 column loads with the default cache policy
-// instead of nontemporal, bit 13 nontemporal output stores.
+// instead of nontemporal, bit 13 nontemporal output stores, bit 14 (tests) no inclusive
+// prefixes published (every look-back walks back to tile 0; exact output).
 template <int V, int NC>
 __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   __shared__ uint64_t lds[kThreads / 64 + 1];
@@ -558,7 +559,9 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
     base = (uint64_t)tile * 15 * kTileRecs;
   } else if (tile > 0) {
     base = lookback_finish<LB, !(V & 1024)>(a.status, tile, w, lds, &s_first, (V & 32) ? &polls : nullptr, s_lbslots);
-    if (threadIdx.x == 0) st_status(a.status + tile, kFlagP | (base + agg));
+    // (variant 16384, tests only: no inclusive prefix is published, so every look-back walks
+    // window after window back to tile 0 -- the multi-window path, with exact output)
+    if (threadIdx.x == 0 && !(V & 16384)) st_status(a.status + tile, kFlagP | (base + agg));
     if (V & 32) atomicMax(&s_polls, polls);
   }
   if (tile == nt - 1 && threadIdx.x == 0) {
@@ -635,6 +638,8 @@ PZ_WIRE_VAL_KERNEL(pz_wire_val_v2048_kernel, 2048, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v4096_kernel, 4096, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v8192_kernel, 8192, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v12288_kernel, 12288, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v16384_kernel, 16384, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v16512_kernel, 16512, 3)
 #undef PZ_WIRE_VAL_KERNEL
 
 // Records with bytes fields: tiles of kBytesSub x 256 records, one per thread per sub-tile.
@@ -736,7 +741,7 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
       switch (g_wire_variant) {
 #define PZ_CASE(V) \
   case V: hipLaunchKernelGGL(pz_wire_val_v##V##_kernel, g, b, 0, s, a, n32); break;
-        PZ_CASE(1) PZ_CASE(2) PZ_CASE(4) PZ_CASE(8) PZ_CASE(7) PZ_CASE(15) PZ_CASE(16) PZ_CASE(512) PZ_CASE(1024) PZ_CASE(2048) PZ_CASE(4096) PZ_CASE(8192) PZ_CASE(12288)
+        PZ_CASE(1) PZ_CASE(2) PZ_CASE(4) PZ_CASE(8) PZ_CASE(7) PZ_CASE(15) PZ_CASE(16) PZ_CASE(512) PZ_CASE(1024) PZ_CASE(2048) PZ_CASE(4096) PZ_CASE(8192) PZ_CASE(12288) PZ_CASE(16384) PZ_CASE(16512)
 #undef PZ_CASE
 #define PZ_TRACE(V)                                                     \
   case V:                                                               \

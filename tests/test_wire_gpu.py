@@ -167,3 +167,42 @@ def test_scalar_columns_many_tiles(which, offsets):
         assert raw == b"".join(oracle_record(v, i) for i in range(n))
     else:
         assert wire.validators_device(v, 11) == wire.validators(v)
+
+
+@pytest.mark.parametrize("variant", [16384, 16384 | 128])
+def test_lookback_multi_window(variant):
+    """The wave-reduced look-back over several windows: with no inclusive prefix published
+    (wire.hip variant bit 14; bit 7 shrinks the window to 512 predecessors) every tile sums
+    aggregates window after window back to tile 0.  3,000 tiles: up to 2 (6) windows per tile.
+    The bytes must equal the product kernel's, which must equal the host encoder's."""
+    import torch
+
+    n = 4096 * 3000 - 77
+    rng = np.random.default_rng(21)
+    bal = rng.integers(16, 49, size=n, dtype=np.uint64)
+    end = np.full(n, 9999999999999999999, np.uint64)
+    start = (rng.integers(0, 3, size=n).astype(np.uint64) * rng.integers(0, 1 << 40, size=n, dtype=np.uint64))
+    cols_t = [torch.from_numpy(a.view(np.int64)).cuda() for a in (bal, start, end)]
+    dll = _lib.lib.dll
+    bound = int(dll.pz_wire_validators_bound(n, 0))
+    d_scr = torch.zeros(int(dll.pz_wire_scratch_bytes(n)) // 8, dtype=torch.int64, device="cuda")
+    d_tot = torch.zeros(1, dtype=torch.int64, device="cuda")
+    cols = _lib.ValidatorCols(None, None, None, None, None, None, *[t.data_ptr() for t in cols_t])
+    sh = torch.cuda.current_stream().cuda_stream
+
+    def encode(v):
+        out = torch.zeros(bound, dtype=torch.uint8, device="cuda")
+        old = dll.pz_debug_set_wire_variant(v)
+        try:
+            _lib.lib.call("pz_dev_wire_validators", ctypes.byref(cols), n, 11, out.data_ptr(), None, d_scr.data_ptr(),
+                          d_tot.data_ptr(), sh)
+            torch.cuda.synchronize()
+        finally:
+            dll.pz_debug_set_wire_variant(old)
+        return out[:int(d_tot.item())]
+
+    ref = encode(0)
+    assert torch.equal(encode(variant), ref)
+    k = 50_000  # the host encoder on a prefix (the framing is per record, so prefixes agree)
+    want = wire.validators(pb.Validators(k, balance=bal[:k], start_dynasty=start[:k], end_dynasty=end[:k]))
+    assert ref[:len(want)].cpu().numpy().tobytes() == want
