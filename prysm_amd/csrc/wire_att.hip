@@ -285,7 +285,8 @@ __device__ __forceinline__ uint32_t rscan32(uint32_t x) {
   return x;
 }
 
-extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_write_kernel(AttArgs a) {
+template <int W>
+__device__ __forceinline__ void wire_att_write_body(const AttArgs& a) {
   __shared__ __attribute__((aligned(16))) uint8_t stage[kWaves][kRecs][kStageAlloc];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int sl = lane & (kRow - 1), ri = lane / kRow;
@@ -446,6 +447,17 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_write_kernel(
   }
 }
 
+// 63 VGPRs either way; left alone the SGPRs (about 100) hold it at 7 waves per SIMD.  Capped
+// at 8 (28 SGPRs spill to VGPR lanes): 0.432 -> 0.383 ms per 1M-record encode
+// (tools/wire_att_probe.py r2t, same-process A/B).
+extern "C" __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))
+pz_wire_att_write_kernel(AttArgs a) {
+  wire_att_write_body<8>(a);
+}
+extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_write_w7_kernel(AttArgs a) {
+  wire_att_write_body<7>(a);  // A/B: the compiler's own occupancy (7 waves per SIMD)
+}
+
 int att_args(const pz_attestation_cols* c, uint64_t n, uint32_t field_num, AttArgs* a) {
   if (!c) return fail(PZ_EINVAL, "columns are null");
   if (field_num >= (1u << 29)) return fail(PZ_EINVAL, "field number %u out of range", field_num);
@@ -499,10 +511,15 @@ hipError_t launch_sizes_offsets(AttArgs a, void* scratch, hipStream_t s) {
                                  a.offs + 1, (size_t)a.n, rocprim::plus<uint64_t>(), s);
 }
 
+int g_att_write_variant = 0;  // tools/ A/B only: 1 = uncapped (7 waves per SIMD)
+
 hipError_t launch_write(const AttArgs& a, hipStream_t s) {
   if (!a.n) return hipSuccess;
-  hipLaunchKernelGGL(pz_wire_att_write_kernel, dim3((uint32_t)((a.n + kRecs * kWaves - 1) / (kRecs * kWaves))),
-                     dim3(kThreads), 0, s, a);
+  const dim3 g((uint32_t)((a.n + kRecs * kWaves - 1) / (kRecs * kWaves))), b(kThreads);
+  if (g_att_write_variant & 1)
+    hipLaunchKernelGGL(pz_wire_att_write_w7_kernel, g, b, 0, s, a);
+  else
+    hipLaunchKernelGGL(pz_wire_att_write_kernel, g, b, 0, s, a);
   return hipGetLastError();
 }
 
@@ -604,3 +621,9 @@ int pz_wire_attestations(const pz_attestation_cols* c, uint64_t n, uint32_t fiel
 }
 
 }  // extern "C"
+
+extern "C" int pz_debug_set_att_write_variant(int v) {
+  const int old = pz::g_att_write_variant;
+  pz::g_att_write_variant = v;
+  return old;
+}

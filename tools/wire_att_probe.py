@@ -45,6 +45,18 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
+    dll = _lib.lib.dll
+    if hasattr(dll, "pz_debug_set_att_write_variant"):  # same-process A/B of the write kernel
+        for v in (0, 1, 0, 1, 0):
+            dll.pz_debug_set_att_write_variant(v)
+            e0.record()
+            for _ in range(reps):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            print("  write variant %d  encode %.3f ms" % (v, e0.elapsed_time(e1) / reps), flush=True)
+        dll.pz_debug_set_att_write_variant(0)
+        run()
     # the CSR hash kernel over the encoded records (the encode + hash leg's second launch)
     dig = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
 
