@@ -762,14 +762,23 @@ pz_epoch_pre_kernel(EpochArgs a, FusedArgs f, uint64_t pbpi, uint64_t npb) {
     const uint64_t cb = beg + chunk * kPopBytesPerBlock;
     uint64_t cnt = 0;
     if (cb < end) {
+      // the chunk's 16-B words from cb & ~15: every load issued before any is used (a loop
+      // with one load per trip waited out four round trips per block)
+      constexpr int kW = (int)(kPopBytesPerBlock / (16 * kThreads)) + 1;
       const uint64_t ce = end < cb + kPopBytesPerBlock ? end : cb + kPopBytesPerBlock;
-      for (uint64_t u = (cb & ~15ull) + 16ull * tid; u < ce; u += 16ull * kThreads) {
-        if (u >= cb && u + 16 <= ce) {
-          const uint4 q = *reinterpret_cast<const uint4*>(a.bits + u);
-          cnt += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
-        } else {
-          for (uint64_t k = u < cb ? cb : u; k < u + 16 && k < ce; ++k) cnt += __popc((uint32_t)a.bits[k]);
-        }
+      uint4 q[kW];
+#pragma unroll
+      for (int k = 0; k < kW; ++k) {  // branch-free: the state pads its bitfield buffer by 16 B
+        const uint64_t u = (cb & ~15ull) + 16ull * (k * kThreads + tid);
+        q[k] = *reinterpret_cast<const uint4*>(a.bits + (u < ce ? u : (cb & ~15ull)));
+      }
+#pragma unroll
+      for (int k = 0; k < kW; ++k) {
+        const uint64_t u = (cb & ~15ull) + 16ull * (k * kThreads + tid);
+        if (u >= cb && u + 16 <= ce)
+          cnt += __popc(q[k].x) + __popc(q[k].y) + __popc(q[k].z) + __popc(q[k].w);
+        else
+          for (uint64_t j = u < cb ? cb : u; j < u + 16 && j < ce; ++j) cnt += __popc((uint32_t)a.bits[j]);
       }
     }
     const uint64_t c = block_reduce<false>(cnt, sh);
