@@ -386,9 +386,11 @@ int set_count_variant(int v) {
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ void winner_one(const EpochArgs& a, uint64_t ga) {
   const uint64_t inst = (uint32_t)ga / (uint32_t)a.natt;
+  // the shard id loads beside the tallies (two dependent round trips per attestation, not three)
   const uint64_t v = a.vote[ga], t = a.total[ga];
+  const uint32_t shard = a.att_shard[ga];
+  asm volatile("" ::"v"(shard));  // keeps the compiler from sinking the load into the branch
   if (3ull * v >= 2ull * t) {  // uint64 wrap, as in Go
-    const uint32_t shard = a.att_shard[ga];
     if (shard >= a.nrec) {
       atomicAdd((unsigned long long*)&a.scal[inst * kScal + kErrXl], (unsigned long long)kErrShard);
       return;
