@@ -60,6 +60,8 @@ hipError_t launch_epoch_reward(const EpochArgs& a, hipStream_t s);
 //   mid   : winners on the (reduced) tallies
 // The host enables it only when no attestation names a shard >= nrec (that panic depends on
 // the tallies, i.e. on balances the fused pass has already rewarded).
+constexpr uint64_t kLastCoMaxBytes = 16384;  // last bitfields up to 131,072 validators
+constexpr uint64_t kLastCoPos = 8192;         // positions per gathering block (one word per thread)
 constexpr int kPre = 2;  // pre[inst]: {bit count, PZ_XLERR_BITFIELD if a bitfield is short}
 struct FusedCommittee {        // per (instance, committee)
   uint64_t boff;              // bits offset of its single attestation's bitfield
@@ -82,6 +84,9 @@ struct FusedArgs {
   int rank0;                  // 1: this rank writes the per-instance scalars (bit count, flags,
                               //    applied, nact, max index) that the all-reduce must not multiply
   uint64_t vstride;           // row stride of balance/start/end (>= nval, even)
+  uint32_t* lastco;           // [B][lcw] or NULL: the reward bit of every position p (bit co_index[p]
+  uint64_t lcw;               //   of the instance's last bitfield), LSB-first, gathered by `pre`
+                              //   through LDS when the last bitfield fits kLastCoMaxBytes
   int own_only;               // sharded: winners proposed only for the attestations whose
                               //    committee this rank holds (pz_epoch_fwin_kernel)
 };

@@ -751,10 +751,61 @@ hipError_t launch_epoch_reward_mode(const EpochArgs& a, int mode, hipStream_t s)
 // Pre: [popcount blocks (B x pbpi) | one thread per attestation].  Every rank counts every
 // bitfield byte (2 MB per 16.7 M validator-epochs) so that its fused pass knows the
 // threshold without a collective; rank 0 alone reports the count in scal.
+// Third range (f.lastco): the reward bits in position order.  A block stages its instance's last
+// bitfield in LDS (branch-free 16-B loads over the padded buffer), then each thread gathers 32
+// positions' bits -- bit co_index[p], MSB-first as CheckBit (checkbit.go:4-15) -- into one word.
+// The random lookups run from LDS here instead of from L2 behind each fused wave's stream.
+// (Several instances per block, sharing the co_index loads, held ~200 VGPRs: the compiler
+// hoists the 32 positions' address math out of the instance loop.)
+__device__ __forceinline__ void lastco_block(const EpochArgs& a, const FusedArgs& f, uint64_t blk, uint64_t lcb) {
+  __shared__ __attribute__((aligned(16))) uint8_t lbf[kLastCoMaxBytes + 32];
+  const int tid = threadIdx.x;
+  const uint64_t inst = blk / lcb, chunk = blk - inst * lcb;
+  const uint64_t lb = a.boffs[inst * a.natt + a.natt - 1], L = a.boffs[inst * a.natt + a.natt] - lb;
+  const uint64_t b16 = lb & ~15ull, n16 = (L + (lb & 15) + 15) / 16;
+  constexpr int kLoads = (int)((kLastCoMaxBytes + 16) / (16 * kThreads)) + 1;
+  uint4 q[kLoads];
+#pragma unroll
+  for (int k = 0; k < kLoads; ++k) {
+    const uint64_t w = (uint64_t)k * kThreads + tid;
+    q[k] = *reinterpret_cast<const uint4*>(a.bits + (w < n16 ? b16 + 16 * w : b16));
+  }
+#pragma unroll
+  for (int k = 0; k < kLoads; ++k) {
+    const uint64_t w = (uint64_t)k * kThreads + tid;
+    if (w < n16) *reinterpret_cast<uint4*>(lbf + 16 * w) = q[k];
+  }
+  __syncthreads();
+  const uint8_t* bf = lbf + (lb & 15);
+  const uint64_t wj = chunk * (kLastCoPos / 32) + tid;  // this thread's output word
+  if (wj >= f.lcw) return;
+  const uint64_t p0 = wj * 32, np = f.vstride;
+  uint4 ci[8];
+#pragma unroll
+  for (int g = 0; g < 8; ++g)  // 4 positions per load (the state pads co_index by 16 B); a group past the row reads 0
+    ci[g] = *reinterpret_cast<const uint4*>(a.co_index + (p0 + 4 * g < np ? p0 + 4 * g : 0));
+  uint32_t word = 0;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    const uint32_t idx[4] = {ci[g].x, ci[g].y, ci[g].z, ci[g].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint64_t p = p0 + 4 * g + e;
+      const uint32_t i = idx[e];
+      if (p < a.nval && i < 8 * L) word |= (uint32_t)((bf[i >> 3] >> (7 - (i & 7))) & 1) << (4 * g + e);
+    }
+  }
+  f.lastco[inst * f.lcw + wj] = word;
+}
+
 extern "C" __global__ void __launch_bounds__(kThreads)
-pz_epoch_pre_kernel(EpochArgs a, FusedArgs f, uint64_t pbpi, uint64_t npb) {
+pz_epoch_pre_kernel(EpochArgs a, FusedArgs f, uint64_t pbpi, uint64_t npb, uint64_t nab, uint64_t lcb) {
   __shared__ uint64_t sh[kThreads / 64];
   const int tid = threadIdx.x;
+  if (blockIdx.x >= npb + nab) {
+    lastco_block(a, f, blockIdx.x - npb - nab, lcb);
+    return;
+  }
   if (blockIdx.x < npb) {
     const uint64_t pb = blockIdx.x;
     const uint64_t inst = (uint32_t)pb / (uint32_t)pbpi, chunk = (uint32_t)pb - (uint32_t)inst * (uint32_t)pbpi;
@@ -814,7 +865,8 @@ constexpr uint32_t kNoAtt = 0xFFFFFFFEu, kManyAtt = 0xFFFFFFFFu;
 // MODE: an ablation knob for tools/ (0 in the product; results are wrong otherwise): bit 0 no
 // crosslink tallies, bit 1 reward bit from the balance instead of the last bitfield, bit 2 no
 // balance store, bit 3 no start/end loads (every validator taken as active), bit 4 start/end
-// loads with the default cache policy, bit 5 instance-major grid.
+// loads with the default cache policy, bit 5 instance-major grid; bit 8 (product when the
+// state has FusedArgs.lastco) the reward bits read in position order instead of looked up.
 //
 // Measured choices (tools/fused_parts.py, 65,536 x 256 / 1M x 16 step, us): start/end loads
 // nontemporal (read once per step: leaving the 256 MiB Infinity Cache to the balances, which
@@ -866,6 +918,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     const FusedCommittee ci = cinfo_ro[inst * f.ncomm + it.z];
     uint4 qb[2], qs[2], qe[2];
     uint2 cix[2];
+    uint32_t lcw_[2];  // f.lastco: the words holding the pair's reward bits
     uint32_t by0[2], by1[2];  // the committee bitfield bytes holding each element's bit
     bool v0[2], v1[2];
 #pragma unroll
@@ -885,7 +938,13 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
         qs[j] = ld16_nt(S + pp);
         qe[j] = ld16_nt(E + pp);
       }
-      cix[j] = (MODE & 2) ? make_uint2(0, 0) : *reinterpret_cast<const uint2*>(a.co_index + pp);
+      if (MODE & 256) {  // compile-time: a runtime branch here split the load batch
+        lcw_[j] = f.lastco[inst * f.lcw + (pp >> 5)];
+        cix[j] = make_uint2(0, 0);
+      } else {
+        lcw_[j] = 0;
+        cix[j] = (MODE & 2) ? make_uint2(0, 0) : *reinterpret_cast<const uint2*>(a.co_index + pp);
+      }
       // branch-free, clamped: issued with the stream loads (bits past the bitfield are masked
       // below; the pre pass has raised that panic)
       by0[j] = by1[j] = 0;
@@ -949,8 +1008,12 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
       nm += (v0[j] && !a0 ? 1 : 0) + (v1[j] && !a1 ? 1 : 0);
       if (applied) {  // every validator active: rank == index, the validator at p is co_index[p]
         // an element outside the piece looks up bit 0 (its co_index may be a row's pad)
-        const bool r0 = (MODE & 2) ? (b0 & 1) : bit_at(lastbf, v0[j] ? cix[j].x : 0u);
-        const bool r1 = (MODE & 2) ? (b1 & 1) : bit_at(lastbf, v1[j] ? cix[j].y : 0u);
+        const bool r0 = (MODE & 2) ? (b0 & 1)
+                        : (MODE & 256) ? ((lcw_[j] >> (p & 31)) & 1)
+                                       : bit_at(lastbf, v0[j] ? cix[j].x : 0u);
+        const bool r1 = (MODE & 2) ? (b1 & 1)
+                        : (MODE & 256) ? ((lcw_[j] >> ((p + 1) & 31)) & 1)
+                                       : bit_at(lastbf, v1[j] ? cix[j].y : 0u);
         b0 = r0 ? b0 + PZ_ATTESTER_REWARD : b0 - PZ_ATTESTER_REWARD;
         b1 = r1 ? b1 + PZ_ATTESTER_REWARD : b1 - PZ_ATTESTER_REWARD;
         if (MODE & 4)
@@ -1025,6 +1088,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     fused_body<MODE>(a, f, pre_ro, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);          \
   }
 PZ_FUSED_KERNEL(pz_epoch_fused_kernel, 0)
+PZ_FUSED_KERNEL(pz_epoch_fused_lc_kernel, 256)  // reward bits from FusedArgs.lastco
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg1_kernel, 1)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg2_kernel, 2)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg3_kernel, 3)
@@ -1143,18 +1207,25 @@ hipError_t launch_epoch_fwin(const EpochArgs& a, const FusedArgs& f, hipStream_t
   return hipGetLastError();
 }
 
-hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
+hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f0, hipStream_t s) {
+  FusedArgs f = f0;
+  if (g_fused_variant) f.lastco = nullptr;  // ablations (tools/; 128: this A/B) look the bits up in the fused pass
   uint64_t pbpi = (a.max_inst_bytes + kPopBytesPerBlock - 1) / kPopBytesPerBlock;
   if (pbpi == 0) pbpi = 1;  // chunk 0 of each instance also resets the winners
   const uint64_t npb = (uint64_t)a.ninst * pbpi;
   const uint64_t nab = ((uint64_t)a.ninst * a.natt + kThreads - 1) / kThreads;
+  const uint64_t lcb = f.lastco ? (f.lcw * 32 + kLastCoPos - 1) / kLastCoPos : 0;  // gathering blocks per instance
+  const uint64_t nlb = lcb * a.ninst;
   if (!a.ninst || !a.natt) return hipSuccess;
-  hipLaunchKernelGGL(pz_epoch_pre_kernel, dim3((uint32_t)(npb + nab)), dim3(kThreads), 0, s, a, f, pbpi, npb);
+  hipLaunchKernelGGL(pz_epoch_pre_kernel, dim3((uint32_t)(npb + nab + nlb)), dim3(kThreads), 0, s, a, f, pbpi, npb,
+                     nab, lcb);
   return hipGetLastError();
 }
 
-hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
+hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream_t s) {
   if (!a.ninst) return hipSuccess;
+  FusedArgs f = f0;
+  if (g_fused_variant) f.lastco = nullptr;  // as launch_epoch_pre
   // at least one group: group 0 writes the per-instance scalars and zeroes the next step's
   // accumulators, also on a rank whose range holds no piece
   const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
@@ -1175,7 +1246,11 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f, hipStream_
     case 16: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg16_kernel); break;
     case 32: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg32_kernel); break;
     case 48: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg48_kernel); break;
-    default: PZ_LAUNCH_FUSED(pz_epoch_fused_kernel);
+    default:
+      if (f.lastco)
+        PZ_LAUNCH_FUSED(pz_epoch_fused_lc_kernel);
+      else
+        PZ_LAUNCH_FUSED(pz_epoch_fused_kernel);
   }
 #undef PZ_LAUNCH_FUSED
   return hipGetLastError();

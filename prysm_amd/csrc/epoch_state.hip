@@ -618,6 +618,15 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
         q.f.own_only = st->world > 1 ? 1 : 0;
         q.f.vstride = s.np;
         if (!fused_ok(a)) rc = fail(PZ_EINVAL, "one-pass epoch: validator arrays not on the 16-B path");
+        // the reward bits in position order (gathered by `pre` through LDS) when every
+        // instance's last bitfield fits the gathering block's stage
+        uint64_t maxl = 0;
+        for (uint64_t b = i0; b < i0 + Bp && st->natt; ++b)
+          maxl = std::max<uint64_t>(maxl, h->boffs[b * st->natt + st->natt] - h->boffs[b * st->natt + st->natt - 1]);
+        if (!rc && st->natt && maxl <= kLastCoMaxBytes && s.np) {
+          q.f.lcw = (s.np + 31) / 32;
+          rc = dalloc(s, &q.f.lastco, (size_t)Bp * q.f.lcw);
+        }
       }
       q.cur = 1;  // flip() below binds red[0] as the first step's buffer
     }

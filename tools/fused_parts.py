@@ -15,7 +15,7 @@ import torch  # noqa: E402
 from prysm_amd import _lib, casper, synth  # noqa: E402
 from prysm_amd.native import NativeEpoch  # noqa: E402
 
-VARIANTS = [0, 1, 2, 4, 8, 15, 16, 32]
+VARIANTS = [0, 128, 1, 2, 4, 8, 15, 16, 32]
 
 
 def run(nval, ninst, rounds=5, reps=10):
@@ -60,7 +60,7 @@ def run(nval, ninst, rounds=5, reps=10):
 def main():
     out = {"note": "us per pz_epoch_state step (pre + fused + winners) by fused variant; "
                    "1 no tallies, 2 no last-bitfield lookups, 4 no store, 8 no start/end loads, "
-                   "16 default-policy start/end loads, 32 instance-major grid",
+                   "16 default-policy start/end loads, 32 instance-major grid, 128 reward bits looked up in the fused pass (no position-order gather)",
            "65536x256": run(65536, 256), "1048576x16": run(1 << 20, 16)}
     print(json.dumps(out, indent=1))
 
