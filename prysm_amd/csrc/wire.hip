@@ -138,7 +138,8 @@ __device__ __forceinline__ void put_rec(const WireValArgs& a, const Rec& r, uint
 }
 
 // ---- tile offsets ----------------------------------------------------------------------------
-// Exclusive scan of one value per thread over the 256-thread block; returns the block total.
+// Exclusive scan of one value per thread over the 512-thread block (shfl_up steps); returns the
+// block total.  The scalar kernel scans its packed sizes with block_scan_packed (DPP) instead.
 __device__ __forceinline__ uint64_t block_scan(uint64_t x, uint64_t* excl, uint64_t* lds4) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint64_t inc = x;
@@ -458,6 +459,9 @@ __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t f
 // Dropped: building the stage by dword ORs from a register accumulator instead of byte
 // writes 305 (the 64-bit shifts cost more VALU than the LDS byte writes); persistent
 // workgroups pipelining the next tile's phase 1 under the look-back 278 (128 VGPRs + spills).
+// Round 2 (r2f-r2n): a coalesced look-back window without spills 175; its entries re-read
+// halfway through the build, the window reduced by waves (one barrier), DPP sub-tile scans
+// 163.5; nontemporal column loads 154.
 // V: an ablation knob for tools/wire_probe.py (0 in the product; output wrong otherwise):
 // bit 0 tile = blockIdx (no ticket), bit 1 no stage build, bit 2 no look-back, bit 3 no store,
 // bit 4 reload the values for the build instead of holding them, bit 5 (the product plus)
