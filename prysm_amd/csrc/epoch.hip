@@ -756,13 +756,26 @@ hipError_t launch_epoch_reward_mode(const EpochArgs& a, int mode, hipStream_t s)
 // positions' bits -- bit co_index[p], MSB-first as CheckBit (checkbit.go:4-15) -- into one word.
 // The random lookups run from LDS here instead of from L2 behind each fused wave's stream.
 // (Several instances per block, sharing the co_index loads, held ~200 VGPRs: the compiler
-// hoists the 32 positions' address math out of the instance loop.)
+// hoists the 32 positions' address math out of the instance loop.)  Thread t takes positions
+// p0 + 256k + t (k < 32), so each co_index load is coalesced across the wave (32 contiguous
+// positions per thread made every load touch 64 lines: 16 us of pre at 65,536 x 256), and a
+// ballot turns 64 lanes' bits into the two position-order words lane k stores.
 __device__ __forceinline__ void lastco_block(const EpochArgs& a, const FusedArgs& f, uint64_t blk, uint64_t lcb) {
   __shared__ __attribute__((aligned(16))) uint8_t lbf[kLastCoMaxBytes + 32];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t inst = blk / lcb, chunk = blk - inst * lcb;
   const uint64_t lb = a.boffs[inst * a.natt + a.natt - 1], L = a.boffs[inst * a.natt + a.natt] - lb;
   const uint64_t b16 = lb & ~15ull, n16 = (L + (lb & 15) + 15) / 16;
+  const uint64_t p0 = chunk * kLastCoPos, np = f.vstride;
+  constexpr int kK = (int)(kLastCoPos / kThreads);  // 32 positions per thread
+  uint32_t ci[kK];
+  typedef const __attribute__((address_space(1))) uint32_t gword;
+  gword* cb = (gword*)(uintptr_t)(a.co_index + p0);  // scalar base, 32-bit lane offsets
+#pragma unroll
+  for (int k = 0; k < kK; ++k) {  // issued with the stage's loads below
+    const uint32_t d = (uint32_t)k * kThreads + tid;
+    ci[k] = cb[p0 + d < np ? d : 0];
+  }
   constexpr int kLoads = (int)((kLastCoMaxBytes + 16) / (16 * kThreads)) + 1;
   uint4 q[kLoads];
 #pragma unroll
@@ -777,25 +790,20 @@ __device__ __forceinline__ void lastco_block(const EpochArgs& a, const FusedArgs
   }
   __syncthreads();
   const uint8_t* bf = lbf + (lb & 15);
-  const uint64_t wj = chunk * (kLastCoPos / 32) + tid;  // this thread's output word
-  if (wj >= f.lcw) return;
-  const uint64_t p0 = wj * 32, np = f.vstride;
-  uint4 ci[8];
+  uint64_t mine = 0;  // lane k keeps the ballot of step k
 #pragma unroll
-  for (int g = 0; g < 8; ++g)  // 4 positions per load (the state pads co_index by 16 B); a group past the row reads 0
-    ci[g] = *reinterpret_cast<const uint4*>(a.co_index + (p0 + 4 * g < np ? p0 + 4 * g : 0));
-  uint32_t word = 0;
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    const uint32_t idx[4] = {ci[g].x, ci[g].y, ci[g].z, ci[g].w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const uint64_t p = p0 + 4 * g + e;
-      const uint32_t i = idx[e];
-      if (p < a.nval && i < 8 * L) word |= (uint32_t)((bf[i >> 3] >> (7 - (i & 7))) & 1) << (4 * g + e);
-    }
+  for (int k = 0; k < kK; ++k) {
+    const uint64_t p = p0 + (uint64_t)k * kThreads + tid;
+    const uint32_t i = ci[k];
+    const bool bit = p < a.nval && i < 8 * L && ((bf[i >> 3] >> (7 - (i & 7))) & 1);
+    const uint64_t m = __ballot(bit);
+    if (lane == k) mine = m;
   }
-  f.lastco[inst * f.lcw + wj] = word;
+  if (lane < kK) {  // positions p0 + 256 lane + 64 wave .. +63: words w0, w0 + 1
+    const uint64_t w0 = (p0 + (uint64_t)lane * kThreads + 64 * wave) / 32;
+    if (w0 < f.lcw) f.lastco[inst * f.lcw + w0] = (uint32_t)mine;
+    if (w0 + 1 < f.lcw) f.lastco[inst * f.lcw + w0 + 1] = (uint32_t)(mine >> 32);
+  }
 }
 
 extern "C" __global__ void __launch_bounds__(kThreads)
