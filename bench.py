@@ -109,7 +109,36 @@ def parse():
                    help="validators per epoch instance (default: 65,536 at N=1, 1,048,576 at N>1)")
     p.add_argument("--epoch-instances", type=int, default=0,
                    help="independent epoch instances per step (default: 16.7M validator-epochs/step)")
+    p.add_argument("--single-process", action="store_true",
+                   help="one process drives --gpus devices through pz_init_devices (ncclCommInitAll, grouped "
+                        "RCCL calls over per-device streams): the form a Go node links (service.go:229)")
+    p.add_argument("--no-single-process-leg", action="store_true",
+                   help="at N > 1 under torchrun, skip rank 0's --single-process child run after the main legs")
+    p.add_argument("--single-process-timeout", type=float, default=300.0)
+    p.add_argument("--launch-selftest", action="store_true",
+                   help="launcher check: every rank prints its RANK/WORLD_SIZE and exits before any GPU call")
     return p.parse_args()
+
+
+def launch_ranks(args):
+    """``--gpus N`` (N > 1) without a launcher around this process (WORLD_SIZE unset): start
+    ``torch.distributed.run`` with N ranks as a CHILD process, forward its output and return
+    its exit code.  Nothing GPU-related has been imported or touched here (argparse only), so
+    the ranks are the only processes that initialise the GPUs; the parent just waits."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL)
+    env["PZ_BENCH_LAUNCH"] = "torchrun child of bench.py --gpus %d" % args.gpus
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print("bench: %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
 
 
 # Algorithmic HBM bytes per validator-epoch (SURVEY.md §8d, BASELINE.md §3): 16 B start/end
@@ -825,20 +854,36 @@ def cpu_baseline(records_np):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.single_process:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_selftest:
+        print(json.dumps({"rank": rank, "world": world, "gpus": args.gpus,
+                          "launch": os.environ.get("PZ_BENCH_LAUNCH", "external launcher")}), flush=True)
+        return
+    if args.single_process:
+        return single_process_main(args)
+    if world > 1 and args.gpus not in (1, world):
+        print("bench: --gpus %d but WORLD_SIZE %d: reporting the %d ranks that run" % (args.gpus, world, world),
+              file=sys.stderr, flush=True)
     import torch
     import torch.distributed as dist
 
     from prysm_amd import _lib, synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         # "nccl" is RCCL over xGMI; "gloo" only rehearses the N > 1 code path with several
         # ranks sharing one GPU (collectives through host copies; not a measurement)
         dist.init_process_group(args.backend)
     if args.backend == "gloo":
         local %= max(1, torch.cuda.device_count())
+        if world > 1 and args.epoch_path == "native":
+            # RCCL refuses two ranks on one device ("Duplicate GPU"), so the rehearsal runs the
+            # same orchestration through torch.distributed (labelled in epoch.config.path)
+            args.epoch_path = "torch"
+            args.epoch_path_note = "gloo rehearsal (ranks share a GPU; RCCL needs one device per rank)"
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     _lib.lib.call("pz_init", local)
@@ -879,18 +924,20 @@ def main():
 
     comm = None
     if world > 1 and not args.no_epoch and args.epoch_path == "native":
-        # every rank must take the same path: agree on whether the communicator came up
+        # every rank must take the same path: agree on whether the communicator came up; a
+        # failure ends the run (non-zero exit), it never switches to another path
         err = None
         try:
             comm = native_comm(dist, rank, world, local)
-        except Exception as e:  # reported in the JSON line, never silent
+        except Exception as e:
             err = "%s: %s" % (type(e).__name__, e)
         ok = torch.tensor([0.0 if err else 1.0], device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         if ok.item() < 1.0:
-            comm = None
-            args.epoch_path = "torch"
-            args.native_comm_error = err or "another rank failed to create its communicator"
+            print("bench: rank %d: the library's RCCL communicator did not come up: %s"
+                  % (rank, err or "another rank failed"), file=sys.stderr, flush=True)
+            dist.destroy_process_group()
+            sys.exit(3)
     epoch = None if args.no_epoch else epoch_leg(args, torch, dist, dev, rank, world, comm=comm)
     # configs[3]'s instance size (1,048,576 validators) on this one GPU: the N = 1 point of
     # the 1/2/4/8-GPU series that the N > 1 epoch leg runs (16 instances per GPU per step)
@@ -953,9 +1000,12 @@ def main():
                 gpu = d_out.cpu().numpy().reshape(n, 32)
                 line["parity"] = "bit-exact vs cpu_baseline on all %d digests: %s" % (
                     n, bool(np.array_equal(gpu, digests)))
+        line["launch"] = (os.environ.get("PZ_BENCH_LAUNCH", "torchrun (external launcher)") if world > 1
+                          else "single process, one GPU")
+        line["rccl_world"] = comm.world if comm is not None else None
         if epoch is not None:
-            if getattr(args, "native_comm_error", None):
-                epoch["native_comm_error"] = args.native_comm_error
+            if getattr(args, "epoch_path_note", None):
+                epoch["config"]["path_note"] = args.epoch_path_note
             line["epoch"] = epoch
         if epoch_1m is not None:
             line["epoch_1m_single_gpu"] = epoch_1m
@@ -969,10 +1019,134 @@ def main():
             line["wire_att"] = watt_out
         if shuf is not None:
             line["shuffle"] = shuf
-        print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if comm is not None:
+        comm.free()
+    if rank == 0:
+        if world > 1 and args.backend == "nccl" and not args.no_single_process_leg:
+            # the other ranks have left the process group (and exit); rank 0 runs the
+            # one-process form over all the node's GPUs in a child process with a time limit
+            del d_in, d_out
+            torch.cuda.synchronize(dev)
+            torch.cuda.empty_cache()
+            line["single_process"] = single_process_child(args, world)
+        print(json.dumps(line), flush=True)
+
+
+def single_process_child(args, ndev):
+    """Rank 0's child run of ``bench.py --single-process --gpus ndev`` (hash + epoch legs),
+    under a time limit; its JSON line, or the reason it has none."""
+    import subprocess
+
+    cmd = [sys.executable, os.path.abspath(__file__), "--single-process", "--gpus", str(ndev), "--steps",
+           str(args.steps), "--warmup", str(args.warmup), "--records", str(args.records), "--no-cpu-baseline"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
+                                                           "GROUP_RANK", "ROLE_RANK", "MASTER_PORT")}
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=args.single_process_timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out after %.0f s" % args.single_process_timeout, "cmd": " ".join(cmd)}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": "exit %d" % r.returncode, "stderr_tail": r.stderr[-2000:], "cmd": " ".join(cmd)}
+    return json.loads(lines[-1])
+
+
+def single_process_main(args):
+    """``--single-process --gpus N``: ONE process drives N GPUs, the form a Go node links (one
+    beacon-chain process, ``blockchain/service.go:229``).  The communicator is
+    ``pz_init_devices(N)`` (ncclCommInitAll; every collective is a grouped RCCL call over the
+    per-device streams, comm.hip), and:
+
+    * hash: each device hashes its own 1M-record batch (configs[1] per GPU, no collective);
+    * epoch: configs[3], B = 16 N instances of 1,048,576 validators sharded over the N
+      devices by ``pz_epoch_state`` (one-pass step, one grouped collective per part).
+
+    Wall clock over K steps on all devices; device time by HIP events on every shard's stream."""
+    import torch
+
+    from prysm_amd import _lib, casper, synth
+    from prysm_amd.native import Comm, NativeEpoch
+
+    N = args.gpus
+    comm = Comm.devices(N)
+    devs = [torch.device("cuda", i) for i in range(N)]
+    n = args.records
+    d_in, d_out, streams = [], [], []
+    for i, dv in enumerate(devs):
+        torch.cuda.set_device(dv)
+        _lib.lib.call("pz_init", i)
+        d_in.append(torch.from_numpy(synth.attestation_records_512(n, seed=2 + i).reshape(-1)).to(dv))
+        d_out.append(torch.empty(n * 32, dtype=torch.uint8, device=dv))
+        streams.append(torch.cuda.current_stream(dv))
+
+    def hash_step():
+        for i, dv in enumerate(devs):
+            torch.cuda.set_device(dv)
+            _lib.lib.call("pz_dev_blake2b512_fixed", d_in[i].data_ptr(), 512, 512, n, d_out[i].data_ptr(), 32,
+                          ctypes.c_void_p(streams[i].cuda_stream))
+
+    def sync_all():
+        for dv in devs:
+            torch.cuda.synchronize(dv)
+
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < args.clock_warm_ms:
+        for _ in range(8):
+            hash_step()
+        sync_all()
+    for _ in range(args.warmup):
+        hash_step()
+    sync_all()
+    evs = []
+    for i, dv in enumerate(devs):
+        torch.cuda.set_device(dv)
+        evs.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+        evs[-1][0].record(streams[i])
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        hash_step()
+    for i, dv in enumerate(devs):
+        torch.cuda.set_device(dv)
+        evs[i][1].record(streams[i])
+    sync_all()
+    wall = time.perf_counter() - t0
+    kern_ms = max(e0.elapsed_time(e1) for e0, e1 in evs) / args.steps
+    hash_out = {"value": n * N * args.steps / wall, "unit": "hashes/s", "ms_per_step": wall / args.steps * 1e3,
+                "kernel_ms_max_over_devices": kern_ms,
+                "roofline_frac": n * 4 * OPS_PER_COMPRESSION / (kern_ms * 1e-3) / VALU_PEAK}
+    del d_in, d_out
+    torch.cuda.set_device(devs[0])
+
+    nval = 1 << 20
+    ninst = 16 * N
+    shuffled = casper.shuffle_indices(b"A" + bytes(31), np.arange(nval, dtype=np.uint32))
+    inst = synth.epoch_batch(nval, ninst, seed=3, shuffled=shuffled)
+    de = NativeEpoch(inst, device=0, comm=comm)
+    del inst
+    for _ in range(args.warmup + 30):
+        de.step()
+    de.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        de.step()
+    de.sync()
+    wall_e = time.perf_counter() - t0
+    epoch_out = {"value": nval * ninst * args.steps / wall_e, "unit": "validator-epochs/s",
+                 "ms_per_step": wall_e / args.steps * 1e3,
+                 "config": {"validators": nval, "instances_per_step": ninst,
+                            "layout": "committee order, one-pass step" if de.one_pass else
+                                      "committee order, two-pass step" if de.committee_order else "index order",
+                            "shards": [list(de.shard(i)[:3]) for i in range(de.nlocal)]},
+                 "algorithmic_GBps_per_gpu": nval * 16 * EPOCH_BYTES_PER_VALIDATOR / (wall_e / args.steps) / 1e9}
+    de.free()
+    line = {"metric": METRIC, "mode": "single process, %d GPUs (pz_init_devices -> ncclCommInitAll)" % N,
+            "n_gpus": N, "rccl_world": comm.world, "rccl_nlocal": comm.nlocal, "steps": args.steps,
+            "warmup": args.warmup, "hash": hash_out, "epoch": epoch_out}
+    comm.free()
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

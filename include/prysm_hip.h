@@ -500,7 +500,8 @@ int  pz_epoch_state_validators(const pz_epoch_state* st, int local, uint32_t* in
 /* The sharded one-pass step leaves each attestation's vote/total complete only on the rank
  * holding its committee (its winners are exact everywhere: proposed by that rank, combined by
  * a minimum all-reduce); this collective (every rank calls it) completes them on every rank
- * for pz_epoch_state_results.  A no-op for the other steps. */
+ * for pz_epoch_state_results.  A no-op for the other steps, and for a step whose tallies it
+ * has already completed (calling it twice never sums complete tallies again). */
 int  pz_epoch_state_tallies(pz_epoch_state* st);
 /* *committee_order: 0 index order, 1 committee order (two-pass step), 2 committee order with
  * the one-pass step. */

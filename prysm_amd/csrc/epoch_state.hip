@@ -67,6 +67,7 @@ struct pz_epoch_state {
   bool fused = false;              // one-pass step (epoch.h "one-pass epoch") on that layout
   std::vector<uint32_t> co_inv;    // storage position -> validator index (committee order)
   uint64_t steps = 0;
+  uint64_t tallied = ~0ull;        // the step whose vote/total pz_epoch_state_tallies completed
   std::vector<Shard> sh;
   ~pz_epoch_state();
 };
@@ -716,6 +717,8 @@ int pz_epoch_state_tallies(pz_epoch_state* st) {
   if (!st) return fail(PZ_EINVAL, "state is null");
   if (!st->steps) return fail(PZ_EINVAL, "no step has run");
   if (!(st->fused && st->world > 1) || !st->natt) return PZ_OK;  // already complete on every rank
+  // summed once per step: a second all-reduce of complete tallies would multiply them by world
+  if (st->tallied == st->steps) return PZ_OK;
   const int L = (int)st->sh.size();
   std::vector<hipStream_t> streams(L);
   std::vector<uint64_t*> bufs(L);
@@ -733,7 +736,9 @@ int pz_epoch_state_tallies(pz_epoch_state* st) {
     for (int i = 0; i < L; ++i)
       if ((rc = wait(st->sh[i], st->sh[i].part[p].ev_nb))) return rc;
   }
-  return pz_epoch_state_sync(st);
+  if ((rc = pz_epoch_state_sync(st))) return rc;
+  st->tallied = st->steps;
+  return PZ_OK;
 }
 
 int pz_epoch_state_layout(const pz_epoch_state* st, int* committee_order) {

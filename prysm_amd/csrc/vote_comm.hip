@@ -37,18 +37,25 @@ struct RankWork {
     if (done) (void)hipEventDestroy(done);
     if (s) (void)hipStreamDestroy(s);
   }
+  // Device copy of host[0, count) followed by `pad` zero bytes (the whole buffer zeroed when
+  // host is null); never reads past host + count.
   template <typename T>
-  T* up(const T* host, size_t count, int* rc) {
+  T* up(const T* host, size_t count, int* rc, size_t pad = 0) {
     if (*rc) return nullptr;
     void* p = nullptr;
-    hipError_t e = hipMalloc(&p, std::max<size_t>(count * sizeof(T), 16));
+    const size_t bytes = count * sizeof(T), alloc = std::max<size_t>(bytes + pad, 16);
+    hipError_t e = hipMalloc(&p, alloc);
     if (e != hipSuccess) {
       *rc = hip_fail(e, "hipMalloc (vote tally)");
       return nullptr;
     }
     allocs.push_back(p);
-    if (host && count) e = hipMemcpyAsync(p, host, count * sizeof(T), hipMemcpyHostToDevice, s);
-    else e = hipMemsetAsync(p, 0, std::max<size_t>(count * sizeof(T), 16), s);
+    if (host && bytes) {
+      e = hipMemcpyAsync(p, host, bytes, hipMemcpyHostToDevice, s);
+      if (e == hipSuccess && alloc > bytes) e = hipMemsetAsync(static_cast<uint8_t*>(p) + bytes, 0, alloc - bytes, s);
+    } else {
+      e = hipMemsetAsync(p, 0, alloc, s);
+    }
     if (e != hipSuccess) *rc = hip_fail(e, "H2D (vote tally)");
     return static_cast<T*>(p);
   }
@@ -82,7 +89,9 @@ extern "C" int pz_comm_vote_tally(const pz_comm* comm, const uint32_t* committee
   std::vector<uint64_t*> bufs(L);
   std::vector<hipStream_t> streams(L);
   std::vector<hipEvent_t> evs(L);
-  std::vector<uint32_t> slice;
+  // every rank's bitmap words, packed [nslots][wn]: one host buffer per rank, alive until the
+  // final sync, so no rank's upload waits for another's
+  std::vector<std::vector<uint32_t>> slices(L);
   rc = PZ_OK;
   for (int i = 0; i < L && !rc; ++i) {
     RankWork& w = rk[i];
@@ -104,7 +113,7 @@ extern "C" int pz_comm_vote_tally(const pz_comm* comm, const uint32_t* committee
     v.committee = w.up(committee + coffs[0], rcf[ncomm], &rc);
     v.coffs = w.up(rcf.data(), ncomm + 1, &rc);
     v.att_comm = w.up(att_comm, natt, &rc);
-    v.bits = w.up(bits ? bits + boffs[0] : bits, rb[natt] + 16, &rc);
+    v.bits = w.up(bits ? bits + boffs[0] : bits, rb[natt], &rc, 16);  // 16-B zero pad for the wide loads
     v.boffs = w.up(rb.data(), natt + 1, &rc);
     v.item_att = w.up(item_att, nitems, &rc);
     v.item_slot = w.up(item_slot, nitems, &rc);
@@ -113,7 +122,7 @@ extern "C" int pz_comm_vote_tally(const pz_comm* comm, const uint32_t* committee
     v.nval = w.hi - w.lo;
     v.val_offset = w.lo;
     v.nval_global = nval;
-    // this rank's words of every slot's bitmap, packed [nslots][wn]
+    std::vector<uint32_t>& slice = slices[i];
     slice.assign(std::max<uint64_t>(nslots * w.wn, 1), 0);
     for (uint64_t s = 0; s < nslots; ++s)
       std::memcpy(slice.data() + s * w.wn, bitmaps + s * words_per_slot + w.wlo, w.wn * 4);
@@ -133,22 +142,20 @@ extern "C" int pz_comm_vote_tally(const pz_comm* comm, const uint32_t* committee
       e = launch_vote_tally(v, w.s);
       if (e != hipSuccess) rc = hip_fail(e, "pz_vote_tally_kernel (sharded)");
     }
-    // hipStreamSynchronize here would serialize the uploads of the next rank behind this
-    // one's; the all-reduce orders itself after every rank's stream instead
+    // no sync here: the local ranks tally concurrently, and the all-reduce orders itself
+    // after every rank's stream
     bufs[i] = w.red;
     streams[i] = w.s;
     evs[i] = w.done;
-    // slice is reused by the next rank: its H2D must have read it
-    if (!rc && (e = hipStreamSynchronize(w.s)) != hipSuccess) rc = hip_fail(e, "sync (vote tally upload)");
   }
   if (!rc && world > 1) rc = c->allreduce_u64(bufs.data(), nslots + 1, streams.data(), evs.data());
   std::vector<uint64_t> red(nslots + 1);
   for (int i = 0; i < L && !rc; ++i) {
     RankWork& w = rk[i];
     (void)hipSetDevice(w.dev);
+    std::vector<uint32_t>& slice = slices[i];
     hipError_t e = world > 1 ? hipStreamWaitEvent(w.s, w.done, 0) : hipSuccess;
     if (e == hipSuccess && i == 0) e = hipMemcpyAsync(red.data(), w.red, (nslots + 1) * 8, hipMemcpyDeviceToHost, w.s);
-    slice.assign(std::max<uint64_t>(nslots * w.wn, 1), 0);
     if (e == hipSuccess && w.wn)
       e = hipMemcpyAsync(slice.data(), w.v.bitmaps, nslots * w.wn * 4, hipMemcpyDeviceToHost, w.s);
     if (e == hipSuccess) e = hipStreamSynchronize(w.s);

@@ -193,12 +193,15 @@ def hash_batch_sharded(data, offsets, rank, world, group=None, out_bytes=32, has
     if group is False or world == 1:
         return mine
     per = -(-n // world)  # all-gather needs equal sizes: pad every slice to ceil(n / world)
-    send = torch.zeros(per * out_bytes, dtype=torch.uint8)
-    send[:mine.size] = torch.from_numpy(mine.reshape(-1).copy())
+    # RCCL ("nccl") gathers device tensors only: the slices go through this rank's GPU there
+    on_dev = dist.get_backend(group) == "nccl"
+    where = torch.device("cuda", torch.cuda.current_device()) if on_dev else torch.device("cpu")
+    send = torch.zeros(per * out_bytes, dtype=torch.uint8, device=where)
+    send[:mine.size] = torch.from_numpy(mine.reshape(-1).copy()).to(where)
     bufs = [torch.zeros_like(send) for _ in range(world)]
     dist.all_gather(bufs, send, group=group)
     out = np.zeros((n, out_bytes), np.uint8)
     for r in range(world):
         a, b = message_shard(n, r, world)
-        out[a:b] = bufs[r].numpy()[:(b - a) * out_bytes].reshape(b - a, out_bytes)
+        out[a:b] = bufs[r].cpu().numpy()[:(b - a) * out_bytes].reshape(b - a, out_bytes)
     return out

@@ -286,6 +286,28 @@ def test_max_active_index_scalar():
         assert int(scal[b, _lib.SCAL_NACT]) == act.size
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_native_epoch_tallies_twice_is_idempotent(world):
+    """pz_epoch_state_tallies sums the owner ranks' vote/total once per step; a second
+    call in the same step returns the same (complete) tallies, not world x them, and the next
+    step's call sums that step's tallies again."""
+    inst = _inst(20000, 2, False)
+    ne = NativeEpoch(inst, comm=Comm.loopback(world))
+    assert ne.one_pass
+    for _ in range(2):
+        ne.step()
+        ne.tallies()
+        ne.tallies()
+        want = [oracle_epoch(inst, b) for b in range(2)]
+        for local in range(world):
+            _, _, vote, total, _ = ne.results(local)
+            for b, (nb, _a, _n, v, t, _w) in enumerate(want):
+                np.testing.assert_array_equal(vote[b], v)
+                np.testing.assert_array_equal(total[b], t)
+        for b, (nb, *_rest) in enumerate(want):
+            inst["balance"][b] = nb
+
+
 def test_native_epoch_sharded_ranges_are_committee_aligned():
     """The sharded one-pass step splits the committee-order positions at committee starts: no
     committee straddles two ranks, and without pz_epoch_state_tallies a rank's vote/total are

@@ -70,6 +70,39 @@ def test_vote_cache_vs_oracle(world):
         assert vc.voters(h).tolist() == sorted(voters)
 
 
+@pytest.mark.parametrize("world", [0, 1, 3])
+def test_vote_tally_bitfield_at_page_end(world):
+    """the bitfields end exactly at a page whose successor is unmapped (PROT_NONE):
+    the tally reads only the caller's bytes (a read past them would fault here)."""
+    import ctypes
+    import mmap
+
+    from prysm_amd.native import Comm
+    page = mmap.PAGESIZE
+    buf = mmap.mmap(-1, 2 * page, prot=mmap.PROT_READ | mmap.PROT_WRITE)
+    base = ctypes.addressof(ctypes.c_char.from_buffer(buf))
+    libc = ctypes.CDLL(None, use_errno=True)
+    assert libc.mprotect(ctypes.c_void_p(base + page), page, 0) == 0  # guard page: PROT_NONE
+    nval = 1000
+    committee = np.arange(200, dtype=np.uint32)
+    coffs = np.array([0, 100, 200], U64)
+    balance = np.arange(nval, dtype=np.uint64) + U64(1)
+    bits = np.frombuffer(buf, dtype=np.uint8, count=26, offset=page - 26)
+    bits[:] = 0xF0
+    bits[12] &= 0xF0
+    bits[25] &= 0xF0
+    boffs = np.array([0, 13, 26], U64)
+    vc = VoteCache(nval)
+    items = [(0, vc.slot(b"a" * 32)), (1, vc.slot(b"b" * 32))]
+    vc.tally(committee, coffs, np.array([0, 1], np.uint32), bits, boffs, items, balance,
+             comm=Comm.loopback(world) if world else None)
+    for k, h in enumerate((b"a" * 32, b"b" * 32)):
+        mem = committee[100 * k:100 * (k + 1)]
+        voted = np.unpackbits(bits[13 * k:13 * (k + 1)])[:100].astype(bool)
+        assert vc.total(h) == int(balance[mem[voted]].sum())
+    libc.mprotect(ctypes.c_void_p(base + page), page, mmap.PROT_READ | mmap.PROT_WRITE)
+
+
 def test_sharded_vote_tally_panics():
     """A committee member >= len(validators) (core.go:329 indexes Validators[v]) and a short
     bitfield (CheckBit, core.go:328): the sharded tally raises PZ_EINDEX like the one-GPU form."""
