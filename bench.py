@@ -100,6 +100,8 @@ def parse():
                    help="auto: committee order when every validator is active and the committees partition "
                         "the set, one-pass step (pz_epoch_host.layout); twopass: that layout, two-pass step; "
                         "index: validator-index order")
+    p.add_argument("--no-epoch-cold", action="store_true",
+                   help="skip the epoch legs' cold-data rotation over 4 instance sets")
     p.add_argument("--no-replay", action="store_true")
     p.add_argument("--no-wire", action="store_true")
     p.add_argument("--no-attcheck", action="store_true")
@@ -145,8 +147,6 @@ def launch_ranks(args):
 # dynasty + 16 B balance read-modify-write + 1/8 B last-bitfield bit + 1/8 B committee bitfield
 # popcount + 12 B crosslink committee gather (u32 member + u64 balance).
 EPOCH_BYTES_PER_VALIDATOR = 44.25
-EPOCH_KERNELS = ("pz_epoch_pre_kernel", "pz_epoch_fused_kernel", "pz_epoch_mid_kernel")  # one-pass step
-EPOCH_KERNELS_TWOPASS = ("pz_epoch_count_kernel", "pz_epoch_mid_kernel", "pz_epoch_reward_kernel")
 HASH_KERNEL = "pz_b2b_fixed_persistent_kernel"
 CPU_SAMPLE_S = 8.0  # seconds of CPU work per cpu_baseline leg (three legs: ~25 s in all)
 
@@ -221,7 +221,8 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
     local_units = (hi - lo) * ninst
     achieved = local_units * EPOCH_BYTES_PER_VALIDATOR / (step_ms * 1e-3)
     one_pass = native and de.one_pass
-    kern = EPOCH_KERNELS if one_pass else EPOCH_KERNELS_TWOPASS
+    workload = {(65536, 256): "epoch65k", (1 << 20, 16): "epoch1m"}.get((nval, ninst)) if world == 1 else None
+    traffic = pmc_traffic(["pz_epoch_*"], workload) if workload else None
     out = {
         "metric": "validator-epoch updates/s",
         "value": units / wall,
@@ -244,13 +245,13 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                             if native else "DeviceEpoch (pz_dev_epoch_* + torch.distributed collectives)")},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
-                     "traffic": (pmc_traffic(kern) if (nval, ninst) == (65536, 256) else
-                                 pmc_traffic(kern, PMC_SUMMARY_EPOCH_1M) if (nval, ninst) == (1 << 20, 16)
-                                 else None),
-                     "traffic_source": ("%s (%s, %d x %d workload)"
-                                        % (PMC_SUMMARY if nval == 65536 else PMC_SUMMARY_EPOCH_1M, "+".join(kern),
-                                           nval, ninst)),
-                     "kernel": ("epoch step: pz_epoch_pre (bit count) + pz_epoch_fused (one pass: classify, "
+                     "bytes_model": "SURVEY.md §8d: 44.25 B per validator-epoch (the committee-order layout "
+                                    "does not move the 12 B committee gather it prices: see traffic)",
+                     "traffic": traffic,
+                     "traffic_source": ("%s (every pz_epoch_* kernel of the %d x %d step)"
+                                        % (pmc_summary_path(workload), nval, ninst)) if workload else None,
+                     "traffic_frac": (traffic / (step_ms * 1e-3) / HBM_PEAK) if traffic else None,
+                     "kernel": ("epoch step: pz_epoch_pre (bit count) + pz_epoch_fused[_lc] (one pass: classify, "
                                 "crosslink tallies, rewards, next-cycle sum) + pz_epoch_mid (winners); device "
                                 "time of the whole step" if one_pass else
                                 "epoch step (count+winner+compact+reward, device time of the whole step)"),
@@ -258,6 +259,8 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                      "algorithmic_bytes_per_launch": local_units * EPOCH_BYTES_PER_VALIDATOR},
     }
     del de
+    if world == 1 and native and workload and not args.no_epoch_cold:
+        out["cold"] = epoch_cold(args, torch, dev, nval, ninst, shuffled, workload)
     if rank == 0 and world == 1:
         out["parity"] = epoch_parity(inst, dev)
     if world == 1 and baseline:
@@ -265,6 +268,47 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
     if rank == 0 and world == 1 and not args.no_cpu_baseline and baseline:
         out["cpu_baseline"] = epoch_cpu_baseline(inst)
     return out
+
+
+def epoch_cold(args, torch, dev, nval, ninst, shuffled, workload, nsets=4):
+    """The same step with the timed steps rotated over ``nsets`` distinct instance sets (each
+    ~400 MB; together far above the 256 MiB Infinity Cache), all bound to one stream, so every
+    step reads its state from HBM: the epoch against HBM, not against the cache the
+    back-to-back steps of one set enjoy."""
+    from prysm_amd import synth
+    from prysm_amd.native import NativeEpoch
+
+    stream = torch.cuda.Stream(device=dev)  # a real stream: a null handle means "the state's own"
+    sets = []
+    for k in range(nsets):
+        de = NativeEpoch(synth.epoch_batch(nval, ninst, seed=3 + k, shuffled=shuffled), device=dev.index)
+        de.bind_stream(stream.cuda_stream)
+        sets.append(de)
+    steps = max(nsets, (args.steps + nsets - 1) // nsets * nsets)
+    for _ in range(2):
+        for de in sets:
+            de.step()
+    stream.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(steps):
+        sets[i % nsets].step()
+    ev1.record(stream)
+    stream.synchronize()
+    wall = time.perf_counter() - t0
+    step_ms = ev0.elapsed_time(ev1) / steps
+    for de in sets:
+        de.free()
+    units = nval * ninst
+    alg = units * EPOCH_BYTES_PER_VALIDATOR
+    traffic = pmc_traffic(["pz_epoch_*"], workload + "_cold")
+    return {"what": "%d steps rotated over %d distinct %d x %d instance sets (%.1f GB of validator state), one "
+                    "stream" % (steps, nsets, nval, ninst, nsets * units * 24 / 1e9),
+            "value": units * steps / wall, "unit": "validator-epochs/s", "step_device_ms": step_ms,
+            "frac": alg / (step_ms * 1e-3) / HBM_PEAK,
+            "traffic": traffic, "traffic_source": pmc_summary_path(workload + "_cold") if traffic else None,
+            "traffic_frac": (traffic / (step_ms * 1e-3) / HBM_PEAK) if traffic else None}
 
 
 def epoch_parity(inst, dev):
@@ -291,27 +335,50 @@ def epoch_parity(inst, dev):
 
 
 def epoch_single_instance(args, torch, dev, nval, shuffled):
-    """the latency of ONE epoch instance (B = 1) at configs[2]'s size,
-    launch-bound at this size (2.9 MB of algorithmic traffic); device time by HIP events."""
-    from prysm_amd import synth
+    """the latency of ONE epoch instance (B = 1) at configs[2]'s size
+    (2.9 MB of algorithmic traffic): the single-launch step (pz_epoch_one_kernel), device time
+    by HIP events, median over the steps; beside it the three-launch step (pre + fused + mid)
+    on the same instance."""
+    from prysm_amd import _lib, synth
     from prysm_amd.native import NativeEpoch
 
-    de = NativeEpoch(synth.epoch_batch(nval, 1, seed=3, shuffled=shuffled), device=dev.index)
-    stream = torch.cuda.ExternalStream(de.shard(0)[3], device=dev)
-    for _ in range(args.warmup + 20):
-        de.step()
-    stream.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for e0, e1 in evs:
-        e0.record(stream)
-        de.step()
-        e1.record(stream)
-    stream.synchronize()
-    wall = time.perf_counter() - t0
-    ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in evs]))
-    return {"validators": nval, "instances_per_step": 1, "device_ms_median": ms,
-            "wall_ms_per_step": wall / args.steps * 1e3, "validator_epochs_per_s": nval / (ms * 1e-3)}
+    def measure():
+        de = NativeEpoch(synth.epoch_batch(nval, 1, seed=3, shuffled=shuffled), device=dev.index)
+        stream = torch.cuda.ExternalStream(de.shard(0)[3], device=dev)
+        for _ in range(args.warmup + 20):
+            de.step()
+        stream.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(max(args.steps, 20))]
+        t0 = time.perf_counter()
+        for e0, e1 in evs:
+            e0.record(stream)
+            de.step()
+            e1.record(stream)
+        stream.synchronize()
+        wall = time.perf_counter() - t0
+        # back to back: one event pair around K steps (each step's launch overhead hidden
+        # behind the previous step, as a node stepping epochs in a row would see it)
+        b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        b0.record(stream)
+        for _ in range(len(evs)):
+            de.step()
+        b1.record(stream)
+        stream.synchronize()
+        de.free()
+        return (float(np.median([e0.elapsed_time(e1) for e0, e1 in evs])), wall / len(evs) * 1e3,
+                b0.elapsed_time(b1) / len(evs))
+
+    ms, wall_ms, b2b = measure()
+    old = _lib.lib.dll.pz_debug_set_fused_variant(128)  # the single launch off: pre + fused + mid
+    try:
+        ms3, wall3, b2b3 = measure()
+    finally:
+        _lib.lib.dll.pz_debug_set_fused_variant(old)
+    return {"validators": nval, "instances_per_step": 1, "path": "pz_epoch_one_kernel (single launch)",
+            "device_ms_median": ms, "wall_ms_per_step": wall_ms, "back_to_back_ms_per_step": b2b,
+            "validator_epochs_per_s": nval / (ms * 1e-3),
+            "three_launches": {"device_ms_median": ms3, "wall_ms_per_step": wall3, "back_to_back_ms_per_step": b2b3}}
 
 
 def epoch_cpu_baseline(inst):
@@ -548,6 +615,24 @@ def attcheck_columns(natt, seed):
     return cols, tab
 
 
+def attcheck_batch(torch, dev, cols, tab, natt):
+    """The pz_att_check_batch over device copies of ``attcheck_columns`` (and the tensors it
+    points into, which the caller keeps alive)."""
+    from prysm_amd import _lib
+
+    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v.view(np.int32) if v.dtype == np.uint32
+                             else v).to(dev) for k, v in list(cols.items()) + list(tab.items())}
+    t["status"] = torch.empty(natt, dtype=torch.int32, device=dev)
+    t["committee"] = torch.empty(natt, dtype=torch.int32, device=dev)
+    t["pstart"] = torch.empty(natt, dtype=torch.int64, device=dev)
+    b = _lib.AttCheckBatch(natt, t["slot"].data_ptr(), t["justified_slot"].data_ptr(), t["shard_id"].data_ptr(),
+                           t["n_oblique"].data_ptr(), t["bits"].data_ptr(), t["boffs"].data_ptr(),
+                           t["block_slot"].data_ptr(), 0, 0, 128, 256, t["arr_offs"].data_ptr(),
+                           t["arr_shard"].data_ptr(), t["arr_comm"].data_ptr(), t["coffs"].data_ptr(),
+                           t["status"].data_ptr(), t["committee"].data_ptr(), t["pstart"].data_ptr())
+    return b, t
+
+
 def attcheck_leg(args, torch, dist, dev, rank, world):
     """processAttestation's checks for a batch of 4M attestations on the
     GPU (pz_dev_check_attestations, one lane each); attestations shard over the ranks."""
@@ -555,16 +640,8 @@ def attcheck_leg(args, torch, dist, dev, rank, world):
 
     natt = 1 << 22
     cols, tab = attcheck_columns(natt, seed=11 + rank)
-    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v.view(np.int32) if v.dtype == np.uint32
-                             else v).to(dev) for k, v in list(cols.items()) + list(tab.items())}
-    status = torch.empty(natt, dtype=torch.int32, device=dev)
-    comm = torch.empty(natt, dtype=torch.int32, device=dev)
-    pstart = torch.empty(natt, dtype=torch.int64, device=dev)
-    b = _lib.AttCheckBatch(natt, t["slot"].data_ptr(), t["justified_slot"].data_ptr(), t["shard_id"].data_ptr(),
-                           t["n_oblique"].data_ptr(), t["bits"].data_ptr(), t["boffs"].data_ptr(),
-                           t["block_slot"].data_ptr(), 0, 0, 128, 256, t["arr_offs"].data_ptr(),
-                           t["arr_shard"].data_ptr(), t["arr_comm"].data_ptr(), t["coffs"].data_ptr(),
-                           status.data_ptr(), comm.data_ptr(), pstart.data_ptr())
+    b, t = attcheck_batch(torch, dev, cols, tab, natt)
+    status = t["status"]
     stream = torch.cuda.current_stream(dev)
     sh = ctypes.c_void_p(stream.cuda_stream)
 
@@ -786,22 +863,31 @@ def shuffle_leg(args):
     return out
 
 
-PMC_SUMMARY = os.path.join("profiles", "r02", "pmc_summary.json")
-PMC_SUMMARY_EPOCH_1M = os.path.join("profiles", "r02", "pmc_summary_epoch1m.json")
+PMC_DIR = os.path.join("profiles", "r03")
+PMC_SUMMARY = os.path.join(PMC_DIR, "pmc_main.json")
 
 
-def pmc_traffic(kernels, summary=PMC_SUMMARY):
-    """HBM bytes per launch of ``kernels`` (summed) from the committed rocprofv3 --pmc summary
-    (tools/gpu_pmc.sh + tools/pmc_summary.py: FETCH_SIZE doubled per the gfx950 correction,
-    WRITE_SIZE as is).  PMC counters cannot be read inside this process, so the figure comes
-    from a separate profiled run of the same workload; None if the summary is absent."""
-    path = os.path.join(ROOT, summary)
+def pmc_summary_path(workload):
+    return os.path.join(PMC_DIR, "pmc_%s.json" % workload)
+
+
+def pmc_traffic(kernels, workload="main"):
+    """HBM bytes per launch of ``kernels`` (summed; a name ending in '*' takes every kernel of
+    the workload with that prefix) from the committed rocprofv3 --pmc summary of tools/
+    pmc_workload.py's ``workload`` (tools/gpu_pmc.sh + tools/pmc_summary.py: FETCH_SIZE doubled
+    per the gfx950 correction, WRITE_SIZE as is).  PMC counters cannot be read inside this
+    process, so the figure comes from a separate profiled run of the same workload; None if
+    the summary is absent or lacks a kernel."""
+    path = os.path.join(ROOT, pmc_summary_path(workload))
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
+    names = []
+    for k in kernels:
+        names += sorted(n for n in d if n.startswith(k[:-1])) if k.endswith("*") else [k]
     try:
-        return float(sum(d[k]["hbm_bytes_per_launch"] for k in kernels))
+        return float(sum(d[k]["hbm_bytes_per_launch"] for k in names)) if names else None
     except KeyError:
         return None
 
@@ -859,9 +945,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.launch_selftest:
-        print(json.dumps({"rank": rank, "world": world, "gpus": args.gpus,
-                          "launch": os.environ.get("PZ_BENCH_LAUNCH", "external launcher")}), flush=True)
+    if args.launch_selftest:  # one write(2) per line: lines of concurrent ranks never interleave
+        os.write(1, (json.dumps({"rank": rank, "world": world, "gpus": args.gpus,
+                                 "launch": os.environ.get("PZ_BENCH_LAUNCH", "external launcher")}) + "\n").encode())
         return
     if args.single_process:
         return single_process_main(args)

@@ -488,6 +488,11 @@ int  pz_epoch_state_sync(pz_epoch_state* st);
 /* Local rank `local`'s validator range, device and compute stream (for event timing). */
 int  pz_epoch_state_shard(const pz_epoch_state* st, int local, uint64_t* lo, uint64_t* hi, int* device,
                           void** stream);
+/* From now on local rank `local` enqueues its steps on the caller's hipStream_t `stream` (of
+ * that rank's device; NULL: back to the state's own stream).  Work already enqueued is waited
+ * for first.  Several states bound to one stream step in issue order (e.g. a caller rotating
+ * over state sets larger than the caches, or ordering the step after its own kernels). */
+int  pz_epoch_state_bind_stream(pz_epoch_state* st, int local, void* stream);
 /* After a step (synchronises): the balances of the hi-lo validators local rank `local` holds
  * ([B][hi-lo], in its storage order: pz_epoch_state_validators names them), and the reduced
  * scal [B][PZ_SCAL_COUNT], vote / total [B][natt] and winners [B][nrec] (any may be NULL). */

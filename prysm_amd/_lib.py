@@ -113,6 +113,7 @@ SIGNATURES = {
     "pz_epoch_state_step": [vp],
     "pz_epoch_state_sync": [vp],
     "pz_epoch_state_shard": [vp, ctypes.c_int, c_u64p, c_u64p, c_intp, vp],
+    "pz_epoch_state_bind_stream": [vp, ctypes.c_int, vp],
     "pz_epoch_state_results": [vp, ctypes.c_int, vp, vp, vp, vp, vp],
     "pz_epoch_state_free": [vp],
     "pz_epoch_state_validators": [vp, ctypes.c_int, vp],

@@ -22,6 +22,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -149,21 +150,45 @@ struct Reader {
   }
 };
 
-// One AttestationRecord (messages.proto:110-119), owning its canonical encoding.
+// The oblique parent hashes of one attestation: (offset, length) pairs into its encoding,
+// held in the call arena's pool.
+struct OblSpan {
+  const std::pair<uint32_t, uint32_t>* p = nullptr;
+  uint32_t n = 0;
+  const std::pair<uint32_t, uint32_t>* begin() const { return p; }
+  const std::pair<uint32_t, uint32_t>* end() const { return p + n; }
+  size_t size() const { return n; }
+};
+
+// One AttestationRecord (messages.proto:110-119): its canonical encoding is a span of the call
+// arena's copy of the input blocks, which the record keeps alive (AttP aliases the arena).
 struct Att {
-  std::string enc;
+  const uint8_t* base = nullptr;  // the encoding
+  uint32_t len = 0;
   uint64_t slot = 0, shard = 0, jslot = 0;
   uint32_t sbh_off = 0, sbh_len = 0, bf_off = 0, bf_len = 0;
-  std::vector<std::pair<uint32_t, uint32_t>> obl;  // (offset, length) into enc
-  const uint8_t* at(uint32_t off) const { return (const uint8_t*)enc.data() + off; }
+  uint32_t obl_first = 0;  // its first pair in the arena pool (OblSpan bound after the parse)
+  OblSpan obl;
+  const uint8_t* at(uint32_t off) const { return base + off; }
 };
 using AttP = std::shared_ptr<const Att>;
 
+// One pz_chain_process_blocks call's input: a copy of its serialized blocks and every
+// attestation record parsed from them, allocated once (per-record allocations made the parse
+// allocator-bound).  Records that stay pending after the call keep it alive.
+struct CallArena {
+  std::vector<uint8_t> bytes;
+  std::vector<Att> atts;  // reserved to the exact count: AttP points into it
+  std::vector<std::pair<uint32_t, uint32_t>> obl;
+};
+
 // messages.pb.go:889-896: 1-3 varint, 4-6 bytes, 7 repeated bytes, 8 packed varints
-static bool parse_att(const uint8_t* p, size_t n, Att* a) {
+static bool parse_att(const uint8_t* p, size_t n, Att* a, std::vector<std::pair<uint32_t, uint32_t>>& pool) {
   static const uint32_t kTypes[9] = {9, 0, 0, 0, 2, 2, 2, 2, 2};
-  a->enc.assign((const char*)p, n);
-  const uint8_t* base = (const uint8_t*)a->enc.data();
+  a->base = p;
+  a->len = (uint32_t)n;
+  a->obl_first = (uint32_t)pool.size();
+  const uint8_t* base = p;
   Reader r{base, base + n};
   uint32_t prev = 0, f, wt;
   const uint8_t* q;
@@ -182,7 +207,8 @@ static bool parse_att(const uint8_t* p, size_t n, Att* a) {
       if (f == 5) { a->sbh_off = (uint32_t)(q - base); a->sbh_len = (uint32_t)len; }
       if (f == 6) { a->bf_off = (uint32_t)(q - base); a->bf_len = (uint32_t)len; }
     } else if (f == 7) {
-      a->obl.push_back({(uint32_t)(q - base), (uint32_t)len});
+      pool.push_back({(uint32_t)(q - base), (uint32_t)len});
+      ++a->obl.n;
     } else {  // f == 8: packed, never empty
       if (!len) return false;
       Reader s{q, q + len};
@@ -202,7 +228,7 @@ struct Block {
 };
 
 // messages.pb.go:224-232: 1 bytes, 2 varint, 3-6 bytes, 7 Timestamp, 8 repeated records
-static bool parse_block(const uint8_t* p, size_t n, Block* b) {
+static bool parse_block(const uint8_t* p, size_t n, Block* b, const std::shared_ptr<CallArena>& ar) {
   static const uint32_t kTypes[9] = {9, 2, 0, 2, 2, 2, 2, 2, 2};
   static const uint32_t kTsTypes[3] = {9, 0, 0};
   b->data = p;
@@ -234,9 +260,11 @@ static bool parse_block(const uint8_t* p, size_t n, Block* b) {
       }
       if (!t.ok) return false;
     } else {  // f == 8
-      auto a = std::make_shared<Att>();
-      if (!parse_att(q, len, a.get())) return false;
-      b->atts.push_back(a);
+      if (ar->atts.size() == ar->atts.capacity()) return false;  // more records than counted
+      ar->atts.emplace_back();
+      Att* a = &ar->atts.back();
+      if (!parse_att(q, len, a, ar->obl)) return false;
+      b->atts.push_back(AttP(ar, a));  // aliases the arena: no allocation per record
     }
   }
   return r.ok;
@@ -373,6 +401,18 @@ struct Engine {
   DevArr<uint8_t> e_pack;    // one H2D per transition: bitfields, offsets, committees, ...
   PinBuf e_pin, e_pin_out;   // its pinned staging; the results' pinned landing (scal, winners)
   PinBuf tot_pin;            // the vote totals the justification loop reads
+  hipEvent_t ev_totals = nullptr;  // the tally flush + totals D2H of a transition are done
+  hipEvent_t ev_epoch = nullptr;   // the last enqueued epoch's results have landed
+  // The epoch of the last transition, enqueued but not yet collected: its results (the
+  // crosslink records, the next state's TotalDeposits, a panic) are first needed at the next
+  // transition or by the state bytes/roots, so the walk never waits for it.
+  struct DeferredEpoch {
+    bool live = false;
+    std::vector<AttP> pending;  // the attestations it ran over (a winner's ShardBlockHash)
+    std::shared_ptr<CState> src, dst;  // the state it read (xl mutated in place), the new state
+    uint64_t block_slot = 0;
+    size_t nrec = 0;
+  } deferred;
   // hashing scratch
   PinBuf pin_msgs, pin_offs, pin_dig;  // pinned staging of the digest batch
   DevArr<uint8_t> h_in, h_out;
@@ -718,15 +758,9 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, std::
   if (g.q_comm.size() >= kFlushAtts) flush_votes_enqueue(g);  // bounds the queue; no host wait
 }
 
-// processCrosslinks + CalculateRewards + next-cycle balance on the device -> next balance.
-// Host staging of one device epoch; lives until the stream sync after epoch_enqueue.
-struct EpochJob {
-  std::vector<uint32_t> win;
-  size_t nrec = 0;
-  uint64_t scal[kScal] = {};
-};
-
-static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending, EpochJob& J) {
+// processCrosslinks + CalculateRewards + next-cycle balance on the device: enqueued, its
+// results landing in pinned memory behind g.ev_epoch (collected by epoch_collect).
+static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending) {
   const size_t na = pending.size();
   std::vector<Crosslink>& xl = *C.xl;
   const size_t nrec = xl.size();
@@ -760,7 +794,7 @@ static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending
   uint64_t* small = reinterpret_cast<uint64_t*>(h + o_small);
   small[0] = C.dynasty;
   small[1] = C.tdep;
-  // the previous transition's copies finished at its sync, so the staging is free
+  // the previous epoch was collected (its event completed), so the staging is free
   check(g.e_pack.alloc(total));
   hchk(hipMemcpyAsync(g.e_pack.p, h, total, hipMemcpyHostToDevice, g.s), "H2D epoch");
   check(g.e_scal.alloc(kScal));
@@ -801,49 +835,59 @@ static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending
   hchk(launch_epoch_count(a, true, true, true, g.s), "epoch count");
   hchk(launch_epoch_mid(a, a.nrec > 0 && na > 0, true, g.s), "epoch mid");
   hchk(launch_epoch_reward(a, g.s), "epoch reward");
-  check(g.e_pin_out.reserve(sizeof J.scal + nrec * 4 + 16));
-  hchk(hipMemcpyAsync(g.e_pin_out.p, g.e_scal.p, sizeof J.scal, hipMemcpyDeviceToHost, g.s), "D2H");
+  check(g.e_pin_out.reserve(kScal * 8 + nrec * 4 + 16));
+  hchk(hipMemcpyAsync(g.e_pin_out.p, g.e_scal.p, kScal * 8, hipMemcpyDeviceToHost, g.s), "D2H");
   if (nrec)
-    hchk(hipMemcpyAsync(g.e_pin_out.p + sizeof J.scal, g.e_win.p, nrec * 4, hipMemcpyDeviceToHost, g.s), "D2H");
-  J.nrec = nrec;
+    hchk(hipMemcpyAsync(g.e_pin_out.p + kScal * 8, g.e_win.p, nrec * 4, hipMemcpyDeviceToHost, g.s), "D2H");
+  if (!g.ev_epoch) hchk(hipEventCreateWithFlags(&g.ev_epoch, hipEventDisableTiming), "event");
+  hchk(hipEventRecord(g.ev_epoch, g.s), "event");
+  g.deferred.nrec = nrec;
 }
 
-// After the stream sync: the epoch results out of their pinned landing.
-static void epoch_collect(Engine& g, EpochJob& J) {
-  std::memcpy(J.scal, g.e_pin_out.p, sizeof J.scal);
-  J.win.resize(J.nrec);
-  if (J.nrec) std::memcpy(J.win.data(), g.e_pin_out.p + sizeof J.scal, J.nrec * 4);
-}
-
-// After the sync: the reference's panics, the crosslink winners, the next-cycle balance.
-static uint64_t epoch_finish(Engine& g, CState& C, const std::vector<AttP>& pending, uint64_t block_slot,
-                             const EpochJob& J) {
-  const size_t na = pending.size();
+// The deferred epoch's results, once its event has completed: the reference's panics, the
+// crosslink winners (core.go:549-555) and the next-cycle balance (TotalDeposits of the state
+// it built).  Called before anything reads them: the next transition, the state bytes, the
+// roots, and the end of every pz_chain_process_blocks call (so a panic fails that call).
+static void epoch_collect(Engine& g) {
+  Engine::DeferredEpoch& D = g.deferred;
+  if (!D.live) return;
+  D.live = false;
+  hchk(hipEventSynchronize(g.ev_epoch), "event sync (epoch)");
+  uint64_t scal[kScal];
+  std::memcpy(scal, g.e_pin_out.p, sizeof scal);
+  const uint32_t* win = reinterpret_cast<const uint32_t*>(g.e_pin_out.p + sizeof scal);
+  std::vector<AttP> pending;
+  pending.swap(D.pending);
+  CState& C = *D.src;
   std::vector<Crosslink>& xl = *C.xl;
-  const uint64_t* scal = J.scal;
-  const std::vector<uint32_t>& win = J.win;
   if (scal[kErrXl]) throw Panic{"processCrosslinks: index out of range (committee member, bitfield or shard)"};
   const uint64_t dep = scal[kPop] * PZ_DEFAULT_BALANCE;
   const bool thr = dep * 3ull >= C.tdep * 2ull;
   if (thr && scal[kNact] > 0 && scal[kErrRwd]) throw Panic{"CalculateRewards: CheckBit index out of range (incentives.go:23)"};
-  if (na && !xl.empty()) {
-    for (size_t s = 0; s < xl.size(); ++s) {
+  if (!pending.empty() && !xl.empty()) {
+    for (size_t s = 0; s < xl.size() && s < D.nrec; ++s) {
       if (win[s] == 0xffffffffu) continue;
       const Att& w = *pending[win[s]];
       xl[s].dynasty = C.dynasty;
       xl[s].hash.assign((const char*)w.at(w.sbh_off), w.sbh_len);
-      xl[s].slot = block_slot;
+      xl[s].slot = D.block_slot;
     }
   }
   if (scal[kApplied]) g.val_enc_valid = false;
-  return scal[kNextBal];
+  D.dst->tdep = scal[kNextBal];
+  D.src.reset();
+  D.dst.reset();
 }
 
 // stateRecalc (core.go:398-497) -> (new C, new A).
 static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slot, CP* nc_out, AP* na_out) {
-  // One stream sync for the whole transition: the pending vote tallies, the D2H of the
-  // totals the justification loop reads, and the device epoch (processCrosslinks,
-  // CalculateRewards, next balance; independent of the justification) are all enqueued first.
+  // The previous transition's epoch first: this one reads the crosslink records and the
+  // TotalDeposits it produced (long since done: 64 blocks of walk have passed).
+  epoch_collect(g);
+  // The host waits only for what the justification loop reads (core.go:411-431): the pending
+  // vote tallies and the D2H of their totals.  The device epoch (processCrosslinks,
+  // CalculateRewards, next balance) does not depend on it and is enqueued behind them, to be
+  // collected at the next transition; the stream orders every later tally after its rewards.
   flush_votes_enqueue(g);
   flush_err_enqueue(g);
   PhaseTimer pt(g.prof[kProfRecalc]);
@@ -855,11 +899,17 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
     check(g.tot_pin.reserve(nslots * 8));
     hchk(hipMemcpyAsync(g.tot_pin.p, g.totals.p, nslots * 8, hipMemcpyDeviceToHost, g.s), "D2H");
   }
-  EpochJob job;
-  epoch_enqueue(g, *C, A->pending, job);
-  hchk(hipStreamSynchronize(g.s), "sync");
+  if (!g.ev_totals) hchk(hipEventCreateWithFlags(&g.ev_totals, hipEventDisableTiming), "event");
+  hchk(hipEventRecord(g.ev_totals, g.s), "event");
+  epoch_enqueue(g, *C, A->pending);
+  auto nc = std::make_shared<CState>();
+  g.deferred.live = true;
+  g.deferred.pending = A->pending;
+  g.deferred.src = C;
+  g.deferred.dst = nc;
+  g.deferred.block_slot = block_slot;
+  hchk(hipEventSynchronize(g.ev_totals), "event sync (vote totals)");
   flush_votes_finish(g);
-  epoch_collect(g, job);
   if (nslots) {
     const uint64_t* all = reinterpret_cast<const uint64_t*>(g.tot_pin.p);
     for (uint64_t i = 0; i < kCycle && i < A->recent.size(); ++i) {
@@ -877,8 +927,6 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
     }
     if (streak >= kCycle + 1 && slot - kCycle > finalized) finalized = slot - kCycle;
   }
-  const uint64_t nxt = epoch_finish(g, *C, A->pending, block_slot, job);
-  auto nc = std::make_shared<CState>();
   nc->lsr = lsr + kCycle;
   nc->jslot = justified;
   nc->streak = streak;
@@ -886,7 +934,7 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   nc->start_shard = 0;
   nc->dynasty = 0;  // core.go:467-478 does not set CurrentDynasty
   nc->seed_reset = C->seed_reset;
-  nc->tdep = nxt;
+  nc->tdep = 0;  // the epoch's next-cycle balance, set by epoch_collect
   nc->xl = C->xl;
   auto na = std::make_shared<AState>();
   for (auto& p : A->pending)
@@ -934,7 +982,7 @@ static const std::string& validators_enc(Engine& g) {
 
 static std::string encode_active(const AState& A) {  // messages.proto:94-97
   std::string o;
-  for (auto& p : A.pending) put_msg(o, 1, (const uint8_t*)p->enc.data(), p->enc.size());
+  for (auto& p : A.pending) put_msg(o, 1, p->base, p->len);
   for (auto& h : A.recent) put_msg(o, 2, h.b, A.recent_raw_empty ? 0 : 32);
   return o;
 }
@@ -1214,12 +1262,28 @@ static int reload(Engine& g, const uint8_t* data, uint64_t len) {
 }
 
 // ---- blockProcessing (service.go:238-363) ---------------------------------------------------
-static int parse_all(const uint8_t* data, const uint64_t* offs, uint64_t n, std::vector<Block>& blocks) {
+// Parsed on the calling thread, into one arena per call.  (On host threads, with a heap
+// record per attestation, the parse itself was 2x slower -- the allocator shared by the
+// threads -- and the walk that reads the records 10-20 % slower: records left in other cores'
+// caches; profiles/r03/replay_threads_r3c.txt.)
+static int parse_all(const uint8_t* data, const uint64_t* offs, uint64_t n, uint64_t natt, std::vector<Block>& blocks,
+                     std::shared_ptr<CallArena>* keep) {
+  auto ar = std::make_shared<CallArena>();
+  *keep = ar;  // the blocks' bytes live here for the whole call (records alias it beyond)
+  for (uint64_t i = 0; i < n; ++i)
+    if (offs[i + 1] < offs[i]) return fail(PZ_EINVAL, "block %llu: offsets not monotone", (unsigned long long)i);
+  const uint64_t o0 = n ? offs[0] : 0, total = n ? offs[n] - o0 : 0;
+  ar->bytes.resize(total + 16);
+  if (total) std::memcpy(ar->bytes.data(), data + o0, total);
+  ar->atts.reserve(natt);
+  ar->obl.reserve(natt);
   blocks.resize(n);
+  const uint8_t* base = ar->bytes.data() - o0;
   for (uint64_t i = 0; i < n; ++i) {
-    if (offs[i + 1] < offs[i] || !parse_block(data + offs[i], offs[i + 1] - offs[i], &blocks[i]))
+    if (!parse_block(base + offs[i], offs[i + 1] - offs[i], &blocks[i], ar))
       return fail(PZ_EINVAL, "block %llu is not a canonical BeaconBlock encoding", (unsigned long long)i);
   }
+  for (Att& a : ar->atts) a.obl.p = ar->obl.data() + a.obl_first;  // the pool no longer grows
   return PZ_OK;
 }
 
@@ -1251,13 +1315,13 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
   for (auto& b : blocks) {
     natt += b.atts.size();
     total += b.len;
-    for (auto& a : b.atts) total += a->enc.size() + 10 + a->sbh_len + 32 * a->obl.size();
+    for (auto& a : b.atts) total += a->len + 10 + a->sbh_len + 32 * a->obl.size();
   }
   const uint64_t nmsg = n + 2 * natt, thr = serial_threshold();
   bool any_long = false;
   for (auto& b : blocks) any_long |= b.len >= thr;
   for (auto& b : blocks)
-    for (auto& a : b.atts) any_long |= a->enc.size() >= thr || 10 + a->sbh_len + 32 * a->obl.size() >= thr;
+    for (auto& a : b.atts) any_long |= a->len >= thr || 10 + a->sbh_len + 32 * a->obl.size() >= thr;
   std::vector<uint8_t> dg_slow;
   const uint8_t* dg;
   uint64_t dstride;
@@ -1267,43 +1331,63 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
     check(g.pin_dig.reserve(nmsg * 32));
     uint8_t* buf = g.pin_msgs.p;
     uint64_t* ho = reinterpret_cast<uint64_t*>(g.pin_offs.p);
+    // offsets first (serial, a few adds per message), then the bytes on host threads
+    std::vector<uint64_t> first_att(n + 1, 0);
     uint64_t pos = 0, k = 0;
     ho[k++] = 0;
-    for (auto& b : blocks) {
-      std::memcpy(buf + pos, b.data, b.len);
-      ho[k++] = pos += b.len;
+    for (uint64_t bi = 0; bi < n; ++bi) {
+      ho[k++] = pos += blocks[bi].len;
+      first_att[bi + 1] = first_att[bi] + blocks[bi].atts.size();
     }
     for (auto& b : blocks)
-      for (auto& a : b.atts) {
-        std::memcpy(buf + pos, a->enc.data(), a->enc.size());
-        ho[k++] = pos += a->enc.size();
-      }
+      for (auto& a : b.atts) ho[k++] = pos += a->len;
     for (auto& b : blocks)
-      for (auto& a : b.atts) {  // Key() preimage (types/attestation.go:61-77)
-        uint8_t* q = buf + pos;
-        std::memset(q, 0, 10);
-        uint8_t v[10];
-        size_t vl = 0;
-        for (uint64_t x = a->slot; ; x >>= 7) {
-          v[vl++] = (uint8_t)(x >= 0x80 ? (x & 0x7F) | 0x80 : x);
-          if (x < 0x80) break;
+      for (auto& a : b.atts) ho[k++] = pos += 10 + a->sbh_len + 32 * a->obl.size();
+    auto fill = [&](uint64_t b0, uint64_t b1) {
+      for (uint64_t bi = b0; bi < b1; ++bi) {
+        const Block& b = blocks[bi];
+        std::memcpy(buf + ho[bi], b.data, b.len);
+        for (uint64_t j = 0; j < b.atts.size(); ++j) {
+          const Att& a = *b.atts[j];
+          const uint64_t ga = first_att[bi] + j;
+          std::memcpy(buf + ho[n + ga], a.base, a.len);
+          // Key() preimage (types/attestation.go:61-77): a 10-byte buffer holding
+          // uvarint(slot) overwritten by uvarint(shard), ShardBlockHash, each oblique hash
+          // copied into a [32]byte
+          uint8_t* q = buf + ho[n + natt + ga];
+          std::memset(q, 0, 10);
+          uint8_t v[10];
+          size_t vl = 0;
+          for (uint64_t x = a.slot; ; x >>= 7) {
+            v[vl++] = (uint8_t)(x >= 0x80 ? (x & 0x7F) | 0x80 : x);
+            if (x < 0x80) break;
+          }
+          std::memcpy(q, v, vl);
+          vl = 0;
+          for (uint64_t x = a.shard; ; x >>= 7) {
+            v[vl++] = (uint8_t)(x >= 0x80 ? (x & 0x7F) | 0x80 : x);
+            if (x < 0x80) break;
+          }
+          std::memcpy(q, v, vl);
+          std::memcpy(q + 10, a.at(a.sbh_off), a.sbh_len);
+          uint64_t kl = 10 + a.sbh_len;
+          for (auto& o : a.obl) {
+            const H32 h = copy32(a.at(o.first), o.second);
+            std::memcpy(q + kl, h.b, 32);
+            kl += 32;
+          }
         }
-        std::memcpy(q, v, vl);
-        vl = 0;
-        for (uint64_t x = a->shard; ; x >>= 7) {
-          v[vl++] = (uint8_t)(x >= 0x80 ? (x & 0x7F) | 0x80 : x);
-          if (x < 0x80) break;
-        }
-        std::memcpy(q, v, vl);
-        std::memcpy(q + 10, a->at(a->sbh_off), a->sbh_len);
-        uint64_t kl = 10 + a->sbh_len;
-        for (auto& o : a->obl) {
-          const H32 h = copy32(a->at(o.first), o.second);
-          std::memcpy(q + kl, h.b, 32);
-          kl += 32;
-        }
-        ho[k++] = pos += kl;
       }
+    };
+    const uint64_t T = std::max<uint64_t>(1, std::min<uint64_t>(host_threads(), n / 256));
+    if (T == 1) {
+      fill(0, n);
+    } else {
+      std::vector<std::thread> th;
+      for (uint64_t t = 1; t < T; ++t) th.emplace_back(fill, n * t / T, n * (t + 1) / T);
+      fill(0, n / T);
+      for (auto& x : th) x.join();
+    }
     check(g.h_in.alloc(pos + 16));
     check(g.h_out.alloc(nmsg * 32));
     check(g.h_offs.alloc(nmsg + 1));
@@ -1323,7 +1407,7 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
     }
     for (auto& b : blocks)
       for (auto& a : b.atts) {
-        buf += a->enc;
+        buf.append((const char*)a->base, a->len);
         ho.push_back(buf.size());
       }
     for (auto& b : blocks)
@@ -1459,6 +1543,7 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
   }
   g.prof[kProfWalk] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_walk).count();
   flush_votes(g);
+  epoch_collect(g);  // a panic of the last transition's epoch fails this call
   PhaseTimer pt(g.prof[kProfMsgHash]);
   const size_t nm = msg_att.size();
   if (nm) {
@@ -1544,6 +1629,8 @@ void pz_chain_free(pz_chain* c) {
   if (c->g.q_arena) (void)hipHostFree(c->g.q_arena);
   if (c->g.h_err) (void)hipHostFree(c->g.h_err);
   if (c->g.q_arena_ev) (void)hipEventDestroy(c->g.q_arena_ev);
+  if (c->g.ev_totals) (void)hipEventDestroy(c->g.ev_totals);
+  if (c->g.ev_epoch) (void)hipEventDestroy(c->g.ev_epoch);
   hipStream_t s = c->g.s;
   delete c;
   if (s) (void)hipStreamDestroy(s);
@@ -1585,10 +1672,11 @@ int pz_chain_process_blocks(pz_chain* c, const uint8_t* blocks, const uint64_t* 
   if (natt > att_cap || (natt && !att_out)) return fail(PZ_EINVAL, "att_out holds %llu results, need %llu",
                                                         (unsigned long long)att_cap, (unsigned long long)natt);
   std::vector<Block> parsed;
+  std::shared_ptr<CallArena> arena;
   int rc;
   {
     PhaseTimer pt(c->g.prof[kProfParse]);
-    rc = parse_all(blocks, offsets, n, parsed);  // before any state changes
+    rc = parse_all(blocks, offsets, n, natt, parsed, &arena);  // before any state changes
   }
   if (rc) return rc;
   try {
@@ -1610,6 +1698,7 @@ int pz_chain_roots(pz_chain* c, uint8_t out[4 * 32], int* has_candidate) {
   Engine& g = c->g;
   try {
     hchk(hipSetDevice(g.device), "hipSetDevice");
+    epoch_collect(g);
     std::string buf;
     std::vector<uint64_t> offs{0};
     buf += encode_active(*g.A);
@@ -1627,6 +1716,9 @@ int pz_chain_roots(pz_chain* c, uint8_t out[4 * 32], int* has_candidate) {
     std::memset(out, 0, 4 * 32);
     for (size_t i = 0; i + 1 < offs.size(); ++i) std::memcpy(out + 32 * i, &d[64 * i], 32);
     if (has_candidate) *has_candidate = g.has_cand ? 1 : 0;
+  } catch (Panic& p) {  // the last transition's epoch, collected here
+    g.poisoned = true;
+    return fail(PZ_EINDEX, "the reference panics here: %s", p.what.c_str());
   } catch (int rc) {
     return rc;
   }
@@ -1641,10 +1733,14 @@ int pz_chain_state_bytes(pz_chain* c, int which, uint8_t* out, uint64_t cap, uin
   if (which >= 2 && !g.has_cand) return fail(PZ_EINVAL, "no candidate state");
   try {
     hchk(hipSetDevice(g.device), "hipSetDevice");
+    epoch_collect(g);
     const std::string b = (which & 1) ? encode_crystallized(g, which >= 2 ? *g.cand_C : *g.C)
                                       : encode_active(which >= 2 ? *g.cand_A : *g.A);
     *len = b.size();
     if (out && cap >= b.size()) std::memcpy(out, b.data(), b.size());
+  } catch (Panic& p) {
+    g.poisoned = true;
+    return fail(PZ_EINDEX, "the reference panics here: %s", p.what.c_str());
   } catch (int rc) {
     return rc;
   }

@@ -89,10 +89,27 @@ struct FusedArgs {
                               //   through LDS when the last bitfield fits kLastCoMaxBytes
   int own_only;               // sharded: winners proposed only for the attestations whose
                               //    committee this rank holds (pz_epoch_fwin_kernel)
+  // single-launch step (one instance, one rank: the latency path, pz_epoch_one_kernel)
+  int one;                    // 1: launch_epoch_one replaces pre + fused + mid
+  uint32_t* ticket;           // blocks done this step (the last one forms the winners; reset by it)
+  uint64_t* vote_next;        // [natt] the next step's tallies, zeroed by this step's last block
+  uint64_t* total_next;
+  const uint32_t* att_csize;  // [natt] the size of each attestation's committee (a layout of the
+                              //   inputs made at upload, so the length check needs no coffs hop)
 };
+// The single-launch step's limits: every block counts the instance's bitfields itself and the
+// last block keeps one LDS word per crosslink record.
+constexpr uint64_t kOneMaxBitBytes = 32768;
+constexpr uint32_t kOneMaxAtt = 2048;
+constexpr uint32_t kOneMaxRec = 4096;
 hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_epoch_fwin(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
+// One instance, one rank, in ONE launch (f.one): every block counts the bitfields and checks
+// their lengths itself (no pre pass), streams its committee pieces as `fused` does, and the
+// last block to finish (an arrival ticket) forms the winners in LDS (no mid pass).
+hipError_t launch_epoch_one(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
+bool epoch_one_enabled(const FusedArgs& f);  // f.one and no tools/ ablation selected
 bool fused_ok(const EpochArgs& a);  // 16-B vector path available (16-B aligned validator rows)
 int set_fused_variant(int v);       // tools/ A/B only (pz_debug_set_fused_variant)
 

@@ -889,6 +889,12 @@ __device__ __forceinline__ uint4 ld16_nt(const uint64_t* p) {
   return make_uint4(x.x, x.y, x.z, x.w);
 }
 
+__device__ __forceinline__ void fused_block_end(const EpochArgs& a, const FusedArgs& f, const uint32_t* xg,
+                                                const uint64_t* xt, const uint64_t* xv, const uint64_t* xs,
+                                                const uint64_t* xn, uint64_t inst, uint64_t grp, int lane,
+                                                bool skip, bool applied, uint64_t pop, uint64_t ferr, bool rwd_err);
+__device__ __forceinline__ void one_tail(const EpochArgs& a, const FusedArgs& f, int tid);
+
 template <int MODE>
 __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro,
                                            const uint64_t* __restrict__ boffs_ro, const uint64_t* __restrict__ tdep_ro,
@@ -899,18 +905,48 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
   // per wave: {attestation of its committee (single-attestation committees), total, vote, next sum, nomatch}
   __shared__ uint64_t xt[kFusedWaves], xv[kFusedWaves], xs[kFusedWaves], xn[kFusedWaves];
   __shared__ uint32_t xg[kFusedWaves];
+  constexpr bool ONE = (MODE & 512) != 0;  // single-launch step (launch_epoch_one)
   const uint64_t inst = (MODE & 32) ? blockIdx.y : blockIdx.x;
   const uint64_t grp = (MODE & 32) ? blockIdx.x : blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint64_t item = grp * kFusedWaves + wave;
-  const uint64_t pop = pre_ro[inst * kPre], ferr = pre_ro[inst * kPre + 1];
+  uint64_t pop = 0, ferr = 0;
+  if (!ONE) {
+    pop = pre_ro[inst * kPre];
+    ferr = pre_ro[inst * kPre + 1];
+  }
   const uint64_t lb = boffs_ro[inst * a.natt + a.natt - 1];
   const uint64_t L = boffs_ro[inst * a.natt + a.natt] - lb;
-  const bool thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (tdep_ro[inst] * 2ull);  // incentives.go:18-20
   const bool rwd_err = (a.nval_global - 1) >= 8 * L;  // CheckBit(last, N-1) panics (incentives.go:23)
-  const bool skip = ferr != 0 || (thr && rwd_err);     // Go panics: balances stay untouched
-  const bool applied = thr && !skip;
+  bool thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (tdep_ro[inst] * 2ull);  // incentives.go:18-20
+  bool skip = ferr != 0 || (thr && rwd_err);     // Go panics: balances stay untouched
+  bool applied = thr && !skip;
+  // ONE: this block's own bit count (GetAttestersTotalDeposit, validator.go:93-102) and
+  // bitfield-length checks (core.go:538-541) over the whole instance, issued before the stream
+  constexpr int kOneLoads = ONE ? (int)((kOneMaxBitBytes + 16) / (16 * 64 * kFusedWaves)) + 1 : 1;
+  constexpr int kOneAtts = ONE ? (int)(kOneMaxAtt / (64 * kFusedWaves)) : 1;
+  uint4 pq[kOneLoads];
+  uint32_t ocs[kOneAtts];
+  uint64_t ob0[kOneAtts], ob1[kOneAtts];
+  // ONE: the instance's bitfield bytes [pbase, pend), staged in LDS by the loads above; the
+  // reward bits are then looked up there (the last bitfield is the region's tail)
+  __shared__ uint4 lbits[ONE ? kOneLoads * 64 * kFusedWaves : 1];
+  const uint64_t pbeg = ONE ? boffs_ro[0] : 0, pend = ONE ? boffs_ro[a.natt] : 0, pbase = pbeg & ~15ull;
+  if (ONE) {
+#pragma unroll
+    for (int k = 0; k < kOneLoads; ++k) {  // branch-free: the bitfield buffer is padded by 16 B
+      const uint64_t u = pbase + 16ull * ((uint64_t)k * 64 * kFusedWaves + tid);
+      pq[k] = *reinterpret_cast<const uint4*>(a.bits + (u < pend ? u : pbase));
+    }
+#pragma unroll
+    for (int k = 0; k < kOneAtts; ++k) {
+      const uint64_t g = (uint64_t)k * 64 * kFusedWaves + tid, gc = g < a.natt ? g : 0;
+      ocs[k] = f.att_csize[gc];
+      ob0[k] = boffs_ro[gc];
+      ob1[k] = boffs_ro[gc + 1];
+    }
+  }
   uint64_t sum = 0, nm = 0, ts = 0, vs = 0;
   uint32_t g1 = kNoAtt;  // the wave's single attestation, combined across the block below
   // every wave runs the body (a wave without a piece has no element in range)
@@ -962,6 +998,51 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
         by1[j] = a.bits[ci.boff + ((q + 1 < last ? q + 1 : last) >> 3)];
       }
     }
+    if (ONE) {  // the block's bit count and length checks -> threshold (no other block involved)
+      __shared__ uint64_t xp[kFusedWaves], xe[kFusedWaves];
+      uint64_t c = 0, e = 0;
+#pragma unroll
+      for (int k = 0; k < kOneLoads; ++k) {
+        const uint64_t u = pbase + 16ull * ((uint64_t)k * 64 * kFusedWaves + tid);
+        if (u + 16 <= pbeg || u >= pend) continue;
+        const uint32_t w[4] = {pq[k].x, pq[k].y, pq[k].z, pq[k].w};
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {  // bytes of [pbeg, pend) only
+          uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const uint64_t at = u + 4 * d + b;
+            if (at < pbeg || at >= pend) m &= ~(0xFFu << (8 * b));
+          }
+          c += __popc(w[d] & m);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kOneAtts; ++k) {
+        const uint64_t g = (uint64_t)k * 64 * kFusedWaves + tid;
+        if (g < a.natt && ocs[k] > 8 * (ob1[k] - ob0[k])) e = 1;
+      }
+#pragma unroll
+      for (int k = 0; k < kOneLoads; ++k) lbits[k * 64 * kFusedWaves + tid] = pq[k];
+      c = wave_sum(c);
+      e = wave_sum(e);
+      if (lane == 0) {
+        xp[wave] = c;
+        xe[wave] = e;
+      }
+      __syncthreads();
+      uint64_t pc = 0, pe = 0;
+#pragma unroll
+      for (int w = 0; w < kFusedWaves; ++w) {
+        pc += xp[w];
+        pe += xe[w];
+      }
+      pop = pc;
+      ferr = pe ? (uint64_t)kErrBitfield : 0;
+      thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (tdep_ro[inst] * 2ull);
+      skip = ferr != 0 || (thr && rwd_err);
+      applied = thr && !skip;
+    }
     // crosslink tallies on the pre-reward balances (core.go:533-545): position g of the
     // committee is bit g - cb of each of its attestations' bitfields
     if (!(MODE & 1) && ci.ga != kNoAtt) {
@@ -1006,7 +1087,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     }
     // classify (validator.go:45-53), reward (incentives.go:22-27), store, sum (core.go:459-464)
     const uint64_t d = a.dynasty[inst];
-    const uint8_t* lastbf = a.bits + lb;
+    const uint8_t* lastbf = ONE ? reinterpret_cast<const uint8_t*>(lbits) + (lb - pbase) : a.bits + lb;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const uint64_t p = p0 + (uint64_t)j * 128 + 2 * lane;
@@ -1047,7 +1128,16 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     xn[wave] = nm;
   }
   __syncthreads();
-  if (wave != 0) return;
+  if (!ONE && wave != 0) return;
+  if (wave == 0) fused_block_end(a, f, xg, xt, xv, xs, xn, inst, grp, lane, skip, applied, pop, ferr, rwd_err);
+  if (ONE) one_tail(a, f, tid);
+}
+
+// Wave 0 of a fused block: the block's tallies, next-cycle sum and per-instance scalars.
+__device__ __forceinline__ void fused_block_end(const EpochArgs& a, const FusedArgs& f, const uint32_t* xg,
+                                                const uint64_t* xt, const uint64_t* xv, const uint64_t* xs,
+                                                const uint64_t* xn, uint64_t inst, uint64_t grp, int lane,
+                                                bool skip, bool applied, uint64_t pop, uint64_t ferr, bool rwd_err) {
   // Wave 0 adds the block's tallies: consecutive pieces of one committee are merged, and one
   // atomic instruction carries every total (lanes 0-7) and vote (lanes 8-15).
   if (lane < 2 * kFusedWaves) {
@@ -1087,6 +1177,42 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
   }
 }
 
+// ONE: the arrival ticket, and in the last block to arrive the crosslink winners of the one
+// instance (core.go:549-555: the first attestation, in order, whose 3*vote >= 2*total and whose
+// dynasty beats the shard's record), formed in LDS from the complete tallies.  Hand-off
+// (MI355X_MICROARCH.md, the table's first row): every wave drains its tally atomics
+// (s_waitcnt vmcnt(0)) before the block barrier, one lane adds to ONE counter, the block whose
+// add returns the last count reads the tallies with agent-scope (sc1) loads; the tallies are
+// only ever written by agent-scope atomics and sc1 stores, so no L2 holds a stale copy.
+__device__ __forceinline__ void one_tail(const EpochArgs& a, const FusedArgs& f, int tid) {
+  __shared__ uint32_t last, wl[kOneMaxRec];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t t = __hip_atomic_fetch_add(f.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x * gridDim.y - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!last) return;
+  const int nt = (int)blockDim.x;
+  for (uint32_t r = tid; r < a.nrec; r += nt) wl[r] = 0xFFFFFFFFu;
+  __syncthreads();
+  const uint64_t d = a.dynasty[0];
+  for (uint32_t g = tid; g < a.natt; g += nt) {
+    const uint64_t v = __hip_atomic_load(&a.vote[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t t = __hip_atomic_load(&a.total[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t shard = a.att_shard[g];  // < nrec: the host takes the one-pass step only then
+    if (3ull * v >= 2ull * t && d > a.rec_dynasty[shard]) atomicMin(&wl[shard], g);
+  }
+  for (uint32_t g = tid; g < a.natt; g += nt) {  // the next step's tallies start from zero
+    __hip_atomic_store(&f.vote_next[g], (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&f.total_next[g], (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  for (uint32_t r = tid; r < a.nrec; r += nt) a.winner[r] = wl[r];
+  if (tid == 0) __hip_atomic_store(f.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 #define PZ_FUSED_KERNEL(NAME, MODE)                                                                       \
   extern "C" __global__ void __launch_bounds__(64 * kFusedWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) \
   NAME(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro, const uint64_t* __restrict__ boffs_ro, \
@@ -1108,6 +1234,16 @@ PZ_FUSED_KERNEL(pz_epoch_fused_dbg16_kernel, 16)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg32_kernel, 32)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg48_kernel, 48)
 #undef PZ_FUSED_KERNEL
+
+// The single-launch step (one instance): no occupancy target (a few dozen blocks), so the
+// bit-count loads the prologue holds do not spill.
+extern "C" __global__ void __launch_bounds__(64 * kFusedWaves)
+pz_epoch_one_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ boffs_ro,
+                    const uint64_t* __restrict__ tdep_ro, const uint4* __restrict__ items_ro,
+                    const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,
+                    const uint32_t* __restrict__ catt_ro) {
+  fused_body<512>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
+}
 
 static int g_fused_variant = 0;  // tools/ A/B only
 int set_fused_variant(int v) {
@@ -1261,6 +1397,15 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream
         PZ_LAUNCH_FUSED(pz_epoch_fused_kernel);
   }
 #undef PZ_LAUNCH_FUSED
+  return hipGetLastError();
+}
+
+bool epoch_one_enabled(const FusedArgs& f) { return f.one && g_fused_variant == 0; }
+
+hipError_t launch_epoch_one(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
+  const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
+  hipLaunchKernelGGL(pz_epoch_one_kernel, dim3(1, (uint32_t)groups), dim3(64 * kFusedWaves), 0, s, a, f, a.boffs,
+                     a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt);
   return hipGetLastError();
 }
 

@@ -47,7 +47,8 @@ struct Part {
 
 struct Shard {
   int dev = 0, grank = 0;
-  hipStream_t s = nullptr;
+  hipStream_t s = nullptr;    // where steps are enqueued: own, or a caller's (bind_stream)
+  hipStream_t own = nullptr;  // created and destroyed by the state
   uint64_t lo = 0, hi = 0, n = 0, wl = 0;
   uint64_t np = 0;  // row stride of the validator arrays: n, or n rounded up to even for the
                     // one-pass step (its 16-B pairs start at even local indices of every row)
@@ -125,6 +126,11 @@ int step_world1(pz_epoch_state* st) {
     (void)hipSetDevice(s.dev);
     for (uint32_t p = 0; p < st->nparts; ++p) {
       EpochArgs& a = s.part[p].a;
+      if (st->fused && epoch_one_enabled(s.part[p].f)) {  // one instance: the single-launch step
+        hipError_t e = launch_epoch_one(a, s.part[p].f, s.s);
+        if (e != hipSuccess) return hip_fail(e, "epoch step (single launch)");
+        continue;
+      }
       if (st->fused) {
         hipError_t e = launch_epoch_pre(a, s.part[p].f, s.s);
         if (e == hipSuccess) e = launch_epoch_fused(a, s.part[p].f, s.s);
@@ -155,6 +161,8 @@ void flip(pz_epoch_state* st) {
       const uint64_t pre = Bp * kScal + 2 * Bp * natt;  // after {scal, vote, total}: not all-reduced
       q.f.pre = q.red[q.cur] + pre;
       q.f.pre_next = q.red[q.cur ^ 1] + pre;
+      q.f.vote_next = q.red[q.cur ^ 1] + Bp * kScal;
+      q.f.total_next = q.red[q.cur ^ 1] + Bp * kScal + Bp * natt;
     }
 }
 
@@ -395,13 +403,14 @@ pz_epoch_state::~pz_epoch_state() {
   for (Shard& s : sh) {
     (void)hipSetDevice(s.dev);
     if (s.s) (void)hipStreamSynchronize(s.s);
+    if (s.own && s.own != s.s) (void)hipStreamSynchronize(s.own);
     for (void* p : s.allocs) (void)hipFree(p);
     for (Part& q : s.part) {
       if (q.ev_red) (void)hipEventDestroy(q.ev_red);
       if (q.ev_gather) (void)hipEventDestroy(q.ev_gather);
       if (q.ev_nb) (void)hipEventDestroy(q.ev_nb);
     }
-    if (s.s) (void)hipStreamDestroy(s.s);
+    if (s.own) (void)hipStreamDestroy(s.own);
   }
 }
 
@@ -476,11 +485,12 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
     DeviceCtx* dc;
     if ((rc = device_ctx(s.dev, &dc))) break;
     (void)hipSetDevice(s.dev);
-    hipError_t e = hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking);
+    hipError_t e = hipStreamCreateWithFlags(&s.own, hipStreamNonBlocking);
     if (e != hipSuccess) {
       rc = hip_fail(e, "hipStreamCreate");
       break;
     }
+    s.s = s.own;
     uint64_t *bal, *start, *end, *dyn, *tdep, *boffs = nullptr, *coffs = nullptr, *recd = nullptr;
     uint8_t* bits = nullptr;
     uint32_t *committee = nullptr, *cpos = nullptr, *att_comm = nullptr, *att_shard = nullptr;
@@ -628,6 +638,20 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
           q.f.lcw = (s.np + 31) / 32;
           rc = dalloc(s, &q.f.lastco, (size_t)Bp * q.f.lcw);
         }
+        // one instance on one rank: the single-launch step (latency path), within its limits
+        if (!rc && Bp == 1 && st->world == 1 && st->natt && st->natt <= kOneMaxAtt && st->nrec <= kOneMaxRec &&
+            max_inst_bytes <= kOneMaxBitBytes) {
+          q.f.one = 1;
+          std::vector<uint32_t> cs(st->natt);
+          for (uint64_t g = 0; g < st->natt; ++g) {
+            const uint32_t c = h->att_comm[i0 * st->natt + g];
+            cs[g] = (uint32_t)(h->coffs[c + 1] - h->coffs[c]);
+          }
+          uint32_t* d_cs = nullptr;
+          rc = dalloc(s, &q.f.ticket, 1);
+          if (!rc) rc = upload(s, &d_cs, cs.data(), cs.size());
+          q.f.att_csize = d_cs;
+        }
       }
       q.cur = 1;  // flip() below binds red[0] as the first step's buffer
     }
@@ -677,6 +701,17 @@ int pz_epoch_state_shard(const pz_epoch_state* st, int local, uint64_t* lo, uint
   if (hi) *hi = s.hi;
   if (device) *device = s.dev;
   if (stream) *stream = s.s;
+  return PZ_OK;
+}
+
+int pz_epoch_state_bind_stream(pz_epoch_state* st, int local, void* stream) {
+  if (!st) return fail(PZ_EINVAL, "state is null");
+  if (local < 0 || local >= (int)st->sh.size()) return fail(PZ_EINVAL, "local rank %d of %zu", local, st->sh.size());
+  Shard& s = st->sh[local];
+  (void)hipSetDevice(s.dev);
+  hipError_t e = hipStreamSynchronize(s.s);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize (bind stream)");
+  s.s = stream ? (hipStream_t)stream : s.own;
   return PZ_OK;
 }
 

@@ -5,6 +5,8 @@
 // The AVX2 path keeps the 4x4 state as four row vectors and runs the four column G functions
 // (then the four diagonal ones) as one vector G, re-aligning rows with permute4x64 between the
 // halves of a round; rotr32/24/16 are in-lane shuffles and rotr63 is (x >> 63) | (x + x).
+#include <sched.h>
+#include <cstdlib>
 #include "serial_hash.h"
 
 #include <immintrin.h>
@@ -179,6 +181,20 @@ uint64_t set_serial_threshold(uint64_t bytes) { return g_threshold.exchange(byte
 }  // namespace pz
 
 namespace pz {
+
+unsigned host_threads() {
+  static const unsigned n = [] {
+    if (const char* e = std::getenv("PZ_HOST_THREADS")) {
+      const long v = std::strtol(e, nullptr, 10);
+      if (v >= 1 && v <= 256) return (unsigned)v;
+    }
+    unsigned c = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) c = std::max(1, CPU_COUNT(&set));
+    return std::min(16u, c);
+  }();
+  return n;
+}
 
 std::vector<uint64_t> long_messages(const uint64_t* offsets, uint64_t n) {
   std::vector<uint64_t> w;

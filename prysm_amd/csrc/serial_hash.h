@@ -36,6 +36,11 @@ uint64_t set_serial_threshold(uint64_t bytes);
 uint64_t small_batch_threshold();
 uint64_t set_small_batch_threshold(uint64_t compressions);
 
+// Host threads the library uses for its own parallel host work (block parsing, digest
+// staging, long messages): the CPUs this process may run on, at most 16 (the CPU share of
+// one GPU on the bench hosts); PZ_HOST_THREADS overrides it.
+unsigned host_threads();
+
 // Indices of the messages of a CSR batch that go to the host (length >= threshold).
 std::vector<uint64_t> long_messages(const uint64_t* offsets, uint64_t n);
 

@@ -139,6 +139,12 @@ class NativeEpoch:
     def sync(self):
         lib.call("pz_epoch_state_sync", self.st)
 
+    def bind_stream(self, stream_handle, local=0):
+        """Enqueue local rank ``local``'s steps on the caller's stream (a ``hipStream_t``
+        handle; None: the state's own stream) -- pz_epoch_state_bind_stream."""
+        lib.call("pz_epoch_state_bind_stream", self.st, local,
+                 ctypes.c_void_p(stream_handle) if stream_handle else None)
+
     def shard(self, local=0):
         """(lo, hi, device, stream handle) of local rank ``local``."""
         lo, hi, dev, s = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int(), ctypes.c_void_p()

@@ -71,6 +71,68 @@ def test_native_epoch_single_device(n, B, inactive, layout):
     _check(ne, inst, steps=2)
 
 
+@pytest.mark.parametrize("n", [65536, 4096, 4097, 1000, 130])
+@pytest.mark.parametrize("density", [0.5, 0.75])
+def test_native_epoch_single_launch(n, density):
+    """One instance on one device: the single-launch step (pz_epoch_one_kernel: every block
+    counts the bits itself, the last block to arrive forms the winners), three steps in a row
+    (the ticket and the next step's tallies are reset in-kernel), bit-exact."""
+    inst = _inst(n, 1, False, density=density)
+    ne = NativeEpoch(inst, device=0)
+    assert ne.one_pass
+    _check(ne, inst, steps=3)
+
+
+@pytest.mark.parametrize("case", ["reward_panic", "short_bitfield", "many_atts"])
+def test_native_epoch_single_launch_edges(case):
+    """The single-launch step's panics (CheckBit(last, N-1), a bitfield shorter than its
+    committee: scal flags, balances untouched) and a committee with two attestations (the
+    per-attestation atomics), against the oracle or the three-launch step."""
+    n = 4096
+    inst = _inst(n, 1, False, last_bits=n - 8 if case == "reward_panic" else None)
+    if case == "short_bitfield":
+        bo = inst["boffs"].astype(np.int64)
+        inst["bits"] = np.delete(inst["bits"], int(bo[3]) - 1)
+        bo[3:] -= 1
+        inst["boffs"] = bo.astype(np.uint64)
+    if case == "many_atts":  # the final (N-bit) attestation names committee 0 too
+        inst["att_comm"] = inst["att_comm"].copy()
+        inst["att_comm"][-1] = 0
+    ne = NativeEpoch(inst, device=0)
+    assert ne.one_pass
+    if case == "many_atts":
+        _check(ne, inst, steps=2)
+        return
+    ne.step()
+    bal, scal, vote, total, _ = ne.results()
+    assert scal[0, _lib.SCAL_APPLIED] == 0
+    np.testing.assert_array_equal(bal[0], inst["balance"][0][ne.validators()])
+    if case == "reward_panic":
+        assert scal[0, _lib.SCAL_ERR_RWD] != 0
+    else:
+        assert int(scal[0, _lib.SCAL_ERR_XL]) == 2  # PZ_XLERR_BITFIELD
+
+
+def test_native_epoch_single_launch_matches_three_launches():
+    """A/B: the same instance stepped by the single launch and by pre + fused + mid
+    (pz_debug_set_fused_variant(128) disables the single launch): identical results."""
+    inst = _inst(65536, 1, False)
+    outs = []
+    for v in (0, 128):
+        k = {key: (val.copy() if isinstance(val, np.ndarray) else val) for key, val in inst.items()}
+        old = _lib.lib.dll.pz_debug_set_fused_variant(v)
+        try:
+            ne = NativeEpoch(k, device=0)
+            for _ in range(2):
+                ne.step()
+            outs.append(ne.results())
+            ne.free()
+        finally:
+            _lib.lib.dll.pz_debug_set_fused_variant(old)
+    for x, y in zip(*outs):
+        np.testing.assert_array_equal(x, y)
+
+
 @pytest.mark.parametrize("density", [0.5, 0.75])
 def test_native_epoch_one_pass_threshold(density):
     """Half the bits set: GetAttestersTotalDeposit stays under 2/3 of TotalDeposits, so no

@@ -14,6 +14,9 @@ import os
 import sys
 
 
+MIN_CLOCK_NS = 50_000  # shorter dispatches report no clock (r02 printed 7.4 GHz for a 3 us kernel)
+
+
 def main(d):
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     clk = collections.defaultdict(list)
@@ -28,7 +31,10 @@ def main(d):
             per[kname][cname].append(v)
             if cname == "GRBM_GUI_ACTIVE":
                 t0, t1 = meta[disp]
-                clk[kname].append(v / 8 / max(t1 - t0, 1))  # GHz (sum over 8 XCDs / ns)
+                # GHz (sum over 8 XCDs / ns), only for dispatches long enough that the counter
+                # window (which extends past a short kernel's timestamps) does not dominate
+                if t1 - t0 >= MIN_CLOCK_NS:
+                    clk[kname].append(v / 8 / (t1 - t0))
     out = {}
     for kname, cs in per.items():
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
@@ -41,6 +47,9 @@ def main(d):
             e["hbm_bytes_per_launch"] = e["hbm_read_bytes"] + e["hbm_write_bytes"]
         if clk.get(kname):
             e["effective_clock_GHz"] = sum(clk[kname]) / len(clk[kname])
+        elif "GRBM_GUI_ACTIVE" in avg:
+            e["effective_clock_GHz"] = None
+            e["clock_note"] = "dispatch shorter than %d us: no clock derived" % (MIN_CLOCK_NS // 1000)
         out[kname] = e
     json.dump(out, sys.stdout, indent=1, sort_keys=True)
     print()

@@ -1,7 +1,17 @@
-"""Small fixed workload for rocprofv3 --pmc passes: 3 hash launches (1M x 512 B), 3 epoch
-steps (65,536 validators x 256 instances), 3 validator-span encodings (16.7 M records) and 3
-attestation-check batches (4M) and 3 attestation encodings (1M), the bench's workloads, plus a torch copy as a bandwidth
-yardstick."""
+"""Fixed workloads for rocprofv3 --pmc passes (tools/gpu_pmc.sh), one per summary: the
+summary averages counters per kernel NAME, so workloads that launch the same kernel at
+different shapes or cache states get their own run.
+
+  main           3 launches each of the bench's hash (1M x 512 B), validator-span encode
+                 (16.7 M records), attestation checks (4M) and attestation encode (1M), plus a
+                 134 MB torch copy (the FETCH_SIZE yardstick)
+  epoch65k       3 steps of the bench's configs[2] epoch (65,536 validators x 256 instances)
+  epoch1m        3 steps of configs[3]'s size on one GPU (1,048,576 x 16)
+  epoch65k_cold  the configs[2] step rotated over 4 distinct instance sets (4 x 400 MB, far
+                 above the 256 MiB Infinity Cache): every step reads its set cold from HBM
+  epoch1m_cold   the same at 1,048,576 x 16
+  epoch_single   20 steps of ONE 65,536-validator instance (the single-launch latency path)
+"""
 import ctypes
 import os
 import sys
@@ -14,42 +24,39 @@ import torch  # noqa: E402
 from prysm_amd import _lib, casper, synth  # noqa: E402
 from prysm_amd.native import NativeEpoch  # noqa: E402
 
+DEV = torch.device("cuda", 0)
 
-def epoch_1m():
-    """Only the bench's configs[3]-sized epoch on one GPU (1,048,576 validators x 16
-    instances), 3 steps: its own counter passes, since the summary averages per kernel name."""
-    dev = torch.device("cuda", 0)
-    s = torch.cuda.current_stream(dev)
-    nval, B = 1 << 20, 16
-    inst = synth.epoch_batch(nval, B, seed=3,
-                             shuffled=casper.shuffle_indices(b"A" + bytes(31), np.arange(nval, dtype=np.uint32)))
-    de = NativeEpoch(inst, device=0)  # the bench's path (pz_epoch_state, one-pass step)
-    for _ in range(3):
-        de.step()
-    de.sync()
+
+def _epoch_sets(nval, B, nsets):
+    shuffled = casper.shuffle_indices(b"A" + bytes(31), np.arange(nval, dtype=np.uint32))
+    return [NativeEpoch(synth.epoch_batch(nval, B, seed=3 + k, shuffled=shuffled), device=0) for k in range(nsets)]
+
+
+def epoch(nval, B, nsets, rounds):
+    """The bench's epoch path (pz_epoch_state, one-pass step); with nsets > 1 the steps rotate
+    over the sets on one stream (pz_epoch_state_bind_stream)."""
+    sets = _epoch_sets(nval, B, nsets)
+    s = torch.cuda.Stream(device=DEV)  # a real stream (a null handle means the state's own)
+    for de in sets:
+        de.bind_stream(s.cuda_stream)
+    for _ in range(rounds):
+        for de in sets:
+            de.step()
     torch.cuda.synchronize()
-    print("pmc epoch_1m workload done")
+    for de in sets:
+        de.free()
+    print("pmc epoch workload done: %d x %d, %d set(s), %d round(s)" % (nval, B, nsets, rounds))
 
 
-def main():
-    if len(sys.argv) > 1 and sys.argv[1] == "epoch_1m":
-        return epoch_1m()
-    dev = torch.device("cuda", 0)
-    s = torch.cuda.current_stream(dev)
+def main_workload():
+    s = torch.cuda.current_stream(DEV)
     sh = ctypes.c_void_p(s.cuda_stream)
     n = 1 << 20
-    d_in = torch.from_numpy(synth.attestation_records_512(n, seed=2).reshape(-1)).to(dev)
-    d_out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    d_in = torch.from_numpy(synth.attestation_records_512(n, seed=2).reshape(-1)).to(DEV)
+    d_out = torch.empty(n * 32, dtype=torch.uint8, device=DEV)
     for _ in range(3):
         _lib.lib.call("pz_dev_blake2b512_fixed", d_in.data_ptr(), 512, 512, n, d_out.data_ptr(), 32, sh)
-    nval, B = 65536, 256
-    inst = synth.epoch_batch(nval, B, seed=3,
-                             shuffled=casper.shuffle_indices(b"A" + bytes(31), np.arange(nval, dtype=np.uint32)))
-    de = NativeEpoch(inst, device=0)  # the bench's path (pz_epoch_state, one-pass step)
-    for _ in range(3):
-        de.step()
-    de.sync()
-    x = torch.empty(nval * B, dtype=torch.int64, device=dev)
+    x = torch.empty(1 << 24, dtype=torch.int64, device=DEV)
     y = torch.empty_like(x)
     for _ in range(3):
         x.copy_(y)
@@ -57,45 +64,48 @@ def main():
     import bench  # noqa: E402
     nw = 16 << 20
     rng = np.random.default_rng(7)
-    cols_t = [torch.from_numpy(a.view(np.int64)).to(dev) for a in (
+    cols_t = [torch.from_numpy(a.view(np.int64)).to(DEV) for a in (
         rng.integers(16, 49, size=nw, dtype=np.uint64), np.zeros(nw, np.uint64),
         np.full(nw, 9999999999999999999, np.uint64))]
-    w_out = torch.empty(int(_lib.lib.dll.pz_wire_validators_bound(nw, 0)), dtype=torch.uint8, device=dev)
-    w_scr = torch.empty(int(_lib.lib.dll.pz_wire_scratch_bytes(nw)) // 8, dtype=torch.int64, device=dev)
-    w_tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    w_out = torch.empty(int(_lib.lib.dll.pz_wire_validators_bound(nw, 0)), dtype=torch.uint8, device=DEV)
+    w_scr = torch.empty(int(_lib.lib.dll.pz_wire_scratch_bytes(nw)) // 8, dtype=torch.int64, device=DEV)
+    w_tot = torch.zeros(1, dtype=torch.int64, device=DEV)
     vc = _lib.ValidatorCols(None, None, None, None, None, None, *[t.data_ptr() for t in cols_t])
     for _ in range(3):
         _lib.lib.call("pz_dev_wire_validators", ctypes.byref(vc), nw, 11, w_out.data_ptr(), None, w_scr.data_ptr(),
                       w_tot.data_ptr(), sh)
-    cols, tab = bench.attcheck_columns(1 << 22, seed=11)
-    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v.view(np.int32) if v.dtype == np.uint32
-                             else v).to(dev) for k, v in list(cols.items()) + list(tab.items())}
+    del cols_t, w_out, w_scr
     na = 1 << 22
-    st = torch.empty(na, dtype=torch.int32, device=dev)
-    cm = torch.empty(na, dtype=torch.int32, device=dev)
-    ps = torch.empty(na, dtype=torch.int64, device=dev)
-    b = _lib.AttCheckBatch(na, t["slot"].data_ptr(), t["justified_slot"].data_ptr(), t["shard_id"].data_ptr(),
-                           t["n_oblique"].data_ptr(), t["bits"].data_ptr(), t["boffs"].data_ptr(),
-                           t["block_slot"].data_ptr(), 0, 0, 128, 256, t["arr_offs"].data_ptr(),
-                           t["arr_shard"].data_ptr(), t["arr_comm"].data_ptr(), t["coffs"].data_ptr(),
-                           st.data_ptr(), cm.data_ptr(), ps.data_ptr())
+    cols, tab = bench.attcheck_columns(na, seed=11)
+    b, keep = bench.attcheck_batch(torch, DEV, cols, tab, na)
     for _ in range(3):
         _lib.lib.call("pz_dev_check_attestations", ctypes.byref(b), sh)
+    del keep
     # the bench's wire_att leg: the 1M config-2 records encoded from their columns
     from prysm_amd import wire
     cols = synth.attestation_columns_512(n, seed=2)
-    tc = {k: torch.from_numpy(cols[k].view(np.int64) if cols[k].dtype == np.uint64 else cols[k]).to(dev)
+    tc = {k: torch.from_numpy(cols[k].view(np.int64) if cols[k].dtype == np.uint64 else cols[k]).to(DEV)
           for k in wire.ATT_COLS}
     ac = _lib.AttestationCols(*[tc[k].data_ptr() for k in wire.ATT_COLS])
-    a_out = torch.empty(n * 512 + 16, dtype=torch.uint8, device=dev)
-    a_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    a_scr = torch.empty(int(_lib.lib.dll.pz_wire_attestations_scratch_bytes(n)), dtype=torch.uint8, device=dev)
+    a_out = torch.empty(n * 512 + 16, dtype=torch.uint8, device=DEV)
+    a_offs = torch.empty(n + 1, dtype=torch.int64, device=DEV)
+    a_scr = torch.empty(int(_lib.lib.dll.pz_wire_attestations_scratch_bytes(n)), dtype=torch.uint8, device=DEV)
     for _ in range(3):
         _lib.lib.call("pz_dev_wire_attestations", ctypes.byref(ac), n, 0, a_out.data_ptr(), a_offs.data_ptr(),
                       a_scr.data_ptr(), sh)
     torch.cuda.synchronize()
-    print("pmc workload done")
+    print("pmc main workload done")
+
+
+WORKLOADS = {
+    "main": main_workload,
+    "epoch65k": lambda: epoch(65536, 256, 1, 3),
+    "epoch1m": lambda: epoch(1 << 20, 16, 1, 3),
+    "epoch65k_cold": lambda: epoch(65536, 256, 4, 2),
+    "epoch1m_cold": lambda: epoch(1 << 20, 16, 4, 2),
+    "epoch_single": lambda: epoch(65536, 1, 1, 20),
+}
 
 
 if __name__ == "__main__":
-    main()
+    WORKLOADS[sys.argv[1] if len(sys.argv) > 1 else "main"]()
