@@ -578,7 +578,7 @@ def wire_att_leg(args, torch, dist, dev, rank, world, d_digests):
     return out
 
 
-ATT_BYTES = 65  # per attestation: 5 u64 columns + its boffs entry + the bitfield's last byte + 16 B out
+ATT_BYTES = 65  # per attestation: 5 u64 columns + its boffs entry + the bitfield's last byte (its own column) + 16 B out
 
 
 def attcheck_columns(natt, seed):
@@ -615,11 +615,16 @@ def attcheck_columns(natt, seed):
     return cols, tab
 
 
-def attcheck_batch(torch, dev, cols, tab, natt):
+def attcheck_batch(torch, dev, cols, tab, natt, last_byte=True):
     """The pz_att_check_batch over device copies of ``attcheck_columns`` (and the tensors it
-    points into, which the caller keeps alive)."""
+    points into, which the caller keeps alive).  ``last_byte``: the caller-side column of each
+    bitfield's last byte (bits[boffs[i+1]-1]), so the trailing-bits check reads 1 B per
+    attestation instead of touching every bitfield line."""
     from prysm_amd import _lib
 
+    cols = dict(cols)
+    if last_byte:
+        cols["last_byte"] = cols["bits"][(cols["boffs"][1:].astype(np.int64) - 1) % max(1, cols["bits"].size)]
     t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v.view(np.int32) if v.dtype == np.uint32
                              else v).to(dev) for k, v in list(cols.items()) + list(tab.items())}
     t["status"] = torch.empty(natt, dtype=torch.int32, device=dev)
@@ -629,7 +634,8 @@ def attcheck_batch(torch, dev, cols, tab, natt):
                            t["n_oblique"].data_ptr(), t["bits"].data_ptr(), t["boffs"].data_ptr(),
                            t["block_slot"].data_ptr(), 0, 0, 128, 256, t["arr_offs"].data_ptr(),
                            t["arr_shard"].data_ptr(), t["arr_comm"].data_ptr(), t["coffs"].data_ptr(),
-                           t["status"].data_ptr(), t["committee"].data_ptr(), t["pstart"].data_ptr())
+                           t["status"].data_ptr(), t["committee"].data_ptr(), t["pstart"].data_ptr(),
+                           t["last_byte"].data_ptr() if last_byte else None)
     return b, t
 
 
@@ -710,6 +716,40 @@ def attcheck_leg(args, torch, dist, dev, rank, world):
     return out
 
 
+def replay_sharded_leg(args, torch, dist, dev, rank, world, comm):
+    """BASELINE configs[4] as ONE chain batch-sharded over the N GPUs:
+    every rank replays the same 10,000 blocks (the walk is sequential host work, done by each
+    process), and the device work is split by validator range -- each GPU holds 1/N of the
+    balances, of every vote-cache voter bitmap and of every epoch; a transition all-reduces the
+    64 justification totals and the epoch's partial sums over RCCL (pz_chain_new_comm)."""
+    from prysm_amd import synth
+    from prysm_amd.blockchain import BeaconChain, serialize_blocks
+
+    nval, nb = 65536, args.replay_blocks
+    blocks = synth.chain_blocks(nval, nb, seed=6)
+    data, offs = serialize_blocks(blocks)
+    w_data, w_offs = serialize_blocks(blocks[:min(nb, 130)])
+    BeaconChain(nval, comm=comm).process_serialized(w_data, w_offs)  # warm-up
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    ch = BeaconChain(nval, comm=comm)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    br, ar = ch.process_serialized(data, offs)
+    wall = time.perf_counter() - t0
+    wall = max_over_ranks(wall, torch, dist, dev)
+    roots = ch.roots()
+    out = {"metric": "sync-replay blocks/s (one chain over N GPUs)", "value": nb / wall, "unit": "blocks/s",
+           "ms_per_block": wall / nb * 1e3,
+           "config": {"workload": "the configs[4] chain (10,000 blocks, 65,536 validators) as ONE chain",
+                      "parallelism": "validator-range shard x%d of the vote cache and the epoch; RCCL all-reduce of "
+                                     "the 64 justification totals + the epoch's partial sums per transition" % world},
+           "processed": int((br["status"] == 0).sum()), "transitions": int(br["transition"].sum()),
+           "cand_crystallized_root": roots.get("cand_crystallized", b"").hex()}
+    return out
+
+
 def replay_leg(args, torch, dist, dev, rank, world):
     """BASELINE configs[4]: sync replay of a synthetic 10,000-block chain through the block
     pipeline (blockchain/service.go:229-363): per block the block digest, 5 attestations'
@@ -765,7 +805,8 @@ def replay_leg(args, torch, dist, dev, rank, world):
            "input": "serialized canonical BeaconBlock encodings, %.1f MB" % (int(offs[-1]) / 1e6),
            "processed": sum(r["status"] == "processed" for r in recs),
            "transitions": sum(r["transition"] for r in recs),
-           "state_roots": state_roots}
+           "state_roots": state_roots,
+           "cand_crystallized_root": root_vals["host_serial"].get("cand_crystallized", b"").hex()}
     if rank == 0 and world == 1:
         # the checker: the whole timed chain through the C restatement of the block pipeline
         # (checker mode), compared with the GPU engine's records and roots
@@ -1031,6 +1072,8 @@ def main():
     if epoch is not None and world == 1 and not args.epoch_validators:
         epoch_1m = epoch_leg(args, torch, dist, dev, rank, world, nval=1 << 20, ninst=16, baseline=False)
     replay = None if args.no_replay else replay_leg(args, torch, dist, dev, rank, world)
+    replay_sh = (replay_sharded_leg(args, torch, dist, dev, rank, world, comm)
+                 if (world > 1 and comm is not None and not args.no_replay) else None)
     wire_out = None if args.no_wire else wire_leg(args, torch, dist, dev, rank, world)
     att_out = None if args.no_attcheck else attcheck_leg(args, torch, dist, dev, rank, world)
     watt_out = None if args.no_wire else wire_att_leg(args, torch, dist, dev, rank, world, d_out)
@@ -1096,6 +1139,12 @@ def main():
         if epoch_1m is not None:
             line["epoch_1m_single_gpu"] = epoch_1m
         if replay is not None:
+            if replay_sh is not None:
+                # the replicas' chains are the same seed-6 chain only on rank 0; its root is
+                # the one the sharded chain must reproduce
+                replay_sh["root_matches_rank0_replica"] = (
+                    replay_sh["cand_crystallized_root"] == replay.get("cand_crystallized_root", ""))
+                replay["sharded"] = replay_sh
             line["replay"] = replay
         if wire_out is not None:
             line["wire"] = wire_out
@@ -1127,7 +1176,8 @@ def single_process_child(args, ndev):
     import subprocess
 
     cmd = [sys.executable, os.path.abspath(__file__), "--single-process", "--gpus", str(ndev), "--steps",
-           str(args.steps), "--warmup", str(args.warmup), "--records", str(args.records), "--no-cpu-baseline"]
+           str(args.steps), "--warmup", str(args.warmup), "--records", str(args.records), "--no-cpu-baseline",
+           "--replay-blocks", str(args.replay_blocks)]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
                                                            "GROUP_RANK", "ROLE_RANK", "MASTER_PORT")}
     try:
@@ -1228,9 +1278,23 @@ def single_process_main(args):
                             "shards": [list(de.shard(i)[:3]) for i in range(de.nlocal)]},
                  "algorithmic_GBps_per_gpu": nval * 16 * EPOCH_BYTES_PER_VALIDATOR / (wall_e / args.steps) / 1e9}
     de.free()
+    # configs[4] as one chain over the N devices of this process (pz_chain_new_comm)
+    from prysm_amd.blockchain import BeaconChain, serialize_blocks
+    blocks = synth.chain_blocks(65536, args.replay_blocks, seed=6)
+    data, offs = serialize_blocks(blocks)
+    BeaconChain(65536, comm=comm).process_serialized(*serialize_blocks(blocks[:130]))
+    ch = BeaconChain(65536, comm=comm)
+    t0 = time.perf_counter()
+    br, _ = ch.process_serialized(data, offs)
+    wall_r = time.perf_counter() - t0
+    roots = ch.roots()
+    replay_out = {"value": args.replay_blocks / wall_r, "unit": "blocks/s", "transitions": int(br["transition"].sum()),
+                  "processed": int((br["status"] == 0).sum()),
+                  "cand_crystallized_root": roots.get("cand_crystallized", b"").hex()}
+    del ch
     line = {"metric": METRIC, "mode": "single process, %d GPUs (pz_init_devices -> ncclCommInitAll)" % N,
             "n_gpus": N, "rccl_world": comm.world, "rccl_nlocal": comm.nlocal, "steps": args.steps,
-            "warmup": args.warmup, "hash": hash_out, "epoch": epoch_out}
+            "warmup": args.warmup, "hash": hash_out, "epoch": epoch_out, "replay_one_chain": replay_out}
     comm.free()
     print(json.dumps(line), flush=True)
 

@@ -569,6 +569,10 @@ typedef struct pz_att_check_batch {
   int32_t*  status;
   uint32_t* committee;
   uint64_t* parents_start;
+  const uint8_t* last_byte;        /* optional (NULL: read from bits): natt bytes, the last byte of
+                                      each bitfield (bits[boffs[i+1]-1]; any value when empty), a
+                                      caller-side column so the trailing-bits check streams 1 B per
+                                      attestation instead of touching every bitfield line */
 } pz_att_check_batch;
 int pz_check_attestations(const pz_att_check_batch* b);                  /* host pointers */
 int pz_dev_check_attestations(const pz_att_check_batch* b, void* stream); /* device pointers */
@@ -599,6 +603,16 @@ int  pz_chain_new(uint64_t nval, int device, pz_chain** out);
  * processed.  PZ_EINVAL when the bytes do not decode (proto.Unmarshal's error). */
 int  pz_chain_new_from_state(const uint8_t* cstate, uint64_t len, const uint8_t* saved_hashes, uint64_t nsaved,
                              int device, pz_chain** out);
+/* One chain over the ranks of `comm` (blockchain/core.go:300-345,
+ * 398-497): each local rank holds the 64-aligned validator range [lo, hi) of the balances, its
+ * columns of every vote-cache voter bitmap (so a voter's dedup bit lives on one rank) and its
+ * partial VoteTotalDeposit sums; a stateRecalc all-reduces the 64 totals the justification
+ * loop reads (65 words with the tally panic flag) and runs the epoch sharded like
+ * pz_epoch_state (partial crosslink tallies, bit counts and next-cycle balances all-reduced,
+ * rewards on each range).  The block walk, digests and messages run on local rank 0 of every
+ * process (one process per GPU replays the same blocks; the device work is split).  Genesis
+ * only: every validator stays active, so rank == index.  `comm` must outlive the chain. */
+int  pz_chain_new_comm(uint64_t nval, pz_comm* comm, pz_chain** out);
 void pz_chain_free(pz_chain* chain);
 /* Number of attestations in a batch of serialized blocks (host only; sizes att_out). */
 int  pz_count_attestations(const uint8_t* blocks, const uint64_t* offsets, uint64_t n, uint64_t* count);

@@ -71,6 +71,7 @@ SIGNATURES = {
     "pz_dev_epoch_finish": [vp, vp],
     "pz_dev_epoch_gather_compact": [vp, vp, u32, u64, vp, vp],
     "pz_chain_new": [u64, ctypes.c_int, vp],
+    "pz_chain_new_comm": [u64, vp, vp],
     "pz_chain_new_from_state": [vp, u64, vp, u64, ctypes.c_int, vp],
     "pz_chain_free": [vp],
     "pz_count_attestations": [vp, vp, u64, c_u64p],
@@ -183,6 +184,7 @@ class AttCheckBatch(ctypes.Structure):
         ("bits", vp), ("boffs", vp), ("block_slot", vp), ("last_justified_slot", u64),
         ("last_state_recalc", u64), ("n_recent", u64), ("narr", u64), ("arr_offs", vp), ("arr_shard", vp),
         ("arr_comm", vp), ("coffs", vp), ("status", vp), ("committee", vp), ("parents_start", vp),
+        ("last_byte", vp),
     ]
 
 

@@ -95,14 +95,21 @@ def serialize_blocks(blocks):
 class BeaconChain:
     """A chain from the genesis states of ``nval`` validators on one GPU."""
 
-    def __init__(self, nval, device=None):
+    def __init__(self, nval, device=None, comm=None):
+        """``comm`` (a ``prysm_amd.native.Comm``): one chain over the communicator's ranks,
+        each holding a validator range of the balances, the vote cache and the epoch
+        (pz_chain_new_comm)."""
         idx = 0
         if device is not None:
             import torch
             d = torch.device(device)
             idx = d.index or 0
         self._h = ctypes.c_void_p()
-        lib.call("pz_chain_new", nval, idx, ctypes.byref(self._h))
+        self.comm = comm  # kept alive as long as the chain
+        if comm is not None:
+            lib.call("pz_chain_new_comm", nval, comm.h, ctypes.byref(self._h))
+        else:
+            lib.call("pz_chain_new", nval, idx, ctypes.byref(self._h))
         self.nval = nval
 
     @classmethod

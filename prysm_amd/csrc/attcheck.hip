@@ -24,9 +24,11 @@ namespace {
 constexpr int kThreads = 256;
 
 // One attestation's checks from its loaded scalars (Go's order; see the file comment).
+// lastb: the bitfield's last byte when the caller supplies the column (b.last_byte), else -1
+// (read from bits).
 __device__ __forceinline__ void check_one(const pz_att_check_batch& b, uint64_t s, uint64_t bs, uint64_t js,
                                           uint64_t nob, uint64_t shard, uint64_t b0, uint64_t b1, int32_t* st_out,
-                                          uint32_t* comm_out, uint64_t* pstart_out) {
+                                          uint32_t* comm_out, uint64_t* pstart_out, int lastb = -1) {
   int32_t st = PZ_ATT_PROCESSED;
   uint32_t comm = UINT32_MAX;
   uint64_t pstart = 0;
@@ -57,8 +59,8 @@ __device__ __forceinline__ void check_one(const pz_att_check_batch& b, uint64_t 
         const uint64_t blen = b1 - b0;
         if ((k + 7) / 8 != blen)
           st = PZ_ATT_BITFIELD_LEN;
-        else if ((k & 7) && (b.bits[b0 + blen - 1] & (0xFFu >> (k & 7))))  // only when bits pad the byte
-          st = PZ_ATT_TRAILING_BITS;
+        else if ((k & 7) && ((lastb >= 0 ? (uint32_t)lastb : (uint32_t)b.bits[b0 + blen - 1]) & (0xFFu >> (k & 7))))
+          st = PZ_ATT_TRAILING_BITS;  // only when bits pad the byte
       }
     }
   }
@@ -77,7 +79,7 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_kernel(pz_at
   uint32_t comm;
   uint64_t pstart;
   check_one(b, b.slot[i], b.block_slot[i], b.justified_slot[i], b.n_oblique[i], b.shard_id[i], b.boffs[i],
-            b.boffs[i + 1], &st, &comm, &pstart);
+            b.boffs[i + 1], &st, &comm, &pstart, b.last_byte ? (int)b.last_byte[i] : -1);
   b.status[i] = st;
   if (b.committee) b.committee[i] = comm;
   if (b.parents_start) b.parents_start[i] = pstart;
@@ -99,7 +101,7 @@ __device__ __forceinline__ void att_check_x2_body(const pz_att_check_batch& b) {
     uint32_t comm;
     uint64_t pstart;
     check_one(b, b.slot[i], b.block_slot[i], b.justified_slot[i], b.n_oblique[i], b.shard_id[i], b.boffs[i],
-              b.boffs[i + 1], &st, &comm, &pstart);
+              b.boffs[i + 1], &st, &comm, &pstart, b.last_byte ? (int)b.last_byte[i] : -1);
     b.status[i] = st;
     if (b.committee) b.committee[i] = comm;
     if (b.parents_start) b.parents_start[i] = pstart;
@@ -116,11 +118,18 @@ __device__ __forceinline__ void att_check_x2_body(const pz_att_check_batch& b) {
   const ulonglong2 s = ld2(b.slot + i), bs = ld2(b.block_slot + i), js = ld2(b.justified_slot + i);
   const ulonglong2 nob = ld2(b.n_oblique + i), sh = ld2(b.shard_id + i), bo = ld2(b.boffs + i);
   const uint64_t bo2 = b.boffs[i + 2];
+  // the caller's last-byte column: both bytes in one 2-B load (i is even), beside the columns
+  int lb0 = -1, lb1 = -1;
+  if (b.last_byte) {
+    const uint32_t w = *reinterpret_cast<const uint16_t*>(b.last_byte + i);
+    lb0 = (int)(w & 0xFF);
+    lb1 = (int)(w >> 8);
+  }
   int32_t st0, st1;
   uint32_t c0, c1;
   uint64_t p0, p1;
-  check_one(b, s.x, bs.x, js.x, nob.x, sh.x, bo.x, bo.y, &st0, &c0, &p0);
-  check_one(b, s.y, bs.y, js.y, nob.y, sh.y, bo.y, bo2, &st1, &c1, &p1);
+  check_one(b, s.x, bs.x, js.x, nob.x, sh.x, bo.x, bo.y, &st0, &c0, &p0, lb0);
+  check_one(b, s.y, bs.y, js.y, nob.y, sh.y, bo.y, bo2, &st1, &c1, &p1, lb1);
   *reinterpret_cast<int2*>(b.status + i) = make_int2(st0, st1);
   if (b.committee) *reinterpret_cast<uint2*>(b.committee + i) = make_uint2(c0, c1);
   if (b.parents_start) *reinterpret_cast<ulonglong2*>(b.parents_start + i) = make_ulonglong2(p0, p1);
@@ -151,7 +160,8 @@ hipError_t launch_att_check(const pz_att_check_batch& b, hipStream_t s) {
   const bool x2 = al(b.slot) && al(b.block_slot) && al(b.justified_slot) && al(b.n_oblique) && al(b.shard_id) &&
                   al(b.boffs) && (reinterpret_cast<uintptr_t>(b.status) & 7) == 0 &&
                   (!b.committee || (reinterpret_cast<uintptr_t>(b.committee) & 7) == 0) &&
-                  (!b.parents_start || al(b.parents_start));
+                  (!b.parents_start || al(b.parents_start)) &&
+                  (!b.last_byte || (reinterpret_cast<uintptr_t>(b.last_byte) & 1) == 0);
   if (x2) {
     const uint64_t lanes = (b.natt + 1) / 2;
     if (g_attcheck_variant & 1)
@@ -212,6 +222,7 @@ int pz_check_attestations(const pz_att_check_batch* hb) {
     d.arr_comm = st.up(hb->arr_comm, ne);
     d.coffs = st.up(hb->coffs, ncomm + 1);
   }
+  if (hb->last_byte) d.last_byte = st.up(hb->last_byte, n);
   d.status = st.up<int32_t>(nullptr, n);
   d.committee = hb->committee ? st.up<uint32_t>(nullptr, n) : nullptr;
   d.parents_start = hb->parents_start ? st.up<uint64_t>(nullptr, n) : nullptr;

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <map>
 #include <mutex>
@@ -28,6 +29,7 @@
 #include <vector>
 
 #include "blake2b_kernels.h"
+#include "comm.h"
 #include "serial_hash.h"
 #include "epoch.h"
 #include "runtime.h"
@@ -341,38 +343,68 @@ enum ProfSlot {
 // flushing only at the transitions (10,000 blocks, 65,536 validators).
 constexpr size_t kFlushAtts = 1 << 16;
 
+// One local rank's device state.  An unsharded chain has one rank holding every validator;
+// a chain over a pz_comm (pz_chain_new_comm) gives each rank the
+// 64-aligned validator range [lo, hi): its balances, its columns of every vote-cache voter
+// bitmap and its partial VoteTotalDeposit sums, and its part of every epoch.
+struct RankDev {
+  int dev = 0, grank = 0;
+  hipStream_t s = nullptr;
+  uint64_t lo = 0, hi = 0, n = 0;
+  // validators [lo, hi) (shared by every CrystallizedState, like the Go pointer slice)
+  DevArr<uint64_t> balance, start, end;
+  // field 11 of the CrystallizedState for this range, encoded on the device (wire.hip)
+  DevArr<uint8_t> w_out;
+  DevArr<uint64_t> w_scratch, w_total;
+  // ShardAndCommitteesForSlots, replicated; and the members inside [lo, hi) with their
+  // committee positions (the sharded epoch's crosslink partial sums)
+  DevArr<uint32_t> committee, lcomm, lcpos;
+  DevArr<uint64_t> coffs, lcoffs;
+  // the vote cache: this range's words of every slot's voter bitmap, partial totals
+  DevArr<uint32_t> bitmaps;
+  DevArr<uint64_t> totals;
+  DevArr<uint8_t> present;
+  uint64_t words = 0;
+  DevArr<uint8_t> d_qpack;
+  DevArr<uint64_t> d_err;      // sticky tally panic flag
+  DevArr<uint32_t> d_id_slot;  // hash-log id -> vote-cache slot, uploaded up to Engine::d_id_slot_n
+  DevArr<uint32_t> ubits, uflag, d_leader;
+  DevArr<uint64_t> t64;        // the gathered justification totals + panic flag (65 words)
+  // epoch scratch: red = {scal[8], vote[natt], total[natt]} (one all-reduce when sharded)
+  DevArr<uint64_t> e_red, e_mask, e_nb;
+  DevArr<uint32_t> e_blk, e_list, e_win;
+  DevArr<uint8_t> e_pack;      // one H2D per transition: bitfields, offsets, committees, ...
+  hipEvent_t q_ev = nullptr;   // this rank's copy of the pinned tally arena is done
+  hipEvent_t ev_epoch = nullptr, ev_red = nullptr, ev_nb = nullptr, ev_t64 = nullptr;
+};
+
 struct Engine {
   uint64_t nval = 0;
   int device = 0;
-  hipStream_t s = nullptr;
+  hipStream_t s = nullptr;  // local rank 0's stream: hashing, the digest and message batches
+  pz_comm* comm = nullptr;  // null: one device, every validator
+  int world = 1;
+  std::vector<RankDev> rk;
   std::mutex mu;
   bool poisoned = false;
-  // validators (shared by every CrystallizedState, like the Go pointer slice)
-  DevArr<uint64_t> balance, start, end;
   std::vector<uint64_t> h_balance, h_start, h_end;  // genesis / reloaded values (uploaded once)
-  // the other ValidatorRecord fields, resident only when a reloaded state has them non-zero
+  // the other ValidatorRecord fields, resident (on rank 0) only when a reloaded state has them
+  // non-zero (reloading is unsharded)
   DevArr<uint64_t> pubkey, wshard, wa_offs, rc_offs;
   DevArr<uint8_t> wa, rc;
   bool has_pk = false, has_ws = false, has_wa = false, has_rc = false;
   uint64_t val_bytes = 0;  // total withdrawal_address + randao_commitment bytes
-  // field 11 of the CrystallizedState, encoded on the device from the resident validator
-  // arrays (wire.hip); re-encoded only after rewards changed a balance
+  // field 11 of the CrystallizedState, re-encoded only after rewards changed a balance
   std::string val_enc;
   bool val_enc_valid = false;
-  DevArr<uint8_t> w_out;
-  DevArr<uint64_t> w_scratch, w_total;
   // ShardAndCommitteesForSlots (immutable in this reference: stateRecalc copies it)
-  DevArr<uint32_t> committee;
-  DevArr<uint64_t> coffs;
   std::vector<uint64_t> csize;
   std::vector<std::vector<std::pair<uint64_t, uint32_t>>> lookup;  // [array] -> (shard, committee id)
   std::string arrays_enc;  // field 12 of the CrystallizedState, every array
   // block vote cache (one map shared by every ActiveState)
   std::unordered_map<H32, uint32_t, H32Hash> slot_of;
   std::vector<H32> slot_hash;
-  DevArr<uint32_t> bitmaps;
-  DevArr<uint64_t> totals;
-  uint64_t words = 0, cap = 0;
+  uint64_t cap = 0;
   // pending tally work: per queued attestation its committee, bitfield, the hash-log ids of
   // its 64 signed parent hashes and a mask of the ones equal to an oblique parent hash; the
   // device expands them into (attestation, parent) items (pz_vote_ids_kernel)
@@ -381,28 +413,15 @@ struct Engine {
   std::vector<uint32_t> q_comm, q_ids;
   std::vector<uint64_t> q_skip;
   // flushes run asynchronously to the walk: the queue is packed into a pinned arena and
-  // copied with one H2D; the arena is reused once its event says the copy is done
+  // copied with one H2D per rank; the arena is reused once every rank's copy is done
   uint8_t* q_arena = nullptr;
   size_t q_arena_cap = 0;
-  hipEvent_t q_arena_ev = nullptr;
   bool q_arena_busy = false;
-  DevArr<uint8_t> d_qpack, present;
-  DevArr<uint64_t> d_err;    // sticky tally panic flag
-  uint64_t* h_err = nullptr;  // its pinned host copy, read after a sync
-  DevArr<uint32_t> d_id_slot;  // hash-log id -> vote-cache slot, uploaded up to d_id_slot_n
   uint64_t d_id_slot_n = 0;
-  // per (slot, committee) union bitfields and touched flags of the tally's first pass
-  DevArr<uint32_t> ubits, uflag;
-  DevArr<uint32_t> d_leader;
   uint64_t ncomm = 0, cwords = 1;
-  // epoch scratch
-  DevArr<uint64_t> e_scal, e_mask, e_vote, e_total;
-  DevArr<uint32_t> e_blk, e_list, e_win;
-  DevArr<uint8_t> e_pack;    // one H2D per transition: bitfields, offsets, committees, ...
-  PinBuf e_pin, e_pin_out;   // its pinned staging; the results' pinned landing (scal, winners)
-  PinBuf tot_pin;            // the vote totals the justification loop reads
-  hipEvent_t ev_totals = nullptr;  // the tally flush + totals D2H of a transition are done
-  hipEvent_t ev_epoch = nullptr;   // the last enqueued epoch's results have landed
+  PinBuf e_pin, e_pin_out;   // the epoch inputs' pinned staging; the results' pinned landing
+  PinBuf tot_pin;            // the gathered justification totals (65 words)
+  hipEvent_t ev_totals = nullptr;  // the tally flush + the totals' D2H of a transition are done
   // The epoch of the last transition, enqueued but not yet collected: its results (the
   // crosslink records, the next state's TotalDeposits, a panic) are first needed at the next
   // transition or by the state bytes/roots, so the walk never waits for it.
@@ -413,7 +432,7 @@ struct Engine {
     uint64_t block_slot = 0;
     size_t nrec = 0;
   } deferred;
-  // hashing scratch
+  // hashing scratch (rank 0)
   PinBuf pin_msgs, pin_offs, pin_dig;  // pinned staging of the digest batch
   DevArr<uint8_t> h_in, h_out;
   DevArr<uint64_t> h_offs;
@@ -470,6 +489,23 @@ static void upload(Engine& g, DevArr<T>& d, const T* h, size_t n) {
   check(d.alloc(n));
   if (n) hchk(hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, g.s), "H2D");
 }
+template <typename T>
+static void upload(RankDev& r, DevArr<T>& d, const T* h, size_t n) {
+  hchk(hipSetDevice(r.dev), "hipSetDevice");
+  check(d.alloc(n));
+  if (n) hchk(hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, r.s), "H2D");
+}
+// Ranks of the chain's partition this process drives (rank 0's device left current).
+static void each_rank(Engine& g, const std::function<void(RankDev&)>& f) {
+  for (RankDev& r : g.rk) {
+    hchk(hipSetDevice(r.dev), "hipSetDevice");
+    f(r);
+  }
+  hchk(hipSetDevice(g.rk[0].dev), "hipSetDevice");
+}
+static void sync_ranks(Engine& g) {
+  each_rank(g, [](RankDev& r) { hchk(hipStreamSynchronize(r.s), "sync"); });
+}
 
 // Many messages -> 64-byte digests (one CSR launch).  Blocks until done.
 static void hash_many(Engine& g, const std::string& data, const std::vector<uint64_t>& offs, std::vector<uint8_t>& out) {
@@ -525,36 +561,39 @@ static uint32_t vote_slot(Engine& g, const H32& h) {
   const uint32_t s = (uint32_t)g.slot_hash.size();
   g.slot_of.emplace(h, s);
   g.slot_hash.push_back(h);
-  if (s >= g.cap) {  // grow the device arrays, keeping their contents
+  if (s >= g.cap) {  // grow every rank's device arrays, keeping their contents
     const uint64_t nc = std::max<uint64_t>(64, 2 * g.cap);
-    DevArr<uint32_t> bm;
-    DevArr<uint64_t> tt;
-    DevArr<uint8_t> pr;
-    check(bm.alloc(nc * g.words));
-    check(tt.alloc(nc));
-    check(pr.alloc(nc));
-    hchk(hipMemsetAsync(bm.p, 0, nc * g.words * 4, g.s), "memset");
-    hchk(hipMemsetAsync(tt.p, 0, nc * 8, g.s), "memset");
-    hchk(hipMemsetAsync(pr.p, 0, nc, g.s), "memset");
-    if (g.cap) {
-      hchk(hipMemcpyAsync(bm.p, g.bitmaps.p, g.cap * g.words * 4, hipMemcpyDeviceToDevice, g.s), "D2D");
-      hchk(hipMemcpyAsync(tt.p, g.totals.p, g.cap * 8, hipMemcpyDeviceToDevice, g.s), "D2D");
-      hchk(hipMemcpyAsync(pr.p, g.present.p, g.cap, hipMemcpyDeviceToDevice, g.s), "D2D");
-    }
-    hchk(hipStreamSynchronize(g.s), "sync");
-    std::swap(g.bitmaps.p, bm.p);
-    std::swap(g.bitmaps.n, bm.n);
-    std::swap(g.totals.p, tt.p);
-    std::swap(g.totals.n, tt.n);
-    std::swap(g.present.p, pr.p);
-    std::swap(g.present.n, pr.n);
-    // the union buffers are all zero between flushes (and a slot is only created outside
-    // one): reallocate them zeroed
-    check(g.ubits.alloc(nc * g.ncomm * g.cwords));
-    check(g.uflag.alloc(nc * g.ncomm));
-    hchk(hipMemsetAsync(g.ubits.p, 0, nc * g.ncomm * g.cwords * 4, g.s), "memset");
-    hchk(hipMemsetAsync(g.uflag.p, 0, nc * g.ncomm * 4, g.s), "memset");
-    hchk(hipStreamSynchronize(g.s), "sync");
+    each_rank(g, [&](RankDev& r) {
+      DevArr<uint32_t> bm;
+      DevArr<uint64_t> tt;
+      DevArr<uint8_t> pr;
+      check(bm.alloc(nc * r.words));
+      check(tt.alloc(nc));
+      check(pr.alloc(nc));
+      hchk(hipMemsetAsync(bm.p, 0, nc * r.words * 4, r.s), "memset");
+      hchk(hipMemsetAsync(tt.p, 0, nc * 8, r.s), "memset");
+      hchk(hipMemsetAsync(pr.p, 0, nc, r.s), "memset");
+      if (g.cap) {
+        if (r.words)
+          hchk(hipMemcpyAsync(bm.p, r.bitmaps.p, g.cap * r.words * 4, hipMemcpyDeviceToDevice, r.s), "D2D");
+        hchk(hipMemcpyAsync(tt.p, r.totals.p, g.cap * 8, hipMemcpyDeviceToDevice, r.s), "D2D");
+        hchk(hipMemcpyAsync(pr.p, r.present.p, g.cap, hipMemcpyDeviceToDevice, r.s), "D2D");
+      }
+      hchk(hipStreamSynchronize(r.s), "sync");
+      std::swap(r.bitmaps.p, bm.p);
+      std::swap(r.bitmaps.n, bm.n);
+      std::swap(r.totals.p, tt.p);
+      std::swap(r.totals.n, tt.n);
+      std::swap(r.present.p, pr.p);
+      std::swap(r.present.n, pr.n);
+      // the union buffers are all zero between flushes (and a slot is only created outside
+      // one): reallocate them zeroed
+      check(r.ubits.alloc(nc * g.ncomm * g.cwords));
+      check(r.uflag.alloc(nc * g.ncomm));
+      hchk(hipMemsetAsync(r.ubits.p, 0, nc * g.ncomm * g.cwords * 4, r.s), "memset");
+      hchk(hipMemsetAsync(r.uflag.p, 0, nc * g.ncomm * 4, r.s), "memset");
+      hchk(hipStreamSynchronize(r.s), "sync");
+    });
     g.cap = nc;
   }
   return s;
@@ -576,10 +615,9 @@ static uint32_t log_hash(Engine& g, const H32& h, bool votable = true) {
   return (uint32_t)(g.hlog.size() - 1);
 }
 
-// Enqueue the pending tally items; no host wait (the pinned arena and the event make the
-// H2D asynchronous).  Balances only change in stateRecalc's epoch, which the stream orders
-// after every flush, so a flush may run any time before it.  flush_votes_finish must follow
-// a stream sync.
+// Enqueue the pending tally items on every rank; no host wait (the pinned arena and its
+// per-rank events make the H2D asynchronous).  Balances only change in stateRecalc's epoch,
+// which each rank's stream orders after every flush, so a flush may run any time before it.
 static bool flush_votes_enqueue(Engine& g) {
   if (g.q_comm.empty()) return false;
   PhaseTimer pt(g.prof[kProfFlush]);
@@ -591,7 +629,7 @@ static bool flush_votes_enqueue(Engine& g) {
                o_ids = o_comm + al(natt * 4), o_slots = o_ids + al(g.q_ids.size() * 4),
                o_bits = o_slots + al(new_ids * 4), total = o_bits + al(g.q_bits.size());
   if (g.q_arena_busy) {
-    hchk(hipEventSynchronize(g.q_arena_ev), "event sync");
+    for (RankDev& r : g.rk) hchk(hipEventSynchronize(r.q_ev), "event sync");
     g.q_arena_busy = false;
   }
   if (total > g.q_arena_cap) {
@@ -601,65 +639,69 @@ static bool flush_votes_enqueue(Engine& g) {
     hchk(hipHostMalloc((void**)&g.q_arena, cap, hipHostMallocDefault), "hipHostMalloc");
     g.q_arena_cap = cap;
   }
-  if (!g.q_arena_ev) hchk(hipEventCreateWithFlags(&g.q_arena_ev, hipEventDisableTiming), "event");
   std::memcpy(g.q_arena + o_boffs, g.q_boffs.data(), g.q_boffs.size() * 8);
   std::memcpy(g.q_arena + o_skip, g.q_skip.data(), natt * 8);
   std::memcpy(g.q_arena + o_comm, g.q_comm.data(), natt * 4);
   std::memcpy(g.q_arena + o_ids, g.q_ids.data(), g.q_ids.size() * 4);
   std::memcpy(g.q_arena + o_slots, g.id_slot.data() + g.d_id_slot_n, new_ids * 4);
   std::memcpy(g.q_arena + o_bits, g.q_bits.data(), g.q_bits.size());
-  // Growing a device buffer frees the old one, which in-flight flushes may still read:
-  // drain the stream first (rare: the buffers double).
-  if (total > g.d_qpack.n || nid > g.d_id_slot.n || natt * 64 + 1 > g.d_leader.n) {
-    hchk(hipStreamSynchronize(g.s), "sync");
-    check(g.d_qpack.alloc(std::max<uint64_t>(total, 2 * g.d_qpack.n)));
-    check(g.d_leader.alloc(std::max<uint64_t>(natt * 64 + 1, 2 * g.d_leader.n)));
-    if (nid > g.d_id_slot.n) {  // the id -> slot map keeps its device contents
-      DevArr<uint32_t> grown;
-      check(grown.alloc(std::max<uint64_t>(nid, 2 * g.d_id_slot.n)));
-      if (g.d_id_slot_n)
-        hchk(hipMemcpyAsync(grown.p, g.d_id_slot.p, g.d_id_slot_n * 4, hipMemcpyDeviceToDevice, g.s), "D2D");
-      hchk(hipStreamSynchronize(g.s), "sync");
-      std::swap(g.d_id_slot.p, grown.p);
-      std::swap(g.d_id_slot.n, grown.n);
+  each_rank(g, [&](RankDev& r) {
+    // Growing a device buffer frees the old one, which in-flight flushes may still read:
+    // drain the stream first (rare: the buffers double).
+    if (total > r.d_qpack.n || nid > r.d_id_slot.n || natt * 64 + 1 > r.d_leader.n) {
+      hchk(hipStreamSynchronize(r.s), "sync");
+      check(r.d_qpack.alloc(std::max<uint64_t>(total, 2 * r.d_qpack.n)));
+      check(r.d_leader.alloc(std::max<uint64_t>(natt * 64 + 1, 2 * r.d_leader.n)));
+      if (nid > r.d_id_slot.n) {  // the id -> slot map keeps its device contents
+        DevArr<uint32_t> grown;
+        check(grown.alloc(std::max<uint64_t>(nid, 2 * r.d_id_slot.n)));
+        if (g.d_id_slot_n)
+          hchk(hipMemcpyAsync(grown.p, r.d_id_slot.p, g.d_id_slot_n * 4, hipMemcpyDeviceToDevice, r.s), "D2D");
+        hchk(hipStreamSynchronize(r.s), "sync");
+        std::swap(r.d_id_slot.p, grown.p);
+        std::swap(r.d_id_slot.n, grown.n);
+      }
     }
-  }
-  hchk(hipMemcpyAsync(g.d_qpack.p, g.q_arena, total, hipMemcpyHostToDevice, g.s), "H2D");
-  if (new_ids)
-    hchk(hipMemcpyAsync(g.d_id_slot.p + g.d_id_slot_n, g.d_qpack.p + o_slots, new_ids * 4, hipMemcpyDeviceToDevice,
-                        g.s), "D2D");
-  hchk(hipEventRecord(g.q_arena_ev, g.s), "event");
+    hchk(hipMemcpyAsync(r.d_qpack.p, g.q_arena, total, hipMemcpyHostToDevice, r.s), "H2D");
+    if (new_ids)
+      hchk(hipMemcpyAsync(r.d_id_slot.p + g.d_id_slot_n, r.d_qpack.p + o_slots, new_ids * 4, hipMemcpyDeviceToDevice,
+                          r.s), "D2D");
+    if (!r.q_ev) hchk(hipEventCreateWithFlags(&r.q_ev, hipEventDisableTiming), "event");
+    hchk(hipEventRecord(r.q_ev, r.s), "event");
+    if (!r.d_err.p) {
+      check(r.d_err.alloc(1));
+      hchk(hipMemsetAsync(r.d_err.p, 0, 8, r.s), "memset");
+    }
+    VoteIdArgs v;
+    std::memset(&v, 0, sizeof v);
+    v.committee = r.committee.p;
+    v.coffs = r.coffs.p;
+    v.att_comm = reinterpret_cast<const uint32_t*>(r.d_qpack.p + o_comm);
+    v.bits = r.d_qpack.p + o_bits;
+    v.boffs = reinterpret_cast<const uint64_t*>(r.d_qpack.p + o_boffs);
+    v.ids = reinterpret_cast<const uint32_t*>(r.d_qpack.p + o_ids);
+    v.skip = reinterpret_cast<const uint64_t*>(r.d_qpack.p + o_skip);
+    v.id_slot = r.d_id_slot.p;
+    v.natt = natt;
+    v.balance = r.balance.p;
+    v.nval = r.n;
+    v.val_offset = r.lo;
+    v.nval_global = g.nval;
+    v.bitmaps = r.bitmaps.p;
+    v.words_per_slot = r.words;
+    v.totals = r.totals.p;
+    v.present = r.present.p;
+    v.err = r.d_err.p;  // sticky: read (and the chain poisoned) at the next sync point
+    v.ubits = r.ubits.p;
+    v.uflag = r.uflag.p;
+    v.leader = r.d_leader.p + 1;
+    v.nlead = r.d_leader.p;
+    v.ncomm = g.ncomm;
+    v.cwords = g.cwords;
+    hchk(launch_vote_ids(v, r.s), "vote tally");
+  });
   g.q_arena_busy = true;
   g.d_id_slot_n = nid;
-  if (!g.d_err.p) {
-    check(g.d_err.alloc(1));
-    hchk(hipMemsetAsync(g.d_err.p, 0, 8, g.s), "memset");
-  }
-  VoteIdArgs v;
-  std::memset(&v, 0, sizeof v);
-  v.committee = g.committee.p;
-  v.coffs = g.coffs.p;
-  v.att_comm = reinterpret_cast<const uint32_t*>(g.d_qpack.p + o_comm);
-  v.bits = g.d_qpack.p + o_bits;
-  v.boffs = reinterpret_cast<const uint64_t*>(g.d_qpack.p + o_boffs);
-  v.ids = reinterpret_cast<const uint32_t*>(g.d_qpack.p + o_ids);
-  v.skip = reinterpret_cast<const uint64_t*>(g.d_qpack.p + o_skip);
-  v.id_slot = g.d_id_slot.p;
-  v.natt = natt;
-  v.balance = g.balance.p;
-  v.nval = g.nval;
-  v.bitmaps = g.bitmaps.p;
-  v.words_per_slot = g.words;
-  v.totals = g.totals.p;
-  v.present = g.present.p;
-  v.err = g.d_err.p;  // sticky: read (and the chain poisoned) at the next sync point
-  v.ubits = g.ubits.p;
-  v.uflag = g.uflag.p;
-  v.leader = g.d_leader.p + 1;
-  v.nlead = g.d_leader.p;
-  v.ncomm = g.ncomm;
-  v.cwords = g.cwords;
-  hchk(launch_vote_ids(v, g.s), "vote tally");
   g.q_bits.clear();
   g.q_boffs.assign(1, 0);
   g.q_comm.clear();
@@ -668,26 +710,52 @@ static bool flush_votes_enqueue(Engine& g) {
   return true;
 }
 
-// Enqueue the copy of the sticky panic flag; flush_votes_finish reads it after the sync.
-static void flush_err_enqueue(Engine& g) {
-  if (!g.d_err.p) return;
-  if (!g.h_err) hchk(hipHostMalloc((void**)&g.h_err, 8, hipHostMallocDefault), "hipHostMalloc");
-  hchk(hipMemcpyAsync(g.h_err, g.d_err.p, 8, hipMemcpyDeviceToHost, g.s), "D2H");
+// Enqueue, behind every rank's pending tallies, the gather of the 64 justification totals
+// (slot UINT32_MAX: 0) and the sticky tally panic flag into each rank's t64, their sum over
+// the ranks (one 65-word all-reduce when sharded: the partial VoteTotalDeposit sums of the
+// validator ranges) and the D2H of rank 0's into g.tot_pin, then g.ev_totals.
+static void tally_gather_enqueue(Engine& g, const VoteGatherSlots& q) {
+  check(g.tot_pin.reserve((kJustifySlots + 1) * 8));
+  std::vector<uint64_t*> bufs;
+  std::vector<hipStream_t> streams;
+  std::vector<hipEvent_t> evs;
+  each_rank(g, [&](RankDev& r) {
+    check(r.t64.alloc(kJustifySlots + 1));
+    if (!r.d_err.p) {
+      check(r.d_err.alloc(1));
+      hchk(hipMemsetAsync(r.d_err.p, 0, 8, r.s), "memset");
+    }
+    if (!r.ev_t64) hchk(hipEventCreateWithFlags(&r.ev_t64, hipEventDisableTiming), "event");
+    hchk(launch_vote_gather(r.totals.p, q, r.d_err.p, r.t64.p, r.s), "vote gather");
+    bufs.push_back(r.t64.p);
+    streams.push_back(r.s);
+    evs.push_back(r.ev_t64);
+  });
+  if (g.world > 1) {
+    check(g.comm->allreduce_u64(bufs.data(), kJustifySlots + 1, streams.data(), evs.data()));
+    hchk(hipSetDevice(g.rk[0].dev), "hipSetDevice");
+    hchk(hipStreamWaitEvent(g.rk[0].s, g.rk[0].ev_t64, 0), "wait");
+  }
+  hchk(hipMemcpyAsync(g.tot_pin.p, g.rk[0].t64.p, (kJustifySlots + 1) * 8, hipMemcpyDeviceToHost, g.rk[0].s), "D2H");
+  if (!g.ev_totals) hchk(hipEventCreateWithFlags(&g.ev_totals, hipEventDisableTiming), "event");
+  hchk(hipEventRecord(g.ev_totals, g.rk[0].s), "event");
 }
 
-// After a stream sync that completed flush_err_enqueue: raise the panic a tally detected.
-static void flush_votes_finish(Engine& g) {
-  if (g.h_err && *g.h_err) throw Panic{"calculateBlockVoteCache: CheckBit / validator index out of range"};
+// After g.ev_totals: raise the panic a tally detected.
+static void tally_gather_finish(Engine& g) {
+  hchk(hipEventSynchronize(g.ev_totals), "event sync (vote totals)");
+  if (reinterpret_cast<const uint64_t*>(g.tot_pin.p)[kJustifySlots])
+    throw Panic{"calculateBlockVoteCache: CheckBit / validator index out of range"};
 }
 
+// Every queued tally done, its panic (if any) raised.
 static void flush_votes(Engine& g) {
   flush_votes_enqueue(g);
-  flush_err_enqueue(g);
-  {
-    PhaseTimer pt(g.prof[kProfFlush]);
-    hchk(hipStreamSynchronize(g.s), "sync");
-  }
-  flush_votes_finish(g);
+  VoteGatherSlots q;
+  for (int j = 0; j < kJustifySlots; ++j) q.slot[j] = UINT32_MAX;
+  tally_gather_enqueue(g, q);
+  PhaseTimer pt(g.prof[kProfFlush]);
+  tally_gather_finish(g);
 }
 
 // ---- core.go ------------------------------------------------------------------------------------
@@ -794,53 +862,99 @@ static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending
   uint64_t* small = reinterpret_cast<uint64_t*>(h + o_small);
   small[0] = C.dynasty;
   small[1] = C.tdep;
-  // the previous epoch was collected (its event completed), so the staging is free
-  check(g.e_pack.alloc(total));
-  hchk(hipMemcpyAsync(g.e_pack.p, h, total, hipMemcpyHostToDevice, g.s), "H2D epoch");
-  check(g.e_scal.alloc(kScal));
-  check(g.e_vote.alloc(na + 1));
-  check(g.e_total.alloc(na + 1));
-  check(g.e_win.alloc(nrec + 1));
-  hchk(hipMemsetAsync(g.e_scal.p, 0, kScal * 8, g.s), "memset");
-  uint8_t* d = g.e_pack.p;
-  EpochArgs a;
-  std::memset(&a, 0, sizeof a);
-  a.ninst = 1;
-  a.nval = a.nval_global = g.nval;
-  a.kind = PZ_KIND_ACTIVE;
-  a.balance = g.balance.p;
-  a.start = g.start.p;
-  a.end = g.end.p;
-  a.dynasty = reinterpret_cast<const uint64_t*>(d + o_small);
-  a.total_deposit = reinterpret_cast<const uint64_t*>(d + o_small) + 1;
-  a.natt = (uint32_t)na;
-  a.bits = d + o_bits;
-  a.boffs = reinterpret_cast<const uint64_t*>(d + o_boffs);
-  a.max_inst_bytes = nbits;
-  a.pop_rank = 0;
-  a.pop_world = 1;
-  a.committee = g.committee.p;
-  a.coffs = g.coffs.p;
-  a.att_comm = reinterpret_cast<const uint32_t*>(d + o_comm);
-  a.att_shard = reinterpret_cast<const uint32_t*>(d + o_shard);
-  a.nrec = (uint32_t)nrec;
-  a.rec_dynasty = reinterpret_cast<const uint64_t*>(d + o_rdyn);
-  a.winner = g.e_win.p;
-  a.vote = g.e_vote.p;
-  a.total = g.e_total.p;
-  a.scal = g.e_scal.p;
-  a.act_mask = g.e_mask.p;
-  a.blk_cnt = g.e_blk.p;
-  a.act_list = g.e_list.p;
-  hchk(launch_epoch_count(a, true, true, true, g.s), "epoch count");
-  hchk(launch_epoch_mid(a, a.nrec > 0 && na > 0, true, g.s), "epoch mid");
-  hchk(launch_epoch_reward(a, g.s), "epoch reward");
+  // the previous epoch was collected (every rank's event completed), so the staging is free
+  const uint64_t nred = kScal + 2 * (uint64_t)na;  // {scal, vote, total}: one all-reduce when sharded
+  std::vector<uint64_t*> bufs, nbs;
+  std::vector<hipStream_t> streams;
+  std::vector<hipEvent_t> evs, evn;
+  std::vector<EpochArgs> args;
+  each_rank(g, [&](RankDev& r) {
+    check(r.e_pack.alloc(total));
+    hchk(hipMemcpyAsync(r.e_pack.p, h, total, hipMemcpyHostToDevice, r.s), "H2D epoch");
+    check(r.e_red.alloc(nred + 1));
+    check(r.e_nb.alloc(1));
+    check(r.e_win.alloc(nrec + 1));
+    hchk(hipMemsetAsync(r.e_red.p, 0, kScal * 8, r.s), "memset");
+    uint8_t* d = r.e_pack.p;
+    EpochArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.ninst = 1;
+    a.nval = r.n;
+    a.val_offset = r.lo;
+    a.nval_global = g.nval;
+    a.kind = PZ_KIND_ACTIVE;
+    a.balance = r.balance.p;
+    a.start = r.start.p;
+    a.end = r.end.p;
+    a.dynasty = reinterpret_cast<const uint64_t*>(d + o_small);
+    a.total_deposit = reinterpret_cast<const uint64_t*>(d + o_small) + 1;
+    a.natt = (uint32_t)na;
+    a.bits = d + o_bits;
+    a.boffs = reinterpret_cast<const uint64_t*>(d + o_boffs);
+    a.max_inst_bytes = nbits;
+    a.pop_rank = (uint32_t)r.grank;
+    a.pop_world = (uint32_t)g.world;
+    // sharded: the members inside [lo, hi) with their committee positions (rank 0 also keeps
+    // any member >= nval, whose processCrosslinks panic it raises)
+    a.committee = g.world > 1 ? r.lcomm.p : r.committee.p;
+    a.coffs = g.world > 1 ? r.lcoffs.p : r.coffs.p;
+    a.cpos = g.world > 1 ? r.lcpos.p : nullptr;
+    a.att_comm = reinterpret_cast<const uint32_t*>(d + o_comm);
+    a.att_shard = reinterpret_cast<const uint32_t*>(d + o_shard);
+    a.nrec = (uint32_t)nrec;
+    a.rec_dynasty = reinterpret_cast<const uint64_t*>(d + o_rdyn);
+    a.winner = r.e_win.p;
+    a.scal = r.e_red.p;
+    a.vote = r.e_red.p + kScal;
+    a.total = r.e_red.p + kScal + na;
+    a.act_mask = r.e_mask.p;
+    a.blk_cnt = r.e_blk.p;
+    a.act_list = r.e_list.p;
+    hchk(launch_epoch_count(a, true, true, true, r.s), "epoch count");
+    if (g.world == 1) {
+      hchk(launch_epoch_mid(a, a.nrec > 0 && na > 0, true, r.s), "epoch mid");
+      hchk(launch_epoch_reward(a, r.s), "epoch reward");
+    }
+    args.push_back(a);
+    bufs.push_back(r.e_red.p);
+    nbs.push_back(r.e_nb.p);
+    streams.push_back(r.s);
+    if (!r.ev_red) hchk(hipEventCreateWithFlags(&r.ev_red, hipEventDisableTiming), "event");
+    if (!r.ev_nb) hchk(hipEventCreateWithFlags(&r.ev_nb, hipEventDisableTiming), "event");
+    evs.push_back(r.ev_red);
+    evn.push_back(r.ev_nb);
+  });
+  if (g.world > 1) {
+    // the partial crosslink tallies, bit counts and flags of the ranges summed (the step of
+    // pz_epoch_state, epoch_state.hip, for one instance; every validator is active in a
+    // sharded chain, so rank == index and no active-list gather is needed), then winners and
+    // rewards on each range, then the partial next-cycle balances summed
+    check(g.comm->allreduce_u64(bufs.data(), nred, streams.data(), evs.data()));
+    for (size_t i = 0; i < g.rk.size(); ++i) {
+      RankDev& r = g.rk[i];
+      hchk(hipSetDevice(r.dev), "hipSetDevice");
+      hchk(hipStreamWaitEvent(r.s, r.ev_red, 0), "wait");
+      hchk(launch_epoch_mid(args[i], args[i].nrec > 0 && na > 0, false, r.s), "epoch mid");
+      hchk(launch_epoch_reward(args[i], r.s), "epoch reward");
+      hchk(hipMemcpyAsync(r.e_nb.p, r.e_red.p + kNextBal, 8, hipMemcpyDeviceToDevice, r.s), "D2D");
+    }
+    check(g.comm->allreduce_u64(nbs.data(), 1, streams.data(), evn.data()));
+    for (RankDev& r : g.rk) {
+      hchk(hipSetDevice(r.dev), "hipSetDevice");
+      hchk(hipStreamWaitEvent(r.s, r.ev_nb, 0), "wait");
+      hchk(hipMemcpyAsync(r.e_red.p + kNextBal, r.e_nb.p, 8, hipMemcpyDeviceToDevice, r.s), "D2D");
+    }
+  }
+  RankDev& r0 = g.rk[0];
+  hchk(hipSetDevice(r0.dev), "hipSetDevice");
   check(g.e_pin_out.reserve(kScal * 8 + nrec * 4 + 16));
-  hchk(hipMemcpyAsync(g.e_pin_out.p, g.e_scal.p, kScal * 8, hipMemcpyDeviceToHost, g.s), "D2H");
+  hchk(hipMemcpyAsync(g.e_pin_out.p, r0.e_red.p, kScal * 8, hipMemcpyDeviceToHost, r0.s), "D2H");
   if (nrec)
-    hchk(hipMemcpyAsync(g.e_pin_out.p + kScal * 8, g.e_win.p, nrec * 4, hipMemcpyDeviceToHost, g.s), "D2H");
-  if (!g.ev_epoch) hchk(hipEventCreateWithFlags(&g.ev_epoch, hipEventDisableTiming), "event");
-  hchk(hipEventRecord(g.ev_epoch, g.s), "event");
+    hchk(hipMemcpyAsync(g.e_pin_out.p + kScal * 8, r0.e_win.p, nrec * 4, hipMemcpyDeviceToHost, r0.s), "D2H");
+  each_rank(g, [&](RankDev& r) {
+    if (!r.ev_epoch) hchk(hipEventCreateWithFlags(&r.ev_epoch, hipEventDisableTiming), "event");
+    hchk(hipEventRecord(r.ev_epoch, r.s), "event");
+  });
   g.deferred.nrec = nrec;
 }
 
@@ -852,7 +966,7 @@ static void epoch_collect(Engine& g) {
   Engine::DeferredEpoch& D = g.deferred;
   if (!D.live) return;
   D.live = false;
-  hchk(hipEventSynchronize(g.ev_epoch), "event sync (epoch)");
+  for (RankDev& r : g.rk) hchk(hipEventSynchronize(r.ev_epoch), "event sync (epoch)");
   uint64_t scal[kScal];
   std::memcpy(scal, g.e_pin_out.p, sizeof scal);
   const uint32_t* win = reinterpret_cast<const uint32_t*>(g.e_pin_out.p + sizeof scal);
@@ -889,18 +1003,19 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   // CalculateRewards, next balance) does not depend on it and is enqueued behind them, to be
   // collected at the next transition; the stream orders every later tally after its rewards.
   flush_votes_enqueue(g);
-  flush_err_enqueue(g);
   PhaseTimer pt(g.prof[kProfRecalc]);
   uint64_t streak = C->streak, justified = C->jslot, finalized = C->fslot;
   const uint64_t lsr = C->lsr;
   std::vector<uint64_t> tot(kCycle, 0);
-  const uint64_t nslots = A->cache_nil ? 0 : g.slot_hash.size();
-  if (nslots) {
-    check(g.tot_pin.reserve(nslots * 8));
-    hchk(hipMemcpyAsync(g.tot_pin.p, g.totals.p, nslots * 8, hipMemcpyDeviceToHost, g.s), "D2H");
+  VoteGatherSlots q;
+  for (uint64_t i = 0; i < kCycle; ++i) {
+    q.slot[i] = UINT32_MAX;
+    if (!A->cache_nil && i < A->recent.size()) {
+      auto it = g.slot_of.find(A->recent[i]);
+      if (it != g.slot_of.end()) q.slot[i] = it->second;
+    }
   }
-  if (!g.ev_totals) hchk(hipEventCreateWithFlags(&g.ev_totals, hipEventDisableTiming), "event");
-  hchk(hipEventRecord(g.ev_totals, g.s), "event");
+  tally_gather_enqueue(g, q);
   epoch_enqueue(g, *C, A->pending);
   auto nc = std::make_shared<CState>();
   g.deferred.live = true;
@@ -908,15 +1023,8 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   g.deferred.src = C;
   g.deferred.dst = nc;
   g.deferred.block_slot = block_slot;
-  hchk(hipEventSynchronize(g.ev_totals), "event sync (vote totals)");
-  flush_votes_finish(g);
-  if (nslots) {
-    const uint64_t* all = reinterpret_cast<const uint64_t*>(g.tot_pin.p);
-    for (uint64_t i = 0; i < kCycle && i < A->recent.size(); ++i) {
-      auto it = g.slot_of.find(A->recent[i]);
-      tot[i] = it == g.slot_of.end() ? 0 : all[it->second];
-    }
-  }
+  tally_gather_finish(g);
+  std::memcpy(tot.data(), g.tot_pin.p, kCycle * 8);
   for (uint64_t i = 0; i < kCycle; ++i) {
     const uint64_t slot = lsr - kCycle + i;
     if (3ull * tot[i] >= 2ull * C->tdep) {
@@ -953,29 +1061,86 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
 // ---- serialization of the states (state roots) --------------------------------------------
 static const std::string& validators_enc(Engine& g) {
   if (g.val_enc_valid) return g.val_enc;
-  pz_validator_cols v{};
-  v.balance = g.balance.p;
-  v.start_dynasty = g.start.p;
-  v.end_dynasty = g.end.p;
-  if (g.has_pk) v.public_key = g.pubkey.p;
-  if (g.has_ws) v.withdrawal_shard = g.wshard.p;
-  if (g.has_wa) { v.withdrawal_address = g.wa.p; v.withdrawal_address_offs = g.wa_offs.p; }
-  if (g.has_rc) { v.randao_commitment = g.rc.p; v.randao_commitment_offs = g.rc_offs.p; }
-  WireValArgs a;
-  check(wire_val_args(&v, g.nval, 11, &a));
-  const uint64_t bound = pz_wire_validators_bound(g.nval, g.val_bytes);
-  check(g.w_out.alloc(bound));
-  check(g.w_scratch.alloc(wire_tiles(g.nval) + 1));
-  check(g.w_total.alloc(1));
-  a.out = g.w_out.p;
-  a.total = g.w_total.p;
-  hchk(launch_wire_validators(a, g.w_scratch.p, g.s), "pz_wire_val_kernel");
-  uint64_t total = 0;
-  hchk(hipMemcpyAsync(&total, g.w_total.p, 8, hipMemcpyDeviceToHost, g.s), "D2H");
-  hchk(hipStreamSynchronize(g.s), "sync");
-  g.val_enc.resize(total);
-  hchk(hipMemcpyAsync(&g.val_enc[0], g.w_out.p, total, hipMemcpyDeviceToHost, g.s), "D2H");
-  hchk(hipStreamSynchronize(g.s), "sync");
+  // each rank encodes its range (records are framed one by one, so the ranges' encodings
+  // concatenate); across processes the ranges' bytes are all-gathered, padded to the largest
+  std::vector<uint64_t> totals(g.rk.size(), 0);
+  each_rank(g, [&](RankDev& r) {
+    if (!r.n) return;
+    pz_validator_cols v{};
+    v.balance = r.balance.p;
+    v.start_dynasty = r.start.p;
+    v.end_dynasty = r.end.p;
+    if (g.has_pk) v.public_key = g.pubkey.p;
+    if (g.has_ws) v.withdrawal_shard = g.wshard.p;
+    if (g.has_wa) { v.withdrawal_address = g.wa.p; v.withdrawal_address_offs = g.wa_offs.p; }
+    if (g.has_rc) { v.randao_commitment = g.rc.p; v.randao_commitment_offs = g.rc_offs.p; }
+    WireValArgs a;
+    check(wire_val_args(&v, r.n, 11, &a));
+    const uint64_t bound = pz_wire_validators_bound(r.n, g.val_bytes);
+    check(r.w_out.alloc(bound));
+    check(r.w_scratch.alloc(wire_tiles(r.n) + 1));
+    check(r.w_total.alloc(1));
+    a.out = r.w_out.p;
+    a.total = r.w_total.p;
+    hchk(launch_wire_validators(a, r.w_scratch.p, r.s), "pz_wire_val_kernel");
+  });
+  each_rank(g, [&](RankDev& r) {
+    if (!r.n) return;
+    uint64_t t = 0;
+    hchk(hipMemcpyAsync(&t, r.w_total.p, 8, hipMemcpyDeviceToHost, r.s), "D2H");
+    hchk(hipStreamSynchronize(r.s), "sync");
+    totals[&r - g.rk.data()] = t;
+  });
+  g.val_enc.clear();
+  if (g.world == (int)g.rk.size()) {  // every range is in this process
+    for (size_t i = 0; i < g.rk.size(); ++i) {
+      RankDev& r = g.rk[i];
+      if (!totals[i]) continue;
+      const size_t at = g.val_enc.size();
+      g.val_enc.resize(at + totals[i]);
+      hchk(hipSetDevice(r.dev), "hipSetDevice");
+      hchk(hipMemcpyAsync(&g.val_enc[at], r.w_out.p, totals[i], hipMemcpyDeviceToHost, r.s), "D2H");
+      hchk(hipStreamSynchronize(r.s), "sync");
+    }
+  } else {  // one local rank per process: all-gather the lengths, then the padded encodings
+    RankDev& r = g.rk[0];
+    hchk(hipSetDevice(r.dev), "hipSetDevice");
+    DevArr<uint64_t> len1, lens;
+    check(len1.alloc(1));
+    check(lens.alloc(g.world));
+    hchk(hipMemcpyAsync(len1.p, &totals[0], 8, hipMemcpyHostToDevice, r.s), "H2D");
+    hipEvent_t ev;
+    hchk(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
+    const void* snd = len1.p;
+    void* rcv = lens.p;
+    int rc = g.comm->allgather(&snd, &rcv, 8, &r.s, &ev);
+    std::vector<uint64_t> all(g.world);
+    if (!rc) {
+      hchk(hipStreamWaitEvent(r.s, ev, 0), "wait");
+      hchk(hipMemcpyAsync(all.data(), lens.p, g.world * 8, hipMemcpyDeviceToHost, r.s), "D2H");
+      hchk(hipStreamSynchronize(r.s), "sync");
+    }
+    uint64_t mx = 1;
+    for (uint64_t x : all) mx = std::max(mx, x);
+    DevArr<uint8_t> pad, gath;
+    if (!rc) {
+      check(pad.alloc(mx));
+      check(gath.alloc(mx * g.world));
+      if (totals[0]) hchk(hipMemcpyAsync(pad.p, r.w_out.p, totals[0], hipMemcpyDeviceToDevice, r.s), "D2D");
+      const void* s2 = pad.p;
+      void* r2 = gath.p;
+      rc = g.comm->allgather(&s2, &r2, mx, &r.s, &ev);
+    }
+    if (!rc) {
+      std::vector<uint8_t> hostg(mx * g.world);
+      hchk(hipStreamWaitEvent(r.s, ev, 0), "wait");
+      hchk(hipMemcpyAsync(hostg.data(), gath.p, hostg.size(), hipMemcpyDeviceToHost, r.s), "D2H");
+      hchk(hipStreamSynchronize(r.s), "sync");
+      for (int w = 0; w < g.world; ++w) g.val_enc.append((const char*)hostg.data() + (size_t)w * mx, all[w]);
+    }
+    (void)hipEventDestroy(ev);
+    check(rc);
+  }
   g.val_enc_valid = true;
   return g.val_enc;
 }
@@ -1023,16 +1188,43 @@ static void init_tail(Engine& g, const std::vector<uint32_t>& members, const std
   g.ncomm = g.csize.size();
   g.cwords = 1;
   for (uint64_t k : g.csize) g.cwords = std::max<uint64_t>(g.cwords, (k + 31) / 32);
-  upload(g, g.committee, members.data(), members.size());
-  upload(g, g.coffs, offs.data(), offs.size());
-  upload(g, g.balance, g.h_balance.data(), n);
-  upload(g, g.start, g.h_start.data(), n);
-  upload(g, g.end, g.h_end.data(), n);
-  g.words = (n + 31) / 32;
-  check(g.e_mask.alloc((n + 63) / 64 + 1));
-  check(g.e_blk.alloc(vblocks_per_inst(n) + 1));
-  check(g.e_list.alloc(n + 1));
-  hchk(hipStreamSynchronize(g.s), "sync");
+  // 64-aligned validator ranges, as pz_epoch_state / pz_comm_vote_tally split them
+  const uint64_t span = 64 * std::max<uint64_t>(1, (n + 64ull * g.world - 1) / (64ull * g.world));
+  each_rank(g, [&](RankDev& r) {
+    r.lo = std::min<uint64_t>(n, (uint64_t)r.grank * span);
+    r.hi = std::min<uint64_t>(n, (uint64_t)(r.grank + 1) * span);
+    if (g.world == 1) r.lo = 0, r.hi = n;
+    r.n = r.hi - r.lo;
+    r.words = (r.n + 31) / 32;
+    upload(r, r.committee, members.data(), members.size());
+    upload(r, r.coffs, offs.data(), offs.size());
+    upload(r, r.balance, g.h_balance.data() + r.lo, r.n);
+    upload(r, r.start, g.h_start.data() + r.lo, r.n);
+    upload(r, r.end, g.h_end.data() + r.lo, r.n);
+    if (g.world > 1) {  // the members inside [lo, hi) and their committee positions
+      std::vector<uint32_t> mem, pos;
+      std::vector<uint64_t> lo_offs(offs.size(), 0);
+      for (size_t c = 0; c + 1 < offs.size(); ++c) {
+        for (uint64_t k = offs[c]; k < offs[c + 1]; ++k) {
+          const uint32_t v = members[k];
+          if ((v >= r.lo && v < r.hi) || (r.grank == 0 && v >= n)) {
+            mem.push_back(v);
+            pos.push_back((uint32_t)(k - offs[c]));
+          }
+        }
+        lo_offs[c + 1] = mem.size();
+      }
+      mem.push_back(0);
+      pos.push_back(0);
+      upload(r, r.lcomm, mem.data(), mem.size());
+      upload(r, r.lcpos, pos.data(), pos.size());
+      upload(r, r.lcoffs, lo_offs.data(), lo_offs.size());
+    }
+    check(r.e_mask.alloc((r.n + 63) / 64 + 1));
+    check(r.e_blk.alloc(vblocks_per_inst(r.n) + 1));
+    check(r.e_list.alloc(r.n + 1));
+    hchk(hipStreamSynchronize(r.s), "sync");
+  });
   auto A = std::make_shared<AState>();
   g.hlog.clear();
   g.id_slot.clear();
@@ -1574,25 +1766,67 @@ struct pz_chain {
 
 extern "C" {
 
-int pz_chain_new(uint64_t nval, int device, pz_chain** out) {
+// The chain's ranks: one on `device`, or one per local rank of `comm` (each on its device).
+static void make_ranks(Engine& g, int device, pz_comm* comm) {
+  g.comm = comm;
+  g.world = comm ? comm->world : 1;
+  const int L = comm ? comm->nlocal : 1;
+  g.rk.resize(L);
+  for (int i = 0; i < L; ++i) {
+    RankDev& r = g.rk[i];
+    r.dev = comm ? comm->dev[i] : device;
+    r.grank = comm ? comm->rank0 + i : 0;
+    check(pz_init(r.dev));
+    hchk(hipSetDevice(r.dev), "hipSetDevice");
+    hchk(hipStreamCreateWithFlags(&r.s, hipStreamNonBlocking), "hipStreamCreate");
+  }
+  g.device = g.rk[0].dev;
+  g.s = g.rk[0].s;
+  hchk(hipSetDevice(g.device), "hipSetDevice");
+}
+
+static void destroy_chain(pz_chain* c) {
+  Engine& g = c->g;
+  std::vector<std::pair<int, hipStream_t>> streams;
+  for (RankDev& r : g.rk) {
+    (void)hipSetDevice(r.dev);
+    if (r.s) (void)hipStreamSynchronize(r.s);
+    for (hipEvent_t e : {r.q_ev, r.ev_epoch, r.ev_red, r.ev_nb, r.ev_t64})
+      if (e) (void)hipEventDestroy(e);
+    streams.push_back({r.dev, r.s});
+  }
+  if (g.q_arena) (void)hipHostFree(g.q_arena);
+  if (g.ev_totals) (void)hipEventDestroy(g.ev_totals);
+  delete c;
+  for (auto& ds : streams)
+    if (ds.second) {
+      (void)hipSetDevice(ds.first);
+      (void)hipStreamDestroy(ds.second);
+    }
+}
+
+static int new_chain(uint64_t nval, int device, pz_comm* comm, pz_chain** out) {
   if (!out) return fail(PZ_EINVAL, "out is null");
   *out = nullptr;
   if (nval == 0 || nval > PZ_MAX_VALIDATORS) return fail(PZ_ETOOMANY, "validator count %llu out of range", (unsigned long long)nval);
-  int rc = pz_init(device);
-  if (rc) return rc;
   auto* c = new pz_chain();
   c->g.nval = nval;
-  c->g.device = device;
   try {
-    hchk(hipStreamCreateWithFlags(&c->g.s, hipStreamNonBlocking), "hipStreamCreate");
+    make_ranks(c->g, device, comm);
     check(genesis(c->g));
   } catch (int e) {
-    if (c->g.s) (void)hipStreamDestroy(c->g.s);
-    delete c;
+    destroy_chain(c);
     return e;
   }
   *out = c;
   return PZ_OK;
+}
+
+int pz_chain_new(uint64_t nval, int device, pz_chain** out) { return new_chain(nval, device, nullptr, out); }
+
+int pz_chain_new_comm(uint64_t nval, pz_comm* comm, pz_chain** out) {
+  if (!comm) return fail(PZ_EINVAL, "comm is null");
+  return new_chain(nval, 0, comm, out);
 }
 
 int pz_chain_new_from_state(const uint8_t* cstate, uint64_t len, const uint8_t* saved_hashes, uint64_t nsaved,
@@ -1601,12 +1835,9 @@ int pz_chain_new_from_state(const uint8_t* cstate, uint64_t len, const uint8_t* 
   *out = nullptr;
   if (!cstate || !len) return fail(PZ_EINVAL, "empty stored state");
   if (nsaved && !saved_hashes) return fail(PZ_EINVAL, "saved_hashes is null");
-  int rc = pz_init(device);
-  if (rc) return rc;
   auto* c = new pz_chain();
-  c->g.device = device;
   try {
-    hchk(hipStreamCreateWithFlags(&c->g.s, hipStreamNonBlocking), "hipStreamCreate");
+    make_ranks(c->g, device, nullptr);
     check(reload(c->g, cstate, len));
     for (uint64_t i = 0; i < nsaved; ++i) {
       H32 h;
@@ -1614,8 +1845,7 @@ int pz_chain_new_from_state(const uint8_t* cstate, uint64_t len, const uint8_t* 
       c->g.saved.insert(h);
     }
   } catch (int e) {
-    if (c->g.s) (void)hipStreamDestroy(c->g.s);
-    delete c;
+    destroy_chain(c);
     return e;
   }
   *out = c;
@@ -1624,16 +1854,7 @@ int pz_chain_new_from_state(const uint8_t* cstate, uint64_t len, const uint8_t* 
 
 void pz_chain_free(pz_chain* c) {
   if (!c) return;
-  (void)hipSetDevice(c->g.device);
-  if (c->g.s) (void)hipStreamSynchronize(c->g.s);
-  if (c->g.q_arena) (void)hipHostFree(c->g.q_arena);
-  if (c->g.h_err) (void)hipHostFree(c->g.h_err);
-  if (c->g.q_arena_ev) (void)hipEventDestroy(c->g.q_arena_ev);
-  if (c->g.ev_totals) (void)hipEventDestroy(c->g.ev_totals);
-  if (c->g.ev_epoch) (void)hipEventDestroy(c->g.ev_epoch);
-  hipStream_t s = c->g.s;
-  delete c;
-  if (s) (void)hipStreamDestroy(s);
+  destroy_chain(c);
 }
 
 int pz_count_attestations(const uint8_t* blocks, const uint64_t* offsets, uint64_t n, uint64_t* count) {
@@ -1752,17 +1973,46 @@ int pz_chain_vote_totals(pz_chain* c, uint8_t* hashes, uint64_t* totals, uint64_
   std::lock_guard<std::mutex> lk(c->g.mu);
   Engine& g = c->g;
   const AState& A = g.has_cand ? *g.cand_A : *g.A;
-  // the Go map holds the hashes some attestation signed (present), with their totals
+  // the Go map holds the hashes some attestation signed (present), with their totals: the
+  // sum of the ranks' partial VoteTotalDeposit (an all-reduce of a copy across processes)
   std::vector<uint8_t> pres;
   std::vector<uint64_t> tot;
   if (!A.cache_nil && !g.slot_hash.empty()) {
-    pres.resize(g.slot_hash.size());
-    tot.resize(g.slot_hash.size());
-    hipError_t e = hipSetDevice(g.device);
-    if (e == hipSuccess) e = hipMemcpyAsync(pres.data(), g.present.p, pres.size(), hipMemcpyDeviceToHost, g.s);
-    if (e == hipSuccess) e = hipMemcpyAsync(tot.data(), g.totals.p, tot.size() * 8, hipMemcpyDeviceToHost, g.s);
-    if (e == hipSuccess) e = hipStreamSynchronize(g.s);
-    if (e != hipSuccess) return hip_fail(e, "D2H vote totals");
+    const uint64_t ns = g.slot_hash.size();
+    pres.resize(ns);
+    tot.assign(ns, 0);
+    try {
+      RankDev& r0 = g.rk[0];
+      hchk(hipSetDevice(r0.dev), "hipSetDevice");
+      hchk(hipMemcpyAsync(pres.data(), r0.present.p, ns, hipMemcpyDeviceToHost, r0.s), "D2H");
+      if (g.world == (int)g.rk.size()) {
+        std::vector<uint64_t> part(ns);
+        for (RankDev& r : g.rk) {
+          hchk(hipSetDevice(r.dev), "hipSetDevice");
+          hchk(hipMemcpyAsync(part.data(), r.totals.p, ns * 8, hipMemcpyDeviceToHost, r.s), "D2H");
+          hchk(hipStreamSynchronize(r.s), "sync");
+          for (uint64_t i = 0; i < ns; ++i) tot[i] += part[i];
+        }
+      } else {
+        DevArr<uint64_t> cp;
+        check(cp.alloc(ns));
+        hchk(hipMemcpyAsync(cp.p, r0.totals.p, ns * 8, hipMemcpyDeviceToDevice, r0.s), "D2D");
+        hipEvent_t ev;
+        hchk(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
+        uint64_t* b = cp.p;
+        int rc = g.comm->allreduce_u64(&b, ns, &r0.s, &ev);
+        if (!rc) {
+          hchk(hipStreamWaitEvent(r0.s, ev, 0), "wait");
+          hchk(hipMemcpyAsync(tot.data(), cp.p, ns * 8, hipMemcpyDeviceToHost, r0.s), "D2H");
+          hchk(hipStreamSynchronize(r0.s), "sync");
+        }
+        (void)hipEventDestroy(ev);
+        check(rc);
+      }
+      hchk(hipStreamSynchronize(r0.s), "sync");
+    } catch (int rc) {
+      return rc;
+    }
   }
   uint64_t n = 0;
   for (uint8_t p : pres) n += p;

@@ -32,6 +32,18 @@ struct VoteIdArgs {
   uint32_t* leader;  // the items that tally their group (compact list, *nlead entries)
   uint32_t* nlead;
   uint64_t ncomm, cwords;
+  uint64_t val_offset;   // a validator-range shard: balance and bitmaps hold [val_offset, val_offset + nval)
+  uint64_t nval_global;  // of nval_global validators (0: nval, unsharded)
 };
 hipError_t launch_vote_ids(const VoteIdArgs& a, hipStream_t s);
+
+// The 64 totals a stateRecalc's justification loop reads (blockchain/core.go:413-418) and the
+// sticky tally panic flag, gathered into out[0..64] (slot UINT32_MAX: no map entry, total 0):
+// one small D2H (or one 65-word all-reduce of a validator-range-sharded cache) per transition.
+constexpr int kJustifySlots = 64;
+struct VoteGatherSlots {
+  uint32_t slot[kJustifySlots];
+};
+hipError_t launch_vote_gather(const uint64_t* totals, VoteGatherSlots slots, const uint64_t* err, uint64_t* out,
+                              hipStream_t s);
 }  // namespace pz

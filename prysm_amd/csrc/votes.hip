@@ -119,7 +119,7 @@ pz_vote_leader_kernel(VoteIdArgs a) {
     uint32_t* u = a.ubits + grp * a.cwords;
     const uint64_t k = a.coffs[c + 1] - a.coffs[c];
     tally_item(a.committee, a.coffs, c, reinterpret_cast<const uint8_t*>(u), (k + 7) / 8, a.balance, a.nval,
-               a.bitmaps + (uint64_t)slot * a.words_per_slot, a.totals + slot, a.err);
+               a.bitmaps + (uint64_t)slot * a.words_per_slot, a.totals + slot, a.err, a.val_offset, a.nval_global);
     // leave the group empty for the next flush
     for (uint64_t w = threadIdx.x & 63; w < a.cwords; w += 64) u[w] = 0;
     if ((threadIdx.x & 63) == 0) a.uflag[grp] = 0;
@@ -133,6 +133,21 @@ hipError_t launch_vote_ids(const VoteIdArgs& a, hipStream_t s) {
   const uint64_t uthreads = a.natt * 64 * kUnionLanes;
   hipLaunchKernelGGL(pz_vote_union_kernel, dim3((uint32_t)((uthreads + 255) / 256)), dim3(256), 0, s, a);
   hipLaunchKernelGGL(pz_vote_leader_kernel, dim3(kLeaderWaves / 4), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+extern "C" __global__ void __launch_bounds__(64)
+pz_vote_gather_kernel(const uint64_t* __restrict__ totals, VoteGatherSlots q, const uint64_t* __restrict__ err,
+                      uint64_t* __restrict__ out) {
+  const int j = threadIdx.x;
+  const uint32_t sl = q.slot[j];
+  out[j] = sl == 0xFFFFFFFFu ? 0 : totals[sl];
+  if (j == 0) out[kJustifySlots] = err ? *err : 0;
+}
+
+hipError_t launch_vote_gather(const uint64_t* totals, VoteGatherSlots slots, const uint64_t* err, uint64_t* out,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(pz_vote_gather_kernel, dim3(1), dim3(kJustifySlots), 0, s, totals, slots, err, out);
   return hipGetLastError();
 }
 

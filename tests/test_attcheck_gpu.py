@@ -95,11 +95,13 @@ def test_empty_batch():
     assert len(status) == 0
 
 
+@pytest.mark.parametrize("lastb", [False, True])
 @pytest.mark.parametrize("natt,shift", [(4097, 0), (4096, 1), (1, 0)])
-def test_device_forms_match_c_port(natt, shift):
+def test_device_forms_match_c_port(natt, shift, lastb):
     """pz_dev_check_attestations on bench.attcheck_columns' inputs: 16-B-aligned columns take
     the two-per-lane kernel (odd tail included), columns shifted by one element the one-per-lane
-    kernel; both equal the C port (oracle/c/attcheck_ref.c)."""
+    kernel; both equal the C port (oracle/c/attcheck_ref.c), with the trailing-bits byte read
+    from the bitfields or from the caller's last-byte column."""
     import ctypes
 
     import torch
@@ -117,7 +119,10 @@ def test_device_forms_match_c_port(natt, shift):
         return buf, buf[shift:]
 
     keep, t = [], {}
-    for k, v in list(cols.items()) + list(tab.items()):
+    extra = {}
+    if lastb:
+        extra["last_byte"] = cols["bits"][(cols["boffs"][1:].astype(np.int64) - 1) % cols["bits"].size]
+    for k, v in list(cols.items()) + list(tab.items()) + list(extra.items()):
         buf, view = put(v)
         keep.append(buf)
         t[k] = view
@@ -128,7 +133,8 @@ def test_device_forms_match_c_port(natt, shift):
                            t["n_oblique"].data_ptr(), t["bits"].data_ptr(), t["boffs"].data_ptr(),
                            t["block_slot"].data_ptr(), 0, 0, 128, 256, t["arr_offs"].data_ptr(),
                            t["arr_shard"].data_ptr(), t["arr_comm"].data_ptr(), t["coffs"].data_ptr(),
-                           status.data_ptr(), comm.data_ptr(), pstart.data_ptr())
+                           status.data_ptr(), comm.data_ptr(), pstart.data_ptr(),
+                           t["last_byte"].data_ptr() if lastb else None)
     _lib.lib.call("pz_dev_check_attestations", ctypes.byref(b), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     torch.cuda.synchronize()
     port = cport.AttCheck(cols["slot"], cols["justified_slot"], cols["shard_id"], cols["n_oblique"], cols["bits"],

@@ -65,10 +65,11 @@ def test_bench_world2_gloo_rehearsal():
 
 @pytest.mark.gpu
 def test_bench_single_process_one_device():
-    r = _run(["--single-process", "--gpus", "1", "--records", "4096", "--steps", "2", "--warmup", "1",
+    r = _run(["--single-process", "--gpus", "1", "--records", "4096", "--steps", "2", "--warmup", "1", "--replay-blocks", "130",
               "--clock-warm-ms", "0"], 600)
     assert r.returncode == 0, r.stderr[-3000:]
     (line,) = _json_lines(r.stdout)
     assert line["rccl_world"] == 1 and line["rccl_nlocal"] == 1
     assert line["epoch"]["config"]["layout"] == "committee order, one-pass step"
     assert line["hash"]["value"] > 0 and line["epoch"]["value"] > 0
+    assert line["replay_one_chain"]["transitions"] == 2

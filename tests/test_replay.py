@@ -347,3 +347,67 @@ def test_gpu_reload_rejects_undecodable_state():
     with pytest.raises(_lib.PzError) as ei:
         BeaconChain.from_state(b"\x0a\xff", [])
     assert ei.value.code == _lib.PZ_EINVAL
+
+
+# ---- one chain over a communicator (the vote cache and the epoch sharded
+# by validator range; on the one-GPU test box over the loopback communicator, every rank on
+# cuda:0 with the same code RCCL drives) ---------------------------------------------------------
+def _sharded(nval, blocks, world):
+    from prysm_amd.blockchain import BeaconChain
+    from prysm_amd.native import Comm
+    comm = Comm.devices(1) if world == "rccl1" else Comm.loopback(world)
+    ch = BeaconChain(nval, comm=comm)
+    recs = ch.process_blocks(blocks)
+    return recs, ch.roots()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 3, 8, "rccl1"])
+def test_gpu_sharded_chain_matches_golden(world):
+    g = golden()
+    recs, roots = _sharded(g["nval"], synth.chain_blocks(g["nval"], g["nblocks"], seed=g["seed"]), world)
+    _compare(recs, roots, g)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_sharded_chain_rejections_vs_oracle(world):
+    from oracle import replay
+    blocks = edited_chain()
+    o_recs, o_roots = replay.replay(blocks, 1000)
+    recs, roots = _sharded(1000, blocks, world)
+    strip = lambda rs: [{**r, "atts": [a if "error" not in a else {"error": True} for a in r["atts"]]} for r in rs]  # noqa: E731
+    assert strip(_hexrecs(recs)) == strip(_hexrecs(o_recs))
+    for k in ("chain_active", "chain_crystallized", "cand_active", "cand_crystallized"):
+        assert roots[k] == o_roots[k], k
+    assert roots["vote_totals"] == o_roots["vote_totals"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_sharded_chain_reward_panic(world):
+    from prysm_amd.blockchain import BeaconChain, ChainPanic
+    from prysm_amd.native import Comm
+    g = golden()
+    ch = BeaconChain(g["nval"], comm=Comm.loopback(world))
+    with pytest.raises(ChainPanic):
+        ch.process_blocks(synth.chain_blocks(g["nval"], 70, seed=g["seed"], participation=(1.0,)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_sharded_chain_configs4_full_vs_c_port(world):
+    """BASELINE configs[4] as ONE chain over `world` ranks: the 10,000-block, 156-transition
+    chain at 65,536 validators, every block, attestation, root and vote-cache total bit-exact
+    against the C restatement of the block pipeline."""
+    from prysm_amd.blockchain import BeaconChain, serialize_blocks
+    from prysm_amd.native import Comm
+    from replay_port_helpers import mismatches, port_replay
+    nval = 65536
+    blocks = synth.chain_blocks(nval, 10000, seed=6)
+    data, offs = serialize_blocks(blocks)
+    ch = BeaconChain(nval, comm=Comm.loopback(world))
+    br, ar = ch.process_serialized(data, offs)
+    assert int(br["transition"].sum()) == 156
+    out, port_roots = port_replay(data, offs, nval, len(ar))
+    assert mismatches(br, ar, ch.roots(), out, port_roots) == []
