@@ -14,7 +14,12 @@
 //   write  one 16-lane DPP row per record: the record is assembled in an LDS stage (literals
 //          by the row's lanes, data segments copied with aligned dword loads) and stored in
 //          16-byte blocks
-// The columns of a record are read twice (size, write); the output is written once.
+// The columns of a record are read twice (size, write); the output is written once.  A
+// one-launch form (pz_wire_att_kernel below: tiles of 256 records, a decoupled look-back, the
+// writes in 16 rounds per workgroup) is exact but 2.8x slower (1.085 against 0.382 ms per 1M
+// records, profiles/r03/wire_att_onepass_dropped_r3g.txt): each workgroup's 16 rounds run
+// their dependent round trips one after another, and the loop spills 56 VGPRs at 8 waves per
+// SIMD.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -43,6 +48,8 @@ struct AttArgs {
   uint64_t* sizes;
   uint64_t* offs;  // n+1
   uint8_t* out;
+  uint64_t* status;  // one-pass kernel: [tiles] look-back status words, zero at launch
+  uint32_t* ticket;  // one-pass kernel: tile ticket, zero at launch
 };
 
 __device__ __forceinline__ uint32_t vlen(uint64_t x) { return (uint32_t)((70 - __clzll(x | 1)) / 7); }
@@ -285,16 +292,18 @@ __device__ __forceinline__ uint32_t rscan32(uint32_t x) {
   return x;
 }
 
-template <int W>
-__device__ __forceinline__ void wire_att_write_body(const AttArgs& a) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kWaves][kRecs][kStageAlloc];
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+// The wave's records i0 .. i0 + 3, one per DPP row.  Output offsets: from a.offs (the
+// three-launch form), or -- the one-pass kernel -- base + excl[local0 + r] for the wave's r-th
+// record (excl: the tile's exclusive size scan in LDS, excl[tile size] = the tile's total).
+template <bool FUSED>
+__device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*stage)[kStageAlloc], uint64_t i0,
+                                                    const uint64_t* excl, uint64_t base, uint32_t local0) {
+  const int lane = threadIdx.x & 63;
   const int sl = lane & (kRow - 1), ri = lane / kRow;
-  const uint64_t i0 = ((uint64_t)blockIdx.x * kWaves + w) * kRecs;  // the wave's records: i0 .. i0 + 3
   if (i0 >= a.n) return;
   const uint64_t i = i0 + ri;
   const bool valid = i < a.n;
-  const uint64_t hv = valid && sl < kHeadWords ? head_word(a, sl, i) : 0;
+  const uint64_t hv = valid && sl < (FUSED ? kHeadWords - 2 : kHeadWords) ? head_word(a, sl, i) : 0;
   Head h;
   h.v[0] = bc64<0>(hv);
   h.v[1] = bc64<1>(hv);
@@ -309,7 +318,15 @@ __device__ __forceinline__ void wire_att_write_body(const AttArgs& a) {
   h.o1 = bc64<10>(hv);
   h.s0 = bc64<11>(hv);
   h.s1 = bc64<12>(hv);
-  const uint64_t o = bc64<13>(hv), size = bc64<14>(hv) - o;
+  uint64_t o, size;
+  if (FUSED) {
+    const uint64_t e0 = valid ? excl[local0 + ri] : 0, e1 = valid ? excl[local0 + ri + 1] : 0;
+    o = base + e0;
+    size = e1 - e0;
+  } else {
+    o = bc64<13>(hv);
+    size = bc64<14>(hv) - o;
+  }
   const uint64_t nob = h.o1 - h.o0, nsig = h.s1 - h.s0;
   bool fast = valid && size <= kStage && nob <= kMaxOblique && nsig <= kRow;
   // one sub-lane per element / signature value; segment s = sub-lane s
@@ -353,7 +370,7 @@ __device__ __forceinline__ void wire_att_write_body(const AttArgs& a) {
   for (int k = 0; k <= (int)kSegWords; ++k) wv[k] = (uint32_t)k < nw ? ws[k] : 0;
   // 1. layout
   const uint32_t sh = (uint32_t)o & 15;
-  uint8_t* st = stage[w][ri] + sh;
+  uint8_t* st = stage[ri] + sh;
   uint32_t seg_dst = 0;
   if (fast) {  // row-uniform, so the row's DPP reads below see only active lanes
     // Lane-parallel: sub-lane k (1-8) owns item k of the record -- fields 1-3 (tag +
@@ -415,7 +432,7 @@ __device__ __forceinline__ void wire_att_write_body(const AttArgs& a) {
   // 3. store: stage block q <-> output block (o >> 4) + q
   const uint32_t sz = fast ? (uint32_t)size : 0;
   const uint32_t nblk = (sh + sz + 15) / 16;
-  const uint8_t* sb = stage[w][ri];
+  const uint8_t* sb = stage[ri];
   uint8_t* ob = a.out + (o - sh);
   for (uint32_t q = sl; q < nblk; q += kRow) {
     const uint32_t lo = 16 * q, hi = lo + 16;
@@ -443,7 +460,129 @@ __device__ __forceinline__ void wire_att_write_body(const AttArgs& a) {
     g.s1 = rl64(hv, kRow * u + 12);
     uint64_t fixed, obl8, sigb8;
     record_parts(a, g, &fixed, &obl8, &sigb8);
-    write_record(a, g, body_size(fixed, obl8, sigb8), sigb8, a.out + rl64(hv, kRow * u + 13));
+    const uint64_t ou = FUSED ? base + excl[local0 + u] : rl64(hv, kRow * u + 13);
+    write_record(a, g, body_size(fixed, obl8, sigb8), sigb8, a.out + ou);
+  }
+}
+
+template <int W>
+__device__ __forceinline__ void wire_att_write_body(const AttArgs& a) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kWaves][kRecs][kStageAlloc];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t i0 = ((uint64_t)blockIdx.x * kWaves + w) * kRecs;  // the wave's records: i0 .. i0 + 3
+  wire_att_write_rows<false>(a, stage[w], i0, nullptr, 0, 0);
+}
+
+// ---- one pass: sizes, a decoupled look-back and the writes in one launch -------------------
+// A workgroup takes tiles of kTile records by ticket (predecessors always started first, so the
+// look-back never waits on a tile that is not running).  Phase 1 sizes the tile's records, one
+// lane each (the size kernel's body: coalesced heads, independent element / value loads), and
+// block-scans them; the tile publishes its aggregate, looks back for its exclusive base and
+// publishes its inclusive prefix (status words: flag in the top two bits, value below, one
+// relaxed agent-scope store or load each -- no fence, which on gfx950 writes back L2).  Phase
+// 2 writes the records, 16 per round, one per DPP row (wire_att_write_rows): their heads come
+// back from L2, the segment bytes once from HBM.  Against size + scan + write it drops the
+// size kernel's re-read of every head and element offset from HBM, the sizes array, the scan's
+// two launches and the write kernel's offset loads.
+constexpr uint32_t kTile = kThreads;
+constexpr uint64_t kFlagA = 1ull << 62, kFlagP = 2ull << 62, kVal = kFlagA - 1;
+
+__device__ __forceinline__ uint64_t ld_status(uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_status_fresh(uint64_t* p) {  // at the coherence point
+  return __hip_atomic_fetch_add(p, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The tile's exclusive base: windows of kTile predecessors, one status word per thread; the
+// nearest inclusive prefix (P) ends the walk, the aggregates (A) nearer than it are added.
+__device__ uint64_t lookback_tile(uint64_t* status, uint64_t tile, uint32_t* s_first, uint64_t* s_part) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint64_t prefix = 0;
+  for (int64_t j = (int64_t)tile - 1;; j -= kTile) {
+    const int64_t idx = j - tid;
+    uint64_t v = idx >= 0 ? ld_status(status + idx) : kFlagP;  // before tile 0: prefix 0
+    for (uint32_t spins = 0; !(v >> 62); ++spins) {
+      __builtin_amdgcn_s_sleep(1);
+      v = spins < 256 ? ld_status(status + idx) : ld_status_fresh(status + idx);
+    }
+    if (tid == 0) *s_first = kTile;
+    __syncthreads();
+    const uint64_t pm = __ballot((v >> 62) == 2);
+    if (pm && lane == (int)__builtin_ctzll(pm)) atomicMin(s_first, (uint32_t)tid);
+    __syncthreads();
+    const uint32_t first = *s_first;
+    uint64_t part = (uint32_t)tid <= first ? (v & kVal) : 0;
+    part = wsum(part);
+    if (lane == 0) s_part[w] = part;
+    __syncthreads();
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) sum += s_part[k];
+    __syncthreads();  // s_first / s_part are rewritten by the next window
+    prefix += sum;
+    if (first < kTile) return prefix;
+  }
+}
+
+__device__ __forceinline__ uint64_t record_size(const AttArgs& a, uint64_t i) {
+  Head h;
+  load_head(a, i, h);
+  uint64_t body = 0, sigb = 0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    body += h.v[k] ? 1 + vlen(h.v[k]) : 0;
+    body += h.bl[k] ? 1 + vlen(h.bl[k]) + h.bl[k] : 0;
+  }
+#pragma unroll 4
+  for (uint64_t e = h.o0; e < h.o1; ++e) {
+    const uint64_t l = a.ooff[e + 1] - a.ooff[e];
+    body += 1 + vlen(l) + l;
+  }
+#pragma unroll 4
+  for (uint64_t e = h.s0; e < h.s1; ++e) sigb += vlen(a.sig[e]);
+  body += sigb ? 1 + vlen(sigb) + sigb : 0;
+  return a.field ? a.tag_len + vlen(body) + body : body;
+}
+
+extern "C" __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))
+pz_wire_att_kernel(AttArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kWaves][kRecs][kStageAlloc];
+  __shared__ uint64_t s_excl[kTile + 1], s_wave[kWaves], s_part[kWaves], s_base;
+  __shared__ uint32_t s_tile, s_first;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tid == 0) s_tile = atomicAdd(a.ticket, 1u);
+  __syncthreads();
+  const uint64_t tile = s_tile, t0 = tile * kTile;
+  if (t0 >= a.n) return;  // (never: the grid has exactly the tiles)
+  const uint64_t i = t0 + tid;
+  const uint64_t size = i < a.n ? record_size(a, i) : 0;
+  const uint64_t incl = wscan(size);
+  if (lane == 63) s_wave[w] = incl;
+  __syncthreads();
+  uint64_t before = 0, agg = 0;
+#pragma unroll
+  for (int k = 0; k < kWaves; ++k) {
+    before += k < w ? s_wave[k] : 0;
+    agg += s_wave[k];
+  }
+  s_excl[tid] = before + incl - size;
+  if (tid == 0) {
+    s_excl[kTile] = agg;
+    st_status(a.status + tile, (tile == 0 ? kFlagP : kFlagA) | agg);
+  }
+  const uint64_t base = tile == 0 ? 0 : lookback_tile(a.status, tile, &s_first, s_part);
+  if (tid == 0 && tile > 0) st_status(a.status + tile, kFlagP | (base + agg));
+  if (i < a.n) a.offs[i + 1] = base + before + incl;
+  if (i == 0) a.offs[0] = 0;
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t r = 0; r < kTile / (kWaves * kRecs); ++r) {
+    const uint32_t local0 = (r * kWaves + w) * kRecs;
+    wire_att_write_rows<true>(a, stage[w], t0 + local0, s_excl, base, local0);
   }
 }
 
@@ -511,7 +650,21 @@ hipError_t launch_sizes_offsets(AttArgs a, void* scratch, hipStream_t s) {
                                  a.offs + 1, (size_t)a.n, rocprim::plus<uint64_t>(), s);
 }
 
-int g_att_write_variant = 0;  // tools/ A/B only: 1 = uncapped (7 waves per SIMD)
+int g_att_write_variant = 0;  // tools/ A/B only: 1 = uncapped (7 waves per SIMD), 2 = the looped one-pass kernel
+
+uint64_t att_tiles(uint64_t n) { return (n + kTile - 1) / kTile; }
+
+// The one-pass encode: status words and ticket (the scratch's head) reset, then one launch.
+hipError_t launch_one_pass(AttArgs a, void* scratch, hipStream_t s) {
+  if (!a.n) return hipMemsetAsync(a.offs, 0, 8, s);
+  const uint64_t tiles = att_tiles(a.n);
+  a.status = static_cast<uint64_t*>(scratch);
+  a.ticket = reinterpret_cast<uint32_t*>(a.status + tiles);
+  hipError_t e = hipMemsetAsync(scratch, 0, tiles * 8 + 8, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(pz_wire_att_kernel, dim3((uint32_t)tiles), dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_write(const AttArgs& a, hipStream_t s) {
   if (!a.n) return hipSuccess;
@@ -530,7 +683,9 @@ using namespace pz;
 
 extern "C" {
 
-uint64_t pz_wire_attestations_scratch_bytes(uint64_t n) { return ((n * 8 + 255) & ~uint64_t(255)) + scan_bytes(n); }
+uint64_t pz_wire_attestations_scratch_bytes(uint64_t n) {
+  return std::max<uint64_t>(((n * 8 + 255) & ~uint64_t(255)) + scan_bytes(n), att_tiles(n) * 8 + 8);
+}
 
 uint64_t pz_wire_attestations_bound(uint64_t n, uint64_t bytes_total, uint64_t n_oblique, uint64_t n_sig) {
   // frame 5+10, fields 1-3 3x11, fields 4-6 3x(1+10), field 8 header 11, per element 11, per value 10
@@ -546,8 +701,13 @@ int pz_dev_wire_attestations(const pz_attestation_cols* c, uint64_t n, uint32_t 
   a.out = d_out;
   a.offs = d_offsets;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipError_t e = launch_sizes_offsets(a, d_scratch, s);
-  if (e == hipSuccess) e = launch_write(a, s);
+  hipError_t e;
+  if (g_att_write_variant & 2) {  // tools/ A/B: the looped one-pass kernel (measured 2.8x slower)
+    e = launch_one_pass(a, d_scratch, s);
+  } else {
+    e = launch_sizes_offsets(a, d_scratch, s);
+    if (e == hipSuccess) e = launch_write(a, s);
+  }
   return e == hipSuccess ? PZ_OK : hip_fail(e, "pz_wire_att kernels");
 }
 

@@ -47,7 +47,7 @@ def main():
     ms = e0.elapsed_time(e1) / reps
     dll = _lib.lib.dll
     if hasattr(dll, "pz_debug_set_att_write_variant"):  # same-process A/B of the write kernel
-        for v in (0, 1, 0, 1, 0):
+        for v in (0, 2, 0, 2, 0):  # size + scan + write / the looped one-pass kernel
             dll.pz_debug_set_att_write_variant(v)
             e0.record()
             for _ in range(reps):
