@@ -16,7 +16,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -179,9 +181,9 @@ using AttP = std::shared_ptr<const Att>;
 // attestation record parsed from them, allocated once (per-record allocations made the parse
 // allocator-bound).  Records that stay pending after the call keep it alive.
 struct CallArena {
-  std::vector<uint8_t> bytes;
+  std::unique_ptr<uint8_t[]> bytes;  // (not zero-filled)
   std::vector<Att> atts;  // reserved to the exact count: AttP points into it
-  std::vector<std::pair<uint32_t, uint32_t>> obl;
+  std::vector<std::pair<uint32_t, uint32_t>> obl;  // reserved to a bound: Att::obl points into it
 };
 
 // messages.pb.go:889-896: 1-3 varint, 4-6 bytes, 7 repeated bytes, 8 packed varints
@@ -209,6 +211,7 @@ static bool parse_att(const uint8_t* p, size_t n, Att* a, std::vector<std::pair<
       if (f == 5) { a->sbh_off = (uint32_t)(q - base); a->sbh_len = (uint32_t)len; }
       if (f == 6) { a->bf_off = (uint32_t)(q - base); a->bf_len = (uint32_t)len; }
     } else if (f == 7) {
+      if (pool.size() == pool.capacity()) return false;  // (the bound makes this unreachable)
       pool.push_back({(uint32_t)(q - base), (uint32_t)len});
       ++a->obl.n;
     } else {  // f == 8: packed, never empty
@@ -218,6 +221,7 @@ static bool parse_att(const uint8_t* p, size_t n, Att* a, std::vector<std::pair<
       if (!s.ok) return false;
     }
   }
+  a->obl.p = pool.data() + a->obl_first;  // the pool never reallocates (reserved to a bound)
   return r.ok;
 }
 
@@ -334,7 +338,7 @@ struct PinBuf {
 
 enum ProfSlot {
   kProfParse, kProfHash1, kProfCheck, kProfQueue, kProfFlush, kProfRecalc, kProfMsgHash, kProfWalk, kProfProcess,
-  kProfCount, kProfSlots
+  kProfCount, kProfFlushWait, kProfSlots
 };
 
 // Queued attestations that force a tally flush before the next stateRecalc.  Flushing more
@@ -342,6 +346,17 @@ enum ProfSlot {
 // every 16 / 64 / 256 attestations gave 57k / 86k / 97k blocks/s against 102k for
 // flushing only at the transitions (10,000 blocks, 65,536 validators).
 constexpr size_t kFlushAtts = 1 << 16;
+
+// The pipelined walk's producer runs at most kRing chunks of kChunk blocks ahead (Feeder).
+constexpr uint64_t kChunk = 512;
+constexpr int kRing = 4;
+
+// Staging of one digest batch (pinned host buffers and their device copies).
+struct DigestBufs {
+  PinBuf msgs, offs, dig;
+  DevArr<uint8_t> d_in, d_out;
+  DevArr<uint64_t> d_offs;
+};
 
 // One local rank's device state.  An unsharded chain has one rank holding every validator;
 // a chain over a pz_comm (pz_chain_new_comm) gives each rank the
@@ -382,6 +397,10 @@ struct Engine {
   uint64_t nval = 0;
   int device = 0;
   hipStream_t s = nullptr;  // local rank 0's stream: hashing, the digest and message batches
+  hipStream_t s2 = nullptr;  // local rank 0's second stream: the pipelined digest batches
+  DigestBufs dbatch;         // the digest batch of an unpipelined call
+  DigestBufs ring[kRing];    // the pipelined calls' digest batches, reused chunk after chunk
+  hipEvent_t ring_ev[kRing] = {};
   pz_comm* comm = nullptr;  // null: one device, every validator
   int world = 1;
   std::vector<RankDev> rk;
@@ -468,6 +487,25 @@ struct PhaseTimer {
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
   explicit PhaseTimer(double& a) : acc(a) {}
   ~PhaseTimer() { acc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); }
+};
+// Per-attestation phases (checks, vote queueing) are timed only when PZ_CHAIN_PROFILE is set:
+// two clock reads per attestation cost ~4 ms per 10,000 blocks of the walk they measure.
+static bool fine_profile() {
+  static const bool on = std::getenv("PZ_CHAIN_PROFILE") != nullptr;
+  return on;
+}
+struct FineTimer {
+  double* acc = nullptr;
+  std::chrono::steady_clock::time_point t0;
+  explicit FineTimer(double& a) {
+    if (fine_profile()) {
+      acc = &a;
+      t0 = std::chrono::steady_clock::now();
+    }
+  }
+  ~FineTimer() {
+    if (acc) *acc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
 };
 
 struct Panic {
@@ -629,6 +667,7 @@ static bool flush_votes_enqueue(Engine& g) {
                o_ids = o_comm + al(natt * 4), o_slots = o_ids + al(g.q_ids.size() * 4),
                o_bits = o_slots + al(new_ids * 4), total = o_bits + al(g.q_bits.size());
   if (g.q_arena_busy) {
+    FineTimer pw(g.prof[kProfFlushWait]);
     for (RankDev& r : g.rk) hchk(hipEventSynchronize(r.q_ev), "event sync");
     g.q_arena_busy = false;
   }
@@ -778,25 +817,45 @@ static uint32_t attester_committee(const Engine& g, const CState& C, const Att& 
   throw Rejected{PZ_ATT_NO_COMMITTEE};
 }
 
+// uvarint(x) at p (Go's binary.PutUvarint); returns the bytes written.
+static size_t put_uvarint(uint8_t* p, uint64_t x) {
+  size_t n = 0;
+  while (x >= 0x80) {
+    p[n++] = (uint8_t)(x | 0x80);
+    x >>= 7;
+  }
+  p[n++] = (uint8_t)x;
+  return n;
+}
+
+// What processAttestation found out about an attestation that calculateBlockVoteCache, run
+// next on the same block state, would compute again: its signed parent hashes (hash-log ids)
+// and its committee.
+struct AttLookup {
+  bool have = false;
+  uint32_t comm = 0;
+  std::vector<uint32_t> parents;
+};
+
 // processAttestation (core.go:240-297) -> builds the message whose digest the reference logs.
-static void process_attestation(Engine& g, uint64_t block_slot, const Att& a, std::vector<uint32_t>& parents) {
+static void process_attestation(Engine& g, uint64_t block_slot, const Att& a, AttLookup& L) {
+  L.have = false;
   if ((int64_t)a.slot > (int64_t)block_slot) throw Rejected{PZ_ATT_SLOT_HIGH};
   if ((int64_t)a.slot < (int64_t)block_slot - (int64_t)kCycle) throw Rejected{PZ_ATT_SLOT_LOW};
   if (a.jslot != g.C->jslot) throw Rejected{PZ_ATT_JUSTIFIED};
+  std::vector<uint32_t>& parents = L.parents;
   signed_parents(g, *g.A, block_slot, a, parents);
   const uint32_t c = attester_committee(g, *g.C, a);
+  L.comm = c;
+  L.have = true;
   const uint64_t k = g.csize[c];
   if ((k + 7) / 8 != a.bf_len) throw Rejected{PZ_ATT_BITFIELD_LEN};  // core.go:379-382
   if (k % 8 && (a.at(a.bf_off)[a.bf_len - 1] & (0xFFu >> (k % 8)))) throw Rejected{PZ_ATT_TRAILING_BITS};
   // the message: a 10-byte buffer holding uvarint(slot % 64) overwritten by uvarint(shard)
   // at offset 0, then "parent ' '" x 64, then ShardBlockHash; assembled on the device
   uint8_t hdr[16] = {0};
-  std::string v;
-  put_varint(v, a.slot % kCycle);
-  std::memcpy(hdr, v.data(), v.size());
-  v.clear();
-  put_varint(v, a.shard);
-  std::memcpy(hdr, v.data(), v.size());
+  put_uvarint(hdr, a.slot % kCycle);
+  put_uvarint(hdr, a.shard);
   g.m_hdr.insert(g.m_hdr.end(), hdr, hdr + 16);
   g.m_ids.insert(g.m_ids.end(), parents.begin(), parents.end());
   g.m_sbh.insert(g.m_sbh.end(), a.at(a.sbh_off), a.at(a.sbh_off) + a.sbh_len);
@@ -804,9 +863,16 @@ static void process_attestation(Engine& g, uint64_t block_slot, const Att& a, st
 }
 
 // calculateBlockVoteCache (core.go:300-345): queue one tally item per signed parent hash.
-static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, std::vector<uint32_t>& parents) {
-  signed_parents(g, *g.A, block_slot, a, parents);
-  const uint32_t c = attester_committee(g, *g.C, a);
+// The parents and committee come from processAttestation's lookup when it got that far (the
+// block state is the same), else they are looked up here.
+static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, AttLookup& L) {
+  if (!L.have) {
+    signed_parents(g, *g.A, block_slot, a, L.parents);
+    L.comm = attester_committee(g, *g.C, a);
+    L.have = true;
+  }
+  const std::vector<uint32_t>& parents = L.parents;
+  const uint32_t c = L.comm;
   const uint64_t k = g.csize[c];
   uint64_t skip = 0;  // parents equal to one of the raw oblique parent hashes (core.go:313-320)
   for (auto& o : a.obl)
@@ -1458,24 +1524,39 @@ static int reload(Engine& g, const uint8_t* data, uint64_t len) {
 // record per attestation, the parse itself was 2x slower -- the allocator shared by the
 // threads -- and the walk that reads the records 10-20 % slower: records left in other cores'
 // caches; profiles/r03/replay_threads_r3c.txt.)
+// The call's arena: a copy of the input bytes (filled by whoever parses them), the records
+// reserved to the counted number, the oblique pool to a bound (an element takes >= 2 bytes).
+static std::shared_ptr<CallArena> make_arena(const uint64_t* offs, uint64_t n, uint64_t natt) {
+  auto ar = std::make_shared<CallArena>();
+  const uint64_t total = n ? offs[n] - offs[0] : 0;
+  ar->bytes.reset(new uint8_t[total + 16]);
+  ar->atts.reserve(natt);
+  ar->obl.reserve(total / 2 + 1);
+  return ar;
+}
+
+// Blocks [b0, b1): copied into the arena and parsed; returns the first malformed block or b1.
+static uint64_t parse_range(const uint8_t* data, const uint64_t* offs, uint64_t b0, uint64_t b1, CallArena& ar,
+                            const std::shared_ptr<CallArena>& owner, std::vector<Block>& blocks) {
+  const uint64_t o0 = offs[0];
+  for (uint64_t i = b0; i < b1; ++i)
+    if (offs[i + 1] < offs[i]) return i;
+  if (b1 > b0) std::memcpy(ar.bytes.get() + (offs[b0] - o0), data + offs[b0], offs[b1] - offs[b0]);
+  const uint8_t* base = ar.bytes.get() - o0;
+  for (uint64_t i = b0; i < b1; ++i)
+    if (!parse_block(base + offs[i], offs[i + 1] - offs[i], &blocks[i], owner)) return i;
+  return b1;
+}
+
+// Every block, on the calling thread, before anything else (the path that keeps a call
+// all-or-nothing; pz_chain_process_blocks pipelines the parse otherwise).
 static int parse_all(const uint8_t* data, const uint64_t* offs, uint64_t n, uint64_t natt, std::vector<Block>& blocks,
                      std::shared_ptr<CallArena>* keep) {
-  auto ar = std::make_shared<CallArena>();
+  auto ar = make_arena(offs, n, natt);
   *keep = ar;  // the blocks' bytes live here for the whole call (records alias it beyond)
-  for (uint64_t i = 0; i < n; ++i)
-    if (offs[i + 1] < offs[i]) return fail(PZ_EINVAL, "block %llu: offsets not monotone", (unsigned long long)i);
-  const uint64_t o0 = n ? offs[0] : 0, total = n ? offs[n] - o0 : 0;
-  ar->bytes.resize(total + 16);
-  if (total) std::memcpy(ar->bytes.data(), data + o0, total);
-  ar->atts.reserve(natt);
-  ar->obl.reserve(natt);
   blocks.resize(n);
-  const uint8_t* base = ar->bytes.data() - o0;
-  for (uint64_t i = 0; i < n; ++i) {
-    if (!parse_block(base + offs[i], offs[i + 1] - offs[i], &blocks[i], ar))
-      return fail(PZ_EINVAL, "block %llu is not a canonical BeaconBlock encoding", (unsigned long long)i);
-  }
-  for (Att& a : ar->atts) a.obl.p = ar->obl.data() + a.obl_first;  // the pool no longer grows
+  const uint64_t bad = parse_range(data, offs, 0, n, *ar, ar, blocks);
+  if (bad < n) return fail(PZ_EINVAL, "block %llu is not a canonical BeaconBlock encoding", (unsigned long long)bad);
   return PZ_OK;
 }
 
@@ -1497,135 +1578,201 @@ static void sync_hash_log(Engine& g) {
   g.d_hlog_n = n;
 }
 
-static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, pz_att_result* ar) {
-  const uint64_t n = blocks.size();
-  const auto t_hash1 = std::chrono::steady_clock::now();
-  // device pass 1: block digests, attestation Hash and Key, built straight into pinned
-  // memory (one H2D, one 32-byte-digest D2H); hash_many (64-byte digests, host threads for
-  // serial chains) only when a message reaches the serial threshold
-  uint64_t natt = 0, total = 0;
-  for (auto& b : blocks) {
-    natt += b.atts.size();
-    total += b.len;
-    for (auto& a : b.atts) total += a->len + 10 + a->sbh_len + 32 * a->obl.size();
+// Digest messages of blocks [b0, b1) and their na attestations (a0.. in call order), laid out
+// [blocks][attestation encodings][Key() preimages] in pinned memory, then H2D, one CSR BLAKE2b
+// launch and the D2H of the 32-byte digests, all on stream s.
+// The host half: the messages into D's pinned buffers; returns their bytes (offsets in D.offs).
+static uint64_t stage_host(const std::vector<Block>& blocks, uint64_t b0, uint64_t b1, uint64_t na, DigestBufs& D) {
+  const uint64_t nb = b1 - b0, nmsg = nb + 2 * na;
+  uint64_t total = 0;
+  for (uint64_t bi = b0; bi < b1; ++bi) {
+    total += blocks[bi].len;
+    for (auto& a : blocks[bi].atts) total += a->len + 10 + a->sbh_len + 32 * a->obl.size();
   }
-  const uint64_t nmsg = n + 2 * natt, thr = serial_threshold();
-  bool any_long = false;
-  for (auto& b : blocks) any_long |= b.len >= thr;
-  for (auto& b : blocks)
-    for (auto& a : b.atts) any_long |= a->len >= thr || 10 + a->sbh_len + 32 * a->obl.size() >= thr;
-  std::vector<uint8_t> dg_slow;
-  const uint8_t* dg;
-  uint64_t dstride;
-  if (!any_long) {
-    check(g.pin_msgs.reserve(total + 16));
-    check(g.pin_offs.reserve((nmsg + 1) * 8));
-    check(g.pin_dig.reserve(nmsg * 32));
-    uint8_t* buf = g.pin_msgs.p;
-    uint64_t* ho = reinterpret_cast<uint64_t*>(g.pin_offs.p);
-    // offsets first (serial, a few adds per message), then the bytes on host threads
-    std::vector<uint64_t> first_att(n + 1, 0);
-    uint64_t pos = 0, k = 0;
-    ho[k++] = 0;
-    for (uint64_t bi = 0; bi < n; ++bi) {
-      ho[k++] = pos += blocks[bi].len;
-      first_att[bi + 1] = first_att[bi] + blocks[bi].atts.size();
-    }
-    for (auto& b : blocks)
-      for (auto& a : b.atts) ho[k++] = pos += a->len;
-    for (auto& b : blocks)
-      for (auto& a : b.atts) ho[k++] = pos += 10 + a->sbh_len + 32 * a->obl.size();
-    auto fill = [&](uint64_t b0, uint64_t b1) {
-      for (uint64_t bi = b0; bi < b1; ++bi) {
-        const Block& b = blocks[bi];
-        std::memcpy(buf + ho[bi], b.data, b.len);
-        for (uint64_t j = 0; j < b.atts.size(); ++j) {
-          const Att& a = *b.atts[j];
-          const uint64_t ga = first_att[bi] + j;
-          std::memcpy(buf + ho[n + ga], a.base, a.len);
-          // Key() preimage (types/attestation.go:61-77): a 10-byte buffer holding
-          // uvarint(slot) overwritten by uvarint(shard), ShardBlockHash, each oblique hash
-          // copied into a [32]byte
-          uint8_t* q = buf + ho[n + natt + ga];
-          std::memset(q, 0, 10);
-          uint8_t v[10];
-          size_t vl = 0;
-          for (uint64_t x = a.slot; ; x >>= 7) {
-            v[vl++] = (uint8_t)(x >= 0x80 ? (x & 0x7F) | 0x80 : x);
-            if (x < 0x80) break;
-          }
-          std::memcpy(q, v, vl);
-          vl = 0;
-          for (uint64_t x = a.shard; ; x >>= 7) {
-            v[vl++] = (uint8_t)(x >= 0x80 ? (x & 0x7F) | 0x80 : x);
-            if (x < 0x80) break;
-          }
-          std::memcpy(q, v, vl);
-          std::memcpy(q + 10, a.at(a.sbh_off), a.sbh_len);
-          uint64_t kl = 10 + a.sbh_len;
-          for (auto& o : a.obl) {
-            const H32 h = copy32(a.at(o.first), o.second);
-            std::memcpy(q + kl, h.b, 32);
-            kl += 32;
-          }
-        }
+  check(D.msgs.reserve(total + 16));  // (the pipelined producer's buffers were reserved to fit)
+  check(D.offs.reserve((nmsg + 1) * 8));
+  check(D.dig.reserve(nmsg * 32 + 32));
+  uint8_t* buf = D.msgs.p;
+  uint64_t* ho = reinterpret_cast<uint64_t*>(D.offs.p);
+  uint64_t pos = 0, k = 0, ka = nb + 1, kk = nb + na + 1;
+  ho[0] = 0;
+  for (uint64_t bi = b0; bi < b1; ++bi) ho[++k] = pos += blocks[bi].len;
+  uint64_t pa = pos;
+  for (uint64_t bi = b0; bi < b1; ++bi)
+    for (auto& a : blocks[bi].atts) ho[ka++] = pa += a->len;
+  uint64_t pk = pa;
+  for (uint64_t bi = b0; bi < b1; ++bi)
+    for (auto& a : blocks[bi].atts) ho[kk++] = pk += 10 + a->sbh_len + 32 * a->obl.size();
+  uint64_t m = nb;
+  for (uint64_t bi = b0; bi < b1; ++bi) {
+    const Block& b = blocks[bi];
+    std::memcpy(buf + ho[bi - b0], b.data, b.len);
+    for (auto& ap : b.atts) {
+      const Att& a = *ap;
+      std::memcpy(buf + ho[m], a.base, a.len);
+      // Key() preimage (types/attestation.go:61-77): a 10-byte buffer holding uvarint(slot)
+      // overwritten by uvarint(shard), ShardBlockHash, each oblique hash copied into a [32]byte
+      uint8_t* q = buf + ho[m + na];
+      std::memset(q, 0, 10);
+      uint8_t v[10];
+      size_t vl = 0;
+      for (uint64_t x = a.slot; ; x >>= 7) {
+        v[vl++] = (uint8_t)(x >= 0x80 ? (x & 0x7F) | 0x80 : x);
+        if (x < 0x80) break;
       }
-    };
-    const uint64_t T = std::max<uint64_t>(1, std::min<uint64_t>(host_threads(), n / 256));
-    if (T == 1) {
-      fill(0, n);
-    } else {
-      std::vector<std::thread> th;
-      for (uint64_t t = 1; t < T; ++t) th.emplace_back(fill, n * t / T, n * (t + 1) / T);
-      fill(0, n / T);
-      for (auto& x : th) x.join();
-    }
-    check(g.h_in.alloc(pos + 16));
-    check(g.h_out.alloc(nmsg * 32));
-    check(g.h_offs.alloc(nmsg + 1));
-    hchk(hipMemcpyAsync(g.h_offs.p, ho, (nmsg + 1) * 8, hipMemcpyHostToDevice, g.s), "H2D offsets");
-    if (pos) hchk(hipMemcpyAsync(g.h_in.p, buf, pos, hipMemcpyHostToDevice, g.s), "H2D msgs");
-    hchk(launch_b2b_csr(g.h_in.p, g.h_offs.p, nmsg, g.h_out.p, 32, g.s), "blake2b csr");
-    hchk(hipMemcpyAsync(g.pin_dig.p, g.h_out.p, nmsg * 32, hipMemcpyDeviceToHost, g.s), "D2H digests");
-    hchk(hipStreamSynchronize(g.s), "sync");
-    dg = g.pin_dig.p;
-    dstride = 32;
-  } else {
-    std::string buf;
-    std::vector<uint64_t> ho{0};
-    for (auto& b : blocks) {
-      buf.append((const char*)b.data, b.len);
-      ho.push_back(buf.size());
-    }
-    for (auto& b : blocks)
-      for (auto& a : b.atts) {
-        buf.append((const char*)a->base, a->len);
-        ho.push_back(buf.size());
+      std::memcpy(q, v, vl);
+      vl = 0;
+      for (uint64_t x = a.shard; ; x >>= 7) {
+        v[vl++] = (uint8_t)(x >= 0x80 ? (x & 0x7F) | 0x80 : x);
+        if (x < 0x80) break;
       }
-    for (auto& b : blocks)
-      for (auto& a : b.atts) {  // Key() preimage (types/attestation.go:61-77)
-        std::string k(10, '\0'), v;
-        put_varint(v, a->slot);
-        std::memcpy(&k[0], v.data(), v.size());
-        v.clear();
-        put_varint(v, a->shard);
-        std::memcpy(&k[0], v.data(), v.size());
-        k.append((const char*)a->at(a->sbh_off), a->sbh_len);
-        for (auto& o : a->obl) {
-          const H32 h = copy32(a->at(o.first), o.second);
-          k.append((const char*)h.b, 32);
-        }
-        buf += k;
-        ho.push_back(buf.size());
+      std::memcpy(q, v, vl);
+      std::memcpy(q + 10, a.at(a.sbh_off), a.sbh_len);
+      uint64_t kl = 10 + a.sbh_len;
+      for (auto& o : a.obl) {
+        const H32 h = copy32(a.at(o.first), o.second);
+        std::memcpy(q + kl, h.b, 32);
+        kl += 32;
       }
-    hash_many(g, buf, ho, dg_slow);
-    dg = dg_slow.data();
-    dstride = 64;
+      ++m;
+    }
   }
-  g.prof[kProfHash1] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_hash1).count();
+  return pk;
+}
+
+// The device half: H2D, one CSR BLAKE2b launch, D2H of the 32-byte digests, on stream s.
+static void stage_launch(uint64_t nmsg, uint64_t bytes, DigestBufs& D, hipStream_t s) {
+  check(D.d_in.alloc(bytes + 16));
+  check(D.d_out.alloc(nmsg * 32));
+  check(D.d_offs.alloc(nmsg + 1));
+  hchk(hipMemcpyAsync(D.d_offs.p, D.offs.p, (nmsg + 1) * 8, hipMemcpyHostToDevice, s), "H2D offsets");
+  if (bytes) hchk(hipMemcpyAsync(D.d_in.p, D.msgs.p, bytes, hipMemcpyHostToDevice, s), "H2D msgs");
+  hchk(launch_b2b_csr(D.d_in.p, D.d_offs.p, nmsg, D.d_out.p, 32, s), "blake2b csr");
+  hchk(hipMemcpyAsync(D.dig.p, D.d_out.p, nmsg * 32, hipMemcpyDeviceToHost, s), "D2H digests");
+}
+
+static void stage_digests(const std::vector<Block>& blocks, uint64_t b0, uint64_t b1, uint64_t na, DigestBufs& D,
+                          hipStream_t s) {
+  const uint64_t bytes = stage_host(blocks, b0, b1, na, D);
+  stage_launch((b1 - b0) + 2 * na, bytes, D, s);
+}
+
+// Where the walk finds its blocks and their digests (block / attestation Hash / Key, 32 B).
+// Batch: everything parsed and hashed before the walk.  Pipelined: a producer thread parses
+// chunks of kChunk blocks into the arena and enqueues each chunk's digest batch on its own
+// stream while the walk consumes the previous chunks (SURVEY.md §8 a3/a4 hashing off the walk's
+// critical path); it stays at most kRing chunks ahead.
+struct Feeder {
+  std::vector<Block>* blocks = nullptr;
+  uint64_t n = 0, natt = 0;
+  // batch
+  const uint8_t* dg = nullptr;
+  uint64_t dstride = 32;
+  // pipelined
+  bool piped = false;
+  struct Slot {
+    DigestBufs* d = nullptr;  // Engine::ring[j % kRing]
+    hipEvent_t ev = nullptr;  // Engine::ring_ev[j % kRing]
+    uint64_t b0 = 0, b1 = 0, a0 = 0, na = 0, bytes = 0;
+    uint64_t launched = UINT64_MAX;  // the chunk whose digest batch was launched from this slot
+  } slot[kRing];
+  hipStream_t s2 = nullptr;
+  std::atomic<uint64_t> ready{0};     // chunks parsed and their digests enqueued
+  std::atomic<uint64_t> consumed{0};  // chunks the walk has finished
+  std::atomic<uint64_t> bad{UINT64_MAX};  // first malformed block
+  std::atomic<int> rc{0};
+  std::atomic<bool> stop{false};
+  uint64_t cur = UINT64_MAX;  // the chunk the walk is in
+  double wait_s = 0;
+
+  // false: block bi is not there (a malformed block at or before it ends the walk)
+  bool ensure(uint64_t bi) {
+    if (!piped) return true;
+    const uint64_t j = bi / kChunk;
+    if (j == cur) return bi < bad.load(std::memory_order_acquire);
+    if (cur != UINT64_MAX) consumed.store(cur + 1, std::memory_order_release);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (ready.load(std::memory_order_acquire) <= j && !rc.load() &&
+           bad.load(std::memory_order_acquire) > bi)
+      std::this_thread::yield();
+    if (rc.load()) throw rc.load();
+    if (bi >= bad.load(std::memory_order_acquire)) return false;
+    launch(j);
+    // the next chunk's batch goes out now, so it is done when the walk gets there
+    if (ready.load(std::memory_order_acquire) > j + 1) launch(j + 1);
+    Slot& S = slot[j % kRing];
+    hchk(hipEventSynchronize(S.ev), "event sync (digests)");
+    wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    cur = j;
+    return true;
+  }
+  // Every HIP call of the pipeline is made here, on the walk's thread: HIP calls from the
+  // producer thread (its own stream) made each of the walk's tally flushes ~4x slower (runtime
+  // lock contention; profiles/r03/replay_pipeline_r3i.txt).
+  void launch(uint64_t j) {
+    Slot& S = slot[j % kRing];
+    if (S.launched == j) return;
+    S.launched = j;
+    const uint64_t nmsg = (S.b1 - S.b0) + 2 * S.na;
+    if (nmsg) stage_launch(nmsg, S.bytes, *S.d, s2);
+    hchk(hipEventRecord(S.ev, s2), "event");
+  }
+  const uint8_t* blk(uint64_t bi) const {
+    if (!piped) return dg + bi * dstride;
+    const Slot& S = slot[(bi / kChunk) % kRing];
+    return S.d->dig.p + (bi - S.b0) * 32;
+  }
+  const uint8_t* hash(uint64_t bi, uint64_t ga) const {
+    if (!piped) return dg + (n + ga) * dstride;
+    const Slot& S = slot[(bi / kChunk) % kRing];
+    return S.d->dig.p + ((S.b1 - S.b0) + (ga - S.a0)) * 32;
+  }
+  const uint8_t* key(uint64_t bi, uint64_t ga) const {
+    if (!piped) return dg + (n + natt + ga) * dstride;
+    const Slot& S = slot[(bi / kChunk) % kRing];
+    return S.d->dig.p + ((S.b1 - S.b0) + S.na + (ga - S.a0)) * 32;
+  }
+};
+
+// The producer: chunk after chunk, parse into the arena and enqueue the digest batch.
+static void feed(Engine& g, Feeder& F, const uint8_t* data, const uint64_t* offs, std::shared_ptr<CallArena> ar) {
+  try {
+    uint64_t a0 = 0;
+    for (uint64_t j = 0, b0 = 0; b0 < F.n; ++j, b0 += kChunk) {
+      while (F.consumed.load(std::memory_order_acquire) + kRing <= j) {
+        if (F.stop.load()) return;
+        std::this_thread::yield();
+      }
+      Feeder::Slot& S = F.slot[j % kRing];
+      uint64_t b1 = std::min(F.n, b0 + kChunk);
+      const uint64_t good = parse_range(data, offs, b0, b1, *ar, ar, *F.blocks);
+      b1 = good;
+      uint64_t na = 0;
+      for (uint64_t bi = b0; bi < b1; ++bi) na += (*F.blocks)[bi].atts.size();
+      S.b0 = b0;
+      S.b1 = b1;
+      S.a0 = a0;
+      S.na = na;
+      a0 += na;
+      S.d = &g.ring[j % kRing];
+      S.ev = g.ring_ev[j % kRing];
+      S.bytes = b1 > b0 ? stage_host(*F.blocks, b0, b1, na, *S.d) : 0;
+      if (good < std::min(F.n, b0 + kChunk)) F.bad.store(good, std::memory_order_release);
+      F.ready.store(j + 1, std::memory_order_release);
+      if (good < std::min(F.n, b0 + kChunk)) return;
+    }
+  } catch (int rc) {
+    F.rc.store(rc ? rc : PZ_EDEVICE);
+  }
+}
+
+static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar) {
+  const uint64_t n = F.n, natt = F.natt;
+  std::vector<Block>& blocks = *F.blocks;
   // the walk
   std::vector<uint64_t> msg_att;
-  std::vector<uint32_t> parents;
+  std::vector<AttLookup> look;  // per attestation of the current block
+  std::vector<AttP> processed;
   std::vector<uint32_t> block_id(n);
   uint64_t ai = 0;
   g.m_hdr.clear();
@@ -1635,16 +1782,21 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
   g.m_hdr.reserve(16 * natt);
   g.m_ids.reserve(kCycle * natt);
   msg_att.reserve(natt);
-  for (uint64_t bi = 0; bi < n; ++bi) {
-    H32 h;
-    std::memcpy(h.b, dg + bi * dstride, 32);
-    block_id[bi] = log_hash(g, h);
-  }
   auto t_walk = std::chrono::steady_clock::now();
+  uint64_t logged = 0;  // block digests are logged a chunk at a time, as they arrive
   for (uint64_t bi = 0; bi < n; ++bi) {
+    if (!F.ensure(bi)) break;  // a malformed block: the call ends before it (EINVAL)
+    if (bi == logged) {
+      const uint64_t e = F.piped ? std::min(n, (bi / kChunk + 1) * kChunk) : n;
+      for (; logged < e && (!F.piped || logged < F.bad.load()); ++logged) {
+        H32 h;
+        std::memcpy(h.b, F.blk(logged), 32);
+        block_id[logged] = log_hash(g, h);
+      }
+    }
     const Block& b = blocks[bi];
     pz_block_result& r = br[bi];
-    std::memcpy(r.hash, dg + bi * dstride, 32);
+    std::memcpy(r.hash, F.blk(bi), 32);
     r.status = PZ_BLOCK_PROCESSED;
     r.transition = 0;
     r.first_att = (uint32_t)ai;
@@ -1662,13 +1814,14 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
       r.status = PZ_BLOCK_NO_PARENT;
       continue;
     }
-    std::vector<AttP> processed;
+    processed.clear();
+    if (look.size() < b.atts.size()) look.resize(b.atts.size());
     bool can_atts = false;
     for (uint64_t j = 0; j < b.atts.size(); ++j) {
       pz_att_result& x = ar[a0 + j];
       try {
-        PhaseTimer pt(g.prof[kProfCheck]);
-        process_attestation(g, b.slot, *b.atts[j], parents);
+        FineTimer pt(g.prof[kProfCheck]);
+        process_attestation(g, b.slot, *b.atts[j], look[j]);
       } catch (Rejected& e) {
         can_atts = false;
         x.status = e.code;
@@ -1676,8 +1829,8 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
       }
       can_atts = true;
       x.status = PZ_ATT_PROCESSED;
-      std::memcpy(x.hash, dg + (n + a0 + j) * dstride, 32);
-      std::memcpy(x.key, dg + (n + natt + a0 + j) * dstride, 32);
+      std::memcpy(x.hash, F.hash(bi, a0 + j), 32);
+      std::memcpy(x.key, F.key(bi, a0 + j), 32);
       x.msg_len = (uint32_t)(10 + 33 * kCycle + b.atts[j]->sbh_len);
       msg_att.push_back(a0 + j);
       processed.push_back(b.atts[j]);
@@ -1687,10 +1840,10 @@ static void process(Engine& g, std::vector<Block>& blocks, pz_block_result* br, 
       continue;
     }
     bool cache_nil = true;  // the map returned by the last calculateBlockVoteCache call
-    for (auto& a : b.atts) {
+    for (uint64_t j = 0; j < b.atts.size(); ++j) {
       try {
-        PhaseTimer pt(g.prof[kProfQueue]);
-        queue_vote_cache(g, b.slot, *a, parents);
+        FineTimer pt(g.prof[kProfQueue]);
+        queue_vote_cache(g, b.slot, *b.atts[j], look[j]);
         cache_nil = g.A->cache_nil;
       } catch (Rejected&) {
         cache_nil = true;
@@ -1783,6 +1936,7 @@ static void make_ranks(Engine& g, int device, pz_comm* comm) {
   g.device = g.rk[0].dev;
   g.s = g.rk[0].s;
   hchk(hipSetDevice(g.device), "hipSetDevice");
+  hchk(hipStreamCreateWithFlags(&g.s2, hipStreamNonBlocking), "hipStreamCreate");
 }
 
 static void destroy_chain(pz_chain* c) {
@@ -1797,6 +1951,13 @@ static void destroy_chain(pz_chain* c) {
   }
   if (g.q_arena) (void)hipHostFree(g.q_arena);
   if (g.ev_totals) (void)hipEventDestroy(g.ev_totals);
+  for (hipEvent_t e : g.ring_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (g.s2) {
+    (void)hipSetDevice(g.device);
+    (void)hipStreamSynchronize(g.s2);
+    streams.push_back({g.device, g.s2});
+  }
   delete c;
   for (auto& ds : streams)
     if (ds.second) {
@@ -1892,24 +2053,126 @@ int pz_chain_process_blocks(pz_chain* c, const uint8_t* blocks, const uint64_t* 
   if (rc0) return rc0;
   if (natt > att_cap || (natt && !att_out)) return fail(PZ_EINVAL, "att_out holds %llu results, need %llu",
                                                         (unsigned long long)att_cap, (unsigned long long)natt);
-  std::vector<Block> parsed;
+  Engine& g = c->g;
+  std::vector<Block> parsed(n);
+  Feeder F;
+  F.blocks = &parsed;
+  F.n = n;
+  F.natt = natt;
+  const uint64_t thr = serial_threshold();
+  bool long_msg = false;
+  for (uint64_t i = 0; i < n && !long_msg; ++i) long_msg = offsets[i + 1] >= offsets[i] && offsets[i + 1] - offsets[i] >= thr;
   std::shared_ptr<CallArena> arena;
-  int rc;
-  {
-    PhaseTimer pt(c->g.prof[kProfParse]);
-    rc = parse_all(blocks, offsets, n, natt, parsed, &arena);  // before any state changes
+  std::vector<uint8_t> dg_slow;
+  // The batch path (default): the whole call parsed, one digest batch, then the walk.  The
+  // pipelined form (a producer thread parsing a chunk ahead, PZ_CHAIN_PIPELINE=1) measured
+  // slower on the 10,000-block replay (177-183k vs 200-229k blocks/s; the producer slows the
+  // walk's own host work, profiles/r03/replay_pipeline_r3*.txt), so it is an A/B knob.  Both
+  // end the call at a malformed block with PZ_EINVAL, the blocks before it processed.
+  const char* pe = std::getenv("PZ_CHAIN_PIPELINE");
+  F.piped = !long_msg && n >= 2 * kChunk && pe && pe[0] == '1';
+  if (!F.piped) {
+    {
+      PhaseTimer pt(g.prof[kProfParse]);
+      arena = make_arena(offsets, n, natt);
+      const uint64_t good = parse_range(blocks, offsets, 0, n, *arena, arena, parsed);
+      if (good < n) {  // the walk stops before the malformed block
+        F.bad.store(good);
+        F.n = good;
+        F.natt = 0;
+        for (uint64_t bi = 0; bi < good; ++bi) F.natt += parsed[bi].atts.size();
+      }
+    }
+    try {
+      PhaseTimer pt(g.prof[kProfHash1]);
+      if (!long_msg) {
+        if (F.n) stage_digests(parsed, 0, F.n, F.natt, g.dbatch, g.s);
+        hchk(hipStreamSynchronize(g.s), "sync");
+        F.dg = g.dbatch.dig.p;
+        F.dstride = 32;
+      } else {  // 64-byte digests; messages at or over the threshold on host threads
+        std::string buf;
+        std::vector<uint64_t> ho{0};
+        const uint64_t ng = F.n;
+        for (uint64_t bi = 0; bi < ng; ++bi) {
+          buf.append((const char*)parsed[bi].data, parsed[bi].len);
+          ho.push_back(buf.size());
+        }
+        for (uint64_t bi = 0; bi < ng; ++bi)
+          for (auto& a : parsed[bi].atts) {
+            buf.append((const char*)a->base, a->len);
+            ho.push_back(buf.size());
+          }
+        for (uint64_t bi = 0; bi < ng; ++bi)
+          for (auto& a : parsed[bi].atts) {  // Key() preimage (types/attestation.go:61-77)
+            std::string k(10, '\0'), v;
+            put_varint(v, a->slot);
+            std::memcpy(&k[0], v.data(), v.size());
+            v.clear();
+            put_varint(v, a->shard);
+            std::memcpy(&k[0], v.data(), v.size());
+            k.append((const char*)a->at(a->sbh_off), a->sbh_len);
+            for (auto& o : a->obl) {
+              const H32 h = copy32(a->at(o.first), o.second);
+              k.append((const char*)h.b, 32);
+            }
+            buf += k;
+            ho.push_back(buf.size());
+          }
+        hash_many(g, buf, ho, dg_slow);
+        F.dg = dg_slow.data();
+        F.dstride = 64;
+      }
+    } catch (int rc) {
+      return rc;
+    }
+  } else {
+    // the parse and the digest batches run a chunk ahead of the walk on a producer thread
+    arena = make_arena(offsets, n, natt);
   }
-  if (rc) return rc;
+  std::thread producer;
+  if (F.piped) {
+    // the ring's pinned buffers and events, sized here for the largest chunk (the producer
+    // makes no HIP call): the messages of a chunk are its blocks, their attestation encodings
+    // (spans of the blocks) and Key() preimages of at most 10 + 16x the attestation's bytes
+    uint64_t mx = 0;
+    for (uint64_t b0 = 0; b0 < n; b0 += kChunk) mx = std::max(mx, offsets[std::min(n, b0 + kChunk)] - offsets[b0]);
+    try {
+      for (int k = 0; k < kRing; ++k) {
+        check(g.ring[k].msgs.reserve(18 * mx + 10 * (mx / 8) + 16));
+        check(g.ring[k].offs.reserve((kChunk + 2 * (mx / 8) + 2) * 8));
+        check(g.ring[k].dig.reserve((kChunk + 2 * (mx / 8) + 2) * 32));
+        if (!g.ring_ev[k]) hchk(hipEventCreateWithFlags(&g.ring_ev[k], hipEventDisableTiming), "event");
+      }
+    } catch (int rc) {
+      return rc;
+    }
+    F.s2 = g.s2;
+    producer = std::thread(feed, std::ref(g), std::ref(F), blocks, offsets, arena);
+  }
+  struct Join {  // the producer is stopped and joined on every way out (it reads F and parsed)
+    Feeder& F;
+    std::thread& t;
+    ~Join() {
+      F.stop.store(true);
+      F.consumed.store(UINT64_MAX / 2);
+      if (t.joinable()) t.join();
+    }
+  } join{F, producer};
   try {
-    PhaseTimer pt(c->g.prof[kProfProcess]);
-    process(c->g, parsed, block_out, att_out);
+    PhaseTimer pt(g.prof[kProfProcess]);
+    process(g, F, block_out, att_out);
   } catch (Panic& p) {
-    c->g.poisoned = true;
+    g.poisoned = true;
     return fail(PZ_EINDEX, "the reference panics here: %s", p.what.c_str());
   } catch (int rc) {
-    c->g.poisoned = true;
+    g.poisoned = true;
     return rc;
   }
+  g.prof[kProfHash1] += F.wait_s;
+  const uint64_t bad = F.bad.load();
+  if (bad < n) return fail(PZ_EINVAL, "block %llu is not a canonical BeaconBlock encoding (blocks before it were "
+                                      "processed)", (unsigned long long)bad);
   return PZ_OK;
 }
 
@@ -2036,4 +2299,23 @@ extern "C" int pz_debug_chain_profile(pz_chain* c, double* out, int n) {
   if (!c || !out) return PZ_EINVAL;
   for (int i = 0; i < n && i < pz::chain::kProfSlots; ++i) out[i] = c->g.prof[i];
   return pz::chain::kProfSlots;
+}
+
+// Internal (tools/, CPU-only: no device call): the block parser of pz_chain_process_blocks on
+// its own, `reps` times; returns the wall seconds of the fastest run.
+extern "C" int pz_debug_parse(const uint8_t* data, const uint64_t* offs, uint64_t n, uint64_t natt, int reps,
+                              double* seconds) {
+  double best = 1e30;
+  for (int r = 0; r < reps; ++r) {
+    const auto t0 = std::chrono::steady_clock::now();
+    {
+      std::vector<pz::chain::Block> blocks;
+      std::shared_ptr<pz::chain::CallArena> arena;
+      const int rc = pz::chain::parse_all(data, offs, n, natt, blocks, &arena);
+      if (rc) return rc;
+    }
+    best = std::min(best, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+  }
+  if (seconds) *seconds = best;
+  return PZ_OK;
 }

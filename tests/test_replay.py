@@ -411,3 +411,30 @@ def test_gpu_sharded_chain_configs4_full_vs_c_port(world):
     assert int(br["transition"].sum()) == 156
     out, port_roots = port_replay(data, offs, nval, len(ar))
     assert mismatches(br, ar, ch.roots(), out, port_roots) == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipeline", ["0", "1"])
+def test_gpu_malformed_block_ends_the_call_there(pipeline, monkeypatch):
+    """A block that is not a canonical encoding ends the call there with PZ_EINVAL, the blocks
+    before it processed (as the reference's sync service handles each block as it arrives), in
+    the batch path and in the pipelined one (PZ_CHAIN_PIPELINE=1: calls of >= 1,024 blocks parse
+    and hash a chunk ahead of the walk).  The chain is then exactly the chain of those blocks."""
+    monkeypatch.setenv("PZ_CHAIN_PIPELINE", pipeline)
+    from prysm_amd import _lib
+    from prysm_amd.blockchain import BeaconChain, serialize_blocks
+    blocks = synth.chain_blocks(1024, 1100, seed=3)
+    data, offs = serialize_blocks(blocks)
+    bad = 1050
+    chunks = [bytes(data[int(offs[i]):int(offs[i + 1])]) for i in range(len(blocks))]
+    chunks[bad] = b"\x10\x00" + chunks[bad]  # a zero scalar Marshal would omit: not canonical
+    raw = b"".join(chunks)
+    o2 = np.zeros(len(chunks) + 1, dtype=np.uint64)
+    o2[1:] = np.cumsum([len(c) for c in chunks])
+    ch = BeaconChain(1024)
+    with pytest.raises(_lib.PzError) as e:
+        ch.process_serialized(np.frombuffer(raw, dtype=np.uint8), o2)
+    assert e.value.code == _lib.PZ_EINVAL and ("block %d " % bad) in str(e.value)
+    ref = BeaconChain(1024)
+    ref.process_serialized(*serialize_blocks(blocks[:bad]))
+    assert ch.roots() == ref.roots()
