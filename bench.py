@@ -303,12 +303,39 @@ def epoch_cold(args, torch, dev, nval, ninst, shuffled, workload, nsets=4):
     units = nval * ninst
     alg = units * EPOCH_BYTES_PER_VALIDATOR
     traffic = pmc_traffic(["pz_epoch_*"], workload + "_cold")
+    yard = cold_stream_yardstick(torch, dev, units, nsets, steps)
     return {"what": "%d steps rotated over %d distinct %d x %d instance sets (%.1f GB of validator state), one "
                     "stream" % (steps, nsets, nval, ninst, nsets * units * 24 / 1e9),
             "value": units * steps / wall, "unit": "validator-epochs/s", "step_device_ms": step_ms,
             "frac": alg / (step_ms * 1e-3) / HBM_PEAK,
             "traffic": traffic, "traffic_source": pmc_summary_path(workload + "_cold") if traffic else None,
-            "traffic_frac": (traffic / (step_ms * 1e-3) / HBM_PEAK) if traffic else None}
+            "traffic_frac": (traffic / (step_ms * 1e-3) / HBM_PEAK) if traffic else None,
+            "yardstick": yard}
+
+
+def cold_stream_yardstick(torch, dev, units, nsets, steps):
+    """What a stock elementwise kernel reaches on the same traffic shape, cold: per element 3
+    reads + 1 write of 8 B (the epoch's balance/start/end in, balance out) -- torch's
+    ``addcmul_`` on float64, rotated over ``nsets`` distinct sets on one stream.  The epoch's
+    counter-byte fraction is read against this, not only against the 8 TB/s spec."""
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):
+        sets = [[torch.rand(units, dtype=torch.float64, device=dev) for _ in range(3)] for _ in range(nsets)]
+        for x, y, z in sets:
+            x.addcmul_(y, z)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for i in range(steps):
+            x, y, z = sets[i % nsets]
+            x.addcmul_(y, z)
+        e1.record(s)
+    s.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    del sets
+    torch.cuda.empty_cache()
+    return {"what": "torch addcmul_ float64 (3 x 8 B read + 8 B written per element), %d elements, %d sets, "
+                    "cold" % (units, nsets),
+            "ms": ms, "frac": units * 32 / (ms * 1e-3) / HBM_PEAK}
 
 
 def epoch_parity(inst, dev):
@@ -750,6 +777,59 @@ def replay_sharded_leg(args, torch, dist, dev, rank, world, comm):
     return out
 
 
+PROF_PHASES = ("parse", "digest_batch", "checks", "vote_queue", "vote_flush", "state_recalc", "msg_digests", "walk",
+               "process", "count_atts", "flush_arena_wait")
+
+
+def chain_phases_ms(ch):
+    """The chain engine's always-on phase clocks (pz_debug_chain_profile; the per-attestation
+    ones, checks and vote_queue, run only under PZ_CHAIN_PROFILE and read 0 here)."""
+    import ctypes
+    from prysm_amd import _lib
+    pv = (ctypes.c_double * 16)()
+    fn = _lib.lib.dll.pz_debug_chain_profile
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    k = fn(ch._h, pv, 16)
+    return {PROF_PHASES[i]: round(pv[i] * 1e3, 3) for i in range(min(k, len(PROF_PHASES))) if pv[i] > 0}
+
+
+def _compressions(nbytes):
+    return max(1, -(-int(nbytes) // 128))
+
+
+def replay_roofline(blocks, offs, ar, wall, ch):
+    """configs[4]'s roofline.  The device work per block, priced at the chip's peaks: the
+    BLAKE2b compressions of its digests (block encoding, and per attestation its encoding, its
+    Key() preimage and the 64-byte signed-message digest) at OPS_PER_COMPRESSION on the VALU
+    model of the hash leg, and the vote-cache tally's bytes (per queued attestation: the
+    bitfield, 63 parent ids, the k members' 8-byte balances, and per signed parent and member a
+    4-byte voter-bitmap word read and written) at HBM peak.  ``peak`` is the blocks/s that device work alone would
+    allow; the walk itself is sequential host work, so ``bound`` is "host" and
+    the phase clocks say where the wall time goes."""
+    from prysm_amd import wire
+    nb = len(blocks)
+    comp = sum(_compressions(int(offs[i + 1]) - int(offs[i])) for i in range(nb))
+    tally_b = 0
+    for b in blocks:
+        for a in b.attestations:
+            comp += _compressions(len(wire.attestation_record(a)))
+            comp += _compressions(10 + len(a.shard_block_hash) + 32 * len(a.oblique_parent_hashes))
+            k = 8 * len(a.attester_bitfield)
+            tally_b += len(a.attester_bitfield) + 63 * 4 + 8 * k + 63 * k * 8
+    comp += sum(_compressions(int(m)) for m in ar["msg_len"] if m)
+    dev_s = comp * OPS_PER_COMPRESSION / VALU_PEAK + tally_b / HBM_PEAK
+    achieved = nb / wall
+    peak = nb / dev_s
+    return {"bound": "host", "achieved": achieved, "peak": peak, "unit": "blocks/s", "frac": achieved / peak,
+            "traffic": None,
+            "model": {"compressions_per_block": comp / nb, "valu_slots_per_compression": OPS_PER_COMPRESSION,
+                      "tally_bytes_per_block": tally_b / nb, "device_floor_ms": dev_s * 1e3,
+                      "wall_ms": wall * 1e3},
+            "host_phases_ms": chain_phases_ms(ch),
+            "note": "device floor = compressions x VALU slots / 78.6 T + tally bytes / 8 TB/s; the rest of the "
+                    "wall is the sequential host walk (parse, checks, vote queue, stateRecalc's round trip)"}
+
+
 def replay_leg(args, torch, dist, dev, rank, world):
     """BASELINE configs[4]: sync replay of a synthetic 10,000-block chain through the block
     pipeline (blockchain/service.go:229-363): per block the block digest, 5 attestations'
@@ -806,7 +886,8 @@ def replay_leg(args, torch, dist, dev, rank, world):
            "processed": sum(r["status"] == "processed" for r in recs),
            "transitions": sum(r["transition"] for r in recs),
            "state_roots": state_roots,
-           "cand_crystallized_root": root_vals["host_serial"].get("cand_crystallized", b"").hex()}
+           "cand_crystallized_root": root_vals["host_serial"].get("cand_crystallized", b"").hex(),
+           "roofline": replay_roofline(blocks, offs, ar, wall, ch)}
     if rank == 0 and world == 1:
         # the checker: the whole timed chain through the C restatement of the block pipeline
         # (checker mode), compared with the GPU engine's records and roots

@@ -382,8 +382,9 @@ struct RankDev {
   uint64_t words = 0;
   DevArr<uint8_t> d_qpack;
   DevArr<uint64_t> d_err;      // sticky tally panic flag
-  DevArr<uint32_t> d_id_slot;  // hash-log id -> vote-cache slot, uploaded up to Engine::d_id_slot_n
-  DevArr<uint32_t> ubits, uflag, d_leader;
+  DevArr<uint32_t> ubits, uflag;
+  DevArr<uint32_t> d_leader;  // [2 leader counters, used alternately][leader list]
+  uint32_t lead_par = 0;      // the counter this rank's next flush counts in
   DevArr<uint64_t> t64;        // the gathered justification totals + panic flag (65 words)
   // epoch scratch: red = {scal[8], vote[natt], total[natt]} (one all-reduce when sharded)
   DevArr<uint64_t> e_red, e_mask, e_nb;
@@ -429,14 +430,13 @@ struct Engine {
   // device expands them into (attestation, parent) items (pz_vote_ids_kernel)
   std::vector<uint8_t> q_bits;
   std::vector<uint64_t> q_boffs{0};
-  std::vector<uint32_t> q_comm, q_ids;
+  std::vector<uint32_t> q_comm, q_slots;  // q_slots: natt x 64 vote-cache slots of the signed parents
   std::vector<uint64_t> q_skip;
   // flushes run asynchronously to the walk: the queue is packed into a pinned arena and
   // copied with one H2D per rank; the arena is reused once every rank's copy is done
   uint8_t* q_arena = nullptr;
   size_t q_arena_cap = 0;
   bool q_arena_busy = false;
-  uint64_t d_id_slot_n = 0;
   uint64_t ncomm = 0, cwords = 1;
   PinBuf e_pin, e_pin_out;   // the epoch inputs' pinned staging; the results' pinned landing
   PinBuf tot_pin;            // the gathered justification totals (65 words)
@@ -659,13 +659,12 @@ static uint32_t log_hash(Engine& g, const H32& h, bool votable = true) {
 static bool flush_votes_enqueue(Engine& g) {
   if (g.q_comm.empty()) return false;
   PhaseTimer pt(g.prof[kProfFlush]);
-  const uint64_t nid = g.id_slot.size(), new_ids = nid - g.d_id_slot_n;
   const uint64_t natt = g.q_comm.size();
   auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
-  // packed layout: boffs | skip | comm | ids | new id slots | bits
+  // packed layout: boffs | skip | comm | slots | bits
   const size_t o_boffs = 0, o_skip = o_boffs + al(g.q_boffs.size() * 8), o_comm = o_skip + al(natt * 8),
-               o_ids = o_comm + al(natt * 4), o_slots = o_ids + al(g.q_ids.size() * 4),
-               o_bits = o_slots + al(new_ids * 4), total = o_bits + al(g.q_bits.size());
+               o_slots = o_comm + al(natt * 4), o_bits = o_slots + al(g.q_slots.size() * 4),
+               total = o_bits + al(g.q_bits.size());
   if (g.q_arena_busy) {
     FineTimer pw(g.prof[kProfFlushWait]);
     for (RankDev& r : g.rk) hchk(hipEventSynchronize(r.q_ev), "event sync");
@@ -675,36 +674,30 @@ static bool flush_votes_enqueue(Engine& g) {
     if (g.q_arena) (void)hipHostFree(g.q_arena);
     g.q_arena = nullptr;
     const size_t cap = std::max(total, 2 * g.q_arena_cap);
-    hchk(hipHostMalloc((void**)&g.q_arena, cap, hipHostMallocDefault), "hipHostMalloc");
+    hchk(hipHostMalloc((void**)&g.q_arena, cap, hipHostMallocPortable | hipHostMallocMapped), "hipHostMalloc");
     g.q_arena_cap = cap;
   }
   std::memcpy(g.q_arena + o_boffs, g.q_boffs.data(), g.q_boffs.size() * 8);
   std::memcpy(g.q_arena + o_skip, g.q_skip.data(), natt * 8);
   std::memcpy(g.q_arena + o_comm, g.q_comm.data(), natt * 4);
-  std::memcpy(g.q_arena + o_ids, g.q_ids.data(), g.q_ids.size() * 4);
-  std::memcpy(g.q_arena + o_slots, g.id_slot.data() + g.d_id_slot_n, new_ids * 4);
+  std::memcpy(g.q_arena + o_slots, g.q_slots.data(), g.q_slots.size() * 4);
   std::memcpy(g.q_arena + o_bits, g.q_bits.data(), g.q_bits.size());
   each_rank(g, [&](RankDev& r) {
     // Growing a device buffer frees the old one, which in-flight flushes may still read:
     // drain the stream first (rare: the buffers double).
-    if (total > r.d_qpack.n || nid > r.d_id_slot.n || natt * 64 + 1 > r.d_leader.n) {
+    if (total > r.d_qpack.n || natt * 64 + 2 > r.d_leader.n) {
       hchk(hipStreamSynchronize(r.s), "sync");
-      check(r.d_qpack.alloc(std::max<uint64_t>(total, 2 * r.d_qpack.n)));
-      check(r.d_leader.alloc(std::max<uint64_t>(natt * 64 + 1, 2 * r.d_leader.n)));
-      if (nid > r.d_id_slot.n) {  // the id -> slot map keeps its device contents
-        DevArr<uint32_t> grown;
-        check(grown.alloc(std::max<uint64_t>(nid, 2 * r.d_id_slot.n)));
-        if (g.d_id_slot_n)
-          hchk(hipMemcpyAsync(grown.p, r.d_id_slot.p, g.d_id_slot_n * 4, hipMemcpyDeviceToDevice, r.s), "D2D");
-        hchk(hipStreamSynchronize(r.s), "sync");
-        std::swap(r.d_id_slot.p, grown.p);
-        std::swap(r.d_id_slot.n, grown.n);
+      if (total > r.d_qpack.n) check(r.d_qpack.alloc(std::max<uint64_t>(total, 2 * r.d_qpack.n)));
+      if (natt * 64 + 2 > r.d_leader.n) {
+        check(r.d_leader.alloc(std::max<uint64_t>(natt * 64 + 2, 2 * r.d_leader.n)));
+        hchk(hipMemsetAsync(r.d_leader.p, 0, 8, r.s), "memset");  // both counters
       }
     }
-    hchk(hipMemcpyAsync(r.d_qpack.p, g.q_arena, total, hipMemcpyHostToDevice, r.s), "H2D");
-    if (new_ids)
-      hchk(hipMemcpyAsync(r.d_id_slot.p + g.d_id_slot_n, r.d_qpack.p + o_slots, new_ids * 4, hipMemcpyDeviceToDevice,
-                          r.s), "D2D");
+    // the pack crosses PCIe in a kernel of this stream (a copy-engine H2D costs ~13 us more on
+    // the transition's critical path: the kernel behind it waits for the engine's signal)
+    void* src = nullptr;
+    hchk(hipHostGetDevicePointer(&src, g.q_arena, 0), "hipHostGetDevicePointer");
+    hchk(launch_stage_h2d(src, r.d_qpack.p, total, r.s), "stage H2D");
     if (!r.q_ev) hchk(hipEventCreateWithFlags(&r.q_ev, hipEventDisableTiming), "event");
     hchk(hipEventRecord(r.q_ev, r.s), "event");
     if (!r.d_err.p) {
@@ -718,9 +711,8 @@ static bool flush_votes_enqueue(Engine& g) {
     v.att_comm = reinterpret_cast<const uint32_t*>(r.d_qpack.p + o_comm);
     v.bits = r.d_qpack.p + o_bits;
     v.boffs = reinterpret_cast<const uint64_t*>(r.d_qpack.p + o_boffs);
-    v.ids = reinterpret_cast<const uint32_t*>(r.d_qpack.p + o_ids);
+    v.slots = reinterpret_cast<const uint32_t*>(r.d_qpack.p + o_slots);
     v.skip = reinterpret_cast<const uint64_t*>(r.d_qpack.p + o_skip);
-    v.id_slot = r.d_id_slot.p;
     v.natt = natt;
     v.balance = r.balance.p;
     v.nval = r.n;
@@ -733,18 +725,19 @@ static bool flush_votes_enqueue(Engine& g) {
     v.err = r.d_err.p;  // sticky: read (and the chain poisoned) at the next sync point
     v.ubits = r.ubits.p;
     v.uflag = r.uflag.p;
-    v.leader = r.d_leader.p + 1;
-    v.nlead = r.d_leader.p;
+    v.leader = r.d_leader.p + 2;
+    v.nlead = r.d_leader.p + r.lead_par;  // counted by this flush's union pass
+    v.nlead_next = r.d_leader.p + (r.lead_par ^ 1);  // zeroed by its leader pass for the next flush
+    r.lead_par ^= 1;
     v.ncomm = g.ncomm;
     v.cwords = g.cwords;
     hchk(launch_vote_ids(v, r.s), "vote tally");
   });
   g.q_arena_busy = true;
-  g.d_id_slot_n = nid;
   g.q_bits.clear();
   g.q_boffs.assign(1, 0);
   g.q_comm.clear();
-  g.q_ids.clear();
+  g.q_slots.clear();
   g.q_skip.clear();
   return true;
 }
@@ -765,6 +758,13 @@ static void tally_gather_enqueue(Engine& g, const VoteGatherSlots& q) {
       hchk(hipMemsetAsync(r.d_err.p, 0, 8, r.s), "memset");
     }
     if (!r.ev_t64) hchk(hipEventCreateWithFlags(&r.ev_t64, hipEventDisableTiming), "event");
+    if (g.world == 1) {
+      // one rank: the gather stores straight into the pinned totals (no D2H copy behind it)
+      void* dp = nullptr;
+      hchk(hipHostGetDevicePointer(&dp, g.tot_pin.p, 0), "hipHostGetDevicePointer");
+      hchk(launch_vote_gather(r.totals.p, q, r.d_err.p, static_cast<uint64_t*>(dp), r.s), "vote gather");
+      return;
+    }
     hchk(launch_vote_gather(r.totals.p, q, r.d_err.p, r.t64.p, r.s), "vote gather");
     bufs.push_back(r.t64.p);
     streams.push_back(r.s);
@@ -775,7 +775,9 @@ static void tally_gather_enqueue(Engine& g, const VoteGatherSlots& q) {
     hchk(hipSetDevice(g.rk[0].dev), "hipSetDevice");
     hchk(hipStreamWaitEvent(g.rk[0].s, g.rk[0].ev_t64, 0), "wait");
   }
-  hchk(hipMemcpyAsync(g.tot_pin.p, g.rk[0].t64.p, (kJustifySlots + 1) * 8, hipMemcpyDeviceToHost, g.rk[0].s), "D2H");
+  if (g.world > 1)
+    hchk(hipMemcpyAsync(g.tot_pin.p, g.rk[0].t64.p, (kJustifySlots + 1) * 8, hipMemcpyDeviceToHost, g.rk[0].s),
+         "D2H");
   if (!g.ev_totals) hchk(hipEventCreateWithFlags(&g.ev_totals, hipEventDisableTiming), "event");
   hchk(hipEventRecord(g.ev_totals, g.rk[0].s), "event");
 }
@@ -885,7 +887,7 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, AttLo
   if (k > 8ull * a.bf_len) throw Panic{"calculateBlockVoteCache: CheckBit index out of range (core.go:330)"};
   g.q_comm.push_back(c);
   g.q_skip.push_back(skip);
-  g.q_ids.insert(g.q_ids.end(), parents.begin(), parents.end());
+  for (size_t j = 0; j < 64; ++j) g.q_slots.push_back(j < parents.size() ? g.id_slot[parents[j]] : UINT32_MAX);
   const uint8_t* bf = a.at(a.bf_off);
   g.q_bits.insert(g.q_bits.end(), bf, bf + (k + 7) / 8);
   g.q_boffs.push_back(g.q_bits.size());

@@ -96,6 +96,8 @@ struct FusedArgs {
   uint64_t* total_next;
   const uint32_t* att_csize;  // [natt] the size of each attestation's committee (a layout of the
                               //   inputs made at upload, so the length check needs no coffs hop)
+  const uint4* items_ci;      // [B][nitems] each piece's FusedCommittee {boff lo, boff hi, nbits,
+                              //   ga} per instance, read beside its item (no items -> cinfo hop)
 };
 // The single-launch step's limits: every block counts the instance's bitfields itself and the
 // last block keeps one LDS word per crosslink record.

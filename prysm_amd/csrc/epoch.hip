@@ -955,11 +955,17 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     // {first position, count, committee, committee start}
     const uint4 it = have ? items_ro[item] : make_uint4((uint32_t)a.val_offset, 0, 0, (uint32_t)a.val_offset);
     const uint64_t ws = it.x, we = (uint64_t)it.x + it.y, cb = it.w;
+    FusedCommittee ci;  // loaded beside the item: no dependent hop before the stream loads
+    {
+      const uint4 ic = have ? f.items_ci[inst * f.nitems + item] : make_uint4(0, 0, 0, kNoAtt);
+      ci.boff = pack64(ic.x, ic.y);
+      ci.nbits = ic.z;
+      ci.ga = ic.w;
+    }
     const uint64_t p0 = (ws - a.val_offset) & ~1ull;  // local and even: the 16-B pair of ws
     uint64_t* Bal = a.balance + inst * f.vstride;
     const uint64_t* S = a.start + inst * f.vstride;
     const uint64_t* E = a.end + inst * f.vstride;
-    const FusedCommittee ci = cinfo_ro[inst * f.ncomm + it.z];
     uint4 qb[2], qs[2], qe[2];
     uint2 cix[2];
     uint32_t lcw_[2];  // f.lastco: the words holding the pair's reward bits
@@ -992,7 +998,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
       // branch-free, clamped: issued with the stream loads (bits past the bitfield are masked
       // below; the pre pass has raised that panic)
       by0[j] = by1[j] = 0;
-      if (!(MODE & 1) && ci.ga < kNoAtt && ci.nbits) {
+      if (!ONE && !(MODE & 1) && ci.ga < kNoAtt && ci.nbits) {  // (ONE: from LDS, below)
         const uint64_t q = g - cb, last = ci.nbits - 1;
         by0[j] = a.bits[ci.boff + ((q < last ? q : last) >> 3)];
         by1[j] = a.bits[ci.boff + ((q + 1 < last ? q + 1 : last) >> 3)];
@@ -1042,6 +1048,15 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
       thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (tdep_ro[inst] * 2ull);
       skip = ferr != 0 || (thr && rwd_err);
       applied = thr && !skip;
+      if (!(MODE & 1) && ci.ga < kNoAtt && ci.nbits) {  // the committee's bitfield bytes, staged above
+        const uint8_t* lb8 = reinterpret_cast<const uint8_t*>(lbits) + (ci.boff - pbase);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const uint64_t q = a.val_offset + p0 + (uint64_t)j * 128 + 2 * lane - cb, last = ci.nbits - 1;
+          by0[j] = lb8[(q < last ? q : last) >> 3];
+          by1[j] = lb8[(q + 1 < last ? q + 1 : last) >> 3];
+        }
+      }
     }
     // crosslink tallies on the pre-reward balances (core.go:533-545): position g of the
     // committee is bit g - cb of each of its attestations' bitfields

@@ -539,13 +539,13 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
     }
     if (st->nrec && (rc = upload(s, &recd, h->rec_dynasty, (size_t)st->B * st->nrec))) break;
     uint32_t *d_catt_offs = nullptr, *d_catt = nullptr;
-    uint4* d_items = nullptr;
+    uint4 *d_items = nullptr, *d_items_ci = nullptr;
     FusedCommittee* d_cinfo = nullptr;
     uint64_t nitems = 0;
+    std::vector<uint4> items;
     if (st->fused) {
       // committee pieces inside [lo, hi): <= 256 positions from the committee's first even
       // local position (local index = position - lo; the kernel pairs even local indices)
-      std::vector<uint4> items;
       for (uint64_t c = 0; c < st->ncomm; ++c) {
         const uint64_t cb = h->coffs[c], ce = h->coffs[c + 1];
         const uint64_t r0 = std::max(cb, s.lo), r1 = std::min(ce, s.hi), base = s.lo + ((r0 - s.lo) & ~1ull);
@@ -556,7 +556,15 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
         }
       }
       nitems = items.size();
+      // each piece's committee info per instance, read beside the piece (no items -> cinfo hop)
+      std::vector<uint4> ic((size_t)st->B * nitems);
+      for (uint64_t b = 0; b < st->B; ++b)
+        for (uint64_t k = 0; k < nitems; ++k) {
+          const FusedCommittee& ci = cinfo[b * st->ncomm + items[k].z];
+          ic[b * nitems + k] = make_uint4((uint32_t)ci.boff, (uint32_t)(ci.boff >> 32), ci.nbits, ci.ga);
+        }
       if ((rc = upload(s, &d_items, items.data(), items.size())) || (rc = upload(s, &d_cinfo, cinfo.data(), cinfo.size())) ||
+          (rc = upload(s, &d_items_ci, ic.data(), ic.size())) ||
           (rc = upload(s, &d_catt_offs, catt_offs.data(), catt_offs.size())) ||
           (rc = upload(s, &d_catt, catt.data(), catt.size())))
         break;
@@ -622,6 +630,7 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
         q.f.items = d_items;
         q.f.nitems = nitems;
         q.f.cinfo = d_cinfo + i0 * st->ncomm;
+        q.f.items_ci = d_items_ci + i0 * nitems;
         q.f.catt_offs = d_catt_offs + i0 * (st->ncomm + 1);
         q.f.catt = d_catt + i0 * st->natt;
         q.f.ncomm = st->ncomm;

@@ -16,9 +16,8 @@ struct VoteIdArgs {
   const uint32_t* att_comm;  // natt
   const uint8_t* bits;       // CSR bitfields
   const uint64_t* boffs;     // natt+1
-  const uint32_t* ids;       // natt x 64 hash-log ids of the signed parent hashes
+  const uint32_t* slots;     // natt x 64 vote-cache slots of the signed parent hashes
   const uint64_t* skip;      // natt: bit j set = parent j equals an oblique parent hash
-  const uint32_t* id_slot;   // hash-log id -> vote-cache slot
   uint64_t natt;
   const uint64_t* balance;
   uint64_t nval;
@@ -30,12 +29,16 @@ struct VoteIdArgs {
   uint32_t* ubits;   // per (slot, committee) group: union bitfield, cwords words (zero between flushes)
   uint32_t* uflag;   // per group: touched in this flush (zero between flushes)
   uint32_t* leader;  // the items that tally their group (compact list, *nlead entries)
-  uint32_t* nlead;
+  uint32_t* nlead;       // zero when the flush starts (the previous flush's leader pass zeroed it)
+  uint32_t* nlead_next;  // the other counter: zeroed here for the next flush
   uint64_t ncomm, cwords;
   uint64_t val_offset;   // a validator-range shard: balance and bitmaps hold [val_offset, val_offset + nval)
   uint64_t nval_global;  // of nval_global validators (0: nval, unsharded)
 };
 hipError_t launch_vote_ids(const VoteIdArgs& a, hipStream_t s);
+// Copy `bytes` (a multiple of 16) from mapped pinned host memory to device memory in a kernel on
+// stream s: 16 B per lane, so the bytes cross PCIe in one round trip of coalesced reads.
+hipError_t launch_stage_h2d(const void* host_mapped, void* dev, uint64_t bytes, hipStream_t s);
 
 // The 64 totals a stateRecalc's justification loop reads (blockchain/core.go:413-418) and the
 // sticky tally panic flag, gathered into out[0..64] (slot UINT32_MAX: no map entry, total 0):

@@ -11,6 +11,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "../../include/prysm_hip.h"
 #include "votes.h"
 
@@ -143,7 +146,7 @@ pz_vote_union_kernel(VoteIdArgs a) {
   const uint64_t att = item >> 6;
   if (att >= a.natt) return;
   if ((a.skip[att] >> (item & 63)) & 1) return;  // an oblique parent hash (core.go:313-320) is skipped
-  const uint32_t slot = a.id_slot[a.ids[item]];
+  const uint32_t slot = a.slots[item];
   const uint32_t c = a.att_comm[att];
   const uint64_t grp = (uint64_t)slot * a.ncomm + c;
   const uint64_t k = a.coffs[c + 1] - a.coffs[c];
@@ -164,14 +167,16 @@ pz_vote_union_kernel(VoteIdArgs a) {
 }
 
 // A fixed grid of kLeaderWaves waves walks the compact leader list of pass 1.
-constexpr uint32_t kLeaderWaves = 2048;
+constexpr uint32_t kLeaderWaves = 4096;  // 2048 / 4096 / 8192 A/B: profiles/r03/replay_leader_waves_r3m.txt
 extern "C" __global__ void __launch_bounds__(256)
 pz_vote_leader_kernel(VoteIdArgs a) {
   const uint32_t n = *a.nlead;
-  for (uint32_t li = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; li < n; li += kLeaderWaves) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.nlead_next = 0;  // (no wave of this flush reads it)
+  const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t li = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; li < n; li += waves) {
     const uint64_t item = a.leader[li];
     const uint64_t att = item >> 6;
-    const uint32_t slot = a.id_slot[a.ids[item]];
+    const uint32_t slot = a.slots[item];
     const uint32_t c = a.att_comm[att];
     const uint64_t grp = (uint64_t)slot * a.ncomm + c;
     uint32_t* u = a.ubits + grp * a.cwords;
@@ -190,11 +195,28 @@ pz_vote_leader_kernel(VoteIdArgs a) {
 
 hipError_t launch_vote_ids(const VoteIdArgs& a, hipStream_t s) {
   if (!a.natt) return hipSuccess;
-  hipError_t e = hipMemsetAsync(a.nlead, 0, 4, s);
-  if (e != hipSuccess) return e;
   const uint64_t uthreads = a.natt * 64 * kUnionLanes;
   hipLaunchKernelGGL(pz_vote_union_kernel, dim3((uint32_t)((uthreads + 255) / 256)), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(pz_vote_leader_kernel, dim3(kLeaderWaves / 4), dim3(256), 0, s, a);
+  static const uint32_t lw = [] {  // tools/ A/B knob for the leader grid
+    const char* e = std::getenv("PZ_LEADER_WAVES");
+    return e ? (uint32_t)std::max(4L, std::atol(e)) : kLeaderWaves;
+  }();
+  hipLaunchKernelGGL(pz_vote_leader_kernel, dim3(lw / 4), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+pz_stage_h2d_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n16) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+hipError_t launch_stage_h2d(const void* host_mapped, void* dev, uint64_t bytes, hipStream_t s) {
+  const uint64_t n16 = bytes / 16;
+  if (!n16) return hipSuccess;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n16 + 255) / 256, 1024);
+  hipLaunchKernelGGL(pz_stage_h2d_kernel, dim3(blocks), dim3(256), 0, s, static_cast<const uint4*>(host_mapped),
+                     static_cast<uint4*>(dev), n16);
   return hipGetLastError();
 }
 

@@ -551,7 +551,7 @@ __device__ __forceinline__ uint64_t record_size(const AttArgs& a, uint64_t i) {
 extern "C" __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))
 pz_wire_att_kernel(AttArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t stage[kWaves][kRecs][kStageAlloc];
-  __shared__ uint64_t s_excl[kTile + 1], s_wave[kWaves], s_part[kWaves], s_base;
+  __shared__ uint64_t s_excl[kTile + 1], s_wave[kWaves], s_part[kWaves];
   __shared__ uint32_t s_tile, s_first;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid == 0) s_tile = atomicAdd(a.ticket, 1u);
