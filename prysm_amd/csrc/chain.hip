@@ -383,7 +383,7 @@ struct RankDev {
   DevArr<uint8_t> d_qpack;
   DevArr<uint64_t> d_err;      // sticky tally panic flag
   DevArr<uint32_t> ubits, uflag;
-  DevArr<uint32_t> d_leader;  // [2 leader counters, used alternately][leader list]
+  DevArr<uint32_t> d_leader;  // [2 leader counters, used alternately; pad][uint4 leader records]
   uint32_t lead_par = 0;      // the counter this rank's next flush counts in
   DevArr<uint64_t> t64;        // the gathered justification totals + panic flag (65 words)
   // epoch scratch: red = {scal[8], vote[natt], total[natt]} (one all-reduce when sharded)
@@ -685,11 +685,12 @@ static bool flush_votes_enqueue(Engine& g) {
   each_rank(g, [&](RankDev& r) {
     // Growing a device buffer frees the old one, which in-flight flushes may still read:
     // drain the stream first (rare: the buffers double).
-    if (total > r.d_qpack.n || natt * 64 + 2 > r.d_leader.n) {
+    const uint64_t lead_words = 4 + natt * 64 * 4;  // 2 counters (+ pad to 16 B), then uint4 records
+    if (total > r.d_qpack.n || lead_words > r.d_leader.n) {
       hchk(hipStreamSynchronize(r.s), "sync");
       if (total > r.d_qpack.n) check(r.d_qpack.alloc(std::max<uint64_t>(total, 2 * r.d_qpack.n)));
-      if (natt * 64 + 2 > r.d_leader.n) {
-        check(r.d_leader.alloc(std::max<uint64_t>(natt * 64 + 2, 2 * r.d_leader.n)));
+      if (lead_words > r.d_leader.n) {
+        check(r.d_leader.alloc(std::max<uint64_t>(lead_words, 2 * r.d_leader.n)));
         hchk(hipMemsetAsync(r.d_leader.p, 0, 8, r.s), "memset");  // both counters
       }
     }
@@ -725,7 +726,7 @@ static bool flush_votes_enqueue(Engine& g) {
     v.err = r.d_err.p;  // sticky: read (and the chain poisoned) at the next sync point
     v.ubits = r.ubits.p;
     v.uflag = r.uflag.p;
-    v.leader = r.d_leader.p + 2;
+    v.leader = reinterpret_cast<uint4*>(r.d_leader.p + 4);
     v.nlead = r.d_leader.p + r.lead_par;  // counted by this flush's union pass
     v.nlead_next = r.d_leader.p + (r.lead_par ^ 1);  // zeroed by its leader pass for the next flush
     r.lead_par ^= 1;

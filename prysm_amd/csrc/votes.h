@@ -28,7 +28,8 @@ struct VoteIdArgs {
   uint64_t* err;
   uint32_t* ubits;   // per (slot, committee) group: union bitfield, cwords words (zero between flushes)
   uint32_t* uflag;   // per group: touched in this flush (zero between flushes)
-  uint32_t* leader;  // the items that tally their group (compact list, *nlead entries)
+  uint4* leader;     // the groups to tally (compact list, *nlead entries): {slot, committee,
+                     //   committee's first member offset, committee size}
   uint32_t* nlead;       // zero when the flush starts (the previous flush's leader pass zeroed it)
   uint32_t* nlead_next;  // the other counter: zeroed here for the next flush
   uint64_t ncomm, cwords;

@@ -71,6 +71,7 @@ __device__ __forceinline__ void tally_item_x4(const uint32_t* __restrict__ commi
   if (!nval_global) nval_global = nval;
   const int lane = threadIdx.x & 63;
   uint32_t v[4], word[4];
+  uint64_t bal[4];
   bool on[4];
   uint64_t err = 0, add = 0;
 #pragma unroll
@@ -96,6 +97,7 @@ __device__ __forceinline__ void tally_item_x4(const uint32_t* __restrict__ commi
     const uint64_t lv = (uint64_t)v[q] - lo;
     if (on[q] && lv >= nval) on[q] = false;  // another rank's validator
     word[q] = on[q] ? bm[lv >> 5] : 0xFFFFFFFFu;
+    bal[q] = on[q] ? balance[lv] : 0;  // issued with the word: used only if the atomic sets the bit
   }
   uint32_t old[4];
 #pragma unroll
@@ -108,7 +110,7 @@ __device__ __forceinline__ void tally_item_x4(const uint32_t* __restrict__ commi
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const uint64_t lv = (uint64_t)v[q] - lo;
-    if (on[q] && !(old[q] & (1u << (lv & 31)))) add += balance[lv];
+    if (on[q] && !(old[q] & (1u << (lv & 31)))) add += bal[q];
   }
   add = wsum64(add);
   const uint64_t e1 = __ballot(err != 0);
@@ -145,13 +147,14 @@ pz_vote_union_kernel(VoteIdArgs a) {
   const uint32_t sub = (uint32_t)(t % kUnionLanes);
   const uint64_t att = item >> 6;
   if (att >= a.natt) return;
-  if ((a.skip[att] >> (item & 63)) & 1) return;  // an oblique parent hash (core.go:313-320) is skipped
+  // every load that depends only on the item first (one round trip), the skip test after
+  const uint64_t sk = a.skip[att];
   const uint32_t slot = a.slots[item];
   const uint32_t c = a.att_comm[att];
+  const uint64_t bb = a.boffs[att], nbytes = a.boffs[att + 1] - bb;  // the queue holds ceil(k/8) bytes
+  if ((sk >> (item & 63)) & 1) return;  // an oblique parent hash (core.go:313-320) is skipped
   const uint64_t grp = (uint64_t)slot * a.ncomm + c;
-  const uint64_t k = a.coffs[c + 1] - a.coffs[c];
-  const uint64_t bb = a.boffs[att], blen = a.boffs[att + 1] - bb;
-  const uint64_t nbytes = min(blen, (k + 7) / 8);  // bits at positions >= k are never read
+  const uint64_t cb = a.coffs[c], ce = a.coffs[c + 1];  // (with the bit loads below)
   uint32_t* u = a.ubits + grp * a.cwords;
   for (uint64_t w = sub; 4 * w < nbytes; w += kUnionLanes) {
     uint32_t x = 0;
@@ -162,7 +165,9 @@ pz_vote_union_kernel(VoteIdArgs a) {
   }
   if (sub == 0) {
     a.present[slot] = 1;  // the map entry exists (core.go:322-326)
-    if (atomicOr(&a.uflag[grp], 1u) == 0) a.leader[atomicAdd(a.nlead, 1u)] = (uint32_t)item;
+    // the leader's record carries what its pass needs, so that pass starts at the committee
+    if (atomicOr(&a.uflag[grp], 1u) == 0)
+      a.leader[atomicAdd(a.nlead, 1u)] = make_uint4(slot, c, (uint32_t)cb, (uint32_t)(ce - cb));
   }
 }
 
@@ -174,13 +179,11 @@ pz_vote_leader_kernel(VoteIdArgs a) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.nlead_next = 0;  // (no wave of this flush reads it)
   const uint32_t waves = gridDim.x * (blockDim.x >> 6);
   for (uint32_t li = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; li < n; li += waves) {
-    const uint64_t item = a.leader[li];
-    const uint64_t att = item >> 6;
-    const uint32_t slot = a.slots[item];
-    const uint32_t c = a.att_comm[att];
+    const uint4 rec = a.leader[li];  // {slot, committee, its first member, its size}
+    const uint32_t slot = rec.x, c = rec.y;
     const uint64_t grp = (uint64_t)slot * a.ncomm + c;
     uint32_t* u = a.ubits + grp * a.cwords;
-    const uint64_t cb = a.coffs[c], k = a.coffs[c + 1] - cb;
+    const uint64_t cb = rec.z, k = rec.w;
     if (k <= 256)
       tally_item_x4(a.committee, cb, k, reinterpret_cast<const uint8_t*>(u), (k + 7) / 8, a.balance, a.nval,
                     a.bitmaps + (uint64_t)slot * a.words_per_slot, a.totals + slot, a.err, a.val_offset, a.nval_global);
