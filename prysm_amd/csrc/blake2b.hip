@@ -369,12 +369,15 @@ __device__ __forceinline__ void load_block_csr(const uint8_t* p, uint64_t rem, u
   for (int k = 0; k < 16; ++k) m[k] = pack(d[2 * k], d[2 * k + 1]);
 }
 
+// Message i is msgs[begs[i], ends[i]): CSR passes (offsets, offsets + 1); the span form
+// (launch_b2b_spans) hashes messages that overlap or leave gaps, e.g. attestation records
+// inside their blocks' bytes.
 extern "C" __global__ void __launch_bounds__(256)
-pz_b2b_csr_kernel(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ offsets,
-                  uint64_t n, uint8_t* __restrict__ out, uint32_t out_bytes) {
+pz_b2b_csr_kernel(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ begs,
+                  const uint64_t* __restrict__ ends, uint64_t n, uint8_t* __restrict__ out, uint32_t out_bytes) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint64_t beg = offsets[i], end = offsets[i + 1];
+  const uint64_t beg = begs[i], end = ends[i];
   const uint64_t len = end - beg;
   const uint64_t nblocks = len == 0 ? 1 : (len + 127) / 128;
   uint64_t h[8];
@@ -397,35 +400,42 @@ pz_b2b_csr_kernel(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__
 // ------------------------------------------------------------------------------------------
 // processAttestation messages (blockchain/core.go:277-290), assembled on the fly from device
 // data instead of being materialised on the host: message i is
-//   hdr[i][0..10) | for r < 64: hlog[ids[64 i + r]] (32 B) ' ' | sbh[sbh_offs[i] .. sbh_offs[i+1])
+//   hdr[i][0..10) | for r < 64: hlog[id(i, r)] (32 B) ' ' | sbh[sbh_offs[i] .. sbh_offs[i+1])
 // (10 + 64 x 33 + len(ShardBlockHash) bytes; the 64 signed parent hashes are ids into the
-// engine's hash log, which holds the block digests the GPU already computed).  One lane per
+// engine's hash log, which holds the block digests the GPU already computed: the first nw
+// from the engine's recent-hash trail, the rest the attestation's own oblique ids).  One lane per
 // message; each 128-byte block is assembled into the lane's LDS row (33-dword stride, no
 // bank conflicts), then read back as the 16 message words.
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t kAttMsgParents = 64, kAttMsgRec = 33, kAttMsgHdr = 10;
 
-__device__ __forceinline__ uint32_t attmsg_byte(uint32_t o, const uint8_t* hd, const uint32_t* id,
-                                                const uint8_t* hlog, const uint8_t* sb, uint32_t sl) {
+__device__ __forceinline__ uint32_t attmsg_byte(uint32_t o, const uint8_t* hd, const uint32_t* win, uint32_t nw,
+                                                const uint32_t* obl, const uint8_t* hlog, const uint8_t* sb,
+                                                uint32_t sl) {
   if (o < kAttMsgHdr) return hd[o];
   o -= kAttMsgHdr;
   if (o < kAttMsgParents * kAttMsgRec) {
     const uint32_t r = o / kAttMsgRec, w = o - kAttMsgRec * r;
-    return w < 32 ? hlog[(uint64_t)id[r] * 32 + w] : 0x20u;
+    const uint32_t id = r < nw ? win[r] : obl[r - nw];
+    return w < 32 ? hlog[(uint64_t)id * 32 + w] : 0x20u;
   }
   o -= kAttMsgParents * kAttMsgRec;
   return o < sl ? sb[o] : 0u;
 }
 
 extern "C" __global__ void __launch_bounds__(256)
-pz_b2b_attmsg_kernel(const uint8_t* __restrict__ hlog, const uint32_t* __restrict__ ids,
+pz_b2b_attmsg_kernel(const uint8_t* __restrict__ hlog, const uint32_t* __restrict__ trail,
+                     const AttMsgRef* __restrict__ ref, const uint32_t* __restrict__ oids,
                      const uint8_t* __restrict__ hdr, const uint8_t* __restrict__ sbh,
                      const uint64_t* __restrict__ sbh_offs, uint64_t n, uint8_t* __restrict__ out) {
   __shared__ uint32_t rows[256 * 33];
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;  // no block-wide barrier below: lanes only touch their own row
   uint32_t* row = rows + threadIdx.x * 33;
-  const uint32_t* id = ids + i * kAttMsgParents;
+  const AttMsgRef rf = ref[i];
+  const uint32_t* win = trail + rf.wstart;
+  const uint32_t* obl = oids + rf.ooff;
+  const uint32_t nw = rf.nw;
   const uint8_t* hd = hdr + i * 16;
   const uint8_t* sb = sbh + sbh_offs[i];
   const uint32_t sl = (uint32_t)(sbh_offs[i + 1] - sbh_offs[i]);
@@ -436,8 +446,9 @@ pz_b2b_attmsg_kernel(const uint8_t* __restrict__ hlog, const uint32_t* __restric
   for (uint64_t t = 0; t < nblocks; ++t) {
     for (uint32_t k = 0; k < 32; ++k) {
       const uint32_t o = (uint32_t)(t * 128) + 4 * k;
-      row[k] = attmsg_byte(o, hd, id, hlog, sb, sl) | (attmsg_byte(o + 1, hd, id, hlog, sb, sl) << 8) |
-               (attmsg_byte(o + 2, hd, id, hlog, sb, sl) << 16) | (attmsg_byte(o + 3, hd, id, hlog, sb, sl) << 24);
+      row[k] = attmsg_byte(o, hd, win, nw, obl, hlog, sb, sl) | (attmsg_byte(o + 1, hd, win, nw, obl, hlog, sb, sl) << 8) |
+               (attmsg_byte(o + 2, hd, win, nw, obl, hlog, sb, sl) << 16) |
+               (attmsg_byte(o + 3, hd, win, nw, obl, hlog, sb, sl) << 24);
     }
     uint64_t m[16];
 #pragma unroll
@@ -503,15 +514,24 @@ hipError_t launch_b2b_csr(const uint8_t* msgs, const uint64_t* offsets, uint64_t
   if (n == 0) return hipSuccess;
   const uint64_t blocks = (n + 255) / 256;
   hipLaunchKernelGGL(pz_b2b_csr_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, msgs,
-                     offsets, n, out, out_bytes);
+                     offsets, offsets + 1, n, out, out_bytes);
   return hipGetLastError();
 }
 
-hipError_t launch_b2b_attmsg(const uint8_t* hlog, const uint32_t* ids, const uint8_t* hdr, const uint8_t* sbh,
-                            const uint64_t* sbh_offs, uint64_t n, uint8_t* out, hipStream_t stream) {
+hipError_t launch_b2b_spans(const uint8_t* msgs, const uint64_t* begs, const uint64_t* ends, uint64_t n, uint8_t* out,
+                            uint32_t out_bytes, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(pz_b2b_attmsg_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, hlog, ids, hdr,
-                     sbh, sbh_offs, n, out);
+  hipLaunchKernelGGL(pz_b2b_csr_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, msgs, begs, ends, n,
+                     out, out_bytes);
+  return hipGetLastError();
+}
+
+hipError_t launch_b2b_attmsg(const uint8_t* hlog, const uint32_t* trail, const AttMsgRef* ref, const uint32_t* oids,
+                             const uint8_t* hdr, const uint8_t* sbh, const uint64_t* sbh_offs, uint64_t n, uint8_t* out,
+                             hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(pz_b2b_attmsg_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, hlog, trail, ref,
+                     oids, hdr, sbh, sbh_offs, n, out);
   return hipGetLastError();
 }
 

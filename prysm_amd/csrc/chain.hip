@@ -56,9 +56,88 @@ struct H32Hash {
 };
 static const H32 kZero = {};
 
+// Open-addressing table keyed by 32-byte hashes: linear probing, power-of-two capacity, load
+// at most 1/2.  The probed array holds 16-B slots {tag, value, used}: a 64-bit tag of the key
+// rejects a mismatch without touching the key, which sits in a parallel array.  The walk
+// inserts every block hash (the saved set) and every logged hash (the vote-cache slots);
+// node-based std::unordered_* paid a malloc per insert and a pointer chase per probe (~8 % of
+// the walk), 40-B inline entries a cache miss per probe (tools/walk_sampler.py, profiles/r03).
+template <typename V>
+struct H32Table {
+  struct Slot {
+    uint64_t tag;
+    V v;
+    uint8_t used;
+  };
+  std::vector<Slot> t;
+  std::vector<H32> keys;
+  size_t n = 0, mask = 0;
+  // digests are uniform, but BytesToHash of a short oblique hash is zero-padded on the left:
+  // both ends go into the tag, and the slot index takes its high bits after a multiply
+  static uint64_t tag_of(const H32& h) {
+    uint64_t a, b;
+    std::memcpy(&a, h.b, 8);
+    std::memcpy(&b, h.b + 24, 8);
+    return a ^ (b * 0x9E3779B97F4A7C15ull);
+  }
+  size_t index(uint64_t tag) const { return (size_t)((tag * 0xD6E8FEB86659FD93ull) >> 32) & mask; }
+  size_t size() const { return n; }
+  void clear() {
+    t.clear();
+    keys.clear();
+    n = mask = 0;
+  }
+  void grow() {
+    std::vector<Slot> old;
+    std::vector<H32> oldk;
+    old.swap(t);
+    oldk.swap(keys);
+    const size_t cap = old.empty() ? 1024 : 2 * old.size();
+    t.assign(cap, Slot{0, V{}, 0});
+    keys.resize(cap);
+    mask = cap - 1;
+    for (size_t j = 0; j < old.size(); ++j)
+      if (old[j].used) {
+        size_t i = index(old[j].tag);
+        while (t[i].used) i = (i + 1) & mask;
+        t[i] = old[j];
+        keys[i] = oldk[j];
+      }
+  }
+  void reserve(size_t m) {
+    while (2 * m > t.size()) grow();
+  }
+  const V* find(const H32& k) const {
+    if (!n) return nullptr;
+    const uint64_t tg = tag_of(k);
+    for (size_t i = index(tg);; i = (i + 1) & mask) {
+      if (!t[i].used) return nullptr;
+      if (t[i].tag == tg && keys[i] == k) return &t[i].v;
+    }
+  }
+  bool count(const H32& k) const { return find(k) != nullptr; }
+  // inserts (k, v) unless k is present; returns the stored value
+  V insert(const H32& k, V v) {
+    if (2 * (n + 1) > t.size()) grow();
+    const uint64_t tg = tag_of(k);
+    size_t i = index(tg);
+    for (; t[i].used; i = (i + 1) & mask)
+      if (t[i].tag == tg && keys[i] == k) return t[i].v;
+    t[i] = Slot{tg, v, 1};
+    keys[i] = k;
+    ++n;
+    return v;
+  }
+};
+
 // go-ethereum common.BytesToHash: last 32 bytes, right-aligned.
 static H32 bytes_to_hash(const uint8_t* p, size_t n) {
-  H32 h = kZero;
+  H32 h;
+  if (n >= 32) {
+    std::memcpy(h.b, p + n - 32, 32);
+    return h;
+  }
+  h = kZero;
   if (n > 32) {
     p += n - 32;
     n = 32;
@@ -165,7 +244,8 @@ struct OblSpan {
 };
 
 // One AttestationRecord (messages.proto:110-119): its canonical encoding is a span of the call
-// arena's copy of the input blocks, which the record keeps alive (AttP aliases the arena).
+// arena's copy of the input blocks.  Records are referred to by plain pointers; the Engine
+// keeps every arena that a live state's pending attestations point into (keep_arenas).
 struct Att {
   const uint8_t* base = nullptr;  // the encoding
   uint32_t len = 0;
@@ -175,14 +255,26 @@ struct Att {
   OblSpan obl;
   const uint8_t* at(uint32_t off) const { return base + off; }
 };
-using AttP = std::shared_ptr<const Att>;
+using AttP = const Att*;
+
+// A block's attestations: a run of the arena's record pointers.
+struct AttSpan {
+  const AttP* p = nullptr;
+  uint32_t n = 0;
+  const AttP* begin() const { return p; }
+  const AttP* end() const { return p + n; }
+  size_t size() const { return n; }
+  AttP operator[](size_t i) const { return p[i]; }
+};
 
 // One pz_chain_process_blocks call's input: a copy of its serialized blocks and every
 // attestation record parsed from them, allocated once (per-record allocations made the parse
-// allocator-bound).  Records that stay pending after the call keep it alive.
+// allocator-bound).  The Engine keeps it while a live state's pending attestations point in.
 struct CallArena {
-  std::unique_ptr<uint8_t[]> bytes;  // (not zero-filled)
+  uint8_t* bytes = nullptr;  // (not zero-filled) the Engine's pinned arena, or `own`
+  std::unique_ptr<uint8_t[]> own;
   std::vector<Att> atts;  // reserved to the exact count: AttP points into it
+  std::vector<AttP> ptrs;  // &atts[i], in order: each Block's AttSpan is a run of it
   std::vector<std::pair<uint32_t, uint32_t>> obl;  // reserved to a bound: Att::obl points into it
 };
 
@@ -230,15 +322,17 @@ struct Block {
   size_t len;
   uint64_t slot = 0;
   H32 parent = kZero;  // Block.ParentHash(): copy into [32]byte (types/block.go:80-84)
-  std::vector<AttP> atts;
+  AttSpan atts;
 };
 
 // messages.pb.go:224-232: 1 bytes, 2 varint, 3-6 bytes, 7 Timestamp, 8 repeated records
-static bool parse_block(const uint8_t* p, size_t n, Block* b, const std::shared_ptr<CallArena>& ar) {
+static bool parse_block(const uint8_t* p, size_t n, Block* b, CallArena* ar) {
   static const uint32_t kTypes[9] = {9, 2, 0, 2, 2, 2, 2, 2, 2};
   static const uint32_t kTsTypes[3] = {9, 0, 0};
   b->data = p;
   b->len = n;
+  b->atts.p = ar->ptrs.data() + ar->ptrs.size();  // (reserved: never reallocates)
+  b->atts.n = 0;
   Reader r{p, p + n};
   uint32_t prev = 0, f, wt;
   const uint8_t* q;
@@ -270,7 +364,8 @@ static bool parse_block(const uint8_t* p, size_t n, Block* b, const std::shared_
       ar->atts.emplace_back();
       Att* a = &ar->atts.back();
       if (!parse_att(q, len, a, ar->obl)) return false;
-      b->atts.push_back(AttP(ar, a));  // aliases the arena: no allocation per record
+      ar->ptrs.push_back(a);
+      ++b->atts.n;
     }
   }
   return r.ok;
@@ -284,8 +379,11 @@ struct Crosslink {
 
 struct AState {               // types.ActiveState
   std::vector<AttP> pending;  // PendingAttestations
-  std::vector<H32> recent;    // RecentBlockHashes, normalised
-  std::vector<uint32_t> recent_ids;  // the same hashes as ids into Engine::hlog
+  // RecentBlockHashes (normalised) as hash-log ids: Engine::trail[tail - len, tail).  The
+  // states of one chain push onto the trail's end in turn, so a window is a range of it, not a
+  // copy per state (push_recent re-appends a window that is not at the end).
+  uint64_t tail = 0;
+  uint32_t len = 0;
   bool recent_raw_empty = false;  // genesis: every entry is a zero-length byte slice
   bool cache_nil = false;     // the shared vote-cache map, or nil (SetBlockVoteCache(nil))
 };
@@ -321,14 +419,24 @@ struct DevArr {
 struct PinBuf {
   uint8_t* p = nullptr;
   size_t n = 0;
+  void* d = nullptr;  // its device address, looked up once (a runtime call per use showed in the walk)
   int reserve(size_t bytes) {
     if (bytes <= n && p) return PZ_OK;
     if (p) (void)hipHostFree(p);
     p = nullptr;
+    d = nullptr;
     n = 0;
     hipError_t e = hipHostMalloc((void**)&p, std::max<size_t>(bytes, 1), hipHostMallocDefault);
     if (e != hipSuccess) return hip_fail(e, "hipHostMalloc");
     n = bytes;
+    return PZ_OK;
+  }
+  int dev(void** out) {
+    if (!d) {
+      hipError_t e = hipHostGetDevicePointer(&d, p, 0);
+      if (e != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer");
+    }
+    *out = d;
     return PZ_OK;
   }
   ~PinBuf() {
@@ -422,7 +530,7 @@ struct Engine {
   std::vector<std::vector<std::pair<uint64_t, uint32_t>>> lookup;  // [array] -> (shard, committee id)
   std::string arrays_enc;  // field 12 of the CrystallizedState, every array
   // block vote cache (one map shared by every ActiveState)
-  std::unordered_map<H32, uint32_t, H32Hash> slot_of;
+  H32Table<uint32_t> slot_of;
   std::vector<H32> slot_hash;
   uint64_t cap = 0;
   // pending tally work: per queued attestation its committee, bitfield, the hash-log ids of
@@ -435,6 +543,7 @@ struct Engine {
   // flushes run asynchronously to the walk: the queue is packed into a pinned arena and
   // copied with one H2D per rank; the arena is reused once every rank's copy is done
   uint8_t* q_arena = nullptr;
+  void* q_arena_dev = nullptr;  // its device address
   size_t q_arena_cap = 0;
   bool q_arena_busy = false;
   uint64_t ncomm = 0, cwords = 1;
@@ -462,21 +571,30 @@ struct Engine {
   uint64_t cand_slot = 0;
   AP cand_A;
   CP cand_C;
-  std::unordered_set<H32, H32Hash> saved;
+  H32Table<uint8_t> saved;
+  // the call arenas whose records a live state still holds (pending attestations)
+  std::vector<std::shared_ptr<CallArena>> arenas;
   // append-only hash log: every block digest and oblique parent hash the walk meets gets an
   // id; RecentBlockHashes carry ids too, so signed parent hashes are id ranges (no hashing of
   // 32-byte keys per vote) and the processAttestation messages are assembled on the device
   std::vector<H32> hlog;
   std::vector<uint32_t> id_slot;  // vote-cache slot of each id (resolved when it is logged)
+  std::vector<uint32_t> trail;    // the recent-hash windows of the states (AState::tail, len)
+  DevArr<uint32_t> d_trail;
+  uint64_t d_trail_n = 0;
   DevArr<uint8_t> d_hlog;
   uint64_t d_hlog_n = 0;
   // processAttestation message batch (10-byte header, 64 parent ids, ShardBlockHash)
   std::vector<uint8_t> m_hdr, m_sbh;
-  std::vector<uint32_t> m_ids;
+  std::vector<AttMsgRef> m_ref;   // per message: its parents' trail window and oblique ids
+  std::vector<uint32_t> m_oids;
   std::vector<uint64_t> m_sboff{0};
   DevArr<uint8_t> d_mhdr, d_msbh, d_mout;
-  DevArr<uint32_t> d_mids;
+  DevArr<uint32_t> d_moids;
+  DevArr<AttMsgRef> d_mref;
   DevArr<uint64_t> d_msboff;
+  PinBuf m_pin;  // the message digests' D2H
+  PinBuf arena_pin;  // the call arena's bytes: parsed in place, H2D'd whole for the digest batch
   // wall-time accumulators (seconds) per phase, read by pz_debug_chain_profile
   double prof[kProfSlots] = {};
 };
@@ -594,10 +712,9 @@ static void hash_many(Engine& g, const std::string& data, const std::vector<uint
 
 // ---- vote cache -------------------------------------------------------------------------------
 static uint32_t vote_slot(Engine& g, const H32& h) {
-  auto it = g.slot_of.find(h);
-  if (it != g.slot_of.end()) return it->second;
   const uint32_t s = (uint32_t)g.slot_hash.size();
-  g.slot_of.emplace(h, s);
+  const uint32_t got = g.slot_of.insert(h, s);
+  if (got != s) return got;
   g.slot_hash.push_back(h);
   if (s >= g.cap) {  // grow every rank's device arrays, keeping their contents
     const uint64_t nc = std::max<uint64_t>(64, 2 * g.cap);
@@ -673,6 +790,7 @@ static bool flush_votes_enqueue(Engine& g) {
   if (total > g.q_arena_cap) {
     if (g.q_arena) (void)hipHostFree(g.q_arena);
     g.q_arena = nullptr;
+    g.q_arena_dev = nullptr;
     const size_t cap = std::max(total, 2 * g.q_arena_cap);
     hchk(hipHostMalloc((void**)&g.q_arena, cap, hipHostMallocPortable | hipHostMallocMapped), "hipHostMalloc");
     g.q_arena_cap = cap;
@@ -696,8 +814,8 @@ static bool flush_votes_enqueue(Engine& g) {
     }
     // the pack crosses PCIe in a kernel of this stream (a copy-engine H2D costs ~13 us more on
     // the transition's critical path: the kernel behind it waits for the engine's signal)
-    void* src = nullptr;
-    hchk(hipHostGetDevicePointer(&src, g.q_arena, 0), "hipHostGetDevicePointer");
+    if (!g.q_arena_dev) hchk(hipHostGetDevicePointer(&g.q_arena_dev, g.q_arena, 0), "hipHostGetDevicePointer");
+    void* src = g.q_arena_dev;
     hchk(launch_stage_h2d(src, r.d_qpack.p, total, r.s), "stage H2D");
     if (!r.q_ev) hchk(hipEventCreateWithFlags(&r.q_ev, hipEventDisableTiming), "event");
     hchk(hipEventRecord(r.q_ev, r.s), "event");
@@ -762,7 +880,7 @@ static void tally_gather_enqueue(Engine& g, const VoteGatherSlots& q) {
     if (g.world == 1) {
       // one rank: the gather stores straight into the pinned totals (no D2H copy behind it)
       void* dp = nullptr;
-      hchk(hipHostGetDevicePointer(&dp, g.tot_pin.p, 0), "hipHostGetDevicePointer");
+      check(g.tot_pin.dev(&dp));
       hchk(launch_vote_gather(r.totals.p, q, r.d_err.p, static_cast<uint64_t*>(dp), r.s), "vote gather");
       return;
     }
@@ -801,14 +919,45 @@ static void flush_votes(Engine& g) {
 }
 
 // ---- core.go ------------------------------------------------------------------------------------
-// getSignedParentHashes (core.go:348-360); Go slices up to cap, beyond len panics.
-// Returns ids into the hash log; always 64 of them (end - start + len(obliques)).
-static void signed_parents(Engine& g, const AState& A, uint64_t block_slot, const Att& a, std::vector<uint32_t>& out) {
+// The signed parent hashes of an attestation (getSignedParentHashes, core.go:348-360) as
+// hash-log ids: the window trail[wstart, wstart + nw) of RecentBlockHashes, then the oblique
+// parent hashes (ids obl[0, nobl)); always 64 in all.
+struct Parents {
+  uint64_t wstart = 0;
+  uint32_t nw = 0;
+  std::vector<uint32_t> obl;
+  uint32_t id(const Engine& g, size_t j) const;
+};
+
+uint32_t Parents::id(const Engine& g, size_t j) const { return j < nw ? g.trail[wstart + j] : obl[j - nw]; }
+
+// Hash-log id i of the window of A (RecentBlockHashes[i]).
+static inline uint32_t recent_id(const Engine& g, const AState& A, uint64_t i) { return g.trail[A.tail - A.len + i]; }
+
+// RecentBlockHashes = append(RecentBlockHashes, id)[-2 * kCycle:] (computeNewActiveState,
+// core.go:223-237): appended at the trail's end, after re-appending A's window if another
+// state's pushes came after it.
+static void push_recent(Engine& g, AState& A, uint32_t id) {
+  if (A.tail != g.trail.size()) {
+    const uint64_t b = A.tail - A.len, at = g.trail.size();
+    g.trail.resize(at + A.len);
+    for (uint32_t i = 0; i < A.len; ++i) g.trail[at + i] = g.trail[b + i];
+    A.tail = g.trail.size();
+  }
+  g.trail.push_back(id);
+  ++A.tail;
+  A.len = (uint32_t)std::min<uint64_t>(A.len + 1, 2 * kCycle);
+}
+
+// Go slices up to cap, beyond len panics.
+static void signed_parents(Engine& g, const AState& A, uint64_t block_slot, const Att& a, Parents& out) {
   const uint64_t start = block_slot - a.slot;
   const uint64_t end = block_slot - a.slot - (uint64_t)a.obl.size() + kCycle;
-  if (start > end || end > A.recent_ids.size()) throw Panic{"slice bounds out of range (core.go:353)"};
-  out.assign(A.recent_ids.begin() + (ptrdiff_t)start, A.recent_ids.begin() + (ptrdiff_t)end);
-  for (auto& o : a.obl) out.push_back(log_hash(g, bytes_to_hash(a.at(o.first), o.second), o.second != 32));
+  if (start > end || end > A.len) throw Panic{"slice bounds out of range (core.go:353)"};
+  out.wstart = A.tail - A.len + start;
+  out.nw = (uint32_t)(end - start);
+  out.obl.clear();
+  for (auto& o : a.obl) out.obl.push_back(log_hash(g, bytes_to_hash(a.at(o.first), o.second), o.second != 32));
 }
 
 // getAttesterIndices (core.go:363-374) -> committee id.
@@ -837,7 +986,7 @@ static size_t put_uvarint(uint8_t* p, uint64_t x) {
 struct AttLookup {
   bool have = false;
   uint32_t comm = 0;
-  std::vector<uint32_t> parents;
+  Parents parents;
 };
 
 // processAttestation (core.go:240-297) -> builds the message whose digest the reference logs.
@@ -846,7 +995,7 @@ static void process_attestation(Engine& g, uint64_t block_slot, const Att& a, At
   if ((int64_t)a.slot > (int64_t)block_slot) throw Rejected{PZ_ATT_SLOT_HIGH};
   if ((int64_t)a.slot < (int64_t)block_slot - (int64_t)kCycle) throw Rejected{PZ_ATT_SLOT_LOW};
   if (a.jslot != g.C->jslot) throw Rejected{PZ_ATT_JUSTIFIED};
-  std::vector<uint32_t>& parents = L.parents;
+  Parents& parents = L.parents;
   signed_parents(g, *g.A, block_slot, a, parents);
   const uint32_t c = attester_committee(g, *g.C, a);
   L.comm = c;
@@ -860,7 +1009,8 @@ static void process_attestation(Engine& g, uint64_t block_slot, const Att& a, At
   put_uvarint(hdr, a.slot % kCycle);
   put_uvarint(hdr, a.shard);
   g.m_hdr.insert(g.m_hdr.end(), hdr, hdr + 16);
-  g.m_ids.insert(g.m_ids.end(), parents.begin(), parents.end());
+  g.m_ref.push_back(AttMsgRef{(uint32_t)parents.wstart, parents.nw, (uint32_t)g.m_oids.size(), 0});
+  g.m_oids.insert(g.m_oids.end(), parents.obl.begin(), parents.obl.end());
   g.m_sbh.insert(g.m_sbh.end(), a.at(a.sbh_off), a.at(a.sbh_off) + a.sbh_len);
   g.m_sboff.push_back(g.m_sbh.size());
 }
@@ -874,21 +1024,40 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, AttLo
     L.comm = attester_committee(g, *g.C, a);
     L.have = true;
   }
-  const std::vector<uint32_t>& parents = L.parents;
+  const Parents& parents = L.parents;
   const uint32_t c = L.comm;
   const uint64_t k = g.csize[c];
-  uint64_t skip = 0;  // parents equal to one of the raw oblique parent hashes (core.go:313-320)
-  for (auto& o : a.obl)
-    if (o.second == 32)
-      for (size_t j = 0; j < parents.size(); ++j)
-        if (std::memcmp(g.hlog[parents[j]].b, a.at(o.first), 32) == 0) skip |= 1ull << j;
+  // Parents equal to one of the raw oblique parent hashes are skipped (core.go:313-320); only
+  // a 32-byte oblique can equal a [32]byte parent.  The parents are the recent window then the
+  // obliques themselves (always 64 of them), so a 32-byte oblique's own position is skipped,
+  // and any other parent with its bytes has the vote-cache slot its bytes were given (slots
+  // are per distinct hash; a 32-byte oblique id has none, which no slot equals).
+  const size_t nobl = a.obl.size(), np = parents.nw + nobl;
+  uint64_t skip = 0;
+  uint32_t match[64];
+  int nmatch = 0;
+  for (size_t i = 0; i < nobl; ++i) {
+    const auto& o = a.obl.p[i];
+    if (o.second != 32) continue;
+    skip |= 1ull << (np - nobl + i);
+    H32 h;
+    std::memcpy(h.b, a.at(o.first), 32);
+    if (const uint32_t* sl = g.slot_of.find(h)) match[nmatch++] = *sl;
+  }
+  uint32_t slots[64];
+  for (size_t j = 0; j < 64; ++j) {
+    const uint32_t sl = j < np ? g.id_slot[parents.id(g, j)] : UINT32_MAX;
+    slots[j] = sl;
+    for (int m = 0; m < nmatch; ++m)
+      if (sl == match[m]) skip |= 1ull << j;
+  }
   if (skip == ~0ull) return;  // no map access at all
   if (g.A->cache_nil) throw Panic{"assignment to entry in nil map (core.go:323)"};
   // the member loop reaches CheckBit(bitfield, 8 * len) when the committee is longer
   if (k > 8ull * a.bf_len) throw Panic{"calculateBlockVoteCache: CheckBit index out of range (core.go:330)"};
   g.q_comm.push_back(c);
   g.q_skip.push_back(skip);
-  for (size_t j = 0; j < 64; ++j) g.q_slots.push_back(j < parents.size() ? g.id_slot[parents[j]] : UINT32_MAX);
+  g.q_slots.insert(g.q_slots.end(), slots, slots + 64);
   const uint8_t* bf = a.at(a.bf_off);
   g.q_bits.insert(g.q_bits.end(), bf, bf + (k + 7) / 8);
   g.q_boffs.push_back(g.q_bits.size());
@@ -1079,9 +1248,8 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   VoteGatherSlots q;
   for (uint64_t i = 0; i < kCycle; ++i) {
     q.slot[i] = UINT32_MAX;
-    if (!A->cache_nil && i < A->recent.size()) {
-      auto it = g.slot_of.find(A->recent[i]);
-      if (it != g.slot_of.end()) q.slot[i] = it->second;
+    if (!A->cache_nil && i < A->len) {
+      if (const uint32_t* sl = g.slot_of.find(g.hlog[recent_id(g, *A, i)])) q.slot[i] = *sl;
     }
   }
   tally_gather_enqueue(g, q);
@@ -1116,12 +1284,8 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   auto na = std::make_shared<AState>();
   for (auto& p : A->pending)
     if (p->slot > lsr) na->pending.push_back(p);
-  na->recent = A->recent;
-  na->recent_ids = A->recent_ids;
-  if (na->recent.size() > 2 * kCycle) {
-    na->recent.erase(na->recent.begin(), na->recent.end() - 2 * kCycle);
-    na->recent_ids.erase(na->recent_ids.begin(), na->recent_ids.end() - 2 * kCycle);
-  }
+  na->tail = A->tail;  // (the window is at most 2 * kCycle long)
+  na->len = A->len;
   na->cache_nil = A->cache_nil;
   *nc_out = nc;
   *na_out = na;
@@ -1214,10 +1378,10 @@ static const std::string& validators_enc(Engine& g) {
   return g.val_enc;
 }
 
-static std::string encode_active(const AState& A) {  // messages.proto:94-97
+static std::string encode_active(const Engine& g, const AState& A) {  // messages.proto:94-97
   std::string o;
   for (auto& p : A.pending) put_msg(o, 1, p->base, p->len);
-  for (auto& h : A.recent) put_msg(o, 2, h.b, A.recent_raw_empty ? 0 : 32);
+  for (uint32_t i = 0; i < A.len; ++i) put_msg(o, 2, g.hlog[recent_id(g, A, i)].b, A.recent_raw_empty ? 0 : 32);
   return o;
 }
 
@@ -1299,8 +1463,10 @@ static void init_tail(Engine& g, const std::vector<uint32_t>& members, const std
   g.id_slot.clear();
   g.d_hlog_n = 0;
   const uint32_t zero_id = log_hash(g, kZero);
-  A->recent.assign(2 * kCycle, kZero);
-  A->recent_ids.assign(2 * kCycle, zero_id);
+  g.trail.assign(2 * kCycle, zero_id);
+  g.d_trail_n = 0;
+  A->tail = g.trail.size();
+  A->len = (uint32_t)(2 * kCycle);
   A->recent_raw_empty = true;
   g.A = A;
   g.C = C;
@@ -1529,26 +1695,97 @@ static int reload(Engine& g, const uint8_t* data, uint64_t len) {
 // caches; profiles/r03/replay_threads_r3c.txt.)
 // The call's arena: a copy of the input bytes (filled by whoever parses them), the records
 // reserved to the counted number, the oblique pool to a bound (an element takes >= 2 bytes).
-static std::shared_ptr<CallArena> make_arena(const uint64_t* offs, uint64_t n, uint64_t natt) {
+static std::shared_ptr<CallArena> make_arena(const uint64_t* offs, uint64_t n, uint64_t natt, PinBuf* pin = nullptr) {
   auto ar = std::make_shared<CallArena>();
   const uint64_t total = n ? offs[n] - offs[0] : 0;
-  ar->bytes.reset(new uint8_t[total + 16]);
+  if (pin) {
+    check(pin->reserve(total + 16));
+    ar->bytes = pin->p;
+  } else {
+    ar->own.reset(new uint8_t[total + 16]);
+    ar->bytes = ar->own.get();
+  }
+  std::memset(ar->bytes + total, 0, 16);
   ar->atts.reserve(natt);
+  ar->ptrs.reserve(natt);
   ar->obl.reserve(total / 2 + 1);
   return ar;
 }
 
 // Blocks [b0, b1): copied into the arena and parsed; returns the first malformed block or b1.
 static uint64_t parse_range(const uint8_t* data, const uint64_t* offs, uint64_t b0, uint64_t b1, CallArena& ar,
-                            const std::shared_ptr<CallArena>& owner, std::vector<Block>& blocks) {
+                            std::vector<Block>& blocks) {
   const uint64_t o0 = offs[0];
   for (uint64_t i = b0; i < b1; ++i)
     if (offs[i + 1] < offs[i]) return i;
-  if (b1 > b0) std::memcpy(ar.bytes.get() + (offs[b0] - o0), data + offs[b0], offs[b1] - offs[b0]);
-  const uint8_t* base = ar.bytes.get() - o0;
+  if (b1 > b0) std::memcpy(ar.bytes + (offs[b0] - o0), data + offs[b0], offs[b1] - offs[b0]);
+  const uint8_t* base = ar.bytes - o0;
   for (uint64_t i = b0; i < b1; ++i)
-    if (!parse_block(base + offs[i], offs[i + 1] - offs[i], &blocks[i], owner)) return i;
+    if (!parse_block(base + offs[i], offs[i + 1] - offs[i], &blocks[i], &ar)) return i;
   return b1;
+}
+
+// After a call: the records a live state still holds (the pending attestations of the
+// chain's, the candidate's and the deferred epoch's states) move out of the call's arena --
+// the Engine's pinned buffer, which the next call reuses -- into a small heap arena of their
+// own; earlier such arenas stay while a live record points into them.
+static void keep_arenas(Engine& g, CallArena* cur) {
+  std::vector<std::vector<AttP>*> lists;
+  if (g.A) lists.push_back(&g.A->pending);
+  if (g.cand_A) lists.push_back(&g.cand_A->pending);
+  if (g.deferred.live) lists.push_back(&g.deferred.pending);
+  if (cur && !cur->atts.empty()) {
+    const Att* lo = cur->atts.data();
+    const Att* hi = lo + cur->atts.size();
+    std::vector<AttP> mv;
+    for (auto* l : lists)
+      for (AttP p : *l)
+        if (p >= lo && p < hi) mv.push_back(p);
+    std::sort(mv.begin(), mv.end());
+    mv.erase(std::unique(mv.begin(), mv.end()), mv.end());
+    if (!mv.empty()) {
+      auto na = std::make_shared<CallArena>();
+      size_t bytes = 0, nobl = 0;
+      for (AttP p : mv) {
+        bytes += p->len;
+        nobl += p->obl.n;
+      }
+      na->own.reset(new uint8_t[bytes + 16]);
+      na->bytes = na->own.get();
+      std::memset(na->bytes + bytes, 0, 16);
+      na->atts.reserve(mv.size());
+      na->obl.reserve(nobl + 1);
+      size_t pos = 0;
+      for (AttP p : mv) {
+        Att a = *p;
+        std::memcpy(na->bytes + pos, p->base, p->len);
+        a.base = na->bytes + pos;
+        pos += p->len;
+        a.obl_first = (uint32_t)na->obl.size();
+        for (auto& o : p->obl) na->obl.push_back(o);
+        a.obl.p = na->obl.data() + a.obl_first;  // (reserved: never reallocates)
+        na->atts.push_back(a);
+      }
+      for (auto* l : lists)
+        for (AttP& p : *l)
+          if (p >= lo && p < hi) p = &na->atts[std::lower_bound(mv.begin(), mv.end(), p) - mv.begin()];
+      g.arenas.push_back(na);
+    }
+  }
+  std::vector<char> used(g.arenas.size(), 0);
+  for (auto* l : lists)
+    for (AttP p : *l)
+      for (size_t k = 0; k < g.arenas.size(); ++k) {
+        const std::vector<Att>& a = g.arenas[k]->atts;
+        if (!a.empty() && p >= a.data() && p < a.data() + a.size()) {
+          used[k] = 1;
+          break;
+        }
+      }
+  size_t j = 0;
+  for (size_t k = 0; k < g.arenas.size(); ++k)
+    if (used[k]) g.arenas[j++] = g.arenas[k];
+  g.arenas.resize(j);
 }
 
 // Every block, on the calling thread, before anything else (the path that keeps a call
@@ -1558,7 +1795,7 @@ static int parse_all(const uint8_t* data, const uint64_t* offs, uint64_t n, uint
   auto ar = make_arena(offs, n, natt);
   *keep = ar;  // the blocks' bytes live here for the whole call (records alias it beyond)
   blocks.resize(n);
-  const uint64_t bad = parse_range(data, offs, 0, n, *ar, ar, blocks);
+  const uint64_t bad = parse_range(data, offs, 0, n, *ar, blocks);
   if (bad < n) return fail(PZ_EINVAL, "block %llu is not a canonical BeaconBlock encoding", (unsigned long long)bad);
   return PZ_OK;
 }
@@ -1579,6 +1816,23 @@ static void sync_hash_log(Engine& g) {
   hchk(hipMemcpyAsync(g.d_hlog.p + g.d_hlog_n * 32, g.hlog[g.d_hlog_n].b, (n - g.d_hlog_n) * 32,
                       hipMemcpyHostToDevice, g.s), "H2D hash log");
   g.d_hlog_n = n;
+}
+
+// The same for the recent-hash trail.
+static void sync_trail(Engine& g) {
+  const uint64_t n = g.trail.size();
+  if (n == g.d_trail_n) return;
+  if (n > g.d_trail.n) {
+    DevArr<uint32_t> nb;
+    check(nb.alloc(std::max<uint64_t>(n, 2 * g.d_trail.n)));
+    if (g.d_trail_n) hchk(hipMemcpyAsync(nb.p, g.d_trail.p, g.d_trail_n * 4, hipMemcpyDeviceToDevice, g.s), "D2D");
+    hchk(hipStreamSynchronize(g.s), "sync");
+    std::swap(g.d_trail.p, nb.p);
+    std::swap(g.d_trail.n, nb.n);
+  }
+  hchk(hipMemcpyAsync(g.d_trail.p + g.d_trail_n, g.trail.data() + g.d_trail_n, (n - g.d_trail_n) * 4,
+                      hipMemcpyHostToDevice, g.s), "H2D trail");
+  g.d_trail_n = n;
 }
 
 // Digest messages of blocks [b0, b1) and their na attestations (a0.. in call order), laid out
@@ -1651,6 +1905,60 @@ static void stage_launch(uint64_t nmsg, uint64_t bytes, DigestBufs& D, hipStream
   hchk(hipMemcpyAsync(D.d_offs.p, D.offs.p, (nmsg + 1) * 8, hipMemcpyHostToDevice, s), "H2D offsets");
   if (bytes) hchk(hipMemcpyAsync(D.d_in.p, D.msgs.p, bytes, hipMemcpyHostToDevice, s), "H2D msgs");
   hchk(launch_b2b_csr(D.d_in.p, D.d_offs.p, nmsg, D.d_out.p, 32, s), "blake2b csr");
+  hchk(hipMemcpyAsync(D.dig.p, D.d_out.p, nmsg * 32, hipMemcpyDeviceToHost, s), "D2H digests");
+}
+
+// The batch path's digest batch, reading blocks and attestation encodings where they lie in
+// the call's pinned arena (one H2D of the arena, no copy of them on the host); only the Key()
+// preimages are built.  Digests [blocks][attestation Hash][Key], 32 B each, land in D.dig.
+static void stage_digests_arena(const std::vector<Block>& blocks, uint64_t nb, uint64_t na, const CallArena& ar,
+                                uint64_t abytes, DigestBufs& D, hipStream_t s) {
+  const uint64_t nmsg = nb + 2 * na, aal = (abytes + 15) & ~15ull;
+  uint64_t kbytes = 0;
+  for (uint64_t bi = 0; bi < nb; ++bi)
+    for (auto& a : blocks[bi].atts) kbytes += 10 + a->sbh_len + 32 * a->obl.size();
+  check(D.msgs.reserve(kbytes + 16));
+  check(D.offs.reserve(2 * nmsg * 8 + 8));
+  check(D.dig.reserve(nmsg * 32 + 32));
+  uint64_t* beg = reinterpret_cast<uint64_t*>(D.offs.p);
+  uint64_t* end = beg + nmsg;
+  uint64_t m = 0, ka = nb, kk = nb + na, kpos = 0;
+  for (uint64_t bi = 0; bi < nb; ++bi) {
+    const Block& b = blocks[bi];
+    beg[m] = (uint64_t)(b.data - ar.bytes);
+    end[m] = beg[m] + b.len;
+    ++m;
+    for (auto& ap : b.atts) {
+      const Att& a = *ap;
+      beg[ka] = (uint64_t)(a.base - ar.bytes);
+      end[ka] = beg[ka] + a.len;
+      ++ka;
+      // Key() preimage (types/attestation.go:61-77): a 10-byte buffer holding uvarint(slot)
+      // overwritten by uvarint(shard), ShardBlockHash, each oblique hash copied into a [32]byte
+      uint8_t* q = D.msgs.p + kpos;
+      std::memset(q, 0, 10);
+      put_uvarint(q, a.slot);
+      put_uvarint(q, a.shard);
+      std::memcpy(q + 10, a.at(a.sbh_off), a.sbh_len);
+      uint64_t kl = 10 + a.sbh_len;
+      for (auto& o : a.obl) {
+        const H32 h = copy32(a.at(o.first), o.second);
+        std::memcpy(q + kl, h.b, 32);
+        kl += 32;
+      }
+      beg[kk] = aal + kpos;
+      end[kk++] = aal + kpos + kl;
+      kpos += kl;
+    }
+  }
+  check(D.d_in.alloc(aal + kbytes + 16));
+  check(D.d_out.alloc(nmsg * 32));
+  check(D.d_offs.alloc(2 * nmsg + 1));
+  hchk(hipMemcpyAsync(D.d_offs.p, beg, 2 * nmsg * 8, hipMemcpyHostToDevice, s), "H2D spans");
+  hchk(hipMemcpyAsync(D.d_in.p, ar.bytes, abytes + 16, hipMemcpyHostToDevice, s), "H2D arena");  // (+ its zero pad)
+  if (kbytes) hchk(hipMemcpyAsync(D.d_in.p + aal, D.msgs.p, kbytes, hipMemcpyHostToDevice, s), "H2D keys");
+  hchk(hipMemsetAsync(D.d_in.p + aal + kbytes, 0, 16, s), "memset");
+  hchk(launch_b2b_spans(D.d_in.p, D.d_offs.p, D.d_offs.p + nmsg, nmsg, D.d_out.p, 32, s), "blake2b spans");
   hchk(hipMemcpyAsync(D.dig.p, D.d_out.p, nmsg * 32, hipMemcpyDeviceToHost, s), "D2H digests");
 }
 
@@ -1748,7 +2056,7 @@ static void feed(Engine& g, Feeder& F, const uint8_t* data, const uint64_t* offs
       }
       Feeder::Slot& S = F.slot[j % kRing];
       uint64_t b1 = std::min(F.n, b0 + kChunk);
-      const uint64_t good = parse_range(data, offs, b0, b1, *ar, ar, *F.blocks);
+      const uint64_t good = parse_range(data, offs, b0, b1, *ar, *F.blocks);
       b1 = good;
       uint64_t na = 0;
       for (uint64_t bi = b0; bi < b1; ++bi) na += (*F.blocks)[bi].atts.size();
@@ -1779,11 +2087,18 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
   std::vector<uint32_t> block_id(n);
   uint64_t ai = 0;
   g.m_hdr.clear();
-  g.m_ids.clear();
+  g.m_ref.clear();
+  g.m_oids.clear();
   g.m_sbh.clear();
   g.m_sboff.assign(1, 0);
   g.m_hdr.reserve(16 * natt);
-  g.m_ids.reserve(kCycle * natt);
+  g.m_ref.reserve(natt);
+  // the tables grow once per call, not by doubling inside the walk
+  g.saved.reserve(g.saved.size() + n);
+  g.slot_of.reserve(g.slot_of.size() + n);  // (plus any oblique hash shorter than 32 B: grows)
+  g.hlog.reserve(g.hlog.size() + n + 2 * natt);
+  g.id_slot.reserve(g.id_slot.size() + n + 2 * natt);
+  g.trail.reserve(g.trail.size() + n + 2 * kCycle);
   msg_att.reserve(natt);
   auto t_walk = std::chrono::steady_clock::now();
   uint64_t logged = 0;  // block digests are logged a chunk at a time, as they arrive
@@ -1859,7 +2174,7 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
       g.cand_A.reset();
       g.cand_C.reset();
     }
-    g.saved.insert(h);
+    g.saved.insert(h, 1);
     if (g.has_cand) {
       r.status = PZ_BLOCK_SAVED_NOT_CANDIDATE;
       continue;
@@ -1877,13 +2192,8 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
     // computeNewActiveState (core.go:223-237)
     A->cache_nil = cache_nil;
     A->pending.insert(A->pending.end(), processed.begin(), processed.end());
-    A->recent.push_back(h);
-    A->recent_ids.push_back(block_id[bi]);
+    push_recent(g, *A, block_id[bi]);
     A->recent_raw_empty = false;
-    if (A->recent.size() > 2 * kCycle) {
-      A->recent.erase(A->recent.begin(), A->recent.end() - 2 * kCycle);
-      A->recent_ids.erase(A->recent_ids.begin(), A->recent_ids.end() - 2 * kCycle);
-    }
     g.has_cand = true;
     g.cand_slot = b.slot;
     g.cand_A = A;
@@ -1897,14 +2207,18 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
   if (nm) {
     sync_hash_log(g);
     upload(g, g.d_mhdr, g.m_hdr.data(), g.m_hdr.size());
-    upload(g, g.d_mids, g.m_ids.data(), g.m_ids.size());
+    sync_trail(g);
+    upload(g, g.d_mref, g.m_ref.data(), g.m_ref.size());
+    upload(g, g.d_moids, g.m_oids.data(), g.m_oids.size() + 1);  // (+1: never an empty allocation)
     upload(g, g.d_msbh, g.m_sbh.data(), g.m_sbh.size() + 1);  // (+1: never an empty allocation)
     upload(g, g.d_msboff, g.m_sboff.data(), g.m_sboff.size());
     check(g.d_mout.alloc(nm * 64));
-    hchk(launch_b2b_attmsg(g.d_hlog.p, g.d_mids.p, g.d_mhdr.p, g.d_msbh.p, g.d_msboff.p, nm, g.d_mout.p, g.s),
+    hchk(launch_b2b_attmsg(g.d_hlog.p, g.d_trail.p, g.d_mref.p, g.d_moids.p, g.d_mhdr.p, g.d_msbh.p, g.d_msboff.p, nm,
+                           g.d_mout.p, g.s),
          "attestation message digests");
-    std::vector<uint8_t> md(nm * 64);
-    hchk(hipMemcpyAsync(md.data(), g.d_mout.p, nm * 64, hipMemcpyDeviceToHost, g.s), "D2H");
+    check(g.m_pin.reserve(nm * 64));  // (a fresh pageable vector cost a zero fill and page faults per call)
+    const uint8_t* md = g.m_pin.p;
+    hchk(hipMemcpyAsync(g.m_pin.p, g.d_mout.p, nm * 64, hipMemcpyDeviceToHost, g.s), "D2H");
     hchk(hipStreamSynchronize(g.s), "sync");  // also keeps the pageable sources alive
     for (size_t i = 0; i < nm; ++i) std::memcpy(ar[msg_att[i]].msg_digest, &md[i * 64], 64);
   }
@@ -2006,7 +2320,7 @@ int pz_chain_new_from_state(const uint8_t* cstate, uint64_t len, const uint8_t* 
     for (uint64_t i = 0; i < nsaved; ++i) {
       H32 h;
       std::memcpy(h.b, saved_hashes + 32 * i, 32);
-      c->g.saved.insert(h);
+      c->g.saved.insert(h, 1);
     }
   } catch (int e) {
     destroy_chain(c);
@@ -2066,6 +2380,11 @@ int pz_chain_process_blocks(pz_chain* c, const uint8_t* blocks, const uint64_t* 
   bool long_msg = false;
   for (uint64_t i = 0; i < n && !long_msg; ++i) long_msg = offsets[i + 1] >= offsets[i] && offsets[i + 1] - offsets[i] >= thr;
   std::shared_ptr<CallArena> arena;
+  struct Keep {  // on every way out, the arenas the chain's states still point into stay
+    Engine& g;
+    std::shared_ptr<CallArena>& a;
+    ~Keep() { keep_arenas(g, a.get()); }
+  } keep{g, arena};
   std::vector<uint8_t> dg_slow;
   // The batch path (default): the whole call parsed, one digest batch, then the walk.  The
   // pipelined form (a producer thread parsing a chunk ahead, PZ_CHAIN_PIPELINE=1) measured
@@ -2075,21 +2394,23 @@ int pz_chain_process_blocks(pz_chain* c, const uint8_t* blocks, const uint64_t* 
   const char* pe = std::getenv("PZ_CHAIN_PIPELINE");
   F.piped = !long_msg && n >= 2 * kChunk && pe && pe[0] == '1';
   if (!F.piped) {
-    {
+    try {
       PhaseTimer pt(g.prof[kProfParse]);
-      arena = make_arena(offsets, n, natt);
-      const uint64_t good = parse_range(blocks, offsets, 0, n, *arena, arena, parsed);
+      arena = make_arena(offsets, n, natt, &g.arena_pin);
+      const uint64_t good = parse_range(blocks, offsets, 0, n, *arena, parsed);
       if (good < n) {  // the walk stops before the malformed block
         F.bad.store(good);
         F.n = good;
         F.natt = 0;
         for (uint64_t bi = 0; bi < good; ++bi) F.natt += parsed[bi].atts.size();
       }
+    } catch (int rc) {
+      return rc;
     }
     try {
       PhaseTimer pt(g.prof[kProfHash1]);
       if (!long_msg) {
-        if (F.n) stage_digests(parsed, 0, F.n, F.natt, g.dbatch, g.s);
+        if (F.n) stage_digests_arena(parsed, F.n, F.natt, *arena, offsets[n] - offsets[0], g.dbatch, g.s);
         hchk(hipStreamSynchronize(g.s), "sync");
         F.dg = g.dbatch.dig.p;
         F.dstride = 32;
@@ -2131,7 +2452,11 @@ int pz_chain_process_blocks(pz_chain* c, const uint8_t* blocks, const uint64_t* 
     }
   } else {
     // the parse and the digest batches run a chunk ahead of the walk on a producer thread
-    arena = make_arena(offsets, n, natt);
+    try {
+      arena = make_arena(offsets, n, natt, &g.arena_pin);
+    } catch (int rc) {
+      return rc;
+    }
   }
   std::thread producer;
   if (F.piped) {
@@ -2188,12 +2513,12 @@ int pz_chain_roots(pz_chain* c, uint8_t out[4 * 32], int* has_candidate) {
     epoch_collect(g);
     std::string buf;
     std::vector<uint64_t> offs{0};
-    buf += encode_active(*g.A);
+    buf += encode_active(g, *g.A);
     offs.push_back(buf.size());
     buf += encode_crystallized(g, *g.C);
     offs.push_back(buf.size());
     if (g.has_cand) {
-      buf += encode_active(*g.cand_A);
+      buf += encode_active(g, *g.cand_A);
       offs.push_back(buf.size());
       buf += encode_crystallized(g, *g.cand_C);
       offs.push_back(buf.size());
@@ -2222,7 +2547,7 @@ int pz_chain_state_bytes(pz_chain* c, int which, uint8_t* out, uint64_t cap, uin
     hchk(hipSetDevice(g.device), "hipSetDevice");
     epoch_collect(g);
     const std::string b = (which & 1) ? encode_crystallized(g, which >= 2 ? *g.cand_C : *g.C)
-                                      : encode_active(which >= 2 ? *g.cand_A : *g.A);
+                                      : encode_active(g, which >= 2 ? *g.cand_A : *g.A);
     *len = b.size();
     if (out && cap >= b.size()) std::memcpy(out, b.data(), b.size());
   } catch (Panic& p) {
