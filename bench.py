@@ -847,8 +847,11 @@ def replay_leg(args, torch, dist, dev, rank, world):
     nval, nb = 65536, args.replay_blocks
     blocks = synth.chain_blocks(nval, nb, seed=6 + rank)
     data, offs = serialize_blocks(blocks)  # sync delivers serialized blocks (sync/service.go:147-164)
-    w_data, w_offs = serialize_blocks(blocks[:min(nb, 130)])
-    BeaconChain(nval, dev).process_serialized(w_data, w_offs)  # warm-up
+    # warm-up: the same chain on a throwaway BeaconChain (kernels loaded; the library's pinned
+    # staging pool, which a long-running node keeps, holds buffers of this size)
+    w = BeaconChain(nval, dev)
+    w.process_serialized(data, offs)
+    del w  # (pz_chain_free: its pinned buffers go back to the pool)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

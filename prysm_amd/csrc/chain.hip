@@ -87,12 +87,12 @@ struct H32Table {
     keys.clear();
     n = mask = 0;
   }
-  void grow() {
+  void grow(size_t cap = 0) {
     std::vector<Slot> old;
     std::vector<H32> oldk;
     old.swap(t);
     oldk.swap(keys);
-    const size_t cap = old.empty() ? 1024 : 2 * old.size();
+    if (!cap) cap = old.empty() ? 1024 : 2 * old.size();
     t.assign(cap, Slot{0, V{}, 0});
     keys.resize(cap);
     mask = cap - 1;
@@ -105,7 +105,9 @@ struct H32Table {
       }
   }
   void reserve(size_t m) {
-    while (2 * m > t.size()) grow();
+    size_t cap = t.empty() ? 1024 : t.size();
+    while (2 * m > cap) cap *= 2;
+    if (cap > t.size()) grow(cap);  // one rehash
   }
   const V* find(const H32& k) const {
     if (!n) return nullptr;
@@ -271,15 +273,19 @@ struct AttSpan {
 // attestation record parsed from them, allocated once (per-record allocations made the parse
 // allocator-bound).  The Engine keeps it while a live state's pending attestations point in.
 struct CallArena {
+  using Pool = std::vector<std::pair<uint32_t, uint32_t>>;
   uint8_t* bytes = nullptr;  // (not zero-filled) the Engine's pinned arena, or `own`
   std::unique_ptr<uint8_t[]> own;
-  std::vector<Att> atts;  // reserved to the exact count: AttP points into it
-  std::vector<AttP> ptrs;  // &atts[i], in order: each Block's AttSpan is a run of it
-  std::vector<std::pair<uint32_t, uint32_t>> obl;  // reserved to a bound: Att::obl points into it
+  std::vector<Att> atts;  // sized to the exact count: block i's records at [first[i], first[i+1])
+  std::vector<AttP> ptrs;  // &atts[j]: each Block's AttSpan is a run of it
+  std::vector<uint64_t> first;  // per block, its first record (a prefix of the per-block counts)
+  // one pool per range parsed by one thread, each reserved to a bound (an element takes >= 2
+  // bytes): Att::obl points into it
+  std::vector<Pool> obl;
 };
 
 // messages.pb.go:889-896: 1-3 varint, 4-6 bytes, 7 repeated bytes, 8 packed varints
-static bool parse_att(const uint8_t* p, size_t n, Att* a, std::vector<std::pair<uint32_t, uint32_t>>& pool) {
+static bool parse_att(const uint8_t* p, size_t n, Att* a, CallArena::Pool& pool) {
   static const uint32_t kTypes[9] = {9, 0, 0, 0, 2, 2, 2, 2, 2};
   a->base = p;
   a->len = (uint32_t)n;
@@ -326,12 +332,14 @@ struct Block {
 };
 
 // messages.pb.go:224-232: 1 bytes, 2 varint, 3-6 bytes, 7 Timestamp, 8 repeated records
-static bool parse_block(const uint8_t* p, size_t n, Block* b, CallArena* ar) {
+// Block i's records go to ar->atts[first[i], first[i+1]).
+static bool parse_block(const uint8_t* p, size_t n, Block* b, CallArena* ar, uint64_t i, CallArena::Pool& pool) {
   static const uint32_t kTypes[9] = {9, 2, 0, 2, 2, 2, 2, 2, 2};
   static const uint32_t kTsTypes[3] = {9, 0, 0};
   b->data = p;
   b->len = n;
-  b->atts.p = ar->ptrs.data() + ar->ptrs.size();  // (reserved: never reallocates)
+  const uint64_t a0 = ar->first[i], a1 = ar->first[i + 1];
+  b->atts.p = ar->ptrs.data() + a0;
   b->atts.n = 0;
   Reader r{p, p + n};
   uint32_t prev = 0, f, wt;
@@ -360,15 +368,14 @@ static bool parse_block(const uint8_t* p, size_t n, Block* b, CallArena* ar) {
       }
       if (!t.ok) return false;
     } else {  // f == 8
-      if (ar->atts.size() == ar->atts.capacity()) return false;  // more records than counted
-      ar->atts.emplace_back();
-      Att* a = &ar->atts.back();
-      if (!parse_att(q, len, a, ar->obl)) return false;
-      ar->ptrs.push_back(a);
+      if (a0 + b->atts.n >= a1) return false;  // more records than counted (unreachable)
+      Att* a = &ar->atts[a0 + b->atts.n];
+      if (!parse_att(q, len, a, pool)) return false;
+      ar->ptrs[a0 + b->atts.n] = a;
       ++b->atts.n;
     }
   }
-  return r.ok;
+  return r.ok && b->atts.n == a1 - a0;
 }
 
 // ---- chain state ----------------------------------------------------------------------------
@@ -415,20 +422,49 @@ struct DevArr {
   }
 };
 
-// Grow-only pinned host buffer (hipHostMalloc), for asynchronous-capable H2D / D2H.
+// Pinned host memory is slow to get (its pages are locked and mapped for the device: ~ms per
+// 10 MB), so freed PinBufs go to a process-wide pool that later chains of the process reuse
+// (sizes rounded up to powers of two, at most kPinPoolBytes kept).  The pool is never
+// destroyed: it outlives static destructors that may run after the HIP runtime's.
+constexpr size_t kPinPoolBytes = size_t(1) << 30;
+struct PinPool {
+  std::mutex mu;
+  std::multimap<size_t, void*> free;
+  size_t bytes = 0;
+};
+static PinPool& pin_pool() {
+  static PinPool* p = new PinPool();
+  return *p;
+}
+
+// Grow-only pinned host buffer, for asynchronous-capable H2D / D2H and device-mapped reads.
 struct PinBuf {
   uint8_t* p = nullptr;
   size_t n = 0;
   void* d = nullptr;  // its device address, looked up once (a runtime call per use showed in the walk)
   int reserve(size_t bytes) {
     if (bytes <= n && p) return PZ_OK;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    d = nullptr;
-    n = 0;
-    hipError_t e = hipHostMalloc((void**)&p, std::max<size_t>(bytes, 1), hipHostMallocDefault);
-    if (e != hipSuccess) return hip_fail(e, "hipHostMalloc");
-    n = bytes;
+    release();
+    size_t want = 4096;
+    while (want < bytes) want *= 2;
+    PinPool& pool = pin_pool();
+    {
+      std::lock_guard<std::mutex> lk(pool.mu);
+      auto it = pool.free.lower_bound(want);
+      if (it != pool.free.end() && it->first <= 4 * want) {
+        p = static_cast<uint8_t*>(it->second);
+        n = it->first;
+        pool.bytes -= it->first;
+        pool.free.erase(it);
+        return PZ_OK;
+      }
+    }
+    hipError_t e = hipHostMalloc((void**)&p, want, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return hip_fail(e, "hipHostMalloc");
+    }
+    n = want;
     return PZ_OK;
   }
   int dev(void** out) {
@@ -439,9 +475,23 @@ struct PinBuf {
     *out = d;
     return PZ_OK;
   }
-  ~PinBuf() {
+  void release() {
+    if (!p) return;
+    PinPool& pool = pin_pool();
+    {
+      std::lock_guard<std::mutex> lk(pool.mu);
+      if (pool.bytes + n <= kPinPoolBytes) {
+        pool.free.emplace(n, p);
+        pool.bytes += n;
+        p = nullptr;
+      }
+    }
     if (p) (void)hipHostFree(p);
+    p = nullptr;
+    d = nullptr;
+    n = 0;
   }
+  ~PinBuf() { release(); }
 };
 
 enum ProfSlot {
@@ -542,9 +592,7 @@ struct Engine {
   std::vector<uint64_t> q_skip;
   // flushes run asynchronously to the walk: the queue is packed into a pinned arena and
   // copied with one H2D per rank; the arena is reused once every rank's copy is done
-  uint8_t* q_arena = nullptr;
-  void* q_arena_dev = nullptr;  // its device address
-  size_t q_arena_cap = 0;
+  PinBuf q_arena;
   bool q_arena_busy = false;
   uint64_t ncomm = 0, cwords = 1;
   PinBuf e_pin, e_pin_out;   // the epoch inputs' pinned staging; the results' pinned landing
@@ -571,6 +619,9 @@ struct Engine {
   uint64_t cand_slot = 0;
   AP cand_A;
   CP cand_C;
+  // saved block hashes (blockchain.go's SaveBlock): a flag per vote-cache slot (every block
+  // digest is logged with a slot), plus a table for the hashes a reloaded chain starts with
+  std::vector<uint8_t> slot_saved;
   H32Table<uint8_t> saved;
   // the call arenas whose records a live state still holds (pending attestations)
   std::vector<std::shared_ptr<CallArena>> arenas;
@@ -711,13 +762,10 @@ static void hash_many(Engine& g, const std::string& data, const std::vector<uint
 }
 
 // ---- vote cache -------------------------------------------------------------------------------
-static uint32_t vote_slot(Engine& g, const H32& h) {
-  const uint32_t s = (uint32_t)g.slot_hash.size();
-  const uint32_t got = g.slot_of.insert(h, s);
-  if (got != s) return got;
-  g.slot_hash.push_back(h);
-  if (s >= g.cap) {  // grow every rank's device arrays, keeping their contents
-    const uint64_t nc = std::max<uint64_t>(64, 2 * g.cap);
+// Every rank's vote-cache arrays grown to nc slots, keeping their contents (outside a flush).
+static void grow_slots(Engine& g, uint64_t nc) {
+  if (nc <= g.cap) return;
+  {
     each_rank(g, [&](RankDev& r) {
       DevArr<uint32_t> bm;
       DevArr<uint64_t> tt;
@@ -751,7 +799,22 @@ static uint32_t vote_slot(Engine& g, const H32& h) {
     });
     g.cap = nc;
   }
+}
+
+static uint32_t vote_slot(Engine& g, const H32& h) {
+  const uint32_t s = (uint32_t)g.slot_hash.size();
+  const uint32_t got = g.slot_of.insert(h, s);
+  if (got != s) return got;
+  g.slot_hash.push_back(h);
+  g.slot_saved.push_back(0);
+  if (s >= g.cap) grow_slots(g, std::max<uint64_t>(64, 2 * g.cap));
   return s;
+}
+
+static bool is_saved(const Engine& g, const H32& h) {
+  const uint32_t* sl = g.slot_of.find(h);
+  if (sl && g.slot_saved[*sl]) return true;
+  return g.saved.size() && g.saved.count(h);
 }
 
 // Every logged hash gets its vote-cache slot at once (a slot is storage; whether the Go map
@@ -773,8 +836,12 @@ static uint32_t log_hash(Engine& g, const H32& h, bool votable = true) {
 // Enqueue the pending tally items on every rank; no host wait (the pinned arena and its
 // per-rank events make the H2D asynchronous).  Balances only change in stateRecalc's epoch,
 // which each rank's stream orders after every flush, so a flush may run any time before it.
-static bool flush_votes_enqueue(Engine& g) {
+// With `gq` (a stateRecalc's flush on one rank), the leader pass also gathers the 64
+// justification totals into g.tot_pin and g.ev_totals is recorded behind it: returns true
+// when it did so (tally_gather_enqueue's work is then done).
+static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr) {
   if (g.q_comm.empty()) return false;
+  const bool gather = gq && g.world == 1;
   PhaseTimer pt(g.prof[kProfFlush]);
   const uint64_t natt = g.q_comm.size();
   auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
@@ -787,19 +854,13 @@ static bool flush_votes_enqueue(Engine& g) {
     for (RankDev& r : g.rk) hchk(hipEventSynchronize(r.q_ev), "event sync");
     g.q_arena_busy = false;
   }
-  if (total > g.q_arena_cap) {
-    if (g.q_arena) (void)hipHostFree(g.q_arena);
-    g.q_arena = nullptr;
-    g.q_arena_dev = nullptr;
-    const size_t cap = std::max(total, 2 * g.q_arena_cap);
-    hchk(hipHostMalloc((void**)&g.q_arena, cap, hipHostMallocPortable | hipHostMallocMapped), "hipHostMalloc");
-    g.q_arena_cap = cap;
-  }
-  std::memcpy(g.q_arena + o_boffs, g.q_boffs.data(), g.q_boffs.size() * 8);
-  std::memcpy(g.q_arena + o_skip, g.q_skip.data(), natt * 8);
-  std::memcpy(g.q_arena + o_comm, g.q_comm.data(), natt * 4);
-  std::memcpy(g.q_arena + o_slots, g.q_slots.data(), g.q_slots.size() * 4);
-  std::memcpy(g.q_arena + o_bits, g.q_bits.data(), g.q_bits.size());
+  check(g.q_arena.reserve(total));
+  uint8_t* qa = g.q_arena.p;
+  std::memcpy(qa + o_boffs, g.q_boffs.data(), g.q_boffs.size() * 8);
+  std::memcpy(qa + o_skip, g.q_skip.data(), natt * 8);
+  std::memcpy(qa + o_comm, g.q_comm.data(), natt * 4);
+  std::memcpy(qa + o_slots, g.q_slots.data(), g.q_slots.size() * 4);
+  std::memcpy(qa + o_bits, g.q_bits.data(), g.q_bits.size());
   each_rank(g, [&](RankDev& r) {
     // Growing a device buffer frees the old one, which in-flight flushes may still read:
     // drain the stream first (rare: the buffers double).
@@ -809,16 +870,18 @@ static bool flush_votes_enqueue(Engine& g) {
       if (total > r.d_qpack.n) check(r.d_qpack.alloc(std::max<uint64_t>(total, 2 * r.d_qpack.n)));
       if (lead_words > r.d_leader.n) {
         check(r.d_leader.alloc(std::max<uint64_t>(lead_words, 2 * r.d_leader.n)));
-        hchk(hipMemsetAsync(r.d_leader.p, 0, 8, r.s), "memset");  // both counters
+        hchk(hipMemsetAsync(r.d_leader.p, 0, 16, r.s), "memset");  // both counters and the gather ticket
       }
     }
     // the pack crosses PCIe in a kernel of this stream (a copy-engine H2D costs ~13 us more on
     // the transition's critical path: the kernel behind it waits for the engine's signal)
-    if (!g.q_arena_dev) hchk(hipHostGetDevicePointer(&g.q_arena_dev, g.q_arena, 0), "hipHostGetDevicePointer");
-    void* src = g.q_arena_dev;
+    void* src = nullptr;
+    check(g.q_arena.dev(&src));
     hchk(launch_stage_h2d(src, r.d_qpack.p, total, r.s), "stage H2D");
-    if (!r.q_ev) hchk(hipEventCreateWithFlags(&r.q_ev, hipEventDisableTiming), "event");
-    hchk(hipEventRecord(r.q_ev, r.s), "event");
+    if (!gather) {  // (gathering: g.ev_totals, later in the stream, frees the arena)
+      if (!r.q_ev) hchk(hipEventCreateWithFlags(&r.q_ev, hipEventDisableTiming), "event");
+      hchk(hipEventRecord(r.q_ev, r.s), "event");
+    }
     if (!r.d_err.p) {
       check(r.d_err.alloc(1));
       hchk(hipMemsetAsync(r.d_err.p, 0, 8, r.s), "memset");
@@ -850,15 +913,27 @@ static bool flush_votes_enqueue(Engine& g) {
     r.lead_par ^= 1;
     v.ncomm = g.ncomm;
     v.cwords = g.cwords;
+    if (gather) {
+      check(g.tot_pin.reserve((kJustifySlots + 1) * 8));
+      void* dp = nullptr;
+      check(g.tot_pin.dev(&dp));
+      v.gather_out = static_cast<uint64_t*>(dp);
+      v.ticket = r.d_leader.p + 2;
+      v.gq = *gq;
+    }
     hchk(launch_vote_ids(v, r.s), "vote tally");
+    if (gather) {
+      if (!g.ev_totals) hchk(hipEventCreateWithFlags(&g.ev_totals, hipEventDisableTiming), "event");
+      hchk(hipEventRecord(g.ev_totals, r.s), "event");
+    }
   });
-  g.q_arena_busy = true;
+  g.q_arena_busy = !gather;
   g.q_bits.clear();
   g.q_boffs.assign(1, 0);
   g.q_comm.clear();
   g.q_slots.clear();
   g.q_skip.clear();
-  return true;
+  return gather;
 }
 
 // Enqueue, behind every rank's pending tallies, the gather of the 64 justification totals
@@ -904,6 +979,7 @@ static void tally_gather_enqueue(Engine& g, const VoteGatherSlots& q) {
 // After g.ev_totals: raise the panic a tally detected.
 static void tally_gather_finish(Engine& g) {
   hchk(hipEventSynchronize(g.ev_totals), "event sync (vote totals)");
+  g.q_arena_busy = false;  // every rank's flush is behind g.ev_totals
   if (reinterpret_cast<const uint64_t*>(g.tot_pin.p)[kJustifySlots])
     throw Panic{"calculateBlockVoteCache: CheckBit / validator index out of range"};
 }
@@ -1109,9 +1185,11 @@ static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending
   each_rank(g, [&](RankDev& r) {
     check(r.e_pack.alloc(total));
     hchk(hipMemcpyAsync(r.e_pack.p, h, total, hipMemcpyHostToDevice, r.s), "H2D epoch");
-    check(r.e_red.alloc(nred + 1));
+    // one rank: the winners sit right after the scalars, so one D2H brings both back
+    const uint64_t wn = g.world == 1 ? (nrec + 1) / 2 : 0;
+    check(r.e_red.alloc(nred + wn + 1));
     check(r.e_nb.alloc(1));
-    check(r.e_win.alloc(nrec + 1));
+    if (g.world > 1) check(r.e_win.alloc(nrec + 1));
     hchk(hipMemsetAsync(r.e_red.p, 0, kScal * 8, r.s), "memset");
     uint8_t* d = r.e_pack.p;
     EpochArgs a;
@@ -1141,10 +1219,10 @@ static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending
     a.att_shard = reinterpret_cast<const uint32_t*>(d + o_shard);
     a.nrec = (uint32_t)nrec;
     a.rec_dynasty = reinterpret_cast<const uint64_t*>(d + o_rdyn);
-    a.winner = r.e_win.p;
+    a.winner = g.world == 1 ? reinterpret_cast<uint32_t*>(r.e_red.p + kScal) : r.e_win.p;
     a.scal = r.e_red.p;
-    a.vote = r.e_red.p + kScal;
-    a.total = r.e_red.p + kScal + na;
+    a.vote = r.e_red.p + kScal + wn;
+    a.total = r.e_red.p + kScal + wn + na;
     a.act_mask = r.e_mask.p;
     a.blk_cnt = r.e_blk.p;
     a.act_list = r.e_list.p;
@@ -1186,9 +1264,13 @@ static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending
   RankDev& r0 = g.rk[0];
   hchk(hipSetDevice(r0.dev), "hipSetDevice");
   check(g.e_pin_out.reserve(kScal * 8 + nrec * 4 + 16));
-  hchk(hipMemcpyAsync(g.e_pin_out.p, r0.e_red.p, kScal * 8, hipMemcpyDeviceToHost, r0.s), "D2H");
-  if (nrec)
-    hchk(hipMemcpyAsync(g.e_pin_out.p + kScal * 8, r0.e_win.p, nrec * 4, hipMemcpyDeviceToHost, r0.s), "D2H");
+  if (g.world == 1) {
+    hchk(hipMemcpyAsync(g.e_pin_out.p, r0.e_red.p, kScal * 8 + nrec * 4, hipMemcpyDeviceToHost, r0.s), "D2H");
+  } else {
+    hchk(hipMemcpyAsync(g.e_pin_out.p, r0.e_red.p, kScal * 8, hipMemcpyDeviceToHost, r0.s), "D2H");
+    if (nrec)
+      hchk(hipMemcpyAsync(g.e_pin_out.p + kScal * 8, r0.e_win.p, nrec * 4, hipMemcpyDeviceToHost, r0.s), "D2H");
+  }
   each_rank(g, [&](RankDev& r) {
     if (!r.ev_epoch) hchk(hipEventCreateWithFlags(&r.ev_epoch, hipEventDisableTiming), "event");
     hchk(hipEventRecord(r.ev_epoch, r.s), "event");
@@ -1240,11 +1322,6 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   // vote tallies and the D2H of their totals.  The device epoch (processCrosslinks,
   // CalculateRewards, next balance) does not depend on it and is enqueued behind them, to be
   // collected at the next transition; the stream orders every later tally after its rewards.
-  flush_votes_enqueue(g);
-  PhaseTimer pt(g.prof[kProfRecalc]);
-  uint64_t streak = C->streak, justified = C->jslot, finalized = C->fslot;
-  const uint64_t lsr = C->lsr;
-  std::vector<uint64_t> tot(kCycle, 0);
   VoteGatherSlots q;
   for (uint64_t i = 0; i < kCycle; ++i) {
     q.slot[i] = UINT32_MAX;
@@ -1252,7 +1329,12 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
       if (const uint32_t* sl = g.slot_of.find(g.hlog[recent_id(g, *A, i)])) q.slot[i] = *sl;
     }
   }
-  tally_gather_enqueue(g, q);
+  const bool gathered = flush_votes_enqueue(g, &q);
+  PhaseTimer pt(g.prof[kProfRecalc]);
+  uint64_t streak = C->streak, justified = C->jslot, finalized = C->fslot;
+  const uint64_t lsr = C->lsr;
+  std::vector<uint64_t> tot(kCycle, 0);
+  if (!gathered) tally_gather_enqueue(g, q);
   epoch_enqueue(g, *C, A->pending);
   auto nc = std::make_shared<CState>();
   g.deferred.live = true;
@@ -1694,8 +1776,9 @@ static int reload(Engine& g, const uint8_t* data, uint64_t len) {
 // threads -- and the walk that reads the records 10-20 % slower: records left in other cores'
 // caches; profiles/r03/replay_threads_r3c.txt.)
 // The call's arena: a copy of the input bytes (filled by whoever parses them), the records
-// reserved to the counted number, the oblique pool to a bound (an element takes >= 2 bytes).
-static std::shared_ptr<CallArena> make_arena(const uint64_t* offs, uint64_t n, uint64_t natt, PinBuf* pin = nullptr) {
+// sized to the per-block counts (`first`, n + 1 entries), `npools` oblique pools.
+static std::shared_ptr<CallArena> make_arena(const uint64_t* offs, uint64_t n, std::vector<uint64_t>&& first,
+                                             size_t npools, PinBuf* pin = nullptr) {
   auto ar = std::make_shared<CallArena>();
   const uint64_t total = n ? offs[n] - offs[0] : 0;
   if (pin) {
@@ -1706,23 +1789,84 @@ static std::shared_ptr<CallArena> make_arena(const uint64_t* offs, uint64_t n, u
     ar->bytes = ar->own.get();
   }
   std::memset(ar->bytes + total, 0, 16);
-  ar->atts.reserve(natt);
-  ar->ptrs.reserve(natt);
-  ar->obl.reserve(total / 2 + 1);
+  ar->first = std::move(first);
+  const uint64_t natt = ar->first.empty() ? 0 : ar->first.back();
+  ar->atts.resize(natt);
+  ar->ptrs.resize(natt);
+  ar->obl.resize(std::max<size_t>(npools, 1));
   return ar;
 }
 
-// Blocks [b0, b1): copied into the arena and parsed; returns the first malformed block or b1.
+// Records per block (field 8 of BeaconBlock, messages.pb.go:224-232) as the prefix `first`
+// (n + 1 entries); PZ_EINVAL when the offsets are not monotone.  The canonical-form checks are
+// the parser's.
+static int count_per_block(const uint8_t* data, const uint64_t* offs, uint64_t n, std::vector<uint64_t>& first) {
+  first.assign(n + 1, 0);
+  for (uint64_t i = 0; i < n; ++i) {
+    if (offs[i + 1] < offs[i]) return fail(PZ_EINVAL, "offsets not monotone");
+    Reader r{data + offs[i], data + offs[i + 1]};
+    uint64_t c = 0;
+    while (r.more()) {
+      const uint64_t key = r.varint();
+      if ((key >> 3) == 8 && (key & 7) == 2) ++c;
+      r.skip((uint32_t)(key & 7));
+    }
+    first[i + 1] = first[i] + c;
+  }
+  return PZ_OK;
+}
+
+// Blocks [b0, b1): copied into the arena and parsed, their oblique hashes into pool `pl`
+// (reserved here); returns the first malformed block or b1.
 static uint64_t parse_range(const uint8_t* data, const uint64_t* offs, uint64_t b0, uint64_t b1, CallArena& ar,
-                            std::vector<Block>& blocks) {
+                            std::vector<Block>& blocks, size_t pl) {
   const uint64_t o0 = offs[0];
   for (uint64_t i = b0; i < b1; ++i)
     if (offs[i + 1] < offs[i]) return i;
   if (b1 > b0) std::memcpy(ar.bytes + (offs[b0] - o0), data + offs[b0], offs[b1] - offs[b0]);
+  CallArena::Pool& pool = ar.obl[pl];
+  pool.reserve((offs[b1] - offs[b0]) / 2 + 1);
   const uint8_t* base = ar.bytes - o0;
   for (uint64_t i = b0; i < b1; ++i)
-    if (!parse_block(base + offs[i], offs[i + 1] - offs[i], &blocks[i], &ar)) return i;
+    if (!parse_block(base + offs[i], offs[i + 1] - offs[i], &blocks[i], &ar, i, pool)) return i;
   return b1;
+}
+
+// Threads for the parse of a call of `bytes` input bytes: PZ_PARSE_THREADS (default 8; the
+// CPU share of one GPU on the bench boxes is 16), one per ~1 MB.
+static int parse_threads(uint64_t bytes) {
+  static const int cap = [] {
+    const char* e = std::getenv("PZ_PARSE_THREADS");
+    return e ? std::max(1, std::atoi(e)) : 8;
+  }();
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cap, bytes >> 20));
+}
+
+// Blocks [0, n) over ar.obl.size() threads (ranges of about equal bytes; records need no
+// allocation, so the threads share nothing but the arena's disjoint ranges); returns the first
+// malformed block or n.
+static uint64_t parse_parallel(const uint8_t* data, const uint64_t* offs, uint64_t n, CallArena& ar,
+                               std::vector<Block>& blocks) {
+  const size_t T = ar.obl.size();
+  if (T <= 1 || n < 2 * T) return parse_range(data, offs, 0, n, ar, blocks, 0);
+  for (uint64_t i = 0; i < n; ++i)
+    if (offs[i + 1] < offs[i]) return i;
+  std::vector<uint64_t> cut(T + 1, n);
+  cut[0] = 0;
+  const uint64_t total = offs[n] - offs[0];
+  for (size_t t = 1; t < T; ++t) {
+    const uint64_t want = offs[0] + total / T * t;
+    cut[t] = std::max<uint64_t>(cut[t - 1], std::lower_bound(offs, offs + n, want) - offs);
+  }
+  std::vector<uint64_t> bad(T, UINT64_MAX);
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < T; ++t)
+    th.emplace_back([&, t] { bad[t] = parse_range(data, offs, cut[t], cut[t + 1], ar, blocks, t); });
+  bad[0] = parse_range(data, offs, cut[0], cut[1], ar, blocks, 0);
+  for (auto& x : th) x.join();
+  for (size_t t = 0; t < T; ++t)
+    if (bad[t] < cut[t + 1]) return bad[t];
+  return n;
 }
 
 // After a call: the records a live state still holds (the pending attestations of the
@@ -1754,16 +1898,17 @@ static void keep_arenas(Engine& g, CallArena* cur) {
       na->bytes = na->own.get();
       std::memset(na->bytes + bytes, 0, 16);
       na->atts.reserve(mv.size());
-      na->obl.reserve(nobl + 1);
+      na->obl.resize(1);
+      na->obl[0].reserve(nobl + 1);
       size_t pos = 0;
       for (AttP p : mv) {
         Att a = *p;
         std::memcpy(na->bytes + pos, p->base, p->len);
         a.base = na->bytes + pos;
         pos += p->len;
-        a.obl_first = (uint32_t)na->obl.size();
-        for (auto& o : p->obl) na->obl.push_back(o);
-        a.obl.p = na->obl.data() + a.obl_first;  // (reserved: never reallocates)
+        a.obl_first = (uint32_t)na->obl[0].size();
+        for (auto& o : p->obl) na->obl[0].push_back(o);
+        a.obl.p = na->obl[0].data() + a.obl_first;  // (reserved: never reallocates)
         na->atts.push_back(a);
       }
       for (auto* l : lists)
@@ -1790,12 +1935,15 @@ static void keep_arenas(Engine& g, CallArena* cur) {
 
 // Every block, on the calling thread, before anything else (the path that keeps a call
 // all-or-nothing; pz_chain_process_blocks pipelines the parse otherwise).
-static int parse_all(const uint8_t* data, const uint64_t* offs, uint64_t n, uint64_t natt, std::vector<Block>& blocks,
-                     std::shared_ptr<CallArena>* keep) {
-  auto ar = make_arena(offs, n, natt);
+static int parse_all(const uint8_t* data, const uint64_t* offs, uint64_t n, std::vector<Block>& blocks,
+                     std::shared_ptr<CallArena>* keep, int threads) {
+  std::vector<uint64_t> first;
+  int rc = count_per_block(data, offs, n, first);
+  if (rc) return rc;
+  auto ar = make_arena(offs, n, std::move(first), (size_t)threads);
   *keep = ar;  // the blocks' bytes live here for the whole call (records alias it beyond)
   blocks.resize(n);
-  const uint64_t bad = parse_range(data, offs, 0, n, *ar, blocks);
+  const uint64_t bad = parse_parallel(data, offs, n, *ar, blocks);
   if (bad < n) return fail(PZ_EINVAL, "block %llu is not a canonical BeaconBlock encoding", (unsigned long long)bad);
   return PZ_OK;
 }
@@ -2056,7 +2204,7 @@ static void feed(Engine& g, Feeder& F, const uint8_t* data, const uint64_t* offs
       }
       Feeder::Slot& S = F.slot[j % kRing];
       uint64_t b1 = std::min(F.n, b0 + kChunk);
-      const uint64_t good = parse_range(data, offs, b0, b1, *ar, *F.blocks);
+      const uint64_t good = parse_range(data, offs, b0, b1, *ar, *F.blocks, (size_t)j);
       b1 = good;
       uint64_t na = 0;
       for (uint64_t bi = b0; bi < b1; ++bi) na += (*F.blocks)[bi].atts.size();
@@ -2094,11 +2242,13 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
   g.m_hdr.reserve(16 * natt);
   g.m_ref.reserve(natt);
   // the tables grow once per call, not by doubling inside the walk
-  g.saved.reserve(g.saved.size() + n);
   g.slot_of.reserve(g.slot_of.size() + n);  // (plus any oblique hash shorter than 32 B: grows)
   g.hlog.reserve(g.hlog.size() + n + 2 * natt);
   g.id_slot.reserve(g.id_slot.size() + n + 2 * natt);
   g.trail.reserve(g.trail.size() + n + 2 * kCycle);
+  // every block digest takes a vote-cache slot: one growth for the call, not a doubling (and
+  // a stream sync) every few hundred blocks
+  if (g.slot_hash.size() + n >= g.cap) grow_slots(g, std::max<uint64_t>(2 * g.cap, g.slot_hash.size() + n + 64));
   msg_att.reserve(natt);
   auto t_walk = std::chrono::steady_clock::now();
   uint64_t logged = 0;  // block digests are logged a chunk at a time, as they arrive
@@ -2128,7 +2278,7 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
     }
     H32 h;
     std::memcpy(h.b, r.hash, 32);
-    if (b.slot > 1 && !g.saved.count(b.parent)) {
+    if (b.slot > 1 && !is_saved(g, b.parent)) {
       r.status = PZ_BLOCK_NO_PARENT;
       continue;
     }
@@ -2174,7 +2324,7 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
       g.cand_A.reset();
       g.cand_C.reset();
     }
-    g.saved.insert(h, 1);
+    g.slot_saved[g.id_slot[block_id[bi]]] = 1;
     if (g.has_cand) {
       r.status = PZ_BLOCK_SAVED_NOT_CANDIDATE;
       continue;
@@ -2266,7 +2416,6 @@ static void destroy_chain(pz_chain* c) {
       if (e) (void)hipEventDestroy(e);
     streams.push_back({r.dev, r.s});
   }
-  if (g.q_arena) (void)hipHostFree(g.q_arena);
   if (g.ev_totals) (void)hipEventDestroy(g.ev_totals);
   for (hipEvent_t e : g.ring_ev)
     if (e) (void)hipEventDestroy(e);
@@ -2339,15 +2488,10 @@ int pz_count_attestations(const uint8_t* blocks, const uint64_t* offsets, uint64
   if (!count) return fail(PZ_EINVAL, "count is null");
   *count = 0;
   if (n && (!blocks || !offsets)) return fail(PZ_EINVAL, "null pointer");
-  for (uint64_t i = 0; i < n; ++i) {
-    if (offsets[i + 1] < offsets[i]) return fail(PZ_EINVAL, "offsets not monotone");
-    Reader r{blocks + offsets[i], blocks + offsets[i + 1]};
-    while (r.more()) {
-      const uint64_t key = r.varint();
-      if ((key >> 3) == 8 && (key & 7) == 2) ++*count;
-      r.skip((uint32_t)(key & 7));
-    }
-  }
+  std::vector<uint64_t> first;
+  const int rc = count_per_block(blocks, offsets, n, first);
+  if (rc) return rc;
+  *count = first[n];
   return PZ_OK;
 }
 
@@ -2361,13 +2505,14 @@ int pz_chain_process_blocks(pz_chain* c, const uint8_t* blocks, const uint64_t* 
   hipError_t e = hipSetDevice(c->g.device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   // the output capacity is checked before any state changes
-  uint64_t natt = 0;
+  std::vector<uint64_t> first;
   int rc0;
   {
     PhaseTimer pt(c->g.prof[kProfCount]);
-    rc0 = pz_count_attestations(blocks, offsets, n, &natt);
+    rc0 = count_per_block(blocks, offsets, n, first);
   }
   if (rc0) return rc0;
+  const uint64_t natt = first[n];
   if (natt > att_cap || (natt && !att_out)) return fail(PZ_EINVAL, "att_out holds %llu results, need %llu",
                                                         (unsigned long long)att_cap, (unsigned long long)natt);
   Engine& g = c->g;
@@ -2396,8 +2541,8 @@ int pz_chain_process_blocks(pz_chain* c, const uint8_t* blocks, const uint64_t* 
   if (!F.piped) {
     try {
       PhaseTimer pt(g.prof[kProfParse]);
-      arena = make_arena(offsets, n, natt, &g.arena_pin);
-      const uint64_t good = parse_range(blocks, offsets, 0, n, *arena, parsed);
+      arena = make_arena(offsets, n, std::move(first), (size_t)parse_threads(offsets[n] - offsets[0]), &g.arena_pin);
+      const uint64_t good = parse_parallel(blocks, offsets, n, *arena, parsed);
       if (good < n) {  // the walk stops before the malformed block
         F.bad.store(good);
         F.n = good;
@@ -2453,7 +2598,7 @@ int pz_chain_process_blocks(pz_chain* c, const uint8_t* blocks, const uint64_t* 
   } else {
     // the parse and the digest batches run a chunk ahead of the walk on a producer thread
     try {
-      arena = make_arena(offsets, n, natt, &g.arena_pin);
+      arena = make_arena(offsets, n, std::move(first), (size_t)((n + kChunk - 1) / kChunk), &g.arena_pin);
     } catch (int rc) {
       return rc;
     }
@@ -2629,20 +2774,41 @@ extern "C" int pz_debug_chain_profile(pz_chain* c, double* out, int n) {
   return pz::chain::kProfSlots;
 }
 
-// Internal (tools/, CPU-only: no device call): the block parser of pz_chain_process_blocks on
-// its own, `reps` times; returns the wall seconds of the fastest run.
-extern "C" int pz_debug_parse(const uint8_t* data, const uint64_t* offs, uint64_t n, uint64_t natt, int reps,
-                              double* seconds) {
+// Internal (tests/, tools/; CPU-only: no device call): the block parser of
+// pz_chain_process_blocks on its own with `threads` threads, `reps` times; returns the wall
+// seconds of the fastest run and a checksum of what it parsed (every block's slot, parent and
+// record count, every record's fields and oblique spans), so that thread counts can be
+// compared.  A malformed block fails with PZ_EINVAL naming the first one.
+extern "C" int pz_debug_parse(const uint8_t* data, const uint64_t* offs, uint64_t n, uint64_t threads, int reps,
+                              double* seconds, uint64_t* checksum) {
   double best = 1e30;
   for (int r = 0; r < reps; ++r) {
     const auto t0 = std::chrono::steady_clock::now();
     {
       std::vector<pz::chain::Block> blocks;
       std::shared_ptr<pz::chain::CallArena> arena;
-      const int rc = pz::chain::parse_all(data, offs, n, natt, blocks, &arena);
+      const int rc = pz::chain::parse_all(data, offs, n, blocks, &arena, (int)std::max<uint64_t>(1, threads));
       if (rc) return rc;
+      best = std::min(best, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+      if (checksum && r == 0) {
+        uint64_t h = 1469598103934665603ull;
+        auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
+        for (const auto& b : blocks) {
+          mix(b.slot);
+          mix(b.len);
+          for (int k = 0; k < 32; ++k) mix(b.parent.b[k]);
+          mix(b.atts.size());
+          for (auto ap : b.atts) {
+            const auto& a = *ap;
+            mix((uint64_t)(a.base - b.data));
+            mix(a.len); mix(a.slot); mix(a.shard); mix(a.jslot);
+            mix(a.sbh_off); mix(a.sbh_len); mix(a.bf_off); mix(a.bf_len);
+            for (auto& o : a.obl) { mix(o.first); mix(o.second); }
+          }
+        }
+        *checksum = h;
+      }
     }
-    best = std::min(best, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
   }
   if (seconds) *seconds = best;
   return PZ_OK;

@@ -9,6 +9,14 @@ namespace pz {
 typedef pz_vote_batch VoteArgs;
 hipError_t launch_vote_tally(const VoteArgs& a, hipStream_t s);
 
+// The 64 totals a stateRecalc's justification loop reads (blockchain/core.go:413-418) and the
+// sticky tally panic flag, gathered into out[0..64] (slot UINT32_MAX: no map entry, total 0):
+// one small D2H (or one 65-word all-reduce of a validator-range-sharded cache) per transition.
+constexpr int kJustifySlots = 64;
+struct VoteGatherSlots {
+  uint32_t slot[kJustifySlots];
+};
+
 // The block engine's tally (chain.hip): natt attestations x their 64 signed parent hashes.
 struct VoteIdArgs {
   const uint32_t* committee;
@@ -35,19 +43,18 @@ struct VoteIdArgs {
   uint64_t ncomm, cwords;
   uint64_t val_offset;   // a validator-range shard: balance and bitmaps hold [val_offset, val_offset + nval)
   uint64_t nval_global;  // of nval_global validators (0: nval, unsharded)
+  // non-null: the leader pass's last block to finish also does launch_vote_gather's work into
+  // gather_out (a stateRecalc's flush: one kernel boundary less on the walk's wait); `ticket`
+  // is a zero device word, left zero
+  uint64_t* gather_out;
+  uint32_t* ticket;
+  VoteGatherSlots gq;
 };
 hipError_t launch_vote_ids(const VoteIdArgs& a, hipStream_t s);
 // Copy `bytes` (a multiple of 16) from mapped pinned host memory to device memory in a kernel on
 // stream s: 16 B per lane, so the bytes cross PCIe in one round trip of coalesced reads.
 hipError_t launch_stage_h2d(const void* host_mapped, void* dev, uint64_t bytes, hipStream_t s);
 
-// The 64 totals a stateRecalc's justification loop reads (blockchain/core.go:413-418) and the
-// sticky tally panic flag, gathered into out[0..64] (slot UINT32_MAX: no map entry, total 0):
-// one small D2H (or one 65-word all-reduce of a validator-range-sharded cache) per transition.
-constexpr int kJustifySlots = 64;
-struct VoteGatherSlots {
-  uint32_t slot[kJustifySlots];
-};
 hipError_t launch_vote_gather(const uint64_t* totals, VoteGatherSlots slots, const uint64_t* err, uint64_t* out,
                               hipStream_t s);
 }  // namespace pz

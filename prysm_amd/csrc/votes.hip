@@ -194,6 +194,30 @@ pz_vote_leader_kernel(VoteIdArgs a) {
     for (uint64_t w = threadIdx.x & 63; w < a.cwords; w += 64) u[w] = 0;
     if ((threadIdx.x & 63) == 0) a.uflag[grp] = 0;
   }
+  if (!a.gather_out) return;
+  // The fused gather (MI355X_MICROARCH.md's last-block hand-off): every wave drains its tally
+  // atomics before the block barrier, one lane per block takes a ticket, and the block that
+  // takes the last one reads the complete totals with agent-scope loads (they are only written
+  // by device-scope atomics) into the pinned output.
+  __shared__ uint32_t last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!last) return;
+  const int j = threadIdx.x;
+  if (j < kJustifySlots) {
+    const uint32_t sl = a.gq.slot[j];
+    a.gather_out[j] =
+        sl == 0xFFFFFFFFu ? 0 : __hip_atomic_load(&a.totals[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (j == 0) {
+    a.gather_out[kJustifySlots] = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 hipError_t launch_vote_ids(const VoteIdArgs& a, hipStream_t s) {

@@ -25,7 +25,7 @@ def main():
     ch = BeaconChain(nval)
     torch.cuda.synchronize()
     print("genesis %.3f s" % (time.perf_counter() - t), flush=True)
-    ch.process_blocks(blocks[:70])  # warm-up (kernels loaded)
+    ch.process_serialized(*serialize_blocks(blocks))  # warm-up (kernels loaded, pinned pool filled)
     ch = BeaconChain(nval)
     prof = cProfile.Profile() if "--cprofile" in sys.argv else None
     t = time.perf_counter()
