@@ -596,7 +596,9 @@ struct Engine {
   bool q_arena_busy = false;
   uint64_t ncomm = 0, cwords = 1;
   PinBuf e_pin, e_pin_out;   // the epoch inputs' pinned staging; the results' pinned landing
-  PinBuf tot_pin;            // the gathered justification totals (65 words)
+  PinBuf tot_pin;            // the gathered justification totals (65 words; + a sequence word)
+  uint64_t gather_seq = 0;   // the last sequence number the fused gather was asked to write
+  bool gather_poll = false;  // the current transition's totals arrive with their sequence word
   hipEvent_t ev_totals = nullptr;  // the tally flush + the totals' D2H of a transition are done
   // The epoch of the last transition, enqueued but not yet collected: its results (the
   // crosslink records, the next state's TotalDeposits, a panic) are first needed at the next
@@ -914,12 +916,15 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr) 
     v.ncomm = g.ncomm;
     v.cwords = g.cwords;
     if (gather) {
-      check(g.tot_pin.reserve((kJustifySlots + 1) * 8));
+      check(g.tot_pin.reserve((kJustifySlots + 2) * 8));
       void* dp = nullptr;
       check(g.tot_pin.dev(&dp));
       v.gather_out = static_cast<uint64_t*>(dp);
       v.ticket = r.d_leader.p + 2;
       v.gq = *gq;
+      v.gather_seq = ++g.gather_seq;
+      // (pooled pinned memory holds old words: clear the sequence word before the launch)
+      reinterpret_cast<volatile uint64_t*>(g.tot_pin.p)[kJustifySlots + 1] = 0;
     }
     hchk(launch_vote_ids(v, r.s), "vote tally");
     if (gather) {
@@ -928,6 +933,7 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr) 
     }
   });
   g.q_arena_busy = !gather;
+  g.gather_poll = gather;
   g.q_bits.clear();
   g.q_boffs.assign(1, 0);
   g.q_comm.clear();
@@ -978,6 +984,27 @@ static void tally_gather_enqueue(Engine& g, const VoteGatherSlots& q) {
 
 // After g.ev_totals: raise the panic a tally detected.
 static void tally_gather_finish(Engine& g) {
+  if (g.gather_poll) {
+    // The fused gather writes its sequence word last (system-scope release): spin on the pinned
+    // word instead of sleeping in the event wait, whose wake-up took ~10-20 us of every
+    // transition's critical path.  Bounded: past ~50 ms the event wait decides (an error
+    // surfaces there).
+    g.gather_poll = false;
+    const volatile uint64_t* sq = reinterpret_cast<const volatile uint64_t*>(g.tot_pin.p) + kJustifySlots + 1;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t k = 0; *sq != g.gather_seq; ++k) {
+      __builtin_ia32_pause();
+      if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (*sq == g.gather_seq) {
+      // every rank's flush is done: its stage kernel preceded the leader pass
+      g.q_arena_busy = false;
+      if (reinterpret_cast<const uint64_t*>(g.tot_pin.p)[kJustifySlots])
+        throw Panic{"calculateBlockVoteCache: CheckBit / validator index out of range"};
+      return;
+    }
+  }
   hchk(hipEventSynchronize(g.ev_totals), "event sync (vote totals)");
   g.q_arena_busy = false;  // every rank's flush is behind g.ev_totals
   if (reinterpret_cast<const uint64_t*>(g.tot_pin.p)[kJustifySlots])

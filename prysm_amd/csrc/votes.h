@@ -49,6 +49,9 @@ struct VoteIdArgs {
   uint64_t* gather_out;
   uint32_t* ticket;
   VoteGatherSlots gq;
+  // gather_out[kJustifySlots + 1] is set to gather_seq last, behind a system-scope release, so
+  // that the host can poll the pinned words instead of sleeping in an event wait
+  uint64_t gather_seq;
 };
 hipError_t launch_vote_ids(const VoteIdArgs& a, hipStream_t s);
 // Copy `bytes` (a multiple of 16) from mapped pinned host memory to device memory in a kernel on
