@@ -397,6 +397,7 @@ def epoch_single_instance(args, torch, dev, nval, shuffled):
                 b0.elapsed_time(b1) / len(evs))
 
     ms, wall_ms, b2b = measure()
+    floor = event_pair_floor(args, torch, dev)
     old = _lib.lib.dll.pz_debug_set_fused_variant(128)  # the single launch off: pre + fused + mid
     try:
         ms3, wall3, b2b3 = measure()
@@ -404,8 +405,32 @@ def epoch_single_instance(args, torch, dev, nval, shuffled):
         _lib.lib.dll.pz_debug_set_fused_variant(old)
     return {"validators": nval, "instances_per_step": 1, "path": "pz_epoch_one_kernel (single launch)",
             "device_ms_median": ms, "wall_ms_per_step": wall_ms, "back_to_back_ms_per_step": b2b,
+            "device_ms_net_of_event_floor": ms - floor["empty_ms"], "event_floor": floor,
             "validator_epochs_per_s": nval / (ms * 1e-3),
             "three_launches": {"device_ms_median": ms3, "wall_ms_per_step": wall3, "back_to_back_ms_per_step": b2b3}}
+
+
+def event_pair_floor(args, torch, dev):
+    """What the event-pair clock of epoch_single_instance reads with nothing between the two
+    events, and around one one-element torch kernel, on a fresh stream (tools/launch_floor.py:
+    ~4.8 and ~8.6 us on an MI355X): the floor under any single-launch latency measured so."""
+    s = torch.cuda.Stream(device=dev)
+    x = torch.zeros(1, device=dev)
+
+    def med(fn, k=max(args.steps, 50)):
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(k)]
+        with torch.cuda.stream(s):
+            for _ in range(10):
+                fn()
+            for e0, e1 in evs:
+                e0.record(s)
+                fn()
+                e1.record(s)
+        s.synchronize()
+        return float(np.median([e0.elapsed_time(e1) for e0, e1 in evs]))
+
+    return {"empty_ms": med(lambda: None), "tiny_kernel_ms": med(lambda: x.add_(1)),
+            "what": "median HIP-event pair around nothing / one 1-element torch kernel"}
 
 
 def epoch_cpu_baseline(inst):

@@ -98,6 +98,14 @@ struct FusedArgs {
                               //   inputs made at upload, so the length check needs no coffs hop)
   const uint4* items_ci;      // [B][nitems] each piece's FusedCommittee {boff lo, boff hi, nbits,
                               //   ga} per instance, read beside its item (no items -> cinfo hop)
+  // single-launch step, every attested committee one piece (so one wave holds each
+  // attestation's complete tallies): that wave proposes the attestation as its shard's winner
+  // (atomicMin) and zeroes its next-step tallies; no last-block pass.  The winners ping-pong:
+  // this step resets winner_next (all 0xFFFFFFFF) for the next one.
+  int win_in_wave;
+  uint32_t* winner_next;
+  const uint2* att_win;       // [natt] {shard, record dynasty of that shard} per attestation (an
+                              //   upload-time layout: loaded beside the stream, no shard -> record hop)
 };
 // The single-launch step's limits: every block counts the instance's bitfields itself and the
 // last block keeps one LDS word per crosslink record.

@@ -895,6 +895,19 @@ __device__ __forceinline__ void fused_block_end(const EpochArgs& a, const FusedA
                                                 bool skip, bool applied, uint64_t pop, uint64_t ferr, bool rwd_err);
 __device__ __forceinline__ void one_tail(const EpochArgs& a, const FusedArgs& f, int tid);
 
+// FusedArgs.win_in_wave: attestation g's complete tallies (vote v, committee total t) are in
+// this wave -- the winner rule of core.go:549-555 (the first attestation, in order, with
+// 3*vote >= 2*total whose dynasty beats its shard's record) as an atomicMin over g, and g's
+// next-step tallies zeroed.
+// w = f.att_win[g]: {shard (< nrec: the host takes the one-launch step only then), its record's
+// dynasty}.
+__device__ __forceinline__ void one_win(const EpochArgs& a, const FusedArgs& f, uint32_t g, uint64_t v, uint64_t t,
+                                        uint2 w) {
+  if (3ull * v >= 2ull * t && a.dynasty[0] > (uint64_t)w.y) atomicMin(&a.winner[w.x], g);
+  f.vote_next[g] = 0;
+  f.total_next[g] = 0;
+}
+
 template <int MODE>
 __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro,
                                            const uint64_t* __restrict__ boffs_ro, const uint64_t* __restrict__ tdep_ro,
@@ -962,6 +975,9 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
       ci.nbits = ic.z;
       ci.ga = ic.w;
     }
+    // (one launch, winners in the waves: the single attestation's shard and record dynasty,
+    // loaded with the stream below rather than after the tallies)
+    const uint2 win1 = (ONE && f.win_in_wave && ci.ga < kNoAtt) ? f.att_win[ci.ga] : make_uint2(0, 0);
     const uint64_t p0 = (ws - a.val_offset) & ~1ull;  // local and even: the 16-B pair of ws
     uint64_t* Bal = a.balance + inst * f.vstride;
     const uint64_t* S = a.start + inst * f.vstride;
@@ -1077,6 +1093,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
         }
         vs = wave_sum(v);
         g1 = ci.ga;
+        if (ONE && f.win_in_wave && lane == 0) one_win(a, f, ci.ga, vs, ts, win1);
       } else {  // several attestations of this committee: direct atomics per attestation
         const uint32_t* co = catt_offs_ro + inst * (f.ncomm + 1);
         for (uint32_t k = co[it.z]; k < co[it.z + 1]; ++k) {
@@ -1092,6 +1109,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
             if (v1[j] && q + 1 < nbits && bit_at(bf, q + 1)) v += pack64(qb[j].z, qb[j].w);
           }
           v = wave_sum(v);
+          if (ONE && f.win_in_wave && lane == 0) one_win(a, f, (uint32_t)ga, v, ts, f.att_win[ga]);
           if (lane < 2) {  // one instruction: lane 0 the total, lane 1 the vote
             uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + ga;
             const uint64_t x = lane ? v : ts;
@@ -1145,7 +1163,12 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
   __syncthreads();
   if (!ONE && wave != 0) return;
   if (wave == 0) fused_block_end(a, f, xg, xt, xv, xs, xn, inst, grp, lane, skip, applied, pop, ferr, rwd_err);
-  if (ONE) one_tail(a, f, tid);
+  if (ONE && f.win_in_wave) {  // the next step's winners start empty (this step's are in a.winner)
+    for (uint32_t r = (uint32_t)(grp * blockDim.x) + tid; r < a.nrec; r += gridDim.y * blockDim.x)
+      f.winner_next[r] = 0xFFFFFFFFu;
+  } else if (ONE) {
+    one_tail(a, f, tid);
+  }
 }
 
 // Wave 0 of a fused block: the block's tallies, next-cycle sum and per-instance scalars.

@@ -36,6 +36,7 @@ struct Part {
   uint64_t* red[2] = {nullptr, nullptr};  // ping-pong {scal[B][8], vote[B*natt], total[B*natt]}
   int cur = 0;
   uint64_t* results = nullptr;            // the red buffer of the last completed step
+  uint32_t* win_results = nullptr;        // FusedArgs.win_in_wave: the winners of the last step
   uint64_t* mask_send = nullptr;          // [B][sw]
   uint64_t* gmask = nullptr;              // [world][B][sw]
   uint32_t* gblk = nullptr;               // [B][vblocks(N)]
@@ -153,6 +154,10 @@ void flip(pz_epoch_state* st) {
       Part& q = s.part[p];
       q.results = q.red[q.cur];
       q.cur ^= 1;
+      if (q.f.win_in_wave) {  // the winners ping-pong too (the step just enqueued wrote a.winner)
+        q.win_results = q.a.winner;
+        std::swap(q.a.winner, q.f.winner_next);
+      }
       const uint64_t Bp = q.B, natt = st->natt;
       q.a.scal = q.red[q.cur];
       q.a.vote = q.red[q.cur] + Bp * kScal;
@@ -660,6 +665,34 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
           rc = dalloc(s, &q.f.ticket, 1);
           if (!rc) rc = upload(s, &d_cs, cs.data(), cs.size());
           q.f.att_csize = d_cs;
+          // winners formed in the waves when every attested committee is one piece (its
+          // complete tallies in one wave); else the last block forms them (one_tail)
+          std::vector<uint32_t> pieces(st->ncomm, 0);
+          for (const uint4& it : items) ++pieces[it.z];
+          bool one_piece = st->nrec > 0;
+          for (uint64_t g = 0; g < st->natt && one_piece; ++g) one_piece = pieces[h->att_comm[i0 * st->natt + g]] == 1;
+          if (!rc && one_piece) {
+            // per attestation {shard, its record's dynasty} (the records are inputs of the state)
+            std::vector<uint2> aw(st->natt);
+            for (uint64_t g = 0; g < st->natt; ++g) {
+              const uint32_t sh = h->att_shard[i0 * st->natt + g];
+              aw[g] = make_uint2(sh, (uint32_t)h->rec_dynasty[i0 * st->nrec + sh]);
+              if (h->rec_dynasty[i0 * st->nrec + sh] >> 32) one_piece = false;  // (a 32-bit dynasty)
+            }
+            uint2* d_aw = nullptr;
+            if (one_piece) rc = upload(s, &d_aw, aw.data(), aw.size());
+            q.f.att_win = d_aw;
+          }
+          if (!rc && one_piece) {
+            uint32_t* w2 = nullptr;
+            rc = dalloc(s, &w2, st->nrec);
+            hipError_t e2 = hipSuccess;
+            if (!rc) e2 = hipMemsetAsync(w2, 0xFF, (size_t)st->nrec * 4, s.s);
+            if (!rc && e2 == hipSuccess) e2 = hipMemsetAsync(a.winner, 0xFF, (size_t)st->nrec * 4, s.s);
+            if (!rc && e2 != hipSuccess) rc = hip_fail(e2, "hipMemsetAsync (winners)");
+            q.f.win_in_wave = 1;
+            q.f.winner_next = w2;
+          }
         }
       }
       q.cur = 1;  // flip() below binds red[0] as the first step's buffer
@@ -743,7 +776,8 @@ int pz_epoch_state_results(pz_epoch_state* st, int local, uint64_t* balance, uin
     if (e == hipSuccess && total && na)
       e = hipMemcpy(total + i0 * na, q.results + Bp * kScal + Bp * na, Bp * na * 8, hipMemcpyDeviceToHost);
     if (e == hipSuccess && winner && st->nrec)
-      e = hipMemcpy(winner + i0 * st->nrec, q.a.winner, Bp * st->nrec * 4, hipMemcpyDeviceToHost);
+      e = hipMemcpy(winner + i0 * st->nrec, q.win_results ? q.win_results : q.a.winner, Bp * st->nrec * 4,
+                    hipMemcpyDeviceToHost);
   }
   return e == hipSuccess ? PZ_OK : hip_fail(e, "epoch state results D2H");
 }

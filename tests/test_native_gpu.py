@@ -71,12 +71,14 @@ def test_native_epoch_single_device(n, B, inactive, layout):
     _check(ne, inst, steps=2)
 
 
-@pytest.mark.parametrize("n", [65536, 4096, 4097, 1000, 130])
+@pytest.mark.parametrize("n", [65536, 32768, 16385, 4096, 4097, 1000, 130])
 @pytest.mark.parametrize("density", [0.5, 0.75])
 def test_native_epoch_single_launch(n, density):
     """One instance on one device: the single-launch step (pz_epoch_one_kernel: every block
-    counts the bits itself, the last block to arrive forms the winners), three steps in a row
-    (the ticket and the next step's tallies are reset in-kernel), bit-exact."""
+    counts the bits itself; the winners formed in the waves when every attested committee is
+    one piece, else by the last block to arrive -- 32,768 validators give 256-member
+    committees, some of them two pieces), three steps in a row (the ticket, the winners' ping-pong
+    and the next step's tallies are reset in-kernel), bit-exact."""
     inst = _inst(n, 1, False, density=density)
     ne = NativeEpoch(inst, device=0)
     assert ne.one_pass

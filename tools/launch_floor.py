@@ -12,7 +12,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from prysm_amd import synth  # noqa: E402
+from prysm_amd import casper, synth  # noqa: E402
 from prysm_amd.native import NativeEpoch  # noqa: E402
 
 
@@ -36,7 +36,8 @@ def pairs(stream, fn, k):
 def main():
     k = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     dev = torch.device("cuda", 0)
-    de = NativeEpoch(synth.epoch_batch(65536, 1, seed=3, shuffled=False), device=0)
+    shuffled = casper.shuffle_indices(b"A" + bytes(31), np.arange(65536, dtype=np.uint32))  # as bench.py
+    de = NativeEpoch(synth.epoch_batch(65536, 1, seed=3, shuffled=shuffled), device=0)
     stream = torch.cuda.ExternalStream(de.shard(0)[3], device=dev)
     x = torch.zeros(1, device=dev)
     for _ in range(50):
