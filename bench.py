@@ -147,6 +147,19 @@ def launch_ranks(args):
 # dynasty + 16 B balance read-modify-write + 1/8 B last-bitfield bit + 1/8 B committee bitfield
 # popcount + 12 B crosslink committee gather (u32 member + u64 balance).
 EPOCH_BYTES_PER_VALIDATOR = 44.25
+
+
+def epoch_layout_bytes(inst, one_pass):
+    """Bytes per validator-epoch the one-pass committee-order step must move:
+    the balance read and written (16), the {start, end} dynasties (8 in the packed 32-bit column
+    the state uploads when every CurrentDynasty is below 2^32 - 1, else 16), and the instance's
+    bitfields once (their bytes / nval); co_index is shared by the instances (L2).  None for
+    the other layouts (SURVEY.md §8d's 44.25 B stays their model)."""
+    if not one_pass:
+        return None
+    packed = int(np.max(inst["dynasty"])) < 0xFFFFFFFF and not os.environ.get("PZ_EPOCH_SE64")
+    bits = float(inst["boffs"][-1]) / (inst["ninst"] * inst["nval"])
+    return 16 + (8 if packed else 16) + bits
 HASH_KERNEL = "pz_b2b_fixed_persistent_kernel"
 CPU_SAMPLE_S = 8.0  # seconds of CPU work per cpu_baseline leg (three legs: ~25 s in all)
 
@@ -219,8 +232,11 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
         wall = max_over_ranks(wall, torch, dist, dev)
     units = nval * ninst * args.steps
     local_units = (hi - lo) * ninst
-    achieved = local_units * EPOCH_BYTES_PER_VALIDATOR / (step_ms * 1e-3)
     one_pass = native and de.one_pass
+    lay = epoch_layout_bytes(inst, one_pass)
+    bpv = lay if lay is not None else EPOCH_BYTES_PER_VALIDATOR
+    achieved = local_units * bpv / (step_ms * 1e-3)
+    survey = local_units * EPOCH_BYTES_PER_VALIDATOR / (step_ms * 1e-3)
     workload = {(65536, 256): "epoch65k", (1 << 20, 16): "epoch1m"}.get((nval, ninst)) if world == 1 else None
     traffic = pmc_traffic(["pz_epoch_*"], workload) if workload else None
     out = {
@@ -245,22 +261,28 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                             if native else "DeviceEpoch (pz_dev_epoch_* + torch.distributed collectives)")},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
-                     "bytes_model": "SURVEY.md §8d: 44.25 B per validator-epoch (the committee-order layout "
-                                    "does not move the 12 B committee gather it prices: see traffic)",
+                     "bytes_model": (("the one-pass committee-order layout's bytes: %.2f B per validator-epoch "
+                                      "(balance read + write 16, {start, end} %d, bitfields %.2f; DESIGN.md §3)"
+                                      % (bpv, round(bpv - 16 - (bpv % 1)), bpv % 1)) if lay is not None else
+                                     "SURVEY.md §8d: 44.25 B per validator-epoch"),
+                     "survey_model": {"bytes_per_validator_epoch": EPOCH_BYTES_PER_VALIDATOR,
+                                      "achieved": survey / 1e9, "frac": survey / HBM_PEAK,
+                                      "note": "SURVEY.md §8d's figure prices a 12 B committee gather and 16 B of "
+                                              "start/end the committee-order layout does not move"},
                      "traffic": traffic,
                      "traffic_source": ("%s (every pz_epoch_* kernel of the %d x %d step)"
                                         % (pmc_summary_path(workload), nval, ninst)) if workload else None,
                      "traffic_frac": (traffic / (step_ms * 1e-3) / HBM_PEAK) if traffic else None,
-                     "kernel": ("epoch step: pz_epoch_pre (bit count) + pz_epoch_fused[_lc] (one pass: classify, "
+                     "kernel": ("epoch step: pz_epoch_pre (bit count) + pz_epoch_fused[_lc][_se] (one pass: classify, "
                                 "crosslink tallies, rewards, next-cycle sum) + pz_epoch_mid (winners); device "
                                 "time of the whole step" if one_pass else
                                 "epoch step (count+winner+compact+reward, device time of the whole step)"),
                      "step_device_ms": step_ms,
-                     "algorithmic_bytes_per_launch": local_units * EPOCH_BYTES_PER_VALIDATOR},
+                     "algorithmic_bytes_per_launch": local_units * bpv},
     }
     del de
     if world == 1 and native and workload and not args.no_epoch_cold:
-        out["cold"] = epoch_cold(args, torch, dev, nval, ninst, shuffled, workload)
+        out["cold"] = epoch_cold(args, torch, dev, nval, ninst, shuffled, workload, bpv=bpv)
     if rank == 0 and world == 1:
         out["parity"] = epoch_parity(inst, dev)
     if world == 1 and baseline:
@@ -270,7 +292,7 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
     return out
 
 
-def epoch_cold(args, torch, dev, nval, ninst, shuffled, workload, nsets=4):
+def epoch_cold(args, torch, dev, nval, ninst, shuffled, workload, nsets=4, bpv=EPOCH_BYTES_PER_VALIDATOR):
     """The same step with the timed steps rotated over ``nsets`` distinct instance sets (each
     ~400 MB; together far above the 256 MiB Infinity Cache), all bound to one stream, so every
     step reads its state from HBM: the epoch against HBM, not against the cache the
@@ -301,13 +323,14 @@ def epoch_cold(args, torch, dev, nval, ninst, shuffled, workload, nsets=4):
     for de in sets:
         de.free()
     units = nval * ninst
-    alg = units * EPOCH_BYTES_PER_VALIDATOR
+    alg = units * bpv
     traffic = pmc_traffic(["pz_epoch_*"], workload + "_cold")
     yard = cold_stream_yardstick(torch, dev, units, nsets, steps)
     return {"what": "%d steps rotated over %d distinct %d x %d instance sets (%.1f GB of validator state), one "
                     "stream" % (steps, nsets, nval, ninst, nsets * units * 24 / 1e9),
             "value": units * steps / wall, "unit": "validator-epochs/s", "step_device_ms": step_ms,
             "frac": alg / (step_ms * 1e-3) / HBM_PEAK,
+            "survey_frac": units * EPOCH_BYTES_PER_VALIDATOR / (step_ms * 1e-3) / HBM_PEAK,
             "traffic": traffic, "traffic_source": pmc_summary_path(workload + "_cold") if traffic else None,
             "traffic_frac": (traffic / (step_ms * 1e-3) / HBM_PEAK) if traffic else None,
             "yardstick": yard}

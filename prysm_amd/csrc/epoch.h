@@ -104,6 +104,10 @@ struct FusedArgs {
   // this step resets winner_next (all 0xFFFFFFFF) for the next one.
   int win_in_wave;
   uint32_t* winner_next;
+  // [B][vstride] {start, end} dynasty of each position, saturated to 32 bits (set only when
+  // every instance's CurrentDynasty is below 2^32 - 1, which makes the saturated bounds classify
+  // exactly): the stream reads 8 B of them per validator instead of 16
+  const uint2* se;
   const uint2* att_win;       // [natt] {shard, record dynasty of that shard} per attestation (an
                               //   upload-time layout: loaded beside the stream, no shard -> record hop)
 };

@@ -994,7 +994,10 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
       v1[j] = g + 1 >= ws && g + 1 < we;
       const uint64_t pp = (v0[j] || v1[j]) ? p : p0;
       qb[j] = *reinterpret_cast<const uint4*>(Bal + pp);
-      if (MODE & 8) {
+      if (MODE & 1024) {  // {start, end} of the pair's two validators, 32-bit saturated: one 16-B load
+        qs[j] = ld16_nt(reinterpret_cast<const uint64_t*>(f.se + inst * f.vstride + pp));
+        qe[j] = make_uint4(0, 0, 0, 0);
+      } else if (MODE & 8) {
         qs[j] = make_uint4(0, 0, 0, 0);
         qe[j] = make_uint4(~0u, ~0u, ~0u, ~0u);
       } else if (MODE & 16) {
@@ -1125,8 +1128,11 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     for (int j = 0; j < 2; ++j) {
       const uint64_t p = p0 + (uint64_t)j * 128 + 2 * lane;
       uint64_t b0 = pack64(qb[j].x, qb[j].y), b1 = pack64(qb[j].z, qb[j].w);
-      const bool a0 = pack64(qs[j].x, qs[j].y) <= d && d < pack64(qe[j].x, qe[j].y);
-      const bool a1 = pack64(qs[j].z, qs[j].w) <= d && d < pack64(qe[j].z, qe[j].w);
+      // (MODE & 1024: d < 2^32 - 1, so the saturated 32-bit bounds classify exactly)
+      const bool a0 = (MODE & 1024) ? ((uint64_t)qs[j].x <= d && d < (uint64_t)qs[j].y)
+                                    : (pack64(qs[j].x, qs[j].y) <= d && d < pack64(qe[j].x, qe[j].y));
+      const bool a1 = (MODE & 1024) ? ((uint64_t)qs[j].z <= d && d < (uint64_t)qs[j].w)
+                                    : (pack64(qs[j].z, qs[j].w) <= d && d < pack64(qe[j].z, qe[j].w));
       nm += (v0[j] && !a0 ? 1 : 0) + (v1[j] && !a1 ? 1 : 0);
       if (applied) {  // every validator active: rank == index, the validator at p is co_index[p]
         // an element outside the piece looks up bit 0 (its co_index may be a row's pad)
@@ -1261,6 +1267,8 @@ __device__ __forceinline__ void one_tail(const EpochArgs& a, const FusedArgs& f,
   }
 PZ_FUSED_KERNEL(pz_epoch_fused_kernel, 0)
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_kernel, 256)  // reward bits from FusedArgs.lastco
+PZ_FUSED_KERNEL(pz_epoch_fused_se_kernel, 1024)  // start/end from FusedArgs.se
+PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_kernel, 1280)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg1_kernel, 1)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg2_kernel, 2)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg3_kernel, 3)
@@ -1281,6 +1289,13 @@ pz_epoch_one_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ boffs
                     const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,
                     const uint32_t* __restrict__ catt_ro) {
   fused_body<512>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
+}
+extern "C" __global__ void __launch_bounds__(64 * kFusedWaves)
+pz_epoch_one_se_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ boffs_ro,
+                       const uint64_t* __restrict__ tdep_ro, const uint4* __restrict__ items_ro,
+                       const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,
+                       const uint32_t* __restrict__ catt_ro) {
+  fused_body<512 + 1024>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
 }
 
 static int g_fused_variant = 0;  // tools/ A/B only
@@ -1429,8 +1444,12 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream
     case 32: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg32_kernel); break;
     case 48: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg48_kernel); break;
     default:
-      if (f.lastco)
+      if (f.lastco && f.se)
+        PZ_LAUNCH_FUSED(pz_epoch_fused_lc_se_kernel);
+      else if (f.lastco)
         PZ_LAUNCH_FUSED(pz_epoch_fused_lc_kernel);
+      else if (f.se)
+        PZ_LAUNCH_FUSED(pz_epoch_fused_se_kernel);
       else
         PZ_LAUNCH_FUSED(pz_epoch_fused_kernel);
   }
@@ -1442,8 +1461,12 @@ bool epoch_one_enabled(const FusedArgs& f) { return f.one && g_fused_variant == 
 
 hipError_t launch_epoch_one(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
   const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
-  hipLaunchKernelGGL(pz_epoch_one_kernel, dim3(1, (uint32_t)groups), dim3(64 * kFusedWaves), 0, s, a, f, a.boffs,
-                     a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt);
+  if (f.se)
+    hipLaunchKernelGGL(pz_epoch_one_se_kernel, dim3(1, (uint32_t)groups), dim3(64 * kFusedWaves), 0, s, a, f, a.boffs,
+                       a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt);
+  else
+    hipLaunchKernelGGL(pz_epoch_one_kernel, dim3(1, (uint32_t)groups), dim3(64 * kFusedWaves), 0, s, a, f, a.boffs,
+                       a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt);
   return hipGetLastError();
 }
 

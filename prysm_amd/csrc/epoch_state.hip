@@ -120,6 +120,23 @@ int upload_perm(Shard& s, uint64_t** p, const uint64_t* host, uint32_t B, uint64
   return e == hipSuccess ? PZ_OK : hip_fail(e, "hipMemcpy H2D (epoch state)");
 }
 
+// The one-pass stream's {start, end} column (FusedArgs.se): rows of np, the positions [lo, hi)
+// of committee order, each bound saturated to 32 bits (pad elements: {0, 0}).
+int upload_se(Shard& s, uint2** p, const uint64_t* start, const uint64_t* end, uint32_t B, uint64_t N,
+              const uint32_t* inv) {
+  int rc = dalloc(s, p, (size_t)B * s.np, false);
+  if (rc || !s.n) return rc;
+  auto sat = [](uint64_t x) { return (uint32_t)std::min<uint64_t>(x, 0xFFFFFFFFull); };
+  std::vector<uint2> tmp((size_t)B * s.np, make_uint2(0, 0));
+  for (uint64_t b = 0; b < B; ++b)
+    for (uint64_t q = 0; q < s.n; ++q) {
+      const uint64_t v = b * N + inv[s.lo + q];
+      tmp[b * s.np + q] = make_uint2(sat(start[v]), sat(end[v]));
+    }
+  hipError_t e = hipMemcpy(*p, tmp.data(), tmp.size() * 8, hipMemcpyHostToDevice);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "hipMemcpy H2D (epoch state)");
+}
+
 uint64_t shard_words(uint64_t N, int world) { return std::max<uint64_t>(1, (N + 64ull * world - 1) / (64ull * world)); }
 
 int step_world1(pz_epoch_state* st) {
@@ -503,6 +520,7 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
     uint64_t* act_mask;
     const uint64_t vbpi = vblocks_per_inst(s.n);
     uint32_t* co_index = nullptr;
+    uint2* se = nullptr;
     if (st->co) {
       const uint32_t* inv = st->co_inv.data();
       if ((rc = upload_perm(s, &bal, h->balance, st->B, st->N, inv)) ||
@@ -514,6 +532,10 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
       std::vector<uint32_t> ci(inv + s.lo, inv + s.hi);
       ci.resize(std::max<uint64_t>(s.np, s.n), s.n ? inv[s.lo] : 0);
       if ((rc = upload(s, &co_index, ci.data(), ci.size()))) break;
+      // the one-pass stream's 8-B {start, end} when every CurrentDynasty is below 2^32 - 1
+      bool small_d = st->fused && !std::getenv("PZ_EPOCH_SE64");  // (PZ_EPOCH_SE64: A/B knob)
+      for (uint64_t b = 0; b < st->B && small_d; ++b) small_d = h->dynasty[b] < 0xFFFFFFFFull;
+      if (small_d && (rc = upload_se(s, &se, h->start, h->end, st->B, st->N, inv))) break;
     } else if ((rc = upload_range(s, &bal, h->balance, st->B, st->N)) ||
                (rc = upload_range(s, &start, h->start, st->B, st->N)) ||
                (rc = upload_range(s, &end, h->end, st->B, st->N))) {
@@ -642,6 +664,7 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
         q.f.rank0 = s.grank == 0 ? 1 : 0;
         q.f.own_only = st->world > 1 ? 1 : 0;
         q.f.vstride = s.np;
+        q.f.se = se ? se + i0 * s.np : nullptr;
         if (!fused_ok(a)) rc = fail(PZ_EINVAL, "one-pass epoch: validator arrays not on the 16-B path");
         // the reward bits in position order (gathered by `pre` through LDS) when every
         // instance's last bitfield fits the gathering block's stage

@@ -135,6 +135,18 @@ def test_native_epoch_single_launch_matches_three_launches():
         np.testing.assert_array_equal(x, y)
 
 
+@pytest.mark.parametrize("B", [1, 3])
+def test_native_epoch_one_pass_dynasty_past_32_bits(B):
+    """A CurrentDynasty of 2^32 - 1 or more: the state keeps the 64-bit {start, end} stream (the
+    packed 32-bit column classifies exactly only below it); same results as the oracle, on the
+    single launch (B = 1) and the pre + fused + mid step."""
+    inst = _inst(4096, B, False)
+    inst["dynasty"] = np.full(B, (1 << 32) + 3, dtype=np.uint64)
+    ne = NativeEpoch(inst, device=0)
+    assert ne.one_pass
+    _check(ne, inst, steps=2)
+
+
 @pytest.mark.parametrize("density", [0.5, 0.75])
 def test_native_epoch_one_pass_threshold(density):
     """Half the bits set: GetAttestersTotalDeposit stays under 2/3 of TotalDeposits, so no
