@@ -104,11 +104,14 @@ struct FusedArgs {
   // this step resets winner_next (all 0xFFFFFFFF) for the next one.
   int win_in_wave;
   uint32_t* winner_next;
+  // the multi-instance step (pre + fused), one rank, every attested committee one piece: the
+  // fused waves form the winners the same way (pre resets them), and mid is not launched
+  int win_fused;
   // [B][vstride] {start, end} dynasty of each position, saturated to 32 bits (set only when
   // every instance's CurrentDynasty is below 2^32 - 1, which makes the saturated bounds classify
   // exactly): the stream reads 8 B of them per validator instead of 16
   const uint2* se;
-  const uint2* att_win;       // [natt] {shard, record dynasty of that shard} per attestation (an
+  const uint2* att_win;       // [B][natt] {shard, record dynasty of that shard} per attestation (an
                               //   upload-time layout: loaded beside the stream, no shard -> record hop)
 };
 // The single-launch step's limits: every block counts the instance's bitfields itself and the

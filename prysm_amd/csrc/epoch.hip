@@ -901,11 +901,14 @@ __device__ __forceinline__ void one_tail(const EpochArgs& a, const FusedArgs& f,
 // next-step tallies zeroed.
 // w = f.att_win[g]: {shard (< nrec: the host takes the one-launch step only then), its record's
 // dynasty}.
-__device__ __forceinline__ void one_win(const EpochArgs& a, const FusedArgs& f, uint32_t g, uint64_t v, uint64_t t,
-                                        uint2 w) {
-  if (3ull * v >= 2ull * t && a.dynasty[0] > (uint64_t)w.y) atomicMin(&a.winner[w.x], g);
-  f.vote_next[g] = 0;
-  f.total_next[g] = 0;
+template <bool ONE>
+__device__ __forceinline__ void one_win(const EpochArgs& a, const FusedArgs& f, uint64_t inst, uint32_t g, uint64_t v,
+                                        uint64_t t, uint2 w) {
+  if (3ull * v >= 2ull * t && a.dynasty[inst] > (uint64_t)w.y) atomicMin(&a.winner[inst * a.nrec + w.x], g);
+  if (ONE) {  // (the multi-instance step's pre zeroes the tallies)
+    f.vote_next[g] = 0;
+    f.total_next[g] = 0;
+  }
 }
 
 template <int MODE>
@@ -977,7 +980,8 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     }
     // (one launch, winners in the waves: the single attestation's shard and record dynasty,
     // loaded with the stream below rather than after the tallies)
-    const uint2 win1 = (ONE && f.win_in_wave && ci.ga < kNoAtt) ? f.att_win[ci.ga] : make_uint2(0, 0);
+    const bool wiw = ONE ? f.win_in_wave != 0 : f.win_fused != 0;
+    const uint2 win1 = (wiw && ci.ga < kNoAtt) ? f.att_win[inst * a.natt + ci.ga] : make_uint2(0, 0);
     const uint64_t p0 = (ws - a.val_offset) & ~1ull;  // local and even: the 16-B pair of ws
     uint64_t* Bal = a.balance + inst * f.vstride;
     const uint64_t* S = a.start + inst * f.vstride;
@@ -1096,7 +1100,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
         }
         vs = wave_sum(v);
         g1 = ci.ga;
-        if (ONE && f.win_in_wave && lane == 0) one_win(a, f, ci.ga, vs, ts, win1);
+        if (wiw && lane == 0) one_win<ONE>(a, f, inst, ci.ga, vs, ts, win1);
       } else {  // several attestations of this committee: direct atomics per attestation
         const uint32_t* co = catt_offs_ro + inst * (f.ncomm + 1);
         for (uint32_t k = co[it.z]; k < co[it.z + 1]; ++k) {
@@ -1112,7 +1116,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
             if (v1[j] && q + 1 < nbits && bit_at(bf, q + 1)) v += pack64(qb[j].z, qb[j].w);
           }
           v = wave_sum(v);
-          if (ONE && f.win_in_wave && lane == 0) one_win(a, f, (uint32_t)ga, v, ts, f.att_win[ga]);
+          if (wiw && lane == 0) one_win<ONE>(a, f, inst, (uint32_t)ga, v, ts, f.att_win[inst * a.natt + ga]);
           if (lane < 2) {  // one instruction: lane 0 the total, lane 1 the vote
             uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + ga;
             const uint64_t x = lane ? v : ts;

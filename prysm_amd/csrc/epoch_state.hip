@@ -152,7 +152,7 @@ int step_world1(pz_epoch_state* st) {
       if (st->fused) {
         hipError_t e = launch_epoch_pre(a, s.part[p].f, s.s);
         if (e == hipSuccess) e = launch_epoch_fused(a, s.part[p].f, s.s);
-        if (e == hipSuccess) e = launch_epoch_mid(a, st->nrec != 0, false, s.s);
+        if (e == hipSuccess && !s.part[p].f.win_fused) e = launch_epoch_mid(a, st->nrec != 0, false, s.s);
         if (e != hipSuccess) return hip_fail(e, "epoch step (one pass)");
         continue;
       }
@@ -675,6 +675,27 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
           q.f.lcw = (s.np + 31) / 32;
           rc = dalloc(s, &q.f.lastco, (size_t)Bp * q.f.lcw);
         }
+        // winners formed in the fused waves when every attested committee of every instance
+        // is one piece (its complete tallies in one wave), on one rank: per attestation its
+        // {shard, that record's dynasty} (the records are inputs of the state)
+        bool win_waves = !rc && st->world == 1 && st->natt && st->nrec > 0;
+        if (win_waves) {
+          std::vector<uint32_t> pieces(st->ncomm, 0);
+          for (const uint4& it : items) ++pieces[it.z];
+          std::vector<uint2> aw((size_t)Bp * st->natt);
+          for (uint64_t b = 0; b < Bp && win_waves; ++b)
+            for (uint64_t g = 0; g < st->natt && win_waves; ++g) {
+              const uint64_t ga = (i0 + b) * st->natt + g;
+              const uint32_t sh = h->att_shard[ga];
+              win_waves = pieces[h->att_comm[ga]] == 1 && sh < st->nrec;
+              const uint64_t rd = win_waves ? h->rec_dynasty[(i0 + b) * st->nrec + sh] : 0;
+              if (rd >> 32) win_waves = false;  // (a 32-bit record dynasty)
+              aw[b * st->natt + g] = make_uint2(sh, (uint32_t)rd);
+            }
+          uint2* d_aw = nullptr;
+          if (win_waves) rc = upload(s, &d_aw, aw.data(), aw.size());
+          q.f.att_win = d_aw;
+        }
         // one instance on one rank: the single-launch step (latency path), within its limits
         if (!rc && Bp == 1 && st->world == 1 && st->natt && st->natt <= kOneMaxAtt && st->nrec <= kOneMaxRec &&
             max_inst_bytes <= kOneMaxBitBytes) {
@@ -688,25 +709,9 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
           rc = dalloc(s, &q.f.ticket, 1);
           if (!rc) rc = upload(s, &d_cs, cs.data(), cs.size());
           q.f.att_csize = d_cs;
-          // winners formed in the waves when every attested committee is one piece (its
-          // complete tallies in one wave); else the last block forms them (one_tail)
-          std::vector<uint32_t> pieces(st->ncomm, 0);
-          for (const uint4& it : items) ++pieces[it.z];
-          bool one_piece = st->nrec > 0;
-          for (uint64_t g = 0; g < st->natt && one_piece; ++g) one_piece = pieces[h->att_comm[i0 * st->natt + g]] == 1;
-          if (!rc && one_piece) {
-            // per attestation {shard, its record's dynasty} (the records are inputs of the state)
-            std::vector<uint2> aw(st->natt);
-            for (uint64_t g = 0; g < st->natt; ++g) {
-              const uint32_t sh = h->att_shard[i0 * st->natt + g];
-              aw[g] = make_uint2(sh, (uint32_t)h->rec_dynasty[i0 * st->nrec + sh]);
-              if (h->rec_dynasty[i0 * st->nrec + sh] >> 32) one_piece = false;  // (a 32-bit dynasty)
-            }
-            uint2* d_aw = nullptr;
-            if (one_piece) rc = upload(s, &d_aw, aw.data(), aw.size());
-            q.f.att_win = d_aw;
-          }
-          if (!rc && one_piece) {
+          // else the last block forms the winners (one_tail); in the waves they ping-pong: a step
+          // resets the next one's buffer
+          if (!rc && win_waves) {
             uint32_t* w2 = nullptr;
             rc = dalloc(s, &w2, st->nrec);
             hipError_t e2 = hipSuccess;
@@ -716,6 +721,12 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
             q.f.win_in_wave = 1;
             q.f.winner_next = w2;
           }
+        } else if (!rc && win_waves && std::getenv("PZ_EPOCH_WIN_FUSED")) {
+          // (A/B knob: the same in the multi-instance fused waves, pre resetting the winners and
+          // no mid launch, measured 0.2-2 us per step SLOWER than the mid launch it removes at
+          // 65,536 x 256 and 1M x 16: the waves' extra loads and atomics cost more;
+          // profiles/r03/epoch_ab_r3af.txt)
+          q.f.win_fused = 1;
         }
       }
       q.cur = 1;  // flip() below binds red[0] as the first step's buffer
