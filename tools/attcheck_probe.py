@@ -19,16 +19,8 @@ import bench  # noqa: E402
 def main():
     natt = 1 << 22
     cols, tab = bench.attcheck_columns(natt, seed=11)
-    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v.view(np.int32) if v.dtype == np.uint32
-                             else v).cuda() for k, v in list(cols.items()) + list(tab.items())}
-    st = torch.empty(natt, dtype=torch.int32, device="cuda")
-    cm = torch.empty(natt, dtype=torch.int32, device="cuda")
-    ps = torch.empty(natt, dtype=torch.int64, device="cuda")
-    b = _lib.AttCheckBatch(natt, t["slot"].data_ptr(), t["justified_slot"].data_ptr(), t["shard_id"].data_ptr(),
-                           t["n_oblique"].data_ptr(), t["bits"].data_ptr(), t["boffs"].data_ptr(),
-                           t["block_slot"].data_ptr(), 0, 0, 128, 256, t["arr_offs"].data_ptr(),
-                           t["arr_shard"].data_ptr(), t["arr_comm"].data_ptr(), t["coffs"].data_ptr(),
-                           st.data_ptr(), cm.data_ptr(), ps.data_ptr())
+    b, t = bench.attcheck_batch(torch, torch.device("cuda", 0), cols, tab, natt, last_byte=True)  # the bench's batch
+    st, cm, ps = t["status"], t["committee"], t["pstart"]
     sh = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for _ in range(200):
         _lib.lib.call("pz_dev_check_attestations", ctypes.byref(b), sh)
@@ -47,8 +39,8 @@ def main():
     print("attcheck: %d attestations  %.4f ms  %.1f G/s  result digest %d" % (natt, ms, natt / ms / 1e6, digest),
           flush=True)
     dll = _lib.lib.dll
-    if hasattr(dll, "pz_debug_set_attcheck_variant"):  # same-process A/B (1: default-policy column loads)
-        for v in (0, 1, 0, 1, 0):
+    if hasattr(dll, "pz_debug_set_attcheck_variant"):  # same-process A/B (1: default-policy loads, 2: nt stores)
+        for v in [int(x) for x in os.environ.get("VARIANTS", "0,2,0,2,0,2").split(",")]:
             dll.pz_debug_set_attcheck_variant(v)
             ms = timed()
             d = int(st.sum().item()) * 31 + int(cm.sum().item()) * 7 + int(ps.sum().item())
