@@ -107,6 +107,10 @@ struct FusedArgs {
   // the multi-instance step (pre + fused), one rank, every attested committee one piece: the
   // fused waves form the winners the same way (pre resets them), and mid is not launched
   int win_fused;
+  // the single launch over B instances (pz_epoch_multi_kernel): each block counts its
+  // instance's bitfields (within kMultiMaxBitBytes, at most kMultiMaxAtt attestations); needs
+  // win_in_wave (winners ping-pong per instance) and att_csize [B][natt]
+  int multi;
   // [B][vstride] {start, end} dynasty of each position, saturated to 32 bits (set only when
   // every instance's CurrentDynasty is below 2^32 - 1, which makes the saturated bounds classify
   // exactly): the stream reads 8 B of them per validator instead of 16
@@ -119,6 +123,10 @@ struct FusedArgs {
 constexpr uint64_t kOneMaxBitBytes = 32768;
 constexpr uint32_t kOneMaxAtt = 2048;
 constexpr uint32_t kOneMaxRec = 4096;
+constexpr uint64_t kMultiMaxBitBytes = 16384;
+constexpr uint32_t kMultiMaxAtt = 512;
+bool epoch_multi_enabled(const FusedArgs& f);
+hipError_t launch_epoch_multi(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_epoch_fwin(const EpochArgs& a, const FusedArgs& f, hipStream_t s);

@@ -901,13 +901,13 @@ __device__ __forceinline__ void one_tail(const EpochArgs& a, const FusedArgs& f,
 // next-step tallies zeroed.
 // w = f.att_win[g]: {shard (< nrec: the host takes the one-launch step only then), its record's
 // dynasty}.
-template <bool ONE>
+template <bool PRO>
 __device__ __forceinline__ void one_win(const EpochArgs& a, const FusedArgs& f, uint64_t inst, uint32_t g, uint64_t v,
                                         uint64_t t, uint2 w) {
   if (3ull * v >= 2ull * t && a.dynasty[inst] > (uint64_t)w.y) atomicMin(&a.winner[inst * a.nrec + w.x], g);
-  if (ONE) {  // (the multi-instance step's pre zeroes the tallies)
-    f.vote_next[g] = 0;
-    f.total_next[g] = 0;
+  if (PRO) {  // (with a pre launch, pre zeroes the tallies)
+    f.vote_next[inst * a.natt + g] = 0;
+    f.total_next[inst * a.natt + g] = 0;
   }
 }
 
@@ -922,13 +922,16 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
   __shared__ uint64_t xt[kFusedWaves], xv[kFusedWaves], xs[kFusedWaves], xn[kFusedWaves];
   __shared__ uint32_t xg[kFusedWaves];
   constexpr bool ONE = (MODE & 512) != 0;  // single-launch step (launch_epoch_one)
+  // single launch over B instances (launch_epoch_multi): ONE's per-block prologue, inst = blockIdx.x
+  constexpr bool MULTI = (MODE & 2048) != 0;
+  constexpr bool PRO = ONE || MULTI;  // each block counts its instance's bitfields itself
   const uint64_t inst = (MODE & 32) ? blockIdx.y : blockIdx.x;
   const uint64_t grp = (MODE & 32) ? blockIdx.x : blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint64_t item = grp * kFusedWaves + wave;
   uint64_t pop = 0, ferr = 0;
-  if (!ONE) {
+  if (!PRO) {
     pop = pre_ro[inst * kPre];
     ferr = pre_ro[inst * kPre + 1];
   }
@@ -940,16 +943,19 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
   bool applied = thr && !skip;
   // ONE: this block's own bit count (GetAttestersTotalDeposit, validator.go:93-102) and
   // bitfield-length checks (core.go:538-541) over the whole instance, issued before the stream
-  constexpr int kOneLoads = ONE ? (int)((kOneMaxBitBytes + 16) / (16 * 64 * kFusedWaves)) + 1 : 1;
-  constexpr int kOneAtts = ONE ? (int)(kOneMaxAtt / (64 * kFusedWaves)) : 1;
+  constexpr uint64_t kProBits = MULTI ? kMultiMaxBitBytes : kOneMaxBitBytes;
+  constexpr uint32_t kProAtt = MULTI ? kMultiMaxAtt : kOneMaxAtt;
+  constexpr int kOneLoads = PRO ? (int)((kProBits + 16) / (16 * 64 * kFusedWaves)) + 1 : 1;
+  constexpr int kOneAtts = PRO ? (int)((kProAtt + 64 * kFusedWaves - 1) / (64 * kFusedWaves)) : 1;
   uint4 pq[kOneLoads];
   uint32_t ocs[kOneAtts];
   uint64_t ob0[kOneAtts], ob1[kOneAtts];
   // ONE: the instance's bitfield bytes [pbase, pend), staged in LDS by the loads above; the
   // reward bits are then looked up there (the last bitfield is the region's tail)
-  __shared__ uint4 lbits[ONE ? kOneLoads * 64 * kFusedWaves : 1];
-  const uint64_t pbeg = ONE ? boffs_ro[0] : 0, pend = ONE ? boffs_ro[a.natt] : 0, pbase = pbeg & ~15ull;
-  if (ONE) {
+  __shared__ uint4 lbits[PRO ? kOneLoads * 64 * kFusedWaves : 1];
+  const uint64_t pbeg = PRO ? boffs_ro[inst * a.natt] : 0, pend = PRO ? boffs_ro[inst * a.natt + a.natt] : 0,
+                 pbase = pbeg & ~15ull;
+  if (PRO) {
 #pragma unroll
     for (int k = 0; k < kOneLoads; ++k) {  // branch-free: the bitfield buffer is padded by 16 B
       const uint64_t u = pbase + 16ull * ((uint64_t)k * 64 * kFusedWaves + tid);
@@ -957,7 +963,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     }
 #pragma unroll
     for (int k = 0; k < kOneAtts; ++k) {
-      const uint64_t g = (uint64_t)k * 64 * kFusedWaves + tid, gc = g < a.natt ? g : 0;
+      const uint64_t g = (uint64_t)k * 64 * kFusedWaves + tid, gc = inst * a.natt + (g < a.natt ? g : 0);
       ocs[k] = f.att_csize[gc];
       ob0[k] = boffs_ro[gc];
       ob1[k] = boffs_ro[gc + 1];
@@ -980,7 +986,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     }
     // (one launch, winners in the waves: the single attestation's shard and record dynasty,
     // loaded with the stream below rather than after the tallies)
-    const bool wiw = ONE ? f.win_in_wave != 0 : f.win_fused != 0;
+    const bool wiw = PRO ? f.win_in_wave != 0 : f.win_fused != 0;
     const uint2 win1 = (wiw && ci.ga < kNoAtt) ? f.att_win[inst * a.natt + ci.ga] : make_uint2(0, 0);
     const uint64_t p0 = (ws - a.val_offset) & ~1ull;  // local and even: the 16-B pair of ws
     uint64_t* Bal = a.balance + inst * f.vstride;
@@ -1021,13 +1027,13 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
       // branch-free, clamped: issued with the stream loads (bits past the bitfield are masked
       // below; the pre pass has raised that panic)
       by0[j] = by1[j] = 0;
-      if (!ONE && !(MODE & 1) && ci.ga < kNoAtt && ci.nbits) {  // (ONE: from LDS, below)
+      if (!PRO && !(MODE & 1) && ci.ga < kNoAtt && ci.nbits) {  // (PRO: from LDS, below)
         const uint64_t q = g - cb, last = ci.nbits - 1;
         by0[j] = a.bits[ci.boff + ((q < last ? q : last) >> 3)];
         by1[j] = a.bits[ci.boff + ((q + 1 < last ? q + 1 : last) >> 3)];
       }
     }
-    if (ONE) {  // the block's bit count and length checks -> threshold (no other block involved)
+    if (PRO) {  // the block's bit count and length checks -> threshold (no other block involved)
       __shared__ uint64_t xp[kFusedWaves], xe[kFusedWaves];
       uint64_t c = 0, e = 0;
 #pragma unroll
@@ -1100,7 +1106,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
         }
         vs = wave_sum(v);
         g1 = ci.ga;
-        if (wiw && lane == 0) one_win<ONE>(a, f, inst, ci.ga, vs, ts, win1);
+        if (wiw && lane == 0) one_win<PRO>(a, f, inst, ci.ga, vs, ts, win1);
       } else {  // several attestations of this committee: direct atomics per attestation
         const uint32_t* co = catt_offs_ro + inst * (f.ncomm + 1);
         for (uint32_t k = co[it.z]; k < co[it.z + 1]; ++k) {
@@ -1116,7 +1122,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
             if (v1[j] && q + 1 < nbits && bit_at(bf, q + 1)) v += pack64(qb[j].z, qb[j].w);
           }
           v = wave_sum(v);
-          if (wiw && lane == 0) one_win<ONE>(a, f, inst, (uint32_t)ga, v, ts, f.att_win[inst * a.natt + ga]);
+          if (wiw && lane == 0) one_win<PRO>(a, f, inst, (uint32_t)ga, v, ts, f.att_win[inst * a.natt + ga]);
           if (lane < 2) {  // one instruction: lane 0 the total, lane 1 the vote
             uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + ga;
             const uint64_t x = lane ? v : ts;
@@ -1127,7 +1133,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     }
     // classify (validator.go:45-53), reward (incentives.go:22-27), store, sum (core.go:459-464)
     const uint64_t d = a.dynasty[inst];
-    const uint8_t* lastbf = ONE ? reinterpret_cast<const uint8_t*>(lbits) + (lb - pbase) : a.bits + lb;
+    const uint8_t* lastbf = PRO ? reinterpret_cast<const uint8_t*>(lbits) + (lb - pbase) : a.bits + lb;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const uint64_t p = p0 + (uint64_t)j * 128 + 2 * lane;
@@ -1171,11 +1177,11 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     xn[wave] = nm;
   }
   __syncthreads();
-  if (!ONE && wave != 0) return;
+  if (!PRO && wave != 0) return;
   if (wave == 0) fused_block_end(a, f, xg, xt, xv, xs, xn, inst, grp, lane, skip, applied, pop, ferr, rwd_err);
-  if (ONE && f.win_in_wave) {  // the next step's winners start empty (this step's are in a.winner)
+  if (PRO && f.win_in_wave) {  // the next step's winners start empty (this step's are in a.winner)
     for (uint32_t r = (uint32_t)(grp * blockDim.x) + tid; r < a.nrec; r += gridDim.y * blockDim.x)
-      f.winner_next[r] = 0xFFFFFFFFu;
+      f.winner_next[inst * a.nrec + r] = 0xFFFFFFFFu;
   } else if (ONE) {
     one_tail(a, f, tid);
   }
@@ -1300,6 +1306,23 @@ pz_epoch_one_se_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ bo
                        const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,
                        const uint32_t* __restrict__ catt_ro) {
   fused_body<512 + 1024>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
+}
+
+// The single launch over B instances: grid (B, piece groups), every attested committee one piece
+// (winners in the waves), each instance's bitfields within kMultiMaxBitBytes.
+extern "C" __global__ void __launch_bounds__(64 * kFusedWaves) __attribute__((amdgpu_waves_per_eu(8, 8)))
+pz_epoch_multi_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ boffs_ro,
+                      const uint64_t* __restrict__ tdep_ro, const uint4* __restrict__ items_ro,
+                      const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,
+                      const uint32_t* __restrict__ catt_ro) {
+  fused_body<2048 + 1024>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
+}
+extern "C" __global__ void __launch_bounds__(64 * kFusedWaves) __attribute__((amdgpu_waves_per_eu(8, 8)))
+pz_epoch_multi_se64_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ boffs_ro,
+                           const uint64_t* __restrict__ tdep_ro, const uint4* __restrict__ items_ro,
+                           const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,
+                           const uint32_t* __restrict__ catt_ro) {
+  fused_body<2048>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
 }
 
 static int g_fused_variant = 0;  // tools/ A/B only
@@ -1471,6 +1494,20 @@ hipError_t launch_epoch_one(const EpochArgs& a, const FusedArgs& f, hipStream_t 
   else
     hipLaunchKernelGGL(pz_epoch_one_kernel, dim3(1, (uint32_t)groups), dim3(64 * kFusedWaves), 0, s, a, f, a.boffs,
                        a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt);
+  return hipGetLastError();
+}
+
+bool epoch_multi_enabled(const FusedArgs& f) { return f.multi && g_fused_variant == 0; }
+
+hipError_t launch_epoch_multi(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
+  const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
+  const dim3 grid(a.ninst, (uint32_t)groups), block(64 * kFusedWaves);
+  if (f.se)
+    hipLaunchKernelGGL(pz_epoch_multi_kernel, grid, block, 0, s, a, f, a.boffs, a.total_deposit, f.items, f.cinfo,
+                       f.catt_offs, f.catt);
+  else
+    hipLaunchKernelGGL(pz_epoch_multi_se64_kernel, grid, block, 0, s, a, f, a.boffs, a.total_deposit, f.items,
+                       f.cinfo, f.catt_offs, f.catt);
   return hipGetLastError();
 }
 

@@ -149,6 +149,11 @@ int step_world1(pz_epoch_state* st) {
         if (e != hipSuccess) return hip_fail(e, "epoch step (single launch)");
         continue;
       }
+      if (st->fused && epoch_multi_enabled(s.part[p].f)) {  // B instances, one launch
+        hipError_t e = launch_epoch_multi(a, s.part[p].f, s.s);
+        if (e != hipSuccess) return hip_fail(e, "epoch step (multi-instance launch)");
+        continue;
+      }
       if (st->fused) {
         hipError_t e = launch_epoch_pre(a, s.part[p].f, s.s);
         if (e == hipSuccess) e = launch_epoch_fused(a, s.part[p].f, s.s);
@@ -721,6 +726,31 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
             q.f.win_in_wave = 1;
             q.f.winner_next = w2;
           }
+        } else if (!rc && win_waves && Bp > 1 && max_inst_bytes <= kMultiMaxBitBytes && st->natt <= kMultiMaxAtt &&
+                   std::getenv("PZ_EPOCH_MULTI")) {
+          // (A/B knob) B instances in ONE launch (pz_epoch_multi_kernel): each block counts its
+          // instance's bitfields itself, the waves form the winners (ping-pong per instance); no
+          // pre, no mid.  Measured level with pre + fused + mid at 65,536 x 256 (99.0-100.0 vs
+          // 99.1-99.5 us, profiles/r03/epoch_ab_multi_r3ai.txt): the per-block prologue and the
+          // scratch it spills at 8 waves per SIMD cost what the two launches cost
+          q.f.multi = 1;
+          std::vector<uint32_t> cs((size_t)Bp * st->natt);
+          for (uint64_t b = 0; b < Bp; ++b)
+            for (uint64_t g = 0; g < st->natt; ++g) {
+              const uint32_t c = h->att_comm[(i0 + b) * st->natt + g];
+              cs[b * st->natt + g] = (uint32_t)(h->coffs[c + 1] - h->coffs[c]);
+            }
+          uint32_t* d_cs = nullptr;
+          rc = upload(s, &d_cs, cs.data(), cs.size());
+          q.f.att_csize = d_cs;
+          uint32_t* w2 = nullptr;
+          if (!rc) rc = dalloc(s, &w2, (size_t)Bp * st->nrec);
+          hipError_t e2 = hipSuccess;
+          if (!rc) e2 = hipMemsetAsync(w2, 0xFF, (size_t)Bp * st->nrec * 4, s.s);
+          if (!rc && e2 == hipSuccess) e2 = hipMemsetAsync(a.winner, 0xFF, (size_t)Bp * st->nrec * 4, s.s);
+          if (!rc && e2 != hipSuccess) rc = hip_fail(e2, "hipMemsetAsync (winners)");
+          q.f.win_in_wave = 1;
+          q.f.winner_next = w2;
         } else if (!rc && win_waves && std::getenv("PZ_EPOCH_WIN_FUSED")) {
           // (A/B knob: the same in the multi-instance fused waves, pre resetting the winners and
           // no mid launch, measured 0.2-2 us per step SLOWER than the mid launch it removes at

@@ -135,6 +135,19 @@ def test_native_epoch_single_launch_matches_three_launches():
         np.testing.assert_array_equal(x, y)
 
 
+@pytest.mark.parametrize("knob", ["PZ_EPOCH_MULTI", "PZ_EPOCH_WIN_FUSED"])
+@pytest.mark.parametrize("n,B,density", [(65536, 3, 0.75), (4097, 5, 0.75), (8192, 4, 0.5)])
+def test_native_epoch_one_pass_ab_knobs(knob, n, B, density, monkeypatch):
+    """The one-pass step's A/B forms read at state creation: one launch over the
+    B instances (PZ_EPOCH_MULTI) and winners in the fused waves without the mid launch
+    (PZ_EPOCH_WIN_FUSED), bit-exact against the oracle over two steps."""
+    monkeypatch.setenv(knob, "1")
+    inst = _inst(n, B, False, density=density)
+    ne = NativeEpoch(inst, device=0)
+    assert ne.one_pass
+    _check(ne, inst, steps=2)
+
+
 @pytest.mark.parametrize("B", [1, 3])
 def test_native_epoch_one_pass_dynasty_past_32_bits(B):
     """A CurrentDynasty of 2^32 - 1 or more: the state keeps the 64-bit {start, end} stream (the

@@ -1,8 +1,8 @@
 """Same-process A/B of the one-pass epoch step's build-time choices (tools/ only):
 python tools/epoch_ab.py [ROUNDS]
-Each arm sets environment knobs read when a pz_epoch_state is created (PZ_EPOCH_WIN_FUSED: the
-winners formed in the fused waves instead of by the mid launch; PZ_EPOCH_SE64: the 64-bit
-start/end stream), builds 65,536 x 256 and 1M x 16 states and prints the device ms per step (one event
+Each arm sets environment knobs read when a pz_epoch_state is created (PZ_EPOCH_MULTI: one launch
+over the B instances instead of pre + fused + mid; PZ_EPOCH_WIN_FUSED: winners in the fused waves,
+no mid; PZ_EPOCH_SE64: the 64-bit start/end stream), builds 65,536 x 256 and 1M x 16 states and prints the device ms per step (one event
 pair around 48 back-to-back steps, as bench.py's epoch leg)."""
 import os
 import sys
@@ -14,7 +14,7 @@ import torch  # noqa: E402
 from prysm_amd import casper, synth  # noqa: E402
 from prysm_amd.native import NativeEpoch  # noqa: E402
 
-ARMS = [("product", {}), ("win_fused", {"PZ_EPOCH_WIN_FUSED": "1"}), ("se64", {"PZ_EPOCH_SE64": "1"})]
+ARMS = [("product", {}), ("multi", {"PZ_EPOCH_MULTI": "1"}), ("se64", {"PZ_EPOCH_SE64": "1"})]
 
 
 def time_state(inst, dev, steps=48):
