@@ -1887,8 +1887,13 @@ static uint64_t parse_parallel(const uint8_t* data, const uint64_t* offs, uint64
   }
   std::vector<uint64_t> bad(T, UINT64_MAX);
   std::vector<std::thread> th;
-  for (size_t t = 1; t < T; ++t)
-    th.emplace_back([&, t] { bad[t] = parse_range(data, offs, cut[t], cut[t + 1], ar, blocks, t); });
+  size_t started = 1;
+  try {
+    for (size_t t = 1; t < T; ++t, ++started)
+      th.emplace_back([&, t] { bad[t] = parse_range(data, offs, cut[t], cut[t + 1], ar, blocks, t); });
+  } catch (const std::exception&) {  // no thread to be had: the rest on this one
+  }
+  for (size_t t = started; t < T; ++t) bad[t] = parse_range(data, offs, cut[t], cut[t + 1], ar, blocks, t);
   bad[0] = parse_range(data, offs, cut[0], cut[1], ar, blocks, 0);
   for (auto& x : th) x.join();
   for (size_t t = 0; t < T; ++t)

@@ -4,7 +4,10 @@
 // instruction pointer and up to kDepth - 1 of its callers (the unwinder steps through the
 // signal frame; backtrace() is called once at start so that it is loaded before any signal).
 // pz_debug_sample_stop maps each PC to (object file, offset in it) with dladdr, for
-// llvm-symbolizer.  Not for product use: one sampler per process.
+// llvm-symbolizer.  Not for product use: one sampler per process; backtrace() in a signal
+// handler is not async-signal-safe in general (it is warmed up at start, and glibc's loader
+// lock it may take is recursive, so a sample that lands inside the walk's own unwinding --
+// a rejected attestation's throw -- re-enters it on the same thread).
 #include <dlfcn.h>
 #include <execinfo.h>
 #include <signal.h>
