@@ -975,7 +975,11 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
   const bool have = item < f.nitems;
   {
     // {first position, count, committee, committee start}
-    const uint4 it = have ? items_ro[item] : make_uint4((uint32_t)a.val_offset, 0, 0, (uint32_t)a.val_offset);
+    // (ablation 64: the piece computed from its index -- 256 positions, wrong tallies -- so the
+    // stream loads do not wait for the item load)
+    const uint4 it = (MODE & 64) ? make_uint4((uint32_t)(a.val_offset + ((item * 256) % (a.nval & ~255ull ? a.nval & ~255ull : 256))),
+                                              have ? 256u : 0u, 0, (uint32_t)a.val_offset)
+                     : have ? items_ro[item] : make_uint4((uint32_t)a.val_offset, 0, 0, (uint32_t)a.val_offset);
     const uint64_t ws = it.x, we = (uint64_t)it.x + it.y, cb = it.w;
     FusedCommittee ci;  // loaded beside the item: no dependent hop before the stream loads
     {
@@ -1289,6 +1293,7 @@ PZ_FUSED_KERNEL(pz_epoch_fused_dbg15_kernel, 15)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg16_kernel, 16)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg32_kernel, 32)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg48_kernel, 48)
+PZ_FUSED_KERNEL(pz_epoch_fused_dbg1088_kernel, 1088)  // se, piece from its index (no item -> stream hop)
 #undef PZ_FUSED_KERNEL
 
 // The single-launch step (one instance): no occupancy target (a few dozen blocks), so the
@@ -1470,6 +1475,8 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream
     case 16: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg16_kernel); break;
     case 32: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg32_kernel); break;
     case 48: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg48_kernel); break;
+    case 1024: PZ_LAUNCH_FUSED(pz_epoch_fused_se_kernel); break;  // (ablation baseline: no lastco)
+    case 1088: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg1088_kernel); break;
     default:
       if (f.lastco && f.se)
         PZ_LAUNCH_FUSED(pz_epoch_fused_lc_se_kernel);

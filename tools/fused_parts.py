@@ -2,7 +2,8 @@
 pz_epoch_state step per variant, interleaved rounds, HIP events on the state's stream.
 Variant bits (epoch.hip fused_body): 1 no tallies, 2 no last-bitfield lookups, 4 no store,
 8 no start/end loads, 16 default-policy
-start/end loads, 32 instance-major grid.  Results are wrong for variants != 0 (timing only)."""
+start/end loads, 32 instance-major grid, 64 the piece from its index (no item -> stream hop), 1024
+the packed start/end column (1024 alone: the product's kernel without the reward-bit gather).  Results are wrong for variants != 0 (timing only)."""
 import json
 import os
 import sys
@@ -15,7 +16,7 @@ import torch  # noqa: E402
 from prysm_amd import _lib, casper, synth  # noqa: E402
 from prysm_amd.native import NativeEpoch  # noqa: E402
 
-VARIANTS = [0, 128, 1, 2, 4, 8, 15, 16, 32]
+VARIANTS = [int(x) for x in os.environ.get("VARIANTS", "0,128,1,2,4,8,15,16,32").split(",")]
 
 
 def run(nval, ninst, rounds=5, reps=10):
