@@ -826,7 +826,7 @@ def replay_sharded_leg(args, torch, dist, dev, rank, world, comm):
 
 
 PROF_PHASES = ("parse", "digest_batch", "checks", "vote_queue", "vote_flush", "state_recalc", "msg_digests", "walk",
-               "process", "count_atts", "flush_arena_wait")
+               "process", "count_atts", "flush_arena_wait", "msg_send", "msg_hash_log", "msg_wait")
 
 
 def chain_phases_ms(ch):

@@ -11,15 +11,22 @@ hipError_t launch_b2b_csr(const uint8_t* msgs, const uint64_t* offsets, uint64_t
 // message i = msgs[begs[i], ends[i]) (spans may overlap; 4 readable bytes past each end)
 hipError_t launch_b2b_spans(const uint8_t* msgs, const uint64_t* begs, const uint64_t* ends, uint64_t n, uint8_t* out,
                             uint32_t out_bytes, hipStream_t stream);
-// Where message i's 64 signed parent ids are: trail[wstart, wstart + nw), then oids[ooff, ooff + 64 - nw).
-struct AttMsgRef {
-  uint32_t wstart, nw, ooff, pad;
+// One processAttestation message: its 10-byte header, where its 64 signed parent ids are
+// (trail[wstart, wstart + nw), then 64 - nw oblique ids at var[vo..]) and its ShardBlockHash
+// (sl bytes right after those ids).  32 bytes, appended by the walk into pinned memory.
+struct AttMsg {
+  uint8_t hdr[10];
+  uint16_t nw;
+  uint32_t wstart;
+  uint32_t sl;
+  uint32_t pad;
+  uint64_t vo;  // byte offset into var (a multiple of 4)
 };
+static_assert(sizeof(AttMsg) == 32, "AttMsg is 32 bytes");
 // processAttestation message digests (64 B each) from the engine's device hash log:
-// message i = hdr[16 i .. 16 i + 10) | 64 x (hlog[id(i, r)] | ' ') | sbh[sbh_offs[i]..sbh_offs[i+1]).
-hipError_t launch_b2b_attmsg(const uint8_t* hlog, const uint32_t* trail, const AttMsgRef* ref, const uint32_t* oids,
-                             const uint8_t* hdr, const uint8_t* sbh, const uint64_t* sbh_offs, uint64_t n, uint8_t* out,
-                             hipStream_t stream);
+// message i = hdr | 64 x (hlog[id(i, r)] | ' ') | ShardBlockHash.
+hipError_t launch_b2b_attmsg(const uint8_t* hlog, const uint32_t* trail, const AttMsg* rec, const uint8_t* var, uint64_t n,
+                             uint8_t* out, hipStream_t stream);
 }  // namespace pz
 
 namespace pz {

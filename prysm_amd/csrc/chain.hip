@@ -494,9 +494,55 @@ struct PinBuf {
   ~PinBuf() { release(); }
 };
 
+// Append-only pinned array for data that asynchronous H2D copies read while the walk keeps
+// appending: growing copies into a new buffer and keeps the old ones alive until reset(), which
+// the caller makes only once no copy is in flight.
+template <typename T>
+struct PinVec {
+  std::vector<std::unique_ptr<PinBuf>> bufs;  // the last one is current
+  size_t n = 0;
+  T* data() const { return bufs.empty() ? nullptr : reinterpret_cast<T*>(bufs.back()->p); }
+  size_t cap() const { return bufs.empty() ? 0 : bufs.back()->n / sizeof(T); }
+  void reserve(size_t c) {
+    if (c <= cap()) return;
+    auto nb = std::make_unique<PinBuf>();
+    if (int rc = nb->reserve(c * sizeof(T))) throw rc;
+    if (n) std::memcpy(nb->p, bufs.back()->p, n * sizeof(T));
+    bufs.push_back(std::move(nb));
+  }
+  T* grow(size_t k) {  // k more elements at the end
+    if (n + k > cap()) reserve(std::max(2 * cap(), n + k));
+    T* p = data() + n;
+    n += k;
+    return p;
+  }
+  void trim() {  // drop the outgrown buffers (no copy may still read them)
+    if (bufs.size() > 1) bufs.erase(bufs.begin(), bufs.end() - 1);
+  }
+  void reset() {
+    n = 0;
+    trim();
+  }
+  // the std::vector subset the hash log and the trail use
+  size_t size() const { return n; }
+  size_t capacity() const { return cap(); }
+  T& operator[](size_t i) { return data()[i]; }
+  const T& operator[](size_t i) const { return data()[i]; }
+  void push_back(const T& x) { *grow(1) = x; }
+  void resize(size_t k) {
+    if (k > n) grow(k - n);
+    else n = k;
+  }
+  void assign(size_t k, const T& x) {
+    n = 0;
+    T* p = grow(k);
+    for (size_t i = 0; i < k; ++i) p[i] = x;
+  }
+};
+
 enum ProfSlot {
   kProfParse, kProfHash1, kProfCheck, kProfQueue, kProfFlush, kProfRecalc, kProfMsgHash, kProfWalk, kProfProcess,
-  kProfCount, kProfFlushWait, kProfSlots
+  kProfCount, kProfFlushWait, kProfMsgSend, kProfMsgLog, kProfMsgWait, kProfSlots
 };
 
 // Queued attestations that force a tally flush before the next stateRecalc.  Flushing more
@@ -630,22 +676,25 @@ struct Engine {
   // append-only hash log: every block digest and oblique parent hash the walk meets gets an
   // id; RecentBlockHashes carry ids too, so signed parent hashes are id ranges (no hashing of
   // 32-byte keys per vote) and the processAttestation messages are assembled on the device
-  std::vector<H32> hlog;
+  // (hlog and trail are pinned: the message batches' H2D of their new entries is a DMA that
+  // neither stages through a host copy nor blocks the walk)
+  PinVec<H32> hlog;
   std::vector<uint32_t> id_slot;  // vote-cache slot of each id (resolved when it is logged)
-  std::vector<uint32_t> trail;    // the recent-hash windows of the states (AState::tail, len)
+  PinVec<uint32_t> trail;         // the recent-hash windows of the states (AState::tail, len)
   DevArr<uint32_t> d_trail;
   uint64_t d_trail_n = 0;
   DevArr<uint8_t> d_hlog;
   uint64_t d_hlog_n = 0;
-  // processAttestation message batch (10-byte header, 64 parent ids, ShardBlockHash)
-  std::vector<uint8_t> m_hdr, m_sbh;
-  std::vector<AttMsgRef> m_ref;   // per message: its parents' trail window and oblique ids
-  std::vector<uint32_t> m_oids;
-  std::vector<uint64_t> m_sboff{0};
-  DevArr<uint8_t> d_mhdr, d_msbh, d_mout;
-  DevArr<uint32_t> d_moids;
-  DevArr<AttMsgRef> d_mref;
-  DevArr<uint64_t> d_msboff;
+  // processAttestation messages of the call: a 32-byte record each, plus their oblique parent
+  // ids and ShardBlockHash bytes in m_var, appended by the walk straight into pinned memory and
+  // digested a batch at a time on stream ms while the walk goes on (msg_send)
+  PinVec<AttMsg> m_rec;
+  PinVec<uint8_t> m_var;
+  uint64_t m_sent = 0, m_var_sent = 0;  // records / var bytes already sent this call
+  bool m_busy = false;                  // ms may still be reading the pinned buffers
+  hipStream_t ms = nullptr;             // local rank 0's message stream
+  DevArr<AttMsg> d_mrec;
+  DevArr<uint8_t> d_mvar, d_mout;
   PinBuf m_pin;  // the message digests' D2H
   PinBuf arena_pin;  // the call arena's bytes: parsed in place, H2D'd whole for the digest batch
   // wall-time accumulators (seconds) per phase, read by pz_debug_chain_profile
@@ -829,6 +878,7 @@ static bool is_saved(const Engine& g, const H32& h) {
 // flush and cost 40 ms per 10,000 blocks (153 -> 88 k blocks/s, tools/gpu_replay_ab.sh).  `votable` is
 // false for an id that can never be tallied: a 32-byte oblique parent hash is only ever a
 // parent of its own attestation, which skips it (core.go:313-320).
+static void msg_drain(Engine& g);
 static uint32_t log_hash(Engine& g, const H32& h, bool votable = true) {
   g.hlog.push_back(h);
   g.id_slot.push_back(votable ? vote_slot(g, h) : UINT32_MAX);
@@ -1111,11 +1161,18 @@ static void process_attestation(Engine& g, uint64_t block_slot, const Att& a, At
   uint8_t hdr[16] = {0};
   put_uvarint(hdr, a.slot % kCycle);
   put_uvarint(hdr, a.shard);
-  g.m_hdr.insert(g.m_hdr.end(), hdr, hdr + 16);
-  g.m_ref.push_back(AttMsgRef{(uint32_t)parents.wstart, parents.nw, (uint32_t)g.m_oids.size(), 0});
-  g.m_oids.insert(g.m_oids.end(), parents.obl.begin(), parents.obl.end());
-  g.m_sbh.insert(g.m_sbh.end(), a.at(a.sbh_off), a.at(a.sbh_off) + a.sbh_len);
-  g.m_sboff.push_back(g.m_sbh.size());
+  const size_t nobl = parents.obl.size(), vb = (4 * nobl + a.sbh_len + 3) & ~size_t(3);
+  AttMsg* m = g.m_rec.grow(1);
+  std::memcpy(m->hdr, hdr, sizeof m->hdr);
+  m->nw = (uint16_t)parents.nw;
+  m->wstart = (uint32_t)parents.wstart;
+  m->sl = (uint32_t)a.sbh_len;
+  m->pad = 0;
+  m->vo = g.m_var.n;
+  uint8_t* v = g.m_var.grow(vb);
+  if (nobl) std::memcpy(v, parents.obl.data(), 4 * nobl);
+  std::memcpy(v + 4 * nobl, a.at(a.sbh_off), a.sbh_len);
+  std::memset(v + 4 * nobl + a.sbh_len, 0, vb - 4 * nobl - a.sbh_len);
 }
 
 // calculateBlockVoteCache (core.go:300-345): queue one tally item per signed parent hash.
@@ -1568,7 +1625,8 @@ static void init_tail(Engine& g, const std::vector<uint32_t>& members, const std
     hchk(hipStreamSynchronize(r.s), "sync");
   });
   auto A = std::make_shared<AState>();
-  g.hlog.clear();
+  msg_drain(g);
+  g.hlog.reset();
   g.id_slot.clear();
   g.d_hlog_n = 0;
   const uint32_t zero_id = log_hash(g, kZero);
@@ -1987,14 +2045,14 @@ static void sync_hash_log(Engine& g) {
   if (n == g.d_hlog_n) return;
   if (n * 32 > g.d_hlog.n) {
     DevArr<uint8_t> nb;
-    check(nb.alloc(std::max<uint64_t>(n * 32, 2 * g.d_hlog.n)));
-    if (g.d_hlog_n) hchk(hipMemcpyAsync(nb.p, g.d_hlog.p, g.d_hlog_n * 32, hipMemcpyDeviceToDevice, g.s), "D2D");
-    hchk(hipStreamSynchronize(g.s), "sync");
+    check(nb.alloc(std::max<uint64_t>(g.hlog.capacity() * 32, 2 * g.d_hlog.n)));  // (the call's reserve: once a call)
+    if (g.d_hlog_n) hchk(hipMemcpyAsync(nb.p, g.d_hlog.p, g.d_hlog_n * 32, hipMemcpyDeviceToDevice, g.ms), "D2D");
+    hchk(hipStreamSynchronize(g.ms), "sync");
     std::swap(g.d_hlog.p, nb.p);
     std::swap(g.d_hlog.n, nb.n);
   }
   hchk(hipMemcpyAsync(g.d_hlog.p + g.d_hlog_n * 32, g.hlog[g.d_hlog_n].b, (n - g.d_hlog_n) * 32,
-                      hipMemcpyHostToDevice, g.s), "H2D hash log");
+                      hipMemcpyHostToDevice, g.ms), "H2D hash log");
   g.d_hlog_n = n;
 }
 
@@ -2004,15 +2062,67 @@ static void sync_trail(Engine& g) {
   if (n == g.d_trail_n) return;
   if (n > g.d_trail.n) {
     DevArr<uint32_t> nb;
-    check(nb.alloc(std::max<uint64_t>(n, 2 * g.d_trail.n)));
-    if (g.d_trail_n) hchk(hipMemcpyAsync(nb.p, g.d_trail.p, g.d_trail_n * 4, hipMemcpyDeviceToDevice, g.s), "D2D");
-    hchk(hipStreamSynchronize(g.s), "sync");
+    check(nb.alloc(std::max<uint64_t>(g.trail.capacity(), 2 * g.d_trail.n)));
+    if (g.d_trail_n) hchk(hipMemcpyAsync(nb.p, g.d_trail.p, g.d_trail_n * 4, hipMemcpyDeviceToDevice, g.ms), "D2D");
+    hchk(hipStreamSynchronize(g.ms), "sync");
     std::swap(g.d_trail.p, nb.p);
     std::swap(g.d_trail.n, nb.n);
   }
   hchk(hipMemcpyAsync(g.d_trail.p + g.d_trail_n, g.trail.data() + g.d_trail_n, (n - g.d_trail_n) * 4,
-                      hipMemcpyHostToDevice, g.s), "H2D trail");
+                      hipMemcpyHostToDevice, g.ms), "H2D trail");
   g.d_trail_n = n;
+}
+
+// Wait for the message batches in flight (their H2D copies read the pinned hash log, trail
+// and records).
+static void msg_drain(Engine& g) {
+  if (!g.m_busy) return;
+  hchk(hipStreamSynchronize(g.ms), "sync (message batch)");
+  g.m_busy = false;
+}
+
+// processAttestation messages per batch sent while the walk goes on (PZ_MSG_BATCH; 0, the
+// default: one batch at the end of the call).  The kernel is latency-bound (one lane runs a
+// message's 17 compressions), ~0.13 ms for any batch up to 65,536 messages, so the last batch
+// costs the same wait as one whole-call batch: 8,192 measured no better than 0 on the
+// configs[4] replay (profiles/r03/msg_batch_ab_r3ap.txt), and costs six more sends.
+static uint64_t msg_batch() {  // (read per call: a test sets it)
+  const char* e = std::getenv("PZ_MSG_BATCH");
+  return e ? std::strtoull(e, nullptr, 10) : uint64_t(0);
+}
+
+// Digest the messages the walk appended since the last batch, on stream ms: the new hash-log
+// and trail entries, the records and var bytes H2D (pinned: no host staging), one
+// pz_b2b_attmsg_kernel launch over the batch and the D2H of its digests into g.m_pin.  Nothing
+// waits here; msg_drain / the end of the call does.
+static void msg_send(Engine& g) {
+  const uint64_t n = g.m_rec.n, k = n - g.m_sent;
+  if (!k) return;
+  PhaseTimer pt(g.prof[kProfMsgSend]);
+  {
+    PhaseTimer pl(g.prof[kProfMsgLog]);
+    sync_hash_log(g);
+    sync_trail(g);
+  }
+  if (g.m_var.n + 4 > g.d_mvar.n) {  // grow, keeping what earlier batches sent
+    DevArr<uint8_t> nb;
+    check(nb.alloc(std::max<uint64_t>(g.m_var.capacity() + 4, 2 * g.d_mvar.n)));  // (once a call, bar a regrowth)
+    if (g.m_var_sent) hchk(hipMemcpyAsync(nb.p, g.d_mvar.p, g.m_var_sent, hipMemcpyDeviceToDevice, g.ms), "D2D");
+    hchk(hipStreamSynchronize(g.ms), "sync");
+    std::swap(g.d_mvar.p, nb.p);
+    std::swap(g.d_mvar.n, nb.n);
+  }
+  if (g.m_var.n > g.m_var_sent)
+    hchk(hipMemcpyAsync(g.d_mvar.p + g.m_var_sent, g.m_var.data() + g.m_var_sent, g.m_var.n - g.m_var_sent,
+                        hipMemcpyHostToDevice, g.ms), "H2D message ids / ShardBlockHash");
+  hchk(hipMemcpyAsync(g.d_mrec.p + g.m_sent, g.m_rec.data() + g.m_sent, k * sizeof(AttMsg), hipMemcpyHostToDevice, g.ms),
+       "H2D message records");
+  hchk(launch_b2b_attmsg(g.d_hlog.p, g.d_trail.p, g.d_mrec.p + g.m_sent, g.d_mvar.p, k, g.d_mout.p + g.m_sent * 64, g.ms),
+       "attestation message digests");
+  hchk(hipMemcpyAsync(g.m_pin.p + g.m_sent * 64, g.d_mout.p + g.m_sent * 64, k * 64, hipMemcpyDeviceToHost, g.ms), "D2H");
+  g.m_sent = n;
+  g.m_var_sent = g.m_var.n;
+  g.m_busy = true;
 }
 
 // Digest messages of blocks [b0, b1) and their na attestations (a0.. in call order), laid out
@@ -2266,13 +2376,18 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
   std::vector<AttP> processed;
   std::vector<uint32_t> block_id(n);
   uint64_t ai = 0;
-  g.m_hdr.clear();
-  g.m_ref.clear();
-  g.m_oids.clear();
-  g.m_sbh.clear();
-  g.m_sboff.assign(1, 0);
-  g.m_hdr.reserve(16 * natt);
-  g.m_ref.reserve(natt);
+  msg_drain(g);  // (a failed call may have left a batch in flight)
+  g.hlog.trim();
+  g.trail.trim();
+  g.m_rec.reset();
+  g.m_var.reset();
+  g.m_sent = g.m_var_sent = 0;
+  g.m_rec.reserve(natt + 1);  // every message is an attestation of the call: no growth
+  g.m_var.reserve(64 * natt + 4096);
+  check(g.m_pin.reserve(natt * 64 + 64));
+  check(g.d_mrec.alloc(natt + 1));
+  check(g.d_mout.alloc(natt * 64 + 64));
+  const uint64_t mbatch = msg_batch();
   // the tables grow once per call, not by doubling inside the walk
   g.slot_of.reserve(g.slot_of.size() + n);  // (plus any oblique hash shorter than 32 B: grows)
   g.hlog.reserve(g.hlog.size() + n + 2 * natt);
@@ -2370,6 +2485,7 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
       state_recalc(g, C, A, b.slot, &nc, &na);
       C = nc;
       A = na;
+      if (mbatch && g.m_rec.n - g.m_sent >= mbatch) msg_send(g);  // (the walk just waited on the device)
     }
     // computeNewActiveState (core.go:223-237)
     A->cache_nil = cache_nil;
@@ -2386,24 +2502,14 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
   epoch_collect(g);  // a panic of the last transition's epoch fails this call
   PhaseTimer pt(g.prof[kProfMsgHash]);
   const size_t nm = msg_att.size();
-  if (nm) {
-    sync_hash_log(g);
-    upload(g, g.d_mhdr, g.m_hdr.data(), g.m_hdr.size());
-    sync_trail(g);
-    upload(g, g.d_mref, g.m_ref.data(), g.m_ref.size());
-    upload(g, g.d_moids, g.m_oids.data(), g.m_oids.size() + 1);  // (+1: never an empty allocation)
-    upload(g, g.d_msbh, g.m_sbh.data(), g.m_sbh.size() + 1);  // (+1: never an empty allocation)
-    upload(g, g.d_msboff, g.m_sboff.data(), g.m_sboff.size());
-    check(g.d_mout.alloc(nm * 64));
-    hchk(launch_b2b_attmsg(g.d_hlog.p, g.d_trail.p, g.d_mref.p, g.d_moids.p, g.d_mhdr.p, g.d_msbh.p, g.d_msboff.p, nm,
-                           g.d_mout.p, g.s),
-         "attestation message digests");
-    check(g.m_pin.reserve(nm * 64));  // (a fresh pageable vector cost a zero fill and page faults per call)
-    const uint8_t* md = g.m_pin.p;
-    hchk(hipMemcpyAsync(g.m_pin.p, g.d_mout.p, nm * 64, hipMemcpyDeviceToHost, g.s), "D2H");
-    hchk(hipStreamSynchronize(g.s), "sync");  // also keeps the pageable sources alive
-    for (size_t i = 0; i < nm; ++i) std::memcpy(ar[msg_att[i]].msg_digest, &md[i * 64], 64);
+  if (g.m_rec.n != nm) throw fail(PZ_EDEVICE, "message batch out of step with the walk");
+  msg_send(g);
+  {
+    PhaseTimer pw(g.prof[kProfMsgWait]);
+    msg_drain(g);
   }
+  const uint8_t* md = g.m_pin.p;
+  for (size_t i = 0; i < nm; ++i) std::memcpy(ar[msg_att[i]].msg_digest, &md[i * 64], 64);
 }
 
 }  // namespace chain
@@ -2436,6 +2542,7 @@ static void make_ranks(Engine& g, int device, pz_comm* comm) {
   g.s = g.rk[0].s;
   hchk(hipSetDevice(g.device), "hipSetDevice");
   hchk(hipStreamCreateWithFlags(&g.s2, hipStreamNonBlocking), "hipStreamCreate");
+  hchk(hipStreamCreateWithFlags(&g.ms, hipStreamNonBlocking), "hipStreamCreate");
 }
 
 static void destroy_chain(pz_chain* c) {
@@ -2451,11 +2558,12 @@ static void destroy_chain(pz_chain* c) {
   if (g.ev_totals) (void)hipEventDestroy(g.ev_totals);
   for (hipEvent_t e : g.ring_ev)
     if (e) (void)hipEventDestroy(e);
-  if (g.s2) {
-    (void)hipSetDevice(g.device);
-    (void)hipStreamSynchronize(g.s2);
-    streams.push_back({g.device, g.s2});
-  }
+  for (hipStream_t x : {g.s2, g.ms})
+    if (x) {
+      (void)hipSetDevice(g.device);
+      (void)hipStreamSynchronize(x);
+      streams.push_back({g.device, x});
+    }
   delete c;
   for (auto& ds : streams)
     if (ds.second) {

@@ -143,6 +143,38 @@ def test_gpu_replay_many_calls_equal_one_call_65536():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("batch", ["1", "37", "5000"])
+def test_gpu_replay_message_batches_equal_one_batch(monkeypatch, batch):
+    """PZ_MSG_BATCH > 0 digests the processAttestation messages in batches sent after the
+    transitions, on their own stream, while the walk goes on (chain.hip msg_send): every
+    message digest, record and root equals the one-batch call's, over a chain fed in one call
+    and in calls of 1-60 blocks."""
+    from prysm_amd.blockchain import BeaconChain, serialize_blocks
+    nval = 65536
+    blocks = synth.chain_blocks(nval, 400, seed=9)
+    d, o = serialize_blocks(blocks)
+    monkeypatch.delenv("PZ_MSG_BATCH", raising=False)
+    one = BeaconChain(nval)
+    br1, ar1 = one.process_serialized(d, o)
+    monkeypatch.setenv("PZ_MSG_BATCH", batch)
+    two = BeaconChain(nval)
+    br2, ar2 = two.process_serialized(d, o)
+    np.testing.assert_array_equal(br2, br1)
+    np.testing.assert_array_equal(ar2, ar1)
+    assert two.roots() == one.roots()
+    many = BeaconChain(nval)
+    rng = np.random.default_rng(4)
+    ars, i = [], 0
+    while i < len(blocks):
+        k = int(rng.integers(1, 61))
+        d, o = serialize_blocks(blocks[i:i + k])
+        ars.append(many.process_serialized(d, o)[1].copy())
+        i += k
+    np.testing.assert_array_equal(np.concatenate(ars), ar1)
+    assert many.roots() == one.roots()
+
+
+@pytest.mark.gpu
 def test_gpu_replay_vs_live_oracle_65536():
     from oracle import replay
     nval = 65536
@@ -199,6 +231,44 @@ def test_oracle_edited_chain_statuses():
     assert st[:19] == ["processed"] * 19 and st[19] == "attestations_rejected" and set(st[20:]) == {"no_parent"}
     errs = [a["error"] for r in recs for a in r["atts"] if "error" in a]
     assert len(errs) == 5
+
+
+def shaped_message_chain():
+    """processAttestation messages of every shape the device gather handles: ShardBlockHash of
+    0-300 bytes (not a multiple of 4, crossing a 128-byte block edge) and 0-3 oblique parent
+    hashes, full (32 B, logged ids) and short (7 B, zero-padded unvotable ids)."""
+    import dataclasses
+    blocks = synth.chain_blocks(1024, 40, seed=8)
+    rng = np.random.default_rng(8)
+    sb_lens = [0, 1, 3, 5, 31, 33, 100, 300]
+    for bi, b in enumerate(blocks):
+        atts = []
+        for j, a in enumerate(b.attestations):
+            sb = rng.integers(0, 256, sb_lens[(bi + j) % len(sb_lens)], dtype=np.uint8).tobytes()
+            obl = [rng.integers(0, 256, 32 if q % 2 == 0 else 7, dtype=np.uint8).tobytes() for q in range((bi + 2 * j) % 4)]
+            atts.append(dataclasses.replace(a, shard_block_hash=sb, oblique_parent_hashes=obl))
+        b.attestations = atts
+    return _relink(blocks)
+
+
+def test_oracle_shaped_message_chain_processes():
+    from oracle import replay
+    recs, _ = replay.replay(shaped_message_chain(), 1024)
+    assert all(r["status"] == "processed" for r in recs)
+    assert all("error" not in a for r in recs for a in r["atts"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", ["0", "3"])
+def test_gpu_replay_shaped_messages_vs_oracle(monkeypatch, batch):
+    from oracle import replay
+    blocks = shaped_message_chain()
+    o_recs, o_roots = replay.replay(blocks, 1024)
+    monkeypatch.setenv("PZ_MSG_BATCH", batch)
+    recs, roots = _product(1024, blocks)
+    assert _hexrecs(recs) == _hexrecs(o_recs)
+    for k in ("chain_active", "chain_crystallized", "cand_active", "cand_crystallized"):
+        assert roots[k] == o_roots[k], k
 
 
 def future_slot_chain():

@@ -48,7 +48,8 @@ def main():
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     k = fn(ch._h, pv, 16)
     names = ["parse", "digests1", "att_checks+msg", "vote_queue", "vote_flush", "state_recalc", "msg_digests",
-             "walk(all)", "process(all)", "count_atts", "flush_arena_wait"]
+             "walk(all)", "process(all)", "count_atts", "flush_arena_wait", "msg_send",
+             "msg_hash_log", "msg_wait"]
     print("phases (s): " + ", ".join("%s %.4f" % (names[i], pv[i]) for i in range(k)), flush=True)
     t = time.perf_counter()
     ch.roots()
