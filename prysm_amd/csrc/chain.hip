@@ -606,6 +606,9 @@ struct Engine {
   DigestBufs dbatch;         // the digest batch of an unpipelined call
   DigestBufs ring[kRing];    // the pipelined calls' digest batches, reused chunk after chunk
   hipEvent_t ring_ev[kRing] = {};
+  // the batch path's digest batch runs on s2 in two parts: the block digests (the walk waits
+  // for ev_dblk) and the attestations' Hash / Key (results only: collected after the walk)
+  hipEvent_t ev_dblk = nullptr, ev_datt = nullptr;
   pz_comm* comm = nullptr;  // null: one device, every validator
   int world = 1;
   std::vector<RankDev> rk;
@@ -2201,8 +2204,12 @@ static void stage_launch(uint64_t nmsg, uint64_t bytes, DigestBufs& D, hipStream
 // The batch path's digest batch, reading blocks and attestation encodings where they lie in
 // the call's pinned arena (one H2D of the arena, no copy of them on the host); only the Key()
 // preimages are built.  Digests [blocks][attestation Hash][Key], 32 B each, land in D.dig.
+// Two launches on s: the nb block digests, D2H'd and then ev_blk; the attestations' Hash and
+// Key behind them, then ev_att.  The host builds the Key() preimages while the arena and the
+// block digests are on the way.
 static void stage_digests_arena(const std::vector<Block>& blocks, uint64_t nb, uint64_t na, const CallArena& ar,
-                                uint64_t abytes, DigestBufs& D, hipStream_t s) {
+                                uint64_t abytes, DigestBufs& D, hipStream_t s, hipEvent_t ev_blk, hipEvent_t ev_att) {
+  hchk(hipStreamSynchronize(s), "sync");  // (a failed call's attestation part may still read D)
   const uint64_t nmsg = nb + 2 * na, aal = (abytes + 15) & ~15ull;
   uint64_t kbytes = 0;
   for (uint64_t bi = 0; bi < nb; ++bi)
@@ -2210,15 +2217,25 @@ static void stage_digests_arena(const std::vector<Block>& blocks, uint64_t nb, u
   check(D.msgs.reserve(kbytes + 16));
   check(D.offs.reserve(2 * nmsg * 8 + 8));
   check(D.dig.reserve(nmsg * 32 + 32));
+  check(D.d_in.alloc(aal + kbytes + 16));
+  check(D.d_out.alloc(nmsg * 32));
+  check(D.d_offs.alloc(2 * nmsg + 1));
+  // the arena's DMA first: it crosses PCIe while the spans and Key() preimages are built
+  hchk(hipMemcpyAsync(D.d_in.p, ar.bytes, abytes + 16, hipMemcpyHostToDevice, s), "H2D arena");  // (+ its zero pad)
   uint64_t* beg = reinterpret_cast<uint64_t*>(D.offs.p);
   uint64_t* end = beg + nmsg;
-  uint64_t m = 0, ka = nb, kk = nb + na, kpos = 0;
   for (uint64_t bi = 0; bi < nb; ++bi) {
-    const Block& b = blocks[bi];
-    beg[m] = (uint64_t)(b.data - ar.bytes);
-    end[m] = beg[m] + b.len;
-    ++m;
-    for (auto& ap : b.atts) {
+    beg[bi] = (uint64_t)(blocks[bi].data - ar.bytes);
+    end[bi] = beg[bi] + blocks[bi].len;
+  }
+  hchk(hipMemcpyAsync(D.d_offs.p, beg, nb * 8, hipMemcpyHostToDevice, s), "H2D spans");
+  hchk(hipMemcpyAsync(D.d_offs.p + nmsg, end, nb * 8, hipMemcpyHostToDevice, s), "H2D spans");
+  hchk(launch_b2b_spans(D.d_in.p, D.d_offs.p, D.d_offs.p + nmsg, nb, D.d_out.p, 32, s), "blake2b spans (blocks)");
+  hchk(hipMemcpyAsync(D.dig.p, D.d_out.p, nb * 32, hipMemcpyDeviceToHost, s), "D2H digests");
+  hchk(hipEventRecord(ev_blk, s), "event");
+  uint64_t ka = nb, kk = nb + na, kpos = 0;
+  for (uint64_t bi = 0; bi < nb; ++bi) {
+    for (auto& ap : blocks[bi].atts) {
       const Att& a = *ap;
       beg[ka] = (uint64_t)(a.base - ar.bytes);
       end[ka] = beg[ka] + a.len;
@@ -2241,15 +2258,16 @@ static void stage_digests_arena(const std::vector<Block>& blocks, uint64_t nb, u
       kpos += kl;
     }
   }
-  check(D.d_in.alloc(aal + kbytes + 16));
-  check(D.d_out.alloc(nmsg * 32));
-  check(D.d_offs.alloc(2 * nmsg + 1));
-  hchk(hipMemcpyAsync(D.d_offs.p, beg, 2 * nmsg * 8, hipMemcpyHostToDevice, s), "H2D spans");
-  hchk(hipMemcpyAsync(D.d_in.p, ar.bytes, abytes + 16, hipMemcpyHostToDevice, s), "H2D arena");  // (+ its zero pad)
-  if (kbytes) hchk(hipMemcpyAsync(D.d_in.p + aal, D.msgs.p, kbytes, hipMemcpyHostToDevice, s), "H2D keys");
-  hchk(hipMemsetAsync(D.d_in.p + aal + kbytes, 0, 16, s), "memset");
-  hchk(launch_b2b_spans(D.d_in.p, D.d_offs.p, D.d_offs.p + nmsg, nmsg, D.d_out.p, 32, s), "blake2b spans");
-  hchk(hipMemcpyAsync(D.dig.p, D.d_out.p, nmsg * 32, hipMemcpyDeviceToHost, s), "D2H digests");
+  if (na) {
+    hchk(hipMemcpyAsync(D.d_offs.p + nb, beg + nb, 2 * na * 8, hipMemcpyHostToDevice, s), "H2D spans");
+    hchk(hipMemcpyAsync(D.d_offs.p + nmsg + nb, end + nb, 2 * na * 8, hipMemcpyHostToDevice, s), "H2D spans");
+    if (kbytes) hchk(hipMemcpyAsync(D.d_in.p + aal, D.msgs.p, kbytes, hipMemcpyHostToDevice, s), "H2D keys");
+    hchk(hipMemsetAsync(D.d_in.p + aal + kbytes, 0, 16, s), "memset");
+    hchk(launch_b2b_spans(D.d_in.p, D.d_offs.p + nb, D.d_offs.p + nmsg + nb, 2 * na, D.d_out.p + nb * 32, 32, s),
+         "blake2b spans (attestations)");
+    hchk(hipMemcpyAsync(D.dig.p + nb * 32, D.d_out.p + nb * 32, 2 * na * 32, hipMemcpyDeviceToHost, s), "D2H digests");
+  }
+  hchk(hipEventRecord(ev_att, s), "event");
 }
 
 static void stage_digests(const std::vector<Block>& blocks, uint64_t b0, uint64_t b1, uint64_t na, DigestBufs& D,
@@ -2284,6 +2302,7 @@ struct Feeder {
   std::atomic<int> rc{0};
   std::atomic<bool> stop{false};
   uint64_t cur = UINT64_MAX;  // the chunk the walk is in
+  hipEvent_t att_ev = nullptr;  // non-null: the attestations' Hash / Key land behind it (after the walk)
   double wait_s = 0;
 
   // false: block bi is not there (a malformed block at or before it ends the walk)
@@ -2444,8 +2463,10 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
       }
       can_atts = true;
       x.status = PZ_ATT_PROCESSED;
-      std::memcpy(x.hash, F.hash(bi, a0 + j), 32);
-      std::memcpy(x.key, F.key(bi, a0 + j), 32);
+      if (!F.att_ev) {
+        std::memcpy(x.hash, F.hash(bi, a0 + j), 32);
+        std::memcpy(x.key, F.key(bi, a0 + j), 32);
+      }
       x.msg_len = (uint32_t)(10 + 33 * kCycle + b.atts[j]->sbh_len);
       msg_att.push_back(a0 + j);
       processed.push_back(b.atts[j]);
@@ -2510,6 +2531,14 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
   }
   const uint8_t* md = g.m_pin.p;
   for (size_t i = 0; i < nm; ++i) std::memcpy(ar[msg_att[i]].msg_digest, &md[i * 64], 64);
+  if (F.att_ev) {  // the processed attestations' Hash and Key (the batch path's second part)
+    hchk(hipEventSynchronize(F.att_ev), "event sync (attestation digests)");
+    for (size_t i = 0; i < nm; ++i) {
+      const uint64_t ga = msg_att[i];
+      std::memcpy(ar[ga].hash, F.dg + (n + ga) * 32, 32);
+      std::memcpy(ar[ga].key, F.dg + (n + natt + ga) * 32, 32);
+    }
+  }
 }
 
 }  // namespace chain
@@ -2555,7 +2584,8 @@ static void destroy_chain(pz_chain* c) {
       if (e) (void)hipEventDestroy(e);
     streams.push_back({r.dev, r.s});
   }
-  if (g.ev_totals) (void)hipEventDestroy(g.ev_totals);
+  for (hipEvent_t e : {g.ev_totals, g.ev_dblk, g.ev_datt})
+    if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : g.ring_ev)
     if (e) (void)hipEventDestroy(e);
   for (hipStream_t x : {g.s2, g.ms})
@@ -2695,8 +2725,14 @@ int pz_chain_process_blocks(pz_chain* c, const uint8_t* blocks, const uint64_t* 
     try {
       PhaseTimer pt(g.prof[kProfHash1]);
       if (!long_msg) {
-        if (F.n) stage_digests_arena(parsed, F.n, F.natt, *arena, offsets[n] - offsets[0], g.dbatch, g.s);
-        hchk(hipStreamSynchronize(g.s), "sync");
+        if (!g.ev_dblk) hchk(hipEventCreateWithFlags(&g.ev_dblk, hipEventDisableTiming), "event");
+        if (!g.ev_datt) hchk(hipEventCreateWithFlags(&g.ev_datt, hipEventDisableTiming), "event");
+        if (F.n) {
+          stage_digests_arena(parsed, F.n, F.natt, *arena, offsets[n] - offsets[0], g.dbatch, g.s2, g.ev_dblk,
+                              g.ev_datt);
+          hchk(hipEventSynchronize(g.ev_dblk), "event sync (block digests)");
+          F.att_ev = g.ev_datt;
+        }
         F.dg = g.dbatch.dig.p;
         F.dstride = 32;
       } else {  // 64-byte digests; messages at or over the threshold on host threads
