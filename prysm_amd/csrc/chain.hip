@@ -272,11 +272,35 @@ struct AttSpan {
 // One pz_chain_process_blocks call's input: a copy of its serialized blocks and every
 // attestation record parsed from them, allocated once (per-record allocations made the parse
 // allocator-bound).  The Engine keeps it while a live state's pending attestations point in.
+// Record storage allocated without constructing anything: the parse threads construct their own
+// ranges (a value-initialised std::vector<Att> zeroed and faulted in 4.4 MB per 10,000 blocks
+// on the calling thread before any parse thread started).
+struct AttStore {
+  Att* p = nullptr;
+  size_t n = 0;
+  AttStore() = default;
+  AttStore(const AttStore&) = delete;
+  AttStore& operator=(const AttStore&) = delete;
+  ~AttStore() { std::free(p); }
+  void alloc(size_t count) {  // (Att is trivially destructible: nothing to destroy first)
+    std::free(p);
+    p = nullptr;
+    n = count;
+    if (count && !(p = static_cast<Att*>(std::malloc(count * sizeof(Att))))) throw std::bad_alloc();
+  }
+  Att* data() const { return p; }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  Att& operator[](size_t i) const { return p[i]; }
+};
+static_assert(std::is_trivially_destructible<Att>::value && std::is_trivially_copyable<Att>::value,
+              "AttStore places records without destructors");
+
 struct CallArena {
   using Pool = std::vector<std::pair<uint32_t, uint32_t>>;
   uint8_t* bytes = nullptr;  // (not zero-filled) the Engine's pinned arena, or `own`
   std::unique_ptr<uint8_t[]> own;
-  std::vector<Att> atts;  // sized to the exact count: block i's records at [first[i], first[i+1])
+  AttStore atts;  // sized to the exact count: block i's records at [first[i], first[i+1])
   std::vector<AttP> ptrs;  // &atts[j]: each Block's AttSpan is a run of it
   std::vector<uint64_t> first;  // per block, its first record (a prefix of the per-block counts)
   // one pool per range parsed by one thread, each reserved to a bound (an element takes >= 2
@@ -369,7 +393,7 @@ static bool parse_block(const uint8_t* p, size_t n, Block* b, CallArena* ar, uin
       if (!t.ok) return false;
     } else {  // f == 8
       if (a0 + b->atts.n >= a1) return false;  // more records than counted (unreachable)
-      Att* a = &ar->atts[a0 + b->atts.n];
+      Att* a = new (&ar->atts[a0 + b->atts.n]) Att();  // (constructed here, on the parsing thread)
       if (!parse_att(q, len, a, pool)) return false;
       ar->ptrs[a0 + b->atts.n] = a;
       ++b->atts.n;
@@ -1879,7 +1903,7 @@ static std::shared_ptr<CallArena> make_arena(const uint64_t* offs, uint64_t n, s
   std::memset(ar->bytes + total, 0, 16);
   ar->first = std::move(first);
   const uint64_t natt = ar->first.empty() ? 0 : ar->first.back();
-  ar->atts.resize(natt);
+  ar->atts.alloc(natt);
   ar->ptrs.resize(natt);
   ar->obl.resize(std::max<size_t>(npools, 1));
   return ar;
@@ -1925,9 +1949,9 @@ static uint64_t parse_range(const uint8_t* data, const uint64_t* offs, uint64_t 
 static int parse_threads(uint64_t bytes) {
   static const int cap = [] {
     const char* e = std::getenv("PZ_PARSE_THREADS");
-    return e ? std::max(1, std::atoi(e)) : 8;
+    return e ? std::max(1, std::atoi(e)) : 16;
   }();
-  return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cap, bytes >> 20));
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cap, bytes >> 19));
 }
 
 // Blocks [0, n) over ar.obl.size() threads (ranges of about equal bytes; records need no
@@ -1990,10 +2014,10 @@ static void keep_arenas(Engine& g, CallArena* cur) {
       na->own.reset(new uint8_t[bytes + 16]);
       na->bytes = na->own.get();
       std::memset(na->bytes + bytes, 0, 16);
-      na->atts.reserve(mv.size());
+      na->atts.alloc(mv.size());
       na->obl.resize(1);
       na->obl[0].reserve(nobl + 1);
-      size_t pos = 0;
+      size_t pos = 0, k = 0;
       for (AttP p : mv) {
         Att a = *p;
         std::memcpy(na->bytes + pos, p->base, p->len);
@@ -2002,7 +2026,7 @@ static void keep_arenas(Engine& g, CallArena* cur) {
         a.obl_first = (uint32_t)na->obl[0].size();
         for (auto& o : p->obl) na->obl[0].push_back(o);
         a.obl.p = na->obl[0].data() + a.obl_first;  // (reserved: never reallocates)
-        na->atts.push_back(a);
+        new (&na->atts[k++]) Att(a);
       }
       for (auto* l : lists)
         for (AttP& p : *l)
@@ -2014,7 +2038,7 @@ static void keep_arenas(Engine& g, CallArena* cur) {
   for (auto* l : lists)
     for (AttP p : *l)
       for (size_t k = 0; k < g.arenas.size(); ++k) {
-        const std::vector<Att>& a = g.arenas[k]->atts;
+        const AttStore& a = g.arenas[k]->atts;
         if (!a.empty() && p >= a.data() && p < a.data() + a.size()) {
           used[k] = 1;
           break;
@@ -2029,11 +2053,11 @@ static void keep_arenas(Engine& g, CallArena* cur) {
 // Every block, on the calling thread, before anything else (the path that keeps a call
 // all-or-nothing; pz_chain_process_blocks pipelines the parse otherwise).
 static int parse_all(const uint8_t* data, const uint64_t* offs, uint64_t n, std::vector<Block>& blocks,
-                     std::shared_ptr<CallArena>* keep, int threads) {
+                     std::shared_ptr<CallArena>* keep, int threads, PinBuf* pin = nullptr) {
   std::vector<uint64_t> first;
   int rc = count_per_block(data, offs, n, first);
   if (rc) return rc;
-  auto ar = make_arena(offs, n, std::move(first), (size_t)threads);
+  auto ar = make_arena(offs, n, std::move(first), (size_t)threads, pin);
   *keep = ar;  // the blocks' bytes live here for the whole call (records alias it beyond)
   blocks.resize(n);
   const uint64_t bad = parse_parallel(data, offs, n, *ar, blocks);
@@ -2958,12 +2982,17 @@ extern "C" int pz_debug_chain_profile(pz_chain* c, double* out, int n) {
 extern "C" int pz_debug_parse(const uint8_t* data, const uint64_t* offs, uint64_t n, uint64_t threads, int reps,
                               double* seconds, uint64_t* checksum) {
   double best = 1e30;
+  // PZ_DEBUG_PARSE_PIN=1: the arena in pooled pinned memory, as pz_chain_process_blocks has it
+  // (a device call: GPU boxes only)
+  const char* pe = std::getenv("PZ_DEBUG_PARSE_PIN");
+  pz::chain::PinBuf pin;
   for (int r = 0; r < reps; ++r) {
     const auto t0 = std::chrono::steady_clock::now();
     {
       std::vector<pz::chain::Block> blocks;
       std::shared_ptr<pz::chain::CallArena> arena;
-      const int rc = pz::chain::parse_all(data, offs, n, blocks, &arena, (int)std::max<uint64_t>(1, threads));
+      const int rc = pz::chain::parse_all(data, offs, n, blocks, &arena, (int)std::max<uint64_t>(1, threads),
+                                          pe && pe[0] == '1' ? &pin : nullptr);
       if (rc) return rc;
       best = std::min(best, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
       if (checksum && r == 0) {
