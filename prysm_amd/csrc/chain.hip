@@ -1944,8 +1944,9 @@ static uint64_t parse_range(const uint8_t* data, const uint64_t* offs, uint64_t 
   return b1;
 }
 
-// Threads for the parse of a call of `bytes` input bytes: PZ_PARSE_THREADS (default 8; the
-// CPU share of one GPU on the bench boxes is 16), one per ~1 MB.
+// Threads for the parse of a call of `bytes` input bytes: PZ_PARSE_THREADS (default 16, the
+// CPU share of one GPU on the bench boxes), one per 512 KB (10,000 blocks: 1.76 ms on 8,
+// 1.22 ms on 16, profiles/r03/parse_probe_after_r3at.txt).
 static int parse_threads(uint64_t bytes) {
   static const int cap = [] {
     const char* e = std::getenv("PZ_PARSE_THREADS");
