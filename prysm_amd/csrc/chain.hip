@@ -26,6 +26,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <condition_variable>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -1955,6 +1956,67 @@ static int parse_threads(uint64_t bytes) {
   return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cap, bytes >> 19));
 }
 
+// The parse's worker threads, started once per process and kept (starting eight threads per
+// call showed as 2 % of the replay's samples in pthread_create, profiles/r03/walk_sampler_r3av.txt).
+// Never destroyed, like the pinned pool: idle workers wait on a condition variable.
+struct WorkPool {
+  std::mutex mu;
+  std::condition_variable cv, done;
+  std::vector<std::function<void()>> jobs;
+  size_t next = 0, left = 0;
+  int threads = 0;
+  bool failed = false;
+  std::mutex run_mu;  // one batch at a time (chains on other threads share the pool)
+  // Runs fns[1..] on the workers and fns[0] here; returns when all are done.  Throws (PZ_EDEVICE
+  // semantics: check's int) when a job threw.
+  void run(std::vector<std::function<void()>>& fns) {
+    std::lock_guard<std::mutex> one(run_mu);
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      while (threads < (int)fns.size() - 1) {
+        std::thread([this] { work(); }).detach();
+        ++threads;
+      }
+      jobs.assign(fns.begin() + 1, fns.end());
+      next = 0;
+      left = jobs.size();
+      failed = false;
+    }
+    cv.notify_all();
+    bool mine_failed = false;
+    try {
+      fns[0]();
+    } catch (...) {
+      mine_failed = true;
+    }
+    std::unique_lock<std::mutex> lk(mu);
+    done.wait(lk, [this] { return left == 0; });
+    jobs.clear();
+    if (mine_failed || failed) throw (int)PZ_EDEVICE;
+  }
+  void work() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [this] { return next < jobs.size(); });
+      std::function<void()> f = jobs[next++];
+      lk.unlock();
+      bool bad = false;
+      try {
+        f();
+      } catch (...) {
+        bad = true;
+      }
+      lk.lock();
+      if (bad) failed = true;
+      if (--left == 0) done.notify_all();
+    }
+  }
+};
+static WorkPool& work_pool() {
+  static WorkPool* p = new WorkPool();
+  return *p;
+}
+
 // Blocks [0, n) over ar.obl.size() threads (ranges of about equal bytes; records need no
 // allocation, so the threads share nothing but the arena's disjoint ranges); returns the first
 // malformed block or n.
@@ -1972,16 +2034,14 @@ static uint64_t parse_parallel(const uint8_t* data, const uint64_t* offs, uint64
     cut[t] = std::max<uint64_t>(cut[t - 1], std::lower_bound(offs, offs + n, want) - offs);
   }
   std::vector<uint64_t> bad(T, UINT64_MAX);
-  std::vector<std::thread> th;
-  size_t started = 1;
+  std::vector<std::function<void()>> fns;
+  for (size_t t = 0; t < T; ++t)
+    fns.push_back([&, t] { bad[t] = parse_range(data, offs, cut[t], cut[t + 1], ar, blocks, t); });
   try {
-    for (size_t t = 1; t < T; ++t, ++started)
-      th.emplace_back([&, t] { bad[t] = parse_range(data, offs, cut[t], cut[t + 1], ar, blocks, t); });
-  } catch (const std::exception&) {  // no thread to be had: the rest on this one
+    work_pool().run(fns);
+  } catch (const std::system_error&) {  // no thread to be had: every range on this one
+    for (size_t t = 0; t < T; ++t) bad[t] = parse_range(data, offs, cut[t], cut[t + 1], ar, blocks, t);
   }
-  for (size_t t = started; t < T; ++t) bad[t] = parse_range(data, offs, cut[t], cut[t + 1], ar, blocks, t);
-  bad[0] = parse_range(data, offs, cut[0], cut[1], ar, blocks, 0);
-  for (auto& x : th) x.join();
   for (size_t t = 0; t < T; ++t)
     if (bad[t] < cut[t + 1]) return bad[t];
   return n;

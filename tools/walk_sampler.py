@@ -93,7 +93,7 @@ def main():
         if obj_o[i] != 0xFFFFFFFF:
             want[obj_o[i]].add(offs_o[i] - (1 if i % D else 0))
     sym = {k: symbolize(objs[k], v) for k, v in want.items()}
-    leaf_obj, leaf_fn, line_c, fn_c, pair_c = (collections.Counter() for _ in range(5))
+    leaf_obj, leaf_fn, line_c, fn_c, pair_c, chain_c = (collections.Counter() for _ in range(6))
     for i in range(n):
         fr = []
         for d in range(D):
@@ -114,6 +114,8 @@ def main():
                     break
             if ours:
                 break
+        own = [loc for ob, ch in fr for fn, loc in ch if loc.split(":")[0] in OURS]
+        chain_c[" <- ".join(own[:4])] += 1
         if ours is None:
             ours = ("(no engine frame)", "")
         line_c["%s  %s" % (ours[1], ours[0])] += 1
@@ -122,7 +124,8 @@ def main():
             pair_c["%s <- %s" % (fr[0][1][0][0][:40], ours[1])] += 1
     for title, cnt, k in (("leaf object", leaf_obj, 10), ("leaf function", leaf_fn, 25),
                           ("engine function (innermost own-source frame)", fn_c, 25),
-                          ("engine line", line_c, 60), ("outside the library: leaf <- engine line", pair_c, 30)):
+                          ("engine line", line_c, 60), ("outside the library: leaf <- engine line", pair_c, 30),
+                          ("engine call chains (innermost four own-source frames)", chain_c, 40)):
         print("\n%s, %% of samples:" % title)
         for f, c in cnt.most_common(k):
             print("  %6.2f%%  %s" % (100.0 * c / n, f[:160]))
