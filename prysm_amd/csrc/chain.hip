@@ -26,6 +26,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <pthread.h>
 #include <condition_variable>
 #include <unordered_map>
 #include <unordered_set>
@@ -2012,8 +2013,19 @@ struct WorkPool {
     }
   }
 };
+// A forked child has none of the parent's workers (and maybe a locked mutex): it starts a pool
+// of its own on first use.
+static std::atomic<WorkPool*> g_work_pool{nullptr};
+static void work_pool_after_fork() { g_work_pool.store(nullptr); }
 static WorkPool& work_pool() {
-  static WorkPool* p = new WorkPool();
+  static const bool hooked = (pthread_atfork(nullptr, nullptr, work_pool_after_fork), true);
+  (void)hooked;
+  WorkPool* p = g_work_pool.load();
+  if (!p) {
+    static std::mutex mk;
+    std::lock_guard<std::mutex> lk(mk);
+    if (!(p = g_work_pool.load())) g_work_pool.store(p = new WorkPool());
+  }
   return *p;
 }
 

@@ -53,3 +53,17 @@ def test_empty_and_tiny_calls(chain):
     for n in (1, 2, 3):
         o = np.ascontiguousarray(offs[: n + 1])
         assert _parse(data, o, 1) == _parse(data, o, 8)
+
+
+def test_parse_in_a_forked_child(chain):
+    """The parse's worker pool is per process: a child forked after the parent parsed starts
+    its own workers instead of waiting on the parent's (chain.hip work_pool)."""
+    import os
+    data, offs = chain
+    ref = _parse(data, offs, 8)
+    pid = os.fork()
+    if pid == 0:
+        os._exit(0 if _parse(data, offs, 8) == ref else 3)
+    _, st = os.waitpid(pid, 0)
+    assert os.WIFEXITED(st) and os.WEXITSTATUS(st) == 0
+    assert _parse(data, offs, 8) == ref
