@@ -2308,9 +2308,13 @@ static void stage_digests_arena(const std::vector<Block>& blocks, uint64_t nb, u
                                 uint64_t abytes, DigestBufs& D, hipStream_t s, hipEvent_t ev_blk, hipEvent_t ev_att) {
   hchk(hipStreamSynchronize(s), "sync");  // (a failed call's attestation part may still read D)
   const uint64_t nmsg = nb + 2 * na, aal = (abytes + 15) & ~15ull;
-  uint64_t kbytes = 0;
-  for (uint64_t bi = 0; bi < nb; ++bi)
-    for (auto& a : blocks[bi].atts) kbytes += 10 + a->sbh_len + 32 * a->obl.size();
+  std::vector<uint64_t> kb(nb + 1, 0);  // per block, where its Key() preimages start
+  for (uint64_t bi = 0; bi < nb; ++bi) {
+    uint64_t k = 0;
+    for (auto& a : blocks[bi].atts) k += 10 + a->sbh_len + 32 * a->obl.size();
+    kb[bi + 1] = kb[bi] + k;
+  }
+  const uint64_t kbytes = kb[nb];
   check(D.msgs.reserve(kbytes + 16));
   check(D.offs.reserve(2 * nmsg * 8 + 8));
   check(D.dig.reserve(nmsg * 32 + 32));
@@ -2330,29 +2334,45 @@ static void stage_digests_arena(const std::vector<Block>& blocks, uint64_t nb, u
   hchk(launch_b2b_spans(D.d_in.p, D.d_offs.p, D.d_offs.p + nmsg, nb, D.d_out.p, 32, s), "blake2b spans (blocks)");
   hchk(hipMemcpyAsync(D.dig.p, D.d_out.p, nb * 32, hipMemcpyDeviceToHost, s), "D2H digests");
   hchk(hipEventRecord(ev_blk, s), "event");
-  uint64_t ka = nb, kk = nb + na, kpos = 0;
-  for (uint64_t bi = 0; bi < nb; ++bi) {
-    for (auto& ap : blocks[bi].atts) {
-      const Att& a = *ap;
-      beg[ka] = (uint64_t)(a.base - ar.bytes);
-      end[ka] = beg[ka] + a.len;
-      ++ka;
-      // Key() preimage (types/attestation.go:61-77): a 10-byte buffer holding uvarint(slot)
-      // overwritten by uvarint(shard), ShardBlockHash, each oblique hash copied into a [32]byte
-      uint8_t* q = D.msgs.p + kpos;
-      std::memset(q, 0, 10);
-      put_uvarint(q, a.slot);
-      put_uvarint(q, a.shard);
-      std::memcpy(q + 10, a.at(a.sbh_off), a.sbh_len);
-      uint64_t kl = 10 + a.sbh_len;
-      for (auto& o : a.obl) {
-        const H32 h = copy32(a.at(o.first), o.second);
-        std::memcpy(q + kl, h.b, 32);
-        kl += 32;
+  // the attestation spans and Key() preimages of blocks [b0, b1), on the parse's worker pool
+  // (serial, this loop was ~3 % of the replay's samples, profiles/r03/walk_sampler_r3av.txt)
+  auto fill = [&](uint64_t b0, uint64_t b1) {
+    uint64_t ka = nb + ar.first[b0], kk = nb + na + ar.first[b0], kpos = kb[b0];
+    for (uint64_t bi = b0; bi < b1; ++bi) {
+      for (auto& ap : blocks[bi].atts) {
+        const Att& a = *ap;
+        beg[ka] = (uint64_t)(a.base - ar.bytes);
+        end[ka] = beg[ka] + a.len;
+        ++ka;
+        // Key() preimage (types/attestation.go:61-77): a 10-byte buffer holding uvarint(slot)
+        // overwritten by uvarint(shard), ShardBlockHash, each oblique hash copied into a [32]byte
+        uint8_t* q = D.msgs.p + kpos;
+        std::memset(q, 0, 10);
+        put_uvarint(q, a.slot);
+        put_uvarint(q, a.shard);
+        std::memcpy(q + 10, a.at(a.sbh_off), a.sbh_len);
+        uint64_t kl = 10 + a.sbh_len;
+        for (auto& o : a.obl) {
+          const H32 h = copy32(a.at(o.first), o.second);
+          std::memcpy(q + kl, h.b, 32);
+          kl += 32;
+        }
+        beg[kk] = aal + kpos;
+        end[kk++] = aal + kpos + kl;
+        kpos += kl;
       }
-      beg[kk] = aal + kpos;
-      end[kk++] = aal + kpos + kl;
-      kpos += kl;
+    }
+  };
+  const uint64_t T = std::min<uint64_t>((uint64_t)parse_threads(kbytes + 32 * na), nb / 64 + 1);
+  if (T <= 1) {
+    fill(0, nb);
+  } else {
+    std::vector<std::function<void()>> fns;
+    for (uint64_t t = 0; t < T; ++t) fns.push_back([&, t] { fill(nb * t / T, nb * (t + 1) / T); });
+    try {
+      work_pool().run(fns);
+    } catch (const std::system_error&) {  // no thread to be had
+      fill(0, nb);
     }
   }
   if (na) {
