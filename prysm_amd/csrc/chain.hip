@@ -1911,13 +1911,11 @@ static std::shared_ptr<CallArena> make_arena(const uint64_t* offs, uint64_t n, s
   return ar;
 }
 
-// Records per block (field 8 of BeaconBlock, messages.pb.go:224-232) as the prefix `first`
-// (n + 1 entries); PZ_EINVAL when the offsets are not monotone.  The canonical-form checks are
-// the parser's.
-static int count_per_block(const uint8_t* data, const uint64_t* offs, uint64_t n, std::vector<uint64_t>& first) {
-  first.assign(n + 1, 0);
-  for (uint64_t i = 0; i < n; ++i) {
-    if (offs[i + 1] < offs[i]) return fail(PZ_EINVAL, "offsets not monotone");
+// Blocks [i0, i1): their record counts (field 8 of BeaconBlock, messages.pb.go:224-232) into
+// cnt[i + 1]; returns the first block whose offsets are not monotone, or i1.
+static uint64_t count_range(const uint8_t* data, const uint64_t* offs, uint64_t i0, uint64_t i1, uint64_t* cnt) {
+  for (uint64_t i = i0; i < i1; ++i) {
+    if (offs[i + 1] < offs[i]) return i;
     Reader r{data + offs[i], data + offs[i + 1]};
     uint64_t c = 0;
     while (r.more()) {
@@ -1925,9 +1923,9 @@ static int count_per_block(const uint8_t* data, const uint64_t* offs, uint64_t n
       if ((key >> 3) == 8 && (key & 7) == 2) ++c;
       r.skip((uint32_t)(key & 7));
     }
-    first[i + 1] = first[i] + c;
+    cnt[i + 1] = c;
   }
-  return PZ_OK;
+  return i1;
 }
 
 // Blocks [b0, b1): copied into the arena and parsed, their oblique hashes into pool `pl`
@@ -2027,6 +2025,38 @@ static WorkPool& work_pool() {
     if (!(p = g_work_pool.load())) g_work_pool.store(p = new WorkPool());
   }
   return *p;
+}
+
+// Records per block as the prefix `first` (n + 1 entries); PZ_EINVAL when the offsets are not
+// monotone.  The canonical-form checks are the parser's.  Large calls count on the worker pool
+// (the count runs twice per call from Python, once to size the results: 0.3 ms each serially
+// per 10,000 blocks).
+static int count_per_block(const uint8_t* data, const uint64_t* offs, uint64_t n, std::vector<uint64_t>& first) {
+  first.assign(n + 1, 0);
+  const uint64_t bytes = n && offs[n] >= offs[0] ? offs[n] - offs[0] : 0;
+  const uint64_t T = n >= 2048 ? std::min<uint64_t>((uint64_t)parse_threads(bytes), n / 1024) : 1;
+  uint64_t bad = n;
+  if (T <= 1) {
+    bad = count_range(data, offs, 0, n, first.data());
+  } else {
+    std::vector<uint64_t> b(T, UINT64_MAX);
+    std::vector<std::function<void()>> fns;
+    for (uint64_t t = 0; t < T; ++t)
+      fns.push_back([&, t] { b[t] = count_range(data, offs, n * t / T, n * (t + 1) / T, first.data()); });
+    try {
+      work_pool().run(fns);
+      for (uint64_t t = 0; t < T; ++t)
+        if (b[t] < n * (t + 1) / T) {
+          bad = b[t];
+          break;
+        }
+    } catch (const std::system_error&) {  // no thread to be had
+      bad = count_range(data, offs, 0, n, first.data());
+    }
+  }
+  if (bad < n) return fail(PZ_EINVAL, "offsets not monotone");
+  for (uint64_t i = 0; i < n; ++i) first[i + 1] += first[i];
+  return PZ_OK;
 }
 
 // Blocks [0, n) over ar.obl.size() threads (ranges of about equal bytes; records need no
