@@ -2677,13 +2677,29 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
     msg_drain(g);
   }
   const uint8_t* md = g.m_pin.p;
-  for (size_t i = 0; i < nm; ++i) std::memcpy(ar[msg_att[i]].msg_digest, &md[i * 64], 64);
-  if (F.att_ev) {  // the processed attestations' Hash and Key (the batch path's second part)
-    hchk(hipEventSynchronize(F.att_ev), "event sync (attestation digests)");
-    for (size_t i = 0; i < nm; ++i) {
+  const bool hk = F.att_ev != nullptr;  // the processed attestations' Hash and Key too (the batch path's second part)
+  if (hk) hchk(hipEventSynchronize(F.att_ev), "event sync (attestation digests)");
+  // 128 B per processed attestation into the caller's results: on the worker pool when large
+  auto put = [&](size_t i0, size_t i1) {
+    for (size_t i = i0; i < i1; ++i) {
       const uint64_t ga = msg_att[i];
-      std::memcpy(ar[ga].hash, F.dg + (n + ga) * 32, 32);
-      std::memcpy(ar[ga].key, F.dg + (n + natt + ga) * 32, 32);
+      std::memcpy(ar[ga].msg_digest, &md[i * 64], 64);
+      if (hk) {
+        std::memcpy(ar[ga].hash, F.dg + (n + ga) * 32, 32);
+        std::memcpy(ar[ga].key, F.dg + (n + natt + ga) * 32, 32);
+      }
+    }
+  };
+  const size_t T = std::min<size_t>((size_t)parse_threads((uint64_t)nm * 128), nm / 2048 + 1);
+  if (T <= 1) {
+    put(0, nm);
+  } else {
+    std::vector<std::function<void()>> fns;
+    for (size_t t = 0; t < T; ++t) fns.push_back([&, t] { put(nm * t / T, nm * (t + 1) / T); });
+    try {
+      work_pool().run(fns);
+    } catch (const std::system_error&) {  // no thread to be had
+      put(0, nm);
     }
   }
 }
