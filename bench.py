@@ -164,15 +164,45 @@ HASH_KERNEL = "pz_b2b_fixed_persistent_kernel"
 CPU_SAMPLE_S = 8.0  # seconds of CPU work per cpu_baseline leg (three legs: ~25 s in all)
 
 
-def native_comm(dist, rank, world, local):
-    """The library's own RCCL communicator over the torchrun ranks: rank 0's ncclUniqueId
-    (pz_comm_unique_id) reaches the others through the launcher's TCP store."""
+def native_comm(dist, rank, world, local, shm=False):
+    """The library's own communicator over the torchrun ranks.  RCCL: rank 0's ncclUniqueId
+    (pz_comm_unique_id) reaches the others through the launcher's TCP store.  ``shm`` (the
+    gloo rehearsal, ranks sharing one GPU, which RCCL refuses): pz_comm_init_shm -- the same
+    collective call sequence staged through host memory, checked for divergence -- on a
+    shared-memory group whose name rank 0 passes through the store."""
     from prysm_amd.native import Comm
     store = dist.distributed_c10d._get_default_store()
+    if shm:
+        if rank == 0:
+            store.set("pz_shm_name", "/pz_bench_%d_%d" % (os.getpid(), int(time.time() * 1e3) % 1000000))
+        name = store.get("pz_shm_name").decode()
+        return Comm.shm(name, world, rank, local, timeout_ms=300000)
     if rank == 0:
         store.set("pz_comm_uid", Comm.unique_id())
     uid = store.get("pz_comm_uid")
     return Comm.rank(uid, world, rank, local)
+
+
+def all_ranks(ok, torch, dist, dev):
+    """True iff ``ok`` holds on every rank (MIN all-reduce; every rank must call it)."""
+    on_dev = dist.get_backend() == "nccl"
+    t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=dev if on_dev else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item() > 0.5)
+
+
+def hash_spot_check(records_np, d_out, k=65536):
+    """This rank's digests of its first and last ``k`` records against the C port (the
+    checker at N > 1, where the full-batch check of the N = 1 cpu_baseline leg does not run)."""
+    from oracle import cport
+    n = records_np.shape[0]
+    k = min(k, n)
+    got = d_out.view(n, 32)
+    ok = True
+    for lo in sorted({0, n - k}):
+        want = cport.hash_fixed(np.ascontiguousarray(records_np[lo:lo + k]), 512, 32)
+        ok &= bool(np.array_equal(got[lo:lo + k].cpu().numpy(), want))
+    return ok, "records [0, %d) and [%d, %d)" % (k, n - k, n)
 
 
 def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseline=True, comm=None):
@@ -280,16 +310,73 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                      "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": local_units * bpv},
     }
+    if world > 1 and native and comm is not None:
+        out["collectives"] = epoch_collective_time(args, de, comm, stream)
     del de
     if world == 1 and native and workload and not args.no_epoch_cold:
         out["cold"] = epoch_cold(args, torch, dev, nval, ninst, shuffled, workload, bpv=bpv)
     if rank == 0 and world == 1:
         out["parity"] = epoch_parity(inst, dev)
+    elif world > 1 and native:
+        ok, what = epoch_parity_sharded(inst, dev, comm)
+        out["parity"] = "%s, on every rank: %s" % (what, all_ranks(ok, torch, dist, dev))
     if world == 1 and baseline:
         out["single_instance"] = epoch_single_instance(args, torch, dev, nval, shuffled)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and baseline:
         out["cpu_baseline"] = epoch_cpu_baseline(inst)
     return out
+
+
+def epoch_collective_time(args, de, comm, stream):
+    """After the timed loop: ``args.steps`` more steps with the communicator's collectives
+    bracketed by HIP events on its stream (pz_comm_set_timing), so the timed loop itself
+    carries no extra event packets.  The collectives' own device time per step; the step's
+    device time beside it (the part of the collectives the two-part pipeline does not hide is
+    at most their sum)."""
+    import torch
+    for _ in range(2):
+        de.step()
+    stream.synchronize()
+    comm.set_timing(True)
+    comm.collective_time()  # restart the sum
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        de.step()
+    e1.record(stream)
+    stream.synchronize()
+    ms, count = comm.collective_time()
+    comm.set_timing(False)
+    return {"ms_per_step": ms / args.steps, "per_step": count / args.steps,
+            "step_device_ms_same_pass": e0.elapsed_time(e1) / args.steps,
+            "what": "device time of the communicator's collectives (HIP events on its stream of this rank, "
+                    "rank 0 reported), %d steps after the timed loop" % args.steps}
+
+
+def epoch_parity_sharded(inst, dev, comm):
+    """The checker at N > 1: instance 0 of the timed workload, one fresh step through a
+    sharded pz_epoch_state over the same communicator (a collective: every rank builds and
+    steps it), each rank's validator range (balances, next-cycle total, applied flag) and the
+    complete tallies and winners against oracle/epoch_np."""
+    from prysm_amd import _lib, synth
+    from prysm_amd.native import NativeEpoch
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from epoch_ref_helpers import oracle_epoch
+
+    one = synth.epoch_instances(inst, 1)
+    de = NativeEpoch(one, device=dev.index, comm=comm)
+    de.step()
+    de.sync()
+    de.tallies()
+    bal, scal, vote, total, win = de.results()
+    idx = de.validators()
+    de.free()
+    nb, applied, nxt, v, t, w = oracle_epoch(one, 0)
+    ok = (np.array_equal(bal[0], nb[idx]) and bool(scal[0, _lib.SCAL_APPLIED]) == applied
+          and int(scal[0, _lib.SCAL_NEXT_BAL]) == nxt and np.array_equal(vote[0], v)
+          and np.array_equal(total[0], t) and np.array_equal(win[0], w))
+    return ok, ("instance 0 of the timed workload, one step sharded over the %d ranks, each rank's %d validators "
+                "bit-exact vs oracle/epoch_np" % (comm.world, len(idx)))
 
 
 def epoch_cold(args, torch, dev, nval, ninst, shuffled, workload, nsets=4, bpv=EPOCH_BYTES_PER_VALIDATOR):
@@ -545,13 +632,15 @@ def wire_leg(args, torch, dist, dev, rank, world):
                      "kernel": "pz_wire_val_kernel (device time of the step, tile-status memset included)", "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": alg},
     }
+    # the checker (every rank): the first state's bytes against the C port
+    from oracle import cport
+    one = pb.Validators(nval, balance=bal[:nval], start_dynasty=start[:nval], end_dynasty=end[:nval])
+    want = cport.wire_validators(one)
+    got = d_out[:len(want)].cpu().numpy().tobytes()
+    ok = got == want if world == 1 else all_ranks(got == want, torch, dist, dev)
+    out["parity"] = "byte-exact vs the C port on the first state's %d bytes%s: %s" % (
+        len(want), "" if world == 1 else " of every rank", ok)
     if rank == 0 and world == 1:
-        # the checker: the first state's bytes against the C port, which is also the baseline
-        from oracle import cport
-        one = pb.Validators(nval, balance=bal[:nval], start_dynasty=start[:nval], end_dynasty=end[:nval])
-        want = cport.wire_validators(one)
-        got = d_out[:len(want)].cpu().numpy().tobytes()
-        out["parity"] = "byte-exact vs the C port on the first state's %d bytes: %s" % (len(want), got == want)
         if not args.no_cpu_baseline:
             reps, dt = cport.wire_validators_timed(one, min_seconds=CPU_SAMPLE_S / 2)
             out["cpu_baseline"] = {"value": reps * nval / dt, "unit": "records/s", "cores": 1, "kind": "port",
@@ -766,17 +855,19 @@ def attcheck_leg(args, torch, dist, dev, rank, world):
                      "kernel": "pz_att_check_x2_kernel", "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": alg},
     }
-    if rank == 0 and world == 1:
-        from oracle import cport
-        ns = 1 << 20
-        sub = {k: (v[:ns + 1] if k == "boffs" else v[:ns]) for k, v in cols.items() if k != "bits"}
-        port = cport.AttCheck(sub["slot"], sub["justified_slot"], sub["shard_id"], sub["n_oblique"], cols["bits"],
-                              sub["boffs"], sub["block_slot"])
-        try:
-            want = port.run(0, 0, 128, tab["arr_offs"], tab["arr_shard"], tab["arr_comm"], tab["coffs"])
-            got = status[:ns].cpu().numpy()
-            out["parity"] = "status of the first %d attestations equal to the C port: %s" % (
-                ns, bool(np.array_equal(got, want)))
+    from oracle import cport
+    ns = 1 << 20
+    sub = {k: (v[:ns + 1] if k == "boffs" else v[:ns]) for k, v in cols.items() if k != "bits"}
+    port = cport.AttCheck(sub["slot"], sub["justified_slot"], sub["shard_id"], sub["n_oblique"], cols["bits"],
+                          sub["boffs"], sub["block_slot"])
+    try:
+        want = port.run(0, 0, 128, tab["arr_offs"], tab["arr_shard"], tab["arr_comm"], tab["coffs"])
+        got = status[:ns].cpu().numpy()
+        ok = bool(np.array_equal(got, want))
+        ok = ok if world == 1 else all_ranks(ok, torch, dist, dev)
+        out["parity"] = "status of the first %d attestations%s equal to the C port: %s" % (
+            ns, "" if world == 1 else " of every rank", ok)
+        if rank == 0 and world == 1:
             if not args.no_cpu_baseline:
                 reps, t1 = 0, time.perf_counter()
                 while reps == 0 or time.perf_counter() - t1 < CPU_SAMPLE_S / 4:
@@ -786,8 +877,8 @@ def attcheck_leg(args, torch, dist, dev, rank, world):
                 out["cpu_baseline"] = {"value": reps * ns / dt, "unit": "attestations/s", "cores": 1, "kind": "port",
                                        "sample": "%d passes over %d attestations (AoS records, 1 thread, "
                                                  "oracle/c/attcheck_ref.c), %.2f s" % (reps, ns, dt)}
-        finally:
-            port.close()
+    finally:
+        port.close()
     return out
 
 
@@ -810,23 +901,44 @@ def replay_sharded_leg(args, torch, dist, dev, rank, world, comm):
     ch = BeaconChain(nval, comm=comm)
     torch.cuda.synchronize(dev)
     dist.barrier()
+    comm.set_timing(True)  # event pairs on the communicator's stream (the walk is host-bound)
+    comm.collective_time()
     t0 = time.perf_counter()
     br, ar = ch.process_serialized(data, offs)
     wall = time.perf_counter() - t0
     wall = max_over_ranks(wall, torch, dist, dev)
+    cms, cn = comm.collective_time()
+    comm.set_timing(False)
     roots = ch.roots()
+    # the checker, on every rank: its copy of the one chain against the C restatement of
+    # blockProcessing (every rank walks the same blocks, so every rank's results must be exact)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from replay_port_helpers import mismatches, port_replay
+    t1 = time.perf_counter()
+    p_out, p_roots = port_replay(data, offs, nval, len(ar))
+    bad = mismatches(br, ar, roots, p_out, p_roots)
+    ok = all_ranks(not bad, torch, dist, dev)
     out = {"metric": "sync-replay blocks/s (one chain over N GPUs)", "value": nb / wall, "unit": "blocks/s",
            "ms_per_block": wall / nb * 1e3,
            "config": {"workload": "the configs[4] chain (10,000 blocks, 65,536 validators) as ONE chain",
-                      "parallelism": "validator-range shard x%d of the vote cache and the epoch; RCCL all-reduce of "
-                                     "the 64 justification totals + the epoch's partial sums per transition" % world},
+                      "parallelism": "validator-range shard x%d of the vote cache and the epoch; all-reduce of "
+                                     "the 64 justification totals + the epoch's partial sums per transition (%s)"
+                                     % (world, "RCCL" if dist.get_backend() == "nccl" else "SHM rehearsal")},
            "processed": int((br["status"] == 0).sum()), "transitions": int(br["transition"].sum()),
+           "collectives": {"count": cn, "device_ms": cms, "per_transition": cn / max(1, int(br["transition"].sum())),
+                           "what": "rank 0's collectives over the timed replay, HIP events on the communicator stream"},
+           "parity": ("all %d blocks, %d attestations, the 4 state roots and %d vote-cache totals of every rank's copy "
+                      "vs oracle/c/replay_ref.c (%.1f s): %s" % (nb, len(ar), len(p_roots["vote_totals"]),
+                                                                 time.perf_counter() - t1,
+                                                                 "bit-exact on every rank" if ok else
+                                                                 "MISMATCH " + (", ".join(bad) or "on another rank"))),
            "cand_crystallized_root": roots.get("cand_crystallized", b"").hex()}
     return out
 
 
 PROF_PHASES = ("parse", "digest_batch", "checks", "vote_queue", "vote_flush", "state_recalc", "msg_digests", "walk",
-               "process", "count_atts", "flush_arena_wait", "msg_send", "msg_hash_log", "msg_wait")
+               "process", "count_atts", "flush_arena_wait", "msg_send", "msg_hash_log", "msg_wait",
+               "poll_fallbacks")  # the last is a count (tally-total polls that fell back to the event wait)
 
 
 def chain_phases_ms(ch):
@@ -838,7 +950,10 @@ def chain_phases_ms(ch):
     fn = _lib.lib.dll.pz_debug_chain_profile
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     k = fn(ch._h, pv, 16)
-    return {PROF_PHASES[i]: round(pv[i] * 1e3, 3) for i in range(min(k, len(PROF_PHASES))) if pv[i] > 0}
+    out = {PROF_PHASES[i]: round(pv[i] * 1e3, 3) for i in range(min(k, len(PROF_PHASES) - 1)) if pv[i] > 0}
+    if k >= len(PROF_PHASES):
+        out["poll_fallbacks"] = int(pv[len(PROF_PHASES) - 1])  # always reported, 0 included
+    return out
 
 
 def _compressions(nbytes):
@@ -948,18 +1063,22 @@ def replay_leg(args, torch, dist, dev, rank, world):
            "state_roots": state_roots,
            "cand_crystallized_root": root_vals["host_serial"].get("cand_crystallized", b"").hex(),
            "roofline": replay_roofline(blocks, offs, ar, wall, ch)}
+    # the checker (every rank, its own replica): the whole timed chain through the C
+    # restatement of the block pipeline (checker mode), compared with the GPU engine's records
+    # and roots
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from replay_port_helpers import mismatches, port_replay
+    t1 = time.perf_counter()
+    p_out, p_roots = port_replay(data, offs, nval, len(ar))
+    bad = mismatches(br, ar, root_vals["host_serial"], p_out, p_roots)
+    ok = not bad if world == 1 else all_ranks(not bad, torch, dist, dev)
+    out["parity"] = ("all %d blocks and %d attestations (digests, statuses, transitions), the 4 state roots and "
+                     "%d vote-cache totals vs the C restatement of blockProcessing (oracle/c/replay_ref.c), "
+                     "%.1f s%s: %s" % (nb, len(ar), len(p_roots["vote_totals"]), time.perf_counter() - t1,
+                                       "" if world == 1 else ", each rank's own chain",
+                                       "bit-exact" + ("" if world == 1 else " on every rank") if ok else
+                                       "MISMATCH " + (", ".join(bad) or "on another rank")))
     if rank == 0 and world == 1:
-        # the checker: the whole timed chain through the C restatement of the block pipeline
-        # (checker mode), compared with the GPU engine's records and roots
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        from replay_port_helpers import mismatches, port_replay
-        t1 = time.perf_counter()
-        p_out, p_roots = port_replay(data, offs, nval, len(ar))
-        bad = mismatches(br, ar, root_vals["host_serial"], p_out, p_roots)
-        out["parity"] = ("all %d blocks and %d attestations (digests, statuses, transitions), the 4 state roots and "
-                         "%d vote-cache totals vs the C restatement of blockProcessing (oracle/c/replay_ref.c), "
-                         "%.1f s: %s" % (nb, len(ar), len(p_roots["vote_totals"]), time.perf_counter() - t1,
-                                         "bit-exact" if not bad else "MISMATCH " + ", ".join(bad)))
         if not args.no_cpu_baseline:
             from oracle import cport
             sd, so = serialize_blocks(blocks[:args.cpu_replay_blocks])
@@ -1147,11 +1266,12 @@ def main():
         dist.init_process_group(args.backend)
     if args.backend == "gloo":
         local %= max(1, torch.cuda.device_count())
-        if world > 1 and args.epoch_path == "native":
-            # RCCL refuses two ranks on one device ("Duplicate GPU"), so the rehearsal runs the
-            # same orchestration through torch.distributed (labelled in epoch.config.path)
-            args.epoch_path = "torch"
-            args.epoch_path_note = "gloo rehearsal (ranks share a GPU; RCCL needs one device per rank)"
+        if world > 1:
+            # RCCL refuses two ranks on one device ("Duplicate GPU"): the rehearsal's library
+            # communicator is the SHM one (pz_comm_init_shm), which issues the RCCL backend's
+            # collective sequence through host memory and fails loudly if the ranks diverge
+            args.epoch_path_note = ("gloo rehearsal: ranks share a GPU, the library's collectives over "
+                                    "pz_comm_init_shm (host-staged; a code-path check, not a speed)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     _lib.lib.call("pz_init", local)
@@ -1190,13 +1310,21 @@ def main():
     if world > 1:
         wall = max_over_ranks(wall, torch, dist, dev)
 
+    # the checker at N > 1 (and at N = 1 without the cpu_baseline leg, whose full-batch check
+    # it replaces): this rank's first and last 65,536 digests against the C port
+    spot = None
+    if world > 1 or args.no_cpu_baseline:
+        ok, what = hash_spot_check(recs, d_out)
+        spot = "%s%s vs the C port (oracle/c/blake2b_ref.c): %s" % (
+            what, "" if world == 1 else " of every rank", ok if world == 1 else all_ranks(ok, torch, dist, dev))
+
     comm = None
     if world > 1 and not args.no_epoch and args.epoch_path == "native":
         # every rank must take the same path: agree on whether the communicator came up; a
         # failure ends the run (non-zero exit), it never switches to another path
         err = None
         try:
-            comm = native_comm(dist, rank, world, local)
+            comm = native_comm(dist, rank, world, local, shm=args.backend == "gloo")
         except Exception as e:
             err = "%s: %s" % (type(e).__name__, e)
         ok = torch.tensor([0.0 if err else 1.0], device=dev if dist.get_backend() == "nccl" else "cpu")
@@ -1270,6 +1398,8 @@ def main():
                 gpu = d_out.cpu().numpy().reshape(n, 32)
                 line["parity"] = "bit-exact vs cpu_baseline on all %d digests: %s" % (
                     n, bool(np.array_equal(gpu, digests)))
+        if spot is not None:
+            line["parity"] = spot
         line["launch"] = (os.environ.get("PZ_BENCH_LAUNCH", "torchrun (external launcher)") if world > 1
                           else "single process, one GPU")
         line["rccl_world"] = comm.world if comm is not None else None
@@ -1391,9 +1521,11 @@ def single_process_main(args):
     sync_all()
     wall = time.perf_counter() - t0
     kern_ms = max(e0.elapsed_time(e1) for e0, e1 in evs) / args.steps
+    spots = [hash_spot_check(synth.attestation_records_512(n, seed=2 + i), d_out[i]) for i in range(N)]
     hash_out = {"value": n * N * args.steps / wall, "unit": "hashes/s", "ms_per_step": wall / args.steps * 1e3,
                 "kernel_ms_max_over_devices": kern_ms,
-                "roofline_frac": n * 4 * OPS_PER_COMPRESSION / (kern_ms * 1e-3) / VALU_PEAK}
+                "roofline_frac": n * 4 * OPS_PER_COMPRESSION / (kern_ms * 1e-3) / VALU_PEAK,
+                "parity": "%s of every device vs the C port: %s" % (spots[0][1], all(ok for ok, _ in spots))}
     del d_in, d_out
     torch.cuda.set_device(devs[0])
 
@@ -1401,7 +1533,9 @@ def single_process_main(args):
     ninst = 16 * N
     shuffled = casper.shuffle_indices(b"A" + bytes(31), np.arange(nval, dtype=np.uint32))
     inst = synth.epoch_batch(nval, ninst, seed=3, shuffled=shuffled)
+    one = synth.epoch_instances(inst, 1)  # the checker's instance
     de = NativeEpoch(inst, device=0, comm=comm)
+    bpv = epoch_layout_bytes(inst, de.one_pass) or EPOCH_BYTES_PER_VALIDATOR
     del inst
     for _ in range(args.warmup + 30):
         de.step()
@@ -1411,14 +1545,42 @@ def single_process_main(args):
         de.step()
     de.sync()
     wall_e = time.perf_counter() - t0
+    comm.set_timing(True)
+    comm.collective_time()
+    for _ in range(args.steps):
+        de.step()
+    cms, cn = comm.collective_time()
+    comm.set_timing(False)
     epoch_out = {"value": nval * ninst * args.steps / wall_e, "unit": "validator-epochs/s",
                  "ms_per_step": wall_e / args.steps * 1e3,
                  "config": {"validators": nval, "instances_per_step": ninst,
                             "layout": "committee order, one-pass step" if de.one_pass else
                                       "committee order, two-pass step" if de.committee_order else "index order",
                             "shards": [list(de.shard(i)[:3]) for i in range(de.nlocal)]},
-                 "algorithmic_GBps_per_gpu": nval * 16 * EPOCH_BYTES_PER_VALIDATOR / (wall_e / args.steps) / 1e9}
+                 "bytes_per_validator_epoch": bpv,
+                 "algorithmic_GBps_per_gpu": nval * 16 * bpv / (wall_e / args.steps) / 1e9,
+                 "collectives": {"ms_per_step": cms / args.steps, "per_step": cn / args.steps,
+                                 "what": "device time of the grouped collectives (max over the devices), HIP events "
+                                         "on the communicator's streams, %d steps after the timed loop" % args.steps}}
     de.free()
+    # the checker: instance 0, one fresh sharded step, every device's range vs oracle/epoch_np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from epoch_ref_helpers import oracle_epoch
+    pe = NativeEpoch(one, device=0, comm=comm)
+    pe.step()
+    pe.sync()
+    pe.tallies()
+    nb, applied, nxt, v, t, w = oracle_epoch(one, 0)
+    ok = True
+    for i in range(pe.nlocal):
+        bal, scal, vote, total, win = pe.results(i)
+        idx = pe.validators(i)
+        ok &= (np.array_equal(bal[0], nb[idx]) and bool(scal[0, _lib.SCAL_APPLIED]) == applied
+               and int(scal[0, _lib.SCAL_NEXT_BAL]) == nxt and np.array_equal(vote[0], v)
+               and np.array_equal(total[0], t) and np.array_equal(win[0], w))
+    pe.free()
+    epoch_out["parity"] = ("instance 0, one sharded step, every device's validator range bit-exact vs "
+                           "oracle/epoch_np: %s" % ok)
     # configs[4] as one chain over the N devices of this process (pz_chain_new_comm)
     from prysm_amd.blockchain import BeaconChain, serialize_blocks
     blocks = synth.chain_blocks(65536, args.replay_blocks, seed=6)
@@ -1426,11 +1588,16 @@ def single_process_main(args):
     BeaconChain(65536, comm=comm).process_serialized(*serialize_blocks(blocks[:130]))
     ch = BeaconChain(65536, comm=comm)
     t0 = time.perf_counter()
-    br, _ = ch.process_serialized(data, offs)
+    br, ar = ch.process_serialized(data, offs)
     wall_r = time.perf_counter() - t0
     roots = ch.roots()
+    from replay_port_helpers import mismatches, port_replay
+    p_out, p_roots = port_replay(data, offs, 65536, len(ar))
+    bad = mismatches(br, ar, roots, p_out, p_roots)
     replay_out = {"value": args.replay_blocks / wall_r, "unit": "blocks/s", "transitions": int(br["transition"].sum()),
                   "processed": int((br["status"] == 0).sum()),
+                  "parity": "every block, attestation, root and vote-cache total vs oracle/c/replay_ref.c: %s" % (
+                      "bit-exact" if not bad else "MISMATCH " + ", ".join(bad)),
                   "cand_crystallized_root": roots.get("cand_crystallized", b"").hex()}
     del ch
     line = {"metric": METRIC, "mode": "single process, %d GPUs (pz_init_devices -> ncclCommInitAll)" % N,

@@ -412,7 +412,15 @@ int pz_dev_epoch_gather_compact(const pz_epoch_batch* b, const uint64_t* gathere
  *                         pz_comm_unique_id passed to every rank by the launcher;
  *   pz_comm_init_loopback `world` ranks in this process on ONE device, collectives by device
  *                         copies and a sum kernel (no RCCL): the sharded code path on a
- *                         one-GPU machine (tests).
+ *                         one-GPU machine (tests);
+ *   pz_comm_init_shm      one process per rank, ranks free to share a device: collectives
+ *                         staged through host memory and a POSIX shared-memory group named
+ *                         `name` (rank 0 creates it, O_EXCL; unlinked once every rank attached),
+ *                         synchronous.  The one-process-per-GPU call sequence on a one-GPU
+ *                         machine (tests, the bench's gloo rehearsal).  Every collective checks
+ *                         that all ranks issued the same one (kind and sizes): a divergence fails
+ *                         with PZ_EINVAL naming both calls, a rank missing for timeout_ms (0:
+ *                         60 s) with PZ_EDEVICE -- where RCCL would hang.
  * librccl is resolved at run time (the copy already mapped into the process, else /opt/rocm's). */
 #define PZ_COMM_ID_BYTES 128
 typedef struct pz_comm pz_comm;
@@ -420,6 +428,14 @@ int  pz_comm_unique_id(uint8_t id[PZ_COMM_ID_BYTES]);
 int  pz_comm_init_rank(const uint8_t id[PZ_COMM_ID_BYTES], int world, int rank, int device, pz_comm** out);
 int  pz_init_devices(int ndev, const int* devices /* NULL: 0..ndev-1 */, pz_comm** out);
 int  pz_comm_init_loopback(int world, int device, pz_comm** out);
+int  pz_comm_init_shm(const char* name, int world, int rank, int device, uint32_t timeout_ms, pz_comm** out);
+/* Collective timing: with timing on, every collective is bracketed by a HIP event pair on the
+ * communicator's stream of each local rank (after its wait for the compute stream: the
+ * collective's own time, exposed or overlapped).  pz_comm_collective_time returns the sum over
+ * the collectives since the last call (the max over local ranks for each) and their count, and
+ * restarts the sum; it waits for the pending collectives. */
+int  pz_comm_set_timing(pz_comm* comm, int on);
+int  pz_comm_collective_time(pz_comm* comm, double* ms, uint64_t* count);
 /* world = ranks in the partition, nlocal = ranks this process drives (global ranks
  * first_rank .. first_rank+nlocal-1). */
 int  pz_comm_size(const pz_comm* comm, int* world, int* nlocal, int* first_rank);
@@ -616,7 +632,12 @@ int  pz_chain_new_comm(uint64_t nval, pz_comm* comm, pz_chain** out);
 void pz_chain_free(pz_chain* chain);
 /* Number of attestations in a batch of serialized blocks (host only; sizes att_out). */
 int  pz_count_attestations(const uint8_t* blocks, const uint64_t* offsets, uint64_t n, uint64_t* count);
-/* att_out: capacity att_cap >= the total number of attestations in the batch. */
+/* att_out: capacity att_cap >= the total number of attestations in the batch.
+ * A reference panic returns PZ_EINDEX and poisons the chain.  A stateRecalc's device epoch
+ * (processCrosslinks, CalculateRewards) is collected at the next transition or at the end of
+ * the call, so its panic is reported up to 63 blocks later: the message names the transition's
+ * block index and slot, and the result rows of the blocks after that block are undefined (the
+ * reference stops at it, blockchain/service.go:345-354). */
 int  pz_chain_process_blocks(pz_chain* chain, const uint8_t* blocks, const uint64_t* offsets, uint64_t n,
                              pz_block_result* block_out, pz_att_result* att_out, uint64_t att_cap);
 /* State roots (types/state.go:138-149, 237-248): out[0..31] chain ActiveState, [32..63] chain

@@ -106,6 +106,9 @@ SIGNATURES = {
     "pz_comm_init_rank": [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp],
     "pz_init_devices": [ctypes.c_int, vp, vp],
     "pz_comm_init_loopback": [ctypes.c_int, ctypes.c_int, vp],
+    "pz_comm_init_shm": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, u32, vp],
+    "pz_comm_set_timing": [vp, ctypes.c_int],
+    "pz_comm_collective_time": [vp, vp, vp],
     "pz_comm_size": [vp, c_intp, c_intp, c_intp],
     "pz_comm_device": [vp, ctypes.c_int, c_intp],
     "pz_comm_free": [vp],

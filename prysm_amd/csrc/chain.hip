@@ -467,7 +467,11 @@ static PinPool& pin_pool() {
 struct PinBuf {
   uint8_t* p = nullptr;
   size_t n = 0;
-  void* d = nullptr;  // its device address, looked up once (a runtime call per use showed in the walk)
+  // its device address for each device that reads it, looked up once per device (a runtime
+  // call per use showed in the walk).  hipHostMalloc memory is mapped into every device's
+  // address space, but the device address is asked of the device that will use it: a chain
+  // over several devices (pz_chain_new_comm) reads the tally arena from every rank's device.
+  std::vector<std::pair<int, void*>> d;
   int reserve(size_t bytes) {
     if (bytes <= n && p) return PZ_OK;
     release();
@@ -493,12 +497,19 @@ struct PinBuf {
     n = want;
     return PZ_OK;
   }
-  int dev(void** out) {
-    if (!d) {
-      hipError_t e = hipHostGetDevicePointer(&d, p, 0);
-      if (e != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer");
-    }
-    *out = d;
+  // (the calling thread's current device must be `device`: hipHostGetDevicePointer answers
+  // for the current device)
+  int dev(int device, void** out) {
+    for (const auto& x : d)
+      if (x.first == device) {
+        *out = x.second;
+        return PZ_OK;
+      }
+    void* q = nullptr;
+    hipError_t e = hipHostGetDevicePointer(&q, p, 0);
+    if (e != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer");
+    d.emplace_back(device, q);
+    *out = q;
     return PZ_OK;
   }
   void release() {
@@ -514,7 +525,7 @@ struct PinBuf {
     }
     if (p) (void)hipHostFree(p);
     p = nullptr;
-    d = nullptr;
+    d.clear();
     n = 0;
   }
   ~PinBuf() { release(); }
@@ -568,7 +579,9 @@ struct PinVec {
 
 enum ProfSlot {
   kProfParse, kProfHash1, kProfCheck, kProfQueue, kProfFlush, kProfRecalc, kProfMsgHash, kProfWalk, kProfProcess,
-  kProfCount, kProfFlushWait, kProfMsgSend, kProfMsgLog, kProfMsgWait, kProfSlots
+  kProfCount, kProfFlushWait, kProfMsgSend, kProfMsgLog, kProfMsgWait,
+  kProfPollFallback,  // a count, not seconds: sequence-word polls that fell back to the event wait
+  kProfSlots
 };
 
 // Queued attestations that force a tally flush before the next stateRecalc.  Flushing more
@@ -683,6 +696,7 @@ struct Engine {
     std::vector<AttP> pending;  // the attestations it ran over (a winner's ShardBlockHash)
     std::shared_ptr<CState> src, dst;  // the state it read (xl mutated in place), the new state
     uint64_t block_slot = 0;
+    uint64_t block_index = 0;  // the transition block's index in the call (named by a panic)
     size_t nrec = 0;
   } deferred;
   // hashing scratch (rank 0)
@@ -957,7 +971,7 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr) 
     // the pack crosses PCIe in a kernel of this stream (a copy-engine H2D costs ~13 us more on
     // the transition's critical path: the kernel behind it waits for the engine's signal)
     void* src = nullptr;
-    check(g.q_arena.dev(&src));
+    check(g.q_arena.dev(r.dev, &src));
     hchk(launch_stage_h2d(src, r.d_qpack.p, total, r.s), "stage H2D");
     if (!gather) {  // (gathering: g.ev_totals, later in the stream, frees the arena)
       if (!r.q_ev) hchk(hipEventCreateWithFlags(&r.q_ev, hipEventDisableTiming), "event");
@@ -997,7 +1011,7 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr) 
     if (gather) {
       check(g.tot_pin.reserve((kJustifySlots + 2) * 8));
       void* dp = nullptr;
-      check(g.tot_pin.dev(&dp));
+      check(g.tot_pin.dev(r.dev, &dp));
       v.gather_out = static_cast<uint64_t*>(dp);
       v.ticket = r.d_leader.p + 2;
       v.gq = *gq;
@@ -1040,7 +1054,7 @@ static void tally_gather_enqueue(Engine& g, const VoteGatherSlots& q) {
     if (g.world == 1) {
       // one rank: the gather stores straight into the pinned totals (no D2H copy behind it)
       void* dp = nullptr;
-      check(g.tot_pin.dev(&dp));
+      check(g.tot_pin.dev(r.dev, &dp));
       hchk(launch_vote_gather(r.totals.p, q, r.d_err.p, static_cast<uint64_t*>(dp), r.s), "vote gather");
       return;
     }
@@ -1076,6 +1090,7 @@ static void tally_gather_finish(Engine& g) {
       if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
     }
     std::atomic_thread_fence(std::memory_order_acquire);
+    if (*sq != g.gather_seq) g.prof[kProfPollFallback] += 1;  // reported, so a fallback is not silent
     if (*sq == g.gather_seq) {
       // every rank's flush is done: its stage kernel preceded the leader pass
       g.q_arena_busy = false;
@@ -1407,10 +1422,18 @@ static void epoch_collect(Engine& g) {
   pending.swap(D.pending);
   CState& C = *D.src;
   std::vector<Crosslink>& xl = *C.xl;
-  if (scal[kErrXl]) throw Panic{"processCrosslinks: index out of range (committee member, bitfield or shard)"};
+  // The epoch is collected up to 63 blocks after its transition (or at the end of the call), so
+  // a panic names the transition block; the result rows of the blocks after it are undefined
+  // (the reference stops at that block; include/prysm_hip.h, pz_chain_process_blocks).
+  char where[160];
+  snprintf(where, sizeof where, " (stateRecalc of block %llu of this call, slot %llu; result rows after that block are undefined)",
+           (unsigned long long)D.block_index, (unsigned long long)D.block_slot);
+  if (scal[kErrXl])
+    throw Panic{std::string("processCrosslinks: index out of range (committee member, bitfield or shard)") + where};
   const uint64_t dep = scal[kPop] * PZ_DEFAULT_BALANCE;
   const bool thr = dep * 3ull >= C.tdep * 2ull;
-  if (thr && scal[kNact] > 0 && scal[kErrRwd]) throw Panic{"CalculateRewards: CheckBit index out of range (incentives.go:23)"};
+  if (thr && scal[kNact] > 0 && scal[kErrRwd])
+    throw Panic{std::string("CalculateRewards: CheckBit index out of range (incentives.go:23)") + where};
   if (!pending.empty() && !xl.empty()) {
     for (size_t s = 0; s < xl.size() && s < D.nrec; ++s) {
       if (win[s] == 0xffffffffu) continue;
@@ -1427,7 +1450,8 @@ static void epoch_collect(Engine& g) {
 }
 
 // stateRecalc (core.go:398-497) -> (new C, new A).
-static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slot, CP* nc_out, AP* na_out) {
+static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slot, uint64_t block_index, CP* nc_out,
+                         AP* na_out) {
   // The previous transition's epoch first: this one reads the crosslink records and the
   // TotalDeposits it produced (long since done: 64 blocks of walk have passed).
   epoch_collect(g);
@@ -1455,6 +1479,7 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   g.deferred.src = C;
   g.deferred.dst = nc;
   g.deferred.block_slot = block_slot;
+  g.deferred.block_index = block_index;
   tally_gather_finish(g);
   std::memcpy(tot.data(), g.tot_pin.p, kCycle * 8);
   for (uint64_t i = 0; i < kCycle; ++i) {
@@ -1997,11 +2022,13 @@ struct WorkPool {
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
       cv.wait(lk, [this] { return next < jobs.size(); });
-      std::function<void()> f = jobs[next++];
+      // by pointer: the batch's vector is only cleared after every job has finished (run()), and a
+      // copy here would sit outside the try (a throwing copy would end the process)
+      std::function<void()>* f = &jobs[next++];
       lk.unlock();
       bool bad = false;
       try {
-        f();
+        (*f)();
       } catch (...) {
         bad = true;
       }
@@ -2052,6 +2079,8 @@ static int count_per_block(const uint8_t* data, const uint64_t* offs, uint64_t n
         }
     } catch (const std::system_error&) {  // no thread to be had
       bad = count_range(data, offs, 0, n, first.data());
+    } catch (int code) {  // a worker's job threw (WorkPool::run): both C-ABI callers return it
+      return fail(code, "block count: a worker thread failed");
     }
   }
   if (bad < n) return fail(PZ_EINVAL, "offsets not monotone");
@@ -2650,7 +2679,7 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
       r.transition = 1;
       CP nc;
       AP na;
-      state_recalc(g, C, A, b.slot, &nc, &na);
+      state_recalc(g, C, A, b.slot, bi, &nc, &na);
       C = nc;
       A = na;
       if (mbatch && g.m_rec.n - g.m_sent >= mbatch) msg_send(g);  // (the walk just waited on the device)

@@ -10,6 +10,12 @@
 //   LOOPBACK  every rank lives in this process on ONE device; collectives are device copies
 //             and one summing kernel.  It exists so that the sharded code paths (the same
 //             ones RCCL drives) run on a one-GPU box in the parity tests.
+//   SHM       one process per rank, the ranks free to share a device: each collective is a
+//             D2H of the rank's buffer, a round through a POSIX shared-memory group
+//             (shm_group.h) and an H2D of the result, synchronous on the host.  It runs the
+//             one-process-per-GPU form (the bench under torchrun) on a one-GPU box, and it checks
+//             that every rank issued the same collective sequence (a divergence RCCL would turn
+//             into a hang fails the call with both ranks' calls named).
 //
 // A collective is ordered after each local rank's compute stream (an event), runs on the
 // rank's collective stream, and marks completion with a per-rank event the caller waits on
@@ -17,6 +23,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+
+#include "shm_group.h"
 
 #include <cstddef>
 #include <cstdint>
@@ -45,7 +53,7 @@ int rccl_api(const RcclApi** out);
 }  // namespace pz
 
 struct pz_comm {
-  enum Kind { RCCL, LOOPBACK } kind = RCCL;
+  enum Kind { RCCL, LOOPBACK, SHM } kind = RCCL;
   int world = 1;      // ranks in the partition
   int nlocal = 1;     // ranks driven by this process
   int rank0 = 0;      // global rank of local rank 0 (local ranks are contiguous)
@@ -55,6 +63,20 @@ struct pz_comm {
   std::vector<hipEvent_t> ev_in;      // per local rank: compute stream -> collective stream
   const pz::RcclApi* api = nullptr;
   uint64_t** d_ptrs = nullptr;        // LOOPBACK: device array of the ranks' buffer pointers
+  pz::ShmGroup* shm = nullptr;        // SHM: the process group
+  std::vector<uint8_t> shm_stage;     // SHM: host copy of the rank's buffer
+
+  // Collective timing (pz_comm_set_timing): an event pair on every local rank's collective
+  // stream around each collective; pz_comm_collective_time sums the pairs (max over the local
+  // ranks per collective) and recycles the events.
+  bool timing = false;
+  struct TimedOp {
+    std::vector<hipEvent_t> t0, t1;
+  };
+  std::vector<TimedOp> timed;
+  bool time_open = false;  // the last collective's start was recorded (its end is due)
+  std::vector<hipEvent_t> ev_pool;
+  hipStream_t cs(int i) const { return cstream[kind == LOOPBACK ? 0 : i]; }
 
   // Sum all-reduce of `count` u64 in place: bufs[i] is local rank i's buffer; the collective
   // starts after everything enqueued so far on compute[i]; done[i] is recorded when local

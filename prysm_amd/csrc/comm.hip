@@ -5,8 +5,10 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
+#include <string>
 
 #include "runtime.h"
 
@@ -101,8 +103,36 @@ static int order_after(pz_comm* c, const hipStream_t* compute) {
   for (int i = 0; i < c->nlocal; ++i) {
     hipError_t e = hipSetDevice(c->dev[i]);
     if (e == hipSuccess) e = hipEventRecord(c->ev_in[i], compute[i]);
-    if (e == hipSuccess) e = hipStreamWaitEvent(c->cstream[c->kind == pz_comm::LOOPBACK ? 0 : i], c->ev_in[i], 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->cs(i), c->ev_in[i], 0);
     if (e != hipSuccess) return hip_fail(e, "collective ordering");
+  }
+  return PZ_OK;
+}
+
+static hipEvent_t timing_event(pz_comm* c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// With timing on: the start of a collective on every local rank's collective stream (after
+// order_after, so the wait for the compute stream is not counted).
+static int time_begin(pz_comm* c) {
+  if (!c->timing) return PZ_OK;
+  c->timed.emplace_back();
+  c->time_open = true;
+  pz_comm::TimedOp& t = c->timed.back();
+  for (int i = 0; i < c->nlocal; ++i) {
+    (void)hipSetDevice(c->dev[i]);
+    t.t0.push_back(timing_event(c));
+    t.t1.push_back(timing_event(c));
+    hipError_t e = hipEventRecord(t.t0.back(), c->cs(i));
+    if (e != hipSuccess) return hip_fail(e, "collective timing event");
   }
   return PZ_OK;
 }
@@ -110,14 +140,36 @@ static int order_after(pz_comm* c, const hipStream_t* compute) {
 static int mark_done(pz_comm* c, hipEvent_t* done) {
   for (int i = 0; i < c->nlocal; ++i) {
     hipError_t e = hipSetDevice(c->dev[i]);
-    if (e == hipSuccess) e = hipEventRecord(done[i], c->cstream[c->kind == pz_comm::LOOPBACK ? 0 : i]);
+    if (e == hipSuccess && c->time_open) e = hipEventRecord(c->timed.back().t1[i], c->cs(i));
+    if (e == hipSuccess) e = hipEventRecord(done[i], c->cs(i));
     if (e != hipSuccess) return hip_fail(e, "collective completion event");
   }
+  c->time_open = false;
+  return PZ_OK;
+}
+
+// SHM: the local rank's buffer to host memory, through the process group, and back -- on the
+// collective stream, which is drained on both sides (the group is synchronous).
+template <typename F>
+static int shm_run(pz_comm* c, void* dbuf, size_t down_bytes, size_t up_bytes, size_t up_offset, F&& collective) {
+  (void)hipSetDevice(c->dev[0]);
+  c->shm_stage.resize(std::max(down_bytes, up_offset + up_bytes));
+  hipError_t e = hipSuccess;
+  if (down_bytes) e = hipMemcpyAsync(c->shm_stage.data(), dbuf, down_bytes, hipMemcpyDeviceToHost, c->cstream[0]);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->cstream[0]);
+  if (e != hipSuccess) return hip_fail(e, "shm collective: D2H");
+  std::string err;
+  int rc = collective(c->shm_stage.data(), &err);
+  if (rc) return fail(rc, "%s", err.c_str());
+  if (up_bytes) e = hipMemcpyAsync(dbuf, c->shm_stage.data() + up_offset, up_bytes, hipMemcpyHostToDevice, c->cstream[0]);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->cstream[0]);
+  if (e != hipSuccess) return hip_fail(e, "shm collective: H2D");
   return PZ_OK;
 }
 
 int pz_comm::allreduce_u64(uint64_t* const* bufs, size_t count, const hipStream_t* compute, hipEvent_t* done) {
   int rc = order_after(this, compute);
+  if (!rc) rc = time_begin(this);
   if (rc) return rc;
   if (count && world > 1) {
     if (kind == LOOPBACK) {
@@ -128,6 +180,11 @@ int pz_comm::allreduce_u64(uint64_t* const* bufs, size_t count, const hipStream_
                          world, (uint64_t)count);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return hip_fail(e, "pz_loopback_sum_kernel");
+    } else if (kind == SHM) {
+      rc = shm_run(this, bufs[0], count * 8, count * 8, 0, [&](uint8_t* h, std::string* err) {
+        return shm->sum_u64(reinterpret_cast<uint64_t*>(h), count, err);
+      });
+      if (rc) return rc;
     } else {
       if (nlocal > 1) api->GroupStart();
       ncclResult_t r = ncclSuccess;
@@ -146,6 +203,7 @@ int pz_comm::allreduce_u64(uint64_t* const* bufs, size_t count, const hipStream_
 int pz_comm::allreduce_sum_min(uint64_t* const* sbufs, size_t scount, uint32_t* const* mbufs, size_t mcount,
                                const hipStream_t* compute, hipEvent_t* done) {
   int rc = order_after(this, compute);
+  if (!rc) rc = time_begin(this);
   if (rc) return rc;
   if (world > 1 && (scount || mcount)) {
     if (kind == LOOPBACK) {
@@ -164,6 +222,25 @@ int pz_comm::allreduce_sum_min(uint64_t* const* sbufs, size_t scount, uint32_t* 
       }
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return hip_fail(e, "loopback sum/min");
+    } else if (kind == SHM) {
+      // both buffers through one group round sequence: stage = [sum words][min words]
+      (void)hipSetDevice(dev[0]);
+      shm_stage.resize(scount * 8 + mcount * 4);
+      hipError_t e = hipSuccess;
+      if (scount) e = hipMemcpyAsync(shm_stage.data(), sbufs[0], scount * 8, hipMemcpyDeviceToHost, cstream[0]);
+      if (e == hipSuccess && mcount)
+        e = hipMemcpyAsync(shm_stage.data() + scount * 8, mbufs[0], mcount * 4, hipMemcpyDeviceToHost, cstream[0]);
+      if (e == hipSuccess) e = hipStreamSynchronize(cstream[0]);
+      if (e != hipSuccess) return hip_fail(e, "shm collective: D2H");
+      std::string err;
+      rc = shm->sum_min(reinterpret_cast<uint64_t*>(shm_stage.data()), scount,
+                        reinterpret_cast<uint32_t*>(shm_stage.data() + scount * 8), mcount, &err);
+      if (rc) return fail(rc, "%s", err.c_str());
+      if (scount) e = hipMemcpyAsync(sbufs[0], shm_stage.data(), scount * 8, hipMemcpyHostToDevice, cstream[0]);
+      if (e == hipSuccess && mcount)
+        e = hipMemcpyAsync(mbufs[0], shm_stage.data() + scount * 8, mcount * 4, hipMemcpyHostToDevice, cstream[0]);
+      if (e == hipSuccess) e = hipStreamSynchronize(cstream[0]);
+      if (e != hipSuccess) return hip_fail(e, "shm collective: H2D");
     } else {
       api->GroupStart();
       ncclResult_t r = ncclSuccess;
@@ -184,14 +261,28 @@ int pz_comm::allreduce_sum_min(uint64_t* const* sbufs, size_t scount, uint32_t* 
 int pz_comm::allgather(const void* const* send, void* const* recv, size_t bytes, const hipStream_t* compute,
                        hipEvent_t* done) {
   int rc = order_after(this, compute);
+  if (!rc) rc = time_begin(this);
   if (rc) return rc;
   if (bytes) {
-    if (kind == LOOPBACK || world == 1) {
+    if (kind == SHM && world > 1) {
+      // D2H of this rank's contribution, the gather through the group, H2D of all of it
+      (void)hipSetDevice(dev[0]);
+      shm_stage.resize(bytes + (size_t)world * bytes);
+      hipError_t e = hipMemcpyAsync(shm_stage.data(), send[0], bytes, hipMemcpyDeviceToHost, cstream[0]);
+      if (e == hipSuccess) e = hipStreamSynchronize(cstream[0]);
+      if (e != hipSuccess) return hip_fail(e, "shm all-gather: D2H");
+      std::string err;
+      rc = shm->allgather(shm_stage.data(), shm_stage.data() + bytes, bytes, &err);
+      if (rc) return fail(rc, "%s", err.c_str());
+      e = hipMemcpyAsync(recv[0], shm_stage.data() + bytes, (size_t)world * bytes, hipMemcpyHostToDevice, cstream[0]);
+      if (e == hipSuccess) e = hipStreamSynchronize(cstream[0]);
+      if (e != hipSuccess) return hip_fail(e, "shm all-gather: H2D");
+    } else if (kind == LOOPBACK || world == 1) {
       for (int i = 0; i < nlocal; ++i) {
         (void)hipSetDevice(dev[i]);
         for (int r = 0; r < world; ++r) {
           hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(recv[i]) + (size_t)r * bytes, send[r], bytes,
-                                        hipMemcpyDeviceToDevice, cstream[kind == LOOPBACK ? 0 : i]);
+                                        hipMemcpyDeviceToDevice, cs(i));
           if (e != hipSuccess) return hip_fail(e, "loopback all-gather copy");
         }
       }
@@ -222,6 +313,12 @@ pz_comm::~pz_comm() {
   if (api)
     for (ncclComm_t n : nccl)
       if (n) api->CommDestroy(n);
+  for (TimedOp& t : timed) {
+    for (hipEvent_t e : t.t0) (void)hipEventDestroy(e);
+    for (hipEvent_t e : t.t1) (void)hipEventDestroy(e);
+  }
+  for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
+  delete shm;
 }
 
 // Creates the per-local-rank streams/events after dev[] is set.
@@ -332,6 +429,60 @@ int pz_comm_init_loopback(int world, int device, pz_comm** out) {
     return rc;
   }
   *out = c;
+  return PZ_OK;
+}
+
+int pz_comm_init_shm(const char* name, int world, int rank, int device, uint32_t timeout_ms, pz_comm** out) {
+  if (!name || !out) return fail(PZ_EINVAL, "null pointer");
+  *out = nullptr;
+  if (world < 1 || rank < 0 || rank >= world) return fail(PZ_EINVAL, "rank %d of world %d", rank, world);
+  pz_comm* c = new pz_comm();
+  c->kind = pz_comm::SHM;
+  c->world = world;
+  c->nlocal = 1;
+  c->rank0 = rank;
+  c->dev = {device};
+  int rc = comm_setup(c);
+  if (rc) {
+    delete c;
+    return rc;
+  }
+  std::string err;
+  rc = ShmGroup::open(name, world, rank, timeout_ms ? timeout_ms : 60000, uint64_t(8) << 20, &c->shm, &err);
+  if (rc) {
+    delete c;
+    return fail(rc, "%s", err.c_str());
+  }
+  *out = c;
+  return PZ_OK;
+}
+
+int pz_comm_set_timing(pz_comm* c, int on) {
+  if (!c) return fail(PZ_EINVAL, "comm is null");
+  c->timing = on != 0;
+  return PZ_OK;
+}
+
+int pz_comm_collective_time(pz_comm* c, double* ms, uint64_t* count) {
+  if (!c || !ms || !count) return fail(PZ_EINVAL, "null pointer");
+  double sum = 0;
+  for (pz_comm::TimedOp& t : c->timed) {
+    float mx = 0;
+    for (size_t i = 0; i < t.t0.size(); ++i) {
+      (void)hipSetDevice(c->dev[i]);
+      hipError_t e = hipEventSynchronize(t.t1[i]);
+      float v = 0;
+      if (e == hipSuccess) e = hipEventElapsedTime(&v, t.t0[i], t.t1[i]);
+      if (e != hipSuccess) return hip_fail(e, "collective timing");
+      mx = std::max(mx, v);
+      c->ev_pool.push_back(t.t0[i]);
+      c->ev_pool.push_back(t.t1[i]);
+    }
+    sum += mx;
+  }
+  *ms = sum;
+  *count = c->timed.size();
+  c->timed.clear();
   return PZ_OK;
 }
 

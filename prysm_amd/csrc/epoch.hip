@@ -925,8 +925,21 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
   // single launch over B instances (launch_epoch_multi): ONE's per-block prologue, inst = blockIdx.x
   constexpr bool MULTI = (MODE & 2048) != 0;
   constexpr bool PRO = ONE || MULTI;  // each block counts its instance's bitfields itself
-  const uint64_t inst = (MODE & 32) ? blockIdx.y : blockIdx.x;
-  const uint64_t grp = (MODE & 32) ? blockIdx.x : blockIdx.y;
+  // MODE & 4096: a 1-D grid mapped XCD-aware.  Blocks are dealt round-robin over the 8 XCDs
+  // (MI355X_MICROARCH.md, "Workgroup dispatch"; for speed only, the map is a bijection either
+  // way): block L runs on XCD L % 8, so the blocks of piece group y -- every instance's --
+  // are given to XCD y % 8 and the group's co_index words (shared by the instances) are
+  // fetched into one L2 instead of all eight.  Per XCD the order is group-major, instance-minor.
+  uint64_t inst, grp;
+  if (MODE & 4096) {
+    const uint32_t L = blockIdx.x, j = L >> 3, B = (uint32_t)a.ninst;
+    inst = j % B;
+    grp = 8ull * (j / B) + (L & 7);
+    if (grp * kFusedWaves >= f.nitems && grp != 0) return;  // the pad groups (group 0 always runs)
+  } else {
+    inst = (MODE & 32) ? blockIdx.y : blockIdx.x;
+    grp = (MODE & 32) ? blockIdx.x : blockIdx.y;
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint64_t item = grp * kFusedWaves + wave;
@@ -1283,6 +1296,8 @@ PZ_FUSED_KERNEL(pz_epoch_fused_kernel, 0)
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_kernel, 256)  // reward bits from FusedArgs.lastco
 PZ_FUSED_KERNEL(pz_epoch_fused_se_kernel, 1024)  // start/end from FusedArgs.se
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_kernel, 1280)
+PZ_FUSED_KERNEL(pz_epoch_fused_se_xcd_kernel, 1024 + 4096)     // the XCD-aware 1-D grid
+PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_xcd_kernel, 1280 + 4096)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg1_kernel, 1)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg2_kernel, 2)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg3_kernel, 3)
@@ -1436,9 +1451,13 @@ hipError_t launch_epoch_fwin(const EpochArgs& a, const FusedArgs& f, hipStream_t
   return hipGetLastError();
 }
 
+// Ablations look the reward bits up in the fused pass (tools/; 128: this A/B); the grid-order
+// variant (the XCD-aware 4096) keeps the product's gather.
+static bool ablation_no_lastco() { return g_fused_variant && g_fused_variant != 4096; }
+
 hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f0, hipStream_t s) {
   FusedArgs f = f0;
-  if (g_fused_variant) f.lastco = nullptr;  // ablations (tools/; 128: this A/B) look the bits up in the fused pass
+  if (ablation_no_lastco()) f.lastco = nullptr;
   uint64_t pbpi = (a.max_inst_bytes + kPopBytesPerBlock - 1) / kPopBytesPerBlock;
   if (pbpi == 0) pbpi = 1;  // chunk 0 of each instance also resets the winners
   const uint64_t npb = (uint64_t)a.ninst * pbpi;
@@ -1454,11 +1473,21 @@ hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f0, hipStream_t
 hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream_t s) {
   if (!a.ninst) return hipSuccess;
   FusedArgs f = f0;
-  if (g_fused_variant) f.lastco = nullptr;  // as launch_epoch_pre
+  if (ablation_no_lastco()) f.lastco = nullptr;  // as launch_epoch_pre
   // at least one group: group 0 writes the per-instance scalars and zeroes the next step's
   // accumulators, also on a rank whose range holds no piece
   const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
   const int variant = g_fused_variant;
+  if (variant == 4096 && f.se) {  // the XCD-aware 1-D grid: groups padded to a multiple of 8
+    const dim3 grid1((uint32_t)(((groups + 7) / 8) * 8 * a.ninst)), blk(64 * kFusedWaves);
+    if (f.lastco)
+      hipLaunchKernelGGL(pz_epoch_fused_lc_se_xcd_kernel, grid1, blk, 0, s, a, f, f.pre, a.boffs, a.total_deposit,
+                         f.items, f.cinfo, f.catt_offs, f.catt);
+    else
+      hipLaunchKernelGGL(pz_epoch_fused_se_xcd_kernel, grid1, blk, 0, s, a, f, f.pre, a.boffs, a.total_deposit,
+                         f.items, f.cinfo, f.catt_offs, f.catt);
+    return hipGetLastError();
+  }
   // instance-minor: x = instance, y = piece group (ablation 32: instance-major)
   const dim3 grid = (variant & 32) ? dim3((uint32_t)groups, a.ninst) : dim3(a.ninst, (uint32_t)groups);
   const dim3 block(64 * kFusedWaves);

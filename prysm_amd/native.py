@@ -55,6 +55,26 @@ class Comm:
         lib.call("pz_comm_init_loopback", world, device, ctypes.byref(h))
         return cls(h)
 
+    @classmethod
+    def shm(cls, name, world, rank, device=0, timeout_ms=60000):
+        """One process per rank, ranks free to share a device: collectives staged through host
+        memory and the POSIX shared-memory group ``name`` (every rank passes the same name;
+        rank 0 creates it).  Checks that all ranks issue the same collective sequence."""
+        h = ctypes.c_void_p()
+        lib.call("pz_comm_init_shm", name.encode(), world, rank, device, timeout_ms, ctypes.byref(h))
+        return cls(h)
+
+    def set_timing(self, on=True):
+        """Bracket every collective with HIP events on the communicator's streams."""
+        lib.call("pz_comm_set_timing", self.h, 1 if on else 0)
+
+    def collective_time(self):
+        """(ms, count): the summed device time of the collectives since the last call (max over
+        this process's local ranks per collective) and how many there were."""
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        lib.call("pz_comm_collective_time", self.h, ctypes.byref(ms), ctypes.byref(n))
+        return ms.value, n.value
+
     def hash_batch(self, data, offsets, out_bytes=32):
         """pz_comm_blake2b512_batch: this process's ranks' slices of the CSR batch; rows of
         other processes' slices are left zero."""

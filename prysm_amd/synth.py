@@ -89,6 +89,21 @@ def epoch_batch(nval, ninst, seed=3, shuffled=None, density=0.75, last_bits=None
                 max_inst_bytes=per_inst)
 
 
+def epoch_instances(inst, k):
+    """The first ``k`` instances of an ``epoch_batch`` (every instance's bitfields have the
+    same layout, so instance i's CSR range is i * max_inst_bytes onward)."""
+    natt, per = int(inst["natt"]), int(inst["max_inst_bytes"])
+    out = dict(inst)
+    out["ninst"] = k
+    for key in ("start", "end", "balance", "dynasty", "total_deposit", "rec_dynasty"):
+        out[key] = inst[key][:k].copy()
+    for key in ("att_comm", "att_shard", "att_slot"):
+        out[key] = inst[key][:k * natt].copy()
+    out["bits"] = inst["bits"][:k * per].copy()
+    out["boffs"] = inst["boffs"][:k * natt + 1].copy()
+    return out
+
+
 def attestation_records_512(n, seed=2):
     """(n, 512) uint8 array of canonical AttestationRecord encodings."""
     rng = np.random.default_rng(seed)

@@ -85,6 +85,21 @@ def test_native_epoch_single_launch(n, density):
     _check(ne, inst, steps=3)
 
 
+@pytest.mark.parametrize("n,B", [(65536, 5), (32768, 9), (4097, 3), (1000, 2)])
+def test_native_epoch_xcd_grid(n, B):
+    """The one-pass step's fused pass on the XCD-aware 1-D grid (fused variant 4096: block L
+    on XCD L % 8 takes piece group 8 (L / 8 / B) + L % 8 of instance (L / 8) % B, the pad groups
+    exit), two steps bit-exact against the oracle."""
+    inst = _inst(n, B, False)
+    ne = NativeEpoch(inst, device=0)
+    assert ne.one_pass
+    old = _lib.lib.dll.pz_debug_set_fused_variant(4096)
+    try:
+        _check(ne, inst, steps=2)
+    finally:
+        _lib.lib.dll.pz_debug_set_fused_variant(old)
+
+
 @pytest.mark.parametrize("case", ["reward_panic", "short_bitfield", "many_atts"])
 def test_native_epoch_single_launch_edges(case):
     """The single-launch step's panics (CheckBit(last, N-1), a bitfield shorter than its

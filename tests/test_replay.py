@@ -314,7 +314,9 @@ def test_gpu_replay_reproduces_reward_panic():
     g = golden()
     assert g["full_participation_panics_at"]
     ch = BeaconChain(g["nval"])
-    with pytest.raises(ChainPanic):
+    # the deferred epoch is collected at the end of the call (block 69): the panic names the
+    # transition's block and slot, after which the call's result rows are undefined
+    with pytest.raises(ChainPanic, match=r"CalculateRewards.*stateRecalc of block \d+ of this call, slot 64"):
         ch.process_blocks(synth.chain_blocks(g["nval"], 70, seed=g["seed"], participation=(1.0,)))
 
 
