@@ -151,15 +151,22 @@ EPOCH_BYTES_PER_VALIDATOR = 44.25
 
 def epoch_layout_bytes(inst, one_pass):
     """Bytes per validator-epoch the one-pass committee-order step must move:
-    the balance read and written (16), the {start, end} dynasties (8 in the packed 32-bit column
-    the state uploads when every CurrentDynasty is below 2^32 - 1, else 16), and the instance's
+    the balance read and written (16), the {start, end} dynasties (4 in the 16-bit saturated
+    column the state uploads when every CurrentDynasty is below 0xFFFF, 8 in the 32-bit one
+    below 2^32 - 1, else 16), and the instance's
     bitfields once (their bytes / nval); co_index is shared by the instances (L2).  None for
     the other layouts (SURVEY.md §8d's 44.25 B stays their model)."""
     if not one_pass:
         return None
-    packed = int(np.max(inst["dynasty"])) < 0xFFFFFFFF and not os.environ.get("PZ_EPOCH_SE64")
+    dmax = int(np.max(inst["dynasty"]))
+    if os.environ.get("PZ_EPOCH_SE64") or dmax >= 0xFFFFFFFF:
+        se = 16  # the 64-bit start and end columns
+    elif dmax < 0xFFFF and not os.environ.get("PZ_EPOCH_SE32"):
+        se = 4  # {start, end} saturated to 16 bits (epoch_state.hip upload_se16)
+    else:
+        se = 8  # saturated to 32 bits
     bits = float(inst["boffs"][-1]) / (inst["ninst"] * inst["nval"])
-    return 16 + (8 if packed else 16) + bits
+    return 16 + se + bits
 HASH_KERNEL = "pz_b2b_fixed_persistent_kernel"
 CPU_SAMPLE_S = 8.0  # seconds of CPU work per cpu_baseline leg (three legs: ~25 s in all)
 
@@ -938,7 +945,7 @@ def replay_sharded_leg(args, torch, dist, dev, rank, world, comm):
 
 PROF_PHASES = ("parse", "digest_batch", "checks", "vote_queue", "vote_flush", "state_recalc", "msg_digests", "walk",
                "process", "count_atts", "flush_arena_wait", "msg_send", "msg_hash_log", "msg_wait",
-               "poll_fallbacks")  # the last is a count (tally-total polls that fell back to the event wait)
+               "totals_wait", "poll_fallbacks")  # the last is a count (tally-total polls that fell back to the event wait)
 
 
 def chain_phases_ms(ch):

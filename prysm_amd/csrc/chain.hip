@@ -539,6 +539,13 @@ struct PinVec {
   std::vector<std::unique_ptr<PinBuf>> bufs;  // the last one is current
   size_t n = 0;
   T* data() const { return bufs.empty() ? nullptr : reinterpret_cast<T*>(bufs.back()->p); }
+  // the current buffer's address on `device` (the calling thread's current device), or null
+  const T* dev(int device) const {
+    if (bufs.empty()) return nullptr;
+    void* q = nullptr;
+    if (int rc = bufs.back()->dev(device, &q)) throw rc;
+    return static_cast<const T*>(q);
+  }
   size_t cap() const { return bufs.empty() ? 0 : bufs.back()->n / sizeof(T); }
   void reserve(size_t c) {
     if (c <= cap()) return;
@@ -580,6 +587,7 @@ struct PinVec {
 enum ProfSlot {
   kProfParse, kProfHash1, kProfCheck, kProfQueue, kProfFlush, kProfRecalc, kProfMsgHash, kProfWalk, kProfProcess,
   kProfCount, kProfFlushWait, kProfMsgSend, kProfMsgLog, kProfMsgWait,
+  kProfTotalsWait,    // the walk waiting for a transition's justification totals (inside state_recalc)
   kProfPollFallback,  // a count, not seconds: sequence-word polls that fell back to the event wait
   kProfSlots
 };
@@ -632,8 +640,10 @@ struct RankDev {
   // epoch scratch: red = {scal[8], vote[natt], total[natt]} (one all-reduce when sharded)
   DevArr<uint64_t> e_red, e_mask, e_nb;
   DevArr<uint32_t> e_blk, e_list, e_win;
-  DevArr<uint8_t> e_pack;      // one H2D per transition: bitfields, offsets, committees, ...
-  hipEvent_t q_ev = nullptr;   // this rank's copy of the pinned tally arena is done
+  DevArr<uint8_t> e_pack;      // one H2D per transition: bitfields, offsets, committees, ... (sharded)
+  DevArr<uint32_t> e_ticket;   // one rank: the reward pass's hand-off ticket (left zero)
+  hipEvent_t q_ev = nullptr;   // this rank's copy of the pinned tally arena is done (staged path)
+  hipEvent_t vq_ev[2] = {};    // this rank's last reader of Engine::vq[i] is done
   hipEvent_t ev_epoch = nullptr, ev_red = nullptr, ev_nb = nullptr, ev_t64 = nullptr;
 };
 
@@ -674,10 +684,18 @@ struct Engine {
   // pending tally work: per queued attestation its committee, bitfield, the hash-log ids of
   // its 64 signed parent hashes and a mask of the ones equal to an oblique parent hash; the
   // device expands them into (attestation, parent) items (pz_vote_ids_kernel)
-  std::vector<uint8_t> q_bits;
-  std::vector<uint64_t> q_boffs{0};
-  std::vector<uint32_t> q_comm, q_slots;  // q_slots: natt x 64 vote-cache slots of the signed parents
-  std::vector<uint64_t> q_skip;
+  // The walk writes the queue straight into pinned memory, which the union pass reads in place
+  // (launch_vote_ids_direct): two queues, the walk filling one while a flush's kernels may
+  // still read the other (RankDev::vq_ev).
+  struct VoteQueue {
+    PinVec<uint8_t> bits;
+    PinVec<uint64_t> boffs;             // natt + 1
+    PinVec<uint32_t> comm, slots;       // slots: natt x 64 vote-cache slots of the signed parents
+    PinVec<uint64_t> skip;
+    bool busy = false;
+    size_t natt() const { return comm.size(); }
+  } vq[2];
+  int vq_cur = 0;
   // flushes run asynchronously to the walk: the queue is packed into a pinned arena and
   // copied with one H2D per rank; the arena is reused once every rank's copy is done
   PinBuf q_arena;
@@ -698,7 +716,9 @@ struct Engine {
     uint64_t block_slot = 0;
     uint64_t block_index = 0;  // the transition block's index in the call (named by a panic)
     size_t nrec = 0;
+    uint64_t seq = 0;  // one rank: the results arrive in g.e_pin_out with this sequence word
   } deferred;
+  uint64_t epoch_seq = 0;
   // hashing scratch (rank 0)
   PinBuf pin_msgs, pin_offs, pin_dig;  // pinned staging of the digest batch
   DevArr<uint8_t> h_in, h_out;
@@ -934,28 +954,39 @@ static uint32_t log_hash(Engine& g, const H32& h, bool votable = true) {
 // With `gq` (a stateRecalc's flush on one rank), the leader pass also gathers the 64
 // justification totals into g.tot_pin and g.ev_totals is recorded behind it: returns true
 // when it did so (tally_gather_enqueue's work is then done).
+// PZ_VOTE_STAGED=1 (A/B knob): the round-3 path -- the queue packed into one pinned arena, a
+// stage kernel copying it to the device, then the per-item union pass.
+static bool vote_staged() {  // (read per flush, so that one test process can run both paths)
+  const char* e = std::getenv("PZ_VOTE_STAGED");
+  return e && e[0] == '1';
+}
+
 static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr) {
-  if (g.q_comm.empty()) return false;
+  Engine::VoteQueue& Q = g.vq[g.vq_cur];
+  if (Q.natt() == 0) return false;
   const bool gather = gq && g.world == 1;
+  const bool staged = vote_staged();
   PhaseTimer pt(g.prof[kProfFlush]);
-  const uint64_t natt = g.q_comm.size();
+  const uint64_t natt = Q.natt();
   auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
-  // packed layout: boffs | skip | comm | slots | bits
-  const size_t o_boffs = 0, o_skip = o_boffs + al(g.q_boffs.size() * 8), o_comm = o_skip + al(natt * 8),
-               o_slots = o_comm + al(natt * 4), o_bits = o_slots + al(g.q_slots.size() * 4),
-               total = o_bits + al(g.q_bits.size());
-  if (g.q_arena_busy) {
-    FineTimer pw(g.prof[kProfFlushWait]);
-    for (RankDev& r : g.rk) hchk(hipEventSynchronize(r.q_ev), "event sync");
-    g.q_arena_busy = false;
+  // staged: packed layout boffs | skip | comm | slots | bits
+  const size_t o_boffs = 0, o_skip = o_boffs + al(Q.boffs.size() * 8), o_comm = o_skip + al(natt * 8),
+               o_slots = o_comm + al(natt * 4), o_bits = o_slots + al(Q.slots.size() * 4),
+               total = staged ? o_bits + al(Q.bits.size()) : 0;
+  if (staged) {
+    if (g.q_arena_busy) {
+      FineTimer pw(g.prof[kProfFlushWait]);
+      for (RankDev& r : g.rk) hchk(hipEventSynchronize(r.q_ev), "event sync");
+      g.q_arena_busy = false;
+    }
+    check(g.q_arena.reserve(total));
+    uint8_t* qa = g.q_arena.p;
+    std::memcpy(qa + o_boffs, Q.boffs.data(), Q.boffs.size() * 8);
+    std::memcpy(qa + o_skip, Q.skip.data(), natt * 8);
+    std::memcpy(qa + o_comm, Q.comm.data(), natt * 4);
+    std::memcpy(qa + o_slots, Q.slots.data(), Q.slots.size() * 4);
+    if (Q.bits.size()) std::memcpy(qa + o_bits, Q.bits.data(), Q.bits.size());
   }
-  check(g.q_arena.reserve(total));
-  uint8_t* qa = g.q_arena.p;
-  std::memcpy(qa + o_boffs, g.q_boffs.data(), g.q_boffs.size() * 8);
-  std::memcpy(qa + o_skip, g.q_skip.data(), natt * 8);
-  std::memcpy(qa + o_comm, g.q_comm.data(), natt * 4);
-  std::memcpy(qa + o_slots, g.q_slots.data(), g.q_slots.size() * 4);
-  std::memcpy(qa + o_bits, g.q_bits.data(), g.q_bits.size());
   each_rank(g, [&](RankDev& r) {
     // Growing a device buffer frees the old one, which in-flight flushes may still read:
     // drain the stream first (rare: the buffers double).
@@ -968,14 +999,16 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr) 
         hchk(hipMemsetAsync(r.d_leader.p, 0, 16, r.s), "memset");  // both counters and the gather ticket
       }
     }
-    // the pack crosses PCIe in a kernel of this stream (a copy-engine H2D costs ~13 us more on
-    // the transition's critical path: the kernel behind it waits for the engine's signal)
-    void* src = nullptr;
-    check(g.q_arena.dev(r.dev, &src));
-    hchk(launch_stage_h2d(src, r.d_qpack.p, total, r.s), "stage H2D");
-    if (!gather) {  // (gathering: g.ev_totals, later in the stream, frees the arena)
-      if (!r.q_ev) hchk(hipEventCreateWithFlags(&r.q_ev, hipEventDisableTiming), "event");
-      hchk(hipEventRecord(r.q_ev, r.s), "event");
+    if (staged) {
+      // the pack crosses PCIe in a kernel of this stream (a copy-engine H2D costs ~13 us more on
+      // the transition's critical path: the kernel behind it waits for the engine's signal)
+      void* src = nullptr;
+      check(g.q_arena.dev(r.dev, &src));
+      hchk(launch_stage_h2d(src, r.d_qpack.p, total, r.s), "stage H2D");
+      if (!gather) {  // (gathering: g.ev_totals, later in the stream, frees the arena)
+        if (!r.q_ev) hchk(hipEventCreateWithFlags(&r.q_ev, hipEventDisableTiming), "event");
+        hchk(hipEventRecord(r.q_ev, r.s), "event");
+      }
     }
     if (!r.d_err.p) {
       check(r.d_err.alloc(1));
@@ -985,11 +1018,19 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr) 
     std::memset(&v, 0, sizeof v);
     v.committee = r.committee.p;
     v.coffs = r.coffs.p;
-    v.att_comm = reinterpret_cast<const uint32_t*>(r.d_qpack.p + o_comm);
-    v.bits = r.d_qpack.p + o_bits;
-    v.boffs = reinterpret_cast<const uint64_t*>(r.d_qpack.p + o_boffs);
-    v.slots = reinterpret_cast<const uint32_t*>(r.d_qpack.p + o_slots);
-    v.skip = reinterpret_cast<const uint64_t*>(r.d_qpack.p + o_skip);
+    if (staged) {
+      v.att_comm = reinterpret_cast<const uint32_t*>(r.d_qpack.p + o_comm);
+      v.bits = r.d_qpack.p + o_bits;
+      v.boffs = reinterpret_cast<const uint64_t*>(r.d_qpack.p + o_boffs);
+      v.slots = reinterpret_cast<const uint32_t*>(r.d_qpack.p + o_slots);
+      v.skip = reinterpret_cast<const uint64_t*>(r.d_qpack.p + o_skip);
+    } else {  // read in place (pinned, mapped into this rank's device)
+      v.att_comm = Q.comm.dev(r.dev);
+      v.bits = Q.bits.dev(r.dev);
+      v.boffs = Q.boffs.dev(r.dev);
+      v.slots = Q.slots.dev(r.dev);
+      v.skip = Q.skip.dev(r.dev);
+    }
     v.natt = natt;
     v.balance = r.balance.p;
     v.nval = r.n;
@@ -1019,19 +1060,30 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr) 
       // (pooled pinned memory holds old words: clear the sequence word before the launch)
       reinterpret_cast<volatile uint64_t*>(g.tot_pin.p)[kJustifySlots + 1] = 0;
     }
-    hchk(launch_vote_ids(v, r.s), "vote tally");
-    if (gather) {
-      if (!g.ev_totals) hchk(hipEventCreateWithFlags(&g.ev_totals, hipEventDisableTiming), "event");
-      hchk(hipEventRecord(g.ev_totals, r.s), "event");
+    hchk(staged ? launch_vote_ids(v, r.s) : launch_vote_ids_direct(v, r.s), "vote tally");
+    if (!gather) {  // (gathering: the walk waits for the leader pass before any later flush)
+      if (!r.vq_ev[g.vq_cur]) hchk(hipEventCreateWithFlags(&r.vq_ev[g.vq_cur], hipEventDisableTiming), "event");
+      hchk(hipEventRecord(r.vq_ev[g.vq_cur], r.s), "event");
     }
   });
-  g.q_arena_busy = !gather;
+  if (staged) g.q_arena_busy = !gather;
   g.gather_poll = gather;
-  g.q_bits.clear();
-  g.q_boffs.assign(1, 0);
-  g.q_comm.clear();
-  g.q_slots.clear();
-  g.q_skip.clear();
+  // the walk goes on in the other queue, once the flush before last has stopped reading it (a
+  // gathering flush is waited for by tally_gather_finish before the walk goes on)
+  Q.busy = !gather;
+  g.vq_cur ^= 1;
+  Engine::VoteQueue& N = g.vq[g.vq_cur];
+  if (N.busy) {
+    FineTimer pw(g.prof[kProfFlushWait]);
+    for (RankDev& r : g.rk)
+      if (r.vq_ev[g.vq_cur]) hchk(hipEventSynchronize(r.vq_ev[g.vq_cur]), "event sync");
+    N.busy = false;
+  }
+  N.bits.reset();
+  N.boffs.reset();
+  N.comm.reset();
+  N.slots.reset();
+  N.skip.reset();
   return gather;
 }
 
@@ -1077,6 +1129,8 @@ static void tally_gather_enqueue(Engine& g, const VoteGatherSlots& q) {
 
 // After g.ev_totals: raise the panic a tally detected.
 static void tally_gather_finish(Engine& g) {
+  PhaseTimer pt(g.prof[kProfTotalsWait]);
+  const bool polled = g.gather_poll;  // (a gathering flush records no event: its fallback syncs the stream)
   if (g.gather_poll) {
     // The fused gather writes its sequence word last (system-scope release): spin on the pinned
     // word instead of sleeping in the event wait, whose wake-up took ~10-20 us of every
@@ -1099,7 +1153,10 @@ static void tally_gather_finish(Engine& g) {
       return;
     }
   }
-  hchk(hipEventSynchronize(g.ev_totals), "event sync (vote totals)");
+  if (polled)
+    hchk(hipStreamSynchronize(g.rk[0].s), "stream sync (vote totals)");
+  else
+    hchk(hipEventSynchronize(g.ev_totals), "event sync (vote totals)");
   g.q_arena_busy = false;  // every rank's flush is behind g.ev_totals
   if (reinterpret_cast<const uint64_t*>(g.tot_pin.p)[kJustifySlots])
     throw Panic{"calculateBlockVoteCache: CheckBit / validator index out of range"};
@@ -1259,13 +1316,16 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, AttLo
   if (g.A->cache_nil) throw Panic{"assignment to entry in nil map (core.go:323)"};
   // the member loop reaches CheckBit(bitfield, 8 * len) when the committee is longer
   if (k > 8ull * a.bf_len) throw Panic{"calculateBlockVoteCache: CheckBit index out of range (core.go:330)"};
-  g.q_comm.push_back(c);
-  g.q_skip.push_back(skip);
-  g.q_slots.insert(g.q_slots.end(), slots, slots + 64);
+  Engine::VoteQueue& Q = g.vq[g.vq_cur];
+  if (Q.boffs.size() == 0) Q.boffs.push_back(0);
+  Q.comm.push_back(c);
+  Q.skip.push_back(skip);
+  std::memcpy(Q.slots.grow(64), slots, sizeof slots);
   const uint8_t* bf = a.at(a.bf_off);
-  g.q_bits.insert(g.q_bits.end(), bf, bf + (k + 7) / 8);
-  g.q_boffs.push_back(g.q_bits.size());
-  if (g.q_comm.size() >= kFlushAtts) flush_votes_enqueue(g);  // bounds the queue; no host wait
+  const size_t nbf = (k + 7) / 8;
+  if (nbf) std::memcpy(Q.bits.grow(nbf), bf, nbf);
+  Q.boffs.push_back(Q.bits.size());
+  if (Q.natt() >= kFlushAtts) flush_votes_enqueue(g);  // bounds the queue; no host wait
 }
 
 // processCrosslinks + CalculateRewards + next-cycle balance on the device: enqueued, its
@@ -1306,6 +1366,71 @@ static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending
   small[1] = C.tdep;
   // the previous epoch was collected (every rank's event completed), so the staging is free
   const uint64_t nred = kScal + 2 * (uint64_t)na;  // {scal, vote, total}: one all-reduce when sharded
+  if (g.world == 1) {
+    // One rank: three launches and no other runtime call.  The kernels read the pack where the
+    // host wrote it (pinned, mapped), and the reward pass's last block hands the scalars and
+    // winners back into pinned memory behind a sequence word (epoch_collect polls it) and
+    // zeroes the scalars for the next epoch -- instead of an H2D, a memset, a D2H and an event.
+    RankDev& r = g.rk[0];
+    hchk(hipSetDevice(r.dev), "hipSetDevice");
+    const uint64_t wn = (nrec + 1) / 2;
+    const size_t had = r.e_red.n;
+    check(r.e_red.alloc(nred + wn + 1));
+    if (r.e_red.n != had) hchk(hipMemsetAsync(r.e_red.p, 0, kScal * 8, r.s), "memset");  // (once per growth)
+    if (!r.e_ticket.p) {
+      check(r.e_ticket.alloc(1));
+      hchk(hipMemsetAsync(r.e_ticket.p, 0, 4, r.s), "memset");
+    }
+    check(g.e_pin_out.reserve((kScal + wn + 1) * 8));
+    void *hp = nullptr, *op = nullptr;
+    check(g.e_pin.dev(r.dev, &hp));
+    check(g.e_pin_out.dev(r.dev, &op));
+    reinterpret_cast<volatile uint64_t*>(g.e_pin_out.p)[kScal + wn] = 0;  // (pooled memory: old words)
+    uint8_t* d = static_cast<uint8_t*>(hp);
+    EpochArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.ninst = 1;
+    a.nval = r.n;
+    a.val_offset = r.lo;
+    a.nval_global = g.nval;
+    a.kind = PZ_KIND_ACTIVE;
+    a.balance = r.balance.p;
+    a.start = r.start.p;
+    a.end = r.end.p;
+    a.dynasty = reinterpret_cast<const uint64_t*>(d + o_small);
+    a.total_deposit = reinterpret_cast<const uint64_t*>(d + o_small) + 1;
+    a.natt = (uint32_t)na;
+    a.bits = d + o_bits;
+    a.boffs = reinterpret_cast<const uint64_t*>(d + o_boffs);
+    a.max_inst_bytes = nbits;
+    a.pop_rank = 0;
+    a.pop_world = 1;
+    a.committee = r.committee.p;
+    a.coffs = r.coffs.p;
+    a.att_comm = reinterpret_cast<const uint32_t*>(d + o_comm);
+    a.att_shard = reinterpret_cast<const uint32_t*>(d + o_shard);
+    a.nrec = (uint32_t)nrec;
+    a.rec_dynasty = reinterpret_cast<const uint64_t*>(d + o_rdyn);
+    a.winner = reinterpret_cast<uint32_t*>(r.e_red.p + kScal);
+    a.scal = r.e_red.p;
+    a.vote = r.e_red.p + kScal + wn;
+    a.total = r.e_red.p + kScal + wn + na;
+    a.act_mask = r.e_mask.p;
+    a.blk_cnt = r.e_blk.p;
+    a.act_list = r.e_list.p;
+    EpochHandoff ho;
+    ho.ticket = r.e_ticket.p;
+    ho.out = static_cast<uint64_t*>(op);
+    ho.nrec = (uint32_t)nrec;
+    ho.seq = ++g.epoch_seq;
+    hchk(launch_epoch_count(a, true, true, true, r.s), "epoch count");
+    hchk(launch_epoch_mid(a, a.nrec > 0 && na > 0, true, r.s), "epoch mid");
+    hchk(launch_epoch_reward_handoff(a, ho, r.s), "epoch reward");
+    g.deferred.nrec = nrec;
+    g.deferred.seq = ho.seq;
+    return;
+  }
+  g.deferred.seq = 0;
   std::vector<uint64_t*> bufs, nbs;
   std::vector<hipStream_t> streams;
   std::vector<hipEvent_t> evs, evn;
@@ -1414,7 +1539,22 @@ static void epoch_collect(Engine& g) {
   Engine::DeferredEpoch& D = g.deferred;
   if (!D.live) return;
   D.live = false;
-  for (RankDev& r : g.rk) hchk(hipEventSynchronize(r.ev_epoch), "event sync (epoch)");
+  if (D.seq) {  // one rank: poll the reward pass's sequence word (written last), bounded
+    const volatile uint64_t* sq = reinterpret_cast<const volatile uint64_t*>(g.e_pin_out.p) + kScal + (D.nrec + 1) / 2;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t k = 0; *sq != D.seq; ++k) {
+      __builtin_ia32_pause();
+      if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
+    }
+    if (*sq != D.seq) {  // not yet (or an error): the stream decides
+      g.prof[kProfPollFallback] += 1;
+      hchk(hipStreamSynchronize(g.rk[0].s), "stream sync (epoch)");
+      if (*sq != D.seq) throw (int)fail(PZ_EDEVICE, "epoch results never arrived (sequence %llu)", (unsigned long long)D.seq);
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  } else {
+    for (RankDev& r : g.rk) hchk(hipEventSynchronize(r.ev_epoch), "event sync (epoch)");
+  }
   uint64_t scal[kScal];
   std::memcpy(scal, g.e_pin_out.p, sizeof scal);
   const uint32_t* win = reinterpret_cast<const uint32_t*>(g.e_pin_out.p + sizeof scal);
@@ -2772,7 +2912,7 @@ static void destroy_chain(pz_chain* c) {
   for (RankDev& r : g.rk) {
     (void)hipSetDevice(r.dev);
     if (r.s) (void)hipStreamSynchronize(r.s);
-    for (hipEvent_t e : {r.q_ev, r.ev_epoch, r.ev_red, r.ev_nb, r.ev_t64})
+    for (hipEvent_t e : {r.q_ev, r.vq_ev[0], r.vq_ev[1], r.ev_epoch, r.ev_red, r.ev_nb, r.ev_t64})
       if (e) (void)hipEventDestroy(e);
     streams.push_back({r.dev, r.s});
   }

@@ -48,6 +48,17 @@ hipError_t launch_epoch_gather_compact(const EpochArgs& a, const uint64_t* gmask
 hipError_t launch_epoch_mid(const EpochArgs& a, bool winners, bool compact, hipStream_t s);
 // Pass 2: rewards (in place) + post-reward active balance sum.
 hipError_t launch_epoch_reward(const EpochArgs& a, hipStream_t s);
+// ONE instance's reward pass whose last block hands the results to the host: out (mapped pinned)
+// receives the kScal scalars, then the nrec u32 winners, then -- last, behind a system-scope
+// release -- `seq` in the u64 at index kScal + (nrec + 1) / 2; the scalars are zeroed for the
+// next count and `ticket` (a zero device word) is left zero.
+struct EpochHandoff {
+  uint32_t* ticket;
+  uint64_t* out;
+  uint32_t nrec;
+  uint64_t seq;
+};
+hipError_t launch_epoch_reward_handoff(const EpochArgs& a, const EpochHandoff& h, hipStream_t s);
 
 // ---- one-pass epoch (committee-order layout, every validator active) ----------------------
 // GetAttestersTotalDeposit depends on the bitfields only and CalculateRewards' reward bit of
@@ -115,6 +126,9 @@ struct FusedArgs {
   // every instance's CurrentDynasty is below 2^32 - 1, which makes the saturated bounds classify
   // exactly): the stream reads 8 B of them per validator instead of 16
   const uint2* se;
+  // [B][vstride] the same bounds saturated to 16 bits, {start | end << 16} (set instead of `se`
+  // when every instance's CurrentDynasty is below 0xFFFF): 4 B per validator
+  const uint32_t* se16;
   const uint2* att_win;       // [B][natt] {shard, record dynasty of that shard} per attestation (an
                               //   upload-time layout: loaded beside the stream, no shard -> record hop)
 };

@@ -666,9 +666,10 @@ __device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
     uint64_t s = block_reduce<false>(sum, sh);
     if (tid == 0) {
       if (s && !skip) atomicAdd((unsigned long long*)&a.scal[inst * kScal + kNextBal], (unsigned long long)s);
-      if (chunk == 0) {
-        a.scal[inst * kScal + kApplied] = applied ? 1 : 0;
-        a.scal[inst * kScal + kNact] = nact;
+      if (chunk == 0) {  // agent-scope (sc1) stores: a hand-off's last block reads them (below)
+        __hip_atomic_store(&a.scal[inst * kScal + kApplied], (uint64_t)(applied ? 1 : 0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.scal[inst * kScal + kNact], nact, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     if (a.scal_next && chunk == 0 && tid < kScal) a.scal_next[inst * kScal + tid] = 0;
@@ -679,13 +680,13 @@ __device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
   const uint64_t* sc = a.scal + inst * kScal;
   const uint64_t pop = sc[kPop], nact = a.nval_global - sc[kNoMatch];
   const bool xl_err = sc[kErrXl] != 0;
-  if (chunk == 0 && tid == 0) a.scal[inst * kScal + kNact] = nact;
+  if (chunk == 0 && tid == 0) __hip_atomic_store(&a.scal[inst * kScal + kNact], nact, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t dep = pop * PZ_DEFAULT_BALANCE;                 // GetAttestersTotalDeposit
   const bool applied = (dep * 3ull) >= (a.total_deposit[inst] * 2ull);  // uint64 wrap
   const bool rwd_err = applied && nact > 0 && sc[kErrRwd] != 0;
   if (a.scal_next && chunk == 0 && tid < kScal) a.scal_next[inst * kScal + tid] = 0;
   if (xl_err || rwd_err) {  // Go panics before/while rewarding: leave balances untouched
-    if (chunk == 0 && tid == 0) a.scal[inst * kScal + kApplied] = 0;
+    if (chunk == 0 && tid == 0) __hip_atomic_store(&a.scal[inst * kScal + kApplied], (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   const bool all_active = (nact == a.nval_global);
@@ -714,7 +715,7 @@ __device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
   uint64_t s = block_reduce<false>(sum, sh);
   if (tid == 0) {
     if (s) atomicAdd((unsigned long long*)&a.scal[inst * kScal + kNextBal], (unsigned long long)s);
-    if (chunk == 0) a.scal[inst * kScal + kApplied] = applied ? 1 : 0;
+    if (chunk == 0) __hip_atomic_store(&a.scal[inst * kScal + kApplied], (uint64_t)(applied ? 1 : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -729,6 +730,56 @@ PZ_REWARD_KERNEL(pz_epoch_reward_dbg1_kernel, 1)
 PZ_REWARD_KERNEL(pz_epoch_reward_dbg2_kernel, 2)
 PZ_REWARD_KERNEL(pz_epoch_reward_dbg3_kernel, 3)
 #undef PZ_REWARD_KERNEL
+
+// The reward pass of ONE instance with its results handed to the host (EpochHandoff): the
+// last block to finish copies the instance's scalars and the winners mid wrote into mapped
+// pinned memory, zeroes the scalars for the next epoch's count, and writes the sequence word
+// last behind a system-scope release -- so the host polls one word instead of a D2H, an event
+// record and an event wait (three runtime calls per transition of the chain engine).
+// Hand-off (MI355X_MICROARCH.md, the table's first row): every wave drains its stores and
+// atomics (s_waitcnt vmcnt(0)) before the block barrier, one lane per block adds to ONE
+// counter, the block whose add returns the last count reads with agent-scope (sc1) loads what
+// the other blocks wrote by atomics or agent-scope stores (reward_body's scalar writes).
+extern "C" __global__ void __launch_bounds__(kThreads)
+pz_epoch_reward_handoff_kernel(EpochArgs a, uint64_t vbpi, int vec, const uint64_t* __restrict__ scal_ro,
+                               const uint64_t* __restrict__ boffs_ro, const uint64_t* __restrict__ tdep_ro,
+                               EpochHandoff h) {
+  reward_body<0>(a, vbpi, vec, scal_ro, boffs_ro, tdep_ro);
+  __shared__ uint32_t last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = __hip_atomic_fetch_add(h.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x * gridDim.y - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!last) return;
+  const uint32_t tid = threadIdx.x;
+  if (tid < kScal) {
+    h.out[tid] = __hip_atomic_load(&a.scal[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.scal[tid], (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  uint32_t* w = reinterpret_cast<uint32_t*>(h.out + kScal);
+  for (uint32_t r = tid; r < h.nrec; r += kThreads)
+    w[r] = __hip_atomic_load(&a.winner[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) __hip_atomic_store(h.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&h.out[kScal + (h.nrec + 1) / 2], h.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+static bool vec_ok(const EpochArgs& a);
+hipError_t launch_epoch_reward_handoff(const EpochArgs& a, const EpochHandoff& h, hipStream_t s) {
+  if (a.ninst != 1) return hipErrorInvalidValue;
+  const uint64_t vbpi = std::max<uint64_t>(1, vblocks_per_inst(a.nval));
+  hipLaunchKernelGGL(pz_epoch_reward_handoff_kernel, dim3(1, (uint32_t)vbpi), dim3(kThreads), 0, s, a, vbpi,
+                     vec_ok(a) ? 1 : 0, a.scal, a.boffs, a.total_deposit, h);
+  return hipGetLastError();
+}
 
 hipError_t launch_epoch_reward_mode(const EpochArgs& a, int mode, hipStream_t s) {
   const uint64_t vbpi = vblocks_per_inst(a.nval);
@@ -888,6 +939,11 @@ __device__ __forceinline__ uint4 ld16_nt(const uint64_t* p) {
   const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
   return make_uint4(x.x, x.y, x.z, x.w);
 }
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 ld8_nt(const uint32_t* p) {
+  const v2u x = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
+  return make_uint2(x.x, x.y);
+}
 
 __device__ __forceinline__ void fused_block_end(const EpochArgs& a, const FusedArgs& f, const uint32_t* xg,
                                                 const uint64_t* xt, const uint64_t* xv, const uint64_t* xs,
@@ -1021,7 +1077,11 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
       v1[j] = g + 1 >= ws && g + 1 < we;
       const uint64_t pp = (v0[j] || v1[j]) ? p : p0;
       qb[j] = *reinterpret_cast<const uint4*>(Bal + pp);
-      if (MODE & 1024) {  // {start, end} of the pair's two validators, 32-bit saturated: one 16-B load
+      if (MODE & 16384) {  // 16-bit saturated {start | end << 16}: one 8-B load for the pair
+        const uint2 w = ld8_nt(f.se16 + inst * f.vstride + pp);
+        qs[j] = make_uint4(w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16);
+        qe[j] = make_uint4(0, 0, 0, 0);
+      } else if (MODE & 1024) {  // {start, end} of the pair's two validators, 32-bit saturated: one 16-B load
         qs[j] = ld16_nt(reinterpret_cast<const uint64_t*>(f.se + inst * f.vstride + pp));
         qe[j] = make_uint4(0, 0, 0, 0);
       } else if (MODE & 8) {
@@ -1298,6 +1358,10 @@ PZ_FUSED_KERNEL(pz_epoch_fused_se_kernel, 1024)  // start/end from FusedArgs.se
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_kernel, 1280)
 PZ_FUSED_KERNEL(pz_epoch_fused_se_xcd_kernel, 1024 + 4096)     // the XCD-aware 1-D grid
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_xcd_kernel, 1280 + 4096)
+PZ_FUSED_KERNEL(pz_epoch_fused_se16_kernel, 1024 + 16384)       // start/end from FusedArgs.se16
+PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_kernel, 1280 + 16384)
+PZ_FUSED_KERNEL(pz_epoch_fused_se16_xcd_kernel, 1024 + 4096 + 16384)
+PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_xcd_kernel, 1280 + 4096 + 16384)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg1_kernel, 1)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg2_kernel, 2)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg3_kernel, 3)
@@ -1327,6 +1391,13 @@ pz_epoch_one_se_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ bo
                        const uint32_t* __restrict__ catt_ro) {
   fused_body<512 + 1024>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
 }
+extern "C" __global__ void __launch_bounds__(64 * kFusedWaves)
+pz_epoch_one_se16_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ boffs_ro,
+                         const uint64_t* __restrict__ tdep_ro, const uint4* __restrict__ items_ro,
+                         const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,
+                         const uint32_t* __restrict__ catt_ro) {
+  fused_body<512 + 1024 + 16384>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
+}
 
 // The single launch over B instances: grid (B, piece groups), every attested committee one piece
 // (winners in the waves), each instance's bitfields within kMultiMaxBitBytes.
@@ -1336,6 +1407,13 @@ pz_epoch_multi_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ bof
                       const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,
                       const uint32_t* __restrict__ catt_ro) {
   fused_body<2048 + 1024>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
+}
+extern "C" __global__ void __launch_bounds__(64 * kFusedWaves) __attribute__((amdgpu_waves_per_eu(8, 8)))
+pz_epoch_multi_se16_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ boffs_ro,
+                           const uint64_t* __restrict__ tdep_ro, const uint4* __restrict__ items_ro,
+                           const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,
+                           const uint32_t* __restrict__ catt_ro) {
+  fused_body<2048 + 1024 + 16384>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
 }
 extern "C" __global__ void __launch_bounds__(64 * kFusedWaves) __attribute__((amdgpu_waves_per_eu(8, 8)))
 pz_epoch_multi_se64_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ boffs_ro,
@@ -1478,22 +1556,25 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream
   // accumulators, also on a rank whose range holds no piece
   const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
   const int variant = g_fused_variant;
-  if (variant == 4096 && f.se) {  // the XCD-aware 1-D grid: groups padded to a multiple of 8
+  if (variant == 4096 && (f.se || f.se16)) {  // the XCD-aware 1-D grid: groups padded to a multiple of 8
     const dim3 grid1((uint32_t)(((groups + 7) / 8) * 8 * a.ninst)), blk(64 * kFusedWaves);
-    if (f.lastco)
-      hipLaunchKernelGGL(pz_epoch_fused_lc_se_xcd_kernel, grid1, blk, 0, s, a, f, f.pre, a.boffs, a.total_deposit,
-                         f.items, f.cinfo, f.catt_offs, f.catt);
-    else
-      hipLaunchKernelGGL(pz_epoch_fused_se_xcd_kernel, grid1, blk, 0, s, a, f, f.pre, a.boffs, a.total_deposit,
-                         f.items, f.cinfo, f.catt_offs, f.catt);
+#define PZ_LAUNCH_XCD(K) \
+  hipLaunchKernelGGL(K, grid1, blk, 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt)
+    if (f.se16 && f.lastco) PZ_LAUNCH_XCD(pz_epoch_fused_lc_se16_xcd_kernel);
+    else if (f.se16) PZ_LAUNCH_XCD(pz_epoch_fused_se16_xcd_kernel);
+    else if (f.lastco) PZ_LAUNCH_XCD(pz_epoch_fused_lc_se_xcd_kernel);
+    else PZ_LAUNCH_XCD(pz_epoch_fused_se_xcd_kernel);
+#undef PZ_LAUNCH_XCD
     return hipGetLastError();
   }
+  // (the ablations that read FusedArgs.se run the product's kernel when the state holds se16)
+  const int var = ((variant & 1024) && !f.se) ? 0 : variant;
   // instance-minor: x = instance, y = piece group (ablation 32: instance-major)
   const dim3 grid = (variant & 32) ? dim3((uint32_t)groups, a.ninst) : dim3(a.ninst, (uint32_t)groups);
   const dim3 block(64 * kFusedWaves);
 #define PZ_LAUNCH_FUSED(K) \
   hipLaunchKernelGGL(K, grid, block, 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt)
-  switch (variant) {
+  switch (var) {
     case 1: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg1_kernel); break;
     case 2: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg2_kernel); break;
     case 3: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg3_kernel); break;
@@ -1507,7 +1588,11 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream
     case 1024: PZ_LAUNCH_FUSED(pz_epoch_fused_se_kernel); break;  // (ablation baseline: no lastco)
     case 1088: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg1088_kernel); break;
     default:
-      if (f.lastco && f.se)
+      if (f.lastco && f.se16)
+        PZ_LAUNCH_FUSED(pz_epoch_fused_lc_se16_kernel);
+      else if (f.se16)
+        PZ_LAUNCH_FUSED(pz_epoch_fused_se16_kernel);
+      else if (f.lastco && f.se)
         PZ_LAUNCH_FUSED(pz_epoch_fused_lc_se_kernel);
       else if (f.lastco)
         PZ_LAUNCH_FUSED(pz_epoch_fused_lc_kernel);
@@ -1524,7 +1609,10 @@ bool epoch_one_enabled(const FusedArgs& f) { return f.one && g_fused_variant == 
 
 hipError_t launch_epoch_one(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
   const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
-  if (f.se)
+  if (f.se16)
+    hipLaunchKernelGGL(pz_epoch_one_se16_kernel, dim3(1, (uint32_t)groups), dim3(64 * kFusedWaves), 0, s, a, f,
+                       a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt);
+  else if (f.se)
     hipLaunchKernelGGL(pz_epoch_one_se_kernel, dim3(1, (uint32_t)groups), dim3(64 * kFusedWaves), 0, s, a, f, a.boffs,
                        a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt);
   else
@@ -1538,7 +1626,10 @@ bool epoch_multi_enabled(const FusedArgs& f) { return f.multi && g_fused_variant
 hipError_t launch_epoch_multi(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
   const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
   const dim3 grid(a.ninst, (uint32_t)groups), block(64 * kFusedWaves);
-  if (f.se)
+  if (f.se16)
+    hipLaunchKernelGGL(pz_epoch_multi_se16_kernel, grid, block, 0, s, a, f, a.boffs, a.total_deposit, f.items,
+                       f.cinfo, f.catt_offs, f.catt);
+  else if (f.se)
     hipLaunchKernelGGL(pz_epoch_multi_kernel, grid, block, 0, s, a, f, a.boffs, a.total_deposit, f.items, f.cinfo,
                        f.catt_offs, f.catt);
   else

@@ -137,6 +137,22 @@ int upload_se(Shard& s, uint2** p, const uint64_t* start, const uint64_t* end, u
   return e == hipSuccess ? PZ_OK : hip_fail(e, "hipMemcpy H2D (epoch state)");
 }
 
+// FusedArgs.se16: the same positions, each bound saturated to 16 bits, {start | end << 16}.
+int upload_se16(Shard& s, uint32_t** p, const uint64_t* start, const uint64_t* end, uint32_t B, uint64_t N,
+                const uint32_t* inv) {
+  int rc = dalloc(s, p, (size_t)B * s.np, false);
+  if (rc || !s.n) return rc;
+  auto sat = [](uint64_t x) { return (uint32_t)std::min<uint64_t>(x, 0xFFFFull); };
+  std::vector<uint32_t> tmp((size_t)B * s.np, 0u);
+  for (uint64_t b = 0; b < B; ++b)
+    for (uint64_t q = 0; q < s.n; ++q) {
+      const uint64_t v = b * N + inv[s.lo + q];
+      tmp[b * s.np + q] = sat(start[v]) | (sat(end[v]) << 16);
+    }
+  hipError_t e = hipMemcpy(*p, tmp.data(), tmp.size() * 4, hipMemcpyHostToDevice);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "hipMemcpy H2D (epoch state)");
+}
+
 uint64_t shard_words(uint64_t N, int world) { return std::max<uint64_t>(1, (N + 64ull * world - 1) / (64ull * world)); }
 
 int step_world1(pz_epoch_state* st) {
@@ -526,6 +542,7 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
     const uint64_t vbpi = vblocks_per_inst(s.n);
     uint32_t* co_index = nullptr;
     uint2* se = nullptr;
+    uint32_t* se16 = nullptr;
     if (st->co) {
       const uint32_t* inv = st->co_inv.data();
       if ((rc = upload_perm(s, &bal, h->balance, st->B, st->N, inv)) ||
@@ -537,10 +554,19 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
       std::vector<uint32_t> ci(inv + s.lo, inv + s.hi);
       ci.resize(std::max<uint64_t>(s.np, s.n), s.n ? inv[s.lo] : 0);
       if ((rc = upload(s, &co_index, ci.data(), ci.size()))) break;
-      // the one-pass stream's 8-B {start, end} when every CurrentDynasty is below 2^32 - 1
-      bool small_d = st->fused && !std::getenv("PZ_EPOCH_SE64");  // (PZ_EPOCH_SE64: A/B knob)
+      // the one-pass stream's {start, end}: 4 B when every CurrentDynasty is below 0xFFFF, 8 B
+      // when below 2^32 - 1 (saturated bounds classify exactly below the saturation value),
+      // else the 64-bit columns.  (A/B knobs: PZ_EPOCH_SE32 skips the 16-bit column,
+      // PZ_EPOCH_SE64 both.)
+      bool small_d = st->fused && !std::getenv("PZ_EPOCH_SE64");
+      bool tiny_d = small_d && !std::getenv("PZ_EPOCH_SE32");
       for (uint64_t b = 0; b < st->B && small_d; ++b) small_d = h->dynasty[b] < 0xFFFFFFFFull;
-      if (small_d && (rc = upload_se(s, &se, h->start, h->end, st->B, st->N, inv))) break;
+      for (uint64_t b = 0; b < st->B && tiny_d; ++b) tiny_d = h->dynasty[b] < 0xFFFFull;
+      if (tiny_d) {
+        if ((rc = upload_se16(s, &se16, h->start, h->end, st->B, st->N, inv))) break;
+      } else if (small_d && (rc = upload_se(s, &se, h->start, h->end, st->B, st->N, inv))) {
+        break;
+      }
     } else if ((rc = upload_range(s, &bal, h->balance, st->B, st->N)) ||
                (rc = upload_range(s, &start, h->start, st->B, st->N)) ||
                (rc = upload_range(s, &end, h->end, st->B, st->N))) {
@@ -670,6 +696,7 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
         q.f.own_only = st->world > 1 ? 1 : 0;
         q.f.vstride = s.np;
         q.f.se = se ? se + i0 * s.np : nullptr;
+        q.f.se16 = se16 ? se16 + i0 * s.np : nullptr;
         if (!fused_ok(a)) rc = fail(PZ_EINVAL, "one-pass epoch: validator arrays not on the 16-B path");
         // the reward bits in position order (gathered by `pre` through LDS) when every
         // instance's last bitfield fits the gathering block's stage

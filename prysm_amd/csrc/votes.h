@@ -54,6 +54,9 @@ struct VoteIdArgs {
   uint64_t gather_seq;
 };
 hipError_t launch_vote_ids(const VoteIdArgs& a, hipStream_t s);
+// The same two passes with the queue arrays (att_comm, bits, boffs, slots, skip) in mapped
+// pinned host memory, read in place by a per-attestation union pass (no staging copy).
+hipError_t launch_vote_ids_direct(const VoteIdArgs& a, hipStream_t s);
 // Copy `bytes` (a multiple of 16) from mapped pinned host memory to device memory in a kernel on
 // stream s: 16 B per lane, so the bytes cross PCIe in one round trip of coalesced reads.
 hipError_t launch_stage_h2d(const void* host_mapped, void* dev, uint64_t bytes, hipStream_t s);

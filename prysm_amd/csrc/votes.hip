@@ -232,6 +232,50 @@ pz_vote_leader_kernel(VoteIdArgs a) {
   }
 }
 
+// Pass 1 without a staging copy: the queue is read where the walk wrote it (pinned host memory,
+// mapped), one wave per attestation, so its bytes cross the host link once -- the 64 parent
+// slots (one coalesced 256-B load), the scalars, then the bitfield bytes (one byte per lane) --
+// instead of once into a device copy that 64 items then re-read.  Lane j ORs the bitfield into
+// the union of parent j's (slot, committee) group and elects the group's leader.
+extern "C" __global__ void __launch_bounds__(256)
+pz_vote_union_att_kernel(VoteIdArgs a) {
+  const uint64_t att = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (att >= a.natt) return;
+  const uint64_t sk = a.skip[att];
+  const uint32_t c = a.att_comm[att];
+  const uint64_t bb = a.boffs[att], nbytes = a.boffs[att + 1] - bb;
+  const uint32_t slot = a.slots[att * 64 + lane];
+  const uint64_t cb = a.coffs[c], ce = a.coffs[c + 1];
+  // an oblique parent hash (core.go:313-320) is skipped
+  const bool mine = !((sk >> lane) & 1) && slot != 0xFFFFFFFFu;
+  const uint64_t grp = (uint64_t)slot * a.ncomm + c;
+  uint32_t* u = a.ubits + grp * a.cwords;
+  for (uint64_t base = 0; base < nbytes; base += 64) {
+    const uint32_t byte = base + lane < nbytes ? (uint32_t)a.bits[bb + base + lane] : 0u;
+    const uint64_t nw = (std::min<uint64_t>(64, nbytes - base) + 3) / 4;
+    for (uint64_t w = 0; w < nw; ++w) {  // word w of this chunk: bytes 4w..4w+3, little-endian
+      const uint32_t x = (uint32_t)__shfl(byte, (int)(4 * w)) | ((uint32_t)__shfl(byte, (int)(4 * w + 1)) << 8) |
+                         ((uint32_t)__shfl(byte, (int)(4 * w + 2)) << 16) |
+                         ((uint32_t)__shfl(byte, (int)(4 * w + 3)) << 24);
+      if (mine && x) atomicOr(&u[base / 4 + w], x);
+    }
+  }
+  if (mine) {
+    a.present[slot] = 1;  // the map entry exists (core.go:322-326)
+    if (atomicOr(&a.uflag[grp], 1u) == 0)
+      a.leader[atomicAdd(a.nlead, 1u)] = make_uint4(slot, c, (uint32_t)cb, (uint32_t)(ce - cb));
+  }
+}
+
+hipError_t launch_vote_ids_direct(const VoteIdArgs& a, hipStream_t s) {
+  if (!a.natt) return hipSuccess;
+  const uint64_t threads = a.natt * 64;
+  hipLaunchKernelGGL(pz_vote_union_att_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(pz_vote_leader_kernel, dim3(kLeaderWaves / 4), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_vote_ids(const VoteIdArgs& a, hipStream_t s) {
   if (!a.natt) return hipSuccess;
   const uint64_t uthreads = a.natt * 64 * kUnionLanes;

@@ -175,6 +175,25 @@ def test_native_epoch_one_pass_dynasty_past_32_bits(B):
     _check(ne, inst, steps=2)
 
 
+@pytest.mark.parametrize("B", [1, 3])
+@pytest.mark.parametrize("d", [0xFFFE, 0xFFFF, 0xFFFFFFFE])
+def test_native_epoch_one_pass_saturated_bounds(B, d):
+    """The stream's narrow {start, end} columns classify exactly at their limits: CurrentDynasty
+    just below 0xFFFF (the 16-bit saturated column), at 0xFFFF and just below 2^32 - 1 (the 32-bit
+    one), with start and end drawn around both saturation values (start <= d < end everywhere, so
+    the committee order and the one-pass step hold), on the single launch and on pre + fused +
+    mid, two steps against the oracle."""
+    inst = _inst(4096, B, False)
+    rng = np.random.default_rng(2)
+    inst["dynasty"] = np.full(B, d, dtype=np.uint64)
+    inst["start"] = rng.choice(np.array([0, 1, d - 1, d], dtype=np.uint64), size=inst["start"].shape)
+    ends = np.array([d + 1, 0xFFFF, 0x10000, 0xFFFFFFFF, 1 << 32, 1 << 40, 9999999999999999999], dtype=np.uint64)
+    inst["end"] = rng.choice(ends[ends > d], size=inst["end"].shape)
+    ne = NativeEpoch(inst, device=0)
+    assert ne.one_pass
+    _check(ne, inst, steps=2)
+
+
 @pytest.mark.parametrize("density", [0.5, 0.75])
 def test_native_epoch_one_pass_threshold(density):
     """Half the bits set: GetAttestersTotalDeposit stays under 2/3 of TotalDeposits, so no

@@ -533,6 +533,29 @@ def test_gpu_sharded_chain_configs4_full_vs_c_port(world):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("staged", ["0", "1"])
+def test_gpu_replay_vote_queue_paths_vs_c_port(staged, monkeypatch):
+    """The vote-cache flush both ways: the walk's pinned queue read in place by the
+    per-attestation union pass (the product), and the round-3 path (PZ_VOTE_STAGED=1: the queue
+    packed into one arena, staged to the device, per-item union), over 2,000 blocks of the
+    configs[4] chain (31 transitions) against the C restatement, with a flush bound crossed
+    mid-cycle too (PZ_FLUSH_ATTS is not a knob: kFlushAtts = 65,536 queued attestations is
+    reached only by longer calls; the two-queue ping-pong runs at every transition)."""
+    monkeypatch.setenv("PZ_VOTE_STAGED", staged)
+    from prysm_amd.blockchain import BeaconChain, serialize_blocks
+    from replay_port_helpers import mismatches, port_replay
+    nval = 65536
+    blocks = synth.chain_blocks(nval, 2000, seed=6)
+    data, offs = serialize_blocks(blocks)
+    ch = BeaconChain(nval)
+    br, ar = ch.process_serialized(data[: int(offs[1000])], offs[:1001])  # two calls: the queues
+    br2, ar2 = ch.process_serialized(data, offs[1000:])                     # carry over a call
+    br, ar = np.concatenate([br, br2]), np.concatenate([ar, ar2])
+    out, port_roots = port_replay(data, offs, nval, len(ar))
+    assert mismatches(br, ar, ch.roots(), out, port_roots) == []
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("pipeline", ["0", "1"])
 def test_gpu_malformed_block_ends_the_call_there(pipeline, monkeypatch):
     """A block that is not a canonical encoding ends the call there with PZ_EINVAL, the blocks

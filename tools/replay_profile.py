@@ -26,31 +26,46 @@ def main():
     torch.cuda.synchronize()
     print("genesis %.3f s" % (time.perf_counter() - t), flush=True)
     ch.process_serialized(*serialize_blocks(blocks))  # warm-up (kernels loaded, pinned pool filled)
-    ch = BeaconChain(nval)
     prof = cProfile.Profile() if "--cprofile" in sys.argv else None
     t = time.perf_counter()
     data, offs = serialize_blocks(blocks)
     print("serialize %.3f s (%.1f MB)" % (time.perf_counter() - t, offs[-1] / 1e6), flush=True)
-    t = time.perf_counter()
-    if prof:
-        prof.enable()
-    br, ar = ch.process_serialized(data, offs)
-    torch.cuda.synchronize()
-    if prof:
-        prof.disable()
-    dt = time.perf_counter() - t
-    print("process_serialized %.3f s -> %.1f blocks/s (%d processed, %d attestations)"
-          % (dt, nblocks / dt, int((br["status"] == 0).sum()), len(ar)), flush=True)
     import ctypes
-    from prysm_amd import _lib
-    pv = (ctypes.c_double * 16)()
-    fn = _lib.lib.dll.pz_debug_chain_profile
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-    k = fn(ch._h, pv, 16)
     names = ["parse", "digests1", "att_checks+msg", "vote_queue", "vote_flush", "state_recalc", "msg_digests",
              "walk(all)", "process(all)", "count_atts", "flush_arena_wait", "msg_send",
-             "msg_hash_log", "msg_wait"]
-    print("phases (s): " + ", ".join("%s %.4f" % (names[i], pv[i]) for i in range(k)), flush=True)
+             "msg_hash_log", "msg_wait", "totals_wait", "poll_fallbacks(count)"]
+    # AB=VAR: alternate the environment variable VAR between 0 and 1 over the replays (an A/B of
+    # a per-call knob such as PZ_VOTE_STAGED in one process); REPS replays per value
+    ab = os.environ.get("AB")
+    reps = int(os.environ.get("REPS", "3"))
+    res = {}
+    for r in range(reps * (2 if ab else 1)):
+        val = str(r % 2) if ab else None
+        if ab:
+            os.environ[ab] = val
+        ch = BeaconChain(nval)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        if prof:
+            prof.enable()
+        br, ar = ch.process_serialized(data, offs)
+        torch.cuda.synchronize()
+        if prof:
+            prof.disable()
+        dt = time.perf_counter() - t
+        res.setdefault(val, []).append(nblocks / dt)
+        print("%sprocess_serialized %.3f s -> %.1f blocks/s (%d processed, %d attestations)"
+              % ("[%s=%s] " % (ab, val) if ab else "", dt, nblocks / dt, int((br["status"] == 0).sum()), len(ar)),
+              flush=True)
+        pv = (ctypes.c_double * 16)()
+        fn = _lib.lib.dll.pz_debug_chain_profile
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        k = fn(ch._h, pv, 16)
+        print("  phases (s): " + ", ".join("%s %.4f" % (names[i], pv[i]) for i in range(min(k, len(names)))),
+              flush=True)
+    for val, xs in res.items():
+        print("median%s: %.1f blocks/s over %d replays" % ("" if val is None else " [%s=%s]" % (ab, val),
+                                                          float(sorted(xs)[len(xs) // 2]), len(xs)), flush=True)
     t = time.perf_counter()
     ch.roots()
     print("roots %.3f s" % (time.perf_counter() - t), flush=True)
