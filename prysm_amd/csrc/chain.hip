@@ -719,6 +719,10 @@ struct Engine {
     uint64_t seq = 0;  // one rank: the results arrive in g.e_pin_out with this sequence word
   } deferred;
   uint64_t epoch_seq = 0;
+  // whether every validator is active at dynasty aa_dyn (the validators' dynasties never change
+  // in a chain: stateRecalc does not rotate the set), cached per dynasty value
+  uint64_t aa_dyn = UINT64_MAX;
+  bool aa = false;
   // hashing scratch (rank 0)
   PinBuf pin_msgs, pin_offs, pin_dig;  // pinned staging of the digest batch
   DevArr<uint8_t> h_in, h_out;
@@ -954,26 +958,56 @@ static uint32_t log_hash(Engine& g, const H32& h, bool votable = true) {
 // With `gq` (a stateRecalc's flush on one rank), the leader pass also gathers the 64
 // justification totals into g.tot_pin and g.ev_totals is recorded behind it: returns true
 // when it did so (tally_gather_enqueue's work is then done).
-// PZ_VOTE_STAGED=1 (A/B knob): the round-3 path -- the queue packed into one pinned arena, a
-// stage kernel copying it to the device, then the per-item union pass.
-static bool vote_staged() {  // (read per flush, so that one test process can run both paths)
-  const char* e = std::getenv("PZ_VOTE_STAGED");
-  return e && e[0] == '1';
+// One rank's stateRecalc epoch, prepared on the host (the pack in g.e_pin, the arguments) by the
+// transition's vote flush between its union and leader launches -- the host packs while the
+// device runs the stage and union passes -- and its count blocks ride in the leader launch
+// (pz_vote_leader_count_kernel), reading the pinned pack in place: two launches less per
+// transition.  `staged` / `counted`: done (else epoch_launch_rest does them).
+struct EpochLaunch {
+  EpochArgs a;
+  EpochHandoff ho;
+  size_t total = 0;      // pack bytes (a multiple of 16)
+  bool win = false;      // crosslink winners to form
+  bool staged = false, counted = false;
+  bool ready = false;    // prepared (by the flush's hook, or by state_recalc when nothing was flushed)
+};
+using EpochPrep = std::function<EpochLaunch*()>;
+
+// How a flush reaches the device (PZ_VOTE_PATH, read per flush so that one test process can
+// run every path; A/B knob):
+//   segments (product)  the walk's pinned queue arrays copied into the device pack by ONE
+//                       multi-segment stage kernel, then the per-item union pass;
+//   packed              round 3: the queue memcpy'd into one pinned arena first, one stage copy;
+//   direct              no copy: a per-attestation union pass reads the pinned queue in place
+//                       (measured slower: every wave waits out host-link round trips).
+// PZ_VOTE_UNION=att: the per-attestation union pass over the device copy instead of per item.
+enum VotePath { kVoteSegments, kVotePacked, kVoteDirect };
+static VotePath vote_path() {
+  const char* e = std::getenv("PZ_VOTE_PATH");
+  if (!e) return kVoteSegments;
+  if (!std::strcmp(e, "packed")) return kVotePacked;
+  if (!std::strcmp(e, "direct")) return kVoteDirect;
+  return kVoteSegments;
+}
+static bool vote_union_att() {
+  const char* e = std::getenv("PZ_VOTE_UNION");
+  return e && !std::strcmp(e, "att");
 }
 
-static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr) {
+static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, const EpochPrep* prep = nullptr) {
   Engine::VoteQueue& Q = g.vq[g.vq_cur];
   if (Q.natt() == 0) return false;
   const bool gather = gq && g.world == 1;
-  const bool staged = vote_staged();
+  const VotePath path = vote_path();
+  const bool staged = path != kVoteDirect;  // a device copy of the queue
   PhaseTimer pt(g.prof[kProfFlush]);
   const uint64_t natt = Q.natt();
   auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
-  // staged: packed layout boffs | skip | comm | slots | bits
+  // the device pack: boffs | skip | comm | slots | bits
   const size_t o_boffs = 0, o_skip = o_boffs + al(Q.boffs.size() * 8), o_comm = o_skip + al(natt * 8),
                o_slots = o_comm + al(natt * 4), o_bits = o_slots + al(Q.slots.size() * 4),
                total = staged ? o_bits + al(Q.bits.size()) : 0;
-  if (staged) {
+  if (path == kVotePacked) {
     if (g.q_arena_busy) {
       FineTimer pw(g.prof[kProfFlushWait]);
       for (RankDev& r : g.rk) hchk(hipEventSynchronize(r.q_ev), "event sync");
@@ -999,7 +1033,7 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr) 
         hchk(hipMemsetAsync(r.d_leader.p, 0, 16, r.s), "memset");  // both counters and the gather ticket
       }
     }
-    if (staged) {
+    if (path == kVotePacked) {
       // the pack crosses PCIe in a kernel of this stream (a copy-engine H2D costs ~13 us more on
       // the transition's critical path: the kernel behind it waits for the engine's signal)
       void* src = nullptr;
@@ -1009,6 +1043,19 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr) 
         if (!r.q_ev) hchk(hipEventCreateWithFlags(&r.q_ev, hipEventDisableTiming), "event");
         hchk(hipEventRecord(r.q_ev, r.s), "event");
       }
+    } else if (path == kVoteSegments) {
+      // the queue's pinned arrays straight into the pack, one launch (no host-side copy)
+      StageSegs sg;
+      sg.nseg = 0;
+      auto seg = [&](const void* src, size_t off, size_t bytes) {
+        if (bytes) sg.seg[sg.nseg++] = StageSeg{src, r.d_qpack.p + off, (bytes + 15) / 16};
+      };
+      seg(Q.boffs.dev(r.dev), o_boffs, Q.boffs.size() * 8);
+      seg(Q.skip.dev(r.dev), o_skip, natt * 8);
+      seg(Q.comm.dev(r.dev), o_comm, natt * 4);
+      seg(Q.slots.dev(r.dev), o_slots, Q.slots.size() * 4);
+      seg(Q.bits.dev(r.dev), o_bits, Q.bits.size());
+      hchk(launch_stage_h2d_segs(sg, r.s), "stage H2D");
     }
     if (!r.d_err.p) {
       check(r.d_err.alloc(1));
@@ -1060,13 +1107,25 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr) 
       // (pooled pinned memory holds old words: clear the sequence word before the launch)
       reinterpret_cast<volatile uint64_t*>(g.tot_pin.p)[kJustifySlots + 1] = 0;
     }
-    hchk(staged ? launch_vote_ids(v, r.s) : launch_vote_ids_direct(v, r.s), "vote tally");
+    if (prep && path == kVoteSegments && !vote_union_att()) {
+      // the union, then (host: the transition's epoch packed meanwhile) the leader pass with the
+      // epoch's count blocks
+      hchk(launch_vote_union(v, r.s), "vote union");
+      EpochLaunch* el = (*prep)();
+      hchk(launch_vote_leader_count(v, el->a, r.s), "vote leader + epoch count");
+      el->counted = true;
+    } else {
+      hchk(!staged ? launch_vote_ids_direct(v, r.s) : vote_union_att() ? launch_vote_ids_att(v, r.s)
+                                                                        : launch_vote_ids(v, r.s),
+           "vote tally");
+      if (prep) (*prep)();
+    }
     if (!gather) {  // (gathering: the walk waits for the leader pass before any later flush)
       if (!r.vq_ev[g.vq_cur]) hchk(hipEventCreateWithFlags(&r.vq_ev[g.vq_cur], hipEventDisableTiming), "event");
       hchk(hipEventRecord(r.vq_ev[g.vq_cur], r.s), "event");
     }
   });
-  if (staged) g.q_arena_busy = !gather;
+  if (path == kVotePacked) g.q_arena_busy = !gather;
   g.gather_poll = gather;
   // the walk goes on in the other queue, once the flush before last has stopped reading it (a
   // gathering flush is waited for by tally_gather_finish before the walk goes on)
@@ -1328,9 +1387,113 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, AttLo
   if (Q.natt() >= kFlushAtts) flush_votes_enqueue(g);  // bounds the queue; no host wait
 }
 
+// One rank: the epoch's arguments over the pack in g.e_pin (already built), its device buffers,
+// and the hand-off that returns its results.  The kernels read the pack from r.e_pack, which
+// the transition's flush stages (or epoch_launch_rest); PZ_EPOCH_PACK=direct (A/B knob) lets
+// them read the pinned pack in place instead.
+static EpochLaunch epoch_prepare_args(Engine& g, CState& C, size_t na, size_t nrec, uint64_t nbits, size_t o_boffs,
+                                      size_t o_rdyn, size_t o_small, size_t o_comm, size_t o_shard, size_t o_bits,
+                                      size_t total, bool in_place) {
+  EpochLaunch el;
+  RankDev& r = g.rk[0];
+  hchk(hipSetDevice(r.dev), "hipSetDevice");
+  const uint64_t nred = kScal + 2 * (uint64_t)na;
+  const uint64_t wn = (nrec + 1) / 2;
+  const size_t had = r.e_red.n;
+  check(r.e_red.alloc(nred + wn + 1));
+  if (r.e_red.n != had) hchk(hipMemsetAsync(r.e_red.p, 0, kScal * 8, r.s), "memset");  // (once per growth)
+  if (!r.e_ticket.p) {
+    check(r.e_ticket.alloc(1));
+    hchk(hipMemsetAsync(r.e_ticket.p, 0, 4, r.s), "memset");
+  }
+  check(g.e_pin_out.reserve((kScal + wn + 1) * 8));
+  void *hp = nullptr, *op = nullptr;
+  check(g.e_pin.dev(r.dev, &hp));
+  check(g.e_pin_out.dev(r.dev, &op));
+  reinterpret_cast<volatile uint64_t*>(g.e_pin_out.p)[kScal + wn] = 0;  // (pooled memory: old words)
+  const char* pk = std::getenv("PZ_EPOCH_PACK");
+  const bool direct = in_place || (pk && !std::strcmp(pk, "direct"));
+  uint8_t* d = static_cast<uint8_t*>(hp);
+  if (!direct) {
+    check(r.e_pack.alloc(total));
+    d = r.e_pack.p;
+  }
+  el.total = total;
+  el.staged = direct;  // nothing to stage when the kernels read the pinned pack
+  EpochArgs& a = el.a;
+  std::memset(&a, 0, sizeof a);
+  a.ninst = 1;
+  a.nval = r.n;
+  a.val_offset = r.lo;
+  a.nval_global = g.nval;
+  a.kind = PZ_KIND_ACTIVE;
+  a.balance = r.balance.p;
+  a.start = r.start.p;
+  a.end = r.end.p;
+  a.dynasty = reinterpret_cast<const uint64_t*>(d + o_small);
+  a.total_deposit = reinterpret_cast<const uint64_t*>(d + o_small) + 1;
+  a.natt = (uint32_t)na;
+  a.bits = d + o_bits;
+  a.boffs = reinterpret_cast<const uint64_t*>(d + o_boffs);
+  a.max_inst_bytes = nbits;
+  a.pop_rank = 0;
+  a.pop_world = 1;
+  a.committee = r.committee.p;
+  a.coffs = r.coffs.p;
+  a.att_comm = reinterpret_cast<const uint32_t*>(d + o_comm);
+  a.att_shard = reinterpret_cast<const uint32_t*>(d + o_shard);
+  a.nrec = (uint32_t)nrec;
+  a.rec_dynasty = reinterpret_cast<const uint64_t*>(d + o_rdyn);
+  a.winner = reinterpret_cast<uint32_t*>(r.e_red.p + kScal);
+  a.scal = r.e_red.p;
+  a.vote = r.e_red.p + kScal + wn;
+  a.total = r.e_red.p + kScal + wn + na;
+  a.act_mask = r.e_mask.p;
+  a.blk_cnt = r.e_blk.p;
+  a.act_list = r.e_list.p;
+  el.ho.ticket = r.e_ticket.p;
+  el.ho.out = static_cast<uint64_t*>(op);
+  el.ho.nrec = (uint32_t)nrec;
+  el.ho.seq = ++g.epoch_seq;
+  el.win = a.nrec > 0 && na > 0;
+  if (g.aa_dyn != C.dynasty) {
+    g.aa_dyn = C.dynasty;
+    g.aa = true;
+    for (uint64_t v = 0; v < g.nval && g.aa; ++v) g.aa = g.h_start[v] <= C.dynasty && C.dynasty < g.h_end[v];
+  }
+  g.deferred.nrec = nrec;
+  g.deferred.seq = el.ho.seq;
+  el.ready = true;
+  return el;
+}
+
+// The launches of a prepared one-rank epoch that the flush did not take: the stage copy and the
+// count pass (if the flush did not carry them), then winners + rewards + hand-off (one launch
+// when every validator is active, else mid with the compaction, then rewards + hand-off).
+static void epoch_launch_rest(Engine& g, EpochLaunch& el) {
+  RankDev& r = g.rk[0];
+  hchk(hipSetDevice(r.dev), "hipSetDevice");
+  if (!el.staged) {
+    void* hp = nullptr;
+    check(g.e_pin.dev(r.dev, &hp));
+    hchk(launch_stage_h2d(hp, r.e_pack.p, el.total, r.s), "stage H2D (epoch)");
+  }
+  if (!el.counted) hchk(launch_epoch_count(el.a, true, true, true, r.s), "epoch count");
+  if (g.aa) {  // no compaction: the winners run beside the rewards (one launch)
+    hchk(launch_epoch_reward_handoff(el.a, el.ho, el.win, r.s), "epoch reward");
+  } else {
+    hchk(launch_epoch_mid(el.a, el.win, true, r.s), "epoch mid");
+    hchk(launch_epoch_reward_handoff(el.a, el.ho, false, r.s), "epoch reward");
+  }
+}
+
 // processCrosslinks + CalculateRewards + next-cycle balance on the device: enqueued, its
 // results landing in pinned memory behind g.ev_epoch (collected by epoch_collect).
-static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending) {
+// out (one rank): prepare only -- the pack and the arguments into *out, the kernels read the pack
+// in place (in_place) or from the stage copy; the caller launches (the flush and
+// epoch_launch_rest).
+static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending, EpochLaunch* out = nullptr,
+                          bool in_place = false) {
   const size_t na = pending.size();
   std::vector<Crosslink>& xl = *C.xl;
   const size_t nrec = xl.size();
@@ -1367,67 +1530,12 @@ static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending
   // the previous epoch was collected (every rank's event completed), so the staging is free
   const uint64_t nred = kScal + 2 * (uint64_t)na;  // {scal, vote, total}: one all-reduce when sharded
   if (g.world == 1) {
-    // One rank: three launches and no other runtime call.  The kernels read the pack where the
-    // host wrote it (pinned, mapped), and the reward pass's last block hands the scalars and
-    // winners back into pinned memory behind a sequence word (epoch_collect polls it) and
-    // zeroes the scalars for the next epoch -- instead of an H2D, a memset, a D2H and an event.
-    RankDev& r = g.rk[0];
-    hchk(hipSetDevice(r.dev), "hipSetDevice");
-    const uint64_t wn = (nrec + 1) / 2;
-    const size_t had = r.e_red.n;
-    check(r.e_red.alloc(nred + wn + 1));
-    if (r.e_red.n != had) hchk(hipMemsetAsync(r.e_red.p, 0, kScal * 8, r.s), "memset");  // (once per growth)
-    if (!r.e_ticket.p) {
-      check(r.e_ticket.alloc(1));
-      hchk(hipMemsetAsync(r.e_ticket.p, 0, 4, r.s), "memset");
-    }
-    check(g.e_pin_out.reserve((kScal + wn + 1) * 8));
-    void *hp = nullptr, *op = nullptr;
-    check(g.e_pin.dev(r.dev, &hp));
-    check(g.e_pin_out.dev(r.dev, &op));
-    reinterpret_cast<volatile uint64_t*>(g.e_pin_out.p)[kScal + wn] = 0;  // (pooled memory: old words)
-    uint8_t* d = static_cast<uint8_t*>(hp);
-    EpochArgs a;
-    std::memset(&a, 0, sizeof a);
-    a.ninst = 1;
-    a.nval = r.n;
-    a.val_offset = r.lo;
-    a.nval_global = g.nval;
-    a.kind = PZ_KIND_ACTIVE;
-    a.balance = r.balance.p;
-    a.start = r.start.p;
-    a.end = r.end.p;
-    a.dynasty = reinterpret_cast<const uint64_t*>(d + o_small);
-    a.total_deposit = reinterpret_cast<const uint64_t*>(d + o_small) + 1;
-    a.natt = (uint32_t)na;
-    a.bits = d + o_bits;
-    a.boffs = reinterpret_cast<const uint64_t*>(d + o_boffs);
-    a.max_inst_bytes = nbits;
-    a.pop_rank = 0;
-    a.pop_world = 1;
-    a.committee = r.committee.p;
-    a.coffs = r.coffs.p;
-    a.att_comm = reinterpret_cast<const uint32_t*>(d + o_comm);
-    a.att_shard = reinterpret_cast<const uint32_t*>(d + o_shard);
-    a.nrec = (uint32_t)nrec;
-    a.rec_dynasty = reinterpret_cast<const uint64_t*>(d + o_rdyn);
-    a.winner = reinterpret_cast<uint32_t*>(r.e_red.p + kScal);
-    a.scal = r.e_red.p;
-    a.vote = r.e_red.p + kScal + wn;
-    a.total = r.e_red.p + kScal + wn + na;
-    a.act_mask = r.e_mask.p;
-    a.blk_cnt = r.e_blk.p;
-    a.act_list = r.e_list.p;
-    EpochHandoff ho;
-    ho.ticket = r.e_ticket.p;
-    ho.out = static_cast<uint64_t*>(op);
-    ho.nrec = (uint32_t)nrec;
-    ho.seq = ++g.epoch_seq;
-    hchk(launch_epoch_count(a, true, true, true, r.s), "epoch count");
-    hchk(launch_epoch_mid(a, a.nrec > 0 && na > 0, true, r.s), "epoch mid");
-    hchk(launch_epoch_reward_handoff(a, ho, r.s), "epoch reward");
-    g.deferred.nrec = nrec;
-    g.deferred.seq = ho.seq;
+    EpochLaunch el =
+        epoch_prepare_args(g, C, na, nrec, nbits, o_boffs, o_rdyn, o_small, o_comm, o_shard, o_bits, total, in_place);
+    if (out)
+      *out = el;
+    else
+      epoch_launch_rest(g, el);
     return;
   }
   g.deferred.seq = 0;
@@ -1606,13 +1714,25 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
       if (const uint32_t* sl = g.slot_of.find(g.hlog[recent_id(g, *A, i)])) q.slot[i] = *sl;
     }
   }
-  const bool gathered = flush_votes_enqueue(g, &q);
+  // one rank: the epoch is prepared inside the flush (between its union and leader launches)
+  const bool one = g.world == 1;
+  EpochLaunch el;
+  const EpochPrep prep = [&]() -> EpochLaunch* {
+    epoch_enqueue(g, *C, A->pending, &el, true);
+    return &el;
+  };
+  const bool gathered = flush_votes_enqueue(g, &q, one ? &prep : nullptr);
   PhaseTimer pt(g.prof[kProfRecalc]);
   uint64_t streak = C->streak, justified = C->jslot, finalized = C->fslot;
   const uint64_t lsr = C->lsr;
   std::vector<uint64_t> tot(kCycle, 0);
   if (!gathered) tally_gather_enqueue(g, q);
-  epoch_enqueue(g, *C, A->pending);
+  if (one) {
+    if (!el.ready) epoch_enqueue(g, *C, A->pending, &el);  // (nothing was flushed)
+    epoch_launch_rest(g, el);
+  } else {
+    epoch_enqueue(g, *C, A->pending);
+  }
   auto nc = std::make_shared<CState>();
   g.deferred.live = true;
   g.deferred.pending = A->pending;

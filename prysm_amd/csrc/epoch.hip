@@ -17,6 +17,7 @@
 
 #include "../../include/prysm_hip.h"
 #include "epoch.h"
+#include "votes_dev.h"
 
 namespace pz {
 
@@ -209,7 +210,7 @@ __device__ __forceinline__ void crosslink_wave(const EpochArgs& a, uint64_t ga, 
 // non-matching-count atomic (timing probe only: its results are wrong); 8 / 16 = the crosslink
 // balance gathers as nontemporal / sc1 loads.
 template <int V>
-__device__ __forceinline__ void count_body(const EpochArgs& a, const CountGrid& g) {
+__device__ __forceinline__ void count_body(const EpochArgs& a, const CountGrid& g, uint64_t bid) {
   __shared__ uint64_t sh[kThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -217,8 +218,8 @@ __device__ __forceinline__ void count_body(const EpochArgs& a, const CountGrid& 
   // Grid order: [crosslink blocks | validator blocks | popcount blocks]: the latency-bound
   // gathers start first.  (An even interleave measured slower: its per-block 64-bit index
   // division costs more than the overlap gains.)
-  if (blockIdx.x < g.nxb) {
-    const uint64_t x = blockIdx.x;
+  if (bid < g.nxb) {
+    const uint64_t x = bid;
     uint64_t inst, j;
     if (g.xl_affine) {  // blocks x and x+8 share an XCD: keep one instance's balances in one L2
       const uint64_t qj = x >> 3;
@@ -234,7 +235,7 @@ __device__ __forceinline__ void count_body(const EpochArgs& a, const CountGrid& 
     crosslink_wave<V>(a, inst * a.natt + att, lane);
     return;
   }
-  const uint64_t b = blockIdx.x - g.nxb;
+  const uint64_t b = bid - g.nxb;
 
   if (b < g.nvb) {  // ---- classify + count + active mask + max active index
     // Instance-major order, one chunk of 2,048 validators per block (DRAM locality).  The
@@ -362,7 +363,7 @@ __device__ __forceinline__ void count_body(const EpochArgs& a, const CountGrid& 
 }
 
 #define PZ_COUNT_KERNEL(NAME, V) \
-  extern "C" __global__ void __launch_bounds__(kThreads) NAME(EpochArgs a, CountGrid g) { count_body<V>(a, g); }
+  extern "C" __global__ void __launch_bounds__(kThreads) NAME(EpochArgs a, CountGrid g) { count_body<V>(a, g, blockIdx.x); }
 PZ_COUNT_KERNEL(pz_epoch_count_kernel, 0)
 PZ_COUNT_KERNEL(pz_epoch_count_v1_kernel, 1)
 PZ_COUNT_KERNEL(pz_epoch_count_v2_kernel, 2)
@@ -554,7 +555,7 @@ template <int MODE>
 __device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
                                             const uint64_t* __restrict__ scal_ro,
                                             const uint64_t* __restrict__ boffs_ro,
-                                            const uint64_t* __restrict__ tdep_ro) {
+                                            const uint64_t* __restrict__ tdep_ro, uint64_t inst_, uint64_t chunk_) {
   __shared__ uint64_t sh[kThreads / 64];
   // 2-D grid: x = instance, y = chunk (no per-block division).  The next
   // step's accumulators (scal_next) are zeroed at the END: a store ahead of the scalar reads
@@ -563,7 +564,7 @@ __device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
     // instance-minor order (x = instance, y = chunk): the next-cycle-total atomics of one
     // instance never arrive in a burst (measured at 1M x 16: 39 us for the pass against 45 in
     // rounds of kGroup chunks and 45 instance-major; at 65,536 x 256 all three ~39-40 us)
-    const uint64_t inst = blockIdx.x, chunk = blockIdx.y;
+    const uint64_t inst = inst_, chunk = chunk_;
     const int tid = threadIdx.x;
     uint64_t* B = a.balance + inst * a.nval;
     const uint64_t base = chunk * kValPerBlock;
@@ -675,7 +676,7 @@ __device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
     if (a.scal_next && chunk == 0 && tid < kScal) a.scal_next[inst * kScal + tid] = 0;
     return;
   }
-  const uint64_t inst = blockIdx.x, chunk = blockIdx.y;
+  const uint64_t inst = inst_, chunk = chunk_;
   const int tid = threadIdx.x;
   const uint64_t* sc = a.scal + inst * kScal;
   const uint64_t pop = sc[kPop], nact = a.nval_global - sc[kNoMatch];
@@ -723,7 +724,7 @@ __device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
   extern "C" __global__ void __launch_bounds__(kThreads)                                         \
   NAME(EpochArgs a, uint64_t vbpi, int vec, const uint64_t* __restrict__ scal_ro,                \
        const uint64_t* __restrict__ boffs_ro, const uint64_t* __restrict__ tdep_ro) {            \
-    reward_body<MODE>(a, vbpi, vec, scal_ro, boffs_ro, tdep_ro);                                  \
+    reward_body<MODE>(a, vbpi, vec, scal_ro, boffs_ro, tdep_ro, blockIdx.x, blockIdx.y);          \
   }
 PZ_REWARD_KERNEL(pz_epoch_reward_kernel, 0)
 PZ_REWARD_KERNEL(pz_epoch_reward_dbg1_kernel, 1)
@@ -740,17 +741,27 @@ PZ_REWARD_KERNEL(pz_epoch_reward_dbg3_kernel, 3)
 // atomics (s_waitcnt vmcnt(0)) before the block barrier, one lane per block adds to ONE
 // counter, the block whose add returns the last count reads with agent-scope (sc1) loads what
 // the other blocks wrote by atomics or agent-scope stores (reward_body's scalar writes).
+// nwb > 0: the crosslink winners of every attestation (the mid pass's winner threads) run as
+// the grid's first nwb blocks, beside the reward blocks -- one launch less when no compaction is
+// needed (every validator active: the reward pass reads no active list).  The winners read only
+// the count pass's tallies; a winner's processCrosslinks panic (a shard >= nrec) is then raised
+// with rewards already applied, which no caller reads (the chain is poisoned by the panic).
 extern "C" __global__ void __launch_bounds__(kThreads)
 pz_epoch_reward_handoff_kernel(EpochArgs a, uint64_t vbpi, int vec, const uint64_t* __restrict__ scal_ro,
                                const uint64_t* __restrict__ boffs_ro, const uint64_t* __restrict__ tdep_ro,
-                               EpochHandoff h) {
-  reward_body<0>(a, vbpi, vec, scal_ro, boffs_ro, tdep_ro);
+                               EpochHandoff h, uint32_t nwb) {
+  if (blockIdx.x < nwb) {
+    const uint64_t ga = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ga < (uint64_t)a.natt) winner_one(a, ga);
+  } else {
+    reward_body<0>(a, vbpi, vec, scal_ro, boffs_ro, tdep_ro, 0, blockIdx.x - nwb);
+  }
   __shared__ uint32_t last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t t = __hip_atomic_fetch_add(h.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == gridDim.x * gridDim.y - 1 ? 1u : 0u;
+    last = t == gridDim.x - 1 ? 1u : 0u;
   }
   __syncthreads();
   if (!last) return;
@@ -773,11 +784,12 @@ pz_epoch_reward_handoff_kernel(EpochArgs a, uint64_t vbpi, int vec, const uint64
 }
 
 static bool vec_ok(const EpochArgs& a);
-hipError_t launch_epoch_reward_handoff(const EpochArgs& a, const EpochHandoff& h, hipStream_t s) {
+hipError_t launch_epoch_reward_handoff(const EpochArgs& a, const EpochHandoff& h, bool winners, hipStream_t s) {
   if (a.ninst != 1) return hipErrorInvalidValue;
   const uint64_t vbpi = std::max<uint64_t>(1, vblocks_per_inst(a.nval));
-  hipLaunchKernelGGL(pz_epoch_reward_handoff_kernel, dim3(1, (uint32_t)vbpi), dim3(kThreads), 0, s, a, vbpi,
-                     vec_ok(a) ? 1 : 0, a.scal, a.boffs, a.total_deposit, h);
+  const uint32_t nwb = winners ? (uint32_t)(((uint64_t)a.natt + kThreads - 1) / kThreads) : 0u;
+  hipLaunchKernelGGL(pz_epoch_reward_handoff_kernel, dim3((uint32_t)(nwb + vbpi)), dim3(kThreads), 0, s, a, vbpi,
+                     vec_ok(a) ? 1 : 0, a.scal, a.boffs, a.total_deposit, h, nwb);
   return hipGetLastError();
 }
 
@@ -1042,7 +1054,134 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
   uint32_t g1 = kNoAtt;  // the wave's single attestation, combined across the block below
   // every wave runs the body (a wave without a piece has no element in range)
   const bool have = item < f.nitems;
-  {
+  if constexpr ((MODE & 32768) != 0) {
+    // QUAD lanes (the multi-instance se/se16 kernels): lane l takes the 4 contiguous positions
+    // p0 + 4l .. +3 of the piece (p0 the piece's window start, 4-aligned locally), so that every
+    // column load is 16 B per lane -- balance 2 x 16 B, {start, end} 16 B (se16) or 2 x 16 B
+    // (se), co_index 16 B -- where the pair layout read se16 and co_index 8 B per lane (an 8-B
+    // access streams at 0.54-0.70 of the 16-B rate, MI355X_MICROARCH.md).
+    static_assert(!PRO && (MODE & 1024), "quad lanes serve the multi-instance se/se16 kernels");
+    const uint4 it = have ? items_ro[item] : make_uint4((uint32_t)a.val_offset, 0, 0, (uint32_t)a.val_offset);
+    const uint64_t ws = it.x, we = (uint64_t)it.x + it.y, cb = it.w;
+    FusedCommittee ci;
+    {
+      const uint4 ic = have ? f.items_ci[inst * f.nitems + item] : make_uint4(0, 0, 0, kNoAtt);
+      ci.boff = pack64(ic.x, ic.y);
+      ci.nbits = ic.z;
+      ci.ga = ic.w;
+    }
+    const bool wiw = f.win_fused != 0;
+    const uint2 win1 = (wiw && ci.ga < kNoAtt) ? f.att_win[inst * a.natt + ci.ga] : make_uint2(0, 0);
+    const uint64_t p0 = (ws - a.val_offset) & ~3ull;
+    const uint64_t p = p0 + 4ull * lane, g = a.val_offset + p;
+    bool v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = g + i >= ws && g + i < we;
+    const uint64_t pp = (v[0] || v[1] || v[2] || v[3]) ? p : p0;
+    uint64_t* Bal = a.balance + inst * f.vstride;
+    const uint4 qb0 = *reinterpret_cast<const uint4*>(Bal + pp);
+    const uint4 qb1 = *reinterpret_cast<const uint4*>(Bal + pp + 2);
+    uint32_t sv[4], ev[4];
+    if (MODE & 16384) {
+      const uint4 w = ld16_nt(reinterpret_cast<const uint64_t*>(f.se16 + inst * f.vstride + pp));
+      sv[0] = w.x & 0xFFFFu, ev[0] = w.x >> 16, sv[1] = w.y & 0xFFFFu, ev[1] = w.y >> 16;
+      sv[2] = w.z & 0xFFFFu, ev[2] = w.z >> 16, sv[3] = w.w & 0xFFFFu, ev[3] = w.w >> 16;
+    } else {
+      const uint4 w0 = ld16_nt(reinterpret_cast<const uint64_t*>(f.se + inst * f.vstride + pp));
+      const uint4 w1 = ld16_nt(reinterpret_cast<const uint64_t*>(f.se + inst * f.vstride + pp + 2));
+      sv[0] = w0.x, ev[0] = w0.y, sv[1] = w0.z, ev[1] = w0.w, sv[2] = w1.x, ev[2] = w1.y, sv[3] = w1.z, ev[3] = w1.w;
+    }
+    uint32_t lcw = 0;
+    uint4 cix = make_uint4(0, 0, 0, 0);
+    if (MODE & 256)
+      lcw = f.lastco[inst * f.lcw + (pp >> 5)];
+    else
+      cix = *reinterpret_cast<const uint4*>(a.co_index + pp);
+    // the committee bitfield bytes holding the lane's positions (two at most), branch-free and
+    // clamped to the bitfield: x = g + i - cb is position g + i's bit; lanes before the committee
+    // start clamp to bit 0
+    const int64_t qs = (int64_t)(g - cb);
+    const int64_t last = (int64_t)ci.nbits - 1;
+    const int64_t qlo = qs < 0 ? 0 : qs > last ? last : qs;
+    const int64_t qhi = qs + 3 < 0 ? 0 : qs + 3 > last ? last : qs + 3;
+    uint32_t byA = 0, byB = 0;
+    if (!(MODE & 1) && ci.ga < kNoAtt && ci.nbits) {
+      byA = a.bits[ci.boff + ((uint64_t)qlo >> 3)];
+      byB = a.bits[ci.boff + ((uint64_t)qhi >> 3)];
+    }
+    uint64_t b[4] = {pack64(qb0.x, qb0.y), pack64(qb0.z, qb0.w), pack64(qb1.x, qb1.y), pack64(qb1.z, qb1.w)};
+    // crosslink tallies on the pre-reward balances (core.go:533-545)
+    if (!(MODE & 1) && ci.ga != kNoAtt) {
+      uint64_t t = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) t += v[i] ? b[i] : 0;
+      ts = wave_sum(t);
+      if (ci.ga != kManyAtt) {
+        uint64_t vv = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t x = qs + i;
+          const uint32_t by = ((x >> 3) == (qlo >> 3)) ? byA : byB;
+          if (v[i] && (uint64_t)x < (uint64_t)ci.nbits && ((by >> (7 - (uint32_t)(x & 7))) & 1)) vv += b[i];
+        }
+        vs = wave_sum(vv);
+        g1 = ci.ga;
+        if (wiw && lane == 0) one_win<false>(a, f, inst, ci.ga, vs, ts, win1);
+      } else {  // several attestations of this committee: direct atomics per attestation
+        const uint32_t* co = catt_offs_ro + inst * (f.ncomm + 1);
+        for (uint32_t k = co[it.z]; k < co[it.z + 1]; ++k) {
+          const uint64_t ga = catt_ro[inst * a.natt + k];
+          const uint64_t boff = boffs_ro[inst * a.natt + ga];
+          const uint64_t nbits = 8 * (boffs_ro[inst * a.natt + ga + 1] - boff);
+          const uint8_t* bf = a.bits + boff;
+          uint64_t vv = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint64_t x = (uint64_t)(qs + i);
+            if (v[i] && x < nbits && bit_at(bf, x)) vv += b[i];
+          }
+          vv = wave_sum(vv);
+          if (wiw && lane == 0) one_win<false>(a, f, inst, (uint32_t)ga, vv, ts, f.att_win[inst * a.natt + ga]);
+          if (lane < 2) {
+            uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + ga;
+            const uint64_t xx = lane ? vv : ts;
+            if (xx) atomicAdd((unsigned long long*)dst, (unsigned long long)xx);
+          }
+        }
+      }
+    }
+    // classify (validator.go:45-53; the saturated bounds classify exactly: d is below the
+    // saturation value), reward (incentives.go:22-27), store, sum (core.go:459-464)
+    const uint64_t d = a.dynasty[inst];
+    const uint8_t* lastbf = a.bits + lb;
+    const uint32_t ci4[4] = {cix.x, cix.y, cix.z, cix.w};
+    bool act[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      act[i] = (uint64_t)sv[i] <= d && d < (uint64_t)ev[i];
+      nm += (v[i] && !act[i]) ? 1 : 0;
+    }
+    if (applied) {  // every validator active: rank == index, the validator at p is co_index[p]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool r = (MODE & 256) ? ((lcw >> ((p + i) & 31)) & 1) : bit_at(lastbf, v[i] ? ci4[i] : 0u);
+        b[i] = r ? b[i] + PZ_ATTESTER_REWARD : b[i] - PZ_ATTESTER_REWARD;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int i = 2 * h;
+        if (v[i] && v[i + 1])
+          *reinterpret_cast<uint4*>(Bal + p + i) =
+              make_uint4((uint32_t)b[i], (uint32_t)(b[i] >> 32), (uint32_t)b[i + 1], (uint32_t)(b[i + 1] >> 32));
+        else if (v[i])
+          Bal[p + i] = b[i];
+        else if (v[i + 1])
+          Bal[p + i + 1] = b[i + 1];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sum += (v[i] && act[i]) ? b[i] : 0;
+  } else {
     // {first position, count, committee, committee start}
     // (ablation 64: the piece computed from its index -- 256 positions, wrong tallies -- so the
     // stream loads do not wait for the item load)
@@ -1354,12 +1493,18 @@ __device__ __forceinline__ void one_tail(const EpochArgs& a, const FusedArgs& f,
   }
 PZ_FUSED_KERNEL(pz_epoch_fused_kernel, 0)
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_kernel, 256)  // reward bits from FusedArgs.lastco
-PZ_FUSED_KERNEL(pz_epoch_fused_se_kernel, 1024)  // start/end from FusedArgs.se
-PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_kernel, 1280)
+// the product's multi-instance kernels take quad lanes (32768)
+PZ_FUSED_KERNEL(pz_epoch_fused_se_kernel, 1024 + 32768)  // start/end from FusedArgs.se
+PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_kernel, 1280 + 32768)
 PZ_FUSED_KERNEL(pz_epoch_fused_se_xcd_kernel, 1024 + 4096)     // the XCD-aware 1-D grid
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_xcd_kernel, 1280 + 4096)
-PZ_FUSED_KERNEL(pz_epoch_fused_se16_kernel, 1024 + 16384)       // start/end from FusedArgs.se16
-PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_kernel, 1280 + 16384)
+PZ_FUSED_KERNEL(pz_epoch_fused_se16_kernel, 1024 + 16384 + 32768)  // start/end from FusedArgs.se16
+PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_kernel, 1280 + 16384 + 32768)
+// (A/B, variant 32768: the round-3 pair lanes)
+PZ_FUSED_KERNEL(pz_epoch_fused_se_pair_kernel, 1024)
+PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_pair_kernel, 1280)
+PZ_FUSED_KERNEL(pz_epoch_fused_se16_pair_kernel, 1024 + 16384)
+PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_pair_kernel, 1280 + 16384)
 PZ_FUSED_KERNEL(pz_epoch_fused_se16_xcd_kernel, 1024 + 4096 + 16384)
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_xcd_kernel, 1280 + 4096 + 16384)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg1_kernel, 1)
@@ -1374,6 +1519,240 @@ PZ_FUSED_KERNEL(pz_epoch_fused_dbg32_kernel, 32)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg48_kernel, 48)
 PZ_FUSED_KERNEL(pz_epoch_fused_dbg1088_kernel, 1088)  // se, piece from its index (no item -> stream hop)
 #undef PZ_FUSED_KERNEL
+
+// ---- the streaming form of the fused pass (product at B > 1, one rank or sharded) -------------
+// Persistent waves: W = gridDim.x * 8 waves, W a multiple of B, so wave w always serves
+// instance w % B and takes its pieces item = w / B + j * (W / B) in turn (adjacent waves: the
+// same pieces of the next instance, whose co_index words they share in L2).  The loads of each
+// piece are software-pipelined (the round-3 wave ran one piece through three dependent round
+// trips -- item, stream, reward-bit lookups -- and retired): while piece k's reward bits are
+// looked up, piece k+1's stream is in flight and piece k+2's item is being fetched.  There is
+// no block barrier: each wave adds its pieces' tallies (two atomics per piece, to the piece's
+// attestation) and, at its end, its instance's next-cycle partial sum (one atomic per wave).
+// Lane l takes 4 contiguous positions of a piece (16-B column loads, as the quad lanes).
+struct StreamA {  // piece descriptor: {first position, count, committee, committee start}, committee info
+  uint4 it, ic;
+};
+struct StreamB {  // the piece's stream
+  uint4 qb0, qb1, se, cix;
+  uint32_t lcw, byA, byB;
+  uint2 win1;
+};
+
+template <int MODE>
+__device__ __forceinline__ StreamA stream_load_a(const FusedArgs& f, const uint4* __restrict__ items_ro, uint64_t inst,
+                                                 uint64_t item, uint64_t val_offset) {
+  StreamA x;
+  const bool have = item < f.nitems;
+  x.it = have ? items_ro[item] : make_uint4((uint32_t)val_offset, 0, 0, (uint32_t)val_offset);
+  x.ic = have ? f.items_ci[inst * f.nitems + item] : make_uint4(0, 0, 0, kNoAtt);
+  return x;
+}
+
+template <int MODE>
+__device__ __forceinline__ StreamB stream_load_b(const EpochArgs& a, const FusedArgs& f, uint64_t inst, const StreamA& x,
+                                                 int lane) {
+  StreamB y;
+  const uint64_t ws = x.it.x, we = (uint64_t)x.it.x + x.it.y, cb = x.it.w;
+  const uint64_t p0 = (ws - a.val_offset) & ~3ull, p = p0 + 4ull * lane, g = a.val_offset + p;
+  const bool any = g + 3 >= ws && g < we;
+  const uint64_t pp = any ? p : p0;
+  const uint64_t* Bal = a.balance + inst * f.vstride;
+  y.qb0 = *reinterpret_cast<const uint4*>(Bal + pp);
+  y.qb1 = *reinterpret_cast<const uint4*>(Bal + pp + 2);
+  y.se = ld16_nt(reinterpret_cast<const uint64_t*>(f.se16 + inst * f.vstride + pp));  // {start | end << 16}
+  const uint32_t ga = x.ic.w;
+  // (MODE & 131072: the winners formed in the waves, FusedArgs.win_fused)
+  y.win1 = ((MODE & 131072) && ga < kNoAtt) ? f.att_win[inst * a.natt + ga] : make_uint2(0, 0);
+  if (MODE & 256) {  // the reward bits in position order (pre's gather)
+    y.lcw = f.lastco[inst * f.lcw + (pp >> 5)];
+    y.cix = make_uint4(0, 0, 0, 0);
+  } else {
+    y.cix = *reinterpret_cast<const uint4*>(a.co_index + pp);
+    y.lcw = 0;
+  }
+  const uint64_t boff = pack64(x.ic.x, x.ic.y);
+  const uint32_t nbits = x.ic.z;
+  const int64_t qs = (int64_t)(g - cb), last = (int64_t)nbits - 1;
+  const int64_t qlo = qs < 0 ? 0 : qs > last ? last : qs;
+  const int64_t qhi = qs + 3 < 0 ? 0 : qs + 3 > last ? last : qs + 3;
+  y.byA = y.byB = 0;
+  if (ga < kNoAtt && nbits) {
+    y.byA = a.bits[boff + ((uint64_t)qlo >> 3)];
+    y.byB = a.bits[boff + ((uint64_t)qhi >> 3)];
+  }
+  return y;
+}
+
+template <int MODE>
+__device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro,
+                                                   const uint64_t* __restrict__ boffs_ro,
+                                                   const uint64_t* __restrict__ tdep_ro,
+                                                   const uint4* __restrict__ items_ro,
+                                                   const uint32_t* __restrict__ catt_offs_ro,
+                                                   const uint32_t* __restrict__ catt_ro) {
+  static_assert((MODE & 16384) != 0, "the streaming pass reads the 16-bit {start, end} column");
+  const int lane = threadIdx.x & 63;
+  const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t B = a.ninst, W = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t inst = w % B, item0 = w / B, stride = W / B;
+  // the instance's scalars (GetAttestersTotalDeposit from `pre`, the threshold, the panics)
+  const uint64_t pop = pre_ro[inst * kPre], ferr = pre_ro[inst * kPre + 1];
+  const uint64_t lb = boffs_ro[inst * a.natt + a.natt - 1];
+  const uint64_t L = boffs_ro[inst * a.natt + a.natt] - lb;
+  const bool rwd_err = (a.nval_global - 1) >= 8 * L;              // CheckBit(last, N-1) panics (incentives.go:23)
+  const bool thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (tdep_ro[inst] * 2ull);  // incentives.go:18-20
+  const bool skip = ferr != 0 || (thr && rwd_err);                  // Go panics: balances stay untouched
+  const bool applied = thr && !skip;
+  const uint64_t d = a.dynasty[inst];
+  const uint8_t* lastbf = a.bits + lb;
+  uint64_t* Bal = a.balance + inst * f.vstride;
+  uint64_t sum = 0, nm = 0;
+  // pipeline: A(k+1) and B(k) in flight when piece k is processed; A(k+2) issued during it
+  uint64_t item = item0;
+  StreamA ca = stream_load_a<MODE>(f, items_ro, inst, item, a.val_offset);
+  StreamB cb_ = stream_load_b<MODE>(a, f, inst, ca, lane);
+  StreamA na = stream_load_a<MODE>(f, items_ro, inst, item + stride, a.val_offset);
+  for (; item < f.nitems; item += stride) {
+    // the reward bits of this piece (dependent on its co_index words): issued first
+    const uint64_t ws = ca.it.x, we = (uint64_t)ca.it.x + ca.it.y, cbase = ca.it.w;
+    const uint64_t p0 = (ws - a.val_offset) & ~3ull, p = p0 + 4ull * lane, g = a.val_offset + p;
+    bool v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = g + i >= ws && g + i < we;
+    uint32_t rb[4] = {0, 0, 0, 0};
+    if (!(MODE & 256) && applied) {
+      const uint32_t ci4[4] = {cb_.cix.x, cb_.cix.y, cb_.cix.z, cb_.cix.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t ix = v[i] ? ci4[i] : 0u;
+        rb[i] = lastbf[ix >> 3];
+      }
+    }
+    // the next piece's stream, then the one after's descriptor
+    StreamB nb = stream_load_b<MODE>(a, f, inst, na, lane);
+    const StreamA nna = stream_load_a<MODE>(f, items_ro, inst, item + 2 * stride, a.val_offset);
+    uint64_t b[4] = {pack64(cb_.qb0.x, cb_.qb0.y), pack64(cb_.qb0.z, cb_.qb0.w), pack64(cb_.qb1.x, cb_.qb1.y),
+                     pack64(cb_.qb1.z, cb_.qb1.w)};
+    // crosslink tallies on the pre-reward balances (core.go:533-545)
+    const uint32_t ga = ca.ic.w, nbits = ca.ic.z;
+    if (ga != kNoAtt) {
+      uint64_t t = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) t += v[i] ? b[i] : 0;
+      const uint64_t ts = wave_sum(t);
+      const int64_t qs = (int64_t)(g - cbase), last = (int64_t)nbits - 1;
+      const int64_t qlo = qs < 0 ? 0 : qs > last ? last : qs;
+      if (ga != kManyAtt) {
+        uint64_t vv = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t x = qs + i;
+          const uint32_t by = ((x >> 3) == (qlo >> 3)) ? cb_.byA : cb_.byB;
+          if (v[i] && (uint64_t)x < (uint64_t)nbits && ((by >> (7 - (uint32_t)(x & 7))) & 1)) vv += b[i];
+        }
+        const uint64_t vs = wave_sum(vv);
+        if ((MODE & 131072) && lane == 0) one_win<false>(a, f, inst, ga, vs, ts, cb_.win1);
+        if (lane < 2) {  // one instruction: lane 0 the total, lane 1 the vote
+          uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + ga;
+          const uint64_t xx = lane ? vs : ts;
+          if (xx) atomicAdd((unsigned long long*)dst, (unsigned long long)xx);
+        }
+      } else {  // several attestations of this committee: one pair of atomics per attestation
+        const uint32_t* co = catt_offs_ro + inst * (f.ncomm + 1);
+        for (uint32_t k = co[ca.it.z]; k < co[ca.it.z + 1]; ++k) {
+          const uint64_t gk = catt_ro[inst * a.natt + k];
+          const uint64_t boff = boffs_ro[inst * a.natt + gk];
+          const uint64_t nb2 = 8 * (boffs_ro[inst * a.natt + gk + 1] - boff);
+          const uint8_t* bf = a.bits + boff;
+          uint64_t vv = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint64_t x = (uint64_t)(qs + i);
+            if (v[i] && x < nb2 && bit_at(bf, x)) vv += b[i];
+          }
+          vv = wave_sum(vv);
+          if ((MODE & 131072) && lane == 0) one_win<false>(a, f, inst, (uint32_t)gk, vv, ts, f.att_win[inst * a.natt + gk]);
+          if (lane < 2) {
+            uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + gk;
+            const uint64_t xx = lane ? vv : ts;
+            if (xx) atomicAdd((unsigned long long*)dst, (unsigned long long)xx);
+          }
+        }
+      }
+    }
+    // classify (validator.go:45-53), reward (incentives.go:22-27), store, sum (core.go:459-464)
+    const uint32_t sw[4] = {cb_.se.x, cb_.se.y, cb_.se.z, cb_.se.w};
+    bool act[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      act[i] = (uint64_t)(sw[i] & 0xFFFFu) <= d && d < (uint64_t)(sw[i] >> 16);
+      nm += (v[i] && !act[i]) ? 1 : 0;
+    }
+    if (applied) {
+      const uint32_t ci4[4] = {cb_.cix.x, cb_.cix.y, cb_.cix.z, cb_.cix.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool r = (MODE & 256) ? ((cb_.lcw >> ((p + i) & 31)) & 1)
+                                    : ((rb[i] >> (7 - ((v[i] ? ci4[i] : 0u) & 7))) & 1);
+        b[i] = r ? b[i] + PZ_ATTESTER_REWARD : b[i] - PZ_ATTESTER_REWARD;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int i = 2 * h;
+        if (v[i] && v[i + 1])
+          *reinterpret_cast<uint4*>(Bal + p + i) =
+              make_uint4((uint32_t)b[i], (uint32_t)(b[i] >> 32), (uint32_t)b[i + 1], (uint32_t)(b[i + 1] >> 32));
+        else if (v[i])
+          Bal[p + i] = b[i];
+        else if (v[i + 1])
+          Bal[p + i + 1] = b[i + 1];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sum += (v[i] && act[i]) ? b[i] : 0;
+    ca = na;
+    cb_ = nb;
+    na = nna;
+  }
+  sum = wave_sum(sum);
+  nm = wave_sum(nm);
+  uint64_t* sc = a.scal + inst * kScal;
+  if (lane == 0) {
+    if (sum && !skip) atomicAdd((unsigned long long*)&sc[kNextBal], (unsigned long long)sum);
+    if (nm) {  // the layout's rank == index premise is broken (the state never allows it)
+      atomicAdd((unsigned long long*)&sc[kNoMatch], (unsigned long long)nm);
+      atomicOr((unsigned long long*)&sc[kErrXl], (unsigned long long)kErrLayout);
+    }
+  }
+  if (item0 == 0) {  // the wave holding the instance's first piece: the per-instance scalars
+    if (lane == 0 && f.rank0) {
+      sc[kPop] = pop;
+      sc[kApplied] = applied ? 1 : 0;
+      sc[kNact] = a.nval_global;
+      sc[kMaxIdx1] = a.nval_global;
+      sc[kErrRwd] = rwd_err ? 1 : 0;
+      if (ferr) atomicAdd((unsigned long long*)&sc[kErrXl], (unsigned long long)ferr);
+    }
+    if (a.scal_next && lane < kScal) a.scal_next[inst * kScal + lane] = 0;
+    if (lane < kPre) f.pre_next[inst * kPre + lane] = 0;
+  }
+}
+
+#define PZ_STREAM_KERNEL(NAME, MODE)                                                                         \
+  extern "C" __global__ void __launch_bounds__(256) NAME(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro, \
+                                                        const uint64_t* __restrict__ boffs_ro,                  \
+                                                        const uint64_t* __restrict__ tdep_ro,                   \
+                                                        const uint4* __restrict__ items_ro,                     \
+                                                        const uint32_t* __restrict__ catt_offs_ro,              \
+                                                        const uint32_t* __restrict__ catt_ro) {                 \
+    stream_kernel_body<MODE>(a, f, pre_ro, boffs_ro, tdep_ro, items_ro, catt_offs_ro, catt_ro);                  \
+  }
+PZ_STREAM_KERNEL(pz_epoch_stream_se16_kernel, 1024 + 16384)
+PZ_STREAM_KERNEL(pz_epoch_stream_lc_se16_kernel, 1280 + 16384)
+PZ_STREAM_KERNEL(pz_epoch_stream_se16_win_kernel, 1024 + 16384 + 131072)
+PZ_STREAM_KERNEL(pz_epoch_stream_lc_se16_win_kernel, 1280 + 16384 + 131072)
+#undef PZ_STREAM_KERNEL
 
 // The single-launch step (one instance): no occupancy target (a few dozen blocks), so the
 // bit-count loads the prologue holds do not spill.
@@ -1436,7 +1815,7 @@ static bool vec_ok(const EpochArgs& a) {
   return (a.nval % 2 == 0) && al(a.start) && al(a.end) && al(a.balance);
 }
 
-hipError_t launch_epoch_count(const EpochArgs& a, bool do_val, bool do_pop, bool do_xl, hipStream_t s) {
+static CountGrid count_grid(const EpochArgs& a, bool do_val, bool do_pop, bool do_xl) {
   CountGrid g;
   g.vbpi = vblocks_per_inst(a.nval);
   g.nvb = do_val ? (g_count_variant & 1 ? (g.vbpi + kGroup - 1) / kGroup * kGroup * a.ninst
@@ -1455,6 +1834,11 @@ hipError_t launch_epoch_count(const EpochArgs& a, bool do_val, bool do_pop, bool
   g.xl_affine = a.ninst >= 8 ? 1 : 0;
   const uint64_t xl_inst = g.xl_affine ? ((uint64_t)a.ninst + 7) / 8 * 8 : a.ninst;
   g.nxb = (do_xl && a.natt) ? xl_inst * g.xl_j : 0;
+  return g;
+}
+
+hipError_t launch_epoch_count(const EpochArgs& a, bool do_val, bool do_pop, bool do_xl, hipStream_t s) {
+  const CountGrid g = count_grid(a, do_val, do_pop, do_xl);
   const uint64_t blocks = g.nvb + g.npb + g.nxb;
   if (!blocks) return hipSuccess;
   const dim3 grid((uint32_t)blocks);
@@ -1468,6 +1852,26 @@ hipError_t launch_epoch_count(const EpochArgs& a, bool do_val, bool do_pop, bool
     case 16: hipLaunchKernelGGL(pz_epoch_count_v16_kernel, grid, dim3(kThreads), 0, s, a, g); break;
     default: hipLaunchKernelGGL(pz_epoch_count_kernel, grid, dim3(kThreads), 0, s, a, g);
   }
+  return hipGetLastError();
+}
+
+// A stateRecalc's vote-cache leader pass and its epoch's count pass in ONE launch (the chain
+// engine, one rank): blocks [0, nlb) are the leader pass (votes_dev.h), the rest the count
+// pass's blocks.  The two read the same pre-reward balances and write disjoint buffers; the
+// leader blocks come first, so the walk's wait (their gathered totals) is not behind the count.
+extern "C" __global__ void __launch_bounds__(kThreads)
+pz_vote_leader_count_kernel(VoteIdArgs v, uint32_t nlb, EpochArgs a, CountGrid g) {
+  if (blockIdx.x < nlb)
+    vote_leader_body(v, nlb, blockIdx.x);
+  else
+    count_body<0>(a, g, blockIdx.x - nlb);
+}
+
+hipError_t launch_vote_leader_count(const VoteIdArgs& v, const EpochArgs& a, hipStream_t s) {
+  const CountGrid g = count_grid(a, true, true, true);
+  const uint32_t nlb = kLeaderWaves / 4;
+  const uint64_t blocks = nlb + g.nvb + g.npb + g.nxb;
+  hipLaunchKernelGGL(pz_vote_leader_count_kernel, dim3((uint32_t)blocks), dim3(kThreads), 0, s, v, nlb, a, g);
   return hipGetLastError();
 }
 
@@ -1531,7 +1935,11 @@ hipError_t launch_epoch_fwin(const EpochArgs& a, const FusedArgs& f, hipStream_t
 
 // Ablations look the reward bits up in the fused pass (tools/; 128: this A/B); the grid-order
 // variant (the XCD-aware 4096) keeps the product's gather.
-static bool ablation_no_lastco() { return g_fused_variant && g_fused_variant != 4096; }
+// (grid/lane-layout variants keep it: 4096 XCD-aware grid, 32768 pair lanes, 65536 one piece per
+// wave with quad lanes -- the streaming pass off)
+static bool ablation_no_lastco() {
+  return g_fused_variant && g_fused_variant != 4096 && g_fused_variant != 32768 && g_fused_variant != 65536;
+}
 
 hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f0, hipStream_t s) {
   FusedArgs f = f0;
@@ -1546,6 +1954,26 @@ hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f0, hipStream_t
   hipLaunchKernelGGL(pz_epoch_pre_kernel, dim3((uint32_t)(npb + nab + nlb)), dim3(kThreads), 0, s, a, f, pbpi, npb,
                      nab, lcb);
   return hipGetLastError();
+}
+
+// Blocks (4 waves each) of the streaming pass: about one resident wave per SIMD slot
+// (occupancy x CUs), rounded to a multiple of lcm(4, B) waves so that every wave serves one
+// instance, and no more waves than pieces.
+static uint64_t resident_waves(const void* kernel) {
+  int dev = 0, cus = 256, per = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess || per < 1) per = 4;
+  return (uint64_t)cus * (uint64_t)per * 4;
+}
+static uint32_t stream_blocks(uint64_t B, uint64_t nitems, bool lc) {
+  static const uint64_t res_plain = resident_waves((const void*)pz_epoch_stream_se16_kernel);
+  static const uint64_t res_lc = resident_waves((const void*)pz_epoch_stream_lc_se16_kernel);
+  const uint64_t resident = lc ? res_lc : res_plain;
+  const uint64_t l = B % 4 == 0 ? B : B % 2 == 0 ? 2 * B : 4 * B;  // lcm(4, B)
+  const uint64_t want = std::min<uint64_t>(resident, B * std::max<uint64_t>(1, nitems));
+  const uint64_t W = std::max<uint64_t>(l, want / l * l);
+  return (uint32_t)(W / 4);
 }
 
 hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream_t s) {
@@ -1567,6 +1995,17 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream
 #undef PZ_LAUNCH_XCD
     return hipGetLastError();
   }
+  if (variant == 0 && f.se16 && a.ninst > 1) {  // the streaming form (persistent, pipelined waves)
+    const uint32_t nb = stream_blocks(a.ninst, f.nitems, f.lastco != nullptr);
+#define PZ_LAUNCH_STREAM(K) \
+  hipLaunchKernelGGL(K, dim3(nb), dim3(256), 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.catt_offs, f.catt)
+    if (f.win_fused && f.lastco) PZ_LAUNCH_STREAM(pz_epoch_stream_lc_se16_win_kernel);
+    else if (f.win_fused) PZ_LAUNCH_STREAM(pz_epoch_stream_se16_win_kernel);
+    else if (f.lastco) PZ_LAUNCH_STREAM(pz_epoch_stream_lc_se16_kernel);
+    else PZ_LAUNCH_STREAM(pz_epoch_stream_se16_kernel);
+#undef PZ_LAUNCH_STREAM
+    return hipGetLastError();
+  }
   // (the ablations that read FusedArgs.se run the product's kernel when the state holds se16)
   const int var = ((variant & 1024) && !f.se) ? 0 : variant;
   // instance-minor: x = instance, y = piece group (ablation 32: instance-major)
@@ -1574,6 +2013,13 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream
   const dim3 block(64 * kFusedWaves);
 #define PZ_LAUNCH_FUSED(K) \
   hipLaunchKernelGGL(K, grid, block, 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt)
+  if (variant == 32768 && (f.se || f.se16)) {  // A/B: the pair lanes of round 3
+    if (f.se16 && f.lastco) PZ_LAUNCH_FUSED(pz_epoch_fused_lc_se16_pair_kernel);
+    else if (f.se16) PZ_LAUNCH_FUSED(pz_epoch_fused_se16_pair_kernel);
+    else if (f.lastco) PZ_LAUNCH_FUSED(pz_epoch_fused_lc_se_pair_kernel);
+    else PZ_LAUNCH_FUSED(pz_epoch_fused_se_pair_kernel);
+    return hipGetLastError();
+  }
   switch (var) {
     case 1: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg1_kernel); break;
     case 2: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg2_kernel); break;

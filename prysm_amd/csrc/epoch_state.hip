@@ -523,7 +523,7 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
     s.grank = comm ? comm->rank0 + i : 0;
     shard_range(h, pl, s.grank, st->world, &s.lo, &s.hi);
     s.n = s.hi - s.lo;
-    s.np = st->fused ? (s.n + 1) & ~1ull : s.n;
+    s.np = st->fused ? (s.n + 3) & ~3ull : s.n;  // (rows of the one-pass stream: 16-B quads of u32)
     s.wl = (s.n + 63) / 64;
     DeviceCtx* dc;
     if ((rc = device_ctx(s.dev, &dc))) break;
@@ -602,11 +602,13 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
     uint64_t nitems = 0;
     std::vector<uint4> items;
     if (st->fused) {
-      // committee pieces inside [lo, hi): <= 256 positions from the committee's first even
-      // local position (local index = position - lo; the kernel pairs even local indices)
+      // committee pieces inside [lo, hi): <= 256 positions of a window that starts at the
+      // committee's first local position rounded down to a multiple of 4 (local index = position
+      // - lo; the quad kernels give each lane 4 positions from there, the pair kernels 2 from the
+      // piece's even position)
       for (uint64_t c = 0; c < st->ncomm; ++c) {
         const uint64_t cb = h->coffs[c], ce = h->coffs[c + 1];
-        const uint64_t r0 = std::max(cb, s.lo), r1 = std::min(ce, s.hi), base = s.lo + ((r0 - s.lo) & ~1ull);
+        const uint64_t r0 = std::max(cb, s.lo), r1 = std::min(ce, s.hi), base = s.lo + ((r0 - s.lo) & ~3ull);
         for (uint64_t x = r0; x < r1;) {
           const uint64_t y = std::min(r1, base + ((x - base) / 256 + 1) * 256);
           items.push_back(make_uint4((uint32_t)x, (uint32_t)(y - x), (uint32_t)c, (uint32_t)cb));

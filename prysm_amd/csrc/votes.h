@@ -54,9 +54,26 @@ struct VoteIdArgs {
   uint64_t gather_seq;
 };
 hipError_t launch_vote_ids(const VoteIdArgs& a, hipStream_t s);
+// Pass 1 alone (the per-item union); pass 2 then runs as launch_vote_leader_count (epoch.h).
+hipError_t launch_vote_union(const VoteIdArgs& a, hipStream_t s);
 // The same two passes with the queue arrays (att_comm, bits, boffs, slots, skip) in mapped
 // pinned host memory, read in place by a per-attestation union pass (no staging copy).
 hipError_t launch_vote_ids_direct(const VoteIdArgs& a, hipStream_t s);
+// The per-attestation union pass (as launch_vote_ids_direct) over device copies of the queue.
+hipError_t launch_vote_ids_att(const VoteIdArgs& a, hipStream_t s);
+// Up to 6 copies from mapped pinned memory to device memory in ONE launch (16 B per lane; the
+// sources may be read up to 15 bytes past their ends, so a source buffer's capacity must cover
+// ceil16 of its bytes).
+struct StageSeg {
+  const void* src;
+  void* dst;
+  uint64_t n16;
+};
+struct StageSegs {
+  StageSeg seg[6];
+  int nseg;
+};
+hipError_t launch_stage_h2d_segs(const StageSegs& g, hipStream_t s);
 // Copy `bytes` (a multiple of 16) from mapped pinned host memory to device memory in a kernel on
 // stream s: 16 B per lane, so the bytes cross PCIe in one round trip of coalesced reads.
 hipError_t launch_stage_h2d(const void* host_mapped, void* dev, uint64_t bytes, hipStream_t s);

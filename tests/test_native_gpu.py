@@ -85,15 +85,18 @@ def test_native_epoch_single_launch(n, density):
     _check(ne, inst, steps=3)
 
 
+@pytest.mark.parametrize("variant", [4096, 32768, 65536])
 @pytest.mark.parametrize("n,B", [(65536, 5), (32768, 9), (4097, 3), (1000, 2)])
-def test_native_epoch_xcd_grid(n, B):
-    """The one-pass step's fused pass on the XCD-aware 1-D grid (fused variant 4096: block L
-    on XCD L % 8 takes piece group 8 (L / 8 / B) + L % 8 of instance (L / 8) % B, the pad groups
-    exit), two steps bit-exact against the oracle."""
+def test_native_epoch_fused_forms(n, B, variant):
+    """The other forms of the one-pass step's fused pass (the product is the streaming pass:
+    persistent pipelined waves): 4096 the XCD-aware 1-D grid (block L on XCD L % 8 takes piece
+    group 8 (L / 8 / B) + L % 8 of instance (L / 8) % B, the pad groups exit), 32768 one piece
+    per wave on pair lanes (round 3), 65536 one piece per wave on quad lanes; two steps each,
+    bit-exact against the oracle."""
     inst = _inst(n, B, False)
     ne = NativeEpoch(inst, device=0)
     assert ne.one_pass
-    old = _lib.lib.dll.pz_debug_set_fused_variant(4096)
+    old = _lib.lib.dll.pz_debug_set_fused_variant(variant)
     try:
         _check(ne, inst, steps=2)
     finally:

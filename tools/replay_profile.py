@@ -34,13 +34,15 @@ def main():
     names = ["parse", "digests1", "att_checks+msg", "vote_queue", "vote_flush", "state_recalc", "msg_digests",
              "walk(all)", "process(all)", "count_atts", "flush_arena_wait", "msg_send",
              "msg_hash_log", "msg_wait", "totals_wait", "poll_fallbacks(count)"]
-    # AB=VAR: alternate the environment variable VAR between 0 and 1 over the replays (an A/B of
-    # a per-call knob such as PZ_VOTE_STAGED in one process); REPS replays per value
+    # AB=VAR: alternate the environment variable VAR over the values AB_VALUES (default "0,1")
+    # across the replays (an A/B of a per-call knob such as PZ_VOTE_PATH in one process); REPS
+    # replays per value
     ab = os.environ.get("AB")
+    vals = os.environ.get("AB_VALUES", "0,1").split(",")
     reps = int(os.environ.get("REPS", "3"))
     res = {}
-    for r in range(reps * (2 if ab else 1)):
-        val = str(r % 2) if ab else None
+    for r in range(reps * (len(vals) if ab else 1)):
+        val = vals[r % len(vals)] if ab else None
         if ab:
             os.environ[ab] = val
         ch = BeaconChain(nval)
