@@ -147,26 +147,30 @@ def launch_ranks(args):
 # dynasty + 16 B balance read-modify-write + 1/8 B last-bitfield bit + 1/8 B committee bitfield
 # popcount + 12 B crosslink committee gather (u32 member + u64 balance).
 EPOCH_BYTES_PER_VALIDATOR = 44.25
+COLD_STATE_BYTES = 800_000_000  # the epoch cold leg's streamed state, >= 3x the 256 MiB Infinity Cache
 
 
-def epoch_layout_bytes(inst, one_pass):
-    """Bytes per validator-epoch the one-pass committee-order step must move:
-    the balance read and written (16), the {start, end} dynasties (4 in the 16-bit saturated
-    column the state uploads when every CurrentDynasty is below 0xFFFF, 8 in the 32-bit one
-    below 2^32 - 1, else 16), and the instance's
-    bitfields once (their bytes / nval); co_index is shared by the instances (L2).  None for
-    the other layouts (SURVEY.md §8d's 44.25 B stays their model)."""
-    if not one_pass:
+def epoch_layout_bytes(inst, de):
+    """Bytes per validator-epoch the one-pass committee-order step must move, from
+    the widths the state actually uploaded (pz_epoch_state_columns): the balance read and
+    written (2 x 4 B as u32 offsets from a per-instance base, or 2 x 8 B), the {start, end}
+    dynasties (4 B in the 16-bit saturated column, 8 B in the 32-bit one, else 16 B), and the
+    instance's bitfields once (their bytes / nval); co_index is shared by the instances (L2).
+    None for the other layouts (SURVEY.md §8d's 44.25 B stays their model)."""
+    if de is None or not getattr(de, "one_pass", False):
         return None
-    dmax = int(np.max(inst["dynasty"]))
-    if os.environ.get("PZ_EPOCH_SE64") or dmax >= 0xFFFFFFFF:
-        se = 16  # the 64-bit start and end columns
-    elif dmax < 0xFFFF and not os.environ.get("PZ_EPOCH_SE32"):
-        se = 4  # {start, end} saturated to 16 bits (epoch_state.hip upload_se16)
-    else:
-        se = 8  # saturated to 32 bits
     bits = float(inst["boffs"][-1]) / (inst["ninst"] * inst["nval"])
-    return 16 + se + bits
+    return 2 * de.balance_bytes + de.dynasty_bytes + bits
+
+
+def epoch_bytes_model(de, bpv):
+    if bpv is None:
+        return "SURVEY.md §8d: 44.25 B per validator-epoch"
+    return ("the one-pass committee-order layout's bytes: %.2f B per validator-epoch (balance read + write "
+            "2 x %d, {start, end} %d, bitfields %.2f; DESIGN.md §3)"
+            % (bpv, de.balance_bytes, de.dynasty_bytes, bpv - 2 * de.balance_bytes - de.dynasty_bytes))
+
+
 HASH_KERNEL = "pz_b2b_fixed_persistent_kernel"
 CPU_SAMPLE_S = 8.0  # seconds of CPU work per cpu_baseline leg (three legs: ~25 s in all)
 
@@ -270,7 +274,7 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
     units = nval * ninst * args.steps
     local_units = (hi - lo) * ninst
     one_pass = native and de.one_pass
-    lay = epoch_layout_bytes(inst, one_pass)
+    lay = epoch_layout_bytes(inst, de if native else None)
     bpv = lay if lay is not None else EPOCH_BYTES_PER_VALIDATOR
     achieved = local_units * bpv / (step_ms * 1e-3)
     survey = local_units * EPOCH_BYTES_PER_VALIDATOR / (step_ms * 1e-3)
@@ -298,10 +302,7 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                             if native else "DeviceEpoch (pz_dev_epoch_* + torch.distributed collectives)")},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
-                     "bytes_model": (("the one-pass committee-order layout's bytes: %.2f B per validator-epoch "
-                                      "(balance read + write 16, {start, end} %d, bitfields %.2f; DESIGN.md §3)"
-                                      % (bpv, round(bpv - 16 - (bpv % 1)), bpv % 1)) if lay is not None else
-                                     "SURVEY.md §8d: 44.25 B per validator-epoch"),
+                     "bytes_model": epoch_bytes_model(de, lay),
                      "survey_model": {"bytes_per_validator_epoch": EPOCH_BYTES_PER_VALIDATOR,
                                       "achieved": survey / 1e9, "frac": survey / HBM_PEAK,
                                       "note": "SURVEY.md §8d's figure prices a 12 B committee gather and 16 B of "
@@ -386,7 +387,7 @@ def epoch_parity_sharded(inst, dev, comm):
                 "bit-exact vs oracle/epoch_np" % (comm.world, len(idx)))
 
 
-def epoch_cold(args, torch, dev, nval, ninst, shuffled, workload, nsets=4, bpv=EPOCH_BYTES_PER_VALIDATOR):
+def epoch_cold(args, torch, dev, nval, ninst, shuffled, workload, nsets=4, bpv=None):
     """The same step with the timed steps rotated over ``nsets`` distinct instance sets (each
     ~400 MB; together far above the 256 MiB Infinity Cache), all bound to one stream, so every
     step reads its state from HBM: the epoch against HBM, not against the cache the
@@ -396,10 +397,19 @@ def epoch_cold(args, torch, dev, nval, ninst, shuffled, workload, nsets=4, bpv=E
 
     stream = torch.cuda.Stream(device=dev)  # a real stream: a null handle means "the state's own"
     sets = []
-    for k in range(nsets):
-        de = NativeEpoch(synth.epoch_batch(nval, ninst, seed=3 + k, shuffled=shuffled), device=dev.index)
+    k = 0
+    while k < nsets:
+        inst_k = synth.epoch_batch(nval, ninst, seed=3 + k, shuffled=shuffled)
+        de = NativeEpoch(inst_k, device=dev.index)
         de.bind_stream(stream.cuda_stream)
         sets.append(de)
+        if k == 0:  # enough sets that the streamed state is >= 3x the 256 MiB Infinity Cache
+            if bpv is None:
+                bpv = epoch_layout_bytes(inst_k, de) or EPOCH_BYTES_PER_VALIDATOR
+            sets_bb = de.balance_bytes
+            state_bytes = nval * ninst * (de.balance_bytes + de.dynasty_bytes)
+            nsets = max(nsets, -(-COLD_STATE_BYTES // state_bytes))
+        k += 1
     steps = max(nsets, (args.steps + nsets - 1) // nsets * nsets)
     for _ in range(2):
         for de in sets:
@@ -420,14 +430,16 @@ def epoch_cold(args, torch, dev, nval, ninst, shuffled, workload, nsets=4, bpv=E
     alg = units * bpv
     traffic = pmc_traffic(["pz_epoch_*"], workload + "_cold")
     yard = cold_stream_yardstick(torch, dev, units, nsets, steps)
-    return {"what": "%d steps rotated over %d distinct %d x %d instance sets (%.1f GB of validator state), one "
-                    "stream" % (steps, nsets, nval, ninst, nsets * units * 24 / 1e9),
+    yard_layout = cold_layout_yardstick(torch, dev, units, nsets, steps, sets_bb)
+    return {"what": "%d steps rotated over %d distinct %d x %d instance sets (%.2f GB of streamed validator "
+                    "state: balances and the {start, end} column), one stream"
+                    % (steps, nsets, nval, ninst, nsets * state_bytes / 1e9),
             "value": units * steps / wall, "unit": "validator-epochs/s", "step_device_ms": step_ms,
             "frac": alg / (step_ms * 1e-3) / HBM_PEAK,
             "survey_frac": units * EPOCH_BYTES_PER_VALIDATOR / (step_ms * 1e-3) / HBM_PEAK,
             "traffic": traffic, "traffic_source": pmc_summary_path(workload + "_cold") if traffic else None,
             "traffic_frac": (traffic / (step_ms * 1e-3) / HBM_PEAK) if traffic else None,
-            "yardstick": yard}
+            "yardstick": yard, "yardstick_layout": yard_layout}
 
 
 def cold_stream_yardstick(torch, dev, units, nsets, steps):
@@ -453,6 +465,33 @@ def cold_stream_yardstick(torch, dev, units, nsets, steps):
     return {"what": "torch addcmul_ float64 (3 x 8 B read + 8 B written per element), %d elements, %d sets, "
                     "cold" % (units, nsets),
             "ms": ms, "frac": units * 32 / (ms * 1e-3) / HBM_PEAK}
+
+
+def cold_layout_yardstick(torch, dev, units, nsets, steps, balance_bytes):
+    """A stock elementwise kernel on the epoch layout's own traffic shape, cold: torch's in-place
+    ``x.add_(y)`` with x the balance column's width (int32 for the u32 offsets, int64) and y
+    int32 (the {start, end} column's 4 B), i.e. read 2 columns, write one, per element."""
+    dt = torch.int32 if balance_bytes == 4 else torch.int64
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):
+        sets = [(torch.zeros(units, dtype=dt, device=dev), torch.ones(units, dtype=torch.int32, device=dev))
+                for _ in range(nsets)]
+        for x, y in sets:
+            x.add_(y)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for i in range(steps):
+            x, y = sets[i % nsets]
+            x.add_(y)
+        e1.record(s)
+    s.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    del sets
+    torch.cuda.empty_cache()
+    per = 2 * balance_bytes + 4
+    return {"what": "torch in-place add_ (%s += int32: %d B read + %d B written per element), %d elements, %d "
+                    "sets, cold" % (str(dt).replace("torch.", ""), balance_bytes + 4, balance_bytes, units, nsets),
+            "ms": ms, "frac": units * per / (ms * 1e-3) / HBM_PEAK}
 
 
 def epoch_parity(inst, dev):
@@ -1542,7 +1581,7 @@ def single_process_main(args):
     inst = synth.epoch_batch(nval, ninst, seed=3, shuffled=shuffled)
     one = synth.epoch_instances(inst, 1)  # the checker's instance
     de = NativeEpoch(inst, device=0, comm=comm)
-    bpv = epoch_layout_bytes(inst, de.one_pass) or EPOCH_BYTES_PER_VALIDATOR
+    bpv = epoch_layout_bytes(inst, de) or EPOCH_BYTES_PER_VALIDATOR
     del inst
     for _ in range(args.warmup + 30):
         de.step()

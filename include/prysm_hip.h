@@ -527,6 +527,13 @@ int  pz_epoch_state_tallies(pz_epoch_state* st);
 /* *committee_order: 0 index order, 1 committee order (two-pass step), 2 committee order with
  * the one-pass step. */
 int  pz_epoch_state_layout(const pz_epoch_state* st, int* committee_order);
+/* The widths the one-pass stream reads per validator-epoch (the roofline's bytes; no reference
+ * counterpart -- the Go state holds *pb.ValidatorRecord, types/state.go, messages.pb.go:803-809):
+ * *balance_bytes 4 when the balances are held as u32 offsets from a per-instance u64 base
+ * (every instance's balances within 2^30 of each other; results are the u64 values, exact mod
+ * 2^64; the state re-bases the offsets every 2^29 steps), else 8; *dynasty_bytes 4, 8 or 16 for
+ * the {start, end} column (16-, 32-bit saturated, or the u64 columns).  The widest part wins. */
+int  pz_epoch_state_columns(const pz_epoch_state* st, uint32_t* balance_bytes, uint32_t* dynasty_bytes);
 void pz_epoch_state_free(pz_epoch_state* st);
 /* Host only (no device call): the layout a pz_epoch_state would choose for h (as
  * pz_epoch_state_layout) and global rank `rank`'s storage positions [lo, hi) in a world of

@@ -122,6 +122,7 @@ SIGNATURES = {
     "pz_epoch_state_free": [vp],
     "pz_epoch_state_validators": [vp, ctypes.c_int, vp],
     "pz_epoch_state_layout": [vp, c_intp],
+    "pz_epoch_state_columns": [vp, vp, vp],
     "pz_epoch_state_tallies": [vp],
     "pz_epoch_plan": [vp, ctypes.c_int, ctypes.c_int, c_u64p, c_u64p, c_intp],
 }

@@ -1740,6 +1740,14 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   g.deferred.dst = nc;
   g.deferred.block_slot = block_slot;
   g.deferred.block_index = block_index;
+  // (the new ActiveState does not depend on the totals: built while the device tallies)
+  auto na = std::make_shared<AState>();
+  na->pending.reserve(A->pending.size());
+  for (auto& p : A->pending)
+    if (p->slot > lsr) na->pending.push_back(p);
+  na->tail = A->tail;  // (the window is at most 2 * kCycle long)
+  na->len = A->len;
+  na->cache_nil = A->cache_nil;
   tally_gather_finish(g);
   std::memcpy(tot.data(), g.tot_pin.p, kCycle * 8);
   for (uint64_t i = 0; i < kCycle; ++i) {
@@ -1761,12 +1769,6 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   nc->seed_reset = C->seed_reset;
   nc->tdep = 0;  // the epoch's next-cycle balance, set by epoch_collect
   nc->xl = C->xl;
-  auto na = std::make_shared<AState>();
-  for (auto& p : A->pending)
-    if (p->slot > lsr) na->pending.push_back(p);
-  na->tail = A->tail;  // (the window is at most 2 * kCycle long)
-  na->len = A->len;
-  na->cache_nil = A->cache_nil;
   *nc_out = nc;
   *na_out = na;
 }

@@ -135,8 +135,17 @@ struct FusedArgs {
   // [B][vstride] the same bounds saturated to 16 bits, {start | end << 16} (set instead of `se`
   // when every instance's CurrentDynasty is below 0xFFFF): 4 B per validator
   const uint32_t* se16;
+  uint64_t last_max;          // the largest last bitfield (bytes) of the instances (the LDS streaming pass)
   const uint2* att_win;       // [B][natt] {shard, record dynasty of that shard} per attestation (an
                               //   upload-time layout: loaded beside the stream, no shard -> record hop)
+  // [B][vstride] the balances as u32 offsets from a per-instance u64 base (bal32_base[B]):
+  // balance = base + offset (mod 2^64).  Set instead of EpochArgs.balance (which is then stale)
+  // when every instance's balances lie within 2^30 of each other; a step moves an offset by at
+  // most PZ_ATTESTER_REWARD, so the offsets stay inside u32 for 2^30 steps, and the state
+  // re-bases them well before (epoch_state.hip).  The stream reads and writes 4 B of balance per
+  // validator instead of 8, and every sum is taken on the reconstructed u64 values.
+  uint32_t* bal32;
+  const uint64_t* bal32_base;
 };
 // The single-launch step's limits: every block counts the instance's bitfields itself and the
 // last block keeps one LDS word per crosslink record.

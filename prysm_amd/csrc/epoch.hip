@@ -14,6 +14,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <mutex>
 
 #include "../../include/prysm_hip.h"
 #include "epoch.h"
@@ -1061,6 +1063,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     // (se), co_index 16 B -- where the pair layout read se16 and co_index 8 B per lane (an 8-B
     // access streams at 0.54-0.70 of the 16-B rate, MI355X_MICROARCH.md).
     static_assert(!PRO && (MODE & 1024), "quad lanes serve the multi-instance se/se16 kernels");
+    static_assert(!(MODE & 524288) || (MODE & 32768), "u32 balance offsets on the quad lanes only");
     const uint4 it = have ? items_ro[item] : make_uint4((uint32_t)a.val_offset, 0, 0, (uint32_t)a.val_offset);
     const uint64_t ws = it.x, we = (uint64_t)it.x + it.y, cb = it.w;
     FusedCommittee ci;
@@ -1078,9 +1081,18 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = g + i >= ws && g + i < we;
     const uint64_t pp = (v[0] || v[1] || v[2] || v[3]) ? p : p0;
+    constexpr bool B32 = (MODE & 524288) != 0;  // balances as u32 offsets (FusedArgs.bal32)
     uint64_t* Bal = a.balance + inst * f.vstride;
-    const uint4 qb0 = *reinterpret_cast<const uint4*>(Bal + pp);
-    const uint4 qb1 = *reinterpret_cast<const uint4*>(Bal + pp + 2);
+    uint32_t* Bal32 = B32 ? f.bal32 + inst * f.vstride : nullptr;
+    uint4 qb0, qb1;
+    if (B32) {
+      qb0 = *reinterpret_cast<const uint4*>(Bal32 + pp);
+      qb1 = make_uint4(0, 0, 0, 0);
+    } else {
+      qb0 = *reinterpret_cast<const uint4*>(Bal + pp);
+      qb1 = *reinterpret_cast<const uint4*>(Bal + pp + 2);
+    }
+    const uint64_t bbase = B32 ? f.bal32_base[inst] : 0;
     uint32_t sv[4], ev[4];
     if (MODE & 16384) {
       const uint4 w = ld16_nt(reinterpret_cast<const uint64_t*>(f.se16 + inst * f.vstride + pp));
@@ -1109,7 +1121,12 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
       byA = a.bits[ci.boff + ((uint64_t)qlo >> 3)];
       byB = a.bits[ci.boff + ((uint64_t)qhi >> 3)];
     }
-    uint64_t b[4] = {pack64(qb0.x, qb0.y), pack64(qb0.z, qb0.w), pack64(qb1.x, qb1.y), pack64(qb1.z, qb1.w)};
+    uint64_t b[4];
+    if (B32) {  // u64 balance = base + offset, wrapping as Go's uint64 does
+      b[0] = bbase + qb0.x, b[1] = bbase + qb0.y, b[2] = bbase + qb0.z, b[3] = bbase + qb0.w;
+    } else {
+      b[0] = pack64(qb0.x, qb0.y), b[1] = pack64(qb0.z, qb0.w), b[2] = pack64(qb1.x, qb1.y), b[3] = pack64(qb1.z, qb1.w);
+    }
     // crosslink tallies on the pre-reward balances (core.go:533-545)
     if (!(MODE & 1) && ci.ga != kNoAtt) {
       uint64_t t = 0;
@@ -1167,16 +1184,27 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
         const bool r = (MODE & 256) ? ((lcw >> ((p + i) & 31)) & 1) : bit_at(lastbf, v[i] ? ci4[i] : 0u);
         b[i] = r ? b[i] + PZ_ATTESTER_REWARD : b[i] - PZ_ATTESTER_REWARD;
       }
+      if (B32) {  // the offsets back: (base + o +- 1) - base = o +- 1, inside u32 (the state's re-base bound)
+        if (v[0] && v[1] && v[2] && v[3]) {
+          *reinterpret_cast<uint4*>(Bal32 + p) = make_uint4((uint32_t)(b[0] - bbase), (uint32_t)(b[1] - bbase),
+                                                            (uint32_t)(b[2] - bbase), (uint32_t)(b[3] - bbase));
+        } else {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int i = 2 * h;
-        if (v[i] && v[i + 1])
-          *reinterpret_cast<uint4*>(Bal + p + i) =
-              make_uint4((uint32_t)b[i], (uint32_t)(b[i] >> 32), (uint32_t)b[i + 1], (uint32_t)(b[i + 1] >> 32));
-        else if (v[i])
-          Bal[p + i] = b[i];
-        else if (v[i + 1])
-          Bal[p + i + 1] = b[i + 1];
+          for (int i = 0; i < 4; ++i)
+            if (v[i]) Bal32[p + i] = (uint32_t)(b[i] - bbase);
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = 2 * h;
+          if (v[i] && v[i + 1])
+            *reinterpret_cast<uint4*>(Bal + p + i) =
+                make_uint4((uint32_t)b[i], (uint32_t)(b[i] >> 32), (uint32_t)b[i + 1], (uint32_t)(b[i + 1] >> 32));
+          else if (v[i])
+            Bal[p + i] = b[i];
+          else if (v[i + 1])
+            Bal[p + i + 1] = b[i + 1];
+        }
       }
     }
 #pragma unroll
@@ -1500,6 +1528,11 @@ PZ_FUSED_KERNEL(pz_epoch_fused_se_xcd_kernel, 1024 + 4096)     // the XCD-aware 
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_xcd_kernel, 1280 + 4096)
 PZ_FUSED_KERNEL(pz_epoch_fused_se16_kernel, 1024 + 16384 + 32768)  // start/end from FusedArgs.se16
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_kernel, 1280 + 16384 + 32768)
+// balances as u32 offsets (FusedArgs.bal32, 524288)
+PZ_FUSED_KERNEL(pz_epoch_fused_se16_b32_kernel, 1024 + 16384 + 32768 + 524288)
+PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_b32_kernel, 1280 + 16384 + 32768 + 524288)
+PZ_FUSED_KERNEL(pz_epoch_fused_se_b32_kernel, 1024 + 32768 + 524288)
+PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_b32_kernel, 1280 + 32768 + 524288)
 // (A/B, variant 32768: the round-3 pair lanes)
 PZ_FUSED_KERNEL(pz_epoch_fused_se_pair_kernel, 1024)
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_pair_kernel, 1280)
@@ -1584,18 +1617,35 @@ __device__ __forceinline__ StreamB stream_load_b(const EpochArgs& a, const Fused
   return y;
 }
 
+// MODE & 262144 (LDS): workgroups of 16 waves; block (instance i, slice j) -- blockIdx = i * bpi
+// + j -- stages instance i's last bitfield in LDS once and its waves take the pieces j + bpi *
+// (wave + 16 t), looking the reward bits up in LDS (ds_read_u8) instead of gathering one random
+// L2 line per position.  The 16 blocks of slice j (one per instance) share an XCD (blockIdx
+// differs by multiples of bpi = 16 when B = 16), so its co_index words are fetched into one L2.
 template <int MODE>
 __device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro,
                                                    const uint64_t* __restrict__ boffs_ro,
                                                    const uint64_t* __restrict__ tdep_ro,
                                                    const uint4* __restrict__ items_ro,
                                                    const uint32_t* __restrict__ catt_offs_ro,
-                                                   const uint32_t* __restrict__ catt_ro) {
+                                                   const uint32_t* __restrict__ catt_ro, uint32_t bpi) {
   static_assert((MODE & 16384) != 0, "the streaming pass reads the 16-bit {start, end} column");
+  constexpr bool LDS = (MODE & 262144) != 0;
+  extern __shared__ uint4 lbf_dyn[];
   const int lane = threadIdx.x & 63;
-  const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t B = a.ninst, W = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  const uint64_t inst = w % B, item0 = w / B, stride = W / B;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nwv = blockDim.x >> 6;
+  const uint64_t B = a.ninst;
+  uint64_t inst, item0, stride;
+  if (LDS) {
+    inst = blockIdx.x / bpi;
+    item0 = (blockIdx.x - inst * bpi) + (uint64_t)bpi * wv;
+    stride = (uint64_t)bpi * nwv;
+  } else {
+    const uint64_t w = (uint64_t)blockIdx.x * nwv + wv, W = (uint64_t)gridDim.x * nwv;
+    inst = w % B;
+    item0 = w / B;
+    stride = W / B;
+  }
   // the instance's scalars (GetAttestersTotalDeposit from `pre`, the threshold, the panics)
   const uint64_t pop = pre_ro[inst * kPre], ferr = pre_ro[inst * kPre + 1];
   const uint64_t lb = boffs_ro[inst * a.natt + a.natt - 1];
@@ -1613,6 +1663,26 @@ __device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, con
   StreamA ca = stream_load_a<MODE>(f, items_ro, inst, item, a.val_offset);
   StreamB cb_ = stream_load_b<MODE>(a, f, inst, ca, lane);
   StreamA na = stream_load_a<MODE>(f, items_ro, inst, item + stride, a.val_offset);
+  const uint8_t* lbf8 = reinterpret_cast<const uint8_t*>(lbf_dyn) + (lb & 15);
+  if (LDS) {  // the instance's last bitfield into LDS (16-B chunks from lb & ~15; the buffer is padded)
+    const uint64_t n16 = (L + (lb & 15) + 15) / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(a.bits + (lb & ~15ull));
+    constexpr int kU = 8;  // chunks in flight per thread per round
+    for (uint64_t k0 = 0; k0 < n16; k0 += (uint64_t)kU * blockDim.x) {
+      uint4 t[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const uint64_t k = k0 + (uint64_t)u * blockDim.x + threadIdx.x;
+        t[u] = k < n16 ? src[k] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const uint64_t k = k0 + (uint64_t)u * blockDim.x + threadIdx.x;
+        if (k < n16) lbf_dyn[k] = t[u];
+      }
+    }
+    __syncthreads();
+  }
   for (; item < f.nitems; item += stride) {
     // the reward bits of this piece (dependent on its co_index words): issued first
     const uint64_t ws = ca.it.x, we = (uint64_t)ca.it.x + ca.it.y, cbase = ca.it.w;
@@ -1626,7 +1696,7 @@ __device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, con
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t ix = v[i] ? ci4[i] : 0u;
-        rb[i] = lastbf[ix >> 3];
+        rb[i] = LDS ? lbf8[ix >> 3] : lastbf[ix >> 3];
       }
     }
     // the next piece's stream, then the one after's descriptor
@@ -1739,19 +1809,21 @@ __device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, con
   }
 }
 
-#define PZ_STREAM_KERNEL(NAME, MODE)                                                                         \
-  extern "C" __global__ void __launch_bounds__(256) NAME(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro, \
-                                                        const uint64_t* __restrict__ boffs_ro,                  \
-                                                        const uint64_t* __restrict__ tdep_ro,                   \
-                                                        const uint4* __restrict__ items_ro,                     \
-                                                        const uint32_t* __restrict__ catt_offs_ro,              \
-                                                        const uint32_t* __restrict__ catt_ro) {                 \
-    stream_kernel_body<MODE>(a, f, pre_ro, boffs_ro, tdep_ro, items_ro, catt_offs_ro, catt_ro);                  \
+#define PZ_STREAM_KERNEL(NAME, MODE, T)                                                                      \
+  extern "C" __global__ void __launch_bounds__(T) NAME(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro, \
+                                                      const uint64_t* __restrict__ boffs_ro,                    \
+                                                      const uint64_t* __restrict__ tdep_ro,                     \
+                                                      const uint4* __restrict__ items_ro,                       \
+                                                      const uint32_t* __restrict__ catt_offs_ro,                \
+                                                      const uint32_t* __restrict__ catt_ro, uint32_t bpi) {     \
+    stream_kernel_body<MODE>(a, f, pre_ro, boffs_ro, tdep_ro, items_ro, catt_offs_ro, catt_ro, bpi);             \
   }
-PZ_STREAM_KERNEL(pz_epoch_stream_se16_kernel, 1024 + 16384)
-PZ_STREAM_KERNEL(pz_epoch_stream_lc_se16_kernel, 1280 + 16384)
-PZ_STREAM_KERNEL(pz_epoch_stream_se16_win_kernel, 1024 + 16384 + 131072)
-PZ_STREAM_KERNEL(pz_epoch_stream_lc_se16_win_kernel, 1280 + 16384 + 131072)
+PZ_STREAM_KERNEL(pz_epoch_stream_se16_kernel, 1024 + 16384, 256)
+PZ_STREAM_KERNEL(pz_epoch_stream_lc_se16_kernel, 1280 + 16384, 256)
+PZ_STREAM_KERNEL(pz_epoch_stream_se16_win_kernel, 1024 + 16384 + 131072, 256)
+PZ_STREAM_KERNEL(pz_epoch_stream_lc_se16_win_kernel, 1280 + 16384 + 131072, 256)
+PZ_STREAM_KERNEL(pz_epoch_stream_lds_se16_kernel, 1024 + 16384 + 262144, 1024)
+PZ_STREAM_KERNEL(pz_epoch_stream_lds_se16_win_kernel, 1024 + 16384 + 131072 + 262144, 1024)
 #undef PZ_STREAM_KERNEL
 
 // The single-launch step (one instance): no occupancy target (a few dozen blocks), so the
@@ -1938,12 +2010,14 @@ hipError_t launch_epoch_fwin(const EpochArgs& a, const FusedArgs& f, hipStream_t
 // (grid/lane-layout variants keep it: 4096 XCD-aware grid, 32768 pair lanes, 65536 one piece per
 // wave with quad lanes -- the streaming pass off)
 static bool ablation_no_lastco() {
-  return g_fused_variant && g_fused_variant != 4096 && g_fused_variant != 32768 && g_fused_variant != 65536;
+  return g_fused_variant && g_fused_variant != 4096 && g_fused_variant != 32768 && g_fused_variant != 65536 &&
+         g_fused_variant != 131072 && g_fused_variant != 262144;
 }
 
+static bool use_lds_form(const EpochArgs& a, const FusedArgs& f);
 hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f0, hipStream_t s) {
   FusedArgs f = f0;
-  if (ablation_no_lastco()) f.lastco = nullptr;
+  if (ablation_no_lastco() || use_lds_form(a, f0)) f.lastco = nullptr;
   uint64_t pbpi = (a.max_inst_bytes + kPopBytesPerBlock - 1) / kPopBytesPerBlock;
   if (pbpi == 0) pbpi = 1;  // chunk 0 of each instance also resets the winners
   const uint64_t npb = (uint64_t)a.ninst * pbpi;
@@ -1954,6 +2028,24 @@ hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f0, hipStream_t
   hipLaunchKernelGGL(pz_epoch_pre_kernel, dim3((uint32_t)(npb + nab + nlb)), dim3(kThreads), 0, s, a, f, pbpi, npb,
                      nab, lcb);
   return hipGetLastError();
+}
+
+// The LDS form of the streaming pass: last bitfields up to 128 KiB (1,048,576 validators), about
+// one 16-wave workgroup per CU in all.
+constexpr uint64_t kStreamLdsMax = 131072;
+constexpr uint64_t kStreamLdsBlocks = 256;
+static bool stream_lds_over_lastco() {
+  static const bool on = std::getenv("PZ_EPOCH_LDS_OVER_LASTCO") != nullptr;
+  return on;
+}
+// The product takes the LDS form whenever the last bitfields fit and no position-order gather
+// (lastco, small N) exists; variant 262144 (A/B) and PZ_EPOCH_LDS_OVER_LASTCO take it in place
+// of the gather too (then `pre` skips the gather).
+static bool use_lds_form(const EpochArgs& a, const FusedArgs& f) {
+  const int v = g_fused_variant;
+  if (f.bal32) return false;  // (the u32-offset balances run the quad kernels)
+  if (!((v == 0 || v == 262144) && f.se16 && a.ninst > 1 && f.last_max && f.last_max <= kStreamLdsMax)) return false;
+  return !f.lastco || v == 262144 || stream_lds_over_lastco();
 }
 
 // Blocks (4 waves each) of the streaming pass: about one resident wave per SIMD slot
@@ -1984,6 +2076,17 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream
   // accumulators, also on a rank whose range holds no piece
   const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
   const int variant = g_fused_variant;
+  if (f.bal32) {  // balances as u32 offsets: the quad kernels, instance-minor (no A/B variant applies)
+    const dim3 grid(a.ninst, (uint32_t)groups), block(64 * kFusedWaves);
+#define PZ_LAUNCH_B32(K) \
+  hipLaunchKernelGGL(K, grid, block, 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt)
+    if (f.se16 && f.lastco) PZ_LAUNCH_B32(pz_epoch_fused_lc_se16_b32_kernel);
+    else if (f.se16) PZ_LAUNCH_B32(pz_epoch_fused_se16_b32_kernel);
+    else if (f.lastco) PZ_LAUNCH_B32(pz_epoch_fused_lc_se_b32_kernel);
+    else PZ_LAUNCH_B32(pz_epoch_fused_se_b32_kernel);
+#undef PZ_LAUNCH_B32
+    return hipGetLastError();
+  }
   if (variant == 4096 && (f.se || f.se16)) {  // the XCD-aware 1-D grid: groups padded to a multiple of 8
     const dim3 grid1((uint32_t)(((groups + 7) / 8) * 8 * a.ninst)), blk(64 * kFusedWaves);
 #define PZ_LAUNCH_XCD(K) \
@@ -1995,10 +2098,32 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream
 #undef PZ_LAUNCH_XCD
     return hipGetLastError();
   }
-  if (variant == 0 && f.se16 && a.ninst > 1) {  // the streaming form (persistent, pipelined waves)
+  if (use_lds_form(a, f)) {
+    // the streaming form with the last bitfield in LDS (the product when it fits; at small N the
+    // position-order gather of `pre` (lastco) is kept unless PZ_EPOCH_LDS_OVER_LASTCO)
+    const uint32_t bpi = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(f.nitems, kStreamLdsBlocks / a.ninst));
+    const size_t lds = (size_t)((f.last_max + 15 + 16) / 16) * 16;
+    static std::once_flag once;
+    std::call_once(once, [] {
+      (void)hipFuncSetAttribute((const void*)pz_epoch_stream_lds_se16_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsMax + 64);
+      (void)hipFuncSetAttribute((const void*)pz_epoch_stream_lds_se16_win_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsMax + 64);
+    });
+#define PZ_LAUNCH_LDS(K)                                                                                   \
+  hipLaunchKernelGGL(K, dim3((uint32_t)(a.ninst * bpi)), dim3(1024), lds, s, a, f, f.pre, a.boffs, a.total_deposit, \
+                     f.items, f.catt_offs, f.catt, bpi)
+    if (f.win_fused) PZ_LAUNCH_LDS(pz_epoch_stream_lds_se16_win_kernel);
+    else PZ_LAUNCH_LDS(pz_epoch_stream_lds_se16_kernel);
+#undef PZ_LAUNCH_LDS
+    return hipGetLastError();
+  }
+  if ((variant == 0 || variant == 131072) && f.se16 && a.ninst > 1) {
+    // the streaming form (persistent, pipelined waves; variant 131072: this form where the product
+    // takes the LDS one)
     const uint32_t nb = stream_blocks(a.ninst, f.nitems, f.lastco != nullptr);
 #define PZ_LAUNCH_STREAM(K) \
-  hipLaunchKernelGGL(K, dim3(nb), dim3(256), 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.catt_offs, f.catt)
+  hipLaunchKernelGGL(K, dim3(nb), dim3(256), 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.catt_offs, f.catt, 0u)
     if (f.win_fused && f.lastco) PZ_LAUNCH_STREAM(pz_epoch_stream_lc_se16_win_kernel);
     else if (f.win_fused) PZ_LAUNCH_STREAM(pz_epoch_stream_se16_win_kernel);
     else if (f.lastco) PZ_LAUNCH_STREAM(pz_epoch_stream_lc_se16_kernel);

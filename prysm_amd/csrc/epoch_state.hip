@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -70,6 +71,10 @@ struct pz_epoch_state {
   std::vector<uint32_t> co_inv;    // storage position -> validator index (committee order)
   uint64_t steps = 0;
   uint64_t tallied = ~0ull;        // the step whose vote/total pz_epoch_state_tallies completed
+  // FusedArgs.bal32 (some part holds its balances as u32 offsets): steps left before the
+  // offsets are re-based (each step moves an offset by at most 1; see kBal32Window)
+  bool b32 = false;
+  uint64_t b32_left = 0;
   std::vector<Shard> sh;
   ~pz_epoch_state();
 };
@@ -151,6 +156,84 @@ int upload_se16(Shard& s, uint32_t** p, const uint64_t* start, const uint64_t* e
     }
   hipError_t e = hipMemcpy(*p, tmp.data(), tmp.size() * 4, hipMemcpyHostToDevice);
   return e == hipSuccess ? PZ_OK : hip_fail(e, "hipMemcpy H2D (epoch state)");
+}
+
+// FusedArgs.bal32: an instance's balances are held as u32 offsets from base = min - 2^30 when
+// max - min < 2^30, so every offset starts in [2^30, 2^31).  A step adds or subtracts
+// PZ_ATTESTER_REWARD (1) at most, so after kBal32Period steps the offsets are still inside
+// [2^30 - 2^29, 2^31 + 2^29), well inside u32, and the state re-bases them then (bal32_rebase).
+// Arithmetic is mod 2^64 throughout (base + offset), so a balance that wraps below zero, as
+// Go's uint64 does, stays exact; the re-base then finds the spread too wide and returns that
+// part to the u64 column.
+constexpr uint64_t kBal32Window = 1ull << 30;
+constexpr uint64_t kBal32Period = 1ull << 29;
+static uint64_t bal32_period() {  // PZ_EPOCH_B32_PERIOD: tests exercise the re-base
+  const char* e = std::getenv("PZ_EPOCH_B32_PERIOD");
+  const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
+  return v && v < kBal32Period ? v : kBal32Period;
+}
+
+// The base of every instance of [i0, i0 + Bp) over the values vals(b, q), q < n; false if some
+// instance's spread is kBal32Window or more.
+template <typename F>
+static bool bal32_bases(uint64_t Bp, uint64_t n, F vals, std::vector<uint64_t>& base) {
+  base.assign(Bp, 0);
+  for (uint64_t b = 0; b < Bp; ++b) {
+    uint64_t lo = ~0ull, hi = 0;
+    for (uint64_t q = 0; q < n; ++q) {
+      const uint64_t v = vals(b, q);
+      lo = std::min(lo, v);
+      hi = std::max(hi, v);
+    }
+    if (n && hi - lo >= kBal32Window) return false;
+    base[b] = (n ? lo : 0) - kBal32Window;
+  }
+  return true;
+}
+
+// Upload the offsets [Bp][np] (pad positions 0) and bases of one part.
+template <typename F>
+static int bal32_upload(Shard& s, Part& q, F vals, const std::vector<uint64_t>& base, bool alloc) {
+  std::vector<uint32_t> off((size_t)q.B * s.np, 0u);
+  for (uint64_t b = 0; b < q.B; ++b)
+    for (uint64_t p = 0; p < s.n; ++p) off[b * s.np + p] = (uint32_t)(vals(b, p) - base[b]);
+  if (alloc) {
+    uint64_t* d_base = nullptr;
+    int rc = dalloc(s, &q.f.bal32, off.size(), false);
+    if (!rc) rc = dalloc(s, &d_base, q.B, false);
+    if (rc) return rc;
+    q.f.bal32_base = d_base;
+  }
+  hipError_t e = hipMemcpy(q.f.bal32, off.data(), off.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(const_cast<uint64_t*>(q.f.bal32_base), base.data(), base.size() * 8, hipMemcpyHostToDevice);
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "hipMemcpy H2D (epoch state, u32 balances)");
+}
+
+// The part's balances as u64 [Bp][n] on the host (from the offsets or the u64 column).
+static int part_balances(const Shard& s, const Part& q, uint64_t* out, uint64_t ld) {
+  hipError_t e;
+  if (!q.f.bal32) {
+    e = hipMemcpy2D(out, ld * 8, q.a.balance, s.np * 8, s.n * 8, q.B, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? PZ_OK : hip_fail(e, "epoch state results D2H");
+  }
+  std::vector<uint32_t> off((size_t)q.B * s.np);
+  std::vector<uint64_t> base(q.B);
+  e = hipMemcpy(off.data(), q.f.bal32, off.size() * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(base.data(), q.f.bal32_base, base.size() * 8, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "epoch state results D2H (u32 balances)");
+  for (uint64_t b = 0; b < q.B; ++b)
+    for (uint64_t p = 0; p < s.n; ++p) out[b * ld + p] = base[b] + off[b * s.np + p];
+  return PZ_OK;
+}
+
+// Re-base every part's offsets (or, if an instance's spread has grown to the window, return
+// the part to the u64 column).  Rare: once per kBal32Period steps.
+static int bal32_rebase(pz_epoch_state* st);
+
+static bool win_fused_off() {
+  const char* e = std::getenv("PZ_EPOCH_WIN_FUSED");
+  return e && e[0] == '0';
 }
 
 uint64_t shard_words(uint64_t N, int world) { return std::max<uint64_t>(1, (N + 64ull * world - 1) / (64ull * world)); }
@@ -705,6 +788,7 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
         uint64_t maxl = 0;
         for (uint64_t b = i0; b < i0 + Bp && st->natt; ++b)
           maxl = std::max<uint64_t>(maxl, h->boffs[b * st->natt + st->natt] - h->boffs[b * st->natt + st->natt - 1]);
+        q.f.last_max = maxl;
         if (!rc && st->natt && maxl <= kLastCoMaxBytes && s.np) {
           q.f.lcw = (s.np + 31) / 32;
           rc = dalloc(s, &q.f.lastco, (size_t)Bp * q.f.lcw);
@@ -780,12 +864,23 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
           if (!rc && e2 != hipSuccess) rc = hip_fail(e2, "hipMemsetAsync (winners)");
           q.f.win_in_wave = 1;
           q.f.winner_next = w2;
-        } else if (!rc && win_waves && std::getenv("PZ_EPOCH_WIN_FUSED")) {
-          // (A/B knob: the same in the multi-instance fused waves, pre resetting the winners and
-          // no mid launch, measured 0.2-2 us per step SLOWER than the mid launch it removes at
-          // 65,536 x 256 and 1M x 16: the waves' extra loads and atomics cost more;
-          // profiles/r03/epoch_ab_r3af.txt)
+        } else if (!rc && win_waves && !win_fused_off()) {
+          // the same in the multi-instance streaming pass: pre resets the winners, the wave
+          // holding a committee proposes its attestation (one_win), and no mid launch follows.
+          // (Round 3's per-piece waves measured 0.2-2 us per step slower than the mid launch,
+          // profiles/r03/epoch_ab_r3af.txt; the streaming pass loads the {shard, dynasty} word
+          // in its pipelined stage.  PZ_EPOCH_WIN_FUSED=0: the mid launch, for A/B.)
           q.f.win_fused = 1;
+        }
+        // the balances as u32 offsets (FusedArgs.bal32) for the multi-instance quad kernels
+        if (!rc && (se || se16) && !q.f.one && !q.f.multi && Bp > 1 && s.n && !std::getenv("PZ_EPOCH_BAL64")) {
+          const uint32_t* inv = st->co_inv.data();
+          auto vals = [&](uint64_t b, uint64_t p) { return h->balance[(i0 + b) * st->N + inv[s.lo + p]]; };
+          std::vector<uint64_t> base;
+          if (bal32_bases(Bp, s.n, vals, base)) {
+            rc = bal32_upload(s, q, vals, base, true);
+            st->b32 = true;
+          }
         }
       }
       q.cur = 1;  // flip() below binds red[0] as the first step's buffer
@@ -803,6 +898,7 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
       return hip_fail(e, "epoch state upload");
     }
   }
+  st->b32_left = bal32_period();
   flip(st);
   *out = st;
   return PZ_OK;
@@ -810,10 +906,16 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
 
 int pz_epoch_state_step(pz_epoch_state* st) {
   if (!st) return fail(PZ_EINVAL, "state is null");
-  int rc = st->world > 1 ? step_sharded(st) : step_world1(st);
+  int rc;
+  if (st->b32 && st->b32_left == 0) {
+    if ((rc = bal32_rebase(st))) return rc;
+    st->b32_left = bal32_period();
+  }
+  rc = st->world > 1 ? step_sharded(st) : step_world1(st);
   if (rc) return rc;
   flip(st);
   ++st->steps;
+  if (st->b32) --st->b32_left;
   return PZ_OK;
 }
 
@@ -861,8 +963,7 @@ int pz_epoch_state_results(pz_epoch_state* st, int local, uint64_t* balance, uin
   for (uint32_t p = 0; p < st->nparts && e == hipSuccess; ++p) {
     const Part& q = s.part[p];
     const uint64_t Bp = q.B, i0 = q.i0, na = st->natt;
-    if (balance && s.n)
-      e = hipMemcpy2D(balance + i0 * s.n, s.n * 8, q.a.balance, s.np * 8, s.n * 8, Bp, hipMemcpyDeviceToHost);
+    if (balance && s.n && (rc = part_balances(s, q, balance + i0 * s.n, s.n))) return rc;
     if (e == hipSuccess && scal) e = hipMemcpy(scal + i0 * kScal, q.results, Bp * kScal * 8, hipMemcpyDeviceToHost);
     if (e == hipSuccess && vote && na)
       e = hipMemcpy(vote + i0 * na, q.results + Bp * kScal, Bp * na * 8, hipMemcpyDeviceToHost);
@@ -873,6 +974,50 @@ int pz_epoch_state_results(pz_epoch_state* st, int local, uint64_t* balance, uin
                     hipMemcpyDeviceToHost);
   }
   return e == hipSuccess ? PZ_OK : hip_fail(e, "epoch state results D2H");
+}
+
+namespace {
+int bal32_rebase(pz_epoch_state* st) {
+  int rc = pz_epoch_state_sync(st);
+  if (rc) return rc;
+  bool any = false;
+  for (Shard& s : st->sh) {
+    (void)hipSetDevice(s.dev);
+    for (uint32_t p = 0; p < st->nparts; ++p) {
+      Part& q = s.part[p];
+      if (!q.f.bal32) continue;
+      std::vector<uint64_t> v((size_t)q.B * s.n), base;
+      if ((rc = part_balances(s, q, v.data(), s.n))) return rc;
+      auto vals = [&](uint64_t b, uint64_t x) { return v[b * s.n + x]; };
+      if (bal32_bases(q.B, s.n, vals, base)) {
+        if ((rc = bal32_upload(s, q, vals, base, false))) return rc;
+        any = true;
+        continue;
+      }
+      // the spread outgrew the window: this part returns to the u64 column
+      hipError_t e = hipMemcpy2D(q.a.balance, s.np * 8, v.data(), s.n * 8, s.n * 8, q.B, hipMemcpyHostToDevice);
+      if (e != hipSuccess) return hip_fail(e, "hipMemcpy2D H2D (epoch state re-base)");
+      q.f.bal32 = nullptr;
+      q.f.bal32_base = nullptr;
+    }
+  }
+  st->b32 = any;
+  return PZ_OK;
+}
+}  // namespace
+
+int pz_epoch_state_columns(const pz_epoch_state* st, uint32_t* balance_bytes, uint32_t* dynasty_bytes) {
+  if (!st || !balance_bytes || !dynasty_bytes) return fail(PZ_EINVAL, "null pointer");
+  uint32_t bb = 0, db = 0;
+  for (const Shard& s : st->sh)
+    for (uint32_t p = 0; p < st->nparts; ++p) {
+      const Part& q = s.part[p];
+      bb = std::max<uint32_t>(bb, q.f.bal32 ? 4 : 8);
+      db = std::max<uint32_t>(db, q.f.se16 ? 4 : q.f.se ? 8 : 16);
+    }
+  *balance_bytes = bb;
+  *dynasty_bytes = db;
+  return PZ_OK;
 }
 
 int pz_epoch_state_validators(const pz_epoch_state* st, int local, uint32_t* index) {

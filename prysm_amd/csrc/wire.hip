@@ -30,9 +30,10 @@ namespace pz {
 namespace {
 
 constexpr int kThreads = 512;
-constexpr int kPer = 4, kSubRecs = kThreads * kPer;  // scalar kernel: sub-tiles of 2,048 records
-constexpr int kSub = 2, kTileRecs = kSub * kSubRecs;  // 4,096 records (one ticket) per tile
-constexpr int kStageBytes = 64 * 1024;                // the whole tile's encoding (16 B per record)
+// scalar kernel: sub-tiles of kThreads x kPer = 2,048 records, kSub of them (4,096 records, one
+// ticket) per tile, and a 64 KiB stage for the tile's encoding (16 B per record); wire_val_body
+// derives these from its PER parameter
+constexpr int kPer = 4, kSub = 2;
 constexpr int kBytesSub = 8, kBytesTileRecs = kBytesSub * kThreads;  // bytes-field kernel: 4,096
 
 // varint length: (70 - clz) / 7 for 70 - clz in [6, 70] as a multiply by 37 and a shift (a
@@ -410,10 +411,10 @@ __device__ __forceinline__ void store_stage(uint8_t* out, uint64_t base, const u
 // Record (j, p, t) of a tile = tile*kTileRecs + j*kSubRecs + p*kThreads + t: every column load
 // of a wave reads 512 contiguous bytes.  kNt: nontemporal loads (the columns are read once;
 // tools/wire_probe.py r2m: 164 -> 154 us per 16.7 M records).
-template <int NC, bool kNt = false>
-__device__ __forceinline__ void load_sub(const WireValArgs& a, uint64_t first, SRec<NC> (&r)[kPer]) {
+template <int NC, bool kNt = false, int PER = kPer>
+__device__ __forceinline__ void load_sub(const WireValArgs& a, uint64_t first, SRec<NC> (&r)[PER]) {
 #pragma unroll
-  for (int p = 0; p < kPer; ++p) {
+  for (int p = 0; p < PER; ++p) {
     const uint64_t i = first + p * kThreads + threadIdx.x;
 #pragma unroll
     for (int k = 0; k < NC; ++k) r[p].v[k] = i < a.n ? (kNt ? __builtin_nontemporal_load(a.ccol[k] + i) : a.ccol[k][i]) : 0;
@@ -423,12 +424,13 @@ __device__ __forceinline__ void load_sub(const WireValArgs& a, uint64_t first, S
 // Sizes of one sub-tile's records and their offsets inside the sub-tile (record order), from
 // ONE block scan: a record is at most 61 bytes and a sub-tile row p of 512 records at most
 // 31,232, so the four rows' sizes travel as four 16-bit lanes of one u64.
-template <int NC, bool kShflScan = false>
-__device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t first, const SRec<NC> (&r)[kPer],
-                                                uint32_t (&off)[kPer], uint64_t* lds) {
+template <int NC, bool kShflScan = false, int PER = kPer>
+__device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t first, const SRec<NC> (&r)[PER],
+                                                uint32_t (&off)[PER], uint64_t* lds) {
+  static_assert(PER <= 4, "four 16-bit rows per scan");
   uint64_t packed = 0;
 #pragma unroll
-  for (int p = 0; p < kPer; ++p) {
+  for (int p = 0; p < PER; ++p) {
     const uint64_t i = first + p * kThreads + threadIdx.x;
     packed |= (uint64_t)(i < a.n ? frame_size(a, srec_body(r[p])) : 0) << (16 * p);
   }
@@ -437,7 +439,7 @@ __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t f
   __syncthreads();  // lds is reused by the next scan
   uint32_t row = 0;
 #pragma unroll
-  for (int p = 0; p < kPer; ++p) {
+  for (int p = 0; p < PER; ++p) {
     off[p] = row + (uint32_t)((e >> (16 * p)) & 0xffff);
     row += (uint32_t)((t >> (16 * p)) & 0xffff);
   }
@@ -473,8 +475,12 @@ __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t f
 // __shfl_up (ds_bpermute) instead of DPP, bit 12 column loads with the default cache policy
 // instead of nontemporal, bit 13 nontemporal output stores, bit 14 (tests) no inclusive
 // prefixes published (every look-back walks back to tile 0; exact output).
-template <int V, int NC>
+// PER: records per thread per sub-tile (kPer in the product: 4,096-record tiles and a 64 KiB
+// stage, two tiles per CU).  Smaller PER shrinks the tile, its stage and its held values
+// (round 4 A/B: three tiles per CU at PER 3).
+template <int V, int NC, int PER = kPer>
 __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
+  constexpr int kSubRecs = kThreads * PER, kTileRecs = kSub * kSubRecs, kStageBytes = 16 * kTileRecs;
   __shared__ uint64_t lds[kThreads / 64 + 1];
   __shared__ uint32_t s_tile, s_first, s_polls;
   __shared__ uint64_t s_build_end, s_lbslots[2 * 4 * (kThreads / 64)];
@@ -495,21 +501,21 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   const uint64_t tfirst = (uint64_t)tile * kTileRecs;
   constexpr bool kHold = !(V & 16) && NC <= 3;  // 4-5 columns held would spill: reload them
   // phase 1: sizes -> offsets inside the tile
-  SRec<NC> r[kSub][kPer];
+  SRec<NC> r[kSub][PER];
   // A record's body size is recomputed for its build rather than held: 8 more live VGPRs
   // spilled, and a spill reload's vmcnt(0) waited for the look-back loads in flight.
-  uint32_t off[kSub][kPer], agg = 0;
+  uint32_t off[kSub][PER], agg = 0;
   if (kHold) {  // every sub-tile's loads in flight at once: one round trip, not kSub
 #pragma unroll
-    for (int j = 0; j < kSub; ++j) load_sub<NC, !(V & 4096)>(a, tfirst + (uint64_t)j * kSubRecs, r[j]);
+    for (int j = 0; j < kSub; ++j) load_sub<NC, !(V & 4096), PER>(a, tfirst + (uint64_t)j * kSubRecs, r[j]);
   }
 #pragma unroll
   for (int j = 0; j < kSub; ++j) {
-    if (!kHold) load_sub(a, tfirst + (uint64_t)j * kSubRecs, r[0]);
+    if (!kHold) load_sub<NC, false, PER>(a, tfirst + (uint64_t)j * kSubRecs, r[0]);
     const uint32_t sub =
-        sub_offsets<NC, (V & 2048) != 0>(a, tfirst + (uint64_t)j * kSubRecs, r[kHold ? j : 0], off[j], lds);
+        sub_offsets<NC, (V & 2048) != 0, PER>(a, tfirst + (uint64_t)j * kSubRecs, r[kHold ? j : 0], off[j], lds);
 #pragma unroll
-    for (int p = 0; p < kPer; ++p) off[j][p] += agg;
+    for (int p = 0; p < PER; ++p) off[j][p] += agg;
     agg += sub;
   }
   // Every column load has landed (the scans used them).  Say so to the compiler's wait-count
@@ -534,9 +540,9 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
     uint8_t* st = reinterpret_cast<uint8_t*>(stage);
 #pragma unroll
     for (int j = 0; j < kSub; ++j) {
-      if (!kHold) load_sub(a, tfirst + (uint64_t)j * kSubRecs, r[0]);
+      if (!kHold) load_sub<NC, false, PER>(a, tfirst + (uint64_t)j * kSubRecs, r[0]);
 #pragma unroll
-      for (int p = 0; p < kPer; ++p)
+      for (int p = 0; p < PER; ++p)
         if (tfirst + j * kSubRecs + p * kThreads + threadIdx.x < a.n) {
           const SRec<NC>& rec = r[kHold ? j : 0][p];
           put_srec(a, rec, srec_body(rec), st + off[j][p]);
@@ -560,7 +566,7 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   }
   uint64_t base = 0;
   if (V & 4) {
-    base = (uint64_t)tile * 15 * kTileRecs;
+    base = (uint64_t)tile * 15 * kTileRecs;  // (ablation: output wrong)
   } else if (tile > 0) {
     base = lookback_finish<LB, !(V & 1024)>(a.status, tile, w, lds, &s_first, (V & 32) ? &polls : nullptr, s_lbslots);
     // (variant 16384, tests only: no inclusive prefix is published, so every look-back walks
@@ -596,9 +602,9 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   }
 #pragma unroll
   for (int j = 0; j < kSub; ++j) {
-    if (!kHold) load_sub(a, tfirst + (uint64_t)j * kSubRecs, r[0]);
+    if (!kHold) load_sub<NC, false, PER>(a, tfirst + (uint64_t)j * kSubRecs, r[0]);
 #pragma unroll
-    for (int p = 0; p < kPer; ++p) {
+    for (int p = 0; p < PER; ++p) {
       const uint64_t i = tfirst + j * kSubRecs + p * kThreads + threadIdx.x;
       if (i < a.n) {
         const uint64_t o = base + off[j][p];
@@ -645,6 +651,18 @@ PZ_WIRE_VAL_KERNEL(pz_wire_val_v12288_kernel, 12288, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v16384_kernel, 16384, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v16512_kernel, 16512, 3)
 #undef PZ_WIRE_VAL_KERNEL
+// Round 4 tile-geometry A/B (3 columns): PER records per thread per sub-tile, W waves per SIMD
+// (the VGPR cap: 6 -> 80, 8 -> 64).  PER 3: 3,072-record tiles, a 48 KiB stage, three tiles
+// per CU; PER 2: 2,048-record tiles, a 32 KiB stage, three (W 6) or four (W 8) per CU.
+#define PZ_WIRE_VAL_GEOM(NAME, PER, W)                                                         \
+  extern "C" __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(W, W))) \
+  NAME(WireValArgs a, uint32_t nt) {                                                         \
+    wire_val_body<0, 3, PER>(a, nt);                                                         \
+  }
+PZ_WIRE_VAL_GEOM(pz_wire_val_p3w6_kernel, 3, 6)
+PZ_WIRE_VAL_GEOM(pz_wire_val_p2w6_kernel, 2, 6)
+PZ_WIRE_VAL_GEOM(pz_wire_val_p2w8_kernel, 2, 8)
+#undef PZ_WIRE_VAL_GEOM
 
 // Records with bytes fields: tiles of kBytesSub x 256 records, one per thread per sub-tile.
 // Phase 1 scans the sizes; after the look-back, phase 2 reads the records again and writes
@@ -702,27 +720,29 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_zero_kernel(uint6
 
 }  // namespace
 
-static uint64_t tile_recs(bool bytes) { return bytes ? kBytesTileRecs : kTileRecs; }
-
-uint64_t wire_tiles(uint64_t n) {  // scratch bound: the smaller tile of the two kernels
-  constexpr uint64_t t = kBytesTileRecs < kTileRecs ? kBytesTileRecs : kTileRecs;
-  return (n + t - 1) / t;
-}
-
 static int g_wire_variant = 0;       // tools/ A/B only
 static uint64_t* g_wire_trace = nullptr;  // tools/ only
+
+// the tile-geometry variants (3 columns): 32768 PER 3 / W 6, 65536 PER 2 / W 6, 98304 PER 2 / W 8
+static int geom_per(const WireValArgs& a) {
+  if (a.nc != 3) return kPer;
+  switch (g_wire_variant) {
+    case 32768: return 3;
+    case 65536: case 98304: return 2;
+    default: return kPer;
+  }
+}
+
+static uint64_t tile_recs(bool bytes, int per) { return bytes ? kBytesTileRecs : (uint64_t)kSub * kThreads * per; }
+
+uint64_t wire_tiles(uint64_t n) {  // scratch bound: the smallest tile of the kernels (PER 2)
+  constexpr uint64_t t = kBytesTileRecs < kSub * kThreads * 2 ? kBytesTileRecs : kSub * kThreads * 2;
+  return (n + t - 1) / t;
+}
 
 // Scratch: status[nt] then the ticket; zeroed before every launch.
 hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t s) {
   const bool bytes = a.wa_offs || a.rc_offs;
-  const uint64_t nt = (a.n + tile_recs(bytes) - 1) / tile_recs(bytes);
-  if (nt == 0) {
-    hipError_t e = hipMemsetAsync(a.total, 0, 8, s);
-    if (e == hipSuccess && a.offs) e = hipMemsetAsync(a.offs, 0, 8, s);
-    return e;
-  }
-  a.status = scratch;
-  a.ticket = reinterpret_cast<uint32_t*>(scratch + nt);
   a.nc = 0;  // the non-NULL columns, in field order (the scalar-only kernel holds only these)
   const uint32_t tags[5] = {1 << 3, 2 << 3, 5 << 3, 6 << 3, 7 << 3};
   for (int k = 0; k < 5; ++k)
@@ -730,6 +750,15 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
       a.ccol[a.nc] = a.col[k];
       a.ctag[a.nc++] = tags[k];
     }
+  const uint64_t tr = tile_recs(bytes, geom_per(a));
+  const uint64_t nt = (a.n + tr - 1) / tr;
+  if (nt == 0) {
+    hipError_t e = hipMemsetAsync(a.total, 0, 8, s);
+    if (e == hipSuccess && a.offs) e = hipMemsetAsync(a.offs, 0, 8, s);
+    return e;
+  }
+  a.status = scratch;
+  a.ticket = reinterpret_cast<uint32_t*>(scratch + nt);
   {
     const uint64_t words = nt + 1;
     const uint32_t blocks = (uint32_t)std::min<uint64_t>(64, (words + kThreads - 1) / kThreads);
@@ -755,6 +784,9 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
     break;
         PZ_TRACE(32) PZ_TRACE(34) PZ_TRACE(36) PZ_TRACE(96) PZ_TRACE(160) PZ_TRACE(288) PZ_TRACE(544) PZ_TRACE(1056)
 #undef PZ_TRACE
+        case 32768: hipLaunchKernelGGL(pz_wire_val_p3w6_kernel, g, b, 0, s, a, n32); break;
+        case 65536: hipLaunchKernelGGL(pz_wire_val_p2w6_kernel, g, b, 0, s, a, n32); break;
+        case 98304: hipLaunchKernelGGL(pz_wire_val_p2w8_kernel, g, b, 0, s, a, n32); break;
         default: hipLaunchKernelGGL(pz_wire_val_kernel, g, b, 0, s, a, n32);
       }
     } else {

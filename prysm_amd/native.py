@@ -152,6 +152,11 @@ class NativeEpoch:
         lib.call("pz_epoch_state_layout", self.st, ctypes.byref(co))
         self.committee_order = bool(co.value)
         self.one_pass = co.value == 2
+        bb, db = ctypes.c_uint32(), ctypes.c_uint32()
+        lib.call("pz_epoch_state_columns", self.st, ctypes.byref(bb), ctypes.byref(db))
+        # bytes the one-pass stream reads per validator-epoch: balance (u32 offsets or u64) and
+        # the {start, end} column (16-bit, 32-bit saturated or u64)
+        self.balance_bytes, self.dynasty_bytes = int(bb.value), int(db.value)
 
     def step(self):
         lib.call("pz_epoch_state_step", self.st)

@@ -60,7 +60,7 @@ LAYOUTS = ["auto", "twopass", "index"]
 
 @pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("n,B,inactive", [(65536, 3, False), (5000, 2, True), (4096, 9, False), (3000, 5, True),
-                                          (4097, 2, False), (1000, 3, False), (130, 2, False)])
+                                          (4097, 2, False), (1000, 3, False), (130, 2, False), (1 << 20, 2, False)])
 def test_native_epoch_single_device(n, B, inactive, layout):
     inst = _inst(n, B, inactive)
     ne = NativeEpoch(inst, device=0, layout=layout)
@@ -85,22 +85,69 @@ def test_native_epoch_single_launch(n, density):
     _check(ne, inst, steps=3)
 
 
-@pytest.mark.parametrize("variant", [4096, 32768, 65536])
+@pytest.mark.parametrize("variant", [0, 4096, 32768, 65536, 131072, 262144])
 @pytest.mark.parametrize("n,B", [(65536, 5), (32768, 9), (4097, 3), (1000, 2)])
-def test_native_epoch_fused_forms(n, B, variant):
-    """The other forms of the one-pass step's fused pass (the product is the streaming pass:
-    persistent pipelined waves): 4096 the XCD-aware 1-D grid (block L on XCD L % 8 takes piece
-    group 8 (L / 8 / B) + L % 8 of instance (L / 8) % B, the pad groups exit), 32768 one piece
-    per wave on pair lanes (round 3), 65536 one piece per wave on quad lanes; two steps each,
-    bit-exact against the oracle."""
+def test_native_epoch_fused_forms(n, B, variant, monkeypatch):
+    """The u64-balance forms of the one-pass step's fused pass (PZ_EPOCH_BAL64: the product holds
+    the balances as u32 offsets, below): 0 the product's u64 choice (the streaming pass, LDS-staged
+    when no position-order gather exists), 4096 the XCD-aware 1-D grid (block L on XCD L % 8 takes
+    piece group 8 (L / 8 / B) + L % 8 of instance (L / 8) % B, the pad groups exit), 32768 one
+    piece per wave on pair lanes (round 3), 65536 one piece per wave on quad lanes, 131072 the
+    streaming pass, 262144 the streaming pass with the last bitfield staged in LDS taken in place
+    of pre's position-order gather; two steps each, bit-exact against the oracle."""
+    monkeypatch.setenv("PZ_EPOCH_BAL64", "1")
     inst = _inst(n, B, False)
     ne = NativeEpoch(inst, device=0)
-    assert ne.one_pass
+    assert ne.one_pass and ne.balance_bytes == 8
     old = _lib.lib.dll.pz_debug_set_fused_variant(variant)
     try:
         _check(ne, inst, steps=2)
     finally:
         _lib.lib.dll.pz_debug_set_fused_variant(old)
+
+
+@pytest.mark.parametrize("n,B,density", [(65536, 5, 0.75), (1 << 20, 2, 0.75), (4097, 3, 0.5), (1000, 2, 0.75)])
+def test_native_epoch_bal32_offsets(n, B, density):
+    """The product's multi-instance layout: balances as u32 offsets from a per-instance u64 base
+    (FusedArgs.bal32, pz_epoch_state_columns reports 4 B), three steps against the oracle."""
+    inst = _inst(n, B, False, density=density)
+    ne = NativeEpoch(inst, device=0)
+    assert ne.one_pass and (ne.balance_bytes, ne.dynasty_bytes) == (4, 4)
+    _check(ne, inst, steps=3)
+
+
+def test_native_epoch_bal32_rebase(monkeypatch):
+    """The offsets re-based every 2 steps (PZ_EPOCH_B32_PERIOD; 2^29 in the product): five
+    steps, each compared with the oracle."""
+    monkeypatch.setenv("PZ_EPOCH_B32_PERIOD", "2")
+    inst = _inst(65536, 3, False)
+    ne = NativeEpoch(inst, device=0)
+    assert ne.balance_bytes == 4
+    _check(ne, inst, steps=5)
+
+
+def test_native_epoch_bal32_wide_spread():
+    """An instance whose balances span 2^30 or more keeps the u64 column (the widest part is
+    reported); the instances beside it are unaffected; bit-exact."""
+    inst = _inst(4096, 3, False)
+    inst["balance"][1, :7] = np.array([1, 1 << 30, 5, 1 << 40, 2, 3, 9999999999999999999], dtype=np.uint64)
+    ne = NativeEpoch(inst, device=0)
+    assert ne.balance_bytes == 8
+    _check(ne, inst, steps=2)
+
+
+def test_native_epoch_bal32_wrap_below_zero(monkeypatch):
+    """Balances of 0 and 1 under penalties wrap below zero as Go's uint64 does (2^64 - 1):
+    exact in the offsets (mod 2^64); the re-base after the wrap finds the spread too wide and
+    the state returns to the u64 column; three steps against the oracle."""
+    monkeypatch.setenv("PZ_EPOCH_B32_PERIOD", "1")
+    inst = _inst(4096, 3, False, density=0.75)
+    rng = np.random.default_rng(4)
+    inst["balance"][:] = rng.integers(0, 2, size=inst["balance"].shape, dtype=np.uint64)
+    ne = NativeEpoch(inst, device=0)
+    assert ne.balance_bytes == 4
+    _check(ne, inst, steps=3)
+    assert (inst["balance"] > (1 << 63)).any()  # some balance wrapped
 
 
 @pytest.mark.parametrize("case", ["reward_panic", "short_bitfield", "many_atts"])
@@ -153,13 +200,13 @@ def test_native_epoch_single_launch_matches_three_launches():
         np.testing.assert_array_equal(x, y)
 
 
-@pytest.mark.parametrize("knob", ["PZ_EPOCH_MULTI", "PZ_EPOCH_WIN_FUSED"])
+@pytest.mark.parametrize("knob,val", [("PZ_EPOCH_MULTI", "1"), ("PZ_EPOCH_WIN_FUSED", "0")])
 @pytest.mark.parametrize("n,B,density", [(65536, 3, 0.75), (4097, 5, 0.75), (8192, 4, 0.5)])
-def test_native_epoch_one_pass_ab_knobs(knob, n, B, density, monkeypatch):
+def test_native_epoch_one_pass_ab_knobs(knob, val, n, B, density, monkeypatch):
     """The one-pass step's A/B forms read at state creation: one launch over the
-    B instances (PZ_EPOCH_MULTI) and winners in the fused waves without the mid launch
-    (PZ_EPOCH_WIN_FUSED), bit-exact against the oracle over two steps."""
-    monkeypatch.setenv(knob, "1")
+    B instances (PZ_EPOCH_MULTI=1) and the winners by the mid launch instead of in the
+    streaming waves (PZ_EPOCH_WIN_FUSED=0), bit-exact against the oracle over two steps."""
+    monkeypatch.setenv(knob, val)
     inst = _inst(n, B, False, density=density)
     ne = NativeEpoch(inst, device=0)
     assert ne.one_pass

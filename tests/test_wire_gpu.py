@@ -206,3 +206,31 @@ def test_lookback_multi_window(variant):
     k = 50_000  # the host encoder on a prefix (the framing is per record, so prefixes agree)
     want = wire.validators(pb.Validators(k, balance=bal[:k], start_dynasty=start[:k], end_dynasty=end[:k]))
     assert ref[:len(want)].cpu().numpy().tobytes() == want
+
+
+@pytest.mark.parametrize("variant", [32768, 65536, 98304])
+@pytest.mark.parametrize("offsets,small", [(False, True), (False, False), (True, False)])
+def test_scalar_tile_geometry(variant, offsets, small):
+    """The tile-geometry A/B of the 3-column kernel (wire.hip PZ_WIRE_VAL_GEOM: 3,072- and
+    2,048-record tiles, 48 / 32 KiB stages): many tiles and a ragged last tile, genesis-like
+    records (~15 B: the LDS stage path) or mixed varint widths (tiles that outgrow the stage
+    write lane by lane), framed against the host encoder and bare with record offsets against
+    the protobuf runtime."""
+    n = 3072 * 13 + 777
+    rng = np.random.default_rng(variant + offsets)
+    if small:
+        start = rng.integers(0, 3, size=n).astype(np.uint64) * rng.integers(0, 1 << 20, size=n, dtype=np.uint64)
+        v = pb.Validators(n, balance=rng.integers(16, 49, size=n, dtype=np.uint64), start_dynasty=start,
+                          end_dynasty=np.full(n, 9999999999999999999, np.uint64))
+    else:
+        v = _scalar_cols(rng, n, ("balance", "start_dynasty", "end_dynasty"))
+    old = _lib.lib.dll.pz_debug_set_wire_variant(variant)
+    try:
+        if offsets:
+            raw, offs = wire.validators_device(v, 0, with_offsets=True)
+            assert offs[0] == 0 and offs[-1] == len(raw)
+            assert raw == b"".join(oracle_record(v, i) for i in range(n))
+        else:
+            assert wire.validators_device(v, 11) == wire.validators(v)
+    finally:
+        _lib.lib.dll.pz_debug_set_wire_variant(old)

@@ -45,6 +45,17 @@ def main():
     alg = n * 24 + total
     print("wire: %d records, %d bytes, %.1f us/launch, %.0f GB/s algorithmic (%.1f%% of 8 TB/s)"
           % (n, total, us, alg / us / 1e3, alg / us / 1e3 / 80))
+    geom = os.environ.get("WIRE_GEOM")
+    if geom:  # tile-geometry variants (wire.hip PZ_WIRE_VAL_GEOM): exact output, compared with the product's
+        want = out[:total].clone()
+        for v in [int(x) for x in geom.split(",")]:
+            _lib.lib.dll.pz_debug_set_wire_variant(v)
+            out.zero_()
+            us_v = timed()
+            same = int(tot.item()) == total and bool(torch.equal(out[:total], want))
+            print("  geometry %6d: %.1f us/launch (%.1f%% of 8 TB/s), output identical: %s"
+                  % (v, us_v, alg / us_v / 1e3 / 80, same), flush=True)
+        _lib.lib.dll.pz_debug_set_wire_variant(0)
     if len(sys.argv) > 2:  # ablation (wire.hip wire_val_body V, one tile per workgroup): results wrong for V != 0
         names = {1: "tile = blockIdx (no ticket)", 2: "no stage build", 4: "no look-back", 8: "no store",
                  7: "1+2+4", 15: "1+2+4+8", 16: "reload values for the build",
