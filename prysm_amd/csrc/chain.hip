@@ -626,16 +626,14 @@ struct RankDev {
   // committee positions (the sharded epoch's crosslink partial sums)
   DevArr<uint32_t> committee, lcomm, lcpos;
   DevArr<uint64_t> coffs, lcoffs;
-  // the vote cache: this range's words of every slot's voter bitmap, partial totals
-  DevArr<uint32_t> bitmaps;
+  // the vote cache, voter-major (votes.h VoteWordArgs): bm[w * n + v] holds this range's
+  // validator v's votes for ids 64 w .. 64 w + 63; partial totals and present flags per id
+  DevArr<uint64_t> bm;
   DevArr<uint64_t> totals;
   DevArr<uint8_t> present;
-  uint64_t words = 0;
   DevArr<uint8_t> d_qpack;
   DevArr<uint64_t> d_err;      // sticky tally panic flag
-  DevArr<uint32_t> ubits, uflag;
-  DevArr<uint32_t> d_leader;  // [2 leader counters, used alternately; pad][uint4 leader records]
-  uint32_t lead_par = 0;      // the counter this rank's next flush counts in
+  DevArr<uint32_t> v_ticket;   // the fused gather's arrival ticket (left zero)
   DevArr<uint64_t> t64;        // the gathered justification totals + panic flag (65 words)
   // epoch scratch: red = {scal[8], vote[natt], total[natt]} (one all-reduce when sharded)
   DevArr<uint64_t> e_red, e_mask, e_nb;
@@ -681,26 +679,25 @@ struct Engine {
   H32Table<uint32_t> slot_of;
   std::vector<H32> slot_hash;
   uint64_t cap = 0;
-  // pending tally work: per queued attestation its committee, bitfield, the hash-log ids of
-  // its 64 signed parent hashes and a mask of the ones equal to an oblique parent hash; the
-  // device expands them into (attestation, parent) items (pz_vote_ids_kernel)
-  // The walk writes the queue straight into pinned memory, which the union pass reads in place
-  // (launch_vote_ids_direct): two queues, the walk filling one while a flush's kernels may
-  // still read the other (RankDev::vq_ev).
+  // pending tally work: per queued attestation its committee's members, its bitfield and the
+  // vote-cache ids of its tallied signed parent hashes as id words and masks (votes.h
+  // VoteWordArgs).  The walk writes the queue straight into pinned memory: two queues, the walk
+  // filling one while a flush's kernels may still read the other (RankDev::vq_ev).
   struct VoteQueue {
+    PinVec<uint4> rec;    // per attestation (votes.h VoteWordArgs.rec)
+    PinVec<uint4> pairs;  // its parents' id words and masks
     PinVec<uint8_t> bits;
-    PinVec<uint64_t> boffs;             // natt + 1
-    PinVec<uint32_t> comm, slots;       // slots: natt x 64 vote-cache slots of the signed parents
-    PinVec<uint64_t> skip;
+    uint32_t chunks = 1;  // max ceil(k / 256) over the queue
     bool busy = false;
-    size_t natt() const { return comm.size(); }
+    size_t natt() const { return rec.size(); }
   } vq[2];
   int vq_cur = 0;
   // flushes run asynchronously to the walk: the queue is packed into a pinned arena and
   // copied with one H2D per rank; the arena is reused once every rank's copy is done
   PinBuf q_arena;
   bool q_arena_busy = false;
-  uint64_t ncomm = 0, cwords = 1;
+  uint64_t ncomm = 0;
+  std::vector<uint64_t> h_coffs;  // the committees' first member offsets (host copy)
   PinBuf e_pin, e_pin_out;   // the epoch inputs' pinned staging; the results' pinned landing
   PinBuf tot_pin;            // the gathered justification totals (65 words; + a sequence word)
   uint64_t gather_seq = 0;   // the last sequence number the fused gather was asked to write
@@ -883,37 +880,30 @@ static void hash_many(Engine& g, const std::string& data, const std::vector<uint
 // Every rank's vote-cache arrays grown to nc slots, keeping their contents (outside a flush).
 static void grow_slots(Engine& g, uint64_t nc) {
   if (nc <= g.cap) return;
+  nc = (nc + 63) & ~63ull;  // whole id words
   {
     each_rank(g, [&](RankDev& r) {
-      DevArr<uint32_t> bm;
+      DevArr<uint64_t> bm;
       DevArr<uint64_t> tt;
       DevArr<uint8_t> pr;
-      check(bm.alloc(nc * r.words));
+      check(bm.alloc(nc / 64 * r.n + 1));
       check(tt.alloc(nc));
       check(pr.alloc(nc));
-      hchk(hipMemsetAsync(bm.p, 0, nc * r.words * 4, r.s), "memset");
+      hchk(hipMemsetAsync(bm.p, 0, (nc / 64 * r.n + 1) * 8, r.s), "memset");
       hchk(hipMemsetAsync(tt.p, 0, nc * 8, r.s), "memset");
       hchk(hipMemsetAsync(pr.p, 0, nc, r.s), "memset");
-      if (g.cap) {
-        if (r.words)
-          hchk(hipMemcpyAsync(bm.p, r.bitmaps.p, g.cap * r.words * 4, hipMemcpyDeviceToDevice, r.s), "D2D");
+      if (g.cap) {  // the old id words are a prefix of the new rows
+        if (r.n) hchk(hipMemcpyAsync(bm.p, r.bm.p, g.cap / 64 * r.n * 8, hipMemcpyDeviceToDevice, r.s), "D2D");
         hchk(hipMemcpyAsync(tt.p, r.totals.p, g.cap * 8, hipMemcpyDeviceToDevice, r.s), "D2D");
         hchk(hipMemcpyAsync(pr.p, r.present.p, g.cap, hipMemcpyDeviceToDevice, r.s), "D2D");
       }
       hchk(hipStreamSynchronize(r.s), "sync");
-      std::swap(r.bitmaps.p, bm.p);
-      std::swap(r.bitmaps.n, bm.n);
+      std::swap(r.bm.p, bm.p);
+      std::swap(r.bm.n, bm.n);
       std::swap(r.totals.p, tt.p);
       std::swap(r.totals.n, tt.n);
       std::swap(r.present.p, pr.p);
       std::swap(r.present.n, pr.n);
-      // the union buffers are all zero between flushes (and a slot is only created outside
-      // one): reallocate them zeroed
-      check(r.ubits.alloc(nc * g.ncomm * g.cwords));
-      check(r.uflag.alloc(nc * g.ncomm));
-      hchk(hipMemsetAsync(r.ubits.p, 0, nc * g.ncomm * g.cwords * 4, r.s), "memset");
-      hchk(hipMemsetAsync(r.uflag.p, 0, nc * g.ncomm * 4, r.s), "memset");
-      hchk(hipStreamSynchronize(r.s), "sync");
     });
     g.cap = nc;
   }
@@ -955,13 +945,12 @@ static uint32_t log_hash(Engine& g, const H32& h, bool votable = true) {
 // Enqueue the pending tally items on every rank; no host wait (the pinned arena and its
 // per-rank events make the H2D asynchronous).  Balances only change in stateRecalc's epoch,
 // which each rank's stream orders after every flush, so a flush may run any time before it.
-// With `gq` (a stateRecalc's flush on one rank), the leader pass also gathers the 64
-// justification totals into g.tot_pin and g.ev_totals is recorded behind it: returns true
-// when it did so (tally_gather_enqueue's work is then done).
+// With `gq` (a stateRecalc's flush on one rank), the tally's last block also gathers the 64
+// justification totals into g.tot_pin (polled by their sequence word): returns true when it
+// did so (tally_gather_enqueue's work is then done).
 // One rank's stateRecalc epoch, prepared on the host (the pack in g.e_pin, the arguments) by the
-// transition's vote flush between its union and leader launches -- the host packs while the
-// device runs the stage and union passes -- and its count blocks ride in the leader launch
-// (pz_vote_leader_count_kernel), reading the pinned pack in place: two launches less per
+// transition's vote flush before its tally launch, whose count blocks ride in that launch
+// (pz_vote_words_count_kernel), reading the pinned pack in place: two launches less per
 // transition.  `staged` / `counted`: done (else epoch_launch_rest does them).
 struct EpochLaunch {
   EpochArgs a;
@@ -976,11 +965,9 @@ using EpochPrep = std::function<EpochLaunch*()>;
 // How a flush reaches the device (PZ_VOTE_PATH, read per flush so that one test process can
 // run every path; A/B knob):
 //   segments (product)  the walk's pinned queue arrays copied into the device pack by ONE
-//                       multi-segment stage kernel, then the per-item union pass;
+//                       multi-segment stage kernel, then the tally;
 //   packed              round 3: the queue memcpy'd into one pinned arena first, one stage copy;
-//   direct              no copy: a per-attestation union pass reads the pinned queue in place
-//                       (measured slower: every wave waits out host-link round trips).
-// PZ_VOTE_UNION=att: the per-attestation union pass over the device copy instead of per item.
+//   direct              no copy: the tally reads the pinned queue in place.
 enum VotePath { kVoteSegments, kVotePacked, kVoteDirect };
 static VotePath vote_path() {
   const char* e = std::getenv("PZ_VOTE_PATH");
@@ -988,10 +975,6 @@ static VotePath vote_path() {
   if (!std::strcmp(e, "packed")) return kVotePacked;
   if (!std::strcmp(e, "direct")) return kVoteDirect;
   return kVoteSegments;
-}
-static bool vote_union_att() {
-  const char* e = std::getenv("PZ_VOTE_UNION");
-  return e && !std::strcmp(e, "att");
 }
 
 static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, const EpochPrep* prep = nullptr) {
@@ -1003,9 +986,8 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
   PhaseTimer pt(g.prof[kProfFlush]);
   const uint64_t natt = Q.natt();
   auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
-  // the device pack: boffs | skip | comm | slots | bits
-  const size_t o_boffs = 0, o_skip = o_boffs + al(Q.boffs.size() * 8), o_comm = o_skip + al(natt * 8),
-               o_slots = o_comm + al(natt * 4), o_bits = o_slots + al(Q.slots.size() * 4),
+  // the device pack: rec | pairs | bits
+  const size_t o_rec = 0, o_pairs = o_rec + natt * 16, o_bits = o_pairs + Q.pairs.size() * 16,
                total = staged ? o_bits + al(Q.bits.size()) : 0;
   if (path == kVotePacked) {
     if (g.q_arena_busy) {
@@ -1015,23 +997,16 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
     }
     check(g.q_arena.reserve(total));
     uint8_t* qa = g.q_arena.p;
-    std::memcpy(qa + o_boffs, Q.boffs.data(), Q.boffs.size() * 8);
-    std::memcpy(qa + o_skip, Q.skip.data(), natt * 8);
-    std::memcpy(qa + o_comm, Q.comm.data(), natt * 4);
-    std::memcpy(qa + o_slots, Q.slots.data(), Q.slots.size() * 4);
+    std::memcpy(qa + o_rec, Q.rec.data(), natt * 16);
+    if (Q.pairs.size()) std::memcpy(qa + o_pairs, Q.pairs.data(), Q.pairs.size() * 16);
     if (Q.bits.size()) std::memcpy(qa + o_bits, Q.bits.data(), Q.bits.size());
   }
   each_rank(g, [&](RankDev& r) {
     // Growing a device buffer frees the old one, which in-flight flushes may still read:
-    // drain the stream first (rare: the buffers double).
-    const uint64_t lead_words = 4 + natt * 64 * 4;  // 2 counters (+ pad to 16 B), then uint4 records
-    if (total > r.d_qpack.n || lead_words > r.d_leader.n) {
+    // drain the stream first (rare: the buffer doubles).
+    if (total > r.d_qpack.n) {
       hchk(hipStreamSynchronize(r.s), "sync");
-      if (total > r.d_qpack.n) check(r.d_qpack.alloc(std::max<uint64_t>(total, 2 * r.d_qpack.n)));
-      if (lead_words > r.d_leader.n) {
-        check(r.d_leader.alloc(std::max<uint64_t>(lead_words, 2 * r.d_leader.n)));
-        hchk(hipMemsetAsync(r.d_leader.p, 0, 16, r.s), "memset");  // both counters and the gather ticket
-      }
+      check(r.d_qpack.alloc(std::max<uint64_t>(total, 2 * r.d_qpack.n)));
     }
     if (path == kVotePacked) {
       // the pack crosses PCIe in a kernel of this stream (a copy-engine H2D costs ~13 us more on
@@ -1039,7 +1014,7 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
       void* src = nullptr;
       check(g.q_arena.dev(r.dev, &src));
       hchk(launch_stage_h2d(src, r.d_qpack.p, total, r.s), "stage H2D");
-      if (!gather) {  // (gathering: g.ev_totals, later in the stream, frees the arena)
+      if (!gather) {  // (gathering: the transition's totals, later in the stream, free the arena)
         if (!r.q_ev) hchk(hipEventCreateWithFlags(&r.q_ev, hipEventDisableTiming), "event");
         hchk(hipEventRecord(r.q_ev, r.s), "event");
       }
@@ -1050,10 +1025,8 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
       auto seg = [&](const void* src, size_t off, size_t bytes) {
         if (bytes) sg.seg[sg.nseg++] = StageSeg{src, r.d_qpack.p + off, (bytes + 15) / 16};
       };
-      seg(Q.boffs.dev(r.dev), o_boffs, Q.boffs.size() * 8);
-      seg(Q.skip.dev(r.dev), o_skip, natt * 8);
-      seg(Q.comm.dev(r.dev), o_comm, natt * 4);
-      seg(Q.slots.dev(r.dev), o_slots, Q.slots.size() * 4);
+      seg(Q.rec.dev(r.dev), o_rec, natt * 16);
+      seg(Q.pairs.dev(r.dev), o_pairs, Q.pairs.size() * 16);
       seg(Q.bits.dev(r.dev), o_bits, Q.bits.size());
       hchk(launch_stage_h2d_segs(sg, r.s), "stage H2D");
     }
@@ -1061,66 +1034,53 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
       check(r.d_err.alloc(1));
       hchk(hipMemsetAsync(r.d_err.p, 0, 8, r.s), "memset");
     }
-    VoteIdArgs v;
+    if (!r.v_ticket.p) {
+      check(r.v_ticket.alloc(1));
+      hchk(hipMemsetAsync(r.v_ticket.p, 0, 4, r.s), "memset");
+    }
+    VoteWordArgs v;
     std::memset(&v, 0, sizeof v);
     v.committee = r.committee.p;
-    v.coffs = r.coffs.p;
     if (staged) {
-      v.att_comm = reinterpret_cast<const uint32_t*>(r.d_qpack.p + o_comm);
+      v.rec = reinterpret_cast<const uint4*>(r.d_qpack.p + o_rec);
+      v.pairs = reinterpret_cast<const uint4*>(r.d_qpack.p + o_pairs);
       v.bits = r.d_qpack.p + o_bits;
-      v.boffs = reinterpret_cast<const uint64_t*>(r.d_qpack.p + o_boffs);
-      v.slots = reinterpret_cast<const uint32_t*>(r.d_qpack.p + o_slots);
-      v.skip = reinterpret_cast<const uint64_t*>(r.d_qpack.p + o_skip);
     } else {  // read in place (pinned, mapped into this rank's device)
-      v.att_comm = Q.comm.dev(r.dev);
+      v.rec = Q.rec.dev(r.dev);
+      v.pairs = Q.pairs.dev(r.dev);
       v.bits = Q.bits.dev(r.dev);
-      v.boffs = Q.boffs.dev(r.dev);
-      v.slots = Q.slots.dev(r.dev);
-      v.skip = Q.skip.dev(r.dev);
     }
     v.natt = natt;
+    v.chunks = Q.chunks;
     v.balance = r.balance.p;
     v.nval = r.n;
     v.val_offset = r.lo;
     v.nval_global = g.nval;
-    v.bitmaps = r.bitmaps.p;
-    v.words_per_slot = r.words;
+    v.bm = r.bm.p;
     v.totals = r.totals.p;
     v.present = r.present.p;
     v.err = r.d_err.p;  // sticky: read (and the chain poisoned) at the next sync point
-    v.ubits = r.ubits.p;
-    v.uflag = r.uflag.p;
-    v.leader = reinterpret_cast<uint4*>(r.d_leader.p + 4);
-    v.nlead = r.d_leader.p + r.lead_par;  // counted by this flush's union pass
-    v.nlead_next = r.d_leader.p + (r.lead_par ^ 1);  // zeroed by its leader pass for the next flush
-    r.lead_par ^= 1;
-    v.ncomm = g.ncomm;
-    v.cwords = g.cwords;
     if (gather) {
       check(g.tot_pin.reserve((kJustifySlots + 2) * 8));
       void* dp = nullptr;
       check(g.tot_pin.dev(r.dev, &dp));
       v.gather_out = static_cast<uint64_t*>(dp);
-      v.ticket = r.d_leader.p + 2;
+      v.ticket = r.v_ticket.p;
       v.gq = *gq;
       v.gather_seq = ++g.gather_seq;
       // (pooled pinned memory holds old words: clear the sequence word before the launch)
       reinterpret_cast<volatile uint64_t*>(g.tot_pin.p)[kJustifySlots + 1] = 0;
     }
-    if (prep && path == kVoteSegments && !vote_union_att()) {
-      // the union, then (host: the transition's epoch packed meanwhile) the leader pass with the
-      // epoch's count blocks
-      hchk(launch_vote_union(v, r.s), "vote union");
+    if (prep) {
+      // (host: the transition's epoch packed before the launch) the tally with the epoch's
+      // count blocks in one launch
       EpochLaunch* el = (*prep)();
-      hchk(launch_vote_leader_count(v, el->a, r.s), "vote leader + epoch count");
+      hchk(launch_vote_words_count(v, el->a, r.s), "vote tally + epoch count");
       el->counted = true;
     } else {
-      hchk(!staged ? launch_vote_ids_direct(v, r.s) : vote_union_att() ? launch_vote_ids_att(v, r.s)
-                                                                        : launch_vote_ids(v, r.s),
-           "vote tally");
-      if (prep) (*prep)();
+      hchk(launch_vote_words(v, r.s), "vote tally");
     }
-    if (!gather) {  // (gathering: the walk waits for the leader pass before any later flush)
+    if (!gather) {  // (gathering: the walk waits for the tally before any later flush)
       if (!r.vq_ev[g.vq_cur]) hchk(hipEventCreateWithFlags(&r.vq_ev[g.vq_cur], hipEventDisableTiming), "event");
       hchk(hipEventRecord(r.vq_ev[g.vq_cur], r.s), "event");
     }
@@ -1138,11 +1098,10 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
       if (r.vq_ev[g.vq_cur]) hchk(hipEventSynchronize(r.vq_ev[g.vq_cur]), "event sync");
     N.busy = false;
   }
+  N.rec.reset();
+  N.pairs.reset();
   N.bits.reset();
-  N.boffs.reset();
-  N.comm.reset();
-  N.slots.reset();
-  N.skip.reset();
+  N.chunks = 1;
   return gather;
 }
 
@@ -1205,7 +1164,7 @@ static void tally_gather_finish(Engine& g) {
     std::atomic_thread_fence(std::memory_order_acquire);
     if (*sq != g.gather_seq) g.prof[kProfPollFallback] += 1;  // reported, so a fallback is not silent
     if (*sq == g.gather_seq) {
-      // every rank's flush is done: its stage kernel preceded the leader pass
+      // every rank's flush is done: its stage kernel preceded the tally
       g.q_arena_busy = false;
       if (reinterpret_cast<const uint64_t*>(g.tot_pin.p)[kJustifySlots])
         throw Panic{"calculateBlockVoteCache: CheckBit / validator index out of range"};
@@ -1375,16 +1334,56 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, AttLo
   if (g.A->cache_nil) throw Panic{"assignment to entry in nil map (core.go:323)"};
   // the member loop reaches CheckBit(bitfield, 8 * len) when the committee is longer
   if (k > 8ull * a.bf_len) throw Panic{"calculateBlockVoteCache: CheckBit index out of range (core.go:330)"};
+  // the tallied parents as id words and masks (votes.h VoteWordArgs): a parent listed twice
+  // is one bit (its voters are counted once, as the Go loop's voter scan does).  The recent
+  // window's ids are consecutive, so the usual attestation spans two id words: branch-free
+  // loops for that case, a search for the rest.
+  uint32_t lo = UINT32_MAX, hi = 0;
+  for (size_t j = 0; j < 64; ++j) {
+    const uint32_t sl = slots[j];
+    const bool ok = sl != UINT32_MAX && !((skip >> j) & 1);
+    lo = ok && sl < lo ? sl : lo;
+    hi = ok && sl > hi ? sl : hi;
+  }
+  uint32_t pw[64];
+  uint64_t pm[64];
+  uint32_t npr = 0;
+  if (lo != UINT32_MAX && (hi >> 6) <= (lo >> 6) + 1) {
+    const uint32_t w0 = lo >> 6;
+    uint64_t m0 = 0, m1 = 0;
+    for (size_t j = 0; j < 64; ++j) {
+      const uint32_t sl = slots[j];
+      const bool ok = sl != UINT32_MAX && !((skip >> j) & 1);
+      const uint32_t b = sl - (w0 << 6);  // < 128 when ok
+      const uint64_t bit = ok ? 1ull << (b & 63) : 0;
+      m0 |= b < 64 ? bit : 0;
+      m1 |= b < 64 ? 0 : bit;
+    }
+    if (m0) pw[npr] = w0, pm[npr++] = m0;
+    if (m1) pw[npr] = w0 + 1, pm[npr++] = m1;
+  } else if (lo != UINT32_MAX) {
+    for (size_t j = 0; j < 64; ++j) {
+      const uint32_t sl = slots[j];
+      if (sl == UINT32_MAX || ((skip >> j) & 1)) continue;
+      const uint32_t w = sl >> 6;
+      uint32_t x = 0;
+      while (x < npr && pw[x] != w) ++x;
+      if (x == npr) pw[npr] = w, pm[npr++] = 0;
+      pm[x] |= 1ull << (sl & 63);
+    }
+  }
   Engine::VoteQueue& Q = g.vq[g.vq_cur];
-  if (Q.boffs.size() == 0) Q.boffs.push_back(0);
-  Q.comm.push_back(c);
-  Q.skip.push_back(skip);
-  std::memcpy(Q.slots.grow(64), slots, sizeof slots);
+  const uint32_t poff = (uint32_t)Q.pairs.size();
+  uint4* pq = Q.pairs.grow(npr);
+  for (uint32_t x = 0; x < npr; ++x) pq[x] = make_uint4((uint32_t)pm[x], (uint32_t)(pm[x] >> 32), pw[x], 0);
+  const uint32_t boff = (uint32_t)Q.bits.size();
   const uint8_t* bf = a.at(a.bf_off);
   const size_t nbf = (k + 7) / 8;
   if (nbf) std::memcpy(Q.bits.grow(nbf), bf, nbf);
-  Q.boffs.push_back(Q.bits.size());
-  if (Q.natt() >= kFlushAtts) flush_votes_enqueue(g);  // bounds the queue; no host wait
+  Q.rec.push_back(make_uint4((uint32_t)g.h_coffs[c], (uint32_t)k, boff, poff | (npr << kVoteRecPairShift)));
+  Q.chunks = std::max<uint32_t>(Q.chunks, (uint32_t)((k + 255) / 256));
+  if (Q.natt() >= kFlushAtts || Q.bits.size() >= (1ull << 31))
+    flush_votes_enqueue(g);  // bounds the queue (and its u32 offsets); no host wait
 }
 
 // One rank: the epoch's arguments over the pack in g.e_pin (already built), its device buffers,
@@ -1714,7 +1713,7 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
       if (const uint32_t* sl = g.slot_of.find(g.hlog[recent_id(g, *A, i)])) q.slot[i] = *sl;
     }
   }
-  // one rank: the epoch is prepared inside the flush (between its union and leader launches)
+  // one rank: the epoch is prepared inside the flush (before its tally launch)
   const bool one = g.world == 1;
   EpochLaunch el;
   const EpochPrep prep = [&]() -> EpochLaunch* {
@@ -1901,8 +1900,8 @@ static void init_tail(Engine& g, const std::vector<uint32_t>& members, const std
   g.csize.resize(offs.size() - 1);
   for (size_t c = 0; c + 1 < offs.size(); ++c) g.csize[c] = offs[c + 1] - offs[c];
   g.ncomm = g.csize.size();
-  g.cwords = 1;
-  for (uint64_t k : g.csize) g.cwords = std::max<uint64_t>(g.cwords, (k + 31) / 32);
+  g.h_coffs = offs;
+  if (offs.back() >= (1ull << 32)) throw (int)fail(PZ_EINVAL, "committee lists above 2^32 members");
   // 64-aligned validator ranges, as pz_epoch_state / pz_comm_vote_tally split them
   const uint64_t span = 64 * std::max<uint64_t>(1, (n + 64ull * g.world - 1) / (64ull * g.world));
   each_rank(g, [&](RankDev& r) {
@@ -1910,7 +1909,6 @@ static void init_tail(Engine& g, const std::vector<uint32_t>& members, const std
     r.hi = std::min<uint64_t>(n, (uint64_t)(r.grank + 1) * span);
     if (g.world == 1) r.lo = 0, r.hi = n;
     r.n = r.hi - r.lo;
-    r.words = (r.n + 31) / 32;
     upload(r, r.committee, members.data(), members.size());
     upload(r, r.coffs, offs.data(), offs.size());
     upload(r, r.balance, g.h_balance.data() + r.lo, r.n);

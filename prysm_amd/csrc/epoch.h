@@ -58,10 +58,10 @@ struct EpochHandoff {
   uint32_t nrec;
   uint64_t seq;
 };
-// The vote-cache leader pass (votes_dev.h) and this one-instance epoch's count pass (all three
-// ranges) in ONE launch, leader blocks first (the chain engine's stateRecalc, one rank).
-struct VoteIdArgs;
-hipError_t launch_vote_leader_count(const VoteIdArgs& v, const EpochArgs& a, hipStream_t s);
+// The vote-cache tally (votes_dev.h, voter-major) and this one-instance epoch's count pass (all
+// three ranges) in ONE launch, tally blocks first (the chain engine's stateRecalc, one rank).
+struct VoteWordArgs;
+hipError_t launch_vote_words_count(const VoteWordArgs& v, const EpochArgs& a, hipStream_t s);
 // winners: the mid pass's crosslink winners run in the same launch (only when no compaction is
 // needed: every validator active).
 hipError_t launch_epoch_reward_handoff(const EpochArgs& a, const EpochHandoff& h, bool winners, hipStream_t s);

@@ -28,6 +28,16 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// The same sum by DPP (votes_dev.h wsum64_dpp: no LDS round trips, where the xor-shuffle form
+// is a dependent chain of 12 ds_bpermute); wave-uniform, every lane active.
+__device__ __forceinline__ uint64_t wave_sum_dpp(uint64_t v) { return wsum64_dpp(v); }
+// Sum over the wave of a per-lane count of at most 4 (a ballot per unit; wave-uniform).
+__device__ __forceinline__ uint64_t wave_count4(const bool (&x)[4]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c += __popcll(__ballot(x[i]));
+  return c;
+}
 __device__ __forceinline__ uint64_t wave_max(uint64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -1094,7 +1104,10 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     }
     const uint64_t bbase = B32 ? f.bal32_base[inst] : 0;
     uint32_t sv[4], ev[4];
-    if (MODE & 16384) {
+    if (MODE & 8) {  // (ablation: no start/end loads, every validator taken as active)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sv[i] = 0, ev[i] = 0xFFFFFFFFu;
+    } else if (MODE & 16384) {
       const uint4 w = ld16_nt(reinterpret_cast<const uint64_t*>(f.se16 + inst * f.vstride + pp));
       sv[0] = w.x & 0xFFFFu, ev[0] = w.x >> 16, sv[1] = w.y & 0xFFFFu, ev[1] = w.y >> 16;
       sv[2] = w.z & 0xFFFFu, ev[2] = w.z >> 16, sv[3] = w.w & 0xFFFFu, ev[3] = w.w >> 16;
@@ -1107,7 +1120,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     uint4 cix = make_uint4(0, 0, 0, 0);
     if (MODE & 256)
       lcw = f.lastco[inst * f.lcw + (pp >> 5)];
-    else
+    else if (!(MODE & 2))  // (ablation 2: no reward-bit lookups)
       cix = *reinterpret_cast<const uint4*>(a.co_index + pp);
     // the committee bitfield bytes holding the lane's positions (two at most), branch-free and
     // clamped to the bitfield: x = g + i - cb is position g + i's bit; lanes before the committee
@@ -1132,7 +1145,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
       uint64_t t = 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) t += v[i] ? b[i] : 0;
-      ts = wave_sum(t);
+      ts = wave_sum_dpp(t);
       if (ci.ga != kManyAtt) {
         uint64_t vv = 0;
 #pragma unroll
@@ -1141,7 +1154,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
           const uint32_t by = ((x >> 3) == (qlo >> 3)) ? byA : byB;
           if (v[i] && (uint64_t)x < (uint64_t)ci.nbits && ((by >> (7 - (uint32_t)(x & 7))) & 1)) vv += b[i];
         }
-        vs = wave_sum(vv);
+        vs = wave_sum_dpp(vv);
         g1 = ci.ga;
         if (wiw && lane == 0) one_win<false>(a, f, inst, ci.ga, vs, ts, win1);
       } else {  // several attestations of this committee: direct atomics per attestation
@@ -1157,7 +1170,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
             const uint64_t x = (uint64_t)(qs + i);
             if (v[i] && x < nbits && bit_at(bf, x)) vv += b[i];
           }
-          vv = wave_sum(vv);
+          vv = wave_sum_dpp(vv);
           if (wiw && lane == 0) one_win<false>(a, f, inst, (uint32_t)ga, vv, ts, f.att_win[inst * a.natt + ga]);
           if (lane < 2) {
             uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + ga;
@@ -1172,19 +1185,22 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     const uint64_t d = a.dynasty[inst];
     const uint8_t* lastbf = a.bits + lb;
     const uint32_t ci4[4] = {cix.x, cix.y, cix.z, cix.w};
-    bool act[4];
+    bool act[4], off[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       act[i] = (uint64_t)sv[i] <= d && d < (uint64_t)ev[i];
-      nm += (v[i] && !act[i]) ? 1 : 0;
+      off[i] = v[i] && !act[i];
     }
+    nm = wave_count4(off);  // (wave-uniform: the block end reads lane 0's)
     if (applied) {  // every validator active: rank == index, the validator at p is co_index[p]
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const bool r = (MODE & 256) ? ((lcw >> ((p + i) & 31)) & 1) : bit_at(lastbf, v[i] ? ci4[i] : 0u);
+        const bool r = (MODE & 2) ? (b[i] & 1)
+                       : (MODE & 256) ? ((lcw >> ((p + i) & 31)) & 1) : bit_at(lastbf, v[i] ? ci4[i] : 0u);
         b[i] = r ? b[i] + PZ_ATTESTER_REWARD : b[i] - PZ_ATTESTER_REWARD;
       }
-      if (B32) {  // the offsets back: (base + o +- 1) - base = o +- 1, inside u32 (the state's re-base bound)
+      if (MODE & 4) {  // (ablation: no balance store)
+      } else if (B32) {  // the offsets back: (base + o +- 1) - base = o +- 1, inside u32 (the state's re-base bound)
         if (v[0] && v[1] && v[2] && v[3]) {
           *reinterpret_cast<uint4*>(Bal32 + p) = make_uint4((uint32_t)(b[0] - bbase), (uint32_t)(b[1] - bbase),
                                                             (uint32_t)(b[2] - bbase), (uint32_t)(b[3] - bbase));
@@ -1209,6 +1225,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) sum += (v[i] && act[i]) ? b[i] : 0;
+    sum = wave_sum_dpp(sum);
   } else {
     // {first position, count, committee, committee start}
     // (ablation 64: the piece computed from its index -- 256 positions, wrong tallies -- so the
@@ -1303,8 +1320,8 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
       }
 #pragma unroll
       for (int k = 0; k < kOneLoads; ++k) lbits[k * 64 * kFusedWaves + tid] = pq[k];
-      c = wave_sum(c);
-      e = wave_sum(e);
+      c = wave_sum_dpp(c);
+      e = wave_sum_dpp(e);
       if (lane == 0) {
         xp[wave] = c;
         xe[wave] = e;
@@ -1338,7 +1355,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         t += (v0[j] ? pack64(qb[j].x, qb[j].y) : 0) + (v1[j] ? pack64(qb[j].z, qb[j].w) : 0);
-      ts = wave_sum(t);
+      ts = wave_sum_dpp(t);
       if (ci.ga != kManyAtt) {
         uint64_t v = 0;
 #pragma unroll
@@ -1348,7 +1365,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
           if (v1[j] && q + 1 < ci.nbits && ((by1[j] >> (7 - (uint32_t)((q + 1) & 7))) & 1))
             v += pack64(qb[j].z, qb[j].w);
         }
-        vs = wave_sum(v);
+        vs = wave_sum_dpp(v);
         g1 = ci.ga;
         if (wiw && lane == 0) one_win<PRO>(a, f, inst, ci.ga, vs, ts, win1);
       } else {  // several attestations of this committee: direct atomics per attestation
@@ -1365,7 +1382,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
             if (v0[j] && q < nbits && bit_at(bf, q)) v += pack64(qb[j].x, qb[j].y);
             if (v1[j] && q + 1 < nbits && bit_at(bf, q + 1)) v += pack64(qb[j].z, qb[j].w);
           }
-          v = wave_sum(v);
+          v = wave_sum_dpp(v);
           if (wiw && lane == 0) one_win<PRO>(a, f, inst, (uint32_t)ga, v, ts, f.att_win[inst * a.natt + ga]);
           if (lane < 2) {  // one instruction: lane 0 the total, lane 1 the vote
             uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + ga;
@@ -1411,8 +1428,10 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
       sum += (v0[j] && a0 ? b0 : 0) + (v1[j] && a1 ? b1 : 0);
     }
   }
-  sum = wave_sum(sum);
-  nm = wave_sum(nm);
+  if constexpr ((MODE & 32768) == 0) {  // (the quad path summed them above)
+    sum = wave_sum_dpp(sum);
+    nm = wave_sum_dpp(nm);
+  }
   if (lane == 0) {
     xg[wave] = g1;
     xt[wave] = ts;
@@ -1533,6 +1552,13 @@ PZ_FUSED_KERNEL(pz_epoch_fused_se16_b32_kernel, 1024 + 16384 + 32768 + 524288)
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_b32_kernel, 1280 + 16384 + 32768 + 524288)
 PZ_FUSED_KERNEL(pz_epoch_fused_se_b32_kernel, 1024 + 32768 + 524288)
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_b32_kernel, 1280 + 32768 + 524288)
+// ablations of the u32-offset kernels (tools/: variant (1 << 20) | x, output wrong for x != 0):
+// x = 1 no crosslink tallies, 2 no reward-bit lookups, 4 no balance store, 8 no start/end loads
+#define PZ_B32_ABL(X)                                                                   \
+  PZ_FUSED_KERNEL(pz_epoch_fused_se16_b32_a##X##_kernel, 1024 + 16384 + 32768 + 524288 + X) \
+  PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_b32_a##X##_kernel, 1280 + 16384 + 32768 + 524288 + X)
+PZ_B32_ABL(1) PZ_B32_ABL(2) PZ_B32_ABL(4) PZ_B32_ABL(8) PZ_B32_ABL(3) PZ_B32_ABL(7) PZ_B32_ABL(15)
+#undef PZ_B32_ABL
 // (A/B, variant 32768: the round-3 pair lanes)
 PZ_FUSED_KERNEL(pz_epoch_fused_se_pair_kernel, 1024)
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_pair_kernel, 1280)
@@ -1710,7 +1736,7 @@ __device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, con
       uint64_t t = 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) t += v[i] ? b[i] : 0;
-      const uint64_t ts = wave_sum(t);
+      const uint64_t ts = wave_sum_dpp(t);
       const int64_t qs = (int64_t)(g - cbase), last = (int64_t)nbits - 1;
       const int64_t qlo = qs < 0 ? 0 : qs > last ? last : qs;
       if (ga != kManyAtt) {
@@ -1721,7 +1747,7 @@ __device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, con
           const uint32_t by = ((x >> 3) == (qlo >> 3)) ? cb_.byA : cb_.byB;
           if (v[i] && (uint64_t)x < (uint64_t)nbits && ((by >> (7 - (uint32_t)(x & 7))) & 1)) vv += b[i];
         }
-        const uint64_t vs = wave_sum(vv);
+        const uint64_t vs = wave_sum_dpp(vv);
         if ((MODE & 131072) && lane == 0) one_win<false>(a, f, inst, ga, vs, ts, cb_.win1);
         if (lane < 2) {  // one instruction: lane 0 the total, lane 1 the vote
           uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + ga;
@@ -1741,7 +1767,7 @@ __device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, con
             const uint64_t x = (uint64_t)(qs + i);
             if (v[i] && x < nb2 && bit_at(bf, x)) vv += b[i];
           }
-          vv = wave_sum(vv);
+          vv = wave_sum_dpp(vv);
           if ((MODE & 131072) && lane == 0) one_win<false>(a, f, inst, (uint32_t)gk, vv, ts, f.att_win[inst * a.natt + gk]);
           if (lane < 2) {
             uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + gk;
@@ -1785,8 +1811,8 @@ __device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, con
     cb_ = nb;
     na = nna;
   }
-  sum = wave_sum(sum);
-  nm = wave_sum(nm);
+  sum = wave_sum_dpp(sum);
+  nm = wave_sum_dpp(nm);
   uint64_t* sc = a.scal + inst * kScal;
   if (lane == 0) {
     if (sum && !skip) atomicAdd((unsigned long long*)&sc[kNextBal], (unsigned long long)sum);
@@ -1927,23 +1953,25 @@ hipError_t launch_epoch_count(const EpochArgs& a, bool do_val, bool do_pop, bool
   return hipGetLastError();
 }
 
-// A stateRecalc's vote-cache leader pass and its epoch's count pass in ONE launch (the chain
-// engine, one rank): blocks [0, nlb) are the leader pass (votes_dev.h), the rest the count
-// pass's blocks.  The two read the same pre-reward balances and write disjoint buffers; the
-// leader blocks come first, so the walk's wait (their gathered totals) is not behind the count.
+// A stateRecalc's vote-cache tally and its epoch's count pass in ONE launch (the chain
+// engine, one rank): blocks [0, ntb) are the voter-major tally (votes_dev.h), the rest the
+// count pass's blocks.  The two read the same pre-reward balances and write disjoint buffers; the
+// tally blocks come first, so the walk's wait (their gathered totals) is not behind the count.
+static_assert(kVoteWordThreads == kThreads, "one block shape for both parts");
 extern "C" __global__ void __launch_bounds__(kThreads)
-pz_vote_leader_count_kernel(VoteIdArgs v, uint32_t nlb, EpochArgs a, CountGrid g) {
-  if (blockIdx.x < nlb)
-    vote_leader_body(v, nlb, blockIdx.x);
+pz_vote_words_count_kernel(VoteWordArgs v, uint32_t ntb, EpochArgs a, CountGrid g) {
+  if (blockIdx.x < ntb)
+    vote_words_body(v, ntb, blockIdx.x);
   else
-    count_body<0>(a, g, blockIdx.x - nlb);
+    count_body<0>(a, g, blockIdx.x - ntb);
 }
 
-hipError_t launch_vote_leader_count(const VoteIdArgs& v, const EpochArgs& a, hipStream_t s) {
+hipError_t launch_vote_words_count(const VoteWordArgs& v, const EpochArgs& a, hipStream_t s) {
   const CountGrid g = count_grid(a, true, true, true);
-  const uint32_t nlb = kLeaderWaves / 4;
-  const uint64_t blocks = nlb + g.nvb + g.npb + g.nxb;
-  hipLaunchKernelGGL(pz_vote_leader_count_kernel, dim3((uint32_t)blocks), dim3(kThreads), 0, s, v, nlb, a, g);
+  const uint32_t ntb = v.natt ? vote_word_blocks(v) : 0;
+  const uint64_t blocks = ntb + g.nvb + g.npb + g.nxb;
+  if (!blocks) return hipSuccess;
+  hipLaunchKernelGGL(pz_vote_words_count_kernel, dim3((uint32_t)blocks), dim3(kThreads), 0, s, v, ntb, a, g);
   return hipGetLastError();
 }
 
@@ -2011,7 +2039,7 @@ hipError_t launch_epoch_fwin(const EpochArgs& a, const FusedArgs& f, hipStream_t
 // wave with quad lanes -- the streaming pass off)
 static bool ablation_no_lastco() {
   return g_fused_variant && g_fused_variant != 4096 && g_fused_variant != 32768 && g_fused_variant != 65536 &&
-         g_fused_variant != 131072 && g_fused_variant != 262144;
+         g_fused_variant != 131072 && g_fused_variant != 262144 && (g_fused_variant >> 20) != 1;
 }
 
 static bool use_lds_form(const EpochArgs& a, const FusedArgs& f);
@@ -2080,6 +2108,18 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream
     const dim3 grid(a.ninst, (uint32_t)groups), block(64 * kFusedWaves);
 #define PZ_LAUNCH_B32(K) \
   hipLaunchKernelGGL(K, grid, block, 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt)
+    if ((variant >> 20) == 1 && f.se16) {  // tools/ ablations
+      switch (variant & 0xFFFF) {
+#define PZ_ABL(X)                                                                  \
+  case X:                                                                          \
+    if (f.lastco) PZ_LAUNCH_B32(pz_epoch_fused_lc_se16_b32_a##X##_kernel);         \
+    else PZ_LAUNCH_B32(pz_epoch_fused_se16_b32_a##X##_kernel);                     \
+    return hipGetLastError();
+        PZ_ABL(1) PZ_ABL(2) PZ_ABL(4) PZ_ABL(8) PZ_ABL(3) PZ_ABL(7) PZ_ABL(15)
+#undef PZ_ABL
+        default: break;
+      }
+    }
     if (f.se16 && f.lastco) PZ_LAUNCH_B32(pz_epoch_fused_lc_se16_b32_kernel);
     else if (f.se16) PZ_LAUNCH_B32(pz_epoch_fused_se16_b32_kernel);
     else if (f.lastco) PZ_LAUNCH_B32(pz_epoch_fused_lc_se_b32_kernel);

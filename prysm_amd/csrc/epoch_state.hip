@@ -789,7 +789,8 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
         for (uint64_t b = i0; b < i0 + Bp && st->natt; ++b)
           maxl = std::max<uint64_t>(maxl, h->boffs[b * st->natt + st->natt] - h->boffs[b * st->natt + st->natt - 1]);
         q.f.last_max = maxl;
-        if (!rc && st->natt && maxl <= kLastCoMaxBytes && s.np) {
+        // (PZ_EPOCH_NO_LASTCO, A/B: no gather; the stream looks each reward bit up)
+        if (!rc && st->natt && maxl <= kLastCoMaxBytes && s.np && !std::getenv("PZ_EPOCH_NO_LASTCO")) {
           q.f.lcw = (s.np + 31) / 32;
           rc = dalloc(s, &q.f.lastco, (size_t)Bp * q.f.lcw);
         }
@@ -880,6 +881,10 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
           if (bal32_bases(Bp, s.n, vals, base)) {
             rc = bal32_upload(s, q, vals, base, true);
             st->b32 = true;
+            // the u32-offset kernels look each reward bit up (co_index -> last bitfield) rather
+            // than read pre's position-order gather: 65,536 x 256 cold 85.5-87.1 -> 79.0-79.4 us
+            // (profiles/r04/epoch_cold_ab_r4i.txt; PZ_EPOCH_B32_LASTCO=1 keeps the gather, A/B)
+            if (!std::getenv("PZ_EPOCH_B32_LASTCO")) q.f.lastco = nullptr, q.f.lcw = 0;
           }
         }
       }

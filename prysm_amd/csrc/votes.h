@@ -17,50 +17,43 @@ struct VoteGatherSlots {
   uint32_t slot[kJustifySlots];
 };
 
-// The block engine's tally (chain.hip): natt attestations x their 64 signed parent hashes.
-struct VoteIdArgs {
-  const uint32_t* committee;
-  const uint64_t* coffs;
-  const uint32_t* att_comm;  // natt
-  const uint8_t* bits;       // CSR bitfields
-  const uint64_t* boffs;     // natt+1
-  const uint32_t* slots;     // natt x 64 vote-cache slots of the signed parent hashes
-  const uint64_t* skip;      // natt: bit j set = parent j equals an oblique parent hash
+// The block engine's tally (chain.hip), voter-major: bit j of bm[w * nval + v] says validator
+// lo + v has voted for the hash of vote-cache id 64 w + j.  An attestation's 64 signed parent
+// hashes are a handful of such words (the recent window's ids are consecutive), so one 64-bit
+// atomicOr per voter and word records its votes for every parent at once, and the voters that
+// are new for all of them (the usual case) add one wave-summed balance per parent.
+struct VoteWordArgs {
+  const uint32_t* committee;  // ShardAndCommittee member lists (CSR, global validator indices)
+  // natt records: {committee's first member offset, committee size k, bitfield byte offset,
+  // pair offset | pair count << 25}
+  const uint4* rec;
+  const uint4* pairs;         // {mask lo, mask hi, id word w, 0}: parents 64 w + j, j in mask
+  const uint8_t* bits;        // the bitfields, ceil(k / 8) bytes each
   uint64_t natt;
+  uint32_t chunks;            // waves per attestation: max over the flush of ceil(k / 256), >= 1
   const uint64_t* balance;
-  uint64_t nval;
-  uint32_t* bitmaps;
-  uint64_t words_per_slot;
-  uint64_t* totals;
-  uint8_t* present;  // per slot: the Go map has an entry
+  uint64_t nval;              // a validator-range shard: balance and bm columns hold [val_offset,
+  uint64_t val_offset;        //   val_offset + nval) of nval_global validators
+  uint64_t nval_global;
+  uint64_t* bm;
+  uint64_t* totals;           // per id: VoteTotalDeposit
+  uint8_t* present;           // per id: the Go map has an entry
   uint64_t* err;
-  uint32_t* ubits;   // per (slot, committee) group: union bitfield, cwords words (zero between flushes)
-  uint32_t* uflag;   // per group: touched in this flush (zero between flushes)
-  uint4* leader;     // the groups to tally (compact list, *nlead entries): {slot, committee,
-                     //   committee's first member offset, committee size}
-  uint32_t* nlead;       // zero when the flush starts (the previous flush's leader pass zeroed it)
-  uint32_t* nlead_next;  // the other counter: zeroed here for the next flush
-  uint64_t ncomm, cwords;
-  uint64_t val_offset;   // a validator-range shard: balance and bitmaps hold [val_offset, val_offset + nval)
-  uint64_t nval_global;  // of nval_global validators (0: nval, unsharded)
-  // non-null: the leader pass's last block to finish also does launch_vote_gather's work into
-  // gather_out (a stateRecalc's flush: one kernel boundary less on the walk's wait); `ticket`
-  // is a zero device word, left zero
+  // non-null: the last tally block to finish gathers the 64 justification totals and the panic
+  // flag into gather_out (pinned), then writes gather_out[kJustifySlots + 1] = gather_seq behind
+  // a system-scope release; `ticket` is a zero device word, left zero
   uint64_t* gather_out;
   uint32_t* ticket;
   VoteGatherSlots gq;
-  // gather_out[kJustifySlots + 1] is set to gather_seq last, behind a system-scope release, so
-  // that the host can poll the pinned words instead of sleeping in an event wait
   uint64_t gather_seq;
 };
-hipError_t launch_vote_ids(const VoteIdArgs& a, hipStream_t s);
-// Pass 1 alone (the per-item union); pass 2 then runs as launch_vote_leader_count (epoch.h).
-hipError_t launch_vote_union(const VoteIdArgs& a, hipStream_t s);
-// The same two passes with the queue arrays (att_comm, bits, boffs, slots, skip) in mapped
-// pinned host memory, read in place by a per-attestation union pass (no staging copy).
-hipError_t launch_vote_ids_direct(const VoteIdArgs& a, hipStream_t s);
-// The per-attestation union pass (as launch_vote_ids_direct) over device copies of the queue.
-hipError_t launch_vote_ids_att(const VoteIdArgs& a, hipStream_t s);
+constexpr uint32_t kVoteRecPairShift = 25;
+constexpr uint32_t kVoteWordThreads = 256;
+// Blocks of the tally part of a launch (4 waves each).
+inline uint32_t vote_word_blocks(const VoteWordArgs& a) {
+  return (uint32_t)((a.natt * a.chunks + 3) / 4);
+}
+hipError_t launch_vote_words(const VoteWordArgs& a, hipStream_t s);
 // Up to 6 copies from mapped pinned memory to device memory in ONE launch (16 B per lane; the
 // sources may be read up to 15 bytes past their ends, so a source buffer's capacity must cover
 // ceil16 of its bytes).

@@ -31,105 +31,18 @@ pz_vote_tally_kernel(VoteArgs a) {
              a.bitmaps + (uint64_t)slot * a.words_per_slot, a.totals + slot, a.err, a.val_offset, a.nval_global);
 }
 
-// The block engine's form: work item (attestation, j) for each of its 64 signed parent
-// hashes, read from the hash log ids the walk recorded; the vote-cache slot of every id is
-// resolved by the host when the id is logged.  No host-side grouping: pass 1 ORs each item's
-// bitfield into the union bitfield of its (slot, committee) group -- dedup makes the union
-// exact -- and elects the group's first item as its leader; pass 2 lets each leader tally the
-// union once and clear it.  (Tallying every item directly made up to 64 waves race on the
-// same voter words with atomics: 100 us per cycle instead of ~25.)
-// kUnionLanes lanes per item (a committee bitfield is at most a few words): 8 items a wave.
-constexpr uint32_t kUnionLanes = 8;
-extern "C" __global__ void __launch_bounds__(256)
-pz_vote_union_kernel(VoteIdArgs a) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t item = t / kUnionLanes;
-  const uint32_t sub = (uint32_t)(t % kUnionLanes);
-  const uint64_t att = item >> 6;
-  if (att >= a.natt) return;
-  // every load that depends only on the item first (one round trip), the skip test after
-  const uint64_t sk = a.skip[att];
-  const uint32_t slot = a.slots[item];
-  const uint32_t c = a.att_comm[att];
-  const uint64_t bb = a.boffs[att], nbytes = a.boffs[att + 1] - bb;  // the queue holds ceil(k/8) bytes
-  if ((sk >> (item & 63)) & 1) return;  // an oblique parent hash (core.go:313-320) is skipped
-  const uint64_t grp = (uint64_t)slot * a.ncomm + c;
-  const uint64_t cb = a.coffs[c], ce = a.coffs[c + 1];  // (with the bit loads below)
-  uint32_t* u = a.ubits + grp * a.cwords;
-  for (uint64_t w = sub; 4 * w < nbytes; w += kUnionLanes) {
-    uint32_t x = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (4 * w + q < nbytes) x |= (uint32_t)a.bits[bb + 4 * w + q] << (8 * q);
-    if (x) atomicOr(&u[w], x);
-  }
-  if (sub == 0) {
-    a.present[slot] = 1;  // the map entry exists (core.go:322-326)
-    // the leader's record carries what its pass needs, so that pass starts at the committee
-    if (atomicOr(&a.uflag[grp], 1u) == 0)
-      a.leader[atomicAdd(a.nlead, 1u)] = make_uint4(slot, c, (uint32_t)cb, (uint32_t)(ce - cb));
-  }
-}
+// The block engine's form (votes.h VoteWordArgs): voter-major, one wave per (attestation,
+// 256-member chunk), every signed parent hash of the attestation in one pass.  Round 3's form
+// (an item per (attestation, parent): a union pass ORing each item's bitfield into its (slot,
+// committee) group, then a leader pass tallying each group with one atomic per voter and
+// parent) took 7.6 + 22 us per stateRecalc flush at 65,536 validators
+// (profiles/r04/replay_kernels_r4h.txt), 64 atomics per voter where this takes one or two.
+extern "C" __global__ void __launch_bounds__(kVoteWordThreads)
+pz_vote_words_kernel(VoteWordArgs a) { vote_words_body(a, gridDim.x, blockIdx.x); }
 
-// A fixed grid of kLeaderWaves waves walks the compact leader list of pass 1.
-extern "C" __global__ void __launch_bounds__(256)
-pz_vote_leader_kernel(VoteIdArgs a) { vote_leader_body(a, gridDim.x, blockIdx.x); }
-
-// Pass 1 without a staging copy: the queue is read where the walk wrote it (pinned host memory,
-// mapped), one wave per attestation, so its bytes cross the host link once -- the 64 parent
-// slots (one coalesced 256-B load), the scalars, then the bitfield bytes (one byte per lane) --
-// instead of once into a device copy that 64 items then re-read.  Lane j ORs the bitfield into
-// the union of parent j's (slot, committee) group and elects the group's leader.
-extern "C" __global__ void __launch_bounds__(256)
-pz_vote_union_att_kernel(VoteIdArgs a) {
-  const uint64_t att = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (att >= a.natt) return;
-  const uint64_t sk = a.skip[att];
-  const uint32_t c = a.att_comm[att];
-  const uint64_t bb = a.boffs[att], nbytes = a.boffs[att + 1] - bb;
-  const uint32_t slot = a.slots[att * 64 + lane];
-  const uint64_t cb = a.coffs[c], ce = a.coffs[c + 1];
-  // an oblique parent hash (core.go:313-320) is skipped
-  const bool mine = !((sk >> lane) & 1) && slot != 0xFFFFFFFFu;
-  const uint64_t grp = (uint64_t)slot * a.ncomm + c;
-  uint32_t* u = a.ubits + grp * a.cwords;
-  for (uint64_t base = 0; base < nbytes; base += 64) {
-    const uint32_t byte = base + lane < nbytes ? (uint32_t)a.bits[bb + base + lane] : 0u;
-    const uint64_t nw = (std::min<uint64_t>(64, nbytes - base) + 3) / 4;
-    for (uint64_t w = 0; w < nw; ++w) {  // word w of this chunk: bytes 4w..4w+3, little-endian
-      const uint32_t x = (uint32_t)__shfl(byte, (int)(4 * w)) | ((uint32_t)__shfl(byte, (int)(4 * w + 1)) << 8) |
-                         ((uint32_t)__shfl(byte, (int)(4 * w + 2)) << 16) |
-                         ((uint32_t)__shfl(byte, (int)(4 * w + 3)) << 24);
-      if (mine && x) atomicOr(&u[base / 4 + w], x);
-    }
-  }
-  if (mine) {
-    a.present[slot] = 1;  // the map entry exists (core.go:322-326)
-    if (atomicOr(&a.uflag[grp], 1u) == 0)
-      a.leader[atomicAdd(a.nlead, 1u)] = make_uint4(slot, c, (uint32_t)cb, (uint32_t)(ce - cb));
-  }
-}
-
-hipError_t launch_vote_ids_att(const VoteIdArgs& a, hipStream_t s);
-hipError_t launch_vote_ids_direct(const VoteIdArgs& a, hipStream_t s) { return launch_vote_ids_att(a, s); }
-
-hipError_t launch_vote_union(const VoteIdArgs& a, hipStream_t s) {
+hipError_t launch_vote_words(const VoteWordArgs& a, hipStream_t s) {
   if (!a.natt) return hipSuccess;
-  const uint64_t uthreads = a.natt * 64 * kUnionLanes;
-  hipLaunchKernelGGL(pz_vote_union_kernel, dim3((uint32_t)((uthreads + 255) / 256)), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_vote_ids(const VoteIdArgs& a, hipStream_t s) {
-  if (!a.natt) return hipSuccess;
-  const uint64_t uthreads = a.natt * 64 * kUnionLanes;
-  hipLaunchKernelGGL(pz_vote_union_kernel, dim3((uint32_t)((uthreads + 255) / 256)), dim3(256), 0, s, a);
-  static const uint32_t lw = [] {  // tools/ A/B knob for the leader grid
-    const char* e = std::getenv("PZ_LEADER_WAVES");
-    return e ? (uint32_t)std::max(4L, std::atol(e)) : kLeaderWaves;
-  }();
-  hipLaunchKernelGGL(pz_vote_leader_kernel, dim3(lw / 4), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(pz_vote_words_kernel, dim3(vote_word_blocks(a)), dim3(kVoteWordThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -155,14 +68,6 @@ hipError_t launch_stage_h2d_segs(const StageSegs& g, hipStream_t s) {
   if (!mx || !g.nseg) return hipSuccess;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((mx + 255) / 256, 256);
   hipLaunchKernelGGL(pz_stage_h2d_segs_kernel, dim3(blocks, (uint32_t)g.nseg), dim3(256), 0, s, g);
-  return hipGetLastError();
-}
-
-hipError_t launch_vote_ids_att(const VoteIdArgs& a, hipStream_t s) {
-  if (!a.natt) return hipSuccess;
-  const uint64_t threads = a.natt * 64;
-  hipLaunchKernelGGL(pz_vote_union_att_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(pz_vote_leader_kernel, dim3(kLeaderWaves / 4), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -1,5 +1,6 @@
-// Device code of the vote-cache tally shared by votes.hip and epoch.hip (the leader pass also
-// runs inside pz_vote_leader_count_kernel, beside a stateRecalc's epoch count blocks).
+// Device code of the vote-cache tally shared by votes.hip and epoch.hip (the block engine's
+// voter-major pass also runs inside pz_vote_words_count_kernel, beside a stateRecalc's epoch
+// count blocks).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -49,105 +50,128 @@ __device__ __forceinline__ void tally_item(const uint32_t* __restrict__ committe
   }
 }
 
-// tally_item for a committee of at most 256 members (the chain's leaders): a lane's four
-// members go through each step together -- bits and member ids, then the voter words, then the
-// atomics, then the balances -- so a wave waits out four round trips, not four per member.
-// (The loop form waited them out member after member: 20 us per transition's leader pass.)
-__device__ __forceinline__ void tally_item_x4(const uint32_t* __restrict__ committee, uint64_t cb, uint64_t k,
-                                              const uint8_t* bf, uint64_t blen, const uint64_t* __restrict__ balance,
-                                              uint64_t nval, uint32_t* bm, uint64_t* total, uint64_t* errp,
-                                              uint64_t lo, uint64_t nval_global) {
-  if (!nval_global) nval_global = nval;
+// 64-bit sum over the wave by DPP (no LDS round trips), wave-uniform.  Every lane of the wave
+// must be active (lane 63 ends holding the total): call it in wave-uniform control flow.
+__device__ __forceinline__ uint64_t wsum64_dpp(uint64_t v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#define PZ_DPP_STEP(CTRL, RM)                                                                   \
+  {                                                                                             \
+    const uint32_t l2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, CTRL, RM, 0xf, false); \
+    const uint32_t h2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, CTRL, RM, 0xf, false); \
+    const uint64_t t = (((uint64_t)hi << 32) | lo) + (((uint64_t)h2 << 32) | l2);               \
+    lo = (uint32_t)t;                                                                           \
+    hi = (uint32_t)(t >> 32);                                                                   \
+  }
+  PZ_DPP_STEP(0xB1, 0xf)   // quad_perm 1,0,3,2
+  PZ_DPP_STEP(0x4E, 0xf)   // quad_perm 2,3,0,1
+  PZ_DPP_STEP(0x141, 0xf)  // row_half_mirror
+  PZ_DPP_STEP(0x140, 0xf)  // row_mirror
+  PZ_DPP_STEP(0x142, 0xa)  // row_bcast15 into rows 1 and 3
+  PZ_DPP_STEP(0x143, 0xc)  // row_bcast31 into rows 2 and 3
+#undef PZ_DPP_STEP
+  const uint32_t rl = (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
+  const uint32_t rh = (uint32_t)__builtin_amdgcn_readlane((int)hi, 63);
+  return ((uint64_t)rh << 32) | rl;
+}
+
+// One wave of the voter-major tally: members [256 chunk, 256 chunk + 256) of attestation
+// `att`'s committee (calculateBlockVoteCache, core.go:300-345, for all of its signed parent
+// hashes at once).  Lane l holds members l + 64 q; its bitfield bit and member id load
+// together, then the balances; then per id word of the attestation's parents one 64-bit
+// atomicOr per voter: the bits it returns clear are the parents this voter is new for.  When
+// every voter of the wave is new for all of the word's parents or for none (the usual cases),
+// each parent's VoteTotalDeposit gains the balance sum of the new ones (lane j adds it for
+// parent bit j); otherwise, per parent, the sum of the voters new for it.  Chunk 0 marks the
+// parents' map entries present (core.go:322-326).
+__device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t wid) {
   const int lane = threadIdx.x & 63;
-  uint32_t v[4], word[4];
-  uint64_t bal[4];
+  const uint64_t att = wid / a.chunks;
+  const uint32_t chunk = (uint32_t)(wid % a.chunks);
+  if (att >= a.natt) return;  // (wave-uniform)
+  const uint4 r = a.rec[att];
+  const uint32_t cb = r.x, k = r.y, boff = r.z;
+  const uint32_t poff = r.w & ((1u << kVoteRecPairShift) - 1), np = r.w >> kVoteRecPairShift;
+  const uint32_t i0 = chunk * 256;
+  if (chunk > 0 && i0 >= k) return;
+  const uint4 pr = (uint32_t)lane < np ? a.pairs[poff + lane] : make_uint4(0, 0, 0, 0);
+  uint32_t v[4], by[4];
   bool on[4];
-  uint64_t err = 0, add = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {  // bits and member ids
-    const uint64_t i = lane + 64 * q;
-    on[q] = false;
-    v[q] = 0;
-    if (i < k) {
-      if (i >= 8 * blen) {
-        err |= PZ_XLERR_BITFIELD;  // CheckBit would panic
-      } else if ((bf[i >> 3] >> (7 - (uint32_t)(i & 7))) & 1u) {
-        on[q] = true;
-        v[q] = committee[cb + i];
+  for (int q = 0; q < 4; ++q) {  // bit bytes and member ids together (one round trip)
+    const uint32_t i = i0 + lane + 64 * q;
+    by[q] = i < k ? a.bits[boff + (i >> 3)] : 0u;
+    v[q] = i < k ? a.committee[cb + i] : 0u;
+  }
+  uint64_t lv[4], bal[4], err = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t i = i0 + lane + 64 * q;
+    on[q] = i < k && ((by[q] >> (7 - (i & 7))) & 1u);
+    if (on[q] && v[q] >= a.nval_global) {  // validators[attesterIndex] would panic
+      err = 1;
+      on[q] = false;
+    }
+    lv[q] = (uint64_t)v[q] - a.val_offset;  // wraps huge below the range
+    if (on[q] && lv[q] >= a.nval) on[q] = false;  // another rank's validator
+    bal[q] = on[q] ? a.balance[lv[q]] : 0;
+  }
+  if (chunk == 0) {
+    for (uint32_t p = 0; p < np; ++p) {
+      const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)pr.z, (int)p);
+      const uint64_t mask = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)pr.y, (int)p) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)pr.x, (int)p);
+      if ((mask >> lane) & 1) a.present[64ull * w + lane] = 1;
+    }
+  }
+  for (uint32_t p = 0; p < np; ++p) {  // (wave-uniform loop)
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)pr.z, (int)p);
+    const uint64_t mask = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)pr.y, (int)p) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)pr.x, (int)p);
+    uint64_t* row = a.bm + (uint64_t)w * a.nval;
+    uint64_t nw[4], xs = 0;
+    bool uni = true;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      nw[q] = 0;
+      if (on[q]) {
+        const uint64_t old = atomicOr((unsigned long long*)&row[lv[q]], (unsigned long long)mask);
+        nw[q] = mask & ~old;
+      }
+      // all or nothing: a voter new for every parent of the word, or for none (the usual cases)
+      uni = uni && (nw[q] == 0 || nw[q] == mask);
+      xs += nw[q] == mask && on[q] ? bal[q] : 0;
+    }
+    if (__ballot(!uni) == 0) {
+      const uint64_t S = wsum64_dpp(xs);  // the balances of the voters new for every parent
+      if (S && ((mask >> lane) & 1)) atomicAdd((unsigned long long*)&a.totals[64ull * w + lane], (unsigned long long)S);
+    } else {
+      for (uint64_t m = mask; m; m &= m - 1) {  // (wave-uniform loop over the word's parents)
+        const int j = __builtin_ctzll(m);
+        uint64_t x = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x += ((nw[q] >> j) & 1) ? bal[q] : 0;
+        const uint64_t sj = wsum64_dpp(x);
+        if (lane == 0 && sj) atomicAdd((unsigned long long*)&a.totals[64ull * w + j], (unsigned long long)sj);
       }
     }
   }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {  // range checks, then the voter words
-    if (on[q] && v[q] >= nval_global) {
-      err |= PZ_XLERR_MEMBER;
-      on[q] = false;
-    }
-    const uint64_t lv = (uint64_t)v[q] - lo;
-    if (on[q] && lv >= nval) on[q] = false;  // another rank's validator
-    word[q] = on[q] ? bm[lv >> 5] : 0xFFFFFFFFu;
-    bal[q] = on[q] ? balance[lv] : 0;  // issued with the word: used only if the atomic sets the bit
-  }
-  uint32_t old[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {  // a bit already set is final; the atomic decides the rest
-    const uint64_t lv = (uint64_t)v[q] - lo;
-    const uint32_t m = 1u << (lv & 31);
-    old[q] = 0xFFFFFFFFu;
-    if (on[q] && !(word[q] & m)) old[q] = atomicOr(&bm[lv >> 5], m);
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint64_t lv = (uint64_t)v[q] - lo;
-    if (on[q] && !(old[q] & (1u << (lv & 31)))) add += bal[q];
-  }
-  add = wsum64(add);
-  const uint64_t e1 = __ballot(err != 0);
-  if (lane == 0) {
-    if (add) atomicAdd((unsigned long long*)total, (unsigned long long)add);
-    if (e1) atomicOr((unsigned long long*)errp, 1ull);
-  }
+  if (__ballot(err != 0) && lane == 0) atomicOr((unsigned long long*)a.err, 1ull);
 }
 
-// A fixed grid of kLeaderWaves waves walks the compact leader list of pass 1.
-constexpr uint32_t kLeaderWaves = 4096;  // 2048 / 4096 / 8192 A/B: profiles/r03/replay_leader_waves_r3m.txt
-// The leader pass over nblk blocks of 256 threads, as block `bid` (a kernel of its own, or the
-// first nblk blocks of a launch shared with other work: pz_vote_leader_count_kernel).
-__device__ __forceinline__ void vote_leader_body(const VoteIdArgs& a, uint32_t nblk, uint32_t bid) {
-  const uint32_t n = *a.nlead;
-  if (bid == 0 && threadIdx.x == 0) *a.nlead_next = 0;  // (no wave of this flush reads it)
-  const uint32_t waves = nblk * (blockDim.x >> 6);
-  for (uint32_t li = ((uint64_t)bid * blockDim.x + threadIdx.x) >> 6; li < n; li += waves) {
-    const uint4 rec = a.leader[li];  // {slot, committee, its first member, its size}
-    const uint32_t slot = rec.x, c = rec.y;
-    const uint64_t grp = (uint64_t)slot * a.ncomm + c;
-    uint32_t* u = a.ubits + grp * a.cwords;
-    const uint64_t cb = rec.z, k = rec.w;
-    if (k <= 256)
-      tally_item_x4(a.committee, cb, k, reinterpret_cast<const uint8_t*>(u), (k + 7) / 8, a.balance, a.nval,
-                    a.bitmaps + (uint64_t)slot * a.words_per_slot, a.totals + slot, a.err, a.val_offset, a.nval_global);
-    else
-      tally_item(a.committee, a.coffs, c, reinterpret_cast<const uint8_t*>(u), (k + 7) / 8, a.balance, a.nval,
-                 a.bitmaps + (uint64_t)slot * a.words_per_slot, a.totals + slot, a.err, a.val_offset, a.nval_global);
-    // leave the group empty for the next flush
-    for (uint64_t w = threadIdx.x & 63; w < a.cwords; w += 64) u[w] = 0;
-    if ((threadIdx.x & 63) == 0) a.uflag[grp] = 0;
-  }
+// The tally part of a launch: nblk blocks of 4 waves, this one `bid`.  With a.gather_out the
+// last block to finish gathers the justification totals (MI355X_MICROARCH.md's last-block
+// hand-off: every wave drains its atomics before the block barrier, one lane per block takes a
+// ticket, the block taking the last reads the totals with agent-scope loads -- they are only
+// written by device-scope atomics -- into the pinned output, the sequence word last).
+__device__ __forceinline__ void vote_words_body(const VoteWordArgs& a, uint32_t nblk, uint32_t bid) {
+  vote_words_wave(a, (uint64_t)bid * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (!a.gather_out) return;
-  // The fused gather (MI355X_MICROARCH.md's last-block hand-off): every wave drains its tally
-  // atomics before the block barrier, one lane per block takes a ticket, and the block that
-  // takes the last one reads the complete totals with agent-scope loads (they are only written
-  // by device-scope atomics) into the pinned output.  Only the blocks that had a leader take
-  // a ticket (wave w takes leaders w, w + waves, ...): 1,024 arrivals on one counter cost
-  // ~10 us, a transition's ~160 about 2 (the fan-in row of the guide's price list).
-  const uint32_t busy = n ? min(nblk, (n + (blockDim.x >> 6) - 1) / (blockDim.x >> 6)) : 1u;
-  if (bid >= busy) return;
   __shared__ uint32_t last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == busy - 1 ? 1u : 0u;
+    last = t == nblk - 1 ? 1u : 0u;
   }
   __syncthreads();
   if (!last) return;

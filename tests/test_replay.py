@@ -533,17 +533,15 @@ def test_gpu_sharded_chain_configs4_full_vs_c_port(world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path,union,epack", [("segments", "item", "copy"), ("segments", "att", "copy"),
-                                              ("packed", "item", "copy"), ("direct", "att", "direct")])
-def test_gpu_replay_vote_queue_paths_vs_c_port(path, union, epack, monkeypatch):
+@pytest.mark.parametrize("path,epack", [("segments", "copy"), ("packed", "copy"), ("direct", "direct")])
+def test_gpu_replay_vote_queue_paths_vs_c_port(path, epack, monkeypatch):
     """Every way a vote-cache flush reaches the device (PZ_VOTE_PATH: the walk's pinned queue
     arrays staged by one multi-segment copy -- the product --, round 3's packed arena, or read
-    in place by the per-attestation union pass) and both union passes (per item, per
-    attestation), over 2,000 blocks of the configs[4] chain (31 transitions, the two queues
-    alternating, carried over a call boundary) against the C restatement; the last case also
-    has the transitions' epoch kernels read their inputs in place (PZ_EPOCH_PACK=direct)."""
+    in place by the voter-major tally) over 2,000 blocks of the configs[4] chain (31
+    transitions, the two queues alternating, carried over a call boundary) against the C
+    restatement; the last case also has the transitions' epoch kernels read their inputs in
+    place (PZ_EPOCH_PACK=direct)."""
     monkeypatch.setenv("PZ_VOTE_PATH", path)
-    monkeypatch.setenv("PZ_VOTE_UNION", union)
     monkeypatch.setenv("PZ_EPOCH_PACK", epack)  # the transition's epoch inputs: staged copy or read in place
     from prysm_amd.blockchain import BeaconChain, serialize_blocks
     from replay_port_helpers import mismatches, port_replay

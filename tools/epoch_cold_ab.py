@@ -3,7 +3,7 @@ Rotates the timed steps over 4 distinct instance sets on one stream (bench.py's 
 form) for configs[2] (65,536 x 256) and the 1M x 16 shape, with pz_debug_set_fused_variant(v)
 for each v in VARIANTS, and prints the device ms per step.  An entry "v/64" runs variant v with
 PZ_EPOCH_BAL64 set (the u64 balance column instead of the product's u32 offsets; read at state
-creation)."""
+creation), "v/nl" with PZ_EPOCH_NO_LASTCO (no position-order reward-bit gather), "v/64/nl" both."""
 import os
 import sys
 import types
@@ -24,11 +24,13 @@ def main():
     for nval, ninst in ((65536, 256), (1 << 20, 16)):
         shuffled = casper.shuffle_indices(b"A" + bytes(31), np.arange(nval, dtype=np.uint32))
         for tag in VARIANTS:
-            v = int(tag.split("/")[0])
-            if tag.endswith("/64"):
-                os.environ["PZ_EPOCH_BAL64"] = "1"
-            else:
-                os.environ.pop("PZ_EPOCH_BAL64", None)
+            v, *flags = tag.split("/")
+            v = int(v)
+            for flag, env in (("64", "PZ_EPOCH_BAL64"), ("nl", "PZ_EPOCH_NO_LASTCO")):
+                if flag in flags:
+                    os.environ[env] = "1"
+                else:
+                    os.environ.pop(env, None)
             old = _lib.lib.dll.pz_debug_set_fused_variant(v)
             try:
                 r = bench.epoch_cold(args, torch, dev, nval, ninst, shuffled, "epoch65k" if nval == 65536 else "epoch1m")
