@@ -680,12 +680,11 @@ struct Engine {
   std::vector<H32> slot_hash;
   uint64_t cap = 0;
   // pending tally work: per queued attestation its committee's members, its bitfield and the
-  // vote-cache ids of its tallied signed parent hashes as id words and masks (votes.h
-  // VoteWordArgs).  The walk writes the queue straight into pinned memory: two queues, the walk
+  // vote-cache ids of its 64 signed parent hashes (votes.h VoteWordArgs).  The walk writes the queue straight into pinned memory: two queues, the walk
   // filling one while a flush's kernels may still read the other (RankDev::vq_ev).
   struct VoteQueue {
-    PinVec<uint4> rec;    // per attestation (votes.h VoteWordArgs.rec)
-    PinVec<uint4> pairs;  // its parents' id words and masks
+    PinVec<uint4> rec;        // per attestation (votes.h VoteWordArgs.rec)
+    PinVec<uint32_t> slots;   // its 64 parents' vote-cache ids
     PinVec<uint8_t> bits;
     uint32_t chunks = 1;  // max ceil(k / 256) over the queue
     bool busy = false;
@@ -964,17 +963,19 @@ using EpochPrep = std::function<EpochLaunch*()>;
 
 // How a flush reaches the device (PZ_VOTE_PATH, read per flush so that one test process can
 // run every path; A/B knob):
-//   segments (product)  the walk's pinned queue arrays copied into the device pack by ONE
-//                       multi-segment stage kernel, then the tally;
-//   packed              round 3: the queue memcpy'd into one pinned arena first, one stage copy;
-//   direct              no copy: the tally reads the pinned queue in place.
+//   direct (product)    no copy: the tally reads the walk's pinned queue in place (a 256-B
+//                       coalesced id load and the bitfield bytes per attestation wave);
+//   segments            the queue arrays copied into a device pack by ONE multi-segment stage
+//                       kernel, then the tally (one launch more per flush: 1-3 % slower,
+//                       profiles/r04/replay_ab_words_r4k.txt);
+//   packed              round 3: the queue memcpy'd into one pinned arena first, one stage copy.
 enum VotePath { kVoteSegments, kVotePacked, kVoteDirect };
 static VotePath vote_path() {
   const char* e = std::getenv("PZ_VOTE_PATH");
-  if (!e) return kVoteSegments;
+  if (!e) return kVoteDirect;
   if (!std::strcmp(e, "packed")) return kVotePacked;
-  if (!std::strcmp(e, "direct")) return kVoteDirect;
-  return kVoteSegments;
+  if (!std::strcmp(e, "segments")) return kVoteSegments;
+  return kVoteDirect;
 }
 
 static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, const EpochPrep* prep = nullptr) {
@@ -986,8 +987,8 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
   PhaseTimer pt(g.prof[kProfFlush]);
   const uint64_t natt = Q.natt();
   auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
-  // the device pack: rec | pairs | bits
-  const size_t o_rec = 0, o_pairs = o_rec + natt * 16, o_bits = o_pairs + Q.pairs.size() * 16,
+  // the device pack: rec | slots | bits
+  const size_t o_rec = 0, o_slots = o_rec + natt * 16, o_bits = o_slots + natt * 64 * 4,
                total = staged ? o_bits + al(Q.bits.size()) : 0;
   if (path == kVotePacked) {
     if (g.q_arena_busy) {
@@ -998,7 +999,7 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
     check(g.q_arena.reserve(total));
     uint8_t* qa = g.q_arena.p;
     std::memcpy(qa + o_rec, Q.rec.data(), natt * 16);
-    if (Q.pairs.size()) std::memcpy(qa + o_pairs, Q.pairs.data(), Q.pairs.size() * 16);
+    std::memcpy(qa + o_slots, Q.slots.data(), natt * 64 * 4);
     if (Q.bits.size()) std::memcpy(qa + o_bits, Q.bits.data(), Q.bits.size());
   }
   each_rank(g, [&](RankDev& r) {
@@ -1026,7 +1027,7 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
         if (bytes) sg.seg[sg.nseg++] = StageSeg{src, r.d_qpack.p + off, (bytes + 15) / 16};
       };
       seg(Q.rec.dev(r.dev), o_rec, natt * 16);
-      seg(Q.pairs.dev(r.dev), o_pairs, Q.pairs.size() * 16);
+      seg(Q.slots.dev(r.dev), o_slots, natt * 64 * 4);
       seg(Q.bits.dev(r.dev), o_bits, Q.bits.size());
       hchk(launch_stage_h2d_segs(sg, r.s), "stage H2D");
     }
@@ -1043,11 +1044,11 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
     v.committee = r.committee.p;
     if (staged) {
       v.rec = reinterpret_cast<const uint4*>(r.d_qpack.p + o_rec);
-      v.pairs = reinterpret_cast<const uint4*>(r.d_qpack.p + o_pairs);
+      v.slots = reinterpret_cast<const uint32_t*>(r.d_qpack.p + o_slots);
       v.bits = r.d_qpack.p + o_bits;
     } else {  // read in place (pinned, mapped into this rank's device)
       v.rec = Q.rec.dev(r.dev);
-      v.pairs = Q.pairs.dev(r.dev);
+      v.slots = Q.slots.dev(r.dev);
       v.bits = Q.bits.dev(r.dev);
     }
     v.natt = natt;
@@ -1099,7 +1100,7 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
     N.busy = false;
   }
   N.rec.reset();
-  N.pairs.reset();
+  N.slots.reset();
   N.bits.reset();
   N.chunks = 1;
   return gather;
@@ -1323,64 +1324,34 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, AttLo
     std::memcpy(h.b, a.at(o.first), 32);
     if (const uint32_t* sl = g.slot_of.find(h)) match[nmatch++] = *sl;
   }
-  uint32_t slots[64];
+  Engine::VoteQueue& Q = g.vq[g.vq_cur];
+  // the 64 parents' vote-cache ids, UINT32_MAX where a parent is not tallied (the device groups
+  // them by id word, votes_dev.h)
+  uint32_t* slots = Q.slots.grow(64);
   for (size_t j = 0; j < 64; ++j) {
     const uint32_t sl = j < np ? g.id_slot[parents.id(g, j)] : UINT32_MAX;
-    slots[j] = sl;
     for (int m = 0; m < nmatch; ++m)
       if (sl == match[m]) skip |= 1ull << j;
+    slots[j] = ((skip >> j) & 1) ? UINT32_MAX : sl;
   }
-  if (skip == ~0ull) return;  // no map access at all
-  if (g.A->cache_nil) throw Panic{"assignment to entry in nil map (core.go:323)"};
+  if (skip == ~0ull) {  // no map access at all
+    Q.slots.resize(Q.slots.size() - 64);
+    return;
+  }
+  if (g.A->cache_nil) {
+    Q.slots.resize(Q.slots.size() - 64);
+    throw Panic{"assignment to entry in nil map (core.go:323)"};
+  }
   // the member loop reaches CheckBit(bitfield, 8 * len) when the committee is longer
-  if (k > 8ull * a.bf_len) throw Panic{"calculateBlockVoteCache: CheckBit index out of range (core.go:330)"};
-  // the tallied parents as id words and masks (votes.h VoteWordArgs): a parent listed twice
-  // is one bit (its voters are counted once, as the Go loop's voter scan does).  The recent
-  // window's ids are consecutive, so the usual attestation spans two id words: branch-free
-  // loops for that case, a search for the rest.
-  uint32_t lo = UINT32_MAX, hi = 0;
-  for (size_t j = 0; j < 64; ++j) {
-    const uint32_t sl = slots[j];
-    const bool ok = sl != UINT32_MAX && !((skip >> j) & 1);
-    lo = ok && sl < lo ? sl : lo;
-    hi = ok && sl > hi ? sl : hi;
+  if (k > 8ull * a.bf_len) {
+    Q.slots.resize(Q.slots.size() - 64);
+    throw Panic{"calculateBlockVoteCache: CheckBit index out of range (core.go:330)"};
   }
-  uint32_t pw[64];
-  uint64_t pm[64];
-  uint32_t npr = 0;
-  if (lo != UINT32_MAX && (hi >> 6) <= (lo >> 6) + 1) {
-    const uint32_t w0 = lo >> 6;
-    uint64_t m0 = 0, m1 = 0;
-    for (size_t j = 0; j < 64; ++j) {
-      const uint32_t sl = slots[j];
-      const bool ok = sl != UINT32_MAX && !((skip >> j) & 1);
-      const uint32_t b = sl - (w0 << 6);  // < 128 when ok
-      const uint64_t bit = ok ? 1ull << (b & 63) : 0;
-      m0 |= b < 64 ? bit : 0;
-      m1 |= b < 64 ? 0 : bit;
-    }
-    if (m0) pw[npr] = w0, pm[npr++] = m0;
-    if (m1) pw[npr] = w0 + 1, pm[npr++] = m1;
-  } else if (lo != UINT32_MAX) {
-    for (size_t j = 0; j < 64; ++j) {
-      const uint32_t sl = slots[j];
-      if (sl == UINT32_MAX || ((skip >> j) & 1)) continue;
-      const uint32_t w = sl >> 6;
-      uint32_t x = 0;
-      while (x < npr && pw[x] != w) ++x;
-      if (x == npr) pw[npr] = w, pm[npr++] = 0;
-      pm[x] |= 1ull << (sl & 63);
-    }
-  }
-  Engine::VoteQueue& Q = g.vq[g.vq_cur];
-  const uint32_t poff = (uint32_t)Q.pairs.size();
-  uint4* pq = Q.pairs.grow(npr);
-  for (uint32_t x = 0; x < npr; ++x) pq[x] = make_uint4((uint32_t)pm[x], (uint32_t)(pm[x] >> 32), pw[x], 0);
   const uint32_t boff = (uint32_t)Q.bits.size();
   const uint8_t* bf = a.at(a.bf_off);
   const size_t nbf = (k + 7) / 8;
   if (nbf) std::memcpy(Q.bits.grow(nbf), bf, nbf);
-  Q.rec.push_back(make_uint4((uint32_t)g.h_coffs[c], (uint32_t)k, boff, poff | (npr << kVoteRecPairShift)));
+  Q.rec.push_back(make_uint4((uint32_t)g.h_coffs[c], (uint32_t)k, boff, 0));
   Q.chunks = std::max<uint32_t>(Q.chunks, (uint32_t)((k + 255) / 256));
   if (Q.natt() >= kFlushAtts || Q.bits.size() >= (1ull << 31))
     flush_votes_enqueue(g);  // bounds the queue (and its u32 offsets); no host wait

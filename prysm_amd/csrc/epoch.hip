@@ -982,9 +982,10 @@ __device__ __forceinline__ void one_tail(const EpochArgs& a, const FusedArgs& f,
 // w = f.att_win[g]: {shard (< nrec: the host takes the one-launch step only then), its record's
 // dynasty}.
 template <bool PRO>
+// d = a.dynasty[inst], loaded once by the caller (not behind the tallies).
 __device__ __forceinline__ void one_win(const EpochArgs& a, const FusedArgs& f, uint64_t inst, uint32_t g, uint64_t v,
-                                        uint64_t t, uint2 w) {
-  if (3ull * v >= 2ull * t && a.dynasty[inst] > (uint64_t)w.y) atomicMin(&a.winner[inst * a.nrec + w.x], g);
+                                        uint64_t t, uint2 w, uint64_t d) {
+  if (3ull * v >= 2ull * t && d > (uint64_t)w.y) atomicMin(&a.winner[inst * a.nrec + w.x], g);
   if (PRO) {  // (with a pre launch, pre zeroes the tallies)
     f.vote_next[inst * a.natt + g] = 0;
     f.total_next[inst * a.natt + g] = 0;
@@ -1023,6 +1024,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint64_t item = grp * kFusedWaves + wave;
+  const uint64_t dyn = a.dynasty[inst];  // (the winner rule's, issued with the first loads)
   uint64_t pop = 0, ferr = 0;
   if (!PRO) {
     pop = pre_ro[inst * kPre];
@@ -1156,7 +1158,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
         }
         vs = wave_sum_dpp(vv);
         g1 = ci.ga;
-        if (wiw && lane == 0) one_win<false>(a, f, inst, ci.ga, vs, ts, win1);
+        if (wiw && lane == 0) one_win<false>(a, f, inst, ci.ga, vs, ts, win1, dyn);
       } else {  // several attestations of this committee: direct atomics per attestation
         const uint32_t* co = catt_offs_ro + inst * (f.ncomm + 1);
         for (uint32_t k = co[it.z]; k < co[it.z + 1]; ++k) {
@@ -1171,7 +1173,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
             if (v[i] && x < nbits && bit_at(bf, x)) vv += b[i];
           }
           vv = wave_sum_dpp(vv);
-          if (wiw && lane == 0) one_win<false>(a, f, inst, (uint32_t)ga, vv, ts, f.att_win[inst * a.natt + ga]);
+          if (wiw && lane == 0) one_win<false>(a, f, inst, (uint32_t)ga, vv, ts, f.att_win[inst * a.natt + ga], dyn);
           if (lane < 2) {
             uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + ga;
             const uint64_t xx = lane ? vv : ts;
@@ -1367,7 +1369,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
         }
         vs = wave_sum_dpp(v);
         g1 = ci.ga;
-        if (wiw && lane == 0) one_win<PRO>(a, f, inst, ci.ga, vs, ts, win1);
+        if (wiw && lane == 0) one_win<PRO>(a, f, inst, ci.ga, vs, ts, win1, dyn);
       } else {  // several attestations of this committee: direct atomics per attestation
         const uint32_t* co = catt_offs_ro + inst * (f.ncomm + 1);
         for (uint32_t k = co[it.z]; k < co[it.z + 1]; ++k) {
@@ -1383,7 +1385,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
             if (v1[j] && q + 1 < nbits && bit_at(bf, q + 1)) v += pack64(qb[j].z, qb[j].w);
           }
           v = wave_sum_dpp(v);
-          if (wiw && lane == 0) one_win<PRO>(a, f, inst, (uint32_t)ga, v, ts, f.att_win[inst * a.natt + ga]);
+          if (wiw && lane == 0) one_win<PRO>(a, f, inst, (uint32_t)ga, v, ts, f.att_win[inst * a.natt + ga], dyn);
           if (lane < 2) {  // one instruction: lane 0 the total, lane 1 the vote
             uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + ga;
             const uint64_t x = lane ? v : ts;
@@ -1616,9 +1618,14 @@ __device__ __forceinline__ StreamB stream_load_b(const EpochArgs& a, const Fused
   const uint64_t p0 = (ws - a.val_offset) & ~3ull, p = p0 + 4ull * lane, g = a.val_offset + p;
   const bool any = g + 3 >= ws && g < we;
   const uint64_t pp = any ? p : p0;
-  const uint64_t* Bal = a.balance + inst * f.vstride;
-  y.qb0 = *reinterpret_cast<const uint4*>(Bal + pp);
-  y.qb1 = *reinterpret_cast<const uint4*>(Bal + pp + 2);
+  if (MODE & 524288) {  // u32 balance offsets (FusedArgs.bal32): one 16-B load
+    y.qb0 = *reinterpret_cast<const uint4*>(f.bal32 + inst * f.vstride + pp);
+    y.qb1 = make_uint4(0, 0, 0, 0);
+  } else {
+    const uint64_t* Bal = a.balance + inst * f.vstride;
+    y.qb0 = *reinterpret_cast<const uint4*>(Bal + pp);
+    y.qb1 = *reinterpret_cast<const uint4*>(Bal + pp + 2);
+  }
   y.se = ld16_nt(reinterpret_cast<const uint64_t*>(f.se16 + inst * f.vstride + pp));  // {start | end << 16}
   const uint32_t ga = x.ic.w;
   // (MODE & 131072: the winners formed in the waves, FusedArgs.win_fused)
@@ -1683,6 +1690,9 @@ __device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, con
   const uint64_t d = a.dynasty[inst];
   const uint8_t* lastbf = a.bits + lb;
   uint64_t* Bal = a.balance + inst * f.vstride;
+  constexpr bool B32 = (MODE & 524288) != 0;
+  uint32_t* Bal32 = B32 ? f.bal32 + inst * f.vstride : nullptr;
+  const uint64_t bbase = B32 ? f.bal32_base[inst] : 0;
   uint64_t sum = 0, nm = 0;
   // pipeline: A(k+1) and B(k) in flight when piece k is processed; A(k+2) issued during it
   uint64_t item = item0;
@@ -1728,8 +1738,13 @@ __device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, con
     // the next piece's stream, then the one after's descriptor
     StreamB nb = stream_load_b<MODE>(a, f, inst, na, lane);
     const StreamA nna = stream_load_a<MODE>(f, items_ro, inst, item + 2 * stride, a.val_offset);
-    uint64_t b[4] = {pack64(cb_.qb0.x, cb_.qb0.y), pack64(cb_.qb0.z, cb_.qb0.w), pack64(cb_.qb1.x, cb_.qb1.y),
-                     pack64(cb_.qb1.z, cb_.qb1.w)};
+    uint64_t b[4];
+    if (B32) {  // u64 balance = base + offset (mod 2^64)
+      b[0] = bbase + cb_.qb0.x, b[1] = bbase + cb_.qb0.y, b[2] = bbase + cb_.qb0.z, b[3] = bbase + cb_.qb0.w;
+    } else {
+      b[0] = pack64(cb_.qb0.x, cb_.qb0.y), b[1] = pack64(cb_.qb0.z, cb_.qb0.w), b[2] = pack64(cb_.qb1.x, cb_.qb1.y),
+      b[3] = pack64(cb_.qb1.z, cb_.qb1.w);
+    }
     // crosslink tallies on the pre-reward balances (core.go:533-545)
     const uint32_t ga = ca.ic.w, nbits = ca.ic.z;
     if (ga != kNoAtt) {
@@ -1748,7 +1763,7 @@ __device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, con
           if (v[i] && (uint64_t)x < (uint64_t)nbits && ((by >> (7 - (uint32_t)(x & 7))) & 1)) vv += b[i];
         }
         const uint64_t vs = wave_sum_dpp(vv);
-        if ((MODE & 131072) && lane == 0) one_win<false>(a, f, inst, ga, vs, ts, cb_.win1);
+        if ((MODE & 131072) && lane == 0) one_win<false>(a, f, inst, ga, vs, ts, cb_.win1, d);
         if (lane < 2) {  // one instruction: lane 0 the total, lane 1 the vote
           uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + ga;
           const uint64_t xx = lane ? vs : ts;
@@ -1768,7 +1783,7 @@ __device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, con
             if (v[i] && x < nb2 && bit_at(bf, x)) vv += b[i];
           }
           vv = wave_sum_dpp(vv);
-          if ((MODE & 131072) && lane == 0) one_win<false>(a, f, inst, (uint32_t)gk, vv, ts, f.att_win[inst * a.natt + gk]);
+          if ((MODE & 131072) && lane == 0) one_win<false>(a, f, inst, (uint32_t)gk, vv, ts, f.att_win[inst * a.natt + gk], d);
           if (lane < 2) {
             uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + gk;
             const uint64_t xx = lane ? vv : ts;
@@ -1793,16 +1808,27 @@ __device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, con
                                     : ((rb[i] >> (7 - ((v[i] ? ci4[i] : 0u) & 7))) & 1);
         b[i] = r ? b[i] + PZ_ATTESTER_REWARD : b[i] - PZ_ATTESTER_REWARD;
       }
+      if (B32) {
+        if (v[0] && v[1] && v[2] && v[3]) {
+          *reinterpret_cast<uint4*>(Bal32 + p) = make_uint4((uint32_t)(b[0] - bbase), (uint32_t)(b[1] - bbase),
+                                                            (uint32_t)(b[2] - bbase), (uint32_t)(b[3] - bbase));
+        } else {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int i = 2 * h;
-        if (v[i] && v[i + 1])
-          *reinterpret_cast<uint4*>(Bal + p + i) =
-              make_uint4((uint32_t)b[i], (uint32_t)(b[i] >> 32), (uint32_t)b[i + 1], (uint32_t)(b[i + 1] >> 32));
-        else if (v[i])
-          Bal[p + i] = b[i];
-        else if (v[i + 1])
-          Bal[p + i + 1] = b[i + 1];
+          for (int i = 0; i < 4; ++i)
+            if (v[i]) Bal32[p + i] = (uint32_t)(b[i] - bbase);
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = 2 * h;
+          if (v[i] && v[i + 1])
+            *reinterpret_cast<uint4*>(Bal + p + i) =
+                make_uint4((uint32_t)b[i], (uint32_t)(b[i] >> 32), (uint32_t)b[i + 1], (uint32_t)(b[i + 1] >> 32));
+          else if (v[i])
+            Bal[p + i] = b[i];
+          else if (v[i + 1])
+            Bal[p + i + 1] = b[i + 1];
+        }
       }
     }
 #pragma unroll
@@ -1850,6 +1876,8 @@ PZ_STREAM_KERNEL(pz_epoch_stream_se16_win_kernel, 1024 + 16384 + 131072, 256)
 PZ_STREAM_KERNEL(pz_epoch_stream_lc_se16_win_kernel, 1280 + 16384 + 131072, 256)
 PZ_STREAM_KERNEL(pz_epoch_stream_lds_se16_kernel, 1024 + 16384 + 262144, 1024)
 PZ_STREAM_KERNEL(pz_epoch_stream_lds_se16_win_kernel, 1024 + 16384 + 131072 + 262144, 1024)
+PZ_STREAM_KERNEL(pz_epoch_stream_se16_b32_kernel, 1024 + 16384 + 524288, 256)  // u32 balance offsets
+PZ_STREAM_KERNEL(pz_epoch_stream_se16_b32_win_kernel, 1024 + 16384 + 131072 + 524288, 256)
 #undef PZ_STREAM_KERNEL
 
 // The single-launch step (one instance): no occupancy target (a few dozen blocks), so the
@@ -2086,10 +2114,11 @@ static uint64_t resident_waves(const void* kernel) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess || per < 1) per = 4;
   return (uint64_t)cus * (uint64_t)per * 4;
 }
-static uint32_t stream_blocks(uint64_t B, uint64_t nitems, bool lc) {
+static uint32_t stream_blocks(uint64_t B, uint64_t nitems, bool lc, bool b32 = false) {
   static const uint64_t res_plain = resident_waves((const void*)pz_epoch_stream_se16_kernel);
   static const uint64_t res_lc = resident_waves((const void*)pz_epoch_stream_lc_se16_kernel);
-  const uint64_t resident = lc ? res_lc : res_plain;
+  static const uint64_t res_b32 = resident_waves((const void*)pz_epoch_stream_se16_b32_win_kernel);
+  const uint64_t resident = b32 ? res_b32 : lc ? res_lc : res_plain;
   const uint64_t l = B % 4 == 0 ? B : B % 2 == 0 ? 2 * B : 4 * B;  // lcm(4, B)
   const uint64_t want = std::min<uint64_t>(resident, B * std::max<uint64_t>(1, nitems));
   const uint64_t W = std::max<uint64_t>(l, want / l * l);
@@ -2104,7 +2133,18 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream
   // accumulators, also on a rank whose range holds no piece
   const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
   const int variant = g_fused_variant;
-  if (f.bal32) {  // balances as u32 offsets: the quad kernels, instance-minor (no A/B variant applies)
+  if (f.bal32 && variant == 131072 && f.se16 && !f.lastco && a.ninst > 1) {
+    // (A/B) the streaming pass on the u32 offsets
+    const uint32_t nb = stream_blocks(a.ninst, f.nitems, false, true);
+    if (f.win_fused)
+      hipLaunchKernelGGL(pz_epoch_stream_se16_b32_win_kernel, dim3(nb), dim3(256), 0, s, a, f, f.pre, a.boffs,
+                         a.total_deposit, f.items, f.catt_offs, f.catt, 0u);
+    else
+      hipLaunchKernelGGL(pz_epoch_stream_se16_b32_kernel, dim3(nb), dim3(256), 0, s, a, f, f.pre, a.boffs,
+                         a.total_deposit, f.items, f.catt_offs, f.catt, 0u);
+    return hipGetLastError();
+  }
+  if (f.bal32) {  // balances as u32 offsets: the quad kernels, instance-minor
     const dim3 grid(a.ninst, (uint32_t)groups), block(64 * kFusedWaves);
 #define PZ_LAUNCH_B32(K) \
   hipLaunchKernelGGL(K, grid, block, 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt)

@@ -19,15 +19,13 @@ struct VoteGatherSlots {
 
 // The block engine's tally (chain.hip), voter-major: bit j of bm[w * nval + v] says validator
 // lo + v has voted for the hash of vote-cache id 64 w + j.  An attestation's 64 signed parent
-// hashes are a handful of such words (the recent window's ids are consecutive), so one 64-bit
-// atomicOr per voter and word records its votes for every parent at once, and the voters that
-// are new for all of them (the usual case) add one wave-summed balance per parent.
+// hashes fall in a handful of such words (the recent window's ids are consecutive), so one
+// 64-bit atomicOr per voter and word records its votes for all of those parents at once.
 struct VoteWordArgs {
   const uint32_t* committee;  // ShardAndCommittee member lists (CSR, global validator indices)
-  // natt records: {committee's first member offset, committee size k, bitfield byte offset,
-  // pair offset | pair count << 25}
-  const uint4* rec;
-  const uint4* pairs;         // {mask lo, mask hi, id word w, 0}: parents 64 w + j, j in mask
+  const uint4* rec;           // natt: {committee's first member offset, its size k, bitfield byte offset, 0}
+  const uint32_t* slots;      // natt x 64: the vote-cache id of each signed parent hash, or
+                              //   UINT32_MAX where the parent is not tallied (skipped, none)
   const uint8_t* bits;        // the bitfields, ceil(k / 8) bytes each
   uint64_t natt;
   uint32_t chunks;            // waves per attestation: max over the flush of ceil(k / 256), >= 1
@@ -47,7 +45,6 @@ struct VoteWordArgs {
   VoteGatherSlots gq;
   uint64_t gather_seq;
 };
-constexpr uint32_t kVoteRecPairShift = 25;
 constexpr uint32_t kVoteWordThreads = 256;
 // Blocks of the tally part of a launch (4 waves each).
 inline uint32_t vote_word_blocks(const VoteWordArgs& a) {

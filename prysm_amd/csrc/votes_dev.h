@@ -74,11 +74,30 @@ __device__ __forceinline__ uint64_t wsum64_dpp(uint64_t v) {
   return ((uint64_t)rh << 32) | rl;
 }
 
+// 64-bit OR over the wave by DPP, wave-uniform (every lane active; as wsum64_dpp).
+__device__ __forceinline__ uint64_t wor64_dpp(uint64_t v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#define PZ_DPP_STEP(CTRL, RM)                                                          \
+  lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, CTRL, RM, 0xf, false);       \
+  hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, CTRL, RM, 0xf, false);
+  PZ_DPP_STEP(0xB1, 0xf)
+  PZ_DPP_STEP(0x4E, 0xf)
+  PZ_DPP_STEP(0x141, 0xf)
+  PZ_DPP_STEP(0x140, 0xf)
+  PZ_DPP_STEP(0x142, 0xa)
+  PZ_DPP_STEP(0x143, 0xc)
+#undef PZ_DPP_STEP
+  const uint32_t rl = (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
+  const uint32_t rh = (uint32_t)__builtin_amdgcn_readlane((int)hi, 63);
+  return ((uint64_t)rh << 32) | rl;
+}
+
 // One wave of the voter-major tally: members [256 chunk, 256 chunk + 256) of attestation
 // `att`'s committee (calculateBlockVoteCache, core.go:300-345, for all of its signed parent
-// hashes at once).  Lane l holds members l + 64 q; its bitfield bit and member id load
-// together, then the balances; then per id word of the attestation's parents one 64-bit
-// atomicOr per voter: the bits it returns clear are the parents this voter is new for.  When
+// hashes at once).  Lane l holds members l + 64 q and parent l's id; the bitfield bits, member
+// ids and parent ids load together, then the balances.  The parents' ids are grouped by id
+// word (a ballot per word, the word's mask by a DPP OR); per word one 64-bit atomicOr per
+// voter, whose returned bits that were clear are the parents this voter is new for.  When
 // every voter of the wave is new for all of the word's parents or for none (the usual cases),
 // each parent's VoteTotalDeposit gains the balance sum of the new ones (lane j adds it for
 // parent bit j); otherwise, per parent, the sum of the voters new for it.  Chunk 0 marks the
@@ -90,10 +109,9 @@ __device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t 
   if (att >= a.natt) return;  // (wave-uniform)
   const uint4 r = a.rec[att];
   const uint32_t cb = r.x, k = r.y, boff = r.z;
-  const uint32_t poff = r.w & ((1u << kVoteRecPairShift) - 1), np = r.w >> kVoteRecPairShift;
   const uint32_t i0 = chunk * 256;
   if (chunk > 0 && i0 >= k) return;
-  const uint4 pr = (uint32_t)lane < np ? a.pairs[poff + lane] : make_uint4(0, 0, 0, 0);
+  const uint32_t sl = a.slots[att * 64 + lane];
   uint32_t v[4], by[4];
   bool on[4];
 #pragma unroll
@@ -115,18 +133,13 @@ __device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t 
     if (on[q] && lv[q] >= a.nval) on[q] = false;  // another rank's validator
     bal[q] = on[q] ? a.balance[lv[q]] : 0;
   }
-  if (chunk == 0) {
-    for (uint32_t p = 0; p < np; ++p) {
-      const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)pr.z, (int)p);
-      const uint64_t mask = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)pr.y, (int)p) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)pr.x, (int)p);
-      if ((mask >> lane) & 1) a.present[64ull * w + lane] = 1;
-    }
-  }
-  for (uint32_t p = 0; p < np; ++p) {  // (wave-uniform loop)
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)pr.z, (int)p);
-    const uint64_t mask = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)pr.y, (int)p) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane((int)pr.x, (int)p);
+  const bool ok = sl != 0xFFFFFFFFu;
+  if (chunk == 0 && ok) a.present[sl] = 1;
+  for (uint64_t pending = __ballot(ok); pending;) {  // (wave-uniform loop over the id words)
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)sl, (int)__builtin_ctzll(pending)) >> 6;
+    const bool in = ok && (sl >> 6) == w;
+    pending &= ~__ballot(in);
+    const uint64_t mask = wor64_dpp(in ? 1ull << (sl & 63) : 0);
     uint64_t* row = a.bm + (uint64_t)w * a.nval;
     uint64_t nw[4], xs = 0;
     bool uni = true;
