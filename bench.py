@@ -1210,7 +1210,7 @@ def shuffle_leg(args):
     return out
 
 
-PMC_DIR = os.path.join("profiles", "r03")
+PMC_DIR = os.path.join("profiles", "r04")
 PMC_SUMMARY = os.path.join(PMC_DIR, "pmc_main.json")
 
 

@@ -1133,8 +1133,15 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     const int64_t qhi = qs + 3 < 0 ? 0 : qs + 3 > last ? last : qs + 3;
     uint32_t byA = 0, byB = 0;
     if (!(MODE & 1) && ci.ga < kNoAtt && ci.nbits) {
-      byA = a.bits[ci.boff + ((uint64_t)qlo >> 3)];
-      byB = a.bits[ci.boff + ((uint64_t)qhi >> 3)];
+      // the lane's (at most two) bytes in ONE 8-B load from the dword below them (the bitfield
+      // buffer is padded by 16 B; bytes outside the bitfield are masked by x < nbits below)
+      (void)qhi;
+      const uint64_t bp = ci.boff + ((uint64_t)qlo >> 3), da = bp & ~3ull;
+      uint64_t win;
+      __builtin_memcpy(&win, __builtin_assume_aligned(a.bits + da, 4), 8);
+      const uint32_t sh = (uint32_t)(bp - da) * 8;
+      byA = (uint32_t)(win >> sh) & 0xFFu;
+      byB = (uint32_t)(win >> (sh + 8)) & 0xFFu;
     }
     uint64_t b[4];
     if (B32) {  // u64 balance = base + offset, wrapping as Go's uint64 does
@@ -1554,6 +1561,7 @@ PZ_FUSED_KERNEL(pz_epoch_fused_se16_b32_kernel, 1024 + 16384 + 32768 + 524288)
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_b32_kernel, 1280 + 16384 + 32768 + 524288)
 PZ_FUSED_KERNEL(pz_epoch_fused_se_b32_kernel, 1024 + 32768 + 524288)
 PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_b32_kernel, 1280 + 32768 + 524288)
+PZ_FUSED_KERNEL(pz_epoch_fused_se16_b32_xcd_kernel, 1024 + 16384 + 32768 + 524288 + 4096)  // (A/B: XCD-aware grid)
 // ablations of the u32-offset kernels (tools/: variant (1 << 20) | x, output wrong for x != 0):
 // x = 1 no crosslink tallies, 2 no reward-bit lookups, 4 no balance store, 8 no start/end loads
 #define PZ_B32_ABL(X)                                                                   \
@@ -2142,6 +2150,14 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream
     else
       hipLaunchKernelGGL(pz_epoch_stream_se16_b32_kernel, dim3(nb), dim3(256), 0, s, a, f, f.pre, a.boffs,
                          a.total_deposit, f.items, f.catt_offs, f.catt, 0u);
+    return hipGetLastError();
+  }
+  if (f.bal32 && variant == 4096 && f.se16 && !f.lastco) {
+    // (A/B) the XCD-aware 1-D grid: a piece group's blocks of every instance on one XCD, so its
+    // co_index words are fetched into one L2 instead of eight
+    const dim3 grid1((uint32_t)(((groups + 7) / 8) * 8 * a.ninst)), blk(64 * kFusedWaves);
+    hipLaunchKernelGGL(pz_epoch_fused_se16_b32_xcd_kernel, grid1, blk, 0, s, a, f, f.pre, a.boffs, a.total_deposit,
+                       f.items, f.cinfo, f.catt_offs, f.catt);
     return hipGetLastError();
   }
   if (f.bal32) {  // balances as u32 offsets: the quad kernels, instance-minor

@@ -116,6 +116,22 @@ def test_native_epoch_bal32_offsets(n, B, density):
     _check(ne, inst, steps=3)
 
 
+@pytest.mark.parametrize("variant", [131072, 4096])
+@pytest.mark.parametrize("n,B", [(65536, 5), (32768, 9), (4097, 3)])
+def test_native_epoch_bal32_forms(n, B, variant):
+    """The u32-offset step's A/B forms: the streaming pass (persistent pipelined waves, 131072)
+    and the XCD-aware grid (4096), with the winners in the waves: three steps against the
+    oracle."""
+    inst = _inst(n, B, False)
+    ne = NativeEpoch(inst, device=0)
+    assert ne.balance_bytes == 4
+    old = _lib.lib.dll.pz_debug_set_fused_variant(variant)
+    try:
+        _check(ne, inst, steps=3)
+    finally:
+        _lib.lib.dll.pz_debug_set_fused_variant(old)
+
+
 def test_native_epoch_bal32_rebase(monkeypatch):
     """The offsets re-based every 2 steps (PZ_EPOCH_B32_PERIOD; 2^29 in the product): five
     steps, each compared with the oracle."""

@@ -7,8 +7,9 @@ different shapes or cache states get their own run.
                  134 MB torch copy (the FETCH_SIZE yardstick)
   epoch65k       3 steps of the bench's configs[2] epoch (65,536 validators x 256 instances)
   epoch1m        3 steps of configs[3]'s size on one GPU (1,048,576 x 16)
-  epoch65k_cold  the configs[2] step rotated over 4 distinct instance sets (4 x 400 MB, far
-                 above the 256 MiB Infinity Cache): every step reads its set cold from HBM
+  epoch65k_cold  the configs[2] step rotated over 6 distinct instance sets (6 x 134 MB of
+                 streamed state with the u32 balance offsets, 3x the 256 MiB Infinity Cache):
+                 every step reads its set cold from HBM (bench.py's epoch.cold)
   epoch1m_cold   the same at 1,048,576 x 16
   epoch_single   20 steps of ONE 65,536-validator instance (the single-launch latency path)
 """
@@ -101,8 +102,8 @@ WORKLOADS = {
     "main": main_workload,
     "epoch65k": lambda: epoch(65536, 256, 1, 3),
     "epoch1m": lambda: epoch(1 << 20, 16, 1, 3),
-    "epoch65k_cold": lambda: epoch(65536, 256, 4, 2),
-    "epoch1m_cold": lambda: epoch(1 << 20, 16, 4, 2),
+    "epoch65k_cold": lambda: epoch(65536, 256, 6, 2),
+    "epoch1m_cold": lambda: epoch(1 << 20, 16, 6, 2),
     "epoch_single": lambda: epoch(65536, 1, 1, 20),
 }
 
