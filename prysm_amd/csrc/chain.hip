@@ -1328,11 +1328,18 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, AttLo
   // the 64 parents' vote-cache ids, UINT32_MAX where a parent is not tallied (the device groups
   // them by id word, votes_dev.h)
   uint32_t* slots = Q.slots.grow(64);
-  for (size_t j = 0; j < 64; ++j) {
-    const uint32_t sl = j < np ? g.id_slot[parents.id(g, j)] : UINT32_MAX;
-    for (int m = 0; m < nmatch; ++m)
-      if (sl == match[m]) skip |= 1ull << j;
-    slots[j] = ((skip >> j) & 1) ? UINT32_MAX : sl;
+  {
+    // (the trail's and the id table's base pointers hoisted: PinVec::operator[] is three
+    // dependent loads, and this loop runs 64 times per attestation)
+    const uint32_t* tr = g.trail.data() + parents.wstart;
+    const uint32_t* ids = g.id_slot.data();
+    const size_t nw = parents.nw;
+    for (size_t j = 0; j < 64; ++j) {
+      const uint32_t sl = j < nw ? ids[tr[j]] : j < np ? ids[parents.obl[j - nw]] : UINT32_MAX;
+      for (int m = 0; m < nmatch; ++m)
+        if (sl == match[m]) skip |= 1ull << j;
+      slots[j] = ((skip >> j) & 1) ? UINT32_MAX : sl;
+    }
   }
   if (skip == ~0ull) {  // no map access at all
     Q.slots.resize(Q.slots.size() - 64);
@@ -1691,7 +1698,13 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
     epoch_enqueue(g, *C, A->pending, &el, true);
     return &el;
   };
-  const bool gathered = flush_votes_enqueue(g, &q, one ? &prep : nullptr);
+  // The tally is launched first and the epoch packed while it runs (its count pass then a
+  // launch of its own): the pack's host time is off the justification loop's wait (totals_wait
+  // 3.5 -> 2.4 ms per 10,000 blocks, profiles/r04/replay_prep_ab_r4n.txt).  PZ_EPOCH_PREP=merged
+  // (A/B, read per transition): pack first, the count blocks inside the tally launch.
+  const char* pe = std::getenv("PZ_EPOCH_PREP");
+  const bool prep_after = !(pe && !std::strcmp(pe, "merged"));
+  const bool gathered = flush_votes_enqueue(g, &q, one && !prep_after ? &prep : nullptr);
   PhaseTimer pt(g.prof[kProfRecalc]);
   uint64_t streak = C->streak, justified = C->jslot, finalized = C->fslot;
   const uint64_t lsr = C->lsr;
