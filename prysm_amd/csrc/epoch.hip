@@ -969,6 +969,7 @@ __device__ __forceinline__ uint2 ld8_nt(const uint32_t* p) {
   return make_uint2(x.x, x.y);
 }
 
+template <int E = kFusedWaves>
 __device__ __forceinline__ void fused_block_end(const EpochArgs& a, const FusedArgs& f, const uint32_t* xg,
                                                 const uint64_t* xt, const uint64_t* xv, const uint64_t* xs,
                                                 const uint64_t* xn, uint64_t inst, uint64_t grp, int lane,
@@ -1460,19 +1461,22 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
 }
 
 // Wave 0 of a fused block: the block's tallies, next-cycle sum and per-instance scalars.
+// E: the block's tally entries, in piece order (one per wave, or two for the two-piece waves).
+template <int E>
 __device__ __forceinline__ void fused_block_end(const EpochArgs& a, const FusedArgs& f, const uint32_t* xg,
                                                 const uint64_t* xt, const uint64_t* xv, const uint64_t* xs,
                                                 const uint64_t* xn, uint64_t inst, uint64_t grp, int lane,
                                                 bool skip, bool applied, uint64_t pop, uint64_t ferr, bool rwd_err) {
   // Wave 0 adds the block's tallies: consecutive pieces of one committee are merged, and one
-  // atomic instruction carries every total (lanes 0-7) and vote (lanes 8-15).
-  if (lane < 2 * kFusedWaves) {
-    const int e = lane & (kFusedWaves - 1);
+  // atomic instruction carries every total (lanes 0 .. E-1) and vote (lanes E .. 2E-1).
+  static_assert((E & (E - 1)) == 0 && 2 * E <= 64, "entries: a power of two, two per lane at most");
+  if (lane < 2 * E) {
+    const int e = lane & (E - 1);
     const uint32_t g = xg[e];
     if (g < kNoAtt && (e == 0 || xg[e - 1] != g)) {  // head of a run of equal attestations
       uint64_t x = 0;
-      for (int k = e; k < kFusedWaves && xg[k] == g; ++k) x += lane < kFusedWaves ? xt[k] : xv[k];
-      uint64_t* dst = (lane < kFusedWaves ? a.total : a.vote) + inst * a.natt + g;
+      for (int k = e; k < E && xg[k] == g; ++k) x += lane < E ? xt[k] : xv[k];
+      uint64_t* dst = (lane < E ? a.total : a.vote) + inst * a.natt + g;
       if (x) atomicAdd((unsigned long long*)dst, (unsigned long long)x);
     }
   }
@@ -1537,6 +1541,185 @@ __device__ __forceinline__ void one_tail(const EpochArgs& a, const FusedArgs& f,
   __syncthreads();
   for (uint32_t r = tid; r < a.nrec; r += nt) a.winner[r] = wl[r];
   if (tid == 0) __hip_atomic_store(f.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Two pieces per wave (A/B, variant 1 << 21 on the u32-offset states): wave w of block (inst,
+// grp) takes pieces 16 grp + w and 16 grp + w + 8, their loads issued together -- both
+// descriptors, then both streams, then both pieces' reward-bit lookups -- so a wave has twice
+// the bytes in flight per dependent round trip; the block merges its 16 pieces' tallies as
+// the one-piece blocks merge 8.  Only the product's form: u32 offsets, 16-bit {start, end},
+// reward bits looked up (no `lastco`).
+constexpr int kPieces2 = 2 * kFusedWaves;
+__device__ __forceinline__ void quad2_body(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro,
+                                           const uint64_t* __restrict__ boffs_ro, const uint64_t* __restrict__ tdep_ro,
+                                           const uint4* __restrict__ items_ro, const uint32_t* __restrict__ catt_offs_ro,
+                                           const uint32_t* __restrict__ catt_ro) {
+  __shared__ uint64_t xt[kPieces2], xv[kPieces2], xs[kFusedWaves], xn[kFusedWaves];
+  __shared__ uint32_t xg[kPieces2];
+  const uint64_t inst = blockIdx.x, grp = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t dyn = a.dynasty[inst];
+  const uint64_t pop = pre_ro[inst * kPre], ferr = pre_ro[inst * kPre + 1];
+  const uint64_t lb = boffs_ro[inst * a.natt + a.natt - 1];
+  const uint64_t L = boffs_ro[inst * a.natt + a.natt] - lb;
+  const bool rwd_err = (a.nval_global - 1) >= 8 * L;  // CheckBit(last, N-1) panics (incentives.go:23)
+  const bool thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (tdep_ro[inst] * 2ull);  // incentives.go:18-20
+  const bool skip = ferr != 0 || (thr && rwd_err);
+  const bool applied = thr && !skip;
+  const bool wiw = f.win_fused != 0;
+  const uint64_t bbase = f.bal32_base[inst];
+  uint32_t* Bal32 = f.bal32 + inst * f.vstride;
+  const uint8_t* lastbf = a.bits + lb;
+  // phase A: both pieces' descriptors
+  uint4 it[2], ic[2];
+  uint64_t item[2];
+  bool have[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    item[k] = grp * kPieces2 + (uint64_t)wave + (uint64_t)k * kFusedWaves;
+    have[k] = item[k] < f.nitems;
+    it[k] = have[k] ? items_ro[item[k]] : make_uint4((uint32_t)a.val_offset, 0, 0, (uint32_t)a.val_offset);
+    ic[k] = have[k] ? f.items_ci[inst * f.nitems + item[k]] : make_uint4(0, 0, 0, kNoAtt);
+  }
+  // phase B: both streams, committee bytes, winner words
+  uint4 qb[2], se[2], cix[2];
+  uint2 win1[2];
+  uint32_t byA[2], byB[2];
+  uint64_t p[2], g[2];
+  int64_t qs[2], qlo[2];
+  bool v[2][4];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint64_t ws = it[k].x, we = (uint64_t)it[k].x + it[k].y, cb = it[k].w;
+    const uint64_t p0 = (ws - a.val_offset) & ~3ull;
+    p[k] = p0 + 4ull * lane;
+    g[k] = a.val_offset + p[k];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[k][i] = g[k] + i >= ws && g[k] + i < we;
+    const uint64_t pp = (v[k][0] || v[k][1] || v[k][2] || v[k][3]) ? p[k] : p0;
+    qb[k] = *reinterpret_cast<const uint4*>(Bal32 + pp);
+    se[k] = ld16_nt(reinterpret_cast<const uint64_t*>(f.se16 + inst * f.vstride + pp));
+    cix[k] = *reinterpret_cast<const uint4*>(a.co_index + pp);
+    const uint32_t ga = ic[k].w, nbits = ic[k].z;
+    win1[k] = (wiw && ga < kNoAtt) ? f.att_win[inst * a.natt + ga] : make_uint2(0, 0);
+    qs[k] = (int64_t)(g[k] - cb);
+    const int64_t last = (int64_t)nbits - 1;
+    qlo[k] = qs[k] < 0 ? 0 : qs[k] > last ? last : qs[k];
+    byA[k] = byB[k] = 0;
+    if (ga < kNoAtt && nbits) {
+      const uint64_t bp = pack64(ic[k].x, ic[k].y) + ((uint64_t)qlo[k] >> 3), da = bp & ~3ull;
+      uint64_t w8;
+      __builtin_memcpy(&w8, __builtin_assume_aligned(a.bits + da, 4), 8);
+      const uint32_t sh = (uint32_t)(bp - da) * 8;
+      byA[k] = (uint32_t)(w8 >> sh) & 0xFFu;
+      byB[k] = (uint32_t)(w8 >> (sh + 8)) & 0xFFu;
+    }
+  }
+  // phase C: both pieces' reward-bit bytes (dependent on their co_index words)
+  uint32_t rb[2][4];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint32_t c4[4] = {cix[k].x, cix[k].y, cix[k].z, cix[k].w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rb[k][i] = applied ? lastbf[(v[k][i] ? c4[i] : 0u) >> 3] : 0u;
+  }
+  // phase D: per piece, tallies on the pre-reward balances, classify, reward, store
+  uint64_t sum = 0;
+  bool off[4] = {false, false, false, false};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    uint64_t b[4] = {bbase + qb[k].x, bbase + qb[k].y, bbase + qb[k].z, bbase + qb[k].w};
+    const uint32_t ga = ic[k].w, nbits = ic[k].z;
+    uint64_t ts = 0, vs = 0;
+    uint32_t g1 = kNoAtt;
+    if (ga != kNoAtt) {  // (wave-uniform)
+      uint64_t t = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) t += v[k][i] ? b[i] : 0;
+      ts = wave_sum_dpp(t);
+      if (ga != kManyAtt) {
+        uint64_t vv = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t x = qs[k] + i;
+          const uint32_t by = ((x >> 3) == (qlo[k] >> 3)) ? byA[k] : byB[k];
+          if (v[k][i] && (uint64_t)x < (uint64_t)nbits && ((by >> (7 - (uint32_t)(x & 7))) & 1)) vv += b[i];
+        }
+        vs = wave_sum_dpp(vv);
+        g1 = ga;
+        if (wiw && lane == 0) one_win<false>(a, f, inst, ga, vs, ts, win1[k], dyn);
+      } else {  // several attestations of this committee: direct atomics per attestation
+        const uint32_t* co = catt_offs_ro + inst * (f.ncomm + 1);
+        for (uint32_t q = co[it[k].z]; q < co[it[k].z + 1]; ++q) {
+          const uint64_t gq = catt_ro[inst * a.natt + q];
+          const uint64_t boff = boffs_ro[inst * a.natt + gq];
+          const uint64_t nb = 8 * (boffs_ro[inst * a.natt + gq + 1] - boff);
+          uint64_t vv = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint64_t x = (uint64_t)(qs[k] + i);
+            if (v[k][i] && x < nb && bit_at(a.bits + boff, x)) vv += b[i];
+          }
+          vv = wave_sum_dpp(vv);
+          if (wiw && lane == 0) one_win<false>(a, f, inst, (uint32_t)gq, vv, ts, f.att_win[inst * a.natt + gq], dyn);
+          if (lane < 2) {
+            uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + gq;
+            const uint64_t xx = lane ? vv : ts;
+            if (xx) atomicAdd((unsigned long long*)dst, (unsigned long long)xx);
+          }
+        }
+      }
+    }
+    if (lane == 0) {
+      const int e = wave + k * kFusedWaves;
+      xg[e] = g1;
+      xt[e] = ts;
+      xv[e] = vs;
+    }
+    const uint32_t sw[4] = {se[k].x, se[k].y, se[k].z, se[k].w};
+    const uint32_t c4[4] = {cix[k].x, cix[k].y, cix[k].z, cix[k].w};
+    bool act[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      act[i] = (uint64_t)(sw[i] & 0xFFFFu) <= dyn && dyn < (uint64_t)(sw[i] >> 16);
+      off[i] = off[i] || (v[k][i] && !act[i]);
+    }
+    if (applied) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool r = (rb[k][i] >> (7 - ((v[k][i] ? c4[i] : 0u) & 7))) & 1;
+        b[i] = r ? b[i] + PZ_ATTESTER_REWARD : b[i] - PZ_ATTESTER_REWARD;
+      }
+      if (v[k][0] && v[k][1] && v[k][2] && v[k][3]) {
+        *reinterpret_cast<uint4*>(Bal32 + p[k]) = make_uint4((uint32_t)(b[0] - bbase), (uint32_t)(b[1] - bbase),
+                                                             (uint32_t)(b[2] - bbase), (uint32_t)(b[3] - bbase));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (v[k][i]) Bal32[p[k] + i] = (uint32_t)(b[i] - bbase);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sum += (v[k][i] && act[i]) ? b[i] : 0;
+  }
+  sum = wave_sum_dpp(sum);
+  const uint64_t nm = wave_count4(off);  // (a position counted once: the pieces are disjoint; nonzero only off the layout)
+  if (lane == 0) {
+    xs[wave] = sum;
+    xn[wave] = nm;
+  }
+  __syncthreads();
+  if (wave == 0) fused_block_end<kPieces2>(a, f, xg, xt, xv, xs, xn, inst, grp, lane, skip, applied, pop, ferr, rwd_err);
+}
+
+extern "C" __global__ void __launch_bounds__(64 * kFusedWaves) __attribute__((amdgpu_waves_per_eu(6, 6)))
+pz_epoch_fused_se16_b32_q2_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro,
+                                  const uint64_t* __restrict__ boffs_ro, const uint64_t* __restrict__ tdep_ro,
+                                  const uint4* __restrict__ items_ro, const FusedCommittee* __restrict__ cinfo_ro,
+                                  const uint32_t* __restrict__ catt_offs_ro, const uint32_t* __restrict__ catt_ro) {
+  (void)cinfo_ro;
+  quad2_body(a, f, pre_ro, boffs_ro, tdep_ro, items_ro, catt_offs_ro, catt_ro);
 }
 
 #define PZ_FUSED_KERNEL(NAME, MODE)                                                                       \
@@ -2075,7 +2258,8 @@ hipError_t launch_epoch_fwin(const EpochArgs& a, const FusedArgs& f, hipStream_t
 // wave with quad lanes -- the streaming pass off)
 static bool ablation_no_lastco() {
   return g_fused_variant && g_fused_variant != 4096 && g_fused_variant != 32768 && g_fused_variant != 65536 &&
-         g_fused_variant != 131072 && g_fused_variant != 262144 && (g_fused_variant >> 20) != 1;
+         g_fused_variant != 131072 && g_fused_variant != 262144 && (g_fused_variant >> 20) != 1 &&
+         g_fused_variant != (1 << 21);
 }
 
 static bool use_lds_form(const EpochArgs& a, const FusedArgs& f);
@@ -2150,6 +2334,12 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream
     else
       hipLaunchKernelGGL(pz_epoch_stream_se16_b32_kernel, dim3(nb), dim3(256), 0, s, a, f, f.pre, a.boffs,
                          a.total_deposit, f.items, f.catt_offs, f.catt, 0u);
+    return hipGetLastError();
+  }
+  if (f.bal32 && variant == (1 << 21) && f.se16 && !f.lastco) {  // (A/B) two pieces per wave
+    const uint64_t g2 = std::max<uint64_t>(1, (f.nitems + kPieces2 - 1) / kPieces2);
+    hipLaunchKernelGGL(pz_epoch_fused_se16_b32_q2_kernel, dim3(a.ninst, (uint32_t)g2), dim3(64 * kFusedWaves), 0, s, a,
+                       f, f.pre, a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt);
     return hipGetLastError();
   }
   if (f.bal32 && variant == 4096 && f.se16 && !f.lastco) {
