@@ -16,8 +16,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
+#include <ctime>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -762,7 +764,16 @@ struct Engine {
   PinBuf arena_pin;  // the call arena's bytes: parsed in place, H2D'd whole for the digest batch
   // wall-time accumulators (seconds) per phase, read by pz_debug_chain_profile
   double prof[kProfSlots] = {};
+  // per transition (tools/replay_timeline.py, correlated with a rocprofv3 kernel trace):
+  // CLOCK_MONOTONIC ns at the flush's start, after its tally launch returned, after the epoch's
+  // launches, and when the totals' sequence word was seen
+  std::vector<std::array<uint64_t, 4>> tl;
 };
+static uint64_t mono_ns() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
 
 // Accumulates the wall time of its scope into Engine::prof[slot].
 struct PhaseTimer {
@@ -1704,7 +1715,9 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   // (A/B, read per transition): pack first, the count blocks inside the tally launch.
   const char* pe = std::getenv("PZ_EPOCH_PREP");
   const bool prep_after = !(pe && !std::strcmp(pe, "merged"));
+  std::array<uint64_t, 4> tl{mono_ns(), 0, 0, 0};
   const bool gathered = flush_votes_enqueue(g, &q, one && !prep_after ? &prep : nullptr);
+  tl[1] = mono_ns();
   PhaseTimer pt(g.prof[kProfRecalc]);
   uint64_t streak = C->streak, justified = C->jslot, finalized = C->fslot;
   const uint64_t lsr = C->lsr;
@@ -1716,6 +1729,7 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   } else {
     epoch_enqueue(g, *C, A->pending);
   }
+  tl[2] = mono_ns();
   auto nc = std::make_shared<CState>();
   g.deferred.live = true;
   g.deferred.pending = A->pending;
@@ -1732,6 +1746,8 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   na->len = A->len;
   na->cache_nil = A->cache_nil;
   tally_gather_finish(g);
+  tl[3] = mono_ns();
+  if (g.tl.size() < (1u << 16)) g.tl.push_back(tl);
   std::memcpy(tot.data(), g.tot_pin.p, kCycle * 8);
   for (uint64_t i = 0; i < kCycle; ++i) {
     const uint64_t slot = lsr - kCycle + i;
@@ -3384,6 +3400,17 @@ extern "C" int pz_debug_chain_profile(pz_chain* c, double* out, int n) {
   if (!c || !out) return PZ_EINVAL;
   for (int i = 0; i < n && i < pz::chain::kProfSlots; ++i) out[i] = c->g.prof[i];
   return pz::chain::kProfSlots;
+}
+
+// Internal (tools/replay_timeline.py): up to n transitions' timestamps (4 u64 each, CLOCK_MONOTONIC
+// ns: flush start, tally launch returned, epoch launches returned, totals seen); returns the
+// count recorded since the chain was created (at most 65,536 are kept).
+extern "C" int pz_debug_chain_timeline(pz_chain* c, uint64_t* out, int n) {
+  if (!c || !out) return PZ_EINVAL;
+  const auto& tl = c->g.tl;
+  for (int i = 0; i < n && i < (int)tl.size(); ++i)
+    for (int k = 0; k < 4; ++k) out[4 * i + k] = tl[i][k];
+  return (int)tl.size();
 }
 
 // Internal (tests/, tools/; CPU-only: no device call): the block parser of
