@@ -311,9 +311,9 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                      "traffic_source": ("%s (every pz_epoch_* kernel of the %d x %d step)"
                                         % (pmc_summary_path(workload), nval, ninst)) if workload else None,
                      "traffic_frac": (traffic / (step_ms * 1e-3) / HBM_PEAK) if traffic else None,
-                     "kernel": ("epoch step: pz_epoch_pre (bit count) + pz_epoch_fused[_lc][_se] (one pass: classify, "
-                                "crosslink tallies, rewards, next-cycle sum) + pz_epoch_mid (winners); device "
-                                "time of the whole step" if one_pass else
+                     "kernel": ("epoch step: pz_epoch_pre (bit count, winner reset) + pz_epoch_fused_se16_b32 (one "
+                                "pass: classify, crosslink tallies, the winners in the waves, rewards on the u32 "
+                                "balance offsets, next-cycle sum); device time of the whole step" if one_pass else
                                 "epoch step (count+winner+compact+reward, device time of the whole step)"),
                      "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": local_units * bpv},

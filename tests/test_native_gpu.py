@@ -342,6 +342,18 @@ def test_native_epoch_committee_order_short_bitfield():
         np.testing.assert_array_equal(bal[0], k["balance"][0][ne.validators()])
 
 
+@pytest.mark.parametrize("ndev", [2, 8])
+def test_native_epoch_sharded_multi_device(ndev):
+    """configs[3]-shaped instances sharded over RCCL across ``ndev`` real GPUs of one process
+    (pz_init_devices), two steps against the oracle; skipped where fewer GPUs are visible."""
+    import torch
+    if torch.cuda.device_count() < ndev:
+        pytest.skip("needs %d GPUs" % ndev)
+    inst = _inst(1 << 20, 2, False)
+    ne = NativeEpoch(inst, device=0, comm=Comm.devices(ndev))
+    _check(ne, inst, steps=2)
+
+
 def test_native_epoch_rccl_world1():
     comm = Comm.devices(1)
     assert (comm.world, comm.nlocal) == (1, 1)

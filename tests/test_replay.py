@@ -489,6 +489,23 @@ def test_gpu_sharded_chain_matches_golden(world):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("ndev", [2, 8])
+def test_gpu_sharded_chain_multi_device_matches_golden(ndev):
+    """The golden chain over RCCL across ``ndev`` real GPUs of one process (pz_init_devices:
+    each rank's device state, pinned queue mappings and streams on its own device); skipped
+    where fewer GPUs are visible (the one-GPU test boxes; the 8-GPU node runs it)."""
+    import torch
+    if torch.cuda.device_count() < ndev:
+        pytest.skip("needs %d GPUs" % ndev)
+    from prysm_amd.blockchain import BeaconChain
+    from prysm_amd.native import Comm
+    g = golden()
+    ch = BeaconChain(g["nval"], comm=Comm.devices(ndev))
+    recs = ch.process_blocks(synth.chain_blocks(g["nval"], g["nblocks"], seed=g["seed"]))
+    _compare(recs, ch.roots(), g)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
 def test_gpu_sharded_chain_rejections_vs_oracle(world):
     from oracle import replay
