@@ -699,6 +699,7 @@ struct Engine {
   bool q_arena_busy = false;
   uint64_t ncomm = 0;
   std::vector<uint64_t> h_coffs;  // the committees' first member offsets (host copy)
+  uint32_t bf_stride = 4;         // the vote queue's bitfield row: >= every committee's bytes, x4
   PinBuf e_pin, e_pin_out;   // the epoch inputs' pinned staging; the results' pinned landing
   PinBuf tot_pin;            // the gathered justification totals (65 words; + a sequence word)
   uint64_t gather_seq = 0;   // the last sequence number the fused gather was asked to write
@@ -1063,6 +1064,7 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
       v.bits = Q.bits.dev(r.dev);
     }
     v.natt = natt;
+    v.bstride = g.bf_stride;
     v.chunks = Q.chunks;
     v.balance = r.balance.p;
     v.nval = r.n;
@@ -1365,11 +1367,13 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, AttLo
     Q.slots.resize(Q.slots.size() - 64);
     throw Panic{"calculateBlockVoteCache: CheckBit index out of range (core.go:330)"};
   }
-  const uint32_t boff = (uint32_t)Q.bits.size();
+  // the bitfield at a fixed stride (VoteWordArgs.bstride), the rest of its row zero
   const uint8_t* bf = a.at(a.bf_off);
   const size_t nbf = (k + 7) / 8;
-  if (nbf) std::memcpy(Q.bits.grow(nbf), bf, nbf);
-  Q.rec.push_back(make_uint4((uint32_t)g.h_coffs[c], (uint32_t)k, boff, 0));
+  uint8_t* row = Q.bits.grow(g.bf_stride);
+  if (nbf) std::memcpy(row, bf, nbf);
+  std::memset(row + nbf, 0, g.bf_stride - nbf);
+  Q.rec.push_back(make_uint4((uint32_t)g.h_coffs[c], (uint32_t)k, 0, 0));
   Q.chunks = std::max<uint32_t>(Q.chunks, (uint32_t)((k + 255) / 256));
   if (Q.natt() >= kFlushAtts || Q.bits.size() >= (1ull << 31))
     flush_votes_enqueue(g);  // bounds the queue (and its u32 offsets); no host wait
@@ -1901,6 +1905,9 @@ static void init_tail(Engine& g, const std::vector<uint32_t>& members, const std
   for (size_t c = 0; c + 1 < offs.size(); ++c) g.csize[c] = offs[c + 1] - offs[c];
   g.ncomm = g.csize.size();
   g.h_coffs = offs;
+  uint64_t kmax = 0;
+  for (uint64_t k : g.csize) kmax = std::max(kmax, k);
+  g.bf_stride = (uint32_t)std::max<uint64_t>(4, ((kmax + 7) / 8 + 3) & ~3ull);
   if (offs.back() >= (1ull << 32)) throw (int)fail(PZ_EINVAL, "committee lists above 2^32 members");
   // 64-aligned validator ranges, as pz_epoch_state / pz_comm_vote_tally split them
   const uint64_t span = 64 * std::max<uint64_t>(1, (n + 64ull * g.world - 1) / (64ull * g.world));

@@ -23,10 +23,12 @@ struct VoteGatherSlots {
 // 64-bit atomicOr per voter and word records its votes for all of those parents at once.
 struct VoteWordArgs {
   const uint32_t* committee;  // ShardAndCommittee member lists (CSR, global validator indices)
-  const uint4* rec;           // natt: {committee's first member offset, its size k, bitfield byte offset, 0}
+  const uint4* rec;           // natt: {committee's first member offset, its size k, 0, 0}
   const uint32_t* slots;      // natt x 64: the vote-cache id of each signed parent hash, or
                               //   UINT32_MAX where the parent is not tallied (skipped, none)
-  const uint8_t* bits;        // the bitfields, ceil(k / 8) bytes each
+  const uint8_t* bits;        // the bitfields, ceil(k / 8) bytes each, attestation a's at a * bstride
+  uint32_t bstride;           //   (a multiple of 4 >= every committee's ceil(k / 8): the bytes load
+                              //   beside the record, not behind it)
   uint64_t natt;
   uint32_t chunks;            // waves per attestation: max over the flush of ceil(k / 256), >= 1
   const uint64_t* balance;

@@ -107,17 +107,24 @@ __device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t 
   const uint64_t att = wid / a.chunks;
   const uint32_t chunk = (uint32_t)(wid % a.chunks);
   if (att >= a.natt) return;  // (wave-uniform)
+  // the record, the parents' slots and the bitfield bytes in one round trip (the bytes sit at a
+  // fixed stride: no record -> bitfield hop), then the member ids
   const uint4 r = a.rec[att];
-  const uint32_t cb = r.x, k = r.y, boff = r.z;
-  const uint32_t i0 = chunk * 256;
-  if (chunk > 0 && i0 >= k) return;
   const uint32_t sl = a.slots[att * 64 + lane];
-  uint32_t v[4], by[4];
+  const uint32_t i0 = chunk * 256;
+  uint32_t by[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t byte = (i0 + lane + 64 * q) >> 3;
+    by[q] = a.bits[(uint64_t)att * a.bstride + (byte < a.bstride ? byte : a.bstride - 1)];
+  }
+  const uint32_t cb = r.x, k = r.y;
+  if (chunk > 0 && i0 >= k) return;
+  uint32_t v[4];
   bool on[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {  // bit bytes and member ids together (one round trip)
+  for (int q = 0; q < 4; ++q) {
     const uint32_t i = i0 + lane + 64 * q;
-    by[q] = i < k ? a.bits[boff + (i >> 3)] : 0u;
     v[q] = i < k ? a.committee[cb + i] : 0u;
   }
   uint64_t lv[4], bal[4], err = 0;
