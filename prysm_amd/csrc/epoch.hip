@@ -1051,18 +1051,23 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
   __shared__ uint4 lbits[PRO ? kOneLoads * 64 * kFusedWaves : 1];
   const uint64_t pbeg = PRO ? boffs_ro[inst * a.natt] : 0, pend = PRO ? boffs_ro[inst * a.natt + a.natt] : 0,
                  pbase = pbeg & ~15ull;
+  // (the rounds the instance's bytes and attestations need: block-uniform, so the unused
+  // rounds of the capacity issue no loads)
+  const uint32_t nlr = PRO ? (uint32_t)((pend - pbase + 16 * 64 * kFusedWaves - 1) / (16 * 64 * kFusedWaves)) : 0;
+  const uint32_t nar = PRO ? (uint32_t)((a.natt + 64 * kFusedWaves - 1) / (64 * kFusedWaves)) : 0;
   if (PRO) {
 #pragma unroll
-    for (int k = 0; k < kOneLoads; ++k) {  // branch-free: the bitfield buffer is padded by 16 B
+    for (int k = 0; k < kOneLoads; ++k) {  // branch-free inside a round: the bitfield buffer is padded by 16 B
       const uint64_t u = pbase + 16ull * ((uint64_t)k * 64 * kFusedWaves + tid);
-      pq[k] = *reinterpret_cast<const uint4*>(a.bits + (u < pend ? u : pbase));
+      pq[k] = (uint32_t)k < nlr ? *reinterpret_cast<const uint4*>(a.bits + (u < pend ? u : pbase)) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int k = 0; k < kOneAtts; ++k) {
       const uint64_t g = (uint64_t)k * 64 * kFusedWaves + tid, gc = inst * a.natt + (g < a.natt ? g : 0);
-      ocs[k] = f.att_csize[gc];
-      ob0[k] = boffs_ro[gc];
-      ob1[k] = boffs_ro[gc + 1];
+      const bool r = (uint32_t)k < nar;
+      ocs[k] = r ? f.att_csize[gc] : 0u;
+      ob0[k] = r ? boffs_ro[gc] : 0;
+      ob1[k] = r ? boffs_ro[gc + 1] : 0;
     }
   }
   uint64_t sum = 0, nm = 0, ts = 0, vs = 0;
@@ -1329,7 +1334,8 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
         if (g < a.natt && ocs[k] > 8 * (ob1[k] - ob0[k])) e = 1;
       }
 #pragma unroll
-      for (int k = 0; k < kOneLoads; ++k) lbits[k * 64 * kFusedWaves + tid] = pq[k];
+      for (int k = 0; k < kOneLoads; ++k)
+        if ((uint32_t)k < nlr) lbits[k * 64 * kFusedWaves + tid] = pq[k];
       c = wave_sum_dpp(c);
       e = wave_sum_dpp(e);
       if (lane == 0) {

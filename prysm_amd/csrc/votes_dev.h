@@ -142,36 +142,57 @@ __device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t 
   }
   const bool ok = sl != 0xFFFFFFFFu;
   if (chunk == 0 && ok) a.present[sl] = 1;
-  for (uint64_t pending = __ballot(ok); pending;) {  // (wave-uniform loop over the id words)
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)sl, (int)__builtin_ctzll(pending)) >> 6;
-    const bool in = ok && (sl >> 6) == w;
-    pending &= ~__ballot(in);
-    const uint64_t mask = wor64_dpp(in ? 1ull << (sl & 63) : 0);
-    uint64_t* row = a.bm + (uint64_t)w * a.nval;
-    uint64_t nw[4], xs = 0;
-    bool uni = true;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      nw[q] = 0;
-      if (on[q]) {
-        const uint64_t old = atomicOr((unsigned long long*)&row[lv[q]], (unsigned long long)mask);
-        nw[q] = mask & ~old;
-      }
-      // all or nothing: a voter new for every parent of the word, or for none (the usual cases)
-      uni = uni && (nw[q] == 0 || nw[q] == mask);
-      xs += nw[q] == mask && on[q] ? bal[q] : 0;
+  // The parents' id words: the first two (the usual attestation spans two) have their atomics
+  // issued together, one round trip for both; any further word follows one at a time.
+  uint64_t pending = __ballot(ok);
+  for (int round = 0; pending; ++round) {  // (wave-uniform)
+    constexpr int kW = 2;
+    uint32_t wv[kW];
+    uint64_t mk[kW];
+    int nwd = 0;
+    for (; pending && nwd < (round == 0 ? kW : 1); ++nwd) {
+      const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)sl, (int)__builtin_ctzll(pending)) >> 6;
+      const bool in = ok && (sl >> 6) == w;
+      pending &= ~__ballot(in);
+      wv[nwd] = w;
+      mk[nwd] = wor64_dpp(in ? 1ull << (sl & 63) : 0);
     }
-    if (__ballot(!uni) == 0) {
-      const uint64_t S = wsum64_dpp(xs);  // the balances of the voters new for every parent
-      if (S && ((mask >> lane) & 1)) atomicAdd((unsigned long long*)&a.totals[64ull * w + lane], (unsigned long long)S);
-    } else {
-      for (uint64_t m = mask; m; m &= m - 1) {  // (wave-uniform loop over the word's parents)
-        const int j = __builtin_ctzll(m);
-        uint64_t x = 0;
+    uint64_t nw[kW][4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) x += ((nw[q] >> j) & 1) ? bal[q] : 0;
-        const uint64_t sj = wsum64_dpp(x);
-        if (lane == 0 && sj) atomicAdd((unsigned long long*)&a.totals[64ull * w + j], (unsigned long long)sj);
+    for (int d = 0; d < kW; ++d) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        nw[d][q] = 0;
+        if (d < nwd && on[q]) {
+          uint64_t* row = a.bm + (uint64_t)wv[d] * a.nval;
+          nw[d][q] = mk[d] & ~(uint64_t)atomicOr((unsigned long long*)&row[lv[q]], (unsigned long long)mk[d]);
+        }
+      }
+    }
+    for (int d = 0; d < nwd; ++d) {
+      const uint64_t mask = mk[d];
+      const uint32_t w = wv[d];
+      uint64_t xs = 0;
+      bool uni = true;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        // all or nothing: a voter new for every parent of the word, or for none (the usual cases)
+        uni = uni && (nw[d][q] == 0 || nw[d][q] == mask);
+        xs += nw[d][q] == mask && on[q] ? bal[q] : 0;
+      }
+      if (__ballot(!uni) == 0) {
+        const uint64_t S = wsum64_dpp(xs);  // the balances of the voters new for every parent
+        if (S && ((mask >> lane) & 1))
+          atomicAdd((unsigned long long*)&a.totals[64ull * w + lane], (unsigned long long)S);
+      } else {
+        for (uint64_t m = mask; m; m &= m - 1) {  // (wave-uniform loop over the word's parents)
+          const int j = __builtin_ctzll(m);
+          uint64_t x = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x += ((nw[d][q] >> j) & 1) ? bal[q] : 0;
+          const uint64_t sj = wsum64_dpp(x);
+          if (lane == 0 && sj) atomicAdd((unsigned long long*)&a.totals[64ull * w + j], (unsigned long long)sj);
+        }
       }
     }
   }
