@@ -97,11 +97,12 @@ __device__ __forceinline__ uint64_t wor64_dpp(uint64_t v) {
 // hashes at once).  Lane l holds members l + 64 q and parent l's id; the bitfield bits, member
 // ids and parent ids load together, then the balances.  The parents' ids are grouped by id
 // word (a ballot per word, the word's mask by a DPP OR); per word one 64-bit atomicOr per
-// voter, whose returned bits that were clear are the parents this voter is new for.  When
-// every voter of the wave is new for all of the word's parents or for none (the usual cases),
-// each parent's VoteTotalDeposit gains the balance sum of the new ones (lane j adds it for
-// parent bit j); otherwise, per parent, the sum of the voters new for it.  Chunk 0 marks the
-// parents' map entries present (core.go:322-326).
+// voter, whose returned bits that were clear are the parents this voter is new for.  With M
+// the parents any voter of the wave is new for: when every voter is new for all of M or for
+// none of it (the usual cases: a new voter, or a voter seen one block before, whose window has
+// moved by one parent), each of M's parents gains the new voters' balance sum (lane j adds it
+// for parent bit j); otherwise, per parent of M, the sum of the voters new for it.  Chunk 0
+// marks the parents' map entries present (core.go:322-326).
 __device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t wid) {
   const int lane = threadIdx.x & 63;
   const uint64_t att = wid / a.chunks;
@@ -170,22 +171,25 @@ __device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t 
       }
     }
     for (int d = 0; d < nwd; ++d) {
-      const uint64_t mask = mk[d];
       const uint32_t w = wv[d];
+      // M: the word's parents some voter of the wave is new for (a block's attestation usually
+      // brings one new parent for voters seen the block before, or all of them for new voters)
+      const uint64_t M = wor64_dpp(nw[d][0] | nw[d][1] | nw[d][2] | nw[d][3]);
+      if (!M) continue;  // (wave-uniform: nothing new)
       uint64_t xs = 0;
       bool uni = true;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        // all or nothing: a voter new for every parent of the word, or for none (the usual cases)
-        uni = uni && (nw[d][q] == 0 || nw[d][q] == mask);
-        xs += nw[d][q] == mask && on[q] ? bal[q] : 0;
+        // all or nothing: a voter new for every one of M's parents, or for none (the usual cases)
+        uni = uni && (nw[d][q] == 0 || nw[d][q] == M);
+        xs += nw[d][q] == M && on[q] ? bal[q] : 0;
       }
       if (__ballot(!uni) == 0) {
-        const uint64_t S = wsum64_dpp(xs);  // the balances of the voters new for every parent
-        if (S && ((mask >> lane) & 1))
+        const uint64_t S = wsum64_dpp(xs);  // the balances of the voters new for M's parents
+        if (S && ((M >> lane) & 1))
           atomicAdd((unsigned long long*)&a.totals[64ull * w + lane], (unsigned long long)S);
       } else {
-        for (uint64_t m = mask; m; m &= m - 1) {  // (wave-uniform loop over the word's parents)
+        for (uint64_t m = M; m; m &= m - 1) {  // (wave-uniform loop over the parents in M)
           const int j = __builtin_ctzll(m);
           uint64_t x = 0;
 #pragma unroll
