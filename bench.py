@@ -984,7 +984,8 @@ def replay_sharded_leg(args, torch, dist, dev, rank, world, comm):
 
 PROF_PHASES = ("parse", "digest_batch", "checks", "vote_queue", "vote_flush", "state_recalc", "msg_digests", "walk",
                "process", "count_atts", "flush_arena_wait", "msg_send", "msg_hash_log", "msg_wait",
-               "totals_wait", "poll_fallbacks")  # the last is a count (tally-total polls that fell back to the event wait)
+               "totals_wait", "poll_fallbacks", "vote_id_rows")  # the last two are counts (tally-total polls that
+#               fell back to the event wait; queued attestations whose parent ids needed an explicit row)
 
 
 def chain_phases_ms(ch):
@@ -992,13 +993,14 @@ def chain_phases_ms(ch):
     ones, checks and vote_queue, run only under PZ_CHAIN_PROFILE and read 0 here)."""
     import ctypes
     from prysm_amd import _lib
-    pv = (ctypes.c_double * 16)()
+    n = len(PROF_PHASES)
+    pv = (ctypes.c_double * n)()
     fn = _lib.lib.dll.pz_debug_chain_profile
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-    k = fn(ch._h, pv, 16)
-    out = {PROF_PHASES[i]: round(pv[i] * 1e3, 3) for i in range(min(k, len(PROF_PHASES) - 1)) if pv[i] > 0}
-    if k >= len(PROF_PHASES):
-        out["poll_fallbacks"] = int(pv[len(PROF_PHASES) - 1])  # always reported, 0 included
+    k = fn(ch._h, pv, n)
+    out = {PROF_PHASES[i]: round(pv[i] * 1e3, 3) for i in range(min(k, n - 2)) if pv[i] > 0}
+    for i in range(n - 2, min(k, n)):
+        out[PROF_PHASES[i]] = int(pv[i])  # the counts, always reported, 0 included
     return out
 
 

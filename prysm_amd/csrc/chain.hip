@@ -591,6 +591,7 @@ enum ProfSlot {
   kProfCount, kProfFlushWait, kProfMsgSend, kProfMsgLog, kProfMsgWait,
   kProfTotalsWait,    // the walk waiting for a transition's justification totals (inside state_recalc)
   kProfPollFallback,  // a count, not seconds: sequence-word polls that fell back to the event wait
+  kProfIdRows,        // a count: queued attestations whose parent ids are no run (an explicit id row)
   kProfSlots
 };
 
@@ -685,9 +686,9 @@ struct Engine {
   // vote-cache ids of its 64 signed parent hashes (votes.h VoteWordArgs).  The walk writes the queue straight into pinned memory: two queues, the walk
   // filling one while a flush's kernels may still read the other (RankDev::vq_ev).
   struct VoteQueue {
-    PinVec<uint4> rec;        // per attestation (votes.h VoteWordArgs.rec)
-    PinVec<uint32_t> slots;   // its 64 parents' vote-cache ids
-    PinVec<uint8_t> bits;
+    PinVec<VoteRec> rec;      // per attestation (votes.h VoteRec)
+    PinVec<uint32_t> slots;   // the explicit 64-id rows (kVoteIdsRow records)
+    PinVec<uint8_t> bits;     // the bitfield rows when they are not inline (bits_inline false)
     uint32_t chunks = 1;  // max ceil(k / 256) over the queue
     bool busy = false;
     size_t natt() const { return rec.size(); }
@@ -700,6 +701,8 @@ struct Engine {
   uint64_t ncomm = 0;
   std::vector<uint64_t> h_coffs;  // the committees' first member offsets (host copy)
   uint32_t bf_stride = 4;         // the vote queue's bitfield row: >= every committee's bytes, x4
+  bool bits_inline = true;        // every committee <= kVoteInlineBits: the bitfields ride in the records
+  bool ids_rows = false;          // (test knob) every attestation's ids in an explicit row
   PinBuf e_pin, e_pin_out;   // the epoch inputs' pinned staging; the results' pinned landing
   PinBuf tot_pin;            // the gathered justification totals (65 words; + a sequence word)
   uint64_t gather_seq = 0;   // the last sequence number the fused gather was asked to write
@@ -1000,7 +1003,7 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
   const uint64_t natt = Q.natt();
   auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
   // the device pack: rec | slots | bits
-  const size_t o_rec = 0, o_slots = o_rec + natt * 16, o_bits = o_slots + natt * 64 * 4,
+  const size_t o_rec = 0, o_slots = o_rec + natt * sizeof(VoteRec), o_bits = o_slots + al(Q.slots.size() * 4),
                total = staged ? o_bits + al(Q.bits.size()) : 0;
   if (path == kVotePacked) {
     if (g.q_arena_busy) {
@@ -1010,8 +1013,8 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
     }
     check(g.q_arena.reserve(total));
     uint8_t* qa = g.q_arena.p;
-    std::memcpy(qa + o_rec, Q.rec.data(), natt * 16);
-    std::memcpy(qa + o_slots, Q.slots.data(), natt * 64 * 4);
+    std::memcpy(qa + o_rec, Q.rec.data(), natt * sizeof(VoteRec));
+    if (Q.slots.size()) std::memcpy(qa + o_slots, Q.slots.data(), Q.slots.size() * 4);
     if (Q.bits.size()) std::memcpy(qa + o_bits, Q.bits.data(), Q.bits.size());
   }
   each_rank(g, [&](RankDev& r) {
@@ -1038,8 +1041,8 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
       auto seg = [&](const void* src, size_t off, size_t bytes) {
         if (bytes) sg.seg[sg.nseg++] = StageSeg{src, r.d_qpack.p + off, (bytes + 15) / 16};
       };
-      seg(Q.rec.dev(r.dev), o_rec, natt * 16);
-      seg(Q.slots.dev(r.dev), o_slots, natt * 64 * 4);
+      seg(Q.rec.dev(r.dev), o_rec, natt * sizeof(VoteRec));
+      seg(Q.slots.dev(r.dev), o_slots, Q.slots.size() * 4);
       seg(Q.bits.dev(r.dev), o_bits, Q.bits.size());
       hchk(launch_stage_h2d_segs(sg, r.s), "stage H2D");
     }
@@ -1055,13 +1058,13 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
     std::memset(&v, 0, sizeof v);
     v.committee = r.committee.p;
     if (staged) {
-      v.rec = reinterpret_cast<const uint4*>(r.d_qpack.p + o_rec);
+      v.rec = reinterpret_cast<const VoteRec*>(r.d_qpack.p + o_rec);
       v.slots = reinterpret_cast<const uint32_t*>(r.d_qpack.p + o_slots);
-      v.bits = r.d_qpack.p + o_bits;
+      v.bits = g.bits_inline ? nullptr : r.d_qpack.p + o_bits;
     } else {  // read in place (pinned, mapped into this rank's device)
       v.rec = Q.rec.dev(r.dev);
-      v.slots = Q.slots.dev(r.dev);
-      v.bits = Q.bits.dev(r.dev);
+      v.slots = Q.slots.size() ? Q.slots.dev(r.dev) : nullptr;
+      v.bits = g.bits_inline ? nullptr : Q.bits.dev(r.dev);
     }
     v.natt = natt;
     v.bstride = g.bf_stride;
@@ -1339,8 +1342,11 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, AttLo
   }
   Engine::VoteQueue& Q = g.vq[g.vq_cur];
   // the 64 parents' vote-cache ids, UINT32_MAX where a parent is not tallied (the device groups
-  // them by id word, votes_dev.h)
-  uint32_t* slots = Q.slots.grow(64);
+  // them by id word, votes_dev.h), and whether they make a run (votes.h VoteRec)
+  uint32_t slots[64];
+  uint64_t step = 0, absent = 0;
+  bool run = !g.ids_rows;
+  uint32_t s0 = UINT32_MAX, prev = 0;
   {
     // (the trail's and the id table's base pointers hoisted: PinVec::operator[] is three
     // dependent loads, and this loop runs 64 times per attestation)
@@ -1351,29 +1357,49 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, AttLo
       const uint32_t sl = j < nw ? ids[tr[j]] : j < np ? ids[parents.obl[j - nw]] : UINT32_MAX;
       for (int m = 0; m < nmatch; ++m)
         if (sl == match[m]) skip |= 1ull << j;
-      slots[j] = ((skip >> j) & 1) ? UINT32_MAX : sl;
+      if (((skip >> j) & 1) || sl == UINT32_MAX) {
+        slots[j] = UINT32_MAX;
+        absent |= 1ull << j;
+        continue;
+      }
+      slots[j] = sl;
+      if (s0 == UINT32_MAX) s0 = sl;
+      else if (sl == prev + 1) step |= 1ull << j;
+      else if (sl != prev) run = false;
+      prev = sl;
     }
   }
-  if (skip == ~0ull) {  // no map access at all
-    Q.slots.resize(Q.slots.size() - 64);
-    return;
-  }
-  if (g.A->cache_nil) {
-    Q.slots.resize(Q.slots.size() - 64);
-    throw Panic{"assignment to entry in nil map (core.go:323)"};
-  }
+  if (skip == ~0ull) return;  // no map access at all
+  if (g.A->cache_nil) throw Panic{"assignment to entry in nil map (core.go:323)"};
   // the member loop reaches CheckBit(bitfield, 8 * len) when the committee is longer
-  if (k > 8ull * a.bf_len) {
-    Q.slots.resize(Q.slots.size() - 64);
-    throw Panic{"calculateBlockVoteCache: CheckBit index out of range (core.go:330)"};
+  if (k > 8ull * a.bf_len) throw Panic{"calculateBlockVoteCache: CheckBit index out of range (core.go:330)"};
+  VoteRec* rec = Q.rec.grow(1);
+  rec->cb = (uint32_t)g.h_coffs[c];
+  rec->k = (uint32_t)k;
+  if (run) {
+    rec->s0 = s0;
+    rec->form = 0;
+    rec->step = step;
+    rec->absent = absent;
+  } else {
+    rec->s0 = (uint32_t)(Q.slots.size() / 64);
+    rec->form = kVoteIdsRow;
+    g.prof[kProfIdRows] += 1;
+    rec->step = rec->absent = 0;
+    std::memcpy(Q.slots.grow(64), slots, sizeof slots);
   }
-  // the bitfield at a fixed stride (VoteWordArgs.bstride), the rest of its row zero
   const uint8_t* bf = a.at(a.bf_off);
   const size_t nbf = (k + 7) / 8;
-  uint8_t* row = Q.bits.grow(g.bf_stride);
-  if (nbf) std::memcpy(row, bf, nbf);
-  std::memset(row + nbf, 0, g.bf_stride - nbf);
-  Q.rec.push_back(make_uint4((uint32_t)g.h_coffs[c], (uint32_t)k, 0, 0));
+  if (g.bits_inline) {  // (k <= 256: at most 32 bytes)
+    std::memset(rec->bits, 0, sizeof rec->bits);
+    if (nbf) std::memcpy(rec->bits, bf, nbf);
+  } else {
+    // the bitfield at a fixed stride (VoteWordArgs.bstride), the rest of its row zero
+    std::memset(rec->bits, 0, sizeof rec->bits);
+    uint8_t* row = Q.bits.grow(g.bf_stride);
+    if (nbf) std::memcpy(row, bf, nbf);
+    std::memset(row + nbf, 0, g.bf_stride - nbf);
+  }
   Q.chunks = std::max<uint32_t>(Q.chunks, (uint32_t)((k + 255) / 256));
   if (Q.natt() >= kFlushAtts || Q.bits.size() >= (1ull << 31))
     flush_votes_enqueue(g);  // bounds the queue (and its u32 offsets); no host wait
@@ -1908,6 +1934,12 @@ static void init_tail(Engine& g, const std::vector<uint32_t>& members, const std
   uint64_t kmax = 0;
   for (uint64_t k : g.csize) kmax = std::max(kmax, k);
   g.bf_stride = (uint32_t)std::max<uint64_t>(4, ((kmax + 7) / 8 + 3) & ~3ull);
+  // (A/B and test knobs: PZ_VOTE_BITS=rows keeps every bitfield in the row array, PZ_VOTE_IDS=rows
+  // every attestation's ids in an explicit row)
+  const char* vb = std::getenv("PZ_VOTE_BITS");
+  g.bits_inline = kmax <= kVoteInlineBits && !(vb && !std::strcmp(vb, "rows"));
+  const char* vi = std::getenv("PZ_VOTE_IDS");
+  g.ids_rows = vi && !std::strcmp(vi, "rows");
   if (offs.back() >= (1ull << 32)) throw (int)fail(PZ_EINVAL, "committee lists above 2^32 members");
   // 64-aligned validator ranges, as pz_epoch_state / pz_comm_vote_tally split them
   const uint64_t span = 64 * std::max<uint64_t>(1, (n + 64ull * g.world - 1) / (64ull * g.world));

@@ -21,14 +21,37 @@ struct VoteGatherSlots {
 // lo + v has voted for the hash of vote-cache id 64 w + j.  An attestation's 64 signed parent
 // hashes fall in a handful of such words (the recent window's ids are consecutive), so one
 // 64-bit atomicOr per voter and word records its votes for all of those parents at once.
+//
+// One queued attestation is one 64-B record, so that the wave tallying it reads all it needs
+// from the walk's pinned queue in ONE host-link request (round 4: a 16-B record, a 256-B id row
+// and the bitfield bytes were ~9 requests per wave, and the flush's waves queued on them).
+// The ids of its 64 signed parent hashes (UINT32_MAX where a parent is not tallied: skipped, or
+// none) are, for the usual attestation, a run: the recent window's ids are assigned in the order
+// the hashes first appear, a skipped slot repeating its predecessor's hash.  So a record gives
+// them as s0 (the first tallied parent's id) + step (bit j: parent j's id is the previous tallied
+// parent's + 1, else the same) + absent (bit j: parent j not tallied); any other attestation
+// keeps an explicit 64-id row and names it (kVoteIdsRow, s0 = the row).
+constexpr uint32_t kVoteIdsRow = 1;  // VoteRec.form: ids in slots[64 * s0, 64 * s0 + 64)
+struct alignas(64) VoteRec {
+  uint32_t cb, k;    // the committee's first member offset (CSR), its size
+  uint32_t s0;       // the first tallied parent's id (kVoteIdsRow: the id row)
+  uint32_t form;     // 0 or kVoteIdsRow
+  uint64_t step;     // (form 0) bit j: id(j) = id(previous tallied parent) + 1, else the same
+  uint64_t absent;   // (form 0) bit j: parent j not tallied
+  uint32_t bits[8];  // VoteWordArgs.bits == null: the bitfield's first 32 bytes (k <= 256), zero-padded
+};
+static_assert(sizeof(VoteRec) == 64, "one 64-B request per record");
+constexpr uint32_t kVoteInlineBits = 256;  // committees up to this size keep their bitfield inline
+
 struct VoteWordArgs {
   const uint32_t* committee;  // ShardAndCommittee member lists (CSR, global validator indices)
-  const uint4* rec;           // natt: {committee's first member offset, its size k, 0, 0}
-  const uint32_t* slots;      // natt x 64: the vote-cache id of each signed parent hash, or
-                              //   UINT32_MAX where the parent is not tallied (skipped, none)
-  const uint8_t* bits;        // the bitfields, ceil(k / 8) bytes each, attestation a's at a * bstride
-  uint32_t bstride;           //   (a multiple of 4 >= every committee's ceil(k / 8): the bytes load
-                              //   beside the record, not behind it)
+  const VoteRec* rec;         // natt records
+  const uint32_t* slots;      // the explicit id rows (kVoteIdsRow records)
+  const uint8_t* bits;        // null: every bitfield inline (every committee <= kVoteInlineBits);
+                              //   else every bitfield here, ceil(k / 8) bytes, attestation a's at
+                              //   a * bstride (a multiple of 4 >= every committee's ceil(k / 8):
+                              //   the bytes load beside the record, not behind it)
+  uint32_t bstride;
   uint64_t natt;
   uint32_t chunks;            // waves per attestation: max over the flush of ceil(k / 256), >= 1
   const uint64_t* balance;
@@ -47,10 +70,12 @@ struct VoteWordArgs {
   VoteGatherSlots gq;
   uint64_t gather_seq;
 };
-constexpr uint32_t kVoteWordThreads = 256;
-// Blocks of the tally part of a launch (4 waves each).
-inline uint32_t vote_word_blocks(const VoteWordArgs& a) {
-  return (uint32_t)((a.natt * a.chunks + 3) / 4);
+constexpr uint32_t kVoteWordThreads = 256;    // the tally blocks beside an epoch count pass
+constexpr uint32_t kVoteWordMaxThreads = 1024;  // pz_vote_words_kernel's blocks (PZ_VOTE_WAVES per block)
+// Blocks of the tally part of a launch (threads / 64 waves each).
+inline uint32_t vote_word_blocks(const VoteWordArgs& a, uint32_t threads = kVoteWordThreads) {
+  const uint64_t wpb = threads / 64;
+  return (uint32_t)((a.natt * a.chunks + wpb - 1) / wpb);
 }
 hipError_t launch_vote_words(const VoteWordArgs& a, hipStream_t s);
 // Up to 6 copies from mapped pinned memory to device memory in ONE launch (16 B per lane; the

@@ -37,12 +37,22 @@ pz_vote_tally_kernel(VoteArgs a) {
 // committee) group, then a leader pass tallying each group with one atomic per voter and
 // parent) took 7.6 + 22 us per stateRecalc flush at 65,536 validators
 // (profiles/r04/replay_kernels_r4h.txt), 64 atomics per voter where this takes one or two.
-extern "C" __global__ void __launch_bounds__(kVoteWordThreads)
+extern "C" __global__ void __launch_bounds__(kVoteWordMaxThreads)
 pz_vote_words_kernel(VoteWordArgs a) { vote_words_body(a, gridDim.x, blockIdx.x); }
+
+// Waves per tally block (PZ_VOTE_WAVES, A/B knob: 4, 8 or 16; default 16): more waves per block
+// sum more of the flush's totals in LDS before the device atomics.  (Read per launch, so that one
+// process can A/B it.)
+static uint32_t vote_word_threads() {
+  const char* e = std::getenv("PZ_VOTE_WAVES");
+  const int w = e ? std::atoi(e) : 16;
+  return (uint32_t)(w == 4 || w == 8 ? w : 16) * 64;
+}
 
 hipError_t launch_vote_words(const VoteWordArgs& a, hipStream_t s) {
   if (!a.natt) return hipSuccess;
-  hipLaunchKernelGGL(pz_vote_words_kernel, dim3(vote_word_blocks(a)), dim3(kVoteWordThreads), 0, s, a);
+  const uint32_t t = vote_word_threads();
+  hipLaunchKernelGGL(pz_vote_words_kernel, dim3(vote_word_blocks(a, t)), dim3(t), 0, s, a);
   return hipGetLastError();
 }
 

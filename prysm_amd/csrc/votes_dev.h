@@ -92,35 +92,79 @@ __device__ __forceinline__ uint64_t wor64_dpp(uint64_t v) {
   return ((uint64_t)rh << 32) | rl;
 }
 
+// A block's justification-total partial sums (LDS): up to kVoteLdsWords id words, one running sum
+// per parent.  Every wave of the flush adds to the same handful of totals (the transition's
+// window), and device-scope atomics on one address serialise (~12 ns each): summed per block
+// first, a flush issues one atomic per (block, parent) instead of one per (wave, parent).
+constexpr int kVoteLdsWords = 4;
+constexpr uint32_t kVoteLdsEmpty = 0xFFFFFFFFu;
+struct VoteLds {
+  uint32_t key[kVoteLdsWords];  // the id word of each slot, or kVoteLdsEmpty
+  unsigned long long acc[kVoteLdsWords][64];
+};
+
 // One wave of the voter-major tally: members [256 chunk, 256 chunk + 256) of attestation
 // `att`'s committee (calculateBlockVoteCache, core.go:300-345, for all of its signed parent
-// hashes at once).  Lane l holds members l + 64 q and parent l's id; the bitfield bits, member
-// ids and parent ids load together, then the balances.  The parents' ids are grouped by id
-// word (a ballot per word, the word's mask by a DPP OR); per word one 64-bit atomicOr per
-// voter, whose returned bits that were clear are the parents this voter is new for.  With M
-// the parents any voter of the wave is new for: when every voter is new for all of M or for
-// none of it (the usual cases: a new voter, or a voter seen one block before, whose window has
-// moved by one parent), each of M's parents gains the new voters' balance sum (lane j adds it
-// for parent bit j); otherwise, per parent of M, the sum of the voters new for it.  Chunk 0
-// marks the parents' map entries present (core.go:322-326).
-__device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t wid) {
+// hashes at once).  Lane l holds members l + 64 q and parent l's id; the record (votes.h VoteRec:
+// the bitfield, the parents' id run) loads in one request, then the member ids, then the
+// balances.  The parents' ids are grouped by id word (a ballot per word, the word's mask by a
+// DPP OR); per word one 64-bit atomicOr per voter, whose returned bits that were clear are the
+// parents this voter is new for.  With M the parents any voter of the wave is new for: when
+// every voter is new for all of M or for none of it (the usual cases: a new voter, or a voter
+// seen one block before, whose window has moved by one parent), each of M's parents gains the
+// new voters' balance sum (lane j adds it for parent bit j); otherwise, per parent of M, the sum
+// of the voters new for it.  The sums go to the block's LDS totals (L).  Chunk 0 marks the
+// parents' map entries present (core.go:322-326).
+// (tools/tally_probe.hip: with `tr` non-null each wave stamps its phases, draining its memory
+// operations first; the product passes none and the stamps compile away)
+#define PZ_VSTAMP(i)                                       \
+  if (tr) {                                                \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+    if ((threadIdx.x & 63) == 0) tr[i] = wall_clock64();   \
+  }
+__device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t wid, VoteLds* L,
+                                                uint64_t* tr = nullptr) {
   const int lane = threadIdx.x & 63;
   const uint64_t att = wid / a.chunks;
   const uint32_t chunk = (uint32_t)(wid % a.chunks);
   if (att >= a.natt) return;  // (wave-uniform)
-  // the record, the parents' slots and the bitfield bytes in one round trip (the bytes sit at a
-  // fixed stride: no record -> bitfield hop), then the member ids
-  const uint4 r = a.rec[att];
-  const uint32_t sl = a.slots[att * 64 + lane];
+  PZ_VSTAMP(0)
+  // The record in one 64-B request (lane l reads its 16-B piece l & 3; the pieces go wave-wide by
+  // readlane), beside it the bitfield bytes when they are not inline (a fixed stride: no record ->
+  // bitfield hop); then the member ids.
+  const uint4 pc = reinterpret_cast<const uint4*>(a.rec + att)[lane & 3];
   const uint32_t i0 = chunk * 256;
   uint32_t by[4];
+  if (a.bits) {  // (wave-uniform)
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t byte = (i0 + lane + 64 * q) >> 3;
-    by[q] = a.bits[(uint64_t)att * a.bstride + (byte < a.bstride ? byte : a.bstride - 1)];
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t byte = (i0 + lane + 64 * q) >> 3;
+      by[q] = a.bits[(uint64_t)att * a.bstride + (byte < a.bstride ? byte : a.bstride - 1)];
+    }
   }
-  const uint32_t cb = r.x, k = r.y;
+  auto rl = [](uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); };
+  const uint32_t cb = rl(pc.x, 0), k = rl(pc.y, 0), s0 = rl(pc.z, 0), form = rl(pc.w, 0);
+  PZ_VSTAMP(1)
   if (chunk > 0 && i0 >= k) return;
+  if (!a.bits) {
+    // member i = lane + 64 q (chunk 0): byte (lane >> 3) + 8 q = byte (lane >> 3) & 3 of word
+    // 2 q + (lane >> 5); the words are lanes 2 and 3's pieces
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int src = q < 2 ? 2 : 3;  // (words 0-3 are lane 2's piece, 4-7 lane 3's)
+      const uint32_t w0 = rl((q & 1) ? pc.z : pc.x, src), w1 = rl((q & 1) ? pc.w : pc.y, src);
+      const uint32_t w = (lane & 32) ? w1 : w0;
+      by[q] = w >> (8 * ((lane >> 3) & 3));
+    }
+  }
+  uint32_t sl;
+  if (form & kVoteIdsRow) {  // (wave-uniform) an explicit id row: one more round trip
+    sl = a.slots[(uint64_t)s0 * 64 + lane];
+  } else {
+    const uint64_t step = ((uint64_t)rl(pc.y, 1) << 32) | rl(pc.x, 1);
+    const uint64_t absent = ((uint64_t)rl(pc.w, 1) << 32) | rl(pc.z, 1);
+    sl = ((absent >> lane) & 1) ? 0xFFFFFFFFu : s0 + (uint32_t)__builtin_popcountll(step & (~0ull >> (63 - lane)));
+  }
   uint32_t v[4];
   bool on[4];
 #pragma unroll
@@ -128,6 +172,7 @@ __device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t 
     const uint32_t i = i0 + lane + 64 * q;
     v[q] = i < k ? a.committee[cb + i] : 0u;
   }
+  PZ_VSTAMP(2)
   uint64_t lv[4], bal[4], err = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -141,6 +186,7 @@ __device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t 
     if (on[q] && lv[q] >= a.nval) on[q] = false;  // another rank's validator
     bal[q] = on[q] ? a.balance[lv[q]] : 0;
   }
+  PZ_VSTAMP(3)
   const bool ok = sl != 0xFFFFFFFFu;
   if (chunk == 0 && ok) a.present[sl] = 1;
   // The parents' id words: the first two (the usual attestation spans two) have their atomics
@@ -170,12 +216,25 @@ __device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t 
         }
       }
     }
+    if (round == 0) PZ_VSTAMP(4)
     for (int d = 0; d < nwd; ++d) {
       const uint32_t w = wv[d];
       // M: the word's parents some voter of the wave is new for (a block's attestation usually
       // brings one new parent for voters seen the block before, or all of them for new voters)
       const uint64_t M = wor64_dpp(nw[d][0] | nw[d][1] | nw[d][2] | nw[d][3]);
       if (!M) continue;  // (wave-uniform: nothing new)
+      // the word's LDS slot (found or claimed by lane 0), or -1: the totals directly
+      int ls = -1;
+      if (lane == 0) {
+        for (int i = 0; i < kVoteLdsWords; ++i) {
+          const uint32_t o = atomicCAS(&L->key[i], kVoteLdsEmpty, w);
+          if (o == kVoteLdsEmpty || o == w) {
+            ls = i;
+            break;
+          }
+        }
+      }
+      ls = __builtin_amdgcn_readlane(ls, 0);
       uint64_t xs = 0;
       bool uni = true;
 #pragma unroll
@@ -186,8 +245,10 @@ __device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t 
       }
       if (__ballot(!uni) == 0) {
         const uint64_t S = wsum64_dpp(xs);  // the balances of the voters new for M's parents
-        if (S && ((M >> lane) & 1))
-          atomicAdd((unsigned long long*)&a.totals[64ull * w + lane], (unsigned long long)S);
+        if (S && ((M >> lane) & 1)) {
+          if (ls >= 0) atomicAdd(&L->acc[ls][lane], (unsigned long long)S);
+          else atomicAdd((unsigned long long*)&a.totals[64ull * w + lane], (unsigned long long)S);
+        }
       } else {
         for (uint64_t m = M; m; m &= m - 1) {  // (wave-uniform loop over the parents in M)
           const int j = __builtin_ctzll(m);
@@ -195,21 +256,40 @@ __device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t 
 #pragma unroll
           for (int q = 0; q < 4; ++q) x += ((nw[d][q] >> j) & 1) ? bal[q] : 0;
           const uint64_t sj = wsum64_dpp(x);
-          if (lane == 0 && sj) atomicAdd((unsigned long long*)&a.totals[64ull * w + j], (unsigned long long)sj);
+          if (lane == 0 && sj) {
+            if (ls >= 0) atomicAdd(&L->acc[ls][j], (unsigned long long)sj);
+            else atomicAdd((unsigned long long*)&a.totals[64ull * w + j], (unsigned long long)sj);
+          }
         }
       }
     }
   }
   if (__ballot(err != 0) && lane == 0) atomicOr((unsigned long long*)a.err, 1ull);
+  PZ_VSTAMP(5)
 }
 
-// The tally part of a launch: nblk blocks of 4 waves, this one `bid`.  With a.gather_out the
+// The tally part of a launch: nblk blocks of blockDim.x / 64 waves, this one `bid` (the block's
+// totals summed in LDS, then one device atomic per parent it added to).  With a.gather_out the
 // last block to finish gathers the justification totals (MI355X_MICROARCH.md's last-block
 // hand-off: every wave drains its atomics before the block barrier, one lane per block takes a
 // ticket, the block taking the last reads the totals with agent-scope loads -- they are only
 // written by device-scope atomics -- into the pinned output, the sequence word last).
-__device__ __forceinline__ void vote_words_body(const VoteWordArgs& a, uint32_t nblk, uint32_t bid) {
-  vote_words_wave(a, (uint64_t)bid * (blockDim.x >> 6) + (threadIdx.x >> 6));
+__device__ __forceinline__ void vote_words_body(const VoteWordArgs& a, uint32_t nblk, uint32_t bid,
+                                                uint64_t* trace = nullptr) {
+  __shared__ VoteLds L;
+  for (uint32_t t = threadIdx.x; t < kVoteLdsWords * 64; t += blockDim.x) L.acc[t >> 6][t & 63] = 0;
+  if (threadIdx.x < kVoteLdsWords) L.key[threadIdx.x] = kVoteLdsEmpty;
+  __syncthreads();
+  const uint64_t wid = (uint64_t)bid * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  uint64_t* tr = trace ? trace + wid * 8 : nullptr;
+  vote_words_wave(a, wid, &L, tr);
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < kVoteLdsWords * 64; t += blockDim.x) {
+    const uint32_t w = L.key[t >> 6];
+    const unsigned long long x = L.acc[t >> 6][t & 63];
+    if (w != kVoteLdsEmpty && x) atomicAdd((unsigned long long*)&a.totals[64ull * w + (t & 63)], x);
+  }
+  PZ_VSTAMP(6)
   if (!a.gather_out) return;
   __shared__ uint32_t last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -238,6 +318,8 @@ __device__ __forceinline__ void vote_words_body(const VoteWordArgs& a, uint32_t 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(&a.gather_out[kJustifySlots + 1], a.gather_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  PZ_VSTAMP(7)
 }
+#undef PZ_VSTAMP
 
 }  // namespace pz

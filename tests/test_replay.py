@@ -550,16 +550,23 @@ def test_gpu_sharded_chain_configs4_full_vs_c_port(world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path,epack", [("segments", "copy"), ("packed", "copy"), ("direct", "direct")])
-def test_gpu_replay_vote_queue_paths_vs_c_port(path, epack, monkeypatch):
+@pytest.mark.parametrize("path,epack,bits,ids", [("segments", "copy", "inline", "run"),
+                                                  ("packed", "copy", "rows", "rows"),
+                                                  ("direct", "direct", "inline", "run"),
+                                                  ("direct", "copy", "rows", "run"),
+                                                  ("direct", "copy", "inline", "rows")])
+def test_gpu_replay_vote_queue_paths_vs_c_port(path, epack, bits, ids, monkeypatch):
     """Every way a vote-cache flush reaches the device (PZ_VOTE_PATH: the walk's pinned queue
-    arrays staged by one multi-segment copy -- the product --, round 3's packed arena, or read
-    in place by the voter-major tally) over 2,000 blocks of the configs[4] chain (31
-    transitions, the two queues alternating, carried over a call boundary) against the C
-    restatement; the last case also has the transitions' epoch kernels read their inputs in
-    place (PZ_EPOCH_PACK=direct)."""
+    read in place by the voter-major tally -- the product --, its arrays staged by one
+    multi-segment copy, or round 3's packed arena) and every record form (votes.h VoteRec: the
+    bitfield inline or in the row array, PZ_VOTE_BITS; the parents' ids as a run or an explicit
+    row, PZ_VOTE_IDS) over 2,000 blocks of the configs[4] chain (31 transitions, the two queues
+    alternating, carried over a call boundary) against the C restatement; the direct/direct case
+    also has the transitions' epoch kernels read their inputs in place (PZ_EPOCH_PACK=direct)."""
     monkeypatch.setenv("PZ_VOTE_PATH", path)
     monkeypatch.setenv("PZ_EPOCH_PACK", epack)  # the transition's epoch inputs: staged copy or read in place
+    monkeypatch.setenv("PZ_VOTE_BITS", bits)  # (read when the chain is made)
+    monkeypatch.setenv("PZ_VOTE_IDS", ids)
     from prysm_amd.blockchain import BeaconChain, serialize_blocks
     from replay_port_helpers import mismatches, port_replay
     nval = 65536

@@ -33,7 +33,7 @@ def main():
     import ctypes
     names = ["parse", "digests1", "att_checks+msg", "vote_queue", "vote_flush", "state_recalc", "msg_digests",
              "walk(all)", "process(all)", "count_atts", "flush_arena_wait", "msg_send",
-             "msg_hash_log", "msg_wait", "totals_wait", "poll_fallbacks(count)"]
+             "msg_hash_log", "msg_wait", "totals_wait", "poll_fallbacks(count)", "vote_id_rows(count)"]
     # AB=VAR: alternate the environment variable VAR over the values AB_VALUES (default "0,1")
     # across the replays (an A/B of a per-call knob such as PZ_VOTE_PATH in one process); REPS
     # replays per value
@@ -59,10 +59,10 @@ def main():
         print("%sprocess_serialized %.3f s -> %.1f blocks/s (%d processed, %d attestations)"
               % ("[%s=%s] " % (ab, val) if ab else "", dt, nblocks / dt, int((br["status"] == 0).sum()), len(ar)),
               flush=True)
-        pv = (ctypes.c_double * 16)()
+        pv = (ctypes.c_double * len(names))()
         fn = _lib.lib.dll.pz_debug_chain_profile
         fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-        k = fn(ch._h, pv, 16)
+        k = fn(ch._h, pv, len(names))
         print("  phases (s): " + ", ".join("%s %.4f" % (names[i], pv[i]) for i in range(min(k, len(names)))),
               flush=True)
     for val, xs in res.items():
