@@ -586,6 +586,8 @@ struct PinVec {
   }
 };
 
+constexpr uint64_t kVoteTraceFlushes = 256, kVoteTraceWaves = 512;  // (PZ_VOTE_TRACE)
+
 enum ProfSlot {
   kProfParse, kProfHash1, kProfCheck, kProfQueue, kProfFlush, kProfRecalc, kProfMsgHash, kProfWalk, kProfProcess,
   kProfCount, kProfFlushWait, kProfMsgSend, kProfMsgLog, kProfMsgWait,
@@ -637,6 +639,7 @@ struct RankDev {
   DevArr<uint8_t> d_qpack;
   DevArr<uint64_t> d_err;      // sticky tally panic flag
   DevArr<uint32_t> v_ticket;   // the fused gather's arrival ticket (left zero)
+  DevArr<uint64_t> v_trace;    // (PZ_VOTE_TRACE, tools/ only) per flush and wave, the tally's phase stamps
   DevArr<uint64_t> t64;        // the gathered justification totals + panic flag (65 words)
   // epoch scratch: red = {scal[8], vote[natt], total[natt]} (one all-reduce when sharded)
   DevArr<uint64_t> e_red, e_mask, e_nb;
@@ -690,6 +693,18 @@ struct Engine {
     PinVec<uint32_t> slots;   // the explicit 64-id rows (kVoteIdsRow records)
     PinVec<uint8_t> bits;     // the bitfield rows when they are not inline (bits_inline false)
     uint32_t chunks = 1;  // max ceil(k / 256) over the queue
+    // the queue's attestations grouped by committee (votes.h VoteGroup), built as they queue;
+    // `groupable` false once a record is not in the run form, a bitfield is not inline, or the
+    // groups outnumber kVoteMaxGroups
+    struct Group {
+      uint32_t c = 0, k = 0;
+      uint32_t idlo = UINT32_MAX, idhi = 0;  // the parents' id range (inclusive)
+      std::vector<uint32_t> atts;
+    };
+    std::vector<Group> grp;
+    std::vector<int32_t> gof;  // per committee: its group + 1, 0 for none
+    bool groupable = true;
+    PinVec<uint32_t> perm;     // the flushed groups' record indices (VoteWordArgs.perm)
     bool busy = false;
     size_t natt() const { return rec.size(); }
   } vq[2];
@@ -768,6 +783,8 @@ struct Engine {
   PinBuf arena_pin;  // the call arena's bytes: parsed in place, H2D'd whole for the digest batch
   // wall-time accumulators (seconds) per phase, read by pz_debug_chain_profile
   double prof[kProfSlots] = {};
+  uint64_t vtrace_n = 0;               // (PZ_VOTE_TRACE) flushes launched traced
+  std::vector<uint64_t> vtrace_w;      //   and their wave counts (0: not recorded)
   // per transition (tools/replay_timeline.py, correlated with a rocprofv3 kernel trace):
   // CLOCK_MONOTONIC ns at the flush's start, after its tally launch returned, after the epoch's
   // launches, and when the totals' sequence word was seen
@@ -1017,6 +1034,47 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
     if (Q.slots.size()) std::memcpy(qa + o_slots, Q.slots.data(), Q.slots.size() * 4);
     if (Q.bits.size()) std::memcpy(qa + o_bits, Q.bits.data(), Q.bits.size());
   }
+  // the grouped form (votes.h VoteGroup): the walk's queue read in place, every record in the run
+  // form, each group within kVoteGroupWords id words (PZ_VOTE_GROUPS=0: A/B and test knob)
+  const char* vg = std::getenv("PZ_VOTE_GROUPS");
+  bool grouped = path == kVoteDirect && Q.groupable && !Q.grp.empty() && !(vg && !std::strcmp(vg, "0"));
+  VoteGroup groups[kVoteMaxGroups];
+  uint32_t nwaves = 0, ngroups = 0;
+  if (grouped) {
+    ngroups = (uint32_t)Q.grp.size();
+    uint32_t* pm = Q.perm.grow(natt);
+    uint32_t o = 0;
+    for (size_t i = 0; i < Q.grp.size() && grouped; ++i) {
+      const Engine::VoteQueue::Group& G = Q.grp[i];
+      VoteGroup& d = groups[i];
+      d.cb = (uint32_t)g.h_coffs[G.c];
+      d.k = G.k;
+      d.first = o;
+      d.n = (uint32_t)G.atts.size();
+      d.wlo = G.idlo == UINT32_MAX ? 0 : G.idlo >> 6;
+      d.nw = G.idlo == UINT32_MAX ? 0 : (G.idhi >> 6) - d.wlo + 1;
+      d.wave0 = nwaves;
+      // (records at a fixed stride, as a block's attestations of its committees in order: no
+      // index array to read)
+      d.stride = 0;
+      if (G.atts.size() == 1) {
+        d.stride = 1;
+      } else {
+        const uint32_t st = G.atts[1] - G.atts[0];
+        bool ap = st > 0;
+        for (size_t j = 2; j < G.atts.size() && ap; ++j) ap = G.atts[j] - G.atts[j - 1] == st;
+        if (ap) d.stride = st;
+      }
+      d.first = d.stride ? G.atts[0] : o;
+      if (d.nw > (uint32_t)kVoteGroupWords) grouped = false;
+      nwaves += std::max<uint32_t>(1, (G.k + 63) / 64);  // (an empty committee: one wave, its parents' map entries)
+      std::memcpy(pm + o, G.atts.data(), G.atts.size() * 4);
+      o += (uint32_t)G.atts.size();
+    }
+  }
+  for (const Engine::VoteQueue::Group& G : Q.grp) Q.gof[G.c] = 0;
+  Q.grp.clear();
+  Q.groupable = true;
   each_rank(g, [&](RankDev& r) {
     // Growing a device buffer frees the old one, which in-flight flushes may still read:
     // drain the stream first (rare: the buffer doubles).
@@ -1067,6 +1125,12 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
       v.bits = g.bits_inline ? nullptr : Q.bits.dev(r.dev);
     }
     v.natt = natt;
+    if (grouped) {
+      v.ngroups = ngroups;
+      std::memcpy(v.groups, groups, ngroups * sizeof(VoteGroup));
+      v.nwaves = nwaves;
+      v.perm = Q.perm.dev(r.dev);
+    }
     v.bstride = g.bf_stride;
     v.chunks = Q.chunks;
     v.balance = r.balance.p;
@@ -1094,6 +1158,19 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
       EpochLaunch* el = (*prep)();
       hchk(launch_vote_words_count(v, el->a, r.s), "vote tally + epoch count");
       el->counted = true;
+    } else if (std::getenv("PZ_VOTE_TRACE") && r.grank == 0) {
+      // (tools/vote_trace.py: the first kVoteTraceFlushes flushes' per-wave phase stamps)
+      if (!r.v_trace.p) {
+        check(r.v_trace.alloc((size_t)kVoteTraceFlushes * kVoteTraceWaves * 8));
+        hchk(hipMemsetAsync(r.v_trace.p, 0, (size_t)kVoteTraceFlushes * kVoteTraceWaves * 64, r.s), "memset");
+      }
+      const uint64_t waves = v.ngroups ? 4ull * v.nwaves : natt * Q.chunks;
+      uint64_t* tr = g.vtrace_n < kVoteTraceFlushes && waves <= kVoteTraceWaves
+                         ? r.v_trace.p + (size_t)g.vtrace_n * kVoteTraceWaves * 8
+                         : nullptr;
+      g.vtrace_w.push_back(tr ? waves : 0);
+      ++g.vtrace_n;
+      hchk(launch_vote_words_traced(v, tr, r.s), "vote tally");
     } else {
       hchk(launch_vote_words(v, r.s), "vote tally");
     }
@@ -1116,6 +1193,7 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
     N.busy = false;
   }
   N.rec.reset();
+  N.perm.reset();
   N.slots.reset();
   N.bits.reset();
   N.chunks = 1;
@@ -1373,6 +1451,29 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, AttLo
   if (g.A->cache_nil) throw Panic{"assignment to entry in nil map (core.go:323)"};
   // the member loop reaches CheckBit(bitfield, 8 * len) when the committee is longer
   if (k > 8ull * a.bf_len) throw Panic{"calculateBlockVoteCache: CheckBit index out of range (core.go:330)"};
+  if (!run || !g.bits_inline) Q.groupable = false;
+  if (Q.groupable) {
+    if (Q.gof.size() < g.ncomm) Q.gof.assign(g.ncomm, 0);
+    int32_t& gi = Q.gof[c];
+    if (!gi) {
+      if (Q.grp.size() >= (size_t)kVoteMaxGroups) {
+        Q.groupable = false;
+      } else {
+        Q.grp.emplace_back();
+        Q.grp.back().c = c;
+        Q.grp.back().k = (uint32_t)k;
+        gi = (int32_t)Q.grp.size();
+      }
+    }
+    if (Q.groupable) {
+      Engine::VoteQueue::Group& G = Q.grp[gi - 1];
+      if (absent != ~0ull) {  // the run's ids: [s0, s0 + popcount(step)]
+        G.idlo = std::min(G.idlo, s0);
+        G.idhi = std::max(G.idhi, s0 + (uint32_t)__builtin_popcountll(step));
+      }
+      G.atts.push_back((uint32_t)Q.natt());
+    }
+  }
   VoteRec* rec = Q.rec.grow(1);
   rec->cb = (uint32_t)g.h_coffs[c];
   rec->k = (uint32_t)k;
@@ -3444,6 +3545,22 @@ extern "C" int pz_debug_chain_profile(pz_chain* c, double* out, int n) {
 // Internal (tools/replay_timeline.py): up to n transitions' timestamps (4 u64 each, CLOCK_MONOTONIC
 // ns: flush start, tally launch returned, epoch launches returned, totals seen); returns the
 // count recorded since the chain was created (at most 65,536 are kept).
+// Internal (tools/vote_trace.py): under PZ_VOTE_TRACE the first flushes' per-wave tally stamps
+// (votes_dev.h PZ_VSTAMP: 8 wall-clock words per wave, kVoteTraceWaves waves per flush) into
+// out[nflush][kVoteTraceWaves][8], each flush's wave count into waves[nflush]; returns the flushes.
+extern "C" int pz_debug_vote_trace(pz_chain* c, uint64_t* out, uint64_t* waves, int nflush) {
+  if (!c || !out || !waves) return PZ_EINVAL;
+  auto& g = c->g;
+  RankDev& r = g.rk[0];
+  if (!r.v_trace.p) return 0;
+  const int n = std::min<int>(nflush, (int)std::min<uint64_t>(g.vtrace_n, kVoteTraceFlushes));
+  if (hipSetDevice(r.dev) != hipSuccess || hipStreamSynchronize(r.s) != hipSuccess) return PZ_EDEVICE;
+  if (hipMemcpy(out, r.v_trace.p, (size_t)n * kVoteTraceWaves * 64, hipMemcpyDeviceToHost) != hipSuccess)
+    return PZ_EDEVICE;
+  for (int i = 0; i < n; ++i) waves[i] = g.vtrace_w[i];
+  return n;
+}
+
 extern "C" int pz_debug_chain_timeline(pz_chain* c, uint64_t* out, int n) {
   if (!c || !out) return PZ_EINVAL;
   const auto& tl = c->g.tl;

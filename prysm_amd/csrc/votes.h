@@ -43,6 +43,24 @@ struct alignas(64) VoteRec {
 static_assert(sizeof(VoteRec) == 64, "one 64-B request per record");
 constexpr uint32_t kVoteInlineBits = 256;  // committees up to this size keep their bitfield inline
 
+// The grouped form of a flush (VoteWordArgs.ngroups > 0): its attestations grouped by committee.
+// A committee's attestations in one flush (one per block that carries it: 64 per transition on
+// the configs[4] chain) share their voters, so a wave per (group, 64 members) ORs each voter's
+// parents over the group's attestations in registers and then makes ONE 64-bit atomicOr per
+// voter and id word, where the per-attestation form made one per attestation (the same voter
+// words hit 64 times a flush: 131 k serialising atomics per transition at 65,536 validators).
+// Needs every record in the run form (the id set of a run is the range [s0, s0 + popcount(step)])
+// with its bitfield inline; a group spans at most kVoteGroupWords id words.
+constexpr int kVoteMaxGroups = 16;
+constexpr int kVoteGroupWords = 4;
+struct VoteGroup {
+  uint32_t cb, k;      // the committee
+  uint32_t first, n;   // its n attestations (below)
+  uint32_t wlo, nw;    // the id words its parents span: [wlo, wlo + nw), nw <= kVoteGroupWords
+  uint32_t wave0;      // its first unit (max(1, ceil(k / 64)) units of 64 members per group)
+  uint32_t stride;     // its records are first + stride * t (0: perm[first + t])
+};
+
 struct VoteWordArgs {
   const uint32_t* committee;  // ShardAndCommittee member lists (CSR, global validator indices)
   const VoteRec* rec;         // natt records
@@ -69,15 +87,23 @@ struct VoteWordArgs {
   uint32_t* ticket;
   VoteGatherSlots gq;
   uint64_t gather_seq;
+  // the grouped form (0 groups: one wave per (attestation, 256 members)): nwaves units, each
+  // one block of kVoteWordThreads
+  uint32_t ngroups, nwaves;
+  const uint32_t* perm;  // the records' indices, group by group
+  VoteGroup groups[kVoteMaxGroups];
 };
 constexpr uint32_t kVoteWordThreads = 256;    // the tally blocks beside an epoch count pass
 constexpr uint32_t kVoteWordMaxThreads = 1024;  // pz_vote_words_kernel's blocks (PZ_VOTE_WAVES per block)
 // Blocks of the tally part of a launch (threads / 64 waves each).
 inline uint32_t vote_word_blocks(const VoteWordArgs& a, uint32_t threads = kVoteWordThreads) {
-  const uint64_t wpb = threads / 64;
-  return (uint32_t)((a.natt * a.chunks + wpb - 1) / wpb);
+  if (a.ngroups) return a.nwaves;  // (one block of kVoteWordThreads per unit)
+  const uint64_t wpb = threads / 64, waves = a.natt * a.chunks;
+  return (uint32_t)((waves + wpb - 1) / wpb);
 }
 hipError_t launch_vote_words(const VoteWordArgs& a, hipStream_t s);
+// (tools/ only) the same with per-wave phase stamps into tr[wave][8] (null: none)
+hipError_t launch_vote_words_traced(const VoteWordArgs& a, uint64_t* tr, hipStream_t s);
 // Up to 6 copies from mapped pinned memory to device memory in ONE launch (16 B per lane; the
 // sources may be read up to 15 bytes past their ends, so a source buffer's capacity must cover
 // ceil16 of its bytes).

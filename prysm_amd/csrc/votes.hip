@@ -51,8 +51,18 @@ static uint32_t vote_word_threads() {
 
 hipError_t launch_vote_words(const VoteWordArgs& a, hipStream_t s) {
   if (!a.natt) return hipSuccess;
-  const uint32_t t = vote_word_threads();
+  const uint32_t t = a.ngroups ? kVoteWordThreads : vote_word_threads();
   hipLaunchKernelGGL(pz_vote_words_kernel, dim3(vote_word_blocks(a, t)), dim3(t), 0, s, a);
+  return hipGetLastError();
+}
+
+extern "C" __global__ void __launch_bounds__(kVoteWordMaxThreads)
+pz_vote_words_traced_kernel(VoteWordArgs a, uint64_t* tr) { vote_words_body(a, gridDim.x, blockIdx.x, tr); }
+
+hipError_t launch_vote_words_traced(const VoteWordArgs& a, uint64_t* tr, hipStream_t s) {
+  if (!a.natt) return hipSuccess;
+  const uint32_t t = a.ngroups ? kVoteWordThreads : vote_word_threads();
+  hipLaunchKernelGGL(pz_vote_words_traced_kernel, dim3(vote_word_blocks(a, t)), dim3(t), 0, s, a, tr);
   return hipGetLastError();
 }
 

@@ -96,12 +96,38 @@ __device__ __forceinline__ uint64_t wor64_dpp(uint64_t v) {
 // per parent.  Every wave of the flush adds to the same handful of totals (the transition's
 // window), and device-scope atomics on one address serialise (~12 ns each): summed per block
 // first, a flush issues one atomic per (block, parent) instead of one per (wave, parent).
+#ifndef PZ_VOTE_GATHER_WT
+#define PZ_VOTE_GATHER_WT 0
+#endif
 constexpr int kVoteLdsWords = 4;
 constexpr uint32_t kVoteLdsEmpty = 0xFFFFFFFFu;
 struct VoteLds {
   uint32_t key[kVoteLdsWords];  // the id word of each slot, or kVoteLdsEmpty
   unsigned long long acc[kVoteLdsWords][64];
 };
+
+// The block's LDS slot for id word w (found, or claimed by lane 0), or -1 when all are taken
+// (the caller then adds to the device totals directly).  Wave-uniform.
+__device__ __forceinline__ int vote_lds_slot(VoteLds* L, uint32_t w) {
+  int ls = -1;
+  if ((threadIdx.x & 63) == 0) {
+    for (int i = 0; i < kVoteLdsWords; ++i) {
+      const uint32_t o = atomicCAS(&L->key[i], kVoteLdsEmpty, w);
+      if (o == kVoteLdsEmpty || o == w) {
+        ls = i;
+        break;
+      }
+    }
+  }
+  return __builtin_amdgcn_readlane(ls, 0);
+}
+
+// The id word w's bits of the id range [lo, hi)
+__device__ __forceinline__ uint64_t range_word_mask(uint32_t lo, uint32_t hi, uint32_t w) {
+  const uint32_t b = 64 * w, l = lo > b ? lo - b : 0, h = hi < b + 64 ? (hi > b ? hi - b : 0) : 64;
+  if (h <= l) return 0;
+  return (h - l == 64 ? ~0ull : ((1ull << (h - l)) - 1)) << l;
+}
 
 // One wave of the voter-major tally: members [256 chunk, 256 chunk + 256) of attestation
 // `att`'s committee (calculateBlockVoteCache, core.go:300-345, for all of its signed parent
@@ -224,17 +250,7 @@ __device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t 
       const uint64_t M = wor64_dpp(nw[d][0] | nw[d][1] | nw[d][2] | nw[d][3]);
       if (!M) continue;  // (wave-uniform: nothing new)
       // the word's LDS slot (found or claimed by lane 0), or -1: the totals directly
-      int ls = -1;
-      if (lane == 0) {
-        for (int i = 0; i < kVoteLdsWords; ++i) {
-          const uint32_t o = atomicCAS(&L->key[i], kVoteLdsEmpty, w);
-          if (o == kVoteLdsEmpty || o == w) {
-            ls = i;
-            break;
-          }
-        }
-      }
-      ls = __builtin_amdgcn_readlane(ls, 0);
+      const int ls = vote_lds_slot(L, w);
       uint64_t xs = 0;
       bool uni = true;
 #pragma unroll
@@ -250,21 +266,163 @@ __device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t 
           else atomicAdd((unsigned long long*)&a.totals[64ull * w + lane], (unsigned long long)S);
         }
       } else {
-        for (uint64_t m = M; m; m &= m - 1) {  // (wave-uniform loop over the parents in M)
-          const int j = __builtin_ctzll(m);
+        // one pass per distinct new-parent mask among the wave's voters (ballot): its voters'
+        // balance sum to each of its parents (a handful of masks, where a per-parent pass made
+        // up to 64 and held the flush's last wave ~13 us, profiles/r04/vote_trace_r4z.txt)
+        uint64_t rq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rq[q] = __ballot(nw[d][q] != 0);
+        for (;;) {  // (wave-uniform)
+          const int qq = rq[0] ? 0 : rq[1] ? 1 : rq[2] ? 2 : rq[3] ? 3 : -1;
+          if (qq < 0) break;
+          const int leader = __builtin_ctzll(rq[qq]);
+          const uint64_t src = qq == 0 ? nw[d][0] : qq == 1 ? nw[d][1] : qq == 2 ? nw[d][2] : nw[d][3];
+          const uint64_t lm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(src >> 32), leader) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)src, leader);
           uint64_t x = 0;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) x += ((nw[d][q] >> j) & 1) ? bal[q] : 0;
-          const uint64_t sj = wsum64_dpp(x);
-          if (lane == 0 && sj) {
-            if (ls >= 0) atomicAdd(&L->acc[ls][j], (unsigned long long)sj);
-            else atomicAdd((unsigned long long*)&a.totals[64ull * w + j], (unsigned long long)sj);
+          for (int q = 0; q < 4; ++q) {
+            const bool mine = nw[d][q] == lm && ((rq[q] >> lane) & 1);
+            rq[q] &= ~__ballot(mine);
+            x += mine ? bal[q] : 0;
+          }
+          const uint64_t Sm = wsum64_dpp(x);
+          if (Sm && ((lm >> lane) & 1)) {
+            if (ls >= 0) atomicAdd(&L->acc[ls][lane], (unsigned long long)Sm);
+            else atomicAdd((unsigned long long*)&a.totals[64ull * w + lane], (unsigned long long)Sm);
           }
         }
       }
     }
   }
   if (__ballot(err != 0) && lane == 0) atomicOr((unsigned long long*)a.err, 1ull);
+  PZ_VSTAMP(5)
+}
+
+// A grouped unit's LDS: the four waves' per-voter unions, merged.
+struct VoteGroupLds {
+  unsigned long long U[kVoteGroupWords][64];  // per word and voter lane: the parents it voted for
+  unsigned long long UP[kVoteGroupWords];     // per word: every record's parents (map entries)
+  uint32_t any[64];                            // per voter lane: its bit is set in some record
+};
+
+// One block (4 waves) of the grouped tally (votes.h VoteGroup): unit `unit` = members
+// [64 m, 64 m + 64) of group g's committee, lane l holding member 64 m + l.  The group's records
+// are split over the 4 waves (16 of every 64 each); a wave loads its records one per lane and
+// computes each one's id range as masks over the group's words (the ids of a run are the range
+// [s0, s0 + popcount(step)]), then a record-by-record loop ORs a record's masks into the union U
+// of every voter whose bit it has.  The waves' unions merge in LDS; then wave w takes word w:
+// one atomicOr per voter, the returned bits that were clear are the parents it is new for, and
+// per distinct new-parent mask in the wave (ballot) its voters' balance sum goes to those
+// parents' LDS totals.  Sums mod 2^64 commute: the totals are those of the reference's
+// sequential loop (calculateBlockVoteCache, core.go:300-345, over the flush's attestations).
+// Every thread of the block calls it (it holds a barrier).
+__device__ __forceinline__ void vote_groups_block(const VoteWordArgs& a, uint32_t unit, VoteLds* L, VoteGroupLds* S,
+                                                  uint64_t* tr = nullptr) {
+  const int lane = threadIdx.x & 63, wq = threadIdx.x >> 6;
+  const bool live = unit < a.nwaves;  // (block-uniform)
+  int g = 0;
+  while (g + 1 < (int)a.ngroups && a.groups[g + 1].wave0 <= unit) ++g;
+  const VoteGroup G = a.groups[g];
+  const uint32_t m = live ? unit - G.wave0 : 0;
+  const uint32_t i = 64 * m + lane;
+  const bool vin = live && i < G.k;
+  PZ_VSTAMP(0)
+  if (live) {
+    uint64_t U[kVoteGroupWords], UP[kVoteGroupWords];
+#pragma unroll
+    for (int w = 0; w < kVoteGroupWords; ++w) U[w] = UP[w] = 0;
+    bool any = false;
+    for (uint32_t a0 = 16 * wq; a0 < G.n; a0 += 64) {  // (wave-uniform) this wave's 16 of every 64
+      const uint32_t n = G.n - a0 < 16 ? G.n - a0 : 16;
+      const uint32_t t0 = a0 + lane;
+      const uint32_t att = lane < (int)n ? (G.stride ? G.first + G.stride * t0 : a.perm[G.first + t0]) : 0u;
+      uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0, r2 = r0, r3 = r0;
+      if (lane < (int)n) {
+        const uint4* rp = reinterpret_cast<const uint4*>(a.rec + att);
+        r0 = rp[0];
+        r1 = rp[1];
+        r2 = rp[2];
+        r3 = rp[3];
+      }
+      // this unit's two bitfield words (members 64 m .. 64 m + 63): words 2 m and 2 m + 1 of the
+      // record's eight (words 0-3 in r2, 4-7 in r3)
+      const uint32_t bA = m == 0 ? r2.x : m == 1 ? r2.z : m == 2 ? r3.x : r3.z;
+      const uint32_t bB = m == 0 ? r2.y : m == 1 ? r2.w : m == 2 ? r3.y : r3.w;
+      uint64_t rm[kVoteGroupWords];
+      {
+        const uint64_t step = ((uint64_t)r1.y << 32) | r1.x, absent = ((uint64_t)r1.w << 32) | r1.z;
+        const bool none = lane >= (int)n || absent == ~0ull;
+        const uint32_t lo = r0.z, hi = r0.z + (uint32_t)__builtin_popcountll(step) + 1;
+#pragma unroll
+        for (int w = 0; w < kVoteGroupWords; ++w) {
+          rm[w] = none ? 0 : range_word_mask(lo, hi, G.wlo + w);
+          UP[w] |= wor64_dpp(rm[w]);
+        }
+      }
+      if (a0 == 16u * wq) PZ_VSTAMP(1)
+      const uint32_t sh = 8 * ((lane >> 3) & 3) + 7 - (lane & 7);
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {  // record by record (unrolled: constant lanes)
+        // (records past n have no bit and no parents: lanes >= n hold zero words)
+        const uint32_t wA = (uint32_t)__builtin_amdgcn_readlane((int)bA, t);
+        const uint32_t wB = (uint32_t)__builtin_amdgcn_readlane((int)bB, t);
+        const bool bit = vin && ((((lane & 32) ? wB : wA) >> sh) & 1u);
+        any = any || bit;
+        const uint64_t sel = bit ? ~0ull : 0ull;
+#pragma unroll
+        for (int w = 0; w < kVoteGroupWords; ++w) {
+          const uint64_t mk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(rm[w] >> 32), t) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rm[w], t);
+          U[w] |= mk & sel;
+        }
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < kVoteGroupWords; ++w) {
+      if (U[w]) atomicOr(&S->U[w][lane], (unsigned long long)U[w]);
+      if (lane == 0 && UP[w]) atomicOr(&S->UP[w], (unsigned long long)UP[w]);
+    }
+    if (any) atomicOr(&S->any[lane], 1u);
+  }
+  PZ_VSTAMP(2)
+  __syncthreads();
+  if (!live) return;
+  const uint32_t v = vin ? a.committee[G.cb + i] : 0u;
+  uint64_t lv = (uint64_t)v - a.val_offset;  // wraps huge below the range
+  bool on = S->any[lane] != 0;
+  uint64_t err = 0;
+  if (on && v >= a.nval_global) {  // validators[attesterIndex] would panic
+    err = 1;
+    on = false;
+  }
+  if (on && lv >= a.nval) on = false;  // another rank's validator
+  if (wq == 0 && __ballot(err != 0) && lane == 0) atomicOr((unsigned long long*)a.err, 1ull);
+  if (wq >= (int)G.nw) return;  // (wave-uniform) wave wq: id word G.wlo + wq
+  const uint32_t wd = G.wlo + wq;
+  const uint64_t U = S->U[wq][lane];
+  if (m == 0 && ((S->UP[wq] >> lane) & 1)) a.present[64ull * wd + lane] = 1;
+  const uint64_t bal = on && U ? a.balance[lv] : 0;
+  PZ_VSTAMP(3)
+  uint64_t nw = 0;
+  if (on && U) nw = U & ~(uint64_t)atomicOr((unsigned long long*)&a.bm[(uint64_t)wd * a.nval + lv], (unsigned long long)U);
+  PZ_VSTAMP(4)
+  uint64_t rem = __ballot(nw != 0);
+  if (rem) {
+    const int ls = vote_lds_slot(L, wd);
+    while (rem) {  // (wave-uniform) one pass per distinct new-parent mask
+      const int leader = __builtin_ctzll(rem);
+      const uint64_t lm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(nw >> 32), leader) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)nw, leader);
+      const bool mine = nw == lm && ((rem >> lane) & 1);
+      rem &= ~__ballot(mine);
+      const uint64_t Sm = wsum64_dpp(mine ? bal : 0);
+      if (Sm && ((lm >> lane) & 1)) {
+        if (ls >= 0) atomicAdd(&L->acc[ls][lane], (unsigned long long)Sm);
+        else atomicAdd((unsigned long long*)&a.totals[64ull * wd + lane], (unsigned long long)Sm);
+      }
+    }
+  }
   PZ_VSTAMP(5)
 }
 
@@ -277,12 +435,21 @@ __device__ __forceinline__ void vote_words_wave(const VoteWordArgs& a, uint64_t 
 __device__ __forceinline__ void vote_words_body(const VoteWordArgs& a, uint32_t nblk, uint32_t bid,
                                                 uint64_t* trace = nullptr) {
   __shared__ VoteLds L;
+  __shared__ VoteGroupLds S;
   for (uint32_t t = threadIdx.x; t < kVoteLdsWords * 64; t += blockDim.x) L.acc[t >> 6][t & 63] = 0;
   if (threadIdx.x < kVoteLdsWords) L.key[threadIdx.x] = kVoteLdsEmpty;
+  if (a.ngroups) {
+    for (uint32_t t = threadIdx.x; t < kVoteGroupWords * 64; t += blockDim.x) S.U[t >> 6][t & 63] = 0;
+    if (threadIdx.x < kVoteGroupWords) S.UP[threadIdx.x] = 0;
+    if (threadIdx.x < 64) S.any[threadIdx.x] = 0;
+  }
   __syncthreads();
   const uint64_t wid = (uint64_t)bid * (blockDim.x >> 6) + (threadIdx.x >> 6);
   uint64_t* tr = trace ? trace + wid * 8 : nullptr;
-  vote_words_wave(a, wid, &L, tr);
+  if (a.ngroups)
+    vote_groups_block(a, bid, &L, &S, tr);  // (blockDim.x == kVoteWordThreads: 4 waves)
+  else
+    vote_words_wave(a, wid, &L, tr);
   __syncthreads();
   for (uint32_t t = threadIdx.x; t < kVoteLdsWords * 64; t += blockDim.x) {
     const uint32_t w = L.key[t >> 6];
@@ -301,6 +468,27 @@ __device__ __forceinline__ void vote_words_body(const VoteWordArgs& a, uint32_t 
   __syncthreads();
   if (!last) return;
   const int j = threadIdx.x;
+#if PZ_VOTE_GATHER_WT
+  // wave 0 alone: write-through (system-scope) stores of the totals and the flag, drained, then
+  // the sequence word -- no L2 write-back fence
+  if (j < 64) {
+    const uint32_t sl = a.gq.slot[j];
+    const uint64_t x =
+        sl == 0xFFFFFFFFu ? 0 : __hip_atomic_load(&a.totals[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.gather_out[j], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (j == 0) {
+      __hip_atomic_store(&a.gather_out[kJustifySlots],
+                         __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (j == 0)
+      __hip_atomic_store(&a.gather_out[kJustifySlots + 1], a.gather_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  PZ_VSTAMP(7)
+  return;
+#endif
   if (j < kJustifySlots) {
     const uint32_t sl = a.gq.slot[j];
     a.gather_out[j] =

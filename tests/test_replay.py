@@ -550,23 +550,27 @@ def test_gpu_sharded_chain_configs4_full_vs_c_port(world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path,epack,bits,ids", [("segments", "copy", "inline", "run"),
-                                                  ("packed", "copy", "rows", "rows"),
-                                                  ("direct", "direct", "inline", "run"),
-                                                  ("direct", "copy", "rows", "run"),
-                                                  ("direct", "copy", "inline", "rows")])
-def test_gpu_replay_vote_queue_paths_vs_c_port(path, epack, bits, ids, monkeypatch):
+@pytest.mark.parametrize("path,epack,bits,ids,groups", [("segments", "copy", "inline", "run", "1"),
+                                                         ("packed", "copy", "rows", "rows", "1"),
+                                                         ("direct", "direct", "inline", "run", "1"),
+                                                         ("direct", "copy", "inline", "run", "0"),
+                                                         ("direct", "copy", "rows", "run", "1"),
+                                                         ("direct", "copy", "inline", "rows", "1")])
+def test_gpu_replay_vote_queue_paths_vs_c_port(path, epack, bits, ids, groups, monkeypatch):
     """Every way a vote-cache flush reaches the device (PZ_VOTE_PATH: the walk's pinned queue
     read in place by the voter-major tally -- the product --, its arrays staged by one
-    multi-segment copy, or round 3's packed arena) and every record form (votes.h VoteRec: the
+    multi-segment copy, or round 3's packed arena), every record form (votes.h VoteRec: the
     bitfield inline or in the row array, PZ_VOTE_BITS; the parents' ids as a run or an explicit
-    row, PZ_VOTE_IDS) over 2,000 blocks of the configs[4] chain (31 transitions, the two queues
-    alternating, carried over a call boundary) against the C restatement; the direct/direct case
-    also has the transitions' epoch kernels read their inputs in place (PZ_EPOCH_PACK=direct)."""
+    row, PZ_VOTE_IDS) and both tally forms (grouped by committee -- the product when every record
+    is a run with its bitfield inline --, or per attestation: PZ_VOTE_GROUPS=0 or any other form)
+    over 2,000 blocks of the configs[4] chain (31 transitions, the two queues alternating,
+    carried over a call boundary) against the C restatement; the direct/direct case also has the
+    transitions' epoch kernels read their inputs in place (PZ_EPOCH_PACK=direct)."""
     monkeypatch.setenv("PZ_VOTE_PATH", path)
     monkeypatch.setenv("PZ_EPOCH_PACK", epack)  # the transition's epoch inputs: staged copy or read in place
     monkeypatch.setenv("PZ_VOTE_BITS", bits)  # (read when the chain is made)
     monkeypatch.setenv("PZ_VOTE_IDS", ids)
+    monkeypatch.setenv("PZ_VOTE_GROUPS", groups)  # (read per flush)
     from prysm_amd.blockchain import BeaconChain, serialize_blocks
     from replay_port_helpers import mismatches, port_replay
     nval = 65536

@@ -5,7 +5,13 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tally_probe.hip -o build/tally_probe
 //   build/tally_probe [natt=320] [k=128] [nval=65536] [waves_per_block=4] [host_queue=1]
+//                     [shuffled=1] [idle_us=0]
+// shuffled 0: committee members in validator order (a voter-position vote cache: an
+// attestation's voter words are contiguous); idle_us > 0: the GPU idles that long before each
+// flush, and each flush's id words are fresh (cold) rows, as in a replay's transitions.
 #include <hip/hip_runtime.h>
+
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -41,6 +47,8 @@ int main(int argc, char** argv) {
   const uint32_t nval = argc > 3 ? atoi(argv[3]) : 65536;
   const uint32_t wpb = argc > 4 ? atoi(argv[4]) : 4;
   const bool host_q = argc > 5 ? atoi(argv[5]) != 0 : true;
+  const bool shuffled = argc > 6 ? atoi(argv[6]) != 0 : true;
+  const int idle_us = argc > 7 ? atoi(argv[7]) : 0;
   if (k > 256 || nval % k || wpb < 1 || wpb > 16) {
     fprintf(stderr, "k <= 256 dividing nval; 1-16 waves per block\n");
     return 2;
@@ -48,7 +56,7 @@ int main(int argc, char** argv) {
   std::mt19937_64 rng(7);
   std::vector<uint32_t> members(nval);
   std::iota(members.begin(), members.end(), 0u);
-  std::shuffle(members.begin(), members.end(), rng);
+  if (shuffled) std::shuffle(members.begin(), members.end(), rng);
   const uint32_t ncomm = nval / k;
   std::vector<VoteRec> rec(natt);
   for (uint32_t i = 0; i < natt; ++i) {
@@ -56,13 +64,13 @@ int main(int argc, char** argv) {
     std::memset(&r, 0, sizeof r);
     r.cb = (uint32_t)((i % ncomm) * k);  // distinct committees: every voter new
     r.k = k;
-    r.s0 = 64 * 5 + 13 + i / 5;  // a run over two id words, one new parent per block
+    r.s0 = 13 + i / 5;  // a run over two id words, one new parent per block (+ the flush's base)
     r.form = 0;
     r.step = ~1ull;
     r.absent = 0;
     for (uint32_t b = 0; b < k; ++b) reinterpret_cast<uint8_t*>(r.bits)[b >> 3] |= (uint8_t)(0x80 >> (b & 7));
   }
-  const uint32_t nwords = 16;
+  const uint32_t nwords = 128;  // flush f uses words 2 (f % 60) and 2 (f % 60) + 1
   uint32_t *d_comm, *d_ticket;
   uint64_t *d_bal, *d_bm, *d_tot, *d_err;
   uint8_t* d_present;
@@ -102,7 +110,6 @@ int main(int argc, char** argv) {
   a.err = d_err;
   a.gather_out = gout;
   a.ticket = d_ticket;
-  for (int j = 0; j < kJustifySlots; ++j) a.gq.slot[j] = 64 * 5 + 13 + j;
   const uint32_t nblk = (natt + wpb - 1) / wpb;
   uint64_t* d_tr;
   CK(hipMalloc(&d_tr, (size_t)nblk * wpb * 8 * 8));
@@ -111,11 +118,31 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   hipStream_t s;
   CK(hipStreamCreate(&s));
+  CK(hipMemset(d_bm, 0, (size_t)nwords * nval * 8));
+  CK(hipMemset(d_tot, 0, nwords * 64 * 8));
+  std::vector<VoteRec> qf(natt);
+  int flush = 0;
+  // one flush: fresh words (idle mode) or the same words cleared first (back to back)
+  auto prepare = [&]() {
+    const uint32_t base = idle_us > 0 ? 128 * (flush % 60) : 0;
+    if (idle_us <= 0) {
+      CK(hipMemsetAsync(d_bm, 0, (size_t)2 * nval * 8, s));
+      CK(hipMemsetAsync(d_tot, 0, 2 * 64 * 8, s));
+    }
+    for (uint32_t i = 0; i < natt; ++i) {
+      qf[i] = rec[i];
+      qf[i].s0 += base;
+    }
+    if (host_q) std::memcpy(q, qf.data(), natt * sizeof(VoteRec));
+    else CK(hipMemcpyAsync(q, qf.data(), natt * sizeof(VoteRec), hipMemcpyHostToDevice, s));
+    for (int j = 0; j < kJustifySlots; ++j) a.gq.slot[j] = base + 13 + j;
+    a.gather_seq = ++flush;
+    CK(hipStreamSynchronize(s));
+    if (idle_us > 0) usleep(idle_us);
+  };
   std::vector<float> ms;
   for (int it = 0; it < 40; ++it) {
-    CK(hipMemsetAsync(d_bm, 0, (size_t)nwords * nval * 8, s));
-    CK(hipMemsetAsync(d_tot, 0, nwords * 64 * 8, s));
-    a.gather_seq = it + 1;
+    prepare();
     CK(hipEventRecord(e0, s));
     hipLaunchKernelGGL(probe_plain, dim3(nblk), dim3(64 * wpb), 0, s, a);
     CK(hipEventRecord(e1, s));
@@ -125,18 +152,17 @@ int main(int argc, char** argv) {
     if (it >= 5) ms.push_back(t * 1000.f);
   }
   std::sort(ms.begin(), ms.end());
-  printf("natt %u k %u nval %u waves/block %u queue %s: plain kernel event time median %.2f us (min %.2f)\n",
-         natt, k, nval, wpb, host_q ? "pinned host" : "device", ms[ms.size() / 2], ms[0]);
+  printf("natt %u k %u nval %u waves/block %u queue %s members %s idle %d us: plain kernel event time median %.2f us (min %.2f)\n",
+         natt, k, nval, wpb, host_q ? "pinned host" : "device", shuffled ? "shuffled" : "in order", idle_us,
+         ms[ms.size() / 2], ms[0]);
   printf("totals[0..3] %llu %llu %llu %llu seq %llu\n", (unsigned long long)gout[0], (unsigned long long)gout[1],
          (unsigned long long)gout[2], (unsigned long long)gout[3], (unsigned long long)gout[kJustifySlots + 1]);
   // traced run
   std::vector<uint64_t> tr((size_t)nblk * wpb * 8);
   std::vector<std::vector<double>> ph(8);
   for (int it = 0; it < 10; ++it) {
-    CK(hipMemsetAsync(d_bm, 0, (size_t)nwords * nval * 8, s));
-    CK(hipMemsetAsync(d_tot, 0, nwords * 64 * 8, s));
     CK(hipMemsetAsync(d_tr, 0, tr.size() * 8, s));
-    a.gather_seq = 1000 + it;
+    prepare();
     hipLaunchKernelGGL(probe_traced, dim3(nblk), dim3(64 * wpb), 0, s, a, d_tr);
     CK(hipStreamSynchronize(s));
     CK(hipMemcpy(tr.data(), d_tr, tr.size() * 8, hipMemcpyDeviceToHost));
