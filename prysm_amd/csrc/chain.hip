@@ -588,6 +588,15 @@ struct PinVec {
 
 constexpr uint64_t kVoteTraceFlushes = 256, kVoteTraceWaves = 512;  // (PZ_VOTE_TRACE)
 
+// A recent window's parent ids as a run (votes.h VoteRec) over its positions [0, nw): shared by
+// every attestation that signs the same window (trail[wstart, wstart + nw) at generation gen).
+struct WindowRun {
+  uint64_t wstart = ~0ull, nw = 0, gen = ~0ull;
+  uint64_t step = 0, absent = 0;
+  uint32_t s0 = UINT32_MAX, prev = 0;
+  bool run = true;
+};
+
 enum ProfSlot {
   kProfParse, kProfHash1, kProfCheck, kProfQueue, kProfFlush, kProfRecalc, kProfMsgHash, kProfWalk, kProfProcess,
   kProfCount, kProfFlushWait, kProfMsgSend, kProfMsgLog, kProfMsgWait,
@@ -716,6 +725,8 @@ struct Engine {
   uint64_t ncomm = 0;
   std::vector<uint64_t> h_coffs;  // the committees' first member offsets (host copy)
   uint32_t bf_stride = 4;         // the vote queue's bitfield row: >= every committee's bytes, x4
+  uint64_t trail_gen = 0;         // bumped whenever the trail is rebuilt (WindowRun's key)
+  WindowRun wrun;                 // the last recent window's parent-id run (queue_vote_cache)
   bool bits_inline = true;        // every committee <= kVoteInlineBits: the bitfields ride in the records
   bool ids_rows = false;          // (test knob) every attestation's ids in an explicit row
   PinBuf e_pin, e_pin_out;   // the epoch inputs' pinned staging; the results' pinned landing
@@ -1419,32 +1430,50 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, AttLo
     if (const uint32_t* sl = g.slot_of.find(h)) match[nmatch++] = *sl;
   }
   Engine::VoteQueue& Q = g.vq[g.vq_cur];
-  // the 64 parents' vote-cache ids, UINT32_MAX where a parent is not tallied (the device groups
-  // them by id word, votes_dev.h), and whether they make a run (votes.h VoteRec)
-  uint32_t slots[64];
+  // the 64 parents' vote-cache ids, UINT32_MAX where a parent is not tallied, as a run (votes.h
+  // VoteRec: s0, step, absent) when they make one
   uint64_t step = 0, absent = 0;
   bool run = !g.ids_rows;
   uint32_t s0 = UINT32_MAX, prev = 0;
-  {
-    // (the trail's and the id table's base pointers hoisted: PinVec::operator[] is three
-    // dependent loads, and this loop runs 64 times per attestation)
-    const uint32_t* tr = g.trail.data() + parents.wstart;
-    const uint32_t* ids = g.id_slot.data();
-    const size_t nw = parents.nw;
+  auto put = [&](size_t j, uint32_t sl) {
+    if (((skip >> j) & 1) || sl == UINT32_MAX) {
+      absent |= 1ull << j;
+      return;
+    }
+    if (s0 == UINT32_MAX) s0 = sl;
+    else if (sl == prev + 1) step |= 1ull << j;
+    else if (sl != prev) run = false;
+    prev = sl;
+  };
+  // (the trail's and the id table's base pointers hoisted: PinVec::operator[] is three dependent
+  // loads)
+  const uint32_t* tr = g.trail.data() + parents.wstart;
+  const uint32_t* ids = g.id_slot.data();
+  const size_t nw = parents.nw;
+  auto id_at = [&](size_t j) -> uint32_t {
+    return j < nw ? ids[tr[j]] : j < np ? ids[parents.obl[j - nw]] : UINT32_MAX;
+  };
+  if (nmatch == 0) {
+    // The window part is the same for every attestation of a block (and its run summary for
+    // every attestation over the same window): computed once per window (the walk's samples had
+    // the 64-parent loop at 12 %), then the obliques' positions one by one.
+    WindowRun& W = g.wrun;
+    if (W.wstart != parents.wstart || W.nw != nw || W.gen != g.trail_gen) {
+      W.wstart = parents.wstart;
+      W.nw = nw;
+      W.gen = g.trail_gen;
+      for (size_t j = 0; j < nw && j < 64; ++j) put(j, id_at(j));
+      W.step = step, W.absent = absent, W.s0 = s0, W.prev = prev, W.run = run;
+    } else {
+      step = W.step, absent = W.absent, s0 = W.s0, prev = W.prev, run = W.run && run;
+    }
+    for (size_t j = nw; j < 64; ++j) put(j, id_at(j));
+  } else {
     for (size_t j = 0; j < 64; ++j) {
-      const uint32_t sl = j < nw ? ids[tr[j]] : j < np ? ids[parents.obl[j - nw]] : UINT32_MAX;
+      const uint32_t sl = id_at(j);
       for (int m = 0; m < nmatch; ++m)
         if (sl == match[m]) skip |= 1ull << j;
-      if (((skip >> j) & 1) || sl == UINT32_MAX) {
-        slots[j] = UINT32_MAX;
-        absent |= 1ull << j;
-        continue;
-      }
-      slots[j] = sl;
-      if (s0 == UINT32_MAX) s0 = sl;
-      else if (sl == prev + 1) step |= 1ull << j;
-      else if (sl != prev) run = false;
-      prev = sl;
+      put(j, sl);
     }
   }
   if (skip == ~0ull) return;  // no map access at all
@@ -1487,7 +1516,8 @@ static void queue_vote_cache(Engine& g, uint64_t block_slot, const Att& a, AttLo
     rec->form = kVoteIdsRow;
     g.prof[kProfIdRows] += 1;
     rec->step = rec->absent = 0;
-    std::memcpy(Q.slots.grow(64), slots, sizeof slots);
+    uint32_t* row = Q.slots.grow(64);
+    for (size_t j = 0; j < 64; ++j) row[j] = ((absent >> j) & 1) ? UINT32_MAX : id_at(j);
   }
   const uint8_t* bf = a.at(a.bf_off);
   const size_t nbf = (k + 7) / 8;
@@ -2085,6 +2115,7 @@ static void init_tail(Engine& g, const std::vector<uint32_t>& members, const std
   g.d_hlog_n = 0;
   const uint32_t zero_id = log_hash(g, kZero);
   g.trail.assign(2 * kCycle, zero_id);
+  ++g.trail_gen;
   g.d_trail_n = 0;
   A->tail = g.trail.size();
   A->len = (uint32_t)(2 * kCycle);
