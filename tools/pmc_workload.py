@@ -22,6 +22,9 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
+if os.environ.get("PZ_PROBE_LIB"):  # (A/B: another build of the library)
+    from prysm_amd import _lib as _pl
+    _pl.library_path = os.environ["PZ_PROBE_LIB"]
 from prysm_amd import _lib, casper, synth  # noqa: E402
 from prysm_amd.native import NativeEpoch  # noqa: E402
 
