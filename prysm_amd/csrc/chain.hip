@@ -588,6 +588,17 @@ struct PinVec {
 
 constexpr uint64_t kVoteTraceFlushes = 256, kVoteTraceWaves = 512;  // (PZ_VOTE_TRACE)
 
+// The walk's A/B and test knobs (environment variables), read once per pz_chain_process_blocks
+// call (read_knobs) rather than at every flush and transition: a getenv scans the whole
+// environment, five of them per transition.
+struct Knobs {
+  int vote_path = 2;            // PZ_VOTE_PATH (VotePath: 0 segments, 1 packed, 2 direct)
+  bool vote_groups = true;      // PZ_VOTE_GROUPS=0: the per-attestation tally
+  bool vote_trace = false;      // PZ_VOTE_TRACE (tools/vote_trace.py)
+  bool epoch_pack_direct = false;  // PZ_EPOCH_PACK=direct
+  bool epoch_prep_after = true;    // PZ_EPOCH_PREP=merged: false
+};
+
 // A recent window's parent ids as a run (votes.h VoteRec) over its positions [0, nw): shared by
 // every attestation that signs the same window (trail[wstart, wstart + nw) at generation gen).
 struct WindowRun {
@@ -727,6 +738,7 @@ struct Engine {
   uint32_t bf_stride = 4;         // the vote queue's bitfield row: >= every committee's bytes, x4
   uint64_t trail_gen = 0;         // bumped whenever the trail is rebuilt (WindowRun's key)
   WindowRun wrun;                 // the last recent window's parent-id run (queue_vote_cache)
+  Knobs kn;                       // (read_knobs)
   bool bits_inline = true;        // every committee <= kVoteInlineBits: the bitfields ride in the records
   bool ids_rows = false;          // (test knob) every attestation's ids in an explicit row
   PinBuf e_pin, e_pin_out;   // the epoch inputs' pinned staging; the results' pinned landing
@@ -1004,28 +1016,32 @@ struct EpochLaunch {
 };
 using EpochPrep = std::function<EpochLaunch*()>;
 
-// How a flush reaches the device (PZ_VOTE_PATH, read per flush so that one test process can
+// How a flush reaches the device (PZ_VOTE_PATH, read per call so that one test process can
 // run every path; A/B knob):
-//   direct (product)    no copy: the tally reads the walk's pinned queue in place (a 256-B
-//                       coalesced id load and the bitfield bytes per attestation wave);
+//   direct (product)    no copy: the tally reads the walk's pinned queue in place (one 64-B
+//                       record per attestation, votes.h VoteRec);
 //   segments            the queue arrays copied into a device pack by ONE multi-segment stage
 //                       kernel, then the tally (one launch more per flush: 1-3 % slower,
 //                       profiles/r04/replay_ab_words_r4k.txt);
 //   packed              round 3: the queue memcpy'd into one pinned arena first, one stage copy.
 enum VotePath { kVoteSegments, kVotePacked, kVoteDirect };
-static VotePath vote_path() {
-  const char* e = std::getenv("PZ_VOTE_PATH");
-  if (!e) return kVoteDirect;
-  if (!std::strcmp(e, "packed")) return kVotePacked;
-  if (!std::strcmp(e, "segments")) return kVoteSegments;
-  return kVoteDirect;
+static void read_knobs(Engine& g) {
+  auto is = [](const char* name, const char* v) {
+    const char* e = std::getenv(name);
+    return e && !std::strcmp(e, v);
+  };
+  g.kn.vote_path = is("PZ_VOTE_PATH", "packed") ? kVotePacked : is("PZ_VOTE_PATH", "segments") ? kVoteSegments : kVoteDirect;
+  g.kn.vote_groups = !is("PZ_VOTE_GROUPS", "0");
+  g.kn.vote_trace = std::getenv("PZ_VOTE_TRACE") != nullptr;
+  g.kn.epoch_pack_direct = is("PZ_EPOCH_PACK", "direct");
+  g.kn.epoch_prep_after = !is("PZ_EPOCH_PREP", "merged");
 }
 
 static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, const EpochPrep* prep = nullptr) {
   Engine::VoteQueue& Q = g.vq[g.vq_cur];
   if (Q.natt() == 0) return false;
   const bool gather = gq && g.world == 1;
-  const VotePath path = vote_path();
+  const VotePath path = (VotePath)g.kn.vote_path;
   const bool staged = path != kVoteDirect;  // a device copy of the queue
   PhaseTimer pt(g.prof[kProfFlush]);
   const uint64_t natt = Q.natt();
@@ -1047,8 +1063,7 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
   }
   // the grouped form (votes.h VoteGroup): the walk's queue read in place, every record in the run
   // form, each group within kVoteGroupWords id words (PZ_VOTE_GROUPS=0: A/B and test knob)
-  const char* vg = std::getenv("PZ_VOTE_GROUPS");
-  bool grouped = path == kVoteDirect && Q.groupable && !Q.grp.empty() && !(vg && !std::strcmp(vg, "0"));
+  bool grouped = path == kVoteDirect && Q.groupable && !Q.grp.empty() && g.kn.vote_groups;
   VoteGroup groups[kVoteMaxGroups];
   uint32_t nwaves = 0, ngroups = 0;
   if (grouped) {
@@ -1169,7 +1184,7 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
       EpochLaunch* el = (*prep)();
       hchk(launch_vote_words_count(v, el->a, r.s), "vote tally + epoch count");
       el->counted = true;
-    } else if (std::getenv("PZ_VOTE_TRACE") && r.grank == 0) {
+    } else if (g.kn.vote_trace && r.grank == 0) {
       // (tools/vote_trace.py: the first kVoteTraceFlushes flushes' per-wave phase stamps)
       if (!r.v_trace.p) {
         check(r.v_trace.alloc((size_t)kVoteTraceFlushes * kVoteTraceWaves * 8));
@@ -1560,8 +1575,7 @@ static EpochLaunch epoch_prepare_args(Engine& g, CState& C, size_t na, size_t nr
   check(g.e_pin.dev(r.dev, &hp));
   check(g.e_pin_out.dev(r.dev, &op));
   reinterpret_cast<volatile uint64_t*>(g.e_pin_out.p)[kScal + wn] = 0;  // (pooled memory: old words)
-  const char* pk = std::getenv("PZ_EPOCH_PACK");
-  const bool direct = in_place || (pk && !std::strcmp(pk, "direct"));
+  const bool direct = in_place || g.kn.epoch_pack_direct;
   uint8_t* d = static_cast<uint8_t*>(hp);
   if (!direct) {
     check(r.e_pack.alloc(total));
@@ -1873,9 +1887,8 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   // The tally is launched first and the epoch packed while it runs (its count pass then a
   // launch of its own): the pack's host time is off the justification loop's wait (totals_wait
   // 3.5 -> 2.4 ms per 10,000 blocks, profiles/r04/replay_prep_ab_r4n.txt).  PZ_EPOCH_PREP=merged
-  // (A/B, read per transition): pack first, the count blocks inside the tally launch.
-  const char* pe = std::getenv("PZ_EPOCH_PREP");
-  const bool prep_after = !(pe && !std::strcmp(pe, "merged"));
+  // (A/B, read per call): pack first, the count blocks inside the tally launch.
+  const bool prep_after = g.kn.epoch_prep_after;
   std::array<uint64_t, 4> tl{mono_ns(), 0, 0, 0};
   const bool gathered = flush_votes_enqueue(g, &q, one && !prep_after ? &prep : nullptr);
   tl[1] = mono_ns();
@@ -3014,6 +3027,7 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
   check(g.d_mrec.alloc(natt + 1));
   check(g.d_mout.alloc(natt * 64 + 64));
   const uint64_t mbatch = msg_batch();
+  read_knobs(g);
   // the tables grow once per call, not by doubling inside the walk
   g.slot_of.reserve(g.slot_of.size() + n);  // (plus any oblique hash shorter than 32 B: grows)
   g.hlog.reserve(g.hlog.size() + n + 2 * natt);

@@ -40,14 +40,9 @@ pz_vote_tally_kernel(VoteArgs a) {
 extern "C" __global__ void __launch_bounds__(kVoteWordMaxThreads)
 pz_vote_words_kernel(VoteWordArgs a) { vote_words_body(a, gridDim.x, blockIdx.x); }
 
-// Waves per tally block (PZ_VOTE_WAVES, A/B knob: 4, 8 or 16; default 16): more waves per block
-// sum more of the flush's totals in LDS before the device atomics.  (Read per launch, so that one
-// process can A/B it.)
-static uint32_t vote_word_threads() {
-  const char* e = std::getenv("PZ_VOTE_WAVES");
-  const int w = e ? std::atoi(e) : 16;
-  return (uint32_t)(w == 4 || w == 8 ? w : 16) * 64;
-}
+// Waves per block of the per-attestation form (16: more of the flush's totals summed in LDS
+// before the device atomics; 4, 8 and 16 measured level, profiles/r04/replay_ab_vote_waves_r4u.txt).
+static uint32_t vote_word_threads() { return 16 * 64; }
 
 hipError_t launch_vote_words(const VoteWordArgs& a, hipStream_t s) {
   if (!a.natt) return hipSuccess;
