@@ -96,9 +96,6 @@ __device__ __forceinline__ uint64_t wor64_dpp(uint64_t v) {
 // per parent.  Every wave of the flush adds to the same handful of totals (the transition's
 // window), and device-scope atomics on one address serialise (~12 ns each): summed per block
 // first, a flush issues one atomic per (block, parent) instead of one per (wave, parent).
-#ifndef PZ_VOTE_GATHER_WT
-#define PZ_VOTE_GATHER_WT 0
-#endif
 constexpr int kVoteLdsWords = 4;
 constexpr uint32_t kVoteLdsEmpty = 0xFFFFFFFFu;
 struct VoteLds {
@@ -468,27 +465,6 @@ __device__ __forceinline__ void vote_words_body(const VoteWordArgs& a, uint32_t 
   __syncthreads();
   if (!last) return;
   const int j = threadIdx.x;
-#if PZ_VOTE_GATHER_WT
-  // wave 0 alone: write-through (system-scope) stores of the totals and the flag, drained, then
-  // the sequence word -- no L2 write-back fence
-  if (j < 64) {
-    const uint32_t sl = a.gq.slot[j];
-    const uint64_t x =
-        sl == 0xFFFFFFFFu ? 0 : __hip_atomic_load(&a.totals[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.gather_out[j], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (j == 0) {
-      __hip_atomic_store(&a.gather_out[kJustifySlots],
-                         __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (j == 0)
-      __hip_atomic_store(&a.gather_out[kJustifySlots + 1], a.gather_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  PZ_VSTAMP(7)
-  return;
-#endif
   if (j < kJustifySlots) {
     const uint32_t sl = a.gq.slot[j];
     a.gather_out[j] =
