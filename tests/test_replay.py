@@ -550,6 +550,26 @@ def test_gpu_sharded_chain_configs4_full_vs_c_port(world):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nval,ncomm", [(131072, 9), (262144, 17), (524288, 33)])
+def test_gpu_replay_wide_committees_vs_c_port(nval, ncomm):
+    """Larger validator sets than configs[4]: 9 slot-0 committees per block (grouped tally),
+    then 17 and 33 (more than kVoteMaxGroups = 16 committees in a flush: the per-attestation
+    form), of up to 249 members (every bitfield inline in the 64-B record), over 130 blocks (two
+    transitions) against the C restatement."""
+    from prysm_amd.blockchain import BeaconChain, serialize_blocks
+    from replay_port_helpers import mismatches, port_replay
+    sizes = synth.genesis_committee_sizes(nval)
+    assert len(sizes) == ncomm and max(k for _, k in sizes) <= 256
+    blocks = synth.chain_blocks(nval, 130, seed=11)
+    data, offs = serialize_blocks(blocks)
+    ch = BeaconChain(nval)
+    br, ar = ch.process_serialized(data, offs)
+    assert int(br["transition"].sum()) == 2
+    out, port_roots = port_replay(data, offs, nval, len(ar))
+    assert mismatches(br, ar, ch.roots(), out, port_roots) == []
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("path,epack,bits,ids,groups", [("segments", "copy", "inline", "run", "1"),
                                                          ("packed", "copy", "rows", "rows", "1"),
                                                          ("direct", "direct", "inline", "run", "1"),
