@@ -51,7 +51,7 @@ constexpr uint32_t kVoteInlineBits = 256;  // committees up to this size keep th
 // words hit 64 times a flush: 131 k serialising atomics per transition at 65,536 validators).
 // Needs every record in the run form (the id set of a run is the range [s0, s0 + popcount(step)])
 // with its bitfield inline; a group spans at most kVoteGroupWords id words.
-constexpr int kVoteMaxGroups = 16;
+constexpr int kVoteMaxGroups = 64;  // (kernel arguments: 2 KB of the 4 KB limit)
 constexpr int kVoteGroupWords = 4;
 struct VoteGroup {
   uint32_t cb, k;      // the committee

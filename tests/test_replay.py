@@ -550,14 +550,16 @@ def test_gpu_sharded_chain_configs4_full_vs_c_port(world):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("groups", ["1", "0"])
 @pytest.mark.parametrize("nval,ncomm", [(131072, 9), (262144, 17), (524288, 33)])
-def test_gpu_replay_wide_committees_vs_c_port(nval, ncomm):
-    """Larger validator sets than configs[4]: 9 slot-0 committees per block (grouped tally),
-    then 17 and 33 (more than kVoteMaxGroups = 16 committees in a flush: the per-attestation
-    form), of up to 249 members (every bitfield inline in the 64-B record), over 130 blocks (two
-    transitions) against the C restatement."""
+def test_gpu_replay_wide_committees_vs_c_port(nval, ncomm, groups, monkeypatch):
+    """Larger validator sets than configs[4]: 9, 17 and 33 slot-0 committees per block, each a
+    group of the grouped tally (votes.h kVoteMaxGroups), of up to 249 members (every bitfield
+    inline in the 64-B record), over 130 blocks (two transitions) against the C restatement;
+    PZ_VOTE_GROUPS=0 runs the per-attestation form over the same chains."""
     from prysm_amd.blockchain import BeaconChain, serialize_blocks
     from replay_port_helpers import mismatches, port_replay
+    monkeypatch.setenv("PZ_VOTE_GROUPS", groups)
     sizes = synth.genesis_committee_sizes(nval)
     assert len(sizes) == ncomm and max(k for _, k in sizes) <= 256
     blocks = synth.chain_blocks(nval, 130, seed=11)
