@@ -135,8 +135,9 @@ __device__ __forceinline__ uint64_t range_word_mask(uint32_t lo, uint32_t hi, ui
 // parents this voter is new for.  With M the parents any voter of the wave is new for: when
 // every voter is new for all of M or for none of it (the usual cases: a new voter, or a voter
 // seen one block before, whose window has moved by one parent), each of M's parents gains the
-// new voters' balance sum (lane j adds it for parent bit j); otherwise, per parent of M, the sum
-// of the voters new for it.  The sums go to the block's LDS totals (L).  Chunk 0 marks the
+// new voters' balance sum (lane j adds it for parent bit j); otherwise, per distinct new-parent
+// mask among the voters, their sum to each of its parents.  The sums go to the block's LDS
+// totals (L).  Chunk 0 marks the
 // parents' map entries present (core.go:322-326).
 // (tools/tally_probe.hip: with `tr` non-null each wave stamps its phases, draining its memory
 // operations first; the product passes none and the stamps compile away)
