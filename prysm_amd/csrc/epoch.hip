@@ -2075,6 +2075,9 @@ PZ_STREAM_KERNEL(pz_epoch_stream_lds_se16_kernel, 1024 + 16384 + 262144, 1024)
 PZ_STREAM_KERNEL(pz_epoch_stream_lds_se16_win_kernel, 1024 + 16384 + 131072 + 262144, 1024)
 PZ_STREAM_KERNEL(pz_epoch_stream_se16_b32_kernel, 1024 + 16384 + 524288, 256)  // u32 balance offsets
 PZ_STREAM_KERNEL(pz_epoch_stream_se16_b32_win_kernel, 1024 + 16384 + 131072 + 524288, 256)
+// (A/B, variant 1 << 22) the LDS form on the u32 offsets: the last bitfield staged per block
+PZ_STREAM_KERNEL(pz_epoch_stream_lds_se16_b32_kernel, 1024 + 16384 + 262144 + 524288, 1024)
+PZ_STREAM_KERNEL(pz_epoch_stream_lds_se16_b32_win_kernel, 1024 + 16384 + 131072 + 262144 + 524288, 1024)
 #undef PZ_STREAM_KERNEL
 
 // The single-launch step (one instance): no occupancy target (a few dozen blocks), so the
@@ -2265,7 +2268,7 @@ hipError_t launch_epoch_fwin(const EpochArgs& a, const FusedArgs& f, hipStream_t
 static bool ablation_no_lastco() {
   return g_fused_variant && g_fused_variant != 4096 && g_fused_variant != 32768 && g_fused_variant != 65536 &&
          g_fused_variant != 131072 && g_fused_variant != 262144 && (g_fused_variant >> 20) != 1 &&
-         g_fused_variant != (1 << 21);
+         g_fused_variant != (1 << 21) && g_fused_variant != (1 << 22);
 }
 
 static bool use_lds_form(const EpochArgs& a, const FusedArgs& f);
@@ -2340,6 +2343,27 @@ hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream
     else
       hipLaunchKernelGGL(pz_epoch_stream_se16_b32_kernel, dim3(nb), dim3(256), 0, s, a, f, f.pre, a.boffs,
                          a.total_deposit, f.items, f.catt_offs, f.catt, 0u);
+    return hipGetLastError();
+  }
+  if (f.bal32 && variant == (1 << 22) && f.se16 && !f.lastco && a.ninst > 1 && f.last_max &&
+      f.last_max <= kStreamLdsMax) {
+    // (A/B) the LDS form of the streaming pass on the u32 offsets: each block stages its
+    // instance's last bitfield once and looks the reward bits up there
+    const uint32_t bpi = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(f.nitems, kStreamLdsBlocks / a.ninst));
+    const size_t lds = (size_t)((f.last_max + 15 + 16) / 16) * 16;
+    static std::once_flag once;
+    std::call_once(once, [] {
+      (void)hipFuncSetAttribute((const void*)pz_epoch_stream_lds_se16_b32_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsMax + 64);
+      (void)hipFuncSetAttribute((const void*)pz_epoch_stream_lds_se16_b32_win_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsMax + 64);
+    });
+    if (f.win_fused)
+      hipLaunchKernelGGL(pz_epoch_stream_lds_se16_b32_win_kernel, dim3((uint32_t)(a.ninst * bpi)), dim3(1024), lds, s,
+                         a, f, f.pre, a.boffs, a.total_deposit, f.items, f.catt_offs, f.catt, bpi);
+    else
+      hipLaunchKernelGGL(pz_epoch_stream_lds_se16_b32_kernel, dim3((uint32_t)(a.ninst * bpi)), dim3(1024), lds, s, a,
+                         f, f.pre, a.boffs, a.total_deposit, f.items, f.catt_offs, f.catt, bpi);
     return hipGetLastError();
   }
   if (f.bal32 && variant == (1 << 21) && f.se16 && !f.lastco) {  // (A/B) two pieces per wave

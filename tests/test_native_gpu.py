@@ -116,12 +116,13 @@ def test_native_epoch_bal32_offsets(n, B, density):
     _check(ne, inst, steps=3)
 
 
-@pytest.mark.parametrize("variant", [131072, 4096, 1 << 21])
+@pytest.mark.parametrize("variant", [131072, 4096, 1 << 21, 1 << 22])
 @pytest.mark.parametrize("n,B", [(65536, 5), (32768, 9), (4097, 3)])
 def test_native_epoch_bal32_forms(n, B, variant):
     """The u32-offset step's A/B forms: the streaming pass (persistent pipelined waves, 131072),
-    the XCD-aware grid (4096) and two pieces per wave (1 << 21), with the winners in the waves:
-    three steps against the oracle."""
+    the XCD-aware grid (4096), two pieces per wave (1 << 21) and the streaming pass with the
+    last bitfield staged in LDS (1 << 22), with the winners in the waves: three steps against
+    the oracle."""
     inst = _inst(n, B, False)
     ne = NativeEpoch(inst, device=0)
     assert ne.balance_bytes == 4
