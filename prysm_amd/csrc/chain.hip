@@ -638,6 +638,19 @@ struct DigestBufs {
 // a chain over a pz_comm (pz_chain_new_comm) gives each rank the
 // 64-aligned validator range [lo, hi): its balances, its columns of every vote-cache voter
 // bitmap and its partial VoteTotalDeposit sums, and its part of every epoch.
+// Device buffers a growth replaced: freed with the chain, not at the growth (a hipFree waits for
+// the whole device, and the copies out of the old buffer are still queued; growth is geometric,
+// so what is kept is at most the live size).
+struct Retired {
+  std::vector<void*> p;
+  void keep(void* x) {
+    if (x) p.push_back(x);
+  }
+  ~Retired() {
+    for (void* x : p) (void)hipFree(x);
+  }
+};
+
 struct RankDev {
   int dev = 0, grank = 0;
   hipStream_t s = nullptr;
@@ -738,6 +751,7 @@ struct Engine {
   uint32_t bf_stride = 4;         // the vote queue's bitfield row: >= every committee's bytes, x4
   uint64_t trail_gen = 0;         // bumped whenever the trail is rebuilt (WindowRun's key)
   WindowRun wrun;                 // the last recent window's parent-id run (queue_vote_cache)
+  Retired retired;                // grown-out device buffers (freed with the chain)
   Knobs kn;                       // (read_knobs)
   bool bits_inline = true;        // every committee <= kVoteInlineBits: the bitfields ride in the records
   bool ids_rows = false;          // (test knob) every attestation's ids in an explicit row
@@ -951,13 +965,20 @@ static void grow_slots(Engine& g, uint64_t nc) {
         hchk(hipMemcpyAsync(tt.p, r.totals.p, g.cap * 8, hipMemcpyDeviceToDevice, r.s), "D2D");
         hchk(hipMemcpyAsync(pr.p, r.present.p, g.cap, hipMemcpyDeviceToDevice, r.s), "D2D");
       }
-      hchk(hipStreamSynchronize(r.s), "sync");
+      // (no stream sync: the old arrays are kept until the chain goes, so the queued copies and
+      // tallies still reading them are safe)
       std::swap(r.bm.p, bm.p);
       std::swap(r.bm.n, bm.n);
       std::swap(r.totals.p, tt.p);
       std::swap(r.totals.n, tt.n);
       std::swap(r.present.p, pr.p);
       std::swap(r.present.n, pr.n);
+      g.retired.keep(bm.p);
+      g.retired.keep(tt.p);
+      g.retired.keep(pr.p);
+      bm.p = nullptr;
+      tt.p = nullptr;
+      pr.p = nullptr;
     });
     g.cap = nc;
   }
@@ -2650,9 +2671,10 @@ static void sync_hash_log(Engine& g) {
     DevArr<uint8_t> nb;
     check(nb.alloc(std::max<uint64_t>(g.hlog.capacity() * 32, 2 * g.d_hlog.n)));  // (the call's reserve: once a call)
     if (g.d_hlog_n) hchk(hipMemcpyAsync(nb.p, g.d_hlog.p, g.d_hlog_n * 32, hipMemcpyDeviceToDevice, g.ms), "D2D");
-    hchk(hipStreamSynchronize(g.ms), "sync");
     std::swap(g.d_hlog.p, nb.p);
     std::swap(g.d_hlog.n, nb.n);
+    g.retired.keep(nb.p);  // (the queued copy reads it)
+    nb.p = nullptr;
   }
   hchk(hipMemcpyAsync(g.d_hlog.p + g.d_hlog_n * 32, g.hlog[g.d_hlog_n].b, (n - g.d_hlog_n) * 32,
                       hipMemcpyHostToDevice, g.ms), "H2D hash log");
@@ -2667,9 +2689,10 @@ static void sync_trail(Engine& g) {
     DevArr<uint32_t> nb;
     check(nb.alloc(std::max<uint64_t>(g.trail.capacity(), 2 * g.d_trail.n)));
     if (g.d_trail_n) hchk(hipMemcpyAsync(nb.p, g.d_trail.p, g.d_trail_n * 4, hipMemcpyDeviceToDevice, g.ms), "D2D");
-    hchk(hipStreamSynchronize(g.ms), "sync");
     std::swap(g.d_trail.p, nb.p);
     std::swap(g.d_trail.n, nb.n);
+    g.retired.keep(nb.p);  // (the queued copy reads it)
+    nb.p = nullptr;
   }
   hchk(hipMemcpyAsync(g.d_trail.p + g.d_trail_n, g.trail.data() + g.d_trail_n, (n - g.d_trail_n) * 4,
                       hipMemcpyHostToDevice, g.ms), "H2D trail");
@@ -2711,9 +2734,10 @@ static void msg_send(Engine& g) {
     DevArr<uint8_t> nb;
     check(nb.alloc(std::max<uint64_t>(g.m_var.capacity() + 4, 2 * g.d_mvar.n)));  // (once a call, bar a regrowth)
     if (g.m_var_sent) hchk(hipMemcpyAsync(nb.p, g.d_mvar.p, g.m_var_sent, hipMemcpyDeviceToDevice, g.ms), "D2D");
-    hchk(hipStreamSynchronize(g.ms), "sync");
     std::swap(g.d_mvar.p, nb.p);
     std::swap(g.d_mvar.n, nb.n);
+    g.retired.keep(nb.p);  // (the queued copy reads it)
+    nb.p = nullptr;
   }
   if (g.m_var.n > g.m_var_sent)
     hchk(hipMemcpyAsync(g.d_mvar.p + g.m_var_sent, g.m_var.data() + g.m_var_sent, g.m_var.n - g.m_var_sent,
