@@ -1066,10 +1066,13 @@ def replay_leg(args, torch, dist, dev, rank, world):
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    # three replays, each of the whole chain on a fresh chain (genesis -- shuffle + uploads -- is
-    # not part of a replay): the median, so one descheduled host thread does not make the line
+    # five replays, each of the whole chain on a fresh chain (genesis -- shuffle + uploads -- is
+    # not part of a replay): the median, so one descheduled host thread or a slow first replay
+    # (the box's host warming up: 12.7 / 11.5 / 10.9 ms in profiles/r04/bench_r4ap.json) does not
+    # make the line
     walls = []
-    for k in range(3):
+    NREP = 5
+    for k in range(NREP):
         ch = BeaconChain(nval, dev)
         torch.cuda.synchronize(dev)
         if world > 1:
@@ -1079,7 +1082,7 @@ def replay_leg(args, torch, dist, dev, rank, world):
         torch.cuda.synchronize(dev)
         w_k = time.perf_counter() - t0
         walls.append(max_over_ranks(w_k, torch, dist, dev) if world > 1 else w_k)
-        if k < 2:
+        if k < NREP - 1:
             del ch
     wall = float(np.median(walls))
     # State roots (types/state.go:138-149, 237-248) of the replayed chain: the 1.7 MB
@@ -1099,7 +1102,7 @@ def replay_leg(args, torch, dist, dev, rank, world):
             for s, t in zip(br["status"], br["transition"])]
     out = {"metric": "sync-replay blocks/s", "value": nb * world / wall, "unit": "blocks/s",
            "ms_per_block": wall / nb * 1e3, "replay_walls_ms": [round(x * 1e3, 3) for x in walls],
-           "timing": "median of 3 replays of the whole chain, each on a fresh chain",
+           "timing": "median of 5 replays of the whole chain, each on a fresh chain",
            "config": {"workload": "sync replay: block + 5 x (attestation Hash, Key, message digest) + vote "
                                   "tally per block, stateRecalc every 64 blocks (BASELINE configs[4])",
                       "validators": nval, "blocks_per_gpu": nb, "attestations_per_block": 5,
