@@ -311,8 +311,8 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                      "traffic_source": ("%s (every pz_epoch_* kernel of the %d x %d step)"
                                         % (pmc_summary_path(workload), nval, ninst)) if workload else None,
                      "traffic_frac": (traffic / (step_ms * 1e-3) / HBM_PEAK) if traffic else None,
-                     "kernel": ("epoch step: pz_epoch_pre (bit count, winner reset) + pz_epoch_fused_se16_b32 (one "
-                                "pass: classify, crosslink tallies, the winners in the waves, rewards on the u32 "
+                     "kernel": ("epoch step: pz_epoch_window_b32_s16 (ONE launch: bit count, last bitfield into "
+                                "LDS, classify, crosslink tallies per committee in LDS, winners, rewards on the u32 "
                                 "balance offsets, next-cycle sum); device time of the whole step" if one_pass else
                                 "epoch step (count+winner+compact+reward, device time of the whole step)"),
                      "step_device_ms": step_ms,
@@ -520,13 +520,14 @@ def epoch_parity(inst, dev):
 def epoch_single_instance(args, torch, dev, nval, shuffled):
     """the latency of ONE epoch instance (B = 1) at configs[2]'s size
     (2.9 MB of algorithmic traffic): the single-launch step (pz_epoch_one_kernel), device time
-    by HIP events, median over the steps; beside it the three-launch step (pre + fused + mid)
-    on the same instance."""
+    by HIP events, median over the steps; beside it the window pass (the multi-instance one-pass
+    kernel, pz_epoch_options.window_only) on the same instance."""
     from prysm_amd import _lib, synth
     from prysm_amd.native import NativeEpoch
 
-    def measure():
-        de = NativeEpoch(synth.epoch_batch(nval, 1, seed=3, shuffled=shuffled), device=dev.index)
+    def measure(window_only=False):
+        de = NativeEpoch(synth.epoch_batch(nval, 1, seed=3, shuffled=shuffled), device=dev.index,
+                         window_only=window_only)
         stream = torch.cuda.ExternalStream(de.shard(0)[3], device=dev)
         for _ in range(args.warmup + 20):
             de.step()
@@ -554,16 +555,12 @@ def epoch_single_instance(args, torch, dev, nval, shuffled):
 
     ms, wall_ms, b2b = measure()
     floor = event_pair_floor(args, torch, dev)
-    old = _lib.lib.dll.pz_debug_set_fused_variant(128)  # the single launch off: pre + fused + mid
-    try:
-        ms3, wall3, b2b3 = measure()
-    finally:
-        _lib.lib.dll.pz_debug_set_fused_variant(old)
+    ms3, wall3, b2b3 = measure(window_only=True)
     return {"validators": nval, "instances_per_step": 1, "path": "pz_epoch_one_kernel (single launch)",
             "device_ms_median": ms, "wall_ms_per_step": wall_ms, "back_to_back_ms_per_step": b2b,
             "device_ms_net_of_event_floor": ms - floor["empty_ms"], "event_floor": floor,
             "validator_epochs_per_s": nval / (ms * 1e-3),
-            "three_launches": {"device_ms_median": ms3, "wall_ms_per_step": wall3, "back_to_back_ms_per_step": b2b3}}
+            "window_pass": {"device_ms_median": ms3, "wall_ms_per_step": wall3, "back_to_back_ms_per_step": b2b3}}
 
 
 def event_pair_floor(args, torch, dev):

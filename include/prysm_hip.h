@@ -78,6 +78,10 @@ int pz_blake2b512_batch(const uint8_t* msgs, const uint64_t* offsets, uint64_t n
  * for the rest of the batch.  Default 65,536; UINT64_MAX keeps everything on
  * the GPU.  Returns the previous value.  The pz_dev_* forms never leave the device. */
 uint64_t pz_set_serial_threshold(uint64_t bytes);
+/* Host threads the library uses beside the GPU (the serial hashes of long messages, the chain
+ * engine's parse and result copies): 0 (the default) min(16, the process's CPU affinity), else n
+ * (at most 256).  Returns the previous setting.  A placement control, not a reference API. */
+uint32_t pz_set_host_threads(uint32_t n);
 
 /* A batch of at most `compressions` BLAKE2b compressions in all (a drop-in Hash() call: one
  * 100-600 B message is 1-5) is hashed on the calling thread: the GPU route's launch, PCIe
@@ -499,6 +503,16 @@ typedef struct pz_epoch_host {
 #define PZ_LAYOUT_TWOPASS 2  /* committee order as AUTO, but the two-pass step (A/B, tests) */
 typedef struct pz_epoch_state pz_epoch_state;
 int  pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epoch_state** out);
+/* The state's options (no reference counterpart: placement and test controls of this library;
+ * NULL or pz_epoch_state_new: every field 0).  There are no environment switches. */
+typedef struct pz_epoch_options {
+  uint64_t rebase_period;  /* u32-offset balances: steps between re-bases of the offsets (0: 2^29,
+                              the product; larger values are clamped to it) */
+  int window_only;         /* 1: one instance on one rank also takes the window pass (the
+                              multi-instance one-pass kernel) instead of pz_epoch_one_kernel */
+} pz_epoch_options;
+int  pz_epoch_state_new_opts(pz_comm* comm, int device, const pz_epoch_host* h, const pz_epoch_options* opts,
+                             pz_epoch_state** out);
 int  pz_epoch_state_step(pz_epoch_state* st);
 int  pz_epoch_state_sync(pz_epoch_state* st);
 /* Local rank `local`'s validator range, device and compute stream (for event timing). */
@@ -637,6 +651,17 @@ int  pz_chain_new_from_state(const uint8_t* cstate, uint64_t len, const uint8_t*
  * only: every validator stays active, so rank == index.  `comm` must outlive the chain. */
 int  pz_chain_new_comm(uint64_t nval, pz_comm* comm, pz_chain** out);
 void pz_chain_free(pz_chain* chain);
+/* The engine's options (no reference counterpart: placement and test controls; every field 0
+ * is the product's choice).  Set them before the chain's first pz_chain_process_blocks call. */
+typedef struct pz_chain_options {
+  uint64_t msg_batch;    /* processAttestation messages digested in batches of at least this many,
+                            sent while the walk goes on (0: one batch at the end of the call) */
+  uint32_t tally_forms;  /* tests: the vote-cache tally's general forms forced (PZ_TALLY_*) */
+} pz_chain_options;
+#define PZ_TALLY_PER_ATTESTATION 1u  /* the per-attestation tally instead of the committee-grouped one */
+#define PZ_TALLY_BITS_ROWS       2u  /* every bitfield in the row array, none inline in its record */
+#define PZ_TALLY_ID_ROWS         4u  /* every attestation's parent ids as an explicit row, no run */
+int  pz_chain_set_options(pz_chain* chain, const pz_chain_options* opts);
 /* Number of attestations in a batch of serialized blocks (host only; sizes att_out). */
 int  pz_count_attestations(const uint8_t* blocks, const uint64_t* offsets, uint64_t n, uint64_t* count);
 /* att_out: capacity att_cap >= the total number of attestations in the batch.

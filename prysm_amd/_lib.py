@@ -58,6 +58,8 @@ SIGNATURES = {
     "pz_version": [],
     "pz_blake2b512_batch": [vp, vp, u64, vp, u32],
     "pz_set_serial_threshold": [u64],
+    "pz_set_host_threads": [u32],
+    "pz_chain_set_options": [vp, vp],
     "pz_set_small_batch_threshold": [u64],
     "pz_dev_blake2b512_batch": [vp, vp, u64, vp, u32, vp],
     "pz_dev_blake2b512_fixed": [vp, u64, u64, u64, vp, u32, vp],
@@ -114,6 +116,7 @@ SIGNATURES = {
     "pz_comm_free": [vp],
     "pz_comm_blake2b512_batch": [vp, vp, vp, u64, vp, u32],
     "pz_epoch_state_new": [vp, ctypes.c_int, vp, vp],
+    "pz_epoch_state_new_opts": [vp, ctypes.c_int, vp, vp, vp],
     "pz_epoch_state_step": [vp],
     "pz_epoch_state_sync": [vp],
     "pz_epoch_state_shard": [vp, ctypes.c_int, c_u64p, c_u64p, c_intp, vp],
@@ -150,6 +153,19 @@ class EpochHost(ctypes.Structure):
         ("committee", vp), ("coffs", vp), ("ncomm", u64), ("att_comm", vp), ("att_shard", vp),
         ("nrec", ctypes.c_uint32), ("rec_dynasty", vp), ("layout", ctypes.c_uint32),
     ]
+
+
+class ChainOptions(ctypes.Structure):
+    """Mirror of ``pz_chain_options`` (include/prysm_hip.h)."""
+    _fields_ = [("msg_batch", u64), ("tally_forms", u32)]
+
+
+TALLY_PER_ATTESTATION, TALLY_BITS_ROWS, TALLY_ID_ROWS = 1, 2, 4  # pz_chain_options.tally_forms
+
+
+class EpochOptions(ctypes.Structure):
+    """Mirror of ``pz_epoch_options`` (include/prysm_hip.h)."""
+    _fields_ = [("rebase_period", u64), ("window_only", ctypes.c_int)]
 
 
 class VoteBatch(ctypes.Structure):
@@ -195,7 +211,7 @@ class AttCheckBatch(ctypes.Structure):
 SCAL_POP, SCAL_NACT, SCAL_ERR_XL, SCAL_ERR_RWD, SCAL_APPLIED, SCAL_NEXT_BAL, SCAL_MAXIDX1, SCAL_NOMATCH = range(8)
 SCAL_COUNT = 8
 KIND_ACTIVE, KIND_EXITED, KIND_QUEUED = 0, 1, 2
-_RESTYPES = {"pz_last_error": ctypes.c_char_p, "pz_chain_free": None, "pz_set_serial_threshold": u64,
+_RESTYPES = {"pz_last_error": ctypes.c_char_p, "pz_chain_free": None, "pz_set_serial_threshold": u64, "pz_set_host_threads": u32,
              "pz_shutdown": None, "pz_state_free": None, "pz_set_small_batch_threshold": u64, "pz_comm_free": None, "pz_epoch_state_free": None,
              "pz_wire_validators_bound": u64, "pz_wire_scratch_bytes": u64,
              "pz_wire_attestations_bound": u64, "pz_wire_attestations_scratch_bytes": u64}
@@ -209,10 +225,12 @@ class _Lib:
 
     def _load(self):
         if self._dll is None:
-            if not os.path.exists(library_path):
-                raise PzError(PZ_EDEVICE, "HIP library not built: %s (run __graft_entry__.build())"
-                              % library_path)
-            dll = ctypes.CDLL(library_path)
+            # PZ_LIB: another build of the library (tests marked `ab` and tools/ load the A/B
+            # library, make -C prysm_amd/csrc ab); the product path loads the in-tree product build
+            path = os.environ.get("PZ_LIB") or library_path
+            if not os.path.exists(path):
+                raise PzError(PZ_EDEVICE, "HIP library not built: %s (run __graft_entry__.build())" % path)
+            dll = ctypes.CDLL(path)
             for name, args in SIGNATURES.items():
                 fn = getattr(dll, name)
                 fn.argtypes = args

@@ -95,10 +95,12 @@ def serialize_blocks(blocks):
 class BeaconChain:
     """A chain from the genesis states of ``nval`` validators on one GPU."""
 
-    def __init__(self, nval, device=None, comm=None):
+    def __init__(self, nval, device=None, comm=None, msg_batch=0, tally_forms=0):
         """``comm`` (a ``prysm_amd.native.Comm``): one chain over the communicator's ranks,
         each holding a validator range of the balances, the vote cache and the epoch
-        (pz_chain_new_comm)."""
+        (pz_chain_new_comm).  ``msg_batch`` / ``tally_forms``:
+        pz_chain_options (message batches sent during the walk; the tally's general forms
+        forced, _lib.TALLY_*)."""
         idx = 0
         if device is not None:
             import torch
@@ -111,6 +113,9 @@ class BeaconChain:
         else:
             lib.call("pz_chain_new", nval, idx, ctypes.byref(self._h))
         self.nval = nval
+        if msg_batch or tally_forms:
+            opts = _lib.ChainOptions(int(msg_batch), int(tally_forms))
+            lib.call("pz_chain_set_options", self._h, ctypes.byref(opts))
 
     @classmethod
     def from_state(cls, crystallized_bytes, saved_hashes=(), device=None):

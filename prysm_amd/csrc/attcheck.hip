@@ -92,7 +92,6 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_kernel(pz_at
 // (tools/attcheck_probe.py, profiles/r02/attcheck_probe_r2o.txt).
 // (The bitfield byte stays a cached load: a 64-B line holds ~2.5 bitfields, so a nontemporal
 // byte load re-fetches it: 87 us against 67, profiles/r02/attcheck_probe_ntb_r2o.txt.)
-template <bool NT, bool NTS = false>
 __device__ __forceinline__ void att_check_x2_body(const pz_att_check_batch& b) {
   const uint64_t i = 2 * ((uint64_t)blockIdx.x * kThreads + threadIdx.x);
   if (i >= b.natt) return;
@@ -108,12 +107,9 @@ __device__ __forceinline__ void att_check_x2_body(const pz_att_check_batch& b) {
     return;
   }
   auto ld2 = [](const uint64_t* p) {
-    if (NT) {
-      typedef unsigned long long v2u __attribute__((ext_vector_type(2)));
-      const v2u x = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
-      return make_ulonglong2(x.x, x.y);
-    }
-    return *reinterpret_cast<const ulonglong2*>(p);
+    typedef unsigned long long v2u __attribute__((ext_vector_type(2)));
+    const v2u x = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
+    return make_ulonglong2(x.x, x.y);
   };
   const ulonglong2 s = ld2(b.slot + i), bs = ld2(b.block_slot + i), js = ld2(b.justified_slot + i);
   const ulonglong2 nob = ld2(b.n_oblique + i), sh = ld2(b.shard_id + i), bo = ld2(b.boffs + i);
@@ -130,30 +126,16 @@ __device__ __forceinline__ void att_check_x2_body(const pz_att_check_batch& b) {
   uint64_t p0, p1;
   check_one(b, s.x, bs.x, js.x, nob.x, sh.x, bo.x, bo.y, &st0, &c0, &p0, lb0);
   check_one(b, s.y, bs.y, js.y, nob.y, sh.y, bo.y, bo2, &st1, &c1, &p1, lb1);
-  if (NTS) {  // A/B: nontemporal output stores (each output is written once, read by the host)
-    typedef int v2i __attribute__((ext_vector_type(2)));
-    typedef unsigned long long v2u __attribute__((ext_vector_type(2)));
-    __builtin_nontemporal_store(v2i{st0, st1}, reinterpret_cast<v2i*>(b.status + i));
-    if (b.committee) __builtin_nontemporal_store(v2i{(int)c0, (int)c1}, reinterpret_cast<v2i*>(b.committee + i));
-    if (b.parents_start) __builtin_nontemporal_store(v2u{p0, p1}, reinterpret_cast<v2u*>(b.parents_start + i));
-    return;
-  }
   *reinterpret_cast<int2*>(b.status + i) = make_int2(st0, st1);
   if (b.committee) *reinterpret_cast<uint2*>(b.committee + i) = make_uint2(c0, c1);
   if (b.parents_start) *reinterpret_cast<ulonglong2*>(b.parents_start + i) = make_ulonglong2(p0, p1);
 }
 
+// (Measured and dropped: default-policy column loads, 80 against 67 us; nontemporal output stores,
+// level -- profiles/r02/attcheck_probe_r2o.txt.)
 extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_x2_kernel(pz_att_check_batch b) {
-  att_check_x2_body<true>(b);
+  att_check_x2_body(b);
 }
-extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_x2_cached_kernel(pz_att_check_batch b) {
-  att_check_x2_body<false>(b);  // A/B: default-policy column loads
-}
-extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_x2_nts_kernel(pz_att_check_batch b) {
-  att_check_x2_body<true, true>(b);  // A/B: nontemporal output stores
-}
-
-static int g_attcheck_variant = 0;  // tools/ A/B only: 1 default-policy column loads, 2 nontemporal stores
 
 int check_args(const pz_att_check_batch* b) {
   if (!b) return fail(PZ_EINVAL, "batch is null");
@@ -175,15 +157,8 @@ hipError_t launch_att_check(const pz_att_check_batch& b, hipStream_t s) {
                   (!b.last_byte || (reinterpret_cast<uintptr_t>(b.last_byte) & 1) == 0);
   if (x2) {
     const uint64_t lanes = (b.natt + 1) / 2;
-    if (g_attcheck_variant & 1)
-      hipLaunchKernelGGL(pz_att_check_x2_cached_kernel, dim3((uint32_t)((lanes + kThreads - 1) / kThreads)),
-                         dim3(kThreads), 0, s, b);
-    else if (g_attcheck_variant & 2)
-      hipLaunchKernelGGL(pz_att_check_x2_nts_kernel, dim3((uint32_t)((lanes + kThreads - 1) / kThreads)),
-                         dim3(kThreads), 0, s, b);
-    else
-      hipLaunchKernelGGL(pz_att_check_x2_kernel, dim3((uint32_t)((lanes + kThreads - 1) / kThreads)), dim3(kThreads),
-                         0, s, b);
+    hipLaunchKernelGGL(pz_att_check_x2_kernel, dim3((uint32_t)((lanes + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                       s, b);
   } else {
     hipLaunchKernelGGL(pz_att_check_kernel, dim3((uint32_t)((b.natt + kThreads - 1) / kThreads)), dim3(kThreads), 0,
                        s, b);
@@ -249,9 +224,3 @@ int pz_check_attestations(const pz_att_check_batch* hb) {
 }
 
 }  // extern "C"
-
-extern "C" int pz_debug_set_attcheck_variant(int v) {
-  const int old = pz::g_attcheck_variant;
-  pz::g_attcheck_variant = v;
-  return old;
-}

@@ -504,7 +504,11 @@ pz_b2b_attmsg_kernel(const uint8_t* __restrict__ hlog, const uint32_t* __restric
 }
 
 // ---- host-side launchers (declared in blake2b_kernels.h) ---------------------------------
-static int g_fixed_variant = 1;  // 1: persistent LDS-DMA kernel (+ plain tail), 0: plain grid
+#ifdef PZ_AB_BUILD
+static int g_fixed_variant = 1;  // (A/B library) 1: persistent LDS-DMA kernel (+ plain tail), 0: plain grid
+#else
+constexpr int g_fixed_variant = 1;
+#endif
 
 static int cu_count() {
   static int cached[64] = {0};
@@ -547,11 +551,13 @@ hipError_t launch_b2b_fixed(const uint8_t* msgs, uint64_t stride, uint64_t len, 
   return launch_plain(msgs + nfull * stride, stride, len, n - nfull, out + nfull * out_bytes, out_bytes, stream);
 }
 
+#ifdef PZ_AB_BUILD
 int set_fixed_variant(int v) {
   const int old = g_fixed_variant;
   g_fixed_variant = v;
   return old;
 }
+#endif
 
 hipError_t launch_b2b_csr(const uint8_t* msgs, const uint64_t* offsets, uint64_t n, uint8_t* out,
                           uint32_t out_bytes, hipStream_t stream) {

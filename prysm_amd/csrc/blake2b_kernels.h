@@ -32,5 +32,7 @@ hipError_t launch_b2b_attmsg(const uint8_t* hlog, const uint32_t* trail, const A
 namespace pz {
 // Kernel variant for the fixed-length path (1: persistent LDS-DMA, 0: plain grid); returns the
 // previous one.  Exposed for in-process A/B timing (pz_debug_set_hash_variant).
+#ifdef PZ_AB_BUILD
 int set_fixed_variant(int v);
+#endif
 }  // namespace pz

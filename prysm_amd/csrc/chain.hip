@@ -586,17 +586,17 @@ struct PinVec {
   }
 };
 
-constexpr uint64_t kVoteTraceFlushes = 256, kVoteTraceWaves = 512;  // (PZ_VOTE_TRACE)
+[[maybe_unused]] constexpr uint64_t kVoteTraceFlushes = 256, kVoteTraceWaves = 512;  // (A/B: PZ_VOTE_TRACE)
 
-// The walk's A/B and test knobs (environment variables), read once per pz_chain_process_blocks
-// call (read_knobs) rather than at every flush and transition: a getenv scans the whole
-// environment, five of them per transition.
+// The walk's per-call switches (read_knobs), set once per pz_chain_process_blocks call: the
+// product's choices plus pz_chain_options; the A/B library (make ab, -DPZ_AB_BUILD) also reads the
+// measured-and-dropped forms from the environment there.
 struct Knobs {
-  int vote_path = 2;            // PZ_VOTE_PATH (VotePath: 0 segments, 1 packed, 2 direct)
-  bool vote_groups = true;      // PZ_VOTE_GROUPS=0: the per-attestation tally
-  bool vote_trace = false;      // PZ_VOTE_TRACE (tools/vote_trace.py)
-  bool epoch_pack_direct = false;  // PZ_EPOCH_PACK=direct
-  bool epoch_prep_after = true;    // PZ_EPOCH_PREP=merged: false
+  int vote_path = 2;            // (A/B: PZ_VOTE_PATH; VotePath: 0 segments, 1 packed, 2 direct)
+  bool vote_groups = true;      // pz_chain_options.tally_forms bit 0: the per-attestation tally
+  bool vote_trace = false;      // (A/B: PZ_VOTE_TRACE, tools/vote_trace.py)
+  bool epoch_pack_direct = false;  // (A/B: PZ_EPOCH_PACK=direct)
+  bool epoch_prep_after = true;    // (A/B: PZ_EPOCH_PREP=merged: false)
 };
 
 // A recent window's parent ids as a run (votes.h VoteRec) over its positions [0, nw): shared by
@@ -753,8 +753,10 @@ struct Engine {
   WindowRun wrun;                 // the last recent window's parent-id run (queue_vote_cache)
   Retired retired;                // grown-out device buffers (freed with the chain)
   Knobs kn;                       // (read_knobs)
+  pz_chain_options opt{};         // pz_chain_set_options (every field 0: the product's choices)
+  uint64_t kmax = 0;              // the largest committee
   bool bits_inline = true;        // every committee <= kVoteInlineBits: the bitfields ride in the records
-  bool ids_rows = false;          // (test knob) every attestation's ids in an explicit row
+  bool ids_rows = false;          // (pz_chain_options.tally_forms bit 2) every attestation's ids in an explicit row
   PinBuf e_pin, e_pin_out;   // the epoch inputs' pinned staging; the results' pinned landing
   PinBuf tot_pin;            // the gathered justification totals (65 words; + a sequence word)
   uint64_t gather_seq = 0;   // the last sequence number the fused gather was asked to write
@@ -843,8 +845,12 @@ struct PhaseTimer {
 // Per-attestation phases (checks, vote queueing) are timed only when PZ_CHAIN_PROFILE is set:
 // two clock reads per attestation cost ~4 ms per 10,000 blocks of the walk they measure.
 static bool fine_profile() {
+#ifdef PZ_AB_BUILD
   static const bool on = std::getenv("PZ_CHAIN_PROFILE") != nullptr;
   return on;
+#else
+  return false;
+#endif
 }
 struct FineTimer {
   double* acc = nullptr;
@@ -1047,15 +1053,18 @@ using EpochPrep = std::function<EpochLaunch*()>;
 //   packed              round 3: the queue memcpy'd into one pinned arena first, one stage copy.
 enum VotePath { kVoteSegments, kVotePacked, kVoteDirect };
 static void read_knobs(Engine& g) {
+  g.kn = Knobs{};
+  g.kn.vote_groups = !(g.opt.tally_forms & PZ_TALLY_PER_ATTESTATION);
+#ifdef PZ_AB_BUILD
   auto is = [](const char* name, const char* v) {
     const char* e = std::getenv(name);
     return e && !std::strcmp(e, v);
   };
   g.kn.vote_path = is("PZ_VOTE_PATH", "packed") ? kVotePacked : is("PZ_VOTE_PATH", "segments") ? kVoteSegments : kVoteDirect;
-  g.kn.vote_groups = !is("PZ_VOTE_GROUPS", "0");
   g.kn.vote_trace = std::getenv("PZ_VOTE_TRACE") != nullptr;
   g.kn.epoch_pack_direct = is("PZ_EPOCH_PACK", "direct");
   g.kn.epoch_prep_after = !is("PZ_EPOCH_PREP", "merged");
+#endif
 }
 
 static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, const EpochPrep* prep = nullptr) {
@@ -1139,7 +1148,9 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
         if (!r.q_ev) hchk(hipEventCreateWithFlags(&r.q_ev, hipEventDisableTiming), "event");
         hchk(hipEventRecord(r.q_ev, r.s), "event");
       }
-    } else if (path == kVoteSegments) {
+    }
+#ifdef PZ_AB_BUILD
+    else if (path == kVoteSegments) {
       // the queue's pinned arrays straight into the pack, one launch (no host-side copy)
       StageSegs sg;
       sg.nseg = 0;
@@ -1151,6 +1162,7 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
       seg(Q.bits.dev(r.dev), o_bits, Q.bits.size());
       hchk(launch_stage_h2d_segs(sg, r.s), "stage H2D");
     }
+#endif
     if (!r.d_err.p) {
       check(r.d_err.alloc(1));
       hchk(hipMemsetAsync(r.d_err.p, 0, 8, r.s), "memset");
@@ -1199,9 +1211,10 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
       // (pooled pinned memory holds old words: clear the sequence word before the launch)
       reinterpret_cast<volatile uint64_t*>(g.tot_pin.p)[kJustifySlots + 1] = 0;
     }
+#ifdef PZ_AB_BUILD
     if (prep) {
-      // (host: the transition's epoch packed before the launch) the tally with the epoch's
-      // count blocks in one launch
+      // (A/B, PZ_EPOCH_PREP=merged: the transition's epoch packed before the launch) the tally
+      // with the epoch's count blocks in one launch
       EpochLaunch* el = (*prep)();
       hchk(launch_vote_words_count(v, el->a, r.s), "vote tally + epoch count");
       el->counted = true;
@@ -1218,7 +1231,11 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
       g.vtrace_w.push_back(tr ? waves : 0);
       ++g.vtrace_n;
       hchk(launch_vote_words_traced(v, tr, r.s), "vote tally");
-    } else {
+    } else
+#else
+    (void)prep;
+#endif
+    {
       hchk(launch_vote_words(v, r.s), "vote tally");
     }
     if (!gather) {  // (gathering: the walk waits for the tally before any later flush)
@@ -2099,12 +2116,11 @@ static void init_tail(Engine& g, const std::vector<uint32_t>& members, const std
   uint64_t kmax = 0;
   for (uint64_t k : g.csize) kmax = std::max(kmax, k);
   g.bf_stride = (uint32_t)std::max<uint64_t>(4, ((kmax + 7) / 8 + 3) & ~3ull);
-  // (A/B and test knobs: PZ_VOTE_BITS=rows keeps every bitfield in the row array, PZ_VOTE_IDS=rows
-  // every attestation's ids in an explicit row)
-  const char* vb = std::getenv("PZ_VOTE_BITS");
-  g.bits_inline = kmax <= kVoteInlineBits && !(vb && !std::strcmp(vb, "rows"));
-  const char* vi = std::getenv("PZ_VOTE_IDS");
-  g.ids_rows = vi && !std::strcmp(vi, "rows");
+  // (pz_chain_options.tally_forms, tests: every bitfield in the row array, every attestation's
+  // ids in an explicit row)
+  g.kmax = kmax;
+  g.bits_inline = kmax <= kVoteInlineBits && !(g.opt.tally_forms & PZ_TALLY_BITS_ROWS);
+  g.ids_rows = (g.opt.tally_forms & PZ_TALLY_ID_ROWS) != 0;
   if (offs.back() >= (1ull << 32)) throw (int)fail(PZ_EINVAL, "committee lists above 2^32 members");
   // 64-aligned validator ranges, as pz_epoch_state / pz_comm_vote_tally split them
   const uint64_t span = 64 * std::max<uint64_t>(1, (n + 64ull * g.world - 1) / (64ull * g.world));
@@ -2438,11 +2454,8 @@ static uint64_t parse_range(const uint8_t* data, const uint64_t* offs, uint64_t 
 // CPU share of one GPU on the bench boxes), one per 512 KB (10,000 blocks: 1.76 ms on 8,
 // 1.22 ms on 16, profiles/r03/parse_probe_after_r3at.txt).
 static int parse_threads(uint64_t bytes) {
-  static const int cap = [] {
-    const char* e = std::getenv("PZ_PARSE_THREADS");
-    return e ? std::max(1, std::atoi(e)) : 16;
-  }();
-  return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cap, bytes >> 19));
+  const uint64_t cap = host_threads();  // (pz_set_host_threads)
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>(cap, bytes >> 19));
 }
 
 // The parse's worker threads, started once per process and kept (starting eight threads per
@@ -2712,10 +2725,7 @@ static void msg_drain(Engine& g) {
 // message's 17 compressions), ~0.13 ms for any batch up to 65,536 messages, so the last batch
 // costs the same wait as one whole-call batch: 8,192 measured no better than 0 on the
 // configs[4] replay (profiles/r03/msg_batch_ab_r3ap.txt), and costs six more sends.
-static uint64_t msg_batch() {  // (read per call: a test sets it)
-  const char* e = std::getenv("PZ_MSG_BATCH");
-  return e ? std::strtoull(e, nullptr, 10) : uint64_t(0);
-}
+static uint64_t msg_batch(const Engine& g) { return g.opt.msg_batch; }  // (pz_chain_options)
 
 // Digest the messages the walk appended since the last batch, on stream ms: the new hash-log
 // and trail entries, the records and var bytes H2D (pinned: no host staging), one
@@ -3050,7 +3060,7 @@ static void process(Engine& g, Feeder& F, pz_block_result* br, pz_att_result* ar
   check(g.m_pin.reserve(natt * 64 + 64));
   check(g.d_mrec.alloc(natt + 1));
   check(g.d_mout.alloc(natt * 64 + 64));
-  const uint64_t mbatch = msg_batch();
+  const uint64_t mbatch = msg_batch(g);
   read_knobs(g);
   // the tables grow once per call, not by doubling inside the walk
   g.slot_of.reserve(g.slot_of.size() + n);  // (plus any oblique hash shorter than 32 B: grows)
@@ -3310,6 +3320,15 @@ int pz_chain_new_from_state(const uint8_t* cstate, uint64_t len, const uint8_t* 
   return PZ_OK;
 }
 
+int pz_chain_set_options(pz_chain* c, const pz_chain_options* opts) {
+  if (!c) return fail(PZ_EINVAL, "chain is null");
+  Engine& g = c->g;
+  g.opt = opts ? *opts : pz_chain_options{};
+  g.bits_inline = g.kmax <= kVoteInlineBits && !(g.opt.tally_forms & PZ_TALLY_BITS_ROWS);
+  g.ids_rows = (g.opt.tally_forms & PZ_TALLY_ID_ROWS) != 0;
+  return PZ_OK;
+}
+
 void pz_chain_free(pz_chain* c) {
   if (!c) return;
   destroy_chain(c);
@@ -3367,8 +3386,12 @@ int pz_chain_process_blocks(pz_chain* c, const uint8_t* blocks, const uint64_t* 
   // slower on the 10,000-block replay (177-183k vs 200-229k blocks/s; the producer slows the
   // walk's own host work, profiles/r03/replay_pipeline_r3*.txt), so it is an A/B knob.  Both
   // end the call at a malformed block with PZ_EINVAL, the blocks before it processed.
+#ifdef PZ_AB_BUILD
   const char* pe = std::getenv("PZ_CHAIN_PIPELINE");
   F.piped = !long_msg && n >= 2 * kChunk && pe && pe[0] == '1';
+#else
+  F.piped = false;
+#endif
   if (!F.piped) {
     try {
       PhaseTimer pt(g.prof[kProfParse]);
@@ -3611,6 +3634,7 @@ extern "C" int pz_debug_chain_profile(pz_chain* c, double* out, int n) {
   return pz::chain::kProfSlots;
 }
 
+#ifdef PZ_AB_BUILD
 // Internal (tools/replay_timeline.py): up to n transitions' timestamps (4 u64 each, CLOCK_MONOTONIC
 // ns: flush start, tally launch returned, epoch launches returned, totals seen); returns the
 // count recorded since the chain was created (at most 65,536 are kept).
@@ -3629,6 +3653,7 @@ extern "C" int pz_debug_vote_trace(pz_chain* c, uint64_t* out, uint64_t* waves, 
   for (int i = 0; i < n; ++i) waves[i] = g.vtrace_w[i];
   return n;
 }
+#endif
 
 extern "C" int pz_debug_chain_timeline(pz_chain* c, uint64_t* out, int n) {
   if (!c || !out) return PZ_EINVAL;
@@ -3648,7 +3673,11 @@ extern "C" int pz_debug_parse(const uint8_t* data, const uint64_t* offs, uint64_
   double best = 1e30;
   // PZ_DEBUG_PARSE_PIN=1: the arena in pooled pinned memory, as pz_chain_process_blocks has it
   // (a device call: GPU boxes only)
+#ifdef PZ_AB_BUILD
   const char* pe = std::getenv("PZ_DEBUG_PARSE_PIN");
+#else
+  const char* pe = nullptr;
+#endif
   pz::chain::PinBuf pin;
   for (int r = 0; r < reps; ++r) {
     const auto t0 = std::chrono::steady_clock::now();

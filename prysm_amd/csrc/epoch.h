@@ -61,7 +61,9 @@ struct EpochHandoff {
 // The vote-cache tally (votes_dev.h, voter-major) and this one-instance epoch's count pass (all
 // three ranges) in ONE launch, tally blocks first (the chain engine's stateRecalc, one rank).
 struct VoteWordArgs;
+#ifdef PZ_AB_BUILD  // the A/B library only
 hipError_t launch_vote_words_count(const VoteWordArgs& v, const EpochArgs& a, hipStream_t s);
+#endif
 // winners: the mid pass's crosslink winners run in the same launch (only when no compaction is
 // needed: every validator active).
 hipError_t launch_epoch_reward_handoff(const EpochArgs& a, const EpochHandoff& h, bool winners, hipStream_t s);
@@ -79,6 +81,7 @@ hipError_t launch_epoch_reward_handoff(const EpochArgs& a, const EpochHandoff& h
 // the tallies, i.e. on balances the fused pass has already rewarded).
 constexpr uint64_t kLastCoMaxBytes = 16384;  // last bitfields up to 131,072 validators
 constexpr uint64_t kLastCoPos = 8192;         // positions per gathering block (one word per thread)
+constexpr uint32_t kNoAtt = 0xFFFFFFFEu, kManyAtt = 0xFFFFFFFFu;  // a committee's attestation: none / several
 constexpr int kPre = 2;  // pre[inst]: {bit count, PZ_XLERR_BITFIELD if a bitfield is short}
 struct FusedCommittee {        // per (instance, committee)
   uint64_t boff;              // bits offset of its single attestation's bitfield
@@ -147,6 +150,38 @@ struct FusedArgs {
   uint32_t* bal32;
   const uint64_t* bal32_base;
 };
+// ---- the window pass (epoch_window.hip): the one-pass step of B instances in ONE launch ------
+// Block (instance, range): a range is a run of this rank's committees (local ids [cr0, cr1),
+// positions [lcs[cr0], lcs[cr1])), so every committee's tallies complete inside one block.
+constexpr int kWinThreads = 1024, kWinDepth = 2;
+struct WinArgs {
+  const uint4* rdesc;         // [R] {cr0, cr1, first window (wdesc index), windows}
+  uint32_t R;                 // ranges per instance (grid: B x R blocks)
+  const uint32_t* wdesc;      // [windows] the first committee overlapping each 256-position window
+  const uint32_t* lcs;        // [nlc + 1] local committee starts (local positions; lcs[nlc] = nval)
+  const uint4* lci;           // [B][nlc + 1] {bitfield offset lo, hi (its single attestation),
+                              //   attestation index | kNoAtt | kManyAtt, first catt index}
+  const uint32_t* lnb;        // [B][nlc] single-attestation committees: min(size, 8 * bitfield bytes)
+  uint32_t nlc;
+  const uint32_t* catt;       // [B][natt] attestation indices grouped by committee (committee order)
+  const uint32_t* att_csize;  // [B][natt] the size of each attestation's committee
+  const uint4* att_win;       // [B][natt] {shard (< nrec), its record's dynasty lo, hi, 0}
+  uint32_t* bal32;            // [B][vstride] u32 balance offsets (or NULL: EpochArgs.balance)
+  const uint64_t* bal32_base; // [B]
+  const uint32_t* se16;       // [B][vstride] {start | end << 16} saturated (or NULL)
+  const uint2* se;            // [B][vstride] {start, end} saturated to 32 bits (or NULL: start/end)
+  uint64_t vstride;
+  uint32_t* winner_next;      // [B][nrec] reset to 0xFFFFFFFF for the next step (ping-pong)
+  uint64_t* vote_next;        // world > 1: [B][natt] the next step's tallies zeroed (non-owned
+  uint64_t* total_next;       //   attestations stay zero for pz_epoch_state_tallies' sum), else NULL
+  int rank0;                  // this rank writes the per-instance scalars
+  // LDS plan: last-bitfield bytes (0: reward bits from L2), vote-bit words, most committees /
+  // attestations of a range, 32-bit words per committee bitfield
+  uint32_t lds_lbf, lds_vw, lds_maxc, lds_maxk, wpc;
+};
+size_t window_lds_bytes(const WinArgs& w);
+hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t s);
+
 // The single-launch step's limits: every block counts the instance's bitfields itself and the
 // last block keeps one LDS word per crosslink record.
 constexpr uint64_t kOneMaxBitBytes = 32768;
@@ -154,17 +189,11 @@ constexpr uint32_t kOneMaxAtt = 2048;
 constexpr uint32_t kOneMaxRec = 4096;
 constexpr uint64_t kMultiMaxBitBytes = 16384;
 constexpr uint32_t kMultiMaxAtt = 512;
-bool epoch_multi_enabled(const FusedArgs& f);
-hipError_t launch_epoch_multi(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
-hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
-hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
-hipError_t launch_epoch_fwin(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
 // One instance, one rank, in ONE launch (f.one): every block counts the bitfields and checks
 // their lengths itself (no pre pass), streams its committee pieces as `fused` does, and the
 // last block to finish (an arrival ticket) forms the winners in LDS (no mid pass).
 hipError_t launch_epoch_one(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
-bool epoch_one_enabled(const FusedArgs& f);  // f.one and no tools/ ablation selected
+bool epoch_one_enabled(const FusedArgs& f);  // f.one
 bool fused_ok(const EpochArgs& a);  // 16-B vector path available (16-B aligned validator rows)
-int set_fused_variant(int v);       // tools/ A/B only (pz_debug_set_fused_variant)
 
 }  // namespace pz

@@ -377,21 +377,7 @@ __device__ __forceinline__ void count_body(const EpochArgs& a, const CountGrid& 
 #define PZ_COUNT_KERNEL(NAME, V) \
   extern "C" __global__ void __launch_bounds__(kThreads) NAME(EpochArgs a, CountGrid g) { count_body<V>(a, g, blockIdx.x); }
 PZ_COUNT_KERNEL(pz_epoch_count_kernel, 0)
-PZ_COUNT_KERNEL(pz_epoch_count_v1_kernel, 1)
-PZ_COUNT_KERNEL(pz_epoch_count_v2_kernel, 2)
-PZ_COUNT_KERNEL(pz_epoch_count_v3_kernel, 3)
-PZ_COUNT_KERNEL(pz_epoch_count_v4_kernel, 4)
-PZ_COUNT_KERNEL(pz_epoch_count_v5_kernel, 5)
-PZ_COUNT_KERNEL(pz_epoch_count_v8_kernel, 8)
-PZ_COUNT_KERNEL(pz_epoch_count_v16_kernel, 16)
 #undef PZ_COUNT_KERNEL
-
-static int g_count_variant = 0;  // tools/ A/B only
-int set_count_variant(int v) {
-  const int old = g_count_variant;
-  g_count_variant = v;
-  return old;
-}
 
 // ------------------------------------------------------------------------------------------
 // Crosslink winners (core.go:549-555): the first attestation, in order, whose 3*vote >=
@@ -739,9 +725,6 @@ __device__ __forceinline__ void reward_body(EpochArgs a, uint64_t vbpi, int vec,
     reward_body<MODE>(a, vbpi, vec, scal_ro, boffs_ro, tdep_ro, blockIdx.x, blockIdx.y);          \
   }
 PZ_REWARD_KERNEL(pz_epoch_reward_kernel, 0)
-PZ_REWARD_KERNEL(pz_epoch_reward_dbg1_kernel, 1)
-PZ_REWARD_KERNEL(pz_epoch_reward_dbg2_kernel, 2)
-PZ_REWARD_KERNEL(pz_epoch_reward_dbg3_kernel, 3)
 #undef PZ_REWARD_KERNEL
 
 // The reward pass of ONE instance with its results handed to the host (EpochHandoff): the
@@ -805,137 +788,9 @@ hipError_t launch_epoch_reward_handoff(const EpochArgs& a, const EpochHandoff& h
   return hipGetLastError();
 }
 
-hipError_t launch_epoch_reward_mode(const EpochArgs& a, int mode, hipStream_t s) {
-  const uint64_t vbpi = vblocks_per_inst(a.nval);
-  if (!vbpi || !a.ninst) return hipSuccess;
-  const int vec = ((a.nval % 2 == 0) && !((reinterpret_cast<uintptr_t>(a.balance) |
-                                           reinterpret_cast<uintptr_t>(a.start) |
-                                           reinterpret_cast<uintptr_t>(a.end)) & 15)) ? 1 : 0;
-  const dim3 grid(a.ninst, (uint32_t)vbpi);
-  if (mode == 1) hipLaunchKernelGGL(pz_epoch_reward_dbg1_kernel, grid, dim3(kThreads), 0, s, a, vbpi, vec, a.scal, a.boffs, a.total_deposit);
-  else if (mode == 2) hipLaunchKernelGGL(pz_epoch_reward_dbg2_kernel, grid, dim3(kThreads), 0, s, a, vbpi, vec, a.scal, a.boffs, a.total_deposit);
-  else if (mode == 3) hipLaunchKernelGGL(pz_epoch_reward_dbg3_kernel, grid, dim3(kThreads), 0, s, a, vbpi, vec, a.scal, a.boffs, a.total_deposit);
-  else hipLaunchKernelGGL(pz_epoch_reward_kernel, grid, dim3(kThreads), 0, s, a, vbpi, vec, a.scal, a.boffs,
-                          a.total_deposit);
-  return hipGetLastError();
-}
-
 // ------------------------------------------------------------------------------------------
 // One-pass epoch (committee order, every validator active; epoch.h "one-pass epoch").
 // ------------------------------------------------------------------------------------------
-// Pre: [popcount blocks (B x pbpi) | one thread per attestation].  Every rank counts every
-// bitfield byte (2 MB per 16.7 M validator-epochs) so that its fused pass knows the
-// threshold without a collective; rank 0 alone reports the count in scal.
-// Third range (f.lastco): the reward bits in position order.  A block stages its instance's last
-// bitfield in LDS (branch-free 16-B loads over the padded buffer), then each thread gathers 32
-// positions' bits -- bit co_index[p], MSB-first as CheckBit (checkbit.go:4-15) -- into one word.
-// The random lookups run from LDS here instead of from L2 behind each fused wave's stream.
-// (Several instances per block, sharing the co_index loads, held ~200 VGPRs: the compiler
-// hoists the 32 positions' address math out of the instance loop.)  Thread t takes positions
-// p0 + 256k + t (k < 32), so each co_index load is coalesced across the wave (32 contiguous
-// positions per thread made every load touch 64 lines: 16 us of pre at 65,536 x 256), and a
-// ballot turns 64 lanes' bits into the two position-order words lane k stores.
-__device__ __forceinline__ void lastco_block(const EpochArgs& a, const FusedArgs& f, uint64_t blk, uint64_t lcb) {
-  __shared__ __attribute__((aligned(16))) uint8_t lbf[kLastCoMaxBytes + 32];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint64_t inst = blk / lcb, chunk = blk - inst * lcb;
-  const uint64_t lb = a.boffs[inst * a.natt + a.natt - 1], L = a.boffs[inst * a.natt + a.natt] - lb;
-  const uint64_t b16 = lb & ~15ull, n16 = (L + (lb & 15) + 15) / 16;
-  const uint64_t p0 = chunk * kLastCoPos, np = f.vstride;
-  constexpr int kK = (int)(kLastCoPos / kThreads);  // 32 positions per thread
-  uint32_t ci[kK];
-  typedef const __attribute__((address_space(1))) uint32_t gword;
-  gword* cb = (gword*)(uintptr_t)(a.co_index + p0);  // scalar base, 32-bit lane offsets
-#pragma unroll
-  for (int k = 0; k < kK; ++k) {  // issued with the stage's loads below
-    const uint32_t d = (uint32_t)k * kThreads + tid;
-    ci[k] = cb[p0 + d < np ? d : 0];
-  }
-  constexpr int kLoads = (int)((kLastCoMaxBytes + 16) / (16 * kThreads)) + 1;
-  uint4 q[kLoads];
-#pragma unroll
-  for (int k = 0; k < kLoads; ++k) {
-    const uint64_t w = (uint64_t)k * kThreads + tid;
-    q[k] = *reinterpret_cast<const uint4*>(a.bits + (w < n16 ? b16 + 16 * w : b16));
-  }
-#pragma unroll
-  for (int k = 0; k < kLoads; ++k) {
-    const uint64_t w = (uint64_t)k * kThreads + tid;
-    if (w < n16) *reinterpret_cast<uint4*>(lbf + 16 * w) = q[k];
-  }
-  __syncthreads();
-  const uint8_t* bf = lbf + (lb & 15);
-  uint64_t mine = 0;  // lane k keeps the ballot of step k
-#pragma unroll
-  for (int k = 0; k < kK; ++k) {
-    const uint64_t p = p0 + (uint64_t)k * kThreads + tid;
-    const uint32_t i = ci[k];
-    const bool bit = p < a.nval && i < 8 * L && ((bf[i >> 3] >> (7 - (i & 7))) & 1);
-    const uint64_t m = __ballot(bit);
-    if (lane == k) mine = m;
-  }
-  if (lane < kK) {  // positions p0 + 256 lane + 64 wave .. +63: words w0, w0 + 1
-    const uint64_t w0 = (p0 + (uint64_t)lane * kThreads + 64 * wave) / 32;
-    if (w0 < f.lcw) f.lastco[inst * f.lcw + w0] = (uint32_t)mine;
-    if (w0 + 1 < f.lcw) f.lastco[inst * f.lcw + w0 + 1] = (uint32_t)(mine >> 32);
-  }
-}
-
-extern "C" __global__ void __launch_bounds__(kThreads)
-pz_epoch_pre_kernel(EpochArgs a, FusedArgs f, uint64_t pbpi, uint64_t npb, uint64_t nab, uint64_t lcb) {
-  __shared__ uint64_t sh[kThreads / 64];
-  const int tid = threadIdx.x;
-  if (blockIdx.x >= npb + nab) {
-    lastco_block(a, f, blockIdx.x - npb - nab, lcb);
-    return;
-  }
-  if (blockIdx.x < npb) {
-    const uint64_t pb = blockIdx.x;
-    const uint64_t inst = (uint32_t)pb / (uint32_t)pbpi, chunk = (uint32_t)pb - (uint32_t)inst * (uint32_t)pbpi;
-    if (chunk == 0 && a.winner)  // the winner pass runs after the fused pass
-      for (uint32_t s = tid; s < a.nrec; s += kThreads) a.winner[inst * a.nrec + s] = 0xffffffffu;
-    const uint64_t beg = a.boffs[inst * a.natt], end = a.boffs[inst * a.natt + a.natt];
-    const uint64_t cb = beg + chunk * kPopBytesPerBlock;
-    uint64_t cnt = 0;
-    if (cb < end) {
-      // the chunk's 16-B words from cb & ~15: every load issued before any is used (a loop
-      // with one load per trip waited out four round trips per block)
-      constexpr int kW = (int)(kPopBytesPerBlock / (16 * kThreads)) + 1;
-      const uint64_t ce = end < cb + kPopBytesPerBlock ? end : cb + kPopBytesPerBlock;
-      uint4 q[kW];
-#pragma unroll
-      for (int k = 0; k < kW; ++k) {  // branch-free: the state pads its bitfield buffer by 16 B
-        const uint64_t u = (cb & ~15ull) + 16ull * (k * kThreads + tid);
-        q[k] = *reinterpret_cast<const uint4*>(a.bits + (u < ce ? u : (cb & ~15ull)));
-      }
-#pragma unroll
-      for (int k = 0; k < kW; ++k) {
-        const uint64_t u = (cb & ~15ull) + 16ull * (k * kThreads + tid);
-        if (u >= cb && u + 16 <= ce)
-          cnt += __popc(q[k].x) + __popc(q[k].y) + __popc(q[k].z) + __popc(q[k].w);
-        else
-          for (uint64_t j = u < cb ? cb : u; j < u + 16 && j < ce; ++j) cnt += __popc((uint32_t)a.bits[j]);
-      }
-    }
-    const uint64_t c = block_reduce<false>(cnt, sh);
-    if (tid == 0 && c) atomicAdd((unsigned long long*)&f.pre[inst * kPre], (unsigned long long)c);
-    return;
-  }
-  // one attestation: zero its tallies (the fused pass accumulates them) and raise the
-  // processCrosslinks panic of a bitfield shorter than its committee (CheckBit at a member
-  // position >= 8*len, core.go:538-541)
-  const uint64_t ga = (uint64_t)(blockIdx.x - npb) * kThreads + tid;
-  if (ga >= (uint64_t)a.ninst * a.natt) return;
-  a.vote[ga] = 0;
-  a.total[ga] = 0;
-  const uint32_t c = a.att_comm[ga];
-  const uint64_t k = a.coffs[c + 1] - a.coffs[c];
-  if (k > 8 * (a.boffs[ga + 1] - a.boffs[ga])) {
-    const uint64_t inst = (uint32_t)ga / (uint32_t)a.natt;
-    atomicOr((unsigned long long*)&f.pre[inst * kPre + 1], (unsigned long long)kErrBitfield);
-  }
-}
-
 // Fused: one wave per committee piece (FusedArgs.items: <= 256 positions of one committee,
 // pairs 16-B aligned), kFusedWaves pieces of one instance per block; grid (B, piece groups).
 // A wave streams start, end, balance and co_index of its piece (16 B per lane per pair, every
@@ -943,7 +798,6 @@ pz_epoch_pre_kernel(EpochArgs a, FusedArgs f, uint64_t pbpi, uint64_t npb, uint6
 // tallies (two wave sums, two atomics per attestation of the committee), then classifies,
 // rewards, stores and sums; the block adds its next-cycle sum with one atomic.
 constexpr int kFusedWaves = 8;
-constexpr uint32_t kNoAtt = 0xFFFFFFFEu, kManyAtt = 0xFFFFFFFFu;
 
 // MODE: an ablation knob for tools/ (0 in the product; results are wrong otherwise): bit 0 no
 // crosslink tallies, bit 1 reward bit from the balance instead of the last bitfield, bit 2 no
@@ -1549,537 +1403,6 @@ __device__ __forceinline__ void one_tail(const EpochArgs& a, const FusedArgs& f,
   if (tid == 0) __hip_atomic_store(f.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Two pieces per wave (A/B, variant 1 << 21 on the u32-offset states): wave w of block (inst,
-// grp) takes pieces 16 grp + w and 16 grp + w + 8, their loads issued together -- both
-// descriptors, then both streams, then both pieces' reward-bit lookups -- so a wave has twice
-// the bytes in flight per dependent round trip; the block merges its 16 pieces' tallies as
-// the one-piece blocks merge 8.  Only the product's form: u32 offsets, 16-bit {start, end},
-// reward bits looked up (no `lastco`).
-constexpr int kPieces2 = 2 * kFusedWaves;
-__device__ __forceinline__ void quad2_body(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro,
-                                           const uint64_t* __restrict__ boffs_ro, const uint64_t* __restrict__ tdep_ro,
-                                           const uint4* __restrict__ items_ro, const uint32_t* __restrict__ catt_offs_ro,
-                                           const uint32_t* __restrict__ catt_ro) {
-  __shared__ uint64_t xt[kPieces2], xv[kPieces2], xs[kFusedWaves], xn[kFusedWaves];
-  __shared__ uint32_t xg[kPieces2];
-  const uint64_t inst = blockIdx.x, grp = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint64_t dyn = a.dynasty[inst];
-  const uint64_t pop = pre_ro[inst * kPre], ferr = pre_ro[inst * kPre + 1];
-  const uint64_t lb = boffs_ro[inst * a.natt + a.natt - 1];
-  const uint64_t L = boffs_ro[inst * a.natt + a.natt] - lb;
-  const bool rwd_err = (a.nval_global - 1) >= 8 * L;  // CheckBit(last, N-1) panics (incentives.go:23)
-  const bool thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (tdep_ro[inst] * 2ull);  // incentives.go:18-20
-  const bool skip = ferr != 0 || (thr && rwd_err);
-  const bool applied = thr && !skip;
-  const bool wiw = f.win_fused != 0;
-  const uint64_t bbase = f.bal32_base[inst];
-  uint32_t* Bal32 = f.bal32 + inst * f.vstride;
-  const uint8_t* lastbf = a.bits + lb;
-  // phase A: both pieces' descriptors
-  uint4 it[2], ic[2];
-  uint64_t item[2];
-  bool have[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    item[k] = grp * kPieces2 + (uint64_t)wave + (uint64_t)k * kFusedWaves;
-    have[k] = item[k] < f.nitems;
-    it[k] = have[k] ? items_ro[item[k]] : make_uint4((uint32_t)a.val_offset, 0, 0, (uint32_t)a.val_offset);
-    ic[k] = have[k] ? f.items_ci[inst * f.nitems + item[k]] : make_uint4(0, 0, 0, kNoAtt);
-  }
-  // phase B: both streams, committee bytes, winner words
-  uint4 qb[2], se[2], cix[2];
-  uint2 win1[2];
-  uint32_t byA[2], byB[2];
-  uint64_t p[2], g[2];
-  int64_t qs[2], qlo[2];
-  bool v[2][4];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const uint64_t ws = it[k].x, we = (uint64_t)it[k].x + it[k].y, cb = it[k].w;
-    const uint64_t p0 = (ws - a.val_offset) & ~3ull;
-    p[k] = p0 + 4ull * lane;
-    g[k] = a.val_offset + p[k];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[k][i] = g[k] + i >= ws && g[k] + i < we;
-    const uint64_t pp = (v[k][0] || v[k][1] || v[k][2] || v[k][3]) ? p[k] : p0;
-    qb[k] = *reinterpret_cast<const uint4*>(Bal32 + pp);
-    se[k] = ld16_nt(reinterpret_cast<const uint64_t*>(f.se16 + inst * f.vstride + pp));
-    cix[k] = *reinterpret_cast<const uint4*>(a.co_index + pp);
-    const uint32_t ga = ic[k].w, nbits = ic[k].z;
-    win1[k] = (wiw && ga < kNoAtt) ? f.att_win[inst * a.natt + ga] : make_uint2(0, 0);
-    qs[k] = (int64_t)(g[k] - cb);
-    const int64_t last = (int64_t)nbits - 1;
-    qlo[k] = qs[k] < 0 ? 0 : qs[k] > last ? last : qs[k];
-    byA[k] = byB[k] = 0;
-    if (ga < kNoAtt && nbits) {
-      const uint64_t bp = pack64(ic[k].x, ic[k].y) + ((uint64_t)qlo[k] >> 3), da = bp & ~3ull;
-      uint64_t w8;
-      __builtin_memcpy(&w8, __builtin_assume_aligned(a.bits + da, 4), 8);
-      const uint32_t sh = (uint32_t)(bp - da) * 8;
-      byA[k] = (uint32_t)(w8 >> sh) & 0xFFu;
-      byB[k] = (uint32_t)(w8 >> (sh + 8)) & 0xFFu;
-    }
-  }
-  // phase C: both pieces' reward-bit bytes (dependent on their co_index words)
-  uint32_t rb[2][4];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const uint32_t c4[4] = {cix[k].x, cix[k].y, cix[k].z, cix[k].w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) rb[k][i] = applied ? lastbf[(v[k][i] ? c4[i] : 0u) >> 3] : 0u;
-  }
-  // phase D: per piece, tallies on the pre-reward balances, classify, reward, store
-  uint64_t sum = 0;
-  bool off[4] = {false, false, false, false};
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    uint64_t b[4] = {bbase + qb[k].x, bbase + qb[k].y, bbase + qb[k].z, bbase + qb[k].w};
-    const uint32_t ga = ic[k].w, nbits = ic[k].z;
-    uint64_t ts = 0, vs = 0;
-    uint32_t g1 = kNoAtt;
-    if (ga != kNoAtt) {  // (wave-uniform)
-      uint64_t t = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) t += v[k][i] ? b[i] : 0;
-      ts = wave_sum_dpp(t);
-      if (ga != kManyAtt) {
-        uint64_t vv = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int64_t x = qs[k] + i;
-          const uint32_t by = ((x >> 3) == (qlo[k] >> 3)) ? byA[k] : byB[k];
-          if (v[k][i] && (uint64_t)x < (uint64_t)nbits && ((by >> (7 - (uint32_t)(x & 7))) & 1)) vv += b[i];
-        }
-        vs = wave_sum_dpp(vv);
-        g1 = ga;
-        if (wiw && lane == 0) one_win<false>(a, f, inst, ga, vs, ts, win1[k], dyn);
-      } else {  // several attestations of this committee: direct atomics per attestation
-        const uint32_t* co = catt_offs_ro + inst * (f.ncomm + 1);
-        for (uint32_t q = co[it[k].z]; q < co[it[k].z + 1]; ++q) {
-          const uint64_t gq = catt_ro[inst * a.natt + q];
-          const uint64_t boff = boffs_ro[inst * a.natt + gq];
-          const uint64_t nb = 8 * (boffs_ro[inst * a.natt + gq + 1] - boff);
-          uint64_t vv = 0;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint64_t x = (uint64_t)(qs[k] + i);
-            if (v[k][i] && x < nb && bit_at(a.bits + boff, x)) vv += b[i];
-          }
-          vv = wave_sum_dpp(vv);
-          if (wiw && lane == 0) one_win<false>(a, f, inst, (uint32_t)gq, vv, ts, f.att_win[inst * a.natt + gq], dyn);
-          if (lane < 2) {
-            uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + gq;
-            const uint64_t xx = lane ? vv : ts;
-            if (xx) atomicAdd((unsigned long long*)dst, (unsigned long long)xx);
-          }
-        }
-      }
-    }
-    if (lane == 0) {
-      const int e = wave + k * kFusedWaves;
-      xg[e] = g1;
-      xt[e] = ts;
-      xv[e] = vs;
-    }
-    const uint32_t sw[4] = {se[k].x, se[k].y, se[k].z, se[k].w};
-    const uint32_t c4[4] = {cix[k].x, cix[k].y, cix[k].z, cix[k].w};
-    bool act[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      act[i] = (uint64_t)(sw[i] & 0xFFFFu) <= dyn && dyn < (uint64_t)(sw[i] >> 16);
-      off[i] = off[i] || (v[k][i] && !act[i]);
-    }
-    if (applied) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool r = (rb[k][i] >> (7 - ((v[k][i] ? c4[i] : 0u) & 7))) & 1;
-        b[i] = r ? b[i] + PZ_ATTESTER_REWARD : b[i] - PZ_ATTESTER_REWARD;
-      }
-      if (v[k][0] && v[k][1] && v[k][2] && v[k][3]) {
-        *reinterpret_cast<uint4*>(Bal32 + p[k]) = make_uint4((uint32_t)(b[0] - bbase), (uint32_t)(b[1] - bbase),
-                                                             (uint32_t)(b[2] - bbase), (uint32_t)(b[3] - bbase));
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (v[k][i]) Bal32[p[k] + i] = (uint32_t)(b[i] - bbase);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) sum += (v[k][i] && act[i]) ? b[i] : 0;
-  }
-  sum = wave_sum_dpp(sum);
-  const uint64_t nm = wave_count4(off);  // (a position counted once: the pieces are disjoint; nonzero only off the layout)
-  if (lane == 0) {
-    xs[wave] = sum;
-    xn[wave] = nm;
-  }
-  __syncthreads();
-  if (wave == 0) fused_block_end<kPieces2>(a, f, xg, xt, xv, xs, xn, inst, grp, lane, skip, applied, pop, ferr, rwd_err);
-}
-
-extern "C" __global__ void __launch_bounds__(64 * kFusedWaves) __attribute__((amdgpu_waves_per_eu(6, 6)))
-pz_epoch_fused_se16_b32_q2_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro,
-                                  const uint64_t* __restrict__ boffs_ro, const uint64_t* __restrict__ tdep_ro,
-                                  const uint4* __restrict__ items_ro, const FusedCommittee* __restrict__ cinfo_ro,
-                                  const uint32_t* __restrict__ catt_offs_ro, const uint32_t* __restrict__ catt_ro) {
-  (void)cinfo_ro;
-  quad2_body(a, f, pre_ro, boffs_ro, tdep_ro, items_ro, catt_offs_ro, catt_ro);
-}
-
-#define PZ_FUSED_KERNEL(NAME, MODE)                                                                       \
-  extern "C" __global__ void __launch_bounds__(64 * kFusedWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) \
-  NAME(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro, const uint64_t* __restrict__ boffs_ro, \
-       const uint64_t* __restrict__ tdep_ro, const uint4* __restrict__ items_ro,                             \
-       const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,              \
-       const uint32_t* __restrict__ catt_ro) {                                                             \
-    fused_body<MODE>(a, f, pre_ro, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);          \
-  }
-PZ_FUSED_KERNEL(pz_epoch_fused_kernel, 0)
-PZ_FUSED_KERNEL(pz_epoch_fused_lc_kernel, 256)  // reward bits from FusedArgs.lastco
-// the product's multi-instance kernels take quad lanes (32768)
-PZ_FUSED_KERNEL(pz_epoch_fused_se_kernel, 1024 + 32768)  // start/end from FusedArgs.se
-PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_kernel, 1280 + 32768)
-PZ_FUSED_KERNEL(pz_epoch_fused_se_xcd_kernel, 1024 + 4096)     // the XCD-aware 1-D grid
-PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_xcd_kernel, 1280 + 4096)
-PZ_FUSED_KERNEL(pz_epoch_fused_se16_kernel, 1024 + 16384 + 32768)  // start/end from FusedArgs.se16
-PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_kernel, 1280 + 16384 + 32768)
-// balances as u32 offsets (FusedArgs.bal32, 524288)
-PZ_FUSED_KERNEL(pz_epoch_fused_se16_b32_kernel, 1024 + 16384 + 32768 + 524288)
-PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_b32_kernel, 1280 + 16384 + 32768 + 524288)
-PZ_FUSED_KERNEL(pz_epoch_fused_se_b32_kernel, 1024 + 32768 + 524288)
-PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_b32_kernel, 1280 + 32768 + 524288)
-PZ_FUSED_KERNEL(pz_epoch_fused_se16_b32_xcd_kernel, 1024 + 16384 + 32768 + 524288 + 4096)  // (A/B: XCD-aware grid)
-// ablations of the u32-offset kernels (tools/: variant (1 << 20) | x, output wrong for x != 0):
-// x = 1 no crosslink tallies, 2 no reward-bit lookups, 4 no balance store, 8 no start/end loads
-#define PZ_B32_ABL(X)                                                                   \
-  PZ_FUSED_KERNEL(pz_epoch_fused_se16_b32_a##X##_kernel, 1024 + 16384 + 32768 + 524288 + X) \
-  PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_b32_a##X##_kernel, 1280 + 16384 + 32768 + 524288 + X)
-PZ_B32_ABL(1) PZ_B32_ABL(2) PZ_B32_ABL(4) PZ_B32_ABL(8) PZ_B32_ABL(3) PZ_B32_ABL(7) PZ_B32_ABL(15)
-#undef PZ_B32_ABL
-// (A/B, variant 32768: the round-3 pair lanes)
-PZ_FUSED_KERNEL(pz_epoch_fused_se_pair_kernel, 1024)
-PZ_FUSED_KERNEL(pz_epoch_fused_lc_se_pair_kernel, 1280)
-PZ_FUSED_KERNEL(pz_epoch_fused_se16_pair_kernel, 1024 + 16384)
-PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_pair_kernel, 1280 + 16384)
-PZ_FUSED_KERNEL(pz_epoch_fused_se16_xcd_kernel, 1024 + 4096 + 16384)
-PZ_FUSED_KERNEL(pz_epoch_fused_lc_se16_xcd_kernel, 1280 + 4096 + 16384)
-PZ_FUSED_KERNEL(pz_epoch_fused_dbg1_kernel, 1)
-PZ_FUSED_KERNEL(pz_epoch_fused_dbg2_kernel, 2)
-PZ_FUSED_KERNEL(pz_epoch_fused_dbg3_kernel, 3)
-PZ_FUSED_KERNEL(pz_epoch_fused_dbg4_kernel, 4)
-PZ_FUSED_KERNEL(pz_epoch_fused_dbg7_kernel, 7)
-PZ_FUSED_KERNEL(pz_epoch_fused_dbg8_kernel, 8)
-PZ_FUSED_KERNEL(pz_epoch_fused_dbg15_kernel, 15)
-PZ_FUSED_KERNEL(pz_epoch_fused_dbg16_kernel, 16)
-PZ_FUSED_KERNEL(pz_epoch_fused_dbg32_kernel, 32)
-PZ_FUSED_KERNEL(pz_epoch_fused_dbg48_kernel, 48)
-PZ_FUSED_KERNEL(pz_epoch_fused_dbg1088_kernel, 1088)  // se, piece from its index (no item -> stream hop)
-#undef PZ_FUSED_KERNEL
-
-// ---- the streaming form of the fused pass (product at B > 1, one rank or sharded) -------------
-// Persistent waves: W = gridDim.x * 8 waves, W a multiple of B, so wave w always serves
-// instance w % B and takes its pieces item = w / B + j * (W / B) in turn (adjacent waves: the
-// same pieces of the next instance, whose co_index words they share in L2).  The loads of each
-// piece are software-pipelined (the round-3 wave ran one piece through three dependent round
-// trips -- item, stream, reward-bit lookups -- and retired): while piece k's reward bits are
-// looked up, piece k+1's stream is in flight and piece k+2's item is being fetched.  There is
-// no block barrier: each wave adds its pieces' tallies (two atomics per piece, to the piece's
-// attestation) and, at its end, its instance's next-cycle partial sum (one atomic per wave).
-// Lane l takes 4 contiguous positions of a piece (16-B column loads, as the quad lanes).
-struct StreamA {  // piece descriptor: {first position, count, committee, committee start}, committee info
-  uint4 it, ic;
-};
-struct StreamB {  // the piece's stream
-  uint4 qb0, qb1, se, cix;
-  uint32_t lcw, byA, byB;
-  uint2 win1;
-};
-
-template <int MODE>
-__device__ __forceinline__ StreamA stream_load_a(const FusedArgs& f, const uint4* __restrict__ items_ro, uint64_t inst,
-                                                 uint64_t item, uint64_t val_offset) {
-  StreamA x;
-  const bool have = item < f.nitems;
-  x.it = have ? items_ro[item] : make_uint4((uint32_t)val_offset, 0, 0, (uint32_t)val_offset);
-  x.ic = have ? f.items_ci[inst * f.nitems + item] : make_uint4(0, 0, 0, kNoAtt);
-  return x;
-}
-
-template <int MODE>
-__device__ __forceinline__ StreamB stream_load_b(const EpochArgs& a, const FusedArgs& f, uint64_t inst, const StreamA& x,
-                                                 int lane) {
-  StreamB y;
-  const uint64_t ws = x.it.x, we = (uint64_t)x.it.x + x.it.y, cb = x.it.w;
-  const uint64_t p0 = (ws - a.val_offset) & ~3ull, p = p0 + 4ull * lane, g = a.val_offset + p;
-  const bool any = g + 3 >= ws && g < we;
-  const uint64_t pp = any ? p : p0;
-  if (MODE & 524288) {  // u32 balance offsets (FusedArgs.bal32): one 16-B load
-    y.qb0 = *reinterpret_cast<const uint4*>(f.bal32 + inst * f.vstride + pp);
-    y.qb1 = make_uint4(0, 0, 0, 0);
-  } else {
-    const uint64_t* Bal = a.balance + inst * f.vstride;
-    y.qb0 = *reinterpret_cast<const uint4*>(Bal + pp);
-    y.qb1 = *reinterpret_cast<const uint4*>(Bal + pp + 2);
-  }
-  y.se = ld16_nt(reinterpret_cast<const uint64_t*>(f.se16 + inst * f.vstride + pp));  // {start | end << 16}
-  const uint32_t ga = x.ic.w;
-  // (MODE & 131072: the winners formed in the waves, FusedArgs.win_fused)
-  y.win1 = ((MODE & 131072) && ga < kNoAtt) ? f.att_win[inst * a.natt + ga] : make_uint2(0, 0);
-  if (MODE & 256) {  // the reward bits in position order (pre's gather)
-    y.lcw = f.lastco[inst * f.lcw + (pp >> 5)];
-    y.cix = make_uint4(0, 0, 0, 0);
-  } else {
-    y.cix = *reinterpret_cast<const uint4*>(a.co_index + pp);
-    y.lcw = 0;
-  }
-  const uint64_t boff = pack64(x.ic.x, x.ic.y);
-  const uint32_t nbits = x.ic.z;
-  const int64_t qs = (int64_t)(g - cb), last = (int64_t)nbits - 1;
-  const int64_t qlo = qs < 0 ? 0 : qs > last ? last : qs;
-  const int64_t qhi = qs + 3 < 0 ? 0 : qs + 3 > last ? last : qs + 3;
-  y.byA = y.byB = 0;
-  if (ga < kNoAtt && nbits) {
-    y.byA = a.bits[boff + ((uint64_t)qlo >> 3)];
-    y.byB = a.bits[boff + ((uint64_t)qhi >> 3)];
-  }
-  return y;
-}
-
-// MODE & 262144 (LDS): workgroups of 16 waves; block (instance i, slice j) -- blockIdx = i * bpi
-// + j -- stages instance i's last bitfield in LDS once and its waves take the pieces j + bpi *
-// (wave + 16 t), looking the reward bits up in LDS (ds_read_u8) instead of gathering one random
-// L2 line per position.  The 16 blocks of slice j (one per instance) share an XCD (blockIdx
-// differs by multiples of bpi = 16 when B = 16), so its co_index words are fetched into one L2.
-template <int MODE>
-__device__ __forceinline__ void stream_kernel_body(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro,
-                                                   const uint64_t* __restrict__ boffs_ro,
-                                                   const uint64_t* __restrict__ tdep_ro,
-                                                   const uint4* __restrict__ items_ro,
-                                                   const uint32_t* __restrict__ catt_offs_ro,
-                                                   const uint32_t* __restrict__ catt_ro, uint32_t bpi) {
-  static_assert((MODE & 16384) != 0, "the streaming pass reads the 16-bit {start, end} column");
-  constexpr bool LDS = (MODE & 262144) != 0;
-  extern __shared__ uint4 lbf_dyn[];
-  const int lane = threadIdx.x & 63;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nwv = blockDim.x >> 6;
-  const uint64_t B = a.ninst;
-  uint64_t inst, item0, stride;
-  if (LDS) {
-    inst = blockIdx.x / bpi;
-    item0 = (blockIdx.x - inst * bpi) + (uint64_t)bpi * wv;
-    stride = (uint64_t)bpi * nwv;
-  } else {
-    const uint64_t w = (uint64_t)blockIdx.x * nwv + wv, W = (uint64_t)gridDim.x * nwv;
-    inst = w % B;
-    item0 = w / B;
-    stride = W / B;
-  }
-  // the instance's scalars (GetAttestersTotalDeposit from `pre`, the threshold, the panics)
-  const uint64_t pop = pre_ro[inst * kPre], ferr = pre_ro[inst * kPre + 1];
-  const uint64_t lb = boffs_ro[inst * a.natt + a.natt - 1];
-  const uint64_t L = boffs_ro[inst * a.natt + a.natt] - lb;
-  const bool rwd_err = (a.nval_global - 1) >= 8 * L;              // CheckBit(last, N-1) panics (incentives.go:23)
-  const bool thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (tdep_ro[inst] * 2ull);  // incentives.go:18-20
-  const bool skip = ferr != 0 || (thr && rwd_err);                  // Go panics: balances stay untouched
-  const bool applied = thr && !skip;
-  const uint64_t d = a.dynasty[inst];
-  const uint8_t* lastbf = a.bits + lb;
-  uint64_t* Bal = a.balance + inst * f.vstride;
-  constexpr bool B32 = (MODE & 524288) != 0;
-  uint32_t* Bal32 = B32 ? f.bal32 + inst * f.vstride : nullptr;
-  const uint64_t bbase = B32 ? f.bal32_base[inst] : 0;
-  uint64_t sum = 0, nm = 0;
-  // pipeline: A(k+1) and B(k) in flight when piece k is processed; A(k+2) issued during it
-  uint64_t item = item0;
-  StreamA ca = stream_load_a<MODE>(f, items_ro, inst, item, a.val_offset);
-  StreamB cb_ = stream_load_b<MODE>(a, f, inst, ca, lane);
-  StreamA na = stream_load_a<MODE>(f, items_ro, inst, item + stride, a.val_offset);
-  const uint8_t* lbf8 = reinterpret_cast<const uint8_t*>(lbf_dyn) + (lb & 15);
-  if (LDS) {  // the instance's last bitfield into LDS (16-B chunks from lb & ~15; the buffer is padded)
-    const uint64_t n16 = (L + (lb & 15) + 15) / 16;
-    const uint4* src = reinterpret_cast<const uint4*>(a.bits + (lb & ~15ull));
-    constexpr int kU = 8;  // chunks in flight per thread per round
-    for (uint64_t k0 = 0; k0 < n16; k0 += (uint64_t)kU * blockDim.x) {
-      uint4 t[kU];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const uint64_t k = k0 + (uint64_t)u * blockDim.x + threadIdx.x;
-        t[u] = k < n16 ? src[k] : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const uint64_t k = k0 + (uint64_t)u * blockDim.x + threadIdx.x;
-        if (k < n16) lbf_dyn[k] = t[u];
-      }
-    }
-    __syncthreads();
-  }
-  for (; item < f.nitems; item += stride) {
-    // the reward bits of this piece (dependent on its co_index words): issued first
-    const uint64_t ws = ca.it.x, we = (uint64_t)ca.it.x + ca.it.y, cbase = ca.it.w;
-    const uint64_t p0 = (ws - a.val_offset) & ~3ull, p = p0 + 4ull * lane, g = a.val_offset + p;
-    bool v[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = g + i >= ws && g + i < we;
-    uint32_t rb[4] = {0, 0, 0, 0};
-    if (!(MODE & 256) && applied) {
-      const uint32_t ci4[4] = {cb_.cix.x, cb_.cix.y, cb_.cix.z, cb_.cix.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t ix = v[i] ? ci4[i] : 0u;
-        rb[i] = LDS ? lbf8[ix >> 3] : lastbf[ix >> 3];
-      }
-    }
-    // the next piece's stream, then the one after's descriptor
-    StreamB nb = stream_load_b<MODE>(a, f, inst, na, lane);
-    const StreamA nna = stream_load_a<MODE>(f, items_ro, inst, item + 2 * stride, a.val_offset);
-    uint64_t b[4];
-    if (B32) {  // u64 balance = base + offset (mod 2^64)
-      b[0] = bbase + cb_.qb0.x, b[1] = bbase + cb_.qb0.y, b[2] = bbase + cb_.qb0.z, b[3] = bbase + cb_.qb0.w;
-    } else {
-      b[0] = pack64(cb_.qb0.x, cb_.qb0.y), b[1] = pack64(cb_.qb0.z, cb_.qb0.w), b[2] = pack64(cb_.qb1.x, cb_.qb1.y),
-      b[3] = pack64(cb_.qb1.z, cb_.qb1.w);
-    }
-    // crosslink tallies on the pre-reward balances (core.go:533-545)
-    const uint32_t ga = ca.ic.w, nbits = ca.ic.z;
-    if (ga != kNoAtt) {
-      uint64_t t = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) t += v[i] ? b[i] : 0;
-      const uint64_t ts = wave_sum_dpp(t);
-      const int64_t qs = (int64_t)(g - cbase), last = (int64_t)nbits - 1;
-      const int64_t qlo = qs < 0 ? 0 : qs > last ? last : qs;
-      if (ga != kManyAtt) {
-        uint64_t vv = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int64_t x = qs + i;
-          const uint32_t by = ((x >> 3) == (qlo >> 3)) ? cb_.byA : cb_.byB;
-          if (v[i] && (uint64_t)x < (uint64_t)nbits && ((by >> (7 - (uint32_t)(x & 7))) & 1)) vv += b[i];
-        }
-        const uint64_t vs = wave_sum_dpp(vv);
-        if ((MODE & 131072) && lane == 0) one_win<false>(a, f, inst, ga, vs, ts, cb_.win1, d);
-        if (lane < 2) {  // one instruction: lane 0 the total, lane 1 the vote
-          uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + ga;
-          const uint64_t xx = lane ? vs : ts;
-          if (xx) atomicAdd((unsigned long long*)dst, (unsigned long long)xx);
-        }
-      } else {  // several attestations of this committee: one pair of atomics per attestation
-        const uint32_t* co = catt_offs_ro + inst * (f.ncomm + 1);
-        for (uint32_t k = co[ca.it.z]; k < co[ca.it.z + 1]; ++k) {
-          const uint64_t gk = catt_ro[inst * a.natt + k];
-          const uint64_t boff = boffs_ro[inst * a.natt + gk];
-          const uint64_t nb2 = 8 * (boffs_ro[inst * a.natt + gk + 1] - boff);
-          const uint8_t* bf = a.bits + boff;
-          uint64_t vv = 0;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint64_t x = (uint64_t)(qs + i);
-            if (v[i] && x < nb2 && bit_at(bf, x)) vv += b[i];
-          }
-          vv = wave_sum_dpp(vv);
-          if ((MODE & 131072) && lane == 0) one_win<false>(a, f, inst, (uint32_t)gk, vv, ts, f.att_win[inst * a.natt + gk], d);
-          if (lane < 2) {
-            uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + gk;
-            const uint64_t xx = lane ? vv : ts;
-            if (xx) atomicAdd((unsigned long long*)dst, (unsigned long long)xx);
-          }
-        }
-      }
-    }
-    // classify (validator.go:45-53), reward (incentives.go:22-27), store, sum (core.go:459-464)
-    const uint32_t sw[4] = {cb_.se.x, cb_.se.y, cb_.se.z, cb_.se.w};
-    bool act[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      act[i] = (uint64_t)(sw[i] & 0xFFFFu) <= d && d < (uint64_t)(sw[i] >> 16);
-      nm += (v[i] && !act[i]) ? 1 : 0;
-    }
-    if (applied) {
-      const uint32_t ci4[4] = {cb_.cix.x, cb_.cix.y, cb_.cix.z, cb_.cix.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool r = (MODE & 256) ? ((cb_.lcw >> ((p + i) & 31)) & 1)
-                                    : ((rb[i] >> (7 - ((v[i] ? ci4[i] : 0u) & 7))) & 1);
-        b[i] = r ? b[i] + PZ_ATTESTER_REWARD : b[i] - PZ_ATTESTER_REWARD;
-      }
-      if (B32) {
-        if (v[0] && v[1] && v[2] && v[3]) {
-          *reinterpret_cast<uint4*>(Bal32 + p) = make_uint4((uint32_t)(b[0] - bbase), (uint32_t)(b[1] - bbase),
-                                                            (uint32_t)(b[2] - bbase), (uint32_t)(b[3] - bbase));
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (v[i]) Bal32[p + i] = (uint32_t)(b[i] - bbase);
-        }
-      } else {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int i = 2 * h;
-          if (v[i] && v[i + 1])
-            *reinterpret_cast<uint4*>(Bal + p + i) =
-                make_uint4((uint32_t)b[i], (uint32_t)(b[i] >> 32), (uint32_t)b[i + 1], (uint32_t)(b[i + 1] >> 32));
-          else if (v[i])
-            Bal[p + i] = b[i];
-          else if (v[i + 1])
-            Bal[p + i + 1] = b[i + 1];
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) sum += (v[i] && act[i]) ? b[i] : 0;
-    ca = na;
-    cb_ = nb;
-    na = nna;
-  }
-  sum = wave_sum_dpp(sum);
-  nm = wave_sum_dpp(nm);
-  uint64_t* sc = a.scal + inst * kScal;
-  if (lane == 0) {
-    if (sum && !skip) atomicAdd((unsigned long long*)&sc[kNextBal], (unsigned long long)sum);
-    if (nm) {  // the layout's rank == index premise is broken (the state never allows it)
-      atomicAdd((unsigned long long*)&sc[kNoMatch], (unsigned long long)nm);
-      atomicOr((unsigned long long*)&sc[kErrXl], (unsigned long long)kErrLayout);
-    }
-  }
-  if (item0 == 0) {  // the wave holding the instance's first piece: the per-instance scalars
-    if (lane == 0 && f.rank0) {
-      sc[kPop] = pop;
-      sc[kApplied] = applied ? 1 : 0;
-      sc[kNact] = a.nval_global;
-      sc[kMaxIdx1] = a.nval_global;
-      sc[kErrRwd] = rwd_err ? 1 : 0;
-      if (ferr) atomicAdd((unsigned long long*)&sc[kErrXl], (unsigned long long)ferr);
-    }
-    if (a.scal_next && lane < kScal) a.scal_next[inst * kScal + lane] = 0;
-    if (lane < kPre) f.pre_next[inst * kPre + lane] = 0;
-  }
-}
-
-#define PZ_STREAM_KERNEL(NAME, MODE, T)                                                                      \
-  extern "C" __global__ void __launch_bounds__(T) NAME(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ pre_ro, \
-                                                      const uint64_t* __restrict__ boffs_ro,                    \
-                                                      const uint64_t* __restrict__ tdep_ro,                     \
-                                                      const uint4* __restrict__ items_ro,                       \
-                                                      const uint32_t* __restrict__ catt_offs_ro,                \
-                                                      const uint32_t* __restrict__ catt_ro, uint32_t bpi) {     \
-    stream_kernel_body<MODE>(a, f, pre_ro, boffs_ro, tdep_ro, items_ro, catt_offs_ro, catt_ro, bpi);             \
-  }
-PZ_STREAM_KERNEL(pz_epoch_stream_se16_kernel, 1024 + 16384, 256)
-PZ_STREAM_KERNEL(pz_epoch_stream_lc_se16_kernel, 1280 + 16384, 256)
-PZ_STREAM_KERNEL(pz_epoch_stream_se16_win_kernel, 1024 + 16384 + 131072, 256)
-PZ_STREAM_KERNEL(pz_epoch_stream_lc_se16_win_kernel, 1280 + 16384 + 131072, 256)
-PZ_STREAM_KERNEL(pz_epoch_stream_lds_se16_kernel, 1024 + 16384 + 262144, 1024)
-PZ_STREAM_KERNEL(pz_epoch_stream_lds_se16_win_kernel, 1024 + 16384 + 131072 + 262144, 1024)
-PZ_STREAM_KERNEL(pz_epoch_stream_se16_b32_kernel, 1024 + 16384 + 524288, 256)  // u32 balance offsets
-PZ_STREAM_KERNEL(pz_epoch_stream_se16_b32_win_kernel, 1024 + 16384 + 131072 + 524288, 256)
-// (A/B, variant 1 << 22) the LDS form on the u32 offsets: the last bitfield staged per block
-PZ_STREAM_KERNEL(pz_epoch_stream_lds_se16_b32_kernel, 1024 + 16384 + 262144 + 524288, 1024)
-PZ_STREAM_KERNEL(pz_epoch_stream_lds_se16_b32_win_kernel, 1024 + 16384 + 131072 + 262144 + 524288, 1024)
-#undef PZ_STREAM_KERNEL
-
 // The single-launch step (one instance): no occupancy target (a few dozen blocks), so the
 // bit-count loads the prologue holds do not spill.
 extern "C" __global__ void __launch_bounds__(64 * kFusedWaves)
@@ -2104,37 +1427,6 @@ pz_epoch_one_se16_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ 
   fused_body<512 + 1024 + 16384>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
 }
 
-// The single launch over B instances: grid (B, piece groups), every attested committee one piece
-// (winners in the waves), each instance's bitfields within kMultiMaxBitBytes.
-extern "C" __global__ void __launch_bounds__(64 * kFusedWaves) __attribute__((amdgpu_waves_per_eu(8, 8)))
-pz_epoch_multi_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ boffs_ro,
-                      const uint64_t* __restrict__ tdep_ro, const uint4* __restrict__ items_ro,
-                      const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,
-                      const uint32_t* __restrict__ catt_ro) {
-  fused_body<2048 + 1024>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
-}
-extern "C" __global__ void __launch_bounds__(64 * kFusedWaves) __attribute__((amdgpu_waves_per_eu(8, 8)))
-pz_epoch_multi_se16_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ boffs_ro,
-                           const uint64_t* __restrict__ tdep_ro, const uint4* __restrict__ items_ro,
-                           const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,
-                           const uint32_t* __restrict__ catt_ro) {
-  fused_body<2048 + 1024 + 16384>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
-}
-extern "C" __global__ void __launch_bounds__(64 * kFusedWaves) __attribute__((amdgpu_waves_per_eu(8, 8)))
-pz_epoch_multi_se64_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ boffs_ro,
-                           const uint64_t* __restrict__ tdep_ro, const uint4* __restrict__ items_ro,
-                           const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,
-                           const uint32_t* __restrict__ catt_ro) {
-  fused_body<2048>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
-}
-
-static int g_fused_variant = 0;  // tools/ A/B only
-int set_fused_variant(int v) {
-  const int old = g_fused_variant;
-  g_fused_variant = v;
-  return old;
-}
-
 // ---- launchers ---------------------------------------------------------------------------
 static bool vec_ok(const EpochArgs& a) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
@@ -2144,8 +1436,7 @@ static bool vec_ok(const EpochArgs& a) {
 static CountGrid count_grid(const EpochArgs& a, bool do_val, bool do_pop, bool do_xl) {
   CountGrid g;
   g.vbpi = vblocks_per_inst(a.nval);
-  g.nvb = do_val ? (g_count_variant & 1 ? (g.vbpi + kGroup - 1) / kGroup * kGroup * a.ninst
-                                        : (uint64_t)a.ninst * g.vbpi) : 0;
+  g.nvb = do_val ? (uint64_t)a.ninst * g.vbpi : 0;
   g.pbpi = (a.max_inst_bytes + kPopBytesPerBlock - 1) / kPopBytesPerBlock;
   // The popcount range also resets the crosslink winners (chunk 0 of each instance), so it
   // keeps one block per instance whenever winners will be computed -- even when no bitfield
@@ -2168,19 +1459,11 @@ hipError_t launch_epoch_count(const EpochArgs& a, bool do_val, bool do_pop, bool
   const uint64_t blocks = g.nvb + g.npb + g.nxb;
   if (!blocks) return hipSuccess;
   const dim3 grid((uint32_t)blocks);
-  switch (g_count_variant) {
-    case 1: hipLaunchKernelGGL(pz_epoch_count_v1_kernel, grid, dim3(kThreads), 0, s, a, g); break;
-    case 2: hipLaunchKernelGGL(pz_epoch_count_v2_kernel, grid, dim3(kThreads), 0, s, a, g); break;
-    case 3: hipLaunchKernelGGL(pz_epoch_count_v3_kernel, grid, dim3(kThreads), 0, s, a, g); break;
-    case 4: hipLaunchKernelGGL(pz_epoch_count_v4_kernel, grid, dim3(kThreads), 0, s, a, g); break;
-    case 5: hipLaunchKernelGGL(pz_epoch_count_v5_kernel, grid, dim3(kThreads), 0, s, a, g); break;
-    case 8: hipLaunchKernelGGL(pz_epoch_count_v8_kernel, grid, dim3(kThreads), 0, s, a, g); break;
-    case 16: hipLaunchKernelGGL(pz_epoch_count_v16_kernel, grid, dim3(kThreads), 0, s, a, g); break;
-    default: hipLaunchKernelGGL(pz_epoch_count_kernel, grid, dim3(kThreads), 0, s, a, g);
-  }
+  hipLaunchKernelGGL(pz_epoch_count_kernel, grid, dim3(kThreads), 0, s, a, g);
   return hipGetLastError();
 }
 
+#ifdef PZ_AB_BUILD
 // A stateRecalc's vote-cache tally and its epoch's count pass in ONE launch (the chain
 // engine, one rank): blocks [0, ntb) are the voter-major tally (votes_dev.h), the rest the
 // count pass's blocks.  The two read the same pre-reward balances and write disjoint buffers; the
@@ -2202,6 +1485,8 @@ hipError_t launch_vote_words_count(const VoteWordArgs& v, const EpochArgs& a, hi
   hipLaunchKernelGGL(pz_vote_words_count_kernel, dim3((uint32_t)blocks), dim3(kThreads), 0, s, v, ntb, a, g);
   return hipGetLastError();
 }
+
+#endif
 
 hipError_t launch_epoch_winners(const EpochArgs& a, hipStream_t s) {
   const uint64_t n = (uint64_t)a.ninst * a.natt;
@@ -2239,260 +1524,7 @@ bool fused_ok(const EpochArgs& a) {
          (reinterpret_cast<uintptr_t>(a.co_index) & 7) == 0;
 }
 
-// Winners of the one-pass step.  Sharded (f.own_only), committees never straddle ranks, so an
-// attestation's tallies are complete on the rank holding its committee's first position (the
-// last rank for an empty committee at the end) and zero elsewhere: each rank proposes the
-// winners among the attestations it owns and a u32 minimum all-reduce picks the first.
-extern "C" __global__ void __launch_bounds__(kThreads) pz_epoch_fwin_kernel(EpochArgs a, FusedArgs f) {
-  const uint64_t ga = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ga >= (uint64_t)a.ninst * a.natt) return;
-  if (f.own_only) {
-    const uint64_t cb = a.coffs[a.att_comm[ga]], lo = a.val_offset, hi = lo + a.nval;
-    if (!((cb >= lo && cb < hi) || (cb == a.nval_global && hi == a.nval_global))) return;
-  }
-  winner_one(a, ga);
-}
-
-hipError_t launch_epoch_fwin(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
-  const uint64_t n = (uint64_t)a.ninst * a.natt;
-  if (!n || !a.nrec) return hipSuccess;
-  hipLaunchKernelGGL(pz_epoch_fwin_kernel, dim3((uint32_t)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, a,
-                     f);
-  return hipGetLastError();
-}
-
-// Ablations look the reward bits up in the fused pass (tools/; 128: this A/B); the grid-order
-// variant (the XCD-aware 4096) keeps the product's gather.
-// (grid/lane-layout variants keep it: 4096 XCD-aware grid, 32768 pair lanes, 65536 one piece per
-// wave with quad lanes -- the streaming pass off)
-static bool ablation_no_lastco() {
-  return g_fused_variant && g_fused_variant != 4096 && g_fused_variant != 32768 && g_fused_variant != 65536 &&
-         g_fused_variant != 131072 && g_fused_variant != 262144 && (g_fused_variant >> 20) != 1 &&
-         g_fused_variant != (1 << 21) && g_fused_variant != (1 << 22);
-}
-
-static bool use_lds_form(const EpochArgs& a, const FusedArgs& f);
-hipError_t launch_epoch_pre(const EpochArgs& a, const FusedArgs& f0, hipStream_t s) {
-  FusedArgs f = f0;
-  if (ablation_no_lastco() || use_lds_form(a, f0)) f.lastco = nullptr;
-  uint64_t pbpi = (a.max_inst_bytes + kPopBytesPerBlock - 1) / kPopBytesPerBlock;
-  if (pbpi == 0) pbpi = 1;  // chunk 0 of each instance also resets the winners
-  const uint64_t npb = (uint64_t)a.ninst * pbpi;
-  const uint64_t nab = ((uint64_t)a.ninst * a.natt + kThreads - 1) / kThreads;
-  const uint64_t lcb = f.lastco ? (f.lcw * 32 + kLastCoPos - 1) / kLastCoPos : 0;  // gathering blocks per instance
-  const uint64_t nlb = lcb * a.ninst;
-  if (!a.ninst || !a.natt) return hipSuccess;
-  hipLaunchKernelGGL(pz_epoch_pre_kernel, dim3((uint32_t)(npb + nab + nlb)), dim3(kThreads), 0, s, a, f, pbpi, npb,
-                     nab, lcb);
-  return hipGetLastError();
-}
-
-// The LDS form of the streaming pass: last bitfields up to 128 KiB (1,048,576 validators), about
-// one 16-wave workgroup per CU in all.
-constexpr uint64_t kStreamLdsMax = 131072;
-constexpr uint64_t kStreamLdsBlocks = 256;
-static bool stream_lds_over_lastco() {
-  static const bool on = std::getenv("PZ_EPOCH_LDS_OVER_LASTCO") != nullptr;
-  return on;
-}
-// The product takes the LDS form whenever the last bitfields fit and no position-order gather
-// (lastco, small N) exists; variant 262144 (A/B) and PZ_EPOCH_LDS_OVER_LASTCO take it in place
-// of the gather too (then `pre` skips the gather).
-static bool use_lds_form(const EpochArgs& a, const FusedArgs& f) {
-  const int v = g_fused_variant;
-  if (f.bal32) return false;  // (the u32-offset balances run the quad kernels)
-  if (!((v == 0 || v == 262144) && f.se16 && a.ninst > 1 && f.last_max && f.last_max <= kStreamLdsMax)) return false;
-  return !f.lastco || v == 262144 || stream_lds_over_lastco();
-}
-
-// Blocks (4 waves each) of the streaming pass: about one resident wave per SIMD slot
-// (occupancy x CUs), rounded to a multiple of lcm(4, B) waves so that every wave serves one
-// instance, and no more waves than pieces.
-static uint64_t resident_waves(const void* kernel) {
-  int dev = 0, cus = 256, per = 0;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess || per < 1) per = 4;
-  return (uint64_t)cus * (uint64_t)per * 4;
-}
-static uint32_t stream_blocks(uint64_t B, uint64_t nitems, bool lc, bool b32 = false) {
-  static const uint64_t res_plain = resident_waves((const void*)pz_epoch_stream_se16_kernel);
-  static const uint64_t res_lc = resident_waves((const void*)pz_epoch_stream_lc_se16_kernel);
-  static const uint64_t res_b32 = resident_waves((const void*)pz_epoch_stream_se16_b32_win_kernel);
-  const uint64_t resident = b32 ? res_b32 : lc ? res_lc : res_plain;
-  const uint64_t l = B % 4 == 0 ? B : B % 2 == 0 ? 2 * B : 4 * B;  // lcm(4, B)
-  const uint64_t want = std::min<uint64_t>(resident, B * std::max<uint64_t>(1, nitems));
-  const uint64_t W = std::max<uint64_t>(l, want / l * l);
-  return (uint32_t)(W / 4);
-}
-
-hipError_t launch_epoch_fused(const EpochArgs& a, const FusedArgs& f0, hipStream_t s) {
-  if (!a.ninst) return hipSuccess;
-  FusedArgs f = f0;
-  if (ablation_no_lastco()) f.lastco = nullptr;  // as launch_epoch_pre
-  // at least one group: group 0 writes the per-instance scalars and zeroes the next step's
-  // accumulators, also on a rank whose range holds no piece
-  const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
-  const int variant = g_fused_variant;
-  if (f.bal32 && variant == 131072 && f.se16 && !f.lastco && a.ninst > 1) {
-    // (A/B) the streaming pass on the u32 offsets
-    const uint32_t nb = stream_blocks(a.ninst, f.nitems, false, true);
-    if (f.win_fused)
-      hipLaunchKernelGGL(pz_epoch_stream_se16_b32_win_kernel, dim3(nb), dim3(256), 0, s, a, f, f.pre, a.boffs,
-                         a.total_deposit, f.items, f.catt_offs, f.catt, 0u);
-    else
-      hipLaunchKernelGGL(pz_epoch_stream_se16_b32_kernel, dim3(nb), dim3(256), 0, s, a, f, f.pre, a.boffs,
-                         a.total_deposit, f.items, f.catt_offs, f.catt, 0u);
-    return hipGetLastError();
-  }
-  if (f.bal32 && variant == (1 << 22) && f.se16 && !f.lastco && a.ninst > 1 && f.last_max &&
-      f.last_max <= kStreamLdsMax) {
-    // (A/B) the LDS form of the streaming pass on the u32 offsets: each block stages its
-    // instance's last bitfield once and looks the reward bits up there
-    const uint32_t bpi = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(f.nitems, kStreamLdsBlocks / a.ninst));
-    const size_t lds = (size_t)((f.last_max + 15 + 16) / 16) * 16;
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute((const void*)pz_epoch_stream_lds_se16_b32_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsMax + 64);
-      (void)hipFuncSetAttribute((const void*)pz_epoch_stream_lds_se16_b32_win_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsMax + 64);
-    });
-    if (f.win_fused)
-      hipLaunchKernelGGL(pz_epoch_stream_lds_se16_b32_win_kernel, dim3((uint32_t)(a.ninst * bpi)), dim3(1024), lds, s,
-                         a, f, f.pre, a.boffs, a.total_deposit, f.items, f.catt_offs, f.catt, bpi);
-    else
-      hipLaunchKernelGGL(pz_epoch_stream_lds_se16_b32_kernel, dim3((uint32_t)(a.ninst * bpi)), dim3(1024), lds, s, a,
-                         f, f.pre, a.boffs, a.total_deposit, f.items, f.catt_offs, f.catt, bpi);
-    return hipGetLastError();
-  }
-  if (f.bal32 && variant == (1 << 21) && f.se16 && !f.lastco) {  // (A/B) two pieces per wave
-    const uint64_t g2 = std::max<uint64_t>(1, (f.nitems + kPieces2 - 1) / kPieces2);
-    hipLaunchKernelGGL(pz_epoch_fused_se16_b32_q2_kernel, dim3(a.ninst, (uint32_t)g2), dim3(64 * kFusedWaves), 0, s, a,
-                       f, f.pre, a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt);
-    return hipGetLastError();
-  }
-  if (f.bal32 && variant == 4096 && f.se16 && !f.lastco) {
-    // (A/B) the XCD-aware 1-D grid: a piece group's blocks of every instance on one XCD, so its
-    // co_index words are fetched into one L2 instead of eight
-    const dim3 grid1((uint32_t)(((groups + 7) / 8) * 8 * a.ninst)), blk(64 * kFusedWaves);
-    hipLaunchKernelGGL(pz_epoch_fused_se16_b32_xcd_kernel, grid1, blk, 0, s, a, f, f.pre, a.boffs, a.total_deposit,
-                       f.items, f.cinfo, f.catt_offs, f.catt);
-    return hipGetLastError();
-  }
-  if (f.bal32) {  // balances as u32 offsets: the quad kernels, instance-minor
-    const dim3 grid(a.ninst, (uint32_t)groups), block(64 * kFusedWaves);
-#define PZ_LAUNCH_B32(K) \
-  hipLaunchKernelGGL(K, grid, block, 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt)
-    if ((variant >> 20) == 1 && f.se16) {  // tools/ ablations
-      switch (variant & 0xFFFF) {
-#define PZ_ABL(X)                                                                  \
-  case X:                                                                          \
-    if (f.lastco) PZ_LAUNCH_B32(pz_epoch_fused_lc_se16_b32_a##X##_kernel);         \
-    else PZ_LAUNCH_B32(pz_epoch_fused_se16_b32_a##X##_kernel);                     \
-    return hipGetLastError();
-        PZ_ABL(1) PZ_ABL(2) PZ_ABL(4) PZ_ABL(8) PZ_ABL(3) PZ_ABL(7) PZ_ABL(15)
-#undef PZ_ABL
-        default: break;
-      }
-    }
-    if (f.se16 && f.lastco) PZ_LAUNCH_B32(pz_epoch_fused_lc_se16_b32_kernel);
-    else if (f.se16) PZ_LAUNCH_B32(pz_epoch_fused_se16_b32_kernel);
-    else if (f.lastco) PZ_LAUNCH_B32(pz_epoch_fused_lc_se_b32_kernel);
-    else PZ_LAUNCH_B32(pz_epoch_fused_se_b32_kernel);
-#undef PZ_LAUNCH_B32
-    return hipGetLastError();
-  }
-  if (variant == 4096 && (f.se || f.se16)) {  // the XCD-aware 1-D grid: groups padded to a multiple of 8
-    const dim3 grid1((uint32_t)(((groups + 7) / 8) * 8 * a.ninst)), blk(64 * kFusedWaves);
-#define PZ_LAUNCH_XCD(K) \
-  hipLaunchKernelGGL(K, grid1, blk, 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt)
-    if (f.se16 && f.lastco) PZ_LAUNCH_XCD(pz_epoch_fused_lc_se16_xcd_kernel);
-    else if (f.se16) PZ_LAUNCH_XCD(pz_epoch_fused_se16_xcd_kernel);
-    else if (f.lastco) PZ_LAUNCH_XCD(pz_epoch_fused_lc_se_xcd_kernel);
-    else PZ_LAUNCH_XCD(pz_epoch_fused_se_xcd_kernel);
-#undef PZ_LAUNCH_XCD
-    return hipGetLastError();
-  }
-  if (use_lds_form(a, f)) {
-    // the streaming form with the last bitfield in LDS (the product when it fits; at small N the
-    // position-order gather of `pre` (lastco) is kept unless PZ_EPOCH_LDS_OVER_LASTCO)
-    const uint32_t bpi = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(f.nitems, kStreamLdsBlocks / a.ninst));
-    const size_t lds = (size_t)((f.last_max + 15 + 16) / 16) * 16;
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute((const void*)pz_epoch_stream_lds_se16_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsMax + 64);
-      (void)hipFuncSetAttribute((const void*)pz_epoch_stream_lds_se16_win_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsMax + 64);
-    });
-#define PZ_LAUNCH_LDS(K)                                                                                   \
-  hipLaunchKernelGGL(K, dim3((uint32_t)(a.ninst * bpi)), dim3(1024), lds, s, a, f, f.pre, a.boffs, a.total_deposit, \
-                     f.items, f.catt_offs, f.catt, bpi)
-    if (f.win_fused) PZ_LAUNCH_LDS(pz_epoch_stream_lds_se16_win_kernel);
-    else PZ_LAUNCH_LDS(pz_epoch_stream_lds_se16_kernel);
-#undef PZ_LAUNCH_LDS
-    return hipGetLastError();
-  }
-  if ((variant == 0 || variant == 131072) && f.se16 && a.ninst > 1) {
-    // the streaming form (persistent, pipelined waves; variant 131072: this form where the product
-    // takes the LDS one)
-    const uint32_t nb = stream_blocks(a.ninst, f.nitems, f.lastco != nullptr);
-#define PZ_LAUNCH_STREAM(K) \
-  hipLaunchKernelGGL(K, dim3(nb), dim3(256), 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.catt_offs, f.catt, 0u)
-    if (f.win_fused && f.lastco) PZ_LAUNCH_STREAM(pz_epoch_stream_lc_se16_win_kernel);
-    else if (f.win_fused) PZ_LAUNCH_STREAM(pz_epoch_stream_se16_win_kernel);
-    else if (f.lastco) PZ_LAUNCH_STREAM(pz_epoch_stream_lc_se16_kernel);
-    else PZ_LAUNCH_STREAM(pz_epoch_stream_se16_kernel);
-#undef PZ_LAUNCH_STREAM
-    return hipGetLastError();
-  }
-  // (the ablations that read FusedArgs.se run the product's kernel when the state holds se16)
-  const int var = ((variant & 1024) && !f.se) ? 0 : variant;
-  // instance-minor: x = instance, y = piece group (ablation 32: instance-major)
-  const dim3 grid = (variant & 32) ? dim3((uint32_t)groups, a.ninst) : dim3(a.ninst, (uint32_t)groups);
-  const dim3 block(64 * kFusedWaves);
-#define PZ_LAUNCH_FUSED(K) \
-  hipLaunchKernelGGL(K, grid, block, 0, s, a, f, f.pre, a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt)
-  if (variant == 32768 && (f.se || f.se16)) {  // A/B: the pair lanes of round 3
-    if (f.se16 && f.lastco) PZ_LAUNCH_FUSED(pz_epoch_fused_lc_se16_pair_kernel);
-    else if (f.se16) PZ_LAUNCH_FUSED(pz_epoch_fused_se16_pair_kernel);
-    else if (f.lastco) PZ_LAUNCH_FUSED(pz_epoch_fused_lc_se_pair_kernel);
-    else PZ_LAUNCH_FUSED(pz_epoch_fused_se_pair_kernel);
-    return hipGetLastError();
-  }
-  switch (var) {
-    case 1: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg1_kernel); break;
-    case 2: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg2_kernel); break;
-    case 3: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg3_kernel); break;
-    case 4: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg4_kernel); break;
-    case 7: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg7_kernel); break;
-    case 8: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg8_kernel); break;
-    case 15: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg15_kernel); break;
-    case 16: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg16_kernel); break;
-    case 32: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg32_kernel); break;
-    case 48: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg48_kernel); break;
-    case 1024: PZ_LAUNCH_FUSED(pz_epoch_fused_se_kernel); break;  // (ablation baseline: no lastco)
-    case 1088: PZ_LAUNCH_FUSED(pz_epoch_fused_dbg1088_kernel); break;
-    default:
-      if (f.lastco && f.se16)
-        PZ_LAUNCH_FUSED(pz_epoch_fused_lc_se16_kernel);
-      else if (f.se16)
-        PZ_LAUNCH_FUSED(pz_epoch_fused_se16_kernel);
-      else if (f.lastco && f.se)
-        PZ_LAUNCH_FUSED(pz_epoch_fused_lc_se_kernel);
-      else if (f.lastco)
-        PZ_LAUNCH_FUSED(pz_epoch_fused_lc_kernel);
-      else if (f.se)
-        PZ_LAUNCH_FUSED(pz_epoch_fused_se_kernel);
-      else
-        PZ_LAUNCH_FUSED(pz_epoch_fused_kernel);
-  }
-#undef PZ_LAUNCH_FUSED
-  return hipGetLastError();
-}
-
-bool epoch_one_enabled(const FusedArgs& f) { return f.one && g_fused_variant == 0; }
+bool epoch_one_enabled(const FusedArgs& f) { return f.one != 0; }
 
 hipError_t launch_epoch_one(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
   const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
@@ -2505,23 +1537,6 @@ hipError_t launch_epoch_one(const EpochArgs& a, const FusedArgs& f, hipStream_t 
   else
     hipLaunchKernelGGL(pz_epoch_one_kernel, dim3(1, (uint32_t)groups), dim3(64 * kFusedWaves), 0, s, a, f, a.boffs,
                        a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt);
-  return hipGetLastError();
-}
-
-bool epoch_multi_enabled(const FusedArgs& f) { return f.multi && g_fused_variant == 0; }
-
-hipError_t launch_epoch_multi(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
-  const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
-  const dim3 grid(a.ninst, (uint32_t)groups), block(64 * kFusedWaves);
-  if (f.se16)
-    hipLaunchKernelGGL(pz_epoch_multi_se16_kernel, grid, block, 0, s, a, f, a.boffs, a.total_deposit, f.items,
-                       f.cinfo, f.catt_offs, f.catt);
-  else if (f.se)
-    hipLaunchKernelGGL(pz_epoch_multi_kernel, grid, block, 0, s, a, f, a.boffs, a.total_deposit, f.items, f.cinfo,
-                       f.catt_offs, f.catt);
-  else
-    hipLaunchKernelGGL(pz_epoch_multi_se64_kernel, grid, block, 0, s, a, f, a.boffs, a.total_deposit, f.items,
-                       f.cinfo, f.catt_offs, f.catt);
   return hipGetLastError();
 }
 

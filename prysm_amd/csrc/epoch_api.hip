@@ -495,23 +495,14 @@ int pz_shuffle_validators_to_committees(const uint8_t seed[32], const uint64_t* 
 
 }  // extern "C"
 
+#ifdef PZ_AB_BUILD  // the A/B library only (tools/epoch_parts.py)
 // Internal: launch pass 1 with a subset of its block ranges (per-part timing in tools/).
 extern "C" int pz_debug_epoch_count(const pz_epoch_batch* b, int do_val, int do_pop, int do_xl, void* stream) {
   hipError_t e = pz::launch_epoch_count(*b, do_val != 0, do_pop != 0, do_xl != 0, (hipStream_t)stream);
   return e == hipSuccess ? PZ_OK : pz::hip_fail(e, "pz_epoch_count_kernel");
 }
-namespace pz {
-hipError_t launch_epoch_reward_mode(const EpochArgs& a, int mode, hipStream_t s);
-int set_count_variant(int v);
-}
-// Internal: select the count-pass variant for in-process A/B timing (tools/epoch_parts.py).
-extern "C" int pz_debug_set_count_variant(int v) { return pz::set_count_variant(v); }
-extern "C" int pz_debug_set_fused_variant(int v) { return pz::set_fused_variant(v); }
-extern "C" int pz_debug_epoch_reward_mode(const pz_epoch_batch* b, int mode, void* stream) {
-  hipError_t e = pz::launch_epoch_reward_mode(*b, mode, (hipStream_t)stream);
-  return e == hipSuccess ? PZ_OK : pz::hip_fail(e, "pz_epoch_reward_kernel (mode)");
-}
 extern "C" int pz_debug_epoch_reward(const pz_epoch_batch* b, void* stream) {
   hipError_t e = pz::launch_epoch_reward(*b, (hipStream_t)stream);
   return e == hipSuccess ? PZ_OK : pz::hip_fail(e, "pz_epoch_reward_kernel");
 }
+#endif

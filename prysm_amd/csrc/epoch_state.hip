@@ -44,7 +44,9 @@ struct Part {
   uint64_t* nb = nullptr;                 // [B] next-cycle totals, contiguous for the all-reduce
   hipEvent_t ev_red = nullptr, ev_gather = nullptr, ev_nb = nullptr;
   EpochArgs a;
-  FusedArgs f;                            // one-pass step (pz_epoch_state::fused)
+  FusedArgs f;                            // one-pass step, one instance (pz_epoch_one_kernel)
+  bool window = false;                    // one-pass step, the window pass (epoch_window.hip)
+  WinArgs w;
 };
 
 struct Shard {
@@ -75,6 +77,7 @@ struct pz_epoch_state {
   // offsets are re-based (each step moves an offset by at most 1; see kBal32Window)
   bool b32 = false;
   uint64_t b32_left = 0;
+  pz_epoch_options opts{};
   std::vector<Shard> sh;
   ~pz_epoch_state();
 };
@@ -167,10 +170,8 @@ int upload_se16(Shard& s, uint32_t** p, const uint64_t* start, const uint64_t* e
 // part to the u64 column.
 constexpr uint64_t kBal32Window = 1ull << 30;
 constexpr uint64_t kBal32Period = 1ull << 29;
-static uint64_t bal32_period() {  // PZ_EPOCH_B32_PERIOD: tests exercise the re-base
-  const char* e = std::getenv("PZ_EPOCH_B32_PERIOD");
-  const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
-  return v && v < kBal32Period ? v : kBal32Period;
+static uint64_t bal32_period(uint64_t opt) {  // pz_epoch_options.rebase_period (tests: the re-base)
+  return opt && opt < kBal32Period ? opt : kBal32Period;
 }
 
 // The base of every instance of [i0, i0 + Bp) over the values vals(b, q), q < n; false if some
@@ -231,10 +232,6 @@ static int part_balances(const Shard& s, const Part& q, uint64_t* out, uint64_t 
 // the part to the u64 column).  Rare: once per kBal32Period steps.
 static int bal32_rebase(pz_epoch_state* st);
 
-static bool win_fused_off() {
-  const char* e = std::getenv("PZ_EPOCH_WIN_FUSED");
-  return e && e[0] == '0';
-}
 
 uint64_t shard_words(uint64_t N, int world) { return std::max<uint64_t>(1, (N + 64ull * world - 1) / (64ull * world)); }
 
@@ -248,16 +245,12 @@ int step_world1(pz_epoch_state* st) {
         if (e != hipSuccess) return hip_fail(e, "epoch step (single launch)");
         continue;
       }
-      if (st->fused && epoch_multi_enabled(s.part[p].f)) {  // B instances, one launch
-        hipError_t e = launch_epoch_multi(a, s.part[p].f, s.s);
-        if (e != hipSuccess) return hip_fail(e, "epoch step (multi-instance launch)");
-        continue;
-      }
-      if (st->fused) {
-        hipError_t e = launch_epoch_pre(a, s.part[p].f, s.s);
-        if (e == hipSuccess) e = launch_epoch_fused(a, s.part[p].f, s.s);
-        if (e == hipSuccess && !s.part[p].f.win_fused) e = launch_epoch_mid(a, st->nrec != 0, false, s.s);
-        if (e != hipSuccess) return hip_fail(e, "epoch step (one pass)");
+      if (st->fused && s.part[p].window) {  // the window pass: one launch
+        Part& q = s.part[p];
+        q.w.bal32 = q.f.bal32;  // (a re-base may have returned the part to the u64 column)
+        q.w.bal32_base = q.f.bal32_base;
+        hipError_t e = launch_epoch_window(a, q.w, s.s);
+        if (e != hipSuccess) return hip_fail(e, "epoch step (window pass)");
         continue;
       }
       hipError_t e = launch_epoch_count(a, true, true, a.natt != 0, s.s);
@@ -279,6 +272,10 @@ void flip(pz_epoch_state* st) {
         q.win_results = q.a.winner;
         std::swap(q.a.winner, q.f.winner_next);
       }
+      if (q.window) {
+        q.win_results = q.a.winner;
+        std::swap(q.a.winner, q.w.winner_next);
+      }
       const uint64_t Bp = q.B, natt = st->natt;
       q.a.scal = q.red[q.cur];
       q.a.vote = q.red[q.cur] + Bp * kScal;
@@ -289,6 +286,10 @@ void flip(pz_epoch_state* st) {
       q.f.pre_next = q.red[q.cur ^ 1] + pre;
       q.f.vote_next = q.red[q.cur ^ 1] + Bp * kScal;
       q.f.total_next = q.red[q.cur ^ 1] + Bp * kScal + Bp * natt;
+      if (q.window && st->world > 1) {  // non-owned attestations' tallies must read zero
+        q.w.vote_next = q.f.vote_next;
+        q.w.total_next = q.f.total_next;
+      }
     }
 }
 
@@ -318,10 +319,10 @@ int step_sharded_fused(pz_epoch_state* st) {
       Shard& s = st->sh[i];
       Part& q = s.part[p];
       (void)hipSetDevice(s.dev);
-      hipError_t e = launch_epoch_pre(q.a, q.f, s.s);
-      if (e == hipSuccess) e = launch_epoch_fused(q.a, q.f, s.s);
-      if (e == hipSuccess) e = launch_epoch_fwin(q.a, q.f, s.s);
-      if (e != hipSuccess) return hip_fail(e, "epoch one-pass");
+      q.w.bal32 = q.f.bal32;
+      q.w.bal32_base = q.f.bal32_base;
+      hipError_t e = launch_epoch_window(q.a, q.w, s.s);
+      if (e != hipSuccess) return hip_fail(e, "epoch one-pass (window pass)");
       sbufs[i] = q.red[q.cur];
       mbufs[i] = q.a.winner;
       evs[i] = q.ev_red;
@@ -525,6 +526,132 @@ void local_committees(const pz_epoch_host* h, uint64_t lo, uint64_t hi, bool kee
 
 }  // namespace
 
+// The window pass's plan for one part of one rank (epoch.h WinArgs): the rank's committees
+// (those whose first position lies in [lo, hi); the last rank also takes the empty ones at N)
+// split into R ranges of about equal positions, R = CUs / B (one block per CU), each range's
+// 256-position windows with their first committee, the per-instance committee table, and the
+// LDS carve-up.  The last bitfield goes into LDS when the block still fits the CU's 160 KiB.
+static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Part& q, const std::vector<uint32_t>& catt_offs,
+                const std::vector<uint32_t>& catt) {
+  const uint64_t Bp = q.B, i0 = q.i0, natt = st->natt, nc1 = st->ncomm + 1, N = st->N;
+  const uint64_t* coffs = h->coffs;
+  const uint64_t cg0 = std::lower_bound(coffs, coffs + st->ncomm, s.lo) - coffs;
+  const uint64_t cg1 = s.hi >= N ? st->ncomm : (uint64_t)(std::lower_bound(coffs, coffs + st->ncomm, s.hi) - coffs);
+  const uint32_t nlc = (uint32_t)(cg1 - cg0);
+  std::vector<uint32_t> lcs(nlc + 1);
+  for (uint32_t k = 0; k <= nlc; ++k) lcs[k] = (uint32_t)((k < nlc ? coffs[cg0 + k] : s.hi) - s.lo);
+  // per instance: committee table, single-attestation bit counts, attestation columns
+  std::vector<uint4> lci((size_t)Bp * (nlc + 1));
+  std::vector<uint32_t> lnb((size_t)Bp * std::max<uint32_t>(nlc, 1), 0), csz((size_t)Bp * natt);
+  std::vector<uint4> aw((size_t)Bp * natt);
+  uint32_t wpc = 1;
+  for (uint64_t b = 0; b < Bp; ++b) {
+    const uint32_t* o = catt_offs.data() + (i0 + b) * nc1;
+    const uint64_t gb = (i0 + b) * natt;
+    for (uint32_t k = 0; k <= nlc; ++k) {
+      const uint64_t c = cg0 + k;
+      uint4 e = make_uint4(0, 0, kNoAtt, o[c]);
+      if (k < nlc && o[c + 1] - o[c] == 1) {
+        const uint32_t g = catt[(i0 + b) * natt + o[c]];
+        const uint64_t bo = h->boffs[gb + g], blen = h->boffs[gb + g + 1] - bo;
+        e = make_uint4((uint32_t)bo, (uint32_t)(bo >> 32), g, o[c]);
+        const uint64_t nb = std::min<uint64_t>(coffs[c + 1] - coffs[c], 8 * blen);
+        lnb[b * nlc + k] = (uint32_t)nb;
+        wpc = std::max<uint32_t>(wpc, (uint32_t)((nb + 31) / 32));
+      } else if (k < nlc && o[c + 1] - o[c] > 1) {
+        e.z = kManyAtt;
+      }
+      lci[b * (nlc + 1) + k] = e;
+    }
+    for (uint64_t g = 0; g < natt; ++g) {
+      const uint32_t c = h->att_comm[gb + g], sh = h->att_shard[gb + g];  // (sh < nrec: plan_layout)
+      csz[b * natt + g] = (uint32_t)(coffs[c + 1] - coffs[c]);
+      const uint64_t rd = h->rec_dynasty[(i0 + b) * st->nrec + sh];
+      aw[b * natt + g] = make_uint4(sh, (uint32_t)rd, (uint32_t)(rd >> 32), 0);
+    }
+  }
+  // the last bitfield's LDS copy: from (lb & ~15) to the instance's end, 16-B chunks
+  uint64_t lbf = 0;
+  for (uint64_t b = 0; b < Bp; ++b) {
+    const uint64_t gb = (i0 + b) * natt, lb = h->boffs[gb + natt - 1], pend = h->boffs[gb + natt];
+    lbf = std::max<uint64_t>(lbf, (pend - (lb & ~15ull) + 15) & ~15ull);
+  }
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.dev);
+  uint32_t R = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::max<uint32_t>(nlc, 1), ((uint64_t)cus + Bp - 1) / Bp));
+  std::vector<uint4> rdesc;
+  std::vector<uint32_t> wdesc;
+  WinArgs& w = q.w;
+  std::memset(&w, 0, sizeof w);
+  constexpr size_t kLdsMax = 160 * 1024 - 512;  // (the kernel's static reduction slots)
+  for (;;) {
+    rdesc.assign(R, make_uint4(0, 0, 0, 0));
+    wdesc.clear();
+    uint32_t c = 0, maxc = 0, maxk = 0, maxw = 0;
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint64_t t = (uint64_t)lcs[nlc] * (r + 1) / R;
+      uint32_t c1 = c;
+      if (r + 1 == R) {
+        c1 = nlc;
+      } else {
+        while (c1 < nlc && lcs[c1 + 1] <= t) ++c1;
+        if (c1 == c && c1 < nlc) ++c1;  // at least one committee per range while they last
+      }
+      const uint64_t P0 = lcs[c], P1 = lcs[c1], P0a = P0 & ~3ull;
+      const uint32_t nwin = P1 > P0 ? (uint32_t)((P1 - P0a + 255) / 256) : 0;
+      rdesc[r] = make_uint4(c, c1, (uint32_t)wdesc.size(), nwin);
+      uint32_t cc = c;
+      for (uint32_t k = 0; k < nwin; ++k) {
+        const uint64_t ws = P0a + 256ull * k;
+        while (cc + 1 < c1 && lcs[cc + 1] <= ws) ++cc;
+        wdesc.push_back(cc);
+      }
+      maxc = std::max(maxc, c1 - c);
+      maxw = std::max(maxw, nwin);
+      for (uint64_t b = 0; b < Bp; ++b)
+        maxk = std::max(maxk, lci[b * (nlc + 1) + c1].w - lci[b * (nlc + 1) + c].w);
+      c = c1;
+    }
+    w.R = R;
+    w.lds_maxc = std::max<uint32_t>(maxc, 1);
+    w.lds_maxk = (std::max<uint32_t>(maxk, 1) + 1) & ~1u;  // (keeps the byte arrays after it 16-B aligned)
+    w.lds_vw = 8 * maxw + 2;
+    w.wpc = wpc;
+    w.lds_lbf = (uint32_t)lbf;
+    if (window_lds_bytes(w) <= kLdsMax) break;
+    w.lds_lbf = 0;  // the reward bits looked up in L2 instead
+    if (window_lds_bytes(w) <= kLdsMax) break;
+    if (R >= nlc) return fail(PZ_EINVAL, "window pass: no range split fits the LDS");
+    R = std::min<uint32_t>(nlc, 2 * R);
+  }
+  if (wdesc.empty()) wdesc.push_back(0);
+  uint4 *d_rdesc = nullptr, *d_lci = nullptr, *d_aw = nullptr;
+  uint32_t *d_wdesc = nullptr, *d_lcs = nullptr, *d_lnb = nullptr, *d_csz = nullptr, *d_wn = nullptr;
+  int rc;
+  if ((rc = upload(s, &d_rdesc, rdesc.data(), rdesc.size())) || (rc = upload(s, &d_wdesc, wdesc.data(), wdesc.size())) ||
+      (rc = upload(s, &d_lcs, lcs.data(), lcs.size())) || (rc = upload(s, &d_lci, lci.data(), lci.size())) ||
+      (rc = upload(s, &d_lnb, lnb.data(), lnb.size())) || (rc = upload(s, &d_csz, csz.data(), csz.size())) ||
+      (rc = upload(s, &d_aw, aw.data(), aw.size())) ||
+      (rc = dalloc(s, &d_wn, (size_t)Bp * std::max<uint32_t>(st->nrec, 1))))
+    return rc;
+  w.rdesc = d_rdesc;
+  w.wdesc = d_wdesc;
+  w.lcs = d_lcs;
+  w.lci = d_lci;
+  w.lnb = d_lnb;
+  w.nlc = nlc;
+  w.catt = q.f.catt;
+  w.att_csize = d_csz;
+  w.att_win = d_aw;
+  w.se16 = q.f.se16;
+  w.se = q.f.se;
+  w.vstride = s.np;
+  w.winner_next = d_wn;
+  w.rank0 = s.grank == 0 ? 1 : 0;
+  q.window = true;
+  return PZ_OK;
+}
+
 pz_epoch_state::~pz_epoch_state() {
   for (Shard& s : sh) {
     (void)hipSetDevice(s.dev);
@@ -543,11 +670,17 @@ pz_epoch_state::~pz_epoch_state() {
 extern "C" {
 
 int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epoch_state** out) {
+  return pz_epoch_state_new_opts(comm, device, h, nullptr, out);
+}
+
+int pz_epoch_state_new_opts(pz_comm* comm, int device, const pz_epoch_host* h, const pz_epoch_options* opts,
+                            pz_epoch_state** out) {
   if (!out) return fail(PZ_EINVAL, "out is null");
   *out = nullptr;
   int rc = check_host(h);
   if (rc) return rc;
   pz_epoch_state* st = new pz_epoch_state();
+  if (opts) st->opts = *opts;
   st->comm = comm;
   st->world = comm ? comm->world : 1;
   st->B = h->ninst;
@@ -639,10 +772,8 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
       if ((rc = upload(s, &co_index, ci.data(), ci.size()))) break;
       // the one-pass stream's {start, end}: 4 B when every CurrentDynasty is below 0xFFFF, 8 B
       // when below 2^32 - 1 (saturated bounds classify exactly below the saturation value),
-      // else the 64-bit columns.  (A/B knobs: PZ_EPOCH_SE32 skips the 16-bit column,
-      // PZ_EPOCH_SE64 both.)
-      bool small_d = st->fused && !std::getenv("PZ_EPOCH_SE64");
-      bool tiny_d = small_d && !std::getenv("PZ_EPOCH_SE32");
+      // else the 64-bit columns
+      bool small_d = st->fused, tiny_d = st->fused;
       for (uint64_t b = 0; b < st->B && small_d; ++b) small_d = h->dynasty[b] < 0xFFFFFFFFull;
       for (uint64_t b = 0; b < st->B && tiny_d; ++b) tiny_d = h->dynasty[b] < 0xFFFFull;
       if (tiny_d) {
@@ -783,109 +914,60 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
         q.f.se = se ? se + i0 * s.np : nullptr;
         q.f.se16 = se16 ? se16 + i0 * s.np : nullptr;
         if (!fused_ok(a)) rc = fail(PZ_EINVAL, "one-pass epoch: validator arrays not on the 16-B path");
-        // the reward bits in position order (gathered by `pre` through LDS) when every
-        // instance's last bitfield fits the gathering block's stage
-        uint64_t maxl = 0;
-        for (uint64_t b = i0; b < i0 + Bp && st->natt; ++b)
-          maxl = std::max<uint64_t>(maxl, h->boffs[b * st->natt + st->natt] - h->boffs[b * st->natt + st->natt - 1]);
-        q.f.last_max = maxl;
-        // (PZ_EPOCH_NO_LASTCO, A/B: no gather; the stream looks each reward bit up)
-        if (!rc && st->natt && maxl <= kLastCoMaxBytes && s.np && !std::getenv("PZ_EPOCH_NO_LASTCO")) {
-          q.f.lcw = (s.np + 31) / 32;
-          rc = dalloc(s, &q.f.lastco, (size_t)Bp * q.f.lcw);
-        }
-        // winners formed in the fused waves when every attested committee of every instance
-        // is one piece (its complete tallies in one wave), on one rank: per attestation its
-        // {shard, that record's dynasty} (the records are inputs of the state)
-        bool win_waves = !rc && st->world == 1 && st->natt && st->nrec > 0;
-        if (win_waves) {
+        // one instance on one rank: the single-launch step (latency path), within its limits
+        // and when every attested committee is one piece (the waves form the winners)
+        bool one = !rc && !st->opts.window_only && Bp == 1 && st->world == 1 && st->natt && st->nrec > 0 && st->natt <= kOneMaxAtt &&
+                   st->nrec <= kOneMaxRec && max_inst_bytes <= kOneMaxBitBytes;
+        std::vector<uint2> aw;
+        if (one) {
           std::vector<uint32_t> pieces(st->ncomm, 0);
           for (const uint4& it : items) ++pieces[it.z];
-          std::vector<uint2> aw((size_t)Bp * st->natt);
-          for (uint64_t b = 0; b < Bp && win_waves; ++b)
-            for (uint64_t g = 0; g < st->natt && win_waves; ++g) {
-              const uint64_t ga = (i0 + b) * st->natt + g;
-              const uint32_t sh = h->att_shard[ga];
-              win_waves = pieces[h->att_comm[ga]] == 1 && sh < st->nrec;
-              const uint64_t rd = win_waves ? h->rec_dynasty[(i0 + b) * st->nrec + sh] : 0;
-              if (rd >> 32) win_waves = false;  // (a 32-bit record dynasty)
-              aw[b * st->natt + g] = make_uint2(sh, (uint32_t)rd);
-            }
-          uint2* d_aw = nullptr;
-          if (win_waves) rc = upload(s, &d_aw, aw.data(), aw.size());
-          q.f.att_win = d_aw;
+          aw.resize(st->natt);
+          for (uint64_t g = 0; g < st->natt && one; ++g) {
+            const uint64_t ga = i0 * st->natt + g;
+            const uint32_t sh = h->att_shard[ga];
+            one = pieces[h->att_comm[ga]] == 1 && sh < st->nrec;
+            const uint64_t rd = one ? h->rec_dynasty[i0 * st->nrec + sh] : 0;
+            if (rd >> 32) one = false;  // (a 32-bit record dynasty)
+            aw[g] = make_uint2(sh, (uint32_t)rd);
+          }
         }
-        // one instance on one rank: the single-launch step (latency path), within its limits
-        if (!rc && Bp == 1 && st->world == 1 && st->natt && st->natt <= kOneMaxAtt && st->nrec <= kOneMaxRec &&
-            max_inst_bytes <= kOneMaxBitBytes) {
+        if (one) {
           q.f.one = 1;
+          q.f.win_in_wave = 1;
           std::vector<uint32_t> cs(st->natt);
           for (uint64_t g = 0; g < st->natt; ++g) {
             const uint32_t c = h->att_comm[i0 * st->natt + g];
             cs[g] = (uint32_t)(h->coffs[c + 1] - h->coffs[c]);
           }
-          uint32_t* d_cs = nullptr;
+          uint32_t *d_cs = nullptr, *w2 = nullptr;
+          uint2* d_aw = nullptr;
           rc = dalloc(s, &q.f.ticket, 1);
           if (!rc) rc = upload(s, &d_cs, cs.data(), cs.size());
+          if (!rc) rc = upload(s, &d_aw, aw.data(), aw.size());
+          if (!rc) rc = dalloc(s, &w2, st->nrec);
           q.f.att_csize = d_cs;
-          // else the last block forms the winners (one_tail); in the waves they ping-pong: a step
-          // resets the next one's buffer
-          if (!rc && win_waves) {
-            uint32_t* w2 = nullptr;
-            rc = dalloc(s, &w2, st->nrec);
-            hipError_t e2 = hipSuccess;
-            if (!rc) e2 = hipMemsetAsync(w2, 0xFF, (size_t)st->nrec * 4, s.s);
-            if (!rc && e2 == hipSuccess) e2 = hipMemsetAsync(a.winner, 0xFF, (size_t)st->nrec * 4, s.s);
-            if (!rc && e2 != hipSuccess) rc = hip_fail(e2, "hipMemsetAsync (winners)");
-            q.f.win_in_wave = 1;
-            q.f.winner_next = w2;
-          }
-        } else if (!rc && win_waves && Bp > 1 && max_inst_bytes <= kMultiMaxBitBytes && st->natt <= kMultiMaxAtt &&
-                   std::getenv("PZ_EPOCH_MULTI")) {
-          // (A/B knob) B instances in ONE launch (pz_epoch_multi_kernel): each block counts its
-          // instance's bitfields itself, the waves form the winners (ping-pong per instance); no
-          // pre, no mid.  Measured level with pre + fused + mid at 65,536 x 256 (99.0-100.0 vs
-          // 99.1-99.5 us, profiles/r03/epoch_ab_multi_r3ai.txt): the per-block prologue and the
-          // scratch it spills at 8 waves per SIMD cost what the two launches cost
-          q.f.multi = 1;
-          std::vector<uint32_t> cs((size_t)Bp * st->natt);
-          for (uint64_t b = 0; b < Bp; ++b)
-            for (uint64_t g = 0; g < st->natt; ++g) {
-              const uint32_t c = h->att_comm[(i0 + b) * st->natt + g];
-              cs[b * st->natt + g] = (uint32_t)(h->coffs[c + 1] - h->coffs[c]);
-            }
-          uint32_t* d_cs = nullptr;
-          rc = upload(s, &d_cs, cs.data(), cs.size());
-          q.f.att_csize = d_cs;
-          uint32_t* w2 = nullptr;
-          if (!rc) rc = dalloc(s, &w2, (size_t)Bp * st->nrec);
-          hipError_t e2 = hipSuccess;
-          if (!rc) e2 = hipMemsetAsync(w2, 0xFF, (size_t)Bp * st->nrec * 4, s.s);
-          if (!rc && e2 == hipSuccess) e2 = hipMemsetAsync(a.winner, 0xFF, (size_t)Bp * st->nrec * 4, s.s);
-          if (!rc && e2 != hipSuccess) rc = hip_fail(e2, "hipMemsetAsync (winners)");
-          q.f.win_in_wave = 1;
+          q.f.att_win = d_aw;
           q.f.winner_next = w2;
-        } else if (!rc && win_waves && !win_fused_off()) {
-          // the same in the multi-instance streaming pass: pre resets the winners, the wave
-          // holding a committee proposes its attestation (one_win), and no mid launch follows.
-          // (Round 3's per-piece waves measured 0.2-2 us per step slower than the mid launch,
-          // profiles/r03/epoch_ab_r3af.txt; the streaming pass loads the {shard, dynasty} word
-          // in its pipelined stage.  PZ_EPOCH_WIN_FUSED=0: the mid launch, for A/B.)
-          q.f.win_fused = 1;
+        } else if (!rc) {
+          rc = plan_window(st, h, s, q, catt_offs, catt);
         }
-        // the balances as u32 offsets (FusedArgs.bal32) for the multi-instance quad kernels
-        if (!rc && (se || se16) && !q.f.one && !q.f.multi && Bp > 1 && s.n && !std::getenv("PZ_EPOCH_BAL64")) {
+        // the balances as u32 offsets (FusedArgs.bal32) for the window pass
+        if (!rc && q.window && s.n) {
           const uint32_t* inv = st->co_inv.data();
           auto vals = [&](uint64_t b, uint64_t p) { return h->balance[(i0 + b) * st->N + inv[s.lo + p]]; };
           std::vector<uint64_t> base;
           if (bal32_bases(Bp, s.n, vals, base)) {
             rc = bal32_upload(s, q, vals, base, true);
             st->b32 = true;
-            // the u32-offset kernels look each reward bit up (co_index -> last bitfield) rather
-            // than read pre's position-order gather: 65,536 x 256 cold 85.5-87.1 -> 79.0-79.4 us
-            // (profiles/r04/epoch_cold_ab_r4i.txt; PZ_EPOCH_B32_LASTCO=1 keeps the gather, A/B)
-            if (!std::getenv("PZ_EPOCH_B32_LASTCO")) q.f.lastco = nullptr, q.f.lcw = 0;
           }
+        }
+        // the winners ping-pong (a step resets the next one's buffer): both start empty
+        if (!rc && st->nrec && (q.f.one || q.window)) {
+          uint32_t* nxt = q.f.one ? q.f.winner_next : q.w.winner_next;
+          hipError_t e2 = hipMemsetAsync(nxt, 0xFF, (size_t)Bp * st->nrec * 4, s.s);
+          if (e2 == hipSuccess) e2 = hipMemsetAsync(a.winner, 0xFF, (size_t)Bp * st->nrec * 4, s.s);
+          if (e2 != hipSuccess) rc = hip_fail(e2, "hipMemsetAsync (winners)");
         }
       }
       q.cur = 1;  // flip() below binds red[0] as the first step's buffer
@@ -903,7 +985,7 @@ int pz_epoch_state_new(pz_comm* comm, int device, const pz_epoch_host* h, pz_epo
       return hip_fail(e, "epoch state upload");
     }
   }
-  st->b32_left = bal32_period();
+  st->b32_left = bal32_period(st->opts.rebase_period);
   flip(st);
   *out = st;
   return PZ_OK;
@@ -914,7 +996,7 @@ int pz_epoch_state_step(pz_epoch_state* st) {
   int rc;
   if (st->b32 && st->b32_left == 0) {
     if ((rc = bal32_rebase(st))) return rc;
-    st->b32_left = bal32_period();
+    st->b32_left = bal32_period(st->opts.rebase_period);
   }
   rc = st->world > 1 ? step_sharded(st) : step_world1(st);
   if (rc) return rc;

@@ -1,0 +1,488 @@
+// The window pass: the one-pass epoch step on the committee-order layout in ONE launch
+// (round 5; epoch.h "one-pass epoch" states why one pass is exact).  It replaces round 4's
+// pre + fused launches, whose waves each took one committee piece through three dependent
+// round trips (piece descriptor -> stream -> reward-bit lookups through L2) and ran the
+// 1M x 16 cold step at 0.36 of 8 TB/s.
+//
+// Block (instance i, range r): the committees [cr0, cr1) of this rank, a contiguous run of
+// storage positions [P0, P1) (committee order: committee c is positions [lcs[c], lcs[c+1])).
+// The ranges partition the committees, so every committee's tallies are complete inside ONE
+// block: they are summed in LDS and leave with plain stores, and the block applies the winner
+// rule (core.go:549-555) itself -- no tally atomics to HBM, no winner pass.
+//
+//   prologue  the first windows' loads go out before anything else; then, with them in flight:
+//             GetAttestersTotalDeposit (validator.go:93-102) as a bit count over every
+//             bitfield of the instance (each block counts them: nothing precedes the launch),
+//             whose last bitfield (CalculateRewards reads it by validator index,
+//             incentives.go:22-27) is copied into LDS on the way; the bitfield-length panics
+//             (core.go:538-541); the range's committee bitfields placed in position order in
+//             an LDS bitmap (the vote bits of single-attestation committees)
+//   loop      fixed 256-position windows: lane l takes 4 contiguous positions, every column
+//             load 16 B per lane and issued kWinDepth windows ahead (no load waits on
+//             another); the reward bit of position p is bit co_index[p] of the LDS copy; the
+//             crosslink tallies (core.go:533-545) are per-committee segment sums of the
+//             pre-reward balances (DPP wave sums) added into LDS
+//   epilogue  every attestation of the range: vote / total stored, the winner rule as an
+//             atomicMin on its shard; the block's next-cycle partial sum (core.go:459-464)
+//             as one atomic
+//
+// Committees with several attestations (kManyAtt) take a slower in-loop path per attestation
+// (its bitfield bytes from global memory); committees without one add nothing.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "epoch.h"
+#include "votes_dev.h"
+
+namespace pz {
+
+namespace {
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ldnt16(const void* p) {
+  const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ uint64_t pk64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+__device__ __forceinline__ uint32_t rfl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
+// One window's column words per lane: the balances of its 4 positions (u32 offsets: one 16-B
+// load; u64: two), their {start, end} bounds (16-bit pairs: one load; 32-bit pairs: two; the
+// 64-bit columns: four) and their co_index entries.
+template <bool B32, int SEW>
+struct WinCols {
+  uint4 b[B32 ? 1 : 2];
+  uint4 s[SEW == 16 ? 1 : SEW == 32 ? 2 : 4];
+  uint4 ci;
+  uint32_t c0;  // the first committee overlapping the window
+};
+
+template <bool B32, int SEW>
+__device__ __forceinline__ void win_load(const EpochArgs& a, const WinArgs& w, uint64_t inst, uint32_t wb,
+                                         uint32_t nwin, uint64_t P0, uint64_t P1, uint64_t P0a, uint32_t k, int lane,
+                                         WinCols<B32, SEW>& x) {
+  if (k >= nwin) return;  // (wave-uniform: no window left for this slot)
+  const uint64_t p = P0a + 256ull * k + 4ull * lane;
+  const bool any = p + 3 >= P0 && p < P1;
+  const uint64_t pp = any ? p : P0a;  // (a lane wholly outside the range re-reads the first quad)
+  const uint64_t row = inst * w.vstride + pp;
+  if (B32) {
+    x.b[0] = *reinterpret_cast<const uint4*>(w.bal32 + row);
+  } else {
+    x.b[0] = *reinterpret_cast<const uint4*>(a.balance + row);
+    x.b[B32 ? 0 : 1] = *reinterpret_cast<const uint4*>(a.balance + row + 2);
+  }
+  // the bounds are read once per step: nontemporal, leaving the Infinity Cache to the balances
+  if (SEW == 16) {
+    x.s[0] = ldnt16(w.se16 + row);
+  } else if (SEW == 32) {
+    x.s[0] = ldnt16(w.se + row);
+    x.s[SEW == 32 ? 1 : 0] = ldnt16(w.se + row + 2);
+  } else {
+    x.s[0] = ldnt16(a.start + row);
+    x.s[SEW == 64 ? 1 : 0] = ldnt16(a.start + row + 2);
+    x.s[SEW == 64 ? 2 : 0] = ldnt16(a.end + row);
+    x.s[SEW == 64 ? 3 : 0] = ldnt16(a.end + row + 2);
+  }
+  x.ci = *reinterpret_cast<const uint4*>(a.co_index + pp);
+  x.c0 = w.wdesc[wb + k];
+}
+
+// validator.go:45-53 on position i of the lane's quad (the saturated bounds classify exactly:
+// the host takes the 16- / 32-bit columns only when every CurrentDynasty is below them)
+template <bool B32, int SEW>
+__device__ __forceinline__ bool win_active(const WinCols<B32, SEW>& x, int i, uint64_t d) {
+  if (SEW == 16) {
+    const uint32_t s4[4] = {x.s[0].x, x.s[0].y, x.s[0].z, x.s[0].w};
+    return (uint64_t)(s4[i] & 0xFFFFu) <= d && d < (uint64_t)(s4[i] >> 16);
+  } else if (SEW == 32) {
+    const uint4 q = x.s[i >> 1];
+    const uint32_t lo = (i & 1) ? q.z : q.x, hi = (i & 1) ? q.w : q.y;
+    return (uint64_t)lo <= d && d < (uint64_t)hi;
+  } else {
+    const uint4 qs = x.s[i >> 1], qe = x.s[SEW == 64 ? 2 + (i >> 1) : 0];
+    const uint64_t s = (i & 1) ? pk64(qs.z, qs.w) : pk64(qs.x, qs.y);
+    const uint64_t e = (i & 1) ? pk64(qe.z, qe.w) : pk64(qe.x, qe.y);
+    return s <= d && d < e;
+  }
+}
+
+}  // namespace
+
+// LDS carve-up of one block (bytes; WinArgs.lds_* from the host's plan)
+struct WinLds {
+  uint8_t* lbf;     // [lds_lbf] the instance's last bitfield from (lb & ~15)
+  uint32_t* vb;     // [lds_vw] vote bits of the range, position order from P0a
+  uint32_t* cst;    // [maxc + 1] committee starts relative to P0a
+  uint32_t* kbg;    // [maxc + 1] each committee's first attestation (index into catt)
+  uint64_t* cbo;    // [maxc] single-attestation committees: bitfield offset
+  uint32_t* cnb;    // [maxc] ... and its bits (min(committee size, 8 * bitfield length))
+  uint8_t* kd;      // [maxc] 0 no attestation, 1 one, 2 several
+  uint64_t* tot;    // [maxc] committee totals
+  uint64_t* vot;    // [maxk] vote per attestation (catt index - the range's first)
+};
+
+__device__ __forceinline__ WinLds win_lds(uint8_t* base, const WinArgs& w) {
+  WinLds L;
+  uint8_t* p = base;
+  L.tot = reinterpret_cast<uint64_t*>(p);
+  p += 8ull * w.lds_maxc;
+  L.vot = reinterpret_cast<uint64_t*>(p);
+  p += 8ull * w.lds_maxk;
+  L.cbo = reinterpret_cast<uint64_t*>(p);
+  p += 8ull * w.lds_maxc;
+  L.lbf = p;  // 16-B aligned: every size above is a multiple of 8, and lds_maxc + lds_maxk is even
+  p += w.lds_lbf;
+  L.vb = reinterpret_cast<uint32_t*>(p);
+  p += 4ull * w.lds_vw;
+  L.cst = reinterpret_cast<uint32_t*>(p);
+  p += 4ull * (w.lds_maxc + 1);
+  L.kbg = reinterpret_cast<uint32_t*>(p);
+  p += 4ull * (w.lds_maxc + 1);
+  L.cnb = reinterpret_cast<uint32_t*>(p);
+  p += 4ull * w.lds_maxc;
+  L.kd = p;
+  return L;
+}
+
+size_t window_lds_bytes(const WinArgs& w) {
+  return 8ull * (2 * (size_t)w.lds_maxc + w.lds_maxk) + w.lds_lbf + 4ull * w.lds_vw + 4ull * (3 * (size_t)w.lds_maxc + 2) +
+         w.lds_maxc + 16;
+}
+
+template <bool B32, int SEW, bool LLB>
+__device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w) {
+  extern __shared__ __align__(16) uint8_t lds_dyn[];
+  constexpr int NT = kWinThreads, NW = NT / 64, D = kWinDepth;
+  __shared__ uint64_t red[NW][2];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = rfl(tid >> 6);
+  const uint64_t inst = blockIdx.x / w.R;
+  const uint32_t r = blockIdx.x - (uint32_t)inst * w.R;
+  const uint4 rd = w.rdesc[r];
+  const uint32_t cr0 = rd.x, cr1 = rd.y, wb = rd.z, nwin = rd.w;
+  const uint64_t P0 = w.lcs[cr0], P1 = w.lcs[cr1], P0a = P0 & ~3ull;
+  // the first windows' loads, before anything else
+  WinCols<B32, SEW> q[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) win_load<B32, SEW>(a, w, inst, wb, nwin, P0, P1, P0a, wave + j * NW, lane, q[j]);
+  const WinLds L = win_lds(lds_dyn, w);
+  const uint32_t ncr = cr1 - cr0;
+  for (uint32_t i = tid; i < w.lds_vw; i += NT) L.vb[i] = 0;
+  for (uint32_t i = tid; i < ncr; i += NT) L.tot[i] = 0;
+  const uint64_t gb = inst * a.natt;
+  const uint4* lci = w.lci + inst * (w.nlc + 1);
+  const uint32_t k0 = lci[cr0].w, nk = lci[cr1].w - k0;  // the range's attestations: catt[k0, k0 + nk)
+  for (uint32_t i = tid; i < nk; i += NT) L.vot[i] = 0;
+  // the range's committees: starts, attestation kinds, their catt index and bitfields
+  for (uint32_t c = cr0 + tid; c <= cr1; c += NT) {
+    const uint4 ci = lci[c];
+    const uint32_t cl = c - cr0;
+    L.cst[cl] = (uint32_t)(w.lcs[c] - P0a);
+    L.kbg[cl] = ci.w;
+    if (c < cr1) {
+      L.kd[cl] = ci.z == kNoAtt ? 0 : ci.z == kManyAtt ? 2 : 1;
+      L.cbo[cl] = pk64(ci.x, ci.y);
+      L.cnb[cl] = w.lnb[inst * w.nlc + c];
+    }
+  }
+  // every bitfield's bits (the last one copied into LDS on the way), and their lengths
+  const uint64_t pbeg = a.boffs[gb], pend = a.boffs[gb + a.natt], lb = a.boffs[gb + a.natt - 1];
+  const uint64_t pbase = pbeg & ~15ull, lbase = lb & ~15ull;
+  uint64_t pop = 0, err = 0;
+  {
+    const uint64_t nch = (pend - pbase + 15) / 16;
+    constexpr int U = 8;
+    for (uint64_t c0 = tid; c0 < nch; c0 += (uint64_t)U * NT) {
+      uint4 x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t c = c0 + (uint64_t)u * NT;
+        x[u] = c < nch ? *reinterpret_cast<const uint4*>(a.bits + pbase + 16 * c) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t c = c0 + (uint64_t)u * NT;
+        if (c >= nch) continue;
+        const uint64_t ad = pbase + 16 * c;
+        const uint32_t wd[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+        if (ad >= pbeg && ad + 16 <= pend) {
+          pop += __popc(wd[0]) + __popc(wd[1]) + __popc(wd[2]) + __popc(wd[3]);
+        } else {  // (the region's two edge chunks: its bytes only)
+#pragma unroll
+          for (int dd = 0; dd < 4; ++dd) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb) {
+              const uint64_t at = ad + 4 * dd + bb;
+              if (at >= pbeg && at < pend) m |= 0xFFu << (8 * bb);
+            }
+            pop += __popc(wd[dd] & m);
+          }
+        }
+        if (LLB && ad >= lbase) *reinterpret_cast<uint4*>(L.lbf + (ad - lbase)) = x[u];
+      }
+    }
+    // the crosslink bitfield-length panic (core.go:538-541): a committee longer than its bitfield
+    for (uint32_t g = tid; g < a.natt; g += NT)
+      if ((uint64_t)w.att_csize[gb + g] > 8 * (a.boffs[gb + g + 1] - a.boffs[gb + g])) err = 1;
+  }
+  __syncthreads();  // the committee table is in LDS, the vote bits zeroed
+  // the vote bits: (committee, 32-bit word) items, every load of a round in flight together
+  {
+    const uint32_t wpc = w.wpc, items = ncr * wpc;
+    constexpr int U = 4;
+    for (uint32_t t0 = tid; t0 < items; t0 += U * NT) {
+      uint64_t raw[U];
+      uint32_t sh8[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t t = t0 + u * NT, cl = t / wpc, m = t - cl * wpc;
+        const bool ok = t < items && L.kd[cl] == 1 && 32 * m < L.cnb[cl];
+        const uint64_t ad = (ok ? L.cbo[cl] : 0) + 4 * m, da = ad & ~3ull;
+        sh8[u] = (uint32_t)(ad - da) * 8;
+        raw[u] = 0;
+        if (ok) __builtin_memcpy(&raw[u], __builtin_assume_aligned(a.bits + da, 4), 8);  // (buffer padded by 16 B)
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t t = t0 + u * NT, cl = t / wpc, m = t - cl * wpc;
+        if (!(t < items && L.kd[cl] == 1 && 32 * m < L.cnb[cl])) continue;
+        // bitfield bit j is bit 7 - j % 8 of byte j / 8 (CheckBit, utils/checkbit.go:4-12):
+        // byte-order kept, bits reversed within each byte -> bit j of the word
+        uint32_t W = __builtin_bitreverse32(__builtin_bswap32((uint32_t)(raw[u] >> sh8[u])));
+        const uint32_t left = L.cnb[cl] - 32 * m;
+        if (left < 32) W &= (1u << left) - 1u;
+        const uint32_t o = L.cst[cl] + 32 * m, sh = o & 31;
+        atomicOr(&L.vb[o >> 5], W << sh);
+        if (sh) atomicOr(&L.vb[(o >> 5) + 1], W >> (32 - sh));
+      }
+    }
+  }
+  pop = wsum64_dpp(pop);
+  err = wsum64_dpp(err);
+  if (lane == 0) red[wave][0] = pop, red[wave][1] = err;
+  __syncthreads();
+  pop = 0, err = 0;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) pop += red[k][0], err += red[k][1];
+  const uint64_t lastL = pend - lb;
+  const bool rwd_err = (a.nval_global - 1) >= 8 * lastL;  // CheckBit(last, N-1) panics (incentives.go:23)
+  const bool thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (a.total_deposit[inst] * 2ull);  // incentives.go:18-20
+  const uint64_t ferr = err ? (uint64_t)kErrBitfield : 0;
+  const bool skip = ferr != 0 || (thr && rwd_err);  // Go panics: balances stay untouched
+  const bool applied = thr && !skip;
+  const uint64_t d = a.dynasty[inst];
+  const uint64_t bbase = B32 ? w.bal32_base[inst] : 0;
+  const uint8_t* lbf8 = LLB ? L.lbf + (lb - lbase) : a.bits + lb;
+  uint32_t* Bal32 = B32 ? w.bal32 + inst * w.vstride : nullptr;
+  uint64_t* Bal = a.balance + inst * w.vstride;
+  uint64_t sum = 0, nm = 0;
+  for (uint32_t k = wave; k < nwin; k += D * NW) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const uint32_t kk = k + j * NW;
+      if (kk >= nwin) break;  // (wave-uniform)
+      const WinCols<B32, SEW>& x = q[j];
+      const uint64_t p = P0a + 256ull * kk + 4ull * lane;
+      const uint32_t loc = (uint32_t)(p - P0a);
+      bool v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = p + i >= P0 && p + i < P1;
+      uint64_t b[4];
+      if (B32) {  // u64 balance = base + offset (mod 2^64)
+        b[0] = bbase + x.b[0].x, b[1] = bbase + x.b[0].y, b[2] = bbase + x.b[0].z, b[3] = bbase + x.b[0].w;
+      } else {
+        b[0] = pk64(x.b[0].x, x.b[0].y), b[1] = pk64(x.b[0].z, x.b[0].w);
+        b[2] = pk64(x.b[B32 ? 0 : 1].x, x.b[B32 ? 0 : 1].y), b[3] = pk64(x.b[B32 ? 0 : 1].z, x.b[B32 ? 0 : 1].w);
+      }
+      // the reward bits first: their lookups (LDS or L2) overlap the tallies
+      uint32_t rb[4] = {0, 0, 0, 0};
+      if (applied) {
+        const uint32_t c4[4] = {x.ci.x, x.ci.y, x.ci.z, x.ci.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t ix = v[i] ? c4[i] : 0u;  // (a position outside the range looks bit 0 up)
+          rb[i] = lbf8[ix >> 3] >> (7 - (ix & 7));
+        }
+      }
+      // crosslink tallies on the pre-reward balances: one segment per committee in the window
+      {
+        const uint32_t vw = (L.vb[loc >> 5] >> (loc & 31)) & 0xFu;
+        const uint32_t wend = 256 * kk + 256;
+        uint32_t c = rfl(x.c0);
+        for (;;) {
+          const uint32_t cl = c - cr0;
+          const uint32_t s_lo = rfl(L.cst[cl]), s_hi = rfl(L.cst[cl + 1]), kind = rfl(L.kd[cl]);
+          if (kind) {
+            uint64_t t = 0, vv = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const bool in = v[i] && loc + i >= s_lo && loc + i < s_hi;
+              t += in ? b[i] : 0;
+              vv += (in && ((vw >> i) & 1)) ? b[i] : 0;
+            }
+            t = wsum64_dpp(t);
+            const uint32_t kb = rfl(L.kbg[cl]);
+            if (kind == 1) {
+              vv = wsum64_dpp(vv);
+              if (lane == 0) {
+                if (t) atomicAdd((unsigned long long*)&L.tot[cl], (unsigned long long)t);
+                if (vv) atomicAdd((unsigned long long*)&L.vot[kb - k0], (unsigned long long)vv);
+              }
+            } else {  // several attestations: each one's bits from its bitfield in global memory
+              if (lane == 0 && t) atomicAdd((unsigned long long*)&L.tot[cl], (unsigned long long)t);
+              const uint32_t ke = rfl(L.kbg[cl + 1]);
+              for (uint32_t kq = kb; kq < ke; ++kq) {
+                const uint64_t ga = w.catt[gb + kq];
+                const uint64_t bo = a.boffs[gb + ga], nb = 8 * (a.boffs[gb + ga + 1] - bo);
+                uint64_t s = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                  const uint64_t xb = (uint64_t)(loc + i) - s_lo;  // the position's bit in the bitfield
+                  const bool in = v[i] && loc + i >= s_lo && loc + i < s_hi && xb < nb;
+                  const uint32_t by = in ? a.bits[bo + (xb >> 3)] : 0u;
+                  s += (in && ((by >> (7 - (uint32_t)(xb & 7))) & 1)) ? b[i] : 0;
+                }
+                s = wsum64_dpp(s);
+                if (lane == 0 && s) atomicAdd((unsigned long long*)&L.vot[kq - k0], (unsigned long long)s);
+              }
+            }
+          }
+          ++c;
+          if (s_hi >= wend || c >= cr1) break;
+        }
+      }
+      // classify, reward (incentives.go:22-27), store, next-cycle sum (core.go:459-464)
+      bool act[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        act[i] = win_active<B32, SEW>(x, i, d);
+        nm += (v[i] && !act[i]) ? 1 : 0;
+      }
+      if (applied) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b[i] = (rb[i] & 1) ? b[i] + PZ_ATTESTER_REWARD : b[i] - PZ_ATTESTER_REWARD;
+        const bool all = v[0] && v[1] && v[2] && v[3];
+        if (B32) {  // the offsets back: (base + o +- 1) - base = o +- 1, inside u32 (the state's re-base bound)
+          const uint64_t o = inst * w.vstride + p;
+          if (all) {
+            *reinterpret_cast<uint4*>(w.bal32 + o) = make_uint4((uint32_t)(b[0] - bbase), (uint32_t)(b[1] - bbase),
+                                                                (uint32_t)(b[2] - bbase), (uint32_t)(b[3] - bbase));
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (v[i]) w.bal32[o + i] = (uint32_t)(b[i] - bbase);
+          }
+        } else {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int i = 2 * h;
+            if (v[i] && v[i + 1])
+              *reinterpret_cast<uint4*>(Bal + p + i) =
+                  make_uint4((uint32_t)b[i], (uint32_t)(b[i] >> 32), (uint32_t)b[i + 1], (uint32_t)(b[i + 1] >> 32));
+            else if (v[i])
+              Bal[p + i] = b[i];
+            else if (v[i + 1])
+              Bal[p + i + 1] = b[i + 1];
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sum += (v[i] && act[i]) ? b[i] : 0;
+      win_load<B32, SEW>(a, w, inst, wb, nwin, P0, P1, P0a, kk + D * NW, lane, q[j]);
+    }
+  }
+  (void)Bal32;
+  sum = wsum64_dpp(sum);
+  nm = wsum64_dpp(nm);
+  if (lane == 0) red[wave][0] = sum, red[wave][1] = nm;
+  __syncthreads();  // (also: every wave's LDS tallies are in)
+  uint64_t* sc = a.scal + inst * kScal;
+  if (tid == 0) {
+    uint64_t s = 0, n = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) s += red[k][0], n += red[k][1];
+    if (s && !skip) atomicAdd((unsigned long long*)&sc[kNextBal], (unsigned long long)s);
+    if (n) {  // the layout's rank == index premise is broken (the state never allows it)
+      atomicAdd((unsigned long long*)&sc[kNoMatch], (unsigned long long)n);
+      atomicOr((unsigned long long*)&sc[kErrXl], (unsigned long long)kErrLayout);
+    }
+    if (r == 0 && w.rank0) {  // the per-instance scalars (the all-reduce must not multiply them)
+      sc[kPop] = pop;
+      sc[kApplied] = applied ? 1 : 0;
+      sc[kNact] = a.nval_global;
+      sc[kMaxIdx1] = a.nval_global;
+      sc[kErrRwd] = rwd_err ? 1 : 0;
+      if (ferr) atomicAdd((unsigned long long*)&sc[kErrXl], (unsigned long long)ferr);
+    }
+  }
+  if (r == 0) {  // the next step's accumulators start from zero, its winners empty
+    if (a.scal_next && tid < kScal) a.scal_next[inst * kScal + tid] = 0;
+    for (uint32_t s = tid; s < a.nrec; s += NT) w.winner_next[inst * a.nrec + s] = 0xFFFFFFFFu;
+    if (w.vote_next)
+      for (uint32_t g = tid; g < a.natt; g += NT) w.vote_next[gb + g] = 0, w.total_next[gb + g] = 0;
+  }
+  // the range's attestations: tallies out, the winner rule (core.go:549-555: the first
+  // attestation, in order, whose 3 * vote >= 2 * total and whose dynasty beats its shard's record)
+  for (uint32_t cl = tid; cl < ncr; cl += NT) {
+    if (!L.kd[cl]) continue;
+    const uint64_t T = L.tot[cl];
+    for (uint32_t kq = L.kbg[cl]; kq < L.kbg[cl + 1]; ++kq) {
+      const uint64_t V = L.vot[kq - k0];
+      const uint32_t ga = w.catt[gb + kq];
+      a.vote[gb + ga] = V;
+      a.total[gb + ga] = T;
+      const uint4 aw = w.att_win[gb + ga];  // {shard, its record's dynasty lo, hi}
+      if (3ull * V >= 2ull * T && d > pk64(aw.y, aw.z)) atomicMin(&a.winner[inst * a.nrec + aw.x], ga);
+    }
+  }
+}
+
+#define PZ_WINDOW_KERNEL(NAME, B32, SEW, LLB)                                               \
+  extern "C" __global__ void __launch_bounds__(kWinThreads) NAME(EpochArgs a, WinArgs w) { \
+    window_body<B32, SEW, LLB>(a, w);                                                       \
+  }
+// balances as u32 offsets / u64; {start, end} at 16 / 32 / 64 bits; the last bitfield in LDS or not
+PZ_WINDOW_KERNEL(pz_epoch_window_b32_s16_kernel, true, 16, true)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32_s32_kernel, true, 32, true)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32_s64_kernel, true, 64, true)
+PZ_WINDOW_KERNEL(pz_epoch_window_b64_s16_kernel, false, 16, true)
+PZ_WINDOW_KERNEL(pz_epoch_window_b64_s32_kernel, false, 32, true)
+PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_kernel, false, 64, true)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32_s16_g_kernel, true, 16, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32_s32_g_kernel, true, 32, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32_s64_g_kernel, true, 64, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b64_s16_g_kernel, false, 16, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b64_s32_g_kernel, false, 32, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_g_kernel, false, 64, false)
+#undef PZ_WINDOW_KERNEL
+
+hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t s) {
+  if (!a.ninst || !w.R) return hipSuccess;
+  const bool b32 = w.bal32 != nullptr, llb = w.lds_lbf != 0;
+  const int sew = w.se16 ? 16 : w.se ? 32 : 64;
+  const void* k = nullptr;
+#define PZ_PICK(B, S)                                                                            \
+  k = llb ? (const void*)pz_epoch_window_##B##_s##S##_kernel : (const void*)pz_epoch_window_##B##_s##S##_g_kernel
+  if (b32) {
+    if (sew == 16) PZ_PICK(b32, 16);
+    else if (sew == 32) PZ_PICK(b32, 32);
+    else PZ_PICK(b32, 64);
+  } else {
+    if (sew == 16) PZ_PICK(b64, 16);
+    else if (sew == 32) PZ_PICK(b64, 32);
+    else PZ_PICK(b64, 64);
+  }
+#undef PZ_PICK
+  const size_t lds = window_lds_bytes(w);
+  if (lds > 48 * 1024) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  void* args[] = {const_cast<EpochArgs*>(&a), const_cast<WinArgs*>(&w)};
+  return hipLaunchKernel(k, dim3(a.ninst * w.R), dim3(kWinThreads), args, lds, s);
+}
+
+}  // namespace pz

@@ -336,9 +336,12 @@ int pz_comm_blake2b512_batch(const pz_comm* comm, const uint8_t* msgs, const uin
 }
 
 uint64_t pz_set_serial_threshold(uint64_t bytes) { return set_serial_threshold(bytes); }
+uint32_t pz_set_host_threads(uint32_t n) { return set_host_threads(n); }
 uint64_t pz_set_small_batch_threshold(uint64_t compressions) { return set_small_batch_threshold(compressions); }
 
 }  // extern "C"
 
-// Internal: select the fixed-length hash kernel variant for in-process A/B benchmarking.
+#ifdef PZ_AB_BUILD
+// The A/B library only: select the fixed-length hash kernel variant for in-process A/B timing.
 extern "C" int pz_debug_set_hash_variant(int v) { return pz::set_fixed_variant(v); }
+#endif

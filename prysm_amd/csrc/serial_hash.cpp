@@ -182,12 +182,13 @@ uint64_t set_serial_threshold(uint64_t bytes) { return g_threshold.exchange(byte
 
 namespace pz {
 
+// Host threads for the serial hashes (and the chain's parse): min(16, the affinity set) unless
+// pz_set_host_threads chose a count (16: the CPU share of one GPU on the bench boxes).
+static std::atomic<unsigned> g_host_threads{0};
 unsigned host_threads() {
+  const unsigned v = g_host_threads.load();
+  if (v) return v;
   static const unsigned n = [] {
-    if (const char* e = std::getenv("PZ_HOST_THREADS")) {
-      const long v = std::strtol(e, nullptr, 10);
-      if (v >= 1 && v <= 256) return (unsigned)v;
-    }
     unsigned c = std::max(1u, std::thread::hardware_concurrency());
     cpu_set_t set;
     if (sched_getaffinity(0, sizeof set, &set) == 0) c = std::max(1, CPU_COUNT(&set));
@@ -195,6 +196,7 @@ unsigned host_threads() {
   }();
   return n;
 }
+unsigned set_host_threads(unsigned n) { return g_host_threads.exchange(n > 256 ? 256 : n); }
 
 std::vector<uint64_t> long_messages(const uint64_t* offsets, uint64_t n) {
   std::vector<uint64_t> w;

@@ -40,6 +40,7 @@ uint64_t set_small_batch_threshold(uint64_t compressions);
 // staging, long messages): the CPUs this process may run on, at most 16 (the CPU share of
 // one GPU on the bench hosts); PZ_HOST_THREADS overrides it.
 unsigned host_threads();
+unsigned set_host_threads(unsigned n);  // 0: back to the default; returns the previous setting
 
 // Indices of the messages of a CSR batch that go to the host (length >= threshold).
 std::vector<uint64_t> long_messages(const uint64_t* offsets, uint64_t n);

@@ -103,7 +103,9 @@ inline uint32_t vote_word_blocks(const VoteWordArgs& a, uint32_t threads = kVote
 }
 hipError_t launch_vote_words(const VoteWordArgs& a, hipStream_t s);
 // (tools/ only) the same with per-wave phase stamps into tr[wave][8] (null: none)
+#ifdef PZ_AB_BUILD  // the A/B library only
 hipError_t launch_vote_words_traced(const VoteWordArgs& a, uint64_t* tr, hipStream_t s);
+#endif
 // Up to 6 copies from mapped pinned memory to device memory in ONE launch (16 B per lane; the
 // sources may be read up to 15 bytes past their ends, so a source buffer's capacity must cover
 // ceil16 of its bytes).
@@ -116,7 +118,9 @@ struct StageSegs {
   StageSeg seg[6];
   int nseg;
 };
+#ifdef PZ_AB_BUILD  // the A/B library only
 hipError_t launch_stage_h2d_segs(const StageSegs& g, hipStream_t s);
+#endif
 // Copy `bytes` (a multiple of 16) from mapped pinned host memory to device memory in a kernel on
 // stream s: 16 B per lane, so the bytes cross PCIe in one round trip of coalesced reads.
 hipError_t launch_stage_h2d(const void* host_mapped, void* dev, uint64_t bytes, hipStream_t s);

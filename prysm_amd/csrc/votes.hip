@@ -51,6 +51,7 @@ hipError_t launch_vote_words(const VoteWordArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+#ifdef PZ_AB_BUILD
 extern "C" __global__ void __launch_bounds__(kVoteWordMaxThreads)
 pz_vote_words_traced_kernel(VoteWordArgs a, uint64_t* tr) { vote_words_body(a, gridDim.x, blockIdx.x, tr); }
 
@@ -61,12 +62,15 @@ hipError_t launch_vote_words_traced(const VoteWordArgs& a, uint64_t* tr, hipStre
   return hipGetLastError();
 }
 
+#endif
+
 extern "C" __global__ void __launch_bounds__(256)
 pz_stage_h2d_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n16) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
     dst[i] = src[i];
 }
 
+#ifdef PZ_AB_BUILD
 // Several segments in one launch: block y copies segment y (grid-stride over x).
 extern "C" __global__ void __launch_bounds__(256)
 pz_stage_h2d_segs_kernel(StageSegs g) {
@@ -85,6 +89,8 @@ hipError_t launch_stage_h2d_segs(const StageSegs& g, hipStream_t s) {
   hipLaunchKernelGGL(pz_stage_h2d_segs_kernel, dim3(blocks, (uint32_t)g.nseg), dim3(256), 0, s, g);
   return hipGetLastError();
 }
+
+#endif
 
 hipError_t launch_stage_h2d(const void* host_mapped, void* dev, uint64_t bytes, hipStream_t s) {
   const uint64_t n16 = bytes / 16;

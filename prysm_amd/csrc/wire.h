@@ -32,7 +32,9 @@ uint64_t wire_tiles(uint64_t n);
 int wire_val_args(const pz_validator_cols* v, uint64_t n, uint32_t field_num, WireValArgs* a);
 // scratch: (wire_tiles(n) + 1) u64, zeroed by the launcher
 hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t s);
-int set_wire_variant(int v);  // tools/ A/B only (pz_debug_set_wire_variant)
-void set_wire_trace(uint64_t* dev);  // tools/ only: variant 32's timestamp buffer [tiles][16]
+#ifdef PZ_AB_BUILD
+int set_wire_variant(int v);  // the A/B library only (pz_debug_set_wire_variant)
+void set_wire_trace(uint64_t* dev);  // the A/B library only: variant 32's timestamp buffer [tiles][16]
+#endif
 
 }  // namespace pz

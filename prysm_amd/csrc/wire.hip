@@ -626,43 +626,16 @@ PZ_WIRE_VAL_KERNEL(pz_wire_val_c2_kernel, 0, 2)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_kernel, 0, 3)  // the chain's states: balance, start, end
 PZ_WIRE_VAL_KERNEL(pz_wire_val_c4_kernel, 0, 4)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_c5_kernel, 0, 5)
-// ablation variants (3 columns)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v1_kernel, 1, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v2_kernel, 2, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v4_kernel, 4, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v8_kernel, 8, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v7_kernel, 7, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v15_kernel, 15, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v16_kernel, 16, 3)
+#ifdef PZ_AB_BUILD
+// the A/B library only (make -C prysm_amd/csrc ab): per-tile phase stamps for tools/wire_trace.py,
+// and the multi-window look-back path for tests (no inclusive prefix published: every tile walks
+// back window after window to tile 0; exact output)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v32_kernel, 32, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v34_kernel, 34, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v36_kernel, 36, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v96_kernel, 96, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v160_kernel, 160, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v288_kernel, 288, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v512_kernel, 512, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v544_kernel, 544, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v1024_kernel, 1024, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v1056_kernel, 1056, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v2048_kernel, 2048, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v4096_kernel, 4096, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v8192_kernel, 8192, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v12288_kernel, 12288, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v16384_kernel, 16384, 3)
-PZ_WIRE_VAL_KERNEL(pz_wire_val_v16512_kernel, 16512, 3)
+#endif
 #undef PZ_WIRE_VAL_KERNEL
-// Round 4 tile-geometry A/B (3 columns): PER records per thread per sub-tile, W waves per SIMD
-// (the VGPR cap: 6 -> 80, 8 -> 64).  PER 3: 3,072-record tiles, a 48 KiB stage, three tiles
-// per CU; PER 2: 2,048-record tiles, a 32 KiB stage, three (W 6) or four (W 8) per CU.
-#define PZ_WIRE_VAL_GEOM(NAME, PER, W)                                                         \
-  extern "C" __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(W, W))) \
-  NAME(WireValArgs a, uint32_t nt) {                                                         \
-    wire_val_body<0, 3, PER>(a, nt);                                                         \
-  }
-PZ_WIRE_VAL_GEOM(pz_wire_val_p3w6_kernel, 3, 6)
-PZ_WIRE_VAL_GEOM(pz_wire_val_p2w6_kernel, 2, 6)
-PZ_WIRE_VAL_GEOM(pz_wire_val_p2w8_kernel, 2, 8)
-#undef PZ_WIRE_VAL_GEOM
+// (Round 4 tile-geometry A/B, measured and dropped: 3,072-record tiles at 6 waves per SIMD and
+// 2,048-record tiles at 6 or 8 spill their held values, profiles/r04/wire_geometry_dropped_r4g.txt.)
 
 // Records with bytes fields: tiles of kBytesSub x 256 records, one per thread per sub-tile.
 // Phase 1 scans the sizes; after the look-back, phase 2 reads the records again and writes
@@ -720,18 +693,10 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_zero_kernel(uint6
 
 }  // namespace
 
-static int g_wire_variant = 0;       // tools/ A/B only
-static uint64_t* g_wire_trace = nullptr;  // tools/ only
-
-// the tile-geometry variants (3 columns): 32768 PER 3 / W 6, 65536 PER 2 / W 6, 98304 PER 2 / W 8
-static int geom_per(const WireValArgs& a) {
-  if (a.nc != 3) return kPer;
-  switch (g_wire_variant) {
-    case 32768: return 3;
-    case 65536: case 98304: return 2;
-    default: return kPer;
-  }
-}
+#ifdef PZ_AB_BUILD
+static int g_wire_variant = 0;            // 32: trace (g_wire_trace), 16384: no inclusive prefixes
+static uint64_t* g_wire_trace = nullptr;
+#endif
 
 static uint64_t tile_recs(bool bytes, int per) { return bytes ? kBytesTileRecs : (uint64_t)kSub * kThreads * per; }
 
@@ -750,7 +715,7 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
       a.ccol[a.nc] = a.col[k];
       a.ctag[a.nc++] = tags[k];
     }
-  const uint64_t tr = tile_recs(bytes, geom_per(a));
+  const uint64_t tr = tile_recs(bytes, kPer);
   const uint64_t nt = (a.n + tr - 1) / tr;
   if (nt == 0) {
     hipError_t e = hipMemsetAsync(a.total, 0, 8, s);
@@ -770,26 +735,21 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
   {
     const dim3 g((uint32_t)nt), b(kThreads);
     const uint32_t n32 = (uint32_t)nt;
+#ifdef PZ_AB_BUILD
     if (g_wire_variant && a.nc == 3) {
-      switch (g_wire_variant) {
-#define PZ_CASE(V) \
-  case V: hipLaunchKernelGGL(pz_wire_val_v##V##_kernel, g, b, 0, s, a, n32); break;
-        PZ_CASE(1) PZ_CASE(2) PZ_CASE(4) PZ_CASE(8) PZ_CASE(7) PZ_CASE(15) PZ_CASE(16) PZ_CASE(512) PZ_CASE(1024) PZ_CASE(2048) PZ_CASE(4096) PZ_CASE(8192) PZ_CASE(12288) PZ_CASE(16384) PZ_CASE(16512)
-#undef PZ_CASE
-#define PZ_TRACE(V)                                                     \
-  case V:                                                               \
-    if (!g_wire_trace) return hipErrorInvalidValue;                     \
-    a.trace = g_wire_trace;                                             \
-    hipLaunchKernelGGL(pz_wire_val_v##V##_kernel, g, b, 0, s, a, n32);  \
-    break;
-        PZ_TRACE(32) PZ_TRACE(34) PZ_TRACE(36) PZ_TRACE(96) PZ_TRACE(160) PZ_TRACE(288) PZ_TRACE(544) PZ_TRACE(1056)
-#undef PZ_TRACE
-        case 32768: hipLaunchKernelGGL(pz_wire_val_p3w6_kernel, g, b, 0, s, a, n32); break;
-        case 65536: hipLaunchKernelGGL(pz_wire_val_p2w6_kernel, g, b, 0, s, a, n32); break;
-        case 98304: hipLaunchKernelGGL(pz_wire_val_p2w8_kernel, g, b, 0, s, a, n32); break;
-        default: hipLaunchKernelGGL(pz_wire_val_kernel, g, b, 0, s, a, n32);
+      if (g_wire_variant == 32) {
+        if (!g_wire_trace) return hipErrorInvalidValue;
+        a.trace = g_wire_trace;
+        hipLaunchKernelGGL(pz_wire_val_v32_kernel, g, b, 0, s, a, n32);
+      } else if (g_wire_variant == 16384) {
+        hipLaunchKernelGGL(pz_wire_val_v16384_kernel, g, b, 0, s, a, n32);
+      } else {
+        return hipErrorInvalidValue;
       }
-    } else {
+      return hipGetLastError();
+    }
+#endif
+    {
       switch (a.nc) {
         case 0: hipLaunchKernelGGL(pz_wire_val_c0_kernel, g, b, 0, s, a, n32); break;
         case 1: hipLaunchKernelGGL(pz_wire_val_c1_kernel, g, b, 0, s, a, n32); break;
@@ -803,6 +763,7 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
   return hipGetLastError();
 }
 
+#ifdef PZ_AB_BUILD
 int set_wire_variant(int v) {
   const int old = g_wire_variant;
   g_wire_variant = v;
@@ -810,6 +771,7 @@ int set_wire_variant(int v) {
 }
 
 void set_wire_trace(uint64_t* dev) { g_wire_trace = dev; }
+#endif
 
 int wire_val_args(const pz_validator_cols* v, uint64_t n, uint32_t field_num, WireValArgs* a) {
   if (!v) return fail(PZ_EINVAL, "columns are null");
@@ -848,9 +810,11 @@ uint64_t pz_wire_validators_bound(uint64_t n, uint64_t bytes_total) { return n *
 
 uint64_t pz_wire_scratch_bytes(uint64_t n) { return (wire_tiles(n) + 1) * 8; }
 
+#ifdef PZ_AB_BUILD
 int pz_debug_set_wire_variant(int v) { return set_wire_variant(v); }
 
 void pz_debug_set_wire_trace(void* dev) { set_wire_trace(static_cast<uint64_t*>(dev)); }
+#endif
 
 int pz_dev_wire_validators(const pz_validator_cols* v, uint64_t n, uint32_t field_num, uint8_t* d_out,
                            uint64_t* d_offsets, void* d_scratch, uint64_t* d_total, void* stream) {

@@ -12,7 +12,7 @@ import ctypes
 import numpy as np
 
 from prysm_amd import _lib
-from prysm_amd._lib import EpochHost, SCAL_COUNT, lib, ptr
+from prysm_amd._lib import EpochHost, EpochOptions, SCAL_COUNT, lib, ptr
 
 COMM_ID_BYTES = 128
 
@@ -136,16 +136,19 @@ class NativeEpoch:
     """``pz_epoch_state``: the same inputs as ``prysm_amd.epoch.DeviceEpoch`` (a
     ``synth.epoch_batch``-shaped dict over all validators)."""
 
-    def __init__(self, inst, device=0, comm=None, layout="auto"):
+    def __init__(self, inst, device=0, comm=None, layout="auto", rebase_period=0, window_only=False):
         """``layout``: "auto" (committee order when every validator is active and the
         committees partition the set, with the one-pass step when no attestation names a
-        shard >= nrec), "twopass" (the same layout, two-pass step) or "index"."""
+        shard >= nrec), "twopass" (the same layout, two-pass step) or "index".
+        ``rebase_period`` / ``window_only``: pz_epoch_options (tests: the u32 offsets re-based
+        every k steps; one instance through the window pass instead of pz_epoch_one_kernel)."""
         h, self._keep = _epoch_host(inst, layout)
         self.B, self.N, self.natt, self.nrec = int(h.ninst), int(h.nval), int(h.natt), int(h.nrec)
         self.comm = comm
         self.st = ctypes.c_void_p()
-        lib.call("pz_epoch_state_new", comm.h if comm is not None else None, device, ctypes.byref(h),
-                 ctypes.byref(self.st))
+        opts = EpochOptions(int(rebase_period), 1 if window_only else 0)
+        lib.call("pz_epoch_state_new_opts", comm.h if comm is not None else None, device, ctypes.byref(h),
+                 ctypes.byref(opts), ctypes.byref(self.st))
         self._keep = None  # the library copied everything it needs
         self.nlocal = comm.nlocal if comm is not None else 1
         co = ctypes.c_int(0)

@@ -8,8 +8,25 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+AB_LIB = os.path.join(ROOT, "build", "ab", "libprysm_hip.so")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP C-ABI)")
+    config.addinivalue_line("markers", "ab: measured-and-dropped forms and measurement hooks; runs only against the "
+                                       "A/B library (make -C prysm_amd/csrc ab) under -m ab")
+    # `-m ab` (or an expression naming ab without "not ab"): the session loads the A/B library
+    expr = config.option.markexpr or ""
+    if "ab" in expr.split() and "not ab" not in expr:
+        os.environ["PZ_LIB"] = AB_LIB
+
+
+def pytest_collection_modifyitems(config, items):
+    ab_loaded = os.environ.get("PZ_LIB") == AB_LIB
+    skip = pytest.mark.skip(reason="A/B form: run with -m ab against build/ab/libprysm_hip.so")
+    for it in items:
+        if "ab" in it.keywords and not ab_loaded:
+            it.add_marker(skip)
 
 # Load PyTorch (and its HIP runtime) before the product library: see prysm_amd/_lib.py.
 import torch  # noqa: E402,F401

@@ -74,71 +74,89 @@ def test_native_epoch_single_device(n, B, inactive, layout):
 @pytest.mark.parametrize("n", [65536, 32768, 16385, 4096, 4097, 1000, 130])
 @pytest.mark.parametrize("density", [0.5, 0.75])
 def test_native_epoch_single_launch(n, density):
-    """One instance on one device: the single-launch step (pz_epoch_one_kernel: every block
-    counts the bits itself; the winners formed in the waves when every attested committee is
-    one piece, else by the last block to arrive -- 32,768 validators give 256-member
-    committees, some of them two pieces), three steps in a row (the ticket, the winners' ping-pong
-    and the next step's tallies are reset in-kernel), bit-exact."""
+    """One instance on one device, three steps in a row (tickets, the winners' ping-pong and
+    the next step's tallies are reset in-kernel), bit-exact: the single-launch step
+    (pz_epoch_one_kernel) when every attested committee is one piece, else the window pass (32,768
+    validators give 256-member committees, some of them two pieces)."""
     inst = _inst(n, 1, False, density=density)
     ne = NativeEpoch(inst, device=0)
     assert ne.one_pass
     _check(ne, inst, steps=3)
 
 
-@pytest.mark.parametrize("variant", [0, 4096, 32768, 65536, 131072, 262144])
+def _rebits(inst, seed=9):
+    """New random bitfields sized to the (changed) committees: attestation g < ncomm covers
+    committee g, the final one all N validators; trailing bits clear (core.go:384-392)."""
+    rng = np.random.default_rng(seed)
+    B, natt, N = inst["ninst"], inst["natt"], inst["nval"]
+    sizes = np.diff(inst["coffs"].astype(np.int64))
+    kb = np.concatenate([sizes, [N]])
+    blobs, offs = [], [0]
+    for b in range(B):
+        for g in range(natt):
+            k = int(kb[g])
+            nb = (k + 7) // 8
+            x = (rng.integers(0, 256, size=nb, dtype=np.uint8) | rng.integers(0, 256, size=nb, dtype=np.uint8))
+            if k % 8:
+                x[-1] &= (0xFF << (8 - k % 8)) & 0xFF
+            blobs.append(x)
+            offs.append(offs[-1] + nb)
+    inst["bits"] = np.concatenate(blobs)
+    inst["boffs"] = np.array(offs, dtype=np.uint64)
+    inst["max_inst_bytes"] = int(max(offs[(b + 1) * natt] - offs[b * natt] for b in range(B)))
+    return inst
+
+
+def _widen(inst, bal=False, dyn=None):
+    """Data that selects the window pass's other column forms: balances 2^30 apart (the u64
+    column), a CurrentDynasty at or past 0xFFFF (the 32-bit bounds) or 2^32 - 1 (the u64 bounds)."""
+    if bal:
+        inst["balance"][:, :3] = np.array([1, 1 << 31, 1 << 40], dtype=np.uint64)
+    if dyn is not None:
+        inst["dynasty"] = np.full(inst["ninst"], dyn, dtype=np.uint64)
+    return inst
+
+
+@pytest.mark.parametrize("bal", [False, True])
+@pytest.mark.parametrize("dyn,db", [(None, 4), (0xFFFF, 8), ((1 << 32) + 3, 16)])
 @pytest.mark.parametrize("n,B", [(65536, 5), (32768, 9), (4097, 3), (1000, 2)])
-def test_native_epoch_fused_forms(n, B, variant, monkeypatch):
-    """The u64-balance forms of the one-pass step's fused pass (PZ_EPOCH_BAL64: the product holds
-    the balances as u32 offsets, below): 0 the product's u64 choice (the streaming pass, LDS-staged
-    when no position-order gather exists), 4096 the XCD-aware 1-D grid (block L on XCD L % 8 takes
-    piece group 8 (L / 8 / B) + L % 8 of instance (L / 8) % B, the pad groups exit), 32768 one
-    piece per wave on pair lanes (round 3), 65536 one piece per wave on quad lanes, 131072 the
-    streaming pass, 262144 the streaming pass with the last bitfield staged in LDS taken in place
-    of pre's position-order gather; two steps each, bit-exact against the oracle."""
-    monkeypatch.setenv("PZ_EPOCH_BAL64", "1")
-    inst = _inst(n, B, False)
+def test_native_epoch_window_forms(n, B, bal, dyn, db):
+    """The window pass's six column forms, each selected by the data: balances as u32 offsets or
+    u64 (a spread of 2^30 or more), {start, end} at 16, 32 or 64 bits (by CurrentDynasty); three
+    steps each, bit-exact against the oracle."""
+    inst = _widen(_inst(n, B, False), bal=bal, dyn=dyn)
     ne = NativeEpoch(inst, device=0)
-    assert ne.one_pass and ne.balance_bytes == 8
-    old = _lib.lib.dll.pz_debug_set_fused_variant(variant)
-    try:
-        _check(ne, inst, steps=2)
-    finally:
-        _lib.lib.dll.pz_debug_set_fused_variant(old)
+    assert ne.one_pass and (ne.balance_bytes, ne.dynasty_bytes) == (8 if bal else 4, db)
+    _check(ne, inst, steps=3)
+
+
+@pytest.mark.parametrize("n,B,last_bits", [(65536, 3, 1 << 21), (4097, 2, 1 << 21), (1 << 20, 2, (1 << 20) + 8)])
+def test_native_epoch_window_reward_bits_from_l2(n, B, last_bits):
+    """A last bitfield longer than the block's LDS can hold next to its tables (256 KiB here;
+    CalculateRewards reads only its first N bits): the window pass looks the reward bits up in
+    L2 instead (the kernels' _g form); at 1M validators with a 128 KiB bitfield, the LDS form
+    beside it.  Bit-exact over two steps."""
+    inst = _inst(n, B, False, last_bits=last_bits)
+    ne = NativeEpoch(inst, device=0)
+    assert ne.one_pass
+    _check(ne, inst, steps=2)
 
 
 @pytest.mark.parametrize("n,B,density", [(65536, 5, 0.75), (1 << 20, 2, 0.75), (4097, 3, 0.5), (1000, 2, 0.75)])
 def test_native_epoch_bal32_offsets(n, B, density):
     """The product's multi-instance layout: balances as u32 offsets from a per-instance u64 base
-    (FusedArgs.bal32, pz_epoch_state_columns reports 4 B), three steps against the oracle."""
+    (pz_epoch_state_columns reports 4 B), three steps against the oracle."""
     inst = _inst(n, B, False, density=density)
     ne = NativeEpoch(inst, device=0)
     assert ne.one_pass and (ne.balance_bytes, ne.dynasty_bytes) == (4, 4)
     _check(ne, inst, steps=3)
 
 
-@pytest.mark.parametrize("variant", [131072, 4096, 1 << 21, 1 << 22])
-@pytest.mark.parametrize("n,B", [(65536, 5), (32768, 9), (4097, 3)])
-def test_native_epoch_bal32_forms(n, B, variant):
-    """The u32-offset step's A/B forms: the streaming pass (persistent pipelined waves, 131072),
-    the XCD-aware grid (4096), two pieces per wave (1 << 21) and the streaming pass with the
-    last bitfield staged in LDS (1 << 22), with the winners in the waves: three steps against
-    the oracle."""
-    inst = _inst(n, B, False)
-    ne = NativeEpoch(inst, device=0)
-    assert ne.balance_bytes == 4
-    old = _lib.lib.dll.pz_debug_set_fused_variant(variant)
-    try:
-        _check(ne, inst, steps=3)
-    finally:
-        _lib.lib.dll.pz_debug_set_fused_variant(old)
-
-
-def test_native_epoch_bal32_rebase(monkeypatch):
-    """The offsets re-based every 2 steps (PZ_EPOCH_B32_PERIOD; 2^29 in the product): five
-    steps, each compared with the oracle."""
-    monkeypatch.setenv("PZ_EPOCH_B32_PERIOD", "2")
+def test_native_epoch_bal32_rebase():
+    """The offsets re-based every 2 steps (pz_epoch_options.rebase_period; 2^29 in the
+    product): five steps, each compared with the oracle."""
     inst = _inst(65536, 3, False)
-    ne = NativeEpoch(inst, device=0)
+    ne = NativeEpoch(inst, device=0, rebase_period=2)
     assert ne.balance_bytes == 4
     _check(ne, inst, steps=5)
 
@@ -153,15 +171,14 @@ def test_native_epoch_bal32_wide_spread():
     _check(ne, inst, steps=2)
 
 
-def test_native_epoch_bal32_wrap_below_zero(monkeypatch):
+def test_native_epoch_bal32_wrap_below_zero():
     """Balances of 0 and 1 under penalties wrap below zero as Go's uint64 does (2^64 - 1):
     exact in the offsets (mod 2^64); the re-base after the wrap finds the spread too wide and
     the state returns to the u64 column; three steps against the oracle."""
-    monkeypatch.setenv("PZ_EPOCH_B32_PERIOD", "1")
     inst = _inst(4096, 3, False, density=0.75)
     rng = np.random.default_rng(4)
     inst["balance"][:] = rng.integers(0, 2, size=inst["balance"].shape, dtype=np.uint64)
-    ne = NativeEpoch(inst, device=0)
+    ne = NativeEpoch(inst, device=0, rebase_period=1)
     assert ne.balance_bytes == 4
     _check(ne, inst, steps=3)
     assert (inst["balance"] > (1 << 63)).any()  # some balance wrapped
@@ -197,37 +214,63 @@ def test_native_epoch_single_launch_edges(case):
         assert int(scal[0, _lib.SCAL_ERR_XL]) == 2  # PZ_XLERR_BITFIELD
 
 
-def test_native_epoch_single_launch_matches_three_launches():
-    """A/B: the same instance stepped by the single launch and by pre + fused + mid
-    (pz_debug_set_fused_variant(128) disables the single launch): identical results."""
-    inst = _inst(65536, 1, False)
+@pytest.mark.parametrize("n", [65536, 4096])
+def test_native_epoch_single_launch_matches_window_pass(n):
+    """The same instance stepped by the single launch (pz_epoch_one_kernel) and by the window
+    pass (pz_epoch_options.window_only): identical balances, scalars, tallies and winners over
+    two steps."""
+    inst = _inst(n, 1, False)
     outs = []
-    for v in (0, 128):
+    for wo in (False, True):
         k = {key: (val.copy() if isinstance(val, np.ndarray) else val) for key, val in inst.items()}
-        old = _lib.lib.dll.pz_debug_set_fused_variant(v)
-        try:
-            ne = NativeEpoch(k, device=0)
-            for _ in range(2):
-                ne.step()
-            outs.append(ne.results())
-            ne.free()
-        finally:
-            _lib.lib.dll.pz_debug_set_fused_variant(old)
+        ne = NativeEpoch(k, device=0, window_only=wo)
+        for _ in range(2):
+            ne.step()
+        outs.append(ne.results())
+        ne.free()
     for x, y in zip(*outs):
         np.testing.assert_array_equal(x, y)
 
 
-@pytest.mark.parametrize("knob,val", [("PZ_EPOCH_MULTI", "1"), ("PZ_EPOCH_WIN_FUSED", "0")])
-@pytest.mark.parametrize("n,B,density", [(65536, 3, 0.75), (4097, 5, 0.75), (8192, 4, 0.5)])
-def test_native_epoch_one_pass_ab_knobs(knob, val, n, B, density, monkeypatch):
-    """The one-pass step's A/B forms read at state creation: one launch over the
-    B instances (PZ_EPOCH_MULTI=1) and the winners by the mid launch instead of in the
-    streaming waves (PZ_EPOCH_WIN_FUSED=0), bit-exact against the oracle over two steps."""
-    monkeypatch.setenv(knob, val)
-    inst = _inst(n, B, False, density=density)
-    ne = NativeEpoch(inst, device=0)
+@pytest.mark.parametrize("case", ["many_atts", "short_bitfield", "reward_panic", "empty_committees"])
+@pytest.mark.parametrize("B", [1, 3])
+def test_native_epoch_window_edges(case, B):
+    """The window pass on the single-launch edge cases and more: a committee with two
+    attestations besides the final one (the per-attestation path), a bitfield shorter than its
+    committee and the CheckBit(last, N-1) panic (flags, balances untouched), and empty
+    committees (an attestation with nobody to count: total 0 qualifies under 3 * 0 >= 2 * 0);
+    against the oracle."""
+    n = 4096
+    inst = _inst(n, B, False, last_bits=n - 8 if case == "reward_panic" else None)
+    natt = inst["natt"]
+    if case == "many_atts":  # each instance's final (N-bit) attestation names committee 0 too
+        inst["att_comm"] = inst["att_comm"].copy()
+        inst["att_comm"][natt - 1::natt] = 0
+    if case == "short_bitfield":
+        bo = inst["boffs"].astype(np.int64)
+        inst["bits"] = np.delete(inst["bits"], int(bo[3]) - 1)
+        bo[3:] -= 1
+        inst["boffs"] = bo.astype(np.uint64)
+    if case == "empty_committees":  # committees 5 and 9 emptied into their predecessors
+        coffs = inst["coffs"].astype(np.int64)
+        coffs[5] = coffs[6]
+        coffs[9] = coffs[10]
+        inst["coffs"] = coffs.astype(np.uint64)
+        _rebits(inst)
+    ne = NativeEpoch(inst, device=0, window_only=True)
     assert ne.one_pass
-    _check(ne, inst, steps=2)
+    if case in ("many_atts", "empty_committees"):
+        _check(ne, inst, steps=2)
+        return
+    ne.step()
+    bal, scal, vote, total, _ = ne.results()
+    for b in range(B if case == "reward_panic" else 1):  # (short_bitfield: instance 0's)
+        assert scal[b, _lib.SCAL_APPLIED] == 0
+        np.testing.assert_array_equal(bal[b], inst["balance"][b][ne.validators()])
+        if case == "reward_panic":
+            assert scal[b, _lib.SCAL_ERR_RWD] != 0
+        else:
+            assert int(scal[b, _lib.SCAL_ERR_XL]) == 2  # PZ_XLERR_BITFIELD
 
 
 @pytest.mark.parametrize("B", [1, 3])

@@ -57,9 +57,9 @@ def test_oracle_replay_matches_golden():
     assert sum(r["transition"] for r in recs) == 2 and all(r["status"] == "processed" for r in recs)
 
 
-def _product(nval, blocks):
+def _product(nval, blocks, **opts):
     from prysm_amd.blockchain import BeaconChain
-    ch = BeaconChain(nval)
+    ch = BeaconChain(nval, **opts)
     recs = ch.process_blocks(blocks)
     return recs, ch.roots()
 
@@ -144,8 +144,8 @@ def test_gpu_replay_many_calls_equal_one_call_65536():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("batch", ["1", "37", "5000"])
-def test_gpu_replay_message_batches_equal_one_batch(monkeypatch, batch):
-    """PZ_MSG_BATCH > 0 digests the processAttestation messages in batches sent after the
+def test_gpu_replay_message_batches_equal_one_batch(batch):
+    """pz_chain_options.msg_batch > 0 digests the processAttestation messages in batches sent after the
     transitions, on their own stream, while the walk goes on (chain.hip msg_send): every
     message digest, record and root equals the one-batch call's, over a chain fed in one call
     and in calls of 1-60 blocks."""
@@ -153,16 +153,14 @@ def test_gpu_replay_message_batches_equal_one_batch(monkeypatch, batch):
     nval = 65536
     blocks = synth.chain_blocks(nval, 400, seed=9)
     d, o = serialize_blocks(blocks)
-    monkeypatch.delenv("PZ_MSG_BATCH", raising=False)
     one = BeaconChain(nval)
     br1, ar1 = one.process_serialized(d, o)
-    monkeypatch.setenv("PZ_MSG_BATCH", batch)
-    two = BeaconChain(nval)
+    two = BeaconChain(nval, msg_batch=int(batch))
     br2, ar2 = two.process_serialized(d, o)
     np.testing.assert_array_equal(br2, br1)
     np.testing.assert_array_equal(ar2, ar1)
     assert two.roots() == one.roots()
-    many = BeaconChain(nval)
+    many = BeaconChain(nval, msg_batch=int(batch))
     rng = np.random.default_rng(4)
     ars, i = [], 0
     while i < len(blocks):
@@ -260,12 +258,11 @@ def test_oracle_shaped_message_chain_processes():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("batch", ["0", "3"])
-def test_gpu_replay_shaped_messages_vs_oracle(monkeypatch, batch):
+def test_gpu_replay_shaped_messages_vs_oracle(batch):
     from oracle import replay
     blocks = shaped_message_chain()
     o_recs, o_roots = replay.replay(blocks, 1024)
-    monkeypatch.setenv("PZ_MSG_BATCH", batch)
-    recs, roots = _product(1024, blocks)
+    recs, roots = _product(1024, blocks, msg_batch=int(batch))
     assert _hexrecs(recs) == _hexrecs(o_recs)
     for k in ("chain_active", "chain_crystallized", "cand_active", "cand_crystallized"):
         assert roots[k] == o_roots[k], k
@@ -552,53 +549,34 @@ def test_gpu_sharded_chain_configs4_full_vs_c_port(world):
 @pytest.mark.gpu
 @pytest.mark.parametrize("groups", ["1", "0"])
 @pytest.mark.parametrize("nval,ncomm", [(131072, 9), (262144, 17), (524288, 33)])
-def test_gpu_replay_wide_committees_vs_c_port(nval, ncomm, groups, monkeypatch):
+def test_gpu_replay_wide_committees_vs_c_port(nval, ncomm, groups):
     """Larger validator sets than configs[4]: 9, 17 and 33 slot-0 committees per block, each a
     group of the grouped tally (votes.h kVoteMaxGroups), of up to 249 members (every bitfield
     inline in the 64-B record), over 130 blocks (two transitions) against the C restatement;
-    PZ_VOTE_GROUPS=0 runs the per-attestation form over the same chains."""
+    groups 0 runs the per-attestation form over the same chains (pz_chain_options.tally_forms)."""
+    from prysm_amd import _lib
     from prysm_amd.blockchain import BeaconChain, serialize_blocks
     from replay_port_helpers import mismatches, port_replay
-    monkeypatch.setenv("PZ_VOTE_GROUPS", groups)
     sizes = synth.genesis_committee_sizes(nval)
     assert len(sizes) == ncomm and max(k for _, k in sizes) <= 256
     blocks = synth.chain_blocks(nval, 130, seed=11)
     data, offs = serialize_blocks(blocks)
-    ch = BeaconChain(nval)
+    ch = BeaconChain(nval, tally_forms=0 if groups == "1" else _lib.TALLY_PER_ATTESTATION)
     br, ar = ch.process_serialized(data, offs)
     assert int(br["transition"].sum()) == 2
     out, port_roots = port_replay(data, offs, nval, len(ar))
     assert mismatches(br, ar, ch.roots(), out, port_roots) == []
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("path,epack,bits,ids,groups", [("segments", "copy", "inline", "run", "1"),
-                                                         ("packed", "copy", "rows", "rows", "1"),
-                                                         ("direct", "direct", "inline", "run", "1"),
-                                                         ("direct", "copy", "inline", "run", "0"),
-                                                         ("direct", "copy", "rows", "run", "1"),
-                                                         ("direct", "copy", "inline", "rows", "1")])
-def test_gpu_replay_vote_queue_paths_vs_c_port(path, epack, bits, ids, groups, monkeypatch):
-    """Every way a vote-cache flush reaches the device (PZ_VOTE_PATH: the walk's pinned queue
-    read in place by the voter-major tally -- the product --, its arrays staged by one
-    multi-segment copy, or round 3's packed arena), every record form (votes.h VoteRec: the
-    bitfield inline or in the row array, PZ_VOTE_BITS; the parents' ids as a run or an explicit
-    row, PZ_VOTE_IDS) and both tally forms (grouped by committee -- the product when every record
-    is a run with its bitfield inline --, or per attestation: PZ_VOTE_GROUPS=0 or any other form)
-    over 2,000 blocks of the configs[4] chain (31 transitions, the two queues alternating,
-    carried over a call boundary) against the C restatement; the direct/direct case also has the
-    transitions' epoch kernels read their inputs in place (PZ_EPOCH_PACK=direct)."""
-    monkeypatch.setenv("PZ_VOTE_PATH", path)
-    monkeypatch.setenv("PZ_EPOCH_PACK", epack)  # the transition's epoch inputs: staged copy or read in place
-    monkeypatch.setenv("PZ_VOTE_BITS", bits)  # (read when the chain is made)
-    monkeypatch.setenv("PZ_VOTE_IDS", ids)
-    monkeypatch.setenv("PZ_VOTE_GROUPS", groups)  # (read per flush)
+def _vote_queue_chain(**opts):
+    """2,000 blocks of the configs[4] chain in two calls (31 transitions, the two queues
+    alternating, carried over a call boundary) against the C restatement."""
     from prysm_amd.blockchain import BeaconChain, serialize_blocks
     from replay_port_helpers import mismatches, port_replay
     nval = 65536
     blocks = synth.chain_blocks(nval, 2000, seed=6)
     data, offs = serialize_blocks(blocks)
-    ch = BeaconChain(nval)
+    ch = BeaconChain(nval, **opts)
     br, ar = ch.process_serialized(data[: int(offs[1000])], offs[:1001])  # two calls: the queues
     br2, ar2 = ch.process_serialized(data, offs[1000:])                     # carry over a call
     br, ar = np.concatenate([br, br2]), np.concatenate([ar, ar2])
@@ -607,7 +585,30 @@ def test_gpu_replay_vote_queue_paths_vs_c_port(path, epack, bits, ids, groups, m
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pipeline", ["0", "1"])
+@pytest.mark.parametrize("forms", [0, 1, 2, 4, 7])
+def test_gpu_replay_vote_queue_forms_vs_c_port(forms):
+    """Every record form of the vote queue (votes.h VoteRec: the bitfield inline or in the row
+    array, TALLY_BITS_ROWS; the parents' ids as a run or an explicit row, TALLY_ID_ROWS) and both
+    tally forms (grouped by committee -- the product when every record is a run with its
+    bitfield inline --, or per attestation: TALLY_PER_ATTESTATION or any other form), forced by
+    pz_chain_options.tally_forms, over the configs[4] chain against the C restatement."""
+    _vote_queue_chain(tally_forms=forms)
+
+
+@pytest.mark.gpu
+@pytest.mark.ab
+@pytest.mark.parametrize("path,epack", [("segments", "copy"), ("packed", "copy"), ("direct", "direct")])
+def test_ab_replay_vote_queue_paths_vs_c_port(path, epack, monkeypatch):
+    """The A/B library's measured-and-dropped ways a flush reaches the device (PZ_VOTE_PATH: the
+    queue's arrays staged by one multi-segment copy, or round 3's packed arena) and the
+    transitions' epoch kernels reading their inputs in place (PZ_EPOCH_PACK=direct)."""
+    monkeypatch.setenv("PZ_VOTE_PATH", path)
+    monkeypatch.setenv("PZ_EPOCH_PACK", epack)
+    _vote_queue_chain()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipeline", ["0", pytest.param("1", marks=pytest.mark.ab)])
 def test_gpu_malformed_block_ends_the_call_there(pipeline, monkeypatch):
     """A block that is not a canonical encoding ends the call there with PZ_EINVAL, the blocks
     before it processed (as the reference's sync service handles each block as it arrives), in

@@ -169,11 +169,12 @@ def test_scalar_columns_many_tiles(which, offsets):
         assert wire.validators_device(v, 11) == wire.validators(v)
 
 
-@pytest.mark.parametrize("variant", [16384, 16384 | 128])
+@pytest.mark.ab
+@pytest.mark.parametrize("variant", [16384])
 def test_lookback_multi_window(variant):
-    """The wave-reduced look-back over several windows: with no inclusive prefix published
-    (wire.hip variant bit 14; bit 7 shrinks the window to 512 predecessors) every tile sums
-    aggregates window after window back to tile 0.  3,000 tiles: up to 2 (6) windows per tile.
+    """The wave-reduced look-back over several windows (the A/B library's test path): with no
+    inclusive prefix published (wire.hip variant bit 14) every tile sums aggregates window after
+    window back to tile 0.  3,000 tiles: up to 2 windows per tile.
     The bytes must equal the product kernel's, which must equal the host encoder's."""
     import torch
 
@@ -208,29 +209,3 @@ def test_lookback_multi_window(variant):
     assert ref[:len(want)].cpu().numpy().tobytes() == want
 
 
-@pytest.mark.parametrize("variant", [32768, 65536, 98304])
-@pytest.mark.parametrize("offsets,small", [(False, True), (False, False), (True, False)])
-def test_scalar_tile_geometry(variant, offsets, small):
-    """The tile-geometry A/B of the 3-column kernel (wire.hip PZ_WIRE_VAL_GEOM: 3,072- and
-    2,048-record tiles, 48 / 32 KiB stages): many tiles and a ragged last tile, genesis-like
-    records (~15 B: the LDS stage path) or mixed varint widths (tiles that outgrow the stage
-    write lane by lane), framed against the host encoder and bare with record offsets against
-    the protobuf runtime."""
-    n = 3072 * 13 + 777
-    rng = np.random.default_rng(variant + offsets)
-    if small:
-        start = rng.integers(0, 3, size=n).astype(np.uint64) * rng.integers(0, 1 << 20, size=n, dtype=np.uint64)
-        v = pb.Validators(n, balance=rng.integers(16, 49, size=n, dtype=np.uint64), start_dynasty=start,
-                          end_dynasty=np.full(n, 9999999999999999999, np.uint64))
-    else:
-        v = _scalar_cols(rng, n, ("balance", "start_dynasty", "end_dynasty"))
-    old = _lib.lib.dll.pz_debug_set_wire_variant(variant)
-    try:
-        if offsets:
-            raw, offs = wire.validators_device(v, 0, with_offsets=True)
-            assert offs[0] == 0 and offs[-1] == len(raw)
-            assert raw == b"".join(oracle_record(v, i) for i in range(n))
-        else:
-            assert wire.validators_device(v, 11) == wire.validators(v)
-    finally:
-        _lib.lib.dll.pz_debug_set_wire_variant(old)
