@@ -437,7 +437,9 @@ int  pz_comm_init_shm(const char* name, int world, int rank, int device, uint32_
  * communicator's stream of each local rank (after its wait for the compute stream: the
  * collective's own time, exposed or overlapped).  pz_comm_collective_time returns the sum over
  * the collectives since the last call (the max over local ranks for each) and their count, and
- * restarts the sum; it waits for the pending collectives. */
+ * restarts the sum; it waits for the pending collectives.  Each timed collective holds two
+ * events per local rank until it is collected: a caller that leaves timing on collects
+ * regularly (the bench collects once per timed run). */
 int  pz_comm_set_timing(pz_comm* comm, int on);
 int  pz_comm_collective_time(pz_comm* comm, double* ms, uint64_t* count);
 /* world = ranks in the partition, nlocal = ranks this process drives (global ranks

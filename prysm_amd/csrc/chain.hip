@@ -638,17 +638,20 @@ struct DigestBufs {
 // a chain over a pz_comm (pz_chain_new_comm) gives each rank the
 // 64-aligned validator range [lo, hi): its balances, its columns of every vote-cache voter
 // bitmap and its partial VoteTotalDeposit sums, and its part of every epoch.
-// Device buffers a growth replaced: freed with the chain, not at the growth (a hipFree waits for
-// the whole device, and the copies out of the old buffer are still queued; growth is geometric,
-// so what is kept is at most the live size).
+// Device buffers a growth replaced: not freed at the growth (a hipFree waits for the whole
+// device, and the copies out of the old buffer are still queued) but at the end of the
+// pz_chain_process_blocks call, once its streams have drained (release_retired), so a long-lived
+// chain holds no dead generations between calls.
 struct Retired {
   std::vector<void*> p;
   void keep(void* x) {
     if (x) p.push_back(x);
   }
-  ~Retired() {
+  void release() {
     for (void* x : p) (void)hipFree(x);
+    p.clear();
   }
+  ~Retired() { release(); }
 };
 
 struct RankDev {
@@ -3503,6 +3506,20 @@ int pz_chain_process_blocks(pz_chain* c, const uint8_t* blocks, const uint64_t* 
     return rc;
   }
   g.prof[kProfHash1] += F.wait_s;
+  if (!g.retired.p.empty()) {  // the call's grown-out buffers, once nothing queued reads them
+    try {
+      each_rank(g, [](RankDev& r) {
+        hchk(hipSetDevice(r.dev), "hipSetDevice");
+        hchk(hipStreamSynchronize(r.s), "sync");
+      });
+      hchk(hipSetDevice(g.device), "hipSetDevice");
+      hchk(hipStreamSynchronize(g.s2), "sync");
+      hchk(hipStreamSynchronize(g.ms), "sync");
+    } catch (int rc) {
+      return rc;
+    }
+    g.retired.release();
+  }
   const uint64_t bad = F.bad.load();
   if (bad < n) return fail(PZ_EINVAL, "block %llu is not a canonical BeaconBlock encoding (blocks before it were "
                                       "processed)", (unsigned long long)bad);

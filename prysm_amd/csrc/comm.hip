@@ -465,6 +465,8 @@ int pz_comm_set_timing(pz_comm* c, int on) {
 
 int pz_comm_collective_time(pz_comm* c, double* ms, uint64_t* count) {
   if (!c || !ms || !count) return fail(PZ_EINVAL, "null pointer");
+  // every elapsed time first; the events go back to the pool only once all were read, so an
+  // error leaves each event owned by `timed` alone (the destructor destroys it once)
   double sum = 0;
   for (pz_comm::TimedOp& t : c->timed) {
     float mx = 0;
@@ -475,11 +477,14 @@ int pz_comm_collective_time(pz_comm* c, double* ms, uint64_t* count) {
       if (e == hipSuccess) e = hipEventElapsedTime(&v, t.t0[i], t.t1[i]);
       if (e != hipSuccess) return hip_fail(e, "collective timing");
       mx = std::max(mx, v);
-      c->ev_pool.push_back(t.t0[i]);
-      c->ev_pool.push_back(t.t1[i]);
     }
     sum += mx;
   }
+  for (pz_comm::TimedOp& t : c->timed)
+    for (size_t i = 0; i < t.t0.size(); ++i) {
+      c->ev_pool.push_back(t.t0[i]);
+      c->ev_pool.push_back(t.t1[i]);
+    }
   *ms = sum;
   *count = c->timed.size();
   c->timed.clear();

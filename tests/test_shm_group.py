@@ -86,13 +86,21 @@ def _run(world, n, slot, mode):
     for p in ps:
         p.start()
     res = {}
-    for _ in range(world):
-        r = q.get(timeout=60)
-        res[r[0]] = r[1:]
-    for p in ps:
-        p.join(30)
-        assert p.exitcode == 0
-    assert not os.path.exists("/dev/shm" + name), "segment left behind"
+    try:
+        for _ in range(world):
+            r = q.get(timeout=60)
+            res[r[0]] = r[1:]
+        for p in ps:
+            p.join(30)
+            assert p.exitcode == 0
+        assert not os.path.exists("/dev/shm" + name), "segment left behind"
+    finally:
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+                p.join()
+        if os.path.exists("/dev/shm" + name):  # (a killed rank 0 leaves its segment behind)
+            os.unlink("/dev/shm" + name)
     return res
 
 

@@ -46,6 +46,9 @@ def run_ranks(mode, world, indir, opts, timeout=300):
             if p.poll() is None:
                 p.kill()
                 p.wait()
+        # a rank 0 killed between creating the segment and every rank joining leaves it behind
+        if os.path.exists("/dev/shm" + name):
+            os.unlink("/dev/shm" + name)
     for r, p in enumerate(procs):
         assert p.returncode == 0, "rank %d exited %s:\n%s" % (r, p.returncode, logs[r][-3000:])
     return [np.load(o) for o in outs]
