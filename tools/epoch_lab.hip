@@ -390,6 +390,7 @@ int main(int argc, char** argv) {
   const uint32_t lbytes = (uint32_t)((lastb + 32 + 15) & ~15ull);
   const uint32_t vwords = (maxspan + 256) / 32 + 4;
   const size_t ldsb = lbytes + 4ull * vwords + 4ull * ((maxc + 2) & ~1u) + 16ull * maxc + maxc + 16;
+  setvbuf(stdout, nullptr, _IONBF, 0);
   printf("N %llu B %u R %u ncomm %u maxc %u maxspan %u lds %zu\n", (unsigned long long)N, B, R, ncomm, maxc, maxspan,
          ldsb);
   // blens per instance
@@ -496,12 +497,12 @@ int main(int argc, char** argv) {
   const int steps = nsets * ((48 + nsets - 1) / nsets);
   auto timeit = [&](const char* name, auto launch) {
     for (int w = 0; w < 2; ++w)
-      for (int k = 0; k < nsets; ++k) launch(sets[k].a);
+      for (int k = 0; k < nsets; ++k) launch(k);
     CK(hipDeviceSynchronize());
     float best = 1e9, tot = 0;
     for (int rep = 0; rep < 3; ++rep) {
       CK(hipEventRecord(e0, 0));
-      for (int i = 0; i < steps; ++i) launch(sets[i % nsets].a);
+      for (int i = 0; i < steps; ++i) launch(i % nsets);
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));
       float ms;
@@ -518,11 +519,8 @@ int main(int argc, char** argv) {
   {
     std::vector<uint32_t*> ys(nsets);
     for (int k = 0; k < nsets; ++k) CK(hipMalloc(&ys[k], (size_t)B * vstride * 4));
-    int k = 0;
-    timeit("yardstick x+=y (int32, 12 B/elem)", [&](Args& a) {
-      const int kk = (int)(&a - &sets[0].a);
-      (void)k;
-      hipLaunchKernelGGL(yard_kernel, dim3(2048), dim3(256), 0, 0, a.bal32, ys[kk], (uint64_t)B * vstride / 4);
+    timeit("yardstick x+=y (int32, 12 B/elem)", [&](int k) {
+      hipLaunchKernelGGL(yard_kernel, dim3(2048), dim3(256), 0, 0, sets[k].a.bal32, ys[k], (uint64_t)B * vstride / 4);
     });
     for (auto y : ys) CK(hipFree(y));
   }
@@ -530,8 +528,8 @@ int main(int argc, char** argv) {
   {                                                                                                      \
     CK(hipFuncSetAttribute((const void*)win_kernel<NT, D, FL>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                            (int)ldsb));                                                                  \
-    timeit(NAME, [&](Args& a) {                                                                          \
-      hipLaunchKernelGGL((win_kernel<NT, D, FL>), dim3(B * R), dim3(NT), ldsb, 0, a);                   \
+    timeit(NAME, [&](int k) {                                                                            \
+      hipLaunchKernelGGL((win_kernel<NT, D, FL>), dim3(B * R), dim3(NT), ldsb, 0, sets[k].a);           \
     });                                                                                                  \
   }
   if (which < 0 || which == 0) RUN(1024, 2, 0, "window 1024t D2")

@@ -1,4 +1,5 @@
-"""Per-part device time of the epoch step (HIP events, one process, interleaved rounds)."""
+"""Per-part device time of the two-pass epoch step (HIP events, one process, interleaved rounds).
+Needs the A/B library's part entry points: PZ_LIB=build/ab/libprysm_hip.so python tools/epoch_parts.py"""
 import ctypes
 import json
 import os
@@ -28,17 +29,7 @@ def main(nval=65536, ninst=256, rounds=5, reps=10):
         "count_pop": lambda: dll.pz_debug_epoch_count(bp, 0, 1, 0, sh),
         "count_xl": lambda: dll.pz_debug_epoch_count(bp, 0, 0, 1, sh),
         "count_all": lambda: dll.pz_debug_epoch_count(bp, 1, 1, 1, sh),
-        # same-process A/B of the count-pass variants (pz_debug_set_count_variant)
-        **{"count_val_v%d" % v: (lambda v=v: (dll.pz_debug_set_count_variant(v),
-                                              dll.pz_debug_epoch_count(bp, 1, 0, 0, sh),
-                                              dll.pz_debug_set_count_variant(0))) for v in range(6)},
-        **{"count_xl_v%d" % v: (lambda v=v: (dll.pz_debug_set_count_variant(v),
-                                             dll.pz_debug_epoch_count(bp, 0, 0, 1, sh),
-                                             dll.pz_debug_set_count_variant(0))) for v in (0, 8, 16)},
         "reward": lambda: dll.pz_debug_epoch_reward(bp, sh),
-        "reward_nobits": lambda: dll.pz_debug_epoch_reward_mode(bp, 1, sh),
-        "reward_noreduce": lambda: dll.pz_debug_epoch_reward_mode(bp, 2, sh),
-        "reward_nobits_noreduce": lambda: dll.pz_debug_epoch_reward_mode(bp, 3, sh),
         # yardsticks on the same 16.7M x u64 balance array (same process, same device)
         "torch_copy": lambda: yard.copy_(de.balance.view(-1)),
         "torch_inplace_add": lambda: yard.add_(1),

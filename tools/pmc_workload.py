@@ -112,6 +112,4 @@ WORKLOADS = {
 
 
 if __name__ == "__main__":
-    if os.environ.get("FUSED_VARIANT"):  # an A/B of the epoch step's variant (pz_debug_set_fused_variant)
-        _lib.lib.dll.pz_debug_set_fused_variant(int(os.environ["FUSED_VARIANT"]))
     WORKLOADS[sys.argv[1] if len(sys.argv) > 1 else "main"]()
