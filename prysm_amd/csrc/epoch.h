@@ -153,11 +153,12 @@ struct FusedArgs {
 // ---- the window pass (epoch_window.hip): the one-pass step of B instances in ONE launch ------
 // Block (instance, range): a range is a run of this rank's committees (local ids [cr0, cr1),
 // positions [lcs[cr0], lcs[cr1])), so every committee's tallies complete inside one block.
-constexpr int kWinThreads = 1024, kWinDepth = 2;
+constexpr int kWinThreads = 1024, kWinDepth = 2, kWinDepth16 = 3;  // (pieces in flight per wave)
 struct WinArgs {
-  const uint4* rdesc;         // [R] {cr0, cr1, first window (wdesc index), windows}
+  const uint4* rdesc;         // [R][2] {cr0, cr1, first piece (pdesc index), pieces}, {P0, P1, 0, 0}
   uint32_t R;                 // ranges per instance (grid: B x R blocks)
-  const uint32_t* wdesc;      // [windows] the first committee overlapping each 256-position window
+  const uint2* pdesc;         // [pieces] {first position, (committee << 9) | positions}: <= 256
+                              //   positions of one committee, from its first position rounded down to 4
   const uint32_t* lcs;        // [nlc + 1] local committee starts (local positions; lcs[nlc] = nval)
   const uint4* lci;           // [B][nlc + 1] {bitfield offset lo, hi (its single attestation),
                               //   attestation index | kNoAtt | kManyAtt, first catt index}
@@ -176,8 +177,9 @@ struct WinArgs {
   uint64_t* total_next;       //   attestations stay zero for pz_epoch_state_tallies' sum), else NULL
   int rank0;                  // this rank writes the per-instance scalars
   // LDS plan: last-bitfield bytes (0: reward bits from L2), vote-bit words, most committees /
-  // attestations of a range, 32-bit words per committee bitfield
+  // attestations of a range, 32-bit words per committee bitfield (the vote-bit placement's items)
   uint32_t lds_lbf, lds_vw, lds_maxc, lds_maxk, wpc;
+  uint64_t* trace;            // A/B library only: [blocks][4] phase stamps (s_memrealtime), else NULL
 };
 size_t window_lds_bytes(const WinArgs& w);
 hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t s);

@@ -529,8 +529,7 @@ void local_committees(const pz_epoch_host* h, uint64_t lo, uint64_t hi, bool kee
 // The window pass's plan for one part of one rank (epoch.h WinArgs): the rank's committees
 // (those whose first position lies in [lo, hi); the last rank also takes the empty ones at N)
 // split into R ranges of about equal positions, R = CUs / B (one block per CU), each range's
-// 256-position windows with their first committee, the per-instance committee table, and the
-// LDS carve-up.  The last bitfield goes into LDS when the block still fits the CU's 160 KiB.
+// committee pieces, the per-instance committee table, and the LDS carve-up.  The last bitfield goes into LDS when the block still fits the CU's 160 KiB.
 static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Part& q, const std::vector<uint32_t>& catt_offs,
                 const std::vector<uint32_t>& catt) {
   const uint64_t Bp = q.B, i0 = q.i0, natt = st->natt, nc1 = st->ncomm + 1, N = st->N;
@@ -580,13 +579,14 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.dev);
   uint32_t R = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::max<uint32_t>(nlc, 1), ((uint64_t)cus + Bp - 1) / Bp));
   std::vector<uint4> rdesc;
-  std::vector<uint32_t> wdesc;
+  std::vector<uint2> pdesc;
   WinArgs& w = q.w;
   std::memset(&w, 0, sizeof w);
-  constexpr size_t kLdsMax = 160 * 1024 - 512;  // (the kernel's static reduction slots)
+  constexpr size_t kLdsMax = 160 * 1024 - 1024;  // (the kernel's static reduction slots)
+  if (nlc >= (1u << 23)) return fail(PZ_EINVAL, "window pass: more than 2^23 committees on a rank");
   for (;;) {
-    rdesc.assign(R, make_uint4(0, 0, 0, 0));
-    wdesc.clear();
+    rdesc.assign(2 * (size_t)R, make_uint4(0, 0, 0, 0));
+    pdesc.clear();
     uint32_t c = 0, maxc = 0, maxk = 0, maxw = 0;
     for (uint32_t r = 0; r < R; ++r) {
       const uint64_t t = (uint64_t)lcs[nlc] * (r + 1) / R;
@@ -598,16 +598,23 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
         if (c1 == c && c1 < nlc) ++c1;  // at least one committee per range while they last
       }
       const uint64_t P0 = lcs[c], P1 = lcs[c1], P0a = P0 & ~3ull;
-      const uint32_t nwin = P1 > P0 ? (uint32_t)((P1 - P0a + 255) / 256) : 0;
-      rdesc[r] = make_uint4(c, c1, (uint32_t)wdesc.size(), nwin);
-      uint32_t cc = c;
-      for (uint32_t k = 0; k < nwin; ++k) {
-        const uint64_t ws = P0a + 256ull * k;
-        while (cc + 1 < c1 && lcs[cc + 1] <= ws) ++cc;
-        wdesc.push_back(cc);
+      const uint32_t pb = (uint32_t)pdesc.size();
+      // pieces: a committee's first from its first position to the next 256 boundary after its
+      // rounded-down start, then 256-position runs from 4-aligned starts
+      for (uint32_t cc = c; cc < c1; ++cc) {
+        const uint64_t cs = lcs[cc], ce = lcs[cc + 1];
+        for (uint64_t ps = cs; ps < ce;) {
+          const uint64_t pe = std::min<uint64_t>(ce, (ps & ~3ull) + 256);
+          pdesc.push_back(make_uint2((uint32_t)ps, (cc << 9) | (uint32_t)(pe - ps)));
+          ps = pe;
+        }
       }
+      rdesc[2 * r] = make_uint4(c, c1, pb, (uint32_t)pdesc.size() - pb);
+      rdesc[2 * r + 1] = make_uint4((uint32_t)P0, (uint32_t)P1, 0, 0);
       maxc = std::max(maxc, c1 - c);
-      maxw = std::max(maxw, nwin);
+      // vote-bit words: the range's positions from P0a, plus a piece's overhang past P1 and the
+      // placement's spill word
+      maxw = std::max<uint32_t>(maxw, (uint32_t)((P1 - P0a + 31) / 32) + 10);
       for (uint64_t b = 0; b < Bp; ++b)
         maxk = std::max(maxk, lci[b * (nlc + 1) + c1].w - lci[b * (nlc + 1) + c].w);
       c = c1;
@@ -615,7 +622,7 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
     w.R = R;
     w.lds_maxc = std::max<uint32_t>(maxc, 1);
     w.lds_maxk = (std::max<uint32_t>(maxk, 1) + 1) & ~1u;  // (keeps the byte arrays after it 16-B aligned)
-    w.lds_vw = 8 * maxw + 2;
+    w.lds_vw = (maxw + 3) & ~3u;
     w.wpc = wpc;
     w.lds_lbf = (uint32_t)lbf;
     if (window_lds_bytes(w) <= kLdsMax) break;
@@ -624,18 +631,19 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
     if (R >= nlc) return fail(PZ_EINVAL, "window pass: no range split fits the LDS");
     R = std::min<uint32_t>(nlc, 2 * R);
   }
-  if (wdesc.empty()) wdesc.push_back(0);
+  if (pdesc.empty()) pdesc.push_back(make_uint2(0, 0));
   uint4 *d_rdesc = nullptr, *d_lci = nullptr, *d_aw = nullptr;
-  uint32_t *d_wdesc = nullptr, *d_lcs = nullptr, *d_lnb = nullptr, *d_csz = nullptr, *d_wn = nullptr;
+  uint2* d_pdesc = nullptr;
+  uint32_t *d_lcs = nullptr, *d_lnb = nullptr, *d_csz = nullptr, *d_wn = nullptr;
   int rc;
-  if ((rc = upload(s, &d_rdesc, rdesc.data(), rdesc.size())) || (rc = upload(s, &d_wdesc, wdesc.data(), wdesc.size())) ||
+  if ((rc = upload(s, &d_rdesc, rdesc.data(), rdesc.size())) || (rc = upload(s, &d_pdesc, pdesc.data(), pdesc.size())) ||
       (rc = upload(s, &d_lcs, lcs.data(), lcs.size())) || (rc = upload(s, &d_lci, lci.data(), lci.size())) ||
       (rc = upload(s, &d_lnb, lnb.data(), lnb.size())) || (rc = upload(s, &d_csz, csz.data(), csz.size())) ||
       (rc = upload(s, &d_aw, aw.data(), aw.size())) ||
       (rc = dalloc(s, &d_wn, (size_t)Bp * std::max<uint32_t>(st->nrec, 1))))
     return rc;
   w.rdesc = d_rdesc;
-  w.wdesc = d_wdesc;
+  w.pdesc = d_pdesc;
   w.lcs = d_lcs;
   w.lci = d_lci;
   w.lnb = d_lnb;

@@ -10,18 +10,21 @@
 // block: they are summed in LDS and leave with plain stores, and the block applies the winner
 // rule (core.go:549-555) itself -- no tally atomics to HBM, no winner pass.
 //
-//   prologue  the first windows' loads go out before anything else; then, with them in flight:
+//   prologue  the first pieces' loads go out before anything else; then, with them in flight:
 //             GetAttestersTotalDeposit (validator.go:93-102) as a bit count over every
 //             bitfield of the instance (each block counts them: nothing precedes the launch),
 //             whose last bitfield (CalculateRewards reads it by validator index,
 //             incentives.go:22-27) is copied into LDS on the way; the bitfield-length panics
 //             (core.go:538-541); the range's committee bitfields placed in position order in
-//             an LDS bitmap (the vote bits of single-attestation committees)
-//   loop      fixed 256-position windows: lane l takes 4 contiguous positions, every column
-//             load 16 B per lane and issued kWinDepth windows ahead (no load waits on
-//             another); the reward bit of position p is bit co_index[p] of the LDS copy; the
-//             crosslink tallies (core.go:533-545) are per-committee segment sums of the
-//             pre-reward balances (DPP wave sums) added into LDS
+//             an LDS bitmap (the vote bits of single-attestation committees).  The loads of a
+//             round -- bit-count chunks, length checks, committee table -- go out together.
+//   loop      committee pieces (<= 256 positions of ONE committee, from its first position
+//             rounded down to 4): lane l takes 4 contiguous positions, every column load 16 B
+//             per lane, each wave kWinDepth(16) pieces ahead (descriptors one round further); the
+//             reward bit of position p is bit co_index[p] of the LDS copy; the crosslink tallies
+//             (core.go:533-545) of the piece's committee are four 32-bit DPP wave sums of the
+//             pre-reward u32 balance offsets (low 15 bits with the count above them, high 17
+//             bits), added into LDS
 //   epilogue  every attestation of the range: vote / total stored, the winner rule as an
 //             atomicMin on its shard; the block's next-cycle partial sum (core.go:459-464)
 //             as one atomic
@@ -47,7 +50,19 @@ __device__ __forceinline__ uint4 ldnt16(const void* p) {
 __device__ __forceinline__ uint64_t pk64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 
-// One window's column words per lane: the balances of its 4 positions (u32 offsets: one 16-B
+// Sum of a u32 over the wave by DPP, wave-uniform (every lane active): quad swaps, half-row
+// and row mirrors, row broadcasts 15 / 31 into lane 63.
+__device__ __forceinline__ uint32_t wsum32(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, false);   // quad_perm 1,0,3,2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, false);   // quad_perm 2,3,0,1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xf, 0xf, false);  // row_half_mirror
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xf, 0xf, false);  // row_mirror
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast31
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// One piece's column words per lane: the balances of its 4 positions (u32 offsets: one 16-B
 // load; u64: two), their {start, end} bounds (16-bit pairs: one load; 32-bit pairs: two; the
 // 64-bit columns: four) and their co_index entries.
 template <bool B32, int SEW>
@@ -55,17 +70,19 @@ struct WinCols {
   uint4 b[B32 ? 1 : 2];
   uint4 s[SEW == 16 ? 1 : SEW == 32 ? 2 : 4];
   uint4 ci;
-  uint32_t c0;  // the first committee overlapping the window
 };
 
+// piece descriptor: {first position, (committee << 9) | positions}
+__device__ __forceinline__ uint32_t pc_start(uint2 d) { return d.x; }
+__device__ __forceinline__ uint32_t pc_count(uint2 d) { return d.y & 511u; }
+__device__ __forceinline__ uint32_t pc_comm(uint2 d) { return d.y >> 9; }
+
 template <bool B32, int SEW>
-__device__ __forceinline__ void win_load(const EpochArgs& a, const WinArgs& w, uint64_t inst, uint32_t wb,
-                                         uint32_t nwin, uint64_t P0, uint64_t P1, uint64_t P0a, uint32_t k, int lane,
+__device__ __forceinline__ void win_load(const EpochArgs& a, const WinArgs& w, uint64_t inst, uint2 d, int lane,
                                          WinCols<B32, SEW>& x) {
-  if (k >= nwin) return;  // (wave-uniform: no window left for this slot)
-  const uint64_t p = P0a + 256ull * k + 4ull * lane;
-  const bool any = p + 3 >= P0 && p < P1;
-  const uint64_t pp = any ? p : P0a;  // (a lane wholly outside the range re-reads the first quad)
+  const uint64_t s0 = pc_start(d), pa = s0 & ~3ull, p = pa + 4ull * lane;
+  const bool any = p + 3 >= s0 && p < s0 + pc_count(d);
+  const uint64_t pp = any ? p : pa;  // (a lane wholly outside the piece re-reads the first quad)
   const uint64_t row = inst * w.vstride + pp;
   if (B32) {
     x.b[0] = *reinterpret_cast<const uint4*>(w.bal32 + row);
@@ -86,7 +103,6 @@ __device__ __forceinline__ void win_load(const EpochArgs& a, const WinArgs& w, u
     x.s[SEW == 64 ? 3 : 0] = ldnt16(a.end + row + 2);
   }
   x.ci = *reinterpret_cast<const uint4*>(a.co_index + pp);
-  x.c0 = w.wdesc[wb + k];
 }
 
 // validator.go:45-53 on position i of the lane's quad (the saturated bounds classify exactly:
@@ -113,8 +129,8 @@ __device__ __forceinline__ bool win_active(const WinCols<B32, SEW>& x, int i, ui
 // LDS carve-up of one block (bytes; WinArgs.lds_* from the host's plan)
 struct WinLds {
   uint8_t* lbf;     // [lds_lbf] the instance's last bitfield from (lb & ~15)
-  uint32_t* vb;     // [lds_vw] vote bits of the range, position order from P0a
-  uint32_t* cst;    // [maxc + 1] committee starts relative to P0a
+  uint32_t* vb;     // [lds_vw] vote bits of the range, position order from P0 & ~3
+  uint32_t* cst;    // [maxc + 1] committee starts relative to P0 & ~3
   uint32_t* kbg;    // [maxc + 1] each committee's first attestation (index into catt)
   uint64_t* cbo;    // [maxc] single-attestation committees: bitfield offset
   uint32_t* cnb;    // [maxc] ... and its bits (min(committee size, 8 * bitfield length))
@@ -151,55 +167,83 @@ size_t window_lds_bytes(const WinArgs& w) {
          w.lds_maxc + 16;
 }
 
-template <bool B32, int SEW, bool LLB>
+// AB: measurement ablations, instantiated only in the A/B library (results wrong for AB != 0):
+// 1 no crosslink tallies, 2 no bit count / length checks in the prologue (applied taken as
+// true), 4 no reward-bit lookups, 8 no vote-bit placement.
+template <bool B32, int SEW, bool LLB, int AB = 0, int D = kWinDepth>
 __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w) {
   extern __shared__ __align__(16) uint8_t lds_dyn[];
-  constexpr int NT = kWinThreads, NW = NT / 64, D = kWinDepth;
-  __shared__ uint64_t red[NW][2];
+  constexpr int NT = kWinThreads, NW = NT / 64;
+  __shared__ uint64_t red[NW][2], red2[NW][2];  // (the prologue's and the loop's: no barrier between their uses)
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = rfl(tid >> 6);
+#ifdef PZ_AB_BUILD
+  if (w.trace && tid == 0) w.trace[4ull * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
   const uint64_t inst = blockIdx.x / w.R;
   const uint32_t r = blockIdx.x - (uint32_t)inst * w.R;
-  const uint4 rd = w.rdesc[r];
-  const uint32_t cr0 = rd.x, cr1 = rd.y, wb = rd.z, nwin = rd.w;
-  const uint64_t P0 = w.lcs[cr0], P1 = w.lcs[cr1], P0a = P0 & ~3ull;
-  // the first windows' loads, before anything else
+  const uint4 rd = w.rdesc[2 * r], re = w.rdesc[2 * r + 1];
+  const uint32_t cr0 = rd.x, cr1 = rd.y, pb = rd.z, np = rd.w;
+  const uint64_t P0 = re.x, P0a = P0 & ~3ull;
+  // the wave's first pieces: descriptors, then their streams (one round trip before them);
+  // dn[j]: the descriptor of the piece that takes slot j next
+  uint2 dq[D], dn[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    const uint32_t k = wave + j * NW, k2 = wave + (D + j) * NW;
+    dq[j] = k < np ? w.pdesc[pb + k] : make_uint2(0, 0);
+    dn[j] = k2 < np ? w.pdesc[pb + k2] : make_uint2(0, 0);
+  }
   WinCols<B32, SEW> q[D];
 #pragma unroll
-  for (int j = 0; j < D; ++j) win_load<B32, SEW>(a, w, inst, wb, nwin, P0, P1, P0a, wave + j * NW, lane, q[j]);
+  for (int j = 0; j < D; ++j)
+    if (wave + j * NW < np) win_load<B32, SEW>(a, w, inst, dq[j], lane, q[j]);
   const WinLds L = win_lds(lds_dyn, w);
   const uint32_t ncr = cr1 - cr0;
-  for (uint32_t i = tid; i < w.lds_vw; i += NT) L.vb[i] = 0;
-  for (uint32_t i = tid; i < ncr; i += NT) L.tot[i] = 0;
   const uint64_t gb = inst * a.natt;
   const uint4* lci = w.lci + inst * (w.nlc + 1);
+  const uint64_t pbeg = a.boffs[gb], pend = a.boffs[gb + a.natt], lb = a.boffs[gb + a.natt - 1];
+  const uint64_t pbase = pbeg & ~15ull, lbase = lb & ~15ull;
   const uint32_t k0 = lci[cr0].w, nk = lci[cr1].w - k0;  // the range's attestations: catt[k0, k0 + nk)
+  for (uint32_t i = tid; i < w.lds_vw; i += NT) L.vb[i] = 0;
+  for (uint32_t i = tid; i < ncr; i += NT) L.tot[i] = 0;
   for (uint32_t i = tid; i < nk; i += NT) L.vot[i] = 0;
   // the range's committees: starts, attestation kinds, their catt index and bitfields
   for (uint32_t c = cr0 + tid; c <= cr1; c += NT) {
     const uint4 ci = lci[c];
+    const uint32_t cs = w.lcs[c];
+    const uint32_t nb = c < cr1 ? w.lnb[inst * w.nlc + c] : 0;
     const uint32_t cl = c - cr0;
-    L.cst[cl] = (uint32_t)(w.lcs[c] - P0a);
+    L.cst[cl] = (uint32_t)(cs - P0a);
     L.kbg[cl] = ci.w;
     if (c < cr1) {
       L.kd[cl] = ci.z == kNoAtt ? 0 : ci.z == kManyAtt ? 2 : 1;
       L.cbo[cl] = pk64(ci.x, ci.y);
-      L.cnb[cl] = w.lnb[inst * w.nlc + c];
+      L.cnb[cl] = nb;
     }
   }
-  // every bitfield's bits (the last one copied into LDS on the way), and their lengths
-  const uint64_t pbeg = a.boffs[gb], pend = a.boffs[gb + a.natt], lb = a.boffs[gb + a.natt - 1];
-  const uint64_t pbase = pbeg & ~15ull, lbase = lb & ~15ull;
+  // every bitfield's bits (the last one copied into LDS on the way) and every attestation's
+  // length check, a round's loads of both issued together
   uint64_t pop = 0, err = 0;
-  {
+  if (!(AB & 2)) {
     const uint64_t nch = (pend - pbase + 15) / 16;
-    constexpr int U = 8;
-    for (uint64_t c0 = tid; c0 < nch; c0 += (uint64_t)U * NT) {
+    constexpr int U = 4, UC = 4;  // (U = 8 spills at 1024 threads)
+    for (uint64_t c0 = tid, g0 = tid; c0 < nch || g0 < a.natt; c0 += (uint64_t)U * NT, g0 += (uint64_t)UC * NT) {
       uint4 x[U];
+      uint32_t csz[UC];
+      uint64_t bo0[UC], bo1[UC];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint64_t c = c0 + (uint64_t)u * NT;
         x[u] = c < nch ? *reinterpret_cast<const uint4*>(a.bits + pbase + 16 * c) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < UC; ++u) {
+        const uint64_t g = g0 + (uint64_t)u * NT;
+        const bool in = g < a.natt;
+        csz[u] = in ? w.att_csize[gb + g] : 0u;
+        bo0[u] = in ? a.boffs[gb + g] : 0;
+        bo1[u] = in ? a.boffs[gb + g + 1] : 0;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -223,14 +267,17 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
         }
         if (LLB && ad >= lbase) *reinterpret_cast<uint4*>(L.lbf + (ad - lbase)) = x[u];
       }
+      // the crosslink bitfield-length panic (core.go:538-541): a committee longer than its bitfield
+#pragma unroll
+      for (int u = 0; u < UC; ++u)
+        if ((uint64_t)csz[u] > 8 * (bo1[u] - bo0[u])) err = 1;
     }
-    // the crosslink bitfield-length panic (core.go:538-541): a committee longer than its bitfield
-    for (uint32_t g = tid; g < a.natt; g += NT)
-      if ((uint64_t)w.att_csize[gb + g] > 8 * (a.boffs[gb + g + 1] - a.boffs[gb + g])) err = 1;
+  } else {
+    pop = tid == 0 ? a.total_deposit[inst] : 0;  // (ablation: the threshold holds)
   }
   __syncthreads();  // the committee table is in LDS, the vote bits zeroed
   // the vote bits: (committee, 32-bit word) items, every load of a round in flight together
-  {
+  if (!(AB & 8)) {
     const uint32_t wpc = w.wpc, items = ncr * wpc;
     constexpr int U = 4;
     for (uint32_t t0 = tid; t0 < items; t0 += U * NT) {
@@ -267,6 +314,9 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   pop = 0, err = 0;
 #pragma unroll
   for (int k = 0; k < NW; ++k) pop += red[k][0], err += red[k][1];
+#ifdef PZ_AB_BUILD
+  if (w.trace && tid == 0) w.trace[4ull * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
   const uint64_t lastL = pend - lb;
   const bool rwd_err = (a.nval_global - 1) >= 8 * lastL;  // CheckBit(last, N-1) panics (incentives.go:23)
   const bool thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (a.total_deposit[inst] * 2ull);  // incentives.go:18-20
@@ -276,82 +326,93 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   const uint64_t d = a.dynasty[inst];
   const uint64_t bbase = B32 ? w.bal32_base[inst] : 0;
   const uint8_t* lbf8 = LLB ? L.lbf + (lb - lbase) : a.bits + lb;
-  uint32_t* Bal32 = B32 ? w.bal32 + inst * w.vstride : nullptr;
   uint64_t* Bal = a.balance + inst * w.vstride;
   uint64_t sum = 0, nm = 0;
-  for (uint32_t k = wave; k < nwin; k += D * NW) {
+  for (uint32_t k = wave; k < np; k += D * NW) {
 #pragma unroll
     for (int j = 0; j < D; ++j) {
       const uint32_t kk = k + j * NW;
-      if (kk >= nwin) break;  // (wave-uniform)
+      if (kk >= np) break;  // (wave-uniform)
       const WinCols<B32, SEW>& x = q[j];
-      const uint64_t p = P0a + 256ull * kk + 4ull * lane;
-      const uint32_t loc = (uint32_t)(p - P0a);
+      const uint32_t s0 = rfl(pc_start(dq[j])), cnt = rfl(pc_count(dq[j])), cl = rfl(pc_comm(dq[j])) - cr0;
+      const uint64_t pa = s0 & ~3ull, p = pa + 4ull * lane;
+      const uint32_t kind = rfl(L.kd[cl]), kb = rfl(L.kbg[cl]);  // (LDS, issued early)
+      const uint32_t vloc = (uint32_t)(p - P0a);
       bool v[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = p + i >= P0 && p + i < P1;
+      for (int i = 0; i < 4; ++i) v[i] = p + i >= s0 && p + i < (uint64_t)s0 + cnt;
+      uint32_t o4[4] = {0, 0, 0, 0};
       uint64_t b[4];
       if (B32) {  // u64 balance = base + offset (mod 2^64)
-        b[0] = bbase + x.b[0].x, b[1] = bbase + x.b[0].y, b[2] = bbase + x.b[0].z, b[3] = bbase + x.b[0].w;
+        o4[0] = x.b[0].x, o4[1] = x.b[0].y, o4[2] = x.b[0].z, o4[3] = x.b[0].w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b[i] = bbase + o4[i];
       } else {
         b[0] = pk64(x.b[0].x, x.b[0].y), b[1] = pk64(x.b[0].z, x.b[0].w);
         b[2] = pk64(x.b[B32 ? 0 : 1].x, x.b[B32 ? 0 : 1].y), b[3] = pk64(x.b[B32 ? 0 : 1].z, x.b[B32 ? 0 : 1].w);
       }
-      // the reward bits first: their lookups (LDS or L2) overlap the tallies
+      // the reward bits first: their LDS lookups overlap the tallies
       uint32_t rb[4] = {0, 0, 0, 0};
-      if (applied) {
+      if (applied && !(AB & 4)) {
         const uint32_t c4[4] = {x.ci.x, x.ci.y, x.ci.z, x.ci.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const uint32_t ix = v[i] ? c4[i] : 0u;  // (a position outside the range looks bit 0 up)
+          const uint32_t ix = v[i] ? c4[i] : 0u;  // (a position outside the piece looks bit 0 up)
           rb[i] = lbf8[ix >> 3] >> (7 - (ix & 7));
         }
       }
-      // crosslink tallies on the pre-reward balances: one segment per committee in the window
-      {
-        const uint32_t vw = (L.vb[loc >> 5] >> (loc & 31)) & 0xFu;
-        const uint32_t wend = 256 * kk + 256;
-        uint32_t c = rfl(x.c0);
-        for (;;) {
-          const uint32_t cl = c - cr0;
-          const uint32_t s_lo = rfl(L.cst[cl]), s_hi = rfl(L.cst[cl + 1]), kind = rfl(L.kd[cl]);
-          if (kind) {
-            uint64_t t = 0, vv = 0;
+      // crosslink tallies of the piece's committee on the pre-reward balances (core.go:533-545)
+      if (kind && !(AB & 1)) {
+        const uint32_t vw = (L.vb[vloc >> 5] >> (vloc & 31)) & 0xFu;
+        uint64_t T, V;
+        if (B32) {
+          // offsets split 17 | 15 bits: low parts with the count in bits 23+ (<= 256 x 2^15 < 2^23,
+          // <= 256 positions), high parts (<= 256 x 2^17 < 2^25): four 32-bit sums, exact
+          uint32_t at = 0, ht = 0, av = 0, hv = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t lo = (o4[i] & 0x7FFFu) | (1u << 23), hi = o4[i] >> 15;
+            const bool vt = v[i] && ((vw >> i) & 1);
+            at += v[i] ? lo : 0;
+            ht += v[i] ? hi : 0;
+            av += vt ? lo : 0;
+            hv += vt ? hi : 0;
+          }
+          at = wsum32(at), ht = wsum32(ht), av = wsum32(av), hv = wsum32(hv);
+          T = (uint64_t)(at >> 23) * bbase + (at & 0x7FFFFFu) + ((uint64_t)ht << 15);
+          V = (uint64_t)(av >> 23) * bbase + (av & 0x7FFFFFu) + ((uint64_t)hv << 15);
+        } else {
+          uint64_t t = 0, vv = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            t += v[i] ? b[i] : 0;
+            vv += (v[i] && ((vw >> i) & 1)) ? b[i] : 0;
+          }
+          T = wsum64_dpp(t);
+          V = wsum64_dpp(vv);
+        }
+        if (kind == 1) {
+          if (lane == 0) {
+            if (T) atomicAdd((unsigned long long*)&L.tot[cl], (unsigned long long)T);
+            if (V) atomicAdd((unsigned long long*)&L.vot[kb - k0], (unsigned long long)V);
+          }
+        } else {  // several attestations: each one's bits from its bitfield in global memory
+          if (lane == 0 && T) atomicAdd((unsigned long long*)&L.tot[cl], (unsigned long long)T);
+          const uint32_t ke = rfl(L.kbg[cl + 1]), cs = rfl(L.cst[cl]);
+          for (uint32_t kq = kb; kq < ke; ++kq) {
+            const uint64_t ga = w.catt[gb + kq];
+            const uint64_t bo = a.boffs[gb + ga], nb = 8 * (a.boffs[gb + ga + 1] - bo);
+            uint64_t s = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const bool in = v[i] && loc + i >= s_lo && loc + i < s_hi;
-              t += in ? b[i] : 0;
-              vv += (in && ((vw >> i) & 1)) ? b[i] : 0;
+              const uint64_t xb = (uint64_t)(vloc + i) - cs;  // the position's bit in the bitfield
+              const bool in = v[i] && xb < nb;
+              const uint32_t by = in ? a.bits[bo + (xb >> 3)] : 0u;
+              s += (in && ((by >> (7 - (uint32_t)(xb & 7))) & 1)) ? b[i] : 0;
             }
-            t = wsum64_dpp(t);
-            const uint32_t kb = rfl(L.kbg[cl]);
-            if (kind == 1) {
-              vv = wsum64_dpp(vv);
-              if (lane == 0) {
-                if (t) atomicAdd((unsigned long long*)&L.tot[cl], (unsigned long long)t);
-                if (vv) atomicAdd((unsigned long long*)&L.vot[kb - k0], (unsigned long long)vv);
-              }
-            } else {  // several attestations: each one's bits from its bitfield in global memory
-              if (lane == 0 && t) atomicAdd((unsigned long long*)&L.tot[cl], (unsigned long long)t);
-              const uint32_t ke = rfl(L.kbg[cl + 1]);
-              for (uint32_t kq = kb; kq < ke; ++kq) {
-                const uint64_t ga = w.catt[gb + kq];
-                const uint64_t bo = a.boffs[gb + ga], nb = 8 * (a.boffs[gb + ga + 1] - bo);
-                uint64_t s = 0;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                  const uint64_t xb = (uint64_t)(loc + i) - s_lo;  // the position's bit in the bitfield
-                  const bool in = v[i] && loc + i >= s_lo && loc + i < s_hi && xb < nb;
-                  const uint32_t by = in ? a.bits[bo + (xb >> 3)] : 0u;
-                  s += (in && ((by >> (7 - (uint32_t)(xb & 7))) & 1)) ? b[i] : 0;
-                }
-                s = wsum64_dpp(s);
-                if (lane == 0 && s) atomicAdd((unsigned long long*)&L.vot[kq - k0], (unsigned long long)s);
-              }
-            }
+            s = wsum64_dpp(s);
+            if (lane == 0 && s) atomicAdd((unsigned long long*)&L.vot[kq - k0], (unsigned long long)s);
           }
-          ++c;
-          if (s_hi >= wend || c >= cr1) break;
         }
       }
       // classify, reward (incentives.go:22-27), store, next-cycle sum (core.go:459-464)
@@ -391,19 +452,25 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) sum += (v[i] && act[i]) ? b[i] : 0;
-      win_load<B32, SEW>(a, w, inst, wb, nwin, P0, P1, P0a, kk + D * NW, lane, q[j]);
+      // slot j's next piece: its stream (descriptor loaded a round ago), and the descriptor after
+      const uint32_t k1 = kk + D * NW, k2 = kk + 2 * D * NW;
+      dq[j] = dn[j];
+      if (k1 < np) win_load<B32, SEW>(a, w, inst, dq[j], lane, q[j]);
+      dn[j] = k2 < np ? w.pdesc[pb + k2] : make_uint2(0, 0);
     }
   }
-  (void)Bal32;
   sum = wsum64_dpp(sum);
   nm = wsum64_dpp(nm);
-  if (lane == 0) red[wave][0] = sum, red[wave][1] = nm;
+  if (lane == 0) red2[wave][0] = sum, red2[wave][1] = nm;
   __syncthreads();  // (also: every wave's LDS tallies are in)
+#ifdef PZ_AB_BUILD
+  if (w.trace && tid == 0) w.trace[4ull * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
   uint64_t* sc = a.scal + inst * kScal;
   if (tid == 0) {
     uint64_t s = 0, n = 0;
 #pragma unroll
-    for (int k = 0; k < NW; ++k) s += red[k][0], n += red[k][1];
+    for (int k = 0; k < NW; ++k) s += red2[k][0], n += red2[k][1];
     if (s && !skip) atomicAdd((unsigned long long*)&sc[kNextBal], (unsigned long long)s);
     if (n) {  // the layout's rank == index premise is broken (the state never allows it)
       atomicAdd((unsigned long long*)&sc[kNoMatch], (unsigned long long)n);
@@ -438,13 +505,20 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       if (3ull * V >= 2ull * T && d > pk64(aw.y, aw.z)) atomicMin(&a.winner[inst * a.nrec + aw.x], ga);
     }
   }
+#ifdef PZ_AB_BUILD
+  if (w.trace) {
+    __syncthreads();
+    if (tid == 0) w.trace[4ull * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
-#define PZ_WINDOW_KERNEL(NAME, B32, SEW, LLB)                                               \
-  extern "C" __global__ void __launch_bounds__(kWinThreads) NAME(EpochArgs a, WinArgs w) { \
-    window_body<B32, SEW, LLB>(a, w);                                                       \
+#define PZ_WINDOW_KERNEL(NAME, B32, SEW, LLB)                                                           \
+  extern "C" __global__ void __launch_bounds__(kWinThreads) NAME(EpochArgs a, WinArgs w) {             \
+    window_body<B32, SEW, LLB, 0, (B32 && SEW == 16) ? kWinDepth16 : kWinDepth>(a, w);                 \
   }
 // balances as u32 offsets / u64; {start, end} at 16 / 32 / 64 bits; the last bitfield in LDS or not
+// (the narrow form has the registers for a deeper prefetch)
 PZ_WINDOW_KERNEL(pz_epoch_window_b32_s16_kernel, true, 16, true)
 PZ_WINDOW_KERNEL(pz_epoch_window_b32_s32_kernel, true, 32, true)
 PZ_WINDOW_KERNEL(pz_epoch_window_b32_s64_kernel, true, 64, true)
@@ -458,6 +532,27 @@ PZ_WINDOW_KERNEL(pz_epoch_window_b64_s16_g_kernel, false, 16, false)
 PZ_WINDOW_KERNEL(pz_epoch_window_b64_s32_g_kernel, false, 32, false)
 PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_g_kernel, false, 64, false)
 #undef PZ_WINDOW_KERNEL
+
+#ifdef PZ_AB_BUILD
+// the A/B library's ablations of the product form (u32 offsets, 16-bit bounds, last bitfield in LDS)
+#define PZ_WINDOW_ABL(X, D)                                                                              \
+  extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_abl##X##_d##D##_kernel(EpochArgs a, \
+                                                                                              WinArgs w) {  \
+    window_body<true, 16, true, X, D>(a, w);                                                               \
+  }
+PZ_WINDOW_ABL(0, 2) PZ_WINDOW_ABL(0, 3) PZ_WINDOW_ABL(0, 4)
+PZ_WINDOW_ABL(1, 3) PZ_WINDOW_ABL(2, 3) PZ_WINDOW_ABL(4, 3) PZ_WINDOW_ABL(8, 3) PZ_WINDOW_ABL(15, 3)
+#undef PZ_WINDOW_ABL
+static int g_window_ablation = 0;
+static uint64_t* g_window_trace = nullptr;
+extern "C" int pz_debug_set_window_ablation(int x) {
+  const int old = g_window_ablation;
+  g_window_ablation = x;
+  return old;
+}
+// the next launches stamp [blocks][4] {start, prologue done, loop done, end} into d_trace
+extern "C" void pz_debug_set_window_trace(uint64_t* d_trace) { g_window_trace = d_trace; }
+#endif
 
 hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t s) {
   if (!a.ninst || !w.R) return hipSuccess;
@@ -476,12 +571,34 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
     else PZ_PICK(b64, 64);
   }
 #undef PZ_PICK
+#ifdef PZ_AB_BUILD
+  if (g_window_ablation && b32 && sew == 16 && llb) {
+    switch (g_window_ablation) {  // ablation bits | prefetch depth << 8
+      case 2 << 8: k = (const void*)pz_epoch_window_abl0_d2_kernel; break;
+      case 3 << 8: k = (const void*)pz_epoch_window_abl0_d3_kernel; break;
+      case 4 << 8: k = (const void*)pz_epoch_window_abl0_d4_kernel; break;
+      case 1: k = (const void*)pz_epoch_window_abl1_d3_kernel; break;
+      case 2: k = (const void*)pz_epoch_window_abl2_d3_kernel; break;
+      case 4: k = (const void*)pz_epoch_window_abl4_d3_kernel; break;
+      case 8: k = (const void*)pz_epoch_window_abl8_d3_kernel; break;
+      case 15: k = (const void*)pz_epoch_window_abl15_d3_kernel; break;
+      default: return hipErrorInvalidValue;
+    }
+  }
+#endif
+#ifdef PZ_AB_BUILD
+  WinArgs wt = w;
+  wt.trace = g_window_trace;
+  const WinArgs& wl = wt;
+#else
+  const WinArgs& wl = w;
+#endif
   const size_t lds = window_lds_bytes(w);
   if (lds > 48 * 1024) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  void* args[] = {const_cast<EpochArgs*>(&a), const_cast<WinArgs*>(&w)};
+  void* args[] = {const_cast<EpochArgs*>(&a), const_cast<WinArgs*>(&wl)};
   return hipLaunchKernel(k, dim3(a.ninst * w.R), dim3(kWinThreads), args, lds, s);
 }
 

@@ -89,6 +89,26 @@ def test_half_wave_path_limits(field_num):
     assert any(len(r) > 768 for r in want) and any(len(r) <= 768 for r in want)
 
 
+def test_mixed_paths_across_many_waves():
+    """Row-path and whole-wave records of every size class shuffled over ~2,000 waves: each
+    wave's output offset comes from the look-back over its predecessors (wire_att.hip)."""
+    rng = np.random.default_rng(23)
+    atts = []
+    for _ in range(8000):
+        kind = int(rng.integers(0, 4))
+        nob = (0, 9, 14, 40)[kind]
+        atts.append(pb.AttestationRecord(
+            slot=rand_u64(rng), shard_id=int(rng.integers(0, 1 << 20)), justified_slot=int(rng.integers(0, 2)),
+            justified_block_hash=rand_bytes(rng, 0, 33), shard_block_hash=rand_bytes(rng, 32, 33),
+            attester_bitfield=rand_bytes(rng, 0, 70 if kind < 3 else 300),
+            oblique_parent_hashes=[rand_bytes(rng, 0, 33) for _ in range(nob)],
+            aggregate_sig=[rand_u64(rng) for _ in range(int(rng.integers(0, 18)))]))
+    raw, offs = wire.attestations_device(wire.attestation_columns(atts), len(atts), 0)
+    want = [wire.attestation_record(a) for a in atts]
+    assert raw == b"".join(want)
+    assert np.array_equal(np.diff(offs), [len(r) for r in want])
+
+
 def test_empty_batch():
     raw, offs = wire.attestations_device(wire.attestation_columns([]), 0, 0)
     assert raw == b"" and list(offs) == [0]

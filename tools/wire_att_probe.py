@@ -46,15 +46,16 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     dll = _lib.lib.dll
-    if hasattr(dll, "pz_debug_set_att_write_variant"):  # same-process A/B of the write kernel
-        for v in (0, 2, 0, 2, 0):  # size + scan + write / the looped one-pass kernel
+    if hasattr(dll, "pz_debug_set_att_write_variant"):  # same-process A/B (PZ_PROBE_LIB=build/ab/...)
+        for v in (0, 1, 7, 8, 0, 1):  # one pass (6 waves/SIMD) / size + scan + write / one pass capped at 7, 8
             dll.pz_debug_set_att_write_variant(v)
             e0.record()
             for _ in range(reps):
                 run()
             e1.record()
             torch.cuda.synchronize()
-            print("  write variant %d  encode %.3f ms" % (v, e0.elapsed_time(e1) / reps), flush=True)
+            ok_v = bool(np.array_equal(out[:n * 512].cpu().numpy(), synth.attestation_records_512(n, seed=2).reshape(-1)))
+            print("  variant %d  encode %.3f ms  parity=%s" % (v, e0.elapsed_time(e1) / reps, ok_v), flush=True)
         dll.pz_debug_set_att_write_variant(0)
         run()
     # the CSR hash kernel over the encoded records (the encode + hash leg's second launch)
