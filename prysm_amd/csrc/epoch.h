@@ -153,7 +153,7 @@ struct FusedArgs {
 // ---- the window pass (epoch_window.hip): the one-pass step of B instances in ONE launch ------
 // Block (instance, range): a range is a run of this rank's committees (local ids [cr0, cr1),
 // positions [lcs[cr0], lcs[cr1])), so every committee's tallies complete inside one block.
-constexpr int kWinThreads = 1024, kWinDepth = 2, kWinDepth16 = 3;  // (pieces in flight per wave)
+constexpr int kWinThreads = 1024, kWinDepth = 2, kWinDepth16 = 2;  // (pieces in flight per wave: 3 measured slower, r5f)
 struct WinArgs {
   const uint4* rdesc;         // [R][2] {cr0, cr1, first piece (pdesc index), pieces}, {P0, P1, 0, 0}
   uint32_t R;                 // ranges per instance (grid: B x R blocks)
@@ -180,7 +180,14 @@ struct WinArgs {
   // attestations of a range, 32-bit words per committee bitfield (the vote-bit placement's items)
   uint32_t lds_lbf, lds_vw, lds_maxc, lds_maxk, wpc;
   uint64_t* trace;            // A/B library only: [blocks][4] phase stamps (s_memrealtime), else NULL
+  // R > 1: the R blocks of an instance each count 1/R of its bitfields and meet in one 64-bit
+  // word per instance, {arrivals << 48 | length-panic blocks << 39 | bits}, this step's pacc and
+  // the next step's pacc_next (zeroed by the r == 0 blocks; the two swap every step).  A block
+  // whose partners have not all arrived within kCoopSpinTicks counts everything itself.
+  uint64_t* pacc;
+  uint64_t* pacc_next;
 };
+constexpr uint64_t kCoopSpinTicks = 5000;  // s_memrealtime ticks (100 MHz): 50 us
 size_t window_lds_bytes(const WinArgs& w);
 hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t s);
 

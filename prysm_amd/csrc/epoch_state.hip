@@ -275,6 +275,7 @@ void flip(pz_epoch_state* st) {
       if (q.window) {
         q.win_results = q.a.winner;
         std::swap(q.a.winner, q.w.winner_next);
+        std::swap(q.w.pacc, q.w.pacc_next);  // (the step just enqueued zeroed pacc_next)
       }
       const uint64_t Bp = q.B, natt = st->natt;
       q.a.scal = q.red[q.cur];
@@ -631,17 +632,28 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
     if (R >= nlc) return fail(PZ_EINVAL, "window pass: no range split fits the LDS");
     R = std::min<uint32_t>(nlc, 2 * R);
   }
-  if (pdesc.empty()) pdesc.push_back(make_uint2(0, 0));
+  pdesc.push_back(make_uint2(0, 0));  // (an empty last range's first descriptor load stays in bounds)
   uint4 *d_rdesc = nullptr, *d_lci = nullptr, *d_aw = nullptr;
   uint2* d_pdesc = nullptr;
   uint32_t *d_lcs = nullptr, *d_lnb = nullptr, *d_csz = nullptr, *d_wn = nullptr;
+  uint64_t* d_pacc = nullptr;
   int rc;
   if ((rc = upload(s, &d_rdesc, rdesc.data(), rdesc.size())) || (rc = upload(s, &d_pdesc, pdesc.data(), pdesc.size())) ||
       (rc = upload(s, &d_lcs, lcs.data(), lcs.size())) || (rc = upload(s, &d_lci, lci.data(), lci.size())) ||
       (rc = upload(s, &d_lnb, lnb.data(), lnb.size())) || (rc = upload(s, &d_csz, csz.data(), csz.size())) ||
       (rc = upload(s, &d_aw, aw.data(), aw.size())) ||
-      (rc = dalloc(s, &d_wn, (size_t)Bp * std::max<uint32_t>(st->nrec, 1))))
+      (rc = dalloc(s, &d_wn, (size_t)Bp * std::max<uint32_t>(st->nrec, 1))) || (rc = dalloc(s, &d_pacc, 2 * (size_t)Bp)))
     return rc;
+  // the meeting word's fields (epoch.h WinArgs.pacc): bits below 2^39, at most 511 blocks
+  bool meet = R > 1 && R <= 511;
+  for (uint64_t b = 0; b < Bp && meet; ++b) {
+    const uint64_t gb = (i0 + b) * natt;
+    meet = 8 * (h->boffs[gb + natt] - h->boffs[gb]) < (1ull << 39);
+  }
+  if (meet) {
+    w.pacc = d_pacc;
+    w.pacc_next = d_pacc + Bp;
+  }
   w.rdesc = d_rdesc;
   w.pdesc = d_pdesc;
   w.lcs = d_lcs;

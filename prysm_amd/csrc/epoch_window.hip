@@ -77,45 +77,54 @@ __device__ __forceinline__ uint32_t pc_start(uint2 d) { return d.x; }
 __device__ __forceinline__ uint32_t pc_count(uint2 d) { return d.y & 511u; }
 __device__ __forceinline__ uint32_t pc_comm(uint2 d) { return d.y >> 9; }
 
+// The instance's columns (wave-uniform bases: the loads take a 32-bit per-lane offset)
+struct WinCol {
+  const uint32_t* bal32;
+  const uint64_t* bal;
+  const uint32_t* se16;
+  const uint2* se;
+  const uint64_t* start;
+  const uint64_t* end;
+  const uint32_t* ci;
+};
+
 template <bool B32, int SEW>
-__device__ __forceinline__ void win_load(const EpochArgs& a, const WinArgs& w, uint64_t inst, uint2 d, int lane,
-                                         WinCols<B32, SEW>& x) {
-  const uint64_t s0 = pc_start(d), pa = s0 & ~3ull, p = pa + 4ull * lane;
+__device__ __forceinline__ void win_load(const WinCol& c, uint2 d, uint32_t lane, WinCols<B32, SEW>& x) {
+  const uint32_t s0 = pc_start(d), pa = s0 & ~3u, p = pa + 4 * lane;
   const bool any = p + 3 >= s0 && p < s0 + pc_count(d);
-  const uint64_t pp = any ? p : pa;  // (a lane wholly outside the piece re-reads the first quad)
-  const uint64_t row = inst * w.vstride + pp;
+  const uint32_t pp = any ? p : pa;  // (a lane wholly outside the piece re-reads the first quad)
   if (B32) {
-    x.b[0] = *reinterpret_cast<const uint4*>(w.bal32 + row);
+    x.b[0] = *reinterpret_cast<const uint4*>(c.bal32 + pp);
   } else {
-    x.b[0] = *reinterpret_cast<const uint4*>(a.balance + row);
-    x.b[B32 ? 0 : 1] = *reinterpret_cast<const uint4*>(a.balance + row + 2);
+    x.b[0] = *reinterpret_cast<const uint4*>(c.bal + pp);
+    x.b[B32 ? 0 : 1] = *reinterpret_cast<const uint4*>(c.bal + pp + 2);
   }
   // the bounds are read once per step: nontemporal, leaving the Infinity Cache to the balances
   if (SEW == 16) {
-    x.s[0] = ldnt16(w.se16 + row);
+    x.s[0] = ldnt16(c.se16 + pp);
   } else if (SEW == 32) {
-    x.s[0] = ldnt16(w.se + row);
-    x.s[SEW == 32 ? 1 : 0] = ldnt16(w.se + row + 2);
+    x.s[0] = ldnt16(c.se + pp);
+    x.s[SEW == 32 ? 1 : 0] = ldnt16(c.se + pp + 2);
   } else {
-    x.s[0] = ldnt16(a.start + row);
-    x.s[SEW == 64 ? 1 : 0] = ldnt16(a.start + row + 2);
-    x.s[SEW == 64 ? 2 : 0] = ldnt16(a.end + row);
-    x.s[SEW == 64 ? 3 : 0] = ldnt16(a.end + row + 2);
+    x.s[0] = ldnt16(c.start + pp);
+    x.s[SEW == 64 ? 1 : 0] = ldnt16(c.start + pp + 2);
+    x.s[SEW == 64 ? 2 : 0] = ldnt16(c.end + pp);
+    x.s[SEW == 64 ? 3 : 0] = ldnt16(c.end + pp + 2);
   }
-  x.ci = *reinterpret_cast<const uint4*>(a.co_index + pp);
+  x.ci = *reinterpret_cast<const uint4*>(c.ci + pp);
 }
 
 // validator.go:45-53 on position i of the lane's quad (the saturated bounds classify exactly:
 // the host takes the 16- / 32-bit columns only when every CurrentDynasty is below them)
 template <bool B32, int SEW>
-__device__ __forceinline__ bool win_active(const WinCols<B32, SEW>& x, int i, uint64_t d) {
-  if (SEW == 16) {
+__device__ __forceinline__ bool win_active(const WinCols<B32, SEW>& x, int i, uint32_t d32, uint64_t d) {
+  if (SEW == 16) {  // (then every CurrentDynasty < 0xFFFF: 32-bit compares are exact)
     const uint32_t s4[4] = {x.s[0].x, x.s[0].y, x.s[0].z, x.s[0].w};
-    return (uint64_t)(s4[i] & 0xFFFFu) <= d && d < (uint64_t)(s4[i] >> 16);
-  } else if (SEW == 32) {
+    return (s4[i] & 0xFFFFu) <= d32 && d32 < (s4[i] >> 16);
+  } else if (SEW == 32) {  // (every CurrentDynasty < 2^32 - 1)
     const uint4 q = x.s[i >> 1];
     const uint32_t lo = (i & 1) ? q.z : q.x, hi = (i & 1) ? q.w : q.y;
-    return (uint64_t)lo <= d && d < (uint64_t)hi;
+    return lo <= d32 && d32 < hi;
   } else {
     const uint4 qs = x.s[i >> 1], qe = x.s[SEW == 64 ? 2 + (i >> 1) : 0];
     const uint64_t s = (i & 1) ? pk64(qs.z, qs.w) : pk64(qs.x, qs.y);
@@ -167,37 +176,51 @@ size_t window_lds_bytes(const WinArgs& w) {
          w.lds_maxc + 16;
 }
 
-// AB: measurement ablations, instantiated only in the A/B library (results wrong for AB != 0):
-// 1 no crosslink tallies, 2 no bit count / length checks in the prologue (applied taken as
-// true), 4 no reward-bit lookups, 8 no vote-bit placement.
-template <bool B32, int SEW, bool LLB, int AB = 0, int D = kWinDepth>
+// AB: measurement ablations, instantiated only in the A/B library (results wrong for AB != 0
+// except 16): 1 no crosslink tallies, 2 no bit count / length checks in the prologue (applied
+// taken as true), 4 no reward-bit lookups, 8 no vote-bit placement, 16 every block counts
+// everything (no meeting of the R blocks; exact), 32 the meeting's wait bound at zero (the
+// fallback count in every block that arrives before its partners; exact), 64 the first pieces'
+// loads issued after the prologue (exact), 80 = 64 + 16.
+template <bool B32, int SEW, bool LLB, int AB = 0, int D = kWinDepth, bool TR = false>
 __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w) {
   extern __shared__ __align__(16) uint8_t lds_dyn[];
   constexpr int NT = kWinThreads, NW = NT / 64;
   __shared__ uint64_t red[NW][2], red2[NW][2];  // (the prologue's and the loop's: no barrier between their uses)
+  __shared__ uint64_t tstamp[TR ? 4 : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = rfl(tid >> 6);
-#ifdef PZ_AB_BUILD
-  if (w.trace && tid == 0) w.trace[4ull * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-#endif
+  if (TR && tid == 0) tstamp[0] = __builtin_amdgcn_s_memrealtime();
   const uint64_t inst = blockIdx.x / w.R;
   const uint32_t r = blockIdx.x - (uint32_t)inst * w.R;
   const uint4 rd = w.rdesc[2 * r], re = w.rdesc[2 * r + 1];
   const uint32_t cr0 = rd.x, cr1 = rd.y, pb = rd.z, np = rd.w;
   const uint64_t P0 = re.x, P0a = P0 & ~3ull;
-  // the wave's first pieces: descriptors, then their streams (one round trip before them);
-  // dn[j]: the descriptor of the piece that takes slot j next
-  uint2 dq[D], dn[D];
+  // The wave's pieces go round by round, slot j of round t being piece t * D * NW + j * NW +
+  // wave; past the range's end a slot takes a dummy (the last piece's descriptor with no
+  // positions), so every load below is issued unconditionally and the loop's waits count
+  // exactly the loads in flight.  Lane l loads the descriptor of slot l % D: one load a round.
+  const uint32_t npm = np ? np - 1 : 0, nround = (np + D * NW - 1) / (D * NW);
+  const uint32_t dslot = wave + (uint32_t)(lane % D) * NW;
+  auto desc = [&](uint32_t rnd) {  // this lane's slot's descriptor for round rnd
+    const uint32_t k = rnd * D * NW + dslot;
+    uint2 x = w.pdesc[pb + min(k, npm)];
+    if (k >= np) x.y &= ~511u;  // (a dummy: no positions)
+    return x;
+  };
+  uint2 dv = desc(0);
+  uint2 dq[D];
 #pragma unroll
-  for (int j = 0; j < D; ++j) {
-    const uint32_t k = wave + j * NW, k2 = wave + (D + j) * NW;
-    dq[j] = k < np ? w.pdesc[pb + k] : make_uint2(0, 0);
-    dn[j] = k2 < np ? w.pdesc[pb + k2] : make_uint2(0, 0);
-  }
+  for (int j = 0; j < D; ++j) dq[j] = make_uint2(__builtin_amdgcn_readlane(dv.x, j), __builtin_amdgcn_readlane(dv.y, j));
+  const uint64_t vrow = inst * w.vstride;
+  const WinCol col{w.bal32 + vrow, a.balance + vrow, w.se16 + vrow, w.se + vrow, a.start + vrow, a.end + vrow,
+                   a.co_index};
   WinCols<B32, SEW> q[D];
+  if (!(AB & 64)) {
 #pragma unroll
-  for (int j = 0; j < D; ++j)
-    if (wave + j * NW < np) win_load<B32, SEW>(a, w, inst, dq[j], lane, q[j]);
+    for (int j = 0; j < D; ++j) win_load<B32, SEW>(col, dq[j], lane, q[j]);
+  }
+  dv = desc(1);
   const WinLds L = win_lds(lds_dyn, w);
   const uint32_t ncr = cr1 - cr0;
   const uint64_t gb = inst * a.natt;
@@ -222,86 +245,114 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       L.cnb[cl] = nb;
     }
   }
-  // every bitfield's bits (the last one copied into LDS on the way) and every attestation's
-  // length check, a round's loads of both issued together
+  // GetAttestersTotalDeposit (every bitfield's bits) and the bitfield-length panics.  The
+  // region's 16-B chunks [0, nch) from pbase; the last bitfield's, [clb, nch), go into LDS by
+  // DMA (no registers, 1 KiB per wave instruction) and are counted from there.  With R > 1 the
+  // block counts only its share of the chunks and attestations and the R blocks meet in pacc.
   uint64_t pop = 0, err = 0;
-  if (!(AB & 2)) {
-    const uint64_t nch = (pend - pbase + 15) / 16;
+  const uint64_t nch = (pend - pbase + 15) / 16, clb = LLB ? (lbase - pbase) / 16 : nch;
+  const bool coop = w.pacc != nullptr && w.R > 1 && !(AB & 16);
+  const uint64_t s0 = coop ? nch * r / w.R : 0, s1 = coop ? nch * (r + 1) / w.R : nch;
+  const uint64_t g0s = coop ? (uint64_t)a.natt * r / w.R : 0, g1s = coop ? (uint64_t)a.natt * (r + 1) / w.R : a.natt;
+  // bits of chunk c (its bytes inside [pbeg, pend) only)
+  auto chunk_pop = [&](uint64_t c, uint4 x) -> uint32_t {
+    const uint64_t ad = pbase + 16 * c;
+    const uint32_t wd[4] = {x.x, x.y, x.z, x.w};
+    if (ad >= pbeg && ad + 16 <= pend) return __popc(wd[0]) + __popc(wd[1]) + __popc(wd[2]) + __popc(wd[3]);
+    uint32_t n = 0;
+#pragma unroll
+    for (int dd = 0; dd < 4; ++dd) {
+      uint32_t m = 0;
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {
+        const uint64_t at = ad + 4 * dd + bb;
+        if (at >= pbeg && at < pend) m |= 0xFFu << (8 * bb);
+      }
+      n += __popc(wd[dd] & m);
+    }
+    return n;
+  };
+  // chunks [c_lo, c_hi) below the last bitfield and attestations [g_lo, g_hi) from global memory
+  auto count_range = [&](uint64_t c_lo, uint64_t c_hi, uint64_t g_lo, uint64_t g_hi) {
     constexpr int U = 4, UC = 4;  // (U = 8 spills at 1024 threads)
-    for (uint64_t c0 = tid, g0 = tid; c0 < nch || g0 < a.natt; c0 += (uint64_t)U * NT, g0 += (uint64_t)UC * NT) {
+    const uint64_t nc = c_hi > c_lo ? c_hi - c_lo : 0, ng = g_hi - g_lo;
+    const uint64_t nit = std::max<uint64_t>((nc + U * NT - 1) / (U * NT), (ng + UC * NT - 1) / (UC * NT));
+    for (uint64_t it = 0; it < nit; ++it) {  // (uniform: every load issued, past the end clamped)
+      const uint64_t c0 = it * U * NT + tid, gi0 = it * UC * NT + tid;
       uint4 x[U];
       uint32_t csz[UC];
       uint64_t bo0[UC], bo1[UC];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint64_t c = c0 + (uint64_t)u * NT;
-        x[u] = c < nch ? *reinterpret_cast<const uint4*>(a.bits + pbase + 16 * c) : make_uint4(0, 0, 0, 0);
+        const uint64_t c = c_lo + std::min<uint64_t>(c0 + (uint64_t)u * NT, nc ? nc - 1 : 0);
+        x[u] = *reinterpret_cast<const uint4*>(a.bits + pbase + 16 * c);
       }
 #pragma unroll
       for (int u = 0; u < UC; ++u) {
-        const uint64_t g = g0 + (uint64_t)u * NT;
-        const bool in = g < a.natt;
-        csz[u] = in ? w.att_csize[gb + g] : 0u;
-        bo0[u] = in ? a.boffs[gb + g] : 0;
-        bo1[u] = in ? a.boffs[gb + g + 1] : 0;
+        const uint64_t g = g_lo + std::min<uint64_t>(gi0 + (uint64_t)u * NT, ng ? ng - 1 : 0);
+        csz[u] = w.att_csize[gb + g];
+        bo0[u] = a.boffs[gb + g];
+        bo1[u] = a.boffs[gb + g + 1];
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint64_t c = c0 + (uint64_t)u * NT;
-        if (c >= nch) continue;
-        const uint64_t ad = pbase + 16 * c;
-        const uint32_t wd[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
-        if (ad >= pbeg && ad + 16 <= pend) {
-          pop += __popc(wd[0]) + __popc(wd[1]) + __popc(wd[2]) + __popc(wd[3]);
-        } else {  // (the region's two edge chunks: its bytes only)
-#pragma unroll
-          for (int dd = 0; dd < 4; ++dd) {
-            uint32_t m = 0;
-#pragma unroll
-            for (int bb = 0; bb < 4; ++bb) {
-              const uint64_t at = ad + 4 * dd + bb;
-              if (at >= pbeg && at < pend) m |= 0xFFu << (8 * bb);
-            }
-            pop += __popc(wd[dd] & m);
-          }
-        }
-        if (LLB && ad >= lbase) *reinterpret_cast<uint4*>(L.lbf + (ad - lbase)) = x[u];
-      }
+      for (int u = 0; u < U; ++u)
+        if (c0 + (uint64_t)u * NT < nc) pop += chunk_pop(c_lo + c0 + (uint64_t)u * NT, x[u]);
       // the crosslink bitfield-length panic (core.go:538-541): a committee longer than its bitfield
 #pragma unroll
       for (int u = 0; u < UC; ++u)
-        if ((uint64_t)csz[u] > 8 * (bo1[u] - bo0[u])) err = 1;
+        if (gi0 + (uint64_t)u * NT < ng && (uint64_t)csz[u] > 8 * (bo1[u] - bo0[u])) err = 1;
     }
+  };
+  auto count_lds = [&](uint64_t c_lo, uint64_t c_hi) {  // chunks of the last bitfield, from its LDS copy
+    for (uint64_t c = c_lo + tid; c < c_hi; c += NT)
+      pop += chunk_pop(c, *reinterpret_cast<const uint4*>(L.lbf + 16 * (c - clb)));
+  };
+  if (!(AB & 2)) {
+    if (LLB) {
+      typedef __attribute__((address_space(3))) void lds_void_t;
+      typedef const __attribute__((address_space(1))) void gbl_void_t;
+      const uint64_t nl = nch - clb;
+      for (uint64_t c0 = (uint64_t)wave * 64; c0 < nl; c0 += NT) {  // (wave-uniform c0)
+        const uint64_t c = std::min<uint64_t>(c0 + lane, nl - 1);
+        if (c0 + lane < nl)
+          __builtin_amdgcn_global_load_lds((gbl_void_t*)(a.bits + lbase + 16 * c), (lds_void_t*)(L.lbf + 16 * c0), 16, 0,
+                                           0);
+      }
+    }
+    count_range(s0, std::min(s1, clb), g0s, g1s);
   } else {
     pop = tid == 0 ? a.total_deposit[inst] : 0;  // (ablation: the threshold holds)
   }
-  __syncthreads();  // the committee table is in LDS, the vote bits zeroed
+  __syncthreads();  // the committee table and the last bitfield are in LDS, the vote bits zeroed
+  if (!(AB & 2)) count_lds(std::max(s0, clb), s1);
   // the vote bits: (committee, 32-bit word) items, every load of a round in flight together
   if (!(AB & 8)) {
     const uint32_t wpc = w.wpc, items = ncr * wpc;
     constexpr int U = 4;
-    for (uint32_t t0 = tid; t0 < items; t0 += U * NT) {
-      uint64_t raw[U];
-      uint32_t sh8[U];
+    const uint32_t nit = (items + U * NT - 1) / (U * NT);
+    for (uint32_t it = 0; it < nit; ++it) {  // (uniform; the table reads first, then every load)
+      uint32_t cst[U], nbl[U];
+      uint64_t ad[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t t = t0 + u * NT, cl = t / wpc, m = t - cl * wpc;
+        const uint32_t t = it * U * NT + u * NT + tid, cl = min(t, items - 1) / wpc, m = t - cl * wpc;
         const bool ok = t < items && L.kd[cl] == 1 && 32 * m < L.cnb[cl];
-        const uint64_t ad = (ok ? L.cbo[cl] : 0) + 4 * m, da = ad & ~3ull;
-        sh8[u] = (uint32_t)(ad - da) * 8;
-        raw[u] = 0;
-        if (ok) __builtin_memcpy(&raw[u], __builtin_assume_aligned(a.bits + da, 4), 8);  // (buffer padded by 16 B)
+        nbl[u] = ok ? L.cnb[cl] - 32 * m : 0;
+        cst[u] = L.cst[cl] + 32 * m;
+        ad[u] = ok ? L.cbo[cl] + 4 * m : 0;  // (not taken: the buffer's first word)
       }
+      uint64_t raw[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        __builtin_memcpy(&raw[u], __builtin_assume_aligned(a.bits + (ad[u] & ~3ull), 4), 8);  // (buffer padded by 16 B)
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t t = t0 + u * NT, cl = t / wpc, m = t - cl * wpc;
-        if (!(t < items && L.kd[cl] == 1 && 32 * m < L.cnb[cl])) continue;
+        if (!nbl[u]) continue;
         // bitfield bit j is bit 7 - j % 8 of byte j / 8 (CheckBit, utils/checkbit.go:4-12):
         // byte-order kept, bits reversed within each byte -> bit j of the word
-        uint32_t W = __builtin_bitreverse32(__builtin_bswap32((uint32_t)(raw[u] >> sh8[u])));
-        const uint32_t left = L.cnb[cl] - 32 * m;
-        if (left < 32) W &= (1u << left) - 1u;
-        const uint32_t o = L.cst[cl] + 32 * m, sh = o & 31;
+        uint32_t W = __builtin_bitreverse32(__builtin_bswap32((uint32_t)(raw[u] >> ((ad[u] & 3) * 8))));
+        if (nbl[u] < 32) W &= (1u << nbl[u]) - 1u;
+        const uint32_t o = cst[u], sh = o & 31;
         atomicOr(&L.vb[o >> 5], W << sh);
         if (sh) atomicOr(&L.vb[(o >> 5) + 1], W >> (32 - sh));
       }
@@ -314,9 +365,45 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   pop = 0, err = 0;
 #pragma unroll
   for (int k = 0; k < NW; ++k) pop += red[k][0], err += red[k][1];
-#ifdef PZ_AB_BUILD
-  if (w.trace && tid == 0) w.trace[4ull * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
+  if (coop && !(AB & 2)) {
+    // the instance's R blocks meet: one atomic adds this block's share, then thread 0 polls the
+    // word (at the coherence point) until all R have arrived, or the bound passes and the block
+    // counts everything itself (so no block ever depends on another being resident)
+    __shared__ uint64_t s_meet;
+    if (tid == 0) {
+      const uint64_t add = (1ull << 48) | (err ? 1ull << 39 : 0) | pop;
+      uint64_t v = atomicAdd((unsigned long long*)&w.pacc[inst], (unsigned long long)add) + add;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while ((v >> 48) < w.R && __builtin_amdgcn_s_memrealtime() - t0 < ((AB & 32) ? 0 : kCoopSpinTicks)) {
+        __builtin_amdgcn_s_sleep(2);
+        v = __hip_atomic_fetch_add(&w.pacc[inst], (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      s_meet = v;
+    }
+    __syncthreads();
+    const uint64_t v = s_meet;
+    if ((v >> 48) >= w.R) {
+      pop = v & ((1ull << 39) - 1);
+      err = (v >> 39) & 511;
+    } else {  // (a partner not resident in time: the whole count here)
+      pop = 0, err = 0;
+      count_range(0, clb, 0, a.natt);
+      count_lds(clb, nch);
+      pop = wsum64_dpp(pop);
+      err = wsum64_dpp(err);
+      __syncthreads();
+      if (lane == 0) red[wave][0] = pop, red[wave][1] = err;
+      __syncthreads();
+      pop = 0, err = 0;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) pop += red[k][0], err += red[k][1];
+    }
+  }
+  if (AB & 64) {  // (A/B: the first pieces' loads only now, behind the prologue's)
+#pragma unroll
+    for (int j = 0; j < D; ++j) win_load<B32, SEW>(col, dq[j], lane, q[j]);
+  }
+  if (TR && tid == 0) tstamp[1] = __builtin_amdgcn_s_memrealtime();
   const uint64_t lastL = pend - lb;
   const bool rwd_err = (a.nval_global - 1) >= 8 * lastL;  // CheckBit(last, N-1) panics (incentives.go:23)
   const bool thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (a.total_deposit[inst] * 2ull);  // incentives.go:18-20
@@ -324,29 +411,32 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   const bool skip = ferr != 0 || (thr && rwd_err);  // Go panics: balances stay untouched
   const bool applied = thr && !skip;
   const uint64_t d = a.dynasty[inst];
+  const uint32_t d32 = (uint32_t)std::min<uint64_t>(d, 0xFFFFFFFFull);
   const uint64_t bbase = B32 ? w.bal32_base[inst] : 0;
   const uint8_t* lbf8 = LLB ? L.lbf + (lb - lbase) : a.bits + lb;
-  uint64_t* Bal = a.balance + inst * w.vstride;
-  uint64_t sum = 0, nm = 0;
-  for (uint32_t k = wave; k < np; k += D * NW) {
+  uint64_t* Bal = a.balance + vrow;
+  uint32_t* Bal32 = w.bal32 + vrow;
+  // per lane: the next-cycle sum (B32: of the new offsets, with the active count; base added
+  // at the end), the positions whose bounds do not classify them active
+  uint64_t sum = 0;
+  uint32_t nact = 0, nm = 0;
+  const uint32_t rwd = applied ? 1u : 0u;  // (not applied: the balances stay, offsets +- 0)
+  for (uint32_t t = 0; t < nround; ++t) {
+    const uint2 dnx = dv;     // round t + 1's descriptors (loaded a round ago)
+    dv = desc(t + 2);         // round t + 2's
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-      const uint32_t kk = k + j * NW;
-      if (kk >= np) break;  // (wave-uniform)
       const WinCols<B32, SEW>& x = q[j];
-      const uint32_t s0 = rfl(pc_start(dq[j])), cnt = rfl(pc_count(dq[j])), cl = rfl(pc_comm(dq[j])) - cr0;
-      const uint64_t pa = s0 & ~3ull, p = pa + 4ull * lane;
+      const uint32_t s0 = pc_start(dq[j]), cnt = pc_count(dq[j]), cl = pc_comm(dq[j]) - cr0;
       const uint32_t kind = rfl(L.kd[cl]), kb = rfl(L.kbg[cl]);  // (LDS, issued early)
-      const uint32_t vloc = (uint32_t)(p - P0a);
+      const uint32_t pa = s0 & ~3u, p = pa + 4 * (uint32_t)lane, vloc = p - (uint32_t)P0a;
       bool v[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = p + i >= s0 && p + i < (uint64_t)s0 + cnt;
+      for (int i = 0; i < 4; ++i) v[i] = p + i - s0 < cnt;  // (u32: p + i < s0 wraps high)
       uint32_t o4[4] = {0, 0, 0, 0};
-      uint64_t b[4];
-      if (B32) {  // u64 balance = base + offset (mod 2^64)
+      uint64_t b[4] = {0, 0, 0, 0};
+      if (B32) {
         o4[0] = x.b[0].x, o4[1] = x.b[0].y, o4[2] = x.b[0].z, o4[3] = x.b[0].w;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) b[i] = bbase + o4[i];
       } else {
         b[0] = pk64(x.b[0].x, x.b[0].y), b[1] = pk64(x.b[0].z, x.b[0].w);
         b[2] = pk64(x.b[B32 ? 0 : 1].x, x.b[B32 ? 0 : 1].y), b[3] = pk64(x.b[B32 ? 0 : 1].z, x.b[B32 ? 0 : 1].w);
@@ -382,13 +472,13 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
           T = (uint64_t)(at >> 23) * bbase + (at & 0x7FFFFFu) + ((uint64_t)ht << 15);
           V = (uint64_t)(av >> 23) * bbase + (av & 0x7FFFFFu) + ((uint64_t)hv << 15);
         } else {
-          uint64_t t = 0, vv = 0;
+          uint64_t tt = 0, vv = 0;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            t += v[i] ? b[i] : 0;
+            tt += v[i] ? b[i] : 0;
             vv += (v[i] && ((vw >> i) & 1)) ? b[i] : 0;
           }
-          T = wsum64_dpp(t);
+          T = wsum64_dpp(tt);
           V = wsum64_dpp(vv);
         }
         if (kind == 1) {
@@ -402,16 +492,16 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
           for (uint32_t kq = kb; kq < ke; ++kq) {
             const uint64_t ga = w.catt[gb + kq];
             const uint64_t bo = a.boffs[gb + ga], nb = 8 * (a.boffs[gb + ga + 1] - bo);
-            uint64_t s = 0;
+            uint64_t sv = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const uint64_t xb = (uint64_t)(vloc + i) - cs;  // the position's bit in the bitfield
               const bool in = v[i] && xb < nb;
               const uint32_t by = in ? a.bits[bo + (xb >> 3)] : 0u;
-              s += (in && ((by >> (7 - (uint32_t)(xb & 7))) & 1)) ? b[i] : 0;
+              sv += (in && ((by >> (7 - (uint32_t)(xb & 7))) & 1)) ? (B32 ? bbase + o4[i] : b[i]) : 0;
             }
-            s = wsum64_dpp(s);
-            if (lane == 0 && s) atomicAdd((unsigned long long*)&L.vot[kq - k0], (unsigned long long)s);
+            sv = wsum64_dpp(sv);
+            if (lane == 0 && sv) atomicAdd((unsigned long long*)&L.vot[kq - k0], (unsigned long long)sv);
           }
         }
       }
@@ -419,24 +509,32 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       bool act[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        act[i] = win_active<B32, SEW>(x, i, d);
+        act[i] = win_active<B32, SEW>(x, i, d32, d);
         nm += (v[i] && !act[i]) ? 1 : 0;
       }
-      if (applied) {
+      const bool all = v[0] && v[1] && v[2] && v[3];
+      if (B32) {
+        // the offsets: (base + o +- 1) - base = o +- 1, inside u32 (the state's re-base bound)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) b[i] = (rb[i] & 1) ? b[i] + PZ_ATTESTER_REWARD : b[i] - PZ_ATTESTER_REWARD;
-        const bool all = v[0] && v[1] && v[2] && v[3];
-        if (B32) {  // the offsets back: (base + o +- 1) - base = o +- 1, inside u32 (the state's re-base bound)
-          const uint64_t o = inst * w.vstride + p;
+        for (int i = 0; i < 4; ++i) {
+          o4[i] += (rb[i] & 1) ? rwd : 0u - rwd;
+          const bool ai = v[i] && act[i];
+          sum += ai ? o4[i] : 0u;
+          nact += ai ? 1u : 0u;
+        }
+        if (applied) {
           if (all) {
-            *reinterpret_cast<uint4*>(w.bal32 + o) = make_uint4((uint32_t)(b[0] - bbase), (uint32_t)(b[1] - bbase),
-                                                                (uint32_t)(b[2] - bbase), (uint32_t)(b[3] - bbase));
+            *reinterpret_cast<uint4*>(Bal32 + p) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
           } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-              if (v[i]) w.bal32[o + i] = (uint32_t)(b[i] - bbase);
+              if (v[i]) Bal32[p + i] = o4[i];
           }
-        } else {
+        }
+      } else {
+        if (applied) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) b[i] = (rb[i] & 1) ? b[i] + PZ_ATTESTER_REWARD : b[i] - PZ_ATTESTER_REWARD;
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int i = 2 * h;
@@ -449,23 +547,20 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
               Bal[p + i + 1] = b[i + 1];
           }
         }
-      }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sum += (v[i] && act[i]) ? b[i] : 0;
-      // slot j's next piece: its stream (descriptor loaded a round ago), and the descriptor after
-      const uint32_t k1 = kk + D * NW, k2 = kk + 2 * D * NW;
-      dq[j] = dn[j];
-      if (k1 < np) win_load<B32, SEW>(a, w, inst, dq[j], lane, q[j]);
-      dn[j] = k2 < np ? w.pdesc[pb + k2] : make_uint2(0, 0);
+        for (int i = 0; i < 4; ++i) sum += (v[i] && act[i]) ? b[i] : 0;
+      }
+      // slot j's piece of the next round (past the last round: a dummy, loaded and unused)
+      dq[j] = make_uint2(__builtin_amdgcn_readlane(dnx.x, j), __builtin_amdgcn_readlane(dnx.y, j));
+      win_load<B32, SEW>(col, dq[j], lane, q[j]);
     }
   }
+  if (B32) sum += (uint64_t)nact * bbase;  // (the lane's sum of base + offset over its active positions)
   sum = wsum64_dpp(sum);
-  nm = wsum64_dpp(nm);
-  if (lane == 0) red2[wave][0] = sum, red2[wave][1] = nm;
+  const uint64_t nmw = wsum64_dpp(nm);
+  if (lane == 0) red2[wave][0] = sum, red2[wave][1] = nmw;
   __syncthreads();  // (also: every wave's LDS tallies are in)
-#ifdef PZ_AB_BUILD
-  if (w.trace && tid == 0) w.trace[4ull * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime();
-#endif
+  if (TR && tid == 0) tstamp[2] = __builtin_amdgcn_s_memrealtime();
   uint64_t* sc = a.scal + inst * kScal;
   if (tid == 0) {
     uint64_t s = 0, n = 0;
@@ -487,6 +582,7 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   }
   if (r == 0) {  // the next step's accumulators start from zero, its winners empty
     if (a.scal_next && tid < kScal) a.scal_next[inst * kScal + tid] = 0;
+    if (w.pacc_next && tid == 0) w.pacc_next[inst] = 0;
     for (uint32_t s = tid; s < a.nrec; s += NT) w.winner_next[inst * a.nrec + s] = 0xFFFFFFFFu;
     if (w.vote_next)
       for (uint32_t g = tid; g < a.natt; g += NT) w.vote_next[gb + g] = 0, w.total_next[gb + g] = 0;
@@ -505,12 +601,14 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       if (3ull * V >= 2ull * T && d > pk64(aw.y, aw.z)) atomicMin(&a.winner[inst * a.nrec + aw.x], ga);
     }
   }
-#ifdef PZ_AB_BUILD
-  if (w.trace) {
+  if (TR) {
     __syncthreads();
-    if (tid == 0) w.trace[4ull * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+      const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
+      w.trace[4ull * blockIdx.x] = tstamp[0], w.trace[4ull * blockIdx.x + 1] = tstamp[1];
+      w.trace[4ull * blockIdx.x + 2] = tstamp[2], w.trace[4ull * blockIdx.x + 3] = t3;
+    }
   }
-#endif
 }
 
 #define PZ_WINDOW_KERNEL(NAME, B32, SEW, LLB)                                                           \
@@ -541,7 +639,12 @@ PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_g_kernel, false, 64, false)
     window_body<true, 16, true, X, D>(a, w);                                                               \
   }
 PZ_WINDOW_ABL(0, 2) PZ_WINDOW_ABL(0, 3) PZ_WINDOW_ABL(0, 4)
-PZ_WINDOW_ABL(1, 3) PZ_WINDOW_ABL(2, 3) PZ_WINDOW_ABL(4, 3) PZ_WINDOW_ABL(8, 3) PZ_WINDOW_ABL(15, 3)
+PZ_WINDOW_ABL(1, 2) PZ_WINDOW_ABL(2, 2) PZ_WINDOW_ABL(4, 2) PZ_WINDOW_ABL(8, 2) PZ_WINDOW_ABL(15, 2) PZ_WINDOW_ABL(16, 2)
+PZ_WINDOW_ABL(32, 2) PZ_WINDOW_ABL(64, 2) PZ_WINDOW_ABL(80, 2)
+// the product form with phase stamps (tools/epoch_trace.py)
+extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_kernel(EpochArgs a, WinArgs w) {
+  window_body<true, 16, true, 0, kWinDepth16, true>(a, w);
+}
 #undef PZ_WINDOW_ABL
 static int g_window_ablation = 0;
 static uint64_t* g_window_trace = nullptr;
@@ -572,16 +675,21 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
   }
 #undef PZ_PICK
 #ifdef PZ_AB_BUILD
+  if (g_window_trace && b32 && sew == 16 && llb) k = (const void*)pz_epoch_window_trace_kernel;
   if (g_window_ablation && b32 && sew == 16 && llb) {
     switch (g_window_ablation) {  // ablation bits | prefetch depth << 8
       case 2 << 8: k = (const void*)pz_epoch_window_abl0_d2_kernel; break;
       case 3 << 8: k = (const void*)pz_epoch_window_abl0_d3_kernel; break;
       case 4 << 8: k = (const void*)pz_epoch_window_abl0_d4_kernel; break;
-      case 1: k = (const void*)pz_epoch_window_abl1_d3_kernel; break;
-      case 2: k = (const void*)pz_epoch_window_abl2_d3_kernel; break;
-      case 4: k = (const void*)pz_epoch_window_abl4_d3_kernel; break;
-      case 8: k = (const void*)pz_epoch_window_abl8_d3_kernel; break;
-      case 15: k = (const void*)pz_epoch_window_abl15_d3_kernel; break;
+      case 1: k = (const void*)pz_epoch_window_abl1_d2_kernel; break;
+      case 2: k = (const void*)pz_epoch_window_abl2_d2_kernel; break;
+      case 4: k = (const void*)pz_epoch_window_abl4_d2_kernel; break;
+      case 8: k = (const void*)pz_epoch_window_abl8_d2_kernel; break;
+      case 15: k = (const void*)pz_epoch_window_abl15_d2_kernel; break;
+      case 16: k = (const void*)pz_epoch_window_abl16_d2_kernel; break;
+      case 32: k = (const void*)pz_epoch_window_abl32_d2_kernel; break;
+      case 64: k = (const void*)pz_epoch_window_abl64_d2_kernel; break;
+      case 80: k = (const void*)pz_epoch_window_abl80_d2_kernel; break;
       default: return hipErrorInvalidValue;
     }
   }

@@ -8,17 +8,18 @@
 // (repeated bytes: every element emitted, an empty one as `3a 00`), aggregate_sig 8 (packed
 // varints, omitted when empty).
 //
-// One launch (after a memset of one status word per wave): every wave encodes four records, one
-// per 16-lane DPP row, and finds its output offset by a decoupled look-back over the waves
-// before it (status words: flag in the top two bits, value below).  A wave
-//   1. loads its records' heads (sub-lane k: head word k), element offsets and signature values;
-//   2. sizes them in the rows (DPP row scans) and publishes the wave's total;
-//   3. issues its segment loads (bytes fields and elements, aligned dwords), then looks back
-//      while they are in flight: one status word per lane, 64 predecessors a round;
-//   4. assembles each record in the row's LDS stage at (offset mod 16) and stores 16-byte blocks.
-// Every column byte is read once: round 4's size + rocPRIM scan + write form re-read the heads,
-// element offsets and signature values in the write kernel (1.26x the algorithmic bytes,
-// profiles/r04/pmc_main.json) and ran three dependent launches.
+// Two launches (after a memset of the tile status words and ticket):
+//   size   512 threads x 8 records per tile: every record's encoded size (one lane per record:
+//          head loads coalesced, a record's element / value loads independent), the tile's
+//          scan, its base by a decoupled look-back over the tiles before it, offsets out;
+//   write  one 16-lane DPP row per record, four per wave: the record is assembled in an LDS
+//          stage at (offset mod 16) -- literals by the row's lanes, segments copied with aligned
+//          dword loads and written into the stage as whole dwords -- and stored in 16-B blocks.
+// Round 4 ran size, a rocPRIM inclusive scan (two launches) and the write kernel; the write
+// kernel placed segment bytes into the stage one ds_write_b8 at a time.  A one-launch form with
+// a look-back per wave ran 0.85 ms per 1M records against 0.41 (profiles/r05/
+// wire_att_probe_r5d.txt): ~6,000 waves are in flight, so a wave's look-back walks back over
+// many windows before it meets a published prefix; dropped.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -49,7 +50,8 @@ struct AttArgs {
   uint64_t* sizes;
   uint64_t* offs;  // n+1
   uint8_t* out;
-  uint64_t* status;  // [waves] look-back status words, zero at launch
+  uint64_t* status;  // [tiles] look-back status words, zero at launch
+  uint32_t* ticket;  // tile ticket (after the status words), zero at launch
 };
 
 __device__ __forceinline__ uint32_t vlen(uint64_t x) { return (uint32_t)((70 - __clzll(x | 1)) / 7); }
@@ -267,289 +269,48 @@ __device__ __forceinline__ uint32_t rscan32(uint32_t x) {
   return x;
 }
 
-// ---- the one-pass encode --------------------------------------------------------------------
-constexpr uint64_t kFlagA = 1ull << 62, kFlagP = 2ull << 62, kVal = kFlagA - 1;
-
-__device__ __forceinline__ uint64_t ld_status(uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_status_fresh(uint64_t* p) {  // at the coherence point
-  return __hip_atomic_fetch_add(p, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The wave's exclusive output offset: lane l watches wave g - 1 - l (64 predecessors a round);
-// the nearest inclusive prefix (P) ends the walk, the aggregates (A) nearer than it are added.
-// Forward progress: workgroups are dispatched in blockIdx order, so every predecessor of a
-// running wave has started (wire.hip's measured "tile = blockIdx" form).
-__device__ __forceinline__ uint64_t wave_lookback(uint64_t* status, uint64_t g) {
-  const int lane = threadIdx.x & 63;
-  uint64_t prefix = 0;
-  for (int64_t j = (int64_t)g - 1;; j -= 64) {
-    const int64_t idx = j - lane;
-    uint64_t v = idx >= 0 ? ld_status(status + idx) : kFlagP;  // before wave 0: prefix 0
-    for (uint32_t spins = 0; !(v >> 62); ++spins) {
-      __builtin_amdgcn_s_sleep(1);
-      v = spins < 256 ? ld_status(status + idx) : ld_status_fresh(status + idx);
-    }
-    const uint64_t pm = __ballot((v >> 62) == 2);
-    const int first = pm ? __builtin_ctzll(pm) : 64;
-    prefix += wsum(lane <= first ? (v & kVal) : 0);
-    if (pm) return prefix;
-  }
-}
-
-// Wave g: records 4g .. 4g + 3, one per DPP row.
-__device__ __forceinline__ void att_wave(const AttArgs& a, uint8_t (*stage)[kStageAlloc], uint64_t g) {
-  const int lane = threadIdx.x & 63;
-  const int sl = lane & (kRow - 1), ri = lane / kRow;
-  const uint64_t i = g * kRecs + ri;
-  const bool valid = i < a.n;
-  // 1. heads, then the elements' offsets and the signature values
-  const uint64_t hv = valid && sl < kHeadWords ? head_word(a, sl, i) : 0;
-  Head h;
-  h.v[0] = bc64<0>(hv);
-  h.v[1] = bc64<1>(hv);
-  h.v[2] = bc64<2>(hv);
-  h.b0[0] = bc64<3>(hv);
-  h.bl[0] = bc64<4>(hv) - h.b0[0];
-  h.b0[1] = bc64<5>(hv);
-  h.bl[1] = bc64<6>(hv) - h.b0[1];
-  h.b0[2] = bc64<7>(hv);
-  h.bl[2] = bc64<8>(hv) - h.b0[2];
-  h.o0 = bc64<9>(hv);
-  h.o1 = bc64<10>(hv);
-  h.s0 = bc64<11>(hv);
-  h.s1 = bc64<12>(hv);
-  const uint64_t nob = h.o1 - h.o0, nsig = h.s1 - h.s0;
-  // the row layout takes at most 13 elements and 16 values (row-uniform)
-  const bool rowable = valid && nob <= kMaxOblique && nsig <= kRow;
-  uint64_t eb0 = 0, el64 = 0, sv = 0;
-  if (rowable && (uint64_t)sl < nob) {
-    eb0 = a.ooff[h.o0 + sl];
-    el64 = a.ooff[h.o0 + sl + 1] - eb0;
-  }
-  if (rowable && (uint64_t)sl < nsig) sv = a.sig[h.s0 + sl];
-  // ... and every segment (bytes field, element) at most kSegMax bytes: then every size below
-  // fits 32 bits (at most 13 x 66 + 3 x 66 + 3 x 11 + 163 bytes)
-  const bool seg_long = ((uint64_t)sl < nob && el64 > kSegMax) || (sl < 3 && (sl == 0 ? h.bl[0] : sl == 1 ? h.bl[1] : h.bl[2]) > kSegMax);
-  const uint64_t long_rows = __ballot(rowable && seg_long);
-  const bool small = rowable && !((long_rows >> (kRow * ri)) & 0xffffull);
-  const uint32_t el = small && (uint64_t)sl < nob ? (uint32_t)el64 : 0;
-  // this sub-lane's segment: source and length (element sl - 3 arrives from sub-lane sl - 3)
-  const uint32_t el_seg = shr3(el);
-  const uint64_t eb_seg = ((uint64_t)shr3((uint32_t)(eb0 >> 32)) << 32) | shr3((uint32_t)eb0);
-  uint32_t seg_len = 0;
-  const uint8_t* seg_src = nullptr;
-#pragma unroll
-  for (int k = 0; k < 3; ++k)
-    if (sl == k) {
-      seg_len = (uint32_t)h.bl[k];
-      seg_src = a.bdat[k] + h.b0[k];
-    }
-  if (sl >= 3 && (uint64_t)(sl - 3) < nob) {
-    seg_len = el_seg;
-    seg_src = a.odat + eb_seg;
-  }
-  // 2. sizes in the row: element / value sizes scanned, then the record's items
-  const uint32_t esz = small && (uint64_t)sl < nob ? 1 + vlen(el) + el : 0;
-  const uint32_t ssz = small && (uint64_t)sl < nsig ? vlen(sv) : 0;
-  const uint32_t einc = rscan32(esz), sinc = rscan32(ssz);
-  const uint32_t obl = bc32<15>(einc), sigb = bc32<15>(sinc);
-  // sub-lane k (1-8) owns item k -- fields 1-3 (tag + varint), the headers and bytes of fields
-  // 4-6, the elements of field 7, the header and values of field 8 -- and sub-lane 0 the frame
-  uint64_t val = 0;
-  uint32_t span = 0;
-  if (sl >= 1 && sl <= 3) {
-    val = sl == 1 ? h.v[0] : sl == 2 ? h.v[1] : h.v[2];
-    span = val ? 1 + vlen(val) : 0;
-  } else if (sl >= 4 && sl <= 6) {
-    val = sl == 4 ? h.bl[0] : sl == 5 ? h.bl[1] : h.bl[2];
-    span = val ? 1 + vlen(val) + (uint32_t)val : 0;
-  } else if (sl == 7) {
-    span = obl;
-  } else if (sl == 8) {
-    val = sigb;
-    span = sigb ? 1 + vlen(sigb) + sigb : 0;
-  }
-  const uint32_t inc = rscan32(small ? span : 0);
-  const uint32_t body = bc32<8>(inc);
-  const uint32_t frame = a.field ? a.tag_len + vlen(body) : 0;
-  uint64_t size = small ? frame + body : 0;
-  // records the rows cannot size (more elements / values, a long segment): the whole wave
-  for (int u = 0; u < kRecs; ++u) {
-    if (g * kRecs + u >= a.n) break;
-    if (__builtin_amdgcn_readlane((uint32_t)small, kRow * u)) continue;
-    Head q;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      q.v[k] = rl64(hv, kRow * u + k);
-      q.b0[k] = rl64(hv, kRow * u + 3 + 2 * k);
-      q.bl[k] = rl64(hv, kRow * u + 4 + 2 * k) - q.b0[k];
-    }
-    q.o0 = rl64(hv, kRow * u + 9);
-    q.o1 = rl64(hv, kRow * u + 10);
-    q.s0 = rl64(hv, kRow * u + 11);
-    q.s1 = rl64(hv, kRow * u + 12);
-    uint64_t fixed, obl8, sigb8;
-    record_parts(a, q, &fixed, &obl8, &sigb8);
-    const uint64_t bs = body_size(fixed, obl8, sigb8);
-    if (ri == u) size = a.field ? a.tag_len + vlen(bs) + bs : bs;
-  }
-  const bool fast = small && size <= kStage;
-  // 3. the segment loads go out: dwords aligned on the source covering its bytes
-  typedef const __attribute__((address_space(1))) uint32_t gword;
-  const uint32_t len = fast ? seg_len : 0;
-  const uint32_t r = (uint32_t)(uintptr_t)seg_src & 3;
-  gword* ws = reinterpret_cast<gword*>((uintptr_t)seg_src & ~(uintptr_t)3);
-  const uint32_t nw = len ? (r + len + 3) / 4 : 0;
-  uint32_t wv[kSegWords + 1];
-#pragma unroll
-  for (int k = 0; k <= (int)kSegWords; ++k) wv[k] = (uint32_t)k < nw ? ws[k] : 0;
-  // ... the wave's total out, its offset back (the look-back runs under the segment loads)
-  const uint64_t z0 = rl64(size, 0), z1 = rl64(size, kRow), z2 = rl64(size, 2 * kRow), z3 = rl64(size, 3 * kRow);
-  const uint64_t agg = z0 + z1 + z2 + z3;
-  const uint64_t before = (ri > 0 ? z0 : 0) + (ri > 1 ? z1 : 0) + (ri > 2 ? z2 : 0);
-  if (lane == 0) st_status(a.status + g, (g == 0 ? kFlagP : kFlagA) | agg);
-  const uint64_t base = g == 0 ? 0 : wave_lookback(a.status, g);
-  if (lane == 0 && g > 0) st_status(a.status + g, kFlagP | (base + agg));
-  const uint64_t o = base + before;
-  if (valid && sl == 0) a.offs[i + 1] = o + size;
-  if (g == 0 && lane == 0) a.offs[0] = 0;
-  // 4. layout: the literal bytes into the stage, record byte j at sh + j
-  const uint32_t sh = (uint32_t)o & 15;
-  uint8_t* st = stage[ri] + sh;
-  uint32_t seg_dst = 0;
-  if (fast) {  // row-uniform, so the row's DPP reads below see only active lanes
-    const uint32_t pos = frame + inc - span;
-    if (sl == 0 && a.field) {
-      uint8_t* q = put_varint(st, ((uint64_t)a.field << 3) | 2);
-      put_varint(q, body);
-    }
-    if (sl >= 1 && sl <= 8 && sl != 7 && val) {
-      st[pos] = (uint8_t)((sl << 3) | (sl >= 4 ? 2 : 0));
-      put_varint(st + pos + 1, val);
-    }
-    // bytes field f's data follows item 4 + f's header: sub-lane f (segment f) learns where
-    const uint32_t fd = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(pos + 1 + vlen(val)), 0x104, 0xf, 0xf, false);
-    if (sl < 3) seg_dst = fd;
-    // field 7: sub-lane e writes element e's header; its bytes are segment 3 + e
-    const uint32_t ep = bc32<7>(pos) + einc - esz;
-    if ((uint64_t)sl < nob) {
-      st[ep] = (7 << 3) | 2;
-      put_varint(st + ep + 1, el);
-    }
-    const uint32_t ed = shr3(ep + 1 + vlen(el));
-    if (sl >= 3 && (uint64_t)(sl - 3) < nob) seg_dst = ed;
-    // field 8: one varint per sub-lane after item 8's header.  (A DPP read of a lane that is
-    // inactive returns 0, so every row_newbcast runs outside the per-lane branches.)
-    const uint32_t sp = bc32<8>(pos) + 1 + vlen(sigb);
-    if ((uint64_t)sl < nsig) put_varint(st + sp + sinc - ssz, sv);
-  }
-  // the segment's words realigned on its destination: whole dwords where the stage word is the
-  // segment's alone, bytes at its two edges (shared with the neighbouring items)
-  if (len) {
-    // stage word k of the segment holds source bytes r + 4k - dm .. +3 (dm = d0 mod 4): one
-    // v_alignbyte of the loaded words, shifted down a word when r < dm
-    const uint32_t d0 = sh + seg_dst, dend = d0 + len, dm = d0 & 3;
-    const bool back = r < dm;
-    const uint32_t delta = (r - dm) & 3, nwo = (dm + len + 3) >> 2;
-#pragma unroll
-    for (int k = (int)kSegWords; k > 0; --k) wv[k] = back ? wv[k - 1] : wv[k];
-    wv[0] = back ? 0u : wv[0];
-    uint32_t* sw = reinterpret_cast<uint32_t*>(stage[ri]) + (d0 >> 2);
-    const uint32_t bw = d0 & ~3u;
+// A row's segment into its stage: the source dwords wv (aligned on the source, first byte at
+// r), len bytes, to stage bytes [d0, d0 + len).  Whole stage dwords where the word is the
+// segment's alone, bytes at its two edges (shared with the neighbouring items); the A/B
+// library keeps round 4's byte-by-byte form (DST false).
+template <bool DST>
+__device__ __forceinline__ void stage_segment(uint8_t* row, uint32_t d0, uint32_t (&wv)[kSegWords + 1], uint32_t r,
+                                              uint32_t len) {
+  if (!DST) {
 #pragma unroll
     for (int k = 0; k < (int)kSegWords; ++k) {
-      if ((uint32_t)k >= nwo) break;
-      const uint32_t x = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], delta);
-      const uint32_t b0 = bw + 4 * k;
-      if (b0 >= d0 && b0 + 4 <= dend) {
-        sw[k] = x;
-      } else {
+      const uint32_t d = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], r);
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
-          if (b0 + b >= d0 && b0 + b < dend) stage[ri][b0 + b] = (uint8_t)(x >> (8 * b));
-      }
+      for (int b = 0; b < 4; ++b)
+        if ((uint32_t)(4 * k + b) < len) row[d0 + 4 * k + b] = (uint8_t)(d >> (8 * b));
     }
+    return;
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  // 5. store: stage block q <-> output block (o >> 4) + q
-  const uint32_t sz = fast ? (uint32_t)size : 0;
-  const uint32_t nblk = (sh + sz + 15) / 16;
-  const uint8_t* sb = stage[ri];
-  uint8_t* ob = a.out + (o - sh);
-  for (uint32_t q = sl; q < nblk; q += kRow) {
-    const uint32_t lo = 16 * q, hi = lo + 16;
-    if (lo >= sh && hi <= sh + sz) {
-      *reinterpret_cast<uint4*>(ob + lo) = *reinterpret_cast<const uint4*>(sb + lo);
+  if (!len) return;
+  // stage word k of the segment holds source bytes r + 4k - dm .. +3 (dm = d0 mod 4): one
+  // v_alignbyte of the loaded words, one word lower when r < dm
+  const uint32_t dend = d0 + len, dm = d0 & 3;
+  const bool back = r < dm;
+  const uint32_t delta = (r - dm) & 3, nwo = (dm + len + 3) >> 2;
+  uint32_t* sw = reinterpret_cast<uint32_t*>(row) + (d0 >> 2);
+  const uint32_t bw = d0 & ~3u;
+#pragma unroll
+  for (int k = 0; k < (int)kSegWords; ++k) {
+    const uint32_t lo = back ? (k ? wv[k - 1] : 0u) : wv[k], hi = back ? wv[k] : wv[k + 1];
+    const uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, delta);
+    const uint32_t b0 = bw + 4 * k;
+    if ((uint32_t)k >= nwo) {
+    } else if (b0 >= d0 && b0 + 4 <= dend) {
+      sw[k] = x;
     } else {
-      for (uint32_t x = max(lo, sh); x < min(hi, sh + sz); ++x) ob[x] = sb[x];
-    }
-  }
-  // records the row layout does not take: the whole wave, segment by segment
-  for (int u = 0; u < kRecs; ++u) {
-    const uint64_t iu = g * kRecs + u;
-    if (iu >= a.n) break;
-    if (__builtin_amdgcn_readlane((uint32_t)fast, kRow * u)) continue;
-    Head q;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      q.v[k] = rl64(hv, kRow * u + k);
-      q.b0[k] = rl64(hv, kRow * u + 3 + 2 * k);
-      q.bl[k] = rl64(hv, kRow * u + 4 + 2 * k) - q.b0[k];
+      for (int b = 0; b < 4; ++b)
+        if (b0 + b >= d0 && b0 + b < dend) row[b0 + b] = (uint8_t)(x >> (8 * b));
     }
-    q.o0 = rl64(hv, kRow * u + 9);
-    q.o1 = rl64(hv, kRow * u + 10);
-    q.s0 = rl64(hv, kRow * u + 11);
-    q.s1 = rl64(hv, kRow * u + 12);
-    uint64_t fixed, obl8, sigb8;
-    record_parts(a, q, &fixed, &obl8, &sigb8);
-    write_record(a, q, body_size(fixed, obl8, sigb8), sigb8, a.out + rl64(o, kRow * u));
   }
 }
 
-// 78 VGPRs: 6 waves per SIMD (the A/B library holds the 7- and 8-wave caps, which spill).
-#define PZ_ATT_KERNEL(NAME, W)                                                                      \
-  extern "C" __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(W, W))) \
-  NAME(AttArgs a) {                                                                                 \
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kWaves][kRecs][kStageAlloc];             \
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);                                 \
-    const uint64_t g = (uint64_t)blockIdx.x * kWaves + w;                                           \
-    if (g * kRecs >= a.n) return; /* (the last workgroup's idle waves: no successor reads them) */   \
-    att_wave(a, stage[w], g);                                                                       \
-  }
-PZ_ATT_KERNEL(pz_wire_att_kernel, 6)
-#ifdef PZ_AB_BUILD
-PZ_ATT_KERNEL(pz_wire_att_w7_kernel, 7)
-PZ_ATT_KERNEL(pz_wire_att_w8_kernel, 8)
-int g_att_variant = 0;  // 1: the three-launch form, 7 / 8: the one-pass kernel capped at 7 / 8 waves per SIMD
-#endif
-
-uint64_t att_waves(uint64_t n) { return (n + kRecs - 1) / kRecs; }
-
-hipError_t launch_one_pass(AttArgs a, void* scratch, hipStream_t s) {
-  if (!a.n) return hipMemsetAsync(a.offs, 0, 8, s);
-  const uint64_t waves = att_waves(a.n);
-  a.status = static_cast<uint64_t*>(scratch);
-  hipError_t e = hipMemsetAsync(scratch, 0, waves * 8, s);
-  if (e != hipSuccess) return e;
-  const void* k = (const void*)pz_wire_att_kernel;
-#ifdef PZ_AB_BUILD
-  if (g_att_variant == 7) k = (const void*)pz_wire_att_w7_kernel;
-  if (g_att_variant == 8) k = (const void*)pz_wire_att_w8_kernel;
-#endif
-  void* args[] = {&a};
-  e = hipLaunchKernel(k, dim3((uint32_t)((waves + kWaves - 1) / kWaves)), dim3(kThreads), args, 0, s);
-  return e;
-}
-
-#ifdef PZ_AB_BUILD
-// ---- the A/B library: round 4's three-launch form (size kernel, rocPRIM scan, write kernel) ----
-template <bool FUSED>
+template <bool DST>
 __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*stage)[kStageAlloc], uint64_t i0) {
   const int lane = threadIdx.x & 63;
   const int sl = lane & (kRow - 1), ri = lane / kRow;
@@ -651,13 +412,7 @@ __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*
     const uint32_t sp = bc32<8>(pos) + 1 + vlen(sigb);
     if ((uint64_t)sl < nsig) put_varint(st + sp + sinc - ssz, sv);
   }
-#pragma unroll
-  for (int k = 0; k < (int)kSegWords; ++k) {
-    const uint32_t d = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], r);
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-      if ((uint32_t)(4 * k + b) < len) st[seg_dst + 4 * k + b] = (uint8_t)(d >> (8 * b));
-  }
+  stage_segment<DST>(stage[ri], sh + seg_dst, wv, r, len);
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   const uint32_t sz = fast ? (uint32_t)size : 0;
@@ -693,7 +448,173 @@ __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*
   }
 }
 
-extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_size_kernel(AttArgs a) {
+// ---- the encode: sizes + scan in one launch, then the writes ----------------------------------
+constexpr uint64_t kFlagA = 1ull << 62, kFlagP = 2ull << 62, kVal = kFlagA - 1;
+
+__device__ __forceinline__ uint64_t ld_status(uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_status_fresh(uint64_t* p) {  // at the coherence point
+  return __hip_atomic_fetch_add(p, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Sizing tile: 512 threads x 8 records (thread t takes records t + 512q of the tile: every head
+// load coalesced; 2 waves per SIMD leave 256 VGPRs for 8 records' loads in flight), 256 tiles
+// per 1M records.  Tiles are numbered by a
+// ticket taken at start, so every predecessor of a waiting tile is running or done (the
+// dispatch order of workgroups is not guaranteed); a tile's look-back reads 1,024
+// predecessors' status words a round.
+constexpr int kSizeThreads = 512, kSizeWaves = kSizeThreads / 64, kSizePer = 8;
+constexpr uint32_t kSizeTile = kSizeThreads * kSizePer, kLbWin = kSizeThreads;
+
+__device__ __forceinline__ uint64_t record_size(const AttArgs& a, uint64_t i) {
+  Head h;
+  load_head(a, i, h);
+  uint64_t body = 0, sigb = 0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    body += h.v[k] ? 1 + vlen(h.v[k]) : 0;
+    body += h.bl[k] ? 1 + vlen(h.bl[k]) + h.bl[k] : 0;
+  }
+#pragma unroll 4
+  for (uint64_t e = h.o0; e < h.o1; ++e) {
+    const uint64_t l = a.ooff[e + 1] - a.ooff[e];
+    body += 1 + vlen(l) + l;
+  }
+#pragma unroll 4
+  for (uint64_t e = h.s0; e < h.s1; ++e) sigb += vlen(a.sig[e]);
+  body += sigb ? 1 + vlen(sigb) + sigb : 0;
+  return a.field ? a.tag_len + vlen(body) + body : body;
+}
+
+// Block-wide exclusive scan of one value per thread; *total receives the sum.
+__device__ __forceinline__ uint64_t block_excl(uint64_t x, uint64_t* s_wave, uint64_t* total) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint64_t incl = wscan(x);
+  if (lane == 63) s_wave[w] = incl;
+  __syncthreads();
+  uint64_t before = 0, all = 0;
+#pragma unroll
+  for (int k = 0; k < kSizeWaves; ++k) {
+    before += k < w ? s_wave[k] : 0;
+    all += s_wave[k];
+  }
+  __syncthreads();  // (s_wave is rewritten by the next scan)
+  *total = all;
+  return before + incl - x;
+}
+
+// The tile's exclusive base: thread t watches predecessor tile - 1 - t (512 a round); the nearest inclusive
+// prefix (P) ends the walk, the aggregates (A) nearer than it are added.
+__device__ uint64_t lookback_tiles(uint64_t* status, uint64_t tile, uint32_t* s_first, uint64_t* s_part) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint64_t prefix = 0;
+  for (int64_t j = (int64_t)tile - 1;; j -= kLbWin) {
+    const int64_t idx = j - tid;
+    uint64_t v = idx >= 0 ? ld_status(status + idx) : kFlagP;  // before tile 0: prefix 0
+    for (uint32_t spins = 0; !(v >> 62); ++spins) {
+      __builtin_amdgcn_s_sleep(1);
+      v = spins < 256 ? ld_status(status + idx) : ld_status_fresh(status + idx);
+    }
+    if (tid == 0) *s_first = kLbWin;
+    __syncthreads();
+    if ((v >> 62) == 2) atomicMin(s_first, (uint32_t)tid);
+    __syncthreads();
+    const uint32_t first = *s_first;
+    const uint64_t part = wsum((uint32_t)tid <= first ? (v & kVal) : 0);
+    if (lane == 0) s_part[w] = part;
+    __syncthreads();
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kSizeWaves; ++k) sum += s_part[k];
+    __syncthreads();  // s_first / s_part are rewritten by the next window
+    prefix += sum;
+    if (first < kLbWin) return prefix;
+  }
+}
+
+// Launch 1: every record's size, the tile's scan, its base by look-back, offsets out.
+extern "C" __global__ void __launch_bounds__(kSizeThreads) pz_wire_att_size_kernel(AttArgs a) {
+  __shared__ uint64_t s_wave[kSizeWaves], s_part[kSizeWaves];
+  __shared__ uint32_t s_first, s_tile;
+  const int tid = threadIdx.x;
+  if (tid == 0) s_tile = atomicAdd(a.ticket, 1u);
+  __syncthreads();
+  const uint64_t tile = s_tile, t0 = tile * kSizeTile;
+  uint64_t sz[kSizePer];
+#pragma unroll
+  for (int q = 0; q < kSizePer; ++q) {
+    const uint64_t i = t0 + (uint64_t)q * kSizeThreads + tid;
+    sz[q] = i < a.n ? record_size(a, i) : 0;
+  }
+  uint64_t ex[kSizePer], run = 0;
+#pragma unroll
+  for (int q = 0; q < kSizePer; ++q) {
+    uint64_t tot;
+    ex[q] = run + block_excl(sz[q], s_wave, &tot);
+    run += tot;
+  }
+  if (tid == 0) st_status(a.status + tile, (tile == 0 ? kFlagP : kFlagA) | run);
+  const uint64_t base = tile == 0 ? 0 : lookback_tiles(a.status, tile, &s_first, s_part);
+  if (tid == 0 && tile > 0) st_status(a.status + tile, kFlagP | (base + run));
+#pragma unroll
+  for (int q = 0; q < kSizePer; ++q) {
+    const uint64_t i = t0 + (uint64_t)q * kSizeThreads + tid;
+    if (i < a.n) a.offs[i + 1] = base + ex[q] + sz[q];
+  }
+  if (tile == 0 && tid == 0) a.offs[0] = 0;
+}
+
+// Launch 2: four records per wave, one per DPP row.  63 VGPRs; left alone the SGPRs (about
+// 100) hold it at 7 waves per SIMD.  Capped at 8 (28 SGPRs spill to VGPR lanes): 0.432 ->
+// 0.383 ms per 1M-record encode (tools/wire_att_probe.py r2t, same-process A/B).
+#define PZ_ATT_WRITE(NAME, DST)                                                                      \
+  extern "C" __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))  \
+  NAME(AttArgs a) {                                                                                  \
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kWaves][kRecs][kStageAlloc];              \
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);                                  \
+    wire_att_write_rows<DST>(a, stage[w], ((uint64_t)blockIdx.x * kWaves + w) * kRecs);              \
+  }
+PZ_ATT_WRITE(pz_wire_att_write_kernel, true)
+#ifdef PZ_AB_BUILD
+PZ_ATT_WRITE(pz_wire_att_write_bytes_kernel, false)
+int g_att_variant = 0;  // 1 round 4's three launches, 2 this scan + byte-wise stage
+#endif
+
+uint64_t att_tiles(uint64_t n) { return (n + kSizeTile - 1) / kSizeTile; }
+
+hipError_t launch_write(const AttArgs& a, bool dst, hipStream_t s) {
+  if (!a.n) return hipSuccess;
+  const void* k = (const void*)pz_wire_att_write_kernel;
+#ifdef PZ_AB_BUILD
+  if (!dst) k = (const void*)pz_wire_att_write_bytes_kernel;
+#else
+  (void)dst;
+#endif
+  void* args[] = {const_cast<AttArgs*>(&a)};
+  return hipLaunchKernel(k, dim3((uint32_t)((a.n + kRecs * kWaves - 1) / (kRecs * kWaves))), dim3(kThreads), args, 0,
+                         s);
+}
+
+// sizes + offsets (status words reset first), then the writes
+hipError_t launch_two(AttArgs a, void* scratch, bool dst, hipStream_t s) {
+  if (!a.n) return hipMemsetAsync(a.offs, 0, 8, s);
+  const uint64_t tiles = att_tiles(a.n);
+  a.status = static_cast<uint64_t*>(scratch);
+  a.ticket = reinterpret_cast<uint32_t*>(a.status + tiles);
+  hipError_t e = hipMemsetAsync(scratch, 0, tiles * 8 + 8, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(pz_wire_att_size_kernel, dim3((uint32_t)tiles), dim3(kSizeThreads), 0, s, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return launch_write(a, dst, s);
+}
+
+#ifdef PZ_AB_BUILD
+// ---- round 4's three launches: size kernel, rocPRIM scan, byte-wise write kernel ----------------
+extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_size_r4_kernel(AttArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= a.n) return;
   Head h;
@@ -715,12 +636,6 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_wire_att_size_kernel(A
   a.sizes[i] = a.field ? a.tag_len + vlen(body) + body : body;
 }
 
-extern "C" __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))
-pz_wire_att_write_kernel(AttArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kWaves][kRecs][kStageAlloc];
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  wire_att_write_rows<false>(a, stage[w], ((uint64_t)blockIdx.x * kWaves + w) * kRecs);
-}
 
 size_t scan_bytes(uint64_t n) {
   size_t bytes = 0;
@@ -733,17 +648,16 @@ hipError_t launch_three(AttArgs a, void* scratch, hipStream_t s) {
   a.sizes = static_cast<uint64_t*>(scratch);
   hipError_t e = hipMemsetAsync(a.offs, 0, 8, s);
   if (e != hipSuccess || !a.n) return e;
-  hipLaunchKernelGGL(pz_wire_att_size_kernel, dim3((uint32_t)((a.n + kThreads - 1) / kThreads)), dim3(kThreads), 0, s,
+  hipLaunchKernelGGL(pz_wire_att_size_r4_kernel, dim3((uint32_t)((a.n + kThreads - 1) / kThreads)), dim3(kThreads), 0, s,
                      a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   size_t bytes = scan_bytes(a.n);
   e = rocprim::inclusive_scan(static_cast<uint8_t*>(scratch) + ((a.n * 8 + 255) & ~uint64_t(255)), bytes, a.sizes,
                               a.offs + 1, (size_t)a.n, rocprim::plus<uint64_t>(), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(pz_wire_att_write_kernel, dim3((uint32_t)((a.n + kRecs * kWaves - 1) / (kRecs * kWaves))),
-                     dim3(kThreads), 0, s, a);
-  return hipGetLastError();
+  return launch_write(a, false, s);
 }
+
 #endif
 
 int att_args(const pz_attestation_cols* c, uint64_t n, uint32_t field_num, AttArgs* a) {
@@ -782,8 +696,9 @@ int att_args(const pz_attestation_cols* c, uint64_t n, uint32_t field_num, AttAr
 hipError_t launch_encode(const AttArgs& a, void* scratch, hipStream_t s) {
 #ifdef PZ_AB_BUILD
   if (g_att_variant == 1) return launch_three(a, scratch, s);
+  if (g_att_variant == 2) return launch_two(a, scratch, false, s);
 #endif
-  return launch_one_pass(a, scratch, s);
+  return launch_two(a, scratch, true, s);
 }
 
 }  // namespace
@@ -794,11 +709,11 @@ using namespace pz;
 extern "C" {
 
 uint64_t pz_wire_attestations_scratch_bytes(uint64_t n) {
-  const uint64_t one = ((att_waves(n) * 8 + 255) & ~uint64_t(255));
+  const uint64_t two = ((att_tiles(n) * 8 + 8 + 255) & ~uint64_t(255));
 #ifdef PZ_AB_BUILD
-  return std::max<uint64_t>(one, ((n * 8 + 255) & ~uint64_t(255)) + scan_bytes(n));
+  return std::max<uint64_t>(two, ((n * 8 + 255) & ~uint64_t(255)) + scan_bytes(n));
 #else
-  return std::max<uint64_t>(one, 256);
+  return std::max<uint64_t>(two, 256);
 #endif
 }
 
@@ -816,7 +731,7 @@ int pz_dev_wire_attestations(const pz_attestation_cols* c, uint64_t n, uint32_t 
   a.out = d_out;
   a.offs = d_offsets;
   const hipError_t e = launch_encode(a, d_scratch, static_cast<hipStream_t>(stream));
-  return e == hipSuccess ? PZ_OK : hip_fail(e, "pz_wire_att_kernel");
+  return e == hipSuccess ? PZ_OK : hip_fail(e, "pz_wire_att kernels");
 }
 
 int pz_wire_attestations(const pz_attestation_cols* c, uint64_t n, uint32_t field_num, uint8_t* out, uint64_t cap,
@@ -875,7 +790,7 @@ int pz_wire_attestations(const pz_attestation_cols* c, uint64_t n, uint32_t fiel
   a.out = st.up<uint8_t>(nullptr, pz_wire_attestations_bound(n, bytes_total, ne, ns));
   if (st.rc) return st.rc;
   // one pass into the bound-sized device buffer; the length is known once it has run
-  st.check(launch_encode(a, scratch, st.s), "pz_wire_att_kernel");
+  st.check(launch_encode(a, scratch, st.s), "pz_wire_att kernels");
   uint64_t total = 0;
   st.down(&total, a.offs + n, 1);
   if (st.sync()) return st.rc;

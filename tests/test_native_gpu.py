@@ -232,6 +232,40 @@ def test_native_epoch_single_launch_matches_window_pass(n):
         np.testing.assert_array_equal(x, y)
 
 
+@pytest.mark.ab
+@pytest.mark.parametrize("abl", [16, 32])
+@pytest.mark.parametrize("n,B,short", [(65536, 5, False), (1 << 20, 2, False), (4096, 3, True)])
+def test_native_epoch_window_meeting_fallbacks(abl, n, B, short):
+    """The meeting of an instance's R blocks (each counts 1/R of the bitfields, epoch_window.hip
+    WinArgs.pacc) against its fallbacks, each exact: every block counting everything (16), and
+    the wait bound at zero (32: a block that arrives before its partners counts the whole
+    instance itself).  Two steps against the oracle; or one with a short committee bitfield in
+    instance 0 (its flags, its balances untouched)."""
+    dll = _lib.lib.dll
+    old = dll.pz_debug_set_window_ablation(abl)
+    try:
+        inst = _inst(n, B, False)
+        if short:
+            bo = inst["boffs"].astype(np.int64)
+            inst["bits"] = np.delete(inst["bits"], int(bo[3]) - 1)
+            bo[3:] -= 1
+            inst["boffs"] = bo.astype(np.uint64)
+        ne = NativeEpoch(inst, device=0)
+        assert ne.one_pass and (ne.balance_bytes, ne.dynasty_bytes) == (4, 4)
+        if not short:
+            _check(ne, inst, steps=2)
+            return
+        ne.step()
+        bal, scal, _, _, _ = ne.results()
+        assert scal[0, _lib.SCAL_APPLIED] == 0 and int(scal[0, _lib.SCAL_ERR_XL]) == 2
+        np.testing.assert_array_equal(bal[0], inst["balance"][0][ne.validators()])
+        for b in range(1, B):
+            nb, applied, nxt, v, t, w = oracle_epoch(inst, b)
+            assert bool(scal[b, _lib.SCAL_APPLIED]) == applied
+    finally:
+        dll.pz_debug_set_window_ablation(old)
+
+
 @pytest.mark.parametrize("case", ["many_atts", "short_bitfield", "reward_panic", "empty_committees"])
 @pytest.mark.parametrize("B", [1, 3])
 def test_native_epoch_window_edges(case, B):
