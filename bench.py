@@ -314,9 +314,11 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                      "traffic_source": ("%s (every pz_epoch_* kernel of the %d x %d step)"
                                         % (pmc_summary_path(workload), nval, ninst)) if workload else None,
                      "traffic_frac": (traffic / (step_ms * 1e-3) / HBM_PEAK) if traffic else None,
-                     "kernel": ("epoch step: pz_epoch_window_b32_s16 (ONE launch: bit count, last bitfield into "
-                                "LDS, classify, crosslink tallies per committee in LDS, winners, rewards on the u32 "
-                                "balance offsets, next-cycle sum); device time of the whole step" if one_pass else
+                     "kernel": ("epoch step: pz_epoch_window_b32_s16 (ONE launch: the bit count shared by an "
+                                "instance's blocks, the last bitfield into LDS by DMA, per-instance committee pieces "
+                                "with their vote bits read beside the stream, classify, crosslink tallies per "
+                                "committee in LDS, winners, rewards on the u32 balance offsets, next-cycle sum); "
+                                "device time of the whole step" if one_pass else
                                 "epoch step (count+winner+compact+reward, device time of the whole step)"),
                      "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": local_units * bpv},
@@ -765,7 +767,8 @@ def wire_att_leg(args, torch, dist, dev, rank, world, d_digests):
                      "frac": alg / (ms_e * 1e-3) / HBM_PEAK,
                      "traffic": pmc_traffic(["pz_wire_att_size_kernel", "pz_wire_att_write_kernel"]),
                      "traffic_source": PMC_SUMMARY,
-                     "kernel": "pz_wire_att_size_kernel + scan + pz_wire_att_write_kernel (device time of the encode)",
+                     "kernel": ("pz_wire_att_size_kernel (sizes, tile scan, decoupled look-back) + "
+                                "pz_wire_att_write_kernel (device time of the encode)"),
                      "step_device_ms": ms_e, "encode_hash_device_ms": ms_eh, "algorithmic_bytes_per_launch": alg},
     }
     if d_digests is not None:

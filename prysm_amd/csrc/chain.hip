@@ -2453,8 +2453,8 @@ static uint64_t parse_range(const uint8_t* data, const uint64_t* offs, uint64_t 
   return b1;
 }
 
-// Threads for the parse of a call of `bytes` input bytes: PZ_PARSE_THREADS (default 16, the
-// CPU share of one GPU on the bench boxes), one per 512 KB (10,000 blocks: 1.76 ms on 8,
+// Threads for the parse of a call of `bytes` input bytes: at most pz_set_host_threads (the
+// bench boxes' CPU share of one GPU is 16), one per 512 KB (10,000 blocks: 1.76 ms on 8,
 // 1.22 ms on 16, profiles/r03/parse_probe_after_r3at.txt).
 static int parse_threads(uint64_t bytes) {
   const uint64_t cap = host_threads();  // (pz_set_host_threads)

@@ -151,19 +151,21 @@ struct FusedArgs {
   const uint64_t* bal32_base;
 };
 // ---- the window pass (epoch_window.hip): the one-pass step of B instances in ONE launch ------
-// Block (instance, range): a range is a run of this rank's committees (local ids [cr0, cr1),
-// positions [lcs[cr0], lcs[cr1])), so every committee's tallies complete inside one block.
+// Block (instance, range): a range is a run of this rank's committees (local ids [cr0, cr1)),
+// so every committee's tallies complete inside one block.
 constexpr int kWinThreads = 1024, kWinDepth = 2, kWinDepth16 = 2;  // (pieces in flight per wave: 3 measured slower, r5f)
 struct WinArgs {
-  const uint4* rdesc;         // [R][2] {cr0, cr1, first piece (pdesc index), pieces}, {P0, P1, 0, 0}
+  const uint4* rdesc;         // [R] {cr0, cr1, first piece, pieces}
   uint32_t R;                 // ranges per instance (grid: B x R blocks)
-  const uint2* pdesc;         // [pieces] {first position, (committee << 9) | positions}: <= 256
-                              //   positions of one committee, from its first position rounded down to 4
-  const uint32_t* lcs;        // [nlc + 1] local committee starts (local positions; lcs[nlc] = nval)
-  const uint4* lci;           // [B][nlc + 1] {bitfield offset lo, hi (its single attestation),
-                              //   attestation index | kNoAtt | kManyAtt, first catt index}
-  const uint32_t* lnb;        // [B][nlc] single-attestation committees: min(size, 8 * bitfield bytes)
-  uint32_t nlc;
+  // [B][ptot][2] per instance and piece (<= 256 positions of one committee, from its first
+  // position rounded down to 4): {first position, positions, committee - cr0, kind (0 no
+  // attestation, 1 one, 2 several)}, {its first catt index, the bit of the first position in
+  // the single attestation's bitfield counted from the instance's bitfields (kind 1; kind 2:
+  // the committee's first position), vote bits present from the first position, 0}
+  const uint4* pinfo;
+  uint32_t ptot;
+  const uint2* rk;            // [B][R] {the range's first catt index, its attestations}
+  uint32_t cg0;               // the rank's first committee (global id)
   const uint32_t* catt;       // [B][natt] attestation indices grouped by committee (committee order)
   const uint32_t* att_csize;  // [B][natt] the size of each attestation's committee
   const uint4* att_win;       // [B][natt] {shard (< nrec), its record's dynasty lo, hi, 0}
@@ -176,14 +178,14 @@ struct WinArgs {
   uint64_t* vote_next;        // world > 1: [B][natt] the next step's tallies zeroed (non-owned
   uint64_t* total_next;       //   attestations stay zero for pz_epoch_state_tallies' sum), else NULL
   int rank0;                  // this rank writes the per-instance scalars
-  // LDS plan: last-bitfield bytes (0: reward bits from L2), vote-bit words, most committees /
-  // attestations of a range, 32-bit words per committee bitfield (the vote-bit placement's items)
-  uint32_t lds_lbf, lds_vw, lds_maxc, lds_maxk, wpc;
+  // LDS plan: last-bitfield bytes (0: reward bits from L2), most committees / attestations of a range
+  uint32_t lds_lbf, lds_maxc, lds_maxk;
   uint64_t* trace;            // A/B library only: [blocks][4] phase stamps (s_memrealtime), else NULL
-  // R > 1: the R blocks of an instance each count 1/R of its bitfields and meet in one 64-bit
-  // word per instance, {arrivals << 48 | length-panic blocks << 39 | bits}, this step's pacc and
-  // the next step's pacc_next (zeroed by the r == 0 blocks; the two swap every step).  A block
-  // whose partners have not all arrived within kCoopSpinTicks counts everything itself.
+  // A/B form (epoch_window.hip AB & 16), R > 1: the R blocks of an instance each count 1/R of
+  // its bitfields and meet in one 64-bit word per instance, {arrivals << 48 | length-panic
+  // blocks << 39 | bits}, this step's pacc and the next step's pacc_next (zeroed by the r == 0
+  // blocks; the two swap every step).  A block whose partners have not all arrived within
+  // kCoopSpinTicks counts everything itself.
   uint64_t* pacc;
   uint64_t* pacc_next;
 };

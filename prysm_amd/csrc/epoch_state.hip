@@ -530,7 +530,9 @@ void local_committees(const pz_epoch_host* h, uint64_t lo, uint64_t hi, bool kee
 // The window pass's plan for one part of one rank (epoch.h WinArgs): the rank's committees
 // (those whose first position lies in [lo, hi); the last rank also takes the empty ones at N)
 // split into R ranges of about equal positions, R = CUs / B (one block per CU), each range's
-// committee pieces, the per-instance committee table, and the LDS carve-up.  The last bitfield goes into LDS when the block still fits the CU's 160 KiB.
+// committee pieces with, per instance, the piece's committee and attestation facts (so the
+// kernel reads them beside the stream: no committee table, no vote bitmap), and the LDS
+// carve-up.  The last bitfield goes into LDS when the block still fits the CU's 160 KiB.
 static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Part& q, const std::vector<uint32_t>& catt_offs,
                 const std::vector<uint32_t>& catt) {
   const uint64_t Bp = q.B, i0 = q.i0, natt = st->natt, nc1 = st->ncomm + 1, N = st->N;
@@ -540,35 +542,19 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
   const uint32_t nlc = (uint32_t)(cg1 - cg0);
   std::vector<uint32_t> lcs(nlc + 1);
   for (uint32_t k = 0; k <= nlc; ++k) lcs[k] = (uint32_t)((k < nlc ? coffs[cg0 + k] : s.hi) - s.lo);
-  // per instance: committee table, single-attestation bit counts, attestation columns
-  std::vector<uint4> lci((size_t)Bp * (nlc + 1));
-  std::vector<uint32_t> lnb((size_t)Bp * std::max<uint32_t>(nlc, 1), 0), csz((size_t)Bp * natt);
+  // per instance: the attestation columns
+  std::vector<uint32_t> csz((size_t)Bp * natt);
   std::vector<uint4> aw((size_t)Bp * natt);
-  uint32_t wpc = 1;
   for (uint64_t b = 0; b < Bp; ++b) {
-    const uint32_t* o = catt_offs.data() + (i0 + b) * nc1;
     const uint64_t gb = (i0 + b) * natt;
-    for (uint32_t k = 0; k <= nlc; ++k) {
-      const uint64_t c = cg0 + k;
-      uint4 e = make_uint4(0, 0, kNoAtt, o[c]);
-      if (k < nlc && o[c + 1] - o[c] == 1) {
-        const uint32_t g = catt[(i0 + b) * natt + o[c]];
-        const uint64_t bo = h->boffs[gb + g], blen = h->boffs[gb + g + 1] - bo;
-        e = make_uint4((uint32_t)bo, (uint32_t)(bo >> 32), g, o[c]);
-        const uint64_t nb = std::min<uint64_t>(coffs[c + 1] - coffs[c], 8 * blen);
-        lnb[b * nlc + k] = (uint32_t)nb;
-        wpc = std::max<uint32_t>(wpc, (uint32_t)((nb + 31) / 32));
-      } else if (k < nlc && o[c + 1] - o[c] > 1) {
-        e.z = kManyAtt;
-      }
-      lci[b * (nlc + 1) + k] = e;
-    }
     for (uint64_t g = 0; g < natt; ++g) {
       const uint32_t c = h->att_comm[gb + g], sh = h->att_shard[gb + g];  // (sh < nrec: plan_layout)
       csz[b * natt + g] = (uint32_t)(coffs[c + 1] - coffs[c]);
       const uint64_t rd = h->rec_dynasty[(i0 + b) * st->nrec + sh];
       aw[b * natt + g] = make_uint4(sh, (uint32_t)rd, (uint32_t)(rd >> 32), 0);
     }
+    if (h->boffs[gb + natt] - (h->boffs[gb] & ~15ull) >= (1ull << 28))
+      return fail(PZ_EINVAL, "window pass: an instance's bitfields exceed 256 MiB");
   }
   // the last bitfield's LDS copy: from (lb & ~15) to the instance's end, 16-B chunks
   uint64_t lbf = 0;
@@ -580,15 +566,15 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.dev);
   uint32_t R = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::max<uint32_t>(nlc, 1), ((uint64_t)cus + Bp - 1) / Bp));
   std::vector<uint4> rdesc;
-  std::vector<uint2> pdesc;
+  std::vector<uint4> pieces;  // {first position, positions, committee (local), range}
   WinArgs& w = q.w;
   std::memset(&w, 0, sizeof w);
   constexpr size_t kLdsMax = 160 * 1024 - 1024;  // (the kernel's static reduction slots)
-  if (nlc >= (1u << 23)) return fail(PZ_EINVAL, "window pass: more than 2^23 committees on a rank");
+  auto catt_at = [&](uint64_t b, uint64_t c) { return catt_offs[(i0 + b) * nc1 + c]; };
   for (;;) {
-    rdesc.assign(2 * (size_t)R, make_uint4(0, 0, 0, 0));
-    pdesc.clear();
-    uint32_t c = 0, maxc = 0, maxk = 0, maxw = 0;
+    rdesc.assign(R, make_uint4(0, 0, 0, 0));
+    pieces.clear();
+    uint32_t c = 0, maxc = 0, maxk = 0;
     for (uint32_t r = 0; r < R; ++r) {
       const uint64_t t = (uint64_t)lcs[nlc] * (r + 1) / R;
       uint32_t c1 = c;
@@ -598,33 +584,26 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
         while (c1 < nlc && lcs[c1 + 1] <= t) ++c1;
         if (c1 == c && c1 < nlc) ++c1;  // at least one committee per range while they last
       }
-      const uint64_t P0 = lcs[c], P1 = lcs[c1], P0a = P0 & ~3ull;
-      const uint32_t pb = (uint32_t)pdesc.size();
+      const uint32_t pb = (uint32_t)pieces.size();
       // pieces: a committee's first from its first position to the next 256 boundary after its
       // rounded-down start, then 256-position runs from 4-aligned starts
       for (uint32_t cc = c; cc < c1; ++cc) {
         const uint64_t cs = lcs[cc], ce = lcs[cc + 1];
         for (uint64_t ps = cs; ps < ce;) {
           const uint64_t pe = std::min<uint64_t>(ce, (ps & ~3ull) + 256);
-          pdesc.push_back(make_uint2((uint32_t)ps, (cc << 9) | (uint32_t)(pe - ps)));
+          pieces.push_back(make_uint4((uint32_t)ps, (uint32_t)(pe - ps), cc, r));
           ps = pe;
         }
       }
-      rdesc[2 * r] = make_uint4(c, c1, pb, (uint32_t)pdesc.size() - pb);
-      rdesc[2 * r + 1] = make_uint4((uint32_t)P0, (uint32_t)P1, 0, 0);
+      rdesc[r] = make_uint4(c, c1, pb, (uint32_t)pieces.size() - pb);
       maxc = std::max(maxc, c1 - c);
-      // vote-bit words: the range's positions from P0a, plus a piece's overhang past P1 and the
-      // placement's spill word
-      maxw = std::max<uint32_t>(maxw, (uint32_t)((P1 - P0a + 31) / 32) + 10);
-      for (uint64_t b = 0; b < Bp; ++b)
-        maxk = std::max(maxk, lci[b * (nlc + 1) + c1].w - lci[b * (nlc + 1) + c].w);
+      for (uint64_t b = 0; b < Bp; ++b) maxk = std::max(maxk, catt_at(b, cg0 + c1) - catt_at(b, cg0 + c));
       c = c1;
     }
     w.R = R;
     w.lds_maxc = std::max<uint32_t>(maxc, 1);
-    w.lds_maxk = (std::max<uint32_t>(maxk, 1) + 1) & ~1u;  // (keeps the byte arrays after it 16-B aligned)
-    w.lds_vw = (maxw + 3) & ~3u;
-    w.wpc = wpc;
+    w.lds_maxk = std::max<uint32_t>(maxk, 1);
+    if ((w.lds_maxc + w.lds_maxk) & 1) ++w.lds_maxk;  // (keeps the last bitfield's copy 16-B aligned)
     w.lds_lbf = (uint32_t)lbf;
     if (window_lds_bytes(w) <= kLdsMax) break;
     w.lds_lbf = 0;  // the reward bits looked up in L2 instead
@@ -632,34 +611,58 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
     if (R >= nlc) return fail(PZ_EINVAL, "window pass: no range split fits the LDS");
     R = std::min<uint32_t>(nlc, 2 * R);
   }
-  pdesc.push_back(make_uint2(0, 0));  // (an empty last range's first descriptor load stays in bounds)
-  uint4 *d_rdesc = nullptr, *d_lci = nullptr, *d_aw = nullptr;
-  uint2* d_pdesc = nullptr;
-  uint32_t *d_lcs = nullptr, *d_lnb = nullptr, *d_csz = nullptr, *d_wn = nullptr;
+  pieces.push_back(make_uint4(0, 0, 0, 0));  // (an empty last range's first descriptor load stays in bounds)
+  const uint32_t ptot = (uint32_t)pieces.size();
+  // per instance and piece (epoch.h WinArgs.pinfo) and per instance and range (WinArgs.rk)
+  std::vector<uint4> pinfo(2 * (size_t)Bp * ptot, make_uint4(0, 0, 0, 0));
+  std::vector<uint2> rk((size_t)Bp * R);
+  for (uint64_t b = 0; b < Bp; ++b) {
+    const uint64_t gb = (i0 + b) * natt, pbase = h->boffs[gb] & ~15ull;
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t k0 = catt_at(b, cg0 + rdesc[r].x);
+      rk[b * R + r] = make_uint2(k0, catt_at(b, cg0 + rdesc[r].y) - k0);
+    }
+    for (uint32_t k = 0; k + 1 < ptot; ++k) {
+      const uint4 pc = pieces[k];
+      const uint32_t cc = pc.z, cr0 = rdesc[pc.w].x;
+      const uint64_t c = cg0 + cc, cs = lcs[cc];
+      const uint32_t na = catt_at(b, c + 1) - catt_at(b, c), kb = catt_at(b, c);
+      const uint32_t kind = na == 0 ? 0 : na == 1 ? 1 : 2;
+      uint32_t vbit = 0, vlim = 0;
+      if (kind == 1) {  // the single attestation's bitfield: bit (position - cs), MSB first
+        const uint32_t g = catt[(i0 + b) * natt + kb];
+        const uint64_t bo = h->boffs[gb + g], blen = h->boffs[gb + g + 1] - bo;
+        const uint64_t nb = std::min<uint64_t>(coffs[c + 1] - coffs[c], 8 * blen);
+        vbit = (uint32_t)(8 * (bo - pbase) + (pc.x - cs));
+        vlim = (uint32_t)std::min<uint64_t>(pc.y, nb > pc.x - cs ? nb - (pc.x - cs) : 0);
+      } else if (kind == 2) {  // the per-attestation path: the committee's start and attestations' end
+        vbit = (uint32_t)cs;
+        vlim = catt_at(b, c + 1);
+      }
+      pinfo[2 * (b * ptot + k)] = make_uint4(pc.x, pc.y, cc - cr0, kind);
+      pinfo[2 * (b * ptot + k) + 1] = make_uint4(kb, vbit, vlim, 0);
+    }
+  }
+  uint4 *d_rdesc = nullptr, *d_aw = nullptr, *d_pinfo = nullptr;
+  uint2* d_rk = nullptr;
+  uint32_t *d_csz = nullptr, *d_wn = nullptr;
   uint64_t* d_pacc = nullptr;
   int rc;
-  if ((rc = upload(s, &d_rdesc, rdesc.data(), rdesc.size())) || (rc = upload(s, &d_pdesc, pdesc.data(), pdesc.size())) ||
-      (rc = upload(s, &d_lcs, lcs.data(), lcs.size())) || (rc = upload(s, &d_lci, lci.data(), lci.size())) ||
-      (rc = upload(s, &d_lnb, lnb.data(), lnb.size())) || (rc = upload(s, &d_csz, csz.data(), csz.size())) ||
+  if ((rc = upload(s, &d_rdesc, rdesc.data(), rdesc.size())) || (rc = upload(s, &d_pinfo, pinfo.data(), pinfo.size())) ||
+      (rc = upload(s, &d_rk, rk.data(), rk.size())) || (rc = upload(s, &d_csz, csz.data(), csz.size())) ||
       (rc = upload(s, &d_aw, aw.data(), aw.size())) ||
       (rc = dalloc(s, &d_wn, (size_t)Bp * std::max<uint32_t>(st->nrec, 1))) || (rc = dalloc(s, &d_pacc, 2 * (size_t)Bp)))
     return rc;
   // the meeting word's fields (epoch.h WinArgs.pacc): bits below 2^39, at most 511 blocks
-  bool meet = R > 1 && R <= 511;
-  for (uint64_t b = 0; b < Bp && meet; ++b) {
-    const uint64_t gb = (i0 + b) * natt;
-    meet = 8 * (h->boffs[gb + natt] - h->boffs[gb]) < (1ull << 39);
-  }
-  if (meet) {
+  if (R > 1 && R <= 511) {
     w.pacc = d_pacc;
     w.pacc_next = d_pacc + Bp;
   }
   w.rdesc = d_rdesc;
-  w.pdesc = d_pdesc;
-  w.lcs = d_lcs;
-  w.lci = d_lci;
-  w.lnb = d_lnb;
-  w.nlc = nlc;
+  w.pinfo = d_pinfo;
+  w.ptot = ptot;
+  w.rk = d_rk;
+  w.cg0 = (uint32_t)cg0;
   w.catt = q.f.catt;
   w.att_csize = d_csz;
   w.att_win = d_aw;
@@ -822,7 +825,9 @@ int pz_epoch_state_new_opts(pz_comm* comm, int device, const pz_epoch_host* h, c
         offs.assign(h->coffs, h->coffs + h->ncomm + 1);
       }
       const uint64_t na = (uint64_t)st->B * st->natt;
-      if ((rc = dalloc(s, &bits, nb_total + 16)) || (rc = upload_into(bits, h->bits, nb_total)) ||
+      // (16 B before and after the bitfields: the window pass's vote-bit loads reach up to 4 B
+      // before an instance's first bitfield, the 16-B loads up to 15 B past the last)
+      if ((rc = dalloc(s, &bits, nb_total + 32)) || (rc = upload_into(bits + 16, h->bits, nb_total)) ||
           (rc = upload(s, &boffs, h->boffs, na + 1)) || (rc = upload(s, &committee, mem.data(), mem.size())) ||
           (rc = upload(s, &coffs, offs.data(), offs.size())) || (rc = upload(s, &att_comm, h->att_comm, na)) ||
           (rc = upload(s, &att_shard, h->att_shard, na)))
@@ -901,7 +906,7 @@ int pz_epoch_state_new_opts(pz_comm* comm, int device, const pz_epoch_host* h, c
       a.total_deposit = tdep + i0;
       a.natt = st->natt;
       if (st->natt) {
-        a.bits = bits;
+        a.bits = bits + 16;
         a.boffs = boffs + i0 * st->natt;
         a.max_inst_bytes = max_inst_bytes;
         a.committee = committee;

@@ -4,32 +4,30 @@
 // round trips (piece descriptor -> stream -> reward-bit lookups through L2) and ran the
 // 1M x 16 cold step at 0.36 of 8 TB/s.
 //
-// Block (instance i, range r): the committees [cr0, cr1) of this rank, a contiguous run of
-// storage positions [P0, P1) (committee order: committee c is positions [lcs[c], lcs[c+1])).
-// The ranges partition the committees, so every committee's tallies are complete inside ONE
-// block: they are summed in LDS and leave with plain stores, and the block applies the winner
-// rule (core.go:549-555) itself -- no tally atomics to HBM, no winner pass.
+// Block (instance i, range r): the committees [cr0, cr1) of this rank, whose positions are
+// contiguous (committee order).  The ranges partition the committees, so every committee's
+// tallies are complete inside ONE block: they are summed in LDS and leave with plain stores,
+// and the block applies the winner rule (core.go:549-555) itself -- no tally atomics to HBM,
+// no winner pass.
 //
-//   prologue  the first pieces' loads go out before anything else; then, with them in flight:
-//             GetAttestersTotalDeposit (validator.go:93-102) as a bit count over every
-//             bitfield of the instance (each block counts them: nothing precedes the launch),
-//             whose last bitfield (CalculateRewards reads it by validator index,
-//             incentives.go:22-27) is copied into LDS on the way; the bitfield-length panics
-//             (core.go:538-541); the range's committee bitfields placed in position order in
-//             an LDS bitmap (the vote bits of single-attestation committees).  The loads of a
-//             round -- bit-count chunks, length checks, committee table -- go out together.
+//   prologue  the first pieces' loads go out first; then GetAttestersTotalDeposit
+//             (validator.go:93-102) as a bit count over every bitfield of the instance (each
+//             block counts them: nothing precedes the launch) with the last bitfield
+//             (CalculateRewards reads it by validator index, incentives.go:22-27) copied into
+//             LDS by DMA, and the bitfield-length panics (core.go:538-541)
 //   loop      committee pieces (<= 256 positions of ONE committee, from its first position
-//             rounded down to 4): lane l takes 4 contiguous positions, every column load 16 B
-//             per lane, each wave kWinDepth(16) pieces ahead (descriptors one round further); the
-//             reward bit of position p is bit co_index[p] of the LDS copy; the crosslink tallies
-//             (core.go:533-545) of the piece's committee are four 32-bit DPP wave sums of the
-//             pre-reward u32 balance offsets (low 15 bits with the count above them, high 17
-//             bits), added into LDS
+//             rounded down to 4), each with its per-instance descriptor (committee, attestation
+//             kind, the single attestation's bitfield position): lane l takes 4 contiguous
+//             positions, every column load 16 B per lane plus 8 B of the committee's bitfield
+//             holding the 4 vote bits, kWinDepth pieces ahead; the reward bit of position p is
+//             bit co_index[p] of the LDS copy; the crosslink tallies (core.go:533-545) are four
+//             32-bit DPP wave sums of the pre-reward u32 balance offsets (low 15 bits with the
+//             count above them, high 17 bits), added into LDS
 //   epilogue  every attestation of the range: vote / total stored, the winner rule as an
 //             atomicMin on its shard; the block's next-cycle partial sum (core.go:459-464)
 //             as one atomic
 //
-// Committees with several attestations (kManyAtt) take a slower in-loop path per attestation
+// Committees with several attestations (kind 2) take a slower in-loop path per attestation
 // (its bitfield bytes from global memory); committees without one add nothing.
 #include <hip/hip_runtime.h>
 
@@ -64,18 +62,20 @@ __device__ __forceinline__ uint32_t wsum32(uint32_t x) {
 
 // One piece's column words per lane: the balances of its 4 positions (u32 offsets: one 16-B
 // load; u64: two), their {start, end} bounds (16-bit pairs: one load; 32-bit pairs: two; the
-// 64-bit columns: four) and their co_index entries.
+// 64-bit columns: four), their co_index entries, and 8 bytes of the committee's bitfield
+// holding their 4 vote bits.
 template <bool B32, int SEW>
 struct WinCols {
   uint4 b[B32 ? 1 : 2];
   uint4 s[SEW == 16 ? 1 : SEW == 32 ? 2 : 4];
   uint4 ci;
+  uint2 vb;
 };
 
-// piece descriptor: {first position, (committee << 9) | positions}
-__device__ __forceinline__ uint32_t pc_start(uint2 d) { return d.x; }
-__device__ __forceinline__ uint32_t pc_count(uint2 d) { return d.y & 511u; }
-__device__ __forceinline__ uint32_t pc_comm(uint2 d) { return d.y >> 9; }
+// A piece of one instance (WinArgs.pinfo), wave-uniform
+struct Piece {
+  uint32_t s0, cnt, cl, kind, kb, vbit, vlim;
+};
 
 // The instance's columns (wave-uniform bases: the loads take a 32-bit per-lane offset)
 struct WinCol {
@@ -86,12 +86,17 @@ struct WinCol {
   const uint64_t* start;
   const uint64_t* end;
   const uint32_t* ci;
+  const uint8_t* vbits;  // the instance's bitfields from its 16-B aligned start (vbit counts from here)
 };
 
+// the bit of the lane's first position in the piece's bitfield (kind 1; may precede the
+// bitfield by up to 3 bits when the piece starts mid-quad: the buffer has 16 B before it)
+__device__ __forceinline__ int64_t vbit_of(const Piece& d, uint32_t p) { return (int64_t)d.vbit + (int64_t)p - d.s0; }
+
 template <bool B32, int SEW>
-__device__ __forceinline__ void win_load(const WinCol& c, uint2 d, uint32_t lane, WinCols<B32, SEW>& x) {
-  const uint32_t s0 = pc_start(d), pa = s0 & ~3u, p = pa + 4 * lane;
-  const bool any = p + 3 >= s0 && p < s0 + pc_count(d);
+__device__ __forceinline__ void win_load(const WinCol& c, const Piece& d, uint32_t lane, WinCols<B32, SEW>& x) {
+  const uint32_t pa = d.s0 & ~3u, p = pa + 4 * lane;
+  const bool any = p + 3 >= d.s0 && p < d.s0 + d.cnt;
   const uint32_t pp = any ? p : pa;  // (a lane wholly outside the piece re-reads the first quad)
   if (B32) {
     x.b[0] = *reinterpret_cast<const uint4*>(c.bal32 + pp);
@@ -112,6 +117,21 @@ __device__ __forceinline__ void win_load(const WinCol& c, uint2 d, uint32_t lane
     x.s[SEW == 64 ? 3 : 0] = ldnt16(c.end + pp + 2);
   }
   x.ci = *reinterpret_cast<const uint4*>(c.ci + pp);
+  // the 4 vote bits sit in bytes j / 8 and j / 8 + 1 (j = the first position's bit): 8 bytes
+  // from the dword below them (unused for kind != 1, and then from the region's start)
+  const int64_t j = d.kind == 1 ? vbit_of(d, pp) : 0;
+  const int64_t byte = j >> 3;  // (arithmetic: down to -1)
+  __builtin_memcpy(&x.vb, __builtin_assume_aligned(c.vbits + (byte & ~3ll), 4), 8);
+}
+
+// the lane's 4 vote bits, position i -> bit i (CheckBit, utils/checkbit.go:4-12: bit j of a
+// bitfield is bit 7 - j % 8 of byte j / 8)
+__device__ __forceinline__ uint32_t vote4(const Piece& d, uint32_t p, uint2 raw) {
+  const int64_t j = vbit_of(d, p);
+  const uint32_t sh = (uint32_t)((j >> 3) & 3) * 8, jb = (uint32_t)(j & 7);
+  const uint64_t w8 = pk64(raw.x, raw.y) >> sh;
+  const uint32_t u16 = ((uint32_t)(w8 & 0xFF) << 8) | (uint32_t)((w8 >> 8) & 0xFF);  // bytes j/8, j/8+1, MSB first
+  return __builtin_bitreverse32((u16 >> (12 - jb)) & 0xFu) >> 28;
 }
 
 // validator.go:45-53 on position i of the lane's quad (the saturated bounds classify exactly:
@@ -137,51 +157,28 @@ __device__ __forceinline__ bool win_active(const WinCols<B32, SEW>& x, int i, ui
 
 // LDS carve-up of one block (bytes; WinArgs.lds_* from the host's plan)
 struct WinLds {
-  uint8_t* lbf;     // [lds_lbf] the instance's last bitfield from (lb & ~15)
-  uint32_t* vb;     // [lds_vw] vote bits of the range, position order from P0 & ~3
-  uint32_t* cst;    // [maxc + 1] committee starts relative to P0 & ~3
-  uint32_t* kbg;    // [maxc + 1] each committee's first attestation (index into catt)
-  uint64_t* cbo;    // [maxc] single-attestation committees: bitfield offset
-  uint32_t* cnb;    // [maxc] ... and its bits (min(committee size, 8 * bitfield length))
-  uint8_t* kd;      // [maxc] 0 no attestation, 1 one, 2 several
   uint64_t* tot;    // [maxc] committee totals
   uint64_t* vot;    // [maxk] vote per attestation (catt index - the range's first)
+  uint8_t* lbf;     // [lds_lbf] the instance's last bitfield from (lb & ~15)
 };
 
 __device__ __forceinline__ WinLds win_lds(uint8_t* base, const WinArgs& w) {
   WinLds L;
-  uint8_t* p = base;
-  L.tot = reinterpret_cast<uint64_t*>(p);
-  p += 8ull * w.lds_maxc;
-  L.vot = reinterpret_cast<uint64_t*>(p);
-  p += 8ull * w.lds_maxk;
-  L.cbo = reinterpret_cast<uint64_t*>(p);
-  p += 8ull * w.lds_maxc;
-  L.lbf = p;  // 16-B aligned: every size above is a multiple of 8, and lds_maxc + lds_maxk is even
-  p += w.lds_lbf;
-  L.vb = reinterpret_cast<uint32_t*>(p);
-  p += 4ull * w.lds_vw;
-  L.cst = reinterpret_cast<uint32_t*>(p);
-  p += 4ull * (w.lds_maxc + 1);
-  L.kbg = reinterpret_cast<uint32_t*>(p);
-  p += 4ull * (w.lds_maxc + 1);
-  L.cnb = reinterpret_cast<uint32_t*>(p);
-  p += 4ull * w.lds_maxc;
-  L.kd = p;
+  L.tot = reinterpret_cast<uint64_t*>(base);
+  L.vot = L.tot + w.lds_maxc;
+  L.lbf = reinterpret_cast<uint8_t*>(L.vot + w.lds_maxk);  // (16-B aligned: lds_maxc + lds_maxk is even)
   return L;
 }
 
-size_t window_lds_bytes(const WinArgs& w) {
-  return 8ull * (2 * (size_t)w.lds_maxc + w.lds_maxk) + w.lds_lbf + 4ull * w.lds_vw + 4ull * (3 * (size_t)w.lds_maxc + 2) +
-         w.lds_maxc + 16;
-}
+size_t window_lds_bytes(const WinArgs& w) { return 8ull * ((size_t)w.lds_maxc + w.lds_maxk) + w.lds_lbf + 16; }
 
 // AB: measurement ablations, instantiated only in the A/B library (results wrong for AB != 0
-// except 16): 1 no crosslink tallies, 2 no bit count / length checks in the prologue (applied
-// taken as true), 4 no reward-bit lookups, 8 no vote-bit placement, 16 every block counts
-// everything (no meeting of the R blocks; exact), 32 the meeting's wait bound at zero (the
-// fallback count in every block that arrives before its partners; exact), 64 the first pieces'
-// loads issued after the prologue (exact), 80 = 64 + 16.
+// except 16, 48, 64): 1 no crosslink tallies, 2 no bit count / length checks in the prologue
+// (applied taken as true), 4 no reward-bit lookups, 16 the R blocks of an instance each count
+// 1/R of its bitfields and meet in WinArgs.pacc (exact; measured 2 us slower at 1M x 16 than
+// every block counting everything, profiles/r05/epoch_abl_window_v4_r5h.txt), 48 = 16 with the
+// meeting's wait bound at zero (the fallback count in every block that arrives before its
+// partners; exact), 64 the first pieces' loads issued after the prologue (exact).
 template <bool B32, int SEW, bool LLB, int AB = 0, int D = kWinDepth, bool TR = false>
 __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w) {
   extern __shared__ __align__(16) uint8_t lds_dyn[];
@@ -193,28 +190,41 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   if (TR && tid == 0) tstamp[0] = __builtin_amdgcn_s_memrealtime();
   const uint64_t inst = blockIdx.x / w.R;
   const uint32_t r = blockIdx.x - (uint32_t)inst * w.R;
-  const uint4 rd = w.rdesc[2 * r], re = w.rdesc[2 * r + 1];
+  const uint4 rd = w.rdesc[r];
   const uint32_t cr0 = rd.x, cr1 = rd.y, pb = rd.z, np = rd.w;
-  const uint64_t P0 = re.x, P0a = P0 & ~3ull;
+  const uint2 rkk = w.rk[inst * w.R + r];
+  const uint32_t k0 = rkk.x, nk = rkk.y;  // the range's attestations: catt[k0, k0 + nk)
+  const uint64_t gb = inst * a.natt;
+  const uint64_t pbeg = a.boffs[gb], pend = a.boffs[gb + a.natt], lb = a.boffs[gb + a.natt - 1];
+  const uint64_t pbase = pbeg & ~15ull, lbase = lb & ~15ull;
   // The wave's pieces go round by round, slot j of round t being piece t * D * NW + j * NW +
-  // wave; past the range's end a slot takes a dummy (the last piece's descriptor with no
-  // positions), so every load below is issued unconditionally and the loop's waits count
-  // exactly the loads in flight.  Lane l loads the descriptor of slot l % D: one load a round.
+  // wave; past the range's end a slot takes a dummy (the last piece with no positions), so
+  // every load below is issued unconditionally and the loop's waits count exactly the loads in
+  // flight.  Lanes 2j, 2j + 1 load slot j's two descriptor words: one load a round.
   const uint32_t npm = np ? np - 1 : 0, nround = (np + D * NW - 1) / (D * NW);
-  const uint32_t dslot = wave + (uint32_t)(lane % D) * NW;
-  auto desc = [&](uint32_t rnd) {  // this lane's slot's descriptor for round rnd
+  const uint32_t dslot = wave + (uint32_t)((lane >> 1) % D) * NW;
+  const uint4* pinfo = w.pinfo + 2 * (inst * w.ptot + pb);
+  auto desc = [&](uint32_t rnd) {  // this lane's word of its slot's descriptor for round rnd
     const uint32_t k = rnd * D * NW + dslot;
-    uint2 x = w.pdesc[pb + min(k, npm)];
-    if (k >= np) x.y &= ~511u;  // (a dummy: no positions)
+    uint4 x = pinfo[2 * min(k, npm) + (lane & 1)];
+    if (k >= np && !(lane & 1)) x.y = 0;  // (a dummy: no positions)
     return x;
   };
-  uint2 dv = desc(0);
-  uint2 dq[D];
+  auto piece = [&](const uint4& x, int j) {
+    Piece d;
+    d.s0 = __builtin_amdgcn_readlane(x.x, 2 * j), d.cnt = __builtin_amdgcn_readlane(x.y, 2 * j);
+    d.cl = __builtin_amdgcn_readlane(x.z, 2 * j), d.kind = __builtin_amdgcn_readlane(x.w, 2 * j);
+    d.kb = __builtin_amdgcn_readlane(x.x, 2 * j + 1), d.vbit = __builtin_amdgcn_readlane(x.y, 2 * j + 1);
+    d.vlim = __builtin_amdgcn_readlane(x.z, 2 * j + 1);
+    return d;
+  };
+  uint4 dv = desc(0);
+  Piece dq[D];
 #pragma unroll
-  for (int j = 0; j < D; ++j) dq[j] = make_uint2(__builtin_amdgcn_readlane(dv.x, j), __builtin_amdgcn_readlane(dv.y, j));
+  for (int j = 0; j < D; ++j) dq[j] = piece(dv, j);
   const uint64_t vrow = inst * w.vstride;
   const WinCol col{w.bal32 + vrow, a.balance + vrow, w.se16 + vrow, w.se + vrow, a.start + vrow, a.end + vrow,
-                   a.co_index};
+                   a.co_index, a.bits + pbase};
   WinCols<B32, SEW> q[D];
   if (!(AB & 64)) {
 #pragma unroll
@@ -223,35 +233,15 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   dv = desc(1);
   const WinLds L = win_lds(lds_dyn, w);
   const uint32_t ncr = cr1 - cr0;
-  const uint64_t gb = inst * a.natt;
-  const uint4* lci = w.lci + inst * (w.nlc + 1);
-  const uint64_t pbeg = a.boffs[gb], pend = a.boffs[gb + a.natt], lb = a.boffs[gb + a.natt - 1];
-  const uint64_t pbase = pbeg & ~15ull, lbase = lb & ~15ull;
-  const uint32_t k0 = lci[cr0].w, nk = lci[cr1].w - k0;  // the range's attestations: catt[k0, k0 + nk)
-  for (uint32_t i = tid; i < w.lds_vw; i += NT) L.vb[i] = 0;
   for (uint32_t i = tid; i < ncr; i += NT) L.tot[i] = 0;
   for (uint32_t i = tid; i < nk; i += NT) L.vot[i] = 0;
-  // the range's committees: starts, attestation kinds, their catt index and bitfields
-  for (uint32_t c = cr0 + tid; c <= cr1; c += NT) {
-    const uint4 ci = lci[c];
-    const uint32_t cs = w.lcs[c];
-    const uint32_t nb = c < cr1 ? w.lnb[inst * w.nlc + c] : 0;
-    const uint32_t cl = c - cr0;
-    L.cst[cl] = (uint32_t)(cs - P0a);
-    L.kbg[cl] = ci.w;
-    if (c < cr1) {
-      L.kd[cl] = ci.z == kNoAtt ? 0 : ci.z == kManyAtt ? 2 : 1;
-      L.cbo[cl] = pk64(ci.x, ci.y);
-      L.cnb[cl] = nb;
-    }
-  }
   // GetAttestersTotalDeposit (every bitfield's bits) and the bitfield-length panics.  The
   // region's 16-B chunks [0, nch) from pbase; the last bitfield's, [clb, nch), go into LDS by
   // DMA (no registers, 1 KiB per wave instruction) and are counted from there.  With R > 1 the
   // block counts only its share of the chunks and attestations and the R blocks meet in pacc.
   uint64_t pop = 0, err = 0;
   const uint64_t nch = (pend - pbase + 15) / 16, clb = LLB ? (lbase - pbase) / 16 : nch;
-  const bool coop = w.pacc != nullptr && w.R > 1 && !(AB & 16);
+  const bool coop = (AB & 16) && w.pacc != nullptr && w.R > 1;
   const uint64_t s0 = coop ? nch * r / w.R : 0, s1 = coop ? nch * (r + 1) / w.R : nch;
   const uint64_t g0s = coop ? (uint64_t)a.natt * r / w.R : 0, g1s = coop ? (uint64_t)a.natt * (r + 1) / w.R : a.natt;
   // bits of chunk c (its bytes inside [pbeg, pend) only)
@@ -323,41 +313,8 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   } else {
     pop = tid == 0 ? a.total_deposit[inst] : 0;  // (ablation: the threshold holds)
   }
-  __syncthreads();  // the committee table and the last bitfield are in LDS, the vote bits zeroed
+  __syncthreads();  // the last bitfield is in LDS, the tallies zeroed
   if (!(AB & 2)) count_lds(std::max(s0, clb), s1);
-  // the vote bits: (committee, 32-bit word) items, every load of a round in flight together
-  if (!(AB & 8)) {
-    const uint32_t wpc = w.wpc, items = ncr * wpc;
-    constexpr int U = 4;
-    const uint32_t nit = (items + U * NT - 1) / (U * NT);
-    for (uint32_t it = 0; it < nit; ++it) {  // (uniform; the table reads first, then every load)
-      uint32_t cst[U], nbl[U];
-      uint64_t ad[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t t = it * U * NT + u * NT + tid, cl = min(t, items - 1) / wpc, m = t - cl * wpc;
-        const bool ok = t < items && L.kd[cl] == 1 && 32 * m < L.cnb[cl];
-        nbl[u] = ok ? L.cnb[cl] - 32 * m : 0;
-        cst[u] = L.cst[cl] + 32 * m;
-        ad[u] = ok ? L.cbo[cl] + 4 * m : 0;  // (not taken: the buffer's first word)
-      }
-      uint64_t raw[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        __builtin_memcpy(&raw[u], __builtin_assume_aligned(a.bits + (ad[u] & ~3ull), 4), 8);  // (buffer padded by 16 B)
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (!nbl[u]) continue;
-        // bitfield bit j is bit 7 - j % 8 of byte j / 8 (CheckBit, utils/checkbit.go:4-12):
-        // byte-order kept, bits reversed within each byte -> bit j of the word
-        uint32_t W = __builtin_bitreverse32(__builtin_bswap32((uint32_t)(raw[u] >> ((ad[u] & 3) * 8))));
-        if (nbl[u] < 32) W &= (1u << nbl[u]) - 1u;
-        const uint32_t o = cst[u], sh = o & 31;
-        atomicOr(&L.vb[o >> 5], W << sh);
-        if (sh) atomicOr(&L.vb[(o >> 5) + 1], W >> (32 - sh));
-      }
-    }
-  }
   pop = wsum64_dpp(pop);
   err = wsum64_dpp(err);
   if (lane == 0) red[wave][0] = pop, red[wave][1] = err;
@@ -422,17 +379,17 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   uint32_t nact = 0, nm = 0;
   const uint32_t rwd = applied ? 1u : 0u;  // (not applied: the balances stay, offsets +- 0)
   for (uint32_t t = 0; t < nround; ++t) {
-    const uint2 dnx = dv;     // round t + 1's descriptors (loaded a round ago)
+    const uint4 dnx = dv;     // round t + 1's descriptors (loaded a round ago)
     dv = desc(t + 2);         // round t + 2's
 #pragma unroll
     for (int j = 0; j < D; ++j) {
       const WinCols<B32, SEW>& x = q[j];
-      const uint32_t s0 = pc_start(dq[j]), cnt = pc_count(dq[j]), cl = pc_comm(dq[j]) - cr0;
-      const uint32_t kind = rfl(L.kd[cl]), kb = rfl(L.kbg[cl]);  // (LDS, issued early)
-      const uint32_t pa = s0 & ~3u, p = pa + 4 * (uint32_t)lane, vloc = p - (uint32_t)P0a;
+      const Piece& pc = dq[j];
+      const uint32_t s0p = pc.s0, cnt = pc.cnt, cl = pc.cl, kind = pc.kind, kb = pc.kb;
+      const uint32_t pa = s0p & ~3u, p = pa + 4 * (uint32_t)lane;
       bool v[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = p + i - s0 < cnt;  // (u32: p + i < s0 wraps high)
+      for (int i = 0; i < 4; ++i) v[i] = p + i - s0p < cnt;  // (u32: p + i < s0 wraps high)
       uint32_t o4[4] = {0, 0, 0, 0};
       uint64_t b[4] = {0, 0, 0, 0};
       if (B32) {
@@ -453,7 +410,13 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       }
       // crosslink tallies of the piece's committee on the pre-reward balances (core.go:533-545)
       if (kind && !(AB & 1)) {
-        const uint32_t vw = (L.vb[vloc >> 5] >> (vloc & 31)) & 0xFu;
+        uint32_t vw = 0;  // vote bits present only below vlim (from the piece's first position)
+        if (kind == 1) {
+          vw = vote4(pc, p, x.vb);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (p + i - s0p >= pc.vlim) vw &= ~(1u << i);
+        }
         uint64_t T, V;
         if (B32) {
           // offsets split 17 | 15 bits: low parts with the count in bits 23+ (<= 256 x 2^15 < 2^23,
@@ -481,21 +444,20 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
           T = wsum64_dpp(tt);
           V = wsum64_dpp(vv);
         }
-        if (kind == 1) {
-          if (lane == 0) {
-            if (T) atomicAdd((unsigned long long*)&L.tot[cl], (unsigned long long)T);
-            if (V) atomicAdd((unsigned long long*)&L.vot[kb - k0], (unsigned long long)V);
-          }
-        } else {  // several attestations: each one's bits from its bitfield in global memory
-          if (lane == 0 && T) atomicAdd((unsigned long long*)&L.tot[cl], (unsigned long long)T);
-          const uint32_t ke = rfl(L.kbg[cl + 1]), cs = rfl(L.cst[cl]);
+        if (lane == 0) {
+          if (T) atomicAdd((unsigned long long*)&L.tot[cl], (unsigned long long)T);
+          if (kind == 1 && V) atomicAdd((unsigned long long*)&L.vot[kb - k0], (unsigned long long)V);
+        }
+        if (kind == 2) {  // several attestations: each one's bits from its bitfield in global memory
+          const uint32_t cs = pc.vbit;  // (kind 2: the committee's first position)
+          const uint32_t ke = pc.vlim;  // (kind 2: the committee's attestations end at catt index ke)
           for (uint32_t kq = kb; kq < ke; ++kq) {
             const uint64_t ga = w.catt[gb + kq];
             const uint64_t bo = a.boffs[gb + ga], nb = 8 * (a.boffs[gb + ga + 1] - bo);
             uint64_t sv = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const uint64_t xb = (uint64_t)(vloc + i) - cs;  // the position's bit in the bitfield
+              const uint64_t xb = (uint64_t)(p + i) - cs;  // the position's bit in the bitfield
               const bool in = v[i] && xb < nb;
               const uint32_t by = in ? a.bits[bo + (xb >> 3)] : 0u;
               sv += (in && ((by >> (7 - (uint32_t)(xb & 7))) & 1)) ? (B32 ? bbase + o4[i] : b[i]) : 0;
@@ -551,7 +513,7 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
         for (int i = 0; i < 4; ++i) sum += (v[i] && act[i]) ? b[i] : 0;
       }
       // slot j's piece of the next round (past the last round: a dummy, loaded and unused)
-      dq[j] = make_uint2(__builtin_amdgcn_readlane(dnx.x, j), __builtin_amdgcn_readlane(dnx.y, j));
+      dq[j] = piece(dnx, j);
       win_load<B32, SEW>(col, dq[j], lane, q[j]);
     }
   }
@@ -589,17 +551,14 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   }
   // the range's attestations: tallies out, the winner rule (core.go:549-555: the first
   // attestation, in order, whose 3 * vote >= 2 * total and whose dynasty beats its shard's record)
-  for (uint32_t cl = tid; cl < ncr; cl += NT) {
-    if (!L.kd[cl]) continue;
-    const uint64_t T = L.tot[cl];
-    for (uint32_t kq = L.kbg[cl]; kq < L.kbg[cl + 1]; ++kq) {
-      const uint64_t V = L.vot[kq - k0];
-      const uint32_t ga = w.catt[gb + kq];
-      a.vote[gb + ga] = V;
-      a.total[gb + ga] = T;
-      const uint4 aw = w.att_win[gb + ga];  // {shard, its record's dynasty lo, hi}
-      if (3ull * V >= 2ull * T && d > pk64(aw.y, aw.z)) atomicMin(&a.winner[inst * a.nrec + aw.x], ga);
-    }
+  for (uint32_t kq = tid; kq < nk; kq += NT) {
+    const uint32_t ga = w.catt[gb + k0 + kq];
+    const uint32_t cl = a.att_comm[gb + ga] - w.cg0 - cr0;
+    const uint64_t V = L.vot[kq], T = L.tot[cl];
+    a.vote[gb + ga] = V;
+    a.total[gb + ga] = T;
+    const uint4 aw = w.att_win[gb + ga];  // {shard, its record's dynasty lo, hi}
+    if (3ull * V >= 2ull * T && d > pk64(aw.y, aw.z)) atomicMin(&a.winner[inst * a.nrec + aw.x], ga);
   }
   if (TR) {
     __syncthreads();
@@ -639,8 +598,8 @@ PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_g_kernel, false, 64, false)
     window_body<true, 16, true, X, D>(a, w);                                                               \
   }
 PZ_WINDOW_ABL(0, 2) PZ_WINDOW_ABL(0, 3) PZ_WINDOW_ABL(0, 4)
-PZ_WINDOW_ABL(1, 2) PZ_WINDOW_ABL(2, 2) PZ_WINDOW_ABL(4, 2) PZ_WINDOW_ABL(8, 2) PZ_WINDOW_ABL(15, 2) PZ_WINDOW_ABL(16, 2)
-PZ_WINDOW_ABL(32, 2) PZ_WINDOW_ABL(64, 2) PZ_WINDOW_ABL(80, 2)
+PZ_WINDOW_ABL(1, 2) PZ_WINDOW_ABL(2, 2) PZ_WINDOW_ABL(4, 2) PZ_WINDOW_ABL(7, 2) PZ_WINDOW_ABL(16, 2)
+PZ_WINDOW_ABL(48, 2) PZ_WINDOW_ABL(64, 2)
 // the product form with phase stamps (tools/epoch_trace.py)
 extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_kernel(EpochArgs a, WinArgs w) {
   window_body<true, 16, true, 0, kWinDepth16, true>(a, w);
@@ -684,12 +643,10 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
       case 1: k = (const void*)pz_epoch_window_abl1_d2_kernel; break;
       case 2: k = (const void*)pz_epoch_window_abl2_d2_kernel; break;
       case 4: k = (const void*)pz_epoch_window_abl4_d2_kernel; break;
-      case 8: k = (const void*)pz_epoch_window_abl8_d2_kernel; break;
-      case 15: k = (const void*)pz_epoch_window_abl15_d2_kernel; break;
+      case 7: k = (const void*)pz_epoch_window_abl7_d2_kernel; break;
       case 16: k = (const void*)pz_epoch_window_abl16_d2_kernel; break;
-      case 32: k = (const void*)pz_epoch_window_abl32_d2_kernel; break;
+      case 48: k = (const void*)pz_epoch_window_abl48_d2_kernel; break;
       case 64: k = (const void*)pz_epoch_window_abl64_d2_kernel; break;
-      case 80: k = (const void*)pz_epoch_window_abl80_d2_kernel; break;
       default: return hipErrorInvalidValue;
     }
   }

@@ -233,13 +233,12 @@ def test_native_epoch_single_launch_matches_window_pass(n):
 
 
 @pytest.mark.ab
-@pytest.mark.parametrize("abl", [16, 32])
+@pytest.mark.parametrize("abl", [16, 48])
 @pytest.mark.parametrize("n,B,short", [(65536, 5, False), (1 << 20, 2, False), (4096, 3, True)])
 def test_native_epoch_window_meeting_fallbacks(abl, n, B, short):
-    """The meeting of an instance's R blocks (each counts 1/R of the bitfields, epoch_window.hip
-    WinArgs.pacc) against its fallbacks, each exact: every block counting everything (16), and
-    the wait bound at zero (32: a block that arrives before its partners counts the whole
-    instance itself).  Two steps against the oracle; or one with a short committee bitfield in
+    """The A/B meeting of an instance's R blocks (each counts 1/R of the bitfields, epoch_window.hip
+    WinArgs.pacc; 16) and its fallback (48: the wait bound at zero, so a block that arrives
+    before its partners counts the whole instance itself), each exact.  Two steps against the oracle; or one with a short committee bitfield in
     instance 0 (its flags, its balances untouched)."""
     dll = _lib.lib.dll
     old = dll.pz_debug_set_window_ablation(abl)

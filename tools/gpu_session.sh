@@ -5,6 +5,7 @@
 #
 # STEPS is a comma-separated list, run in order; the first failing step ends the session:
 #   tests      pytest -m gpu (PYTEST_K: a -k expression; PYTEST_FILES: test paths)
+#   abtests    pytest -m ab (the A/B library's forms)
 #   smoke      __graft_entry__.smoke()
 #   bench      python bench.py $BENCH_ARGS               -> $O/bench.json (the JSON line)
 #   prof       rocprofv3 --kernel-trace --stats of a short bench run -> $O/prof/
@@ -22,6 +23,11 @@ run_tests() {
     --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > "$O/pytest_gpu.txt" 2>&1 \
     || { echo "TESTS_FAIL"; tail -40 "$O/pytest_gpu.txt"; exit 12; }
   tail -2 "$O/pytest_gpu.txt"
+}
+run_abtests() {  # the A/B forms against build/ab/libprysm_hip.so (tests/conftest.py: -m ab)
+  timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -m ab -x -v --timeout 120 --timeout-method thread \
+    > "$O/pytest_ab.txt" 2>&1 || { echo "AB_TESTS_FAIL"; tail -40 "$O/pytest_ab.txt"; exit 18; }
+  tail -2 "$O/pytest_ab.txt"
 }
 run_smoke() {
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')" > "$O/smoke.txt" 2>&1 \
@@ -52,6 +58,7 @@ IFS=, read -ra LIST <<< "$STEPS"
 for s in "${LIST[@]}"; do
   case $s in
     tests) run_tests ;;
+    abtests) run_abtests ;;
     smoke) run_smoke ;;
     bench) run_bench ;;
     prof) run_prof ;;

@@ -45,6 +45,14 @@ def main(d):
             e["hbm_write_bytes"] = avg["WRITE_SIZE"] * 1024
         if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
             e["hbm_bytes_per_launch"] = e["hbm_read_bytes"] + e["hbm_write_bytes"]
+        # VALU-busy fraction (the gfx94x derived VALUBusy, which ROCm 7.2 applies to gfx950 too:
+        # SQ_ACTIVE_INST_VALU x 4 / SIMDs / GRBM_GUI_ACTIVE, GRBM summed over the 8 XCDs) and the
+        # SQ-busy fraction (SQ_BUSY_CYCLES over the same GPU-active cycles, 32 SQs per XCD)
+        if "SQ_ACTIVE_INST_VALU" in avg and avg.get("GRBM_GUI_ACTIVE"):
+            gui = avg["GRBM_GUI_ACTIVE"] / 8
+            e["valu_busy_frac"] = avg["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / gui
+            if "SQ_BUSY_CYCLES" in avg:
+                e["sq_busy_frac"] = avg["SQ_BUSY_CYCLES"] / 256 / gui
         if clk.get(kname):
             e["effective_clock_GHz"] = sum(clk[kname]) / len(clk[kname])
         elif "GRBM_GUI_ACTIVE" in avg:
