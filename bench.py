@@ -1226,12 +1226,17 @@ def shuffle_leg(args):
     return out
 
 
-PMC_DIR = os.path.join("profiles", "r04")
-PMC_SUMMARY = os.path.join(PMC_DIR, "pmc_main.json")
+PMC_DIRS = (os.path.join("profiles", "r05"),)  # (this round's tree only: kernel names change between rounds)
+PMC_SUMMARY = os.path.join(PMC_DIRS[0], "pmc_main.json")
 
 
 def pmc_summary_path(workload):
-    return os.path.join(PMC_DIR, "pmc_%s.json" % workload)
+    """The newest round's committed summary of ``workload`` (tools/gpu_pmc.sh)."""
+    for d in PMC_DIRS:
+        path = os.path.join(d, "pmc_%s.json" % workload)
+        if os.path.exists(os.path.join(ROOT, path)):
+            return path
+    return os.path.join(PMC_DIRS[0], "pmc_%s.json" % workload)
 
 
 def pmc_traffic(kernels, workload="main"):

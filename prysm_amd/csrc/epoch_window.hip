@@ -178,7 +178,8 @@ size_t window_lds_bytes(const WinArgs& w) { return 8ull * ((size_t)w.lds_maxc + 
 // 1/R of its bitfields and meet in WinArgs.pacc (exact; measured 2 us slower at 1M x 16 than
 // every block counting everything, profiles/r05/epoch_abl_window_v4_r5h.txt), 48 = 16 with the
 // meeting's wait bound at zero (the fallback count in every block that arrives before its
-// partners; exact), 64 the first pieces' loads issued after the prologue (exact).
+// partners; exact), 64 the first pieces' loads issued after the prologue (exact), 128 an
+// instance's blocks grouped on one XCD (exact), 144 = 128 + 16.
 template <bool B32, int SEW, bool LLB, int AB = 0, int D = kWinDepth, bool TR = false>
 __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w) {
   extern __shared__ __align__(16) uint8_t lds_dyn[];
@@ -188,8 +189,12 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = rfl(tid >> 6);
   if (TR && tid == 0) tstamp[0] = __builtin_amdgcn_s_memrealtime();
-  const uint64_t inst = blockIdx.x / w.R;
-  const uint32_t r = blockIdx.x - (uint32_t)inst * w.R;
+  // block -> (instance, range); AB & 128: an instance's blocks on one XCD (block b runs on XCD
+  // b % 8), so its bitfields are fetched into one L2 once
+  uint32_t lb_id = blockIdx.x;
+  if ((AB & 128) && (gridDim.x & 7) == 0) lb_id = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  const uint64_t inst = lb_id / w.R;
+  const uint32_t r = lb_id - (uint32_t)inst * w.R;
   const uint4 rd = w.rdesc[r];
   const uint32_t cr0 = rd.x, cr1 = rd.y, pb = rd.z, np = rd.w;
   const uint2 rkk = w.rk[inst * w.R + r];
@@ -599,7 +604,7 @@ PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_g_kernel, false, 64, false)
   }
 PZ_WINDOW_ABL(0, 2) PZ_WINDOW_ABL(0, 3) PZ_WINDOW_ABL(0, 4)
 PZ_WINDOW_ABL(1, 2) PZ_WINDOW_ABL(2, 2) PZ_WINDOW_ABL(4, 2) PZ_WINDOW_ABL(7, 2) PZ_WINDOW_ABL(16, 2)
-PZ_WINDOW_ABL(48, 2) PZ_WINDOW_ABL(64, 2)
+PZ_WINDOW_ABL(48, 2) PZ_WINDOW_ABL(64, 2) PZ_WINDOW_ABL(128, 2) PZ_WINDOW_ABL(144, 2)
 // the product form with phase stamps (tools/epoch_trace.py)
 extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_kernel(EpochArgs a, WinArgs w) {
   window_body<true, 16, true, 0, kWinDepth16, true>(a, w);
@@ -646,6 +651,8 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
       case 7: k = (const void*)pz_epoch_window_abl7_d2_kernel; break;
       case 16: k = (const void*)pz_epoch_window_abl16_d2_kernel; break;
       case 48: k = (const void*)pz_epoch_window_abl48_d2_kernel; break;
+      case 128: k = (const void*)pz_epoch_window_abl128_d2_kernel; break;
+      case 144: k = (const void*)pz_epoch_window_abl144_d2_kernel; break;
       case 64: k = (const void*)pz_epoch_window_abl64_d2_kernel; break;
       default: return hipErrorInvalidValue;
     }

@@ -467,8 +467,8 @@ __device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
 // ticket taken at start, so every predecessor of a waiting tile is running or done (the
 // dispatch order of workgroups is not guaranteed); a tile's look-back reads 1,024
 // predecessors' status words a round.
-constexpr int kSizeThreads = 512, kSizeWaves = kSizeThreads / 64, kSizePer = 8;
-constexpr uint32_t kSizeTile = kSizeThreads * kSizePer, kLbWin = kSizeThreads;
+constexpr int kSizeThreads = 512, kSizePer = 8;  // (the product's geometry; the A/B library's others below)
+constexpr uint32_t kSizeTile = kSizeThreads * kSizePer;
 
 __device__ __forceinline__ uint64_t record_size(const AttArgs& a, uint64_t i) {
   Head h;
@@ -491,6 +491,7 @@ __device__ __forceinline__ uint64_t record_size(const AttArgs& a, uint64_t i) {
 }
 
 // Block-wide exclusive scan of one value per thread; *total receives the sum.
+template <int T>
 __device__ __forceinline__ uint64_t block_excl(uint64_t x, uint64_t* s_wave, uint64_t* total) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint64_t incl = wscan(x);
@@ -498,7 +499,7 @@ __device__ __forceinline__ uint64_t block_excl(uint64_t x, uint64_t* s_wave, uin
   __syncthreads();
   uint64_t before = 0, all = 0;
 #pragma unroll
-  for (int k = 0; k < kSizeWaves; ++k) {
+  for (int k = 0; k < T / 64; ++k) {
     before += k < w ? s_wave[k] : 0;
     all += s_wave[k];
   }
@@ -507,19 +508,20 @@ __device__ __forceinline__ uint64_t block_excl(uint64_t x, uint64_t* s_wave, uin
   return before + incl - x;
 }
 
-// The tile's exclusive base: thread t watches predecessor tile - 1 - t (512 a round); the nearest inclusive
-// prefix (P) ends the walk, the aggregates (A) nearer than it are added.
+// The tile's exclusive base: thread t watches predecessor tile - 1 - t (T a round); the nearest
+// inclusive prefix (P) ends the walk, the aggregates (A) nearer than it are added.
+template <int T>
 __device__ uint64_t lookback_tiles(uint64_t* status, uint64_t tile, uint32_t* s_first, uint64_t* s_part) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint64_t prefix = 0;
-  for (int64_t j = (int64_t)tile - 1;; j -= kLbWin) {
+  for (int64_t j = (int64_t)tile - 1;; j -= T) {
     const int64_t idx = j - tid;
     uint64_t v = idx >= 0 ? ld_status(status + idx) : kFlagP;  // before tile 0: prefix 0
     for (uint32_t spins = 0; !(v >> 62); ++spins) {
       __builtin_amdgcn_s_sleep(1);
       v = spins < 256 ? ld_status(status + idx) : ld_status_fresh(status + idx);
     }
-    if (tid == 0) *s_first = kLbWin;
+    if (tid == 0) *s_first = T;
     __syncthreads();
     if ((v >> 62) == 2) atomicMin(s_first, (uint32_t)tid);
     __syncthreads();
@@ -529,44 +531,54 @@ __device__ uint64_t lookback_tiles(uint64_t* status, uint64_t tile, uint32_t* s_
     __syncthreads();
     uint64_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < kSizeWaves; ++k) sum += s_part[k];
+    for (int k = 0; k < T / 64; ++k) sum += s_part[k];
     __syncthreads();  // s_first / s_part are rewritten by the next window
     prefix += sum;
-    if (first < kLbWin) return prefix;
+    if (first < (uint32_t)T) return prefix;
   }
 }
 
 // Launch 1: every record's size, the tile's scan, its base by look-back, offsets out.
-extern "C" __global__ void __launch_bounds__(kSizeThreads) pz_wire_att_size_kernel(AttArgs a) {
-  __shared__ uint64_t s_wave[kSizeWaves], s_part[kSizeWaves];
+template <int T, int P>
+__device__ __forceinline__ void size_body(const AttArgs& a) {
+  __shared__ uint64_t s_wave[T / 64], s_part[T / 64];
   __shared__ uint32_t s_first, s_tile;
   const int tid = threadIdx.x;
   if (tid == 0) s_tile = atomicAdd(a.ticket, 1u);
   __syncthreads();
-  const uint64_t tile = s_tile, t0 = tile * kSizeTile;
-  uint64_t sz[kSizePer];
+  const uint64_t tile = s_tile, t0 = tile * (uint64_t)(T * P);
+  uint64_t sz[P];
 #pragma unroll
-  for (int q = 0; q < kSizePer; ++q) {
-    const uint64_t i = t0 + (uint64_t)q * kSizeThreads + tid;
+  for (int q = 0; q < P; ++q) {
+    const uint64_t i = t0 + (uint64_t)q * T + tid;
     sz[q] = i < a.n ? record_size(a, i) : 0;
   }
-  uint64_t ex[kSizePer], run = 0;
+  uint64_t ex[P], run = 0;
 #pragma unroll
-  for (int q = 0; q < kSizePer; ++q) {
+  for (int q = 0; q < P; ++q) {
     uint64_t tot;
-    ex[q] = run + block_excl(sz[q], s_wave, &tot);
+    ex[q] = run + block_excl<T>(sz[q], s_wave, &tot);
     run += tot;
   }
   if (tid == 0) st_status(a.status + tile, (tile == 0 ? kFlagP : kFlagA) | run);
-  const uint64_t base = tile == 0 ? 0 : lookback_tiles(a.status, tile, &s_first, s_part);
+  const uint64_t base = tile == 0 ? 0 : lookback_tiles<T>(a.status, tile, &s_first, s_part);
   if (tid == 0 && tile > 0) st_status(a.status + tile, kFlagP | (base + run));
 #pragma unroll
-  for (int q = 0; q < kSizePer; ++q) {
-    const uint64_t i = t0 + (uint64_t)q * kSizeThreads + tid;
+  for (int q = 0; q < P; ++q) {
+    const uint64_t i = t0 + (uint64_t)q * T + tid;
     if (i < a.n) a.offs[i + 1] = base + ex[q] + sz[q];
   }
   if (tile == 0 && tid == 0) a.offs[0] = 0;
 }
+
+extern "C" __global__ void __launch_bounds__(kSizeThreads) pz_wire_att_size_kernel(AttArgs a) {
+  size_body<kSizeThreads, kSizePer>(a);
+}
+#ifdef PZ_AB_BUILD
+extern "C" __global__ void __launch_bounds__(512) pz_wire_att_size_512x4_kernel(AttArgs a) { size_body<512, 4>(a); }
+extern "C" __global__ void __launch_bounds__(256) pz_wire_att_size_256x8_kernel(AttArgs a) { size_body<256, 8>(a); }
+extern "C" __global__ void __launch_bounds__(1024) pz_wire_att_size_1024x2_kernel(AttArgs a) { size_body<1024, 2>(a); }
+#endif
 
 // Launch 2: four records per wave, one per DPP row.  63 VGPRs; left alone the SGPRs (about
 // 100) hold it at 7 waves per SIMD.  Capped at 8 (28 SGPRs spill to VGPR lanes): 0.432 ->
@@ -581,10 +593,10 @@ extern "C" __global__ void __launch_bounds__(kSizeThreads) pz_wire_att_size_kern
 PZ_ATT_WRITE(pz_wire_att_write_kernel, true)
 #ifdef PZ_AB_BUILD
 PZ_ATT_WRITE(pz_wire_att_write_bytes_kernel, false)
-int g_att_variant = 0;  // 1 round 4's three launches, 2 this scan + byte-wise stage
+int g_att_variant = 0;  // 1 round 4's three launches, 2 this scan + byte-wise stage, 3-5 other sizing tiles
 #endif
 
-uint64_t att_tiles(uint64_t n) { return (n + kSizeTile - 1) / kSizeTile; }
+uint64_t att_tiles(uint64_t n) { return (n + 2047) / 2048; }  // (scratch: the smallest tile of any geometry)
 
 hipError_t launch_write(const AttArgs& a, bool dst, hipStream_t s) {
   if (!a.n) return hipSuccess;
@@ -602,13 +614,20 @@ hipError_t launch_write(const AttArgs& a, bool dst, hipStream_t s) {
 // sizes + offsets (status words reset first), then the writes
 hipError_t launch_two(AttArgs a, void* scratch, bool dst, hipStream_t s) {
   if (!a.n) return hipMemsetAsync(a.offs, 0, 8, s);
-  const uint64_t tiles = att_tiles(a.n);
+  const void* k = (const void*)pz_wire_att_size_kernel;
+  uint32_t T = kSizeThreads, tile = kSizeTile;
+#ifdef PZ_AB_BUILD
+  if (g_att_variant == 3) k = (const void*)pz_wire_att_size_512x4_kernel, T = 512, tile = 2048;
+  if (g_att_variant == 4) k = (const void*)pz_wire_att_size_256x8_kernel, T = 256, tile = 2048;
+  if (g_att_variant == 5) k = (const void*)pz_wire_att_size_1024x2_kernel, T = 1024, tile = 2048;
+#endif
+  const uint64_t tiles = (a.n + tile - 1) / tile;
   a.status = static_cast<uint64_t*>(scratch);
   a.ticket = reinterpret_cast<uint32_t*>(a.status + tiles);
   hipError_t e = hipMemsetAsync(scratch, 0, tiles * 8 + 8, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(pz_wire_att_size_kernel, dim3((uint32_t)tiles), dim3(kSizeThreads), 0, s, a);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
+  void* args[] = {&a};
+  if ((e = hipLaunchKernel(k, dim3((uint32_t)tiles), dim3(T), args, 0, s)) != hipSuccess) return e;
   return launch_write(a, dst, s);
 }
 
