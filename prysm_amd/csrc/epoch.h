@@ -180,6 +180,10 @@ struct WinArgs {
   int rank0;                  // this rank writes the per-instance scalars
   // LDS plan: last-bitfield bytes (0: reward bits from L2), most committees / attestations of a range
   uint32_t lds_lbf, lds_maxc, lds_maxk;
+  // every instance's u32 offsets within kTallySpan of kTallyFloor (the state keeps them there by
+  // re-basing every kNarrowPeriod steps): each committee's tallies are two 32-bit wave sums of
+  // (offset - floor) instead of four (epoch_window.hip)
+  uint32_t narrow;
   uint64_t* trace;            // A/B library only: [blocks][4] phase stamps (s_memrealtime), else NULL
   // A/B form (epoch_window.hip AB & 16), R > 1: the R blocks of an instance each count 1/R of
   // its bitfields and meet in one 64-bit word per instance, {arrivals << 48 | length-panic
@@ -189,6 +193,8 @@ struct WinArgs {
   uint64_t* pacc;
   uint64_t* pacc_next;
 };
+constexpr uint32_t kTallyFloor = (1u << 30) - (1u << 22);  // offsets start in [2^30, 2^30 + spread)
+constexpr uint64_t kNarrowSpread = 1ull << 21, kNarrowPeriod = 1ull << 21;  // -> [floor, floor + 2^23)
 constexpr uint64_t kCoopSpinTicks = 5000;  // s_memrealtime ticks (100 MHz): 50 us
 size_t window_lds_bytes(const WinArgs& w);
 hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t s);

@@ -170,15 +170,19 @@ int upload_se16(Shard& s, uint32_t** p, const uint64_t* start, const uint64_t* e
 // part to the u64 column.
 constexpr uint64_t kBal32Window = 1ull << 30;
 constexpr uint64_t kBal32Period = 1ull << 29;
-static uint64_t bal32_period(uint64_t opt) {  // pz_epoch_options.rebase_period (tests: the re-base)
-  return opt && opt < kBal32Period ? opt : kBal32Period;
+static uint64_t bal32_period(uint64_t opt, bool narrow) {  // pz_epoch_options.rebase_period (tests: the re-base)
+  const uint64_t cap = narrow ? kNarrowPeriod : kBal32Period;  // (narrow tallies: epoch.h WinArgs.narrow)
+  return opt && opt < cap ? opt : cap;
 }
+
+static bool any_narrow(const pz_epoch_state* st);
 
 // The base of every instance of [i0, i0 + Bp) over the values vals(b, q), q < n; false if some
 // instance's spread is kBal32Window or more.
 template <typename F>
-static bool bal32_bases(uint64_t Bp, uint64_t n, F vals, std::vector<uint64_t>& base) {
+static bool bal32_bases(uint64_t Bp, uint64_t n, F vals, std::vector<uint64_t>& base, uint64_t* spread = nullptr) {
   base.assign(Bp, 0);
+  uint64_t sp = 0;
   for (uint64_t b = 0; b < Bp; ++b) {
     uint64_t lo = ~0ull, hi = 0;
     for (uint64_t q = 0; q < n; ++q) {
@@ -188,7 +192,9 @@ static bool bal32_bases(uint64_t Bp, uint64_t n, F vals, std::vector<uint64_t>& 
     }
     if (n && hi - lo >= kBal32Window) return false;
     base[b] = (n ? lo : 0) - kBal32Window;
+    sp = std::max(sp, n ? hi - lo : 0);
   }
+  if (spread) *spread = sp;
   return true;
 }
 
@@ -982,9 +988,11 @@ int pz_epoch_state_new_opts(pz_comm* comm, int device, const pz_epoch_host* h, c
           const uint32_t* inv = st->co_inv.data();
           auto vals = [&](uint64_t b, uint64_t p) { return h->balance[(i0 + b) * st->N + inv[s.lo + p]]; };
           std::vector<uint64_t> base;
-          if (bal32_bases(Bp, s.n, vals, base)) {
+          uint64_t spread = 0;
+          if (bal32_bases(Bp, s.n, vals, base, &spread)) {
             rc = bal32_upload(s, q, vals, base, true);
             st->b32 = true;
+            q.w.narrow = spread < kNarrowSpread ? 1 : 0;  // (then the state re-bases every kNarrowPeriod steps)
           }
         }
         // the winners ping-pong (a step resets the next one's buffer): both start empty
@@ -1010,7 +1018,7 @@ int pz_epoch_state_new_opts(pz_comm* comm, int device, const pz_epoch_host* h, c
       return hip_fail(e, "epoch state upload");
     }
   }
-  st->b32_left = bal32_period(st->opts.rebase_period);
+  st->b32_left = bal32_period(st->opts.rebase_period, any_narrow(st));
   flip(st);
   *out = st;
   return PZ_OK;
@@ -1021,7 +1029,7 @@ int pz_epoch_state_step(pz_epoch_state* st) {
   int rc;
   if (st->b32 && st->b32_left == 0) {
     if ((rc = bal32_rebase(st))) return rc;
-    st->b32_left = bal32_period(st->opts.rebase_period);
+    st->b32_left = bal32_period(st->opts.rebase_period, any_narrow(st));
   }
   rc = st->world > 1 ? step_sharded(st) : step_world1(st);
   if (rc) return rc;
@@ -1089,6 +1097,13 @@ int pz_epoch_state_results(pz_epoch_state* st, int local, uint64_t* balance, uin
 }
 
 namespace {
+bool any_narrow(const pz_epoch_state* st) {
+  for (const Shard& s : st->sh)
+    for (uint32_t p = 0; p < st->nparts; ++p)
+      if (s.part[p].window && s.part[p].w.narrow) return true;
+  return false;
+}
+
 int bal32_rebase(pz_epoch_state* st) {
   int rc = pz_epoch_state_sync(st);
   if (rc) return rc;
@@ -1101,11 +1116,14 @@ int bal32_rebase(pz_epoch_state* st) {
       std::vector<uint64_t> v((size_t)q.B * s.n), base;
       if ((rc = part_balances(s, q, v.data(), s.n))) return rc;
       auto vals = [&](uint64_t b, uint64_t x) { return v[b * s.n + x]; };
-      if (bal32_bases(q.B, s.n, vals, base)) {
+      uint64_t spread = 0;
+      if (bal32_bases(q.B, s.n, vals, base, &spread)) {
         if ((rc = bal32_upload(s, q, vals, base, false))) return rc;
+        q.w.narrow = spread < kNarrowSpread ? 1 : 0;
         any = true;
         continue;
       }
+      q.w.narrow = 0;
       // the spread outgrew the window: this part returns to the u64 column
       hipError_t e = hipMemcpy2D(q.a.balance, s.np * 8, v.data(), s.n * 8, s.n * 8, q.B, hipMemcpyHostToDevice);
       if (e != hipSuccess) return hip_fail(e, "hipMemcpy2D H2D (epoch state re-base)");

@@ -179,13 +179,14 @@ size_t window_lds_bytes(const WinArgs& w) { return 8ull * ((size_t)w.lds_maxc + 
 // every block counting everything, profiles/r05/epoch_abl_window_v4_r5h.txt), 48 = 16 with the
 // meeting's wait bound at zero (the fallback count in every block that arrives before its
 // partners; exact), 64 the first pieces' loads issued after the prologue (exact), 128 an
-// instance's blocks grouped on one XCD (exact), 144 = 128 + 16.
-template <bool B32, int SEW, bool LLB, int AB = 0, int D = kWinDepth, bool TR = false>
+// instance's blocks grouped on one XCD (exact), 144 = 128 + 16, 4096 the four-sum tallies on
+// narrow offsets (exact).
+template <bool B32, int SEW, bool LLB, int AB = 0, int D = kWinDepth, bool TR = false, bool NA = false>
 __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w) {
   extern __shared__ __align__(16) uint8_t lds_dyn[];
   constexpr int NT = kWinThreads, NW = NT / 64;
   __shared__ uint64_t red[NW][2], red2[NW][2];  // (the prologue's and the loop's: no barrier between their uses)
-  __shared__ uint64_t tstamp[TR ? 4 : 1];
+  __shared__ uint64_t tstamp[4];  // (TR only)
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = rfl(tid >> 6);
   if (TR && tid == 0) tstamp[0] = __builtin_amdgcn_s_memrealtime();
@@ -423,7 +424,23 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
             if (p + i - s0p >= pc.vlim) vw &= ~(1u << i);
         }
         uint64_t T, V;
-        if (B32) {
+        if (B32 && NA && !(AB & 4096)) {
+          // every offset within [floor, floor + 2^23): (offset - floor) sums to < 2^31 over the
+          // <= 256 positions; the voters' count from four ballots (the positions' count is cnt)
+          uint32_t ts = 0, vs = 0, nv = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t x = o4[i] - kTallyFloor;
+            const bool vt = v[i] && ((vw >> i) & 1);
+            ts += v[i] ? x : 0;
+            vs += vt ? x : 0;
+            nv += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(vt));
+          }
+          ts = wsum32(ts), vs = wsum32(vs);
+          const uint64_t fb = bbase + kTallyFloor;
+          T = (uint64_t)cnt * fb + ts;
+          V = (uint64_t)nv * fb + vs;
+        } else if (B32) {
           // offsets split 17 | 15 bits: low parts with the count in bits 23+ (<= 256 x 2^15 < 2^23,
           // <= 256 positions), high parts (<= 256 x 2^17 < 2^25): four 32-bit sums, exact
           uint32_t at = 0, ht = 0, av = 0, hv = 0;
@@ -575,24 +592,30 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   }
 }
 
-#define PZ_WINDOW_KERNEL(NAME, B32, SEW, LLB)                                                           \
+#define PZ_WINDOW_KERNEL(NAME, B32, SEW, LLB, NA)                                                        \
   extern "C" __global__ void __launch_bounds__(kWinThreads) NAME(EpochArgs a, WinArgs w) {             \
-    window_body<B32, SEW, LLB, 0, (B32 && SEW == 16) ? kWinDepth16 : kWinDepth>(a, w);                 \
+    window_body<B32, SEW, LLB, 0, (B32 && SEW == 16) ? kWinDepth16 : kWinDepth, false, NA>(a, w);      \
   }
-// balances as u32 offsets / u64; {start, end} at 16 / 32 / 64 bits; the last bitfield in LDS or not
-// (the narrow form has the registers for a deeper prefetch)
-PZ_WINDOW_KERNEL(pz_epoch_window_b32_s16_kernel, true, 16, true)
-PZ_WINDOW_KERNEL(pz_epoch_window_b32_s32_kernel, true, 32, true)
-PZ_WINDOW_KERNEL(pz_epoch_window_b32_s64_kernel, true, 64, true)
-PZ_WINDOW_KERNEL(pz_epoch_window_b64_s16_kernel, false, 16, true)
-PZ_WINDOW_KERNEL(pz_epoch_window_b64_s32_kernel, false, 32, true)
-PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_kernel, false, 64, true)
-PZ_WINDOW_KERNEL(pz_epoch_window_b32_s16_g_kernel, true, 16, false)
-PZ_WINDOW_KERNEL(pz_epoch_window_b32_s32_g_kernel, true, 32, false)
-PZ_WINDOW_KERNEL(pz_epoch_window_b32_s64_g_kernel, true, 64, false)
-PZ_WINDOW_KERNEL(pz_epoch_window_b64_s16_g_kernel, false, 16, false)
-PZ_WINDOW_KERNEL(pz_epoch_window_b64_s32_g_kernel, false, 32, false)
-PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_g_kernel, false, 64, false)
+// balances as u32 offsets (the narrow tallies or not) / u64; {start, end} at 16 / 32 / 64 bits;
+// the last bitfield in LDS or not
+PZ_WINDOW_KERNEL(pz_epoch_window_b32n_s16_kernel, true, 16, true, true)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32n_s32_kernel, true, 32, true, true)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32n_s64_kernel, true, 64, true, true)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32_s16_kernel, true, 16, true, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32_s32_kernel, true, 32, true, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32_s64_kernel, true, 64, true, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b64_s16_kernel, false, 16, true, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b64_s32_kernel, false, 32, true, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_kernel, false, 64, true, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32n_s16_g_kernel, true, 16, false, true)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32n_s32_g_kernel, true, 32, false, true)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32n_s64_g_kernel, true, 64, false, true)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32_s16_g_kernel, true, 16, false, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32_s32_g_kernel, true, 32, false, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b32_s64_g_kernel, true, 64, false, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b64_s16_g_kernel, false, 16, false, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b64_s32_g_kernel, false, 32, false, false)
+PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_g_kernel, false, 64, false, false)
 #undef PZ_WINDOW_KERNEL
 
 #ifdef PZ_AB_BUILD
@@ -600,14 +623,14 @@ PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_g_kernel, false, 64, false)
 #define PZ_WINDOW_ABL(X, D)                                                                              \
   extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_abl##X##_d##D##_kernel(EpochArgs a, \
                                                                                               WinArgs w) {  \
-    window_body<true, 16, true, X, D>(a, w);                                                               \
+    window_body<true, 16, true, X, D, false, true>(a, w);                                                  \
   }
 PZ_WINDOW_ABL(0, 2) PZ_WINDOW_ABL(0, 3) PZ_WINDOW_ABL(0, 4)
 PZ_WINDOW_ABL(1, 2) PZ_WINDOW_ABL(2, 2) PZ_WINDOW_ABL(4, 2) PZ_WINDOW_ABL(7, 2) PZ_WINDOW_ABL(16, 2)
-PZ_WINDOW_ABL(48, 2) PZ_WINDOW_ABL(64, 2) PZ_WINDOW_ABL(128, 2) PZ_WINDOW_ABL(144, 2)
+PZ_WINDOW_ABL(48, 2) PZ_WINDOW_ABL(64, 2) PZ_WINDOW_ABL(128, 2) PZ_WINDOW_ABL(144, 2) PZ_WINDOW_ABL(4096, 2)
 // the product form with phase stamps (tools/epoch_trace.py)
 extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_kernel(EpochArgs a, WinArgs w) {
-  window_body<true, 16, true, 0, kWinDepth16, true>(a, w);
+  window_body<true, 16, true, 0, kWinDepth16, true, true>(a, w);
 }
 #undef PZ_WINDOW_ABL
 static int g_window_ablation = 0;
@@ -628,7 +651,11 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
   const void* k = nullptr;
 #define PZ_PICK(B, S)                                                                            \
   k = llb ? (const void*)pz_epoch_window_##B##_s##S##_kernel : (const void*)pz_epoch_window_##B##_s##S##_g_kernel
-  if (b32) {
+  if (b32 && w.narrow) {
+    if (sew == 16) PZ_PICK(b32n, 16);
+    else if (sew == 32) PZ_PICK(b32n, 32);
+    else PZ_PICK(b32n, 64);
+  } else if (b32) {
     if (sew == 16) PZ_PICK(b32, 16);
     else if (sew == 32) PZ_PICK(b32, 32);
     else PZ_PICK(b32, 64);
@@ -639,8 +666,9 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
   }
 #undef PZ_PICK
 #ifdef PZ_AB_BUILD
-  if (g_window_trace && b32 && sew == 16 && llb) k = (const void*)pz_epoch_window_trace_kernel;
-  if (g_window_ablation && b32 && sew == 16 && llb) {
+  // (the A/B forms are the narrow product form's)
+  if (g_window_trace && b32 && w.narrow && sew == 16 && llb) k = (const void*)pz_epoch_window_trace_kernel;
+  if (g_window_ablation && b32 && w.narrow && sew == 16 && llb) {
     switch (g_window_ablation) {  // ablation bits | prefetch depth << 8
       case 2 << 8: k = (const void*)pz_epoch_window_abl0_d2_kernel; break;
       case 3 << 8: k = (const void*)pz_epoch_window_abl0_d3_kernel; break;
@@ -652,6 +680,7 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
       case 16: k = (const void*)pz_epoch_window_abl16_d2_kernel; break;
       case 48: k = (const void*)pz_epoch_window_abl48_d2_kernel; break;
       case 128: k = (const void*)pz_epoch_window_abl128_d2_kernel; break;
+      case 4096: k = (const void*)pz_epoch_window_abl4096_d2_kernel; break;
       case 144: k = (const void*)pz_epoch_window_abl144_d2_kernel; break;
       case 64: k = (const void*)pz_epoch_window_abl64_d2_kernel; break;
       default: return hipErrorInvalidValue;

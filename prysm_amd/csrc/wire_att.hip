@@ -288,25 +288,36 @@ __device__ __forceinline__ void stage_segment(uint8_t* row, uint32_t d0, uint32_
   }
   if (!len) return;
   // stage word k of the segment holds source bytes r + 4k - dm .. +3 (dm = d0 mod 4): one
-  // v_alignbyte of the loaded words, one word lower when r < dm
+  // v_alignbyte of the loaded words, one word lower when r < dm.  Words [kf, kl) are the
+  // segment's alone and go out as dwords; the first and the last word, when shared with a
+  // neighbour, are kept and written byte by byte after the loop (so the loop body is the same
+  // few instructions on every lane)
   const uint32_t dend = d0 + len, dm = d0 & 3;
   const bool back = r < dm;
   const uint32_t delta = (r - dm) & 3, nwo = (dm + len + 3) >> 2;
+  const uint32_t kf = (dm == 0 && len >= 4) ? 0u : 1u, kl = (dend & 3) ? nwo - 1 : nwo;
+  const uint32_t nfull = kl > kf ? kl - kf : 0u;  // (a segment inside one word has none)
   uint32_t* sw = reinterpret_cast<uint32_t*>(row) + (d0 >> 2);
   const uint32_t bw = d0 & ~3u;
+  uint32_t xf = 0, xl = 0;
 #pragma unroll
   for (int k = 0; k < (int)kSegWords; ++k) {
     const uint32_t lo = back ? (k ? wv[k - 1] : 0u) : wv[k], hi = back ? wv[k] : wv[k + 1];
     const uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, delta);
-    const uint32_t b0 = bw + 4 * k;
-    if ((uint32_t)k >= nwo) {
-    } else if (b0 >= d0 && b0 + 4 <= dend) {
-      sw[k] = x;
-    } else {
+    if (k == 0) xf = x;
+    xl = (uint32_t)k + 1 == nwo ? x : xl;
+    if ((uint32_t)k - kf < nfull) sw[k] = x;  // (k in [kf, kl); unsigned: k < kf wraps high)
+  }
+  if (kf) {  // the first word: bytes [d0, min(dend, bw + 4))
 #pragma unroll
-      for (int b = 0; b < 4; ++b)
-        if (b0 + b >= d0 && b0 + b < dend) row[b0 + b] = (uint8_t)(x >> (8 * b));
-    }
+    for (int b = 0; b < 4; ++b)
+      if (bw + b >= d0 && bw + b < dend) row[bw + b] = (uint8_t)(xf >> (8 * b));
+  }
+  if ((dend & 3) && nwo > 1) {  // the last word: bytes [bw + 4 (nwo - 1), dend)
+    const uint32_t lw = bw + 4 * (nwo - 1);
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+      if (lw + b < dend) row[lw + b] = (uint8_t)(xl >> (8 * b));
   }
 }
 
