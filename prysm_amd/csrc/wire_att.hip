@@ -248,7 +248,7 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, int k) {
 // Lane K of this lane's row (DPP row_newbcast).
 template <int K>
 __device__ __forceinline__ uint32_t bc32(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x150 + K, 0xf, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + K, 0xf, 0xf, true);
 }
 template <int K>
 __device__ __forceinline__ uint64_t bc64(uint64_t x) {
@@ -257,26 +257,29 @@ __device__ __forceinline__ uint64_t bc64(uint64_t x) {
 
 // Lane l - 3 of the row (0 for l < 3; DPP row_shr:3).
 __device__ __forceinline__ uint32_t shr3(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x113, 0xf, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x113, 0xf, 0xf, true);
 }
 
 // Inclusive scan over each row with DPP shifts of 1, 2, 4, 8.
 __device__ __forceinline__ uint32_t rscan32(uint32_t x) {
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x111, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x112, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x114, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x118, 0xf, 0xf, true);
   return x;
 }
 
-// A row's segment into its stage: the source dwords wv (aligned on the source, first byte at
-// r), len bytes, to stage bytes [d0, d0 + len).  Whole stage dwords where the word is the
-// segment's alone, bytes at its two edges (shared with the neighbouring items); the A/B
-// library keeps round 4's byte-by-byte form (DST false).
-template <bool DST>
-__device__ __forceinline__ void stage_segment(uint8_t* row, uint32_t d0, uint32_t (&wv)[kSegWords + 1], uint32_t r,
-                                              uint32_t len) {
-  if (!DST) {
+// Segment modes (the write kernel's template argument M): 0 round 4's form, the segment placed
+// in the stage byte by byte; 1 the aligned form of early round 5, stage dwords realigned with
+// v_alignbyte, the two edge words written byte-wise; 2 (the product) unaligned pieces, below.
+// 0 and 1 are kept in the A/B library only.
+//
+// Aligned form: the source dwords wv (aligned on the source, first byte at r), len bytes, to
+// stage bytes [d0, d0 + len).
+template <int M>
+__device__ __forceinline__ void stage_segment_aligned(uint8_t* row, uint32_t d0, uint32_t (&wv)[kSegWords + 1],
+                                                      uint32_t r, uint32_t len) {
+  if (M == 0) {
 #pragma unroll
     for (int k = 0; k < (int)kSegWords; ++k) {
       const uint32_t d = __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], r);
@@ -290,8 +293,7 @@ __device__ __forceinline__ void stage_segment(uint8_t* row, uint32_t d0, uint32_
   // stage word k of the segment holds source bytes r + 4k - dm .. +3 (dm = d0 mod 4): one
   // v_alignbyte of the loaded words, one word lower when r < dm.  Words [kf, kl) are the
   // segment's alone and go out as dwords; the first and the last word, when shared with a
-  // neighbour, are kept and written byte by byte after the loop (so the loop body is the same
-  // few instructions on every lane)
+  // neighbour, are written byte by byte after the loop
   const uint32_t dend = d0 + len, dm = d0 & 3;
   const bool back = r < dm;
   const uint32_t delta = (r - dm) & 3, nwo = (dm + len + 3) >> 2;
@@ -308,12 +310,12 @@ __device__ __forceinline__ void stage_segment(uint8_t* row, uint32_t d0, uint32_
     xl = (uint32_t)k + 1 == nwo ? x : xl;
     if ((uint32_t)k - kf < nfull) sw[k] = x;  // (k in [kf, kl); unsigned: k < kf wraps high)
   }
-  if (kf) {  // the first word: bytes [d0, min(dend, bw + 4))
+  if (kf) {
 #pragma unroll
     for (int b = 0; b < 4; ++b)
       if (bw + b >= d0 && bw + b < dend) row[bw + b] = (uint8_t)(xf >> (8 * b));
   }
-  if ((dend & 3) && nwo > 1) {  // the last word: bytes [bw + 4 (nwo - 1), dend)
+  if ((dend & 3) && nwo > 1) {
     const uint32_t lw = bw + 4 * (nwo - 1);
 #pragma unroll
     for (int b = 0; b < 3; ++b)
@@ -321,7 +323,59 @@ __device__ __forceinline__ void stage_segment(uint8_t* row, uint32_t d0, uint32_
   }
 }
 
-template <bool DST>
+// Unaligned form: a segment of len >= 16 bytes is four 16-byte pieces at min(16c, len - 16):
+// every load and every stage write lies inside the segment -- the last piece overlaps the one
+// before it with the same bytes -- so the neighbours' bytes are never touched and no select
+// picks a word: ~25 VALU instructions per segment against ~130 for the aligned form.  (gfx950
+// runs unaligned global and LDS accesses; HSA sets the unaligned mode.)  A segment under 16
+// bytes (none in the bench's records) is loaded at stage time as aligned words and written
+// byte by byte.
+struct SegPieces {  // pieces 0-2; the fourth (a segment over 48 bytes) is loaded at stage time
+  uint4 q[3];
+};
+
+typedef const __attribute__((address_space(1))) uint8_t gbyte;
+
+__device__ __forceinline__ uint4 ldu16(gbyte* p) {
+  uint4 v;
+  __builtin_memcpy(&v, p, 16);
+  return v;
+}
+__device__ __forceinline__ void stu16(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
+
+__device__ __forceinline__ void load_segment_unaligned(const uint8_t* src, uint32_t len, SegPieces& sp) {
+  gbyte* g = reinterpret_cast<gbyte*>((uintptr_t)src);
+  const uint32_t np = len >= 16 ? (len + 15) >> 4 : 0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+    if ((uint32_t)c < np) sp.q[c] = ldu16(g + min(16u * c, len - 16));
+}
+
+__device__ __forceinline__ void stage_segment_unaligned(uint8_t* d, const uint8_t* src, uint32_t len,
+                                                        const SegPieces& sp) {
+  const uint32_t np = len >= 16 ? (len + 15) >> 4 : 0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+    if ((uint32_t)c < np) stu16(d + min(16u * c, len - 16), sp.q[c]);
+  if (np == 4) stu16(d + len - 16, ldu16(reinterpret_cast<gbyte*>((uintptr_t)src) + len - 16));
+  if (len && len < 16) {
+    typedef const __attribute__((address_space(1))) uint32_t gword;
+    gword* ws = reinterpret_cast<gword*>((uintptr_t)src & ~(uintptr_t)3);
+    const uint32_t r = (uint32_t)(uintptr_t)src & 3, nw = (r + len + 3) >> 2;
+    uint32_t w[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) w[k] = (uint32_t)k < nw ? ws[k] : 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t x = __builtin_amdgcn_alignbyte(w[k + 1], w[k], r);
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if ((uint32_t)(4 * k + b) < len) d[4 * k + b] = (uint8_t)(x >> (8 * b));
+    }
+  }
+}
+
+template <int M>
 __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*stage)[kStageAlloc], uint64_t i0) {
   const int lane = threadIdx.x & 63;
   const int sl = lane & (kRow - 1), ri = lane / kRow;
@@ -376,11 +430,16 @@ __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*
   typedef const __attribute__((address_space(1))) uint32_t gword;
   const uint32_t len = fast ? (uint32_t)seg_len : 0;
   const uint32_t r = (uint32_t)(uintptr_t)seg_src & 3;
-  gword* ws = reinterpret_cast<gword*>((uintptr_t)seg_src & ~(uintptr_t)3);
-  const uint32_t nw = len ? (r + len + 3) / 4 : 0;
   uint32_t wv[kSegWords + 1];
+  SegPieces sp;
+  if (M < 2) {
+    gword* ws = reinterpret_cast<gword*>((uintptr_t)seg_src & ~(uintptr_t)3);
+    const uint32_t nw = len ? (r + len + 3) / 4 : 0;
 #pragma unroll
-  for (int k = 0; k <= (int)kSegWords; ++k) wv[k] = (uint32_t)k < nw ? ws[k] : 0;
+    for (int k = 0; k <= (int)kSegWords; ++k) wv[k] = (uint32_t)k < nw ? ws[k] : 0;
+  } else {
+    load_segment_unaligned(seg_src, len, sp);
+  }
   const uint32_t sh = (uint32_t)o & 15;
   uint8_t* st = stage[ri] + sh;
   uint32_t seg_dst = 0;
@@ -411,7 +470,7 @@ __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*
       st[pos] = (uint8_t)((sl << 3) | (sl >= 4 ? 2 : 0));
       put_varint(st + pos + 1, val);
     }
-    const uint32_t fd = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(pos + 1 + vlen(val)), 0x104, 0xf, 0xf, false);
+    const uint32_t fd = (uint32_t)__builtin_amdgcn_mov_dpp((int)(pos + 1 + vlen(val)), 0x104, 0xf, 0xf, true);
     if (sl < 3) seg_dst = fd;
     const uint32_t ep = bc32<7>(pos) + einc - esz;
     if ((uint64_t)sl < nob) {
@@ -423,7 +482,11 @@ __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*
     const uint32_t sp = bc32<8>(pos) + 1 + vlen(sigb);
     if ((uint64_t)sl < nsig) put_varint(st + sp + sinc - ssz, sv);
   }
-  stage_segment<DST>(stage[ri], sh + seg_dst, wv, r, len);
+  if (M < 2) {
+    stage_segment_aligned<M>(stage[ri], sh + seg_dst, wv, r, len);
+  } else {
+    stage_segment_unaligned(stage[ri] + sh + seg_dst, seg_src, len, sp);
+  }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   const uint32_t sz = fast ? (uint32_t)size : 0;
@@ -434,8 +497,30 @@ __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*
     const uint32_t lo = 16 * q, hi = lo + 16;
     if (lo >= sh && hi <= sh + sz) {
       *reinterpret_cast<uint4*>(ob + lo) = *reinterpret_cast<const uint4*>(sb + lo);
-    } else {
+    } else if (M < 2) {
       for (uint32_t x = max(lo, sh); x < min(hi, sh + sz); ++x) ob[x] = sb[x];
+    } else {  // an edge block shared with a neighbour: 1-, 2-, 4- and 8-byte pieces of [x, e)
+      uint32_t x = max(lo, sh);
+      const uint32_t l = min(hi, sh + sz) - x;
+      if (l & 1) ob[x] = sb[x];
+      x += l & 1;
+      if (l & 2) {
+        uint16_t v;
+        __builtin_memcpy(&v, sb + x, 2);
+        __builtin_memcpy(ob + x, &v, 2);
+      }
+      x += l & 2;
+      if (l & 4) {
+        uint32_t v;
+        __builtin_memcpy(&v, sb + x, 4);
+        __builtin_memcpy(ob + x, &v, 4);
+      }
+      x += l & 4;
+      if (l & 8) {
+        uint2 v;
+        __builtin_memcpy(&v, sb + x, 8);
+        __builtin_memcpy(ob + x, &v, 8);
+      }
     }
   }
   for (int u = 0; u < kRecs; ++u) {
@@ -601,10 +686,13 @@ extern "C" __global__ void __launch_bounds__(1024) pz_wire_att_size_1024x2_kerne
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);                                  \
     wire_att_write_rows<DST>(a, stage[w], ((uint64_t)blockIdx.x * kWaves + w) * kRecs);              \
   }
-PZ_ATT_WRITE(pz_wire_att_write_kernel, true)
+PZ_ATT_WRITE(pz_wire_att_write_kernel, 2)
 #ifdef PZ_AB_BUILD
-PZ_ATT_WRITE(pz_wire_att_write_bytes_kernel, false)
-int g_att_variant = 0;  // 1 round 4's three launches, 2 this scan + byte-wise stage, 3-5 other sizing tiles
+PZ_ATT_WRITE(pz_wire_att_write_bytes_kernel, 0)
+PZ_ATT_WRITE(pz_wire_att_write_aligned_kernel, 1)
+// 1 round 4's three launches, 2 this scan + byte-wise stage, 3-5 other sizing tiles, 6 the
+// aligned-dword stage
+int g_att_variant = 0;
 #endif
 
 uint64_t att_tiles(uint64_t n) { return (n + 2047) / 2048; }  // (scratch: the smallest tile of any geometry)
@@ -614,6 +702,7 @@ hipError_t launch_write(const AttArgs& a, bool dst, hipStream_t s) {
   const void* k = (const void*)pz_wire_att_write_kernel;
 #ifdef PZ_AB_BUILD
   if (!dst) k = (const void*)pz_wire_att_write_bytes_kernel;
+  if (g_att_variant == 6) k = (const void*)pz_wire_att_write_aligned_kernel;
 #else
   (void)dst;
 #endif

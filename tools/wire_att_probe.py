@@ -47,7 +47,7 @@ def main():
     ms = e0.elapsed_time(e1) / reps
     dll = _lib.lib.dll
     if hasattr(dll, "pz_debug_set_att_write_variant"):  # same-process A/B (PZ_PROBE_LIB=build/ab/...)
-        for v in (0, 1, 2, 3, 4, 5, 0):  # product / r4 three launches / byte-wise stage / sizing 512x4, 256x8, 1024x2
+        for v in (0, 6, 1, 2, 3, 0):  # product / aligned-dword stage / r4 three launches / byte-wise stage / sizing 512x4
             dll.pz_debug_set_att_write_variant(v)
             e0.record()
             for _ in range(reps):
