@@ -100,6 +100,29 @@ struct Head {  // the record's scalar part, the same on every lane
   h.s1 = a.sfirst ? a.sfirst[i + 1] : 0;
 }
 
+// load_head with every load issued: a NULL column reads a zero pair instead of branching
+// round its load (the branches' joins waited for each load in turn: four round trips per head).
+__device__ const uint64_t kZeroPair[2] = {0, 0};
+
+__device__ __forceinline__ void load_head_flat(const AttArgs& a, uint64_t i, Head& h) {
+  typedef const __attribute__((address_space(1))) uint64_t gu64;
+  gu64* z = reinterpret_cast<gu64*>((uintptr_t)kZeroPair);
+  auto col = [&](const uint64_t* p) { return p ? reinterpret_cast<gu64*>((uintptr_t)(p + i)) : z; };
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    h.v[k] = *col(a.col[k]);
+    gu64* b = col(a.boff[k]);
+    h.b0[k] = b[0];
+    h.bl[k] = b[1] - b[0];
+  }
+  gu64* o = col(a.ofirst);
+  gu64* g = col(a.sfirst);
+  h.o0 = o[0];
+  h.o1 = o[1];
+  h.s0 = g[0];
+  h.s1 = g[1];
+}
+
 // Fields 1-6 (scalars and bytes), the oblique elements and the packed signature body.
 __device__ __forceinline__ void record_parts(const AttArgs& a, const Head& h, uint64_t* fixed, uint64_t* obl,
                                              uint64_t* sigb) {
@@ -586,6 +609,101 @@ __device__ __forceinline__ uint64_t record_size(const AttArgs& a, uint64_t i) {
   return a.field ? a.tag_len + vlen(body) + body : body;
 }
 
+// A thread's P records sized with their loads in flight together.  Round 5's first sizing ran
+// each record's element and value loops in turn (a loop's trip count is data, so nothing of
+// record q + 1 was issued before record q's loops ended): ~5 dependent round trips per record,
+// 40 per thread.  Here the heads of all P records load first; then, G records at a time, each
+// record's first kSizeElems + 1 element offsets and kSizeSigs values load from clamped
+// addresses (no predicate, so no branch keeps the next load waiting) and are masked in the sum.
+// A record with more elements or values than that is sized again by the loops.
+constexpr uint32_t kSizeElems = 12, kSizeSigs = 4;
+
+template <int T, int P, int G>
+__device__ __forceinline__ void size_records(const AttArgs& a, uint64_t t0, uint64_t (&sz)[P]) {
+  const int tid = threadIdx.x;
+  uint64_t fixed[P], o0[P], s0[P];
+  uint32_t no[P], ns[P];  // clamped to kSizeElems + 1 / kSizeSigs + 1 (more: the loops)
+#pragma unroll
+  for (int q4 = 0; q4 < P; q4 += 4) {  // heads four records at a time (13 loads each), all in flight
+    __builtin_amdgcn_sched_barrier(0);
+    Head h[4];
+#pragma unroll
+    for (int r = 0; r < 4 && q4 + r < P; ++r) {
+      const uint64_t i = t0 + (uint64_t)(q4 + r) * T + tid;
+      load_head_flat(a, i < a.n ? i : a.n - 1, h[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4 && q4 + r < P; ++r) {
+      const int q = q4 + r;
+      const uint64_t i = t0 + (uint64_t)q * T + tid;
+      uint64_t f = 0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        f += h[r].v[k] ? 1 + vlen(h[r].v[k]) : 0;
+        f += h[r].bl[k] ? 1 + vlen(h[r].bl[k]) + h[r].bl[k] : 0;
+      }
+      fixed[q] = i < a.n ? f : 0;
+      o0[q] = h[r].o0;
+      s0[q] = h[r].s0;
+      no[q] = (uint32_t)min(h[r].o1 - h[r].o0, (uint64_t)kSizeElems + 1);
+      ns[q] = (uint32_t)min(h[r].s1 - h[r].s0, (uint64_t)kSizeSigs + 1);
+    }
+  }
+  const uint64_t* any = reinterpret_cast<const uint64_t*>(a.status);  // (a valid address; the value is masked)
+  uint32_t longs = 0;
+#pragma unroll
+  for (int g = 0; g < P; g += G) {
+    __builtin_amdgcn_sched_barrier(0);  // (one group's loads live at a time: hoisting them all spills)
+    // element offsets: the first and the last as 64-bit words, the ones between as their low
+    // words (a record whose elements total 2^32 bytes or more takes the loops, so every
+    // length is exact as a 32-bit difference)
+    typedef const __attribute__((address_space(1))) uint32_t gu32;
+    uint64_t ofirst[G], olast[G], sv[G][kSizeSigs];
+    uint32_t lw[G][kSizeElems - 1];
+#pragma unroll
+    for (int r = 0; r < G; ++r) {
+      const int q = g + r;
+      const uint64_t* ob = a.ooff ? a.ooff + o0[q] : any;
+      const uint32_t ol = a.ooff ? min(no[q], kSizeElems) : 0;
+      gu32* obw = reinterpret_cast<gu32*>((uintptr_t)ob);
+      ofirst[r] = ob[0];
+      olast[r] = ob[ol];
+#pragma unroll
+      for (uint32_t e = 1; e < kSizeElems; ++e) lw[r][e - 1] = obw[2 * min(e, ol)];
+      const uint64_t* sb = ns[q] ? a.sig + s0[q] : any;
+      const uint32_t sl = ns[q] ? min(ns[q], kSizeSigs) - 1 : 0;
+#pragma unroll
+      for (uint32_t e = 0; e < kSizeSigs; ++e) sv[r][e] = sb[min(e, sl)];
+    }
+#pragma unroll
+    for (int r = 0; r < G; ++r) {
+      const int q = g + r;
+      const uint64_t i = t0 + (uint64_t)q * T + tid;
+      const uint64_t total = olast[r] - ofirst[r];
+      uint32_t vl = 0, prev = (uint32_t)ofirst[r];
+#pragma unroll
+      for (uint32_t e = 0; e < kSizeElems; ++e) {
+        const uint32_t next = e + 1 < kSizeElems ? lw[r][e] : (uint32_t)olast[r];
+        vl += e < no[q] ? vlen(next - prev) : 0;
+        prev = next;
+      }
+      uint64_t sigb = 0;
+#pragma unroll
+      for (uint32_t e = 0; e < kSizeSigs; ++e) sigb += e < ns[q] ? vlen(sv[r][e]) : 0;
+      const uint64_t obl = no[q] + vl + total;
+      const uint64_t body = fixed[q] + obl + (sigb ? 1 + vlen(sigb) + sigb : 0);
+      sz[q] = i >= a.n ? 0 : a.field ? a.tag_len + vlen(body) + body : body;
+      longs |= (i < a.n && (no[q] > kSizeElems || ns[q] > kSizeSigs || (total >> 32))) ? 1u << q : 0u;
+    }
+  }
+  // records with more elements or values than the loads above: the loops
+  if (__builtin_amdgcn_read_exec() & __ballot(longs != 0)) {
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+      if (longs & (1u << q)) sz[q] = record_size(a, t0 + (uint64_t)q * T + tid);
+  }
+}
+
 // Block-wide exclusive scan of one value per thread; *total receives the sum.
 template <int T>
 __device__ __forceinline__ uint64_t block_excl(uint64_t x, uint64_t* s_wave, uint64_t* total) {
@@ -635,7 +753,7 @@ __device__ uint64_t lookback_tiles(uint64_t* status, uint64_t tile, uint32_t* s_
 }
 
 // Launch 1: every record's size, the tile's scan, its base by look-back, offsets out.
-template <int T, int P>
+template <int T, int P, bool LOOPS = false>
 __device__ __forceinline__ void size_body(const AttArgs& a) {
   __shared__ uint64_t s_wave[T / 64], s_part[T / 64];
   __shared__ uint32_t s_first, s_tile;
@@ -644,10 +762,14 @@ __device__ __forceinline__ void size_body(const AttArgs& a) {
   __syncthreads();
   const uint64_t tile = s_tile, t0 = tile * (uint64_t)(T * P);
   uint64_t sz[P];
+  if (LOOPS) {  // (A/B: round 5's first form, each record's loops in turn)
 #pragma unroll
-  for (int q = 0; q < P; ++q) {
-    const uint64_t i = t0 + (uint64_t)q * T + tid;
-    sz[q] = i < a.n ? record_size(a, i) : 0;
+    for (int q = 0; q < P; ++q) {
+      const uint64_t i = t0 + (uint64_t)q * T + tid;
+      sz[q] = i < a.n ? record_size(a, i) : 0;
+    }
+  } else {
+    size_records<T, P, 2>(a, t0, sz);
   }
   uint64_t ex[P], run = 0;
 #pragma unroll
@@ -674,6 +796,9 @@ extern "C" __global__ void __launch_bounds__(kSizeThreads) pz_wire_att_size_kern
 extern "C" __global__ void __launch_bounds__(512) pz_wire_att_size_512x4_kernel(AttArgs a) { size_body<512, 4>(a); }
 extern "C" __global__ void __launch_bounds__(256) pz_wire_att_size_256x8_kernel(AttArgs a) { size_body<256, 8>(a); }
 extern "C" __global__ void __launch_bounds__(1024) pz_wire_att_size_1024x2_kernel(AttArgs a) { size_body<1024, 2>(a); }
+extern "C" __global__ void __launch_bounds__(kSizeThreads) pz_wire_att_size_loops_kernel(AttArgs a) {
+  size_body<kSizeThreads, kSizePer, true>(a);
+}
 #endif
 
 // Launch 2: four records per wave, one per DPP row.  63 VGPRs; left alone the SGPRs (about
@@ -720,6 +845,7 @@ hipError_t launch_two(AttArgs a, void* scratch, bool dst, hipStream_t s) {
   if (g_att_variant == 3) k = (const void*)pz_wire_att_size_512x4_kernel, T = 512, tile = 2048;
   if (g_att_variant == 4) k = (const void*)pz_wire_att_size_256x8_kernel, T = 256, tile = 2048;
   if (g_att_variant == 5) k = (const void*)pz_wire_att_size_1024x2_kernel, T = 1024, tile = 2048;
+  if (g_att_variant == 7) k = (const void*)pz_wire_att_size_loops_kernel;
 #endif
   const uint64_t tiles = (a.n + tile - 1) / tile;
   a.status = static_cast<uint64_t*>(scratch);

@@ -47,7 +47,7 @@ def main():
     ms = e0.elapsed_time(e1) / reps
     dll = _lib.lib.dll
     if hasattr(dll, "pz_debug_set_att_write_variant"):  # same-process A/B (PZ_PROBE_LIB=build/ab/...)
-        for v in (0, 6, 1, 2, 3, 0):  # product / aligned-dword stage / r4 three launches / byte-wise stage / sizing 512x4
+        for v in (0, 7, 6, 1, 0, 7):  # product / sizing loops (r5 first form) / aligned-dword stage / r4 three launches
             dll.pz_debug_set_att_write_variant(v)
             e0.record()
             for _ in range(reps):
