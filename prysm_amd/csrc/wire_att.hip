@@ -55,6 +55,9 @@ struct AttArgs {
 };
 
 __device__ __forceinline__ uint32_t vlen(uint64_t x) { return (uint32_t)((70 - __clzll(x | 1)) / 7); }
+// 32-bit values: one v_ffbh instead of two; (38 - clz) / 7 as a multiply by 37 and a shift
+// (exact for 38 - clz in [7, 38])
+__device__ __forceinline__ uint32_t vlen32(uint32_t x) { return ((38u - (uint32_t)__clz(x | 1)) * 37u) >> 8; }
 
 __device__ __forceinline__ uint8_t* put_varint(uint8_t* p, uint64_t x) {
   while (x >= 0x80) {
@@ -63,6 +66,53 @@ __device__ __forceinline__ uint8_t* put_varint(uint8_t* p, uint64_t x) {
   }
   *p++ = (uint8_t)x;
   return p;
+}
+
+// put_varint into the LDS stage with at most four stores (8-, 4-, 2- and 1-byte pieces,
+// unaligned): x's 7-bit groups spread into three dwords by bit-field extracts, the
+// continuation bits from n = vlen(x).  ~35 VALU instructions for a 10-byte value against ~60
+// for the byte loop; values under 128 keep the single byte store.
+__device__ __forceinline__ void put_varint_pieces(uint8_t* p, uint64_t x) {
+  if (x < 0x80) {
+    *p = (uint8_t)x;
+    return;
+  }
+  const uint32_t n = vlen(x), lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t m = __builtin_amdgcn_alignbit(hi, lo, 28);  // bits 28..59
+  uint32_t w0 = (lo & 0x7f) | (__builtin_amdgcn_ubfe(lo, 7, 7) << 8) | (__builtin_amdgcn_ubfe(lo, 14, 7) << 16) |
+                (__builtin_amdgcn_ubfe(lo, 21, 7) << 24);
+  uint32_t w1 = (m & 0x7f) | (__builtin_amdgcn_ubfe(m, 7, 7) << 8) | (__builtin_amdgcn_ubfe(m, 14, 7) << 16) |
+                (__builtin_amdgcn_ubfe(m, 21, 7) << 24);
+  uint32_t w2 = __builtin_amdgcn_ubfe(hi, 24, 7) | ((hi >> 31) << 8);
+  const uint32_t k = n - 1;  // bytes 0 .. k-1 carry the continuation bit (k in 1..9)
+  const uint64_t c = k >= 8 ? ~0ull : (1ull << (8 * k)) - 1;
+  w0 |= 0x80808080u & (uint32_t)c;
+  w1 |= 0x80808080u & (uint32_t)(c >> 32);
+  w2 |= k >= 9 ? 0x80u : 0u;
+  if (n >= 8) {
+    const uint2 v = make_uint2(w0, w1);
+    __builtin_memcpy(p, &v, 8);
+    if (n == 10) {
+      const uint16_t h = (uint16_t)w2;
+      __builtin_memcpy(p + 8, &h, 2);
+    } else if (n == 9) {
+      p[8] = (uint8_t)w2;
+    }
+  } else {
+    uint32_t t = w0, o = 0;
+    if (n & 4) {
+      __builtin_memcpy(p, &w0, 4);
+      t = w1;
+      o = 4;
+    }
+    if (n & 2) {
+      const uint16_t h = (uint16_t)t;
+      __builtin_memcpy(p + o, &h, 2);
+      t >>= 16;
+      o += 2;
+    }
+    if (n & 1) p[o] = (uint8_t)t;
+  }
 }
 
 __device__ __forceinline__ uint64_t wsum(uint64_t x) {
@@ -446,7 +496,7 @@ __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*
   }
   const uint64_t long_seg = __ballot(fast && seg_len > kSegMax);
   if ((long_seg >> (kRow * ri)) & 0xffffull) fast = false;
-  const uint32_t esz = fast && (uint64_t)sl < nob ? 1 + vlen(el) + el : 0;
+  const uint32_t esz = fast && (uint64_t)sl < nob ? 1 + vlen32(el) + el : 0;
   const uint32_t ssz = fast && (uint64_t)sl < nsig ? vlen(sv) : 0;
   const uint32_t einc = rscan32(esz), sinc = rscan32(ssz);
   const uint32_t obl = bc32<15>(einc), sigb = bc32<15>(sinc);
@@ -479,11 +529,11 @@ __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*
       span = obl;
     } else if (sl == 8) {
       val = sigb;
-      span = sigb ? 1 + vlen(sigb) + sigb : 0;
+      span = sigb ? 1 + vlen32(sigb) + sigb : 0;
     }
     const uint32_t inc = rscan32(span);
     const uint32_t body = bc32<8>(inc);
-    const uint32_t frame = a.field ? a.tag_len + vlen(body) : 0;
+    const uint32_t frame = a.field ? a.tag_len + vlen32(body) : 0;
     const uint32_t pos = frame + inc - span;
     if (sl == 0 && a.field) {
       uint8_t* q = put_varint(st, ((uint64_t)a.field << 3) | 2);
@@ -500,10 +550,16 @@ __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*
       st[ep] = (7 << 3) | 2;
       put_varint(st + ep + 1, el);
     }
-    const uint32_t ed = shr3(ep + 1 + vlen(el));
+    const uint32_t ed = shr3(ep + 1 + vlen32(el));
     if (sl >= 3 && (uint64_t)(sl - 3) < nob) seg_dst = ed;
-    const uint32_t sp = bc32<8>(pos) + 1 + vlen(sigb);
-    if ((uint64_t)sl < nsig) put_varint(st + sp + sinc - ssz, sv);
+    const uint32_t sp = bc32<8>(pos) + 1 + vlen32(sigb);
+    if ((uint64_t)sl < nsig) {
+      if (M == 2) {
+        put_varint_pieces(st + sp + sinc - ssz, sv);
+      } else {
+        put_varint(st + sp + sinc - ssz, sv);
+      }
+    }
   }
   if (M < 2) {
     stage_segment_aligned<M>(stage[ri], sh + seg_dst, wv, r, len);
@@ -684,7 +740,7 @@ __device__ __forceinline__ void size_records(const AttArgs& a, uint64_t t0, uint
 #pragma unroll
       for (uint32_t e = 0; e < kSizeElems; ++e) {
         const uint32_t next = e + 1 < kSizeElems ? lw[r][e] : (uint32_t)olast[r];
-        vl += e < no[q] ? vlen(next - prev) : 0;
+        vl += e < no[q] ? vlen32(next - prev) : 0;
         prev = next;
       }
       uint64_t sigb = 0;
@@ -815,8 +871,9 @@ PZ_ATT_WRITE(pz_wire_att_write_kernel, 2)
 #ifdef PZ_AB_BUILD
 PZ_ATT_WRITE(pz_wire_att_write_bytes_kernel, 0)
 PZ_ATT_WRITE(pz_wire_att_write_aligned_kernel, 1)
+PZ_ATT_WRITE(pz_wire_att_write_sigloop_kernel, 3)  // the product with the byte-loop signature varints
 // 1 round 4's three launches, 2 this scan + byte-wise stage, 3-5 other sizing tiles, 6 the
-// aligned-dword stage
+// aligned-dword stage, 7 the sizing loops, 8 byte-loop signature varints
 int g_att_variant = 0;
 #endif
 
@@ -828,6 +885,7 @@ hipError_t launch_write(const AttArgs& a, bool dst, hipStream_t s) {
 #ifdef PZ_AB_BUILD
   if (!dst) k = (const void*)pz_wire_att_write_bytes_kernel;
   if (g_att_variant == 6) k = (const void*)pz_wire_att_write_aligned_kernel;
+  if (g_att_variant == 8) k = (const void*)pz_wire_att_write_sigloop_kernel;
 #else
   (void)dst;
 #endif

@@ -47,7 +47,7 @@ def main():
     ms = e0.elapsed_time(e1) / reps
     dll = _lib.lib.dll
     if hasattr(dll, "pz_debug_set_att_write_variant"):  # same-process A/B (PZ_PROBE_LIB=build/ab/...)
-        for v in (0, 7, 6, 1, 0, 7):  # product / sizing loops (r5 first form) / aligned-dword stage / r4 three launches
+        for v in (0, 8, 7, 6, 0, 8, 7):  # product / byte-loop sig varints / sizing loops (r5 first form) / aligned-dword stage
             dll.pz_debug_set_att_write_variant(v)
             e0.record()
             for _ in range(reps):
