@@ -180,7 +180,8 @@ size_t window_lds_bytes(const WinArgs& w) { return 8ull * ((size_t)w.lds_maxc + 
 // meeting's wait bound at zero (the fallback count in every block that arrives before its
 // partners; exact), 64 the first pieces' loads issued after the prologue (exact), 128 an
 // instance's blocks grouped on one XCD (exact), 144 = 128 + 16, 4096 the four-sum tallies on
-// narrow offsets (exact).
+// narrow offsets (exact), 8192 no speculation: the whole count before the loop (exact), 32
+// (alone) the speculating blocks' post-loop meeting skipped, the fallback count every time (exact).
 template <bool B32, int SEW, bool LLB, int AB = 0, int D = kWinDepth, bool TR = false, bool NA = false>
 __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w) {
   extern __shared__ __align__(16) uint8_t lds_dyn[];
@@ -247,7 +248,13 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   // block counts only its share of the chunks and attestations and the R blocks meet in pacc.
   uint64_t pop = 0, err = 0;
   const uint64_t nch = (pend - pbase + 15) / 16, clb = LLB ? (lbase - pbase) / 16 : nch;
-  const bool coop = (AB & 16) && w.pacc != nullptr && w.R > 1;
+  // Speculation (the product, R > 1): each of the instance's R blocks counts its 1/R share and
+  // publishes it without waiting, runs the loop as if the reward applies (the common case), and
+  // meets its partners after the loop, when they have long published; if the reward does not
+  // apply after all, the block puts its own positions back (the rare path).  A/B bit 8192: the
+  // whole count before the loop in every block (round 5's first form).
+  const bool spec = !(AB & (8192 | 16 | 2)) && w.pacc != nullptr && w.R > 1;
+  const bool coop = spec || ((AB & 16) && w.pacc != nullptr && w.R > 1);
   const uint64_t s0 = coop ? nch * r / w.R : 0, s1 = coop ? nch * (r + 1) / w.R : nch;
   const uint64_t g0s = coop ? (uint64_t)a.natt * r / w.R : 0, g1s = coop ? (uint64_t)a.natt * (r + 1) / w.R : a.natt;
   // bits of chunk c (its bytes inside [pbeg, pend) only)
@@ -328,7 +335,12 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   pop = 0, err = 0;
 #pragma unroll
   for (int k = 0; k < NW; ++k) pop += red[k][0], err += red[k][1];
-  if (coop && !(AB & 2)) {
+  if (spec) {  // publish this block's share; the meeting is after the loop
+    if (tid == 0) {
+      const uint64_t add = (1ull << 48) | (err ? 1ull << 39 : 0) | pop;
+      atomicAdd((unsigned long long*)&w.pacc[inst], (unsigned long long)add);
+    }
+  } else if (coop && !(AB & 2)) {
     // the instance's R blocks meet: one atomic adds this block's share, then thread 0 polls the
     // word (at the coherence point) until all R have arrived, or the bound passes and the block
     // counts everything itself (so no block ever depends on another being resident)
@@ -369,10 +381,13 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   if (TR && tid == 0) tstamp[1] = __builtin_amdgcn_s_memrealtime();
   const uint64_t lastL = pend - lb;
   const bool rwd_err = (a.nval_global - 1) >= 8 * lastL;  // CheckBit(last, N-1) panics (incentives.go:23)
-  const bool thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (a.total_deposit[inst] * 2ull);  // incentives.go:18-20
-  const uint64_t ferr = err ? (uint64_t)kErrBitfield : 0;
-  const bool skip = ferr != 0 || (thr && rwd_err);  // Go panics: balances stay untouched
-  const bool applied = thr && !skip;
+  bool thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (a.total_deposit[inst] * 2ull);  // incentives.go:18-20
+  uint64_t ferr = err ? (uint64_t)kErrBitfield : 0;
+  bool skip = ferr != 0 || (thr && rwd_err);  // Go panics: balances stay untouched
+  // (speculating: pop and err are this block's share; rwd_err rules the reward out whatever
+  // the count says, so then there is nothing to speculate on)
+  const bool spec_on = spec && !rwd_err;
+  bool applied = spec_on || (!spec && thr && !skip);
   const uint64_t d = a.dynasty[inst];
   const uint32_t d32 = (uint32_t)std::min<uint64_t>(d, 0xFFFFFFFFull);
   const uint64_t bbase = B32 ? w.bal32_base[inst] : 0;
@@ -383,6 +398,7 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   // at the end), the positions whose bounds do not classify them active
   uint64_t sum = 0;
   uint32_t nact = 0, nm = 0;
+  int32_t dsum = 0;  // the rewards' part of sum (taken back if the speculated reward does not apply)
   const uint32_t rwd = applied ? 1u : 0u;  // (not applied: the balances stay, offsets +- 0)
   for (uint32_t t = 0; t < nround; ++t) {
     const uint4 dnx = dv;     // round t + 1's descriptors (loaded a round ago)
@@ -501,10 +517,12 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
         // the offsets: (base + o +- 1) - base = o +- 1, inside u32 (the state's re-base bound)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          o4[i] += (rb[i] & 1) ? rwd : 0u - rwd;
+          const uint32_t dl = (rb[i] & 1) ? rwd : 0u - rwd;
+          o4[i] += dl;
           const bool ai = v[i] && act[i];
           sum += ai ? o4[i] : 0u;
           nact += ai ? 1u : 0u;
+          dsum += ai ? (int32_t)dl : 0;
         }
         if (applied) {
           if (all) {
@@ -518,7 +536,10 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       } else {
         if (applied) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) b[i] = (rb[i] & 1) ? b[i] + PZ_ATTESTER_REWARD : b[i] - PZ_ATTESTER_REWARD;
+          for (int i = 0; i < 4; ++i) {
+            b[i] = (rb[i] & 1) ? b[i] + PZ_ATTESTER_REWARD : b[i] - PZ_ATTESTER_REWARD;
+            dsum += (v[i] && act[i]) ? ((rb[i] & 1) ? (int32_t)PZ_ATTESTER_REWARD : -(int32_t)PZ_ATTESTER_REWARD) : 0;
+          }
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int i = 2 * h;
@@ -538,6 +559,67 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       dq[j] = piece(dnx, j);
       win_load<B32, SEW>(col, dq[j], lane, q[j]);
     }
+  }
+  if (spec) {
+    // the meeting: every partner published its share in its prologue; the bound and the
+    // fallback (the whole count here) keep a block from ever depending on another's residency
+    __shared__ uint64_t s_meet2;
+    if (tid == 0) {
+      uint64_t v = __hip_atomic_fetch_add(&w.pacc[inst], (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (AB & 32) v = 0;  // (A/B, tests: the fallback count every time)
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while ((v >> 48) < w.R && !(AB & 32) && __builtin_amdgcn_s_memrealtime() - t0 < kCoopSpinTicks) {
+        __builtin_amdgcn_s_sleep(2);
+        v = __hip_atomic_fetch_add(&w.pacc[inst], (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      s_meet2 = v;
+    }
+    __syncthreads();
+    const uint64_t v = s_meet2;
+    if ((v >> 48) >= w.R) {
+      pop = v & ((1ull << 39) - 1);
+      err = (v >> 39) & 511;
+    } else {
+      pop = 0, err = 0;
+      count_range(0, clb, 0, a.natt);
+      count_lds(clb, nch);
+      pop = wsum64_dpp(pop);
+      err = wsum64_dpp(err);
+      if (lane == 0) red[wave][0] = pop, red[wave][1] = err;
+      __syncthreads();
+      pop = 0, err = 0;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) pop += red[k][0], err += red[k][1];
+    }
+    thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (a.total_deposit[inst] * 2ull);
+    ferr = err ? (uint64_t)kErrBitfield : 0;
+    skip = ferr != 0 || (thr && rwd_err);
+    const bool final_applied = thr && !skip;
+    if (spec_on && !final_applied) {
+      // the rare path: this block's positions back to their pre-reward values (each lane the
+      // positions it wrote: piece k of the range went to wave k mod NW)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (uint32_t k = wave; k < np; k += NW) {
+        const uint4 d0 = pinfo[2 * k];
+        const uint32_t pa = d0.x & ~3u, pp = pa + 4 * (uint32_t)lane;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (pp + i - d0.x >= d0.y) continue;  // (u32: outside the piece)
+          const uint32_t ix = a.co_index[pp + i];
+          const bool up = (lbf8[ix >> 3] >> (7 - (ix & 7))) & 1;
+          // (the block's own stores read back at L2: agent-scope loads, past any L1 copy)
+          if (B32) {
+            const uint32_t o = __hip_atomic_load(&Bal32[pp + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            Bal32[pp + i] = o - (up ? 1u : 0u - 1u);
+          } else {
+            const uint64_t o = __hip_atomic_load(&Bal[pp + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            Bal[pp + i] = up ? o - PZ_ATTESTER_REWARD : o + PZ_ATTESTER_REWARD;
+          }
+        }
+      }
+      sum -= (uint64_t)(int64_t)dsum;
+    }
+    applied = final_applied;
   }
   if (B32) sum += (uint64_t)nact * bbase;  // (the lane's sum of base + offset over its active positions)
   sum = wsum64_dpp(sum);
@@ -628,6 +710,7 @@ PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_g_kernel, false, 64, false, false)
 PZ_WINDOW_ABL(0, 2) PZ_WINDOW_ABL(0, 3) PZ_WINDOW_ABL(0, 4)
 PZ_WINDOW_ABL(1, 2) PZ_WINDOW_ABL(2, 2) PZ_WINDOW_ABL(4, 2) PZ_WINDOW_ABL(7, 2) PZ_WINDOW_ABL(16, 2)
 PZ_WINDOW_ABL(48, 2) PZ_WINDOW_ABL(64, 2) PZ_WINDOW_ABL(128, 2) PZ_WINDOW_ABL(144, 2) PZ_WINDOW_ABL(4096, 2)
+PZ_WINDOW_ABL(8192, 2) PZ_WINDOW_ABL(32, 2)
 // the product form with phase stamps (tools/epoch_trace.py)
 extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_kernel(EpochArgs a, WinArgs w) {
   window_body<true, 16, true, 0, kWinDepth16, true, true>(a, w);
@@ -683,6 +766,8 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
       case 4096: k = (const void*)pz_epoch_window_abl4096_d2_kernel; break;
       case 144: k = (const void*)pz_epoch_window_abl144_d2_kernel; break;
       case 64: k = (const void*)pz_epoch_window_abl64_d2_kernel; break;
+      case 8192: k = (const void*)pz_epoch_window_abl8192_d2_kernel; break;
+      case 32: k = (const void*)pz_epoch_window_abl32_d2_kernel; break;
       default: return hipErrorInvalidValue;
     }
   }

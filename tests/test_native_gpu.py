@@ -233,12 +233,14 @@ def test_native_epoch_single_launch_matches_window_pass(n):
 
 
 @pytest.mark.ab
-@pytest.mark.parametrize("abl", [16, 48])
+@pytest.mark.parametrize("abl", [16, 48, 8192, 32])
 @pytest.mark.parametrize("n,B,short", [(65536, 5, False), (1 << 20, 2, False), (4096, 3, True)])
 def test_native_epoch_window_meeting_fallbacks(abl, n, B, short):
     """The A/B meeting of an instance's R blocks (each counts 1/R of the bitfields, epoch_window.hip
     WinArgs.pacc; 16) and its fallback (48: the wait bound at zero, so a block that arrives
-    before its partners counts the whole instance itself), each exact.  Two steps against the oracle; or one with a short committee bitfield in
+    before its partners counts the whole instance itself); the whole count before the loop
+    (8192, no speculation); the speculating product's post-loop fallback count taken every
+    time (32); each exact.  Two steps against the oracle; or one with a short committee bitfield in
     instance 0 (its flags, its balances untouched)."""
     dll = _lib.lib.dll
     old = dll.pz_debug_set_window_ablation(abl)
