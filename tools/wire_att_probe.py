@@ -47,7 +47,10 @@ def main():
     ms = e0.elapsed_time(e1) / reps
     dll = _lib.lib.dll
     if hasattr(dll, "pz_debug_set_att_write_variant"):  # same-process A/B (PZ_PROBE_LIB=build/ab/...)
-        for v in (0, 8, 7, 6, 0, 8, 7):  # product / byte-loop sig varints / sizing loops (r5 first form) / aligned-dword stage
+        # product / byte-loop sig varints / sizing loops (r5 first form) / aligned-dword stage;
+        # WATT_VARIANTS=a,b,... another list
+        vs = [int(x) for x in os.environ.get("WATT_VARIANTS", "0,8,7,6,0,8,7").split(",")]
+        for v in vs:
             dll.pz_debug_set_att_write_variant(v)
             e0.record()
             for _ in range(reps):
