@@ -597,13 +597,17 @@ def test_gpu_replay_vote_queue_forms_vs_c_port(forms):
 
 @pytest.mark.gpu
 @pytest.mark.ab
-@pytest.mark.parametrize("path,epack", [("segments", "copy"), ("packed", "copy"), ("direct", "direct")])
-def test_ab_replay_vote_queue_paths_vs_c_port(path, epack, monkeypatch):
+@pytest.mark.parametrize("path,epack,prep", [("segments", "copy", ""), ("packed", "copy", ""), ("direct", "direct", ""),
+                                             ("direct", "direct", "merged"), ("direct", "copy", "merged")])
+def test_ab_replay_vote_queue_paths_vs_c_port(path, epack, prep, monkeypatch):
     """The A/B library's measured-and-dropped ways a flush reaches the device (PZ_VOTE_PATH: the
-    queue's arrays staged by one multi-segment copy, or round 3's packed arena) and the
-    transitions' epoch kernels reading their inputs in place (PZ_EPOCH_PACK=direct)."""
+    queue's arrays staged by one multi-segment copy, or round 3's packed arena), the
+    transitions' epoch kernels reading their inputs in place (PZ_EPOCH_PACK=direct), and the
+    stateRecalc's tally and epoch count blocks in one grid (PZ_EPOCH_PREP=merged:
+    pz_vote_words_count_kernel)."""
     monkeypatch.setenv("PZ_VOTE_PATH", path)
     monkeypatch.setenv("PZ_EPOCH_PACK", epack)
+    monkeypatch.setenv("PZ_EPOCH_PREP", prep)
     _vote_queue_chain()
 
 
