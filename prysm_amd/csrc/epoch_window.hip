@@ -238,6 +238,9 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
     for (int j = 0; j < D; ++j) win_load<B32, SEW>(col, dq[j], lane, q[j]);
   }
   dv = desc(1);
+  // the epilogue's first attestation per thread: its catt entry now (one VGPR through the loop),
+  // its att_comm / att_win words as the loop ends, so the epilogue starts with them at hand
+  const uint32_t ga0 = (uint32_t)tid < nk ? w.catt[gb + k0 + tid] : 0u;
   const WinLds L = win_lds(lds_dyn, w);
   const uint32_t ncr = cr1 - cr0;
   for (uint32_t i = tid; i < ncr; i += NT) L.tot[i] = 0;
@@ -560,6 +563,12 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       win_load<B32, SEW>(col, dq[j], lane, q[j]);
     }
   }
+  uint32_t cm0 = 0;
+  uint4 aw0 = make_uint4(0, 0, 0, 0);
+  if ((uint32_t)tid < nk) {
+    cm0 = a.att_comm[gb + ga0];
+    aw0 = w.att_win[gb + ga0];
+  }
   if (spec) {
     // the meeting: every partner published its share in its prologue; the bound and the
     // fallback (the whole count here) keep a block from ever depending on another's residency
@@ -656,12 +665,13 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   // the range's attestations: tallies out, the winner rule (core.go:549-555: the first
   // attestation, in order, whose 3 * vote >= 2 * total and whose dynasty beats its shard's record)
   for (uint32_t kq = tid; kq < nk; kq += NT) {
-    const uint32_t ga = w.catt[gb + k0 + kq];
-    const uint32_t cl = a.att_comm[gb + ga] - w.cg0 - cr0;
+    const bool first = kq == (uint32_t)tid;
+    const uint32_t ga = first ? ga0 : w.catt[gb + k0 + kq];
+    const uint32_t cl = (first ? cm0 : a.att_comm[gb + ga]) - w.cg0 - cr0;
     const uint64_t V = L.vot[kq], T = L.tot[cl];
     a.vote[gb + ga] = V;
     a.total[gb + ga] = T;
-    const uint4 aw = w.att_win[gb + ga];  // {shard, its record's dynasty lo, hi}
+    const uint4 aw = first ? aw0 : w.att_win[gb + ga];  // {shard, its record's dynasty lo, hi}
     if (3ull * V >= 2ull * T && d > pk64(aw.y, aw.z)) atomicMin(&a.winner[inst * a.nrec + aw.x], ga);
   }
   if (TR) {
