@@ -382,6 +382,15 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
     for (int j = 0; j < D; ++j) win_load<B32, SEW>(col, dq[j], lane, q[j]);
   }
   if (TR && tid == 0) tstamp[1] = __builtin_amdgcn_s_memrealtime();
+  // the next step's accumulators start from zero, its winners empty (its own buffers: issued
+  // here, the stores drain under the loop instead of at the kernel's end)
+  if (r == 0) {
+    if (a.scal_next && tid < kScal) a.scal_next[inst * kScal + tid] = 0;
+    if (w.pacc_next && tid == 0) w.pacc_next[inst] = 0;
+    for (uint32_t s = tid; s < a.nrec; s += NT) w.winner_next[inst * a.nrec + s] = 0xFFFFFFFFu;
+    if (w.vote_next)
+      for (uint32_t g = tid; g < a.natt; g += NT) w.vote_next[gb + g] = 0, w.total_next[gb + g] = 0;
+  }
   const uint64_t lastL = pend - lb;
   const bool rwd_err = (a.nval_global - 1) >= 8 * lastL;  // CheckBit(last, N-1) panics (incentives.go:23)
   bool thr = (pop * PZ_DEFAULT_BALANCE * 3ull) >= (a.total_deposit[inst] * 2ull);  // incentives.go:18-20
@@ -654,13 +663,6 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       sc[kErrRwd] = rwd_err ? 1 : 0;
       if (ferr) atomicAdd((unsigned long long*)&sc[kErrXl], (unsigned long long)ferr);
     }
-  }
-  if (r == 0) {  // the next step's accumulators start from zero, its winners empty
-    if (a.scal_next && tid < kScal) a.scal_next[inst * kScal + tid] = 0;
-    if (w.pacc_next && tid == 0) w.pacc_next[inst] = 0;
-    for (uint32_t s = tid; s < a.nrec; s += NT) w.winner_next[inst * a.nrec + s] = 0xFFFFFFFFu;
-    if (w.vote_next)
-      for (uint32_t g = tid; g < a.natt; g += NT) w.vote_next[gb + g] = 0, w.total_next[gb + g] = 0;
   }
   // the range's attestations: tallies out, the winner rule (core.go:549-555: the first
   // attestation, in order, whose 3 * vote >= 2 * total and whose dynasty beats its shard's record)
