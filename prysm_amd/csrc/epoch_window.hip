@@ -181,7 +181,9 @@ size_t window_lds_bytes(const WinArgs& w) { return 8ull * ((size_t)w.lds_maxc + 
 // partners; exact), 64 the first pieces' loads issued after the prologue (exact), 128 an
 // instance's blocks grouped on one XCD (exact), 144 = 128 + 16, 4096 the four-sum tallies on
 // narrow offsets (exact), 8192 no speculation: the whole count before the loop (exact), 32
-// (alone) the speculating blocks' post-loop meeting skipped, the fallback count every time (exact).
+// (alone) the speculating blocks' post-loop meeting skipped, the fallback count every time (exact);
+// 16384 the product's L2 form (the reward bits looked up in the last bitfield in global memory,
+// no LDS copy; exact).
 template <bool B32, int SEW, bool LLB, int AB = 0, int D = kWinDepth, bool TR = false, bool NA = false>
 __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w) {
   extern __shared__ __align__(16) uint8_t lds_dyn[];
@@ -780,6 +782,7 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
       case 64: k = (const void*)pz_epoch_window_abl64_d2_kernel; break;
       case 8192: k = (const void*)pz_epoch_window_abl8192_d2_kernel; break;
       case 32: k = (const void*)pz_epoch_window_abl32_d2_kernel; break;
+      case 16384: k = (const void*)pz_epoch_window_b32n_s16_g_kernel; break;  // (the reward bits from L2, no LDS copy)
       default: return hipErrorInvalidValue;
     }
   }
