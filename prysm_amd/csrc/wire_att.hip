@@ -328,6 +328,11 @@ __device__ __forceinline__ uint64_t bc64(uint64_t x) {
   return ((uint64_t)bc32<K>((uint32_t)(x >> 32)) << 32) | bc32<K>((uint32_t)x);
 }
 
+// Lane l - 1 of the row (0 for l = 0; DPP row_shr:1).
+__device__ __forceinline__ uint32_t shr1(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x111, 0xf, 0xf, true);
+}
+
 // Lane l - 3 of the row (0 for l < 3; DPP row_shr:3).
 __device__ __forceinline__ uint32_t shr3(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x113, 0xf, 0xf, true);
@@ -456,48 +461,48 @@ __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*
   const uint64_t i = i0 + ri;
   const bool valid = i < a.n;
   const uint64_t hv = valid && sl < kHeadWords + 2 ? head_word(a, sl, i) : 0;
-  Head h;
-  h.v[0] = bc64<0>(hv);
-  h.v[1] = bc64<1>(hv);
-  h.v[2] = bc64<2>(hv);
-  h.b0[0] = bc64<3>(hv);
-  h.bl[0] = bc64<4>(hv) - h.b0[0];
-  h.b0[1] = bc64<5>(hv);
-  h.bl[1] = bc64<6>(hv) - h.b0[1];
-  h.b0[2] = bc64<7>(hv);
-  h.bl[2] = bc64<8>(hv) - h.b0[2];
-  h.o0 = bc64<9>(hv);
-  h.o1 = bc64<10>(hv);
-  h.s0 = bc64<11>(hv);
-  h.s1 = bc64<12>(hv);
-  const uint64_t o = bc64<13>(hv), size = bc64<14>(hv) - o;
-  const uint64_t nob = h.o1 - h.o0, nsig = h.s1 - h.s0;
-  bool fast = valid && size <= kStage && nob <= kMaxOblique && nsig <= kRow;
+  // Each lane's word below it (row_shr:1) and the difference: lanes 4, 6, 8 hold bl[0..2],
+  // lane 10 the oblique count, 12 the value count, 14 the size.  Only what every lane needs is
+  // broadcast; a lane's own operands come by one shift or one ds_bpermute.  Counts and lengths
+  // travel as 32 bits: the fast path needs size <= kStage, which bounds them all, and a high
+  // word that is not zero (malformed ranges) sends the record to the whole-wave path.
+  const uint64_t hb = ((uint64_t)shr1((uint32_t)(hv >> 32)) << 32) | shr1((uint32_t)hv);
+  const uint64_t hd = hv - hb;
+  const uint64_t o0 = bc64<9>(hv), s0 = bc64<11>(hv), o = bc64<13>(hv), size = bc64<14>(hd);
+  const uint32_t nob = bc32<10>((uint32_t)hd), nsig = bc32<12>((uint32_t)hd);
+  const uint64_t wide = __ballot(sl >= 4 && sl <= 12 && !(sl & 1) && (hd >> 32) != 0);  // (lanes 4-12, even)
+  bool fast = valid && size <= kStage && nob <= (uint32_t)kMaxOblique && nsig <= (uint32_t)kRow &&
+              !((wide >> (kRow * ri)) & 0xffffull);
+  // lanes 0-2: bytes field sl's start (word 3 + 2 sl) and length (difference 4 + 2 sl); lanes
+  // 4-6: field sl - 3's length for its header (difference 2 sl - 4)
+  const int rb = lane & ~(kRow - 1);
+  const int bsrc = rb + (sl < 3 ? 3 + 2 * sl : 0), lsrc = rb + (sl < 3 ? 4 + 2 * sl : sl >= 4 && sl <= 6 ? 2 * sl - 4 : 0);
+  const uint64_t b0s = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(4 * bsrc, (int)(uint32_t)(hv >> 32)) << 32) |
+                       (uint32_t)__builtin_amdgcn_ds_bpermute(4 * bsrc, (int)(uint32_t)hv);
+  const uint32_t bls = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * lsrc, (int)(uint32_t)hd);
   uint64_t eb0 = 0, sv = 0;
   uint32_t el = 0;
-  if (fast && (uint64_t)sl < nob) {
-    eb0 = a.ooff[h.o0 + sl];
-    el = (uint32_t)(a.ooff[h.o0 + sl + 1] - eb0);
+  if (fast && (uint32_t)sl < nob) {
+    eb0 = a.ooff[o0 + sl];
+    el = (uint32_t)(a.ooff[o0 + sl + 1] - eb0);
   }
-  if (fast && (uint64_t)sl < nsig) sv = a.sig[h.s0 + sl];
+  if (fast && (uint32_t)sl < nsig) sv = a.sig[s0 + sl];
   const uint32_t el_seg = shr3(el);
   const uint64_t eb_seg = ((uint64_t)shr3((uint32_t)(eb0 >> 32)) << 32) | shr3((uint32_t)eb0);
   uint64_t seg_len = 0;
   const uint8_t* seg_src = nullptr;
-#pragma unroll
-  for (int k = 0; k < 3; ++k)
-    if (sl == k) {
-      seg_len = h.bl[k];
-      seg_src = a.bdat[k] + h.b0[k];
-    }
-  if (sl >= 3 && (uint64_t)(sl - 3) < nob) {
+  if (sl < 3) {
+    seg_len = bls;
+    seg_src = (sl == 0 ? a.bdat[0] : sl == 1 ? a.bdat[1] : a.bdat[2]) + b0s;
+  }
+  if (sl >= 3 && (uint32_t)(sl - 3) < nob) {
     seg_len = el_seg;
     seg_src = a.odat + eb_seg;
   }
   const uint64_t long_seg = __ballot(fast && seg_len > kSegMax);
   if ((long_seg >> (kRow * ri)) & 0xffffull) fast = false;
-  const uint32_t esz = fast && (uint64_t)sl < nob ? 1 + vlen32(el) + el : 0;
-  const uint32_t ssz = fast && (uint64_t)sl < nsig ? vlen(sv) : 0;
+  const uint32_t esz = fast && (uint32_t)sl < nob ? 1 + vlen32(el) + el : 0;
+  const uint32_t ssz = fast && (uint32_t)sl < nsig ? vlen(sv) : 0;
   const uint32_t einc = rscan32(esz), sinc = rscan32(ssz);
   const uint32_t obl = bc32<15>(einc), sigb = bc32<15>(sinc);
   typedef const __attribute__((address_space(1))) uint32_t gword;
@@ -520,11 +525,11 @@ __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*
     uint64_t val = 0;
     uint32_t span = 0;
     if (sl >= 1 && sl <= 3) {
-      val = sl == 1 ? h.v[0] : sl == 2 ? h.v[1] : h.v[2];
+      val = hb;  // (fields 1-3: the word of lane sl - 1)
       span = val ? 1 + vlen(val) : 0;
     } else if (sl >= 4 && sl <= 6) {
-      val = sl == 4 ? h.bl[0] : sl == 5 ? h.bl[1] : h.bl[2];
-      span = val ? 1 + vlen(val) + (uint32_t)val : 0;
+      val = bls;
+      span = val ? 1 + vlen32(bls) + bls : 0;
     } else if (sl == 7) {
       span = obl;
     } else if (sl == 8) {
@@ -546,14 +551,14 @@ __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*
     const uint32_t fd = (uint32_t)__builtin_amdgcn_mov_dpp((int)(pos + 1 + vlen(val)), 0x104, 0xf, 0xf, true);
     if (sl < 3) seg_dst = fd;
     const uint32_t ep = bc32<7>(pos) + einc - esz;
-    if ((uint64_t)sl < nob) {
+    if ((uint32_t)sl < nob) {
       st[ep] = (7 << 3) | 2;
       put_varint(st + ep + 1, el);
     }
     const uint32_t ed = shr3(ep + 1 + vlen32(el));
-    if (sl >= 3 && (uint64_t)(sl - 3) < nob) seg_dst = ed;
+    if (sl >= 3 && (uint32_t)(sl - 3) < nob) seg_dst = ed;
     const uint32_t sp = bc32<8>(pos) + 1 + vlen32(sigb);
-    if ((uint64_t)sl < nsig) {
+    if ((uint32_t)sl < nsig) {
       if (M == 2) {
         put_varint_pieces(st + sp + sinc - ssz, sv);
       } else {
