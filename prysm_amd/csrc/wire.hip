@@ -307,7 +307,8 @@ __device__ __forceinline__ uint64_t lookback_window_waves(const uint64_t (&w)[LB
 
 template <int LB, bool kWaves = false>
 __device__ uint64_t lookback_finish(uint64_t* status, uint64_t tile, uint64_t (&w)[LB], uint64_t* lds,
-                                    uint32_t* lds_first, uint32_t* polls = nullptr, uint64_t* slots = nullptr) {
+                                    uint32_t* lds_first, uint32_t* polls = nullptr, uint64_t* slots = nullptr,
+                                    uint64_t* lbst = nullptr) {
   constexpr uint32_t kWin = kThreads * LB;
   uint64_t prefix = 0;
   int64_t j = (int64_t)tile - 1;
@@ -331,9 +332,11 @@ __device__ uint64_t lookback_finish(uint64_t* status, uint64_t tile, uint64_t (&
         if (!(w[q] >> 62)) w[q] = spins < 256 ? ld_status(status + idx) : ld_status_fresh(status + idx);
       }
     }
+    if (lbst && win == 0 && threadIdx.x == 0) lbst[0] = wall_clock64();  // (trace: the flags all seen)
     if (kWaves) {  // slots alternate by window: a wave is at most one barrier ahead
       bool found;
       prefix += lookback_window_waves<LB>(w, slots + (win & 1) * 4 * (kThreads / 64), &found, lds_first);
+      if (lbst && win == 0 && threadIdx.x == 0) lbst[1] = wall_clock64();  // (trace: the window reduced)
       if (found) return prefix;
       j -= kWin;
 #pragma unroll
@@ -483,7 +486,7 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   constexpr int kSubRecs = kThreads * PER, kTileRecs = kSub * kSubRecs, kStageBytes = 16 * kTileRecs;
   __shared__ uint64_t lds[kThreads / 64 + 1];
   __shared__ uint32_t s_tile, s_first, s_polls;
-  __shared__ uint64_t s_build_end, s_lbslots[2 * 4 * (kThreads / 64)];
+  __shared__ uint64_t s_build_end, s_lbslots[2 * 4 * (kThreads / 64)], s_lbst[2];
   __shared__ __attribute__((aligned(16))) uint32_t stage[kStageBytes / 4 + 8];
   uint64_t ts[6];
   if (V & 32) {
@@ -568,7 +571,8 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   if (V & 4) {
     base = (uint64_t)tile * 15 * kTileRecs;  // (ablation: output wrong)
   } else if (tile > 0) {
-    base = lookback_finish<LB, !(V & 1024)>(a.status, tile, w, lds, &s_first, (V & 32) ? &polls : nullptr, s_lbslots);
+    base = lookback_finish<LB, !(V & 1024)>(a.status, tile, w, lds, &s_first, (V & 32) ? &polls : nullptr, s_lbslots,
+                                            (V & 32) ? s_lbst : nullptr);
     // (variant 16384, tests only: no inclusive prefix is published, so every look-back walks
     // window after window back to tile 0 -- the multi-window path, with exact output)
     if (threadIdx.x == 0 && !(V & 16384)) st_status(a.status + tile, kFlagP | (base + agg));
@@ -596,6 +600,8 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
         t[10] = tile > 0 ? s_first : 0;      // distance of the nearest published prefix (last window)
         t[11] = s_build_end;                 // the last wave's end of the stage build
         t[12] = s_polls;                     // re-polls, most of any thread
+        t[13] = s_lbst[0];                   // thread 0: every window flag seen
+        t[14] = s_lbst[1];                   // thread 0: the window reduced (after its barrier)
       }
     }
     return;
@@ -632,6 +638,11 @@ PZ_WIRE_VAL_KERNEL(pz_wire_val_c5_kernel, 0, 5)
 // back window after window to tile 0; exact output)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v32_kernel, 32, 3)
 PZ_WIRE_VAL_KERNEL(pz_wire_val_v16384_kernel, 16384, 3)
+// trace forms (tools/wire_trace.py): 288 the first window's round trip timed alone, 36 no
+// look-back (output wrong), 544 no mid-build re-read of the window
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v288_kernel, 288, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v36_kernel, 36, 3)
+PZ_WIRE_VAL_KERNEL(pz_wire_val_v544_kernel, 544, 3)
 #endif
 #undef PZ_WIRE_VAL_KERNEL
 // (Round 4 tile-geometry A/B, measured and dropped: 3,072-record tiles at 6 waves per SIMD and
@@ -737,10 +748,15 @@ hipError_t launch_wire_validators(WireValArgs a, uint64_t* scratch, hipStream_t 
     const uint32_t n32 = (uint32_t)nt;
 #ifdef PZ_AB_BUILD
     if (g_wire_variant && a.nc == 3) {
-      if (g_wire_variant == 32) {
+      if (g_wire_variant == 32 || g_wire_variant == 288 || g_wire_variant == 36 || g_wire_variant == 544) {
         if (!g_wire_trace) return hipErrorInvalidValue;
         a.trace = g_wire_trace;
-        hipLaunchKernelGGL(pz_wire_val_v32_kernel, g, b, 0, s, a, n32);
+        const void* k = g_wire_variant == 288 ? (const void*)pz_wire_val_v288_kernel
+                        : g_wire_variant == 36 ? (const void*)pz_wire_val_v36_kernel
+                        : g_wire_variant == 544 ? (const void*)pz_wire_val_v544_kernel
+                                                : (const void*)pz_wire_val_v32_kernel;
+        void* args[] = {&a, const_cast<uint32_t*>(&n32)};
+        if (hipLaunchKernel(k, g, b, args, 0, s) != hipSuccess) return hipGetLastError();
       } else if (g_wire_variant == 16384) {
         hipLaunchKernelGGL(pz_wire_val_v16384_kernel, g, b, 0, s, a, n32);
       } else {

@@ -76,6 +76,11 @@ def main():
             "repolls_most_of_any_thread": {"median": float(np.median(t[1:, 12])), "p90": float(np.percentile(t[1:, 12], 90))},
             "first_window_round_trip_us": (round(float(np.median((t[1:, 8] - ts[1:, 2]) * 10 / 1e3)), 2)
                                            if variant & 256 else None),
+            # thread 0 inside the look-back (tiles > 0): build end -> every flag seen -> window
+            # reduced (its barrier) -> the phase's end
+            "lookback_flags_us": round(float(np.median((t[1:, 13] - ts[1:, 3]) * 10 / 1e3)), 2),
+            "lookback_reduce_us": round(float(np.median((t[1:, 14] - t[1:, 13]) * 10 / 1e3)), 2),
+            "lookback_tail_us": round(float(np.median((ts[1:, 4] - t[1:, 14]) * 10 / 1e3)), 2),
         })
     dll.pz_debug_set_wire_variant(0)
     dll.pz_debug_set_wire_trace(None)
