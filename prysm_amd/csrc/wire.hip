@@ -482,11 +482,16 @@ __device__ __forceinline__ uint32_t sub_offsets(const WireValArgs& a, uint64_t f
 // stage, two tiles per CU).  Smaller PER shrinks the tile, its stage and its held values
 // (round 4 A/B: three tiles per CU at PER 3).
 template <int V, int NC, int PER = kPer>
-__device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
+__device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt_arg) {
+  // (the tile count held in an SGPR from the start: left to the compiler, its kernel-argument
+  // load was re-issued after the look-back, and a scalar-cache miss there under the streaming
+  // load cost ~2 us per tile -- tools/wire_trace.py's look-back tail)
+  uint32_t nt = nt_arg;
+  asm volatile("" : "+s"(nt));
   constexpr int kSubRecs = kThreads * PER, kTileRecs = kSub * kSubRecs, kStageBytes = 16 * kTileRecs;
   __shared__ uint64_t lds[kThreads / 64 + 1];
   __shared__ uint32_t s_tile, s_first, s_polls;
-  __shared__ uint64_t s_build_end, s_lbslots[2 * 4 * (kThreads / 64)], s_lbst[2];
+  __shared__ uint64_t s_build_end, s_lbslots[2 * 4 * (kThreads / 64)], s_lbst[4];
   __shared__ __attribute__((aligned(16))) uint32_t stage[kStageBytes / 4 + 8];
   uint64_t ts[6];
   if (V & 32) {
@@ -573,10 +578,17 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
   } else if (tile > 0) {
     base = lookback_finish<LB, !(V & 1024)>(a.status, tile, w, lds, &s_first, (V & 32) ? &polls : nullptr, s_lbslots,
                                             (V & 32) ? s_lbst : nullptr);
+    if ((V & 32) && threadIdx.x == 0) s_lbst[2] = wall_clock64();  // (trace: returned)
     // (variant 16384, tests only: no inclusive prefix is published, so every look-back walks
     // window after window back to tile 0 -- the multi-window path, with exact output)
     if (threadIdx.x == 0 && !(V & 16384)) st_status(a.status + tile, kFlagP | (base + agg));
-    if (V & 32) atomicMax(&s_polls, polls);
+    if ((V & 32) && threadIdx.x == 0) s_lbst[3] = wall_clock64();  // (trace: prefix published)
+    if (V & 32) {  // (a wave max first: an LDS atomic of a divergent value compiles to a 64-step lane loop)
+      uint32_t m = polls;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+      if ((threadIdx.x & 63) == 0) atomicMax(&s_polls, m);
+    }
   }
   if (tile == nt - 1 && threadIdx.x == 0) {
     *a.total = base + agg;
@@ -595,13 +607,14 @@ __device__ __forceinline__ void wire_val_body(WireValArgs a, uint32_t nt) {
         for (int k = 0; k < 6; ++k) t[k] = ts[k];
         t[6] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID
         t[7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
-        t[8] = ts_arrive;
+        t[8] = (V & 256) ? ts_arrive : s_lbst[3];  // the first poll's arrival (256) or thread 0's prefix published
         t[9] = polls;                        // re-polls by thread 0 (the nearest entries)
         t[10] = tile > 0 ? s_first : 0;      // distance of the nearest published prefix (last window)
         t[11] = s_build_end;                 // the last wave's end of the stage build
         t[12] = s_polls;                     // re-polls, most of any thread
         t[13] = s_lbst[0];                   // thread 0: every window flag seen
         t[14] = s_lbst[1];                   // thread 0: the window reduced (after its barrier)
+        t[15] = s_lbst[2];                   // thread 0: back from the look-back
       }
     }
     return;

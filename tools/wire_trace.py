@@ -81,6 +81,9 @@ def main():
             "lookback_flags_us": round(float(np.median((t[1:, 13] - ts[1:, 3]) * 10 / 1e3)), 2),
             "lookback_reduce_us": round(float(np.median((t[1:, 14] - t[1:, 13]) * 10 / 1e3)), 2),
             "lookback_tail_us": round(float(np.median((ts[1:, 4] - t[1:, 14]) * 10 / 1e3)), 2),
+            "lookback_return_us": round(float(np.median((t[1:, 15] - t[1:, 14]) * 10 / 1e3)), 2),
+            "prefix_store_us": (round(float(np.median((t[1:, 8] - t[1:, 15]) * 10 / 1e3)), 2)
+                                if not variant & 256 else None),
         })
     dll.pz_debug_set_wire_variant(0)
     dll.pz_debug_set_wire_trace(None)
