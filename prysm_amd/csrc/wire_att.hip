@@ -833,11 +833,39 @@ __device__ __forceinline__ void size_body(const AttArgs& a) {
     size_records<T, P, 2>(a, t0, sz);
   }
   uint64_t ex[P], run = 0;
+  if (LOOPS) {
 #pragma unroll
-  for (int q = 0; q < P; ++q) {
-    uint64_t tot;
-    ex[q] = run + block_excl<T>(sz[q], s_wave, &tot);
-    run += tot;
+    for (int q = 0; q < P; ++q) {
+      uint64_t tot;
+      ex[q] = run + block_excl<T>(sz[q], s_wave, &tot);
+      run += tot;
+    }
+  } else {
+    // the P rows' scans together: P independent wave scans (their shuffles interleave), one
+    // barrier, then each row's offset from the waves' totals -- where a block scan per row
+    // took two barriers each
+    __shared__ uint64_t s_rows[P][T / 64];
+    const int lane = tid & 63, w = tid >> 6;
+    uint64_t incl[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) incl[q] = wscan(sz[q]);
+    if (lane == 63) {
+#pragma unroll
+      for (int q = 0; q < P; ++q) s_rows[q][w] = incl[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      uint64_t before = 0, all = 0;
+#pragma unroll
+      for (int k = 0; k < T / 64; ++k) {
+        const uint64_t x = s_rows[q][k];
+        before += k < w ? x : 0;
+        all += x;
+      }
+      ex[q] = run + before + incl[q] - sz[q];
+      run += all;
+    }
   }
   if (tid == 0) st_status(a.status + tile, (tile == 0 ? kFlagP : kFlagA) | run);
   const uint64_t base = tile == 0 ? 0 : lookback_tiles<T>(a.status, tile, &s_first, s_part);
