@@ -500,7 +500,7 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
           if (T) atomicAdd((unsigned long long*)&L.tot[cl], (unsigned long long)T);
           if (kind == 1 && V) atomicAdd((unsigned long long*)&L.vot[kb - k0], (unsigned long long)V);
         }
-        if (kind == 2) {  // several attestations: each one's bits from its bitfield in global memory
+        if (kind == 2 && !(AB & 65536)) {  // several attestations: each one's bits from its bitfield in global memory
           const uint32_t cs = pc.vbit;  // (kind 2: the committee's first position)
           const uint32_t ke = pc.vlim;  // (kind 2: the committee's attestations end at catt index ke)
           for (uint32_t kq = kb; kq < ke; ++kq) {
@@ -724,7 +724,7 @@ PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_g_kernel, false, 64, false, false)
 PZ_WINDOW_ABL(0, 2) PZ_WINDOW_ABL(0, 3) PZ_WINDOW_ABL(0, 4)
 PZ_WINDOW_ABL(1, 2) PZ_WINDOW_ABL(2, 2) PZ_WINDOW_ABL(4, 2) PZ_WINDOW_ABL(7, 2) PZ_WINDOW_ABL(16, 2)
 PZ_WINDOW_ABL(48, 2) PZ_WINDOW_ABL(64, 2) PZ_WINDOW_ABL(128, 2) PZ_WINDOW_ABL(144, 2) PZ_WINDOW_ABL(4096, 2)
-PZ_WINDOW_ABL(8192, 2) PZ_WINDOW_ABL(32, 2)
+PZ_WINDOW_ABL(8192, 2) PZ_WINDOW_ABL(32, 2) PZ_WINDOW_ABL(65536, 2)
 // the product form with phase stamps (tools/epoch_trace.py)
 extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_kernel(EpochArgs a, WinArgs w) {
   window_body<true, 16, true, 0, kWinDepth16, true, true>(a, w);
@@ -783,6 +783,7 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
       case 8192: k = (const void*)pz_epoch_window_abl8192_d2_kernel; break;
       case 32: k = (const void*)pz_epoch_window_abl32_d2_kernel; break;
       case 16384: k = (const void*)pz_epoch_window_b32n_s16_g_kernel; break;  // (the reward bits from L2, no LDS copy)
+      case 65536: k = (const void*)pz_epoch_window_abl65536_d2_kernel; break;  // (timing: no multi-attestation votes)
       default: return hipErrorInvalidValue;
     }
   }
