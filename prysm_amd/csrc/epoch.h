@@ -168,7 +168,10 @@ struct WinArgs {
   uint32_t cg0;               // the rank's first committee (global id)
   const uint32_t* catt;       // [B][natt] attestation indices grouped by committee (committee order)
   const uint32_t* att_csize;  // [B][natt] the size of each attestation's committee
-  const uint4* att_win;       // [B][natt] {shard (< nrec), its record's dynasty lo, hi, 0}
+  const uint4* cq;            // [B][natt] by catt index, for the epilogue: {attestation, its committee -
+                              //   the range's cr0 | (dynasty > its record's dynasty) << 31, shard, 0}
+  const uint2* ckb;           // [B][natt] by catt index: {bitfield's first byte from the instance's
+                              //   16-B-aligned bitfields start, its bits} (kind-2 pieces)
   uint32_t* bal32;            // [B][vstride] u32 balance offsets (or NULL: EpochArgs.balance)
   const uint64_t* bal32_base; // [B]
   const uint32_t* se16;       // [B][vstride] {start | end << 16} saturated (or NULL)

@@ -550,14 +550,11 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
   for (uint32_t k = 0; k <= nlc; ++k) lcs[k] = (uint32_t)((k < nlc ? coffs[cg0 + k] : s.hi) - s.lo);
   // per instance: the attestation columns
   std::vector<uint32_t> csz((size_t)Bp * natt);
-  std::vector<uint4> aw((size_t)Bp * natt);
   for (uint64_t b = 0; b < Bp; ++b) {
     const uint64_t gb = (i0 + b) * natt;
     for (uint64_t g = 0; g < natt; ++g) {
-      const uint32_t c = h->att_comm[gb + g], sh = h->att_shard[gb + g];  // (sh < nrec: plan_layout)
+      const uint32_t c = h->att_comm[gb + g];
       csz[b * natt + g] = (uint32_t)(coffs[c + 1] - coffs[c]);
-      const uint64_t rd = h->rec_dynasty[(i0 + b) * st->nrec + sh];
-      aw[b * natt + g] = make_uint4(sh, (uint32_t)rd, (uint32_t)(rd >> 32), 0);
     }
     if (h->boffs[gb + natt] - (h->boffs[gb] & ~15ull) >= (1ull << 28))
       return fail(PZ_EINVAL, "window pass: an instance's bitfields exceed 256 MiB");
@@ -649,14 +646,37 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
       pinfo[2 * (b * ptot + k) + 1] = make_uint4(kb, vbit, vlim, 0);
     }
   }
-  uint4 *d_rdesc = nullptr, *d_aw = nullptr, *d_pinfo = nullptr;
-  uint2* d_rk = nullptr;
+  // by catt index (one load per attestation, no catt -> column chains in the kernel): kind-2
+  // pieces' bitfields {first byte - pbase, bits} (< 2^28 bytes per instance: checked above), and
+  // the epilogue's {attestation, committee - its range's cr0 | winner-dynasty bit << 31, shard}
+  // (the state's dynasties and record dynasties are fixed at its creation; sh < nrec: plan_layout)
+  std::vector<uint2> ckb((size_t)Bp * natt);
+  std::vector<uint4> cq((size_t)Bp * natt, make_uint4(0, 0, 0, 0));
+  for (uint64_t b = 0; b < Bp; ++b) {
+    const uint64_t gb = (i0 + b) * natt, pbase = h->boffs[gb] & ~15ull;
+    for (uint64_t k = 0; k < natt; ++k) {
+      const uint32_t g = catt[gb + k];
+      const uint64_t bo = h->boffs[gb + g], blen = h->boffs[gb + g + 1] - bo;
+      ckb[b * natt + k] = make_uint2((uint32_t)(bo - pbase), (uint32_t)(8 * blen));
+    }
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint2 kr = rk[b * R + r];
+      for (uint32_t k = kr.x; k < kr.x + kr.y; ++k) {
+        const uint32_t g = catt[gb + k], sh = h->att_shard[gb + g];
+        const uint32_t cl = (uint32_t)(h->att_comm[gb + g] - cg0 - rdesc[r].x);
+        const bool beats = h->dynasty[i0 + b] > h->rec_dynasty[(i0 + b) * st->nrec + sh];
+        cq[b * natt + k] = make_uint4(g, cl | (beats ? 1u << 31 : 0u), sh, 0);
+      }
+    }
+  }
+  uint4 *d_rdesc = nullptr, *d_cq = nullptr, *d_pinfo = nullptr;
+  uint2 *d_rk = nullptr, *d_ckb = nullptr;
   uint32_t *d_csz = nullptr, *d_wn = nullptr;
   uint64_t* d_pacc = nullptr;
   int rc;
   if ((rc = upload(s, &d_rdesc, rdesc.data(), rdesc.size())) || (rc = upload(s, &d_pinfo, pinfo.data(), pinfo.size())) ||
       (rc = upload(s, &d_rk, rk.data(), rk.size())) || (rc = upload(s, &d_csz, csz.data(), csz.size())) ||
-      (rc = upload(s, &d_aw, aw.data(), aw.size())) ||
+      (rc = upload(s, &d_cq, cq.data(), cq.size())) || (rc = upload(s, &d_ckb, ckb.data(), ckb.size())) ||
       (rc = dalloc(s, &d_wn, (size_t)Bp * std::max<uint32_t>(st->nrec, 1))) || (rc = dalloc(s, &d_pacc, 2 * (size_t)Bp)))
     return rc;
   // the meeting word's fields (epoch.h WinArgs.pacc): bits below 2^39, at most 511 blocks
@@ -671,7 +691,8 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
   w.cg0 = (uint32_t)cg0;
   w.catt = q.f.catt;
   w.att_csize = d_csz;
-  w.att_win = d_aw;
+  w.cq = d_cq;
+  w.ckb = d_ckb;
   w.se16 = q.f.se16;
   w.se = q.f.se;
   w.vstride = s.np;

@@ -240,9 +240,6 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
     for (int j = 0; j < D; ++j) win_load<B32, SEW>(col, dq[j], lane, q[j]);
   }
   dv = desc(1);
-  // the epilogue's first attestation per thread: its catt entry now (one VGPR through the loop),
-  // its att_comm / att_win words as the loop ends, so the epilogue starts with them at hand
-  const uint32_t ga0 = (uint32_t)tid < nk ? w.catt[gb + k0 + tid] : 0u;
   const WinLds L = win_lds(lds_dyn, w);
   const uint32_t ncr = cr1 - cr0;
   for (uint32_t i = tid; i < ncr; i += NT) L.tot[i] = 0;
@@ -503,19 +500,63 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
         if (kind == 2 && !(AB & 65536)) {  // several attestations: each one's bits from its bitfield in global memory
           const uint32_t cs = pc.vbit;  // (kind 2: the committee's first position)
           const uint32_t ke = pc.vlim;  // (kind 2: the committee's attestations end at catt index ke)
-          for (uint32_t kq = kb; kq < ke; ++kq) {
-            const uint64_t ga = w.catt[gb + kq];
-            const uint64_t bo = a.boffs[gb + ga], nb = 8 * (a.boffs[gb + ga + 1] - bo);
-            uint64_t sv = 0;
+          if (AB & 131072) {  // (A/B: one attestation at a time, three dependent round trips each)
+            for (uint32_t kq = kb; kq < ke; ++kq) {
+              const uint64_t ga = w.catt[gb + kq];
+              const uint64_t bo = a.boffs[gb + ga], nb = 8 * (a.boffs[gb + ga + 1] - bo);
+              uint64_t sv = 0;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const uint64_t xb = (uint64_t)(p + i) - cs;  // the position's bit in the bitfield
-              const bool in = v[i] && xb < nb;
-              const uint32_t by = in ? a.bits[bo + (xb >> 3)] : 0u;
-              sv += (in && ((by >> (7 - (uint32_t)(xb & 7))) & 1)) ? (B32 ? bbase + o4[i] : b[i]) : 0;
+              for (int i = 0; i < 4; ++i) {
+                const uint64_t xb = (uint64_t)(p + i) - cs;  // the position's bit in the bitfield
+                const bool in = v[i] && xb < nb;
+                const uint32_t by = in ? a.bits[bo + (xb >> 3)] : 0u;
+                sv += (in && ((by >> (7 - (uint32_t)(xb & 7))) & 1)) ? (B32 ? bbase + o4[i] : b[i]) : 0;
+              }
+              sv = wsum64_dpp(sv);
+              if (lane == 0 && sv) atomicAdd((unsigned long long*)&L.vot[kq - k0], (unsigned long long)sv);
             }
-            sv = wsum64_dpp(sv);
-            if (lane == 0 && sv) atomicAdd((unsigned long long*)&L.vot[kq - k0], (unsigned long long)sv);
+          } else {
+            // two attestations per trip: both bitfields' {first byte, bits} from the plan's catt-ordered
+            // table (one round of loads, no catt -> boffs chain), both bitfields' bytes in the next;
+            // every lane loads (a position outside a bitfield reads its first byte, a bitfield of no
+            // bytes the other one's) and the bytes are pinned, so no load sits in a branch
+            const uint2* ckb = w.ckb + gb;
+            for (uint32_t kq = kb; kq < ke; kq += 2) {
+              const bool two = kq + 1 < ke;
+              uint2 e0 = ckb[kq], e1 = ckb[two ? kq + 1 : kq];
+              asm volatile("" : "+v"(e0.x), "+v"(e0.y), "+v"(e1.x), "+v"(e1.y));  // (both words before the branch)
+              const uint32_t nb0 = e0.y, nb1 = two ? e1.y : 0u;
+              if (!(nb0 | nb1)) continue;
+              const uint8_t* bq0 = col.vbits + (nb0 ? e0.x : e1.x);
+              const uint8_t* bq1 = col.vbits + (nb1 ? e1.x : e0.x);
+              uint32_t by0[4], by1[4];
+              bool in0[4], in1[4];
+              uint32_t xb[4];
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                xb[i] = p + i - cs;  // the position's bit in the bitfields (u32: below cs wraps high)
+                in0[i] = v[i] && xb[i] < nb0;
+                in1[i] = v[i] && xb[i] < nb1;
+                by0[i] = bq0[(in0[i] ? xb[i] : 0u) >> 3];
+                by1[i] = bq1[(in1[i] ? xb[i] : 0u) >> 3];
+              }
+#pragma unroll
+              for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(by0[i]), "+v"(by1[i]));
+              uint64_t sv0 = 0, sv1 = 0;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const uint32_t sh = 7 - (xb[i] & 7);
+                const uint64_t bv = B32 ? bbase + o4[i] : b[i];
+                sv0 += (in0[i] && ((by0[i] >> sh) & 1)) ? bv : 0;
+                sv1 += (in1[i] && ((by1[i] >> sh) & 1)) ? bv : 0;
+              }
+              sv0 = wsum64_dpp(sv0);
+              sv1 = wsum64_dpp(sv1);
+              if (lane == 0) {
+                if (sv0) atomicAdd((unsigned long long*)&L.vot[kq - k0], (unsigned long long)sv0);
+                if (sv1) atomicAdd((unsigned long long*)&L.vot[kq + 1 - k0], (unsigned long long)sv1);
+              }
+            }
           }
         }
       }
@@ -574,12 +615,14 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       win_load<B32, SEW>(col, dq[j], lane, q[j]);
     }
   }
-  uint32_t cm0 = 0;
-  uint4 aw0 = make_uint4(0, 0, 0, 0);
-  if ((uint32_t)tid < nk) {
-    cm0 = a.att_comm[gb + ga0];
-    aw0 = w.att_win[gb + ga0];
-  }
+  // the epilogue's first kEpiPf attestations per thread: their words now, ahead of the meeting
+  // (clamped indices: every load unconditional, none in a branch)
+  constexpr int kEpiPf = 3;
+  uint4 ep[kEpiPf];
+  const uint4* cq = w.cq + gb + k0;
+  const uint32_t nkm = nk ? nk - 1 : 0;
+#pragma unroll
+  for (int u = 0; u < kEpiPf; ++u) ep[u] = nk ? cq[min((uint32_t)tid + u * NT, nkm)] : make_uint4(0, 0, 0, 0);
   if (spec) {
     // the meeting: every partner published its share in its prologue; the bound and the
     // fallback (the whole count here) keep a block from ever depending on another's residency
@@ -668,16 +711,17 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   }
   // the range's attestations: tallies out, the winner rule (core.go:549-555: the first
   // attestation, in order, whose 3 * vote >= 2 * total and whose dynasty beats its shard's record)
-  for (uint32_t kq = tid; kq < nk; kq += NT) {
-    const bool first = kq == (uint32_t)tid;
-    const uint32_t ga = first ? ga0 : w.catt[gb + k0 + kq];
-    const uint32_t cl = (first ? cm0 : a.att_comm[gb + ga]) - w.cg0 - cr0;
+  auto epi = [&](uint32_t kq, const uint4 e) {  // e: {attestation, cl | winner-dynasty bit << 31, shard}
+    const uint32_t ga = e.x, cl = e.y & 0x7FFFFFFFu;
     const uint64_t V = L.vot[kq], T = L.tot[cl];
     a.vote[gb + ga] = V;
     a.total[gb + ga] = T;
-    const uint4 aw = first ? aw0 : w.att_win[gb + ga];  // {shard, its record's dynasty lo, hi}
-    if (3ull * V >= 2ull * T && d > pk64(aw.y, aw.z)) atomicMin(&a.winner[inst * a.nrec + aw.x], ga);
-  }
+    if ((e.y >> 31) && 3ull * V >= 2ull * T) atomicMin(&a.winner[inst * a.nrec + e.z], ga);
+  };
+#pragma unroll
+  for (int u = 0; u < kEpiPf; ++u)
+    if ((uint32_t)tid + u * NT < nk) epi(tid + u * NT, ep[u]);
+  for (uint32_t kq = tid + kEpiPf * NT; kq < nk; kq += NT) epi(kq, cq[kq]);
   if (TR) {
     __syncthreads();
     if (tid == 0) {
@@ -724,7 +768,7 @@ PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_g_kernel, false, 64, false, false)
 PZ_WINDOW_ABL(0, 2) PZ_WINDOW_ABL(0, 3) PZ_WINDOW_ABL(0, 4)
 PZ_WINDOW_ABL(1, 2) PZ_WINDOW_ABL(2, 2) PZ_WINDOW_ABL(4, 2) PZ_WINDOW_ABL(7, 2) PZ_WINDOW_ABL(16, 2)
 PZ_WINDOW_ABL(48, 2) PZ_WINDOW_ABL(64, 2) PZ_WINDOW_ABL(128, 2) PZ_WINDOW_ABL(144, 2) PZ_WINDOW_ABL(4096, 2)
-PZ_WINDOW_ABL(8192, 2) PZ_WINDOW_ABL(32, 2) PZ_WINDOW_ABL(65536, 2)
+PZ_WINDOW_ABL(8192, 2) PZ_WINDOW_ABL(32, 2) PZ_WINDOW_ABL(65536, 2) PZ_WINDOW_ABL(131072, 2)
 // the product form with phase stamps (tools/epoch_trace.py)
 extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_kernel(EpochArgs a, WinArgs w) {
   window_body<true, 16, true, 0, kWinDepth16, true, true>(a, w);
@@ -784,6 +828,7 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
       case 32: k = (const void*)pz_epoch_window_abl32_d2_kernel; break;
       case 16384: k = (const void*)pz_epoch_window_b32n_s16_g_kernel; break;  // (the reward bits from L2, no LDS copy)
       case 65536: k = (const void*)pz_epoch_window_abl65536_d2_kernel; break;  // (timing: no multi-attestation votes)
+      case 131072: k = (const void*)pz_epoch_window_abl131072_d2_kernel; break;  // (one attestation per trip)
       default: return hipErrorInvalidValue;
     }
   }
