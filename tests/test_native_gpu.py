@@ -267,6 +267,38 @@ def test_native_epoch_window_meeting_fallbacks(abl, n, B, short):
         dll.pz_debug_set_window_ablation(old)
 
 
+@pytest.mark.parametrize("case", ["ok", "threshold", "short_bitfield", "reward_panic"])
+def test_native_epoch_window_one_range(case):
+    """256 instances (one block each, R = 1, the bench's configs[2] geometry): the whole count
+    before the loop, no meeting; the threshold missed (half the bits set), a short committee
+    bitfield in instance 0 and the CheckBit(last, N-1) panic.  Two steps against the oracle, or
+    the flags and untouched balances."""
+    n, B = 1024, 256
+    inst = _inst(n, B, False, density=0.5 if case == "threshold" else 0.75,
+                 last_bits=n - 8 if case == "reward_panic" else None)
+    if case == "short_bitfield":
+        bo = inst["boffs"].astype(np.int64)
+        inst["bits"] = np.delete(inst["bits"], int(bo[3]) - 1)
+        bo[3:] -= 1
+        inst["boffs"] = bo.astype(np.uint64)
+    ne = NativeEpoch(inst, device=0)
+    assert ne.one_pass
+    if case in ("ok", "threshold"):
+        _check(ne, inst, steps=2)
+        return
+    ne.step()
+    bal, scal, _, _, _ = ne.results()
+    for b in range(B if case == "reward_panic" else 1):
+        assert scal[b, _lib.SCAL_APPLIED] == 0
+        np.testing.assert_array_equal(bal[b], inst["balance"][b][ne.validators()])
+    if case == "short_bitfield":
+        assert int(scal[0, _lib.SCAL_ERR_XL]) == 2
+        for b in range(1, 4):
+            nb, applied, nxt, v, t, w = oracle_epoch(inst, b)
+            assert bool(scal[b, _lib.SCAL_APPLIED]) == applied
+            np.testing.assert_array_equal(bal[b], nb[ne.validators()])
+
+
 @pytest.mark.parametrize("case", ["many_atts", "short_bitfield", "reward_panic", "empty_committees"])
 @pytest.mark.parametrize("B", [1, 3])
 def test_native_epoch_window_edges(case, B):
