@@ -169,7 +169,8 @@ struct WinArgs {
   const uint32_t* catt;       // [B][natt] attestation indices grouped by committee (committee order)
   const uint32_t* att_csize;  // [B][natt] the size of each attestation's committee
   const uint4* cq;            // [B][natt] by catt index, for the epilogue: {attestation, its committee -
-                              //   the range's cr0 | (dynasty > its record's dynasty) << 31, shard, 0}
+                              //   the range's cr0, shard, its record's dynasty lo}
+  const uint32_t* cqh;        // [B][natt] by catt index: its record's dynasty hi
   const uint2* ckb;           // [B][natt] by catt index: {bitfield's first byte from the instance's
                               //   16-B-aligned bitfields start, its bits} (kind-2 pieces)
   uint32_t* bal32;            // [B][vstride] u32 balance offsets (or NULL: EpochArgs.balance)

@@ -648,10 +648,11 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
   }
   // by catt index (one load per attestation, no catt -> column chains in the kernel): kind-2
   // pieces' bitfields {first byte - pbase, bits} (< 2^28 bytes per instance: checked above), and
-  // the epilogue's {attestation, committee - its range's cr0 | winner-dynasty bit << 31, shard}
-  // (the state's dynasties and record dynasties are fixed at its creation; sh < nrec: plan_layout)
+  // the epilogue's {attestation, committee - its range's cr0, shard, record dynasty} (the record
+  // dynasties are the state's, fixed at its creation like att_win's before; sh < nrec: plan_layout)
   std::vector<uint2> ckb((size_t)Bp * natt);
   std::vector<uint4> cq((size_t)Bp * natt, make_uint4(0, 0, 0, 0));
+  std::vector<uint32_t> cqh((size_t)Bp * natt, 0u);
   for (uint64_t b = 0; b < Bp; ++b) {
     const uint64_t gb = (i0 + b) * natt, pbase = h->boffs[gb] & ~15ull;
     for (uint64_t k = 0; k < natt; ++k) {
@@ -664,19 +665,20 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
       for (uint32_t k = kr.x; k < kr.x + kr.y; ++k) {
         const uint32_t g = catt[gb + k], sh = h->att_shard[gb + g];
         const uint32_t cl = (uint32_t)(h->att_comm[gb + g] - cg0 - rdesc[r].x);
-        const bool beats = h->dynasty[i0 + b] > h->rec_dynasty[(i0 + b) * st->nrec + sh];
-        cq[b * natt + k] = make_uint4(g, cl | (beats ? 1u << 31 : 0u), sh, 0);
+        const uint64_t rd = h->rec_dynasty[(i0 + b) * st->nrec + sh];
+        cq[b * natt + k] = make_uint4(g, cl, sh, (uint32_t)rd);
+        cqh[b * natt + k] = (uint32_t)(rd >> 32);
       }
     }
   }
   uint4 *d_rdesc = nullptr, *d_cq = nullptr, *d_pinfo = nullptr;
   uint2 *d_rk = nullptr, *d_ckb = nullptr;
-  uint32_t *d_csz = nullptr, *d_wn = nullptr;
+  uint32_t *d_csz = nullptr, *d_wn = nullptr, *d_cqh = nullptr;
   uint64_t* d_pacc = nullptr;
   int rc;
   if ((rc = upload(s, &d_rdesc, rdesc.data(), rdesc.size())) || (rc = upload(s, &d_pinfo, pinfo.data(), pinfo.size())) ||
       (rc = upload(s, &d_rk, rk.data(), rk.size())) || (rc = upload(s, &d_csz, csz.data(), csz.size())) ||
-      (rc = upload(s, &d_cq, cq.data(), cq.size())) || (rc = upload(s, &d_ckb, ckb.data(), ckb.size())) ||
+      (rc = upload(s, &d_cq, cq.data(), cq.size())) || (rc = upload(s, &d_cqh, cqh.data(), cqh.size())) || (rc = upload(s, &d_ckb, ckb.data(), ckb.size())) ||
       (rc = dalloc(s, &d_wn, (size_t)Bp * std::max<uint32_t>(st->nrec, 1))) || (rc = dalloc(s, &d_pacc, 2 * (size_t)Bp)))
     return rc;
   // the meeting word's fields (epoch.h WinArgs.pacc): bits below 2^39, at most 511 blocks
@@ -692,6 +694,7 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
   w.catt = q.f.catt;
   w.att_csize = d_csz;
   w.cq = d_cq;
+  w.cqh = d_cqh;
   w.ckb = d_ckb;
   w.se16 = q.f.se16;
   w.se = q.f.se;
