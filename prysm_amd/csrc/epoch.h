@@ -169,8 +169,9 @@ struct WinArgs {
   const uint32_t* catt;       // [B][natt] attestation indices grouped by committee (committee order)
   const uint32_t* att_csize;  // [B][natt] the size of each attestation's committee
   const uint4* cq;            // [B][natt] by catt index, for the epilogue: {attestation, its committee -
-                              //   the range's cr0, shard, its record's dynasty lo}
-  const uint32_t* cqh;        // [B][natt] by catt index: its record's dynasty hi
+                              //   the range's cr0, shard, its record's dynasty saturated to 32 bits}
+  const uint32_t* cqh;        // a dynasty >= 2^32 - 1 in the part: [B][natt] the record dynasty's high
+                              //   word (cq.w its low word), else NULL
   const uint2* ckb;           // [B][natt] by catt index: {bitfield's first byte from the instance's
                               //   16-B-aligned bitfields start, its bits} (kind-2 pieces)
   uint32_t* bal32;            // [B][vstride] u32 balance offsets (or NULL: EpochArgs.balance)

@@ -652,7 +652,9 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
   // dynasties are the state's, fixed at its creation like att_win's before; sh < nrec: plan_layout)
   std::vector<uint2> ckb((size_t)Bp * natt);
   std::vector<uint4> cq((size_t)Bp * natt, make_uint4(0, 0, 0, 0));
-  std::vector<uint32_t> cqh((size_t)Bp * natt, 0u);
+  bool dyn64 = false;  // (a dynasty past the saturated 32-bit compare: the high words too)
+  for (uint64_t b = 0; b < Bp; ++b) dyn64 = dyn64 || h->dynasty[i0 + b] >= 0xFFFFFFFFull;
+  std::vector<uint32_t> cqh(dyn64 ? (size_t)Bp * natt : 0, 0u);
   for (uint64_t b = 0; b < Bp; ++b) {
     const uint64_t gb = (i0 + b) * natt, pbase = h->boffs[gb] & ~15ull;
     for (uint64_t k = 0; k < natt; ++k) {
@@ -666,8 +668,8 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
         const uint32_t g = catt[gb + k], sh = h->att_shard[gb + g];
         const uint32_t cl = (uint32_t)(h->att_comm[gb + g] - cg0 - rdesc[r].x);
         const uint64_t rd = h->rec_dynasty[(i0 + b) * st->nrec + sh];
-        cq[b * natt + k] = make_uint4(g, cl, sh, (uint32_t)rd);
-        cqh[b * natt + k] = (uint32_t)(rd >> 32);
+        cq[b * natt + k] = make_uint4(g, cl, sh, dyn64 ? (uint32_t)rd : (uint32_t)std::min<uint64_t>(rd, 0xFFFFFFFFull));
+        if (dyn64) cqh[b * natt + k] = (uint32_t)(rd >> 32);
       }
     }
   }
@@ -694,7 +696,7 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
   w.catt = q.f.catt;
   w.att_csize = d_csz;
   w.cq = d_cq;
-  w.cqh = d_cqh;
+  w.cqh = dyn64 ? d_cqh : nullptr;
   w.ckb = d_ckb;
   w.se16 = q.f.se16;
   w.se = q.f.se;

@@ -619,15 +619,10 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   // (clamped indices: every load unconditional, none in a branch)
   constexpr int kEpiPf = 3;
   uint4 ep[kEpiPf];
-  uint32_t eph[kEpiPf];
   const uint4* cq = w.cq + gb + k0;
-  const uint32_t* cqh = w.cqh + gb + k0;
   const uint32_t nkm = nk ? nk - 1 : 0;
 #pragma unroll
-  for (int u = 0; u < kEpiPf; ++u) {
-    ep[u] = nk ? cq[min((uint32_t)tid + u * NT, nkm)] : make_uint4(0, 0, 0, 0);
-    eph[u] = nk ? cqh[min((uint32_t)tid + u * NT, nkm)] : 0u;
-  }
+  for (int u = 0; u < kEpiPf; ++u) ep[u] = nk ? cq[min((uint32_t)tid + u * NT, nkm)] : make_uint4(0, 0, 0, 0);
   if (spec) {
     // the meeting: every partner published its share in its prologue; the bound and the
     // fallback (the whole count here) keep a block from ever depending on another's residency
@@ -716,17 +711,21 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   }
   // the range's attestations: tallies out, the winner rule (core.go:549-555: the first
   // attestation, in order, whose 3 * vote >= 2 * total and whose dynasty beats its shard's record)
-  auto epi = [&](uint32_t kq, const uint4 e, uint32_t eh) {  // {attestation, cl, shard, record dynasty}
+  // (the dynasty compare on 32-bit saturated words: exact while the dynasty is below 2^32 - 1,
+  // else the plan adds the record dynasties' high words)
+  const uint32_t* cqh = w.cqh ? w.cqh + gb + k0 : nullptr;
+  auto epi = [&](uint32_t kq, const uint4 e) {  // {attestation, cl, shard, record dynasty}
     const uint32_t ga = e.x;
     const uint64_t V = L.vot[kq], T = L.tot[e.y];
     a.vote[gb + ga] = V;
     a.total[gb + ga] = T;
-    if (3ull * V >= 2ull * T && d > pk64(e.w, eh)) atomicMin(&a.winner[inst * a.nrec + e.z], ga);
+    const bool beats = cqh ? d > pk64(e.w, cqh[kq]) : d32 > e.w;
+    if (3ull * V >= 2ull * T && beats) atomicMin(&a.winner[inst * a.nrec + e.z], ga);
   };
 #pragma unroll
   for (int u = 0; u < kEpiPf; ++u)
-    if ((uint32_t)tid + u * NT < nk) epi(tid + u * NT, ep[u], eph[u]);
-  for (uint32_t kq = tid + kEpiPf * NT; kq < nk; kq += NT) epi(kq, cq[kq], cqh[kq]);
+    if ((uint32_t)tid + u * NT < nk) epi(tid + u * NT, ep[u]);
+  for (uint32_t kq = tid + kEpiPf * NT; kq < nk; kq += NT) epi(kq, cq[kq]);
   if (TR) {
     __syncthreads();
     if (tid == 0) {
