@@ -93,9 +93,6 @@ def parse():
     p.add_argument("--cpu-replay-blocks", type=int, default=1040,
                    help="blocks of the replay chain the CPU baseline (oracle/c/replay_ref.c) processes (~6 s)")
     p.add_argument("--no-epoch", action="store_true")
-    p.add_argument("--epoch-path", default="native", choices=["native", "torch"],
-                   help="native: pz_epoch_state (C ABI, the library's RCCL communicator); torch: DeviceEpoch "
-                        "over torch.distributed (the test double of the same orchestration)")
     p.add_argument("--epoch-layout", default="auto", choices=["auto", "twopass", "index"],
                    help="auto: committee order when every validator is active and the committees partition "
                         "the set, one-pass step (pz_epoch_host.layout); twopass: that layout, two-pass step; "
@@ -224,10 +221,8 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
     (N>1: 1,048,576 validators sharded over the ranks, RCCL all-reduce of the sums).
 
     The step is pz_epoch_state_step: kernels and RCCL collectives enqueued by the C ABI on
-    the library's streams (the path a cgo caller links).  ``--epoch-path torch`` runs the
-    same orchestration through torch.distributed instead (prysm_amd.epoch.DeviceEpoch)."""
+    the library's streams (the path a cgo caller links)."""
     from prysm_amd import casper, synth
-    from prysm_amd.epoch import DeviceEpoch
     from prysm_amd.native import NativeEpoch
 
     nval = nval or args.epoch_validators or (65536 if world == 1 else 1 << 20)
@@ -237,17 +232,11 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
     seed_a = b"A" + bytes(31)  # common.Hash{'A'} (casper/sharding_test.go:57)
     shuffled = casper.shuffle_indices(seed_a, np.arange(nval, dtype=np.uint32))
     inst = synth.epoch_batch(nval, ninst, seed=3, shuffled=shuffled)
-    native = args.epoch_path == "native"
-    if native:
-        de = NativeEpoch(inst, device=dev.index, comm=comm if world > 1 else None, layout=args.epoch_layout)
-        lo, hi, _, sp = de.shard(0)
-        stream = torch.cuda.ExternalStream(sp, device=dev)
-        step = de.step
-    else:
-        de = DeviceEpoch(inst, dev, rank=rank, world=world)
-        lo, hi = de.lo, de.hi
-        stream = torch.cuda.current_stream(dev)
-        step = lambda: de.step(stream)  # noqa: E731
+    native = True
+    de = NativeEpoch(inst, device=dev.index, comm=comm if world > 1 else None, layout=args.epoch_layout)
+    lo, hi, _, sp = de.shard(0)
+    stream = torch.cuda.ExternalStream(sp, device=dev)
+    step = de.step
     # a fixed count (not a time budget): at N > 1 every step holds collectives, so all ranks
     # must run the same number of them
     for _ in range(args.warmup + (30 if args.clock_warm_ms > 0 else 0)):
@@ -302,7 +291,7 @@ def epoch_leg(args, torch, dist, dev, rank, world, nval=None, ninst=None, baseli
                                "committee order, two-pass step" if de.committee_order else "index order")
                               if native else "index order"),
                    "path": ("pz_epoch_state_step (C ABI: HIP kernels + the library's RCCL communicator)"
-                            if native else "DeviceEpoch (pz_dev_epoch_* + torch.distributed collectives)")},
+                            if native else "")},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
                      "bytes_model": epoch_bytes_model(de, lay),
@@ -992,13 +981,13 @@ PROF_PHASES = ("parse", "digest_batch", "checks", "vote_queue", "vote_flush", "s
 
 
 def chain_phases_ms(ch):
-    """The chain engine's always-on phase clocks (pz_debug_chain_profile; the per-attestation
+    """The chain engine's always-on phase clocks (pz_chain_phase_times; the per-attestation
     ones, checks and vote_queue, run only under PZ_CHAIN_PROFILE and read 0 here)."""
     import ctypes
     from prysm_amd import _lib
     n = len(PROF_PHASES)
     pv = (ctypes.c_double * n)()
-    fn = _lib.lib.dll.pz_debug_chain_profile
+    fn = _lib.lib.dll.pz_chain_phase_times
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     k = fn(ch._h, pv, n)
     out = {PROF_PHASES[i]: round(pv[i] * 1e3, 3) for i in range(min(k, n - 2)) if pv[i] > 0}
@@ -1282,8 +1271,66 @@ def host_api_rate(records_np, reps=3):
                     "median of %d calls" % (n, records_np.shape[1], reps)}
 
 
+def avx2_host_rate(records_np, want, seconds):
+    """The library's AVX2 host hasher (prysm_amd/csrc/serial_hash.cpp: the row-vector BLAKE2b
+    compression, the stand-in for Go's x/crypto/blake2b assembly, blake2bAVX2_amd64.s) over the
+    same records: 1 thread (pz_blake2b512_batch with the small-batch threshold above the batch,
+    so the whole batch is hashed on the calling thread), then every host thread the library uses
+    (the serial-message threshold at 0: every message to the host pool, the GPU hashes none).
+    Digests checked against the portable C port's ``want``."""
+    from prysm_amd import _lib
+    n = records_np.shape[0]
+    flat = np.ascontiguousarray(records_np).reshape(-1)
+    offs = np.arange(n + 1, dtype=np.uint64) * records_np.shape[1]
+    out = np.empty(n * 32, dtype=np.uint8)
+    dll = _lib.lib.dll
+    dll.pz_set_small_batch_threshold.restype = ctypes.c_uint64
+    dll.pz_set_small_batch_threshold.argtypes = [ctypes.c_uint64]
+    dll.pz_set_serial_threshold.restype = ctypes.c_uint64
+    dll.pz_set_serial_threshold.argtypes = [ctypes.c_uint64]
+    dll.pz_set_host_threads.restype = ctypes.c_uint32
+    dll.pz_set_host_threads.argtypes = [ctypes.c_uint32]
+
+    def call():
+        _lib.lib.call("pz_blake2b512_batch", _lib.ptr(flat), _lib.ptr(offs), n, _lib.ptr(out), 32)
+
+    def timed():
+        t0 = time.perf_counter()
+        call()
+        ok = bool(np.array_equal(out.reshape(n, 32), want.reshape(n, 32)))
+        passes = 1
+        while time.perf_counter() - t0 < seconds:
+            call()
+            passes += 1
+        return passes, time.perf_counter() - t0, ok
+
+    old = dll.pz_set_small_batch_threshold(1 << 62)
+    try:
+        p1, d1, ok1 = timed()
+    finally:
+        dll.pz_set_small_batch_threshold(old)
+    threads = dll.pz_set_host_threads(0)
+    dll.pz_set_host_threads(threads)
+    old_s = dll.pz_set_serial_threshold(0)
+    old_small = dll.pz_set_small_batch_threshold(0)
+    try:
+        pa, da, oka = timed()
+    finally:
+        dll.pz_set_serial_threshold(old_s)
+        dll.pz_set_small_batch_threshold(old_small)
+    return {"value": p1 * n / d1, "cores": 1, "digests_match_port": ok1,
+            "sample": "%d pass(es) over the %d x 512-B records, 1 thread, the library's AVX2 BLAKE2b "
+                      "(serial_hash.cpp, the stand-in for Go's x/crypto/blake2b AVX2 assembly), %.2f s"
+                      % (p1, n, d1),
+            "all_cores": {"value": pa * n / da, "cores": int(threads), "digests_match_port": oka,
+                          "sample": "the same records over the library's %d host threads (AVX2), %.2f s"
+                                    % (threads, da)}}
+
+
 def cpu_baseline(records_np):
-    """Time the oracle's C restatement (oracle/c) over the same records on 1 core."""
+    """The reference's hash on this host's cores over the same records: the AVX2 hasher on 1
+    core (the honest stand-in for Go's x/crypto/blake2b, which runs AVX2 assembly),
+    beside the oracle's portable C restatement (oracle/c) on 1 core and on all cores."""
     try:
         from oracle import cport
     except Exception as e:  # pragma: no cover - reported, not fatal
@@ -1293,17 +1340,29 @@ def cpu_baseline(records_np):
     t0 = time.perf_counter()
     digests = cport.hash_fixed(records_np, 512, 32)
     passes = 1
-    while time.perf_counter() - t0 < CPU_SAMPLE_S:
+    while time.perf_counter() - t0 < CPU_SAMPLE_S / 2:
         cport.hash_fixed(records_np, 512, 32)
         passes += 1
     dt = time.perf_counter() - t0
     T = cport.host_info()["threads_all_cores"]
-    na, da = cport.hash_all_cores_timed(records_np, 512, T, CPU_SAMPLE_S / 2)
-    return {"value": passes * n / dt, "unit": "hashes/s", "cores": 1, "kind": "port",
-            "sample": "%d pass(es) over the %d x 512-B records of the per-GPU batch, 1 thread, portable C "
-                      "BLAKE2b (oracle/c/blake2b_ref.c), %.2f s" % (passes, n, dt),
-            "all_cores": {"value": na / da, "cores": T,
-                          "sample": "the same records split over %d threads, %.2f s" % (T, da)}}, digests
+    na, da = cport.hash_all_cores_timed(records_np, 512, T, CPU_SAMPLE_S / 4)
+    portable = {"value": passes * n / dt, "cores": 1,
+                "sample": "%d pass(es) over the %d x 512-B records of the per-GPU batch, 1 thread, portable C "
+                          "BLAKE2b (oracle/c/blake2b_ref.c), %.2f s" % (passes, n, dt),
+                "all_cores": {"value": na / da, "cores": T,
+                              "sample": "the same records split over %d threads, %.2f s" % (T, da)}}
+    try:
+        avx = avx2_host_rate(records_np, digests, CPU_SAMPLE_S / 2)
+    except Exception as e:  # pragma: no cover - reported, not fatal
+        avx = None
+        portable["avx2_error"] = str(e)
+    if avx is None:
+        out = dict(portable, unit="hashes/s", kind="port")
+    else:
+        out = {"value": avx["value"], "unit": "hashes/s", "cores": 1, "kind": "port",
+               "sample": avx["sample"], "digests_match_port": avx["digests_match_port"],
+               "all_cores": avx["all_cores"], "portable_c": portable}
+    return out, digests
 
 
 def main():
@@ -1386,7 +1445,7 @@ def main():
             what, "" if world == 1 else " of every rank", ok if world == 1 else all_ranks(ok, torch, dist, dev))
 
     comm = None
-    if world > 1 and not args.no_epoch and args.epoch_path == "native":
+    if world > 1 and not args.no_epoch:
         # every rank must take the same path: agree on whether the communicator came up; a
         # failure ends the run (non-zero exit), it never switches to another path
         err = None

@@ -654,7 +654,8 @@ int  pz_chain_new_from_state(const uint8_t* cstate, uint64_t len, const uint8_t*
 int  pz_chain_new_comm(uint64_t nval, pz_comm* comm, pz_chain** out);
 void pz_chain_free(pz_chain* chain);
 /* The engine's options (no reference counterpart: placement and test controls; every field 0
- * is the product's choice).  Set them before the chain's first pz_chain_process_blocks call. */
+ * is the product's choice).  Set them before the chain's first pz_chain_process_blocks call:
+ * afterwards a change of tally_forms fails with PZ_EINVAL (msg_batch may change at any time). */
 typedef struct pz_chain_options {
   uint64_t msg_batch;    /* processAttestation messages digested in batches of at least this many,
                             sent while the walk goes on (0: one batch at the end of the call) */
@@ -686,6 +687,15 @@ int  pz_chain_state_bytes(pz_chain* chain, int which, uint8_t* out, uint64_t cap
 /* The block vote cache: *count entries (0 when the map is nil); fills hashes[32*i] and
  * totals[i] (VoteTotalDeposit) when cap >= *count. */
 int  pz_chain_vote_totals(pz_chain* chain, uint8_t* hashes, uint64_t* totals, uint64_t cap, uint64_t* count);
+/* Observability (no reference counterpart; the Go node's pprof wall profile of the same
+ * phases): the engine's cumulative wall seconds per phase of pz_chain_process_blocks since the
+ * chain was created, out[0..n): parse, digest batch, attestation checks, vote queueing, tally
+ * flushes, stateRecalc, message digests, the walk, the whole call, attestation counting, arena
+ * waits, message sends / hash log / waits, the tally totals' wait, then two counts (tally-total
+ * polls that fell back to the event wait; queued attestations with an explicit parent-id row).
+ * The checks and vote queueing are clocked only by the A/B library (they read 0 here).
+ * Returns the number of slots the library keeps. */
+int  pz_chain_phase_times(pz_chain* chain, double* out, int n);
 
 #ifdef __cplusplus
 }

@@ -81,6 +81,7 @@ SIGNATURES = {
     "pz_chain_roots": [vp, vp, c_intp],
     "pz_chain_state_bytes": [vp, ctypes.c_int, vp, u64, c_u64p],
     "pz_chain_vote_totals": [vp, vp, vp, u64, c_u64p],
+    "pz_chain_phase_times": [vp, vp, ctypes.c_int],
     "pz_dev_vote_tally": [vp, vp],
     "pz_vote_tally": [vp, vp, u64, vp, vp, vp, u64, vp, vp, u64, vp, u64, vp, u64, u64, vp],
     "pz_comm_vote_tally": [vp, vp, vp, u64, vp, vp, vp, u64, vp, vp, u64, vp, u64, vp, u64, u64, vp],
@@ -225,9 +226,9 @@ class _Lib:
 
     def _load(self):
         if self._dll is None:
-            # PZ_LIB: another build of the library (tests marked `ab` and tools/ load the A/B
-            # library, make -C prysm_amd/csrc ab); the product path loads the in-tree product build
-            path = os.environ.get("PZ_LIB") or library_path
+            # the in-tree product build; no environment switch selects another one (tests marked
+            # `ab` and tools/ point library_path at the A/B library before the first call)
+            path = library_path
             if not os.path.exists(path):
                 raise PzError(PZ_EDEVICE, "HIP library not built: %s (run __graft_entry__.build())" % path)
             dll = ctypes.CDLL(path)

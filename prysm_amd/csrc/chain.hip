@@ -757,6 +757,7 @@ struct Engine {
   Retired retired;                // grown-out device buffers (freed with the chain)
   Knobs kn;                       // (read_knobs)
   pz_chain_options opt{};         // pz_chain_set_options (every field 0: the product's choices)
+  uint64_t calls = 0;             // pz_chain_process_blocks calls that reached the walk
   uint64_t kmax = 0;              // the largest committee
   bool bits_inline = true;        // every committee <= kVoteInlineBits: the bitfields ride in the records
   bool ids_rows = false;          // (pz_chain_options.tally_forms bit 2) every attestation's ids in an explicit row
@@ -3326,9 +3327,17 @@ int pz_chain_new_from_state(const uint8_t* cstate, uint64_t len, const uint8_t* 
 int pz_chain_set_options(pz_chain* c, const pz_chain_options* opts) {
   if (!c) return fail(PZ_EINVAL, "chain is null");
   Engine& g = c->g;
-  g.opt = opts ? *opts : pz_chain_options{};
-  g.bits_inline = g.kmax <= kVoteInlineBits && !(g.opt.tally_forms & PZ_TALLY_BITS_ROWS);
-  g.ids_rows = (g.opt.tally_forms & PZ_TALLY_ID_ROWS) != 0;
+  std::lock_guard<std::mutex> lk(g.mu);
+  const pz_chain_options o = opts ? *opts : pz_chain_options{};
+  const bool bi = g.kmax <= kVoteInlineBits && !(o.tally_forms & PZ_TALLY_BITS_ROWS);
+  const bool ir = (o.tally_forms & PZ_TALLY_ID_ROWS) != 0;
+  // the tally forms shape the vote queue's records: a chain that has queued any under the old
+  // form keeps it (its queue would be read against the other form at the next flush)
+  if ((bi != g.bits_inline || ir != g.ids_rows || o.tally_forms != g.opt.tally_forms) && g.calls)
+    return fail(PZ_EINVAL, "pz_chain_set_options: the tally forms are set before the first pz_chain_process_blocks call");
+  g.opt = o;
+  g.bits_inline = bi;
+  g.ids_rows = ir;
   return PZ_OK;
 }
 
@@ -3369,6 +3378,7 @@ int pz_chain_process_blocks(pz_chain* c, const uint8_t* blocks, const uint64_t* 
   if (natt > att_cap || (natt && !att_out)) return fail(PZ_EINVAL, "att_out holds %llu results, need %llu",
                                                         (unsigned long long)att_cap, (unsigned long long)natt);
   Engine& g = c->g;
+  ++g.calls;
   std::vector<Block> parsed(n);
   Feeder F;
   F.blocks = &parsed;
@@ -3642,10 +3652,10 @@ int pz_chain_vote_totals(pz_chain* c, uint8_t* hashes, uint64_t* totals, uint64_
 
 }  // extern "C"
 
-// Internal (tools/replay_profile.py): cumulative wall seconds per phase of the block pipeline:
-// parse, digest batch 1 (blocks/Hash/Key), attestation checks + message assembly, vote-cache
-// queueing, vote tally flushes, stateRecalc (excluding its flush), message digests.
-extern "C" int pz_debug_chain_profile(pz_chain* c, double* out, int n) {
+// Observability (include/prysm_hip.h): cumulative wall seconds per phase of the block pipeline
+// (parse, digest batch 1 (blocks/Hash/Key), attestation checks + message assembly, vote-cache
+// queueing, vote tally flushes, stateRecalc (excluding its flush), message digests, ...).
+extern "C" int pz_chain_phase_times(pz_chain* c, double* out, int n) {
   if (!c || !out) return PZ_EINVAL;
   for (int i = 0; i < n && i < pz::chain::kProfSlots; ++i) out[i] = c->g.prof[i];
   return pz::chain::kProfSlots;
@@ -3670,7 +3680,6 @@ extern "C" int pz_debug_vote_trace(pz_chain* c, uint64_t* out, uint64_t* waves, 
   for (int i = 0; i < n; ++i) waves[i] = g.vtrace_w[i];
   return n;
 }
-#endif
 
 extern "C" int pz_debug_chain_timeline(pz_chain* c, uint64_t* out, int n) {
   if (!c || !out) return PZ_EINVAL;
@@ -3680,7 +3689,7 @@ extern "C" int pz_debug_chain_timeline(pz_chain* c, uint64_t* out, int n) {
   return (int)tl.size();
 }
 
-// Internal (tests/, tools/; CPU-only: no device call): the block parser of
+// Internal (tests/, tools/: the A/B library; CPU-only: no device call): the block parser of
 // pz_chain_process_blocks on its own with `threads` threads, `reps` times; returns the wall
 // seconds of the fastest run and a checksum of what it parsed (every block's slot, parent and
 // record count, every record's fields and oblique spans), so that thread counts can be
@@ -3690,11 +3699,7 @@ extern "C" int pz_debug_parse(const uint8_t* data, const uint64_t* offs, uint64_
   double best = 1e30;
   // PZ_DEBUG_PARSE_PIN=1: the arena in pooled pinned memory, as pz_chain_process_blocks has it
   // (a device call: GPU boxes only)
-#ifdef PZ_AB_BUILD
   const char* pe = std::getenv("PZ_DEBUG_PARSE_PIN");
-#else
-  const char* pe = nullptr;
-#endif
   pz::chain::PinBuf pin;
   for (int r = 0; r < reps; ++r) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -3728,3 +3733,4 @@ extern "C" int pz_debug_parse(const uint8_t* data, const uint64_t* offs, uint64_
   if (seconds) *seconds = best;
   return PZ_OK;
 }
+#endif  // PZ_AB_BUILD

@@ -154,9 +154,13 @@ struct FusedArgs {
 // Block (instance, range): a range is a run of this rank's committees (local ids [cr0, cr1)),
 // so every committee's tallies complete inside one block.
 constexpr int kWinThreads = 1024, kWinDepth = 2, kWinDepth16 = 2;  // (pieces in flight per wave: 3 measured slower, r5f)
+constexpr uint32_t kWinKargR = 32;  // ranges whose descriptors ride in the kernel arguments (WinArgs.rdk)
 struct WinArgs {
   const uint4* rdesc;         // [R] {cr0, cr1, first piece, pieces}
   uint32_t R;                 // ranges per instance (grid: B x R blocks)
+  // R <= kWinKargR: rdesc's entries again, in the kernel arguments, so a block's first piece
+  // descriptors depend on nothing but the kernarg segment (one dependent round trip less)
+  uint4 rdk[kWinKargR];
   // [B][ptot][2] per instance and piece (<= 256 positions of one committee, from its first
   // position rounded down to 4): {first position, positions, committee - cr0, kind (0 no
   // attestation, 1 one, 2 several)}, {its first catt index, the bit of the first position in

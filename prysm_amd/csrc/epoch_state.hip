@@ -689,6 +689,7 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
     w.pacc_next = d_pacc + Bp;
   }
   w.rdesc = d_rdesc;
+  for (uint32_t r = 0; r < R && r < kWinKargR; ++r) w.rdk[r] = rdesc[r];
   w.pinfo = d_pinfo;
   w.ptot = ptot;
   w.rk = d_rk;

@@ -184,7 +184,7 @@ size_t window_lds_bytes(const WinArgs& w) { return 8ull * ((size_t)w.lds_maxc + 
 // (alone) the speculating blocks' post-loop meeting skipped, the fallback count every time (exact);
 // 16384 the product's L2 form (the reward bits looked up in the last bitfield in global memory,
 // no LDS copy; exact).
-template <bool B32, int SEW, bool LLB, int AB = 0, int D = kWinDepth, bool TR = false, bool NA = false>
+template <bool B32, int SEW, bool LLB, int AB = 0, int D = kWinDepth, bool TR = false, bool NA = false, bool NP = true>
 __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w) {
   extern __shared__ __align__(16) uint8_t lds_dyn[];
   constexpr int NT = kWinThreads, NW = NT / 64;
@@ -199,13 +199,15 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   if ((AB & 128) && (gridDim.x & 7) == 0) lb_id = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
   const uint64_t inst = lb_id / w.R;
   const uint32_t r = lb_id - (uint32_t)inst * w.R;
-  const uint4 rd = w.rdesc[r];
+  // (NP: the range's descriptor from the kernel arguments when they hold it -- a scalar load of
+  // the kernarg segment; the table in global memory only past kWinKargR ranges)
+  typedef const __attribute__((address_space(4))) uint32_t kuint32;
+  const kuint32* rdp = (kuint32*)(NP && w.R <= kWinKargR ? w.rdk : w.rdesc) + 4 * r;
+  const uint4 rd = make_uint4(rdp[0], rdp[1], rdp[2], rdp[3]);
   const uint32_t cr0 = rd.x, cr1 = rd.y, pb = rd.z, np = rd.w;
   const uint2 rkk = w.rk[inst * w.R + r];
   const uint32_t k0 = rkk.x, nk = rkk.y;  // the range's attestations: catt[k0, k0 + nk)
   const uint64_t gb = inst * a.natt;
-  const uint64_t pbeg = a.boffs[gb], pend = a.boffs[gb + a.natt], lb = a.boffs[gb + a.natt - 1];
-  const uint64_t pbase = pbeg & ~15ull, lbase = lb & ~15ull;
   // The wave's pieces go round by round, slot j of round t being piece t * D * NW + j * NW +
   // wave; past the range's end a slot takes a dummy (the last piece with no positions), so
   // every load below is issued unconditionally and the loop's waits count exactly the loads in
@@ -215,39 +217,35 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   const uint4* pinfo = w.pinfo + 2 * (inst * w.ptot + pb);
   auto desc = [&](uint32_t rnd) {  // this lane's word of its slot's descriptor for round rnd
     const uint32_t k = rnd * D * NW + dslot;
-    uint4 x = pinfo[2 * min(k, npm) + (lane & 1)];
-    if (k >= np && !(lane & 1)) x.y = 0;  // (a dummy: no positions)
-    return x;
+    return pinfo[2 * min(k, npm) + (lane & 1)];
   };
-  auto piece = [&](const uint4& x, int j) {
+  auto piece = [&](const uint4& x, int j, uint32_t rnd) {  // slot j's piece of round rnd
     Piece d;
-    d.s0 = __builtin_amdgcn_readlane(x.x, 2 * j), d.cnt = __builtin_amdgcn_readlane(x.y, 2 * j);
+    const bool dummy = rnd * D * NW + (uint32_t)j * NW + wave >= np;  // (a dummy: no positions)
+    d.s0 = __builtin_amdgcn_readlane(x.x, 2 * j);
+    d.cnt = dummy ? 0u : (uint32_t)__builtin_amdgcn_readlane(x.y, 2 * j);
     d.cl = __builtin_amdgcn_readlane(x.z, 2 * j), d.kind = __builtin_amdgcn_readlane(x.w, 2 * j);
     d.kb = __builtin_amdgcn_readlane(x.x, 2 * j + 1), d.vbit = __builtin_amdgcn_readlane(x.y, 2 * j + 1);
     d.vlim = __builtin_amdgcn_readlane(x.z, 2 * j + 1);
     return d;
   };
   uint4 dv = desc(0);
-  Piece dq[D];
-#pragma unroll
-  for (int j = 0; j < D; ++j) dq[j] = piece(dv, j);
+  // NP: round 1's descriptors go out with round 0's (both depend on the kernel arguments alone)
+  const uint4 dv1 = NP ? desc(1) : make_uint4(0, 0, 0, 0);
+  // (NP: nothing is scheduled above this point from below it, so the bitfield offsets' scalar
+  // loads -- and their wait -- come after the descriptors' loads have gone out)
+  if (NP) __builtin_amdgcn_sched_barrier(0);
+  const uint64_t pbeg = a.boffs[gb], pend = a.boffs[gb + a.natt], lb = a.boffs[gb + a.natt - 1];
+  const uint64_t pbase = pbeg & ~15ull, lbase = lb & ~15ull;
   const uint64_t vrow = inst * w.vstride;
   const WinCol col{w.bal32 + vrow, a.balance + vrow, w.se16 + vrow, w.se + vrow, a.start + vrow, a.end + vrow,
                    a.co_index, a.bits + pbase};
-  WinCols<B32, SEW> q[D];
-  if (!(AB & 64)) {
-#pragma unroll
-    for (int j = 0; j < D; ++j) win_load<B32, SEW>(col, dq[j], lane, q[j]);
-  }
-  dv = desc(1);
   const WinLds L = win_lds(lds_dyn, w);
   const uint32_t ncr = cr1 - cr0;
-  for (uint32_t i = tid; i < ncr; i += NT) L.tot[i] = 0;
-  for (uint32_t i = tid; i < nk; i += NT) L.vot[i] = 0;
   // GetAttestersTotalDeposit (every bitfield's bits) and the bitfield-length panics.  The
   // region's 16-B chunks [0, nch) from pbase; the last bitfield's, [clb, nch), go into LDS by
-  // DMA (no registers, 1 KiB per wave instruction) and are counted from there.  With R > 1 the
-  // block counts only its share of the chunks and attestations and the R blocks meet in pacc.
+  // DMA (no registers, 1 KiB per wave instruction) for the reward bits.  With R > 1 the block
+  // counts only its share of the chunks and attestations and the R blocks meet in pacc.
   uint64_t pop = 0, err = 0;
   const uint64_t nch = (pend - pbase + 15) / 16, clb = LLB ? (lbase - pbase) / 16 : nch;
   // Speculation (the product, R > 1): each of the instance's R blocks counts its 1/R share and
@@ -257,8 +255,15 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   // whole count before the loop in every block (round 5's first form).
   const bool spec = !(AB & (8192 | 16 | 2)) && w.pacc != nullptr && w.R > 1;
   const bool coop = spec || ((AB & 16) && w.pacc != nullptr && w.R > 1);
-  const uint64_t s0 = coop ? nch * r / w.R : 0, s1 = coop ? nch * (r + 1) / w.R : nch;
-  const uint64_t g0s = coop ? (uint64_t)a.natt * r / w.R : 0, g1s = coop ? (uint64_t)a.natt * (r + 1) / w.R : a.natt;
+  static_assert(!NP || !(AB & 16), "the A/B meeting before the loop keeps the round-5 prologue");
+  // floor(n r / R) in 32-bit divisions (n < 2^28 bitfield chunks or attestations, R <= 511):
+  // n = q R + m gives q r + floor(m r / R), m r < 2^18
+  auto share = [&](uint64_t n, uint32_t rr) -> uint64_t {
+    const uint32_t q = (uint32_t)n / w.R, m = (uint32_t)n - q * w.R;
+    return (uint64_t)q * rr + (m * rr) / w.R;
+  };
+  const uint64_t s0 = coop ? share(nch, r) : 0, s1 = coop ? share(nch, r + 1) : nch;
+  const uint64_t g0s = coop ? share(a.natt, r) : 0, g1s = coop ? share(a.natt, r + 1) : a.natt;
   // bits of chunk c (its bytes inside [pbeg, pend) only)
   auto chunk_pop = [&](uint64_t c, uint4 x) -> uint32_t {
     const uint64_t ad = pbase + 16 * c;
@@ -276,6 +281,52 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       n += __popc(wd[dd] & m);
     }
     return n;
+  };
+  // NP: the count's loads as {issue, take} halves, so they go out before the first descriptors
+  // are waited for and are taken after the first pieces' loads are in flight.  Iteration `it`
+  // covers chunks [c_lo + it CU NT, +CU NT) and attestations [g_lo + it CG NT, +CG NT) (every
+  // load issued, past the end clamped, as count_range)
+  constexpr int CU = 2, CG = 1;
+  struct CountLd {
+    uint4 x[CU];
+    uint32_t csz[CG];
+    uint64_t bo0[CG], bo1[CG];
+  };
+  auto cnt_issue = [&](uint64_t c_lo, uint64_t nc, uint64_t g_lo, uint64_t ng, uint64_t it, CountLd& cl) {
+    const uint64_t c0 = it * CU * NT + tid, gi0 = it * CG * NT + tid;
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+      const uint64_t c = c_lo + std::min<uint64_t>(c0 + (uint64_t)u * NT, nc ? nc - 1 : 0);
+      cl.x[u] = *reinterpret_cast<const uint4*>(a.bits + pbase + 16 * c);
+    }
+#pragma unroll
+    for (int u = 0; u < CG; ++u) {
+      const uint64_t g = g_lo + std::min<uint64_t>(gi0 + (uint64_t)u * NT, ng ? ng - 1 : 0);
+      cl.csz[u] = w.att_csize[gb + g];
+      cl.bo0[u] = a.boffs[gb + g];
+      cl.bo1[u] = a.boffs[gb + g + 1];
+    }
+  };
+  auto cnt_take = [&](uint64_t c_lo, uint64_t nc, uint64_t ng, uint64_t it, const CountLd& cl) {
+    const uint64_t c0 = it * CU * NT + tid, gi0 = it * CG * NT + tid;
+#pragma unroll
+    for (int u = 0; u < CU; ++u)
+      if (c0 + (uint64_t)u * NT < nc) pop += chunk_pop(c_lo + c0 + (uint64_t)u * NT, cl.x[u]);
+    // the crosslink bitfield-length panic (core.go:538-541): a committee longer than its bitfield
+#pragma unroll
+    for (int u = 0; u < CG; ++u)
+      if (gi0 + (uint64_t)u * NT < ng && (uint64_t)cl.csz[u] > 8 * (cl.bo1[u] - cl.bo0[u])) err = 1;
+  };
+  auto cnt_iters = [&](uint64_t nc, uint64_t ng) {
+    return std::max<uint64_t>((nc + CU * NT - 1) / (CU * NT), (ng + CG * NT - 1) / (CG * NT));
+  };
+  auto count_np = [&](uint64_t c_lo, uint64_t c_hi, uint64_t g_lo, uint64_t g_hi) {  // issue + take
+    const uint64_t nc = c_hi > c_lo ? c_hi - c_lo : 0, ng = g_hi - g_lo;
+    for (uint64_t it = 0, nit = cnt_iters(nc, ng); it < nit; ++it) {
+      CountLd cl;
+      cnt_issue(c_lo, nc, g_lo, ng, it, cl);
+      cnt_take(c_lo, nc, ng, it, cl);
+    }
   };
   // chunks [c_lo, c_hi) below the last bitfield and attestations [g_lo, g_hi) from global memory
   auto count_range = [&](uint64_t c_lo, uint64_t c_hi, uint64_t g_lo, uint64_t g_hi) {
@@ -312,68 +363,129 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
     for (uint64_t c = c_lo + tid; c < c_hi; c += NT)
       pop += chunk_pop(c, *reinterpret_cast<const uint4*>(L.lbf + 16 * (c - clb)));
   };
-  if (!(AB & 2)) {
-    if (LLB) {
-      typedef __attribute__((address_space(3))) void lds_void_t;
-      typedef const __attribute__((address_space(1))) void gbl_void_t;
-      const uint64_t nl = nch - clb;
-      for (uint64_t c0 = (uint64_t)wave * 64; c0 < nl; c0 += NT) {  // (wave-uniform c0)
-        const uint64_t c = std::min<uint64_t>(c0 + lane, nl - 1);
-        if (c0 + lane < nl)
-          __builtin_amdgcn_global_load_lds((gbl_void_t*)(a.bits + lbase + 16 * c), (lds_void_t*)(L.lbf + 16 * c0), 16, 0,
-                                           0);
-      }
-    }
-    count_range(s0, std::min(s1, clb), g0s, g1s);
-  } else {
-    pop = tid == 0 ? a.total_deposit[inst] : 0;  // (ablation: the threshold holds)
-  }
-  __syncthreads();  // the last bitfield is in LDS, the tallies zeroed
-  if (!(AB & 2)) count_lds(std::max(s0, clb), s1);
-  pop = wsum64_dpp(pop);
-  err = wsum64_dpp(err);
-  if (lane == 0) red[wave][0] = pop, red[wave][1] = err;
-  __syncthreads();
-  pop = 0, err = 0;
+  auto last_bitfield_dma = [&]() {
+    typedef __attribute__((address_space(3))) void lds_void_t;
+    typedef const __attribute__((address_space(1))) void gbl_void_t;
+    const uint64_t nl = nch - clb;
+    // (NP: a fixed unrolled count -- the copy fits the CU's LDS -- so the loads issued after it
+    // keep exact waits; a loop of unknown trip count would make every later wait a full drain)
+    constexpr int kDmaMax = (160 * 1024 + 16 * NT - 1) / (16 * NT);
+    if (NP) {
 #pragma unroll
-  for (int k = 0; k < NW; ++k) pop += red[k][0], err += red[k][1];
-  if (spec) {  // publish this block's share; the meeting is after the loop
-    if (tid == 0) {
+      for (int u = 0; u < kDmaMax; ++u) {
+        const uint64_t c0 = (uint64_t)wave * 64 + (uint64_t)u * NT;  // (wave-uniform)
+        if (c0 < nl && c0 + lane < nl)
+          __builtin_amdgcn_global_load_lds((gbl_void_t*)(a.bits + lbase + 16 * (c0 + lane)), (lds_void_t*)(L.lbf + 16 * c0),
+                                           16, 0, 0);
+      }
+      return;
+    }
+    for (uint64_t c0 = (uint64_t)wave * 64; c0 < nl; c0 += NT) {  // (wave-uniform c0)
+      const uint64_t c = std::min<uint64_t>(c0 + lane, nl - 1);
+      if (c0 + lane < nl)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(a.bits + lbase + 16 * c), (lds_void_t*)(L.lbf + 16 * c0), 16, 0,
+                                         0);
+    }
+  };
+  // NP, step 1: the count's first loads, before any wait (the DMA follows the count's take:
+  // issued earlier, its branches would turn every later wait into a full drain)
+  CountLd cl0;
+  const uint64_t ncn = s1 - s0, ngn = g1s - g0s;
+  if (NP && !(AB & 2)) cnt_issue(s0, ncn, g0s, ngn, 0, cl0);
+  Piece dq[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) dq[j] = piece(dv, j, 0);
+  WinCols<B32, SEW> q[D];
+  if (!(AB & 64)) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) win_load<B32, SEW>(col, dq[j], lane, q[j]);
+  }
+  dv = NP ? dv1 : desc(1);
+  if (NP) {
+    // step 2: the count taken (its loads went out with the descriptors, a round trip before the
+    // pieces'), then the last bitfield's DMA, the tallies zeroed, and one barrier for the wave
+    // sums, the DMA and the zeroed tallies; every thread then has the block's count (R = 1: the
+    // instance's -- no meeting, no speculation; R > 1: its share, published by one atomic)
+    if (!(AB & 2)) {
+      cnt_take(s0, ncn, ngn, 0, cl0);
+      for (uint64_t it = 1, nit = cnt_iters(ncn, ngn); it < nit; ++it) {
+        CountLd cl;
+        cnt_issue(s0, ncn, g0s, ngn, it, cl);
+        cnt_take(s0, ncn, ngn, it, cl);
+      }
+      if (LLB) last_bitfield_dma();
+    } else {
+      pop = tid == 0 ? a.total_deposit[inst] : 0;  // (ablation: the threshold holds)
+    }
+    for (uint32_t i = tid; i < ncr; i += NT) L.tot[i] = 0;
+    for (uint32_t i = tid; i < nk; i += NT) L.vot[i] = 0;
+    pop = wsum64_dpp(pop);
+    err = __builtin_amdgcn_ballot_w64(err != 0) ? 1 : 0;
+    if (lane == 0) red[wave][0] = pop, red[wave][1] = err;
+    __syncthreads();
+    pop = 0, err = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) pop += red[k][0], err += red[k][1];
+    if (spec && tid == 0) {
       const uint64_t add = (1ull << 48) | (err ? 1ull << 39 : 0) | pop;
       atomicAdd((unsigned long long*)&w.pacc[inst], (unsigned long long)add);
     }
-  } else if (coop && !(AB & 2)) {
-    // the instance's R blocks meet: one atomic adds this block's share, then thread 0 polls the
-    // word (at the coherence point) until all R have arrived, or the bound passes and the block
-    // counts everything itself (so no block ever depends on another being resident)
-    __shared__ uint64_t s_meet;
-    if (tid == 0) {
-      const uint64_t add = (1ull << 48) | (err ? 1ull << 39 : 0) | pop;
-      uint64_t v = atomicAdd((unsigned long long*)&w.pacc[inst], (unsigned long long)add) + add;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while ((v >> 48) < w.R && __builtin_amdgcn_s_memrealtime() - t0 < ((AB & 32) ? 0 : kCoopSpinTicks)) {
-        __builtin_amdgcn_s_sleep(2);
-        v = __hip_atomic_fetch_add(&w.pacc[inst], (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      s_meet = v;
+  } else {
+    for (uint32_t i = tid; i < ncr; i += NT) L.tot[i] = 0;
+    for (uint32_t i = tid; i < nk; i += NT) L.vot[i] = 0;
+    if (!(AB & 2)) {
+      if (LLB) last_bitfield_dma();
+      count_range(s0, std::min(s1, clb), g0s, g1s);
+    } else {
+      pop = tid == 0 ? a.total_deposit[inst] : 0;  // (ablation: the threshold holds)
     }
+    __syncthreads();  // the last bitfield is in LDS, the tallies zeroed
+    if (!(AB & 2)) count_lds(std::max(s0, clb), s1);
+    pop = wsum64_dpp(pop);
+    err = wsum64_dpp(err);
+    if (lane == 0) red[wave][0] = pop, red[wave][1] = err;
     __syncthreads();
-    const uint64_t v = s_meet;
-    if ((v >> 48) >= w.R) {
-      pop = v & ((1ull << 39) - 1);
-      err = (v >> 39) & 511;
-    } else {  // (a partner not resident in time: the whole count here)
-      pop = 0, err = 0;
-      count_range(0, clb, 0, a.natt);
-      count_lds(clb, nch);
-      pop = wsum64_dpp(pop);
-      err = wsum64_dpp(err);
-      __syncthreads();
-      if (lane == 0) red[wave][0] = pop, red[wave][1] = err;
-      __syncthreads();
-      pop = 0, err = 0;
+    pop = 0, err = 0;
 #pragma unroll
-      for (int k = 0; k < NW; ++k) pop += red[k][0], err += red[k][1];
+    for (int k = 0; k < NW; ++k) pop += red[k][0], err += red[k][1];
+    if (spec) {  // publish this block's share; the meeting is after the loop
+      if (tid == 0) {
+        const uint64_t add = (1ull << 48) | (err ? 1ull << 39 : 0) | pop;
+        atomicAdd((unsigned long long*)&w.pacc[inst], (unsigned long long)add);
+      }
+    } else if (coop && !(AB & 2)) {
+      // the instance's R blocks meet: one atomic adds this block's share, then thread 0 polls the
+      // word (at the coherence point) until all R have arrived, or the bound passes and the block
+      // counts everything itself (so no block ever depends on another being resident)
+      __shared__ uint64_t s_meet;
+      if (tid == 0) {
+        const uint64_t add = (1ull << 48) | (err ? 1ull << 39 : 0) | pop;
+        uint64_t v = atomicAdd((unsigned long long*)&w.pacc[inst], (unsigned long long)add) + add;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while ((v >> 48) < w.R && __builtin_amdgcn_s_memrealtime() - t0 < ((AB & 32) ? 0 : kCoopSpinTicks)) {
+          __builtin_amdgcn_s_sleep(2);
+          v = __hip_atomic_fetch_add(&w.pacc[inst], (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_meet = v;
+      }
+      __syncthreads();
+      const uint64_t v = s_meet;
+      if ((v >> 48) >= w.R) {
+        pop = v & ((1ull << 39) - 1);
+        err = (v >> 39) & 511;
+      } else {  // (a partner not resident in time: the whole count here)
+        pop = 0, err = 0;
+        count_range(0, clb, 0, a.natt);
+        count_lds(clb, nch);
+        pop = wsum64_dpp(pop);
+        err = wsum64_dpp(err);
+        __syncthreads();
+        if (lane == 0) red[wave][0] = pop, red[wave][1] = err;
+        __syncthreads();
+        pop = 0, err = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) pop += red[k][0], err += red[k][1];
+      }
     }
   }
   if (AB & 64) {  // (A/B: the first pieces' loads only now, behind the prologue's)
@@ -611,7 +723,7 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
         for (int i = 0; i < 4; ++i) sum += (v[i] && act[i]) ? b[i] : 0;
       }
       // slot j's piece of the next round (past the last round: a dummy, loaded and unused)
-      dq[j] = piece(dnx, j);
+      dq[j] = piece(dnx, j, t + 1);
       win_load<B32, SEW>(col, dq[j], lane, q[j]);
     }
   }
@@ -644,8 +756,12 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       err = (v >> 39) & 511;
     } else {
       pop = 0, err = 0;
-      count_range(0, clb, 0, a.natt);
-      count_lds(clb, nch);
+      if (NP) {
+        count_np(0, nch, 0, a.natt);
+      } else {
+        count_range(0, clb, 0, a.natt);
+        count_lds(clb, nch);
+      }
       pop = wsum64_dpp(pop);
       err = wsum64_dpp(err);
       if (lane == 0) red[wave][0] = pop, red[wave][1] = err;
@@ -767,7 +883,7 @@ PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_g_kernel, false, 64, false, false)
 #define PZ_WINDOW_ABL(X, D)                                                                              \
   extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_abl##X##_d##D##_kernel(EpochArgs a, \
                                                                                               WinArgs w) {  \
-    window_body<true, 16, true, X, D, false, true>(a, w);                                                  \
+    window_body<true, 16, true, X, D, false, true, !((X) & 16)>(a, w);                                     \
   }
 PZ_WINDOW_ABL(0, 2) PZ_WINDOW_ABL(0, 3) PZ_WINDOW_ABL(0, 4)
 PZ_WINDOW_ABL(1, 2) PZ_WINDOW_ABL(2, 2) PZ_WINDOW_ABL(4, 2) PZ_WINDOW_ABL(7, 2) PZ_WINDOW_ABL(16, 2)
@@ -776,6 +892,14 @@ PZ_WINDOW_ABL(8192, 2) PZ_WINDOW_ABL(32, 2) PZ_WINDOW_ABL(65536, 2) PZ_WINDOW_AB
 // the product form with phase stamps (tools/epoch_trace.py)
 extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_kernel(EpochArgs a, WinArgs w) {
   window_body<true, 16, true, 0, kWinDepth16, true, true>(a, w);
+}
+// round 5's prologue (the count after the first pieces' descriptors, two barriers, the range
+// descriptor from global memory): A/B bit 1 << 18, with and without phase stamps
+extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_np0_kernel(EpochArgs a, WinArgs w) {
+  window_body<true, 16, true, 0, kWinDepth16, false, true, false>(a, w);
+}
+extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_np0_kernel(EpochArgs a, WinArgs w) {
+  window_body<true, 16, true, 0, kWinDepth16, true, true, false>(a, w);
 }
 #undef PZ_WINDOW_ABL
 static int g_window_ablation = 0;
@@ -812,8 +936,10 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
 #undef PZ_PICK
 #ifdef PZ_AB_BUILD
   // (the A/B forms are the narrow product form's)
-  if (g_window_trace && b32 && w.narrow && sew == 16 && llb) k = (const void*)pz_epoch_window_trace_kernel;
-  if (g_window_ablation && b32 && w.narrow && sew == 16 && llb) {
+  if (g_window_trace && b32 && w.narrow && sew == 16 && llb)
+    k = g_window_ablation == (1 << 18) ? (const void*)pz_epoch_window_trace_np0_kernel
+                                       : (const void*)pz_epoch_window_trace_kernel;
+  if (g_window_ablation && !g_window_trace && b32 && w.narrow && sew == 16 && llb) {
     switch (g_window_ablation) {  // ablation bits | prefetch depth << 8
       case 2 << 8: k = (const void*)pz_epoch_window_abl0_d2_kernel; break;
       case 3 << 8: k = (const void*)pz_epoch_window_abl0_d3_kernel; break;
@@ -833,6 +959,7 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
       case 16384: k = (const void*)pz_epoch_window_b32n_s16_g_kernel; break;  // (the reward bits from L2, no LDS copy)
       case 65536: k = (const void*)pz_epoch_window_abl65536_d2_kernel; break;  // (timing: no multi-attestation votes)
       case 131072: k = (const void*)pz_epoch_window_abl131072_d2_kernel; break;  // (one attestation per trip)
+      case 1 << 18: k = (const void*)pz_epoch_window_np0_kernel; break;  // (round 5's prologue)
       default: return hipErrorInvalidValue;
     }
   }

@@ -228,7 +228,9 @@ void SerialHashJob::join() {
 
 }  // namespace pz
 
-// Internal (tests): the host hasher and the routing threshold.
+#ifdef PZ_AB_BUILD
+// Internal (tests, the A/B library): the host hasher on one message.
 extern "C" void pz_debug_host_blake2b512(const uint8_t* msg, uint64_t len, uint8_t out[64]) {
   pz::host_blake2b512(msg, (size_t)len, out);
 }
+#endif

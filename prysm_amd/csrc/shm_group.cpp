@@ -353,7 +353,8 @@ int ShmGroup::allgather(const void* send, void* recv, size_t bytes, std::string*
 
 }  // namespace pz
 
-// ---- host-only test entry points (no device involved; tests/test_shm_group.py) ----------
+// ---- host-only test entry points (the A/B library; no device involved; tests/test_shm_group.py)
+#ifdef PZ_AB_BUILD
 using pz::ShmGroup;
 
 extern "C" {
@@ -388,3 +389,4 @@ int pz_debug_shm_allgather(void* g, const void* send, void* recv, uint64_t bytes
 void pz_debug_shm_close(void* g) { delete static_cast<ShmGroup*>(g); }
 
 }  // extern "C"
+#endif  // PZ_AB_BUILD

@@ -16,13 +16,17 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "ab: measured-and-dropped forms and measurement hooks; runs only against the "
                                        "A/B library (make -C prysm_amd/csrc ab) under -m ab")
     # `-m ab` (or an expression naming ab without "not ab"): the session loads the A/B library
+    # (library_path set in this process only: no environment variable, so child processes the
+    # multiprocess tests start load the product library)
     expr = config.option.markexpr or ""
     if "ab" in expr.split() and "not ab" not in expr:
-        os.environ["PZ_LIB"] = AB_LIB
+        from prysm_amd import _lib
+        _lib.library_path = AB_LIB
 
 
 def pytest_collection_modifyitems(config, items):
-    ab_loaded = os.environ.get("PZ_LIB") == AB_LIB
+    from prysm_amd import _lib
+    ab_loaded = _lib.library_path == AB_LIB
     skip = pytest.mark.skip(reason="A/B form: run with -m ab against build/ab/libprysm_hip.so")
     for it in items:
         if "ab" in it.keywords and not ab_loaded:

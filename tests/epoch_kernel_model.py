@@ -4,7 +4,7 @@
 sums over the shard, popcount chunks split by (pop_rank, pop_world), crosslink partial
 tallies over the members the shard owns, rewards by global rank position.
 
-It lets the multi-rank orchestration in ``prysm_amd.epoch.DeviceEpoch`` (shard ranges,
+It lets the multi-rank orchestration in ``tests/torch_epoch.py DeviceEpoch`` (shard ranges,
 buffer layout, the collective sequence) run on CPU tensors under ``gloo`` with no GPU, so
 that the N>1 path is covered here; the GPU test of the same orchestration uses the real
 kernels (tests/test_multirank.py).  It is never used by the product.

@@ -25,6 +25,17 @@ def test_every_declared_symbol_is_exported():
     assert not missing, missing
 
 
+def test_product_exports_no_debug_entry_points():
+    """The product library carries no pz_debug_* entry points: the measurement
+    hooks and host-only test entry points live in the A/B library (-DPZ_AB_BUILD)."""
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.library_path], capture_output=True, text=True,
+                         check=True).stdout
+    names = [ln.split()[-1] for ln in out.splitlines() if ln.strip()]
+    assert any(n.startswith("pz_") for n in names)
+    assert [n for n in names if n.startswith("pz_debug")] == []
+
+
 def test_binding_covers_header():
     assert set(declared_functions()) <= set(_lib.SIGNATURES)
 
@@ -58,7 +69,8 @@ def test_host_serial_hasher_matches_hashlib():
 
     import numpy as np
 
-    fn = _lib.lib.dll.pz_debug_host_blake2b512
+    from ab_lib import ab_dll
+    fn = ab_dll().pz_debug_host_blake2b512
     fn.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
     fn.restype = None
     rng = np.random.default_rng(1)

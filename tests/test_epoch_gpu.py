@@ -254,7 +254,7 @@ _oracle_epoch = oracle_epoch
 def test_device_epoch_vs_oracle(n, B, inactive):
     import torch
 
-    from prysm_amd.epoch import DeviceEpoch
+    from torch_epoch import DeviceEpoch
     shuffled = casper.shuffle_indices(ref.bytes_to_hash(b"A"), np.arange(n, dtype=np.uint32))
     inst = synth.epoch_batch(n, B, seed=5, shuffled=shuffled)
     if inactive:  # general rank path: some validators exited/queued, rank != index
@@ -285,7 +285,7 @@ def test_device_epoch_configs3_size_vs_oracle():
     the numpy oracle on every balance, tally, winner and the next-cycle total."""
     import torch
 
-    from prysm_amd.epoch import DeviceEpoch
+    from torch_epoch import DeviceEpoch
     n, B = 1 << 20, 2
     shuffled = casper.shuffle_indices(ref.bytes_to_hash(b"A"), np.arange(n, dtype=np.uint32))
     inst = synth.epoch_batch(n, B, seed=5, shuffled=shuffled)
@@ -315,7 +315,7 @@ def test_device_epoch_repeated_steps_ping_pong():
     applied step after step."""
     import torch
 
-    from prysm_amd.epoch import DeviceEpoch
+    from torch_epoch import DeviceEpoch
     n, B = 8192, 8
     shuffled = casper.shuffle_indices(ref.bytes_to_hash(b"A"), np.arange(n, dtype=np.uint32))
     inst = synth.epoch_batch(n, B, seed=21, shuffled=shuffled)

@@ -1,5 +1,5 @@
 """N>1 path of the epoch transition (validator-range shards + all-reduce / all-gather):
-``prysm_amd.epoch.DeviceEpoch``'s multi-rank orchestration at world sizes 2 and 3, checked
+``tests/torch_epoch.py DeviceEpoch``'s multi-rank orchestration at world sizes 2 and 3, checked
 bit-exact against the single-instance oracle.
 
 * CPU (``-m "not gpu"``): gloo on CPU tensors, with the device passes replaced by the numpy
@@ -36,7 +36,7 @@ def _worker(rank, world, port, n, B, inactive, use_gpu, steps):
     from epoch_ref_helpers import oracle_epoch
     from oracle import ref
     from prysm_amd import _lib, casper, synth
-    from prysm_amd.epoch import DeviceEpoch, shard_range
+    from torch_epoch import DeviceEpoch, shard_range
 
     dist.init_process_group("gloo", rank=rank, world_size=world, init_method="tcp://127.0.0.1:%d" % port)
     shuffled = casper.shuffle_indices(ref.bytes_to_hash(b"A"), np.arange(n, dtype=np.uint32)) if use_gpu \

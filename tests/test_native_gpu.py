@@ -352,6 +352,42 @@ def test_native_epoch_one_pass_dynasty_past_32_bits(B):
     _check(ne, inst, steps=2)
 
 
+def _record_dynasties(d):
+    """Crosslink record dynasties around CurrentDynasty d (core.go:549, dynasty > record.Dynasty):
+    d - 1 and 0 (beaten), d and d + 1 (not), 0xFFFFFFFF and 2^32 + k with k's low word below
+    d's (the window pass's 32-bit saturated compare and its high-word table), 2^33 + 1."""
+    c = [0, d - 1, d, d + 1, 0xFFFFFFFF, (1 << 32) + 1, (1 << 33) + 1]
+    return np.array(sorted(set(x for x in c if 0 <= x < (1 << 64))), dtype=np.uint64)
+
+
+@pytest.mark.parametrize("window_only", [True, False])
+@pytest.mark.parametrize("B", [1, 3])
+@pytest.mark.parametrize("d", [5, 0xFFFFFFFE, (1 << 32) + 3])
+def test_native_epoch_record_dynasties(d, B, window_only):
+    """The winner rule's dynasty compare against nonzero crosslink records: each
+    instance's records drawn from values just below, at and above CurrentDynasty and around the
+    32-bit saturation point, so some qualifying attestations beat their shard's record and some
+    do not; the window pass (window_only, and B = 3) and the single launch (B = 1), two steps
+    against oracle/epoch_np.crosslink_winners."""
+    inst = _inst(4096, B, False)
+    rng = np.random.default_rng(11)
+    inst["dynasty"] = np.full(B, d, dtype=np.uint64)
+    inst["rec_dynasty"] = rng.choice(_record_dynasties(d), size=inst["rec_dynasty"].shape)
+    ne = NativeEpoch(inst, device=0, window_only=window_only)
+    assert ne.one_pass
+    want = [oracle_epoch(inst, b) for b in range(B)]
+    # the draw must leave both outcomes: a qualifying attestation that wins and one its record blocks
+    natt = inst["natt"]
+    won = sum(int((w != 0xFFFFFFFF).sum()) for *_r, w in want)
+    blocked = 0
+    for b, (_nb, _a, _n, v, t, w) in enumerate(want):
+        q = 3 * v.astype(object) >= 2 * t.astype(object)
+        sh = inst["att_shard"][b * natt:(b + 1) * natt]
+        blocked += int(sum(1 for g in np.nonzero(q)[0] if not d > int(inst["rec_dynasty"][b][sh[g]])))
+    assert won > 0 and blocked > 0, (won, blocked)
+    _check(ne, inst, steps=2)
+
+
 @pytest.mark.parametrize("B", [1, 3])
 @pytest.mark.parametrize("d", [0xFFFE, 0xFFFF, 0xFFFFFFFE])
 def test_native_epoch_one_pass_saturated_bounds(B, d):

@@ -12,12 +12,14 @@ from prysm_amd.blockchain import serialize_blocks
 
 
 def _parse(data, offs, threads):
-    dll = _lib.lib.dll
+    from ab_lib import ab_dll
+    dll = ab_dll()
     fn = dll.pz_debug_parse
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
     sec, cs = ctypes.c_double(), ctypes.c_uint64()
     rc = fn(data.ctypes.data, offs.ctypes.data, len(offs) - 1, threads, 1, ctypes.byref(sec), ctypes.byref(cs))
+    dll.pz_last_error.restype = ctypes.c_void_p
     msg = dll.pz_last_error()
     return rc, cs.value, ctypes.cast(msg, ctypes.c_char_p).value.decode() if rc else ""
 

@@ -636,3 +636,28 @@ def test_gpu_malformed_block_ends_the_call_there(pipeline, monkeypatch):
     ref = BeaconChain(1024)
     ref.process_serialized(*serialize_blocks(blocks[:bad]))
     assert ch.roots() == ref.roots()
+
+
+@pytest.mark.gpu
+def test_gpu_chain_options_fixed_after_first_call():
+    """pz_chain_set_options: the tally forms shape the vote queue's records, so once
+    a call has queued some, another form fails with PZ_EINVAL and the chain keeps its form (its
+    next call still matches the C restatement); msg_batch may still change."""
+    import ctypes
+
+    from prysm_amd import _lib
+    from prysm_amd.blockchain import BeaconChain, serialize_blocks
+    from replay_port_helpers import mismatches, port_replay
+    nval = 4096
+    blocks = synth.chain_blocks(nval, 140, seed=3)
+    data, offs = serialize_blocks(blocks)
+    ch = BeaconChain(nval)
+    br0, ar0 = ch.process_serialized(data[: int(offs[70])], offs[:71])
+    with pytest.raises(_lib.PzError) as ei:
+        _lib.lib.call("pz_chain_set_options", ch._h, ctypes.byref(_lib.ChainOptions(0, _lib.TALLY_BITS_ROWS)))
+    assert ei.value.code == _lib.PZ_EINVAL
+    _lib.lib.call("pz_chain_set_options", ch._h, ctypes.byref(_lib.ChainOptions(16, 0)))
+    br1, ar1 = ch.process_serialized(data, offs[70:])
+    br, ar = np.concatenate([br0, br1]), np.concatenate([ar0, ar1])
+    out, port_roots = port_replay(data, offs, nval, len(ar))
+    assert mismatches(br, ar, ch.roots(), out, port_roots) == []

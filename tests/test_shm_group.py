@@ -10,11 +10,12 @@ import uuid
 import numpy as np
 import pytest
 
+from ab_lib import ab_dll
 from prysm_amd import _lib
 
 
 def _dll():
-    d = ctypes.CDLL(_lib.library_path)
+    d = ab_dll()
     vp, u64 = ctypes.c_void_p, ctypes.c_uint64
     d.pz_debug_shm_open.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, u64,
                                     ctypes.POINTER(vp)]

@@ -1,4 +1,6 @@
-"""Device-resident mirror of the epoch-transition state (SoA in HBM) and its drivers.
+"""Test double (tests/ only since round 6; the product's epoch driver is pz_epoch_state, which
+prysm_amd.native.NativeEpoch wraps): a device-resident mirror of the epoch-transition state (SoA in
+HBM) driven from Python over torch.distributed.
 
 ``DeviceEpoch`` holds B epoch instances' validator arrays, pending-attestation bitfields and
 committees in HBM (torch tensors are used only as device allocations) and runs the

@@ -2,7 +2,7 @@
 bench.py's epoch.cold form -- the timed steps rotated over distinct instance sets (>= 800 MB of
 streamed state, far above the 256 MiB Infinity Cache) on one stream -- for configs[2]
 (65,536 x 256) and the 1M x 16 shape, REPS times each, with the two stock-kernel yardsticks.
-With PZ_LIB=build/ab/libprysm_hip.so, ABL=a,b,... repeats it per window-pass ablation
+With PZ_PROBE_LIB=build/ab/libprysm_hip.so, ABL=a,b,... repeats it per window-pass ablation
 (epoch_window.hip: bits 1 no tallies, 2 no prologue count, 4 no reward lookups, 8 no vote-bit
 placement; depth << 8 the full kernel at that prefetch depth)."""
 import os
@@ -14,7 +14,10 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from prysm_amd import casper  # noqa: E402
+from prysm_amd import _lib, casper  # noqa: E402
+
+if os.environ.get("PZ_PROBE_LIB"):  # (A/B: another build of the library)
+    _lib.library_path = os.environ["PZ_PROBE_LIB"]
 
 REPS = int(os.environ.get("REPS", "2"))
 SHAPES = [(65536, 256), (1 << 20, 16)]
@@ -26,7 +29,6 @@ def main():
     args = types.SimpleNamespace(steps=48)
     dll = None
     if ABL:
-        from prysm_amd import _lib
         dll = _lib.lib.dll
     for nval, ninst in SHAPES:
         shuffled = casper.shuffle_indices(b"A" + bytes(31), np.arange(nval, dtype=np.uint32))

@@ -1,5 +1,5 @@
 """Per-part device time of the two-pass epoch step (HIP events, one process, interleaved rounds).
-Needs the A/B library's part entry points: PZ_LIB=build/ab/libprysm_hip.so python tools/epoch_parts.py"""
+Needs the A/B library's part entry points: PZ_PROBE_LIB=build/ab/libprysm_hip.so python tools/epoch_parts.py"""
 import ctypes
 import json
 import os
@@ -11,7 +11,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from prysm_amd import _lib, casper, synth  # noqa: E402
-from prysm_amd.epoch import DeviceEpoch  # noqa: E402
+
+if os.environ.get("PZ_PROBE_LIB"):
+    _lib.library_path = os.environ["PZ_PROBE_LIB"]
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+from torch_epoch import DeviceEpoch  # noqa: E402
 
 
 def main(nval=65536, ninst=256, rounds=5, reps=10):

@@ -7,11 +7,12 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ.setdefault("PZ_LIB", os.path.join(ROOT, "build", "ab", "libprysm_hip.so"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from prysm_amd import _lib, casper, synth  # noqa: E402
+
+_lib.library_path = os.environ.get("PZ_PROBE_LIB") or os.path.join(ROOT, "build", "ab", "libprysm_hip.so")
 from prysm_amd.native import NativeEpoch  # noqa: E402
 
 SHAPES = [(1 << 20, 16), (65536, 256)]

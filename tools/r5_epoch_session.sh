@@ -13,7 +13,7 @@ timeout -k 10 600 python -u -m pytest tests/test_native_gpu.py -m ab -x -v --tim
 tail -3 "$O/pytest_epoch_ab.txt"
 ABL= timeout -k 10 300 python -u tools/epoch_cold.py > "$O/epoch_cold.txt" 2>&1 || { echo COLD_FAIL; tail -20 "$O/epoch_cold.txt"; exit 13; }
 cat "$O/epoch_cold.txt"
-PZ_LIB=build/ab/libprysm_hip.so ABL=${EABL:-4096,1,2,4,7} REPS=1 timeout -k 10 400 python -u tools/epoch_cold.py \
+PZ_PROBE_LIB=build/ab/libprysm_hip.so ABL=${EABL:-4096,1,2,4,7} REPS=1 timeout -k 10 400 python -u tools/epoch_cold.py \
   > "$O/epoch_abl.txt" 2>&1 || { echo ABL_FAIL; tail -20 "$O/epoch_abl.txt"; exit 14; }
 cat "$O/epoch_abl.txt"
 timeout -k 10 300 python -u tools/epoch_trace.py > "$O/epoch_trace.txt" 2>&1 || { echo TRACE_FAIL; tail -20 "$O/epoch_trace.txt"; exit 15; }

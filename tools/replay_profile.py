@@ -60,7 +60,7 @@ def main():
               % ("[%s=%s] " % (ab, val) if ab else "", dt, nblocks / dt, int((br["status"] == 0).sum()), len(ar)),
               flush=True)
         pv = (ctypes.c_double * len(names))()
-        fn = _lib.lib.dll.pz_debug_chain_profile
+        fn = _lib.lib.dll.pz_chain_phase_times
         fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         k = fn(ch._h, pv, len(names))
         print("  phases (s): " + ", ".join("%s %.4f" % (names[i], pv[i]) for i in range(min(k, len(names)))),
