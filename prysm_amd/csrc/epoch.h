@@ -155,6 +155,9 @@ struct FusedArgs {
 // so every committee's tallies complete inside one block.
 constexpr int kWinThreads = 1024, kWinDepth = 2, kWinDepth16 = 2;  // (pieces in flight per wave: 3 measured slower, r5f)
 constexpr uint32_t kWinKargR = 32;  // ranges whose descriptors ride in the kernel arguments (WinArgs.rdk)
+// the straight-line DMA counts the product kernel is instantiated for (65,536 / 131,072 /
+// 262,144 / 524,288 / 1,048,576-bit last bitfields, each + up to 15 B of alignment)
+constexpr uint32_t kWinDmaK[] = {1, 2, 3, 5, 9};
 struct WinArgs {
   const uint4* rdesc;         // [R] {cr0, cr1, first piece, pieces}
   uint32_t R;                 // ranges per instance (grid: B x R blocks)
@@ -189,6 +192,10 @@ struct WinArgs {
   int rank0;                  // this rank writes the per-instance scalars
   // LDS plan: last-bitfield bytes (0: reward bits from L2), most committees / attestations of a range
   uint32_t lds_lbf, lds_maxc, lds_maxk;
+  // > 0: every instance's last bitfield copy is at most dma_k x kWinThreads 16-B chunks and
+  // lds_lbf holds that many (padding included), so the product kernel issues exactly dma_k DMA
+  // instructions per wave, straight-line, before its first wait (kWinDmaK); 0: the copy's loop
+  uint32_t dma_k;
   // every instance's u32 offsets within kTallySpan of kTallyFloor (the state keeps them there by
   // re-basing every kNarrowPeriod steps): each committee's tallies are two 32-bit wave sums of
   // (offset - floor) instead of four (epoch_window.hip)

@@ -608,7 +608,24 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
     w.lds_maxk = std::max<uint32_t>(maxk, 1);
     if ((w.lds_maxc + w.lds_maxk) & 1) ++w.lds_maxk;  // (keeps the last bitfield's copy 16-B aligned)
     w.lds_lbf = (uint32_t)lbf;
-    if (window_lds_bytes(w) <= kLdsMax) break;
+    w.dma_k = 0;
+    if (window_lds_bytes(w) <= kLdsMax) {
+      // the straight-line copy: the smallest instantiated count that holds every instance's copy,
+      // its LDS padded to whole wave instructions, when that still fits (and no copy is empty)
+      bool nonempty = true;
+      for (uint64_t b = 0; b < Bp; ++b) {
+        const uint64_t gb = (i0 + b) * natt;
+        nonempty = nonempty && h->boffs[gb + natt] > h->boffs[gb + natt - 1];
+      }
+      for (uint32_t k : kWinDmaK) {
+        if (!nonempty || (uint64_t)k * 16 * kWinThreads < lbf) continue;
+        WinArgs t = w;
+        t.lds_lbf = k * 16 * kWinThreads;
+        if (window_lds_bytes(t) <= kLdsMax) w.lds_lbf = t.lds_lbf, w.dma_k = k;
+        break;
+      }
+      break;
+    }
     w.lds_lbf = 0;  // the reward bits looked up in L2 instead
     if (window_lds_bytes(w) <= kLdsMax) break;
     if (R >= nlc) return fail(PZ_EINVAL, "window pass: no range split fits the LDS");

@@ -93,18 +93,21 @@ struct WinCol {
 // bitfield by up to 3 bits when the piece starts mid-quad: the buffer has 16 B before it)
 __device__ __forceinline__ int64_t vbit_of(const Piece& d, uint32_t p) { return (int64_t)d.vbit + (int64_t)p - d.s0; }
 
-template <bool B32, int SEW>
+// (NTB: the balances stream nontemporally too -- read once and written once per step, they
+// leave the caches to the tables every block re-reads: co_index, the piece descriptors, the
+// bitfields; round 6: 59 -> 53 us per cold 65,536 x 256 step, profiles/r06/epoch_cold_nt_r6c.txt)
+template <bool B32, int SEW, bool NTB = true>
 __device__ __forceinline__ void win_load(const WinCol& c, const Piece& d, uint32_t lane, WinCols<B32, SEW>& x) {
   const uint32_t pa = d.s0 & ~3u, p = pa + 4 * lane;
   const bool any = p + 3 >= d.s0 && p < d.s0 + d.cnt;
   const uint32_t pp = any ? p : pa;  // (a lane wholly outside the piece re-reads the first quad)
   if (B32) {
-    x.b[0] = *reinterpret_cast<const uint4*>(c.bal32 + pp);
+    x.b[0] = NTB ? ldnt16(c.bal32 + pp) : *reinterpret_cast<const uint4*>(c.bal32 + pp);
   } else {
-    x.b[0] = *reinterpret_cast<const uint4*>(c.bal + pp);
-    x.b[B32 ? 0 : 1] = *reinterpret_cast<const uint4*>(c.bal + pp + 2);
+    x.b[0] = NTB ? ldnt16(c.bal + pp) : *reinterpret_cast<const uint4*>(c.bal + pp);
+    x.b[B32 ? 0 : 1] = NTB ? ldnt16(c.bal + pp + 2) : *reinterpret_cast<const uint4*>(c.bal + pp + 2);
   }
-  // the bounds are read once per step: nontemporal, leaving the Infinity Cache to the balances
+  // the bounds are read once per step: nontemporal
   if (SEW == 16) {
     x.s[0] = ldnt16(c.se16 + pp);
   } else if (SEW == 32) {
@@ -184,10 +187,12 @@ size_t window_lds_bytes(const WinArgs& w) { return 8ull * ((size_t)w.lds_maxc + 
 // (alone) the speculating blocks' post-loop meeting skipped, the fallback count every time (exact);
 // 16384 the product's L2 form (the reward bits looked up in the last bitfield in global memory,
 // no LDS copy; exact).
-template <bool B32, int SEW, bool LLB, int AB = 0, int D = kWinDepth, bool TR = false, bool NA = false, bool NP = true>
+template <bool B32, int SEW, bool LLB, int AB = 0, int D = kWinDepth, bool TR = false, bool NA = false, bool NP = true,
+          int KD = 0>
 __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w) {
   extern __shared__ __align__(16) uint8_t lds_dyn[];
   constexpr int NT = kWinThreads, NW = NT / 64;
+  constexpr bool NTB = !(AB & (1 << 20));  // the balances nontemporal (A/B bit 1 << 20: round 5's cached form)
   __shared__ uint64_t red[NW][2], red2[NW][2];  // (the prologue's and the loop's: no barrier between their uses)
   __shared__ uint64_t tstamp[4];  // (TR only)
   const int tid = threadIdx.x, lane = tid & 63;
@@ -387,18 +392,34 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
                                          0);
     }
   };
+  // KD > 0 (the plan's WinArgs.dma_k): exactly KD wave instructions, no branch, no predicate --
+  // past the copy's end a lane re-reads its last chunk into the padding (lds_lbf holds KD x NT
+  // chunks) -- so the loads issued after it keep exact waits and it can go out first
+  auto last_bitfield_dma_k = [&]() {
+    typedef __attribute__((address_space(3))) void lds_void_t;
+    typedef const __attribute__((address_space(1))) void gbl_void_t;
+    const uint32_t nlm = (uint32_t)(nch - clb) - 1;  // (>= 0: the plan takes KD only for non-empty copies)
+#pragma unroll
+    for (int u = 0; u < (KD > 0 ? KD : 1); ++u) {
+      const uint32_t c0 = wave * 64 + (uint32_t)u * NT;
+      const uint32_t c = min(c0 + (uint32_t)lane, nlm);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(a.bits + lbase + 16ull * c), (lds_void_t*)(L.lbf + 16 * c0), 16, 0, 0);
+    }
+  };
   // NP, step 1: the count's first loads, before any wait (the DMA follows the count's take:
   // issued earlier, its branches would turn every later wait into a full drain)
   CountLd cl0;
   const uint64_t ncn = s1 - s0, ngn = g1s - g0s;
+  if (NP && KD > 0 && LLB && !(AB & 2)) last_bitfield_dma_k();  // (straight-line: the waits stay exact)
   if (NP && !(AB & 2)) cnt_issue(s0, ncn, g0s, ngn, 0, cl0);
+  if (NP && (AB & (1 << 21)) && !(AB & 2) && LLB && KD == 0) last_bitfield_dma();  // (A/B: the DMA loop before the first wait)
   Piece dq[D];
 #pragma unroll
   for (int j = 0; j < D; ++j) dq[j] = piece(dv, j, 0);
   WinCols<B32, SEW> q[D];
   if (!(AB & 64)) {
 #pragma unroll
-    for (int j = 0; j < D; ++j) win_load<B32, SEW>(col, dq[j], lane, q[j]);
+    for (int j = 0; j < D; ++j) win_load<B32, SEW, NTB>(col, dq[j], lane, q[j]);
   }
   dv = NP ? dv1 : desc(1);
   if (NP) {
@@ -413,7 +434,7 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
         cnt_issue(s0, ncn, g0s, ngn, it, cl);
         cnt_take(s0, ncn, ngn, it, cl);
       }
-      if (LLB) last_bitfield_dma();
+      if (LLB && KD == 0 && !(AB & (1 << 21))) last_bitfield_dma();
     } else {
       pop = tid == 0 ? a.total_deposit[inst] : 0;  // (ablation: the threshold holds)
     }
@@ -490,7 +511,7 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   }
   if (AB & 64) {  // (A/B: the first pieces' loads only now, behind the prologue's)
 #pragma unroll
-    for (int j = 0; j < D; ++j) win_load<B32, SEW>(col, dq[j], lane, q[j]);
+    for (int j = 0; j < D; ++j) win_load<B32, SEW, NTB>(col, dq[j], lane, q[j]);
   }
   if (TR && tid == 0) tstamp[1] = __builtin_amdgcn_s_memrealtime();
   // the next step's accumulators start from zero, its winners empty (its own buffers: issued
@@ -693,11 +714,20 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
         }
         if (applied) {
           if (all) {
-            *reinterpret_cast<uint4*>(Bal32 + p) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+            if (NTB) {
+              v4u o;
+              o.x = o4[0], o.y = o4[1], o.z = o4[2], o.w = o4[3];
+              __builtin_nontemporal_store(o, reinterpret_cast<v4u*>(Bal32 + p));
+            } else {
+              *reinterpret_cast<uint4*>(Bal32 + p) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+            }
           } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-              if (v[i]) Bal32[p + i] = o4[i];
+              if (v[i]) {
+                if (NTB) __builtin_nontemporal_store(o4[i], Bal32 + p + i);
+                else Bal32[p + i] = o4[i];
+              }
           }
         }
       } else {
@@ -710,13 +740,18 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int i = 2 * h;
-            if (v[i] && v[i + 1])
-              *reinterpret_cast<uint4*>(Bal + p + i) =
-                  make_uint4((uint32_t)b[i], (uint32_t)(b[i] >> 32), (uint32_t)b[i + 1], (uint32_t)(b[i + 1] >> 32));
-            else if (v[i])
-              Bal[p + i] = b[i];
-            else if (v[i + 1])
-              Bal[p + i + 1] = b[i + 1];
+            if (v[i] && v[i + 1]) {
+              v4u o;
+              o.x = (uint32_t)b[i], o.y = (uint32_t)(b[i] >> 32), o.z = (uint32_t)b[i + 1], o.w = (uint32_t)(b[i + 1] >> 32);
+              if (NTB) __builtin_nontemporal_store(o, reinterpret_cast<v4u*>(Bal + p + i));
+              else *reinterpret_cast<v4u*>(Bal + p + i) = o;
+            } else if (v[i]) {
+              if (NTB) __builtin_nontemporal_store(b[i], Bal + p + i);
+              else Bal[p + i] = b[i];
+            } else if (v[i + 1]) {
+              if (NTB) __builtin_nontemporal_store(b[i + 1], Bal + p + i + 1);
+              else Bal[p + i + 1] = b[i + 1];
+            }
           }
         }
 #pragma unroll
@@ -724,7 +759,7 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       }
       // slot j's piece of the next round (past the last round: a dummy, loaded and unused)
       dq[j] = piece(dnx, j, t + 1);
-      win_load<B32, SEW>(col, dq[j], lane, q[j]);
+      win_load<B32, SEW, NTB>(col, dq[j], lane, q[j]);
     }
   }
   // the epilogue's first kEpiPf attestations per thread: their words now, ahead of the meeting
@@ -859,6 +894,14 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
 // balances as u32 offsets (the narrow tallies or not) / u64; {start, end} at 16 / 32 / 64 bits;
 // the last bitfield in LDS or not
 PZ_WINDOW_KERNEL(pz_epoch_window_b32n_s16_kernel, true, 16, true, true)
+// the product form with the straight-line last-bitfield copy (WinArgs.dma_k, kWinDmaK)
+#define PZ_WINDOW_KERNEL_K(K)                                                                                 \
+  extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_b32n_s16_k##K##_kernel(EpochArgs a, \
+                                                                                                WinArgs w) {  \
+    window_body<true, 16, true, 0, kWinDepth16, false, true, true, K>(a, w);                                 \
+  }
+PZ_WINDOW_KERNEL_K(1) PZ_WINDOW_KERNEL_K(2) PZ_WINDOW_KERNEL_K(3) PZ_WINDOW_KERNEL_K(5) PZ_WINDOW_KERNEL_K(9)
+#undef PZ_WINDOW_KERNEL_K
 PZ_WINDOW_KERNEL(pz_epoch_window_b32n_s32_kernel, true, 32, true, true)
 PZ_WINDOW_KERNEL(pz_epoch_window_b32n_s64_kernel, true, 64, true, true)
 PZ_WINDOW_KERNEL(pz_epoch_window_b32_s16_kernel, true, 16, true, false)
@@ -889,17 +932,19 @@ PZ_WINDOW_ABL(0, 2) PZ_WINDOW_ABL(0, 3) PZ_WINDOW_ABL(0, 4)
 PZ_WINDOW_ABL(1, 2) PZ_WINDOW_ABL(2, 2) PZ_WINDOW_ABL(4, 2) PZ_WINDOW_ABL(7, 2) PZ_WINDOW_ABL(16, 2)
 PZ_WINDOW_ABL(48, 2) PZ_WINDOW_ABL(64, 2) PZ_WINDOW_ABL(128, 2) PZ_WINDOW_ABL(144, 2) PZ_WINDOW_ABL(4096, 2)
 PZ_WINDOW_ABL(8192, 2) PZ_WINDOW_ABL(32, 2) PZ_WINDOW_ABL(65536, 2) PZ_WINDOW_ABL(131072, 2)
+PZ_WINDOW_ABL(1048576, 2) PZ_WINDOW_ABL(2097152, 2)
 // the product form with phase stamps (tools/epoch_trace.py)
 extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_kernel(EpochArgs a, WinArgs w) {
   window_body<true, 16, true, 0, kWinDepth16, true, true>(a, w);
 }
-// round 5's prologue (the count after the first pieces' descriptors, two barriers, the range
-// descriptor from global memory): A/B bit 1 << 18, with and without phase stamps
+// round 5's product (its prologue: the count after the first pieces' descriptors, two barriers,
+// the range descriptor from global memory; the balances through the caches): A/B bit 1 << 18,
+// with and without phase stamps
 extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_np0_kernel(EpochArgs a, WinArgs w) {
-  window_body<true, 16, true, 0, kWinDepth16, false, true, false>(a, w);
+  window_body<true, 16, true, 1 << 20, kWinDepth16, false, true, false>(a, w);
 }
 extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_np0_kernel(EpochArgs a, WinArgs w) {
-  window_body<true, 16, true, 0, kWinDepth16, true, true, false>(a, w);
+  window_body<true, 16, true, 1 << 20, kWinDepth16, true, true, false>(a, w);
 }
 #undef PZ_WINDOW_ABL
 static int g_window_ablation = 0;
@@ -922,6 +967,16 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
   k = llb ? (const void*)pz_epoch_window_##B##_s##S##_kernel : (const void*)pz_epoch_window_##B##_s##S##_g_kernel
   if (b32 && w.narrow) {
     if (sew == 16) PZ_PICK(b32n, 16);
+    if (sew == 16 && llb && w.dma_k) {  // (the straight-line copy: WinArgs.dma_k)
+      switch (w.dma_k) {
+        case 1: k = (const void*)pz_epoch_window_b32n_s16_k1_kernel; break;
+        case 2: k = (const void*)pz_epoch_window_b32n_s16_k2_kernel; break;
+        case 3: k = (const void*)pz_epoch_window_b32n_s16_k3_kernel; break;
+        case 5: k = (const void*)pz_epoch_window_b32n_s16_k5_kernel; break;
+        case 9: k = (const void*)pz_epoch_window_b32n_s16_k9_kernel; break;
+        default: return hipErrorInvalidValue;
+      }
+    }
     else if (sew == 32) PZ_PICK(b32n, 32);
     else PZ_PICK(b32n, 64);
   } else if (b32) {
@@ -960,6 +1015,8 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
       case 65536: k = (const void*)pz_epoch_window_abl65536_d2_kernel; break;  // (timing: no multi-attestation votes)
       case 131072: k = (const void*)pz_epoch_window_abl131072_d2_kernel; break;  // (one attestation per trip)
       case 1 << 18: k = (const void*)pz_epoch_window_np0_kernel; break;  // (round 5's prologue)
+      case 1 << 20: k = (const void*)pz_epoch_window_abl1048576_d2_kernel; break;  // (round 5's cached balances)
+      case 1 << 21: k = (const void*)pz_epoch_window_abl2097152_d2_kernel; break;  // (the DMA before the first wait)
       default: return hipErrorInvalidValue;
     }
   }

@@ -298,6 +298,7 @@ constexpr int kRow = 16, kRecs = 64 / kRow, kMaxOblique = kRow - 3;
 //   9-10  oblique element range     11-12  signature value range     (AB form: 13-14 offs[i], offs[i+1])
 constexpr int kHeadWords = 13;
 
+template <bool NTL = false>
 __device__ __forceinline__ uint64_t head_word(const AttArgs& a, int k, uint64_t i) {
   const uint64_t* p = nullptr;
   uint32_t d = 0;
@@ -310,7 +311,7 @@ __device__ __forceinline__ uint64_t head_word(const AttArgs& a, int k, uint64_t 
     p = k < 11 ? a.ofirst : k < 13 ? a.sfirst : a.offs;
     d = (k - 9) & 1;
   }
-  return p ? p[i + d] : 0;
+  return p ? (NTL ? __builtin_nontemporal_load(p + i + d) : p[i + d]) : 0;
 }
 
 __device__ __forceinline__ uint64_t rl64(uint64_t x, int k) {
@@ -453,14 +454,16 @@ __device__ __forceinline__ void stage_segment_unaligned(uint8_t* d, const uint8_
   }
 }
 
-template <int M>
+// NTF (A/B): bit 0 the whole 16-B output blocks stored nontemporally, bit 1 the head words
+// loaded nontemporally
+template <int M, int NTF = 0>
 __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*stage)[kStageAlloc], uint64_t i0) {
   const int lane = threadIdx.x & 63;
   const int sl = lane & (kRow - 1), ri = lane / kRow;
   if (i0 >= a.n) return;
   const uint64_t i = i0 + ri;
   const bool valid = i < a.n;
-  const uint64_t hv = valid && sl < kHeadWords + 2 ? head_word(a, sl, i) : 0;
+  const uint64_t hv = valid && sl < kHeadWords + 2 ? head_word<(NTF & 2) != 0>(a, sl, i) : 0;
   // Each lane's word below it (row_shr:1) and the difference: lanes 4, 6, 8 hold bl[0..2],
   // lane 10 the oblique count, 12 the value count, 14 the size.  Only what every lane needs is
   // broadcast; a lane's own operands come by one shift or one ds_bpermute.  Counts and lengths
@@ -580,7 +583,12 @@ __device__ __forceinline__ void wire_att_write_rows(const AttArgs& a, uint8_t (*
   for (uint32_t q = sl; q < nblk; q += kRow) {
     const uint32_t lo = 16 * q, hi = lo + 16;
     if (lo >= sh && hi <= sh + sz) {
-      *reinterpret_cast<uint4*>(ob + lo) = *reinterpret_cast<const uint4*>(sb + lo);
+      if (NTF & 1) {
+        typedef unsigned int v4u_ __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(*reinterpret_cast<const v4u_*>(sb + lo), reinterpret_cast<v4u_*>(ob + lo));
+      } else {
+        *reinterpret_cast<uint4*>(ob + lo) = *reinterpret_cast<const uint4*>(sb + lo);
+      }
     } else if (M < 2) {
       for (uint32_t x = max(lo, sh); x < min(hi, sh + sz); ++x) ob[x] = sb[x];
     } else {  // an edge block shared with a neighbour: 1-, 2-, 4- and 8-byte pieces of [x, e)
@@ -893,20 +901,23 @@ extern "C" __global__ void __launch_bounds__(kSizeThreads) pz_wire_att_size_loop
 // Launch 2: four records per wave, one per DPP row.  63 VGPRs; left alone the SGPRs (about
 // 100) hold it at 7 waves per SIMD.  Capped at 8 (28 SGPRs spill to VGPR lanes): 0.432 ->
 // 0.383 ms per 1M-record encode (tools/wire_att_probe.py r2t, same-process A/B).
-#define PZ_ATT_WRITE(NAME, DST)                                                                      \
+#define PZ_ATT_WRITE(NAME, DST, NTF)                                                                 \
   extern "C" __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))  \
   NAME(AttArgs a) {                                                                                  \
     __shared__ __attribute__((aligned(16))) uint8_t stage[kWaves][kRecs][kStageAlloc];              \
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);                                  \
-    wire_att_write_rows<DST>(a, stage[w], ((uint64_t)blockIdx.x * kWaves + w) * kRecs);              \
+    wire_att_write_rows<DST, NTF>(a, stage[w], ((uint64_t)blockIdx.x * kWaves + w) * kRecs);         \
   }
-PZ_ATT_WRITE(pz_wire_att_write_kernel, 2)
+PZ_ATT_WRITE(pz_wire_att_write_kernel, 2, 0)
 #ifdef PZ_AB_BUILD
-PZ_ATT_WRITE(pz_wire_att_write_bytes_kernel, 0)
-PZ_ATT_WRITE(pz_wire_att_write_aligned_kernel, 1)
-PZ_ATT_WRITE(pz_wire_att_write_sigloop_kernel, 3)  // the product with the byte-loop signature varints
+PZ_ATT_WRITE(pz_wire_att_write_bytes_kernel, 0, 0)
+PZ_ATT_WRITE(pz_wire_att_write_aligned_kernel, 1, 0)
+PZ_ATT_WRITE(pz_wire_att_write_sigloop_kernel, 3, 0)  // the product with the byte-loop signature varints
+PZ_ATT_WRITE(pz_wire_att_write_nts_kernel, 2, 1)  // nontemporal 16-B output stores
+PZ_ATT_WRITE(pz_wire_att_write_ntsl_kernel, 2, 3)  // + nontemporal head loads
 // 1 round 4's three launches, 2 this scan + byte-wise stage, 3-5 other sizing tiles, 6 the
-// aligned-dword stage, 7 the sizing loops, 8 byte-loop signature varints
+// aligned-dword stage, 7 the sizing loops, 8 byte-loop signature varints, 9 nontemporal output
+// stores, 10 + nontemporal head loads
 int g_att_variant = 0;
 #endif
 
@@ -919,6 +930,8 @@ hipError_t launch_write(const AttArgs& a, bool dst, hipStream_t s) {
   if (!dst) k = (const void*)pz_wire_att_write_bytes_kernel;
   if (g_att_variant == 6) k = (const void*)pz_wire_att_write_aligned_kernel;
   if (g_att_variant == 8) k = (const void*)pz_wire_att_write_sigloop_kernel;
+  if (g_att_variant == 9) k = (const void*)pz_wire_att_write_nts_kernel;
+  if (g_att_variant == 10) k = (const void*)pz_wire_att_write_ntsl_kernel;
 #else
   (void)dst;
 #endif

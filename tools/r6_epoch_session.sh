@@ -24,4 +24,10 @@ if [ -n "$TABL" ]; then
     || { echo TRACE2_FAIL; tail -20 "$O/epoch_trace_abl.txt"; exit 16; }
   cat "$O/epoch_trace_abl.txt"
 fi
+
+if [ -n "$WABL" ]; then
+  PZ_PROBE_LIB=build/ab/libprysm_hip.so ABL=$WABL timeout -k 10 300 python -u tools/epoch_warm.py > "$O/epoch_warm_ab.txt" 2>&1 \
+    || { echo WARM_FAIL; tail -20 "$O/epoch_warm_ab.txt"; exit 17; }
+  cat "$O/epoch_warm_ab.txt"
+fi
 echo "SESSION_DONE"
