@@ -925,7 +925,9 @@ def replay_sharded_leg(args, torch, dist, dev, rank, world, comm):
     every rank replays the same 10,000 blocks (the walk is sequential host work, done by each
     process), and the device work is split by validator range -- each GPU holds 1/N of the
     balances, of every vote-cache voter bitmap and of every epoch; a transition all-reduces the
-    64 justification totals and the epoch's partial sums over RCCL (pz_chain_new_comm)."""
+    64 justification totals, the epoch's partial sums and the previous epoch's next-cycle
+    partial in ONE collective over RCCL (pz_chain_new_comm; the call's final flush carries the
+    last one)."""
     from prysm_amd import synth
     from prysm_amd.blockchain import BeaconChain, serialize_blocks
 
@@ -959,8 +961,9 @@ def replay_sharded_leg(args, torch, dist, dev, rank, world, comm):
     out = {"metric": "sync-replay blocks/s (one chain over N GPUs)", "value": nb / wall, "unit": "blocks/s",
            "ms_per_block": wall / nb * 1e3,
            "config": {"workload": "the configs[4] chain (10,000 blocks, 65,536 validators) as ONE chain",
-                      "parallelism": "validator-range shard x%d of the vote cache and the epoch; all-reduce of "
-                                     "the 64 justification totals + the epoch's partial sums per transition (%s)"
+                      "parallelism": "validator-range shard x%d of the vote cache and the epoch; ONE all-reduce "
+                                     "per transition: the 64 justification totals, the epoch's partial sums and the "
+                                     "previous epoch's next-cycle partial (%s)"
                                      % (world, "RCCL" if dist.get_backend() == "nccl" else "SHM rehearsal")},
            "processed": int((br["status"] == 0).sum()), "transitions": int(br["transition"].sum()),
            "collectives": {"count": cn, "device_ms": cms, "per_transition": cn / max(1, int(br["transition"].sum())),

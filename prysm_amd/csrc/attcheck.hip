@@ -137,6 +137,164 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_x2_kernel(pz
   att_check_x2_body(b);
 }
 
+// ---- round 6: persistent blocks with the committee table in LDS --------------------------------
+// The x2 kernel is latency-bound (VALU-busy 0.15, counted traffic 1.00x): after its column loads
+// every attestation walks the committee table in global memory -- arr_offs[idx], then
+// arr_shard[e] entry by entry (a load per step, the exit data-dependent), arr_comm[e],
+// coffs[comm], coffs[comm + 1] -- four to eight dependent L2 round trips per lane.  Here each
+// block stages the table once into LDS as 32-bit words ({offsets | shards | committees |
+// committee sizes}: the sizes resolved through coffs while staging), then its lanes loop over
+// attestation pairs with the next pair's columns in flight while the current one is checked, so
+// the walk is LDS lookups (~100 cycles each) under the next pair's HBM round trip.  A table too
+// large for the LDS budget, or with a shard id or committee size past 32 bits, or malformed
+// offsets, keeps the global walk (the same check_one) in every block.
+constexpr int kPThreads = 512, kPBlocksPerCU = 2;
+constexpr uint32_t kPTabWords = 12288;  // 48 KiB
+
+struct PairLd {
+  ulonglong2 s, bs, js, nob, sh, bo;
+  uint64_t bo2;
+  uint32_t lb;  // the two last bytes (last_byte column), else 0
+};
+
+__device__ __forceinline__ void load_pair(const pz_att_check_batch& b, uint64_t i, PairLd& x) {
+  auto ld2 = [](const uint64_t* p) {
+    typedef unsigned long long v2u __attribute__((ext_vector_type(2)));
+    const v2u v = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
+    return make_ulonglong2(v.x, v.y);
+  };
+  x.s = ld2(b.slot + i), x.bs = ld2(b.block_slot + i), x.js = ld2(b.justified_slot + i);
+  x.nob = ld2(b.n_oblique + i), x.sh = ld2(b.shard_id + i), x.bo = ld2(b.boffs + i);
+  x.bo2 = b.boffs[i + 2];
+  x.lb = b.last_byte ? (uint32_t)*reinterpret_cast<const uint16_t*>(b.last_byte + i) : 0u;
+}
+
+// check_one with the committee walk in the block's LDS table (same order and types)
+__device__ __forceinline__ void check_one_lds(const pz_att_check_batch& b, const uint32_t* offs, const uint32_t* tsh,
+                                              const uint32_t* tcm, const uint32_t* tkk, uint64_t s, uint64_t bs,
+                                              uint64_t js, uint64_t nob, uint64_t shard, uint64_t b0, uint64_t b1,
+                                              int32_t* st_out, uint32_t* comm_out, uint64_t* pstart_out, int lastb) {
+  int32_t st = PZ_ATT_PROCESSED;
+  uint32_t comm = UINT32_MAX;
+  uint64_t pstart = 0;
+  if ((int64_t)s > (int64_t)bs) {
+    st = PZ_ATT_SLOT_HIGH;
+  } else if ((int64_t)s < (int64_t)bs - PZ_CYCLE_LENGTH) {
+    st = PZ_ATT_SLOT_LOW;
+  } else if (js != b.last_justified_slot) {
+    st = PZ_ATT_JUSTIFIED;
+  } else {
+    const uint64_t start = bs - s, end = bs - s - nob + PZ_CYCLE_LENGTH;
+    const uint64_t idx = s - b.last_state_recalc;
+    if (start > end || end > b.n_recent) {
+      st = PZ_ERANGE;  // Go panics: slice bounds out of range (core.go:353)
+    } else if (idx >= b.narr) {
+      st = PZ_EINDEX;  // Go panics: index out of range (core.go:367)
+    } else {
+      pstart = start;
+      uint64_t k = 0;
+      const bool small = (shard >> 32) == 0;  // (every staged shard id is below 2^32)
+      for (uint32_t e = offs[idx]; e < offs[idx + 1]; ++e)
+        if (small && tsh[e] == (uint32_t)shard) {
+          comm = tcm[e];
+          k = tkk[e];
+          break;
+        }
+      if (comm == UINT32_MAX) {
+        st = PZ_ATT_NO_COMMITTEE;
+      } else {
+        const uint64_t blen = b1 - b0;
+        if ((k + 7) / 8 != blen)
+          st = PZ_ATT_BITFIELD_LEN;
+        else if ((k & 7) && ((lastb >= 0 ? (uint32_t)lastb : (uint32_t)b.bits[b0 + blen - 1]) & (0xFFu >> (k & 7))))
+          st = PZ_ATT_TRAILING_BITS;  // only when bits pad the byte
+      }
+    }
+  }
+  *st_out = st;
+  *comm_out = comm;
+  *pstart_out = pstart;
+}
+
+__device__ __forceinline__ void check_pair(const pz_att_check_batch& b, bool lds, const uint32_t* offs,
+                                           const uint32_t* tsh, const uint32_t* tcm, const uint32_t* tkk, uint64_t i,
+                                           const PairLd& x) {
+  const int lb0 = b.last_byte ? (int)(x.lb & 0xFF) : -1, lb1 = b.last_byte ? (int)(x.lb >> 8) : -1;
+  int32_t st0, st1;
+  uint32_t c0, c1;
+  uint64_t p0, p1;
+  if (lds) {
+    check_one_lds(b, offs, tsh, tcm, tkk, x.s.x, x.bs.x, x.js.x, x.nob.x, x.sh.x, x.bo.x, x.bo.y, &st0, &c0, &p0, lb0);
+    check_one_lds(b, offs, tsh, tcm, tkk, x.s.y, x.bs.y, x.js.y, x.nob.y, x.sh.y, x.bo.y, x.bo2, &st1, &c1, &p1, lb1);
+  } else {
+    check_one(b, x.s.x, x.bs.x, x.js.x, x.nob.x, x.sh.x, x.bo.x, x.bo.y, &st0, &c0, &p0, lb0);
+    check_one(b, x.s.y, x.bs.y, x.js.y, x.nob.y, x.sh.y, x.bo.y, x.bo2, &st1, &c1, &p1, lb1);
+  }
+  *reinterpret_cast<int2*>(b.status + i) = make_int2(st0, st1);
+  if (b.committee) *reinterpret_cast<uint2*>(b.committee + i) = make_uint2(c0, c1);
+  if (b.parents_start) *reinterpret_cast<ulonglong2*>(b.parents_start + i) = make_ulonglong2(p0, p1);
+}
+
+extern "C" __global__ void __launch_bounds__(kPThreads) pz_att_check_p_kernel(pz_att_check_batch b) {
+  __shared__ uint32_t tab[kPTabWords];
+  const int tid = threadIdx.x;
+  const uint64_t npairs = b.natt / 2, stride = (uint64_t)gridDim.x * kPThreads;
+  uint64_t p = (uint64_t)blockIdx.x * kPThreads + tid;
+  // the first pair's columns go out before the table's loads
+  PairLd cur;
+  bool have = p < npairs;
+  if (have) load_pair(b, 2 * p, cur);
+  // stage the table: {arr_offs (narr + 1) | shard | committee | committee size (ne each)}
+  const uint64_t narr = b.narr;
+  const uint64_t ne = narr ? b.arr_offs[narr] : 0;
+  bool ok = narr + 1 + 3 * ne <= kPTabWords;
+  uint32_t* offs = tab;
+  uint32_t* tsh = tab + (ok ? narr + 1 : 0);
+  uint32_t* tcm = tsh + (ok ? ne : 0);
+  uint32_t* tkk = tcm + (ok ? ne : 0);
+  if (ok) {
+    for (uint64_t a = tid; a <= narr; a += kPThreads) {
+      const uint64_t o = b.arr_offs[a];
+      ok = ok && o <= ne && (a == 0 || b.arr_offs[a - 1] <= o);
+      offs[a] = (uint32_t)o;
+    }
+    for (uint64_t e = tid; e < ne; e += kPThreads) {
+      const uint64_t sh = b.arr_shard[e];
+      const uint32_t c = b.arr_comm[e];
+      const uint64_t k = b.coffs[(uint64_t)c + 1] - b.coffs[c];
+      ok = ok && (sh >> 32) == 0 && (k >> 32) == 0;
+      tsh[e] = (uint32_t)sh, tcm[e] = c, tkk[e] = (uint32_t)k;
+    }
+  }
+  const bool lds = __syncthreads_and(ok ? 1 : 0) != 0;
+  while (have) {  // (lanes leave independently: no barrier below)
+    const uint64_t q = p + stride;
+    const bool hq = q < npairs;
+    PairLd nx;
+    if (hq) load_pair(b, 2 * q, nx);
+    check_pair(b, lds, offs, tsh, tcm, tkk, 2 * p, cur);
+    cur = nx;
+    p = q;
+    have = hq;
+  }
+  // the odd tail: the last attestation alone, by the grid's first lane
+  if ((b.natt & 1) && blockIdx.x == 0 && tid == 0) {
+    const uint64_t i = b.natt - 1;
+    int32_t st;
+    uint32_t comm;
+    uint64_t pstart;
+    check_one(b, b.slot[i], b.block_slot[i], b.justified_slot[i], b.n_oblique[i], b.shard_id[i], b.boffs[i],
+              b.boffs[i + 1], &st, &comm, &pstart, b.last_byte ? (int)b.last_byte[i] : -1);
+    b.status[i] = st;
+    if (b.committee) b.committee[i] = comm;
+    if (b.parents_start) b.parents_start[i] = pstart;
+  }
+}
+
+#ifdef PZ_AB_BUILD
+static int g_attcheck_variant = 0;  // 1: round 5's x2 kernel (one pair per lane, the walk in global memory)
+#endif
+
 int check_args(const pz_att_check_batch* b) {
   if (!b) return fail(PZ_EINVAL, "batch is null");
   if (b->natt && (!b->slot || !b->justified_slot || !b->shard_id || !b->n_oblique || !b->boffs || !b->block_slot ||
@@ -155,7 +313,28 @@ hipError_t launch_att_check(const pz_att_check_batch& b, hipStream_t s) {
                   (!b.committee || (reinterpret_cast<uintptr_t>(b.committee) & 7) == 0) &&
                   (!b.parents_start || al(b.parents_start)) &&
                   (!b.last_byte || (reinterpret_cast<uintptr_t>(b.last_byte) & 1) == 0);
-  if (x2) {
+  bool persistent = x2 && b.natt >= 2;
+#ifdef PZ_AB_BUILD
+  if (g_attcheck_variant == 1) persistent = false;
+#endif
+  if (persistent) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                  hipSuccess || cus <= 0)
+        cus = 256;
+    }
+    const uint64_t npairs = b.natt / 2;
+    uint64_t per_cu = kPBlocksPerCU;
+#ifdef PZ_AB_BUILD
+    if (g_attcheck_variant == 2) per_cu = 3;  // (A/B: blocks per CU)
+    if (g_attcheck_variant == 3) per_cu = 1;
+#endif
+    const uint64_t nb = std::max<uint64_t>(1, std::min<uint64_t>((npairs + kPThreads - 1) / kPThreads,
+                                                                 (uint64_t)cus * per_cu));
+    hipLaunchKernelGGL(pz_att_check_p_kernel, dim3((uint32_t)nb), dim3(kPThreads), 0, s, b);
+  } else if (x2) {
     const uint64_t lanes = (b.natt + 1) / 2;
     hipLaunchKernelGGL(pz_att_check_x2_kernel, dim3((uint32_t)((lanes + kThreads - 1) / kThreads)), dim3(kThreads), 0,
                        s, b);
@@ -224,3 +403,11 @@ int pz_check_attestations(const pz_att_check_batch* hb) {
 }
 
 }  // extern "C"
+
+#ifdef PZ_AB_BUILD
+extern "C" int pz_debug_set_attcheck_variant(int v) {
+  const int old = pz::g_attcheck_variant;
+  pz::g_attcheck_variant = v;
+  return old;
+}
+#endif

@@ -676,15 +676,18 @@ struct RankDev {
   DevArr<uint64_t> d_err;      // sticky tally panic flag
   DevArr<uint32_t> v_ticket;   // the fused gather's arrival ticket (left zero)
   DevArr<uint64_t> v_trace;    // (PZ_VOTE_TRACE, tools/ only) per flush and wave, the tally's phase stamps
-  DevArr<uint64_t> t64;        // the gathered justification totals + panic flag (65 words)
+  // sharded (world > 1): the transition's one all-reduce buffer, [totals + panic flag (65) |
+  // TotalDeposits slot (1) | the epoch's {scal, vote, total} partials], and this rank's
+  // post-reward next-cycle partial waiting for the next all-reduce (sharded_reduce_enqueue)
+  DevArr<uint64_t> xred, nbp;
   // epoch scratch: red = {scal[8], vote[natt], total[natt]} (one all-reduce when sharded)
-  DevArr<uint64_t> e_red, e_mask, e_nb;
+  DevArr<uint64_t> e_red, e_mask;
   DevArr<uint32_t> e_blk, e_list, e_win;
   DevArr<uint8_t> e_pack;      // one H2D per transition: bitfields, offsets, committees, ... (sharded)
   DevArr<uint32_t> e_ticket;   // one rank: the reward pass's hand-off ticket (left zero)
   hipEvent_t q_ev = nullptr;   // this rank's copy of the pinned tally arena is done (staged path)
   hipEvent_t vq_ev[2] = {};    // this rank's last reader of Engine::vq[i] is done
-  hipEvent_t ev_epoch = nullptr, ev_red = nullptr, ev_nb = nullptr, ev_t64 = nullptr;
+  hipEvent_t ev_epoch = nullptr, ev_t64 = nullptr;
 };
 
 struct Engine {
@@ -758,6 +761,11 @@ struct Engine {
   Knobs kn;                       // (read_knobs)
   pz_chain_options opt{};         // pz_chain_set_options (every field 0: the product's choices)
   uint64_t calls = 0;             // pz_chain_process_blocks calls that reached the walk
+  // sharded: the last epoch's next-cycle balance is still a partial per rank (nbp), summed by
+  // the next all-reduce (a transition's or the call's final flush), then set as nb_dst's
+  // TotalDeposits
+  bool nb_pending = false, nb_carried = false;
+  CP nb_dst;
   uint64_t kmax = 0;              // the largest committee
   bool bits_inline = true;        // every committee <= kVoteInlineBits: the bitfields ride in the records
   bool ids_rows = false;          // (pz_chain_options.tally_forms bit 2) every attestation's ids in an explicit row
@@ -1269,47 +1277,87 @@ static bool flush_votes_enqueue(Engine& g, const VoteGatherSlots* gq = nullptr, 
 }
 
 // Enqueue, behind every rank's pending tallies, the gather of the 64 justification totals
-// (slot UINT32_MAX: 0) and the sticky tally panic flag into each rank's t64, their sum over
-// the ranks (one 65-word all-reduce when sharded: the partial VoteTotalDeposit sums of the
-// validator ranges) and the D2H of rank 0's into g.tot_pin, then g.ev_totals.
-static void tally_gather_enqueue(Engine& g, const VoteGatherSlots& q) {
-  check(g.tot_pin.reserve((kJustifySlots + 1) * 8));
+// (slot UINT32_MAX: 0) and the sticky tally panic flag, then g.ev_totals: one rank straight
+// into g.tot_pin; sharded, into each rank's xred, summed by one all-reduce (the partial
+// VoteTotalDeposit sums of the validator ranges, with any pending next-cycle partial).
+// sharded (world > 1): every rank's xred [totals + panic flag | TotalDeposits slot | epoch
+// partials (nred words)] summed by ONE all-reduce, each rank's stream waiting for it, rank 0's
+// first kJustifySlots + 2 words D2H into g.tot_pin, then g.ev_totals.  A pending next-cycle
+// partial rode in the TotalDeposits slot: tally_gather_finish hands the sum to g.nb_dst.
+static void sharded_allreduce(Engine& g, uint64_t nred) {
+  check(g.tot_pin.reserve((kJustifySlots + 2) * 8));
   std::vector<uint64_t*> bufs;
   std::vector<hipStream_t> streams;
   std::vector<hipEvent_t> evs;
-  each_rank(g, [&](RankDev& r) {
-    check(r.t64.alloc(kJustifySlots + 1));
-    if (!r.d_err.p) {
-      check(r.d_err.alloc(1));
-      hchk(hipMemsetAsync(r.d_err.p, 0, 8, r.s), "memset");
-    }
+  for (RankDev& r : g.rk) {
     if (!r.ev_t64) hchk(hipEventCreateWithFlags(&r.ev_t64, hipEventDisableTiming), "event");
-    if (g.world == 1) {
-      // one rank: the gather stores straight into the pinned totals (no D2H copy behind it)
-      void* dp = nullptr;
-      check(g.tot_pin.dev(r.dev, &dp));
-      hchk(launch_vote_gather(r.totals.p, q, r.d_err.p, static_cast<uint64_t*>(dp), r.s), "vote gather");
-      return;
-    }
-    hchk(launch_vote_gather(r.totals.p, q, r.d_err.p, r.t64.p, r.s), "vote gather");
-    bufs.push_back(r.t64.p);
+    bufs.push_back(r.xred.p);
     streams.push_back(r.s);
     evs.push_back(r.ev_t64);
-  });
-  if (g.world > 1) {
-    check(g.comm->allreduce_u64(bufs.data(), kJustifySlots + 1, streams.data(), evs.data()));
-    hchk(hipSetDevice(g.rk[0].dev), "hipSetDevice");
-    hchk(hipStreamWaitEvent(g.rk[0].s, g.rk[0].ev_t64, 0), "wait");
   }
-  if (g.world > 1)
-    hchk(hipMemcpyAsync(g.tot_pin.p, g.rk[0].t64.p, (kJustifySlots + 1) * 8, hipMemcpyDeviceToHost, g.rk[0].s),
-         "D2H");
+  check(g.comm->allreduce_u64(bufs.data(), kJustifySlots + 2 + nred, streams.data(), evs.data()));
+  for (RankDev& r : g.rk) {
+    hchk(hipSetDevice(r.dev), "hipSetDevice");
+    hchk(hipStreamWaitEvent(r.s, r.ev_t64, 0), "wait");
+  }
+  RankDev& r0 = g.rk[0];
+  hchk(hipSetDevice(r0.dev), "hipSetDevice");
+  hchk(hipMemcpyAsync(g.tot_pin.p, r0.xred.p, (kJustifySlots + 2) * 8, hipMemcpyDeviceToHost, r0.s), "D2H");
+  if (!g.ev_totals) hchk(hipEventCreateWithFlags(&g.ev_totals, hipEventDisableTiming), "event");
+  hchk(hipEventRecord(g.ev_totals, r0.s), "event");
+  g.nb_carried = g.nb_pending;
+  g.nb_pending = false;
+}
+
+// sharded: a rank's gather into its xred and the TotalDeposits slot (the pending next-cycle
+// partial, else zero; a transition's epoch puts rank 0's known TotalDeposits there instead)
+static void sharded_gather(Engine& g, RankDev& r, const VoteGatherSlots& q, uint64_t nred) {
+  check(r.xred.alloc(kJustifySlots + 2 + nred));
+  check(r.nbp.alloc(1));
+  if (!r.d_err.p) {
+    check(r.d_err.alloc(1));
+    hchk(hipMemsetAsync(r.d_err.p, 0, 8, r.s), "memset");
+  }
+  hchk(launch_vote_gather(r.totals.p, q, r.d_err.p, r.xred.p, r.s), "vote gather");
+  if (g.nb_pending)
+    hchk(hipMemcpyAsync(r.xred.p + kJustifySlots + 1, r.nbp.p, 8, hipMemcpyDeviceToDevice, r.s), "D2D");
+  else
+    hchk(hipMemsetAsync(r.xred.p + kJustifySlots + 1, 0, 8, r.s), "memset");
+}
+
+static void tally_gather_enqueue(Engine& g, const VoteGatherSlots& q) {
+  check(g.tot_pin.reserve((kJustifySlots + 2) * 8));
+  if (g.world > 1) {  // (a call's final flush: the totals and any pending next-cycle partial)
+    each_rank(g, [&](RankDev& r) { sharded_gather(g, r, q, 0); });
+    sharded_allreduce(g, 0);
+    return;
+  }
+  // one rank: the gather stores straight into the pinned totals (no D2H copy behind it)
+  RankDev& r = g.rk[0];
+  hchk(hipSetDevice(r.dev), "hipSetDevice");
+  if (!r.d_err.p) {
+    check(r.d_err.alloc(1));
+    hchk(hipMemsetAsync(r.d_err.p, 0, 8, r.s), "memset");
+  }
+  void* dp = nullptr;
+  check(g.tot_pin.dev(r.dev, &dp));
+  hchk(launch_vote_gather(r.totals.p, q, r.d_err.p, static_cast<uint64_t*>(dp), r.s), "vote gather");
   if (!g.ev_totals) hchk(hipEventCreateWithFlags(&g.ev_totals, hipEventDisableTiming), "event");
   hchk(hipEventRecord(g.ev_totals, g.rk[0].s), "event");
 }
 
 // After g.ev_totals: raise the panic a tally detected.
+static void tally_gather_wait(Engine& g);
 static void tally_gather_finish(Engine& g) {
+  tally_gather_wait(g);
+  if (g.nb_carried) {  // sharded: the last epoch's next-cycle balance, summed over the ranks
+    g.nb_carried = false;
+    if (g.nb_dst) g.nb_dst->tdep = reinterpret_cast<const uint64_t*>(g.tot_pin.p)[kJustifySlots + 1];
+    g.nb_dst.reset();
+  }
+}
+
+static void tally_gather_wait(Engine& g) {
   PhaseTimer pt(g.prof[kProfTotalsWait]);
   const bool polled = g.gather_poll;  // (a gathering flush records no event: its fallback syncs the stream)
   if (g.gather_poll) {
@@ -1698,7 +1746,7 @@ static void epoch_launch_rest(Engine& g, EpochLaunch& el) {
 // in place (in_place) or from the stage copy; the caller launches (the flush and
 // epoch_launch_rest).
 static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending, EpochLaunch* out = nullptr,
-                          bool in_place = false) {
+                          bool in_place = false, const VoteGatherSlots* q = nullptr) {
   const size_t na = pending.size();
   std::vector<Crosslink>& xl = *C.xl;
   const size_t nrec = xl.size();
@@ -1743,20 +1791,30 @@ static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending
       epoch_launch_rest(g, el);
     return;
   }
+  // sharded (world > 1): the transition's ONE collective.  Every rank's xred gets
+  // its tally gather (sharded_gather: the justification totals, and in the TotalDeposits slot the
+  // previous epoch's pending next-cycle partial -- or, with none pending, rank 0's known
+  // TotalDeposits) and this epoch's count-pass partials {scal, vote, total} (every validator is
+  // active in a sharded chain, so rank == index and no active-list gather is needed); one
+  // all-reduce sums them; then on every range the winners (on the complete tallies) and the
+  // rewards (TotalDeposits read from the reduced slot).  The post-reward next-cycle partial
+  // waits in nbp for the next all-reduce (the next transition's, or the call's final flush),
+  // which hands its sum to the new state (tally_gather_finish).
+  if (!q) throw fail(PZ_EINVAL, "sharded epoch without its transition's gather");
   g.deferred.seq = 0;
-  std::vector<uint64_t*> bufs, nbs;
-  std::vector<hipStream_t> streams;
-  std::vector<hipEvent_t> evs, evn;
+  const uint64_t o_red = kJustifySlots + 2;
   std::vector<EpochArgs> args;
+  const bool carry = g.nb_pending;
   each_rank(g, [&](RankDev& r) {
+    sharded_gather(g, r, *q, nred);
     check(r.e_pack.alloc(total));
     hchk(hipMemcpyAsync(r.e_pack.p, h, total, hipMemcpyHostToDevice, r.s), "H2D epoch");
-    // one rank: the winners sit right after the scalars, so one D2H brings both back
-    const uint64_t wn = g.world == 1 ? (nrec + 1) / 2 : 0;
-    check(r.e_red.alloc(nred + wn + 1));
-    check(r.e_nb.alloc(1));
-    if (g.world > 1) check(r.e_win.alloc(nrec + 1));
-    hchk(hipMemsetAsync(r.e_red.p, 0, kScal * 8, r.s), "memset");
+    if (!carry && r.grank == 0)  // (no partial pending: the known TotalDeposits, summed with the others' 0)
+      hchk(hipMemcpyAsync(r.xred.p + kJustifySlots + 1, r.e_pack.p + o_small + 8, 8, hipMemcpyDeviceToDevice, r.s),
+           "D2D");
+    check(r.e_win.alloc(nrec + 1));
+    uint64_t* red = r.xred.p + o_red;
+    hchk(hipMemsetAsync(red, 0, kScal * 8, r.s), "memset");
     uint8_t* d = r.e_pack.p;
     EpochArgs a;
     std::memset(&a, 0, sizeof a);
@@ -1769,74 +1827,45 @@ static void epoch_enqueue(Engine& g, CState& C, const std::vector<AttP>& pending
     a.start = r.start.p;
     a.end = r.end.p;
     a.dynasty = reinterpret_cast<const uint64_t*>(d + o_small);
-    a.total_deposit = reinterpret_cast<const uint64_t*>(d + o_small) + 1;
+    a.total_deposit = r.xred.p + kJustifySlots + 1;  // (read by the reward pass, after the all-reduce)
     a.natt = (uint32_t)na;
     a.bits = d + o_bits;
     a.boffs = reinterpret_cast<const uint64_t*>(d + o_boffs);
     a.max_inst_bytes = nbits;
     a.pop_rank = (uint32_t)r.grank;
     a.pop_world = (uint32_t)g.world;
-    // sharded: the members inside [lo, hi) with their committee positions (rank 0 also keeps
-    // any member >= nval, whose processCrosslinks panic it raises)
-    a.committee = g.world > 1 ? r.lcomm.p : r.committee.p;
-    a.coffs = g.world > 1 ? r.lcoffs.p : r.coffs.p;
-    a.cpos = g.world > 1 ? r.lcpos.p : nullptr;
+    // the members inside [lo, hi) with their committee positions (rank 0 also keeps any member
+    // >= nval, whose processCrosslinks panic it raises)
+    a.committee = r.lcomm.p;
+    a.coffs = r.lcoffs.p;
+    a.cpos = r.lcpos.p;
     a.att_comm = reinterpret_cast<const uint32_t*>(d + o_comm);
     a.att_shard = reinterpret_cast<const uint32_t*>(d + o_shard);
     a.nrec = (uint32_t)nrec;
     a.rec_dynasty = reinterpret_cast<const uint64_t*>(d + o_rdyn);
-    a.winner = g.world == 1 ? reinterpret_cast<uint32_t*>(r.e_red.p + kScal) : r.e_win.p;
-    a.scal = r.e_red.p;
-    a.vote = r.e_red.p + kScal + wn;
-    a.total = r.e_red.p + kScal + wn + na;
+    a.winner = r.e_win.p;
+    a.scal = red;
+    a.vote = red + kScal;
+    a.total = red + kScal + na;
     a.act_mask = r.e_mask.p;
     a.blk_cnt = r.e_blk.p;
     a.act_list = r.e_list.p;
     hchk(launch_epoch_count(a, true, true, true, r.s), "epoch count");
-    if (g.world == 1) {
-      hchk(launch_epoch_mid(a, a.nrec > 0 && na > 0, true, r.s), "epoch mid");
-      hchk(launch_epoch_reward(a, r.s), "epoch reward");
-    }
     args.push_back(a);
-    bufs.push_back(r.e_red.p);
-    nbs.push_back(r.e_nb.p);
-    streams.push_back(r.s);
-    if (!r.ev_red) hchk(hipEventCreateWithFlags(&r.ev_red, hipEventDisableTiming), "event");
-    if (!r.ev_nb) hchk(hipEventCreateWithFlags(&r.ev_nb, hipEventDisableTiming), "event");
-    evs.push_back(r.ev_red);
-    evn.push_back(r.ev_nb);
   });
-  if (g.world > 1) {
-    // the partial crosslink tallies, bit counts and flags of the ranges summed (the step of
-    // pz_epoch_state, epoch_state.hip, for one instance; every validator is active in a
-    // sharded chain, so rank == index and no active-list gather is needed), then winners and
-    // rewards on each range, then the partial next-cycle balances summed
-    check(g.comm->allreduce_u64(bufs.data(), nred, streams.data(), evs.data()));
-    for (size_t i = 0; i < g.rk.size(); ++i) {
-      RankDev& r = g.rk[i];
-      hchk(hipSetDevice(r.dev), "hipSetDevice");
-      hchk(hipStreamWaitEvent(r.s, r.ev_red, 0), "wait");
-      hchk(launch_epoch_mid(args[i], args[i].nrec > 0 && na > 0, false, r.s), "epoch mid");
-      hchk(launch_epoch_reward(args[i], r.s), "epoch reward");
-      hchk(hipMemcpyAsync(r.e_nb.p, r.e_red.p + kNextBal, 8, hipMemcpyDeviceToDevice, r.s), "D2D");
-    }
-    check(g.comm->allreduce_u64(nbs.data(), 1, streams.data(), evn.data()));
-    for (RankDev& r : g.rk) {
-      hchk(hipSetDevice(r.dev), "hipSetDevice");
-      hchk(hipStreamWaitEvent(r.s, r.ev_nb, 0), "wait");
-      hchk(hipMemcpyAsync(r.e_red.p + kNextBal, r.e_nb.p, 8, hipMemcpyDeviceToDevice, r.s), "D2D");
-    }
+  sharded_allreduce(g, nred);
+  for (size_t i = 0; i < g.rk.size(); ++i) {
+    RankDev& r = g.rk[i];
+    hchk(hipSetDevice(r.dev), "hipSetDevice");
+    hchk(launch_epoch_mid(args[i], args[i].nrec > 0 && na > 0, false, r.s), "epoch mid");
+    hchk(launch_epoch_reward(args[i], r.s), "epoch reward");
+    hchk(hipMemcpyAsync(r.nbp.p, args[i].scal + kNextBal, 8, hipMemcpyDeviceToDevice, r.s), "D2D");
   }
   RankDev& r0 = g.rk[0];
   hchk(hipSetDevice(r0.dev), "hipSetDevice");
   check(g.e_pin_out.reserve(kScal * 8 + nrec * 4 + 16));
-  if (g.world == 1) {
-    hchk(hipMemcpyAsync(g.e_pin_out.p, r0.e_red.p, kScal * 8 + nrec * 4, hipMemcpyDeviceToHost, r0.s), "D2H");
-  } else {
-    hchk(hipMemcpyAsync(g.e_pin_out.p, r0.e_red.p, kScal * 8, hipMemcpyDeviceToHost, r0.s), "D2H");
-    if (nrec)
-      hchk(hipMemcpyAsync(g.e_pin_out.p + kScal * 8, r0.e_win.p, nrec * 4, hipMemcpyDeviceToHost, r0.s), "D2H");
-  }
+  hchk(hipMemcpyAsync(g.e_pin_out.p, args[0].scal, kScal * 8, hipMemcpyDeviceToHost, r0.s), "D2H");
+  if (nrec) hchk(hipMemcpyAsync(g.e_pin_out.p + kScal * 8, r0.e_win.p, nrec * 4, hipMemcpyDeviceToHost, r0.s), "D2H");
   each_rank(g, [&](RankDev& r) {
     if (!r.ev_epoch) hchk(hipEventCreateWithFlags(&r.ev_epoch, hipEventDisableTiming), "event");
     hchk(hipEventRecord(r.ev_epoch, r.s), "event");
@@ -1897,7 +1926,7 @@ static void epoch_collect(Engine& g) {
     }
   }
   if (scal[kApplied]) g.val_enc_valid = false;
-  D.dst->tdep = scal[kNextBal];
+  if (g.world == 1) D.dst->tdep = scal[kNextBal];  // (sharded: a partial per rank, summed by the next all-reduce)
   D.src.reset();
   D.dst.reset();
 }
@@ -1938,12 +1967,12 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   uint64_t streak = C->streak, justified = C->jslot, finalized = C->fslot;
   const uint64_t lsr = C->lsr;
   std::vector<uint64_t> tot(kCycle, 0);
-  if (!gathered) tally_gather_enqueue(g, q);
   if (one) {
+    if (!gathered) tally_gather_enqueue(g, q);
     if (!el.ready) epoch_enqueue(g, *C, A->pending, &el);  // (nothing was flushed)
     epoch_launch_rest(g, el);
-  } else {
-    epoch_enqueue(g, *C, A->pending);
+  } else {  // the gather, the epoch and ONE all-reduce
+    epoch_enqueue(g, *C, A->pending, nullptr, false, &q);
   }
   tl[2] = mono_ns();
   auto nc = std::make_shared<CState>();
@@ -1961,7 +1990,11 @@ static void state_recalc(Engine& g, const CP& C, const AP& A, uint64_t block_slo
   na->tail = A->tail;  // (the window is at most 2 * kCycle long)
   na->len = A->len;
   na->cache_nil = A->cache_nil;
-  tally_gather_finish(g);
+  tally_gather_finish(g);  // (sharded: C's TotalDeposits, if its epoch's partials were pending, set here)
+  if (!one) {  // this epoch's next-cycle partials now pending, for the new state
+    g.nb_pending = true;
+    g.nb_dst = nc;
+  }
   tl[3] = mono_ns();
   if (g.tl.size() < (1u << 16)) g.tl.push_back(tl);
   std::memcpy(tot.data(), g.tot_pin.p, kCycle * 8);
@@ -3255,7 +3288,7 @@ static void destroy_chain(pz_chain* c) {
   for (RankDev& r : g.rk) {
     (void)hipSetDevice(r.dev);
     if (r.s) (void)hipStreamSynchronize(r.s);
-    for (hipEvent_t e : {r.q_ev, r.vq_ev[0], r.vq_ev[1], r.ev_epoch, r.ev_red, r.ev_nb, r.ev_t64})
+    for (hipEvent_t e : {r.q_ev, r.vq_ev[0], r.vq_ev[1], r.ev_epoch, r.ev_t64})
       if (e) (void)hipEventDestroy(e);
     streams.push_back({r.dev, r.s});
   }

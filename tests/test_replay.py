@@ -518,6 +518,34 @@ def test_gpu_sharded_chain_rejections_vs_oracle(world):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
+def test_gpu_sharded_chain_one_collective_per_transition(world):
+    """The sharded transition's single collective: the justification totals, the
+    epoch's partial sums and the previous epoch's next-cycle partial ride in ONE all-reduce, and
+    the call's final flush carries the last next-cycle partial -- transitions + 1 collectives per
+    call, two calls in a row (the pending partial crossing the call boundary), each matching
+    the golden roots."""
+    from prysm_amd.blockchain import BeaconChain
+    from prysm_amd.native import Comm
+    g = golden()
+    blocks = synth.chain_blocks(g["nval"], g["nblocks"], seed=g["seed"])
+    comm = Comm.loopback(world)
+    ch = BeaconChain(g["nval"], comm=comm)
+    comm.set_timing(True)
+    comm.collective_time()
+    recs = ch.process_blocks(blocks[:70])
+    _, n1 = comm.collective_time()
+    recs += ch.process_blocks(blocks[70:])
+    _, n2 = comm.collective_time()
+    comm.set_timing(False)
+    t1 = sum(r["transition"] for r in recs[:70])
+    t2 = sum(r["transition"] for r in recs[70:])
+    assert t1 + t2 == 2
+    assert (n1, n2) == (t1 + 1, t2 + 1), (n1, n2, t1, t2)
+    _compare(recs, ch.roots(), g)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
 def test_gpu_sharded_chain_reward_panic(world):
     from prysm_amd.blockchain import BeaconChain, ChainPanic
     from prysm_amd.native import Comm

@@ -39,8 +39,10 @@ def main():
     print("attcheck: %d attestations  %.4f ms  %.1f G/s  result digest %d" % (natt, ms, natt / ms / 1e6, digest),
           flush=True)
     dll = _lib.lib.dll
-    if hasattr(dll, "pz_debug_set_attcheck_variant"):  # same-process A/B (1: default-policy loads, 2: nt stores)
-        for v in [int(x) for x in os.environ.get("VARIANTS", "0,2,0,2,0,2").split(",")]:
+    if hasattr(dll, "pz_debug_set_attcheck_variant"):  # same-process A/B (PZ_PROBE_LIB=build/ab/...)
+        # 0 the product (persistent blocks, the committee table in LDS, 2 blocks per CU), 1 round 5's
+        # x2 kernel (the walk in global memory), 2 / 3 the product at 3 / 1 blocks per CU
+        for v in [int(x) for x in os.environ.get("VARIANTS", "0,1,2,3,0,1").split(",")]:
             dll.pz_debug_set_attcheck_variant(v)
             ms = timed()
             d = int(st.sum().item()) * 31 + int(cm.sum().item()) * 7 + int(ps.sum().item())
