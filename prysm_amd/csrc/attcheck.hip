@@ -148,7 +148,7 @@ extern "C" __global__ void __launch_bounds__(kThreads) pz_att_check_x2_kernel(pz
 // the walk is LDS lookups (~100 cycles each) under the next pair's HBM round trip.  A table too
 // large for the LDS budget, or with a shard id or committee size past 32 bits, or malformed
 // offsets, keeps the global walk (the same check_one) in every block.
-constexpr int kPThreads = 512, kPBlocksPerCU = 2;
+constexpr int kPThreads = 512, kPBlocksPerCU = 3;  // (2: 47.7 us, 3: 46.7, 1: 52.3; profiles/r06/attcheck_probe_r6g.txt)
 constexpr uint32_t kPTabWords = 12288;  // 48 KiB
 
 struct PairLd {
@@ -328,7 +328,7 @@ hipError_t launch_att_check(const pz_att_check_batch& b, hipStream_t s) {
     const uint64_t npairs = b.natt / 2;
     uint64_t per_cu = kPBlocksPerCU;
 #ifdef PZ_AB_BUILD
-    if (g_attcheck_variant == 2) per_cu = 3;  // (A/B: blocks per CU)
+    if (g_attcheck_variant == 2) per_cu = 2;  // (A/B: blocks per CU)
     if (g_attcheck_variant == 3) per_cu = 1;
 #endif
     const uint64_t nb = std::max<uint64_t>(1, std::min<uint64_t>((npairs + kPThreads - 1) / kPThreads,

@@ -40,8 +40,8 @@ def main():
           flush=True)
     dll = _lib.lib.dll
     if hasattr(dll, "pz_debug_set_attcheck_variant"):  # same-process A/B (PZ_PROBE_LIB=build/ab/...)
-        # 0 the product (persistent blocks, the committee table in LDS, 2 blocks per CU), 1 round 5's
-        # x2 kernel (the walk in global memory), 2 / 3 the product at 3 / 1 blocks per CU
+        # 0 the product (persistent blocks, the committee table in LDS, 3 blocks per CU), 1 round 5's
+        # x2 kernel (the walk in global memory), 2 / 3 the product at 2 / 1 blocks per CU
         for v in [int(x) for x in os.environ.get("VARIANTS", "0,1,2,3,0,1").split(",")]:
             dll.pz_debug_set_attcheck_variant(v)
             ms = timed()
