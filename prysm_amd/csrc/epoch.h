@@ -164,7 +164,6 @@ struct WinArgs {
   // R <= kWinKargR: rdesc's entries again, in the kernel arguments, so a block's first piece
   // descriptors depend on nothing but the kernarg segment (one dependent round trip less)
   uint4 rdk[kWinKargR];
-  uint32_t rpos[kWinKargR];  // R <= kWinKargR: each range's first position (the same in every instance)
   // [B][ptot][2] per instance and piece (<= 256 positions of one committee, from its first
   // position rounded down to 4): {first position, positions, committee - cr0, kind (0 no
   // attestation, 1 one, 2 several)}, {its first catt index, the bit of the first position in
@@ -226,16 +225,7 @@ constexpr uint32_t kMultiMaxAtt = 512;
 // One instance, one rank, in ONE launch (f.one): every block counts the bitfields and checks
 // their lengths itself (no pre pass), streams its committee pieces as `fused` does, and the
 // last block to finish (an arrival ticket) forms the winners in LDS (no mid pass).
-// The single launch's piece positions in the kernel arguments (round 6): ws[k] = item k's first
-// global position, ws[nitems] = the last one's end (the pieces are contiguous), so the stream's
-// loads go out right after the kernel-argument load instead of behind the item table's round
-// trip.  n = 0: more than kOnePosMax pieces, the positions come from the item table.
-constexpr uint32_t kOnePosMax = 640;
-struct OnePos {
-  uint32_t n;
-  uint32_t ws[kOnePosMax + 1];
-};
-hipError_t launch_epoch_one(const EpochArgs& a, const FusedArgs& f, hipStream_t s, const OnePos* pos = nullptr);
+hipError_t launch_epoch_one(const EpochArgs& a, const FusedArgs& f, hipStream_t s);
 bool epoch_one_enabled(const FusedArgs& f);  // f.one
 bool fused_ok(const EpochArgs& a);  // 16-B vector path available (16-B aligned validator rows)
 

@@ -853,9 +853,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
                                            const uint4* __restrict__ items_ro,
                                            const FusedCommittee* __restrict__ cinfo_ro,
                                            const uint32_t* __restrict__ catt_offs_ro,
-                                           const uint32_t* __restrict__ catt_ro, const OnePos* opos = nullptr) {
-  // MODE & 2097152 (single launch): the piece's positions from the kernel arguments (OnePos)
-  constexpr bool KPOS = (MODE & 2097152) != 0;
+                                           const uint32_t* __restrict__ catt_ro) {
   // per wave: {attestation of its committee (single-attestation committees), total, vote, next sum, nomatch}
   __shared__ uint64_t xt[kFusedWaves], xv[kFusedWaves], xs[kFusedWaves], xn[kFusedWaves];
   __shared__ uint32_t xg[kFusedWaves];
@@ -1104,11 +1102,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     const uint4 it = (MODE & 64) ? make_uint4((uint32_t)(a.val_offset + ((item * 256) % (a.nval & ~255ull ? a.nval & ~255ull : 256))),
                                               have ? 256u : 0u, 0, (uint32_t)a.val_offset)
                      : have ? items_ro[item] : make_uint4((uint32_t)a.val_offset, 0, 0, (uint32_t)a.val_offset);
-    // (KPOS: the stream's addresses from the kernel arguments; the item's committee fields still
-    // come from the table, needed only at the tallies)
-    const uint64_t ws = KPOS ? (have ? (uint64_t)opos->ws[item] : a.val_offset) : it.x;
-    const uint64_t we = KPOS ? (have ? (uint64_t)opos->ws[item + 1] : a.val_offset) : (uint64_t)it.x + it.y;
-    const uint64_t cb = it.w;
+    const uint64_t ws = it.x, we = (uint64_t)it.x + it.y, cb = it.w;
     FusedCommittee ci;  // loaded beside the item: no dependent hop before the stream loads
     {
       const uint4 ic = have ? f.items_ci[inst * f.nitems + item] : make_uint4(0, 0, 0, kNoAtt);
@@ -1432,23 +1426,6 @@ pz_epoch_one_se16_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ 
                          const uint32_t* __restrict__ catt_ro) {
   fused_body<512 + 1024 + 16384>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
 }
-// the product's single launch with the piece positions in the kernel arguments (OnePos)
-extern "C" __global__ void __launch_bounds__(64 * kFusedWaves)
-pz_epoch_one_se16_kpos_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ boffs_ro,
-                              const uint64_t* __restrict__ tdep_ro, const uint4* __restrict__ items_ro,
-                              const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,
-                              const uint32_t* __restrict__ catt_ro, OnePos pos) {
-  fused_body<512 + 1024 + 16384 + 2097152>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro,
-                                           &pos);
-}
-#ifdef PZ_AB_BUILD
-static int g_one_variant = 0;  // 1: the positions from the item table (round 5's single launch)
-extern "C" int pz_debug_set_one_variant(int v) {
-  const int old = g_one_variant;
-  g_one_variant = v;
-  return old;
-}
-#endif
 
 // ---- launchers ---------------------------------------------------------------------------
 static bool vec_ok(const EpochArgs& a) {
@@ -1549,16 +1526,9 @@ bool fused_ok(const EpochArgs& a) {
 
 bool epoch_one_enabled(const FusedArgs& f) { return f.one != 0; }
 
-hipError_t launch_epoch_one(const EpochArgs& a, const FusedArgs& f, hipStream_t s, const OnePos* pos) {
+hipError_t launch_epoch_one(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
   const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
-  bool kpos = pos && pos->n && f.se16;
-#ifdef PZ_AB_BUILD
-  if (g_one_variant == 1) kpos = false;
-#endif
-  if (kpos)
-    hipLaunchKernelGGL(pz_epoch_one_se16_kpos_kernel, dim3(1, (uint32_t)groups), dim3(64 * kFusedWaves), 0, s, a, f,
-                       a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt, *pos);
-  else if (f.se16)
+  if (f.se16)
     hipLaunchKernelGGL(pz_epoch_one_se16_kernel, dim3(1, (uint32_t)groups), dim3(64 * kFusedWaves), 0, s, a, f,
                        a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt);
   else if (f.se)

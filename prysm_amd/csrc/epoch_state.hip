@@ -45,7 +45,6 @@ struct Part {
   hipEvent_t ev_red = nullptr, ev_gather = nullptr, ev_nb = nullptr;
   EpochArgs a;
   FusedArgs f;                            // one-pass step, one instance (pz_epoch_one_kernel)
-  OnePos opos{};                          // its pieces' positions for the kernel arguments (n = 0: none)
   bool window = false;                    // one-pass step, the window pass (epoch_window.hip)
   WinArgs w;
 };
@@ -248,7 +247,7 @@ int step_world1(pz_epoch_state* st) {
     for (uint32_t p = 0; p < st->nparts; ++p) {
       EpochArgs& a = s.part[p].a;
       if (st->fused && epoch_one_enabled(s.part[p].f)) {  // one instance: the single-launch step
-        hipError_t e = launch_epoch_one(a, s.part[p].f, s.s, &s.part[p].opos);
+        hipError_t e = launch_epoch_one(a, s.part[p].f, s.s);
         if (e != hipSuccess) return hip_fail(e, "epoch step (single launch)");
         continue;
       }
@@ -707,10 +706,7 @@ static int plan_window(pz_epoch_state* st, const pz_epoch_host* h, Shard& s, Par
     w.pacc_next = d_pacc + Bp;
   }
   w.rdesc = d_rdesc;
-  for (uint32_t r = 0; r < R && r < kWinKargR; ++r) {
-    w.rdk[r] = rdesc[r];
-    w.rpos[r] = rdesc[r].w ? pieces[rdesc[r].z].x & ~3u : 0;
-  }
+  for (uint32_t r = 0; r < R && r < kWinKargR; ++r) w.rdk[r] = rdesc[r];
   w.pinfo = d_pinfo;
   w.ptot = ptot;
   w.rk = d_rk;
@@ -1014,14 +1010,6 @@ int pz_epoch_state_new_opts(pz_comm* comm, int device, const pz_epoch_host* h, c
         if (one) {
           q.f.one = 1;
           q.f.win_in_wave = 1;
-          q.opos.n = 0;
-          bool contiguous = nitems <= kOnePosMax;
-          for (uint64_t k = 0; k + 1 < nitems && contiguous; ++k) contiguous = items[k].x + items[k].y == items[k + 1].x;
-          if (contiguous && nitems) {
-            for (uint64_t k = 0; k < nitems; ++k) q.opos.ws[k] = items[k].x;
-            q.opos.ws[nitems] = items[nitems - 1].x + items[nitems - 1].y;
-            q.opos.n = (uint32_t)nitems;
-          }
           std::vector<uint32_t> cs(st->natt);
           for (uint64_t g = 0; g < st->natt; ++g) {
             const uint32_t c = h->att_comm[i0 * st->natt + g];

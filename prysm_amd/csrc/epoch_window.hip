@@ -237,20 +237,6 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
   uint4 dv = desc(0);
   // NP: round 1's descriptors go out with round 0's (both depend on the kernel arguments alone)
   const uint4 dv1 = NP ? desc(1) : make_uint4(0, 0, 0, 0);
-  // NP (u32 offsets, 16-bit bounds): the first two rounds' balance and bound lines prefetched
-  // into L2 from the range's first position (kernel arguments), one 4-B load per thread, 128 B
-  // apart -- issued a round trip before the pieces' own loads, which then meet them in L2
-  // (A/B bit 1 << 22: no prefetch)
-  constexpr bool PF = NP && B32 && SEW == 16 && !(AB & (1 << 22));
-  uint32_t pfv = 0;
-  if (PF) {  // (no branch around the load: the waits after it stay exact; past kWinKargR ranges it reads a
-             // harmless row start)
-    const uint64_t vr = inst * w.vstride;
-    const uint32_t k = (uint32_t)tid & 511;  // (threads 0-511: balances, 512-1023: bounds)
-    const uint64_t pos = std::min<uint64_t>((uint64_t)w.rpos[r & (kWinKargR - 1)] + 32ull * k, w.vstride - 1);
-    const uint32_t* pcol = tid < 512 ? w.bal32 : w.se16;
-    pfv = pcol[vr + pos];
-  }
   // (NP: nothing is scheduled above this point from below it, so the bitfield offsets' scalar
   // loads -- and their wait -- come after the descriptors' loads have gone out)
   if (NP) __builtin_amdgcn_sched_barrier(0);
@@ -441,7 +427,6 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
     // pieces'), then the last bitfield's DMA, the tallies zeroed, and one barrier for the wave
     // sums, the DMA and the zeroed tallies; every thread then has the block's count (R = 1: the
     // instance's -- no meeting, no speculation; R > 1: its share, published by one atomic)
-    if (PF) asm volatile("" ::"v"(pfv));  // (the prefetch lands with the count's loads, before the barrier)
     if (!(AB & 2)) {
       cnt_take(s0, ncn, ngn, 0, cl0);
       for (uint64_t it = 1, nit = cnt_iters(ncn, ngn); it < nit; ++it) {
@@ -947,7 +932,7 @@ PZ_WINDOW_ABL(0, 2) PZ_WINDOW_ABL(0, 3) PZ_WINDOW_ABL(0, 4)
 PZ_WINDOW_ABL(1, 2) PZ_WINDOW_ABL(2, 2) PZ_WINDOW_ABL(4, 2) PZ_WINDOW_ABL(7, 2) PZ_WINDOW_ABL(16, 2)
 PZ_WINDOW_ABL(48, 2) PZ_WINDOW_ABL(64, 2) PZ_WINDOW_ABL(128, 2) PZ_WINDOW_ABL(144, 2) PZ_WINDOW_ABL(4096, 2)
 PZ_WINDOW_ABL(8192, 2) PZ_WINDOW_ABL(32, 2) PZ_WINDOW_ABL(65536, 2) PZ_WINDOW_ABL(131072, 2)
-PZ_WINDOW_ABL(1048576, 2) PZ_WINDOW_ABL(2097152, 2) PZ_WINDOW_ABL(4194304, 2)
+PZ_WINDOW_ABL(1048576, 2) PZ_WINDOW_ABL(2097152, 2)
 // the product form with phase stamps (tools/epoch_trace.py)
 extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_kernel(EpochArgs a, WinArgs w) {
   window_body<true, 16, true, 0, kWinDepth16, true, true>(a, w);
@@ -1032,7 +1017,6 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
       case 1 << 18: k = (const void*)pz_epoch_window_np0_kernel; break;  // (round 5's prologue)
       case 1 << 20: k = (const void*)pz_epoch_window_abl1048576_d2_kernel; break;  // (round 5's cached balances)
       case 1 << 21: k = (const void*)pz_epoch_window_abl2097152_d2_kernel; break;  // (the DMA before the first wait)
-      case 1 << 22: k = (const void*)pz_epoch_window_abl4194304_d2_kernel; break;  // (no L2 prefetch of the first rounds)
       default: return hipErrorInvalidValue;
     }
   }
