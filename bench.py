@@ -889,8 +889,8 @@ def attcheck_leg(args, torch, dist, dev, rank, world):
                                "5%% failing a check" % natt, "parallelism": "attestation-shard x%d" % world},
         "roofline": {"bound": "hbm", "achieved": alg / (step_ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": alg / (step_ms * 1e-3) / HBM_PEAK,
-                     "traffic": pmc_traffic(["pz_att_check_x2_kernel"]), "traffic_source": PMC_SUMMARY,
-                     "kernel": "pz_att_check_x2_kernel", "step_device_ms": step_ms,
+                     "traffic": pmc_traffic(["pz_att_check_p_kernel"]), "traffic_source": PMC_SUMMARY,
+                     "kernel": "pz_att_check_p_kernel", "step_device_ms": step_ms,
                      "algorithmic_bytes_per_launch": alg},
     }
     from oracle import cport
@@ -1218,7 +1218,7 @@ def shuffle_leg(args):
     return out
 
 
-PMC_DIRS = (os.path.join("profiles", "r05"),)  # (this round's tree only: kernel names change between rounds)
+PMC_DIRS = (os.path.join("profiles", "r06"),)  # (this round's tree only: kernel names change between rounds)
 PMC_SUMMARY = os.path.join(PMC_DIRS[0], "pmc_main.json")
 
 
