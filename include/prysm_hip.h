@@ -494,7 +494,11 @@ typedef struct pz_epoch_host {
   const uint32_t* att_comm;        /* [B*natt] */
   const uint32_t* att_shard;       /* [B*natt] */
   uint32_t nrec;                   /* crosslink records per instance */
-  const uint64_t* rec_dynasty;     /* [B][nrec] */
+  const uint64_t* rec_dynasty;     /* [B][nrec].  dynasty, rec_dynasty, the committees and the
+                                      attestations are copied by pz_epoch_state_new and fixed for
+                                      the state's lifetime (no call updates them; the one-pass
+                                      step's plan tables are built from them once).  A caller
+                                      whose records or dynasty change makes a new state. */
   uint32_t layout;                 /* PZ_LAYOUT_AUTO: committee order when every validator is
                                       active and the committees partition the set, else index
                                       order; PZ_LAYOUT_INDEX: always index order;
