@@ -186,7 +186,8 @@ size_t window_lds_bytes(const WinArgs& w) { return 8ull * ((size_t)w.lds_maxc + 
 // narrow offsets (exact), 8192 no speculation: the whole count before the loop (exact), 32
 // (alone) the speculating blocks' post-loop meeting skipped, the fallback count every time (exact);
 // 16384 the product's L2 form (the reward bits looked up in the last bitfield in global memory,
-// no LDS copy; exact).
+// no LDS copy; exact), 1 << 23 the next round's loads issued at the waves' base priority (round
+// 6's first form; exact).
 template <bool B32, int SEW, bool LLB, int AB = 0, int D = kWinDepth, bool TR = false, bool NA = false, bool NP = true,
           int KD = 0>
 __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w) {
@@ -758,8 +759,13 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
         for (int i = 0; i < 4; ++i) sum += (v[i] && act[i]) ? b[i] : 0;
       }
       // slot j's piece of the next round (past the last round: a dummy, loaded and unused)
+      // (at raised priority: the SIMD's arbiter issues the wave's loads ahead of the other
+      // waves' ALU work, so they go out sooner; 54.5 -> 54.0 / 58.2 -> 57.7 us cold,
+      // profiles/r06/epoch_cold_prio_r6k.txt)
       dq[j] = piece(dnx, j, t + 1);
+      if (!(AB & (1 << 23))) __builtin_amdgcn_s_setprio(2);
       win_load<B32, SEW, NTB>(col, dq[j], lane, q[j]);
+      if (!(AB & (1 << 23))) __builtin_amdgcn_s_setprio(0);
     }
   }
   // the epilogue's first kEpiPf attestations per thread: their words now, ahead of the meeting
@@ -932,7 +938,7 @@ PZ_WINDOW_ABL(0, 2) PZ_WINDOW_ABL(0, 3) PZ_WINDOW_ABL(0, 4)
 PZ_WINDOW_ABL(1, 2) PZ_WINDOW_ABL(2, 2) PZ_WINDOW_ABL(4, 2) PZ_WINDOW_ABL(7, 2) PZ_WINDOW_ABL(16, 2)
 PZ_WINDOW_ABL(48, 2) PZ_WINDOW_ABL(64, 2) PZ_WINDOW_ABL(128, 2) PZ_WINDOW_ABL(144, 2) PZ_WINDOW_ABL(4096, 2)
 PZ_WINDOW_ABL(8192, 2) PZ_WINDOW_ABL(32, 2) PZ_WINDOW_ABL(65536, 2) PZ_WINDOW_ABL(131072, 2)
-PZ_WINDOW_ABL(1048576, 2) PZ_WINDOW_ABL(2097152, 2)
+PZ_WINDOW_ABL(1048576, 2) PZ_WINDOW_ABL(2097152, 2) PZ_WINDOW_ABL(8388608, 2)
 // the product form with phase stamps (tools/epoch_trace.py)
 extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_kernel(EpochArgs a, WinArgs w) {
   window_body<true, 16, true, 0, kWinDepth16, true, true>(a, w);
@@ -1017,6 +1023,7 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
       case 1 << 18: k = (const void*)pz_epoch_window_np0_kernel; break;  // (round 5's prologue)
       case 1 << 20: k = (const void*)pz_epoch_window_abl1048576_d2_kernel; break;  // (round 5's cached balances)
       case 1 << 21: k = (const void*)pz_epoch_window_abl2097152_d2_kernel; break;  // (the DMA before the first wait)
+      case 1 << 23: k = (const void*)pz_epoch_window_abl8388608_d2_kernel; break;  // (loads at base priority)
       default: return hipErrorInvalidValue;
     }
   }
