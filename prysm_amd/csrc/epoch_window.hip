@@ -762,6 +762,8 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
       // (at raised priority: the SIMD's arbiter issues the wave's loads ahead of the other
       // waves' ALU work, so they go out sooner; 54.5 -> 54.0 / 58.2 -> 57.7 us cold,
       // profiles/r06/epoch_cold_prio_r6k.txt)
+      // (measured and dropped: the raised priority from the descriptor's readlanes on, and
+      // level 3, both level or slower, profiles/r06/prio_variants_dropped_r6m.txt)
       dq[j] = piece(dnx, j, t + 1);
       if (!(AB & (1 << 23))) __builtin_amdgcn_s_setprio(2);
       win_load<B32, SEW, NTB>(col, dq[j], lane, q[j]);

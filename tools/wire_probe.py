@@ -10,6 +10,9 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from prysm_amd import _lib  # noqa: E402
 
+if os.environ.get("PZ_PROBE_LIB"):  # A/B against another build of the library
+    _lib.library_path = os.environ["PZ_PROBE_LIB"]
+
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
