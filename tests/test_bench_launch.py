@@ -73,3 +73,27 @@ def test_bench_single_process_one_device():
     assert line["epoch"]["config"]["layout"] == "committee order, one-pass step"
     assert line["hash"]["value"] > 0 and line["epoch"]["value"] > 0
     assert line["replay_one_chain"]["transitions"] == 2
+
+
+def test_bench_traffic_summaries_present_and_shipped():
+    """Every kernel whose counted HBM traffic the bench line quotes has it in the committed PMC
+    summaries of this round (a kernel renamed since the counter passes reads None), and those
+    summaries are not excluded from the tree gpurun ships to the GPU box (.gpurunignore)."""
+    import fnmatch
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    quoted = [([bench.HASH_KERNEL], "main"), (["pz_wire_val_kernel"], "main"), (["pz_att_check_p_kernel"], "main"),
+              (["pz_wire_att_size_kernel", "pz_wire_att_write_kernel"], "main")]
+    quoted += [(["pz_epoch_*"], w) for w in ("epoch65k", "epoch1m", "epoch65k_cold", "epoch1m_cold")]
+    for kernels, workload in quoted:
+        assert bench.pmc_traffic(kernels, workload), (kernels, workload)
+    with open(os.path.join(ROOT, ".gpurunignore")) as f:
+        pats = [ln.strip() for ln in f if ln.strip()]
+    for workload in {w for _, w in quoted}:
+        rel = "./" + bench.pmc_summary_path(workload).replace(os.sep, "/")
+        for pat in pats:
+            parts = rel.split("/")
+            prefixes = ["/".join(parts[:i]) for i in range(2, len(parts) + 1)]
+            assert not any(fnmatch.fnmatch(p, pat) or fnmatch.fnmatch(p[2:], pat) for p in prefixes), (rel, pat)
