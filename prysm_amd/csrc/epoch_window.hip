@@ -902,6 +902,10 @@ __device__ __forceinline__ void window_body(const EpochArgs& a, const WinArgs& w
 // balances as u32 offsets (the narrow tallies or not) / u64; {start, end} at 16 / 32 / 64 bits;
 // the last bitfield in LDS or not
 PZ_WINDOW_KERNEL(pz_epoch_window_b32n_s16_kernel, true, 16, true, true)
+// (one piece in flight per wave: the product form when an instance has several ranges, R > 1)
+extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_b32n_s16_d1_kernel(EpochArgs a, WinArgs w) {
+  window_body<true, 16, true, 0, 1, false, true>(a, w);
+}
 // the product form with the straight-line last-bitfield copy (WinArgs.dma_k, kWinDmaK)
 #define PZ_WINDOW_KERNEL_K(K)                                                                                 \
   extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_b32n_s16_k##K##_kernel(EpochArgs a, \
@@ -936,7 +940,7 @@ PZ_WINDOW_KERNEL(pz_epoch_window_b64_s64_g_kernel, false, 64, false, false)
                                                                                               WinArgs w) {  \
     window_body<true, 16, true, X, D, false, true, !((X) & 16)>(a, w);                                     \
   }
-PZ_WINDOW_ABL(0, 2) PZ_WINDOW_ABL(0, 3) PZ_WINDOW_ABL(0, 4)
+PZ_WINDOW_ABL(0, 1) PZ_WINDOW_ABL(0, 2) PZ_WINDOW_ABL(0, 3) PZ_WINDOW_ABL(0, 4)
 PZ_WINDOW_ABL(1, 2) PZ_WINDOW_ABL(2, 2) PZ_WINDOW_ABL(4, 2) PZ_WINDOW_ABL(7, 2) PZ_WINDOW_ABL(16, 2)
 PZ_WINDOW_ABL(48, 2) PZ_WINDOW_ABL(64, 2) PZ_WINDOW_ABL(128, 2) PZ_WINDOW_ABL(144, 2) PZ_WINDOW_ABL(4096, 2)
 PZ_WINDOW_ABL(8192, 2) PZ_WINDOW_ABL(32, 2) PZ_WINDOW_ABL(65536, 2) PZ_WINDOW_ABL(131072, 2)
@@ -973,9 +977,20 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
   const void* k = nullptr;
 #define PZ_PICK(B, S)                                                                            \
   k = llb ? (const void*)pz_epoch_window_##B##_s##S##_kernel : (const void*)pz_epoch_window_##B##_s##S##_g_kernel
+  // One piece in flight per wave, and the last bitfield's copy after the count's take, when an
+  // instance has several ranges (R > 1): 1M x 16 cold 58.0 -> 55.8 us; at R = 1 two pieces and
+  // the straight-line copy first are faster, 54.3 against 57.8 (profiles/r06/
+  // epoch_cold_depth1_r6s.txt; with the straight-line copy one piece gains only 58.0 -> 56.8,
+  // epoch_cold_depth1_kd_r6t.txt)
+  bool d1 = w.R > 1;
+#ifdef PZ_AB_BUILD
+  if (g_window_ablation == (1 << 22)) d1 = false;  // (A/B: the R = 1 form at R > 1 too)
+#endif
   if (b32 && w.narrow) {
     if (sew == 16) PZ_PICK(b32n, 16);
-    if (sew == 16 && llb && w.dma_k) {  // (the straight-line copy: WinArgs.dma_k)
+    if (sew == 16 && llb && d1) {
+      k = (const void*)pz_epoch_window_b32n_s16_d1_kernel;
+    } else if (sew == 16 && llb && w.dma_k) {  // (the straight-line copy: WinArgs.dma_k)
       switch (w.dma_k) {
         case 1: k = (const void*)pz_epoch_window_b32n_s16_k1_kernel; break;
         case 2: k = (const void*)pz_epoch_window_b32n_s16_k2_kernel; break;
@@ -1004,6 +1019,7 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
                                        : (const void*)pz_epoch_window_trace_kernel;
   if (g_window_ablation && !g_window_trace && b32 && w.narrow && sew == 16 && llb) {
     switch (g_window_ablation) {  // ablation bits | prefetch depth << 8
+      case 1 << 8: k = (const void*)pz_epoch_window_abl0_d1_kernel; break;
       case 2 << 8: k = (const void*)pz_epoch_window_abl0_d2_kernel; break;
       case 3 << 8: k = (const void*)pz_epoch_window_abl0_d3_kernel; break;
       case 4 << 8: k = (const void*)pz_epoch_window_abl0_d4_kernel; break;
@@ -1026,6 +1042,7 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
       case 1 << 20: k = (const void*)pz_epoch_window_abl1048576_d2_kernel; break;  // (round 5's cached balances)
       case 1 << 21: k = (const void*)pz_epoch_window_abl2097152_d2_kernel; break;  // (the DMA before the first wait)
       case 1 << 23: k = (const void*)pz_epoch_window_abl8388608_d2_kernel; break;  // (loads at base priority)
+      case 1 << 22: break;  // (the R = 1 product form at R > 1 too: two pieces, the straight-line copy)
       default: return hipErrorInvalidValue;
     }
   }
