@@ -949,6 +949,10 @@ PZ_WINDOW_ABL(1048576, 2) PZ_WINDOW_ABL(2097152, 2) PZ_WINDOW_ABL(8388608, 2)
 extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_kernel(EpochArgs a, WinArgs w) {
   window_body<true, 16, true, 0, kWinDepth16, true, true>(a, w);
 }
+// (and the R > 1 product form's: one piece in flight)
+extern "C" __global__ void __launch_bounds__(kWinThreads) pz_epoch_window_trace_d1_kernel(EpochArgs a, WinArgs w) {
+  window_body<true, 16, true, 0, 1, true, true>(a, w);
+}
 // round 5's product (its prologue: the count after the first pieces' descriptors, two barriers,
 // the range descriptor from global memory; the balances through the caches): A/B bit 1 << 18,
 // with and without phase stamps
@@ -1016,6 +1020,7 @@ hipError_t launch_epoch_window(const EpochArgs& a, const WinArgs& w, hipStream_t
   // (the A/B forms are the narrow product form's)
   if (g_window_trace && b32 && w.narrow && sew == 16 && llb)
     k = g_window_ablation == (1 << 18) ? (const void*)pz_epoch_window_trace_np0_kernel
+        : d1                           ? (const void*)pz_epoch_window_trace_d1_kernel
                                        : (const void*)pz_epoch_window_trace_kernel;
   if (g_window_ablation && !g_window_trace && b32 && w.narrow && sew == 16 && llb) {
     switch (g_window_ablation) {  // ablation bits | prefetch depth << 8
