@@ -149,6 +149,13 @@ struct FusedArgs {
   // validator instead of 8, and every sum is taken on the reconstructed u64 values.
   uint32_t* bal32;
   const uint64_t* bal32_base;
+  uint64_t* trace;  // (A/B library, the single launch's phase stamps: [blocks][8], or NULL)
+  // single launch: each attestation of a committee with several, in catt order (the piece's
+  // items_ci holds its catt range {k0, k1} then): {bitfield offset from the instance's 16-B
+  // aligned bits start, 8 x its length, attestation, 0} and its att_win entry -- the bitfield
+  // bytes are read from the block's LDS copy of the instance's bitfields, no global hop
+  const uint4* one_ck;
+  const uint2* one_cw;
 };
 // ---- the window pass (epoch_window.hip): the one-pass step of B instances in ONE launch ------
 // Block (instance, range): a range is a run of this rank's committees (local ids [cr0, cr1)),

@@ -879,6 +879,11 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint64_t item = grp * kFusedWaves + wave;
+  // MODE & (1 << 22) (A/B: tools/epoch_single.py): thread 0's wall clock at the start, when its
+  // stream loads have landed, after the count's barrier, before the block's tail, at the end
+  constexpr bool TRc = (MODE & (1 << 22)) != 0;
+  uint64_t tst[5] = {0, 0, 0, 0, 0};
+  if (TRc) tst[0] = __builtin_amdgcn_s_memrealtime();
   const uint64_t dyn = a.dynasty[inst];  // (the winner rule's, issued with the first loads)
   uint64_t pop = 0, ferr = 0;
   if (!PRO) {
@@ -905,23 +910,23 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
   __shared__ uint4 lbits[PRO ? kOneLoads * 64 * kFusedWaves : 1];
   const uint64_t pbeg = PRO ? boffs_ro[inst * a.natt] : 0, pend = PRO ? boffs_ro[inst * a.natt + a.natt] : 0,
                  pbase = pbeg & ~15ull;
-  // (the rounds the instance's bytes and attestations need: block-uniform, so the unused
-  // rounds of the capacity issue no loads)
+  // (the rounds the instance's bytes need: block-uniform, so the unused rounds of the
+  // capacity issue no loads)
   const uint32_t nlr = PRO ? (uint32_t)((pend - pbase + 16 * 64 * kFusedWaves - 1) / (16 * 64 * kFusedWaves)) : 0;
-  const uint32_t nar = PRO ? (uint32_t)((a.natt + 64 * kFusedWaves - 1) / (64 * kFusedWaves)) : 0;
   if (PRO) {
 #pragma unroll
     for (int k = 0; k < kOneLoads; ++k) {  // branch-free inside a round: the bitfield buffer is padded by 16 B
       const uint64_t u = pbase + 16ull * ((uint64_t)k * 64 * kFusedWaves + tid);
       pq[k] = (uint32_t)k < nlr ? *reinterpret_cast<const uint4*>(a.bits + (u < pend ? u : pbase)) : make_uint4(0, 0, 0, 0);
     }
+    // (every round's loads issued, past natt at entry 0: a select on the round's use turned each
+    // round's loads into a wait before the next round's -- the length check below skips g >= natt)
 #pragma unroll
     for (int k = 0; k < kOneAtts; ++k) {
       const uint64_t g = (uint64_t)k * 64 * kFusedWaves + tid, gc = inst * a.natt + (g < a.natt ? g : 0);
-      const bool r = (uint32_t)k < nar;
-      ocs[k] = r ? f.att_csize[gc] : 0u;
-      ob0[k] = r ? boffs_ro[gc] : 0;
-      ob1[k] = r ? boffs_ro[gc + 1] : 0;
+      ocs[k] = f.att_csize[gc];
+      ob0[k] = boffs_ro[gc];
+      ob1[k] = boffs_ro[gc + 1];
     }
   }
   uint64_t sum = 0, nm = 0, ts = 0, vs = 0;
@@ -1114,6 +1119,21 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     // loaded with the stream below rather than after the tallies)
     const bool wiw = PRO ? f.win_in_wave != 0 : f.win_fused != 0;
     const uint2 win1 = (wiw && ci.ga < kNoAtt) ? f.att_win[inst * a.natt + ci.ga] : make_uint2(0, 0);
+    // ONE, a committee with several attestations: the first two entries of its catt range
+    // (FusedArgs.one_ck / one_cw) go out with the stream, the bitfields are read from LDS
+    constexpr int kCk = 2;
+    uint4 ck[kCk];
+    uint2 cw[kCk];
+    // (issued by every wave of the single launch, entry 0 when its committee has one: a load
+    // under the branch would go out only after the count's barrier, a round trip late)
+    const bool ckt = ONE && ci.ga == kManyAtt;  // (wave-uniform; the single launch always sets one_ck)
+    const uint32_t ck0 = (uint32_t)ci.boff, ck1 = (uint32_t)(ci.boff >> 32);
+#pragma unroll
+    for (int u = 0; u < kCk; ++u) {
+      const uint32_t k = ckt ? min(ck0 + (uint32_t)u, ck1 - 1) : 0u;
+      ck[u] = ONE ? f.one_ck[k] : make_uint4(0, 0, 0, 0);
+      cw[u] = ONE ? f.one_cw[k] : make_uint2(0, 0);
+    }
     const uint64_t p0 = (ws - a.val_offset) & ~1ull;  // local and even: the 16-B pair of ws
     uint64_t* Bal = a.balance + inst * f.vstride;
     const uint64_t* S = a.start + inst * f.vstride;
@@ -1163,6 +1183,10 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
         by1[j] = a.bits[ci.boff + ((q + 1 < last ? q + 1 : last) >> 3)];
       }
     }
+    if (TRc) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      tst[1] = __builtin_amdgcn_s_memrealtime();
+    }
     if (PRO) {  // the block's bit count and length checks -> threshold (no other block involved)
       __shared__ uint64_t xp[kFusedWaves], xe[kFusedWaves];
       uint64_t c = 0, e = 0;
@@ -1171,6 +1195,10 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
         const uint64_t u = pbase + 16ull * ((uint64_t)k * 64 * kFusedWaves + tid);
         if (u + 16 <= pbeg || u >= pend) continue;
         const uint32_t w[4] = {pq[k].x, pq[k].y, pq[k].z, pq[k].w};
+        if (u >= pbeg && u + 16 <= pend) {  // (a chunk inside the region: no byte masks)
+          c += __popc(w[0]) + __popc(w[1]) + __popc(w[2]) + __popc(w[3]);
+          continue;
+        }
 #pragma unroll
         for (int d = 0; d < 4; ++d) {  // bytes of [pbeg, pend) only
           uint32_t m = 0xFFFFFFFFu;
@@ -1197,6 +1225,13 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
         xe[wave] = e;
       }
       __syncthreads();
+      if (TRc) tst[2] = __builtin_amdgcn_s_memrealtime();
+      // (the several-attestation entries used here, on every path: their loads stay ahead of
+      // the barrier -- left to the compiler they sank into the branch that reads them, one
+      // round trip per attestation after it, 1.7 us for two)
+      if (ONE)
+        asm volatile("" ::"v"(ck[0].x), "v"(ck[0].y), "v"(ck[0].z), "v"(ck[1].x), "v"(ck[1].y), "v"(ck[1].z),
+                     "v"(cw[0].x), "v"(cw[0].y), "v"(cw[1].x), "v"(cw[1].y));
       uint64_t pc = 0, pe = 0;
 #pragma unroll
       for (int w = 0; w < kFusedWaves; ++w) {
@@ -1238,6 +1273,54 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
         vs = wave_sum_dpp(v);
         g1 = ci.ga;
         if (wiw && lane == 0) one_win<PRO>(a, f, inst, ci.ga, vs, ts, win1, dyn);
+      } else if (ckt) {  // several attestations, ONE: the table's entries, bitfields in LDS
+        const uint8_t* l8 = reinterpret_cast<const uint8_t*>(lbits);
+        const uint64_t tk0 = TRc ? __builtin_amdgcn_s_memrealtime() : 0;
+        // the vote sums of attestation k: its bits from the block's LDS copy
+        // (branch-free: every lane reads its bytes, clamped into the bitfield, then masks -- the
+        // reads under the validity tests each waited alone)
+        auto vote_of = [&](const uint4& e) {
+          const uint8_t* bf = l8 + e.x;
+          const uint64_t nbits = e.y, last = nbits ? nbits - 1 : 0;
+          uint32_t b0[2], b1[2];
+          uint64_t qj[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            qj[j] = a.val_offset + p0 + (uint64_t)j * 128 + 2 * lane - cb;
+            b0[j] = bf[(qj[j] < last ? qj[j] : last) >> 3];
+            b1[j] = bf[(qj[j] + 1 < last ? qj[j] + 1 : last) >> 3];
+          }
+          uint64_t v = 0;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const uint64_t q = qj[j];
+            const bool x0 = v0[j] && q < nbits && ((b0[j] >> (7 - (uint32_t)(q & 7))) & 1);
+            const bool x1 = v1[j] && q + 1 < nbits && ((b1[j] >> (7 - (uint32_t)((q + 1) & 7))) & 1);
+            v += (x0 ? pack64(qb[j].x, qb[j].y) : 0) + (x1 ? pack64(qb[j].z, qb[j].w) : 0);
+          }
+          return v;
+        };
+        auto tally_of = [&](const uint4& e, const uint2& wn, uint64_t v) {
+          if (wiw && lane == 0) one_win<PRO>(a, f, inst, e.z, v, ts, wn, dyn);
+          if (lane < 2) {  // one instruction: lane 0 the total, lane 1 the vote
+            uint64_t* dst = (lane ? a.vote : a.total) + inst * a.natt + e.z;
+            const uint64_t x = lane ? v : ts;
+            if (x) atomicAdd((unsigned long long*)dst, (unsigned long long)x);
+          }
+        };
+        // the two preloaded entries together (both sums in flight at once), then any others
+        const bool two = ck1 - ck0 >= 2;  // (wave-uniform; a committee here has at least two)
+        uint64_t va = vote_of(ck[0]), vb = two ? vote_of(ck[1]) : 0;
+        va = wave_sum_dpp(va);
+        vb = wave_sum_dpp(vb);
+        if (TRc && lane == 0) f.trace[8 * (uint64_t)(blockIdx.x * gridDim.y + blockIdx.y) + 7] = __builtin_amdgcn_s_memrealtime() - tk0;
+        tally_of(ck[0], cw[0], va);
+        if (two) tally_of(ck[1], cw[1], vb);
+        for (uint32_t k = ck0 + kCk; k < ck1; ++k) {  // (wave-uniform)
+          const uint4 e = f.one_ck[k];
+          tally_of(e, f.one_cw[k], wave_sum_dpp(vote_of(e)));
+        }
+        if (TRc && lane == 0) f.trace[8 * (uint64_t)(blockIdx.x * gridDim.y + blockIdx.y) + 6] = __builtin_amdgcn_s_memrealtime() - tk0;
       } else {  // several attestations of this committee: direct atomics per attestation
         const uint32_t* co = catt_offs_ro + inst * (f.ncomm + 1);
         for (uint32_t k = co[it.z]; k < co[it.z + 1]; ++k) {
@@ -1310,6 +1393,7 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
     xn[wave] = nm;
   }
   __syncthreads();
+  if (TRc) tst[3] = __builtin_amdgcn_s_memrealtime();
   if (!PRO && wave != 0) return;
   if (wave == 0) fused_block_end(a, f, xg, xt, xv, xs, xn, inst, grp, lane, skip, applied, pop, ferr, rwd_err);
   if (PRO && f.win_in_wave) {  // the next step's winners start empty (this step's are in a.winner)
@@ -1317,6 +1401,13 @@ __device__ __forceinline__ void fused_body(EpochArgs a, FusedArgs f, const uint6
       f.winner_next[inst * a.nrec + r] = 0xFFFFFFFFu;
   } else if (ONE) {
     one_tail(a, f, tid);
+  }
+  if (TRc && tid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tst[4] = __builtin_amdgcn_s_memrealtime();
+    uint64_t* t = f.trace + 8 * (uint64_t)(blockIdx.x * gridDim.y + blockIdx.y);
+    for (int k = 0; k < 5; ++k) t[k] = tst[k];
+    t[5] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID
   }
 }
 
@@ -1426,6 +1517,19 @@ pz_epoch_one_se16_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ 
                          const uint32_t* __restrict__ catt_ro) {
   fused_body<512 + 1024 + 16384>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro, catt_ro);
 }
+#ifdef PZ_AB_BUILD
+// the same with phase stamps (FusedArgs.trace; tools/epoch_single.py)
+extern "C" __global__ void __launch_bounds__(64 * kFusedWaves)
+pz_epoch_one_se16_trace_kernel(EpochArgs a, FusedArgs f, const uint64_t* __restrict__ boffs_ro,
+                               const uint64_t* __restrict__ tdep_ro, const uint4* __restrict__ items_ro,
+                               const FusedCommittee* __restrict__ cinfo_ro, const uint32_t* __restrict__ catt_offs_ro,
+                               const uint32_t* __restrict__ catt_ro) {
+  fused_body<512 + 1024 + 16384 + (1 << 22)>(a, f, nullptr, boffs_ro, tdep_ro, items_ro, cinfo_ro, catt_offs_ro,
+                                             catt_ro);
+}
+static uint64_t* g_one_trace = nullptr;
+extern "C" void pz_debug_set_one_trace(uint64_t* d_trace) { g_one_trace = d_trace; }
+#endif
 
 // ---- launchers ---------------------------------------------------------------------------
 static bool vec_ok(const EpochArgs& a) {
@@ -1528,6 +1632,15 @@ bool epoch_one_enabled(const FusedArgs& f) { return f.one != 0; }
 
 hipError_t launch_epoch_one(const EpochArgs& a, const FusedArgs& f, hipStream_t s) {
   const uint64_t groups = std::max<uint64_t>(1, (f.nitems + kFusedWaves - 1) / kFusedWaves);
+#ifdef PZ_AB_BUILD
+  if (g_one_trace && f.se16) {
+    FusedArgs ft = f;
+    ft.trace = g_one_trace;
+    hipLaunchKernelGGL(pz_epoch_one_se16_trace_kernel, dim3(1, (uint32_t)groups), dim3(64 * kFusedWaves), 0, s, a, ft,
+                       a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt);
+    return hipGetLastError();
+  }
+#endif
   if (f.se16)
     hipLaunchKernelGGL(pz_epoch_one_se16_kernel, dim3(1, (uint32_t)groups), dim3(64 * kFusedWaves), 0, s, a, f,
                        a.boffs, a.total_deposit, f.items, f.cinfo, f.catt_offs, f.catt);

@@ -791,6 +791,9 @@ int pz_epoch_state_new_opts(pz_comm* comm, int device, const pz_epoch_host* h, c
         ci.boff = 0;
         ci.nbits = 0;
         ci.ga = o[c + 1] - o[c] == 0 ? 0xFFFFFFFEu : 0xFFFFFFFFu;
+        // (several attestations: boff carries their catt range {k0, k1}, nbits stays 0 -- the
+        // kernels read a committee's bitfield through boff only when it has exactly one)
+        if (o[c + 1] - o[c] > 1) ci.boff = (uint64_t)o[c] | ((uint64_t)o[c + 1] << 32);
         if (o[c + 1] - o[c] == 1) {
           const uint64_t g = catt[b * st->natt + o[c]], ga = b * st->natt + g;
           ci.ga = (uint32_t)g;
@@ -1015,14 +1018,29 @@ int pz_epoch_state_new_opts(pz_comm* comm, int device, const pz_epoch_host* h, c
             const uint32_t c = h->att_comm[i0 * st->natt + g];
             cs[g] = (uint32_t)(h->coffs[c + 1] - h->coffs[c]);
           }
+          // the several-attestation committees' entries in catt order (FusedArgs.one_ck/one_cw)
+          const uint64_t gb = i0 * st->natt, pbase = h->boffs[gb] & ~15ull;
+          std::vector<uint4> ck(st->natt, make_uint4(0, 0, 0, 0));
+          std::vector<uint2> cw(st->natt, make_uint2(0, 0));
+          for (uint64_t k = 0; k < st->natt; ++k) {
+            const uint32_t g = catt[gb + k];
+            const uint64_t bo = h->boffs[gb + g];
+            ck[k] = make_uint4((uint32_t)(bo - pbase), (uint32_t)(8 * (h->boffs[gb + g + 1] - bo)), g, 0);
+            cw[k] = aw[g];
+          }
           uint32_t *d_cs = nullptr, *w2 = nullptr;
-          uint2* d_aw = nullptr;
+          uint2 *d_aw = nullptr, *d_cw = nullptr;
+          uint4* d_ck = nullptr;
           rc = dalloc(s, &q.f.ticket, 1);
           if (!rc) rc = upload(s, &d_cs, cs.data(), cs.size());
           if (!rc) rc = upload(s, &d_aw, aw.data(), aw.size());
+          if (!rc) rc = upload(s, &d_ck, ck.data(), ck.size());
+          if (!rc) rc = upload(s, &d_cw, cw.data(), cw.size());
           if (!rc) rc = dalloc(s, &w2, st->nrec);
           q.f.att_csize = d_cs;
           q.f.att_win = d_aw;
+          q.f.one_ck = d_ck;
+          q.f.one_cw = d_cw;
           q.f.winner_next = w2;
         } else if (!rc) {
           rc = plan_window(st, h, s, q, catt_offs, catt);

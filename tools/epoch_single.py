@@ -25,6 +25,8 @@ def main():
     args = types.SimpleNamespace(steps=200, warmup=20)
     shuffled = casper.shuffle_indices(b"A" + bytes(31), np.arange(65536, dtype=np.uint32))
     dll = _lib.lib.dll
+    if os.environ.get("TRACE") == "1":
+        return trace(args, dev, shuffled, dll)
     ab = hasattr(dll, "pz_debug_set_one_variant")
     for v in VARIANTS if ab else [0]:
         if ab:
@@ -35,6 +37,33 @@ def main():
                  r["window_pass"]["device_ms_median"]), flush=True)
     if ab:
         dll.pz_debug_set_one_variant(0)
+
+
+def trace(args, dev, shuffled, dll):
+    dll.pz_debug_set_one_trace.argtypes = [_lib.ctypes.c_void_p]
+    buf = torch.zeros(8 * 4096, dtype=torch.int64, device=dev)
+    dll.pz_debug_set_one_trace(buf.data_ptr())
+    r = bench.epoch_single_instance(args, torch, dev, 65536, shuffled)
+    torch.cuda.synchronize(dev)
+    dll.pz_debug_set_one_trace(None)
+    t = buf.view(-1, 8).cpu().numpy()
+    t = t[t[:, 0] != 0]
+    t0 = t[:, 0].min()
+    us = lambda x: x * 0.01  # noqa: E731 (100 MHz)
+    ph = {"start (after the first block's)": t[:, 0] - t0, "stream landed": t[:, 1] - t[:, 0],
+          "count + barrier": t[:, 2] - t[:, 1], "tallies, rewards, stores": t[:, 3] - t[:, 2],
+          "tail (block end, winners reset, drain)": t[:, 4] - t[:, 3]}
+    print("traced kernel: %d blocks, span %.2f us (device median of the timed loop %.4f ms)"
+          % (len(t), us(t[:, 4].max() - t0), r["device_ms_median"]), flush=True)
+    for k, v in ph.items():
+        print("  %-40s p50 %.2f  max %.2f us" % (k, us(np.median(v)), us(v.max())), flush=True)
+    many = np.nonzero(t[:, 6])[0]
+    if len(many):
+        print("  several-attestation loop: " + ", ".join("block %d %.2f us (its sums done at %.2f)"
+                                                      % (b, us(t[b, 6]), us(t[b, 7])) for b in many), flush=True)
+    slow = np.argsort(t[:, 3] - t[:, 2])[-3:][::-1]
+    print("  slowest 'tallies, rewards, stores' blocks (index: phase us): " +
+          ", ".join("%d: %.2f" % (b, us(t[b, 3] - t[b, 2])) for b in slow), flush=True)
 
 
 if __name__ == "__main__":
